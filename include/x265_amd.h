@@ -1,0 +1,243 @@
+/* x265_amd.h — C ABI of the MI355X (gfx950) primitive provider for x265 1.9.
+ *
+ * This is the drop-in boundary.  x265 calls its primitives
+ * one block at a time through the function table `EncoderPrimitives`
+ * (x265_1.9/source/common/primitives.h:203-381); a GPU cannot sit under
+ * single calls of 50 ns - 25 us, so each entry below executes a BATCH of
+ * independent calls of one table entry.  Job i of a batch is exactly the
+ * reference call
+ *
+ *     primitive(a_base + a_off[i], a_stride, b_base + b_off[i], b_stride, ...)
+ *
+ * with the same argument meaning, the same integer results and the same
+ * "write only inside the WxH block" contract as the C primitive it replaces
+ * (pixel.cpp / dct.cpp / ipfilter.cpp / intrapred.cpp).  The per-call table
+ * entry each function replaces is cited on the function.
+ *
+ * Conventions
+ *   - all pointers are DEVICE pointers (hipMalloc / torch tensors);
+ *   - strides and offsets are in ELEMENTS (pixels or int16), as in x265;
+ *   - `depth` is the pixel bit depth: 8 => pixels are uint8_t,
+ *     10 or 12 => pixels are uint16_t (x265 HIGH_BIT_DEPTH builds);
+ *   - `stream` is a hipStream_t (NULL = default stream); calls only enqueue
+ *     work and never synchronise;
+ *   - return value: 0 on success, otherwise a hipError_t code or one of the
+ *     X265AMD_E* codes below (unsupported shape/op).  x265 primitives have no
+ *     error channel (primitives.h typedefs return void/int); the caller maps
+ *     a non-zero status to x265_encoder_encode() < 0 (x265.h:1351-1359).
+ *   - Block shapes: every (w, h) that has a non-NULL entry in the reference
+ *     table for that family (luma, chroma 4:2:0 / 4:2:2 / 4:4:4).
+ */
+#ifndef X265_AMD_H
+#define X265_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define X265AMD_ABI_VERSION 1
+
+enum
+{
+    X265AMD_OK = 0,
+    X265AMD_EINVAL = 1000,   /* unsupported op / shape / depth */
+    X265AMD_ENODEV = 1001    /* no gfx950 device */
+};
+
+/* ----------------------------------------------------------------- runtime */
+int         x265amd_abi_version(void);
+/* Select the HIP device for this host thread; returns 0 or a hipError_t. */
+int         x265amd_set_device(int device);
+/* Human-readable message for a status code returned by any entry. */
+const char* x265amd_strerror(int status);
+/* Name of the gfx target the library was compiled for ("gfx950"). */
+const char* x265amd_target(void);
+
+/* -------------------------------------------------------- a4 a6 a7 a8 a15
+ * Pixel comparison of block A against block B, one scalar per job.
+ *   X265AMD_SAD     pu[].sad          pixel.cpp:39-54       out int32
+ *   X265AMD_SATD    pu[].satd         pixel.cpp:163-242     out int32
+ *   X265AMD_SA8D    cu[].sa8d         pixel.cpp:244-322     out int32
+ *                   (w,h multiple of 16: one (x+2)>>2 per 16x16; multiple of
+ *                    8: per 8x8; 4x4 / 4x8: satd, as the table aliases them)
+ *   X265AMD_SSE_PP  cu[].sse_pp       pixel.cpp:120-139     out uint64 (sse_t)
+ *   X265AMD_SSE_SS  cu[].sse_ss       (int16 operands)      out uint64 (sse_t)
+ *   X265AMD_PSY     cu[].psy_cost_pp  pixel.cpp:672-703     out int32 (w == h)
+ *   X265AMD_SSD_S   cu[].ssd_s        pixel.cpp:324-336     out uint64, B unused
+ *   X265AMD_VAR     cu[].var          pixel.cpp:649-666     out uint64, B unused
+ * sse_t is uint32 at 8-bit (the value wraps mod 2^32 exactly as the
+ * reference's) and uint64 at 10/12-bit; both are returned zero-extended. */
+enum
+{
+    X265AMD_SAD = 0,
+    X265AMD_SATD,
+    X265AMD_SA8D,
+    X265AMD_SSE_PP,
+    X265AMD_SSE_SS,
+    X265AMD_PSY,
+    X265AMD_SSD_S,
+    X265AMD_VAR
+};
+int x265amd_pixelcmp(int op, int depth, int w, int h, int n,
+                     const void* a, intptr_t a_stride, const int64_t* a_off,
+                     const void* b, intptr_t b_stride, const int64_t* b_off,
+                     void* out, void* stream);
+
+/* ---------------------------------------------------------------------- a5
+ * pu[].sad_x3 / pu[].sad_x4 (pixel.cpp:73-118): one fenc block against
+ * nref = 3 or 4 reference blocks sharing ref_stride.  The reference fixes the
+ * fenc stride to FENC_STRIDE (64); here it is a parameter.
+ * ref_off holds nref offsets per job (job-major); out holds nref int32 per job. */
+int x265amd_sad_multi(int nref, int depth, int w, int h, int n,
+                      const void* fenc, intptr_t fenc_stride, const int64_t* fenc_off,
+                      const void* ref, intptr_t ref_stride, const int64_t* ref_off,
+                      int32_t* out, void* stream);
+
+/* ---------------------------------------------------------------------- a9
+ * Sub-pel interpolation (ipfilter.cpp:40-372).  taps = 8 (luma pu[].luma_*)
+ * or 4 (chroma[].pu[].filter_*).  Operand types per op:
+ *   HPP  pixel -> pixel      luma_hpp / filter_hpp
+ *   HPS  pixel -> int16      luma_hps / filter_hps (is_row_ext applies)
+ *   VPP  pixel -> pixel      luma_vpp / filter_vpp
+ *   VPS  pixel -> int16      luma_vps / filter_vps
+ *   VSP  int16 -> pixel      luma_vsp / filter_vsp
+ *   VSS  int16 -> int16      luma_vss / filter_vss
+ *   HVPP pixel -> pixel      luma_hvpp (taps must be 8)
+ *   P2S  pixel -> int16      convert_p2s / p2s (taps ignored)
+ * coeff[i] = coeffIdx of job i; for HVPP bits 0-3 = idxX, bits 4-7 = idxY.
+ * src_off[i] points at the block origin exactly like the reference's `src`
+ * argument (the filter reaches taps/2-1 pixels before and taps/2 after it). */
+enum
+{
+    X265AMD_HPP = 0,
+    X265AMD_HPS,
+    X265AMD_VPP,
+    X265AMD_VPS,
+    X265AMD_VSP,
+    X265AMD_VSS,
+    X265AMD_HVPP,
+    X265AMD_P2S
+};
+int x265amd_interp(int op, int taps, int depth, int w, int h, int n,
+                   const void* src, intptr_t src_stride, const int64_t* src_off,
+                   void* dst, intptr_t dst_stride, const int64_t* dst_off,
+                   const uint8_t* coeff, int is_row_ext, void* stream);
+
+/* ----------------------------------------------------------------- a10 a11
+ * 2-D transforms (dct.cpp:442-610): cu[].dct / cu[].idct for size 4..32 and
+ * dst4x4 / idst4x4.  Forward kinds read `src` with src_stride and write the
+ * N*N coefficients with dst_stride (the reference writes them contiguous:
+ * pass dst_stride = size); inverse kinds read with src_stride (reference:
+ * contiguous) and write the residual with dst_stride. */
+enum
+{
+    X265AMD_DCT = 0,
+    X265AMD_IDCT,
+    X265AMD_DST,
+    X265AMD_IDST
+};
+int x265amd_transform(int kind, int depth, int size, int n,
+                      const int16_t* src, intptr_t src_stride, const int64_t* src_off,
+                      int16_t* dst, intptr_t dst_stride, const int64_t* dst_off,
+                      void* stream);
+
+/* ----------------------------------------------------------------- a12 a13
+ * quant (dct.cpp:664-686): per job coef[num] * quantCoeff[num] -> qCoef,
+ * deltaU; num_sig[i] = the uint32 return value.  nquant (dct.cpp:688-713)
+ * when delta_u == NULL (stores |level|, as the reference).  All buffers of a
+ * job are `num` contiguous elements at base + off[i]. */
+int x265amd_quant(int n, int num,
+                  const int16_t* coef, const int64_t* coef_off,
+                  const int32_t* qtab, const int64_t* qtab_off,
+                  int32_t* delta_u, const int64_t* delta_off,
+                  int16_t* qcoef, const int64_t* qcoef_off,
+                  const int32_t* qbits, const int32_t* add,
+                  uint32_t* num_sig, void* stream);
+/* dequant_normal (dct.cpp:612-634): scale[i], shift[i] per job. */
+int x265amd_dequant_normal(int n, int num,
+                           const int16_t* q, const int64_t* q_off,
+                           int16_t* coef, const int64_t* coef_off,
+                           const int32_t* scale, const int32_t* shift, void* stream);
+/* dequant_scaling (dct.cpp:636-662): deQuantCoef table per job, per[i], shift[i]. */
+int x265amd_dequant_scaling(int n, int num,
+                            const int16_t* q, const int64_t* q_off,
+                            const int32_t* dq, const int64_t* dq_off,
+                            int16_t* coef, const int64_t* coef_off,
+                            const int32_t* per, const int32_t* shift, void* stream);
+
+/* --------------------------------------------------------------------- a14
+ * Intra prediction (intrapred.cpp).  Neighbour buffers follow the reference
+ * layout: [0] top-left, [1..2N] above, [2N+1..4N] left (4N+1 pixels).
+ *   intra_filter  cu[].intra_filter        intrapred.cpp:31-51
+ *   intra_pred    cu[].intra_pred[mode]    planar (0), DC (1), angular 2..34;
+ *                 mode[i], bfilter[i] per job (intrapred.cpp:69-204)
+ *   intra_allangs cu[].intra_pred_allangs  intrapred.cpp:206-234: 33 NxN blocks
+ *                 of modes 2..34, each written row-major at dst + (mode-2)*N*N */
+int x265amd_intra_filter(int depth, int size, int n,
+                         const void* src, const int64_t* src_off,
+                         void* dst, const int64_t* dst_off, void* stream);
+int x265amd_intra_pred(int depth, int size, int n,
+                       void* dst, intptr_t dst_stride, const int64_t* dst_off,
+                       const void* nb, const int64_t* nb_off,
+                       const uint8_t* mode, const uint8_t* bfilter, void* stream);
+int x265amd_intra_allangs(int depth, int size, int n,
+                          void* dst, const int64_t* dst_off,
+                          const void* ref, const int64_t* ref_off,
+                          const void* filt, const int64_t* filt_off,
+                          const uint8_t* bluma, void* stream);
+
+/* --------------------------------------------------------------------- a15
+ * Companion block ops (pixel.cpp:338-436, 490-502, 705-808; dct.cpp:714-742).
+ *   op                 reference entry          dst     a       b       param
+ *   X265AMD_SUB_PS     cu[].sub_ps              int16   pixel   pixel   -
+ *   X265AMD_ADD_PS     cu[].add_ps              pixel   pixel   int16   -
+ *   X265AMD_ADDAVG     pu[].addAvg              pixel   int16   int16   -
+ *   X265AMD_PIXELAVG   pu[].pixelavg_pp         pixel   pixel   pixel   -
+ *   X265AMD_COPY_PP    pu[].copy_pp             pixel   pixel   -       -
+ *   X265AMD_COPY_SP    cu[].copy_sp             pixel   int16   -       -
+ *   X265AMD_COPY_PS    cu[].copy_ps             int16   pixel   -       -
+ *   X265AMD_COPY_SS    cu[].copy_ss             int16   int16   -       -
+ *   X265AMD_BLOCKFILL  cu[].blockfill_s         int16   -       -       value
+ *   X265AMD_CPY2D1D_SHL/SHR cu[].cpy2Dto1D_*    int16   int16   -       shift
+ *   X265AMD_CPY1D2D_SHL/SHR cu[].cpy1Dto2D_*    int16   int16   -       shift
+ *   X265AMD_TRANSPOSE  cu[].transpose           pixel   pixel   -       -
+ * For the 2D<->1D copies the 1-D side uses stride = w (pass it).
+ * calcresidual is SUB_PS with all three strides equal. */
+enum
+{
+    X265AMD_SUB_PS = 0,
+    X265AMD_ADD_PS,
+    X265AMD_ADDAVG,
+    X265AMD_PIXELAVG,
+    X265AMD_COPY_PP,
+    X265AMD_COPY_SP,
+    X265AMD_COPY_PS,
+    X265AMD_COPY_SS,
+    X265AMD_BLOCKFILL,
+    X265AMD_CPY2D1D_SHL,
+    X265AMD_CPY2D1D_SHR,
+    X265AMD_CPY1D2D_SHL,
+    X265AMD_CPY1D2D_SHR,
+    X265AMD_TRANSPOSE
+};
+int x265amd_blockop(int op, int depth, int w, int h, int n,
+                    void* dst, intptr_t dst_stride, const int64_t* dst_off,
+                    const void* a, intptr_t a_stride, const int64_t* a_off,
+                    const void* b, intptr_t b_stride, const int64_t* b_off,
+                    int param, void* stream);
+
+/* count_nonzero (dct.cpp:714-726, num = N*N contiguous int16) and copy_cnt
+ * (dct.cpp:728-742: coeff[N*N] <- residual with res_stride, counting nonzero).
+ * copy_cnt when `res` != NULL, else count_nonzero on `coeff`. */
+int x265amd_count_nonzero(int size, int n,
+                          int16_t* coeff, const int64_t* coeff_off,
+                          const int16_t* res, intptr_t res_stride, const int64_t* res_off,
+                          uint32_t* count, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* X265_AMD_H */

@@ -1,0 +1,97 @@
+"""ctypes front-end of oracle/_build/libcpubatch.so — TEST INFRASTRUCTURE ONLY.
+
+Runs the batch descriptors of the GPU C ABI (include/x265_amd.h) on the CPU
+through one of the per-call oracle libraries:
+
+    CpuOracle("oracle", depth)  -> oracle/_build/liboracle{8,10}.so  (restatement)
+    CpuOracle("ref", depth)     -> oracle/_ref/libx265ref{8,10}.so   (reference C)
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may use
+this module, and only as the checker / CPU baseline.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+_vp, _i64, _ip = C.c_void_p, C.c_int64, C.c_ssize_t
+
+
+def lib_path(kind: str, depth: int) -> str:
+    d = 8 if depth == 8 else 10
+    if kind == "oracle":
+        return os.path.join(HERE, "_build", f"liboracle{d}.so")
+    if kind == "ref":
+        return os.path.join(HERE, "_ref", f"libx265ref{d}.so")
+    raise ValueError(kind)
+
+
+def available(kind: str, depth: int = 8) -> bool:
+    return os.path.exists(lib_path(kind, depth)) and os.path.exists(os.path.join(HERE, "_build", "libcpubatch.so"))
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data_as(_vp)
+
+
+class CpuOracle:
+    _cb = None
+
+    def __init__(self, kind: str, depth: int):
+        if CpuOracle._cb is None:
+            cb = C.CDLL(os.path.join(HERE, "_build", "libcpubatch.so"))
+            cb.cb_open.restype = _vp
+            cb.cb_open.argtypes = [C.c_char_p]
+            CpuOracle._cb = cb
+        self.kind, self.depth = kind, depth
+        self.h = CpuOracle._cb.cb_open(lib_path(kind, depth).encode())
+        if not self.h:
+            raise RuntimeError(f"cannot open oracle library {lib_path(kind, depth)}")
+        self.nthreads = 1
+
+    @property
+    def cb(self):
+        return CpuOracle._cb
+
+    # every wrapper takes numpy arrays and int64 offset arrays (element units)
+    def pixelcmp(self, op, w, h, a, sa, aoff, b, sb, boff, out):
+        self.cb.cb_pixelcmp(_vp(self.h), op, w, h, _i64(len(aoff)), _p(a), _ip(sa), _p(aoff), _p(b), _ip(sb),
+                            _p(boff), _p(out), self.nthreads)
+
+    def sad_multi(self, nref, w, h, f, fs, foff, r, rs, roff, out):
+        rc = self.cb.cb_sad_multi(_vp(self.h), nref, w, h, _i64(len(foff)), _p(f), _ip(fs), _p(foff), _p(r), _ip(rs),
+                                  _p(roff), _p(out), self.nthreads)
+        if rc:
+            raise ValueError("sad_multi oracle requires fenc stride 64")
+
+    def interp(self, op, taps, w, h, s, ss, soff, d, ds, doff, coeff, rowext):
+        self.cb.cb_interp(_vp(self.h), op, taps, w, h, _i64(len(soff)), _p(s), _ip(ss), _p(soff), _p(d), _ip(ds),
+                          _p(doff), _p(coeff), rowext, self.nthreads)
+
+    def transform(self, kind, size, s, ss, soff, d, ds, doff):
+        self.cb.cb_transform(_vp(self.h), kind, size, _i64(len(soff)), _p(s), _ip(ss), _p(soff), _p(d), _ip(ds),
+                             _p(doff), self.nthreads)
+
+    def quant(self, num, c, co, q, qo, dl, dlo, o, oo, qb, ad, sig):
+        self.cb.cb_quant(_vp(self.h), _i64(len(co)), num, _p(c), _p(co), _p(q), _p(qo), _p(dl), _p(dlo), _p(o),
+                         _p(oo), _p(qb), _p(ad), _p(sig), self.nthreads)
+
+    def dequant(self, scaling, num, q, qo, dq, dqo, o, oo, p0, p1):
+        self.cb.cb_dequant(_vp(self.h), int(scaling), _i64(len(qo)), num, _p(q), _p(qo), _p(dq), _p(dqo), _p(o),
+                           _p(oo), _p(p0), _p(p1), self.nthreads)
+
+    def intra(self, kind, size, d, ds, doff, nb, nboff, f, foff, mode, bf):
+        self.cb.cb_intra(_vp(self.h), kind, size, _i64(len(doff)), _p(d), _ip(ds), _p(doff), _p(nb), _p(nboff),
+                         _p(f), _p(foff), _p(mode), _p(bf), self.nthreads)
+
+    def blockop(self, op, w, h, d, ds, doff, a, sa, aoff, b, sb, boff, param):
+        self.cb.cb_blockop(_vp(self.h), op, w, h, _i64(len(doff)), _p(d), _ip(ds), _p(doff), _p(a), _ip(sa),
+                           _p(aoff), _p(b), _ip(sb), _p(boff), param, self.nthreads)
+
+    def count_nonzero(self, size, c, co, r, rs, ro, cnt):
+        self.cb.cb_count_nonzero(_vp(self.h), size, _i64(len(co)), _p(c), _p(co), _p(r), _ip(rs), _p(ro),
+                                 _p(cnt), self.nthreads)

@@ -1,0 +1,383 @@
+/* ref_shim.cpp — exposes the reference x265 1.9 C primitive table through the
+ * flat oracle API (x265_oracle.h).
+ *
+ * TEST INFRASTRUCTURE ONLY.  Compiled together with the reference's own
+ * sources (oracle/Makefile, target `ref`) into oracle/_ref/libx265ref{8,10}.so;
+ * the reference sources themselves are never copied into this repository.
+ *
+ * The table is set up exactly as TestBench's `cprim` is
+ * (test/testbench.cpp:153-156): setupCPrimitives + setupAliasPrimitives, so
+ * intra_pred_allangs stays non-NULL.  Every xo_* call below resolves the
+ * (width, height) it is given to the table entry that the reference encoder
+ * would call for a block of that shape — luma tables first, then the 4:2:0 and
+ * 4:2:2 chroma tables (primitives.h:345-380) — and aborts if no entry exists.
+ */
+#include "common.h"
+#include "primitives.h"
+#include "x265_oracle.h"
+
+#include <cstdio>
+#include <cstdlib>
+
+using namespace X265_NS;
+
+namespace {
+
+EncoderPrimitives g_tab;
+bool g_init = false;
+
+EncoderPrimitives& tab()
+{
+    if (!g_init)
+    {
+        memset(&g_tab, 0, sizeof(g_tab));
+        setupCPrimitives(g_tab);
+        setupAliasPrimitives(g_tab);
+        g_init = true;
+    }
+    return g_tab;
+}
+
+[[noreturn]] void die(const char* what, int w, int h)
+{
+    fprintf(stderr, "ref_shim: no reference entry for %s %dx%d\n", what, w, h);
+    abort();
+}
+
+const int kPuW[NUM_PU_SIZES] = { 4, 8, 16, 32, 64, 8, 4, 16, 8, 32, 16, 64, 32, 16, 12, 16, 4, 32, 24, 32, 8, 64, 48, 64, 16 };
+const int kPuH[NUM_PU_SIZES] = { 4, 8, 16, 32, 64, 4, 8, 8, 16, 16, 32, 32, 64, 12, 16, 4, 16, 24, 32, 8, 32, 48, 64, 16, 64 };
+
+/* PU-indexed entry lookup: luma, then chroma 4:2:0 (w/2,h/2), then 4:2:2 (w/2,h) */
+struct PuRef { int csp; int part; };
+
+PuRef findPu(int w, int h, bool allowLuma, bool allowChroma)
+{
+    if (allowLuma)
+        for (int p = 0; p < NUM_PU_SIZES; p++)
+            if (kPuW[p] == w && kPuH[p] == h) return PuRef{ -1, p };
+    if (allowChroma)
+    {
+        for (int p = 0; p < NUM_PU_SIZES; p++)
+            if (kPuW[p] / 2 == w && kPuH[p] / 2 == h) return PuRef{ X265_CSP_I420, p };
+        for (int p = 0; p < NUM_PU_SIZES; p++)
+            if (kPuW[p] / 2 == w && kPuH[p] == h) return PuRef{ X265_CSP_I422, p };
+    }
+    return PuRef{ -2, -1 };
+}
+
+/* CU-indexed lookup: luma square (4<<i), 4:2:0 square (2<<i), 4:2:2 (2<<i)x(4<<i) */
+PuRef findCu(int w, int h)
+{
+    for (int i = 0; i < NUM_CU_SIZES; i++)
+        if (w == (4 << i) && h == (4 << i)) return PuRef{ -1, i };
+    for (int i = 0; i < NUM_CU_SIZES; i++)
+        if (w == (2 << i) && h == (2 << i)) return PuRef{ X265_CSP_I420, i };
+    for (int i = 0; i < NUM_CU_SIZES; i++)
+        if (w == (2 << i) && h == (4 << i)) return PuRef{ X265_CSP_I422, i };
+    return PuRef{ -2, -1 };
+}
+
+int log2i(int n) { int l = 0; while ((1 << l) < n) l++; return l; }
+
+pixelcmp_t satdFor(int w, int h)
+{
+    PuRef r = findPu(w, h, true, true);
+    pixelcmp_t f = NULL;
+    if (r.csp == -1) f = tab().pu[r.part].satd;
+    else if (r.csp >= 0) f = tab().chroma[r.csp].pu[r.part].satd;
+    if (!f) die("satd", w, h);
+    return f;
+}
+
+} // namespace
+
+extern "C" {
+
+int xo_depth(void) { return X265_DEPTH; }
+
+int xo_sad(int w, int h, const void* a, intptr_t sa, const void* b, intptr_t sb)
+{
+    PuRef r = findPu(w, h, true, false);
+    if (r.csp != -1) die("sad", w, h);
+    return tab().pu[r.part].sad((const pixel*)a, sa, (const pixel*)b, sb);
+}
+
+void xo_sad_x3(int w, int h, const void* fenc, const void* r0, const void* r1, const void* r2, intptr_t rs, int32_t* res)
+{
+    PuRef r = findPu(w, h, true, false);
+    if (r.csp != -1) die("sad_x3", w, h);
+    tab().pu[r.part].sad_x3((const pixel*)fenc, (const pixel*)r0, (const pixel*)r1, (const pixel*)r2, rs, res);
+}
+
+void xo_sad_x4(int w, int h, const void* fenc, const void* r0, const void* r1, const void* r2, const void* r3, intptr_t rs, int32_t* res)
+{
+    PuRef r = findPu(w, h, true, false);
+    if (r.csp != -1) die("sad_x4", w, h);
+    tab().pu[r.part].sad_x4((const pixel*)fenc, (const pixel*)r0, (const pixel*)r1, (const pixel*)r2, (const pixel*)r3, rs, res);
+}
+
+int xo_satd(int w, int h, const void* a, intptr_t sa, const void* b, intptr_t sb)
+{
+    return satdFor(w, h)((const pixel*)a, sa, (const pixel*)b, sb);
+}
+
+int xo_sa8d(int w, int h, const void* a, intptr_t sa, const void* b, intptr_t sb)
+{
+    PuRef r = findCu(w, h);
+    pixelcmp_t f = NULL;
+    if (r.csp == -1) f = tab().cu[r.part].sa8d;
+    else if (r.csp >= 0) f = tab().chroma[r.csp].cu[r.part].sa8d;
+    if (!f) die("sa8d", w, h);
+    return f((const pixel*)a, sa, (const pixel*)b, sb);
+}
+
+uint64_t xo_sse_pp(int w, int h, const void* a, intptr_t sa, const void* b, intptr_t sb)
+{
+    PuRef r = findCu(w, h);
+    pixel_sse_t f = NULL;
+    if (r.csp == -1) f = tab().cu[r.part].sse_pp;
+    else if (r.csp >= 0) f = tab().chroma[r.csp].cu[r.part].sse_pp;
+    if (!f) die("sse_pp", w, h);
+    return (uint64_t)f((const pixel*)a, sa, (const pixel*)b, sb);
+}
+
+uint64_t xo_sse_ss(int w, int h, const int16_t* a, intptr_t sa, const int16_t* b, intptr_t sb)
+{
+    PuRef r = findCu(w, h);
+    if (r.csp != -1 || !tab().cu[r.part].sse_ss) die("sse_ss", w, h);
+    return (uint64_t)tab().cu[r.part].sse_ss(a, sa, b, sb);
+}
+
+uint64_t xo_ssd_s(int n, const int16_t* a, intptr_t sa)
+{
+    return (uint64_t)tab().cu[log2i(n) - 2].ssd_s(a, sa);
+}
+
+int xo_psy_cost_pp(int n, const void* src, intptr_t ss, const void* rec, intptr_t rs)
+{
+    return tab().cu[log2i(n) - 2].psy_cost_pp((const pixel*)src, ss, (const pixel*)rec, rs);
+}
+
+uint64_t xo_var(int n, const void* p, intptr_t s)
+{
+    return tab().cu[log2i(n) - 2].var((const pixel*)p, s);
+}
+
+void xo_interp(int op, int taps, int w, int h, const void* src, intptr_t ss, void* dst, intptr_t ds, int coeffIdx, int extra)
+{
+    EncoderPrimitives& p = tab();
+    const pixel* sp = (const pixel*)src;
+    const int16_t* s16 = (const int16_t*)src;
+    pixel* dp = (pixel*)dst;
+    int16_t* d16 = (int16_t*)dst;
+
+    if (taps == 8 || op == XO_P2S)
+    {
+        PuRef r = findPu(w, h, true, op == XO_P2S);
+        if (r.csp == -1)
+        {
+            EncoderPrimitives::PU& u = p.pu[r.part];
+            switch (op)
+            {
+            case XO_HPP:  u.luma_hpp(sp, ss, dp, ds, coeffIdx); return;
+            case XO_HPS:  u.luma_hps(sp, ss, d16, ds, coeffIdx, extra); return;
+            case XO_VPP:  u.luma_vpp(sp, ss, dp, ds, coeffIdx); return;
+            case XO_VPS:  u.luma_vps(sp, ss, d16, ds, coeffIdx); return;
+            case XO_VSP:  u.luma_vsp(s16, ss, dp, ds, coeffIdx); return;
+            case XO_VSS:  u.luma_vss(s16, ss, d16, ds, coeffIdx); return;
+            case XO_HVPP: u.luma_hvpp(sp, ss, dp, ds, coeffIdx, extra); return;
+            case XO_P2S:  u.convert_p2s(sp, ss, d16, ds); return;
+            }
+        }
+        if (r.csp >= 0 && op == XO_P2S)
+        {
+            p.chroma[r.csp].pu[r.part].p2s(sp, ss, d16, ds);
+            return;
+        }
+        die("luma interp", w, h);
+    }
+
+    /* 4-tap: chroma 4:2:0, then 4:2:2, then 4:4:4 (luma-sized) */
+    EncoderPrimitives::Chroma::PUChroma* c = NULL;
+    PuRef r = findPu(w, h, false, true);
+    if (r.csp >= 0) c = &p.chroma[r.csp].pu[r.part];
+    else
+    {
+        r = findPu(w, h, true, false);
+        if (r.csp == -1) c = &p.chroma[X265_CSP_I444].pu[r.part];
+    }
+    if (!c) die("chroma interp", w, h);
+    switch (op)
+    {
+    case XO_HPP: c->filter_hpp(sp, ss, dp, ds, coeffIdx); return;
+    case XO_HPS: c->filter_hps(sp, ss, d16, ds, coeffIdx, extra); return;
+    case XO_VPP: c->filter_vpp(sp, ss, dp, ds, coeffIdx); return;
+    case XO_VPS: c->filter_vps(sp, ss, d16, ds, coeffIdx); return;
+    case XO_VSP: c->filter_vsp(s16, ss, dp, ds, coeffIdx); return;
+    case XO_VSS: c->filter_vss(s16, ss, d16, ds, coeffIdx); return;
+    }
+    die("chroma interp op", w, h);
+}
+
+void xo_dct(int kind, int n, const int16_t* src, int16_t* dst, intptr_t stride)
+{
+    EncoderPrimitives& p = tab();
+    int i = log2i(n) - 2;
+    switch (kind)
+    {
+    case XO_DCT:  p.cu[i].dct(src, dst, stride); return;
+    case XO_IDCT: p.cu[i].idct(src, dst, stride); return;
+    case XO_DST:  p.dst4x4(src, dst, stride); return;
+    case XO_IDST: p.idst4x4(src, dst, stride); return;
+    }
+}
+
+uint32_t xo_quant(const int16_t* coef, const int32_t* qcoef, int32_t* deltaU, int16_t* qout, int qBits, int add, int numCoeff)
+{
+    return tab().quant(coef, qcoef, deltaU, qout, qBits, add, numCoeff);
+}
+
+uint32_t xo_nquant(const int16_t* coef, const int32_t* qcoef, int16_t* qout, int qBits, int add, int numCoeff)
+{
+    return tab().nquant(coef, qcoef, qout, qBits, add, numCoeff);
+}
+
+void xo_dequant_normal(const int16_t* q, int16_t* coef, int num, int scale, int shift)
+{
+    tab().dequant_normal(q, coef, num, scale, shift);
+}
+
+void xo_dequant_scaling(const int16_t* q, const int32_t* dq, int16_t* coef, int num, int per, int shift)
+{
+    tab().dequant_scaling(q, dq, coef, num, per, shift);
+}
+
+void xo_intra_filter(int n, const void* ref, void* filt)
+{
+    tab().cu[log2i(n) - 2].intra_filter((const pixel*)ref, (pixel*)filt);
+}
+
+void xo_intra_pred(int n, int mode, void* dst, intptr_t ds, const void* src, int bFilter)
+{
+    tab().cu[log2i(n) - 2].intra_pred[mode]((pixel*)dst, ds, (const pixel*)src, mode, bFilter);
+}
+
+void xo_intra_allangs(int n, void* dst, void* ref, void* filt, int bLuma)
+{
+    tab().cu[log2i(n) - 2].intra_pred_allangs((pixel*)dst, (pixel*)ref, (pixel*)filt, bLuma);
+}
+
+void xo_calcresidual(int n, const void* fenc, const void* pred, int16_t* res, intptr_t stride)
+{
+    tab().cu[log2i(n) - 2].calcresidual((const pixel*)fenc, (const pixel*)pred, res, stride);
+}
+
+#define CU_ENTRY(field, what)                                                      \
+    PuRef r = findCu(w, h);                                                        \
+    EncoderPrimitives& p = tab();                                                  \
+    if (r.csp == -2) die(what, w, h);
+
+void xo_sub_ps(int w, int h, int16_t* d, intptr_t ds, const void* a, const void* b, intptr_t sa, intptr_t sb)
+{
+    CU_ENTRY(sub_ps, "sub_ps");
+    pixel_sub_ps_t f = r.csp == -1 ? p.cu[r.part].sub_ps : p.chroma[r.csp].cu[r.part].sub_ps;
+    f(d, ds, (const pixel*)a, (const pixel*)b, sa, sb);
+}
+
+void xo_add_ps(int w, int h, void* d, intptr_t ds, const void* a, const int16_t* b, intptr_t sa, intptr_t sb)
+{
+    CU_ENTRY(add_ps, "add_ps");
+    pixel_add_ps_t f = r.csp == -1 ? p.cu[r.part].add_ps : p.chroma[r.csp].cu[r.part].add_ps;
+    f((pixel*)d, ds, (const pixel*)a, b, sa, sb);
+}
+
+void xo_copy_sp(int w, int h, void* d, intptr_t ds, const int16_t* s, intptr_t ss)
+{
+    CU_ENTRY(copy_sp, "copy_sp");
+    copy_sp_t f = r.csp == -1 ? p.cu[r.part].copy_sp : p.chroma[r.csp].cu[r.part].copy_sp;
+    f((pixel*)d, ds, s, ss);
+}
+
+void xo_copy_ps(int w, int h, int16_t* d, intptr_t ds, const void* s, intptr_t ss)
+{
+    CU_ENTRY(copy_ps, "copy_ps");
+    copy_ps_t f = r.csp == -1 ? p.cu[r.part].copy_ps : p.chroma[r.csp].cu[r.part].copy_ps;
+    f(d, ds, (const pixel*)s, ss);
+}
+
+void xo_copy_ss(int w, int h, int16_t* d, intptr_t ds, const int16_t* s, intptr_t ss)
+{
+    CU_ENTRY(copy_ss, "copy_ss");
+    copy_ss_t f = r.csp == -1 ? p.cu[r.part].copy_ss : p.chroma[r.csp].cu[r.part].copy_ss;
+    f(d, ds, s, ss);
+}
+
+void xo_addavg(int w, int h, const int16_t* a, const int16_t* b, void* d, intptr_t sa, intptr_t sb, intptr_t ds)
+{
+    PuRef r = findPu(w, h, true, true);
+    if (r.csp == -2) die("addAvg", w, h);
+    addAvg_t f = r.csp == -1 ? tab().pu[r.part].addAvg : tab().chroma[r.csp].pu[r.part].addAvg;
+    f(a, b, (pixel*)d, sa, sb, ds);
+}
+
+void xo_pixelavg(int w, int h, void* d, intptr_t ds, const void* a, intptr_t sa, const void* b, intptr_t sb)
+{
+    PuRef r = findPu(w, h, true, false);
+    if (r.csp != -1) die("pixelavg_pp", w, h);
+    tab().pu[r.part].pixelavg_pp((pixel*)d, ds, (const pixel*)a, sa, (const pixel*)b, sb, 32);
+}
+
+void xo_copy_pp(int w, int h, void* d, intptr_t ds, const void* s, intptr_t ss)
+{
+    PuRef r = findPu(w, h, true, true);
+    if (r.csp == -2) die("copy_pp", w, h);
+    copy_pp_t f = r.csp == -1 ? tab().pu[r.part].copy_pp : tab().chroma[r.csp].pu[r.part].copy_pp;
+    f((pixel*)d, ds, (const pixel*)s, ss);
+}
+
+void xo_blockfill_s(int n, int16_t* d, intptr_t ds, int16_t v)
+{
+    tab().cu[log2i(n) - 2].blockfill_s(d, ds, v);
+}
+
+void xo_cpy2Dto1D_shl(int n, int16_t* d, const int16_t* s, intptr_t ss, int shift)
+{
+    tab().cu[log2i(n) - 2].cpy2Dto1D_shl(d, s, ss, shift);
+}
+
+void xo_cpy2Dto1D_shr(int n, int16_t* d, const int16_t* s, intptr_t ss, int shift)
+{
+    tab().cu[log2i(n) - 2].cpy2Dto1D_shr(d, s, ss, shift);
+}
+
+void xo_cpy1Dto2D_shl(int n, int16_t* d, const int16_t* s, intptr_t ds, int shift)
+{
+    tab().cu[log2i(n) - 2].cpy1Dto2D_shl(d, s, ds, shift);
+}
+
+void xo_cpy1Dto2D_shr(int n, int16_t* d, const int16_t* s, intptr_t ds, int shift)
+{
+    tab().cu[log2i(n) - 2].cpy1Dto2D_shr(d, s, ds, shift);
+}
+
+int xo_count_nonzero(int n, const int16_t* q)
+{
+    return tab().cu[log2i(n) - 2].count_nonzero(q);
+}
+
+uint32_t xo_copy_cnt(int n, int16_t* coeff, const int16_t* res, intptr_t rs)
+{
+    return tab().cu[log2i(n) - 2].copy_cnt(coeff, res, rs);
+}
+
+void xo_transpose(int n, void* d, const void* s, intptr_t ss)
+{
+    tab().cu[log2i(n) - 2].transpose((pixel*)d, (const pixel*)s, ss);
+}
+
+void xo_denoise_dct(int16_t* coef, uint32_t* resSum, const uint16_t* offset, int num)
+{
+    tab().denoiseDct(coef, resSum, offset, num);
+}
+
+} // extern "C"

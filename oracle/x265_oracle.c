@@ -1,0 +1,759 @@
+/* x265_oracle.c — from-scratch CPU restatement of the x265 1.9 primitive table.
+ *
+ * TEST INFRASTRUCTURE ONLY (see x265_oracle.h): the checker and the CPU
+ * baseline, never part of the product.  Parity of this file with the
+ * reference is pinned two ways: the committed golden vectors
+ * in tests/golden/ (generated from the reference's own C primitives built by
+ * oracle/Makefile `ref`) and randomized cross-checks against that library.
+ *
+ * Compiled once per bit depth: -DXO_DEPTH=8 (pixel = uint8_t, sse_t = uint32)
+ * or -DXO_DEPTH=10 (pixel = uint16_t, sse_t = uint64), like the reference's
+ * HIGH_BIT_DEPTH builds (common.h:124-142).
+ *
+ * Each function cites the reference lines it restates; all paths are
+ * integer and follow the reference's truncation / clipping points exactly
+ * (SURVEY.md Appendix A).
+ */
+#include "x265_oracle.h"
+
+#include <stdlib.h>
+#include <string.h>
+
+#ifndef XO_DEPTH
+#define XO_DEPTH 8
+#endif
+
+#if XO_DEPTH > 8
+typedef uint16_t pix;
+typedef uint64_t sse_type;
+#else
+typedef uint8_t pix;
+typedef uint32_t sse_type;
+#endif
+
+#define PMAX ((1 << XO_DEPTH) - 1)
+#define FSTRIDE 64                 /* FENC_STRIDE, common.h:70 */
+#define IF_PREC 6                  /* IF_FILTER_PREC, constants.h:70-74 */
+#define IF_IPREC 14                /* IF_INTERNAL_PREC */
+#define IF_OFFS 8192               /* IF_INTERNAL_OFFS */
+
+static int clipp(int v) { return v < 0 ? 0 : (v > PMAX ? PMAX : v); }
+static int clip16(int v) { return v < -32768 ? -32768 : (v > 32767 ? 32767 : v); }
+static int ilog2(int n) { int l = 0; while ((1 << l) < n) l++; return l; }
+
+int xo_depth(void) { return XO_DEPTH; }
+
+/* ======================================================= pixel comparisons */
+
+/* pixel.cpp:39-54 */
+int xo_sad(int w, int h, const void* a_, intptr_t sa, const void* b_, intptr_t sb)
+{
+    const pix* a = (const pix*)a_;
+    const pix* b = (const pix*)b_;
+    int s = 0;
+    for (int y = 0; y < h; y++, a += sa, b += sb)
+        for (int x = 0; x < w; x++) s += abs((int)a[x] - (int)b[x]);
+    return s;
+}
+
+/* pixel.cpp:73-118: fenc uses FENC_STRIDE */
+void xo_sad_x3(int w, int h, const void* f, const void* r0, const void* r1, const void* r2, intptr_t rs, int32_t* res)
+{
+    res[0] = xo_sad(w, h, f, FSTRIDE, r0, rs);
+    res[1] = xo_sad(w, h, f, FSTRIDE, r1, rs);
+    res[2] = xo_sad(w, h, f, FSTRIDE, r2, rs);
+}
+
+void xo_sad_x4(int w, int h, const void* f, const void* r0, const void* r1, const void* r2, const void* r3,
+               intptr_t rs, int32_t* res)
+{
+    xo_sad_x3(w, h, f, r0, r1, r2, rs, res);
+    res[3] = xo_sad(w, h, f, FSTRIDE, r3, rs);
+}
+
+/* 4-point Hadamard butterfly (pixel.cpp:143-152) on ints */
+static void had4(int* v0, int* v1, int* v2, int* v3)
+{
+    int t0 = *v0 + *v1, t1 = *v0 - *v1, t2 = *v2 + *v3, t3 = *v2 - *v3;
+    *v0 = t0 + t2; *v2 = t0 - t2; *v1 = t1 + t3; *v3 = t1 - t3;
+}
+
+/* unrounded 4x4 Hadamard |coef| sum: satd_4x4 returns this >> 1 (pixel.cpp:163-189) */
+static int satd4_raw(const pix* a, intptr_t sa, const pix* b, intptr_t sb)
+{
+    int m[4][4];
+    for (int y = 0; y < 4; y++)
+        for (int x = 0; x < 4; x++) m[y][x] = (int)a[y * sa + x] - (int)b[y * sb + x];
+    for (int y = 0; y < 4; y++) had4(&m[y][0], &m[y][1], &m[y][2], &m[y][3]);
+    int s = 0;
+    for (int x = 0; x < 4; x++)
+    {
+        had4(&m[0][x], &m[1][x], &m[2][x], &m[3][x]);
+        s += abs(m[0][x]) + abs(m[1][x]) + abs(m[2][x]) + abs(m[3][x]);
+    }
+    return s;
+}
+
+/* satd over 4x4 tiles; the tiling (satd4 vs satd8, pixel.cpp:216-242) does not
+ * change the value because each tile's raw sum is even (SURVEY.md note a7) */
+int xo_satd(int w, int h, const void* a_, intptr_t sa, const void* b_, intptr_t sb)
+{
+    const pix* a = (const pix*)a_;
+    const pix* b = (const pix*)b_;
+    int s = 0;
+    for (int y = 0; y < h; y += 4)
+        for (int x = 0; x < w; x += 4) s += satd4_raw(a + y * sa + x, sa, b + y * sb + x, sb) >> 1;
+    return s;
+}
+
+/* unrounded 8x8 Hadamard |coef| sum (_sa8d_8x8, pixel.cpp:244-279) */
+static int sa8d8_raw(const pix* a, intptr_t sa, const pix* b, intptr_t sb)
+{
+    int m[8][8];
+    for (int y = 0; y < 8; y++)
+        for (int x = 0; x < 8; x++) m[y][x] = (int)a[y * sa + x] - (int)b[y * sb + x];
+    for (int pass = 0; pass < 2; pass++)
+    {
+        /* rows on pass 0, columns on pass 1: butterflies of span 1, 2, 4 */
+        for (int line = 0; line < 8; line++)
+            for (int span = 1; span < 8; span <<= 1)
+                for (int i = 0; i < 8; i++)
+                {
+                    if (i & span) continue;
+                    int* p = pass ? &m[i][line] : &m[line][i];
+                    int* q = pass ? &m[i + span][line] : &m[line][i + span];
+                    int u = *p, v = *q;
+                    *p = u + v;
+                    *q = u - v;
+                }
+    }
+    int s = 0;
+    for (int y = 0; y < 8; y++)
+        for (int x = 0; x < 8; x++) s += abs(m[y][x]);
+    return s;
+}
+
+/* cu[].sa8d as the table holds it (pixel.cpp:281-322, primitives.cpp:106,164-171) */
+int xo_sa8d(int w, int h, const void* a_, intptr_t sa, const void* b_, intptr_t sb)
+{
+    const pix* a = (const pix*)a_;
+    const pix* b = (const pix*)b_;
+    if ((w & 7) || (h & 7)) return xo_satd(w, h, a_, sa, b_, sb);
+    int s = 0;
+    if (!(w & 15) && !(h & 15))
+    {
+        for (int y = 0; y < h; y += 16)
+            for (int x = 0; x < w; x += 16)
+            {
+                int r = 0;
+                for (int k = 0; k < 4; k++)
+                {
+                    int oy = y + 8 * (k >> 1), ox = x + 8 * (k & 1);
+                    r += sa8d8_raw(a + oy * sa + ox, sa, b + oy * sb + ox, sb);
+                }
+                s += (r + 2) >> 2;
+            }
+    }
+    else
+    {
+        for (int y = 0; y < h; y += 8)
+            for (int x = 0; x < w; x += 8) s += (sa8d8_raw(a + y * sa + x, sa, b + y * sb + x, sb) + 2) >> 2;
+    }
+    return s;
+}
+
+/* pixel.cpp:120-139: sum in sse_t, each term an int product */
+uint64_t xo_sse_pp(int w, int h, const void* a_, intptr_t sa, const void* b_, intptr_t sb)
+{
+    const pix* a = (const pix*)a_;
+    const pix* b = (const pix*)b_;
+    sse_type s = 0;
+    for (int y = 0; y < h; y++, a += sa, b += sb)
+        for (int x = 0; x < w; x++)
+        {
+            int d = (int)a[x] - (int)b[x];
+            s += (sse_type)(uint32_t)(d * d);
+        }
+    return (uint64_t)s;
+}
+
+uint64_t xo_sse_ss(int w, int h, const int16_t* a, intptr_t sa, const int16_t* b, intptr_t sb)
+{
+    sse_type s = 0;
+    for (int y = 0; y < h; y++, a += sa, b += sb)
+        for (int x = 0; x < w; x++)
+        {
+            int d = a[x] - b[x];
+            s += (sse_type)(uint32_t)(d * d);
+        }
+    return (uint64_t)s;
+}
+
+/* pixel.cpp:324-336 */
+uint64_t xo_ssd_s(int n, const int16_t* a, intptr_t sa)
+{
+    sse_type s = 0;
+    for (int y = 0; y < n; y++, a += sa)
+        for (int x = 0; x < n; x++) s += (sse_type)(uint32_t)(a[x] * a[x]);
+    return (uint64_t)s;
+}
+
+/* AC energy of one block against a zero block (pixel.cpp:672-703) */
+static int psy_energy(int n, const pix* p, intptr_t s)
+{
+    static const pix zero[8] = { 0 };
+    if (n == 4)
+        return (satd4_raw(p, s, zero, 0) >> 1) - (xo_sad(4, 4, p, s, zero, 0) >> 2);
+    return ((sa8d8_raw(p, s, zero, 0) + 2) >> 2) - (xo_sad(8, 8, p, s, zero, 0) >> 2);
+}
+
+int xo_psy_cost_pp(int n, const void* src_, intptr_t ss, const void* rec_, intptr_t rs)
+{
+    const pix* src = (const pix*)src_;
+    const pix* rec = (const pix*)rec_;
+    if (n == 4) return abs(psy_energy(4, src, ss) - psy_energy(4, rec, rs));
+    uint32_t tot = 0;
+    for (int y = 0; y < n; y += 8)
+        for (int x = 0; x < n; x += 8)
+            tot += (uint32_t)abs(psy_energy(8, src + y * ss + x, ss) - psy_energy(8, rec + y * rs + x, rs));
+    return (int)tot;
+}
+
+/* pixel.cpp:649-666 */
+uint64_t xo_var(int n, const void* p_, intptr_t s)
+{
+    const pix* p = (const pix*)p_;
+    uint32_t sum = 0, sqr = 0;
+    for (int y = 0; y < n; y++, p += s)
+        for (int x = 0; x < n; x++) { sum += p[x]; sqr += (uint32_t)p[x] * p[x]; }
+    return sum + ((uint64_t)sqr << 32);
+}
+
+/* ======================================================= interpolation */
+
+static const int16_t kLuma[4][8] = { { 0, 0, 0, 64, 0, 0, 0, 0 }, { -1, 4, -10, 58, 17, -5, 1, 0 },
+                                     { -1, 4, -11, 40, 40, -11, 4, -1 }, { 0, 1, -5, 17, 58, -10, 4, -1 } };
+static const int16_t kChroma[8][4] = { { 0, 64, 0, 0 }, { -2, 58, 10, -2 }, { -4, 54, 16, -2 }, { -6, 46, 28, -4 },
+                                       { -4, 36, 36, -4 }, { -4, 28, 46, -6 }, { -2, 16, 54, -4 }, { -2, 10, 58, -2 } };
+
+static const int16_t* taps_of(int taps, int idx) { return taps == 8 ? kLuma[idx] : kChroma[idx]; }
+
+/* ipfilter.cpp:120-163 horizontal pixel -> int16, optional row extension */
+static void h_ps(int taps, int w, int h, const pix* src, intptr_t ss, int16_t* dst, intptr_t ds, int ci, int rowext)
+{
+    const int16_t* c = taps_of(taps, ci);
+    const int head = IF_IPREC - XO_DEPTH, shift = IF_PREC - head, off = -IF_OFFS * (1 << shift);
+    int rows = h;
+    src -= taps / 2 - 1;
+    if (rowext) { src -= (taps / 2 - 1) * ss; rows += taps - 1; }
+    for (int y = 0; y < rows; y++, src += ss, dst += ds)
+        for (int x = 0; x < w; x++)
+        {
+            int s = 0;
+            for (int k = 0; k < taps; k++) s += src[x + k] * c[k];
+            dst[x] = (int16_t)((s + off) >> shift);
+        }
+}
+
+/* ipfilter.cpp:244-285 (and filterVertical_sp_c :322-363) int16 -> pixel */
+static void v_sp(int taps, int w, int h, const int16_t* src, intptr_t ss, pix* dst, intptr_t ds, int ci)
+{
+    const int16_t* c = taps_of(taps, ci);
+    const int head = IF_IPREC - XO_DEPTH, shift = IF_PREC + head;
+    const int off = (1 << (shift - 1)) + (IF_OFFS << IF_PREC);
+    src -= (taps / 2 - 1) * ss;
+    for (int y = 0; y < h; y++, src += ss, dst += ds)
+        for (int x = 0; x < w; x++)
+        {
+            int s = 0;
+            for (int k = 0; k < taps; k++) s += src[x + k * ss] * c[k];
+            dst[x] = (pix)clipp((int16_t)((s + off) >> shift));
+        }
+}
+
+void xo_interp(int op, int taps, int w, int h, const void* src_, intptr_t ss, void* dst_, intptr_t ds, int ci, int extra)
+{
+    const pix* sp = (const pix*)src_;
+    const int16_t* s16 = (const int16_t*)src_;
+    pix* dp = (pix*)dst_;
+    int16_t* d16 = (int16_t*)dst_;
+    const int head = IF_IPREC - XO_DEPTH;
+    const int16_t* c = taps_of(taps, ci & (taps == 8 ? 3 : 7));
+
+    switch (op)
+    {
+    case XO_HPP: /* ipfilter.cpp:79-118 */
+        sp -= taps / 2 - 1;
+        for (int y = 0; y < h; y++, sp += ss, dp += ds)
+            for (int x = 0; x < w; x++)
+            {
+                int s = 0;
+                for (int k = 0; k < taps; k++) s += sp[x + k] * c[k];
+                dp[x] = (pix)clipp((int16_t)((s + 32) >> IF_PREC));
+            }
+        return;
+    case XO_HPS:
+        h_ps(taps, w, h, sp, ss, d16, ds, ci, extra);
+        return;
+    case XO_VPP: /* ipfilter.cpp:165-204 */
+        sp -= (taps / 2 - 1) * ss;
+        for (int y = 0; y < h; y++, sp += ss, dp += ds)
+            for (int x = 0; x < w; x++)
+            {
+                int s = 0;
+                for (int k = 0; k < taps; k++) s += sp[x + k * ss] * c[k];
+                dp[x] = (pix)clipp((int16_t)((s + 32) >> IF_PREC));
+            }
+        return;
+    case XO_VPS: /* ipfilter.cpp:206-242 */
+    {
+        const int shift = IF_PREC - head, off = -IF_OFFS * (1 << shift);
+        sp -= (taps / 2 - 1) * ss;
+        for (int y = 0; y < h; y++, sp += ss, d16 += ds)
+            for (int x = 0; x < w; x++)
+            {
+                int s = 0;
+                for (int k = 0; k < taps; k++) s += sp[x + k * ss] * c[k];
+                d16[x] = (int16_t)((s + off) >> shift);
+            }
+        return;
+    }
+    case XO_VSP:
+        v_sp(taps, w, h, s16, ss, dp, ds, ci);
+        return;
+    case XO_VSS: /* ipfilter.cpp:287-320 */
+        s16 -= (taps / 2 - 1) * ss;
+        for (int y = 0; y < h; y++, s16 += ss, d16 += ds)
+            for (int x = 0; x < w; x++)
+            {
+                int s = 0;
+                for (int k = 0; k < taps; k++) s += s16[x + k * ss] * c[k];
+                d16[x] = (int16_t)(s >> IF_PREC);
+            }
+        return;
+    case XO_HVPP: /* ipfilter.cpp:365-372: hps with row extension, then vertical sp */
+    {
+        int16_t* im = (int16_t*)malloc(sizeof(int16_t) * w * (h + taps - 1));
+        h_ps(taps, w, h, sp, ss, im, w, ci, 1);
+        v_sp(taps, w, h, im + (taps / 2 - 1) * w, w, dp, ds, extra);
+        free(im);
+        return;
+    }
+    case XO_P2S: /* ipfilter.cpp:40-57 */
+        for (int y = 0; y < h; y++, sp += ss, d16 += ds)
+            for (int x = 0; x < w; x++)
+            {
+                int16_t v = (int16_t)(sp[x] << head);
+                d16[x] = (int16_t)(v - (int16_t)IF_OFFS);
+            }
+        return;
+    }
+}
+
+/* ======================================================= transforms */
+
+/* HEVC matrix generated from the spec rule (see csrc/tables.h) */
+static int tmat(int N, int k, int n)
+{
+    static const int mag[33] = { 64, 90, 90, 90, 89, 88, 87, 85, 83, 82, 80, 78, 75, 73, 70, 67,
+                                 64, 61, 57, 54, 50, 46, 43, 38, 36, 31, 25, 22, 18, 13, 9, 4, 0 };
+    int a = ((k * (32 / N)) * (2 * n + 1)) & 127;
+    return a <= 32 ? mag[a] : a <= 64 ? -mag[64 - a] : a <= 96 ? -mag[a - 64] : mag[128 - a];
+}
+
+/* one forward stage (partialButterflyN, dct.cpp:83-240,418-440) as an exact
+ * matrix product: out[k*N + j] = round(sum_n T[k][n] * in[j*N + n]) */
+static void fwd_stage(int N, const int16_t* in, int16_t* out, int shift)
+{
+    for (int j = 0; j < N; j++)
+        for (int k = 0; k < N; k++)
+        {
+            int s = 0;
+            for (int n = 0; n < N; n++) s += tmat(N, k, n) * in[j * N + n];
+            out[k * N + j] = (int16_t)((s + (1 << (shift - 1))) >> shift);
+        }
+}
+
+/* one inverse stage (partialButterflyInverseN, dct.cpp:242-416):
+ * out[j*N + k] = clip(round(sum_m T[m][k] * in[m*N + j])) */
+static void inv_stage(int N, const int16_t* in, int16_t* out, int shift)
+{
+    for (int j = 0; j < N; j++)
+        for (int k = 0; k < N; k++)
+        {
+            int s = 0;
+            for (int m = 0; m < N; m++) s += tmat(N, m, k) * in[m * N + j];
+            out[j * N + k] = (int16_t)clip16((s + (1 << (shift - 1))) >> shift);
+        }
+}
+
+/* DST-VII forward / inverse stages (fastForwardDst / inversedst, dct.cpp:41-81) */
+static void dst_fwd_stage(const int16_t* b, int16_t* o, int shift)
+{
+    const int rnd = 1 << (shift - 1);
+    for (int i = 0; i < 4; i++)
+    {
+        const int16_t* r = b + 4 * i;
+        int c0 = r[0] + r[3], c1 = r[1] + r[3], c2 = r[0] - r[1], c3 = 74 * r[2];
+        o[i] = (int16_t)((29 * c0 + 55 * c1 + c3 + rnd) >> shift);
+        o[4 + i] = (int16_t)((74 * (r[0] + r[1] - r[3]) + rnd) >> shift);
+        o[8 + i] = (int16_t)((29 * c2 + 55 * c0 - c3 + rnd) >> shift);
+        o[12 + i] = (int16_t)((55 * c2 - 29 * c1 + c3 + rnd) >> shift);
+    }
+}
+
+static void dst_inv_stage(const int16_t* t, int16_t* o, int shift)
+{
+    const int rnd = 1 << (shift - 1);
+    for (int i = 0; i < 4; i++)
+    {
+        int c0 = t[i] + t[8 + i], c1 = t[8 + i] + t[12 + i], c2 = t[i] - t[12 + i], c3 = 74 * t[4 + i];
+        o[4 * i + 0] = (int16_t)clip16((29 * c0 + 55 * c1 + c3 + rnd) >> shift);
+        o[4 * i + 1] = (int16_t)clip16((55 * c2 - 29 * c1 + c3 + rnd) >> shift);
+        o[4 * i + 2] = (int16_t)clip16((74 * (t[i] - t[8 + i] + t[12 + i]) + rnd) >> shift);
+        o[4 * i + 3] = (int16_t)clip16((55 * c0 + 29 * c2 - c3 + rnd) >> shift);
+    }
+}
+
+/* dct.cpp:442-610 */
+void xo_dct(int kind, int n, const int16_t* src, int16_t* dst, intptr_t stride)
+{
+    int16_t a[32 * 32], b[32 * 32];
+    const int lg = ilog2(n);
+    if (kind == XO_DCT || kind == XO_DST)
+    {
+        for (int y = 0; y < n; y++) memcpy(a + y * n, src + y * stride, n * sizeof(int16_t));
+        const int s1 = lg - 1 + (XO_DEPTH - 8), s2 = lg + 6;
+        if (kind == XO_DST) { dst_fwd_stage(a, b, s1); dst_fwd_stage(b, dst, s2); }
+        else { fwd_stage(n, a, b, s1); fwd_stage(n, b, dst, s2); }
+    }
+    else
+    {
+        const int s1 = 7, s2 = 12 - (XO_DEPTH - 8);
+        if (kind == XO_IDST) { dst_inv_stage(src, a, s1); dst_inv_stage(a, b, s2); }
+        else { inv_stage(n, src, a, s1); inv_stage(n, a, b, s2); }
+        for (int y = 0; y < n; y++) memcpy(dst + y * stride, b + y * n, n * sizeof(int16_t));
+    }
+}
+
+/* dct.cpp:664-686 (int32 products wrap like the reference's int arithmetic) */
+uint32_t xo_quant(const int16_t* coef, const int32_t* qc, int32_t* deltaU, int16_t* qout, int qBits, int add, int num)
+{
+    uint32_t sig = 0;
+    for (int i = 0; i < num; i++)
+    {
+        int lv = coef[i];
+        uint32_t tmp = (uint32_t)abs(lv) * (uint32_t)qc[i];
+        int level = (int)(tmp + (uint32_t)add) >> qBits;
+        deltaU[i] = (int)(tmp - ((uint32_t)level << qBits)) >> (qBits - 8);
+        sig += level != 0;
+        if (lv < 0) level = -level;
+        qout[i] = (int16_t)clip16(level);
+    }
+    return sig;
+}
+
+/* dct.cpp:688-713 */
+uint32_t xo_nquant(const int16_t* coef, const int32_t* qc, int16_t* qout, int qBits, int add, int num)
+{
+    uint32_t sig = 0;
+    for (int i = 0; i < num; i++)
+    {
+        int lv = coef[i];
+        uint32_t tmp = (uint32_t)abs(lv) * (uint32_t)qc[i];
+        int level = (int)(tmp + (uint32_t)add) >> qBits;
+        sig += level != 0;
+        if (lv < 0) level = -level;
+        qout[i] = (int16_t)abs(clip16(level));
+    }
+    return sig;
+}
+
+/* dct.cpp:612-634 */
+void xo_dequant_normal(const int16_t* q, int16_t* coef, int num, int scale, int shift)
+{
+    const int add = 1 << (shift - 1);
+    for (int i = 0; i < num; i++) coef[i] = (int16_t)clip16((q[i] * scale + add) >> shift);
+}
+
+/* dct.cpp:636-662 */
+void xo_dequant_scaling(const int16_t* q, const int32_t* dq, int16_t* coef, int num, int per, int shift)
+{
+    shift += 4;
+    if (shift > per)
+    {
+        const int add = 1 << (shift - per - 1);
+        for (int i = 0; i < num; i++) coef[i] = (int16_t)clip16((q[i] * dq[i] + add) >> (shift - per));
+    }
+    else
+        for (int i = 0; i < num; i++) coef[i] = (int16_t)clip16(clip16(q[i] * dq[i]) << (per - shift));
+}
+
+/* ======================================================= intra */
+
+/* intrapred.cpp:31-51 */
+void xo_intra_filter(int n, const void* ref_, void* filt_)
+{
+    const pix* s = (const pix*)ref_;
+    pix* f = (pix*)filt_;
+    const int n2 = 2 * n, n4 = 4 * n;
+    for (int i = 0; i <= n4; i++)
+    {
+        int v;
+        if (i == n2 || i == n4) v = s[i];
+        else if (i == 0) v = (2 * s[0] + s[1] + s[n2 + 1] + 2) >> 2;
+        else if (i == n2 + 1) v = (2 * s[n2 + 1] + s[0] + s[n2 + 2] + 2) >> 2;
+        else v = (2 * s[i] + s[i - 1] + s[i + 1] + 2) >> 2;
+        f[i] = (pix)v;
+    }
+}
+
+static const int kAngle[17] = { -32, -26, -21, -17, -13, -9, -5, -2, 0, 2, 5, 9, 13, 17, 21, 26, 32 };
+static const int kInvAngle[8] = { 4096, 1638, 910, 630, 482, 390, 315, 256 };
+
+/* angular prediction in the vertical frame into out[y*os + x]
+ * (intra_pred_ang_c, intrapred.cpp:102-189, before the horizontal transpose) */
+static void ang_vertical_frame(int n, int mode, const pix* src0, int bfilter, pix* out, intptr_t os)
+{
+    const int n2 = 2 * n;
+    const int hor = mode < 18;
+    pix nb[129];
+    const pix* s = src0;
+    if (hor)
+    {
+        nb[0] = src0[0];
+        for (int i = 0; i < n2; i++) { nb[1 + i] = src0[n2 + 1 + i]; nb[n2 + 1 + i] = src0[1 + i]; }
+        s = nb;
+    }
+    const int aoff = hor ? 10 - mode : mode - 26;
+    const int angle = kAngle[8 + aoff];
+    if (!angle)
+    {
+        for (int y = 0; y < n; y++)
+            for (int x = 0; x < n; x++) out[y * os + x] = s[1 + x];
+        if (bfilter)
+            for (int y = 0; y < n; y++) out[y * os] = (pix)clipp((int16_t)(s[1] + ((s[n2 + 1 + y] - s[0]) >> 1)));
+        return;
+    }
+    /* reference array with index -n..2n, stored at ref[idx + 64] */
+    int ref[200];
+    for (int i = 0; i < n2; i++) ref[64 + i] = s[1 + i];
+    ref[63] = s[0];
+    if (angle < 0)
+    {
+        const int nproj = -((n * angle) >> 5) - 1, inv = kInvAngle[-aoff - 1];
+        int acc = 128;
+        for (int k = 0; k < nproj; k++)
+        {
+            acc += inv;
+            ref[64 - 2 - k] = s[n2 + (acc >> 8)];
+        }
+    }
+    for (int y = 0; y < n; y++)
+    {
+        const int sum = (y + 1) * angle, off = sum >> 5, f = sum & 31;
+        for (int x = 0; x < n; x++)
+        {
+            const int a = ref[64 + off + x];
+            out[y * os + x] = (pix)(f ? ((32 - f) * a + f * ref[64 + off + x + 1] + 16) >> 5 : a);
+        }
+    }
+}
+
+void xo_intra_pred(int n, int mode, void* dst_, intptr_t ds, const void* src_, int bFilter)
+{
+    pix* dst = (pix*)dst_;
+    const pix* s = (const pix*)src_;
+    const pix* above = s + 1;
+    const pix* left = s + 2 * n + 1;
+    if (mode == 0) /* planar, intrapred.cpp:87-100 */
+    {
+        const int lg = ilog2(n);
+        for (int y = 0; y < n; y++)
+            for (int x = 0; x < n; x++)
+                dst[y * ds + x] = (pix)(((n - 1 - x) * left[y] + (n - 1 - y) * above[x] + (x + 1) * above[n] +
+                                         (y + 1) * left[n] + n) >> (lg + 1));
+        return;
+    }
+    if (mode == 1) /* DC, intrapred.cpp:53-85 */
+    {
+        int dc = n;
+        for (int i = 0; i < n; i++) dc += above[i] + left[i];
+        dc /= 2 * n;
+        for (int y = 0; y < n; y++)
+            for (int x = 0; x < n; x++) dst[y * ds + x] = (pix)dc;
+        if (bFilter)
+        {
+            dst[0] = (pix)((above[0] + left[0] + 2 * dc + 2) >> 2);
+            for (int x = 1; x < n; x++) dst[x] = (pix)((above[x] + 3 * dc + 2) >> 2);
+            for (int y = 1; y < n; y++) dst[y * ds] = (pix)((left[y] + 3 * dc + 2) >> 2);
+        }
+        return;
+    }
+    pix tmp[32 * 32];
+    ang_vertical_frame(n, mode, s, bFilter, tmp, n);
+    for (int y = 0; y < n; y++)
+        for (int x = 0; x < n; x++) dst[y * ds + x] = mode < 18 ? tmp[x * n + y] : tmp[y * n + x];
+}
+
+/* intrapred.cpp:206-234: horizontal modes are stored un-transposed */
+void xo_intra_allangs(int n, void* dst_, void* ref, void* filt, int bLuma)
+{
+    static const uint8_t flags[35] = { 0x38, 0x00, 0x38, 0x30, 0x30, 0x30, 0x30, 0x30, 0x30, 0x20, 0x00, 0x20,
+                                       0x30, 0x30, 0x30, 0x30, 0x30, 0x30, 0x38, 0x30, 0x30, 0x30, 0x30, 0x30,
+                                       0x30, 0x20, 0x00, 0x20, 0x30, 0x30, 0x30, 0x30, 0x30, 0x30, 0x38 };
+    pix* dst = (pix*)dst_;
+    for (int mode = 2; mode <= 34; mode++)
+    {
+        const pix* s = (flags[mode] & n) ? (const pix*)filt : (const pix*)ref;
+        ang_vertical_frame(n, mode, s, bLuma, dst + (mode - 2) * n * n, n);
+    }
+}
+
+/* ======================================================= companions */
+
+/* pixel.cpp:416-428 */
+void xo_calcresidual(int n, const void* fenc, const void* pred, int16_t* res, intptr_t stride)
+{
+    xo_sub_ps(n, n, res, stride, fenc, pred, stride, stride);
+}
+
+/* pixel.cpp:760-772 */
+void xo_sub_ps(int w, int h, int16_t* d, intptr_t ds, const void* a_, const void* b_, intptr_t sa, intptr_t sb)
+{
+    const pix* a = (const pix*)a_;
+    const pix* b = (const pix*)b_;
+    for (int y = 0; y < h; y++, a += sa, b += sb, d += ds)
+        for (int x = 0; x < w; x++) d[x] = (int16_t)((int)a[x] - (int)b[x]);
+}
+
+/* pixel.cpp:774-786 */
+void xo_add_ps(int w, int h, void* d_, intptr_t ds, const void* a_, const int16_t* b, intptr_t sa, intptr_t sb)
+{
+    pix* d = (pix*)d_;
+    const pix* a = (const pix*)a_;
+    for (int y = 0; y < h; y++, a += sa, b += sb, d += ds)
+        for (int x = 0; x < w; x++) d[x] = (pix)clipp(a[x] + b[x]);
+}
+
+/* pixel.cpp:788-808 */
+void xo_addavg(int w, int h, const int16_t* a, const int16_t* b, void* d_, intptr_t sa, intptr_t sb, intptr_t ds)
+{
+    pix* d = (pix*)d_;
+    const int shift = IF_IPREC + 1 - XO_DEPTH, off = (1 << (shift - 1)) + 2 * IF_OFFS;
+    for (int y = 0; y < h; y++, a += sa, b += sb, d += ds)
+        for (int x = 0; x < w; x++) d[x] = (pix)clipp((a[x] + b[x] + off) >> shift);
+}
+
+/* pixel.cpp:490-502 */
+void xo_pixelavg(int w, int h, void* d_, intptr_t ds, const void* a_, intptr_t sa, const void* b_, intptr_t sb)
+{
+    pix* d = (pix*)d_;
+    const pix* a = (const pix*)a_;
+    const pix* b = (const pix*)b_;
+    for (int y = 0; y < h; y++, a += sa, b += sb, d += ds)
+        for (int x = 0; x < w; x++) d[x] = (pix)((a[x] + b[x] + 1) >> 1);
+}
+
+/* pixel.cpp:705-758 */
+void xo_copy_pp(int w, int h, void* d_, intptr_t ds, const void* s_, intptr_t ss)
+{
+    pix* d = (pix*)d_;
+    const pix* s = (const pix*)s_;
+    for (int y = 0; y < h; y++) memcpy(d + y * ds, s + y * ss, w * sizeof(pix));
+}
+
+void xo_copy_sp(int w, int h, void* d_, intptr_t ds, const int16_t* s, intptr_t ss)
+{
+    pix* d = (pix*)d_;
+    for (int y = 0; y < h; y++, d += ds, s += ss)
+        for (int x = 0; x < w; x++) d[x] = (pix)s[x];
+}
+
+void xo_copy_ps(int w, int h, int16_t* d, intptr_t ds, const void* s_, intptr_t ss)
+{
+    const pix* s = (const pix*)s_;
+    for (int y = 0; y < h; y++, d += ds, s += ss)
+        for (int x = 0; x < w; x++) d[x] = (int16_t)s[x];
+}
+
+void xo_copy_ss(int w, int h, int16_t* d, intptr_t ds, const int16_t* s, intptr_t ss)
+{
+    for (int y = 0; y < h; y++) memcpy(d + y * ds, s + y * ss, w * sizeof(int16_t));
+}
+
+/* pixel.cpp:338-344 */
+void xo_blockfill_s(int n, int16_t* d, intptr_t ds, int16_t v)
+{
+    for (int y = 0; y < n; y++)
+        for (int x = 0; x < n; x++) d[y * ds + x] = v;
+}
+
+/* pixel.cpp:346-414 */
+void xo_cpy2Dto1D_shl(int n, int16_t* d, const int16_t* s, intptr_t ss, int shift)
+{
+    for (int y = 0; y < n; y++)
+        for (int x = 0; x < n; x++) d[y * n + x] = (int16_t)(s[y * ss + x] << shift);
+}
+
+void xo_cpy2Dto1D_shr(int n, int16_t* d, const int16_t* s, intptr_t ss, int shift)
+{
+    const int16_t rnd = (int16_t)(1 << (shift - 1));
+    for (int y = 0; y < n; y++)
+        for (int x = 0; x < n; x++) d[y * n + x] = (int16_t)((s[y * ss + x] + rnd) >> shift);
+}
+
+void xo_cpy1Dto2D_shl(int n, int16_t* d, const int16_t* s, intptr_t ds, int shift)
+{
+    for (int y = 0; y < n; y++)
+        for (int x = 0; x < n; x++) d[y * ds + x] = (int16_t)(s[y * n + x] << shift);
+}
+
+void xo_cpy1Dto2D_shr(int n, int16_t* d, const int16_t* s, intptr_t ds, int shift)
+{
+    const int16_t rnd = (int16_t)(1 << (shift - 1));
+    for (int y = 0; y < n; y++)
+        for (int x = 0; x < n; x++) d[y * ds + x] = (int16_t)((s[y * n + x] + rnd) >> shift);
+}
+
+/* dct.cpp:714-742 */
+int xo_count_nonzero(int n, const int16_t* q)
+{
+    int c = 0;
+    for (int i = 0; i < n * n; i++) c += q[i] != 0;
+    return c;
+}
+
+uint32_t xo_copy_cnt(int n, int16_t* coeff, const int16_t* res, intptr_t rs)
+{
+    uint32_t c = 0;
+    for (int y = 0; y < n; y++)
+        for (int x = 0; x < n; x++)
+        {
+            coeff[y * n + x] = res[y * rs + x];
+            c += res[y * rs + x] != 0;
+        }
+    return c;
+}
+
+/* pixel.cpp:430-436 */
+void xo_transpose(int n, void* d_, const void* s_, intptr_t ss)
+{
+    pix* d = (pix*)d_;
+    const pix* s = (const pix*)s_;
+    for (int k = 0; k < n; k++)
+        for (int l = 0; l < n; l++) d[k * n + l] = s[l * ss + k];
+}
+
+/* dct.cpp:744-755 */
+void xo_denoise_dct(int16_t* coef, uint32_t* resSum, const uint16_t* offset, int num)
+{
+    for (int i = 0; i < num; i++)
+    {
+        int lv = coef[i], sg = lv >> 31;
+        lv = (lv + sg) ^ sg;
+        resSum[i] += lv;
+        lv -= offset[i];
+        coef[i] = (int16_t)(lv < 0 ? 0 : (lv ^ sg) - sg);
+    }
+}

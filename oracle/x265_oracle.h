@@ -1,0 +1,100 @@
+/* x265_oracle.h — flat C API of the CPU oracle for the x265 1.9 primitive table.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Nothing under oracle/ is part of the product:
+ * only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may
+ * load these libraries, and only as the checker / CPU baseline.
+ *
+ * Two libraries export this exact API, so one set of Python bindings can
+ * drive both:
+ *   oracle/_build/liboracle{8,10}.so  — from-scratch C restatement (x265_oracle.c)
+ *   oracle/_ref/libx265ref{8,10}.so   — the reference's own C primitives compiled
+ *                                       from /root/reference (ref_shim.cpp)
+ *
+ * Every function is one call of one EncoderPrimitives entry
+ * (reference: x265_1.9/source/common/primitives.h:203-381).  Pixels are
+ * `pixel` of the library's depth (uint8_t at 8-bit, uint16_t at 10-bit) and are
+ * passed as void*.  Strides are in elements, as in the reference.
+ */
+#ifndef X265_ORACLE_H
+#define X265_ORACLE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+int      xo_depth(void);
+
+/* pixel.cpp:39-322 — sad / sad_x3 / sad_x4 / satd / sa8d.  sad_x3/x4 read fenc
+ * with the fixed FENC_STRIDE = 64 (pixel.cpp:88,112). */
+int      xo_sad(int w, int h, const void* a, intptr_t sa, const void* b, intptr_t sb);
+void     xo_sad_x3(int w, int h, const void* fenc, const void* r0, const void* r1,
+                   const void* r2, intptr_t rs, int32_t* res);
+void     xo_sad_x4(int w, int h, const void* fenc, const void* r0, const void* r1,
+                   const void* r2, const void* r3, intptr_t rs, int32_t* res);
+int      xo_satd(int w, int h, const void* a, intptr_t sa, const void* b, intptr_t sb);
+/* sa8d as the table holds it: satd for sizes not a multiple of 8, one rounding
+ * per 16x16 when both dims are multiples of 16, else one rounding per 8x8. */
+int      xo_sa8d(int w, int h, const void* a, intptr_t sa, const void* b, intptr_t sb);
+
+/* pixel.cpp:120-139, 324-336, 649-703 */
+uint64_t xo_sse_pp(int w, int h, const void* a, intptr_t sa, const void* b, intptr_t sb);
+uint64_t xo_sse_ss(int w, int h, const int16_t* a, intptr_t sa, const int16_t* b, intptr_t sb);
+uint64_t xo_ssd_s(int n, const int16_t* a, intptr_t sa);
+int      xo_psy_cost_pp(int n, const void* src, intptr_t ss, const void* rec, intptr_t rs);
+uint64_t xo_var(int n, const void* p, intptr_t s);
+
+/* ipfilter.cpp:40-372.  taps = 8 (luma) or 4 (chroma).
+ * extra = isRowExt for HPS, idxY for HVPP (luma only), ignored otherwise. */
+enum { XO_HPP = 0, XO_HPS, XO_VPP, XO_VPS, XO_VSP, XO_VSS, XO_HVPP, XO_P2S };
+void     xo_interp(int op, int taps, int w, int h, const void* src, intptr_t ss,
+                   void* dst, intptr_t ds, int coeffIdx, int extra);
+
+/* dct.cpp:442-610.  DCT/DST read src with `stride`, write N*N contiguous;
+ * IDCT/IDST read N*N contiguous, write dst with `stride`. */
+enum { XO_DCT = 0, XO_IDCT, XO_DST, XO_IDST };
+void     xo_dct(int kind, int n, const int16_t* src, int16_t* dst, intptr_t stride);
+
+/* dct.cpp:612-713 */
+uint32_t xo_quant(const int16_t* coef, const int32_t* qcoef, int32_t* deltaU, int16_t* qout,
+                  int qBits, int add, int numCoeff);
+uint32_t xo_nquant(const int16_t* coef, const int32_t* qcoef, int16_t* qout,
+                   int qBits, int add, int numCoeff);
+void     xo_dequant_normal(const int16_t* q, int16_t* coef, int num, int scale, int shift);
+void     xo_dequant_scaling(const int16_t* q, const int32_t* dq, int16_t* coef, int num,
+                            int per, int shift);
+
+/* intrapred.cpp:31-234.  n = TU size 4..32. */
+void     xo_intra_filter(int n, const void* ref, void* filt);
+void     xo_intra_pred(int n, int mode, void* dst, intptr_t ds, const void* src, int bFilter);
+void     xo_intra_allangs(int n, void* dst, void* ref, void* filt, int bLuma);
+
+/* companions (pixel.cpp:338-436, 490-502, 705-808; dct.cpp:714-755) */
+void     xo_calcresidual(int n, const void* fenc, const void* pred, int16_t* res, intptr_t stride);
+void     xo_sub_ps(int w, int h, int16_t* d, intptr_t ds, const void* a, const void* b,
+                   intptr_t sa, intptr_t sb);
+void     xo_add_ps(int w, int h, void* d, intptr_t ds, const void* a, const int16_t* b,
+                   intptr_t sa, intptr_t sb);
+void     xo_addavg(int w, int h, const int16_t* a, const int16_t* b, void* d,
+                   intptr_t sa, intptr_t sb, intptr_t ds);
+void     xo_pixelavg(int w, int h, void* d, intptr_t ds, const void* a, intptr_t sa,
+                     const void* b, intptr_t sb);
+void     xo_copy_pp(int w, int h, void* d, intptr_t ds, const void* s, intptr_t ss);
+void     xo_copy_sp(int w, int h, void* d, intptr_t ds, const int16_t* s, intptr_t ss);
+void     xo_copy_ps(int w, int h, int16_t* d, intptr_t ds, const void* s, intptr_t ss);
+void     xo_copy_ss(int w, int h, int16_t* d, intptr_t ds, const int16_t* s, intptr_t ss);
+void     xo_blockfill_s(int n, int16_t* d, intptr_t ds, int16_t v);
+void     xo_cpy2Dto1D_shl(int n, int16_t* d, const int16_t* s, intptr_t ss, int shift);
+void     xo_cpy2Dto1D_shr(int n, int16_t* d, const int16_t* s, intptr_t ss, int shift);
+void     xo_cpy1Dto2D_shl(int n, int16_t* d, const int16_t* s, intptr_t ds, int shift);
+void     xo_cpy1Dto2D_shr(int n, int16_t* d, const int16_t* s, intptr_t ds, int shift);
+int      xo_count_nonzero(int n, const int16_t* q);
+uint32_t xo_copy_cnt(int n, int16_t* coeff, const int16_t* res, intptr_t rs);
+void     xo_transpose(int n, void* d, const void* s, intptr_t ss);
+void     xo_denoise_dct(int16_t* coef, uint32_t* resSum, const uint16_t* offset, int num);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

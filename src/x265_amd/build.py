@@ -1,0 +1,64 @@
+"""Build the gfx950 primitive library (libx265amd.so) in-tree with hipcc.
+
+One code object per source file (compiled in parallel), linked into a single
+shared library next to this file so it travels with the repository snapshot
+to the GPU box.  No JIT cache, no torch extension machinery: the product is a
+plain C-ABI shared library (include/x265_amd.h).
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+OBJ = os.path.join(HERE, "_obj")
+LIB = os.path.join(HERE, "libx265amd.so")
+SOURCES = ["pixel.hip", "interp.hip", "transform.hip", "intra.hip", "blockops.hip", "runtime.hip"]
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-Wno-unused-command-line-argument"]
+
+
+def _newer(target: str, deps) -> bool:
+    if not os.path.exists(target):
+        return False
+    t = os.path.getmtime(target)
+    return all(os.path.getmtime(d) <= t for d in deps)
+
+
+def _headers():
+    inc = os.path.join(os.path.dirname(os.path.dirname(HERE)), "include", "x265_amd.h")
+    return [os.path.join(CSRC, h) for h in os.listdir(CSRC) if h.endswith(".h")] + [inc]
+
+
+def _compile(src: str) -> str:
+    out = os.path.join(OBJ, src.replace(".hip", ".o"))
+    deps = [os.path.join(CSRC, src)] + _headers()
+    if _newer(out, deps):
+        return out
+    cmd = [HIPCC, *FLAGS, "-c", os.path.join(CSRC, src), "-o", out]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed for {src}:\n{r.stdout}\n{r.stderr}")
+    return out
+
+
+def build(verbose: bool = True) -> str:
+    os.makedirs(OBJ, exist_ok=True)
+    jobs = min(len(SOURCES), max(1, (os.cpu_count() or 4)), 8)
+    with cf.ThreadPoolExecutor(jobs) as ex:
+        objs = list(ex.map(_compile, SOURCES))
+    if not _newer(LIB, objs):
+        cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", LIB, *objs]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
+    if verbose:
+        print(f"[x265amd] built {LIB}", file=sys.stderr)
+    return LIB
+
+
+if __name__ == "__main__":
+    build()

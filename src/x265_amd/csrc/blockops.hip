@@ -1,0 +1,174 @@
+// blockops.hip — batched companion block operations of the primitive table
+// (SURVEY.md §8(a) row a15): residual / reconstruction / bi-prediction
+// averages / typed block copies / fills / 2D<->1D shifted copies / transpose.
+//
+// Reference semantics: x265_1.9/source/common/pixel.cpp
+//   blockfill_s_c :338-344   cpy2Dto1D_shl/shr :346-379   cpy1Dto2D_shl/shr :381-414
+//   getResidual :416-428     transpose :430-436           pixelavg_pp :490-502
+//   blockcopy_pp/ss/sp/ps :705-758   pixel_sub_ps_c :760-772   pixel_add_ps_c :774-786
+//   addAvg :788-808 (shiftNum = IF_INTERNAL_PREC + 1 - depth, offset includes 2*IF_INTERNAL_OFFS)
+//
+// Work mapping: one block per G-lane group, a lane handles UW (8/4/2)
+// contiguous elements of one row per step, loads and stores vectorised.
+#include "common.h"
+#include "../../../include/x265_amd.h"
+
+namespace x265amd {
+
+template <typename P, int OP>
+struct OpTypes;
+#define OPT(OP, D, A, B) template <typename P> struct OpTypes<P, OP> { typedef D d; typedef A a; typedef B b; };
+OPT(X265AMD_SUB_PS, int16_t, P, P)
+OPT(X265AMD_ADD_PS, P, P, int16_t)
+OPT(X265AMD_ADDAVG, P, int16_t, int16_t)
+OPT(X265AMD_PIXELAVG, P, P, P)
+OPT(X265AMD_COPY_PP, P, P, P)
+OPT(X265AMD_COPY_SP, P, int16_t, int16_t)
+OPT(X265AMD_COPY_PS, int16_t, P, P)
+OPT(X265AMD_COPY_SS, int16_t, int16_t, int16_t)
+OPT(X265AMD_BLOCKFILL, int16_t, int16_t, int16_t)
+OPT(X265AMD_CPY2D1D_SHL, int16_t, int16_t, int16_t)
+OPT(X265AMD_CPY2D1D_SHR, int16_t, int16_t, int16_t)
+OPT(X265AMD_CPY1D2D_SHL, int16_t, int16_t, int16_t)
+OPT(X265AMD_CPY1D2D_SHR, int16_t, int16_t, int16_t)
+OPT(X265AMD_TRANSPOSE, P, P, P)
+#undef OPT
+
+template <typename T, int UW>
+__device__ __forceinline__ void ld(const T* p, int (&o)[UW])
+{
+    if constexpr (std::is_same<T, int16_t>::value) load_row16<UW>(p, o);
+    else load_row<T, UW>(p, o);
+}
+
+template <typename P, int OP, int UW>
+__global__ __launch_bounds__(X265AMD_BLOCK) void k_blockop(int w, int h, int n, int lg, int depth,
+    typename OpTypes<P, OP>::d* __restrict__ dst, intptr_t ds, const int64_t* __restrict__ doff,
+    const typename OpTypes<P, OP>::a* __restrict__ a, intptr_t sa, const int64_t* __restrict__ aoff,
+    const typename OpTypes<P, OP>::b* __restrict__ b, intptr_t sb, const int64_t* __restrict__ boff, int param)
+{
+    typedef typename OpTypes<P, OP>::d D;
+    typedef typename OpTypes<P, OP>::a A;
+    typedef typename OpTypes<P, OP>::b B;
+    const int G = 1 << lg;
+    const int64_t job = (int64_t)xcd_block() * (X265AMD_BLOCK >> lg) + (threadIdx.x >> lg);
+    const int lane = threadIdx.x & (G - 1);
+    if (job >= n) return;
+
+    D* pd = dst + doff[job];
+    const A* pa = OP == X265AMD_BLOCKFILL ? nullptr : a + aoff[job];
+    const B* pb = (OP == X265AMD_SUB_PS || OP == X265AMD_ADD_PS || OP == X265AMD_ADDAVG || OP == X265AMD_PIXELAVG)
+                  ? b + boff[job] : nullptr;
+    const int maxv = (1 << depth) - 1;
+    const int avg_shift = 15 - depth, avg_off = (1 << (avg_shift - 1)) + 2 * 8192;
+    const int ux = w / UW, units = ux * h;
+
+    for (int u = lane; u < units; u += G)
+    {
+        const int x = (u % ux) * UW, y = u / ux;
+        int o[UW];
+        if constexpr (OP == X265AMD_BLOCKFILL)
+        {
+#pragma unroll
+            for (int i = 0; i < UW; i++) o[i] = param;
+        }
+        else if constexpr (OP == X265AMD_TRANSPOSE)
+        {
+            // output row y = source column y
+#pragma unroll
+            for (int i = 0; i < UW; i++) o[i] = pa[(x + i) * sa + y];
+        }
+        else
+        {
+            int va[UW];
+            ld<A, UW>(pa + y * sa + x, va);
+            if constexpr (OP == X265AMD_SUB_PS || OP == X265AMD_ADD_PS || OP == X265AMD_ADDAVG || OP == X265AMD_PIXELAVG)
+            {
+                int vb[UW];
+                ld<B, UW>(pb + y * sb + x, vb);
+#pragma unroll
+                for (int i = 0; i < UW; i++)
+                {
+                    if constexpr (OP == X265AMD_SUB_PS) o[i] = va[i] - vb[i];
+                    else if constexpr (OP == X265AMD_ADD_PS) { const int v = va[i] + vb[i]; o[i] = v < 0 ? 0 : (v > maxv ? maxv : v); }
+                    else if constexpr (OP == X265AMD_ADDAVG) { const int v = (va[i] + vb[i] + avg_off) >> avg_shift; o[i] = v < 0 ? 0 : (v > maxv ? maxv : v); }
+                    else o[i] = (va[i] + vb[i] + 1) >> 1;
+                }
+            }
+            else
+            {
+#pragma unroll
+                for (int i = 0; i < UW; i++)
+                {
+                    if constexpr (OP == X265AMD_CPY2D1D_SHL || OP == X265AMD_CPY1D2D_SHL) o[i] = va[i] << param;
+                    else if constexpr (OP == X265AMD_CPY2D1D_SHR || OP == X265AMD_CPY1D2D_SHR)
+                        o[i] = (va[i] + (int)(int16_t)(1 << (param - 1))) >> param;
+                    else o[i] = va[i];   // typed copies (pixel <-> int16 casts truncate like the reference)
+                }
+            }
+        }
+        store_row<D, UW>(pd + y * ds + x, o);
+    }
+}
+
+template <typename P, int OP>
+static int launch_blockop(int w, int h, int n, int depth, void* dst, intptr_t ds, const int64_t* doff,
+                          const void* a, intptr_t sa, const int64_t* aoff, const void* b, intptr_t sb,
+                          const int64_t* boff, int param, hipStream_t st)
+{
+    typedef typename OpTypes<P, OP>::d D;
+    typedef typename OpTypes<P, OP>::a A;
+    typedef typename OpTypes<P, OP>::b B;
+    const int uw = (w % 8 == 0) ? 8 : (w % 4 == 0) ? 4 : 2;
+    if (w % 2) return X265AMD_EINVAL;
+    const int units = (w / uw) * h;
+    int g = pow2ceil(units);
+    if (g > 64) g = 64;
+    int lg = 0;
+    while ((1 << lg) < g) lg++;
+    const dim3 grid((n + (X265AMD_BLOCK >> lg) - 1) / (X265AMD_BLOCK >> lg));
+#define L(UW) hipLaunchKernelGGL((k_blockop<P, OP, UW>), grid, dim3(X265AMD_BLOCK), 0, st, w, h, n, lg, depth, \
+                                 (D*)dst, ds, doff, (const A*)a, sa, aoff, (const B*)b, sb, boff, param)
+    if (uw == 8) L(8);
+    else if (uw == 4) L(4);
+    else L(2);
+#undef L
+    return (int)hipGetLastError();
+}
+
+template <typename P>
+static int dispatch_blockop(int op, int w, int h, int n, int depth, void* dst, intptr_t ds, const int64_t* doff,
+                            const void* a, intptr_t sa, const int64_t* aoff, const void* b, intptr_t sb,
+                            const int64_t* boff, int param, hipStream_t st)
+{
+#define C(OP) case OP: return launch_blockop<P, OP>(w, h, n, depth, dst, ds, doff, a, sa, aoff, b, sb, boff, param, st)
+    switch (op)
+    {
+    C(X265AMD_SUB_PS); C(X265AMD_ADD_PS); C(X265AMD_ADDAVG); C(X265AMD_PIXELAVG);
+    C(X265AMD_COPY_PP); C(X265AMD_COPY_SP); C(X265AMD_COPY_PS); C(X265AMD_COPY_SS);
+    C(X265AMD_BLOCKFILL); C(X265AMD_CPY2D1D_SHL); C(X265AMD_CPY2D1D_SHR);
+    C(X265AMD_CPY1D2D_SHL); C(X265AMD_CPY1D2D_SHR); C(X265AMD_TRANSPOSE);
+    }
+#undef C
+    return X265AMD_EINVAL;
+}
+
+} // namespace x265amd
+
+using namespace x265amd;
+
+extern "C" int x265amd_blockop(int op, int depth, int w, int h, int n,
+                               void* dst, intptr_t dst_stride, const int64_t* dst_off,
+                               const void* a, intptr_t a_stride, const int64_t* a_off,
+                               const void* b, intptr_t b_stride, const int64_t* b_off,
+                               int param, void* stream)
+{
+    if (n <= 0) return 0;
+    if (w < 2 || h < 1 || w > 64 || h > 64) return X265AMD_EINVAL;
+    hipStream_t st = (hipStream_t)stream;
+    if (depth == 8)
+        return dispatch_blockop<uint8_t>(op, w, h, n, depth, dst, dst_stride, dst_off, a, a_stride, a_off, b, b_stride, b_off, param, st);
+    if (depth == 10 || depth == 12)
+        return dispatch_blockop<uint16_t>(op, w, h, n, depth, dst, dst_stride, dst_off, a, a_stride, a_off, b, b_stride, b_off, param, st);
+    return X265AMD_EINVAL;
+}

@@ -1,0 +1,216 @@
+// common.h — shared device helpers for the x265 primitive kernels (gfx950).
+//
+// Batching model: every C-ABI call processes `n` independent
+// jobs of one primitive family and one block shape.  A job is owned by a
+// power-of-two group of G lanes inside one 64-lane wavefront; each lane walks
+// the job's fixed-size units (a row strip, a 4x4 / 8x8 Hadamard tile, ...)
+// with stride G and the group reduces with cross-lane shuffles.  Operands are
+// addressed as base pointer + per-job element offset (int64) + per-batch
+// stride, so jobs can point anywhere inside device-resident frame planes.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "tables.h"
+
+#define X265AMD_BLOCK 256
+
+namespace x265amd {
+
+// ---------------------------------------------------------------- launch
+// Bijective XCD-aware remap of the hardware block id (guide T1): hardware
+// block b runs on XCD b % 8; give every XCD a contiguous range of logical
+// blocks so jobs that are neighbours in the batch (neighbouring blocks of a
+// frame) share that XCD's L2.  Speed only, never correctness.
+__device__ __forceinline__ uint32_t xcd_block()
+{
+    const uint32_t b = blockIdx.x, nb = gridDim.x;
+    if (nb < 16) return b;
+    const uint32_t q = nb >> 3, r = nb & 7, x = b & 7;
+    return x * q + (x < r ? x : r) + (b >> 3);
+}
+
+// Job/lane coordinates for a G-lane group (G power of two, <= 64).
+template <int G>
+struct Group
+{
+    int64_t job;
+    int lane;
+    __device__ __forceinline__ Group()
+    {
+        const uint32_t lb = xcd_block();
+        job  = (int64_t)lb * (X265AMD_BLOCK / G) + threadIdx.x / G;
+        lane = threadIdx.x & (G - 1);
+    }
+};
+
+// Group reduction (sum) over the G lanes of a group; result valid in all lanes.
+template <int G, typename T>
+__device__ __forceinline__ T group_sum(T v)
+{
+#pragma unroll
+    for (int m = G >> 1; m > 0; m >>= 1)
+        v += __shfl_xor(v, m, 64);
+    return v;
+}
+
+template <int G>
+__device__ __forceinline__ uint64_t group_sum64(uint64_t v)
+{
+#pragma unroll
+    for (int m = G >> 1; m > 0; m >>= 1)
+    {
+        uint32_t lo = __shfl_xor((uint32_t)v, m, 64);
+        uint32_t hi = __shfl_xor((uint32_t)(v >> 32), m, 64);
+        v += ((uint64_t)hi << 32) | lo;
+    }
+    return v;
+}
+
+inline int pow2ceil(int v)
+{
+    int g = 1;
+    while (g < v) g <<= 1;
+    return g;
+}
+
+// ---------------------------------------------------------------- loads
+// Unaligned little-endian loads (gfx950 runs HSA in unaligned mode: these
+// lower to single global_load_dword{,x2,x4}).
+template <typename T>
+__device__ __forceinline__ T ldu(const void* p)
+{
+    T v;
+    __builtin_memcpy(&v, p, sizeof(T));
+    return v;
+}
+template <typename T>
+__device__ __forceinline__ void stu(void* p, T v)
+{
+    __builtin_memcpy(p, &v, sizeof(T));
+}
+
+template <typename P>
+__device__ __forceinline__ int clip_pixel(int v, int maxv)
+{
+    return v < 0 ? 0 : (v > maxv ? maxv : v);
+}
+
+__device__ __forceinline__ int clip16(int v)
+{
+    return v < -32768 ? -32768 : (v > 32767 ? 32767 : v);
+}
+
+// Load UW consecutive pixels (as int) starting at p.
+template <typename P, int UW>
+__device__ __forceinline__ void load_row(const P* p, int (&o)[UW])
+{
+    if constexpr (sizeof(P) == 1)
+    {
+        if constexpr (UW == 8)
+        {
+            uint64_t v = ldu<uint64_t>(p);
+#pragma unroll
+            for (int i = 0; i < 8; i++) o[i] = (int)((v >> (8 * i)) & 0xff);
+        }
+        else if constexpr (UW == 4)
+        {
+            uint32_t v = ldu<uint32_t>(p);
+#pragma unroll
+            for (int i = 0; i < 4; i++) o[i] = (int)((v >> (8 * i)) & 0xff);
+        }
+        else
+        {
+#pragma unroll
+            for (int i = 0; i < UW; i++) o[i] = p[i];
+        }
+    }
+    else
+    {
+        if constexpr (UW == 8)
+        {
+            uint4 v = ldu<uint4>(p);
+            uint32_t w[4] = { v.x, v.y, v.z, v.w };
+#pragma unroll
+            for (int i = 0; i < 4; i++) { o[2 * i] = (int)(w[i] & 0xffff); o[2 * i + 1] = (int)(w[i] >> 16); }
+        }
+        else if constexpr (UW == 4)
+        {
+            uint2 v = ldu<uint2>(p);
+            o[0] = (int)(v.x & 0xffff); o[1] = (int)(v.x >> 16);
+            o[2] = (int)(v.y & 0xffff); o[3] = (int)(v.y >> 16);
+        }
+        else
+        {
+#pragma unroll
+            for (int i = 0; i < UW; i++) o[i] = p[i];
+        }
+    }
+}
+
+// Load UW consecutive int16 values.
+template <int UW>
+__device__ __forceinline__ void load_row16(const int16_t* p, int (&o)[UW])
+{
+    if constexpr (UW == 8)
+    {
+        uint4 v = ldu<uint4>(p);
+        uint32_t w[4] = { v.x, v.y, v.z, v.w };
+#pragma unroll
+        for (int i = 0; i < 4; i++) { o[2 * i] = (int)(int16_t)(w[i] & 0xffff); o[2 * i + 1] = (int)(int16_t)(w[i] >> 16); }
+    }
+    else if constexpr (UW == 4)
+    {
+        uint2 v = ldu<uint2>(p);
+        o[0] = (int16_t)(v.x & 0xffff); o[1] = (int16_t)(v.x >> 16);
+        o[2] = (int16_t)(v.y & 0xffff); o[3] = (int16_t)(v.y >> 16);
+    }
+    else
+    {
+#pragma unroll
+        for (int i = 0; i < UW; i++) o[i] = p[i];
+    }
+}
+
+template <typename P, int UW>
+__device__ __forceinline__ void store_row(P* p, const int (&v)[UW])
+{
+    if constexpr (sizeof(P) == 1 && UW == 8)
+    {
+        uint64_t w = 0;
+#pragma unroll
+        for (int i = 0; i < 8; i++) w |= (uint64_t)(v[i] & 0xff) << (8 * i);
+        stu<uint64_t>(p, w);
+    }
+    else if constexpr (sizeof(P) == 1 && UW == 4)
+    {
+        uint32_t w = 0;
+#pragma unroll
+        for (int i = 0; i < 4; i++) w |= (uint32_t)(v[i] & 0xff) << (8 * i);
+        stu<uint32_t>(p, w);
+    }
+    else if constexpr (sizeof(P) == 2 && UW == 8)
+    {
+        uint4 w;
+        w.x = (uint32_t)(v[0] & 0xffff) | ((uint32_t)v[1] << 16);
+        w.y = (uint32_t)(v[2] & 0xffff) | ((uint32_t)v[3] << 16);
+        w.z = (uint32_t)(v[4] & 0xffff) | ((uint32_t)v[5] << 16);
+        w.w = (uint32_t)(v[6] & 0xffff) | ((uint32_t)v[7] << 16);
+        stu<uint4>(p, w);
+    }
+    else if constexpr (sizeof(P) == 2 && UW == 4)
+    {
+        uint2 w;
+        w.x = (uint32_t)(v[0] & 0xffff) | ((uint32_t)v[1] << 16);
+        w.y = (uint32_t)(v[2] & 0xffff) | ((uint32_t)v[3] << 16);
+        stu<uint2>(p, w);
+    }
+    else
+    {
+#pragma unroll
+        for (int i = 0; i < UW; i++) p[i] = (P)v[i];
+    }
+}
+
+} // namespace x265amd

@@ -1,0 +1,504 @@
+// pixel.hip — batched SAD / SATD / SA8D / SSE / psy-cost / var / sad_x3/x4.
+//
+// Reference semantics: x265_1.9/source/common/pixel.cpp
+//   sad            :39-54        sad_x3/x4 :73-118      sse :120-139
+//   satd_4x4/8x4   :163-214      satd4/8   :216-242
+//   _sa8d_8x8      :244-279      sa8d_8x8 / sa8d_16x16 / sa8d8 / sa8d16 :281-322
+//   pixel_ssd_s    :324-336      pixel_var :649-666     psyCost_pp :672-703
+//
+// Bit-exactness notes:
+//  * the reference's SWAR sum2_t packing equals plain int32 arithmetic for
+//    legal pixel ranges, so the Hadamards here are plain int32;
+//  * SATD: every 4x4 Hadamard's |coef| sum is even, so Σ(raw>>1) = (Σraw)>>1
+//    and any 4x4 tiling gives the reference's value;
+//  * SA8D: the (x+2)>>2 rounding unit matters (8x8 for sa8d8, 16x16 for
+//    sa8d16) and is kept per unit.
+//
+// Work mapping: one job per G-lane group; a lane handles one UWxUH unit per
+// iteration (8x4 / 4x4 strips for SAD/SSE/SATD, 8x8 / 16x16 for SA8D); the
+// group reduces with xor-shuffles.  8-bit SAD uses v_sad_u8 on packed dwords,
+// 10/12-bit v_sad_u16.
+#include "common.h"
+#include "../../../include/x265_amd.h"
+
+namespace x265amd {
+
+// -------------------------------------------------------------- unit math
+
+template <typename P, int UW, int UH>
+__device__ __forceinline__ uint32_t unit_sad(const P* a, intptr_t sa, const P* b, intptr_t sb)
+{
+    uint32_t s = 0;
+#pragma unroll
+    for (int y = 0; y < UH; y++)
+    {
+        if constexpr (sizeof(P) == 1)
+        {
+            if constexpr (UW == 8)
+            {
+                uint2 va = ldu<uint2>(a + y * sa), vb = ldu<uint2>(b + y * sb);
+                s = __builtin_amdgcn_sad_u8(va.x, vb.x, s);
+                s = __builtin_amdgcn_sad_u8(va.y, vb.y, s);
+            }
+            else
+            {
+                uint32_t va = ldu<uint32_t>(a + y * sa), vb = ldu<uint32_t>(b + y * sb);
+                s = __builtin_amdgcn_sad_u8(va, vb, s);
+            }
+        }
+        else
+        {
+            if constexpr (UW == 8)
+            {
+                uint4 va = ldu<uint4>(a + y * sa), vb = ldu<uint4>(b + y * sb);
+                s = __builtin_amdgcn_sad_u16(va.x, vb.x, s);
+                s = __builtin_amdgcn_sad_u16(va.y, vb.y, s);
+                s = __builtin_amdgcn_sad_u16(va.z, vb.z, s);
+                s = __builtin_amdgcn_sad_u16(va.w, vb.w, s);
+            }
+            else
+            {
+                uint2 va = ldu<uint2>(a + y * sa), vb = ldu<uint2>(b + y * sb);
+                s = __builtin_amdgcn_sad_u16(va.x, vb.x, s);
+                s = __builtin_amdgcn_sad_u16(va.y, vb.y, s);
+            }
+        }
+    }
+    return s;
+}
+
+// Σ(a-b)^2 as uint32 per term (the reference's int product, two's complement)
+template <typename T, int UW, int UH, bool IS16>
+__device__ __forceinline__ uint64_t unit_sse(const T* a, intptr_t sa, const T* b, intptr_t sb)
+{
+    uint64_t s = 0;
+#pragma unroll
+    for (int y = 0; y < UH; y++)
+    {
+        int va[UW], vb[UW];
+        if constexpr (IS16) { load_row16<UW>((const int16_t*)a + y * sa, va); load_row16<UW>((const int16_t*)b + y * sb, vb); }
+        else { load_row<T, UW>(a + y * sa, va); load_row<T, UW>(b + y * sb, vb); }
+        uint32_t r = 0;
+#pragma unroll
+        for (int x = 0; x < UW; x++)
+        {
+            int d = va[x] - vb[x];
+            r += (uint32_t)(d * d);
+        }
+        s += r;
+    }
+    return s;
+}
+
+template <int UW, int UH>
+__device__ __forceinline__ uint64_t unit_ssd(const int16_t* a, intptr_t sa)
+{
+    uint64_t s = 0;
+#pragma unroll
+    for (int y = 0; y < UH; y++)
+    {
+        int va[UW];
+        load_row16<UW>(a + y * sa, va);
+        uint32_t r = 0;
+#pragma unroll
+        for (int x = 0; x < UW; x++) r += (uint32_t)(va[x] * va[x]);
+        s += r;
+    }
+    return s;
+}
+
+// var: low 32 bits = Σp, high 32 bits = Σp² (wrapping, as the reference's uint32 sqr)
+template <typename P, int UW, int UH>
+__device__ __forceinline__ uint64_t unit_var(const P* a, intptr_t sa)
+{
+    uint32_t s = 0, q = 0;
+#pragma unroll
+    for (int y = 0; y < UH; y++)
+    {
+        int va[UW];
+        load_row<P, UW>(a + y * sa, va);
+#pragma unroll
+        for (int x = 0; x < UW; x++) { s += va[x]; q += (uint32_t)(va[x] * va[x]); }
+    }
+    return (uint64_t)s + ((uint64_t)q << 32);
+}
+
+// raw 4x4 Hadamard |coef| sum of d (before the reference's >>1)
+__device__ __forceinline__ uint32_t had4x4(int (&d)[4][4])
+{
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+    {
+        int t0 = d[i][0] + d[i][1], t1 = d[i][0] - d[i][1];
+        int t2 = d[i][2] + d[i][3], t3 = d[i][2] - d[i][3];
+        d[i][0] = t0 + t2; d[i][2] = t0 - t2; d[i][1] = t1 + t3; d[i][3] = t1 - t3;
+    }
+    uint32_t s = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++)
+    {
+        int t0 = d[0][j] + d[1][j], t1 = d[0][j] - d[1][j];
+        int t2 = d[2][j] + d[3][j], t3 = d[2][j] - d[3][j];
+        s += abs(t0 + t2) + abs(t0 - t2) + abs(t1 + t3) + abs(t1 - t3);
+    }
+    return s;
+}
+
+// raw 8x8 Hadamard |coef| sum (x265 _sa8d_8x8 before rounding)
+__device__ __forceinline__ uint32_t had8x8(int (&d)[8][8])
+{
+#pragma unroll
+    for (int i = 0; i < 8; i++)
+    {
+        int a0 = d[i][0] + d[i][1], a1 = d[i][0] - d[i][1];
+        int a2 = d[i][2] + d[i][3], a3 = d[i][2] - d[i][3];
+        int a4 = d[i][4] + d[i][5], a5 = d[i][4] - d[i][5];
+        int a6 = d[i][6] + d[i][7], a7 = d[i][6] - d[i][7];
+        int b0 = a0 + a2, b2 = a0 - a2, b1 = a1 + a3, b3 = a1 - a3;
+        int b4 = a4 + a6, b6 = a4 - a6, b5 = a5 + a7, b7 = a5 - a7;
+        d[i][0] = b0 + b4; d[i][4] = b0 - b4; d[i][1] = b1 + b5; d[i][5] = b1 - b5;
+        d[i][2] = b2 + b6; d[i][6] = b2 - b6; d[i][3] = b3 + b7; d[i][7] = b3 - b7;
+    }
+    uint32_t s = 0;
+#pragma unroll
+    for (int j = 0; j < 8; j++)
+    {
+        int a0 = d[0][j] + d[1][j], a1 = d[0][j] - d[1][j];
+        int a2 = d[2][j] + d[3][j], a3 = d[2][j] - d[3][j];
+        int a4 = d[4][j] + d[5][j], a5 = d[4][j] - d[5][j];
+        int a6 = d[6][j] + d[7][j], a7 = d[6][j] - d[7][j];
+        int b0 = a0 + a2, b2 = a0 - a2, b1 = a1 + a3, b3 = a1 - a3;
+        int b4 = a4 + a6, b6 = a4 - a6, b5 = a5 + a7, b7 = a5 - a7;
+        s += abs(b0 + b4) + abs(b0 - b4) + abs(b1 + b5) + abs(b1 - b5)
+           + abs(b2 + b6) + abs(b2 - b6) + abs(b3 + b7) + abs(b3 - b7);
+    }
+    return s;
+}
+
+template <typename P, int UW>
+__device__ __forceinline__ uint32_t unit_satd(const P* a, intptr_t sa, const P* b, intptr_t sb)
+{
+    // UW = 4: one 4x4; UW = 8: two 4x4 side by side (satd_8x4)
+    uint32_t s = 0;
+#pragma unroll
+    for (int half = 0; half < UW / 4; half++)
+    {
+        int d[4][4];
+#pragma unroll
+        for (int y = 0; y < 4; y++)
+        {
+            int va[4], vb[4];
+            load_row<P, 4>(a + y * sa + 4 * half, va);
+            load_row<P, 4>(b + y * sb + 4 * half, vb);
+#pragma unroll
+            for (int x = 0; x < 4; x++) d[y][x] = va[x] - vb[x];
+        }
+        s += had4x4(d);
+    }
+    return s;
+}
+
+template <typename P>
+__device__ __forceinline__ uint32_t raw_sa8d(const P* a, intptr_t sa, const P* b, intptr_t sb)
+{
+    int d[8][8];
+#pragma unroll
+    for (int y = 0; y < 8; y++)
+    {
+        int va[8], vb[8];
+        load_row<P, 8>(a + y * sa, va);
+        load_row<P, 8>(b + y * sb, vb);
+#pragma unroll
+        for (int x = 0; x < 8; x++) d[y][x] = va[x] - vb[x];
+    }
+    return had8x8(d);
+}
+
+// energy helpers for psyCost_pp: Hadamard of the block itself (zero reference)
+template <typename P>
+__device__ __forceinline__ int psy_energy8(const P* a, intptr_t sa)
+{
+    int d[8][8];
+    uint32_t sad = 0;
+#pragma unroll
+    for (int y = 0; y < 8; y++)
+    {
+        int va[8];
+        load_row<P, 8>(a + y * sa, va);
+#pragma unroll
+        for (int x = 0; x < 8; x++) { d[y][x] = va[x]; sad += va[x]; }
+    }
+    int sa8d = (int)((had8x8(d) + 2) >> 2);
+    return sa8d - (int)(sad >> 2);
+}
+
+template <typename P>
+__device__ __forceinline__ int psy_energy4(const P* a, intptr_t sa)
+{
+    int d[4][4];
+    uint32_t sad = 0;
+#pragma unroll
+    for (int y = 0; y < 4; y++)
+    {
+        int va[4];
+        load_row<P, 4>(a + y * sa, va);
+#pragma unroll
+        for (int x = 0; x < 4; x++) { d[y][x] = va[x]; sad += va[x]; }
+    }
+    int satd = (int)(had4x4(d) >> 1);
+    return satd - (int)(sad >> 2);
+}
+
+// -------------------------------------------------------------- kernels
+
+template <int OP, typename P, int UW, int UH>
+__global__ __launch_bounds__(X265AMD_BLOCK) void k_pixelcmp(int w, int h, int n, int lg,
+    const P* __restrict__ a, intptr_t sa, const int64_t* __restrict__ aoff,
+    const P* __restrict__ b, intptr_t sb, const int64_t* __restrict__ boff,
+    void* __restrict__ out, int wrap32)
+{
+    const int G = 1 << lg;
+    const uint32_t lb = xcd_block();
+    const int64_t job = (int64_t)lb * (X265AMD_BLOCK >> lg) + (threadIdx.x >> lg);
+    const int lane = threadIdx.x & (G - 1);
+    const bool live = job < n;
+    const int64_t jj = live ? job : 0;
+
+    const P* pa = a + aoff[jj];
+    const P* pb = (OP == X265AMD_SSD_S || OP == X265AMD_VAR) ? nullptr : b + boff[jj];
+    const int ux = w / UW, units = ux * (h / UH);
+
+    uint64_t acc = 0;
+    if (live)
+    {
+        for (int u = lane; u < units; u += G)
+        {
+            const int x = (u % ux) * UW, y = (u / ux) * UH;
+            const P* qa = pa + y * sa + x;
+            if constexpr (OP == X265AMD_SAD)
+                acc += unit_sad<P, UW, UH>(qa, sa, pb + y * sb + x, sb);
+            else if constexpr (OP == X265AMD_SATD)
+                acc += unit_satd<P, UW>(qa, sa, pb + y * sb + x, sb);
+            else if constexpr (OP == X265AMD_SA8D)
+            {
+                const P* qb = pb + y * sb + x;
+                if constexpr (UW == 8)
+                    acc += (raw_sa8d<P>(qa, sa, qb, sb) + 2) >> 2;
+                else
+                {
+                    uint32_t r = raw_sa8d<P>(qa, sa, qb, sb) + raw_sa8d<P>(qa + 8, sa, qb + 8, sb)
+                               + raw_sa8d<P>(qa + 8 * sa, sa, qb + 8 * sb, sb)
+                               + raw_sa8d<P>(qa + 8 * sa + 8, sa, qb + 8 * sb + 8, sb);
+                    acc += (r + 2) >> 2;
+                }
+            }
+            else if constexpr (OP == X265AMD_SSE_PP)
+                acc += unit_sse<P, UW, UH, false>(qa, sa, pb + y * sb + x, sb);
+            else if constexpr (OP == X265AMD_SSE_SS)
+                acc += unit_sse<P, UW, UH, true>(qa, sa, pb + y * sb + x, sb);
+            else if constexpr (OP == X265AMD_PSY)
+            {
+                const P* qb = pb + y * sb + x;
+                int e;
+                if constexpr (UW == 4) e = psy_energy4<P>(qa, sa) - psy_energy4<P>(qb, sb);
+                else e = psy_energy8<P>(qa, sa) - psy_energy8<P>(qb, sb);
+                acc += (uint32_t)abs(e);
+            }
+            else if constexpr (OP == X265AMD_SSD_S)
+                acc += unit_ssd<UW, UH>((const int16_t*)qa, sa);
+            else if constexpr (OP == X265AMD_VAR)
+                acc += unit_var<P, UW, UH>(qa, sa);
+        }
+    }
+
+    // group reduction (all lanes of the wave participate in the shuffles)
+    if constexpr (OP == X265AMD_SSE_PP || OP == X265AMD_SSE_SS || OP == X265AMD_SSD_S || OP == X265AMD_VAR)
+    {
+        for (int m = G >> 1; m > 0; m >>= 1)
+        {
+            uint32_t lo = __shfl_xor((uint32_t)acc, m, 64);
+            uint32_t hi = __shfl_xor((uint32_t)(acc >> 32), m, 64);
+            acc += ((uint64_t)hi << 32) | lo;
+        }
+        if (live && lane == 0)
+        {
+            uint64_t v = acc;
+            if (wrap32 && OP != X265AMD_VAR) v &= 0xffffffffull;  // sse_t = uint32 at 8-bit
+            ((uint64_t*)out)[job] = v;
+        }
+    }
+    else
+    {
+        uint32_t v = (uint32_t)acc;
+        for (int m = G >> 1; m > 0; m >>= 1) v += __shfl_xor(v, m, 64);
+        if constexpr (OP == X265AMD_SATD) v >>= 1;
+        if (live && lane == 0) ((int32_t*)out)[job] = (int32_t)v;
+    }
+}
+
+template <typename P, int NREF, int UW, int UH>
+__global__ __launch_bounds__(X265AMD_BLOCK) void k_sad_multi(int w, int h, int n, int lg,
+    const P* __restrict__ fenc, intptr_t fs, const int64_t* __restrict__ foff,
+    const P* __restrict__ ref, intptr_t rs, const int64_t* __restrict__ roff,
+    int32_t* __restrict__ out)
+{
+    const int G = 1 << lg;
+    const uint32_t lb = xcd_block();
+    const int64_t job = (int64_t)lb * (X265AMD_BLOCK >> lg) + (threadIdx.x >> lg);
+    const int lane = threadIdx.x & (G - 1);
+    const bool live = job < n;
+    const int64_t jj = live ? job : 0;
+
+    const P* pf = fenc + foff[jj];
+    const P* pr[NREF];
+#pragma unroll
+    for (int k = 0; k < NREF; k++) pr[k] = ref + roff[jj * NREF + k];
+    const int ux = w / UW, units = ux * (h / UH);
+
+    uint32_t acc[NREF];
+#pragma unroll
+    for (int k = 0; k < NREF; k++) acc[k] = 0;
+    if (live)
+    {
+        for (int u = lane; u < units; u += G)
+        {
+            const int x = (u % ux) * UW, y = (u / ux) * UH;
+#pragma unroll
+            for (int k = 0; k < NREF; k++)
+                acc[k] += unit_sad<P, UW, UH>(pf + y * fs + x, fs, pr[k] + y * rs + x, rs);
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < NREF; k++)
+    {
+        uint32_t v = acc[k];
+        for (int m = G >> 1; m > 0; m >>= 1) v += __shfl_xor(v, m, 64);
+        acc[k] = v;
+    }
+    if (live && lane == 0)
+    {
+#pragma unroll
+        for (int k = 0; k < NREF; k++) out[job * NREF + k] = (int32_t)acc[k];
+    }
+}
+
+// -------------------------------------------------------------- dispatch
+
+static inline int grid_for(int n, int lg)
+{
+    const int per = X265AMD_BLOCK >> lg;
+    return (n + per - 1) / per;
+}
+
+template <int OP, typename P, int UW, int UH>
+static int launch_cmp(int w, int h, int n, const void* a, intptr_t sa, const int64_t* aoff,
+                      const void* b, intptr_t sb, const int64_t* boff, void* out, hipStream_t st,
+                      int wrap32)
+{
+    const int units = (w / UW) * (h / UH);
+    int g = pow2ceil(units);
+    if (g > 64) g = 64;
+    int lg = 0;
+    while ((1 << lg) < g) lg++;
+    hipLaunchKernelGGL((k_pixelcmp<OP, P, UW, UH>), dim3(grid_for(n, lg)), dim3(X265AMD_BLOCK), 0, st,
+                       w, h, n, lg, (const P*)a, sa, aoff, (const P*)b, sb, boff, out, wrap32);
+    return (int)hipGetLastError();
+}
+
+template <typename P>
+static int dispatch_cmp(int op, int w, int h, int n, const void* a, intptr_t sa, const int64_t* aoff,
+                        const void* b, intptr_t sb, const int64_t* boff, void* out, hipStream_t st)
+{
+    const int wrap32 = sizeof(P) == 1;
+    const bool w8 = (w % 8) == 0;
+    if ((w % 4) || (h % 4) || w > 64 || h > 64 || w < 4 || h < 4) return X265AMD_EINVAL;
+    switch (op)
+    {
+    case X265AMD_SAD:
+        return w8 ? launch_cmp<X265AMD_SAD, P, 8, 4>(w, h, n, a, sa, aoff, b, sb, boff, out, st, wrap32)
+                  : launch_cmp<X265AMD_SAD, P, 4, 4>(w, h, n, a, sa, aoff, b, sb, boff, out, st, wrap32);
+    case X265AMD_SATD:
+        return w8 ? launch_cmp<X265AMD_SATD, P, 8, 4>(w, h, n, a, sa, aoff, b, sb, boff, out, st, wrap32)
+                  : launch_cmp<X265AMD_SATD, P, 4, 4>(w, h, n, a, sa, aoff, b, sb, boff, out, st, wrap32);
+    case X265AMD_SA8D:
+        if ((w % 16) == 0 && (h % 16) == 0)
+            return launch_cmp<X265AMD_SA8D, P, 16, 16>(w, h, n, a, sa, aoff, b, sb, boff, out, st, wrap32);
+        if ((w % 8) == 0 && (h % 8) == 0)
+            return launch_cmp<X265AMD_SA8D, P, 8, 8>(w, h, n, a, sa, aoff, b, sb, boff, out, st, wrap32);
+        // 4x4 / 4x8 entries of the sa8d tables are satd (primitives.cpp:106,164-171)
+        return w8 ? launch_cmp<X265AMD_SATD, P, 8, 4>(w, h, n, a, sa, aoff, b, sb, boff, out, st, wrap32)
+                  : launch_cmp<X265AMD_SATD, P, 4, 4>(w, h, n, a, sa, aoff, b, sb, boff, out, st, wrap32);
+    case X265AMD_SSE_PP:
+        return w8 ? launch_cmp<X265AMD_SSE_PP, P, 8, 4>(w, h, n, a, sa, aoff, b, sb, boff, out, st, wrap32)
+                  : launch_cmp<X265AMD_SSE_PP, P, 4, 4>(w, h, n, a, sa, aoff, b, sb, boff, out, st, wrap32);
+    case X265AMD_SSE_SS:
+        return w8 ? launch_cmp<X265AMD_SSE_SS, int16_t, 8, 4>(w, h, n, a, sa, aoff, b, sb, boff, out, st, wrap32)
+                  : launch_cmp<X265AMD_SSE_SS, int16_t, 4, 4>(w, h, n, a, sa, aoff, b, sb, boff, out, st, wrap32);
+    case X265AMD_PSY:
+        if (w != h) return X265AMD_EINVAL;
+        return w == 4 ? launch_cmp<X265AMD_PSY, P, 4, 4>(w, h, n, a, sa, aoff, b, sb, boff, out, st, wrap32)
+                      : launch_cmp<X265AMD_PSY, P, 8, 8>(w, h, n, a, sa, aoff, b, sb, boff, out, st, wrap32);
+    case X265AMD_SSD_S:
+        return w8 ? launch_cmp<X265AMD_SSD_S, int16_t, 8, 4>(w, h, n, a, sa, aoff, b, sb, boff, out, st, wrap32)
+                  : launch_cmp<X265AMD_SSD_S, int16_t, 4, 4>(w, h, n, a, sa, aoff, b, sb, boff, out, st, wrap32);
+    case X265AMD_VAR:
+        return w8 ? launch_cmp<X265AMD_VAR, P, 8, 4>(w, h, n, a, sa, aoff, b, sb, boff, out, st, wrap32)
+                  : launch_cmp<X265AMD_VAR, P, 4, 4>(w, h, n, a, sa, aoff, b, sb, boff, out, st, wrap32);
+    }
+    return X265AMD_EINVAL;
+}
+
+template <typename P, int NREF>
+static int dispatch_multi(int w, int h, int n, const void* f, intptr_t fs, const int64_t* foff,
+                          const void* r, intptr_t rs, const int64_t* roff, int32_t* out, hipStream_t st)
+{
+    if ((w % 4) || (h % 4) || w > 64 || h > 64) return X265AMD_EINVAL;
+    const bool w8 = (w % 8) == 0;
+    const int units = (w / (w8 ? 8 : 4)) * (h / 4);
+    int g = pow2ceil(units);
+    if (g > 64) g = 64;
+    int lg = 0;
+    while ((1 << lg) < g) lg++;
+    if (w8)
+        hipLaunchKernelGGL((k_sad_multi<P, NREF, 8, 4>), dim3(grid_for(n, lg)), dim3(X265AMD_BLOCK), 0, st,
+                           w, h, n, lg, (const P*)f, fs, foff, (const P*)r, rs, roff, out);
+    else
+        hipLaunchKernelGGL((k_sad_multi<P, NREF, 4, 4>), dim3(grid_for(n, lg)), dim3(X265AMD_BLOCK), 0, st,
+                           w, h, n, lg, (const P*)f, fs, foff, (const P*)r, rs, roff, out);
+    return (int)hipGetLastError();
+}
+
+} // namespace x265amd
+
+using namespace x265amd;
+
+extern "C" int x265amd_pixelcmp(int op, int depth, int w, int h, int n,
+                                const void* a, intptr_t a_stride, const int64_t* a_off,
+                                const void* b, intptr_t b_stride, const int64_t* b_off,
+                                void* out, void* stream)
+{
+    if (n <= 0) return 0;
+    hipStream_t st = (hipStream_t)stream;
+    if (depth == 8)
+        return dispatch_cmp<uint8_t>(op, w, h, n, a, a_stride, a_off, b, b_stride, b_off, out, st);
+    if (depth == 10 || depth == 12)
+        return dispatch_cmp<uint16_t>(op, w, h, n, a, a_stride, a_off, b, b_stride, b_off, out, st);
+    return X265AMD_EINVAL;
+}
+
+extern "C" int x265amd_sad_multi(int nref, int depth, int w, int h, int n,
+                                 const void* fenc, intptr_t fenc_stride, const int64_t* fenc_off,
+                                 const void* ref, intptr_t ref_stride, const int64_t* ref_off,
+                                 int32_t* out, void* stream)
+{
+    if (n <= 0) return 0;
+    hipStream_t st = (hipStream_t)stream;
+    if (nref != 3 && nref != 4) return X265AMD_EINVAL;
+    if (depth == 8)
+        return nref == 3 ? dispatch_multi<uint8_t, 3>(w, h, n, fenc, fenc_stride, fenc_off, ref, ref_stride, ref_off, out, st)
+                         : dispatch_multi<uint8_t, 4>(w, h, n, fenc, fenc_stride, fenc_off, ref, ref_stride, ref_off, out, st);
+    if (depth == 10 || depth == 12)
+        return nref == 3 ? dispatch_multi<uint16_t, 3>(w, h, n, fenc, fenc_stride, fenc_off, ref, ref_stride, ref_off, out, st)
+                         : dispatch_multi<uint16_t, 4>(w, h, n, fenc, fenc_stride, fenc_off, ref, ref_stride, ref_off, out, st);
+    return X265AMD_EINVAL;
+}

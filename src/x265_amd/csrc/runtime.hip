@@ -1,0 +1,44 @@
+// runtime.hip — device selection and status reporting for the C ABI
+// (include/x265_amd.h).  x265 has no error channel inside its primitives
+// (primitives.h typedefs); failures surface as non-zero status codes here and
+// are mapped by the caller onto x265_encoder_open() == NULL /
+// x265_encoder_encode() < 0 (x265.h:1351-1359).
+#include <hip/hip_runtime.h>
+#include <string.h>
+
+#include "../../../include/x265_amd.h"
+
+extern "C" int x265amd_abi_version(void)
+{
+    return X265AMD_ABI_VERSION;
+}
+
+extern "C" const char* x265amd_target(void)
+{
+    return "gfx950";
+}
+
+extern "C" int x265amd_set_device(int device)
+{
+    int count = 0;
+    hipError_t e = hipGetDeviceCount(&count);
+    if (e != hipSuccess) return (int)e;
+    if (device < 0 || device >= count) return X265AMD_ENODEV;
+    hipDeviceProp_t prop;
+    e = hipGetDeviceProperties(&prop, device);
+    if (e != hipSuccess) return (int)e;
+    // code objects are built for gfx950 only: refuse any other target loudly
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) return X265AMD_ENODEV;
+    return (int)hipSetDevice(device);
+}
+
+extern "C" const char* x265amd_strerror(int status)
+{
+    switch (status)
+    {
+    case X265AMD_OK: return "success";
+    case X265AMD_EINVAL: return "x265amd: unsupported primitive, block shape or bit depth";
+    case X265AMD_ENODEV: return "x265amd: no gfx950 (MI355X) device";
+    default: return hipGetErrorString((hipError_t)status);
+    }
+}

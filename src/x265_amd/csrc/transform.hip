@@ -1,0 +1,492 @@
+// transform.hip — batched 2-D DCT / iDCT 4..32, DST / iDST 4x4, quant,
+// nquant, dequant (normal, scaling), count_nonzero / copy_cnt.
+//
+// Reference semantics: x265_1.9/source/common/dct.cpp
+//   fastForwardDst / inversedst :41-81      partialButterfly{4,8,16,32} :83-240,418-440
+//   partialButterflyInverse*    :242-416    dst4/dct4..32 :442-525   idst4/idct4..32 :527-610
+//   dequant_normal :612-634  dequant_scaling :636-662  quant :664-686  nquant :688-713
+//   count_nonzero :714-726   copy_count :728-742
+// Bit-exactness: forward stages wrap each
+// result to int16, inverse stages clip; the even/odd butterfly used here is
+// an exact integer refactoring of the matrix product (no intermediate
+// rounding), so it reproduces the reference's partial butterflies exactly.
+//
+// Work mapping: N = 4 transforms run one job per lane; N = 8/16/32 run one
+// job per N-lane group, lane r owning row r (forward) or column r (inverse)
+// in stage 1, with the int16 intermediate staged through LDS (row pitch N+2
+// to spread banks) for stage 2.
+#include "common.h"
+#include "../../../include/x265_amd.h"
+
+namespace x265amd {
+
+constexpr TransformMatrix kT32 = make_t32();
+
+template <int N>
+__device__ __forceinline__ constexpr int tcoef(int k, int n)
+{
+    return kT32.m[k * (32 / N)][n];
+}
+
+// forward N-point transform of x[] (exact integer), result in y[]
+template <int N>
+__device__ __forceinline__ void fwd_1d(const int (&x)[N], int (&y)[N])
+{
+    if constexpr (N == 4)
+    {
+        const int e0 = x[0] + x[3], o0 = x[0] - x[3], e1 = x[1] + x[2], o1 = x[1] - x[2];
+        y[0] = 64 * e0 + 64 * e1;
+        y[2] = 64 * e0 - 64 * e1;
+        y[1] = 83 * o0 + 36 * o1;
+        y[3] = 36 * o0 - 83 * o1;
+    }
+    else
+    {
+        int e[N / 2], o[N / 2], ye[N / 2];
+#pragma unroll
+        for (int k = 0; k < N / 2; k++) { e[k] = x[k] + x[N - 1 - k]; o[k] = x[k] - x[N - 1 - k]; }
+        fwd_1d<N / 2>(e, ye);
+#pragma unroll
+        for (int m = 0; m < N / 2; m++) y[2 * m] = ye[m];
+#pragma unroll
+        for (int m = 0; m < N / 2; m++)
+        {
+            int s = 0;
+#pragma unroll
+            for (int k = 0; k < N / 2; k++) s += tcoef<N>(2 * m + 1, k) * o[k];
+            y[2 * m + 1] = s;
+        }
+    }
+}
+
+// inverse N-point transform of coefficient vector c[] (exact integer)
+template <int N>
+__device__ __forceinline__ void inv_1d(const int (&c)[N], int (&y)[N])
+{
+    if constexpr (N == 4)
+    {
+        const int o0 = 83 * c[1] + 36 * c[3], o1 = 36 * c[1] - 83 * c[3];
+        const int e0 = 64 * c[0] + 64 * c[2], e1 = 64 * c[0] - 64 * c[2];
+        y[0] = e0 + o0; y[1] = e1 + o1; y[2] = e1 - o1; y[3] = e0 - o0;
+    }
+    else
+    {
+        int ce[N / 2], e[N / 2];
+#pragma unroll
+        for (int m = 0; m < N / 2; m++) ce[m] = c[2 * m];
+        inv_1d<N / 2>(ce, e);
+#pragma unroll
+        for (int k = 0; k < N / 2; k++)
+        {
+            int o = 0;
+#pragma unroll
+            for (int m = 0; m < N / 2; m++) o += tcoef<N>(2 * m + 1, k) * c[2 * m + 1];
+            y[k] = e[k] + o;
+            y[N - 1 - k] = e[k] - o;
+        }
+    }
+}
+
+__device__ __forceinline__ int fwd_round(int s, int shift) { return (int)(int16_t)((s + (1 << (shift - 1))) >> shift); }
+__device__ __forceinline__ int inv_round(int s, int shift) { return clip16((s + (1 << (shift - 1))) >> shift); }
+
+// DST-VII 4-point (fastForwardDst / inversedst), exact integer
+__device__ __forceinline__ void dst_fwd(const int (&b)[4], int (&y)[4])
+{
+    const int c0 = b[0] + b[3], c1 = b[1] + b[3], c2 = b[0] - b[1], c3 = 74 * b[2];
+    y[0] = 29 * c0 + 55 * c1 + c3;
+    y[1] = 74 * (b[0] + b[1] - b[3]);
+    y[2] = 29 * c2 + 55 * c0 - c3;
+    y[3] = 55 * c2 - 29 * c1 + c3;
+}
+__device__ __forceinline__ void dst_inv(const int (&t)[4], int (&y)[4])
+{
+    const int c0 = t[0] + t[2], c1 = t[2] + t[3], c2 = t[0] - t[3], c3 = 74 * t[1];
+    y[0] = 29 * c0 + 55 * c1 + c3;
+    y[1] = 55 * c2 - 29 * c1 + c3;
+    y[2] = 74 * (t[0] - t[2] + t[3]);
+    y[3] = 55 * c0 + 29 * c2 - c3;
+}
+
+// --------------------------------------------------------------- 4x4: lane per job
+template <int KIND>
+__global__ __launch_bounds__(X265AMD_BLOCK) void k_tr4(int n, int depth,
+    const int16_t* __restrict__ src, intptr_t ss, const int64_t* __restrict__ soff,
+    int16_t* __restrict__ dst, intptr_t ds, const int64_t* __restrict__ doff)
+{
+    const int64_t job = (int64_t)xcd_block() * X265AMD_BLOCK + threadIdx.x;
+    if (job >= n) return;
+    const int16_t* ps = src + soff[job];
+    int16_t* pd = dst + doff[job];
+    int m[4][4], t[4][4];
+#pragma unroll
+    for (int r = 0; r < 4; r++)
+    {
+        int v[4];
+        load_row16<4>(ps + r * ss, v);
+#pragma unroll
+        for (int c = 0; c < 4; c++) m[r][c] = v[c];
+    }
+    const bool fwd = KIND == X265AMD_DCT || KIND == X265AMD_DST;
+    const int sh1 = fwd ? 1 + depth - 8 : 7, sh2 = fwd ? 8 : 12 - (depth - 8);
+    if (fwd)
+    {
+        // stage 1: row i -> column i of t; stage 2: row i of t -> column i of out
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+        {
+            int y[4];
+            if (KIND == X265AMD_DST) dst_fwd(m[i], y); else fwd_1d<4>(m[i], y);
+#pragma unroll
+            for (int k = 0; k < 4; k++) t[k][i] = fwd_round(y[k], sh1);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+        {
+            int y[4];
+            if (KIND == X265AMD_DST) dst_fwd(t[i], y); else fwd_1d<4>(t[i], y);
+#pragma unroll
+            for (int k = 0; k < 4; k++) m[k][i] = fwd_round(y[k], sh2);
+        }
+    }
+    else
+    {
+        // stage 1: column j of input -> row j of t; stage 2: column j of t -> row j of out
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+        {
+            int c[4] = { m[0][j], m[1][j], m[2][j], m[3][j] }, y[4];
+            if (KIND == X265AMD_IDST) dst_inv(c, y); else inv_1d<4>(c, y);
+#pragma unroll
+            for (int k = 0; k < 4; k++) t[j][k] = inv_round(y[k], sh1);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+        {
+            int c[4] = { t[0][j], t[1][j], t[2][j], t[3][j] }, y[4];
+            if (KIND == X265AMD_IDST) dst_inv(c, y); else inv_1d<4>(c, y);
+#pragma unroll
+            for (int k = 0; k < 4; k++) m[j][k] = inv_round(y[k], sh2);
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; r++)
+    {
+        int v[4] = { m[r][0], m[r][1], m[r][2], m[r][3] };
+        store_row<int16_t, 4>(pd + r * ds, v);
+    }
+}
+
+// --------------------------------------------------------------- NxN: N lanes per job
+template <int N, bool FWD>
+__global__ __launch_bounds__(X265AMD_BLOCK) void k_trN(int n, int depth,
+    const int16_t* __restrict__ src, intptr_t ss, const int64_t* __restrict__ soff,
+    int16_t* __restrict__ dst, intptr_t ds, const int64_t* __restrict__ doff)
+{
+    constexpr int P = N + 2;                   // LDS row pitch (int16)
+    constexpr int JOBS = X265AMD_BLOCK / N;
+    __shared__ int16_t lds[JOBS][N * P];
+    const int slot = threadIdx.x / N, r = threadIdx.x % N;
+    const int64_t job = (int64_t)xcd_block() * JOBS + slot;
+    const bool live = job < n;
+    const int64_t jj = live ? job : 0;
+    int16_t* L = lds[slot];
+    constexpr int logN = N == 8 ? 3 : N == 16 ? 4 : 5;
+
+    if (FWD)
+    {
+        const int sh1 = logN - 1 + depth - 8, sh2 = logN + 6;
+        int x[N], y[N];
+        const int16_t* row = src + soff[jj] + r * ss;
+#pragma unroll
+        for (int i = 0; i < N; i += 8)
+        {
+            int t[8];
+            load_row16<8>(row + i, t);
+#pragma unroll
+            for (int k = 0; k < 8; k++) x[i + k] = t[k];
+        }
+        fwd_1d<N>(x, y);
+#pragma unroll
+        for (int k = 0; k < N; k++) L[k * P + r] = (int16_t)fwd_round(y[k], sh1);
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < N; i += 2)
+        {
+            uint32_t v = *(const uint32_t*)&L[r * P + i];
+            x[i] = (int16_t)(v & 0xffff);
+            x[i + 1] = (int16_t)(v >> 16);
+        }
+        fwd_1d<N>(x, y);
+        if (live)
+        {
+            int16_t* pd = dst + doff[jj];
+#pragma unroll
+            for (int k = 0; k < N; k++) pd[k * ds + r] = (int16_t)fwd_round(y[k], sh2);
+        }
+    }
+    else
+    {
+        const int sh1 = 7, sh2 = 12 - (depth - 8);
+        int c[N], y[N];
+        const int16_t* col = src + soff[jj] + r;
+#pragma unroll
+        for (int k = 0; k < N; k++) c[k] = col[k * ss];
+        inv_1d<N>(c, y);
+#pragma unroll
+        for (int k = 0; k < N; k++) L[r * P + k] = (int16_t)inv_round(y[k], sh1);
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < N; k++) c[k] = L[k * P + r];
+        inv_1d<N>(c, y);
+        if (live)
+        {
+            int16_t* pd = dst + doff[jj] + r * ds;
+#pragma unroll
+            for (int i = 0; i < N; i += 8)
+            {
+                int t[8];
+#pragma unroll
+                for (int k = 0; k < 8; k++) t[k] = inv_round(y[i + k], sh2);
+                store_row<int16_t, 8>(pd + i, t);
+            }
+        }
+    }
+}
+
+// --------------------------------------------------------------- quant family
+// one job per 64-lane wave; lane handles 8 coefficients per iteration
+template <bool NQUANT>
+__global__ __launch_bounds__(X265AMD_BLOCK) void k_quant(int n, int num,
+    const int16_t* __restrict__ coef, const int64_t* __restrict__ coff,
+    const int32_t* __restrict__ qtab, const int64_t* __restrict__ qoff,
+    int32_t* __restrict__ delta, const int64_t* __restrict__ doff,
+    int16_t* __restrict__ qout, const int64_t* __restrict__ ooff,
+    const int32_t* __restrict__ qbits, const int32_t* __restrict__ add, uint32_t* __restrict__ numsig)
+{
+    const int64_t job = (int64_t)xcd_block() * (X265AMD_BLOCK / 64) + threadIdx.x / 64;
+    const int lane = threadIdx.x & 63;
+    if (job >= n) return;   // wave-uniform
+    const int16_t* pc = coef + coff[job];
+    const int32_t* pq = qtab + qoff[job];
+    int16_t* po = qout + ooff[job];
+    int32_t* pdl = NQUANT ? nullptr : delta + doff[job];
+    const int qb = qbits[job], ad = add[job], qb8 = qb - 8;
+    uint32_t sig = 0;
+    for (int i = lane * 8; i < num; i += 64 * 8)
+    {
+        int c[8], o[8];
+        load_row16<8>(pc + i, c);
+        const int4 q0 = ldu<int4>(pq + i), q1 = ldu<int4>(pq + i + 4);
+        const int qv[8] = { q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w };
+        int dl[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++)
+        {
+            const int lv = c[k];
+            // int32 products/sums wrap exactly as the reference's int arithmetic (dct.cpp:676-678)
+            const uint32_t tmp = (uint32_t)abs(lv) * (uint32_t)qv[k];
+            int level = (int)(tmp + (uint32_t)ad) >> qb;
+            dl[k] = (int)(tmp - ((uint32_t)level << qb)) >> qb8;
+            sig += level != 0;
+            if (lv < 0) level = -level;
+            level = clip16(level);
+            o[k] = NQUANT ? abs(level) : level;
+        }
+        store_row<int16_t, 8>(po + i, o);
+        if (!NQUANT)
+        {
+            stu<int4>(pdl + i, make_int4(dl[0], dl[1], dl[2], dl[3]));
+            stu<int4>(pdl + i + 4, make_int4(dl[4], dl[5], dl[6], dl[7]));
+        }
+    }
+    for (int m = 32; m > 0; m >>= 1) sig += __shfl_xor(sig, m, 64);
+    if (lane == 0) numsig[job] = sig;
+}
+
+template <bool SCALING>
+__global__ __launch_bounds__(X265AMD_BLOCK) void k_dequant(int n, int num,
+    const int16_t* __restrict__ q, const int64_t* __restrict__ qoff,
+    const int32_t* __restrict__ dq, const int64_t* __restrict__ dqoff,
+    int16_t* __restrict__ out, const int64_t* __restrict__ ooff,
+    const int32_t* __restrict__ p0, const int32_t* __restrict__ p1)
+{
+    const int64_t job = (int64_t)xcd_block() * (X265AMD_BLOCK / 64) + threadIdx.x / 64;
+    const int lane = threadIdx.x & 63;
+    if (job >= n) return;
+    const int16_t* pq = q + qoff[job];
+    int16_t* po = out + ooff[job];
+    for (int i = lane * 8; i < num; i += 64 * 8)
+    {
+        int v[8], o[8];
+        load_row16<8>(pq + i, v);
+        if (!SCALING)
+        {
+            const int scale = p0[job], shift = p1[job], ad = 1 << (shift - 1);
+#pragma unroll
+            for (int k = 0; k < 8; k++) o[k] = clip16((v[k] * scale + ad) >> shift);
+        }
+        else
+        {
+            const int per = p0[job], shift = p1[job] + 4;
+            const int32_t* pd = dq + dqoff[job] + i;
+            const int4 d0 = ldu<int4>(pd), d1 = ldu<int4>(pd + 4);
+            const int dv[8] = { d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w };
+            if (shift > per)
+            {
+                const int ad = 1 << (shift - per - 1);
+#pragma unroll
+                for (int k = 0; k < 8; k++) o[k] = clip16((v[k] * dv[k] + ad) >> (shift - per));
+            }
+            else
+            {
+#pragma unroll
+                for (int k = 0; k < 8; k++) o[k] = clip16(clip16(v[k] * dv[k]) << (per - shift));
+            }
+        }
+        store_row<int16_t, 8>(po + i, o);
+    }
+}
+
+// count_nonzero (res == nullptr) / copy_cnt
+template <int N>
+__global__ __launch_bounds__(X265AMD_BLOCK) void k_count(int n, int16_t* __restrict__ coeff, const int64_t* __restrict__ coff,
+    const int16_t* __restrict__ res, intptr_t rs, const int64_t* __restrict__ roff, uint32_t* __restrict__ cnt)
+{
+    constexpr int G = N * N / 4 < 64 ? N * N / 4 : 64;   // 4 coefficients per lane per step
+    const int64_t job = (int64_t)xcd_block() * (X265AMD_BLOCK / G) + threadIdx.x / G;
+    const int lane = threadIdx.x & (G - 1);
+    const bool live = job < n;
+    uint32_t c = 0;
+    if (live)
+    {
+        int16_t* pc = coeff + coff[job];
+        for (int i = lane * 4; i < N * N; i += G * 4)
+        {
+            int v[4];
+            if (res)
+            {
+                const int y = i / N, x = i % N;
+                load_row16<4>(res + roff[job] + y * rs + x, v);
+                store_row<int16_t, 4>(pc + i, v);
+            }
+            else
+                load_row16<4>(pc + i, v);
+            c += (v[0] != 0) + (v[1] != 0) + (v[2] != 0) + (v[3] != 0);
+        }
+    }
+    for (int m = G >> 1; m > 0; m >>= 1) c += __shfl_xor(c, m, 64);
+    if (live && lane == 0) cnt[job] = c;
+}
+
+} // namespace x265amd
+
+using namespace x265amd;
+
+extern "C" int x265amd_transform(int kind, int depth, int size, int n,
+                                 const int16_t* src, intptr_t src_stride, const int64_t* src_off,
+                                 int16_t* dst, intptr_t dst_stride, const int64_t* dst_off, void* stream)
+{
+    if (n <= 0) return 0;
+    if (depth != 8 && depth != 10 && depth != 12) return X265AMD_EINVAL;
+    hipStream_t st = (hipStream_t)stream;
+    const bool fwd = kind == X265AMD_DCT || kind == X265AMD_DST;
+    if (kind == X265AMD_DST || kind == X265AMD_IDST || size == 4)
+    {
+        if (size != 4) return X265AMD_EINVAL;
+        const dim3 grid((n + X265AMD_BLOCK - 1) / X265AMD_BLOCK);
+        switch (kind)
+        {
+        case X265AMD_DCT: hipLaunchKernelGGL(k_tr4<X265AMD_DCT>, grid, dim3(X265AMD_BLOCK), 0, st, n, depth, src, src_stride, src_off, dst, dst_stride, dst_off); break;
+        case X265AMD_IDCT: hipLaunchKernelGGL(k_tr4<X265AMD_IDCT>, grid, dim3(X265AMD_BLOCK), 0, st, n, depth, src, src_stride, src_off, dst, dst_stride, dst_off); break;
+        case X265AMD_DST: hipLaunchKernelGGL(k_tr4<X265AMD_DST>, grid, dim3(X265AMD_BLOCK), 0, st, n, depth, src, src_stride, src_off, dst, dst_stride, dst_off); break;
+        case X265AMD_IDST: hipLaunchKernelGGL(k_tr4<X265AMD_IDST>, grid, dim3(X265AMD_BLOCK), 0, st, n, depth, src, src_stride, src_off, dst, dst_stride, dst_off); break;
+        default: return X265AMD_EINVAL;
+        }
+        return (int)hipGetLastError();
+    }
+    if (kind != X265AMD_DCT && kind != X265AMD_IDCT) return X265AMD_EINVAL;
+    const int jobs = X265AMD_BLOCK / size;
+    const dim3 grid((n + jobs - 1) / jobs);
+#define T(N)                                                                                                       \
+    if (fwd) hipLaunchKernelGGL((k_trN<N, true>), grid, dim3(X265AMD_BLOCK), 0, st, n, depth, src, src_stride,    \
+                                src_off, dst, dst_stride, dst_off);                                             \
+    else hipLaunchKernelGGL((k_trN<N, false>), grid, dim3(X265AMD_BLOCK), 0, st, n, depth, src, src_stride,       \
+                            src_off, dst, dst_stride, dst_off)
+    switch (size)
+    {
+    case 8: T(8); break;
+    case 16: T(16); break;
+    case 32: T(32); break;
+    default: return X265AMD_EINVAL;
+    }
+#undef T
+    return (int)hipGetLastError();
+}
+
+extern "C" int x265amd_quant(int n, int num, const int16_t* coef, const int64_t* coef_off,
+                             const int32_t* qtab, const int64_t* qtab_off,
+                             int32_t* delta_u, const int64_t* delta_off,
+                             int16_t* qcoef, const int64_t* qcoef_off,
+                             const int32_t* qbits, const int32_t* add, uint32_t* num_sig, void* stream)
+{
+    if (n <= 0) return 0;
+    if (num <= 0 || num % 16 || num > 1024) return X265AMD_EINVAL;
+    const dim3 grid((n + 3) / 4);
+    hipStream_t st = (hipStream_t)stream;
+    if (delta_u)
+        hipLaunchKernelGGL(k_quant<false>, grid, dim3(X265AMD_BLOCK), 0, st, n, num, coef, coef_off, qtab, qtab_off,
+                           delta_u, delta_off, qcoef, qcoef_off, qbits, add, num_sig);
+    else
+        hipLaunchKernelGGL(k_quant<true>, grid, dim3(X265AMD_BLOCK), 0, st, n, num, coef, coef_off, qtab, qtab_off,
+                           delta_u, delta_off, qcoef, qcoef_off, qbits, add, num_sig);
+    return (int)hipGetLastError();
+}
+
+extern "C" int x265amd_dequant_normal(int n, int num, const int16_t* q, const int64_t* q_off,
+                                      int16_t* coef, const int64_t* coef_off,
+                                      const int32_t* scale, const int32_t* shift, void* stream)
+{
+    if (n <= 0) return 0;
+    if (num <= 0 || num % 8 || num > 1024) return X265AMD_EINVAL;
+    hipLaunchKernelGGL(k_dequant<false>, dim3((n + 3) / 4), dim3(X265AMD_BLOCK), 0, (hipStream_t)stream, n, num, q, q_off,
+                       (const int32_t*)nullptr, (const int64_t*)nullptr, coef, coef_off, scale, shift);
+    return (int)hipGetLastError();
+}
+
+extern "C" int x265amd_dequant_scaling(int n, int num, const int16_t* q, const int64_t* q_off,
+                                       const int32_t* dq, const int64_t* dq_off,
+                                       int16_t* coef, const int64_t* coef_off,
+                                       const int32_t* per, const int32_t* shift, void* stream)
+{
+    if (n <= 0) return 0;
+    if (num <= 0 || num % 8 || num > 1024) return X265AMD_EINVAL;
+    hipLaunchKernelGGL(k_dequant<true>, dim3((n + 3) / 4), dim3(X265AMD_BLOCK), 0, (hipStream_t)stream, n, num, q, q_off,
+                       dq, dq_off, coef, coef_off, per, shift);
+    return (int)hipGetLastError();
+}
+
+extern "C" int x265amd_count_nonzero(int size, int n, int16_t* coeff, const int64_t* coeff_off,
+                                     const int16_t* res, intptr_t res_stride, const int64_t* res_off,
+                                     uint32_t* count, void* stream)
+{
+    if (n <= 0) return 0;
+    hipStream_t st = (hipStream_t)stream;
+#define C(N)                                                                                          \
+    {                                                                                                 \
+        constexpr int G = N * N / 4 < 64 ? N * N / 4 : 64;                                            \
+        const int per = X265AMD_BLOCK / G;                                                            \
+        hipLaunchKernelGGL(k_count<N>, dim3((n + per - 1) / per), dim3(X265AMD_BLOCK), 0, st, n, coeff, \
+                           coeff_off, res, res_stride, res_off, count);                               \
+        return (int)hipGetLastError();                                                                \
+    }
+    switch (size)
+    {
+    case 4: C(4);
+    case 8: C(8);
+    case 16: C(16);
+    case 32: C(32);
+    }
+#undef C
+    return X265AMD_EINVAL;
+}

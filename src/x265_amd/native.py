@@ -1,0 +1,119 @@
+"""ctypes binding of libx265amd.so (include/x265_amd.h) for torch device tensors.
+
+This is host plumbing only: torch provides device memory and the stream; all
+arithmetic runs in the hand-written gfx950 kernels of csrc/.  There is no CPU
+fallback — if the library is missing or a call fails, an exception is raised.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libx265amd.so")
+
+_vp, _ip, _int = C.c_void_p, C.c_ssize_t, C.c_int
+
+
+class X265AmdError(RuntimeError):
+    pass
+
+
+def _ptr(t):
+    if t is None:
+        return None
+    return _vp(t.data_ptr())
+
+
+def _stream():
+    import torch
+
+    return _vp(torch.cuda.current_stream().cuda_stream)
+
+
+class Primitives:
+    """Batched primitive calls on torch tensors (all tensors on the current device)."""
+
+    _lib = None
+
+    def __init__(self, device: int | None = None):
+        if Primitives._lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise X265AmdError(f"{LIB_PATH} not built: run __graft_entry__.build()")
+            lib = C.CDLL(LIB_PATH)
+            lib.x265amd_strerror.restype = C.c_char_p
+            lib.x265amd_target.restype = C.c_char_p
+            Primitives._lib = lib
+        self.lib = Primitives._lib
+        if device is not None:
+            self._check(self.lib.x265amd_set_device(int(device)), "set_device")
+
+    def _check(self, rc: int, what: str):
+        if rc != 0:
+            raise X265AmdError(f"x265amd_{what}: {self.lib.x265amd_strerror(rc).decode()} (status {rc})")
+
+    # -- a4 a6 a7 a8 a15
+    def pixelcmp(self, op, depth, w, h, a, sa, aoff, b, sb, boff, out, stream=None):
+        n = aoff.numel()
+        self._check(self.lib.x265amd_pixelcmp(op, depth, w, h, n, _ptr(a), _ip(sa), _ptr(aoff), _ptr(b), _ip(sb),
+                                              _ptr(boff), _ptr(out), stream or _stream()), "pixelcmp")
+
+    # -- a5
+    def sad_multi(self, nref, depth, w, h, f, fs, foff, r, rs, roff, out, stream=None):
+        n = foff.numel()
+        self._check(self.lib.x265amd_sad_multi(nref, depth, w, h, n, _ptr(f), _ip(fs), _ptr(foff), _ptr(r), _ip(rs),
+                                               _ptr(roff), _ptr(out), stream or _stream()), "sad_multi")
+
+    # -- a9
+    def interp(self, op, taps, depth, w, h, s, ss, soff, d, ds, doff, coeff, rowext=0, stream=None):
+        n = soff.numel()
+        self._check(self.lib.x265amd_interp(op, taps, depth, w, h, n, _ptr(s), _ip(ss), _ptr(soff), _ptr(d), _ip(ds),
+                                            _ptr(doff), _ptr(coeff), rowext, stream or _stream()), "interp")
+
+    # -- a10 a11
+    def transform(self, kind, depth, size, s, ss, soff, d, ds, doff, stream=None):
+        n = soff.numel()
+        self._check(self.lib.x265amd_transform(kind, depth, size, n, _ptr(s), _ip(ss), _ptr(soff), _ptr(d), _ip(ds),
+                                               _ptr(doff), stream or _stream()), "transform")
+
+    # -- a12 a13
+    def quant(self, num, c, co, q, qo, dl, dlo, o, oo, qb, ad, sig, stream=None):
+        n = co.numel()
+        self._check(self.lib.x265amd_quant(n, num, _ptr(c), _ptr(co), _ptr(q), _ptr(qo), _ptr(dl), _ptr(dlo), _ptr(o),
+                                           _ptr(oo), _ptr(qb), _ptr(ad), _ptr(sig), stream or _stream()), "quant")
+
+    def dequant_normal(self, num, q, qo, o, oo, scale, shift, stream=None):
+        n = qo.numel()
+        self._check(self.lib.x265amd_dequant_normal(n, num, _ptr(q), _ptr(qo), _ptr(o), _ptr(oo), _ptr(scale),
+                                                    _ptr(shift), stream or _stream()), "dequant_normal")
+
+    def dequant_scaling(self, num, q, qo, dq, dqo, o, oo, per, shift, stream=None):
+        n = qo.numel()
+        self._check(self.lib.x265amd_dequant_scaling(n, num, _ptr(q), _ptr(qo), _ptr(dq), _ptr(dqo), _ptr(o),
+                                                     _ptr(oo), _ptr(per), _ptr(shift), stream or _stream()),
+                    "dequant_scaling")
+
+    # -- a14
+    def intra_filter(self, depth, size, s, soff, d, doff, stream=None):
+        self._check(self.lib.x265amd_intra_filter(depth, size, soff.numel(), _ptr(s), _ptr(soff), _ptr(d), _ptr(doff),
+                                                  stream or _stream()), "intra_filter")
+
+    def intra_pred(self, depth, size, d, ds, doff, nb, nboff, mode, bfilter, stream=None):
+        self._check(self.lib.x265amd_intra_pred(depth, size, doff.numel(), _ptr(d), _ip(ds), _ptr(doff), _ptr(nb),
+                                                _ptr(nboff), _ptr(mode), _ptr(bfilter), stream or _stream()),
+                    "intra_pred")
+
+    def intra_allangs(self, depth, size, d, doff, ref, roff, filt, foff, bluma, stream=None):
+        self._check(self.lib.x265amd_intra_allangs(depth, size, doff.numel(), _ptr(d), _ptr(doff), _ptr(ref),
+                                                   _ptr(roff), _ptr(filt), _ptr(foff), _ptr(bluma),
+                                                   stream or _stream()), "intra_allangs")
+
+    # -- a15
+    def blockop(self, op, depth, w, h, d, ds, doff, a, sa, aoff, b, sb, boff, param=0, stream=None):
+        self._check(self.lib.x265amd_blockop(op, depth, w, h, doff.numel(), _ptr(d), _ip(ds), _ptr(doff), _ptr(a),
+                                             _ip(sa), _ptr(aoff), _ptr(b), _ip(sb), _ptr(boff), int(param),
+                                             stream or _stream()), "blockop")
+
+    def count_nonzero(self, size, c, co, r, rs, ro, cnt, stream=None):
+        self._check(self.lib.x265amd_count_nonzero(size, co.numel(), _ptr(c), _ptr(co), _ptr(r), _ip(rs), _ptr(ro),
+                                                   _ptr(cnt), stream or _stream()), "count_nonzero")

@@ -1,0 +1,525 @@
+"""Deterministic batch test cases for every primitive family of the C ABI.
+
+A Case holds host numpy buffers (inputs, per-job offset arrays, outputs
+pre-filled with a 0xCD sentinel) plus the parameters of one batched call.
+The same Case runs on
+  * the CPU checkers   (oracle/pyoracle.py: restatement or reference C), and
+  * the GPU library    (src/x265_amd/native.py),
+and the WHOLE output buffers are compared, so a write outside a job's block
+is caught exactly like the reference harness catches it
+(ipfilterharness.cpp:49-52,277).
+
+Inputs follow the reference TestBench's three classes — random, minimum,
+maximum (pixelharness.cpp:33-77, mbdstharness.cpp:56-81,
+ipfilterharness.cpp:32-62, intrapredharness.cpp:30-44) — and come from a
+counter-based splitmix64 generator, so the golden fixtures only need to
+store (family, params, seed) and the SHA-256 of each output.
+"""
+from __future__ import annotations
+
+import hashlib
+from dataclasses import dataclass, field
+
+import numpy as np
+
+# ---------------------------------------------------------------- constants
+# op / kind codes, identical to include/x265_amd.h and oracle/x265_oracle.h
+SAD, SATD, SA8D, SSE_PP, SSE_SS, PSY, SSD_S, VAR = range(8)
+HPP, HPS, VPP, VPS, VSP, VSS, HVPP, P2S = range(8)
+DCT, IDCT, DST, IDST = range(4)
+(SUB_PS, ADD_PS, ADDAVG, PIXELAVG, COPY_PP, COPY_SP, COPY_PS, COPY_SS, BLOCKFILL,
+ CPY2D1D_SHL, CPY2D1D_SHR, CPY1D2D_SHL, CPY1D2D_SHR, TRANSPOSE) = range(14)
+
+CMP_NAMES = ["sad", "satd", "sa8d", "sse_pp", "sse_ss", "psy", "ssd_s", "var"]
+INTERP_NAMES = ["hpp", "hps", "vpp", "vps", "vsp", "vss", "hvpp", "p2s"]
+BLOCK_NAMES = ["sub_ps", "add_ps", "addavg", "pixelavg", "copy_pp", "copy_sp", "copy_ps", "copy_ss", "blockfill",
+               "cpy2d1d_shl", "cpy2d1d_shr", "cpy1d2d_shl", "cpy1d2d_shr", "transpose"]
+
+# luma PU sizes (primitives.h:39-53)
+LUMA_PU = [(4, 4), (8, 8), (16, 16), (32, 32), (64, 64), (8, 4), (4, 8), (16, 8), (8, 16), (32, 16), (16, 32),
+           (64, 32), (32, 64), (16, 12), (12, 16), (16, 4), (4, 16), (32, 24), (24, 32), (32, 8), (8, 32),
+           (64, 48), (48, 64), (64, 16), (16, 64)]
+CHROMA420_PU = [(w // 2, h // 2) for (w, h) in LUMA_PU]
+CHROMA422_PU = [(w // 2, h) for (w, h) in LUMA_PU]
+CU_SQ = [4, 8, 16, 32, 64]
+TU_SQ = [4, 8, 16, 32]
+
+
+def unique(seq):
+    out = []
+    for s in seq:
+        if s not in out:
+            out.append(s)
+    return out
+
+
+# satd entries that are non-NULL after setupAliasPrimitives (pixel.cpp:980-1151, primitives.cpp:119-161)
+SATD_SIZES = unique(LUMA_PU + [(w, h) for (w, h) in CHROMA420_PU + CHROMA422_PU if w % 4 == 0 and h % 4 == 0])
+SA8D_SIZES = [(4, 4), (8, 8), (16, 16), (32, 32), (64, 64), (4, 8), (8, 16), (16, 32), (32, 64)]
+SSE_PP_SIZES = [(n, n) for n in CU_SQ] + [(4, 8), (8, 16), (16, 32), (32, 64)]
+# chroma 4:2:0 2x2 (from luma 4x4, intra only) has no filter entries (ipfilter.cpp:424-471)
+INTERP_CHROMA_SIZES = [s for s in unique(CHROMA420_PU + CHROMA422_PU + LUMA_PU) if s != (2, 2)]
+
+
+# ---------------------------------------------------------------- determinism
+def splitmix64(x: np.ndarray) -> np.ndarray:
+    z = (x + np.uint64(0x9E3779B97F4A7C15)).astype(np.uint64)
+    z = ((z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)).astype(np.uint64)
+    z = ((z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)).astype(np.uint64)
+    return z ^ (z >> np.uint64(31))
+
+
+class Det:
+    """Counter-based deterministic generator (splitmix64 of seed:counter)."""
+
+    def __init__(self, seed: int):
+        self.base = np.uint64((seed * 0x100000001B3) & 0xFFFFFFFFFFFFFFFF)
+        self.ctr = 0
+
+    def u64(self, n: int) -> np.ndarray:
+        idx = np.arange(self.ctr, self.ctr + n, dtype=np.uint64)
+        self.ctr += n
+        with np.errstate(over="ignore"):
+            return splitmix64(idx * np.uint64(0x2545F4914F6CDD1D) + self.base)
+
+    def ints(self, lo: int, hi: int, n: int) -> np.ndarray:
+        """integers in [lo, hi)"""
+        return (lo + (self.u64(n) % np.uint64(hi - lo)).astype(np.int64)).astype(np.int64)
+
+
+def seed_of(*parts) -> int:
+    h = hashlib.sha256(repr(parts).encode()).digest()
+    return int.from_bytes(h[:6], "little")
+
+
+def sha(a: np.ndarray) -> str:
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()[:32]
+
+
+def pixel_dtype(depth: int):
+    return np.uint8 if depth == 8 else np.uint16
+
+
+# ---------------------------------------------------------------- buffers
+CLASS_RANDOM, CLASS_MIN, CLASS_MAX = 0, 1, 2
+
+
+@dataclass
+class Plane:
+    """3 class regions (random / min / max) stacked vertically, each `rows` x stride."""
+    data: np.ndarray
+    stride: int
+    rows: int
+
+    def offset(self, cls: int, x: int, y: int) -> int:
+        return (cls * self.rows + y) * self.stride + x
+
+
+def make_plane(det: Det, dtype, stride: int, rows: int, lo: int, hi: int, vmin: int, vmax: int) -> Plane:
+    n = stride * rows
+    rnd = det.ints(lo, hi, n).astype(dtype)
+    data = np.concatenate([rnd, np.full(n, vmin, dtype=dtype), np.full(n, vmax, dtype=dtype)])
+    return Plane(data, stride, rows)
+
+
+def job_offsets(det: Det, plane: Plane, n: int, w: int, h: int, margin: int, classes=None):
+    """random block origins with `margin` elements of context on every side"""
+    cls = det.ints(0, 3, n) if classes is None else np.full(n, classes, np.int64)
+    xs = det.ints(margin, plane.stride - w - margin + 1, n)
+    ys = det.ints(margin, plane.rows - h - margin + 1, n)
+    return np.array([plane.offset(int(c), int(x), int(y)) for c, x, y in zip(cls, xs, ys)], dtype=np.int64)
+
+
+def out_slots(n: int, w: int, h: int, dtype, stride: int | None = None, pad: int = 4):
+    """disjoint output blocks, sentinel-filled, with `pad` elements around each"""
+    stride = stride or (w + 2 * pad)
+    rows = h + 2 * pad
+    buf = np.empty(n * rows * stride, dtype=dtype)
+    buf.view(np.uint8)[:] = 0xCD
+    offs = np.array([(i * rows + pad) * stride + pad for i in range(n)], dtype=np.int64)
+    return buf, stride, offs
+
+
+@dataclass
+class Case:
+    family: str
+    params: dict
+    bufs: dict = field(default_factory=dict)
+    outs: list = field(default_factory=list)
+
+    def key(self) -> str:
+        p = ",".join(f"{k}={v}" for k, v in sorted(self.params.items()))
+        return f"{self.family}({p})"
+
+    def output_hashes(self, outs: dict) -> dict:
+        return {k: sha(outs[k]) for k in self.outs}
+
+
+# ---------------------------------------------------------------- generators
+def case_pixelcmp(op: int, w: int, h: int, depth: int, n: int, seed: int) -> Case:
+    det = Det(seed)
+    pmax = (1 << depth) - 1
+    if op in (SSE_SS, SSD_S):
+        if op == SSE_SS:   # residual_test_buff: [-RMAX-1, RMAX], RMAX = PIXEL_MAX
+            lo, hi, vmin, vmax = -pmax - 1, pmax + 1, -pmax, pmax
+        else:              # sbuf1: [-SMAX-1, SMAX], SMAX = 1 << 12
+            lo, hi, vmin, vmax = -(1 << 12) - 1, (1 << 12) + 1, -(1 << 12), 1 << 12
+        dt = np.int16
+    else:
+        lo, hi, vmin, vmax, dt = 0, pmax, 0, pmax, pixel_dtype(depth)
+    stride = w + 24
+    a = make_plane(det, dt, stride, h + 16, lo, hi, vmin, vmax)
+    b = make_plane(det, dt, stride, h + 16, lo, hi, vmin, vmax)
+    aoff = job_offsets(det, a, n, w, h, 4)
+    boff = job_offsets(det, b, n, w, h, 4)
+    wide = op in (SSE_PP, SSE_SS, SSD_S, VAR)
+    out = np.full(n, 0x7FFFFFFF if not wide else 0xCDCDCDCDCDCDCDCD, dtype=np.uint64 if wide else np.int32)
+    return Case("pixelcmp", dict(op=op, w=w, h=h, depth=depth, n=n, seed=seed),
+                dict(a=a.data, sa=stride, aoff=aoff, b=b.data, sb=stride, boff=boff, out=out), ["out"])
+
+
+def case_sad_multi(nref: int, w: int, h: int, depth: int, n: int, seed: int) -> Case:
+    det = Det(seed)
+    pmax = (1 << depth) - 1
+    dt = pixel_dtype(depth)
+    fenc = make_plane(det, dt, 64, h + 8, 0, pmax, 0, pmax)       # FENC_STRIDE buffers
+    ref = make_plane(det, dt, w + 40, h + 24, 0, pmax, 0, pmax)
+    foff = np.array([fenc.offset(int(c), 0, int(y)) for c, y in zip(det.ints(0, 3, n), det.ints(0, 9, n))],
+                    dtype=np.int64)
+    roff = job_offsets(det, ref, n * nref, w, h, 4)
+    out = np.full(n * nref, 0x7FFFFFFF, dtype=np.int32)
+    return Case("sad_multi", dict(nref=nref, w=w, h=h, depth=depth, n=n, seed=seed),
+                dict(f=fenc.data, fs=64, foff=foff, r=ref.data, rs=ref.stride, roff=roff, out=out), ["out"])
+
+
+def case_interp(op: int, taps: int, w: int, h: int, depth: int, n: int, seed: int, rowext: int = 0) -> Case:
+    det = Det(seed)
+    pmax = (1 << depth) - 1
+    pdt = pixel_dtype(depth)
+    src16 = op in (VSP, VSS)
+    dst16 = op in (HPS, VPS, VSS, P2S)
+    stride = w + 32
+    if src16:   # short_test_buff: [-SMAX, SMAX), SMAX = 1 << 12
+        src = make_plane(det, np.int16, stride, h + 24, -(1 << 12), 1 << 12, -(1 << 12), 1 << 12)
+    else:
+        src = make_plane(det, pdt, stride, h + 24, 0, pmax + 1, 0, pmax)
+    soff = job_offsets(det, src, n, w, h, 8)
+    nidx = 4 if taps == 8 else 8
+    if op == HVPP:
+        coeff = (det.ints(0, 4, n) | (det.ints(0, 4, n) << 4)).astype(np.uint8)
+    else:
+        coeff = det.ints(0, nidx, n).astype(np.uint8)
+    rows = h + (taps - 1 if (op == HPS and rowext) else 0)
+    dst, ds, doff = out_slots(n, w, rows, np.int16 if dst16 else pdt)
+    return Case("interp", dict(op=op, taps=taps, w=w, h=h, depth=depth, n=n, seed=seed, rowext=rowext),
+                dict(s=src.data, ss=stride, soff=soff, d=dst, ds=ds, doff=doff, coeff=coeff), ["d"])
+
+
+def case_transform(kind: int, size: int, depth: int, n: int, seed: int) -> Case:
+    det = Det(seed)
+    pmax = (1 << depth) - 1
+    stride = size + 8
+    if kind in (DCT, DST):     # residual range (mbdstharness.cpp:63)
+        src = make_plane(det, np.int16, stride, size + 8, -pmax, pmax + 1, -pmax, pmax)
+    else:                      # int_idct_test_buff: full int16 range
+        src = make_plane(det, np.int16, stride, size + 8, -32767, 32767, -32767, 32767)
+    soff = job_offsets(det, src, n, size, size, 2)
+    dst, ds, doff = out_slots(n, size, size, np.int16, stride=size + 4)
+    return Case("transform", dict(kind=kind, size=size, depth=depth, n=n, seed=seed),
+                dict(s=src.data, ss=stride, soff=soff, d=dst, ds=ds, doff=doff), ["d"])
+
+
+def case_quant(nquant: bool, size: int, depth: int, n: int, seed: int) -> Case:
+    det = Det(seed)
+    pmax = (1 << depth) - 1
+    num = size * size
+    coef = make_plane(det, np.int16, num, 2, -pmax, pmax + 1, -pmax, pmax)
+    qtab = make_plane(det, np.int32, num, 2, 0, pmax, -pmax, pmax)
+    co = np.array([coef.offset(int(c), 0, int(y)) for c, y in zip(det.ints(0, 3, n), det.ints(0, 2, n))], np.int64)
+    qo = np.array([qtab.offset(int(c), 0, int(y)) for c, y in zip(det.ints(0, 3, n), det.ints(0, 2, n))], np.int64)
+    # quant parameters as the harness draws them (mbdstharness.cpp:206-233)
+    qp = det.ints(0, 51 + 6 * (depth - 8) + 1, n)
+    per = qp // 6
+    log2 = int(np.log2(size))
+    tshift = 15 - depth - log2
+    qbits = (14 + per + tshift).astype(np.int32)
+    slice_i = det.ints(0, 2, n)
+    add = (np.where(slice_i == 1, 171, 85) << (qbits - 9)).astype(np.int32)
+    qout = np.full(n * num, -12851, np.int16)
+    delta = np.full(n * num, -842150451, np.int32)
+    oo = np.arange(n, dtype=np.int64) * num
+    sig = np.full(n, 0xCDCDCDCD, np.uint32)
+    bufs = dict(c=coef.data, co=co, q=qtab.data, qo=qo, o=qout, oo=oo, qb=qbits, ad=add, sig=sig,
+                dl=None if nquant else delta, dlo=None if nquant else oo.copy())
+    outs = ["o", "sig"] + ([] if nquant else ["dl"])
+    return Case("quant", dict(nquant=int(nquant), size=size, depth=depth, n=n, seed=seed), bufs, outs)
+
+
+def case_dequant(scaling: bool, size: int, depth: int, n: int, seed: int) -> Case:
+    det = Det(seed)
+    num = size * size
+    pmax = (1 << depth) - 1
+    q = make_plane(det, np.int16, num, 2, -pmax, pmax + 1, -pmax, pmax)   # short_test_buff (mbdstharness.cpp:63)
+    qo = np.array([q.offset(int(c), 0, int(y)) for c, y in zip(det.ints(0, 3, n), det.ints(0, 2, n))], np.int64)
+    log2 = int(np.log2(size))
+    qp = det.ints(0, 51 + 6 * (depth - 8) + 1, n)
+    per = (qp // 6).astype(np.int32)
+    tshift = 15 - depth - log2
+    shift = np.full(n, 20 - 14 - tshift, np.int32)      # QUANT_IQUANT_SHIFT - QUANT_SHIFT - transformShift
+    out = np.full(n * num, -12851, np.int16)
+    oo = np.arange(n, dtype=np.int64) * num
+    if scaling:
+        dq = make_plane(det, np.int32, num, 2, 0, (1 << depth) - 1, 0, (1 << depth) - 1)
+        dqo = np.array([dq.offset(int(c), 0, int(y)) for c, y in zip(det.ints(0, 3, n), det.ints(0, 2, n))], np.int64)
+        bufs = dict(q=q.data, qo=qo, dq=dq.data, dqo=dqo, o=out, oo=oo, p0=per, p1=shift)
+    else:
+        # scale = invQuantScales[rem] << per, as the harness draws it (mbdstharness.cpp:149-155)
+        inv = np.array([40, 45, 51, 57, 64, 72], np.int32)
+        scale = (inv[qp % 6] << per).astype(np.int32)
+        bufs = dict(q=q.data, qo=qo, dq=None, dqo=None, o=out, oo=oo, p0=scale, p1=shift)
+    return Case("dequant", dict(scaling=int(scaling), size=size, depth=depth, n=n, seed=seed), bufs, ["o"])
+
+
+def case_intra(kind: int, size: int, depth: int, n: int, seed: int, mode: int = -1) -> Case:
+    """kind 0 = intra_filter, 1 = intra_pred (mode per job; -1 = random), 2 = allangs"""
+    det = Det(seed)
+    pmax = (1 << depth) - 1
+    pdt = pixel_dtype(depth)
+    nbn = 4 * size + 1
+    nb = make_plane(det, pdt, nbn + 3, 3, 0, pmax, 0, pmax)
+    nbo = job_offsets(det, nb, n, nbn, 1, 1)
+    filt = make_plane(det, pdt, nbn + 3, 3, 0, pmax, 0, pmax)
+    fo = job_offsets(det, filt, n, nbn, 1, 1)
+    modes = (det.ints(0, 35, n) if mode < 0 else np.full(n, mode, np.int64)).astype(np.uint8)
+    bf = det.ints(0, 2, n).astype(np.uint8)
+    if kind == 0:
+        d, ds, doff = out_slots(n, nbn, 1, pdt)
+    elif kind == 1:
+        d, ds, doff = out_slots(n, size, size, pdt)
+    else:
+        d, ds, doff = out_slots(n, size * size, 33, pdt, stride=size * size, pad=0)
+    return Case("intra", dict(kind=kind, size=size, depth=depth, n=n, seed=seed, mode=mode),
+                dict(d=d, ds=ds, doff=doff, nb=nb.data, nbo=nbo, f=filt.data, fo=fo, mode=modes, bf=bf), ["d"])
+
+
+def case_blockop(op: int, w: int, h: int, depth: int, n: int, seed: int) -> Case:
+    det = Det(seed)
+    pmax = (1 << depth) - 1
+    pdt = pixel_dtype(depth)
+    d16 = op in (SUB_PS, COPY_PS, COPY_SS, BLOCKFILL, CPY2D1D_SHL, CPY2D1D_SHR, CPY1D2D_SHL, CPY1D2D_SHR)
+    stride = w + 16
+    # operand classes per op (pixelharness.cpp:33-77)
+    if op in (ADDAVG,):
+        a = make_plane(det, np.int16, stride, h + 8, 0, 16383, -16384, 16383)
+        b = make_plane(det, np.int16, stride, h + 8, 0, 16383, -16384, 16383)
+    elif op == ADD_PS:
+        a = make_plane(det, pdt, stride, h + 8, 0, pmax, 0, pmax)
+        b = make_plane(det, np.int16, stride, h + 8, -(1 << 12) - 1, (1 << 12) + 1, -(1 << 12), 1 << 12)
+    elif op in (COPY_SP,):
+        a = make_plane(det, np.int16, stride, h + 8, 0, pmax + 1, 0, pmax)
+        b = a
+    elif op in (COPY_SS, CPY2D1D_SHL, CPY2D1D_SHR, CPY1D2D_SHL, CPY1D2D_SHR):
+        a = make_plane(det, np.int16, stride, h + 8, -(1 << 12) - 1, (1 << 12) + 1, -(1 << 12), 1 << 12)
+        b = a
+    else:
+        a = make_plane(det, pdt, stride, h + 8, 0, pmax, 0, pmax)
+        b = make_plane(det, pdt, stride, h + 8, 0, pmax, 0, pmax)
+    aoff = job_offsets(det, a, n, w, h, 2)
+    boff = job_offsets(det, b, n, w, h, 2)
+    if op in (CPY2D1D_SHL, CPY2D1D_SHR, TRANSPOSE):
+        d, ds, doff = out_slots(n, w, h, np.int16 if d16 else pdt, stride=w, pad=0)
+    else:
+        d, ds, doff = out_slots(n, w, h, np.int16 if d16 else pdt)
+    if op in (CPY1D2D_SHL, CPY1D2D_SHR):
+        # 1-D source: contiguous w*w blocks
+        src, _, so = out_slots(n, w, h, np.int16, stride=w, pad=0)
+        src[:] = det.ints(-(1 << 12), 1 << 12, src.size).astype(np.int16)
+        a, aoff, sa = src, so, w
+    else:
+        sa = stride
+        a = a.data
+    if op == BLOCKFILL:
+        param = int(det.ints(-32768, 32768, 1)[0])
+    elif op in (CPY2D1D_SHL, CPY1D2D_SHL):
+        param = int(det.ints(0, 6, 1)[0])
+    elif op in (CPY2D1D_SHR, CPY1D2D_SHR):
+        param = int(det.ints(1, 6, 1)[0])
+    else:
+        param = 0
+    bdata = b.data if hasattr(b, "data") and not isinstance(b, np.ndarray) else b
+    return Case("blockop", dict(op=op, w=w, h=h, depth=depth, n=n, seed=seed),
+                dict(d=d, ds=ds, doff=doff, a=a, sa=sa, aoff=aoff, b=bdata, sb=stride, boff=boff, param=param), ["d"])
+
+
+def case_count(size: int, copy: bool, depth: int, n: int, seed: int) -> Case:
+    det = Det(seed)
+    num = size * size
+    # sparse coefficients (about 1 in 3 non-zero)
+    vals = det.ints(-40, 41, 3 * num * 2).astype(np.int16)
+    vals[det.ints(0, 3, vals.size) != 0] = 0
+    res_stride = size + 8
+    if copy:
+        r = np.zeros(res_stride * (size + 4) * n, np.int16)
+        r[:vals.size] = vals[: min(vals.size, r.size)]
+        ro = np.array([i * res_stride * (size + 4) for i in range(n)], np.int64)
+        c = np.full(n * num, -12851, np.int16)
+        co = np.arange(n, dtype=np.int64) * num
+        bufs = dict(c=c, co=co, r=r, rs=res_stride, ro=ro, cnt=np.full(n, 0xCDCDCDCD, np.uint32))
+        outs = ["c", "cnt"]
+    else:
+        c = np.resize(vals, n * num).astype(np.int16)
+        co = np.arange(n, dtype=np.int64) * num
+        bufs = dict(c=c, co=co, r=None, rs=0, ro=None, cnt=np.full(n, 0xCDCDCDCD, np.uint32))
+        outs = ["cnt"]
+    return Case("count", dict(size=size, copy=int(copy), depth=depth, n=n, seed=seed), bufs, outs)
+
+
+# ---------------------------------------------------------------- catalogue
+def blockop_sizes(op: int):
+    if op in (SUB_PS, ADD_PS, COPY_SP, COPY_PS, COPY_SS):
+        return unique([(n, n) for n in CU_SQ] + [(n // 2, n // 2) for n in CU_SQ] + [(2, 4), (4, 8), (8, 16), (16, 32), (32, 64)])
+    if op in (ADDAVG, COPY_PP):
+        return unique(LUMA_PU + CHROMA420_PU + CHROMA422_PU)
+    if op == PIXELAVG:
+        return LUMA_PU
+    if op == BLOCKFILL or op in (CPY2D1D_SHL, CPY2D1D_SHR, CPY1D2D_SHL, CPY1D2D_SHR, TRANSPOSE):
+        return [(n, n) for n in CU_SQ]
+    return []
+
+
+def all_cases(depth: int, n: int = 6, quick: bool = False):
+    """Every (family, op, shape) the reference table holds, one Case each."""
+    cases = []
+    s = lambda *p: seed_of(depth, *p)
+    for op in (SAD, SATD, SA8D, SSE_PP, SSE_SS, PSY, SSD_S, VAR):
+        if op == SAD:
+            sizes = LUMA_PU
+        elif op == SATD:
+            sizes = SATD_SIZES
+        elif op == SA8D:
+            sizes = SA8D_SIZES
+        elif op == SSE_PP:
+            sizes = SSE_PP_SIZES
+        else:
+            sizes = [(k, k) for k in CU_SQ]
+        for (w, h) in sizes:
+            cases.append(case_pixelcmp(op, w, h, depth, n, s("cmp", op, w, h)))
+    for nref in (3, 4):
+        for (w, h) in LUMA_PU:
+            cases.append(case_sad_multi(nref, w, h, depth, n, s("multi", nref, w, h)))
+    for op in (HPP, HPS, VPP, VPS, VSP, VSS, HVPP, P2S):
+        for (w, h) in LUMA_PU:
+            for rowext in ((0, 1) if op == HPS else (0,)):
+                cases.append(case_interp(op, 8, w, h, depth, n, s("luma", op, w, h, rowext), rowext))
+    for op in (HPP, HPS, VPP, VPS, VSP, VSS):
+        for (w, h) in INTERP_CHROMA_SIZES:
+            if quick and (w, h) not in CHROMA420_PU:
+                continue
+            for rowext in ((0, 1) if op == HPS else (0,)):
+                cases.append(case_interp(op, 4, w, h, depth, n, s("chroma", op, w, h, rowext), rowext))
+    for (w, h) in [s for s in unique(CHROMA420_PU + CHROMA422_PU) if s != (2, 2)]:
+        cases.append(case_interp(P2S, 4, w, h, depth, n, s("cp2s", w, h)))
+    for kind in (DCT, IDCT):
+        for size in TU_SQ:
+            cases.append(case_transform(kind, size, depth, n, s("tr", kind, size)))
+    for kind in (DST, IDST):
+        cases.append(case_transform(kind, 4, depth, n, s("tr", kind, 4)))
+    for nq in (False, True):
+        for size in TU_SQ:
+            cases.append(case_quant(nq, size, depth, n, s("q", nq, size)))
+    for sc in (False, True):
+        for size in TU_SQ:
+            cases.append(case_dequant(sc, size, depth, n, s("dq", sc, size)))
+    for size in TU_SQ:
+        cases.append(case_intra(0, size, depth, n, s("ifilt", size)))
+        for mode in range(35):
+            cases.append(case_intra(1, size, depth, max(2, n // 2), s("ipred", size, mode), mode))
+        cases.append(case_intra(2, size, depth, 2, s("iall", size)))
+    for op in range(14):
+        for (w, h) in blockop_sizes(op):
+            cases.append(case_blockop(op, w, h, depth, n, s("blk", op, w, h)))
+    for size in TU_SQ:
+        for cp in (False, True):
+            cases.append(case_count(size, cp, depth, n, s("cnt", size, cp)))
+    return cases
+
+
+# ---------------------------------------------------------------- executors
+def run_cpu(case: Case, orc) -> dict:
+    """Run a case through a CpuOracle (oracle/pyoracle.py); returns outputs."""
+    b = {k: (v.copy() if isinstance(v, np.ndarray) and k in case.outs else v) for k, v in case.bufs.items()}
+    p = case.params
+    f = case.family
+    if f == "pixelcmp":
+        orc.pixelcmp(p["op"], p["w"], p["h"], b["a"], b["sa"], b["aoff"], b["b"], b["sb"], b["boff"], b["out"])
+    elif f == "sad_multi":
+        orc.sad_multi(p["nref"], p["w"], p["h"], b["f"], b["fs"], b["foff"], b["r"], b["rs"], b["roff"], b["out"])
+    elif f == "interp":
+        orc.interp(p["op"], p["taps"], p["w"], p["h"], b["s"], b["ss"], b["soff"], b["d"], b["ds"], b["doff"],
+                   b["coeff"], p["rowext"])
+    elif f == "transform":
+        orc.transform(p["kind"], p["size"], b["s"], b["ss"], b["soff"], b["d"], b["ds"], b["doff"])
+    elif f == "quant":
+        orc.quant(p["size"] ** 2, b["c"], b["co"], b["q"], b["qo"], b["dl"], b["dlo"], b["o"], b["oo"], b["qb"],
+                  b["ad"], b["sig"])
+    elif f == "dequant":
+        orc.dequant(p["scaling"], p["size"] ** 2, b["q"], b["qo"], b["dq"], b["dqo"], b["o"], b["oo"], b["p0"], b["p1"])
+    elif f == "intra":
+        orc.intra(p["kind"], p["size"], b["d"], b["ds"], b["doff"], b["nb"], b["nbo"], b["f"], b["fo"], b["mode"],
+                  b["bf"])
+    elif f == "blockop":
+        orc.blockop(p["op"], p["w"], p["h"], b["d"], b["ds"], b["doff"], b["a"], b["sa"], b["aoff"], b["b"], b["sb"],
+                    b["boff"], b["param"])
+    elif f == "count":
+        orc.count_nonzero(p["size"], b["c"], b["co"], b["r"], b["rs"], b["ro"], b["cnt"])
+    else:
+        raise ValueError(f)
+    return {k: b[k] for k in case.outs}
+
+
+def run_gpu(case: Case, prims, device="cuda") -> dict:
+    """Run a case through the GPU library (src/x265_amd/native.Primitives)."""
+    import torch
+
+    def dev(v):
+        if isinstance(v, np.ndarray):
+            return torch.from_numpy(np.ascontiguousarray(v)).to(device)
+        return v
+
+    b = {k: dev(v) for k, v in case.bufs.items()}
+    p = case.params
+    f = case.family
+    d = p["depth"]
+    if f == "pixelcmp":
+        prims.pixelcmp(p["op"], d, p["w"], p["h"], b["a"], b["sa"], b["aoff"], b["b"], b["sb"], b["boff"], b["out"])
+    elif f == "sad_multi":
+        prims.sad_multi(p["nref"], d, p["w"], p["h"], b["f"], b["fs"], b["foff"], b["r"], b["rs"], b["roff"], b["out"])
+    elif f == "interp":
+        prims.interp(p["op"], p["taps"], d, p["w"], p["h"], b["s"], b["ss"], b["soff"], b["d"], b["ds"], b["doff"],
+                     b["coeff"], p["rowext"])
+    elif f == "transform":
+        prims.transform(p["kind"], d, p["size"], b["s"], b["ss"], b["soff"], b["d"], b["ds"], b["doff"])
+    elif f == "quant":
+        prims.quant(p["size"] ** 2, b["c"], b["co"], b["q"], b["qo"], b["dl"], b["dlo"], b["o"], b["oo"], b["qb"],
+                    b["ad"], b["sig"])
+    elif f == "dequant":
+        if p["scaling"]:
+            prims.dequant_scaling(p["size"] ** 2, b["q"], b["qo"], b["dq"], b["dqo"], b["o"], b["oo"], b["p0"], b["p1"])
+        else:
+            prims.dequant_normal(p["size"] ** 2, b["q"], b["qo"], b["o"], b["oo"], b["p0"], b["p1"])
+    elif f == "intra":
+        if p["kind"] == 0:
+            prims.intra_filter(d, p["size"], b["nb"], b["nbo"], b["d"], b["doff"])
+        elif p["kind"] == 1:
+            prims.intra_pred(d, p["size"], b["d"], b["ds"], b["doff"], b["nb"], b["nbo"], b["mode"], b["bf"])
+        else:
+            prims.intra_allangs(d, p["size"], b["d"], b["doff"], b["nb"], b["nbo"], b["f"], b["fo"], b["bf"])
+    elif f == "blockop":
+        prims.blockop(p["op"], d, p["w"], p["h"], b["d"], b["ds"], b["doff"], b["a"], b["sa"], b["aoff"], b["b"],
+                      b["sb"], b["boff"], b["param"])
+    elif f == "count":
+        prims.count_nonzero(p["size"], b["c"], b["co"], b["r"], b["rs"], b["ro"], b["cnt"])
+    else:
+        raise ValueError(f)
+    torch.cuda.synchronize()
+    return {k: b[k].cpu().numpy() for k in case.outs}

@@ -1,0 +1,40 @@
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (ROOT, os.path.join(ROOT, "tests"), os.path.join(ROOT, "oracle")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a gfx950 GPU (MI355X)")
+    config.addinivalue_line("markers", "slow: long-running")
+
+
+def _ensure_oracle():
+    """Build the CPU checker libraries (gcc only, seconds) when missing."""
+    import subprocess
+
+    need = [os.path.join(ROOT, "oracle", "_build", f) for f in ("liboracle8.so", "liboracle10.so", "libcpubatch.so")]
+    if not all(os.path.exists(p) for p in need):
+        subprocess.run(["make", "-C", os.path.join(ROOT, "oracle"), "oracle", "cpubatch"], check=True,
+                       capture_output=True)
+
+
+@pytest.fixture(scope="session")
+def oracle_libs():
+    _ensure_oracle()
+    return True
+
+
+@pytest.fixture(scope="session")
+def native_lib():
+    """The product library, built in-tree if missing (hipcc cross-compiles without a GPU)."""
+    from src.x265_amd import build as b
+
+    if not os.path.exists(b.LIB):
+        b.build(verbose=False)
+    return b.LIB
