@@ -177,15 +177,24 @@ static void multi_range(void* p, int64_t lo, int64_t hi)
     MultiCtx* c = (MultiCtx*)p;
     Lib* L = c->L;
     const int psz = L->depth > 8 ? 2 : 1;
+    uint16_t stage[64 * 64];
     for (int64_t i = lo; i < hi; i++)
     {
-        /* the reference reads fenc with FENC_STRIDE; callers of this checker
-         * must pass fenc_stride == 64 (checked in cb_sad_multi) */
+        /* the reference reads fenc with FENC_STRIDE (pixel.cpp:88,112): stage
+         * the block into a 64-stride buffer first, as MotionEstimate::setSourcePU
+         * does (motion.cpp:184-193) */
+        const void* fenc = PX(c->f, c->fo[i]);
+        if (c->fs != 64)
+        {
+            for (int y = 0; y < c->h; y++)
+                memcpy((uint8_t*)stage + y * 64 * psz, (const uint8_t*)fenc + y * c->fs * psz, c->w * psz);
+            fenc = stage;
+        }
         const int64_t* ro = c->ro + i * c->nref;
         if (c->nref == 3)
-            L->sad_x3(c->w, c->h, PX(c->f, c->fo[i]), PX(c->r, ro[0]), PX(c->r, ro[1]), PX(c->r, ro[2]), c->rs, c->out + 3 * i);
+            L->sad_x3(c->w, c->h, fenc, PX(c->r, ro[0]), PX(c->r, ro[1]), PX(c->r, ro[2]), c->rs, c->out + 3 * i);
         else
-            L->sad_x4(c->w, c->h, PX(c->f, c->fo[i]), PX(c->r, ro[0]), PX(c->r, ro[1]), PX(c->r, ro[2]),
+            L->sad_x4(c->w, c->h, fenc, PX(c->r, ro[0]), PX(c->r, ro[1]), PX(c->r, ro[2]),
                       PX(c->r, ro[3]), c->rs, c->out + 4 * i);
     }
 }
@@ -193,7 +202,7 @@ static void multi_range(void* p, int64_t lo, int64_t hi)
 int cb_sad_multi(void* h, int nref, int w, int hh, int64_t n, const void* f, intptr_t fs, const int64_t* fo,
                  const void* r, intptr_t rs, const int64_t* ro, int32_t* out, int nthreads)
 {
-    if (fs != 64) return -1;
+    if (w > 64 || hh > 64) return -1;
     MultiCtx c = { (Lib*)h, nref, w, hh, f, fs, fo, r, rs, ro, out };
     parallel(n, nthreads, multi_range, &c);
     return 0;

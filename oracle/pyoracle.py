@@ -66,7 +66,7 @@ class CpuOracle:
         rc = self.cb.cb_sad_multi(_vp(self.h), nref, w, h, _i64(len(foff)), _p(f), _ip(fs), _p(foff), _p(r), _ip(rs),
                                   _p(roff), _p(out), self.nthreads)
         if rc:
-            raise ValueError("sad_multi oracle requires fenc stride 64")
+            raise ValueError("sad_multi oracle: block larger than 64x64")
 
     def interp(self, op, taps, w, h, s, ss, soff, d, ds, doff, coeff, rowext):
         self.cb.cb_interp(_vp(self.h), op, taps, w, h, _i64(len(soff)), _p(s), _ip(ss), _p(soff), _p(d), _ip(ds),
@@ -95,3 +95,67 @@ class CpuOracle:
     def count_nonzero(self, size, c, co, r, rs, ro, cnt):
         self.cb.cb_count_nonzero(_vp(self.h), size, _i64(len(co)), _p(c), _p(co), _p(r), _ip(rs), _p(ro),
                                  _p(cnt), self.nthreads)
+
+
+class CpuPrims:
+    """The GPU `Primitives` call surface (src/x265_amd/native.py) executed on the
+    CPU through a CpuOracle, on torch CPU tensors.  Used for bench.py's
+    cpu_baseline leg (the same batch descriptors, timed on host cores) and for
+    CPU-only tests of the workload plumbing.  Never a fallback for the product."""
+
+    def __init__(self, kind: str, depth: int, nthreads: int = 1):
+        self.orc = CpuOracle(kind, depth)
+        self.orc.nthreads = nthreads
+
+    @staticmethod
+    def _n(t):
+        return None if t is None else t.numpy()
+
+    def pixelcmp(self, op, depth, w, h, a, sa, aoff, b, sb, boff, out, stream=None):
+        n = self._n
+        self.orc.pixelcmp(op, w, h, n(a), sa, n(aoff), n(b), sb, n(boff), n(out))
+
+    def sad_multi(self, nref, depth, w, h, f, fs, foff, r, rs, roff, out, stream=None):
+        n = self._n
+        # cpubatch stages each fenc block into a FENC_STRIDE buffer like setSourcePU
+        self.orc.sad_multi(nref, w, h, n(f), fs, n(foff), n(r), rs, n(roff), n(out))
+
+    def interp(self, op, taps, depth, w, h, s, ss, soff, d, ds, doff, coeff, rowext=0, stream=None):
+        n = self._n
+        self.orc.interp(op, taps, w, h, n(s), ss, n(soff), n(d), ds, n(doff), n(coeff), rowext)
+
+    def transform(self, kind, depth, size, s, ss, soff, d, ds, doff, stream=None):
+        n = self._n
+        self.orc.transform(kind, size, n(s), ss, n(soff), n(d), ds, n(doff))
+
+    def quant(self, num, c, co, q, qo, dl, dlo, o, oo, qb, ad, sig, stream=None):
+        n = self._n
+        self.orc.quant(num, n(c), n(co), n(q), n(qo), n(dl), n(dlo), n(o), n(oo), n(qb), n(ad), n(sig))
+
+    def dequant_normal(self, num, q, qo, o, oo, scale, shift, stream=None):
+        n = self._n
+        self.orc.dequant(0, num, n(q), n(qo), None, None, n(o), n(oo), n(scale), n(shift))
+
+    def dequant_scaling(self, num, q, qo, dq, dqo, o, oo, per, shift, stream=None):
+        n = self._n
+        self.orc.dequant(1, num, n(q), n(qo), n(dq), n(dqo), n(o), n(oo), n(per), n(shift))
+
+    def intra_filter(self, depth, size, s, soff, d, doff, stream=None):
+        n = self._n
+        self.orc.intra(0, size, n(d), 0, n(doff), n(s), n(soff), None, None, None, None)
+
+    def intra_pred(self, depth, size, d, ds, doff, nb, nboff, mode, bfilter, stream=None):
+        n = self._n
+        self.orc.intra(1, size, n(d), ds, n(doff), n(nb), n(nboff), None, None, n(mode), n(bfilter))
+
+    def intra_allangs(self, depth, size, d, doff, ref, roff, filt, foff, bluma, stream=None):
+        n = self._n
+        self.orc.intra(2, size, n(d), 0, n(doff), n(ref), n(roff), n(filt), n(foff), None, n(bluma))
+
+    def blockop(self, op, depth, w, h, d, ds, doff, a, sa, aoff, b, sb, boff, param=0, stream=None):
+        n = self._n
+        self.orc.blockop(op, w, h, n(d), ds, n(doff), n(a), sa, n(aoff), n(b), sb, n(boff), param)
+
+    def count_nonzero(self, size, c, co, r, rs, ro, cnt, stream=None):
+        n = self._n
+        self.orc.count_nonzero(size, n(c), n(co), n(r), rs, n(ro), n(cnt))
