@@ -41,7 +41,7 @@ __device__ __forceinline__ void ld(const T* p, int (&o)[UW])
     else load_row<T, UW>(p, o);
 }
 
-template <typename P, int OP, int UW>
+template <typename P, int OP, int UW, int UH>
 __global__ __launch_bounds__(X265AMD_BLOCK) void k_blockop(int w, int h, int n, int lg, int depth,
     typename OpTypes<P, OP>::d* __restrict__ dst, intptr_t ds, const int64_t* __restrict__ doff,
     const typename OpTypes<P, OP>::a* __restrict__ a, intptr_t sa, const int64_t* __restrict__ aoff,
@@ -61,11 +61,13 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_blockop(int w, int h, int n, 
                   ? b + boff[job] : nullptr;
     const int maxv = (1 << depth) - 1;
     const int avg_shift = 15 - depth, avg_off = (1 << (avg_shift - 1)) + 2 * 8192;
-    const int ux = w / UW, units = ux * h;
+    const int ux = w / UW, units = ux * (h / UH);
 
     for (int u = lane; u < units; u += G)
+#pragma unroll
+    for (int r = 0; r < UH; r++)
     {
-        const int x = (u % ux) * UW, y = u / ux;
+        const int x = (u % ux) * UW, y = (u / ux) * UH + r;
         int o[UW];
         if constexpr (OP == X265AMD_BLOCKFILL)
         {
@@ -121,17 +123,27 @@ static int launch_blockop(int w, int h, int n, int depth, void* dst, intptr_t ds
     typedef typename OpTypes<P, OP>::b B;
     const int uw = (w % 8 == 0) ? 8 : (w % 4 == 0) ? 4 : 2;
     if (w % 2) return X265AMD_EINVAL;
-    const int units = (w / uw) * h;
-    int g = pow2ceil(units);
+    const int uh = (h % 4 == 0) ? 4 : 1;       // 4-row units keep several row loads in flight per lane
+    const int units = (w / uw) * (h / uh);
+    int g = pow2ceil((units + 1) / 2);
     if (g > 64) g = 64;
     int lg = 0;
     while ((1 << lg) < g) lg++;
     const dim3 grid((n + (X265AMD_BLOCK >> lg) - 1) / (X265AMD_BLOCK >> lg));
-#define L(UW) hipLaunchKernelGGL((k_blockop<P, OP, UW>), grid, dim3(X265AMD_BLOCK), 0, st, w, h, n, lg, depth, \
-                                 (D*)dst, ds, doff, (const A*)a, sa, aoff, (const B*)b, sb, boff, param)
-    if (uw == 8) L(8);
-    else if (uw == 4) L(4);
-    else L(2);
+#define L(UW, UH) hipLaunchKernelGGL((k_blockop<P, OP, UW, UH>), grid, dim3(X265AMD_BLOCK), 0, st, w, h, n, lg, depth, \
+                                     (D*)dst, ds, doff, (const A*)a, sa, aoff, (const B*)b, sb, boff, param)
+    if (uh == 4)
+    {
+        if (uw == 8) L(8, 4);
+        else if (uw == 4) L(4, 4);
+        else L(2, 4);
+    }
+    else
+    {
+        if (uw == 8) L(8, 1);
+        else if (uw == 4) L(4, 1);
+        else L(2, 1);
+    }
 #undef L
     return (int)hipGetLastError();
 }

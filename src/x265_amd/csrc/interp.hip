@@ -250,6 +250,106 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_interp(int w, int h, int n, i
     }
 }
 
+// hv_pp in two on-chip passes: the horizontal int16 intermediate of the
+// (h+7) x w block (interp_horiz_ps_c with row extension) goes to LDS once,
+// then the vertical sp filter reads it back (filterVertical_sp_c).  Jobs per
+// block = 256 / G, LDS = jobs * (h+7) * w int16.
+template <typename P, int UW, int UH>
+__global__ __launch_bounds__(X265AMD_BLOCK) void k_hvpp(int w, int h, int n, int lg, int depth,
+    const P* __restrict__ src, intptr_t ss, const int64_t* __restrict__ soff,
+    P* __restrict__ dst, intptr_t ds, const int64_t* __restrict__ doff, const uint8_t* __restrict__ coeff)
+{
+    extern __shared__ int16_t hv_lds[];
+    const int G = 1 << lg;
+    const int slot = threadIdx.x >> lg, lane = threadIdx.x & (G - 1);
+    const int64_t job0 = (int64_t)xcd_block() * (X265AMD_BLOCK >> lg) + slot;
+    const bool live = job0 < n;
+    const int64_t job = live ? job0 : 0;
+    const IfConst K(depth);
+    int16_t* L = hv_lds + (size_t)slot * (h + 7) * w;
+    const int cidx = coeff[job];
+    int cx[8], cy[8];
+    get_taps<8>(cidx & 15, cx);
+    get_taps<8>(cidx >> 4, cy);
+    const int ux = w / UW;
+
+    if (live)
+    {
+        const P* ps = src + soff[job] - 3 * ss;
+        const int hunits = ux * (h + 7);
+        for (int u = lane; u < hunits; u += G)
+        {
+            const int x = (u % ux) * UW, t = u / ux;
+            int sum[UW], o[UW];
+            hfilter<P, 8, UW>(ps + t * ss + x, cx, sum);
+#pragma unroll
+            for (int i = 0; i < UW; i++) o[i] = (int)(int16_t)((sum[i] + K.ps_off) >> K.ps_shift);
+            store_row<int16_t, UW>(L + t * w + x, o);
+        }
+    }
+    __syncthreads();
+    if (!live) return;
+    P* pd = dst + doff[job];
+    const int vunits = ux * (h / UH);
+    for (int u = lane; u < vunits; u += G)
+    {
+        const int x = (u % ux) * UW, y0 = (u / ux) * UH;
+        int acc[UH][UW];
+#pragma unroll
+        for (int r = 0; r < UH; r++)
+#pragma unroll
+            for (int i = 0; i < UW; i++) acc[r][i] = 0;
+#pragma unroll
+        for (int t = 0; t < UH + 7; t++)
+        {
+            int v[UW];
+            load_row16<UW>(L + (y0 + t) * w + x, v);
+#pragma unroll
+            for (int r = 0; r < UH; r++)
+            {
+                const int k = t - r;
+                if (k >= 0 && k < 8)
+                {
+#pragma unroll
+                    for (int i = 0; i < UW; i++) acc[r][i] += v[i] * cy[k];
+                }
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < UH; r++)
+        {
+            int o[UW];
+#pragma unroll
+            for (int i = 0; i < UW; i++) o[i] = clampp((acc[r][i] + K.sp_off) >> K.sp_shift, K.maxv);
+            store_row<P, UW>(pd + (y0 + r) * ds + x, o);
+        }
+    }
+}
+
+template <typename P>
+static int launch_hvpp(int w, int h, int n, int depth, const void* src, intptr_t ss, const int64_t* soff,
+                       void* dst, intptr_t ds, const int64_t* doff, const uint8_t* coeff, hipStream_t st)
+{
+    const int uw = w % 8 == 0 ? 8 : 4, uh = h % 4 == 0 ? 4 : 1;
+    if (w % 4) return X265AMD_EINVAL;
+    const int units = (w / uw) * (h / uh);
+    int g = pow2ceil((units + 1) / 2);
+    if (g > 64) g = 64;
+    int lg = 0;
+    while ((1 << lg) < g) lg++;
+    // keep the workgroup's intermediate within 64 KiB of LDS
+    while (lg < 6 && (size_t)(X265AMD_BLOCK >> lg) * (h + 7) * w * sizeof(int16_t) > 65536) lg++;
+    const int per = X265AMD_BLOCK >> lg;
+    const size_t lds = (size_t)per * (h + 7) * w * sizeof(int16_t);
+    const dim3 grid((n + per - 1) / per);
+#define L(UW, UH) hipLaunchKernelGGL((k_hvpp<P, UW, UH>), grid, dim3(X265AMD_BLOCK), lds, st, w, h, n, lg, depth, \
+                                     (const P*)src, ss, soff, (P*)dst, ds, doff, coeff)
+    if (uw == 8) { if (uh == 4) L(8, 4); else L(8, 1); }
+    else { if (uh == 4) L(4, 4); else L(4, 1); }
+#undef L
+    return (int)hipGetLastError();
+}
+
 // -------------------------------------------------------------- dispatch
 
 template <typename P, typename S, typename D, int OP, int TAPS, int UW, int UH>
@@ -259,7 +359,7 @@ static int launch_interp(int w, int h, int n, int depth, const void* src, intptr
 {
     const int rows = (OP == X265AMD_HPS && rowext) ? h + TAPS - 1 : h;
     const int units = (w / UW) * (rows / UH);
-    int g = pow2ceil(units);
+    int g = pow2ceil((units + 1) / 2);    // two units per lane
     if (g > 64) g = 64;
     int lg = 0;
     while ((1 << lg) < g) lg++;
@@ -273,24 +373,23 @@ template <typename P, typename S, typename D, int OP, int TAPS>
 static int pick_unit(int w, int h, int n, int depth, const void* src, intptr_t ss, const int64_t* soff,
                      void* dst, intptr_t ds, const int64_t* doff, const uint8_t* coeff, int rowext, hipStream_t st)
 {
-    constexpr bool horiz = OP == X265AMD_HPP || OP == X265AMD_HPS || OP == X265AMD_P2S;
     const int rows = (OP == X265AMD_HPS && rowext) ? h + TAPS - 1 : h;
 #define L(UW, UH) return launch_interp<P, S, D, OP, TAPS, UW, UH>(w, h, n, depth, src, ss, soff, dst, ds, doff, coeff, rowext, st)
     if (w % 8 == 0)
     {
-        if (horiz || rows % 4) L(8, 1);
+        if (rows % 4) L(8, 1);
         L(8, 4);
     }
     if (w % 4 == 0)
     {
-        if (horiz || rows % 4) L(4, 1);
+        if (rows % 4) L(4, 1);
         L(4, 4);
     }
     if (w % 2 == 0)
     {
         if constexpr (TAPS == 4 || OP == X265AMD_P2S || OP == X265AMD_VPP || OP == X265AMD_VPS || OP == X265AMD_VSP || OP == X265AMD_VSS)
         {
-            if (horiz || rows % 4) L(2, 1);
+            if (rows % 4) L(2, 1);
             L(2, 4);
         }
     }
@@ -312,7 +411,7 @@ static int dispatch_interp(int op, int w, int h, int n, int depth, const void* s
     case X265AMD_VSP: return pick_unit<P, int16_t, P, X265AMD_VSP, TAPS>(A);
     case X265AMD_VSS: return pick_unit<P, int16_t, int16_t, X265AMD_VSS, TAPS>(A);
     case X265AMD_HVPP:
-        if constexpr (TAPS == 8) return pick_unit<P, P, P, X265AMD_HVPP, 8>(A);
+        if constexpr (TAPS == 8) return launch_hvpp<P>(w, h, n, depth, src, ss, soff, dst, ds, doff, coeff, st);
         return X265AMD_EINVAL;
     }
 #undef A

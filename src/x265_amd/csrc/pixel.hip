@@ -395,8 +395,10 @@ static int launch_cmp(int w, int h, int n, const void* a, intptr_t sa, const int
                       const void* b, intptr_t sb, const int64_t* boff, void* out, hipStream_t st,
                       int wrap32)
 {
+    // two units per lane: small blocks get one lane per job (all row loads of
+    // the job in flight from one lane), large blocks up to a full wavefront
     const int units = (w / UW) * (h / UH);
-    int g = pow2ceil(units);
+    int g = pow2ceil((units + 1) / 2);
     if (g > 64) g = 64;
     int lg = 0;
     while ((1 << lg) < g) lg++;
@@ -455,7 +457,7 @@ static int dispatch_multi(int w, int h, int n, const void* f, intptr_t fs, const
     if ((w % 4) || (h % 4) || w > 64 || h > 64) return X265AMD_EINVAL;
     const bool w8 = (w % 8) == 0;
     const int units = (w / (w8 ? 8 : 4)) * (h / 4);
-    int g = pow2ceil(units);
+    int g = pow2ceil((units + 1) / 2);
     if (g > 64) g = 64;
     int lg = 0;
     while ((1 << lg) < g) lg++;

@@ -255,25 +255,28 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_trN(int n, int depth,
 }
 
 // --------------------------------------------------------------- quant family
-// one job per 64-lane wave; lane handles 8 coefficients per iteration
+// one job per G-lane group (G = num/8, at most 64); a lane handles 8
+// coefficients per iteration
 template <bool NQUANT>
-__global__ __launch_bounds__(X265AMD_BLOCK) void k_quant(int n, int num,
+__global__ __launch_bounds__(X265AMD_BLOCK) void k_quant(int n, int num, int lg,
     const int16_t* __restrict__ coef, const int64_t* __restrict__ coff,
     const int32_t* __restrict__ qtab, const int64_t* __restrict__ qoff,
     int32_t* __restrict__ delta, const int64_t* __restrict__ doff,
     int16_t* __restrict__ qout, const int64_t* __restrict__ ooff,
     const int32_t* __restrict__ qbits, const int32_t* __restrict__ add, uint32_t* __restrict__ numsig)
 {
-    const int64_t job = (int64_t)xcd_block() * (X265AMD_BLOCK / 64) + threadIdx.x / 64;
-    const int lane = threadIdx.x & 63;
-    if (job >= n) return;   // wave-uniform
+    const int G = 1 << lg;
+    const int64_t job0 = (int64_t)xcd_block() * (X265AMD_BLOCK >> lg) + (threadIdx.x >> lg);
+    const int lane = threadIdx.x & (G - 1);
+    const bool live = job0 < n;
+    const int64_t job = live ? job0 : 0;
     const int16_t* pc = coef + coff[job];
     const int32_t* pq = qtab + qoff[job];
     int16_t* po = qout + ooff[job];
     int32_t* pdl = NQUANT ? nullptr : delta + doff[job];
     const int qb = qbits[job], ad = add[job], qb8 = qb - 8;
     uint32_t sig = 0;
-    for (int i = lane * 8; i < num; i += 64 * 8)
+    for (int i = lane * 8; live && i < num; i += G * 8)
     {
         int c[8], o[8];
         load_row16<8>(pc + i, c);
@@ -300,23 +303,24 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_quant(int n, int num,
             stu<int4>(pdl + i + 4, make_int4(dl[4], dl[5], dl[6], dl[7]));
         }
     }
-    for (int m = 32; m > 0; m >>= 1) sig += __shfl_xor(sig, m, 64);
-    if (lane == 0) numsig[job] = sig;
+    for (int m = G >> 1; m > 0; m >>= 1) sig += __shfl_xor(sig, m, 64);
+    if (live && lane == 0) numsig[job] = sig;
 }
 
 template <bool SCALING>
-__global__ __launch_bounds__(X265AMD_BLOCK) void k_dequant(int n, int num,
+__global__ __launch_bounds__(X265AMD_BLOCK) void k_dequant(int n, int num, int lg,
     const int16_t* __restrict__ q, const int64_t* __restrict__ qoff,
     const int32_t* __restrict__ dq, const int64_t* __restrict__ dqoff,
     int16_t* __restrict__ out, const int64_t* __restrict__ ooff,
     const int32_t* __restrict__ p0, const int32_t* __restrict__ p1)
 {
-    const int64_t job = (int64_t)xcd_block() * (X265AMD_BLOCK / 64) + threadIdx.x / 64;
-    const int lane = threadIdx.x & 63;
+    const int G = 1 << lg;
+    const int64_t job = (int64_t)xcd_block() * (X265AMD_BLOCK >> lg) + (threadIdx.x >> lg);
+    const int lane = threadIdx.x & (G - 1);
     if (job >= n) return;
     const int16_t* pq = q + qoff[job];
     int16_t* po = out + ooff[job];
-    for (int i = lane * 8; i < num; i += 64 * 8)
+    for (int i = lane * 8; i < num; i += G * 8)
     {
         int v[8], o[8];
         load_row16<8>(pq + i, v);
@@ -379,6 +383,15 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_count(int n, int16_t* __restr
     if (live && lane == 0) cnt[job] = c;
 }
 
+// lanes per coefficient job: 8 coefficients per lane, at most one wavefront
+static inline int coef_lanes_log2(int num)
+{
+    int g = num / 8, lg = 0;
+    if (g > 64) g = 64;
+    while ((1 << lg) < g) lg++;
+    return lg;
+}
+
 } // namespace x265amd
 
 using namespace x265amd;
@@ -432,13 +445,14 @@ extern "C" int x265amd_quant(int n, int num, const int16_t* coef, const int64_t*
 {
     if (n <= 0) return 0;
     if (num <= 0 || num % 16 || num > 1024) return X265AMD_EINVAL;
-    const dim3 grid((n + 3) / 4);
+    const int lg = coef_lanes_log2(num);
+    const dim3 grid((n + (X265AMD_BLOCK >> lg) - 1) / (X265AMD_BLOCK >> lg));
     hipStream_t st = (hipStream_t)stream;
     if (delta_u)
-        hipLaunchKernelGGL(k_quant<false>, grid, dim3(X265AMD_BLOCK), 0, st, n, num, coef, coef_off, qtab, qtab_off,
+        hipLaunchKernelGGL(k_quant<false>, grid, dim3(X265AMD_BLOCK), 0, st, n, num, lg, coef, coef_off, qtab, qtab_off,
                            delta_u, delta_off, qcoef, qcoef_off, qbits, add, num_sig);
     else
-        hipLaunchKernelGGL(k_quant<true>, grid, dim3(X265AMD_BLOCK), 0, st, n, num, coef, coef_off, qtab, qtab_off,
+        hipLaunchKernelGGL(k_quant<true>, grid, dim3(X265AMD_BLOCK), 0, st, n, num, lg, coef, coef_off, qtab, qtab_off,
                            delta_u, delta_off, qcoef, qcoef_off, qbits, add, num_sig);
     return (int)hipGetLastError();
 }
@@ -449,7 +463,9 @@ extern "C" int x265amd_dequant_normal(int n, int num, const int16_t* q, const in
 {
     if (n <= 0) return 0;
     if (num <= 0 || num % 8 || num > 1024) return X265AMD_EINVAL;
-    hipLaunchKernelGGL(k_dequant<false>, dim3((n + 3) / 4), dim3(X265AMD_BLOCK), 0, (hipStream_t)stream, n, num, q, q_off,
+    const int lg = coef_lanes_log2(num);
+    hipLaunchKernelGGL(k_dequant<false>, dim3((n + (X265AMD_BLOCK >> lg) - 1) / (X265AMD_BLOCK >> lg)),
+                       dim3(X265AMD_BLOCK), 0, (hipStream_t)stream, n, num, lg, q, q_off,
                        (const int32_t*)nullptr, (const int64_t*)nullptr, coef, coef_off, scale, shift);
     return (int)hipGetLastError();
 }
@@ -461,7 +477,9 @@ extern "C" int x265amd_dequant_scaling(int n, int num, const int16_t* q, const i
 {
     if (n <= 0) return 0;
     if (num <= 0 || num % 8 || num > 1024) return X265AMD_EINVAL;
-    hipLaunchKernelGGL(k_dequant<true>, dim3((n + 3) / 4), dim3(X265AMD_BLOCK), 0, (hipStream_t)stream, n, num, q, q_off,
+    const int lg = coef_lanes_log2(num);
+    hipLaunchKernelGGL(k_dequant<true>, dim3((n + (X265AMD_BLOCK >> lg) - 1) / (X265AMD_BLOCK >> lg)),
+                       dim3(X265AMD_BLOCK), 0, (hipStream_t)stream, n, num, lg, q, q_off,
                        dq, dq_off, coef, coef_off, per, shift);
     return (int)hipGetLastError();
 }

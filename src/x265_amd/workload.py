@@ -235,35 +235,63 @@ class WorkloadBuilder:
         return torch.from_numpy(np.ascontiguousarray(a)).to(self.fs.device)
 
     def _positions(self, n, w, h, chroma=False):
+        """Job block positions the way an encoder visits them: frame by frame,
+        blocks in raster (CTU-row) order; when a frame needs more calls than it
+        has blocks of this shape, each block is evaluated several times in a
+        row (motion-search candidates).  Returns frame, x, y, candidate index."""
         fs, rng = self.fs, self.rng
         pw, ph = (fs.pw // 2, fs.ph // 2) if chroma else (fs.pw, fs.ph)
-        ax, ay = min(w, 8), min(h, 8)
-        x = _aligned(rng, 0, pw - w, ax, n)
-        y = _aligned(rng, 0, ph - h, ay, n)
-        f = (np.arange(n) % fs.F).astype(np.int64)
-        return f, x, y
+        bx, by = max(1, pw // w), max(1, ph // h)
+        nblk = bx * by
+        per = -(-n // fs.F)
+        if per <= nblk:
+            blk = np.sort(rng.choice(nblk, size=per, replace=False))
+            cand = np.zeros(per, np.int64)
+        else:
+            reps = -(-per // nblk)
+            blk = np.repeat(np.arange(nblk), reps)[:per]
+            cand = np.tile(np.arange(reps), nblk)[:per]
+        f = np.repeat(np.arange(fs.F, dtype=np.int64), per)[:n]
+        blk = np.tile(blk, fs.F)[:n]
+        cand = np.tile(cand, fs.F)[:n]
+        x = (blk % bx) * w
+        y = (blk // bx) * h
+        return f, x.astype(np.int64), y.astype(np.int64), cand.astype(np.int64)
 
-    def _mv(self, n, chroma=False):
-        r = MV_RANGE // (2 if chroma else 1)
-        return self.rng.integers(-r, r + 1, n), self.rng.integers(-r // (2 if chroma else 1), r // (2 if chroma else 1) + 1, n)
+    def _mv(self, f, x, y, cand, chroma=False):
+        """Smooth motion field: the source pans (+2,+1)/frame, so the match in
+        frame f-1 sits near (-2,-1); each 64x64 CTU adds a stable +-6 px local
+        motion and each search candidate a +-2 px step around it (clamped to
+        the +-MV_RANGE search window)."""
+        cx, cy = x // (32 if chroma else 64), y // (32 if chroma else 64)
+        lx = ((cx * 7 + cy * 13 + f * 3) % 13) - 6
+        ly = ((cx * 11 + cy * 5 + f * 7) % 13) - 6
+        jx, jy = (cand % 5) - 2, ((cand // 5) % 5) - 2
+        mx = np.clip(-2 + lx + jx, -MV_RANGE, MV_RANGE)
+        my = np.clip(-1 + ly + jy, -MV_RANGE, MV_RANGE)
+        if chroma:
+            mx, my = mx // 2, my // 2
+        return mx.astype(np.int64), my.astype(np.int64)
 
     def _fenc_ref_offsets(self, n, w, h, chroma=False, nref=1):
         fs = self.fs
-        f, x, y = self._positions(n, w, h, chroma)
+        f, x, y, cand = self._positions(n, w, h, chroma)
         r = (f + fs.F - 1) % fs.F
         off = fs.chroma_off if chroma else fs.luma_off
         a = off(f, x, y)
         refs = []
         for k in range(nref):
-            mx, my = self._mv(n, chroma)
+            mx, my = self._mv(f, x, y, cand + 7 * k, chroma)
             refs.append(off(r, x + mx, y + my))
         return a, refs
 
-    def _slots(self, n, w, h, dtype, stride=64):
-        """disjoint per-job output slots of `h` rows x `stride` elements"""
+    def _slots(self, n, w, h, dtype, stride=None):
+        """disjoint per-job output slots of `h` rows x `stride` elements; by
+        default compact (stride = w), the layout a batched caller collects
+        predictions / residuals / coefficients in"""
         import torch
 
-        stride = max(stride, w)
+        stride = max(stride or w, w)
         slot = stride * h
         buf = torch.zeros(n * slot, dtype=dtype, device=self.fs.device)
         offs = self._t(np.arange(n, dtype=np.int64) * slot)
@@ -399,7 +427,7 @@ class WorkloadBuilder:
         host = fs.host["Y"]
 
         def make():
-            f, x, y = self._positions(8192, 2 * size, 1)
+            f, x, y, _ = self._positions(8192, 2 * size, 1)
             offs = fs.luma_off(f, x, y)
             return self._t(np.stack([host[o:o + m] for o in offs]).reshape(-1))
 
@@ -426,15 +454,25 @@ class WorkloadBuilder:
         return bt
 
     def _intra(self, key, n, size, mode):
+        return self.intra_merged(key, size, {mode: n})
+
+    def intra_merged(self, key, size, mode_counts: dict):
+        """One launch for every (TU, mode) evaluation of one TU size; jobs are
+        grouped by mode (wave-uniform prediction direction), as a batched
+        mode search would issue them."""
         import torch
 
         fs = self.fs
         pdt = torch.uint8 if fs.depth == 8 else torch.uint16
+        modes = np.concatenate([np.full(int(round(c)), m, np.uint8) for m, c in sorted(mode_counts.items())])
+        n = len(modes)
+        if n == 0:
+            return None
         nb, nbo = self._nb_pool(size, n)
-        d, ds, doff, slot = self._slots(n, size, size, pdt, stride=64)
+        d, ds, doff, slot = self._slots(n, size, size, pdt)
         bf = np.full(n, 1 if size <= 16 else 0, np.uint8)
         bt = Batch(key, "intra", 0, size, size, n, fs.depth, params=dict(ds=ds),
-                   dev=dict(d=d, doff=doff, nb=nb, nbo=nbo, mode=self._t(np.full(n, mode, np.uint8)),
+                   dev=dict(d=d, doff=doff, nb=nb, nbo=nbo, mode=self._t(modes),
                             bf=self._t(bf)), outs=dict(d=("slot", slot)))
         bt.bytes = n * ((4 * size + 1) + size * size) * (2 if fs.depth > 8 else 1)
         return bt
@@ -467,8 +505,7 @@ class WorkloadBuilder:
             p["param"] = 2 if op in (CPY2D1D_SHL, CPY1D2D_SHL) else 1
         if op == BLOCKFILL:
             p["param"] = 5
-        stride = w if op in (CPY2D1D_SHL, CPY2D1D_SHR, TRANSPOSE) else 64
-        d, ds, doff, slot = self._slots(n, w, h, torch.int16 if d16 else pdt, stride=stride)
+        d, ds, doff, slot = self._slots(n, w, h, torch.int16 if d16 else pdt)
         p["ds"] = ds
         dev.update(d=d, doff=doff)
         bt = Batch(key, "blockop", op, w, h, n, fs.depth, params=p, dev=dev, host_src=hs, outs=dict(d=("slot", slot)))
@@ -543,12 +580,21 @@ def census_batches(fs: FrameSet, frames: int, scale: float = 1.0, families=None,
     census = census or load_census()
     wb = builder or WorkloadBuilder(fs)
     out = []
+    intra = {}
     for key, per_frame in census.items():
         if families is not None and not any(("." + f + ".") in ("." + key + ".") for f in families):
             continue
         if key.startswith("scalar."):
             continue
+        if key.startswith("cu.intra_pred."):
+            p = key.split(".")
+            intra.setdefault(int(p[2].split("x")[0]), {})[int(p[3][4:])] = per_frame * frames * scale
+            continue
         b = wb.batch(key, per_frame * frames * scale)
+        if b is not None:
+            out.append(b)
+    for size, mc in sorted(intra.items()):
+        b = wb.intra_merged(f"cu.intra_pred.{size}x{size}.all_modes", size, mc)
         if b is not None:
             out.append(b)
     if families is None or any(f in ("quant", "dequant_normal", "dst4x4", "nquant") for f in families):

@@ -1,0 +1,193 @@
+#!/usr/bin/env python3
+"""Kernel-level roofline of the gfx950 primitive kernels.
+
+Each kernel runs on a batch of independent calls with DISJOINT operand
+blocks tiled in raster order through buffers of >= --gb GB (default 1.5 GB,
+about 4x the 32 MiB of L2 plus the 256 MiB Infinity Cache), so caches cannot
+inflate bandwidth.  achieved = algorithmic bytes per launch (§8(d) formulas)
+/ mean launch time (HIP events on the launch stream), against the 8 TB/s HBM
+peak of MI355X_MICROARCH.md.  Writes one JSON object per kernel to stdout and
+the table to --out.
+
+    python tools/kernel_roofline.py --out profiles/kernel_roofline_r01.json
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+HBM = 8000.0
+SAD, SATD, SA8D, SSE_PP = 0, 1, 2, 3
+HPP, HPS, VPP, VPS, VSP, VSS, HVPP = range(7)
+DCT, IDCT = 0, 1
+
+
+def tiled_offsets(n, bw, bh, pitch_w, pitch_h, width_px, margin=0):
+    """raster tiling of n blocks with pitch (pitch_w x pitch_h) in a plane of width_px"""
+    per_row = max(1, (width_px - 2 * margin) // pitch_w)
+    j = np.arange(n, dtype=np.int64)
+    x = margin + (j % per_row) * pitch_w
+    y = margin + (j // per_row) * pitch_h
+    rows = int(y.max()) + pitch_h + margin
+    return x, y, rows
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gb", type=float, default=1.5)
+    ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--out", default="")
+    ap.add_argument("--only", default="")
+    a = ap.parse_args()
+
+    import torch
+
+    from src.x265_amd import Primitives
+
+    prims = Primitives(device=0)
+    dev = "cuda"
+    W = 8192  # plane width in pixels
+    results = []
+
+    def timeit(fn):
+        for _ in range(2):
+            fn()
+        torch.cuda.synchronize()
+        st = torch.cuda.current_stream()
+        evs = []
+        for _ in range(a.reps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(st)
+            fn()
+            e1.record(st)
+            evs.append((e0, e1))
+        torch.cuda.synchronize()
+        return sum(x.elapsed_time(y) for x, y in evs) / len(evs)
+
+    def record(name, nbytes, ms, n):
+        gbs = nbytes / (ms * 1e-3) / 1e9
+        r = {"kernel": name, "jobs": n, "bytes_per_launch": int(nbytes), "ms": round(ms, 4),
+             "achieved_GBps": round(gbs, 1), "frac_of_8TBps": round(gbs / HBM, 3)}
+        results.append(r)
+        print(json.dumps(r), flush=True)
+
+    def want(name):
+        return not a.only or any(s in name for s in a.only.split(","))
+
+    def rand_u8(numel):
+        return torch.randint(0, 256, (numel,), dtype=torch.uint8, device=dev)
+
+    # ---------------------------------------------------------------- pixel compare
+    for op, opname, sizes in ((SAD, "sad", [8, 16, 32, 64]), (SATD, "satd", [8, 16, 64]),
+                              (SA8D, "sa8d", [8, 16, 32]), (SSE_PP, "sse_pp", [8, 32])):
+        for s in sizes:
+            name = f"{opname}_{s}x{s}"
+            if not want(name):
+                continue
+            n = int(a.gb * 1e9 / 2 / (s * s))
+            x, y, rows = tiled_offsets(n, s, s, s, s, W)
+            A, B = rand_u8(rows * W), rand_u8(rows * W)
+            off = torch.from_numpy(y * W + x).to(dev)
+            wide = op == SSE_PP
+            out = torch.empty(n, dtype=torch.int64 if wide else torch.int32, device=dev)
+            ms = timeit(lambda: prims.pixelcmp(op, 8, s, s, A, W, off, B, W, off, out))
+            record(name, n * (2 * s * s + (8 if wide else 4)), ms, n)
+            del A, B, off, out
+    # ---------------------------------------------------------------- sad_x4
+    for s in (8, 16, 64):
+        name = f"sad_x4_{s}x{s}"
+        if not want(name):
+            continue
+        n = int(a.gb * 1e9 / 5 / (s * s))
+        x, y, rows = tiled_offsets(n, s, s, s, s, W)
+        F = rand_u8(rows * W)
+        x4, y4, rows4 = tiled_offsets(4 * n, s, s, s, s, W)
+        R = rand_u8(rows4 * W)
+        foff = torch.from_numpy(y * W + x).to(dev)
+        roff = torch.from_numpy(y4 * W + x4).to(dev)
+        out = torch.empty(4 * n, dtype=torch.int32, device=dev)
+        ms = timeit(lambda: prims.sad_multi(4, 8, s, s, F, W, foff, R, W, roff, out))
+        record(name, n * (5 * s * s + 16), ms, n)
+        del F, R, foff, roff, out
+    # ---------------------------------------------------------------- luma interp
+    for op, opname in ((HPP, "luma_hpp"), (VPP, "luma_vpp"), (HVPP, "luma_hvpp")):
+        for s in (8, 16, 64):
+            name = f"{opname}_{s}x{s}"
+            if not want(name):
+                continue
+            ext_w = 7 if op in (HPP, HVPP) else 0
+            ext_h = 7 if op in (VPP, HVPP) else 0
+            n = int(a.gb * 1e9 / ((s + ext_w) * (s + ext_h) + s * s))
+            x, y, rows = tiled_offsets(n, s, s, s + 8, s + 8, W, margin=8)
+            S = rand_u8(rows * W)
+            soff = torch.from_numpy(y * W + x).to(dev)
+            D = torch.empty(n * s * s, dtype=torch.uint8, device=dev)
+            doff = torch.arange(n, dtype=torch.int64, device=dev) * (s * s)
+            coeff = torch.randint(1, 4, (n,), dtype=torch.uint8, device=dev)
+            if op == HVPP:
+                coeff = coeff | (torch.randint(1, 4, (n,), dtype=torch.uint8, device=dev) << 4)
+            ms = timeit(lambda: prims.interp(op, 8, 8, s, s, S, W, soff, D, s, doff, coeff))
+            record(name, n * ((s + ext_w) * (s + ext_h) + s * s), ms, n)
+            del S, soff, D, doff, coeff
+    # ---------------------------------------------------------------- transforms
+    for kind, kname in ((DCT, "dct"), (IDCT, "idct")):
+        for s in (4, 8, 16, 32):
+            name = f"{kname}_{s}x{s}"
+            if not want(name):
+                continue
+            n = int(a.gb * 1e9 / (4 * s * s))
+            Sr = torch.randint(-255, 256, (n * s * s,), dtype=torch.int16, device=dev)
+            Dr = torch.empty(n * s * s, dtype=torch.int16, device=dev)
+            offs = torch.arange(n, dtype=torch.int64, device=dev) * (s * s)
+            ms = timeit(lambda: prims.transform(kind, 8, s, Sr, s, offs, Dr, s, offs))
+            record(name, n * 4 * s * s, ms, n)
+            del Sr, Dr, offs
+    # ---------------------------------------------------------------- quant
+    for s in (4, 8, 16, 32):
+        name = f"quant_{s}x{s}"
+        if not want(name):
+            continue
+        num = s * s
+        n = int(a.gb * 1e9 / (8 * num))
+        C = torch.randint(-255, 256, (n * num,), dtype=torch.int16, device=dev)
+        Q = torch.full((num,), 16384 * 16, dtype=torch.int32, device=dev)
+        offs = torch.arange(n, dtype=torch.int64, device=dev) * num
+        qo = torch.zeros(n, dtype=torch.int64, device=dev)
+        DL = torch.empty(n * num, dtype=torch.int32, device=dev)
+        O = torch.empty(n * num, dtype=torch.int16, device=dev)
+        qb = torch.full((n,), 20, dtype=torch.int32, device=dev)
+        ad = torch.full((n,), 85 << 11, dtype=torch.int32, device=dev)
+        sig = torch.empty(n, dtype=torch.int32, device=dev)
+        ms = timeit(lambda: prims.quant(num, C, offs, Q, qo, DL, offs, O, offs, qb, ad, sig))
+        record(name, n * (8 * num + 4), ms, n)
+        del C, offs, qo, DL, O, qb, ad, sig
+    # ---------------------------------------------------------------- intra
+    for s in (4, 8, 16, 32):
+        name = f"intra_ang_{s}x{s}"
+        if not want(name):
+            continue
+        m = 4 * s + 1
+        n = int(a.gb * 1e9 / (m + s * s))
+        NB = rand_u8(n * m)
+        nbo = torch.arange(n, dtype=torch.int64, device=dev) * m
+        D = torch.empty(n * s * s, dtype=torch.uint8, device=dev)
+        doff = torch.arange(n, dtype=torch.int64, device=dev) * (s * s)
+        mode = torch.from_numpy(np.sort(np.random.default_rng(1).integers(2, 35, n)).astype(np.uint8)).to(dev)
+        bf = torch.ones(n, dtype=torch.uint8, device=dev)
+        ms = timeit(lambda: prims.intra_pred(8, s, D, s, doff, NB, nbo, mode, bf))
+        record(name, n * (m + s * s), ms, n)
+        del NB, nbo, D, doff, mode, bf
+    if a.out:
+        with open(a.out, "w") as f:
+            json.dump({"hbm_peak_GBps": HBM, "working_set_GB": a.gb, "results": results}, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
