@@ -165,17 +165,31 @@ def main():
     from src.x265_amd import Primitives
     from src.x265_amd.workload import FrameSet, WorkloadBuilder, census_batches, load_census
 
+    from src.x265_amd.shard import RefRing
+
     prims = Primitives(device=local)
     census = load_census()
     F = args.frames
-    fs = FrameSet(args.width, args.height, F, args.depth, device=f"cuda:{local}")
+    # GOP shard: rank r encodes frames [r*F, (r+1)*F) of the sequence
+    fs = FrameSet(args.width, args.height, F, args.depth, device=f"cuda:{local}", first_frame=rank * F)
     batches, wb = census_batches(fs, frames=F, census=census, builder=WorkloadBuilder(fs, seed=11 + rank))
     step_bytes = sum(b.bytes for b in batches)
     calls = sum(b.n for b in batches)
+    ring = RefRing(world, rank)
+    ref_send, ref_recv = fs.planes(F - 1), fs.planes(F)
 
-    def step():
+    def kernels():
         for b in batches:
             b.run(prims)
+
+    def exchange():
+        # frame-parallel dependency: my first frame predicts from rank-1's last frame
+        if world > 1:
+            ring.exchange(list(ref_send), list(ref_recv))
+
+    def step():
+        exchange()
+        kernels()
 
     # warmup (also JIT-free: the code objects are prebuilt) + per-kernel timing to find the dominant batch
     for _ in range(max(1, args.warmup)):
@@ -190,18 +204,23 @@ def main():
             s = torch.cuda.Stream()
             s.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(s):
-                step()
+                kernels()
             torch.cuda.current_stream().wait_stream(s)
             graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(graph):
-                step()
+                kernels()
             graph.replay()
             torch.cuda.synchronize()
         except Exception as e:  # capture unsupported: measure eager launches instead
             print(f"[bench] hipGraph capture failed ({e}); eager launches", file=sys.stderr)
             graph = None
 
-    run = graph.replay if graph is not None else step
+    def run():
+        exchange()                     # P2P over RCCL, outside the captured graph
+        if graph is not None:
+            graph.replay()
+        else:
+            kernels()
     for _ in range(args.warmup):
         run()
     barrier(world)

@@ -61,7 +61,8 @@ def load_census(path: str = CENSUS_1080P) -> dict:
 class FrameSet:
     """F padded frames (luma + 4:2:0 chroma) plus int16 residual planes, on one device."""
 
-    def __init__(self, width: int, height: int, nframes: int, depth: int = 8, device: str = "cuda", ctu: int = 64):
+    def __init__(self, width: int, height: int, nframes: int, depth: int = 8, device: str = "cuda", ctu: int = 64,
+                 first_frame: int = 0):
         import torch
 
         self.w, self.h, self.F, self.depth, self.device = width, height, nframes, depth, device
@@ -73,23 +74,40 @@ class FrameSet:
         self.cmx, self.cmy = self.mx, self.my // 2          # picyuv.cpp:71-73 (4:2:0)
         self.cstride = self.pw // 2 + 2 * self.cmx
         self.crows = self.ph // 2 + 2 * self.cmy
-        src = SyntheticSource(width, height, nframes, depth)
+        # stored frames 0..F-1 are the chunk being encoded (synthetic frames
+        # first+1 .. first+F); stored frame F is the REFERENCE SLOT holding the
+        # picture before the chunk (synthetic frame `first`), which frame 0
+        # predicts from.  Under frame sharding the slot is refilled each step
+        # with the previous rank's last frame (shard.RefRing).
+        src = SyntheticSource(width, height, nframes + 1 + first_frame, depth)
         dt = np.uint8 if depth == 8 else np.uint16
-        Y = np.zeros((nframes, self.rows, self.stride), dt)
-        U = np.zeros((nframes, self.crows, self.cstride), dt)
-        V = np.zeros((nframes, self.crows, self.cstride), dt)
-        for i in range(nframes):
-            y, u, v = src.frame(i)
+        S = nframes + 1
+        Y = np.zeros((S, self.rows, self.stride), dt)
+        U = np.zeros((S, self.crows, self.cstride), dt)
+        V = np.zeros((S, self.crows, self.cstride), dt)
+        for i in range(S):
+            y, u, v = src.frame(first_frame + (i + 1 if i < nframes else 0))
             Y[i] = self._pad(y, self.mx, self.my, self.rows, self.stride)
             U[i] = self._pad(u, self.cmx, self.cmy, self.crows, self.cstride)
             V[i] = self._pad(v, self.cmx, self.cmy, self.crows, self.cstride)
-        # residual planes: frame f minus frame f-1 (int16), same layout as luma
-        R = (Y.astype(np.int32) - np.roll(Y, 1, axis=0).astype(np.int32)).astype(np.int16)
+        # residual planes: frame f minus its reference (int16), same layout as luma
+        ref_idx = [self.ref_of(f) for f in range(S)]
+        R = (Y.astype(np.int32) - Y[ref_idx].astype(np.int32)).astype(np.int16)
         self.host = dict(Y=Y.reshape(-1), U=U.reshape(-1), V=V.reshape(-1), R=R.reshape(-1))
         t = lambda a: torch.from_numpy(a).to(device)
         self.luma, self.cb, self.cr, self.resid = t(self.host["Y"]), t(self.host["U"]), t(self.host["V"]), t(self.host["R"])
         self.plane_size = self.rows * self.stride
         self.cplane_size = self.crows * self.cstride
+
+    def ref_of(self, f):
+        """reference frame of stored frame f: the previous frame, or the reference slot for frame 0"""
+        return np.where(np.asarray(f) == 0, self.F, np.asarray(f) - 1) if not np.isscalar(f) else (self.F if f == 0 else f - 1)
+
+    def planes(self, f: int):
+        """flat views (luma, cb, cr) of stored frame f"""
+        return (self.luma[f * self.plane_size:(f + 1) * self.plane_size],
+                self.cb[f * self.cplane_size:(f + 1) * self.cplane_size],
+                self.cr[f * self.cplane_size:(f + 1) * self.cplane_size])
 
     @staticmethod
     def _pad(p, mx, my, rows, stride):
@@ -276,7 +294,7 @@ class WorkloadBuilder:
     def _fenc_ref_offsets(self, n, w, h, chroma=False, nref=1):
         fs = self.fs
         f, x, y, cand = self._positions(n, w, h, chroma)
-        r = (f + fs.F - 1) % fs.F
+        r = fs.ref_of(f)
         off = fs.chroma_off if chroma else fs.luma_off
         a = off(f, x, y)
         refs = []
