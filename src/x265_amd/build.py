@@ -16,7 +16,11 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OBJ = os.path.join(HERE, "_obj")
 LIB = os.path.join(HERE, "libx265amd.so")
-SOURCES = ["pixel.hip", "interp.hip", "transform.hip", "intra.hip", "blockops.hip", "runtime.hip"]
+# (source, object, extra flags): the EncoderPrimitives provider is built once per bit depth
+SOURCES = [("pixel.hip", "pixel.o", []), ("interp.hip", "interp.o", []), ("transform.hip", "transform.o", []),
+           ("intra.hip", "intra.o", []), ("blockops.hip", "blockops.o", []), ("runtime.hip", "runtime.o", []),
+           ("provider.cpp", "provider8.o", ["-DX265_DEPTH=8"]),
+           ("provider.cpp", "provider10.o", ["-DX265_DEPTH=10"])]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-Wno-unused-command-line-argument"]
 
@@ -29,16 +33,19 @@ def _newer(target: str, deps) -> bool:
 
 
 def _headers():
-    inc = os.path.join(os.path.dirname(os.path.dirname(HERE)), "include", "x265_amd.h")
-    return [os.path.join(CSRC, h) for h in os.listdir(CSRC) if h.endswith(".h")] + [inc]
+    inc = os.path.join(os.path.dirname(os.path.dirname(HERE)), "include")
+    return [os.path.join(CSRC, h) for h in os.listdir(CSRC) if h.endswith(".h")] + \
+           [os.path.join(inc, h) for h in os.listdir(inc) if h.endswith(".h")]
 
 
-def _compile(src: str) -> str:
-    out = os.path.join(OBJ, src.replace(".hip", ".o"))
+def _compile(entry) -> str:
+    src, obj, extra = entry
+    out = os.path.join(OBJ, obj)
     deps = [os.path.join(CSRC, src)] + _headers()
     if _newer(out, deps):
         return out
-    cmd = [HIPCC, *FLAGS, "-c", os.path.join(CSRC, src), "-o", out]
+    lang = ["-x", "hip"] if src.endswith(".cpp") else []
+    cmd = [HIPCC, *FLAGS, *extra, *lang, "-c", os.path.join(CSRC, src), "-o", out]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src}:\n{r.stdout}\n{r.stderr}")
