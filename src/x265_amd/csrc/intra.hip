@@ -10,32 +10,30 @@
 // is x265_clip((int16_t)(top + ((left[y] - topLeft) >> 1))).  all-angles
 // stores horizontal modes UN-transposed (intrapred.cpp:219-233).
 //
-// Work mapping: one (TU, mode) job per G-lane group (G = N*N/4, at most 64).
-// The group stages the 4N+1 neighbours in LDS — flipped for horizontal modes,
-// loaded as dwords — plus, for negative angles, the N projected reference
-// samples, so every angular pixel is two LDS reads and one blend.  The mode
-// is decoded once per job from packed register constants (no table loads).
-// Each lane produces 4 adjacent output pixels per step in the OUTPUT
-// orientation, so stores are contiguous and no transpose pass is needed.
+// Work mapping (template on the TU size N): one (TU, mode) job per N-lane
+// group, lane r producing output row r (N pixels, stored as full-row vector
+// stores).  The group builds the reference array of intra_pred_ang_c in LDS
+// exactly once per job, as one CONTIGUOUS int16 array R[-N .. 2N] (projected
+// left samples, top-left, the 2N above samples — all in the mode's flipped
+// frame) plus the N+1 samples of the other side L[0 .. N]; every angular
+// pixel is then two LDS reads and one blend.  The mode is decoded once per job
+// from packed register constants (no table loads).
 #include "common.h"
 #include "../../../include/x265_amd.h"
 
 namespace x265amd {
 
-constexpr int kMaxN = 32;
-constexpr int kLdsPerJob = 5 * kMaxN + 2;   // 4N+1 neighbours + N projected
-
 // |intraPredAngle| for |angleOffset| = 0..8: 0 2 5 9 13 17 21 26 32 (6 bits each)
 constexpr uint64_t kAngleMag = 0ull | (2ull << 6) | (5ull << 12) | (9ull << 18) | (13ull << 24) | (17ull << 30) |
                                (21ull << 36) | (26ull << 42) | (32ull << 48);
-// invAngle for angle = -2 .. -32 indexed by |angleOffset| - 1 (16 bits each)
+// invAngle (intrapred.cpp:124) for |angleOffset| = 8 .. 1, 16 bits each
 constexpr uint64_t kInvLo = 256ull | (315ull << 16) | (390ull << 32) | (482ull << 48);
 constexpr uint64_t kInvHi = 630ull | (910ull << 16) | (1638ull << 32) | (4096ull << 48);
 
 struct ModeInfo
 {
-    int angle;     // signed intraPredAngle (0 for planar / DC)
-    int inv;       // invAngle (negative angles only)
+    int angle;     // signed intraPredAngle (0 for planar / DC / pure H / pure V)
+    int inv;       // invAngle, used for negative angles
     bool hor;      // horizontal mode: flipped neighbours, transposed output
 };
 
@@ -47,34 +45,42 @@ __device__ __forceinline__ ModeInfo decode_mode(int mode)
     const int a = off < 0 ? -off : off;
     const int mag = (int)((kAngleMag >> (6 * a)) & 63);
     mi.angle = off < 0 ? -mag : mag;
-    // invAngleTable[-angleOffset - 1] for negative offsets: 4096, 1638, ... at |off| = 1 .. 8
-    const int k = 8 - a;   // 0 .. 7 -> 256 ... 4096 ascending
+    const int k = 8 - a;
     mi.inv = (int)(((k < 4 ? kInvLo >> (16 * k) : kInvHi >> (16 * (k - 4)))) & 0xffff);
     return mi;
 }
 
-template <typename P>
-__global__ __launch_bounds__(X265AMD_BLOCK) void k_intra_pred(int N, int lg2, int n, int lg, int maxv,
+// element e of the neighbour array as seen by a mode (flip swaps above/left)
+__device__ __forceinline__ int flip_index(int e, int n2, bool hor)
+{
+    return (!hor || e == 0) ? e : (e <= n2 ? e + n2 : e - n2);
+}
+
+template <typename P, int N>
+__global__ __launch_bounds__(X265AMD_BLOCK) void k_intra_pred(int n, int maxv,
     P* __restrict__ dst, intptr_t ds, const int64_t* __restrict__ doff,
     const P* __restrict__ nb, const int64_t* __restrict__ nboff,
     const P* __restrict__ filt, const int64_t* __restrict__ filtoff,
     const uint8_t* __restrict__ mode, const uint8_t* __restrict__ bfilter, int allangs)
 {
-    const int G = 1 << lg;
-    __shared__ int16_t sh[X265AMD_BLOCK / 4][kLdsPerJob];   // G >= 4
-    const int slot = threadIdx.x >> lg, lane = threadIdx.x & (G - 1);
-    const int64_t job = (int64_t)xcd_block() * (X265AMD_BLOCK >> lg) + slot;
+    constexpr int JOBS = X265AMD_BLOCK / N;
+    constexpr int N2 = 2 * N;
+    constexpr int LG2 = N == 4 ? 2 : N == 8 ? 3 : N == 16 ? 4 : 5;
+    constexpr int SLOT = 4 * N + 4;                  // R: 3N+1, L: N+1, padded
+    __shared__ int16_t sh[JOBS][SLOT];
+    const int slot = threadIdx.x / N, r = threadIdx.x % N;
+    const int64_t job = (int64_t)xcd_block() * JOBS + slot;
     const bool live = job < n;
     const int64_t jj = live ? job : 0;
-    int16_t* S = sh[slot];              // 4N+1 neighbours (flipped for horizontal modes)
-    int16_t* Pj = S + 4 * N + 1;        // projected samples: ref[-2-k] = Pj[k]
+    int16_t* R = sh[slot] + N;                       // R[j], j = -N .. 2N
+    int16_t* L = sh[slot] + 3 * N + 2;               // L[y], y = 0 .. N
 
     int m, bf;
     const P* src;
     P* out;
     if (allangs)
     {
-        // job = tu * 33 + (mode - 2); unfiltered or filtered neighbours per g_intraFilterFlags
+        // job = tu * 33 + (mode - 2); filtered or unfiltered neighbours per g_intraFilterFlags
         const int64_t tu = jj / 33;
         m = 2 + (int)(jj % 33);
         bf = bfilter[tu];
@@ -89,111 +95,111 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_intra_pred(int N, int lg2, in
         out = dst + doff[jj];
     }
     const ModeInfo mi = decode_mode(m);
-    const int n2 = 2 * N, tot = 4 * N + 1;
 
-    // ---- stage neighbours: 4 elements per lane per step, flip applied on the LDS write
-    for (int e0 = lane * 4; e0 < tot; e0 += G * 4)
-    {
-        int v[4];
-        if (e0 + 4 <= tot) load_row<P, 4>(src + e0, v);
-        else
-        {
-#pragma unroll
-            for (int k = 0; k < 4; k++) v[k] = e0 + k < tot ? src[e0 + k] : 0;
-        }
-#pragma unroll
-        for (int k = 0; k < 4; k++)
-        {
-            const int e = e0 + k;
-            if (e < tot)
-            {
-                const int d = (!mi.hor || e == 0) ? e : (e <= n2 ? e + n2 : e - n2);
-                S[d] = (int16_t)v[k];
-            }
-        }
-    }
-    // ---- projected left samples for negative angles (intrapred.cpp:152-164)
+    // ---- stage: R[j] = s'[1 + j] for j = -1 .. 2N-1, L[y] = s'[2N + 1 + y] for y = 0 .. N
+    //      (s' = neighbours in the mode's frame), R[-2-k] = projected left samples
+    for (int e = r; e < N2 + 1; e += N) R[e - 1] = (int16_t)src[flip_index(e, N2, mi.hor)];
+    for (int y = r; y <= N; y += N) L[y] = (int16_t)src[flip_index(N2 + 1 + y, N2, mi.hor)];
     if (mi.angle < 0)
     {
-        const int nproj = -((N * mi.angle) >> 5) - 1;
-        for (int k = lane; k < nproj; k += G)
-        {
-            const int si = n2 + ((128 + (k + 1) * mi.inv) >> 8);   // index into the flipped array
-            const int e = (!mi.hor || si == 0) ? si : (si <= n2 ? si + n2 : si - n2);
-            Pj[k] = (int16_t)src[e];
-        }
+        const int nproj = -((N * mi.angle) >> 5) - 1;     // intrapred.cpp:154-164
+        for (int k = r; k < nproj; k += N)
+            R[-2 - k] = (int16_t)src[flip_index(N2 + ((128 + (k + 1) * mi.inv) >> 8), N2, mi.hor)];
     }
     __syncthreads();
-
-    // DC value: group reduction of above + left (all groups run it; used for mode 1 only)
-    int part = 0;
-    for (int i = lane; i < n2; i += G) part += S[i < N ? 1 + i : N + 1 + i];   // above[i] / left[i - N]
-    for (int k = G >> 1; k > 0; k >>= 1) part += __shfl_xor(part, k, 64);
-    const int dc = (part + N) / (2 * N);
-
     if (!live) return;
-    const bool transposed = !allangs;
-    const int per_row = N / 4, units = per_row * N;
-    const intptr_t ostride = allangs ? N : ds;
-    for (int u = lane; u < units; u += G)
+
+    int v[N];
+    if (m == 0)   // planar (intrapred.cpp:87-100), unflipped: above = R[0..N], left = L[0..N]
     {
-        const int r = u / per_row, c = (u % per_row) * 4;
-        int v[4];
-        if (m == 0)   // planar (intrapred.cpp:87-100)
-        {
-            const int16_t* above = S + 1;
-            const int16_t* left = S + n2 + 1;
+        const int lr = L[r], bl = L[N], tr = R[N];
 #pragma unroll
-            for (int k = 0; k < 4; k++)
-                v[k] = ((N - 1 - (c + k)) * left[r] + (N - 1 - r) * above[c + k] + (c + k + 1) * above[N] +
-                        (r + 1) * left[N] + N) >> (lg2 + 1);
-        }
-        else if (m == 1)   // DC (+ dcPredFilter when bFilter)
-        {
+        for (int x = 0; x < N; x++)
+            v[x] = ((N - 1 - x) * lr + (N - 1 - r) * R[x] + (x + 1) * tr + (r + 1) * bl + N) >> (LG2 + 1);
+    }
+    else if (m == 1)   // DC (+ dcPredFilter, intrapred.cpp:53-85)
+    {
+        int t = N;
 #pragma unroll
-            for (int k = 0; k < 4; k++)
+        for (int i = 0; i < N; i++) t += R[i] + L[i];
+        const int dc = t / N2;
+#pragma unroll
+        for (int x = 0; x < N; x++) v[x] = dc;
+        if (bf)
+        {
+            if (r == 0)
             {
-                const int x = c + k;
-                int p = dc;
-                if (bf)
+                v[0] = (R[0] + L[0] + 2 * dc + 2) >> 2;
+#pragma unroll
+                for (int x = 1; x < N; x++) v[x] = (R[x] + 3 * dc + 2) >> 2;
+            }
+            else
+                v[0] = (L[r] + 3 * dc + 2) >> 2;
+        }
+    }
+    else if (!mi.hor || allangs)
+    {
+        // output row r is vertical-frame row y = r: one (offset, fraction) for the whole row
+        const int sum = (r + 1) * mi.angle, off = sum >> 5, f = sum & 31;
+        if (mi.angle == 0)
+        {
+#pragma unroll
+            for (int x = 0; x < N; x++) v[x] = R[x];
+            if (bf)
+            {
+                const int t = (int16_t)(R[0] + ((L[r] - R[-1]) >> 1));
+                v[0] = t < 0 ? 0 : (t > maxv ? maxv : t);
+            }
+        }
+        else
+        {
+            const int16_t* row = R + off;
+#pragma unroll
+            for (int x = 0; x < N; x++) v[x] = ((32 - f) * row[x] + f * row[x + 1] + 16) >> 5;
+        }
+    }
+    else
+    {
+        // horizontal mode, reference orientation: output (r, c) = vertical-frame (y = c, x = r)
+        if (mi.angle == 0)
+        {
+            // x = r: every pixel of the row is R[r], except column x = 0 of the vertical frame (row r = 0)
+#pragma unroll
+            for (int c = 0; c < N; c++)
+            {
+                int p = R[r];
+                if (bf && r == 0)
                 {
-                    if (r == 0 && x == 0) p = (S[1] + S[n2 + 1] + 2 * dc + 2) >> 2;
-                    else if (r == 0) p = (S[1 + x] + 3 * dc + 2) >> 2;
-                    else if (x == 0) p = (S[n2 + 1 + r] + 3 * dc + 2) >> 2;
+                    const int t = (int16_t)(R[0] + ((L[c] - R[-1]) >> 1));
+                    p = t < 0 ? 0 : (t > maxv ? maxv : t);
                 }
-                v[k] = p;
+                v[c] = p;
             }
         }
         else
         {
 #pragma unroll
-            for (int k = 0; k < 4; k++)
+            for (int c = 0; c < N; c++)
             {
-                // vertical-frame coordinates of output pixel (r, c + k)
-                const int y = (mi.hor && transposed) ? c + k : r;
-                const int x = (mi.hor && transposed) ? r : c + k;
-                int p;
-                if (mi.angle == 0)
-                {
-                    p = S[1 + x];
-                    if (bf && x == 0)
-                    {
-                        const int t = (int16_t)(S[1] + ((S[n2 + 1 + y] - S[0]) >> 1));
-                        p = t < 0 ? 0 : (t > maxv ? maxv : t);
-                    }
-                }
-                else
-                {
-                    const int sum = (y + 1) * mi.angle, off = sum >> 5, f = sum & 31;
-                    const int i0 = off + x, i1 = i0 + 1;
-                    const int a = i0 >= -1 ? S[1 + i0] : Pj[-2 - i0];
-                    const int b = i1 >= -1 ? S[1 + i1] : Pj[-2 - i1];
-                    p = f ? ((32 - f) * a + f * b + 16) >> 5 : a;
-                }
-                v[k] = p;
+                const int sum = (c + 1) * mi.angle, off = sum >> 5, f = sum & 31;
+                const int a = R[off + r], b = R[off + r + 1];
+                v[c] = ((32 - f) * a + f * b + 16) >> 5;
             }
         }
-        store_row<P, 4>(out + (int64_t)r * ostride + c, v);
+    }
+    P* orow = out + (int64_t)r * (allangs ? N : ds);
+    if constexpr (N == 4)
+        store_row<P, 4>(orow, v);
+    else
+    {
+#pragma unroll
+        for (int x = 0; x < N; x += 8)
+        {
+            int t[8];
+#pragma unroll
+            for (int k = 0; k < 8; k++) t[k] = v[x + k];
+            store_row<P, 8>(orow + x, t);
+        }
     }
 }
 
@@ -223,16 +229,19 @@ static int launch_pred(int N, int n, int depth, void* dst, intptr_t ds, const in
                        const int64_t* nboff, const void* filt, const int64_t* filtoff, const uint8_t* mode,
                        const uint8_t* bfilter, int allangs, hipStream_t st)
 {
-    int lg2 = 0;
-    while ((1 << lg2) < N) lg2++;
-    int g = N * N / 4;
-    if (g > 64) g = 64;
-    int lg = 0;
-    while ((1 << lg) < g) lg++;
-    const int per = X265AMD_BLOCK >> lg;
-    hipLaunchKernelGGL(k_intra_pred<P>, dim3((n + per - 1) / per), dim3(X265AMD_BLOCK), 0, st, N, lg2, n, lg,
-                       (1 << depth) - 1, (P*)dst, ds, doff, (const P*)nb, nboff, (const P*)filt, filtoff, mode,
-                       bfilter, allangs);
+    const int per = X265AMD_BLOCK / N;
+    const dim3 grid((n + per - 1) / per);
+#define L(NN) hipLaunchKernelGGL((k_intra_pred<P, NN>), grid, dim3(X265AMD_BLOCK), 0, st, n, (1 << depth) - 1, \
+                                 (P*)dst, ds, doff, (const P*)nb, nboff, (const P*)filt, filtoff, mode, bfilter, allangs)
+    switch (N)
+    {
+    case 4: L(4); break;
+    case 8: L(8); break;
+    case 16: L(16); break;
+    case 32: L(32); break;
+    default: return X265AMD_EINVAL;
+    }
+#undef L
     return (int)hipGetLastError();
 }
 
