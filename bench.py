@@ -132,25 +132,23 @@ def cpu_baseline(args, census):
     kind = "reference" if available("ref", args.depth) else "port"
     threads = max(1, min(16, os.cpu_count() or 1))
     prims = CpuPrims("ref" if kind == "reference" else "oracle", args.depth, nthreads=threads)
-    fs = FrameSet(args.width, args.height, 2, args.depth, device="cpu")
-    # calibrate on a small slice, then size the sample to ~args.cpu_seconds
-    scale = 0.02
-    bs, _ = census_batches(fs, frames=1, scale=scale, census=census, builder=WorkloadBuilder(fs, seed=3))
-    t0 = time.perf_counter()
-    for b in bs:
-        b.run(prims)
-    dt = time.perf_counter() - t0
-    scale2 = min(16.0, scale * args.cpu_seconds / max(dt, 1e-3))
-    bs, _ = census_batches(fs, frames=1, scale=scale2, census=census, builder=WorkloadBuilder(fs, seed=4))
+    frames = 2
+    fs = FrameSet(args.width, args.height, frames, args.depth, device="cpu")
+    # the census of `frames` frames, replayed until about args.cpu_seconds of CPU time have passed
+    bs, _ = census_batches(fs, frames=frames, census=census, builder=WorkloadBuilder(fs, seed=4))
     torch.set_num_threads(1)
-    t0 = time.perf_counter()
-    for b in bs:
-        b.run(prims)
-    dt = time.perf_counter() - t0
-    fps = scale2 / dt
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        for b in bs:
+            b.run(prims)
+        reps += 1
+        dt = time.perf_counter() - t0
+        if dt >= args.cpu_seconds:
+            break
+    fps = frames * reps / dt
     return {"value": round(fps, 3), "unit": "fps", "cores": threads, "kind": kind,
-            "sample": f"{scale2:.3f} x one 1080p frame's census workload ({sum(b.n for b in bs)} calls, "
-                      f"same batch descriptors as the GPU path) in {dt:.1f}s on {threads} host threads "
+            "sample": f"{reps} x the census workload of {frames} 1080p frames ({sum(b.n for b in bs)} calls per "
+                      f"pass, the same batch descriptors as the GPU path) in {dt:.1f}s on {threads} host threads "
                       f"({'x265 1.9 C primitives, oracle/_ref' if kind == 'reference' else 'oracle restatement'})",
             "mpix_per_s": round(fps * args.width * args.height / 1e6, 3)}
 
