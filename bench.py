@@ -49,6 +49,7 @@ def parse():
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--depth", type=int, default=8)
     ap.add_argument("--no-graph", action="store_true", help="launch eagerly instead of replaying a hipGraph")
+    ap.add_argument("--no-group", action="store_true", help="one launch per batch instead of grouped multi-shape launches")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample duration")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--breakdown", type=str, default="", help="write per-batch timing JSON here")
@@ -161,7 +162,7 @@ def main():
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs the MI355X (no CPU fallback)")
     from src.x265_amd import Primitives
-    from src.x265_amd.workload import FrameSet, WorkloadBuilder, census_batches, load_census
+    from src.x265_amd.workload import FrameSet, WorkloadBuilder, census_batches, group_launches, load_census
 
     from src.x265_amd.shard import RefRing
 
@@ -171,13 +172,15 @@ def main():
     # GOP shard: rank r encodes frames [r*F, (r+1)*F) of the sequence
     fs = FrameSet(args.width, args.height, F, args.depth, device=f"cuda:{local}", first_frame=rank * F)
     batches, wb = census_batches(fs, frames=F, census=census, builder=WorkloadBuilder(fs, seed=11 + rank))
+    # one launch per kernel class: batches of different block shapes share a grouped launch
+    launches = list(batches) if args.no_group else group_launches(batches)
     step_bytes = sum(b.bytes for b in batches)
     calls = sum(b.n for b in batches)
     ring = RefRing(world, rank)
     ref_send, ref_recv = fs.planes(F - 1), fs.planes(F)
 
     def kernels():
-        for b in batches:
+        for b in launches:
             b.run(prims)
 
     def exchange():
@@ -193,8 +196,8 @@ def main():
     for _ in range(max(1, args.warmup)):
         step()
     torch.cuda.synchronize()
-    ktimes = kernel_times(batches, prims)
-    dominant = max(batches, key=lambda b: ktimes[b.name])
+    ktimes = kernel_times(launches, prims)
+    dominant = max(launches, key=lambda b: ktimes[b.name])
 
     graph = None
     if not args.no_graph:
@@ -277,7 +280,8 @@ def main():
                             "tests/golden/census_1080p_medium.json) replayed as batched gfx950 kernels; "
                             "CPU-side entries (CABAC estimates, SAO, lowres init) excluded",
                 "resolution": f"{args.width}x{args.height}", "depth": args.depth, "frames_per_step_per_gpu": F,
-                "calls_per_step_per_gpu": calls, "launches_per_step": len(batches),
+                "calls_per_step_per_gpu": calls, "batches_per_step": len(batches),
+                "launches_per_step": len(launches),
                 "algorithmic_GB_per_step_per_gpu": round(step_bytes / 1e9, 3),
                 "hipgraph": graph is not None, "parallelism": f"frame-shard x{world}",
             },
@@ -290,7 +294,7 @@ def main():
         if args.breakdown:
             with open(args.breakdown, "w") as f:
                 json.dump({b.name: {"ms": ktimes[b.name], "jobs": b.n, "bytes": b.bytes,
-                                    "GBps": b.bytes / (ktimes[b.name] * 1e-3) / 1e9} for b in batches}, f, indent=1)
+                                    "GBps": b.bytes / (ktimes[b.name] * 1e-3) / 1e9} for b in launches}, f, indent=1)
         print(json.dumps(line), flush=True)
     if world > 1:
         import torch.distributed as dist

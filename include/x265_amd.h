@@ -38,7 +38,8 @@
 extern "C" {
 #endif
 
-#define X265AMD_ABI_VERSION 1
+/* 1: per-shape batched entries; 2: + the *_grouped multi-shape entries */
+#define X265AMD_ABI_VERSION 2
 
 enum
 {
@@ -96,6 +97,26 @@ int x265amd_sad_multi(int nref, int depth, int w, int h, int n,
                       const void* ref, intptr_t ref_stride, const int64_t* ref_off,
                       int32_t* out, void* stream);
 
+/* Grouped forms: `count` batches of one op but any mix of block shapes (and
+ * operands) in as few launches as possible — batches of the same kernel class
+ * share a launch, up to 16 per launch.  Equivalent to calling
+ * x265amd_pixelcmp / x265amd_sad_multi once per batch, in order; the whole
+ * call is rejected (nothing enqueued) if any batch has an invalid shape.
+ * For sad_multi, b/b_stride/b_off are the reference blocks (nref per job). */
+typedef struct x265amd_cmp_batch
+{
+    int w, h, n;
+    const void* a;
+    intptr_t a_stride;
+    const int64_t* a_off;
+    const void* b;
+    intptr_t b_stride;
+    const int64_t* b_off;
+    void* out;
+} x265amd_cmp_batch;
+int x265amd_pixelcmp_grouped(int op, int depth, int count, const x265amd_cmp_batch* batches, void* stream);
+int x265amd_sad_multi_grouped(int nref, int depth, int count, const x265amd_cmp_batch* batches, void* stream);
+
 /* ---------------------------------------------------------------------- a9
  * Sub-pel interpolation (ipfilter.cpp:40-372).  taps = 8 (luma pu[].luma_*)
  * or 4 (chroma[].pu[].filter_*).  Operand types per op:
@@ -125,6 +146,23 @@ int x265amd_interp(int op, int taps, int depth, int w, int h, int n,
                    const void* src, intptr_t src_stride, const int64_t* src_off,
                    void* dst, intptr_t dst_stride, const int64_t* dst_off,
                    const uint8_t* coeff, int is_row_ext, void* stream);
+/* Grouped form: `count` batches of one (op, taps), any mix of block shapes,
+ * packed into as few launches as possible (same semantics as one
+ * x265amd_interp call per batch, in order; rejected whole if any batch is
+ * invalid). */
+typedef struct x265amd_interp_batch
+{
+    int w, h, n, is_row_ext;
+    const void* src;
+    intptr_t src_stride;
+    const int64_t* src_off;
+    void* dst;
+    intptr_t dst_stride;
+    const int64_t* dst_off;
+    const uint8_t* coeff;
+} x265amd_interp_batch;
+int x265amd_interp_grouped(int op, int taps, int depth, int count, const x265amd_interp_batch* batches,
+                           void* stream);
 
 /* ----------------------------------------------------------------- a10 a11
  * 2-D transforms (dct.cpp:442-610): cu[].dct / cu[].idct for size 4..32 and
@@ -228,6 +266,23 @@ int x265amd_blockop(int op, int depth, int w, int h, int n,
                     const void* a, intptr_t a_stride, const int64_t* a_off,
                     const void* b, intptr_t b_stride, const int64_t* b_off,
                     int param, void* stream);
+/* Grouped form: `count` batches of one op, any mix of block shapes, packed
+ * into as few launches as possible (same semantics as one x265amd_blockop
+ * call per batch, in order; rejected whole if any batch is invalid). */
+typedef struct x265amd_block_batch
+{
+    int w, h, n, param;
+    void* dst;
+    intptr_t dst_stride;
+    const int64_t* dst_off;
+    const void* a;
+    intptr_t a_stride;
+    const int64_t* a_off;
+    const void* b;
+    intptr_t b_stride;
+    const int64_t* b_off;
+} x265amd_block_batch;
+int x265amd_blockop_grouped(int op, int depth, int count, const x265amd_block_batch* batches, void* stream);
 
 /* count_nonzero (dct.cpp:714-726, num = N*N contiguous int16) and copy_cnt
  * (dct.cpp:728-742: coeff[N*N] <- residual with res_stride, counting nonzero).

@@ -42,23 +42,24 @@ __device__ __forceinline__ void ld(const T* p, int (&o)[UW])
 }
 
 template <typename P, int OP, int UW, int UH>
-__global__ __launch_bounds__(X265AMD_BLOCK) void k_blockop(int w, int h, int n, int lg, int depth,
-    typename OpTypes<P, OP>::d* __restrict__ dst, intptr_t ds, const int64_t* __restrict__ doff,
-    const typename OpTypes<P, OP>::a* __restrict__ a, intptr_t sa, const int64_t* __restrict__ aoff,
-    const typename OpTypes<P, OP>::b* __restrict__ b, intptr_t sb, const int64_t* __restrict__ boff, int param)
+__global__ __launch_bounds__(X265AMD_BLOCK) void k_blockop(const BatchGroup g)
 {
     typedef typename OpTypes<P, OP>::d D;
     typedef typename OpTypes<P, OP>::a A;
     typedef typename OpTypes<P, OP>::b B;
+    const uint32_t gb = xcd_block();
+    const SubBatch& sub = group_sub(g, gb);
+    const int w = sub.w, h = sub.h, n = sub.n, lg = sub.lg, param = sub.param, depth = g.depth;
+    const intptr_t ds = sub.ds, sa = sub.sa, sb = sub.sb;
     const int G = 1 << lg;
-    const int64_t job = (int64_t)xcd_block() * (X265AMD_BLOCK >> lg) + (threadIdx.x >> lg);
+    const int64_t job = (int64_t)(gb - sub.block0) * (X265AMD_BLOCK >> lg) + (threadIdx.x >> lg);
     const int lane = threadIdx.x & (G - 1);
     if (job >= n) return;
 
-    D* pd = dst + doff[job];
-    const A* pa = OP == X265AMD_BLOCKFILL ? nullptr : a + aoff[job];
+    D* pd = (D*)sub.d + sub.doff[job];
+    const A* pa = OP == X265AMD_BLOCKFILL ? nullptr : (const A*)sub.a + sub.aoff[job];
     const B* pb = (OP == X265AMD_SUB_PS || OP == X265AMD_ADD_PS || OP == X265AMD_ADDAVG || OP == X265AMD_PIXELAVG)
-                  ? b + boff[job] : nullptr;
+                  ? (const B*)sub.b + sub.boff[job] : nullptr;
     const int maxv = (1 << depth) - 1;
     const int avg_shift = 15 - depth, avg_off = (1 << (avg_shift - 1)) + 2 * 8192;
     const int ux = w / UW, units = ux * (h / UH);
@@ -113,47 +114,61 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_blockop(int w, int h, int n, 
     }
 }
 
-template <typename P, int OP>
-static int launch_blockop(int w, int h, int n, int depth, void* dst, intptr_t ds, const int64_t* doff,
-                          const void* a, intptr_t sa, const int64_t* aoff, const void* b, intptr_t sb,
-                          const int64_t* boff, int param, hipStream_t st)
+// kernel class: unit width (8/4/2 elements) x unit height (4 rows when the
+// block allows, so several row loads are in flight per lane, else 1)
+static int blockop_class(int w, int h)
 {
-    typedef typename OpTypes<P, OP>::d D;
-    typedef typename OpTypes<P, OP>::a A;
-    typedef typename OpTypes<P, OP>::b B;
+    if (w < 2 || h < 1 || w > 64 || h > 64 || (w % 2)) return -X265AMD_EINVAL;
     const int uw = (w % 8 == 0) ? 8 : (w % 4 == 0) ? 4 : 2;
-    if (w % 2) return X265AMD_EINVAL;
-    const int uh = (h % 4 == 0) ? 4 : 1;       // 4-row units keep several row loads in flight per lane
-    const int units = (w / uw) * (h / uh);
-    int g = pow2ceil((units + 1) / 2);
-    if (g > 64) g = 64;
-    int lg = 0;
-    while ((1 << lg) < g) lg++;
-    const dim3 grid((n + (X265AMD_BLOCK >> lg) - 1) / (X265AMD_BLOCK >> lg));
-#define L(UW, UH) hipLaunchKernelGGL((k_blockop<P, OP, UW, UH>), grid, dim3(X265AMD_BLOCK), 0, st, w, h, n, lg, depth, \
-                                     (D*)dst, ds, doff, (const A*)a, sa, aoff, (const B*)b, sb, boff, param)
-    if (uh == 4)
-    {
-        if (uw == 8) L(8, 4);
-        else if (uw == 4) L(4, 4);
-        else L(2, 4);
+    const int uh = (h % 4 == 0) ? 4 : 1;
+    return uw * 8 + uh;
+}
+
+template <typename P, int OP>
+static int launch_blockop(int cls, const BatchGroup& g, uint32_t blocks, hipStream_t st)
+{
+#define L(UW, UH) \
+    if (cls == UW * 8 + UH) \
+    { \
+        hipLaunchKernelGGL((k_blockop<P, OP, UW, UH>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, g); \
+        return (int)hipGetLastError(); \
     }
-    else
-    {
-        if (uw == 8) L(8, 1);
-        else if (uw == 4) L(4, 1);
-        else L(2, 1);
-    }
+    L(8, 4) L(4, 4) L(2, 4) L(8, 1) L(4, 1) L(2, 1)
 #undef L
-    return (int)hipGetLastError();
+    return X265AMD_EINVAL;
+}
+
+template <typename P, int OP>
+static int grouped_blockop(int depth, int count, const x265amd_block_batch* bt, hipStream_t st)
+{
+    std::vector<int> cls(count, -1);
+    for (int i = 0; i < count; i++)
+    {
+        if (bt[i].n < 0) return X265AMD_EINVAL;
+        if (bt[i].n == 0) continue;
+        cls[i] = blockop_class(bt[i].w, bt[i].h);
+        if (cls[i] < 0) return -cls[i];
+    }
+    BatchGroup proto{};
+    proto.depth = depth;
+    return launch_grouped(count, cls.data(), proto,
+        [&](int i, SubBatch& s) {
+            const x265amd_block_batch& b = bt[i];
+            s = SubBatch{};
+            s.d = b.dst; s.doff = b.dst_off; s.ds = b.dst_stride;
+            s.a = b.a; s.aoff = b.a_off; s.sa = b.a_stride;
+            s.b = b.b; s.boff = b.b_off; s.sb = b.b_stride;
+            s.w = b.w; s.h = b.h; s.n = b.n; s.param = b.param;
+            const int uw = cls[i] / 8, uh = cls[i] % 8;
+            s.lg = lanes_log2((b.w / uw) * (b.h / uh));
+        },
+        [&](int c, const BatchGroup& g, uint32_t blocks) { return launch_blockop<P, OP>(c, g, blocks, st); });
 }
 
 template <typename P>
-static int dispatch_blockop(int op, int w, int h, int n, int depth, void* dst, intptr_t ds, const int64_t* doff,
-                            const void* a, intptr_t sa, const int64_t* aoff, const void* b, intptr_t sb,
-                            const int64_t* boff, int param, hipStream_t st)
+static int dispatch_blockop(int op, int depth, int count, const x265amd_block_batch* bt, hipStream_t st)
 {
-#define C(OP) case OP: return launch_blockop<P, OP>(w, h, n, depth, dst, ds, doff, a, sa, aoff, b, sb, boff, param, st)
+#define C(OP) case OP: return grouped_blockop<P, OP>(depth, count, bt, st)
     switch (op)
     {
     C(X265AMD_SUB_PS); C(X265AMD_ADD_PS); C(X265AMD_ADDAVG); C(X265AMD_PIXELAVG);
@@ -169,6 +184,16 @@ static int dispatch_blockop(int op, int w, int h, int n, int depth, void* dst, i
 
 using namespace x265amd;
 
+extern "C" int x265amd_blockop_grouped(int op, int depth, int count, const x265amd_block_batch* batches,
+                                       void* stream)
+{
+    if (count < 0 || (count > 0 && !batches)) return X265AMD_EINVAL;
+    hipStream_t st = (hipStream_t)stream;
+    if (depth == 8) return dispatch_blockop<uint8_t>(op, depth, count, batches, st);
+    if (depth == 10 || depth == 12) return dispatch_blockop<uint16_t>(op, depth, count, batches, st);
+    return X265AMD_EINVAL;
+}
+
 extern "C" int x265amd_blockop(int op, int depth, int w, int h, int n,
                                void* dst, intptr_t dst_stride, const int64_t* dst_off,
                                const void* a, intptr_t a_stride, const int64_t* a_off,
@@ -176,11 +201,6 @@ extern "C" int x265amd_blockop(int op, int depth, int w, int h, int n,
                                int param, void* stream)
 {
     if (n <= 0) return 0;
-    if (w < 2 || h < 1 || w > 64 || h > 64) return X265AMD_EINVAL;
-    hipStream_t st = (hipStream_t)stream;
-    if (depth == 8)
-        return dispatch_blockop<uint8_t>(op, w, h, n, depth, dst, dst_stride, dst_off, a, a_stride, a_off, b, b_stride, b_off, param, st);
-    if (depth == 10 || depth == 12)
-        return dispatch_blockop<uint16_t>(op, w, h, n, depth, dst, dst_stride, dst_off, a, a_stride, a_off, b, b_stride, b_off, param, st);
-    return X265AMD_EINVAL;
+    const x265amd_block_batch bt = {w, h, n, param, dst, dst_stride, dst_off, a, a_stride, a_off, b, b_stride, b_off};
+    return x265amd_blockop_grouped(op, depth, 1, &bt, stream);
 }

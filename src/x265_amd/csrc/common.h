@@ -12,6 +12,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <vector>
+
 #include "tables.h"
 
 #define X265AMD_BLOCK 256
@@ -73,6 +75,98 @@ inline int pow2ceil(int v)
     int g = 1;
     while (g < v) g <<= 1;
     return g;
+}
+
+// log2 of the lanes per job: two units per lane, so small blocks get one lane
+// per job (all of the job's row loads in flight from one lane) and large ones
+// up to a full wavefront
+inline int lanes_log2(int units)
+{
+    int g = pow2ceil((units + 1) / 2);
+    if (g > 64) g = 64;
+    int lg = 0;
+    while ((1 << lg) < g) lg++;
+    return lg;
+}
+
+inline uint32_t blocks_for(int n, int lg)
+{
+    const int per = X265AMD_BLOCK >> lg;
+    return (uint32_t)((n + per - 1) / per);
+}
+
+// ---------------------------------------------------------------- grouped launches
+// One launch carries up to kMaxSub sub-batches of one kernel class (same
+// template instantiation) but different block shapes and operands.  The table
+// travels in the kernarg segment (aggregate kernel arguments are passed by
+// reference there, so the dynamic index below is a scalar load, not a copy);
+// every workgroup belongs to exactly one sub-batch and finds it with a uniform
+// scan over block0.  A launch of 16 small shapes fills the chip like one large
+// batch instead of 16 short launches each under-occupying it.
+constexpr int kMaxSub = 16;
+
+struct SubBatch
+{
+    void* d;                // destination / output
+    const int64_t* doff;
+    int64_t ds;
+    const void* a;          // first operand
+    const int64_t* aoff;
+    int64_t sa;
+    const void* b;          // second operand (interp: per-job coefficient index)
+    const int64_t* boff;
+    int64_t sb;
+    int w, h, n, lg;
+    int param;
+    uint32_t block0;        // first logical block of this sub-batch
+};
+
+struct BatchGroup
+{
+    SubBatch s[kMaxSub];
+    int count;
+    int depth;
+    int flag;               // pixelcmp: sse_t wraps to 32 bits
+    int pad;
+};
+
+__device__ __forceinline__ const SubBatch& group_sub(const BatchGroup& g, uint32_t gb)
+{
+    int s = 0;
+#pragma unroll
+    for (int i = 1; i < kMaxSub; i++)
+        if (i < g.count && g.s[i].block0 <= gb) s = i;
+    return g.s[s];
+}
+
+// Host side: packs `count` batches into launches, one kernel class per launch
+// (first-come order, at most kMaxSub sub-batches each).  cls[i] < 0 marks an
+// empty batch.  fill(i, sub) sets everything but block0 (lg included);
+// launch(cls, group, blocks) enqueues one kernel and returns its status.
+template <typename Fill, typename Launch>
+inline int launch_grouped(int count, const int* cls, const BatchGroup& proto, Fill fill, Launch launch)
+{
+    std::vector<char> done(count, 0);
+    for (int i = 0; i < count; i++)
+    {
+        if (done[i] || cls[i] < 0) continue;
+        BatchGroup g = proto;
+        uint32_t blocks = 0;
+        int k = 0;
+        for (int j = i; j < count && k < kMaxSub; j++)
+        {
+            if (done[j] || cls[j] != cls[i]) continue;
+            done[j] = 1;
+            SubBatch& s = g.s[k++];
+            fill(j, s);
+            s.block0 = blocks;
+            blocks += blocks_for(s.n, s.lg);
+        }
+        g.count = k;
+        const int rc = launch(cls[i], g, blocks);
+        if (rc) return rc;
+    }
+    return 0;
 }
 
 // ---------------------------------------------------------------- loads

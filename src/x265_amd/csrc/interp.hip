@@ -16,6 +16,8 @@
 // read window); vertical filters slide a taps-row window through registers so
 // each source row is loaded once per unit; hv_pp recomputes the horizontal
 // int16 intermediate for the UH+7 rows its unit needs, entirely on-chip.
+#include <algorithm>
+
 #include "common.h"
 #include "../../../include/x265_amd.h"
 
@@ -109,27 +111,30 @@ __device__ __forceinline__ void hfilter(const P* src, const int (&c)[TAPS], int 
     }
 }
 
+// Grouped launches (common.h): a = src, d = dst, b = per-job coeffIdx
+// (uint8), param = is_row_ext.
 template <typename P, typename S, typename D, int OP, int TAPS, int UW, int UH>
-__global__ __launch_bounds__(X265AMD_BLOCK) void k_interp(int w, int h, int n, int lg, int depth,
-    const S* __restrict__ src, intptr_t ss, const int64_t* __restrict__ soff,
-    D* __restrict__ dst, intptr_t ds, const int64_t* __restrict__ doff,
-    const uint8_t* __restrict__ coeff, int rowext)
+__global__ __launch_bounds__(X265AMD_BLOCK) void k_interp(const BatchGroup g)
 {
+    const uint32_t gb = xcd_block();
+    const SubBatch& sub = group_sub(g, gb);
+    const int w = sub.w, h = sub.h, n = sub.n, lg = sub.lg;
+    const intptr_t ss = sub.sa, ds = sub.ds;
     const int G = 1 << lg;
-    const uint32_t lb = xcd_block();
-    const int64_t job = (int64_t)lb * (X265AMD_BLOCK >> lg) + (threadIdx.x >> lg);
+    const int64_t job = (int64_t)(gb - sub.block0) * (X265AMD_BLOCK >> lg) + (threadIdx.x >> lg);
     const int lane = threadIdx.x & (G - 1);
     if (job >= n) return;
 
-    const IfConst K(depth);
-    const S* ps = src + soff[job];
-    D* pd = dst + doff[job];
+    const IfConst K(g.depth);
+    const S* ps = (const S*)sub.a + sub.aoff[job];
+    D* pd = (D*)sub.d + sub.doff[job];
+    const uint8_t* coeff = (const uint8_t*)sub.b;
     const int cidx = coeff ? coeff[job] : 0;
 
     int rows = h;
     if constexpr (OP == X265AMD_HPS)
     {
-        if (rowext)
+        if (sub.param)
         {
             ps -= (TAPS / 2 - 1) * ss;
             rows += TAPS - 1;
@@ -138,7 +143,7 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_interp(int w, int h, int n, i
     const int ux = w / UW, units = ux * (rows / UH);
 
     int c[TAPS];
-    get_taps<TAPS>(OP == X265AMD_HVPP ? (cidx & 15) : cidx, c);
+    get_taps<TAPS>(cidx, c);
 
     for (int u = lane; u < units; u += G)
     {
@@ -168,43 +173,6 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_interp(int w, int h, int n, i
 #pragma unroll
                 for (int i = 0; i < UW; i++) v[i] = (int)(int16_t)((int16_t)(v[i] << K.p2s_shift) - 8192);
                 store_row<D, UW>(pd + (y0 + r) * ds + x, v);
-            }
-        }
-        else if constexpr (OP == X265AMD_HVPP)
-        {
-            // immed rows y0 .. y0+UH+6 (immed row i = horizontal ps of src row i-3)
-            int cy[TAPS];
-            get_taps<TAPS>(cidx >> 4, cy);
-            int acc[UH][UW];
-#pragma unroll
-            for (int r = 0; r < UH; r++)
-#pragma unroll
-                for (int i = 0; i < UW; i++) acc[r][i] = 0;
-#pragma unroll
-            for (int t = 0; t < UH + TAPS - 1; t++)
-            {
-                int sum[UW];
-                hfilter<P, TAPS, UW>((const P*)ps + (y0 + t - (TAPS / 2 - 1)) * ss + x, c, sum);
-#pragma unroll
-                for (int i = 0; i < UW; i++) sum[i] = (int)(int16_t)((sum[i] + K.ps_off) >> K.ps_shift);
-#pragma unroll
-                for (int r = 0; r < UH; r++)
-                {
-                    const int k = t - r;
-                    if (k >= 0 && k < TAPS)
-                    {
-#pragma unroll
-                        for (int i = 0; i < UW; i++) acc[r][i] += sum[i] * cy[k];
-                    }
-                }
-            }
-#pragma unroll
-            for (int r = 0; r < UH; r++)
-            {
-                int o[UW];
-#pragma unroll
-                for (int i = 0; i < UW; i++) o[i] = clampp((acc[r][i] + K.sp_off) >> K.sp_shift, K.maxv);
-                store_row<D, UW>(pd + (y0 + r) * ds + x, o);
             }
         }
         else  // vertical: VPP, VPS, VSP, VSS
@@ -253,21 +221,24 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_interp(int w, int h, int n, i
 // hv_pp in two on-chip passes: the horizontal int16 intermediate of the
 // (h+7) x w block (interp_horiz_ps_c with row extension) goes to LDS once,
 // then the vertical sp filter reads it back (filterVertical_sp_c).  Jobs per
-// block = 256 / G, LDS = jobs * (h+7) * w int16.
+// block = 256 / G, LDS = jobs * (h+7) * w int16 (the launch reserves the
+// largest sub-batch's need).
 template <typename P, int UW, int UH>
-__global__ __launch_bounds__(X265AMD_BLOCK) void k_hvpp(int w, int h, int n, int lg, int depth,
-    const P* __restrict__ src, intptr_t ss, const int64_t* __restrict__ soff,
-    P* __restrict__ dst, intptr_t ds, const int64_t* __restrict__ doff, const uint8_t* __restrict__ coeff)
+__global__ __launch_bounds__(X265AMD_BLOCK) void k_hvpp(const BatchGroup g)
 {
     extern __shared__ int16_t hv_lds[];
+    const uint32_t gb = xcd_block();
+    const SubBatch& sub = group_sub(g, gb);
+    const int w = sub.w, h = sub.h, n = sub.n, lg = sub.lg;
+    const intptr_t ss = sub.sa, ds = sub.ds;
     const int G = 1 << lg;
     const int slot = threadIdx.x >> lg, lane = threadIdx.x & (G - 1);
-    const int64_t job0 = (int64_t)xcd_block() * (X265AMD_BLOCK >> lg) + slot;
+    const int64_t job0 = (int64_t)(gb - sub.block0) * (X265AMD_BLOCK >> lg) + slot;
     const bool live = job0 < n;
     const int64_t job = live ? job0 : 0;
-    const IfConst K(depth);
+    const IfConst K(g.depth);
     int16_t* L = hv_lds + (size_t)slot * (h + 7) * w;
-    const int cidx = coeff[job];
+    const int cidx = ((const uint8_t*)sub.b)[job];
     int cx[8], cy[8];
     get_taps<8>(cidx & 15, cx);
     get_taps<8>(cidx >> 4, cy);
@@ -275,7 +246,7 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_hvpp(int w, int h, int n, int
 
     if (live)
     {
-        const P* ps = src + soff[job] - 3 * ss;
+        const P* ps = (const P*)sub.a + sub.aoff[job] - 3 * ss;
         const int hunits = ux * (h + 7);
         for (int u = lane; u < hunits; u += G)
         {
@@ -289,7 +260,7 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_hvpp(int w, int h, int n, int
     }
     __syncthreads();
     if (!live) return;
-    P* pd = dst + doff[job];
+    P* pd = (P*)sub.d + sub.doff[job];
     const int vunits = ux * (h / UH);
     for (int u = lane; u < vunits; u += G)
     {
@@ -326,95 +297,112 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_hvpp(int w, int h, int n, int
     }
 }
 
-template <typename P>
-static int launch_hvpp(int w, int h, int n, int depth, const void* src, intptr_t ss, const int64_t* soff,
-                       void* dst, intptr_t ds, const int64_t* doff, const uint8_t* coeff, hipStream_t st)
-{
-    const int uw = w % 8 == 0 ? 8 : 4, uh = h % 4 == 0 ? 4 : 1;
-    if (w % 4) return X265AMD_EINVAL;
-    const int units = (w / uw) * (h / uh);
-    int g = pow2ceil((units + 1) / 2);
-    if (g > 64) g = 64;
-    int lg = 0;
-    while ((1 << lg) < g) lg++;
-    // keep the workgroup's intermediate within 64 KiB of LDS
-    while (lg < 6 && (size_t)(X265AMD_BLOCK >> lg) * (h + 7) * w * sizeof(int16_t) > 65536) lg++;
-    const int per = X265AMD_BLOCK >> lg;
-    const size_t lds = (size_t)per * (h + 7) * w * sizeof(int16_t);
-    const dim3 grid((n + per - 1) / per);
-#define L(UW, UH) hipLaunchKernelGGL((k_hvpp<P, UW, UH>), grid, dim3(X265AMD_BLOCK), lds, st, w, h, n, lg, depth, \
-                                     (const P*)src, ss, soff, (P*)dst, ds, doff, coeff)
-    if (uw == 8) { if (uh == 4) L(8, 4); else L(8, 1); }
-    else { if (uh == 4) L(4, 4); else L(4, 1); }
-#undef L
-    return (int)hipGetLastError();
-}
-
 // -------------------------------------------------------------- dispatch
 
-template <typename P, typename S, typename D, int OP, int TAPS, int UW, int UH>
-static int launch_interp(int w, int h, int n, int depth, const void* src, intptr_t ss, const int64_t* soff,
-                         void* dst, intptr_t ds, const int64_t* doff, const uint8_t* coeff, int rowext,
-                         hipStream_t st)
+// kernel class of a batch: unit width x unit height, packed as uw * 8 + uh
+template <int OP, int TAPS>
+static int interp_class(int w, int h, int rowext)
 {
+    if (w < 2 || h < 2 || w > 64 || h > 64) return -X265AMD_EINVAL;
+    if constexpr (OP == X265AMD_HVPP)
+    {
+        if (w % 4) return -X265AMD_EINVAL;
+        return (w % 8 == 0 ? 8 : 4) * 8 + (h % 4 == 0 ? 4 : 1);
+    }
     const int rows = (OP == X265AMD_HPS && rowext) ? h + TAPS - 1 : h;
-    const int units = (w / UW) * (rows / UH);
-    int g = pow2ceil((units + 1) / 2);    // two units per lane
-    if (g > 64) g = 64;
-    int lg = 0;
-    while ((1 << lg) < g) lg++;
-    const int per = X265AMD_BLOCK >> lg;
-    hipLaunchKernelGGL((k_interp<P, S, D, OP, TAPS, UW, UH>), dim3((n + per - 1) / per), dim3(X265AMD_BLOCK), 0, st,
-                       w, h, n, lg, depth, (const S*)src, ss, soff, (D*)dst, ds, doff, coeff, rowext);
-    return (int)hipGetLastError();
+    const int uh = rows % 4 ? 1 : 4;
+    if (w % 8 == 0) return 8 * 8 + uh;
+    if (w % 4 == 0) return 4 * 8 + uh;
+    // 2-wide units: the chroma filters and the vertical / p2s luma paths
+    if (w % 2 == 0 && (TAPS == 4 || (OP != X265AMD_HPP && OP != X265AMD_HPS))) return 2 * 8 + uh;
+    return -X265AMD_EINVAL;
+}
+
+// HV_PP: keep the workgroup's intermediate within 64 KiB of LDS
+static int hvpp_lg(int w, int h, int uw, int uh)
+{
+    int lg = lanes_log2((w / uw) * (h / uh));
+    while (lg < 6 && (size_t)(X265AMD_BLOCK >> lg) * (h + 7) * w * sizeof(int16_t) > 65536) lg++;
+    return lg;
 }
 
 template <typename P, typename S, typename D, int OP, int TAPS>
-static int pick_unit(int w, int h, int n, int depth, const void* src, intptr_t ss, const int64_t* soff,
-                     void* dst, intptr_t ds, const int64_t* doff, const uint8_t* coeff, int rowext, hipStream_t st)
+static int launch_interp(int cls, const BatchGroup& g, uint32_t blocks, hipStream_t st)
 {
-    const int rows = (OP == X265AMD_HPS && rowext) ? h + TAPS - 1 : h;
-#define L(UW, UH) return launch_interp<P, S, D, OP, TAPS, UW, UH>(w, h, n, depth, src, ss, soff, dst, ds, doff, coeff, rowext, st)
-    if (w % 8 == 0)
-    {
-        if (rows % 4) L(8, 1);
-        L(8, 4);
+    size_t lds = 0;
+    if constexpr (OP == X265AMD_HVPP)
+        for (int i = 0; i < g.count; i++)
+            lds = std::max(lds, (size_t)(X265AMD_BLOCK >> g.s[i].lg) * (g.s[i].h + 7) * g.s[i].w * sizeof(int16_t));
+#define L(UW, UH) \
+    if (cls == UW * 8 + UH) \
+    { \
+        if constexpr (OP == X265AMD_HVPP) \
+        { \
+            if constexpr (UW >= 4) \
+                hipLaunchKernelGGL((k_hvpp<P, UW, UH>), dim3(blocks), dim3(X265AMD_BLOCK), lds, st, g); \
+        } \
+        else if constexpr (UW >= 4 || TAPS == 4 || (OP != X265AMD_HPP && OP != X265AMD_HPS)) \
+            hipLaunchKernelGGL((k_interp<P, S, D, OP, TAPS, UW, UH>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, g); \
+        return (int)hipGetLastError(); \
     }
-    if (w % 4 == 0)
-    {
-        if (rows % 4) L(4, 1);
-        L(4, 4);
-    }
-    if (w % 2 == 0)
-    {
-        if constexpr (TAPS == 4 || OP == X265AMD_P2S || OP == X265AMD_VPP || OP == X265AMD_VPS || OP == X265AMD_VSP || OP == X265AMD_VSS)
-        {
-            if (rows % 4) L(2, 1);
-            L(2, 4);
-        }
-    }
+    L(8, 4) L(8, 1) L(4, 4) L(4, 1) L(2, 4) L(2, 1)
 #undef L
     return X265AMD_EINVAL;
 }
 
-template <typename P, int TAPS>
-static int dispatch_interp(int op, int w, int h, int n, int depth, const void* src, intptr_t ss, const int64_t* soff,
-                           void* dst, intptr_t ds, const int64_t* doff, const uint8_t* coeff, int rowext, hipStream_t st)
+template <typename P, typename S, typename D, int OP, int TAPS>
+static int grouped_interp(int depth, int count, const x265amd_interp_batch* bt, hipStream_t st)
 {
-#define A w, h, n, depth, src, ss, soff, dst, ds, doff, coeff, rowext, st
+    std::vector<int> cls(count, -1);
+    for (int i = 0; i < count; i++)
+    {
+        if (bt[i].n < 0) return X265AMD_EINVAL;
+        if (bt[i].n == 0) continue;
+        if (OP == X265AMD_HVPP && !bt[i].coeff) return X265AMD_EINVAL;
+        cls[i] = interp_class<OP, TAPS>(bt[i].w, bt[i].h, bt[i].is_row_ext);
+        if (cls[i] < 0) return -cls[i];
+    }
+    BatchGroup proto{};
+    proto.depth = depth;
+    return launch_grouped(count, cls.data(), proto,
+        [&](int i, SubBatch& s) {
+            const x265amd_interp_batch& b = bt[i];
+            s = SubBatch{};
+            s.a = b.src; s.aoff = b.src_off; s.sa = b.src_stride;
+            s.d = b.dst; s.doff = b.dst_off; s.ds = b.dst_stride;
+            s.b = OP == X265AMD_P2S ? nullptr : b.coeff;
+            s.w = b.w; s.h = b.h; s.n = b.n;
+            s.param = OP == X265AMD_HPS ? b.is_row_ext : 0;
+            const int uw = cls[i] / 8, uh = cls[i] % 8;
+            if constexpr (OP == X265AMD_HVPP)
+                s.lg = hvpp_lg(b.w, b.h, uw, uh);
+            else
+            {
+                const int rows = (OP == X265AMD_HPS && s.param) ? b.h + TAPS - 1 : b.h;
+                s.lg = lanes_log2((b.w / uw) * (rows / uh));
+            }
+        },
+        [&](int c, const BatchGroup& g, uint32_t blocks) { return launch_interp<P, S, D, OP, TAPS>(c, g, blocks, st); });
+}
+
+template <typename P, int TAPS>
+static int dispatch_interp(int op, int depth, int count, const x265amd_interp_batch* bt, hipStream_t st)
+{
     switch (op)
     {
-    case X265AMD_HPP: return pick_unit<P, P, P, X265AMD_HPP, TAPS>(A);
-    case X265AMD_HPS: return pick_unit<P, P, int16_t, X265AMD_HPS, TAPS>(A);
-    case X265AMD_VPP: return pick_unit<P, P, P, X265AMD_VPP, TAPS>(A);
-    case X265AMD_VPS: return pick_unit<P, P, int16_t, X265AMD_VPS, TAPS>(A);
-    case X265AMD_VSP: return pick_unit<P, int16_t, P, X265AMD_VSP, TAPS>(A);
-    case X265AMD_VSS: return pick_unit<P, int16_t, int16_t, X265AMD_VSS, TAPS>(A);
+    case X265AMD_HPP: return grouped_interp<P, P, P, X265AMD_HPP, TAPS>(depth, count, bt, st);
+    case X265AMD_HPS: return grouped_interp<P, P, int16_t, X265AMD_HPS, TAPS>(depth, count, bt, st);
+    case X265AMD_VPP: return grouped_interp<P, P, P, X265AMD_VPP, TAPS>(depth, count, bt, st);
+    case X265AMD_VPS: return grouped_interp<P, P, int16_t, X265AMD_VPS, TAPS>(depth, count, bt, st);
+    case X265AMD_VSP: return grouped_interp<P, int16_t, P, X265AMD_VSP, TAPS>(depth, count, bt, st);
+    case X265AMD_VSS: return grouped_interp<P, int16_t, int16_t, X265AMD_VSS, TAPS>(depth, count, bt, st);
     case X265AMD_HVPP:
-        if constexpr (TAPS == 8) return launch_hvpp<P>(w, h, n, depth, src, ss, soff, dst, ds, doff, coeff, st);
+        if constexpr (TAPS == 8) return grouped_interp<P, P, P, X265AMD_HVPP, 8>(depth, count, bt, st);
+        return X265AMD_EINVAL;
+    case X265AMD_P2S:
+        if constexpr (TAPS == 4) return grouped_interp<P, P, int16_t, X265AMD_P2S, 4>(depth, count, bt, st);
         return X265AMD_EINVAL;
     }
-#undef A
     return X265AMD_EINVAL;
 }
 
@@ -422,24 +410,29 @@ static int dispatch_interp(int op, int w, int h, int n, int depth, const void* s
 
 using namespace x265amd;
 
+extern "C" int x265amd_interp_grouped(int op, int taps, int depth, int count, const x265amd_interp_batch* batches,
+                                      void* stream)
+{
+    if (count < 0 || (count > 0 && !batches)) return X265AMD_EINVAL;
+    hipStream_t st = (hipStream_t)stream;
+    const bool hbd = depth == 10 || depth == 12;
+    if (!hbd && depth != 8) return X265AMD_EINVAL;
+    if (op == X265AMD_P2S) taps = 4;        // taps ignored for p2s
+    if (taps == 8)
+        return hbd ? dispatch_interp<uint16_t, 8>(op, depth, count, batches, st)
+                   : dispatch_interp<uint8_t, 8>(op, depth, count, batches, st);
+    if (taps == 4)
+        return hbd ? dispatch_interp<uint16_t, 4>(op, depth, count, batches, st)
+                   : dispatch_interp<uint8_t, 4>(op, depth, count, batches, st);
+    return X265AMD_EINVAL;
+}
+
 extern "C" int x265amd_interp(int op, int taps, int depth, int w, int h, int n,
                               const void* src, intptr_t src_stride, const int64_t* src_off,
                               void* dst, intptr_t dst_stride, const int64_t* dst_off,
                               const uint8_t* coeff, int is_row_ext, void* stream)
 {
     if (n <= 0) return 0;
-    if (w < 2 || h < 2 || w > 64 || h > 64) return X265AMD_EINVAL;
-    hipStream_t st = (hipStream_t)stream;
-    const bool hbd = depth == 10 || depth == 12;
-    if (!hbd && depth != 8) return X265AMD_EINVAL;
-    if (op == X265AMD_P2S)
-        return hbd ? pick_unit<uint16_t, uint16_t, int16_t, X265AMD_P2S, 4>(w, h, n, depth, src, src_stride, src_off, dst, dst_stride, dst_off, nullptr, 0, st)
-                   : pick_unit<uint8_t, uint8_t, int16_t, X265AMD_P2S, 4>(w, h, n, depth, src, src_stride, src_off, dst, dst_stride, dst_off, nullptr, 0, st);
-    if (taps == 8)
-        return hbd ? dispatch_interp<uint16_t, 8>(op, w, h, n, depth, src, src_stride, src_off, dst, dst_stride, dst_off, coeff, is_row_ext, st)
-                   : dispatch_interp<uint8_t, 8>(op, w, h, n, depth, src, src_stride, src_off, dst, dst_stride, dst_off, coeff, is_row_ext, st);
-    if (taps == 4)
-        return hbd ? dispatch_interp<uint16_t, 4>(op, w, h, n, depth, src, src_stride, src_off, dst, dst_stride, dst_off, coeff, is_row_ext, st)
-                   : dispatch_interp<uint8_t, 4>(op, w, h, n, depth, src, src_stride, src_off, dst, dst_stride, dst_off, coeff, is_row_ext, st);
-    return X265AMD_EINVAL;
+    const x265amd_interp_batch bt = {w, h, n, is_row_ext, src, src_stride, src_off, dst, dst_stride, dst_off, coeff};
+    return x265amd_interp_grouped(op, taps, depth, 1, &bt, stream);
 }

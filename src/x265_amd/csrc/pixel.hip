@@ -18,6 +18,9 @@
 // iteration (8x4 / 4x4 strips for SAD/SSE/SATD, 8x8 / 16x16 for SA8D); the
 // group reduces with xor-shuffles.  8-bit SAD uses v_sad_u8 on packed dwords,
 // 10/12-bit v_sad_u16.
+#include <algorithm>
+#include <vector>
+
 #include "common.h"
 #include "../../../include/x265_amd.h"
 
@@ -250,26 +253,55 @@ __device__ __forceinline__ int psy_energy4(const P* a, intptr_t sa)
 }
 
 // -------------------------------------------------------------- kernels
+// (grouped launches, common.h: a = block A, b = block B, d = out)
 
 template <int OP, typename P, int UW, int UH>
-__global__ __launch_bounds__(X265AMD_BLOCK) void k_pixelcmp(int w, int h, int n, int lg,
-    const P* __restrict__ a, intptr_t sa, const int64_t* __restrict__ aoff,
-    const P* __restrict__ b, intptr_t sb, const int64_t* __restrict__ boff,
-    void* __restrict__ out, int wrap32)
+__global__ __launch_bounds__(X265AMD_BLOCK) void k_pixelcmp(const BatchGroup g)
 {
+    const uint32_t gb = xcd_block();
+    const SubBatch& sub = group_sub(g, gb);
+    const int w = sub.w, h = sub.h, n = sub.n, lg = sub.lg, wrap32 = g.flag;
+    const intptr_t sa = sub.sa, sb = sub.sb;
     const int G = 1 << lg;
-    const uint32_t lb = xcd_block();
+    const uint32_t lb = gb - sub.block0;
     const int64_t job = (int64_t)lb * (X265AMD_BLOCK >> lg) + (threadIdx.x >> lg);
     const int lane = threadIdx.x & (G - 1);
     const bool live = job < n;
     const int64_t jj = live ? job : 0;
+    void* __restrict__ out = sub.d;
 
-    const P* pa = a + aoff[jj];
-    const P* pb = (OP == X265AMD_SSD_S || OP == X265AMD_VAR) ? nullptr : b + boff[jj];
+    const P* pa = (const P*)sub.a + sub.aoff[jj];
+    const P* pb = (OP == X265AMD_SSD_S || OP == X265AMD_VAR) ? nullptr : (const P*)sub.b + sub.boff[jj];
     const int ux = w / UW, units = ux * (h / UH);
 
     uint64_t acc = 0;
-    if (live)
+    if constexpr (OP == X265AMD_SA8D && UW == 16)
+    {
+        // sa8d16: one (raw+2)>>2 per 16x16, computed as a quad of 8x8
+        // Hadamards on 4 adjacent lanes (lane&3 = quadrant) whose raw sums meet
+        // by shuffle — a quarter of the registers of a whole-16x16 lane.
+        // G >= 4 and a multiple of 4, so quads never straddle groups.
+        (void)units;
+        const int qx16 = w >> 4, units8 = qx16 * (h >> 4) * 4;
+        if (live)
+        {
+            for (int u0 = 0; u0 < units8; u0 += G)
+            {
+                const int u = u0 + lane;
+                uint32_t r = 0;
+                if (u < units8)
+                {
+                    const int q = u >> 2, k = u & 3;
+                    const int x = (q % qx16) * 16 + (k & 1) * 8, y = (q / qx16) * 16 + (k >> 1) * 8;
+                    r = raw_sa8d<P>(pa + y * sa + x, sa, pb + y * sb + x, sb);
+                }
+                r += __shfl_xor(r, 1, 64);
+                r += __shfl_xor(r, 2, 64);
+                if ((lane & 3) == 0) acc += (r + 2) >> 2;
+            }
+        }
+    }
+    else if (live)
     {
         for (int u = lane; u < units; u += G)
         {
@@ -280,18 +312,7 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_pixelcmp(int w, int h, int n,
             else if constexpr (OP == X265AMD_SATD)
                 acc += unit_satd<P, UW>(qa, sa, pb + y * sb + x, sb);
             else if constexpr (OP == X265AMD_SA8D)
-            {
-                const P* qb = pb + y * sb + x;
-                if constexpr (UW == 8)
-                    acc += (raw_sa8d<P>(qa, sa, qb, sb) + 2) >> 2;
-                else
-                {
-                    uint32_t r = raw_sa8d<P>(qa, sa, qb, sb) + raw_sa8d<P>(qa + 8, sa, qb + 8, sb)
-                               + raw_sa8d<P>(qa + 8 * sa, sa, qb + 8 * sb, sb)
-                               + raw_sa8d<P>(qa + 8 * sa + 8, sa, qb + 8 * sb + 8, sb);
-                    acc += (r + 2) >> 2;
-                }
-            }
+                acc += (raw_sa8d<P>(qa, sa, pb + y * sb + x, sb) + 2) >> 2;
             else if constexpr (OP == X265AMD_SSE_PP)
                 acc += unit_sse<P, UW, UH, false>(qa, sa, pb + y * sb + x, sb);
             else if constexpr (OP == X265AMD_SSE_SS)
@@ -337,22 +358,24 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_pixelcmp(int w, int h, int n,
 }
 
 template <typename P, int NREF, int UW, int UH>
-__global__ __launch_bounds__(X265AMD_BLOCK) void k_sad_multi(int w, int h, int n, int lg,
-    const P* __restrict__ fenc, intptr_t fs, const int64_t* __restrict__ foff,
-    const P* __restrict__ ref, intptr_t rs, const int64_t* __restrict__ roff,
-    int32_t* __restrict__ out)
+__global__ __launch_bounds__(X265AMD_BLOCK) void k_sad_multi(const BatchGroup g)
 {
+    const uint32_t gb = xcd_block();
+    const SubBatch& sub = group_sub(g, gb);
+    const int w = sub.w, h = sub.h, n = sub.n, lg = sub.lg;
+    const intptr_t fs = sub.sa, rs = sub.sb;
     const int G = 1 << lg;
-    const uint32_t lb = xcd_block();
+    const uint32_t lb = gb - sub.block0;
     const int64_t job = (int64_t)lb * (X265AMD_BLOCK >> lg) + (threadIdx.x >> lg);
     const int lane = threadIdx.x & (G - 1);
     const bool live = job < n;
     const int64_t jj = live ? job : 0;
+    int32_t* __restrict__ out = (int32_t*)sub.d;
 
-    const P* pf = fenc + foff[jj];
+    const P* pf = (const P*)sub.a + sub.aoff[jj];
     const P* pr[NREF];
 #pragma unroll
-    for (int k = 0; k < NREF; k++) pr[k] = ref + roff[jj * NREF + k];
+    for (int k = 0; k < NREF; k++) pr[k] = (const P*)sub.b + sub.boff[jj * NREF + k];
     const int ux = w / UW, units = ux * (h / UH);
 
     uint32_t acc[NREF];
@@ -384,95 +407,147 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_sad_multi(int w, int h, int n
 
 // -------------------------------------------------------------- dispatch
 
-static inline int grid_for(int n, int lg)
+// kernel class of a batch: (op, unit width, unit height) packed in an int
+static inline int cmp_pack(int op, int uw, int uh) { return (op << 16) | (uw << 8) | uh; }
+
+static int cmp_class(int op, int w, int h)
 {
-    const int per = X265AMD_BLOCK >> lg;
-    return (n + per - 1) / per;
+    if ((w % 4) || (h % 4) || w > 64 || h > 64 || w < 4 || h < 4) return -X265AMD_EINVAL;
+    const int uwd = (w % 8) ? 4 : 8;
+    switch (op)
+    {
+    case X265AMD_SAD: case X265AMD_SATD: case X265AMD_SSE_PP: case X265AMD_SSE_SS:
+    case X265AMD_SSD_S: case X265AMD_VAR:
+        return cmp_pack(op, uwd, 4);
+    case X265AMD_SA8D:
+        if ((w % 16) == 0 && (h % 16) == 0) return cmp_pack(op, 16, 16);
+        if ((w % 8) == 0 && (h % 8) == 0) return cmp_pack(op, 8, 8);
+        return cmp_pack(X265AMD_SATD, uwd, 4);  // 4x4 / 4x8 sa8d entries are satd (primitives.cpp:106,164-171)
+    case X265AMD_PSY:
+        if (w != h) return -X265AMD_EINVAL;
+        return w == 4 ? cmp_pack(op, 4, 4) : cmp_pack(op, 8, 8);
+    }
+    return -X265AMD_EINVAL;
+}
+
+static int cmp_lg(int cls, int w, int h)
+{
+    const int op = cls >> 16, uw = (cls >> 8) & 0xff, uh = cls & 0xff;
+    if (op == X265AMD_SA8D && uw == 16)      // quads of 8x8 lanes, G >= 4
+        return std::max(2, lanes_log2((w / 8) * (h / 8)));
+    return lanes_log2((w / uw) * (h / uh));
 }
 
 template <int OP, typename P, int UW, int UH>
-static int launch_cmp(int w, int h, int n, const void* a, intptr_t sa, const int64_t* aoff,
-                      const void* b, intptr_t sb, const int64_t* boff, void* out, hipStream_t st,
-                      int wrap32)
+static int launch_cmp(const BatchGroup& g, uint32_t blocks, hipStream_t st)
 {
-    // two units per lane: small blocks get one lane per job (all row loads of
-    // the job in flight from one lane), large blocks up to a full wavefront
-    const int units = (w / UW) * (h / UH);
-    int g = pow2ceil((units + 1) / 2);
-    if (g > 64) g = 64;
-    int lg = 0;
-    while ((1 << lg) < g) lg++;
-    hipLaunchKernelGGL((k_pixelcmp<OP, P, UW, UH>), dim3(grid_for(n, lg)), dim3(X265AMD_BLOCK), 0, st,
-                       w, h, n, lg, (const P*)a, sa, aoff, (const P*)b, sb, boff, out, wrap32);
+    hipLaunchKernelGGL((k_pixelcmp<OP, P, UW, UH>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, g);
     return (int)hipGetLastError();
 }
 
 template <typename P>
-static int dispatch_cmp(int op, int w, int h, int n, const void* a, intptr_t sa, const int64_t* aoff,
-                        const void* b, intptr_t sb, const int64_t* boff, void* out, hipStream_t st)
+static int launch_cmp_class(int cls, const BatchGroup& g, uint32_t blocks, hipStream_t st)
 {
-    const int wrap32 = sizeof(P) == 1;
-    const bool w8 = (w % 8) == 0;
-    if ((w % 4) || (h % 4) || w > 64 || h > 64 || w < 4 || h < 4) return X265AMD_EINVAL;
-    switch (op)
-    {
-    case X265AMD_SAD:
-        return w8 ? launch_cmp<X265AMD_SAD, P, 8, 4>(w, h, n, a, sa, aoff, b, sb, boff, out, st, wrap32)
-                  : launch_cmp<X265AMD_SAD, P, 4, 4>(w, h, n, a, sa, aoff, b, sb, boff, out, st, wrap32);
-    case X265AMD_SATD:
-        return w8 ? launch_cmp<X265AMD_SATD, P, 8, 4>(w, h, n, a, sa, aoff, b, sb, boff, out, st, wrap32)
-                  : launch_cmp<X265AMD_SATD, P, 4, 4>(w, h, n, a, sa, aoff, b, sb, boff, out, st, wrap32);
-    case X265AMD_SA8D:
-        if ((w % 16) == 0 && (h % 16) == 0)
-            return launch_cmp<X265AMD_SA8D, P, 16, 16>(w, h, n, a, sa, aoff, b, sb, boff, out, st, wrap32);
-        if ((w % 8) == 0 && (h % 8) == 0)
-            return launch_cmp<X265AMD_SA8D, P, 8, 8>(w, h, n, a, sa, aoff, b, sb, boff, out, st, wrap32);
-        // 4x4 / 4x8 entries of the sa8d tables are satd (primitives.cpp:106,164-171)
-        return w8 ? launch_cmp<X265AMD_SATD, P, 8, 4>(w, h, n, a, sa, aoff, b, sb, boff, out, st, wrap32)
-                  : launch_cmp<X265AMD_SATD, P, 4, 4>(w, h, n, a, sa, aoff, b, sb, boff, out, st, wrap32);
-    case X265AMD_SSE_PP:
-        return w8 ? launch_cmp<X265AMD_SSE_PP, P, 8, 4>(w, h, n, a, sa, aoff, b, sb, boff, out, st, wrap32)
-                  : launch_cmp<X265AMD_SSE_PP, P, 4, 4>(w, h, n, a, sa, aoff, b, sb, boff, out, st, wrap32);
-    case X265AMD_SSE_SS:
-        return w8 ? launch_cmp<X265AMD_SSE_SS, int16_t, 8, 4>(w, h, n, a, sa, aoff, b, sb, boff, out, st, wrap32)
-                  : launch_cmp<X265AMD_SSE_SS, int16_t, 4, 4>(w, h, n, a, sa, aoff, b, sb, boff, out, st, wrap32);
-    case X265AMD_PSY:
-        if (w != h) return X265AMD_EINVAL;
-        return w == 4 ? launch_cmp<X265AMD_PSY, P, 4, 4>(w, h, n, a, sa, aoff, b, sb, boff, out, st, wrap32)
-                      : launch_cmp<X265AMD_PSY, P, 8, 8>(w, h, n, a, sa, aoff, b, sb, boff, out, st, wrap32);
-    case X265AMD_SSD_S:
-        return w8 ? launch_cmp<X265AMD_SSD_S, int16_t, 8, 4>(w, h, n, a, sa, aoff, b, sb, boff, out, st, wrap32)
-                  : launch_cmp<X265AMD_SSD_S, int16_t, 4, 4>(w, h, n, a, sa, aoff, b, sb, boff, out, st, wrap32);
-    case X265AMD_VAR:
-        return w8 ? launch_cmp<X265AMD_VAR, P, 8, 4>(w, h, n, a, sa, aoff, b, sb, boff, out, st, wrap32)
-                  : launch_cmp<X265AMD_VAR, P, 4, 4>(w, h, n, a, sa, aoff, b, sb, boff, out, st, wrap32);
-    }
+    using S = int16_t;
+#define X265AMD_CMP(OPX, PX, W, H) \
+    if (cls == cmp_pack(OPX, W, H)) return launch_cmp<OPX, PX, W, H>(g, blocks, st);
+    X265AMD_CMP(X265AMD_SAD, P, 8, 4)     X265AMD_CMP(X265AMD_SAD, P, 4, 4)
+    X265AMD_CMP(X265AMD_SATD, P, 8, 4)    X265AMD_CMP(X265AMD_SATD, P, 4, 4)
+    X265AMD_CMP(X265AMD_SA8D, P, 16, 16)  X265AMD_CMP(X265AMD_SA8D, P, 8, 8)
+    X265AMD_CMP(X265AMD_SSE_PP, P, 8, 4)  X265AMD_CMP(X265AMD_SSE_PP, P, 4, 4)
+    X265AMD_CMP(X265AMD_SSE_SS, S, 8, 4)  X265AMD_CMP(X265AMD_SSE_SS, S, 4, 4)
+    X265AMD_CMP(X265AMD_PSY, P, 4, 4)     X265AMD_CMP(X265AMD_PSY, P, 8, 8)
+    X265AMD_CMP(X265AMD_SSD_S, S, 8, 4)   X265AMD_CMP(X265AMD_SSD_S, S, 4, 4)
+    X265AMD_CMP(X265AMD_VAR, P, 8, 4)     X265AMD_CMP(X265AMD_VAR, P, 4, 4)
+#undef X265AMD_CMP
     return X265AMD_EINVAL;
 }
 
-template <typename P, int NREF>
-static int dispatch_multi(int w, int h, int n, const void* f, intptr_t fs, const int64_t* foff,
-                          const void* r, intptr_t rs, const int64_t* roff, int32_t* out, hipStream_t st)
+static int cmp_classes(int count, const x265amd_cmp_batch* bt, std::vector<int>& cls,
+                       int (*classify)(int, int, int), int op)
 {
-    if ((w % 4) || (h % 4) || w > 64 || h > 64) return X265AMD_EINVAL;
-    const bool w8 = (w % 8) == 0;
-    const int units = (w / (w8 ? 8 : 4)) * (h / 4);
-    int g = pow2ceil((units + 1) / 2);
-    if (g > 64) g = 64;
-    int lg = 0;
-    while ((1 << lg) < g) lg++;
-    if (w8)
-        hipLaunchKernelGGL((k_sad_multi<P, NREF, 8, 4>), dim3(grid_for(n, lg)), dim3(X265AMD_BLOCK), 0, st,
-                           w, h, n, lg, (const P*)f, fs, foff, (const P*)r, rs, roff, out);
-    else
-        hipLaunchKernelGGL((k_sad_multi<P, NREF, 4, 4>), dim3(grid_for(n, lg)), dim3(X265AMD_BLOCK), 0, st,
-                           w, h, n, lg, (const P*)f, fs, foff, (const P*)r, rs, roff, out);
-    return (int)hipGetLastError();
+    cls.assign(count, -1);
+    for (int i = 0; i < count; i++)
+    {
+        if (bt[i].n < 0) return X265AMD_EINVAL;
+        if (bt[i].n == 0) continue;
+        const int c = classify(op, bt[i].w, bt[i].h);
+        if (c < 0) return -c;
+        cls[i] = c;
+    }
+    return 0;
+}
+
+static void cmp_fill(const x265amd_cmp_batch& b, int cls, SubBatch& s)
+{
+    s = SubBatch{};
+    s.a = b.a; s.aoff = b.a_off; s.sa = b.a_stride;
+    s.b = b.b; s.boff = b.b_off; s.sb = b.b_stride;
+    s.d = b.out;
+    s.w = b.w; s.h = b.h; s.n = b.n;
+    s.lg = cmp_lg(cls, b.w, b.h);
+}
+
+template <typename P>
+static int dispatch_cmp(int op, int count, const x265amd_cmp_batch* bt, hipStream_t st)
+{
+    std::vector<int> cls;
+    if (int rc = cmp_classes(count, bt, cls, cmp_class, op)) return rc;
+    BatchGroup proto{};
+    proto.flag = sizeof(P) == 1;   // sse_t is uint32 at 8-bit
+    return launch_grouped(count, cls.data(), proto,
+        [&](int i, SubBatch& s) { cmp_fill(bt[i], cls[i], s); },
+        [&](int c, const BatchGroup& g, uint32_t blocks) { return launch_cmp_class<P>(c, g, blocks, st); });
+}
+
+static int sad_multi_class(int, int w, int h)
+{
+    if ((w % 4) || (h % 4) || w > 64 || h > 64 || w < 4 || h < 4) return -X265AMD_EINVAL;
+    return cmp_pack(X265AMD_SAD, (w % 8) ? 4 : 8, 4);
+}
+
+template <typename P, int NREF>
+static int dispatch_multi(int count, const x265amd_cmp_batch* bt, hipStream_t st)
+{
+    std::vector<int> cls;
+    if (int rc = cmp_classes(count, bt, cls, sad_multi_class, 0)) return rc;
+    return launch_grouped(count, cls.data(), BatchGroup{},
+        [&](int i, SubBatch& s) { cmp_fill(bt[i], cls[i], s); },
+        [&](int c, const BatchGroup& g, uint32_t blocks) {
+            if (((c >> 8) & 0xff) == 8)
+                hipLaunchKernelGGL((k_sad_multi<P, NREF, 8, 4>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, g);
+            else
+                hipLaunchKernelGGL((k_sad_multi<P, NREF, 4, 4>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, g);
+            return (int)hipGetLastError();
+        });
 }
 
 } // namespace x265amd
 
 using namespace x265amd;
+
+extern "C" int x265amd_pixelcmp_grouped(int op, int depth, int count, const x265amd_cmp_batch* batches,
+                                        void* stream)
+{
+    if (count < 0 || (count > 0 && !batches)) return X265AMD_EINVAL;
+    hipStream_t st = (hipStream_t)stream;
+    if (depth == 8) return dispatch_cmp<uint8_t>(op, count, batches, st);
+    if (depth == 10 || depth == 12) return dispatch_cmp<uint16_t>(op, count, batches, st);
+    return X265AMD_EINVAL;
+}
+
+extern "C" int x265amd_sad_multi_grouped(int nref, int depth, int count, const x265amd_cmp_batch* batches,
+                                         void* stream)
+{
+    if (count < 0 || (count > 0 && !batches)) return X265AMD_EINVAL;
+    hipStream_t st = (hipStream_t)stream;
+    if (nref != 3 && nref != 4) return X265AMD_EINVAL;
+    if (depth == 8)
+        return nref == 3 ? dispatch_multi<uint8_t, 3>(count, batches, st) : dispatch_multi<uint8_t, 4>(count, batches, st);
+    if (depth == 10 || depth == 12)
+        return nref == 3 ? dispatch_multi<uint16_t, 3>(count, batches, st) : dispatch_multi<uint16_t, 4>(count, batches, st);
+    return X265AMD_EINVAL;
+}
 
 extern "C" int x265amd_pixelcmp(int op, int depth, int w, int h, int n,
                                 const void* a, intptr_t a_stride, const int64_t* a_off,
@@ -480,12 +555,8 @@ extern "C" int x265amd_pixelcmp(int op, int depth, int w, int h, int n,
                                 void* out, void* stream)
 {
     if (n <= 0) return 0;
-    hipStream_t st = (hipStream_t)stream;
-    if (depth == 8)
-        return dispatch_cmp<uint8_t>(op, w, h, n, a, a_stride, a_off, b, b_stride, b_off, out, st);
-    if (depth == 10 || depth == 12)
-        return dispatch_cmp<uint16_t>(op, w, h, n, a, a_stride, a_off, b, b_stride, b_off, out, st);
-    return X265AMD_EINVAL;
+    const x265amd_cmp_batch bt = {w, h, n, a, a_stride, a_off, b, b_stride, b_off, out};
+    return x265amd_pixelcmp_grouped(op, depth, 1, &bt, stream);
 }
 
 extern "C" int x265amd_sad_multi(int nref, int depth, int w, int h, int n,
@@ -494,13 +565,6 @@ extern "C" int x265amd_sad_multi(int nref, int depth, int w, int h, int n,
                                  int32_t* out, void* stream)
 {
     if (n <= 0) return 0;
-    hipStream_t st = (hipStream_t)stream;
-    if (nref != 3 && nref != 4) return X265AMD_EINVAL;
-    if (depth == 8)
-        return nref == 3 ? dispatch_multi<uint8_t, 3>(w, h, n, fenc, fenc_stride, fenc_off, ref, ref_stride, ref_off, out, st)
-                         : dispatch_multi<uint8_t, 4>(w, h, n, fenc, fenc_stride, fenc_off, ref, ref_stride, ref_off, out, st);
-    if (depth == 10 || depth == 12)
-        return nref == 3 ? dispatch_multi<uint16_t, 3>(w, h, n, fenc, fenc_stride, fenc_off, ref, ref_stride, ref_off, out, st)
-                         : dispatch_multi<uint16_t, 4>(w, h, n, fenc, fenc_stride, fenc_off, ref, ref_stride, ref_off, out, st);
-    return X265AMD_EINVAL;
+    const x265amd_cmp_batch bt = {w, h, n, fenc, fenc_stride, fenc_off, ref, ref_stride, ref_off, out};
+    return x265amd_sad_multi_grouped(nref, depth, 1, &bt, stream);
 }

@@ -19,6 +19,53 @@ class X265AmdError(RuntimeError):
     pass
 
 
+# descriptors of the grouped entry points (include/x265_amd.h)
+class CmpBatch(C.Structure):
+    _fields_ = [("w", _int), ("h", _int), ("n", _int), ("a", _vp), ("a_stride", _ip), ("a_off", _vp),
+                ("b", _vp), ("b_stride", _ip), ("b_off", _vp), ("out", _vp)]
+
+
+class BlockBatch(C.Structure):
+    _fields_ = [("w", _int), ("h", _int), ("n", _int), ("param", _int), ("dst", _vp), ("dst_stride", _ip),
+                ("dst_off", _vp), ("a", _vp), ("a_stride", _ip), ("a_off", _vp), ("b", _vp), ("b_stride", _ip),
+                ("b_off", _vp)]
+
+
+class InterpBatch(C.Structure):
+    _fields_ = [("w", _int), ("h", _int), ("n", _int), ("is_row_ext", _int), ("src", _vp), ("src_stride", _ip),
+                ("src_off", _vp), ("dst", _vp), ("dst_stride", _ip), ("dst_off", _vp), ("coeff", _vp)]
+
+
+def _addr(t):
+    return None if t is None else t.data_ptr()
+
+
+def cmp_batches(items):
+    """items: (w, h, a, sa, aoff, b, sb, boff, out) with torch tensors -> CmpBatch array"""
+    arr = (CmpBatch * len(items))()
+    for i, (w, h, a, sa, aoff, b, sb, boff, out) in enumerate(items):
+        arr[i] = CmpBatch(w, h, aoff.numel(), _addr(a), sa, _addr(aoff), _addr(b), sb, _addr(boff), _addr(out))
+    return arr
+
+
+def block_batches(items):
+    """items: (w, h, param, d, ds, doff, a, sa, aoff, b, sb, boff) -> BlockBatch array"""
+    arr = (BlockBatch * len(items))()
+    for i, (w, h, param, d, ds, doff, a, sa, aoff, b, sb, boff) in enumerate(items):
+        arr[i] = BlockBatch(w, h, doff.numel(), int(param), _addr(d), ds, _addr(doff), _addr(a), sa, _addr(aoff),
+                            _addr(b), sb, _addr(boff))
+    return arr
+
+
+def interp_batches(items):
+    """items: (w, h, rowext, s, ss, soff, d, ds, doff, coeff) -> InterpBatch array"""
+    arr = (InterpBatch * len(items))()
+    for i, (w, h, rowext, s, ss, soff, d, ds, doff, coeff) in enumerate(items):
+        arr[i] = InterpBatch(w, h, soff.numel(), int(rowext), _addr(s), ss, _addr(soff), _addr(d), ds, _addr(doff),
+                             _addr(coeff))
+    return arr
+
+
 def _ptr(t):
     if t is None:
         return None
@@ -113,6 +160,23 @@ class Primitives:
         self._check(self.lib.x265amd_blockop(op, depth, w, h, doff.numel(), _ptr(d), _ip(ds), _ptr(doff), _ptr(a),
                                              _ip(sa), _ptr(aoff), _ptr(b), _ip(sb), _ptr(boff), int(param),
                                              stream or _stream()), "blockop")
+
+    # -- grouped forms: `arr` from cmp_batches / block_batches / interp_batches
+    def pixelcmp_grouped(self, op, depth, arr, stream=None):
+        self._check(self.lib.x265amd_pixelcmp_grouped(op, depth, len(arr), arr, stream or _stream()),
+                    "pixelcmp_grouped")
+
+    def sad_multi_grouped(self, nref, depth, arr, stream=None):
+        self._check(self.lib.x265amd_sad_multi_grouped(nref, depth, len(arr), arr, stream or _stream()),
+                    "sad_multi_grouped")
+
+    def blockop_grouped(self, op, depth, arr, stream=None):
+        self._check(self.lib.x265amd_blockop_grouped(op, depth, len(arr), arr, stream or _stream()),
+                    "blockop_grouped")
+
+    def interp_grouped(self, op, taps, depth, arr, stream=None):
+        self._check(self.lib.x265amd_interp_grouped(op, taps, depth, len(arr), arr, stream or _stream()),
+                    "interp_grouped")
 
     def count_nonzero(self, size, c, co, r, rs, ro, cnt, stream=None):
         self._check(self.lib.x265amd_count_nonzero(size, co.numel(), _ptr(c), _ptr(co), _ptr(r), _ip(rs), _ptr(ro),

@@ -228,6 +228,105 @@ class Batch:
         return bad
 
 
+MAX_SUB = 16   # sub-batches per grouped launch (csrc/common.h kMaxSub)
+
+
+def launch_class(b: Batch):
+    """Kernel instantiation a batch runs in (mirrors cmp_class / blockop_class /
+    interp_class in csrc/): batches with equal keys share one grouped launch.
+    None for kinds that are not grouped."""
+    w, h = b.w, b.h
+    if b.kind == "pixelcmp":
+        uwd = 4 if w % 8 else 8
+        if b.op == SA8D:
+            cls = (16, 16) if w % 16 == 0 and h % 16 == 0 else (8, 8) if w % 8 == 0 and h % 8 == 0 else ("satd", uwd)
+        elif b.op == PSY:
+            cls = 4 if w == 4 else 8
+        else:
+            cls = uwd
+        return ("pixelcmp", b.op, b.depth, cls)
+    if b.kind == "sad_multi":
+        return ("sad_multi", b.op, b.depth, 4 if w % 8 else 8)
+    if b.kind == "blockop":
+        return ("blockop", b.op, b.depth, 8 if w % 8 == 0 else 4 if w % 4 == 0 else 2, 4 if h % 4 == 0 else 1)
+    if b.kind == "interp":
+        taps = 4 if b.op == P2S else b.taps
+        rows = h + taps - 1 if b.op == HPS and b.params.get("rowext", 0) else h
+        if b.op == HVPP:
+            rows = h
+        return ("interp", b.op, taps, b.depth, 8 if w % 8 == 0 else 4 if w % 4 == 0 else 2, 4 if rows % 4 == 0 else 1)
+    return None
+
+
+class LaunchGroup:
+    """Up to MAX_SUB batches of one kernel class issued as ONE grouped launch
+    (x265amd_*_grouped).  Each member keeps its own operands and outputs, so
+    verification stays per member batch."""
+
+    def __init__(self, members: list):
+        self.members = members
+        b0 = members[0]
+        self.kind, self.op, self.depth, self.taps = b0.kind, b0.op, b0.depth, b0.taps
+        self.n = sum(b.n for b in members)
+        self.bytes = sum(b.bytes for b in members)
+        self.name = "grp[" + "+".join(b.name for b in members) + "]" if len(members) > 1 else b0.name
+        self._arr = None
+
+    def _descriptors(self):
+        from . import native as nv
+
+        items = []
+        for b in self.members:
+            d, p = b.dev, b.params
+            if self.kind == "pixelcmp":
+                items.append((b.w, b.h, d["a"], p["sa"], d["aoff"], d.get("b"), p.get("sb", 0),
+                              d.get("boff", d["aoff"]), d["out"]))
+            elif self.kind == "sad_multi":
+                items.append((b.w, b.h, d["f"], p["fs"], d["foff"], d["r"], p["rs"], d["roff"], d["out"]))
+            elif self.kind == "blockop":
+                items.append((b.w, b.h, p.get("param", 0), d["d"], p["ds"], d["doff"], d.get("a"), p.get("sa", 0),
+                              d.get("aoff"), d.get("b"), p.get("sb", 0), d.get("boff")))
+            else:
+                items.append((b.w, b.h, p.get("rowext", 0), d["s"], p["ss"], d["soff"], d["d"], p["ds"], d["doff"],
+                              d.get("coeff")))
+        make = {"pixelcmp": nv.cmp_batches, "sad_multi": nv.cmp_batches, "blockop": nv.block_batches,
+                "interp": nv.interp_batches}[self.kind]
+        return make(items)
+
+    def run(self, prims, stream=None):
+        if len(self.members) == 1:
+            return self.members[0].run(prims, stream)
+        if self._arr is None:
+            self._arr = self._descriptors()   # device addresses are fixed for the life of the batches
+        if self.kind == "pixelcmp":
+            prims.pixelcmp_grouped(self.op, self.depth, self._arr, stream)
+        elif self.kind == "sad_multi":
+            prims.sad_multi_grouped(self.op, self.depth, self._arr, stream)
+        elif self.kind == "blockop":
+            prims.blockop_grouped(self.op, self.depth, self._arr, stream)
+        else:
+            prims.interp_grouped(self.op, self.taps, self.depth, self._arr, stream)
+
+
+def group_launches(batches: list, max_sub: int = MAX_SUB) -> list:
+    """Pack batches of one kernel class into LaunchGroups of at most max_sub
+    members (largest first inside a class); other batches become groups of one.
+    Result is ordered by bytes, largest first."""
+    classes, out = {}, []
+    for b in batches:
+        key = launch_class(b)
+        if key is None:
+            out.append(LaunchGroup([b]))
+        else:
+            classes.setdefault(key, []).append(b)
+    for key, bs in classes.items():
+        bs = sorted(bs, key=lambda b: -b.bytes)
+        for i in range(0, len(bs), max_sub):
+            out.append(LaunchGroup(bs[i:i + max_sub]))
+    out.sort(key=lambda g: -g.bytes)
+    return out
+
+
 def _aligned(rng, lo, hi, align, n):
     return (rng.integers(lo // align, hi // align + 1, n) * align).astype(np.int64)
 

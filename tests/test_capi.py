@@ -29,7 +29,7 @@ def test_library_metadata(native_lib):
     lib = ctypes.CDLL(native_lib)
     lib.x265amd_target.restype = ctypes.c_char_p
     lib.x265amd_strerror.restype = ctypes.c_char_p
-    assert lib.x265amd_abi_version() == 1
+    assert lib.x265amd_abi_version() == 2
     assert lib.x265amd_target() == b"gfx950"
     assert b"unsupported" in lib.x265amd_strerror(1000)
 
@@ -44,3 +44,28 @@ def test_invalid_shapes_rejected_without_launch(native_lib):
     assert lib.x265amd_quant(1, 20, None, None, None, None, None, None, None, None, None, None, None, None) == 1000
     # n == 0 is a no-op
     assert lib.x265amd_interp(0, 8, 8, 8, 8, 0, None, 0, None, None, 0, None, None, 0, None) == 0
+
+
+def test_grouped_entries_reject_whole_call_without_launch(native_lib):
+    """A grouped call with one invalid batch enqueues nothing and returns EINVAL."""
+    import sys
+
+    sys.path.insert(0, ROOT)
+    from src.x265_amd.native import BlockBatch, CmpBatch, InterpBatch
+
+    lib = ctypes.CDLL(native_lib)
+    cmp = (CmpBatch * 3)(CmpBatch(8, 8, 1), CmpBatch(16, 16, 1), CmpBatch(6, 8, 1))   # 6x8: invalid
+    assert lib.x265amd_pixelcmp_grouped(0, 8, 3, cmp) == 1000
+    assert lib.x265amd_sad_multi_grouped(4, 8, 3, cmp) == 1000
+    assert lib.x265amd_sad_multi_grouped(5, 8, 1, cmp) == 1000                           # nref
+    psy = (CmpBatch * 1)(CmpBatch(8, 16, 1))                                              # psy needs w == h
+    assert lib.x265amd_pixelcmp_grouped(5, 8, 1, psy) == 1000
+    blk = (BlockBatch * 2)(BlockBatch(8, 8, 1), BlockBatch(3, 8, 1))                     # odd width
+    assert lib.x265amd_blockop_grouped(4, 8, 2, blk) == 1000
+    itp = (InterpBatch * 2)(InterpBatch(8, 8, 1), InterpBatch(2, 8, 1))                   # 2-wide luma hpp
+    assert lib.x265amd_interp_grouped(0, 8, 8, 2, itp) == 1000
+    assert lib.x265amd_interp_grouped(6, 8, 8, 1, (InterpBatch * 1)(InterpBatch(8, 8, 1))) == 1000  # hvpp, no coeff
+    assert lib.x265amd_pixelcmp_grouped(0, 8, -1, None) == 1000
+    # empty batches / empty calls are no-ops
+    assert lib.x265amd_pixelcmp_grouped(0, 8, 0, None) == 0
+    assert lib.x265amd_blockop_grouped(4, 8, 1, (BlockBatch * 1)(BlockBatch(3, 8, 0))) == 0
