@@ -10,6 +10,8 @@
 //
 // Work mapping: one block per G-lane group, a lane handles UW (8/4/2)
 // contiguous elements of one row per step, loads and stores vectorised.
+#include <algorithm>
+
 #include "common.h"
 #include "../../../include/x265_amd.h"
 
@@ -114,26 +116,35 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_blockop(const BatchGroup g)
     }
 }
 
-// kernel class: unit width (8/4/2 elements) x unit height (4 rows when the
-// block allows, so several row loads are in flight per lane, else 1)
+// kernel class: unit width (8/4/2 elements) x unit height (1/2/4 rows) with
+// one unit per lane.  The unit height aims at ~32 bytes of loads per lane:
+// measured on MI355X (tools/kernel_roofline.py, 8x8 and 16x16 blocks), 8-16 B
+// per lane leaves the chip issuing index math and 64+ B serialises each lane's
+// loads; wide int16 operands (addAvg, add_ps) want one row, pixel-only copies four.
+template <typename P, int OP>
 static int blockop_class(int w, int h)
 {
     if (w < 2 || h < 1 || w > 64 || h > 64 || (w % 2)) return -X265AMD_EINVAL;
+    typedef typename OpTypes<P, OP>::a A;
+    typedef typename OpTypes<P, OP>::b B;
+    constexpr bool TWO = OP == X265AMD_SUB_PS || OP == X265AMD_ADD_PS || OP == X265AMD_ADDAVG || OP == X265AMD_PIXELAVG;
+    constexpr int esz = OP == X265AMD_BLOCKFILL ? 2 : (int)sizeof(A) + (TWO ? (int)sizeof(B) : 0);
     const int uw = (w % 8 == 0) ? 8 : (w % 4 == 0) ? 4 : 2;
-    const int uh = (h % 4 == 0) ? 4 : 1;
-    return uw * 8 + uh;
+    const int want = std::max(1, 32 / (uw * esz));
+    const int uh = (want >= 4 && h % 4 == 0) ? 4 : (want >= 2 && h % 2 == 0) ? 2 : 1;
+    return uw * 16 + uh;
 }
 
 template <typename P, int OP>
 static int launch_blockop(int cls, const BatchGroup& g, uint32_t blocks, hipStream_t st)
 {
 #define L(UW, UH) \
-    if (cls == UW * 8 + UH) \
+    if (cls == UW * 16 + UH) \
     { \
         hipLaunchKernelGGL((k_blockop<P, OP, UW, UH>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, g); \
         return (int)hipGetLastError(); \
     }
-    L(8, 4) L(4, 4) L(2, 4) L(8, 1) L(4, 1) L(2, 1)
+    L(8, 4) L(8, 2) L(8, 1) L(4, 4) L(4, 2) L(4, 1) L(2, 4) L(2, 2) L(2, 1)
 #undef L
     return X265AMD_EINVAL;
 }
@@ -146,7 +157,7 @@ static int grouped_blockop(int depth, int count, const x265amd_block_batch* bt, 
     {
         if (bt[i].n < 0) return X265AMD_EINVAL;
         if (bt[i].n == 0) continue;
-        cls[i] = blockop_class(bt[i].w, bt[i].h);
+        cls[i] = blockop_class<P, OP>(bt[i].w, bt[i].h);
         if (cls[i] < 0) return -cls[i];
     }
     BatchGroup proto{};
@@ -159,8 +170,8 @@ static int grouped_blockop(int depth, int count, const x265amd_block_batch* bt, 
             s.a = b.a; s.aoff = b.a_off; s.sa = b.a_stride;
             s.b = b.b; s.boff = b.b_off; s.sb = b.b_stride;
             s.w = b.w; s.h = b.h; s.n = b.n; s.param = b.param;
-            const int uw = cls[i] / 8, uh = cls[i] % 8;
-            s.lg = lanes_log2((b.w / uw) * (b.h / uh));
+            const int uw = cls[i] / 16, uh = cls[i] % 16;
+            s.lg = lanes_log2((b.w / uw) * (b.h / uh), 1);
         },
         [&](int c, const BatchGroup& g, uint32_t blocks) { return launch_blockop<P, OP>(c, g, blocks, st); });
 }

@@ -80,9 +80,9 @@ inline int pow2ceil(int v)
 // log2 of the lanes per job: two units per lane, so small blocks get one lane
 // per job (all of the job's row loads in flight from one lane) and large ones
 // up to a full wavefront
-inline int lanes_log2(int units)
+inline int lanes_log2(int units, int per_lane = 2)
 {
-    int g = pow2ceil((units + 1) / 2);
+    int g = pow2ceil((units + per_lane - 1) / per_lane);
     if (g > 64) g = 64;
     int lg = 0;
     while ((1 << lg) < g) lg++;
@@ -200,9 +200,24 @@ __device__ __forceinline__ int clip16(int v)
 template <typename P, int UW>
 __device__ __forceinline__ void load_row(const P* p, int (&o)[UW])
 {
-    if constexpr (sizeof(P) == 1)
+    if constexpr (UW == 16 && sizeof(P) == 2)
     {
-        if constexpr (UW == 8)
+        int lo[8], hi[8];
+        load_row<P, 8>(p, lo);
+        load_row<P, 8>(p + 8, hi);
+#pragma unroll
+        for (int i = 0; i < 8; i++) { o[i] = lo[i]; o[8 + i] = hi[i]; }
+    }
+    else if constexpr (sizeof(P) == 1)
+    {
+        if constexpr (UW == 16)
+        {
+            uint4 v = ldu<uint4>(p);
+            uint32_t w[4] = { v.x, v.y, v.z, v.w };
+#pragma unroll
+            for (int i = 0; i < 16; i++) o[i] = (int)((w[i >> 2] >> (8 * (i & 3))) & 0xff);
+        }
+        else if constexpr (UW == 8)
         {
             uint64_t v = ldu<uint64_t>(p);
 #pragma unroll
@@ -247,7 +262,15 @@ __device__ __forceinline__ void load_row(const P* p, int (&o)[UW])
 template <int UW>
 __device__ __forceinline__ void load_row16(const int16_t* p, int (&o)[UW])
 {
-    if constexpr (UW == 8)
+    if constexpr (UW == 16)
+    {
+        int lo[8], hi[8];
+        load_row16<8>(p, lo);
+        load_row16<8>(p + 8, hi);
+#pragma unroll
+        for (int i = 0; i < 8; i++) { o[i] = lo[i]; o[8 + i] = hi[i]; }
+    }
+    else if constexpr (UW == 8)
     {
         uint4 v = ldu<uint4>(p);
         uint32_t w[4] = { v.x, v.y, v.z, v.w };
@@ -270,7 +293,22 @@ __device__ __forceinline__ void load_row16(const int16_t* p, int (&o)[UW])
 template <typename P, int UW>
 __device__ __forceinline__ void store_row(P* p, const int (&v)[UW])
 {
-    if constexpr (sizeof(P) == 1 && UW == 8)
+    if constexpr (UW == 16 && sizeof(P) == 2)
+    {
+        int lo[8], hi[8];
+#pragma unroll
+        for (int i = 0; i < 8; i++) { lo[i] = v[i]; hi[i] = v[8 + i]; }
+        store_row<P, 8>(p, lo);
+        store_row<P, 8>(p + 8, hi);
+    }
+    else if constexpr (sizeof(P) == 1 && UW == 16)
+    {
+        uint32_t w[4] = { 0, 0, 0, 0 };
+#pragma unroll
+        for (int i = 0; i < 16; i++) w[i >> 2] |= (uint32_t)(v[i] & 0xff) << (8 * (i & 3));
+        stu<uint4>(p, make_uint4(w[0], w[1], w[2], w[3]));
+    }
+    else if constexpr (sizeof(P) == 1 && UW == 8)
     {
         uint64_t w = 0;
 #pragma unroll

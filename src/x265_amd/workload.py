@@ -248,7 +248,15 @@ def launch_class(b: Batch):
     if b.kind == "sad_multi":
         return ("sad_multi", b.op, b.depth, 4 if w % 8 else 8)
     if b.kind == "blockop":
-        return ("blockop", b.op, b.depth, 8 if w % 8 == 0 else 4 if w % 4 == 0 else 2, 4 if h % 4 == 0 else 1)
+        # csrc/blockops.hip blockop_class: ~32 loaded bytes per lane
+        p = 1 if b.depth == 8 else 2
+        a_b = {SUB_PS: (p, p), ADD_PS: (p, 2), ADDAVG: (2, 2), PIXELAVG: (p, p), COPY_SP: (2, 0), COPY_SS: (2, 0),
+               BLOCKFILL: (2, 0), CPY2D1D_SHL: (2, 0), CPY2D1D_SHR: (2, 0), CPY1D2D_SHL: (2, 0),
+               CPY1D2D_SHR: (2, 0)}.get(b.op, (p, 0))
+        uw = 8 if w % 8 == 0 else 4 if w % 4 == 0 else 2
+        want = max(1, 32 // (uw * sum(a_b)))
+        uh = 4 if want >= 4 and h % 4 == 0 else 2 if want >= 2 and h % 2 == 0 else 1
+        return ("blockop", b.op, b.depth, uw, uh)
     if b.kind == "interp":
         taps = 4 if b.op == P2S else b.taps
         rows = h + taps - 1 if b.op == HPS and b.params.get("rowext", 0) else h

@@ -136,6 +136,33 @@ def main():
             ms = timeit(lambda: prims.interp(op, 8, 8, s, s, S, W, soff, D, s, doff, coeff))
             record(name, n * ((s + ext_w) * (s + ext_h) + s * s), ms, n)
             del S, soff, D, doff, coeff
+    # ---------------------------------------------------------------- block ops
+    # sources tiled in planes (as frame blocks), destinations in compact slots
+    # (as the bench's per-job output slots); (name, op, a int16?, b operand: None / "p" / "s", dst int16?)
+    for bname, op, a16, bkind, d16 in (("copy_pp", 4, False, None, False), ("pixelavg", 3, False, "p", False),
+                                       ("sub_ps", 0, False, "p", True), ("add_ps", 1, False, "s", False),
+                                       ("addavg", 2, True, "s", False)):
+        for s in (8, 16, 64):
+            name = f"{bname}_{s}x{s}"
+            if not want(name):
+                continue
+            esz_a, esz_d = (2 if a16 else 1), (2 if d16 else 1)
+            esz_b = 0 if bkind is None else (2 if bkind == "s" else 1)
+            n = int(a.gb * 1e9 / ((esz_a + esz_b + esz_d) * s * s))
+            x, y, rows = tiled_offsets(n, s, s, s, s, W)
+            mk = (lambda k: torch.randint(-2000, 2000, (k,), dtype=torch.int16, device=dev)) if a16 else rand_u8
+            A = mk(rows * W)
+            off = torch.from_numpy(y * W + x).to(dev)
+            B = None
+            if bkind == "p":
+                B = rand_u8(rows * W)
+            elif bkind == "s":
+                B = torch.randint(-2000, 2000, (rows * W,), dtype=torch.int16, device=dev)
+            D = torch.empty(n * s * s, dtype=torch.int16 if d16 else torch.uint8, device=dev)
+            doff = torch.arange(n, dtype=torch.int64, device=dev) * (s * s)
+            ms = timeit(lambda: prims.blockop(op, 8, s, s, D, s, doff, A, W, off, B, W, off if B is not None else None))
+            record(name, n * (esz_a + esz_b + esz_d) * s * s, ms, n)
+            del A, B, D, off, doff
     # ---------------------------------------------------------------- transforms
     for kind, kname in ((DCT, "dct"), (IDCT, "idct")):
         for s in (4, 8, 16, 32):
