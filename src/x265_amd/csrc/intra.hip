@@ -203,6 +203,167 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_intra_pred(int n, int maxv,
     }
 }
 
+// Small TUs (4x4, 8x8): one (TU, mode) job per LANE.  The whole 4N+1
+// neighbour array is loaded with vector loads and flipped in registers
+// (compile-time indices); planar, DC and the pure H/V modes never leave
+// registers.  Angular modes need data-dependent offsets, so the lane writes its
+// reference array to a private LDS column as PAIRS D[j] = (R[j], R[j+1]) of
+// u16: every angular pixel is then one ds_read_b32 and one v_dot2_u32_u16
+// against the row weights (32 - f, f):  ((32-f)·a + f·b + 16) >> 5.
+template <typename P, int N>
+__global__ __launch_bounds__(X265AMD_BLOCK) void k_intra_lane(int n, int maxv,
+    P* __restrict__ dst, intptr_t ds, const int64_t* __restrict__ doff,
+    const P* __restrict__ nb, const int64_t* __restrict__ nboff,
+    const P* __restrict__ filt, const int64_t* __restrict__ filtoff,
+    const uint8_t* __restrict__ mode, const uint8_t* __restrict__ bfilter, int allangs)
+{
+    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+    constexpr int N2 = 2 * N, NB = 4 * N + 1;
+    constexpr int LG2 = N == 4 ? 2 : 3;
+    __shared__ uint32_t D[3 * N][X265AMD_BLOCK];     // D[j + N][lane], j = -N .. 2N-1
+    const int64_t job = (int64_t)xcd_block() * X265AMD_BLOCK + threadIdx.x;
+    if (job >= n) return;
+
+    int m, bf;
+    const P* src;
+    P* out;
+    intptr_t os;
+    if (allangs)
+    {
+        const int64_t tu = job / 33;
+        m = 2 + (int)(job % 33);
+        bf = bfilter[tu];
+        src = (c_intra.filter_flags[m] & N) ? filt + filtoff[tu] : nb + nboff[tu];
+        out = dst + doff[tu] + (int64_t)(m - 2) * N * N;
+        os = N;
+    }
+    else
+    {
+        m = mode[job];
+        bf = bfilter[job];
+        src = nb + nboff[job];
+        out = dst + doff[job];
+        os = ds;
+    }
+    const ModeInfo mi = decode_mode(m);
+
+    // neighbours s[0 .. 4N] (vector loads), then the mode's frame s'
+    int s[NB];
+#pragma unroll
+    for (int i = 0; i + 16 <= NB; i += 16)
+    {
+        int t[16];
+        load_row<P, 16>(src + i, t);
+#pragma unroll
+        for (int k = 0; k < 16; k++) s[i + k] = t[k];
+    }
+    s[NB - 1] = src[NB - 1];
+    int R[3 * N + 1];                                // R[j + N], j = -N .. 2N
+    int L[N + 1];
+#pragma unroll
+    for (int k = 0; k < N - 1; k++) R[k] = 0;         // j < -1: projected samples (angle < 0) only
+#pragma unroll
+    for (int e = 0; e <= N2; e++)
+    {
+        const int fe = e == 0 ? 0 : e + N2;
+        R[N + e - 1] = mi.hor ? s[fe] : s[e];
+    }
+    R[3 * N] = 0;
+#pragma unroll
+    for (int y = 0; y <= N; y++)
+    {
+        const int e = N2 + 1 + y;
+        L[y] = mi.hor ? s[e - N2] : s[e];
+    }
+
+    int v[N][N];
+    if (m == 0)   // planar (intrapred.cpp:87-100)
+    {
+#pragma unroll
+        for (int y = 0; y < N; y++)
+#pragma unroll
+            for (int x = 0; x < N; x++)
+                v[y][x] = ((N - 1 - x) * L[y] + (N - 1 - y) * R[N + x] + (x + 1) * R[2 * N] + (y + 1) * L[N] + N)
+                          >> (LG2 + 1);
+    }
+    else if (m == 1)   // DC (+ dcPredFilter, intrapred.cpp:53-85)
+    {
+        int t = N;
+#pragma unroll
+        for (int i = 0; i < N; i++) t += R[N + i] + L[i];
+        const int dc = t >> (LG2 + 1);
+#pragma unroll
+        for (int y = 0; y < N; y++)
+#pragma unroll
+            for (int x = 0; x < N; x++) v[y][x] = dc;
+        if (bf)
+        {
+            v[0][0] = (R[N] + L[0] + 2 * dc + 2) >> 2;
+#pragma unroll
+            for (int x = 1; x < N; x++) v[0][x] = (R[N + x] + 3 * dc + 2) >> 2;
+#pragma unroll
+            for (int y = 1; y < N; y++) v[y][0] = (L[y] + 3 * dc + 2) >> 2;
+        }
+    }
+    else if (mi.angle == 0)   // pure vertical / horizontal (+ edge filter)
+    {
+#pragma unroll
+        for (int y = 0; y < N; y++)
+        {
+#pragma unroll
+            for (int x = 0; x < N; x++) v[y][x] = R[N + x];
+            if (bf)
+            {
+                const int t = (int16_t)(R[N] + ((L[y] - R[N - 1]) >> 1));
+                v[y][0] = t < 0 ? 0 : (t > maxv ? maxv : t);
+            }
+        }
+    }
+    else
+    {
+        if (mi.angle < 0)
+        {
+            // projected left samples R[-2-k] = L[i_k - 1], i_k = (128 + (k+1)·invAngle) >> 8
+            const int nproj = -((N * mi.angle) >> 5) - 1;
+#pragma unroll
+            for (int k = 0; k < N - 1; k++)
+            {
+                if (k < nproj)
+                {
+                    const int i = (128 + (k + 1) * mi.inv) >> 8;
+                    int p = L[0];
+#pragma unroll
+                    for (int q = 1; q < N; q++) p = i - 1 == q ? L[q] : p;
+                    R[N - 2 - k] = p;
+                }
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 3 * N; j++) D[j][threadIdx.x] = (uint32_t)R[j] | ((uint32_t)R[j + 1] << 16);
+#pragma unroll
+        for (int y = 0; y < N; y++)
+        {
+            const int sum = (y + 1) * mi.angle, off = sum >> 5, f = sum & 31;
+            const u16x2 wt = {(unsigned short)(32 - f), (unsigned short)f};
+            const uint32_t* row = &D[N + off][threadIdx.x];
+#pragma unroll
+            for (int x = 0; x < N; x++)
+                v[y][x] = (int)(__builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, row[x * X265AMD_BLOCK]), wt, 16u, false) >> 5);
+        }
+    }
+
+    // horizontal modes are transposed back, except in all-angles output
+    const bool tr = mi.hor && !allangs;
+#pragma unroll
+    for (int r = 0; r < N; r++)
+    {
+        int o[N];
+#pragma unroll
+        for (int c = 0; c < N; c++) o[c] = tr ? v[c][r] : v[r][c];
+        store_row<P, N>(out + (int64_t)r * os, o);
+    }
+}
+
 template <typename P>
 __global__ __launch_bounds__(X265AMD_BLOCK) void k_intra_filter(int N, int n, const P* __restrict__ src,
     const int64_t* __restrict__ soff, P* __restrict__ dst, const int64_t* __restrict__ doff)
@@ -229,16 +390,16 @@ static int launch_pred(int N, int n, int depth, void* dst, intptr_t ds, const in
                        const int64_t* nboff, const void* filt, const int64_t* filtoff, const uint8_t* mode,
                        const uint8_t* bfilter, int allangs, hipStream_t st)
 {
-    const int per = X265AMD_BLOCK / N;
+    const int per = N <= 8 ? X265AMD_BLOCK : X265AMD_BLOCK / N;    // lane per job up to 8x8
     const dim3 grid((n + per - 1) / per);
-#define L(NN) hipLaunchKernelGGL((k_intra_pred<P, NN>), grid, dim3(X265AMD_BLOCK), 0, st, n, (1 << depth) - 1, \
-                                 (P*)dst, ds, doff, (const P*)nb, nboff, (const P*)filt, filtoff, mode, bfilter, allangs)
+#define L(K, NN) hipLaunchKernelGGL((K<P, NN>), grid, dim3(X265AMD_BLOCK), 0, st, n, (1 << depth) - 1, \
+                                    (P*)dst, ds, doff, (const P*)nb, nboff, (const P*)filt, filtoff, mode, bfilter, allangs)
     switch (N)
     {
-    case 4: L(4); break;
-    case 8: L(8); break;
-    case 16: L(16); break;
-    case 32: L(32); break;
+    case 4: L(k_intra_lane, 4); break;
+    case 8: L(k_intra_lane, 8); break;
+    case 16: L(k_intra_pred, 16); break;
+    case 32: L(k_intra_pred, 32); break;
     default: return X265AMD_EINVAL;
     }
 #undef L
