@@ -287,6 +287,14 @@ int x265amd_blockop_grouped(int op, int depth, int count, const x265amd_block_ba
 /* count_nonzero (dct.cpp:714-726, num = N*N contiguous int16) and copy_cnt
  * (dct.cpp:728-742: coeff[N*N] <- residual with res_stride, counting nonzero).
  * copy_cnt when `res` != NULL, else count_nonzero on `coeff`. */
+/* denoiseDct (dct.cpp:744-755): each job's num coefficients (contiguous at
+ * coef + coef_off[i]) are shrunk in place by offset[num]; |coef| of every job
+ * is added into res_sum[num], which the whole batch shares like the
+ * reference's per-transform-size accumulator (uint32, wraps like it; the sum
+ * is order-independent).  num = N*N for N = 4..32. */
+int x265amd_denoise_dct(int n, int num, int16_t* coef, const int64_t* coef_off, uint32_t* res_sum,
+                        const uint16_t* offset, void* stream);
+
 int x265amd_count_nonzero(int size, int n,
                           int16_t* coeff, const int64_t* coeff_off,
                           const int16_t* res, intptr_t res_stride, const int64_t* res_off,

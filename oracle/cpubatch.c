@@ -58,6 +58,7 @@ typedef struct
     int (*cnz)(int, const int16_t*);
     uint32_t (*copy_cnt)(int, int16_t*, const int16_t*, intptr_t);
     void (*transpose)(int, void*, const void*, intptr_t);
+    void (*denoise)(int16_t*, uint32_t*, const uint16_t*, int);
 } Lib;
 
 #define SYM(field, name)                                                     \
@@ -84,6 +85,7 @@ void* cb_open(const char* path)
     SYM(fill, "xo_blockfill_s"); SYM(c2d1d_shl, "xo_cpy2Dto1D_shl"); SYM(c2d1d_shr, "xo_cpy2Dto1D_shr");
     SYM(c1d2d_shl, "xo_cpy1Dto2D_shl"); SYM(c1d2d_shr, "xo_cpy1Dto2D_shr"); SYM(cnz, "xo_count_nonzero");
     SYM(copy_cnt, "xo_copy_cnt"); SYM(transpose, "xo_transpose");
+    SYM(denoise, "xo_denoise_dct");
     return L;
 }
 
@@ -435,5 +437,13 @@ int cb_count_nonzero(void* h, int size, int64_t n, int16_t* c, const int64_t* co
 {
     CntCtx x = { (Lib*)h, size, c, co, r, rs, ro, cnt };
     parallel(n, nthreads, cnt_range, &x);
+    return 0;
+}
+
+/* denoiseDct: serial over the jobs, since every job adds into the one shared res_sum */
+int cb_denoise(void* h, int64_t n, int num, int16_t* c, const int64_t* co, uint32_t* res_sum, const uint16_t* offset)
+{
+    Lib* L = (Lib*)h;
+    for (int64_t i = 0; i < n; i++) L->denoise(c + co[i], res_sum, offset, num);
     return 0;
 }

@@ -96,6 +96,9 @@ class CpuOracle:
         self.cb.cb_count_nonzero(_vp(self.h), size, _i64(len(co)), _p(c), _p(co), _p(r), _ip(rs), _p(ro),
                                  _p(cnt), self.nthreads)
 
+    def denoise(self, num, c, co, rsum, offset):
+        self.cb.cb_denoise(_vp(self.h), _i64(len(co)), num, _p(c), _p(co), _p(rsum), _p(offset))
+
 
 class CpuPrims:
     """The GPU `Primitives` call surface (src/x265_amd/native.py) executed on the

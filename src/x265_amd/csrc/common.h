@@ -89,9 +89,9 @@ inline int lanes_log2(int units, int per_lane = 2)
     return lg;
 }
 
-inline uint32_t blocks_for(int n, int lg)
+inline uint32_t blocks_for(int n, int lg, int jpl = 1)
 {
-    const int per = X265AMD_BLOCK >> lg;
+    const int per = (X265AMD_BLOCK >> lg) * (jpl > 1 ? jpl : 1);
     return (uint32_t)((n + per - 1) / per);
 }
 
@@ -118,6 +118,7 @@ struct SubBatch
     int64_t sb;
     int w, h, n, lg;
     int param;
+    int jpl;                // jobs per lane group (0 = 1)
     uint32_t block0;        // first logical block of this sub-batch
 };
 
@@ -160,7 +161,7 @@ inline int launch_grouped(int count, const int* cls, const BatchGroup& proto, Fi
             SubBatch& s = g.s[k++];
             fill(j, s);
             s.block0 = blocks;
-            blocks += blocks_for(s.n, s.lg);
+            blocks += blocks_for(s.n, s.lg, s.jpl);
         }
         g.count = k;
         const int rc = launch(cls[i], g, blocks);

@@ -284,6 +284,21 @@ void dequant_scaling(const int16_t* q, const int32_t* dq, int16_t* coef, int num
     memcpy(coef, c.h<int16_t>(out), 2 * num);
 }
 
+void denoise(int16_t* coef, uint32_t* res_sum, const uint16_t* offset, int num)
+{
+    Ctx& c = ctx();
+    c.reset();
+    const size_t z = stage_value<int64_t>(c, 0);
+    const size_t oo = stage(c, offset, num, num, 1);
+    const size_t oc = stage(c, (const int16_t*)coef, num, num, 1);
+    const size_t orr = stage(c, (const uint32_t*)res_sum, num, num, 1);
+    round_trip(c, [&] {
+        x265amd_denoise_dct(1, num, c.d<int16_t>(oc), c.d<int64_t>(z), c.d<uint32_t>(orr), c.d<uint16_t>(oo), c.st);
+    }, oc, orr + 4 * num - oc);
+    memcpy(coef, c.h<int16_t>(oc), 2 * num);
+    memcpy(res_sum, c.h<uint32_t>(orr), 4 * num);
+}
+
 // ------------------------------------------------------------------ intra
 template <int N>
 void intra_pred(pixel* dst, intptr_t ds, const pixel* src, int mode, int bFilter)
@@ -333,6 +348,93 @@ void allangs(pixel* dst, pixel* ref, pixel* filt, int bLuma)
     memcpy(dst, c.h<pixel>(od), sizeof(pixel) * 33 * N * N);
 }
 
+// ------------------------------------------------------------------ companion block ops (a15)
+// dst (W x H, stride ds) = op(a (stride sa), b (stride sb), param)
+template <int OP, int W, int H, typename D, typename A, typename B>
+void bo_call(D* dst, intptr_t ds, const A* a, intptr_t sa, const B* b, intptr_t sb, int param)
+{
+    Ctx& c = ctx();
+    c.reset();
+    const size_t z = stage_value<int64_t>(c, 0);
+    // transpose reads the W x H source column-wise: the staged window is the same block
+    const size_t oa = a ? stage(c, a, sa, W, H) : z;
+    const size_t ob = b ? stage(c, b, sb, W, H) : z;
+    const size_t od = c.alloc(sizeof(D) * W * H);
+    round_trip(c, [&] {
+        x265amd_blockop(OP, kDepth, W, H, 1, c.d<D>(od), W, c.d<int64_t>(z), a ? c.d<A>(oa) : nullptr, W,
+                        c.d<int64_t>(z), b ? c.d<B>(ob) : nullptr, W, c.d<int64_t>(z), param, c.st);
+    }, od, sizeof(D) * W * H);
+    scatter(c, od, dst, ds, W, H);
+}
+
+template <int W, int H>
+void pixelavg_pp(pixel* d, intptr_t ds, const pixel* s0, intptr_t ss0, const pixel* s1, intptr_t ss1, int)
+{
+    bo_call<X265AMD_PIXELAVG, W, H>(d, ds, s0, ss0, s1, ss1, 0);
+}
+template <int W, int H>
+void add_avg(const int16_t* s0, const int16_t* s1, pixel* d, intptr_t ss0, intptr_t ss1, intptr_t ds)
+{
+    bo_call<X265AMD_ADDAVG, W, H>(d, ds, s0, ss0, s1, ss1, 0);
+}
+template <int W, int H>
+void copy_pp(pixel* d, intptr_t ds, const pixel* s, intptr_t ss) { bo_call<X265AMD_COPY_PP, W, H>(d, ds, s, ss, (const pixel*)nullptr, 0, 0); }
+template <int W, int H>
+void copy_sp(pixel* d, intptr_t ds, const int16_t* s, intptr_t ss) { bo_call<X265AMD_COPY_SP, W, H>(d, ds, s, ss, (const int16_t*)nullptr, 0, 0); }
+template <int W, int H>
+void copy_ps(int16_t* d, intptr_t ds, const pixel* s, intptr_t ss) { bo_call<X265AMD_COPY_PS, W, H>(d, ds, s, ss, (const pixel*)nullptr, 0, 0); }
+template <int W, int H>
+void copy_ss(int16_t* d, intptr_t ds, const int16_t* s, intptr_t ss) { bo_call<X265AMD_COPY_SS, W, H>(d, ds, s, ss, (const int16_t*)nullptr, 0, 0); }
+template <int W, int H>
+void sub_ps(int16_t* d, intptr_t ds, const pixel* a, const pixel* b, intptr_t sa, intptr_t sb)
+{
+    bo_call<X265AMD_SUB_PS, W, H>(d, ds, a, sa, b, sb, 0);
+}
+template <int W, int H>
+void add_ps(pixel* d, intptr_t ds, const pixel* a, const int16_t* b, intptr_t sa, intptr_t sb)
+{
+    bo_call<X265AMD_ADD_PS, W, H>(d, ds, a, sa, b, sb, 0);
+}
+template <int N>
+void calcresidual(const pixel* fenc, const pixel* pred, int16_t* res, intptr_t st)
+{
+    bo_call<X265AMD_SUB_PS, N, N>(res, st, fenc, st, pred, st, 0);
+}
+template <int N>
+void blockfill_s(int16_t* d, intptr_t ds, int16_t v) { bo_call<X265AMD_BLOCKFILL, N, N>(d, ds, (const int16_t*)nullptr, 0, (const int16_t*)nullptr, 0, v); }
+template <int N>
+void cpy2Dto1D_shl(int16_t* d, const int16_t* s, intptr_t ss, int sh) { bo_call<X265AMD_CPY2D1D_SHL, N, N>(d, N, s, ss, (const int16_t*)nullptr, 0, sh); }
+template <int N>
+void cpy2Dto1D_shr(int16_t* d, const int16_t* s, intptr_t ss, int sh) { bo_call<X265AMD_CPY2D1D_SHR, N, N>(d, N, s, ss, (const int16_t*)nullptr, 0, sh); }
+template <int N>
+void cpy1Dto2D_shl(int16_t* d, const int16_t* s, intptr_t ds, int sh) { bo_call<X265AMD_CPY1D2D_SHL, N, N>(d, ds, s, N, (const int16_t*)nullptr, 0, sh); }
+template <int N>
+void cpy1Dto2D_shr(int16_t* d, const int16_t* s, intptr_t ds, int sh) { bo_call<X265AMD_CPY1D2D_SHR, N, N>(d, ds, s, N, (const int16_t*)nullptr, 0, sh); }
+template <int N>
+void transpose(pixel* d, const pixel* s, intptr_t ss) { bo_call<X265AMD_TRANSPOSE, N, N>(d, N, s, ss, (const pixel*)nullptr, 0, 0); }
+
+// count_nonzero (dct.cpp:714-726) / copy_count (dct.cpp:728-742)
+template <int N>
+uint32_t count_call(int16_t* coeff, const int16_t* res, intptr_t rs)
+{
+    Ctx& c = ctx();
+    c.reset();
+    const size_t z = stage_value<int64_t>(c, 0);
+    const size_t oc = res ? c.alloc(2 * N * N) : stage(c, (const int16_t*)coeff, N * N, N * N, 1);
+    const size_t orr = res ? stage(c, res, rs, N, N) : z;
+    const size_t out = c.alloc(4);
+    round_trip(c, [&] {
+        x265amd_count_nonzero(N, 1, c.d<int16_t>(oc), c.d<int64_t>(z), res ? c.d<int16_t>(orr) : nullptr, N,
+                              c.d<int64_t>(z), c.d<uint32_t>(out), c.st);
+    }, oc, out + 4 - oc);
+    if (res) memcpy(coeff, c.h<int16_t>(oc), 2 * N * N);
+    return *c.h<uint32_t>(out);
+}
+template <int N>
+int count_nonzero(const int16_t* q) { return (int)count_call<N>((int16_t*)q, nullptr, 0); }
+template <int N>
+uint32_t copy_cnt(int16_t* coeff, const int16_t* res, intptr_t rs) { return count_call<N>(coeff, res, rs); }
+
 // ------------------------------------------------------------------ table filling
 int g_count;
 
@@ -363,6 +465,9 @@ void luma_pu(EncoderPrimitives::PU& u)
     put(u.luma_vss, &vss<8, W, H>);
     put(u.luma_hvpp, &hvpp<W, H>);
     put(u.convert_p2s, &p2s<W, H>);
+    put(u.pixelavg_pp, &pixelavg_pp<W, H>);
+    put(u.addAvg, &add_avg<W, H>);
+    put(u.copy_pp, &copy_pp<W, H>);
 }
 
 template <int W, int H>
@@ -376,6 +481,11 @@ void chroma_pu(EncoderPrimitives::Chroma::PUChroma& u)
     put(u.filter_vsp, &vsp<4, W, H>);
     put(u.filter_vss, &vss<4, W, H>);
     put(u.p2s, &p2s<W, H>);
+    if constexpr (W % 2 == 0)
+    {
+        put(u.addAvg, &add_avg<W, H>);
+        put(u.copy_pp, &copy_pp<W, H>);
+    }
 }
 
 template <int N>
@@ -389,7 +499,22 @@ void luma_cu(EncoderPrimitives::CU& u)
         for (int m = 0; m < NUM_INTRA_MODE; m++) put(u.intra_pred[m], &intra_pred<N>);
         constexpr int L = N == 4 ? 2 : N == 8 ? 3 : N == 16 ? 4 : 5;
         put(u.intra_pred_allangs, &allangs<L>);
+        put(u.count_nonzero, &count_nonzero<N>);
+        put(u.copy_cnt, &copy_cnt<N>);
     }
+    put(u.calcresidual, &calcresidual<N>);
+    put(u.sub_ps, &sub_ps<N, N>);
+    put(u.add_ps, &add_ps<N, N>);
+    put(u.blockfill_s, &blockfill_s<N>);
+    put(u.cpy2Dto1D_shl, &cpy2Dto1D_shl<N>);
+    put(u.cpy2Dto1D_shr, &cpy2Dto1D_shr<N>);
+    put(u.cpy1Dto2D_shl, &cpy1Dto2D_shl<N>);
+    put(u.cpy1Dto2D_shr, &cpy1Dto2D_shr<N>);
+    put(u.copy_sp, &copy_sp<N, N>);
+    put(u.copy_ps, &copy_ps<N, N>);
+    put(u.copy_ss, &copy_ss<N, N>);
+    put(u.copy_pp, &copy_pp<N, N>);
+    put(u.transpose, &transpose<N>);
     put(u.sa8d, &cmp_pp<X265AMD_SA8D, N, N>);
     put(u.sse_pp, &sse_pp<N, N>);
     put(u.sse_ss, &sse_ss<N>);
@@ -406,6 +531,12 @@ void chroma_cu(EncoderPrimitives::Chroma::CUChroma& u)
         put(u.sa8d, &cmp_pp<X265AMD_SA8D, W, H>);
         put(u.sse_pp, &sse_pp<W, H>);
     }
+    put(u.sub_ps, &sub_ps<W, H>);
+    put(u.add_ps, &add_ps<W, H>);
+    put(u.copy_ps, &copy_ps<W, H>);
+    put(u.copy_sp, &copy_sp<W, H>);
+    put(u.copy_ss, &copy_ss<W, H>);
+    put(u.copy_pp, &copy_pp<W, H>);
 }
 
 // chroma dims of luma PU p for 4:2:0 (w/2, h/2) and 4:2:2 (w/2, h)
@@ -435,6 +566,8 @@ void setupHipPrimitives(EncoderPrimitives& p, int /*cpuMask*/)
     luma_cu<16>(p.cu[2]);
     luma_cu<32>(p.cu[3]);
     luma_cu<64>(p.cu[4]);
+    chroma_cu<2, 2>(p.chroma[I420].cu[0]);
+    chroma_cu<2, 4>(p.chroma[I422].cu[0]);
     chroma_cu<4, 4>(p.chroma[I420].cu[1]);
     chroma_cu<8, 8>(p.chroma[I420].cu[2]);
     chroma_cu<16, 16>(p.chroma[I420].cu[3]);
@@ -449,6 +582,7 @@ void setupHipPrimitives(EncoderPrimitives& p, int /*cpuMask*/)
     put(p.nquant, &nquant);
     put(p.dequant_normal, &dequant_normal);
     put(p.dequant_scaling, &dequant_scaling);
+    put(p.denoiseDct, &denoise);
 }
 
 int hip_provider_count() { return g_count; }

@@ -383,6 +383,54 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_count(int n, int16_t* __restr
     if (live && lane == 0) cnt[job] = c;
 }
 
+// denoiseDct (dct.cpp:744-755) over a batch: every job shrinks its num
+// coefficients in place by offset[] and adds |coef| into the batch's shared
+// res_sum[] (the reference's per-size m_residualSum accumulator).  A block takes
+// kDenoiseJobs jobs; thread t owns coefficient positions t, t+256, ... (for
+// num < 256, num-wide slices of several jobs at once), sums |coef| over its
+// jobs in registers and adds each position into res_sum with one atomic at the
+// end: uint32 addition commutes, so the total equals the serial order's mod 2^32.
+constexpr int kDenoiseJobs = 64;
+
+__global__ __launch_bounds__(X265AMD_BLOCK) void k_denoise(int n, int num, int16_t* __restrict__ coef,
+    const int64_t* __restrict__ coef_off, uint32_t* __restrict__ res_sum, const uint16_t* __restrict__ offset)
+{
+    const int t = threadIdx.x;
+    const int64_t j0 = (int64_t)xcd_block() * kDenoiseJobs;
+    const int span = num < X265AMD_BLOCK ? num : X265AMD_BLOCK;     // positions per pass
+    const int par = X265AMD_BLOCK / span;                            // jobs per pass (num < 256)
+    const int pos0 = t % span, jsub = t / span;
+    if (jsub >= par) return;
+    uint32_t acc[4] = { 0, 0, 0, 0 };                                // num <= 1024 -> <= 4 positions
+    int off[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) off[k] = pos0 + k * span < num ? offset[pos0 + k * span] : 0;
+    for (int jj = jsub; jj < kDenoiseJobs; jj += par)
+    {
+        const int64_t job = j0 + jj;
+        if (job >= n) break;
+        int16_t* c = coef + coef_off[job];
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+        {
+            const int i = pos0 + k * span;
+            if (i >= num) break;
+            int level = c[i];
+            const int sign = level >> 31;
+            level = (level + sign) ^ sign;
+            acc[k] += (uint32_t)level;
+            level -= off[k];
+            c[i] = (int16_t)(level < 0 ? 0 : (level ^ sign) - sign);
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+    {
+        const int i = pos0 + k * span;
+        if (i < num && acc[k]) atomicAdd(&res_sum[i], acc[k]);
+    }
+}
+
 // lanes per coefficient job: 8 coefficients per lane, at most one wavefront
 static inline int coef_lanes_log2(int num)
 {
@@ -481,6 +529,16 @@ extern "C" int x265amd_dequant_scaling(int n, int num, const int16_t* q, const i
     hipLaunchKernelGGL(k_dequant<true>, dim3((n + (X265AMD_BLOCK >> lg) - 1) / (X265AMD_BLOCK >> lg)),
                        dim3(X265AMD_BLOCK), 0, (hipStream_t)stream, n, num, lg, q, q_off,
                        dq, dq_off, coef, coef_off, per, shift);
+    return (int)hipGetLastError();
+}
+
+extern "C" int x265amd_denoise_dct(int n, int num, int16_t* coef, const int64_t* coef_off, uint32_t* res_sum,
+                                   const uint16_t* offset, void* stream)
+{
+    if (n <= 0) return 0;
+    if (num <= 0 || num % 16 || num > 1024 || (num < X265AMD_BLOCK && X265AMD_BLOCK % num)) return X265AMD_EINVAL;
+    hipLaunchKernelGGL(k_denoise, dim3((n + kDenoiseJobs - 1) / kDenoiseJobs), dim3(X265AMD_BLOCK), 0,
+                       (hipStream_t)stream, n, num, coef, coef_off, res_sum, offset);
     return (int)hipGetLastError();
 }
 

@@ -178,6 +178,10 @@ class Primitives:
         self._check(self.lib.x265amd_interp_grouped(op, taps, depth, len(arr), arr, stream or _stream()),
                     "interp_grouped")
 
+    def denoise_dct(self, num, c, co, rsum, offset, stream=None):
+        self._check(self.lib.x265amd_denoise_dct(co.numel(), num, _ptr(c), _ptr(co), _ptr(rsum), _ptr(offset),
+                                                 stream or _stream()), "denoise_dct")
+
     def count_nonzero(self, size, c, co, r, rs, ro, cnt, stream=None):
         self._check(self.lib.x265amd_count_nonzero(size, co.numel(), _ptr(c), _ptr(co), _ptr(r), _ip(rs), _ptr(ro),
                                                    _ptr(cnt), stream or _stream()), "count_nonzero")

@@ -374,6 +374,26 @@ def case_count(size: int, copy: bool, depth: int, n: int, seed: int) -> Case:
     return Case("count", dict(size=size, copy=int(copy), depth=depth, n=n, seed=seed), bufs, outs)
 
 
+def case_denoise(size: int, depth: int, n: int, seed: int) -> Case:
+    """denoiseDct over a batch sharing one resSum (mbdstharness.cpp:303-340 ranges:
+    coefficients (rand & SHORT_MAX) - (rand & SHORT_MAX) or +-SHORT_MAX, offsets
+    rand % UNSIGNED_SHORT_MAX); resSum starts near 2^32 so the uint32 wrap is exercised."""
+    det = Det(seed)
+    num = size * size
+    cls = det.ints(0, 3, n)
+    c = (det.ints(0, 32768, n * num) - det.ints(0, 32768, n * num)).astype(np.int16)
+    c = c.reshape(n, num)
+    c[cls == 1] = -32767
+    c[cls == 2] = 32767
+    co = np.arange(n, dtype=np.int64) * num
+    rsum = (np.uint64(0xFFFF0000) + det.ints(0, 1 << 16, num).astype(np.uint64)).astype(np.uint32)
+    off = det.ints(0, 65535, num).astype(np.uint16)
+    # small offsets on half the positions, so some coefficients survive the shrink
+    off[::2] = (off[::2] % 2048).astype(np.uint16)
+    return Case("denoise", dict(size=size, depth=depth, n=n, seed=seed),
+                dict(c=c.reshape(-1), co=co, rs=rsum, off=off), ["c", "rs"])
+
+
 # ---------------------------------------------------------------- catalogue
 def blockop_sizes(op: int):
     if op in (SUB_PS, ADD_PS, COPY_SP, COPY_PS, COPY_SS):
@@ -441,6 +461,8 @@ def all_cases(depth: int, n: int = 6, quick: bool = False):
     for size in TU_SQ:
         for cp in (False, True):
             cases.append(case_count(size, cp, depth, n, s("cnt", size, cp)))
+    for size in TU_SQ:
+        cases.append(case_denoise(size, depth, n, s("dn", size)))
     return cases
 
 
@@ -472,6 +494,8 @@ def run_cpu(case: Case, orc) -> dict:
                     b["boff"], b["param"])
     elif f == "count":
         orc.count_nonzero(p["size"], b["c"], b["co"], b["r"], b["rs"], b["ro"], b["cnt"])
+    elif f == "denoise":
+        orc.denoise(p["size"] ** 2, b["c"], b["co"], b["rs"], b["off"])
     else:
         raise ValueError(f)
     return {k: b[k] for k in case.outs}
@@ -519,6 +543,8 @@ def run_gpu(case: Case, prims, device="cuda") -> dict:
                       b["sb"], b["boff"], b["param"])
     elif f == "count":
         prims.count_nonzero(p["size"], b["c"], b["co"], b["r"], b["rs"], b["ro"], b["cnt"])
+    elif f == "denoise":
+        prims.denoise_dct(p["size"] ** 2, b["c"], b["co"], b["rs"], b["off"])
     else:
         raise ValueError(f)
     torch.cuda.synchronize()

@@ -62,9 +62,11 @@ static bool same(const T* a, const T* b, size_t n) { return memcmp(a, b, n * siz
 
 int main()
 {
+    setvbuf(stdout, nullptr, _IONBF, 0);   // progress survives a crash
     static EncoderPrimitives tab;
     memset(&tab, 0xAB, sizeof(tab));   // every slot "present" (non-NULL placeholder)
     setupHipPrimitives(tab, 0);
+    printf("provider installed\n");
     Buf A, B;
     std::vector<pixel> o1(64 * 80), o2(64 * 80);
     std::vector<int16_t> s1(64 * 80), s2(64 * 80);
@@ -77,6 +79,7 @@ int main()
         for (int p = 0; p < 25; p++)
         {
             const int w = kPuW[p], h = kPuH[p];
+            if (iter == 0) printf("pu %dx%d\n", w, h);
             EncoderPrimitives::PU& u = tab.pu[p];
             EXPECT(u.sad(A.pp(), S, B.pp() + 1, S) == xo_sad(w, h, A.pp(), S, B.pp() + 1, S), "sad %dx%d", w, h);
             EXPECT(u.satd(A.pp(), S, B.pp() + 3, S) == xo_satd(w, h, A.pp(), S, B.pp() + 3, S), "satd %dx%d", w, h);
@@ -111,6 +114,13 @@ int main()
             EXPECT(same(s1.data(), s2.data(), s1.size()), "luma_vss %dx%d", w, h);
             u.convert_p2s(A.pp(), S, s1.data(), 64); xo_interp(XO_P2S, 8, w, h, A.pp(), S, s2.data(), 64, 0, 0);
             EXPECT(same(s1.data(), s2.data(), s1.size()), "p2s %dx%d", w, h);
+            // companion block ops (a15)
+            u.pixelavg_pp(o1.data(), 64, A.pp(), S, B.pp() + 1, S, 32); xo_pixelavg(w, h, o2.data(), 64, A.pp(), S, B.pp() + 1, S);
+            EXPECT(same(o1.data(), o2.data(), o1.size()), "pixelavg_pp %dx%d", w, h);
+            u.addAvg(A.sp(), B.sp(), o1.data(), S, S, 64); xo_addavg(w, h, A.sp(), B.sp(), o2.data(), S, S, 64);
+            EXPECT(same(o1.data(), o2.data(), o1.size()), "addAvg %dx%d", w, h);
+            u.copy_pp(o1.data(), 64, A.pp(), S); xo_copy_pp(w, h, o2.data(), 64, A.pp(), S);
+            EXPECT(same(o1.data(), o2.data(), o1.size()), "copy_pp %dx%d", w, h);
             // chroma 4:2:0 (w/2 x h/2); the 2x2 entry of the reference table is NULL and is skipped
             const int cw = w / 2, ch = h / 2;
             if (cw >= 2 && ch >= 2 && !(cw == 2 && ch == 2))
@@ -128,6 +138,7 @@ int main()
         for (int i = 0; i < 5; i++)
         {
             const int n = 4 << i;
+            if (iter == 0) printf("cu %d\n", n);
             EncoderPrimitives::CU& c = tab.cu[i];
             EXPECT(c.sa8d(A.pp(), S, B.pp(), S) == xo_sa8d(n, n, A.pp(), S, B.pp(), S), "sa8d %d", n);
             EXPECT((uint64_t)c.sse_pp(A.pp(), S, B.pp(), S) == xo_sse_pp(n, n, A.pp(), S, B.pp(), S), "sse_pp %d", n);
@@ -135,7 +146,44 @@ int main()
             EXPECT((uint64_t)c.ssd_s(A.sp(), S) == xo_ssd_s(n, A.sp(), S), "ssd_s %d", n);
             EXPECT(c.psy_cost_pp(A.pp(), S, B.pp(), S) == xo_psy_cost_pp(n, A.pp(), S, B.pp(), S), "psy %d", n);
             EXPECT(c.var(A.pp(), S) == xo_var(n, A.pp(), S), "var %d", n);
+            // companion block ops (a15): outputs into 0xCD-filled 64-stride buffers
+            memset(s1.data(), 0xCD, s1.size() * 2); memset(s2.data(), 0xCD, s2.size() * 2);
+            // calcresidual uses ONE stride for fenc, pred and residual (pixel.cpp:417): 64 keeps the output in s1
+            c.calcresidual(A.pp(), B.pp(), s1.data(), 64); xo_calcresidual(n, A.pp(), B.pp(), s2.data(), 64);
+            EXPECT(same(s1.data(), s2.data(), s1.size()), "calcresidual %d", n);
+            c.sub_ps(s1.data(), 64, A.pp(), B.pp() + 1, S, S); xo_sub_ps(n, n, s2.data(), 64, A.pp(), B.pp() + 1, S, S);
+            EXPECT(same(s1.data(), s2.data(), s1.size()), "sub_ps %d", n);
+            c.add_ps(o1.data(), 64, A.pp(), B.sp(), S, S); xo_add_ps(n, n, o2.data(), 64, A.pp(), B.sp(), S, S);
+            EXPECT(same(o1.data(), o2.data(), o1.size()), "add_ps %d", n);
+            c.blockfill_s(s1.data(), 64, (int16_t)(iter * 1000 - 2500)); xo_blockfill_s(n, s2.data(), 64, (int16_t)(iter * 1000 - 2500));
+            EXPECT(same(s1.data(), s2.data(), s1.size()), "blockfill_s %d", n);
+            const int sh = 1 + iter % 5;
+            c.cpy2Dto1D_shl(s1.data(), A.sp(), S, sh); xo_cpy2Dto1D_shl(n, s2.data(), A.sp(), S, sh);
+            EXPECT(same(s1.data(), s2.data(), s1.size()), "cpy2Dto1D_shl %d", n);
+            c.cpy2Dto1D_shr(s1.data(), A.sp(), S, sh); xo_cpy2Dto1D_shr(n, s2.data(), A.sp(), S, sh);
+            EXPECT(same(s1.data(), s2.data(), s1.size()), "cpy2Dto1D_shr %d", n);
+            c.cpy1Dto2D_shl(s1.data(), A.sp(), 64, sh); xo_cpy1Dto2D_shl(n, s2.data(), A.sp(), 64, sh);
+            EXPECT(same(s1.data(), s2.data(), s1.size()), "cpy1Dto2D_shl %d", n);
+            c.cpy1Dto2D_shr(s1.data(), A.sp(), 64, sh); xo_cpy1Dto2D_shr(n, s2.data(), A.sp(), 64, sh);
+            EXPECT(same(s1.data(), s2.data(), s1.size()), "cpy1Dto2D_shr %d", n);
+            c.copy_sp(o1.data(), 64, B.sp(), S); xo_copy_sp(n, n, o2.data(), 64, B.sp(), S);
+            EXPECT(same(o1.data(), o2.data(), o1.size()), "copy_sp %d", n);
+            c.copy_ps(s1.data(), 64, A.pp(), S); xo_copy_ps(n, n, s2.data(), 64, A.pp(), S);
+            EXPECT(same(s1.data(), s2.data(), s1.size()), "copy_ps %d", n);
+            c.copy_ss(s1.data(), 64, A.sp(), S); xo_copy_ss(n, n, s2.data(), 64, A.sp(), S);
+            EXPECT(same(s1.data(), s2.data(), s1.size()), "copy_ss %d", n);
+            c.copy_pp(o1.data(), 64, A.pp(), S); xo_copy_pp(n, n, o2.data(), 64, A.pp(), S);
+            EXPECT(same(o1.data(), o2.data(), o1.size()), "cu copy_pp %d", n);
+            c.transpose(o1.data(), A.pp(), S); xo_transpose(n, o2.data(), A.pp(), S);
+            EXPECT(same(o1.data(), o2.data(), o1.size()), "transpose %d", n);
             if (n > 32) continue;
+            {
+                std::vector<int16_t> q(n * n), k1(n * n), k2(n * n);
+                for (auto& v : q) v = (int16_t)(rnd() % 4 == 0 ? (int)(rnd() % 200) - 100 : 0);
+                EXPECT(c.count_nonzero(q.data()) == xo_count_nonzero(n, q.data()), "count_nonzero %d", n);
+                EXPECT(c.copy_cnt(k1.data(), A.sp(), S) == xo_copy_cnt(n, k2.data(), A.sp(), S), "copy_cnt ret %d", n);
+                EXPECT(same(k1.data(), k2.data(), n * n), "copy_cnt %d", n);
+            }
             std::vector<int16_t> res(n * n), co1(n * n), co2(n * n);
             for (auto& v : res) v = (int16_t)((int)(rnd() % (2 * PMAX + 1)) - PMAX);
             c.dct(res.data(), co1.data(), n); xo_dct(XO_DCT, n, res.data(), co2.data(), n);
@@ -172,6 +220,18 @@ int main()
             EXPECT(same(q1.data(), q2.data(), num), "dequant_normal %d", n);
             tab.dequant_scaling(coef.data(), qc.data(), q1.data(), num, 4, 3); xo_dequant_scaling(coef.data(), qc.data(), q2.data(), num, 4, 3);
             EXPECT(same(q1.data(), q2.data(), num), "dequant_scaling %d", n);
+            {
+                std::vector<uint16_t> off(num);
+                std::vector<uint32_t> rs1(num), rs2(num);
+                for (int k = 0; k < num; k++)
+                {
+                    off[k] = (uint16_t)(rnd() % (k & 1 ? 65535 : 2048));
+                    rs1[k] = rs2[k] = 0xFFFFF000u + rnd() % 8192;
+                    q1[k] = q2[k] = (int16_t)((int)(rnd() % 32768) - (int)(rnd() % 32768));
+                }
+                tab.denoiseDct(q1.data(), rs1.data(), off.data(), num); xo_denoise_dct(q2.data(), rs2.data(), off.data(), num);
+                EXPECT(same(q1.data(), q2.data(), num) && same(rs1.data(), rs2.data(), num), "denoiseDct %d", n);
+            }
         }
         std::vector<int16_t> r4(16), c1(16), c2(16);
         for (auto& v : r4) v = (int16_t)((int)(rnd() % (2 * PMAX + 1)) - PMAX);
