@@ -490,7 +490,7 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_hvpp(const BatchGroup g)
 
 // -------------------------------------------------------------- dispatch
 
-// kernel class of a batch: unit width x unit height, packed as uw * 8 + uh
+// kernel class of a batch: unit width x unit height, packed as uw * 16 + uh
 template <int OP, int TAPS>
 static int interp_class(int w, int h, int rowext)
 {
@@ -498,14 +498,15 @@ static int interp_class(int w, int h, int rowext)
     if constexpr (OP == X265AMD_HVPP)
     {
         if (w % 4) return -X265AMD_EINVAL;
-        return (w % 8 == 0 ? 8 : 4) * 8 + (h % 4 == 0 ? 4 : 1);
+        return (w % 8 == 0 ? 8 : 4) * 16 + (h % 4 == 0 ? 4 : 1);
     }
     const int rows = (OP == X265AMD_HPS && rowext) ? h + TAPS - 1 : h;
-    const int uh = rows % 4 ? 1 : 4;
-    if (w % 8 == 0) return 8 * 8 + uh;
-    if (w % 4 == 0) return 4 * 8 + uh;
+    const char* e = getenv("X265AMD_IP_UH8");
+    const int uh = (e && atoi(e) && rows % 8 == 0 && w % 4 == 0) ? 8 : rows % 4 ? 1 : 4;
+    if (w % 8 == 0) return 8 * 16 + uh;
+    if (w % 4 == 0) return 4 * 16 + uh;
     // 2-wide units: the chroma filters and the vertical / p2s luma paths
-    if (w % 2 == 0 && (TAPS == 4 || (OP != X265AMD_HPP && OP != X265AMD_HPS))) return 2 * 8 + uh;
+    if (w % 2 == 0 && (TAPS == 4 || (OP != X265AMD_HPP && OP != X265AMD_HPS))) return 2 * 16 + uh;
     return -X265AMD_EINVAL;
 }
 
@@ -525,7 +526,7 @@ static int launch_interp(int cls, const BatchGroup& g, uint32_t blocks, hipStrea
         for (int i = 0; i < g.count; i++)
             lds = std::max(lds, (size_t)(X265AMD_BLOCK >> g.s[i].lg) * (g.s[i].h + 7) * g.s[i].w * sizeof(int16_t));
 #define L(UW, UH) \
-    if (cls == UW * 8 + UH) \
+    if (cls == UW * 16 + UH) \
     { \
         if constexpr (OP == X265AMD_HVPP) \
         { \
@@ -536,7 +537,7 @@ static int launch_interp(int cls, const BatchGroup& g, uint32_t blocks, hipStrea
             hipLaunchKernelGGL((k_interp<P, S, D, OP, TAPS, UW, UH>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, g); \
         return (int)hipGetLastError(); \
     }
-    L(8, 4) L(8, 1) L(4, 4) L(4, 1) L(2, 4) L(2, 1)
+    L(8, 8) L(4, 8) L(8, 4) L(8, 1) L(4, 4) L(4, 1) L(2, 4) L(2, 1)
 #undef L
     return X265AMD_EINVAL;
 }
@@ -564,7 +565,7 @@ static int grouped_interp(int depth, int count, const x265amd_interp_batch* bt, 
             s.b = OP == X265AMD_P2S ? nullptr : b.coeff;
             s.w = b.w; s.h = b.h; s.n = b.n;
             s.param = OP == X265AMD_HPS ? b.is_row_ext : 0;
-            const int uw = cls[i] / 8, uh = cls[i] % 8;
+            const int uw = cls[i] / 16, uh = cls[i] % 16;
             if constexpr (OP == X265AMD_HVPP)
                 s.lg = hvpp_lg(b.w, b.h, uw, uh);
             else

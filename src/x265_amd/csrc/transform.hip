@@ -254,6 +254,226 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_trN(int n, int depth,
     }
 }
 
+// --------------------------------------------------------------- 16x16 / 32x32 on MFMA
+// One wavefront per transform; both stages are matrix products on the f16
+// matrix cores with FP32 accumulation:  forward  Dst = T * (Src * T^T)^T,
+// inverse  Res = (C^T * T)^T * T  (each stage rounded / wrapped or clipped to
+// int16 exactly as partialButterfly*[Inverse]).  Exactness: every int16
+// operand is split x = hi * 2048 + lo with lo in [0, 2047] and hi in
+// [-16, 15] — both exact in f16 — and the two halves accumulate in separate
+// FP32 tiles whose partial sums stay integers below 2^24 (|lo * t| summed over
+// K = 32 is < 2047 * 90 * 32), so hi * 2048 + lo reproduces the int32 sum.
+// The first stage's accumulator tile feeds the second MFMA straight from
+// registers (column on the lane, rows in the registers: the second product
+// sums over its row index), so no LDS is used.
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+template <int K, typename V>
+__device__ __forceinline__ void split_hl(const int (&x)[K], V& lo, V& hi)
+{
+#pragma unroll
+    for (int j = 0; j < K; j++)
+    {
+        lo[j] = (_Float16)(uint16_t)(x[j] & 2047);
+        hi[j] = (_Float16)(int16_t)(x[j] >> 11);
+    }
+}
+
+constexpr int kTrWaves = X265AMD_BLOCK / 64;
+
+// grid of a matrix-core transform launch: enough waves to fill the chip,
+// each looping over transforms (the constant operands load once per wave)
+static inline uint32_t mfma_grid(int n)
+{
+    const int64_t want = ((int64_t)n + kTrWaves - 1) / kTrWaves;
+    return (uint32_t)(want < 4096 ? want : 4096);
+}
+
+template <bool FWD>
+__global__ __launch_bounds__(X265AMD_BLOCK) void k_tr32_mfma(int n, int depth,
+    const int16_t* __restrict__ src, intptr_t ss, const int64_t* __restrict__ soff,
+    int16_t* __restrict__ dst, intptr_t ds, const int64_t* __restrict__ doff)
+{
+    __shared__ int16_t tile[kTrWaves][32 * 32];     // per-wavefront 32x32 staging tile, row-major
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63, r = l & 31, h = l >> 5;
+    int16_t* T = tile[w];
+    const int sh1 = FWD ? 4 + depth - 8 : 7, sh2 = FWD ? 11 : 12 - (depth - 8);
+    const int io_row = l >> 1, io_col = 16 * (l & 1);  // 16-byte I/O: two lanes per row
+
+    // constant fragments: stage-1 operand in natural k order, stage-2 operand in
+    // the k order of the accumulator registers (row 16s + 8(j>>2) + 4h + (j&3))
+    f16x8 t1[2], t2[2];
+#pragma unroll
+    for (int st = 0; st < 2; st++)
+#pragma unroll
+        for (int j = 0; j < 8; j++)
+        {
+            const int kn = 16 * st + 8 * h + j, kp = 16 * st + 8 * (j >> 2) + 4 * h + (j & 3);
+            t1[st][j] = (_Float16)(FWD ? c_t32.m[r][kn] : c_t32.m[kn][r]);
+            t2[st][j] = (_Float16)(FWD ? c_t32.m[r][kp] : c_t32.m[kp][r]);
+        }
+
+    const int64_t step = (int64_t)gridDim.x * kTrWaves;
+    for (int64_t job = (int64_t)blockIdx.x * kTrWaves + w; job < n; job += step)
+    {
+        const int16_t* s = src + soff[job];
+        int16_t* d = dst + doff[job];
+        // ---- stage 1: forward U = Src * T^T (A = source rows, 16-byte row loads);
+        //      inverse M1 = C^T * T (A = coefficient columns, staged through the tile)
+        int x[2][8];
+        if constexpr (FWD)
+        {
+            load_row16<8>(s + r * ss + 8 * h, x[0]);
+            load_row16<8>(s + r * ss + 16 + 8 * h, x[1]);
+        }
+        else
+        {
+#pragma unroll
+            for (int c = 0; c < 16; c += 8) stu<uint4>(&T[io_row * 32 + io_col + c], ldu<uint4>(s + io_row * ss + io_col + c));
+#pragma unroll
+            for (int st = 0; st < 2; st++)
+#pragma unroll
+                for (int j = 0; j < 8; j++) x[st][j] = T[(16 * st + 8 * h + j) * 32 + r];
+        }
+        f32x16 lo1 = {}, hi1 = {};
+#pragma unroll
+        for (int st = 0; st < 2; st++)
+        {
+            f16x8 xl, xh;
+            split_hl<8>(x[st], xl, xh);
+            lo1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(xl, t1[st], lo1, 0, 0, 0);
+            hi1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(xh, t1[st], hi1, 0, 0, 0);
+        }
+        int v[16];
+#pragma unroll
+        for (int i = 0; i < 16; i++)
+        {
+            const int a = (int)hi1[i] * 2048 + (int)lo1[i];
+            v[i] = FWD ? fwd_round(a, sh1) : inv_round(a, sh1);
+        }
+        // ---- stage 2 from registers: forward Dst = T * U' (U' as B); inverse Res = M1'^T * T (M1' as A)
+        f32x16 lo2 = {}, hi2 = {};
+#pragma unroll
+        for (int st = 0; st < 2; st++)
+        {
+            int y[8];
+#pragma unroll
+            for (int j = 0; j < 8; j++) y[j] = v[8 * st + j];
+            f16x8 xl, xh;
+            split_hl<8>(y, xl, xh);
+            if constexpr (FWD)
+            {
+                lo2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(t2[st], xl, lo2, 0, 0, 0);
+                hi2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(t2[st], xh, hi2, 0, 0, 0);
+            }
+            else
+            {
+                lo2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(xl, t2[st], lo2, 0, 0, 0);
+                hi2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(xh, t2[st], hi2, 0, 0, 0);
+            }
+        }
+        // accumulator (row, col) = ((i&3) + 8(i>>2) + 4h, r) -> tile -> 16-byte row stores
+#pragma unroll
+        for (int i = 0; i < 16; i++)
+        {
+            const int a = (int)hi2[i] * 2048 + (int)lo2[i];
+            T[((i & 3) + 8 * (i >> 2) + 4 * h) * 32 + r] = (int16_t)(FWD ? fwd_round(a, sh2) : inv_round(a, sh2));
+        }
+#pragma unroll
+        for (int c = 0; c < 16; c += 8) stu<uint4>(d + io_row * ds + io_col + c, ldu<uint4>(&T[io_row * 32 + io_col + c]));
+    }
+}
+
+template <bool FWD>
+__global__ __launch_bounds__(X265AMD_BLOCK) void k_tr16_mfma(int n, int depth,
+    const int16_t* __restrict__ src, intptr_t ss, const int64_t* __restrict__ soff,
+    int16_t* __restrict__ dst, intptr_t ds, const int64_t* __restrict__ doff)
+{
+    // 16x16x16 f16: A lane l holds A[l&15][4q + j], B holds B[4q + j][l&15],
+    // the accumulator holds rows 4q + i of column l&15 (q = l >> 4) — the
+    // accumulator order IS the operand k order, and T[l&15][4q+j] (forward) /
+    // T[4q+j][l&15] (inverse) is the constant operand of both stages.
+    // A wave takes JB transforms per iteration (all loads first, then the
+    // MFMA chains interleaved), so one iteration keeps 2 KiB in flight.
+    constexpr int JB = 4;
+    __shared__ int16_t tile[kTrWaves][JB][16 * 16];
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63, r = l & 15, q = l >> 4;
+    const int sh1 = FWD ? 3 + depth - 8 : 7, sh2 = FWD ? 10 : 12 - (depth - 8);
+    const int io_row = l >> 2, io_col = 4 * (l & 3);  // 8-byte I/O: four lanes per row
+
+    f16x4 t;
+#pragma unroll
+    for (int j = 0; j < 4; j++) t[j] = (_Float16)(FWD ? c_t32.m[2 * r][4 * q + j] : c_t32.m[2 * (4 * q + j)][r]);
+
+    const int64_t step = (int64_t)gridDim.x * kTrWaves * JB;
+    for (int64_t job0 = ((int64_t)blockIdx.x * kTrWaves + w) * JB; job0 < n; job0 += step)
+    {
+        int16_t* d[JB];
+        int x[JB][4];
+#pragma unroll
+        for (int b = 0; b < JB; b++)
+        {
+            const int64_t job = job0 + b < n ? job0 + b : job0;   // a tail repeats the first (its result is not stored)
+            const int16_t* s = src + soff[job];
+            d[b] = dst + doff[job];
+            int16_t* T = tile[w][b];
+            if constexpr (FWD) load_row16<4>(s + r * ss + 4 * q, x[b]);
+            else stu<uint2>(&T[io_row * 16 + io_col], ldu<uint2>(s + io_row * ss + io_col));
+        }
+        f32x4 lo[JB], hi[JB];
+#pragma unroll
+        for (int b = 0; b < JB; b++)
+        {
+            if constexpr (!FWD)
+            {
+#pragma unroll
+                for (int j = 0; j < 4; j++) x[b][j] = tile[w][b][(4 * q + j) * 16 + r];
+            }
+            f16x4 xl, xh;
+            split_hl<4>(x[b], xl, xh);
+            lo[b] = __builtin_amdgcn_mfma_f32_16x16x16f16(xl, t, f32x4{}, 0, 0, 0);
+            hi[b] = __builtin_amdgcn_mfma_f32_16x16x16f16(xh, t, f32x4{}, 0, 0, 0);
+        }
+#pragma unroll
+        for (int b = 0; b < JB; b++)
+        {
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+            {
+                const int a = (int)hi[b][i] * 2048 + (int)lo[b][i];
+                x[b][i] = FWD ? fwd_round(a, sh1) : inv_round(a, sh1);
+            }
+            f16x4 xl, xh;
+            split_hl<4>(x[b], xl, xh);
+            if constexpr (FWD)
+            {
+                lo[b] = __builtin_amdgcn_mfma_f32_16x16x16f16(t, xl, f32x4{}, 0, 0, 0);
+                hi[b] = __builtin_amdgcn_mfma_f32_16x16x16f16(t, xh, f32x4{}, 0, 0, 0);
+            }
+            else
+            {
+                lo[b] = __builtin_amdgcn_mfma_f32_16x16x16f16(xl, t, f32x4{}, 0, 0, 0);
+                hi[b] = __builtin_amdgcn_mfma_f32_16x16x16f16(xh, t, f32x4{}, 0, 0, 0);
+            }
+        }
+#pragma unroll
+        for (int b = 0; b < JB; b++)
+        {
+            int16_t* T = tile[w][b];
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+            {
+                const int a = (int)hi[b][i] * 2048 + (int)lo[b][i];
+                T[(4 * q + i) * 16 + r] = (int16_t)(FWD ? fwd_round(a, sh2) : inv_round(a, sh2));
+            }
+            if (job0 + b < n) stu<uint2>(d[b] + io_row * ds + io_col, ldu<uint2>(&T[io_row * 16 + io_col]));
+        }
+    }
+}
+
 // --------------------------------------------------------------- quant family
 // one job per G-lane group (G = num/8, at most 64); a lane handles 8
 // coefficients per iteration
@@ -467,6 +687,16 @@ extern "C" int x265amd_transform(int kind, int depth, int size, int n,
         return (int)hipGetLastError();
     }
     if (kind != X265AMD_DCT && kind != X265AMD_IDCT) return X265AMD_EINVAL;
+    if (size == 16 || size == 32)
+    {
+        // matrix cores: one wavefront per transform
+        const dim3 grid(mfma_grid(size == 16 ? (n + 3) / 4 : n));
+#define M(K) hipLaunchKernelGGL(K, grid, dim3(X265AMD_BLOCK), 0, st, n, depth, src, src_stride, src_off, dst, dst_stride, dst_off)
+        if (size == 32) { if (fwd) M(k_tr32_mfma<true>); else M(k_tr32_mfma<false>); }
+        else { if (fwd) M(k_tr16_mfma<true>); else M(k_tr16_mfma<false>); }
+#undef M
+        return (int)hipGetLastError();
+    }
     const int jobs = X265AMD_BLOCK / size;
     const dim3 grid((n + jobs - 1) / jobs);
 #define T(N)                                                                                                       \

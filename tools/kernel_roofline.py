@@ -175,6 +175,13 @@ def main():
             offs = torch.arange(n, dtype=torch.int64, device=dev) * (s * s)
             ms = timeit(lambda: prims.transform(kind, 8, s, Sr, s, offs, Dr, s, offs))
             record(name, n * 4 * s * s, ms, n)
+            if s >= 16:
+                # matrix-core path (csrc/transform.hip k_tr16/32_mfma): two stages, each an
+                # N x N x N product issued twice (hi / lo f16 halves of every int16 operand)
+                flops = n * 2 * 2 * 2 * s ** 3
+                results[-1]["mfma_TFLOPs"] = round(flops / (ms * 1e-3) / 1e12, 2)
+                results[-1]["mfma_frac_of_2500TF_f16_dense"] = round(flops / (ms * 1e-3) / 2.5e15, 4)
+                print(json.dumps({"kernel": name, "mfma_TFLOPs": results[-1]["mfma_TFLOPs"]}), flush=True)
             del Sr, Dr, offs
     # ---------------------------------------------------------------- quant
     for s in (4, 8, 16, 32):
