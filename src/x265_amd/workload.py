@@ -262,7 +262,9 @@ def launch_class(b: Batch):
         rows = h + taps - 1 if b.op == HPS and b.params.get("rowext", 0) else h
         if b.op == HVPP:
             rows = h
-        return ("interp", b.op, taps, b.depth, 8 if w % 8 == 0 else 4 if w % 4 == 0 else 2, 4 if rows % 4 == 0 else 1)
+        vert = b.op in (VPP, VPS, VSP, VSS)
+        uh = 8 if vert and rows >= 32 and rows % 8 == 0 and w % 4 == 0 else 4 if rows % 4 == 0 else 1
+        return ("interp", b.op, taps, b.depth, 8 if w % 8 == 0 else 4 if w % 4 == 0 else 2, uh)
     return None
 
 
