@@ -279,6 +279,50 @@ __device__ __forceinline__ void vfilter_dot(const uint8_t* col, intptr_t ss, con
         }
 }
 
+// 8-bit vertical taps on packed 16-bit pairs (v_pk_mad_u16): every 8-bit
+// filter sum fits int16 (|Σ c·p| <= 255 * 88 < 2^15), so two adjacent columns
+// share each multiply-add, rows need no byte transpose, and the wrapped 16-bit
+// result equals the exact sum.  acc[r][p] holds columns (2p, 2p+1) of row r.
+template <int TAPS, int UW, int UH>
+__device__ __forceinline__ void vfilter_pk(const uint8_t* col, intptr_t ss, const s16x2 (&cpk)[TAPS],
+                                           s16x2 (&acc)[UH][UW / 2])
+{
+#pragma unroll
+    for (int r = 0; r < UH; r++)
+#pragma unroll
+        for (int p = 0; p < UW / 2; p++) acc[r][p] = (s16x2)0;
+#pragma unroll
+    for (int t = 0; t < UH + TAPS - 1; t++)
+    {
+        uint32_t w[UW / 4];
+        if constexpr (UW == 8)
+        {
+            const uint2 v = ldu<uint2>(col + t * ss);
+            w[0] = v.x;
+            w[1] = v.y;
+        }
+        else
+            w[0] = ldu<uint32_t>(col + t * ss);
+        s16x2 pr[UW / 2];
+#pragma unroll
+        for (int q = 0; q < UW / 4; q++)
+        {
+            pr[2 * q] = __builtin_bit_cast(s16x2, __builtin_amdgcn_perm(w[q], w[q], 0x0c010c00u));
+            pr[2 * q + 1] = __builtin_bit_cast(s16x2, __builtin_amdgcn_perm(w[q], w[q], 0x0c030c02u));
+        }
+#pragma unroll
+        for (int r = 0; r < UH; r++)
+        {
+            const int k = t - r;
+            if (k >= 0 && k < TAPS)
+            {
+#pragma unroll
+                for (int p = 0; p < UW / 2; p++) acc[r][p] = pr[p] * cpk[k] + acc[r][p];
+            }
+        }
+    }
+}
+
 // Grouped launches (common.h): a = src, d = dst, b = per-job coeffIdx
 // (uint8), param = is_row_ext.
 template <typename P, typename S, typename D, int OP, int TAPS, int UW, int UH>
@@ -314,8 +358,8 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_interp(const BatchGroup g)
     constexpr bool DOT = sizeof(S) == 1 && UW >= 4 && OP != X265AMD_P2S;
     int c[TAPS];
     int cp[TAPS / 4];
+    get_taps<TAPS>(cidx, c);
     if constexpr (DOT) pack_taps<TAPS>(cidx, cp);
-    else get_taps<TAPS>(cidx, c);
 
     for (int u = lane; u < units; u += G)
     {
@@ -355,8 +399,49 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_interp(const BatchGroup g)
         }
         else  // vertical: VPP, VPS, VSP, VSS
         {
-            int acc[UH][UW];
             const S* col = ps + (y0 - (TAPS / 2 - 1)) * ss + x;
+            if constexpr (DOT && (OP == X265AMD_VPP || OP == X265AMD_VPS))
+            {
+                s16x2 cpk[TAPS], pacc[UH][UW / 2];
+#pragma unroll
+                for (int k = 0; k < TAPS; k++) cpk[k] = (s16x2)(short)c[k];
+                vfilter_pk<TAPS, UW, UH>((const uint8_t*)col, ss, cpk, pacc);
+#pragma unroll
+                for (int r = 0; r < UH; r++)
+                {
+                    uint32_t o[UW / 2];
+#pragma unroll
+                    for (int p = 0; p < UW / 2; p++)
+                    {
+                        s16x2 v = pacc[r][p];
+                        if constexpr (OP == X265AMD_VPP)
+                        {
+                            v = (v + (s16x2)32) >> (s16x2)6;
+                            v = __builtin_elementwise_min(__builtin_elementwise_max(v, (s16x2)0), (s16x2)255);
+                        }
+                        else
+                            v = v - (s16x2)8192;       // ps at 8-bit: shift 0, offset -IF_INTERNAL_OFFS
+                        o[p] = __builtin_bit_cast(uint32_t, v);
+                    }
+                    D* out = pd + (y0 + r) * ds + x;
+                    if constexpr (OP == X265AMD_VPP)
+                    {
+                        // two pairs -> four pixels per dword
+                        if constexpr (UW == 8)
+                            stu<uint2>(out, make_uint2(__builtin_amdgcn_perm(o[1], o[0], 0x06040200u),
+                                                       __builtin_amdgcn_perm(o[3], o[2], 0x06040200u)));
+                        else
+                            stu<uint32_t>(out, __builtin_amdgcn_perm(o[1], o[0], 0x06040200u));
+                    }
+                    else
+                    {
+                        if constexpr (UW == 8) stu<uint4>(out, make_uint4(o[0], o[1], o[2], o[3]));
+                        else stu<uint2>(out, make_uint2(o[0], o[1]));
+                    }
+                }
+                continue;
+            }
+            int acc[UH][UW];
             if constexpr (DOT)
                 vfilter_dot<TAPS, UW, UH>((const uint8_t*)col, ss, cp, acc);
             else
@@ -490,26 +575,27 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_hvpp(const BatchGroup g)
 
 // -------------------------------------------------------------- dispatch
 
-// kernel class of a batch: unit width x unit height, packed as uw * 16 + uh
+// kernel class of a batch: unit width x unit height, packed as uw * 32 + uh
 template <int OP, int TAPS>
-static int interp_class(int w, int h, int rowext)
+static int interp_class(int w, int h, int rowext, bool pk8)
 {
     if (w < 2 || h < 2 || w > 64 || h > 64) return -X265AMD_EINVAL;
     if constexpr (OP == X265AMD_HVPP)
     {
         if (w % 4) return -X265AMD_EINVAL;
-        return (w % 8 == 0 ? 8 : 4) * 16 + (h % 4 == 0 ? 4 : 1);
+        return (w % 8 == 0 ? 8 : 4) * 32 + (h % 4 == 0 ? 4 : 1);
     }
     const int rows = (OP == X265AMD_HPS && rowext) ? h + TAPS - 1 : h;
-    // vertical filters on tall blocks take 8-row units: UH + taps - 1 source rows
-    // per unit, so the re-read overhead drops from 11/4 to 15/8 rows per output
-    // row (measured: vpp 64x64 40% -> 46% of HBM peak; 8- and 16-row blocks stay at 4)
-    constexpr bool VERT = OP == X265AMD_VPP || OP == X265AMD_VPS || OP == X265AMD_VSP || OP == X265AMD_VSS;
-    const int uh = (VERT && rows >= 32 && rows % 8 == 0 && w % 4 == 0) ? 8 : rows % 4 ? 1 : 4;
-    if (w % 8 == 0) return 8 * 16 + uh;
-    if (w % 4 == 0) return 4 * 16 + uh;
+    // vertical filters take 16-row units on blocks of 16+ rows: UH + taps - 1
+    // source rows per unit, so the re-read overhead drops from 11/4 to 23/16
+    // rows per output row (measured, 8-bit vpp: 64x64 40% -> 55% of HBM peak,
+    // 16x16 36.5% -> 37.7%; 8-row units were worse on 8x8 and 16x16)
+    // (the packed 8-bit vpp / vps path only: its accumulators are half-size)
+    const int uh = (pk8 && rows % 16 == 0 && w % 4 == 0) ? 16 : rows % 4 ? 1 : 4;
+    if (w % 8 == 0) return 8 * 32 + uh;
+    if (w % 4 == 0) return 4 * 32 + uh;
     // 2-wide units: the chroma filters and the vertical / p2s luma paths
-    if (w % 2 == 0 && (TAPS == 4 || (OP != X265AMD_HPP && OP != X265AMD_HPS))) return 2 * 16 + uh;
+    if (w % 2 == 0 && (TAPS == 4 || (OP != X265AMD_HPP && OP != X265AMD_HPS))) return 2 * 32 + uh;
     return -X265AMD_EINVAL;
 }
 
@@ -529,19 +615,19 @@ static int launch_interp(int cls, const BatchGroup& g, uint32_t blocks, hipStrea
         for (int i = 0; i < g.count; i++)
             lds = std::max(lds, (size_t)(X265AMD_BLOCK >> g.s[i].lg) * (g.s[i].h + 7) * g.s[i].w * sizeof(int16_t));
 #define L(UW, UH) \
-    if (cls == UW * 16 + UH) \
+    if (cls == UW * 32 + UH) \
     { \
         if constexpr (OP == X265AMD_HVPP) \
         { \
             if constexpr (UW >= 4) \
                 hipLaunchKernelGGL((k_hvpp<P, UW, UH>), dim3(blocks), dim3(X265AMD_BLOCK), lds, st, g); \
         } \
-        else if constexpr ((UW >= 4 || TAPS == 4 || (OP != X265AMD_HPP && OP != X265AMD_HPS)) && (UH != 8 || VERT)) \
+        else if constexpr ((UW >= 4 || TAPS == 4 || (OP != X265AMD_HPP && OP != X265AMD_HPS)) && (UH < 8 || PK8)) \
             hipLaunchKernelGGL((k_interp<P, S, D, OP, TAPS, UW, UH>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, g); \
         return (int)hipGetLastError(); \
     }
-    constexpr bool VERT = OP == X265AMD_VPP || OP == X265AMD_VPS || OP == X265AMD_VSP || OP == X265AMD_VSS;
-    L(8, 8) L(4, 8) L(8, 4) L(8, 1) L(4, 4) L(4, 1) L(2, 4) L(2, 1)
+    constexpr bool PK8 = sizeof(S) == 1 && (OP == X265AMD_VPP || OP == X265AMD_VPS);
+    L(8, 16) L(4, 16) L(8, 4) L(8, 1) L(4, 4) L(4, 1) L(2, 4) L(2, 1)
 #undef L
     return X265AMD_EINVAL;
 }
@@ -555,7 +641,8 @@ static int grouped_interp(int depth, int count, const x265amd_interp_batch* bt, 
         if (bt[i].n < 0) return X265AMD_EINVAL;
         if (bt[i].n == 0) continue;
         if (OP == X265AMD_HVPP && !bt[i].coeff) return X265AMD_EINVAL;
-        cls[i] = interp_class<OP, TAPS>(bt[i].w, bt[i].h, bt[i].is_row_ext);
+        cls[i] = interp_class<OP, TAPS>(bt[i].w, bt[i].h, bt[i].is_row_ext,
+                                        sizeof(S) == 1 && (OP == X265AMD_VPP || OP == X265AMD_VPS));
         if (cls[i] < 0) return -cls[i];
     }
     BatchGroup proto{};
@@ -569,7 +656,7 @@ static int grouped_interp(int depth, int count, const x265amd_interp_batch* bt, 
             s.b = OP == X265AMD_P2S ? nullptr : b.coeff;
             s.w = b.w; s.h = b.h; s.n = b.n;
             s.param = OP == X265AMD_HPS ? b.is_row_ext : 0;
-            const int uw = cls[i] / 16, uh = cls[i] % 16;
+            const int uw = cls[i] / 32, uh = cls[i] % 32;
             if constexpr (OP == X265AMD_HVPP)
                 s.lg = hvpp_lg(b.w, b.h, uw, uh);
             else

@@ -262,8 +262,8 @@ def launch_class(b: Batch):
         rows = h + taps - 1 if b.op == HPS and b.params.get("rowext", 0) else h
         if b.op == HVPP:
             rows = h
-        vert = b.op in (VPP, VPS, VSP, VSS)
-        uh = 8 if vert and rows >= 32 and rows % 8 == 0 and w % 4 == 0 else 4 if rows % 4 == 0 else 1
+        pk8 = b.op in (VPP, VPS) and b.depth == 8     # csrc/interp.hip: packed 8-bit vertical path
+        uh = 16 if pk8 and rows % 16 == 0 and w % 4 == 0 else 4 if rows % 4 == 0 else 1
         return ("interp", b.op, taps, b.depth, 8 if w % 8 == 0 else 4 if w % 4 == 0 else 2, uh)
     return None
 
