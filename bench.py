@@ -1,10 +1,10 @@
 #!/usr/bin/env python3
 """bench.py — x265 1.9 primitive hot path on MI355X, census-driven.
 
-A *step* replays, for F synthetic 1080p frames resident in HBM, every
-EncoderPrimitives call the reference encoder makes per frame at
---preset medium (exact per-entry census: tests/golden/census_1080p_medium.json,
-oracle/run_census.py), as one batched gfx950 launch per (table entry, block
+A *step* replays, for F synthetic frames resident in HBM (default 1080p), every
+EncoderPrimitives call the reference encoder makes per frame at that
+resolution and preset (exact per-entry census: tests/golden/census_<H>p_<preset>
+[_main10].json, oracle/run_census.py; default 1080p medium), as one batched gfx950 launch per (table entry, block
 shape) through the C ABI (include/x265_amd.h).  Entries that stay on the CPU
 in this design (CABAC estimation, SAO, lowres init, ...) are excluded and
 listed in the output.  `value` is frames per second of that primitive
@@ -48,6 +48,8 @@ def parse():
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--depth", type=int, default=8)
+    ap.add_argument("--preset", default="medium", choices=("medium", "slow"),
+                    help="selects the census of that x265 preset (tests/golden/census_<H>p_<preset>[_main10].json)")
     ap.add_argument("--no-graph", action="store_true", help="launch eagerly instead of replaying a hipGraph")
     ap.add_argument("--no-group", action="store_true", help="one launch per batch instead of grouped multi-shape launches")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample duration")
@@ -123,6 +125,23 @@ def pmc_traffic(launch_name: str):
         return None
 
 
+def pick_census(args):
+    """The reference encoder's per-frame call census for this resolution / preset / depth.
+
+    Falls back to the 1080p medium census scaled by the pixel ratio when no census of the
+    exact configuration has been recorded (oracle/run_census.py records them)."""
+    from src.x265_amd.workload import load_census
+
+    gold = os.path.join(ROOT, "tests", "golden")
+    name = f"census_{args.height}p_{args.preset}{'_main10' if args.depth > 8 else ''}.json"
+    for cand in (name, f"census_{args.height}p_{args.preset}.json"):
+        if os.path.exists(os.path.join(gold, cand)):
+            return load_census(os.path.join(gold, cand)), cand
+    base = load_census()
+    k = args.width * args.height / (1920 * 1080)
+    return {key: v * k for key, v in base.items()}, f"census_1080p_medium.json x {k:.3f} (pixel ratio)"
+
+
 def cpu_baseline(args, census):
     """Reference C primitives over a bounded sample of the same census workload."""
     import torch
@@ -150,7 +169,7 @@ def cpu_baseline(args, census):
             break
     fps = frames * reps / dt
     return {"value": round(fps, 3), "unit": "fps", "cores": threads, "kind": kind,
-            "sample": f"{reps} x the census workload of {frames} 1080p frames ({sum(b.n for b in bs)} calls per "
+            "sample": f"{reps} x the census workload of {frames} {args.width}x{args.height} frames ({sum(b.n for b in bs)} calls per "
                       f"pass, the same batch descriptors as the GPU path) in {dt:.1f}s on {threads} host threads "
                       f"({'x265 1.9 C primitives, oracle/_ref' if kind == 'reference' else 'oracle restatement'})",
             "mpix_per_s": round(fps * args.width * args.height / 1e6, 3)}
@@ -169,7 +188,7 @@ def main():
     from src.x265_amd.shard import RefRing
 
     prims = Primitives(device=local)
-    census = load_census()
+    census, census_name = pick_census(args)
     F = args.frames
     # GOP shard: rank r encodes frames [r*F, (r+1)*F) of the sequence
     fs = FrameSet(args.width, args.height, F, args.depth, device=f"cuda:{local}", first_frame=rank * F)
@@ -253,7 +272,9 @@ def main():
     if rank == 0:
         achieved = dominant.bytes / (dom_ms * 1e-3) / 1e9
         kname = f"{dominant.kind}:{dominant.name}"
-        traffic = pmc_traffic(dominant.name)
+        # the committed PMC summary was recorded on the default configuration only
+        default_cfg = (args.width, args.height, args.depth, args.preset, F) == (1920, 1080, 8, "medium", 8)
+        traffic = pmc_traffic(dominant.name) if default_cfg else None
         roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                     "kernel": kname, "kernel_ms": round(dom_ms, 4), "bytes_per_launch": int(dominant.bytes),
@@ -284,8 +305,8 @@ def main():
             "dtype": "u8" if args.depth == 8 else "u16",
             "data": "synthetic (src/x265_amd/synth.py), HBM-resident",
             "config": {
-                "workload": "x265-1.9 --preset medium per-frame primitive census (1080p, "
-                            "tests/golden/census_1080p_medium.json) replayed as batched gfx950 kernels; "
+                "workload": f"x265-1.9 --preset {args.preset} per-frame primitive census ({args.height}p, "
+                            f"tests/golden/{census_name}) replayed as batched gfx950 kernels; "
                             "CPU-side entries (CABAC estimates, SAO, lowres init) excluded",
                 "resolution": f"{args.width}x{args.height}", "depth": args.depth, "frames_per_step_per_gpu": F,
                 "calls_per_step_per_gpu": calls, "batches_per_step": len(batches),

@@ -30,29 +30,31 @@ def main() -> None:
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--frames", type=int, default=16)
     ap.add_argument("--preset", default="medium")
+    ap.add_argument("--depth", type=int, default=8, choices=(8, 10))
     a = ap.parse_args()
 
     from src.x265_amd.synth import SyntheticSource
 
-    exe = os.path.join(HERE, "_ref", "x265census")
+    exe = os.path.join(HERE, "_ref", "x265census" if a.depth == 8 else "x265census10")
     if not os.path.exists(exe):
-        raise SystemExit("run `make -C oracle census` first")
+        raise SystemExit(f"run `make -C oracle {'census' if a.depth == 8 else 'census10'}` first")
     with tempfile.TemporaryDirectory() as td:
         yuv = os.path.join(td, "in.yuv")
-        SyntheticSource(a.width, a.height, a.frames).write_yuv(yuv)
+        SyntheticSource(a.width, a.height, a.frames, a.depth).write_yuv(yuv)
         out = os.path.join(td, "census.json")
         env = dict(os.environ, X265_CENSUS_OUT=out)
         cmd = [exe, "--input", yuv, "--input-res", f"{a.width}x{a.height}", "--fps", "30", "--preset", a.preset,
+               *(["--input-depth", "10", "--output-depth", "10"] if a.depth == 10 else []),
                "--no-asm", "-o", os.path.join(td, "out.hevc")]
         r = subprocess.run(cmd, env=env, capture_output=True, text=True, check=True)
         counts = json.load(open(out))["counts"]
     per_frame = {k: v / a.frames for k, v in sorted(counts.items())}
-    name = f"census_{a.height}p_{a.preset}.json"
+    name = f"census_{a.height}p_{a.preset}{'' if a.depth == 8 else '_main10'}.json"
     doc = {
         "what": "calls per frame of every EncoderPrimitives slot, x265 1.9 C primitives (reference built by "
                 "oracle/Makefile), exact counts via census_main.cpp",
         "command": " ".join(["x265"] + cmd[1:2] + ["<synthetic>"] + cmd[3:]),
-        "source": f"src/x265_amd/synth.py {a.width}x{a.height} {a.frames} frames 8-bit 4:2:0",
+        "source": f"src/x265_amd/synth.py {a.width}x{a.height} {a.frames} frames {a.depth}-bit 4:2:0",
         "encoder_summary": [l for l in r.stderr.splitlines() if "encoded" in l],
         "frames": a.frames,
         "per_frame": per_frame,
