@@ -59,6 +59,9 @@ typedef struct
     uint32_t (*copy_cnt)(int, int16_t*, const int16_t*, intptr_t);
     void (*transpose)(int, void*, const void*, intptr_t);
     void (*denoise)(int16_t*, uint32_t*, const uint16_t*, int);
+    uint32_t (*tu)(int, int, int, int, int, int, int, const void*, intptr_t, const void*, intptr_t,
+                   int16_t*, intptr_t, int16_t*, void*, intptr_t);
+    void (*scan)(int, int, uint16_t*);
 } Lib;
 
 #define SYM(field, name)                                                     \
@@ -86,6 +89,7 @@ void* cb_open(const char* path)
     SYM(c1d2d_shl, "xo_cpy1Dto2D_shl"); SYM(c1d2d_shr, "xo_cpy1Dto2D_shr"); SYM(cnz, "xo_count_nonzero");
     SYM(copy_cnt, "xo_copy_cnt"); SYM(transpose, "xo_transpose");
     SYM(denoise, "xo_denoise_dct");
+    SYM(tu, "xo_tu_pipeline"); SYM(scan, "xo_scan_table");
     return L;
 }
 
@@ -446,4 +450,45 @@ int cb_denoise(void* h, int64_t n, int num, int16_t* c, const int64_t* co, uint3
     Lib* L = (Lib*)h;
     for (int64_t i = 0; i < n; i++) L->denoise(c + co[i], res_sum, offset, num);
     return 0;
+}
+
+/* f3 fused TU pipeline batch (x265amd_tu_batch); pixel offsets in elements of the library's depth */
+typedef struct
+{
+    Lib* L; int log2, luma, intra, islice, sh;
+    const char* f; intptr_t fs; const int64_t* fo; const char* p; intptr_t ps; const int64_t* po;
+    int16_t* r; intptr_t rs; const int64_t* ro; int16_t* c; const int64_t* co;
+    char* rc; intptr_t rcs; const int64_t* rco; uint32_t* sig; const uint8_t* qp; const uint8_t* scan;
+} TuCtx;
+
+static void tu_range(void* p, int64_t lo, int64_t hi)
+{
+    TuCtx* x = (TuCtx*)p;
+    const int b = x->L->depth > 8 ? 2 : 1, n = 1 << x->log2;
+    int16_t tmp[32 * 32];
+    for (int64_t i = lo; i < hi; i++)
+    {
+        int16_t* r = x->r ? x->r + x->ro[i] : tmp;
+        const intptr_t rs = x->r ? x->rs : n;
+        x->sig[i] = x->L->tu(x->log2, x->luma, x->intra, x->islice, x->sh, x->qp[i], x->scan ? x->scan[i] : 0,
+                             x->f + x->fo[i] * b, x->fs, x->p + x->po[i] * b, x->ps, r, rs, x->c + x->co[i],
+                             x->rc + x->rco[i] * b, x->rcs);
+    }
+}
+
+int cb_tu(void* h, int64_t n, int log2, int luma, int intra, int islice, int sh,
+          const void* f, intptr_t fs, const int64_t* fo, const void* p, intptr_t ps, const int64_t* po,
+          int16_t* r, intptr_t rs, const int64_t* ro, int16_t* c, const int64_t* co,
+          void* rc, intptr_t rcs, const int64_t* rco, uint32_t* sig, const uint8_t* qp, const uint8_t* scan,
+          int nthreads)
+{
+    TuCtx x = { (Lib*)h, log2, luma, intra, islice, sh, (const char*)f, fs, fo, (const char*)p, ps, po, r, rs, ro,
+                c, co, (char*)rc, rcs, rco, sig, qp, scan };
+    parallel(n, nthreads, tu_range, &x);
+    return 0;
+}
+
+void cb_scan_table(void* h, int type, int log2, uint16_t* out)
+{
+    ((Lib*)h)->scan(type, log2, out);
 }

@@ -100,6 +100,17 @@ class CpuOracle:
         self.cb.cb_denoise(_vp(self.h), _i64(len(co)), num, _p(c), _p(co), _p(rsum), _p(offset))
 
 
+    def tu(self, log2, luma, intra, islice, sh, f, fs, fo, p, ps, po, r, rs, ro, c, co, rc, rcs, rco, sig, qp, scan):
+        self.cb.cb_tu(_vp(self.h), _i64(len(fo)), log2, luma, intra, islice, sh, _p(f), _ip(fs), _p(fo), _p(p), _ip(ps),
+                      _p(po), _p(r), _ip(rs), _p(ro), _p(c), _p(co), _p(rc), _ip(rcs), _p(rco), _p(sig), _p(qp),
+                      _p(scan), self.nthreads)
+
+    def scan_table(self, typ, log2):
+        out = np.zeros(1 << (2 * log2), np.uint16)
+        self.cb.cb_scan_table(_vp(self.h), typ, log2, _p(out))
+        return out
+
+
 class CpuPrims:
     """The GPU `Primitives` call surface (src/x265_amd/native.py) executed on the
     CPU through a CpuOracle, on torch CPU tensors.  Used for bench.py's
@@ -162,3 +173,9 @@ class CpuPrims:
     def count_nonzero(self, size, c, co, r, rs, ro, cnt, stream=None):
         n = self._n
         self.orc.count_nonzero(size, n(c), n(co), n(r), rs, n(ro), n(cnt))
+
+    def tu_pipeline(self, depth, log2, luma, intra, islice, sh, f, fs, fo, p, ps, po, r, rs, ro, c, co, rc, rcs, rco,
+                    sig, qp, scan, stream=None):
+        n = self._n
+        self.orc.tu(log2, luma, intra, islice, sh, n(f), fs, n(fo), n(p), ps, n(po), n(r), rs, n(ro), n(c), n(co),
+                    n(rc), rcs, n(rco), n(sig), n(qp), n(scan))

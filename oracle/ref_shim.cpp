@@ -14,7 +14,14 @@
  */
 #include "common.h"
 #include "primitives.h"
+#include "quant.h"
+#include "cudata.h"
+#include "slice.h"
+#include "scalinglist.h"
+#include "entropy.h"
 #include "x265_oracle.h"
+
+#include <pthread.h>
 
 #include <cstdio>
 #include <cstdlib>
@@ -378,6 +385,125 @@ void xo_transpose(int n, void* d, const void* s, intptr_t ss)
 void xo_denoise_dct(int16_t* coef, uint32_t* resSum, const uint16_t* offset, int num)
 {
     tab().denoiseDct(coef, resSum, offset, num);
+}
+
+} // extern "C"
+
+/* f3: the reference's own Quant::transformNxN / invtransformNxN (quant.cpp:397-546),
+ * chained exactly as Search::residualTransformQuantIntra does (search.cpp:689-706).
+ * The Quant object is set up as the encoder sets it up for --preset medium (no RDOQ,
+ * flat scaling lists: Encoder::create -> ScalingList::init/setupQuantMatrices,
+ * Quant::init); the CU carries only the fields those functions read
+ * (cudata.h:165-197): slice (type, PPS sign hiding), prediction mode, intra
+ * directions and lossless flag.  The caller's scan type is expressed as an intra
+ * direction that getTUEntropyCodingParameters maps back to it (cudata.cpp:2038-2041). */
+namespace {
+
+struct TuQuant : public Quant
+{
+    void setQp(int ttype, int qpScaled)
+    {
+        m_qpParam[ttype].qp = MAX_INT;
+        m_qpParam[ttype].setQpParam(qpScaled);
+    }
+};
+
+struct TuContext
+{
+    ScalingList sl;
+    Entropy entropy;
+    TuQuant quant;
+    TuContext()
+    {
+        sl.init();
+        sl.m_bEnabled = false;
+        sl.m_bDataPresent = false;
+        sl.setupQuantMatrices();
+        quant.init(0, 0.0, sl, entropy);
+    }
+};
+
+pthread_once_t g_prim_once = PTHREAD_ONCE_INIT;
+void init_global_prims()
+{
+    /* Quant calls through the process-global table, as in the encoder */
+    setupCPrimitives(primitives);
+    setupAliasPrimitives(primitives);
+}
+
+} // namespace
+
+extern "C" {
+
+uint32_t xo_tu_pipeline(int log2, int is_luma, int is_intra, int i_slice, int sign_hide, int qp, int scan,
+                        const void* fenc, intptr_t fs, const void* pred, intptr_t ps,
+                        int16_t* resi, intptr_t rs, int16_t* coeff, void* recon, intptr_t rcs)
+{
+    pthread_once(&g_prim_once, init_global_prims);
+    static __thread TuContext* ctx = NULL;
+    if (!ctx) ctx = new TuContext();
+
+    PPS pps;
+    memset(&pps, 0, sizeof(pps));
+    pps.bSignHideEnabled = !!sign_hide;
+    SPS sps;
+    memset(&sps, 0, sizeof(sps));
+    sps.quadtreeTULog2MaxSize = 5;
+    Slice slice;
+    slice.m_pps = &pps;
+    slice.m_sps = &sps;
+    slice.m_sliceType = i_slice ? I_SLICE : P_SLICE;
+
+    static const uint8_t kDirOfScan[3] = { DC_IDX, 26, 10 };   /* DIAG, HOR (22..30), VER (6..14) */
+    uint8_t predMode = is_intra ? MODE_INTRA : MODE_INTER, dir = kDirOfScan[scan], bypass = 0;
+    CUData cu;
+    cu.m_slice = &slice;
+    cu.m_chromaFormat = X265_CSP_I420;
+    cu.m_hChromaShift = 1;
+    cu.m_predMode = &predMode;
+    cu.m_lumaIntraDir = &dir;
+    cu.m_chromaIntraDir = &dir;
+    cu.m_tqBypass = &bypass;
+
+    const TextType ttype = is_luma ? TEXT_LUMA : TEXT_CHROMA_U;
+    ctx->quant.setQp(ttype, qp);
+
+    /* the encoder's Yuv buffers share one stride (search.cpp:668-671): stage at stride n */
+    const int n = 1 << log2;
+    ALIGN_VAR_32(pixel, f[32 * 32]);
+    ALIGN_VAR_32(pixel, p[32 * 32]);
+    ALIGN_VAR_32(pixel, rec[32 * 32]);
+    ALIGN_VAR_32(int16_t, r[32 * 32]);
+    ALIGN_VAR_32(coeff_t, c[32 * 32]);
+    for (int y = 0; y < n; y++)
+        for (int x = 0; x < n; x++)
+        {
+            f[y * n + x] = ((const pixel*)fenc)[y * fs + x];
+            p[y * n + x] = ((const pixel*)pred)[y * ps + x];
+        }
+    const int sizeIdx = log2 - 2;
+    primitives.cu[sizeIdx].calcresidual(f, p, r, n);
+    uint32_t numSig = ctx->quant.transformNxN(cu, f, n, r, n, c, log2, ttype, 0, false);
+    if (numSig)
+    {
+        ctx->quant.invtransformNxN(cu, r, n, c, log2, ttype, !!is_intra, false, numSig);
+        primitives.cu[sizeIdx].add_ps(rec, n, p, r, n, n);
+    }
+    else
+        primitives.cu[sizeIdx].copy_pp(rec, n, p, n);
+    for (int y = 0; y < n; y++)
+        for (int x = 0; x < n; x++)
+        {
+            resi[y * rs + x] = r[y * n + x];
+            ((pixel*)recon)[y * rcs + x] = rec[y * n + x];
+        }
+    memcpy(coeff, c, sizeof(coeff_t) * n * n);
+    return numSig;
+}
+
+void xo_scan_table(int type, int log2, uint16_t* out)
+{
+    memcpy(out, g_scanOrder[type][log2 - 2], sizeof(uint16_t) << (2 * log2));
 }
 
 } // extern "C"

@@ -757,3 +757,137 @@ void xo_denoise_dct(int16_t* coef, uint32_t* resSum, const uint16_t* offset, int
         coef[i] = (int16_t)(lv < 0 ? 0 : (lv ^ sg) - sg);
     }
 }
+
+/* ===================================================================== f3
+ * Fused TU pipeline: the body of the bCheckFull branch of
+ * Search::residualTransformQuantIntra (search.cpp:668-706) without the
+ * prediction, i.e. calcresidual -> Quant::transformNxN (quant.cpp:397-491,
+ * no RDOQ / transform skip / bypass / noise reduction, flat scaling list)
+ * -> numSig ? Quant::invtransformNxN (quant.cpp:493-546) + add_ps : copy_pp. */
+
+/* HEVC scan orders (spec 6.5.3-6.5.5; x265 g_scanOrder, constants.cpp:359-456),
+ * generated rather than transcribed: coefficient groups of 4x4 are visited in
+ * the scan of the CG grid, positions inside a CG in the 4x4 scan of the same
+ * type.  type 0 = up-right diagonal, 1 = horizontal, 2 = vertical. */
+static void scan_grid(int type, int n, int* order /* n*n raster indices */)
+{
+    int k = 0;
+    if (type == 1)
+        for (int i = 0; i < n * n; i++) order[k++] = i;
+    else if (type == 2)
+        for (int i = 0; i < n * n; i++) order[k++] = (i % n) * n + i / n;
+    else
+        for (int d = 0; d <= 2 * (n - 1); d++)
+            for (int r = d < n ? d : n - 1; r >= 0 && d - r < n; r--)
+                order[k++] = r * n + (d - r);
+}
+
+void xo_scan_table(int type, int log2, uint16_t* out)
+{
+    const int n = 1 << log2, g = n >> 2;
+    int cg[64], in[16];
+    scan_grid(type, g, cg);
+    scan_grid(type, 4, in);
+    for (int c = 0; c < g * g; c++)
+        for (int i = 0; i < 16; i++)
+        {
+            const int cr = cg[c] / g, cc = cg[c] % g, r = in[i] / 4, q = in[i] % 4;
+            out[c * 16 + i] = (uint16_t)((cr * 4 + r) * n + cc * 4 + q);
+        }
+}
+
+static const int kQuantScales[6] = { 26214, 23302, 20560, 18396, 16384, 14564 };   /* scalinglist.cpp:121 */
+static const int kInvQuantScales[6] = { 40, 45, 51, 57, 64, 72 };                 /* scalinglist.cpp:122 */
+
+/* Quant::signBitHidingHDQ (quant.cpp:247-393) on one TU */
+static uint32_t sign_hide(int16_t* coeff, const int16_t* dct, const int32_t* deltaU, uint32_t numSig,
+                          const uint16_t* scan, int num)
+{
+    int last = -1;
+    for (int p = num - 1; p >= 0; p--)
+        if (coeff[scan[p]]) { last = p; break; }
+    const int cgLast = last >> 4;
+    for (int cg = cgLast; cg >= 0; cg--)
+    {
+        const int base = cg << 4, top = cg == cgLast ? (last & 15) : 15;
+        int first = -1, lastNZ = -1;
+        for (int n = 0; n <= top; n++)
+            if (coeff[scan[base + n]]) { if (first < 0) first = n; lastNZ = n; }
+        if (first < 0 || lastNZ - first < 4)       /* SBH_THRESHOLD, common.h:273 */
+            continue;
+        const int signbit = coeff[scan[base + first]] > 0 ? 0 : 1;
+        int sum = 0;
+        for (int n = first; n <= lastNZ; n++) sum += coeff[scan[base + n]];
+        if (signbit == (sum & 1))
+            continue;
+        int minCost = 0x7fffffff, minPos = -1, finalChange = 0;
+        for (int n = top; n >= 0; n--)
+        {
+            const int pos = scan[base + n];
+            int nzBelow = 0;                       /* any non-zero at scan positions < n */
+            for (int m = 0; m < n; m++) nzBelow |= coeff[scan[base + m]] != 0;
+            int cost, change = 0;
+            if (coeff[pos])
+            {
+                if (deltaU[pos] > 0) { cost = -deltaU[pos]; change = 1; }
+                else if (!nzBelow && abs(coeff[pos]) == 1) cost = 0x7fffffff;
+                else { cost = deltaU[pos]; change = -1; }
+            }
+            else if (!nzBelow)                      /* before the first non-zero */
+            {
+                if ((dct[pos] >= 0 ? 0 : 1) != signbit) cost = 0x7fffffff;
+                else { cost = -deltaU[pos]; change = 1; }
+            }
+            else { cost = -deltaU[pos]; change = 1; }
+            if (cost < minCost) { minCost = cost; finalChange = change; minPos = pos; }
+        }
+        if (coeff[minPos] == 32767 || coeff[minPos] == -32768) finalChange = -1;
+        if (!coeff[minPos]) numSig++;
+        else if (finalChange == -1 && abs(coeff[minPos]) == 1) numSig--;
+        const int sigMask = dct[minPos] < 0 ? -1 : 0;
+        coeff[minPos] = (int16_t)(coeff[minPos] + ((finalChange ^ sigMask) - sigMask));
+    }
+    return numSig;
+}
+
+uint32_t xo_tu_pipeline(int log2, int is_luma, int is_intra, int i_slice, int sign_hide_on, int qp, int scan_type,
+                        const void* fenc, intptr_t fs, const void* pred, intptr_t ps,
+                        int16_t* resi, intptr_t rs, int16_t* coeff, void* recon, intptr_t rcs)
+{
+    const int n = 1 << log2, num = n * n;
+    const int use_dst = log2 == 2 && is_luma && is_intra;
+    const int rem = qp % 6, per = qp / 6;
+    const int tshift = 15 - XO_DEPTH - log2;     /* MAX_TR_DYNAMIC_RANGE - depth - log2 */
+    int16_t dct[32 * 32], dq[32 * 32];
+    int32_t qc[32 * 32], deltaU[32 * 32];
+    uint16_t scan[32 * 32];
+
+    xo_sub_ps(n, n, resi, rs, fenc, pred, fs, ps);   /* calcresidual with per-operand strides */
+    xo_dct(use_dst ? XO_DST : XO_DCT, n, resi, dct, rs);
+    for (int i = 0; i < num; i++) qc[i] = kQuantScales[rem];
+    const int qbits = 14 + per + tshift;
+    const int add = (i_slice ? 171 : 85) << (qbits - 9);
+    uint32_t numSig = xo_quant(dct, qc, deltaU, coeff, qbits, add, num);
+    if (numSig >= 2 && sign_hide_on)
+    {
+        xo_scan_table(scan_type, log2, scan);
+        numSig = sign_hide(coeff, dct, deltaU, numSig, scan, num);
+    }
+    if (!numSig)
+    {
+        xo_copy_pp(n, n, recon, rcs, pred, ps);
+        return 0;
+    }
+    const int shift = 20 - 14 - tshift;           /* QUANT_IQUANT_SHIFT - QUANT_SHIFT - transformShift */
+    xo_dequant_normal(coeff, dq, num, kInvQuantScales[rem] << per, shift);
+    if (numSig == 1 && coeff[0] != 0 && !use_dst)
+    {
+        const int sh2 = 12 - (XO_DEPTH - 8) - 3;
+        const int dc = (((dq[0] + 1) >> 1) * 8 + (1 << (sh2 - 1))) >> sh2;
+        xo_blockfill_s(n, resi, rs, (int16_t)dc);
+    }
+    else
+        xo_dct(use_dst ? XO_IDST : XO_IDCT, n, dq, resi, rs);
+    xo_add_ps(n, n, recon, rcs, pred, resi, ps, rs);
+    return numSig;
+}

@@ -94,6 +94,18 @@ uint32_t xo_copy_cnt(int n, int16_t* coeff, const int16_t* res, intptr_t rs);
 void     xo_transpose(int n, void* d, const void* s, intptr_t ss);
 void     xo_denoise_dct(int16_t* coef, uint32_t* resSum, const uint16_t* offset, int num);
 
+/* f3 fused TU pipeline (quant.cpp:397-546 as driven by search.cpp:689-706):
+ *   resi <- fenc - pred; coeff <- quant(dct/dst(resi)) with sign hiding;
+ *   numSig ? (resi <- idct/idst(dequant(coeff)) or the DC shortcut; recon <- pred + resi)
+ *          : recon <- pred.
+ * qp is the scaled QP (qp + QP_BD_OFFSET); scan 0 diag / 1 hor / 2 ver.
+ * Returns numSig.  coeff is N*N contiguous. */
+uint32_t xo_tu_pipeline(int log2, int is_luma, int is_intra, int i_slice, int sign_hide, int qp, int scan,
+                        const void* fenc, intptr_t fs, const void* pred, intptr_t ps,
+                        int16_t* resi, intptr_t rs, int16_t* coeff, void* recon, intptr_t rcs);
+/* g_scanOrder[type][log2 - 2] (constants.cpp:445-450): scan position -> raster position */
+void     xo_scan_table(int type, int log2, uint16_t* out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,102 @@
+// transform1d.h — exact integer 1-D HEVC transforms shared by the batched
+// transform kernels (transform.hip) and the fused TU pipeline (tu.hip).
+//
+// Reference: x265_1.9/source/common/dct.cpp — partialButterfly{4,8,16,32}
+// :83-240,418-440, partialButterflyInverse* :242-416, fastForwardDst :41-61,
+// inversedst :63-81.  The even/odd decomposition below is an exact integer
+// refactoring of the matrix product (no intermediate rounding), so the
+// per-stage rounding (fwd_round / inv_round) reproduces the reference exactly.
+#pragma once
+#include "common.h"
+
+namespace x265amd {
+
+constexpr TransformMatrix kT32 = make_t32();
+
+template <int N>
+__device__ __forceinline__ constexpr int tcoef(int k, int n)
+{
+    return kT32.m[k * (32 / N)][n];
+}
+
+// forward N-point transform of x[] (exact integer), result in y[]
+template <int N>
+__device__ __forceinline__ void fwd_1d(const int (&x)[N], int (&y)[N])
+{
+    if constexpr (N == 4)
+    {
+        const int e0 = x[0] + x[3], o0 = x[0] - x[3], e1 = x[1] + x[2], o1 = x[1] - x[2];
+        y[0] = 64 * e0 + 64 * e1;
+        y[2] = 64 * e0 - 64 * e1;
+        y[1] = 83 * o0 + 36 * o1;
+        y[3] = 36 * o0 - 83 * o1;
+    }
+    else
+    {
+        int e[N / 2], o[N / 2], ye[N / 2];
+#pragma unroll
+        for (int k = 0; k < N / 2; k++) { e[k] = x[k] + x[N - 1 - k]; o[k] = x[k] - x[N - 1 - k]; }
+        fwd_1d<N / 2>(e, ye);
+#pragma unroll
+        for (int m = 0; m < N / 2; m++) y[2 * m] = ye[m];
+#pragma unroll
+        for (int m = 0; m < N / 2; m++)
+        {
+            int s = 0;
+#pragma unroll
+            for (int k = 0; k < N / 2; k++) s += tcoef<N>(2 * m + 1, k) * o[k];
+            y[2 * m + 1] = s;
+        }
+    }
+}
+
+// inverse N-point transform of coefficient vector c[] (exact integer)
+template <int N>
+__device__ __forceinline__ void inv_1d(const int (&c)[N], int (&y)[N])
+{
+    if constexpr (N == 4)
+    {
+        const int o0 = 83 * c[1] + 36 * c[3], o1 = 36 * c[1] - 83 * c[3];
+        const int e0 = 64 * c[0] + 64 * c[2], e1 = 64 * c[0] - 64 * c[2];
+        y[0] = e0 + o0; y[1] = e1 + o1; y[2] = e1 - o1; y[3] = e0 - o0;
+    }
+    else
+    {
+        int ce[N / 2], e[N / 2];
+#pragma unroll
+        for (int m = 0; m < N / 2; m++) ce[m] = c[2 * m];
+        inv_1d<N / 2>(ce, e);
+#pragma unroll
+        for (int k = 0; k < N / 2; k++)
+        {
+            int o = 0;
+#pragma unroll
+            for (int m = 0; m < N / 2; m++) o += tcoef<N>(2 * m + 1, k) * c[2 * m + 1];
+            y[k] = e[k] + o;
+            y[N - 1 - k] = e[k] - o;
+        }
+    }
+}
+
+__device__ __forceinline__ int fwd_round(int s, int shift) { return (int)(int16_t)((s + (1 << (shift - 1))) >> shift); }
+__device__ __forceinline__ int inv_round(int s, int shift) { return clip16((s + (1 << (shift - 1))) >> shift); }
+
+// DST-VII 4-point (fastForwardDst / inversedst), exact integer
+__device__ __forceinline__ void dst_fwd(const int (&b)[4], int (&y)[4])
+{
+    const int c0 = b[0] + b[3], c1 = b[1] + b[3], c2 = b[0] - b[1], c3 = 74 * b[2];
+    y[0] = 29 * c0 + 55 * c1 + c3;
+    y[1] = 74 * (b[0] + b[1] - b[3]);
+    y[2] = 29 * c2 + 55 * c0 - c3;
+    y[3] = 55 * c2 - 29 * c1 + c3;
+}
+__device__ __forceinline__ void dst_inv(const int (&t)[4], int (&y)[4])
+{
+    const int c0 = t[0] + t[2], c1 = t[2] + t[3], c2 = t[0] - t[3], c3 = 74 * t[1];
+    y[0] = 29 * c0 + 55 * c1 + c3;
+    y[1] = 55 * c2 - 29 * c1 + c3;
+    y[2] = 74 * (t[0] - t[2] + t[3]);
+    y[3] = 55 * c0 + 29 * c2 - c3;
+}
+
+} // namespace x265amd

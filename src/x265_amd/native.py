@@ -36,6 +36,14 @@ class InterpBatch(C.Structure):
                 ("src_off", _vp), ("dst", _vp), ("dst_stride", _ip), ("dst_off", _vp), ("coeff", _vp)]
 
 
+class TuBatch(C.Structure):
+    _fields_ = [("log2_size", _int), ("n", _int), ("is_luma", _int), ("is_intra", _int), ("i_slice", _int),
+                ("sign_hide", _int), ("fenc", _vp), ("fenc_stride", _ip), ("fenc_off", _vp), ("pred", _vp),
+                ("pred_stride", _ip), ("pred_off", _vp), ("resi", _vp), ("resi_stride", _ip), ("resi_off", _vp),
+                ("coeff", _vp), ("coeff_off", _vp), ("recon", _vp), ("recon_stride", _ip), ("recon_off", _vp),
+                ("num_sig", _vp), ("qp", _vp), ("scan", _vp)]
+
+
 def _addr(t):
     return None if t is None else t.data_ptr()
 
@@ -185,3 +193,15 @@ class Primitives:
     def count_nonzero(self, size, c, co, r, rs, ro, cnt, stream=None):
         self._check(self.lib.x265amd_count_nonzero(size, co.numel(), _ptr(c), _ptr(co), _ptr(r), _ip(rs), _ptr(ro),
                                                    _ptr(cnt), stream or _stream()), "count_nonzero")
+
+    # -- f3 fused TU pipeline: one TuBatch per call (or an array from tu_batches)
+    def tu_pipeline(self, depth, log2, luma, intra, islice, sh, f, fs, fo, p, ps, po, r, rs, ro, c, co, rc, rcs, rco,
+                    sig, qp, scan, stream=None):
+        arr = (TuBatch * 1)()
+        arr[0] = TuBatch(log2, fo.numel(), int(luma), int(intra), int(islice), int(sh), _addr(f), fs, _addr(fo),
+                         _addr(p), ps, _addr(po), _addr(r), rs, _addr(ro), _addr(c), _addr(co), _addr(rc), rcs,
+                         _addr(rco), _addr(sig), _addr(qp), _addr(scan))
+        self.tu_pipeline_grouped(depth, arr, stream)
+
+    def tu_pipeline_grouped(self, depth, arr, stream=None):
+        self._check(self.lib.x265amd_tu_pipeline(depth, len(arr), arr, stream or _stream()), "tu_pipeline")

@@ -394,6 +394,56 @@ def case_denoise(size: int, depth: int, n: int, seed: int) -> Case:
                 dict(c=c.reshape(-1), co=co, rs=rsum, off=off), ["c", "rs"])
 
 
+def tu_scan_allowed(log2: int, luma: int, intra: int) -> bool:
+    """getTUEntropyCodingParameters (cudata.cpp:2038-2041, 4:2:0): mode-dependent
+    scans only for intra luma 4x4 / 8x8 and intra chroma 4x4"""
+    return bool(intra) and ((luma and log2 <= 3) or (not luma and log2 == 2))
+
+
+def case_tu(log2: int, luma: int, intra: int, islice: int, sign_hide: int, depth: int, n: int, seed: int) -> Case:
+    """f3 fused TU pipeline (quant.cpp:397-546 chained as search.cpp:689-706).
+    Prediction classes per job: independent random block (residuals up to
+    +-PIXEL_MAX), fenc + noise in [-6, 6] (sparse coefficients, where sign
+    hiding and the DC shortcut trigger) and fenc + noise in [-40, 40]; fenc
+    itself uses the random / min / max classes.  QP uniform over the whole
+    range of the depth (0 .. 51 + QP_BD_OFFSET)."""
+    det = Det(seed)
+    N = 1 << log2
+    pmax = (1 << depth) - 1
+    pdt = pixel_dtype(depth)
+    stride = 3 * N + 8
+    f = make_plane(det, pdt, stride, N + 8, 0, pmax + 1, 0, pmax)
+    indep = det.ints(0, pmax + 1, f.data.size).astype(np.int64)
+    near6 = np.clip(f.data.astype(np.int64) + det.ints(-6, 7, f.data.size), 0, pmax)
+    near40 = np.clip(f.data.astype(np.int64) + det.ints(-40, 41, f.data.size), 0, pmax)
+    p = np.concatenate([indep, near6, near40]).astype(pdt)
+    fo = job_offsets(det, f, n, N, N, 1)
+    kind = det.ints(0, 3, n)
+    po = fo + kind * f.data.size
+    r, rs, ro = out_slots(n, N, N, np.int16)
+    rc, rcs, rco = out_slots(n, N, N, pdt)
+    c, _, co = out_slots(n, N * N, 1, np.int16, stride=N * N, pad=0)
+    sig = np.full(n, 0xCDCDCDCD, np.uint32)
+    qp = det.ints(0, 52 + 6 * (depth - 8), n).astype(np.uint8)
+    scan = (det.ints(0, 3, n) if tu_scan_allowed(log2, luma, intra) else np.zeros(n, np.int64)).astype(np.uint8)
+    return Case("tu", dict(log2=log2, luma=luma, intra=intra, islice=islice, sh=sign_hide, depth=depth, n=n,
+                           seed=seed),
+                dict(f=f.data, fs=stride, fo=fo, p=p, ps=stride, po=po, r=r, rs=rs, ro=ro, c=c, co=co, rc=rc,
+                     rcs=rcs, rco=rco, sig=sig, qp=qp, scan=scan), ["r", "c", "rc", "sig"])
+
+
+def tu_cases(depth: int, n: int = 48):
+    """TU sizes x {luma, chroma} x {intra, inter}, sign hiding on; plus sign hiding off per size"""
+    out = []
+    for log2 in (2, 3, 4, 5):
+        for luma in (1, 0):
+            for intra in (1, 0):
+                islice = int(intra and (log2 + luma) % 2 == 0)
+                out.append(case_tu(log2, luma, intra, islice, 1, depth, n, seed_of(depth, "tu", log2, luma, intra)))
+        out.append(case_tu(log2, 1, 1, 0, 0, depth, n, seed_of(depth, "tu-nosbh", log2)))
+    return out
+
+
 # ---------------------------------------------------------------- catalogue
 def blockop_sizes(op: int):
     if op in (SUB_PS, ADD_PS, COPY_SP, COPY_PS, COPY_SS):
@@ -463,6 +513,7 @@ def all_cases(depth: int, n: int = 6, quick: bool = False):
             cases.append(case_count(size, cp, depth, n, s("cnt", size, cp)))
     for size in TU_SQ:
         cases.append(case_denoise(size, depth, n, s("dn", size)))
+    cases += tu_cases(depth)
     return cases
 
 
@@ -496,6 +547,10 @@ def run_cpu(case: Case, orc) -> dict:
         orc.count_nonzero(p["size"], b["c"], b["co"], b["r"], b["rs"], b["ro"], b["cnt"])
     elif f == "denoise":
         orc.denoise(p["size"] ** 2, b["c"], b["co"], b["rs"], b["off"])
+    elif f == "tu":
+        orc.tu(p["log2"], p["luma"], p["intra"], p["islice"], p["sh"], b["f"], b["fs"], b["fo"], b["p"], b["ps"],
+               b["po"], b["r"], b["rs"], b["ro"], b["c"], b["co"], b["rc"], b["rcs"], b["rco"], b["sig"], b["qp"],
+               b["scan"])
     else:
         raise ValueError(f)
     return {k: b[k] for k in case.outs}
@@ -545,6 +600,10 @@ def run_gpu(case: Case, prims, device="cuda") -> dict:
         prims.count_nonzero(p["size"], b["c"], b["co"], b["r"], b["rs"], b["ro"], b["cnt"])
     elif f == "denoise":
         prims.denoise_dct(p["size"] ** 2, b["c"], b["co"], b["rs"], b["off"])
+    elif f == "tu":
+        prims.tu_pipeline(d, p["log2"], p["luma"], p["intra"], p["islice"], p["sh"], b["f"], b["fs"], b["fo"], b["p"],
+                          b["ps"], b["po"], b["r"], b["rs"], b["ro"], b["c"], b["co"], b["rc"], b["rcs"], b["rco"],
+                          b["sig"], b["qp"], b["scan"])
     else:
         raise ValueError(f)
     torch.cuda.synchronize()

@@ -38,3 +38,14 @@ def native_lib():
     if not os.path.exists(b.LIB):
         b.build(verbose=False)
     return b.LIB
+
+
+@pytest.fixture(scope="session")
+def gpu_prims(native_lib):
+    """The gfx950 library on cuda:0 (GPU tests only; fails loudly without the device)."""
+    import torch
+
+    assert torch.cuda.is_available(), "GPU test needs the MI355X"
+    from src.x265_amd import Primitives
+
+    return Primitives(device=0)
