@@ -179,22 +179,6 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_trN(int n, int depth,
 // The first stage's accumulator tile feeds the second MFMA straight from
 // registers (column on the lane, rows in the registers: the second product
 // sums over its row index), so no LDS is used.
-typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
-typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-
-template <int K, typename V>
-__device__ __forceinline__ void split_hl(const int (&x)[K], V& lo, V& hi)
-{
-#pragma unroll
-    for (int j = 0; j < K; j++)
-    {
-        lo[j] = (_Float16)(uint16_t)(x[j] & 2047);
-        hi[j] = (_Float16)(int16_t)(x[j] >> 11);
-    }
-}
-
 constexpr int kTrWaves = X265AMD_BLOCK / 64;
 
 // grid of a matrix-core transform launch: enough waves to fill the chip,

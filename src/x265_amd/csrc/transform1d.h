@@ -99,4 +99,22 @@ __device__ __forceinline__ void dst_inv(const int (&t)[4], int (&y)[4])
     y[3] = 55 * c0 + 29 * c2 - c3;
 }
 
+// f16 matrix-core operand types and the exact hi/lo split of int16 operands
+// (x = hi * 2048 + lo, both exact in f16; see k_tr32_mfma in transform.hip)
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+template <int K, typename V>
+__device__ __forceinline__ void split_hl(const int (&x)[K], V& lo, V& hi)
+{
+#pragma unroll
+    for (int j = 0; j < K; j++)
+    {
+        lo[j] = (_Float16)(uint16_t)(x[j] & 2047);
+        hi[j] = (_Float16)(int16_t)(x[j] >> 11);
+    }
+}
+
 } // namespace x265amd

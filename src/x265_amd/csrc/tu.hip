@@ -84,13 +84,26 @@ constexpr ScanTabs make_scans()
 static __constant__ ScanTabs c_scan = make_scans();
 
 // s_quantScales / s_invQuantScales (scalinglist.cpp:121-122; HEVC spec 8.6.2)
+// (independent selects, so per-lane rem compiles to v_cndmask rather than branches)
 __device__ __forceinline__ int quant_scale(int rem)
 {
-    return rem == 0 ? 26214 : rem == 1 ? 23302 : rem == 2 ? 20560 : rem == 3 ? 18396 : rem == 4 ? 16384 : 14564;
+    int v = 14564;
+    v = rem == 4 ? 16384 : v;
+    v = rem == 3 ? 18396 : v;
+    v = rem == 2 ? 20560 : v;
+    v = rem == 1 ? 23302 : v;
+    v = rem == 0 ? 26214 : v;
+    return v;
 }
 __device__ __forceinline__ int inv_quant_scale(int rem)
 {
-    return rem == 0 ? 40 : rem == 1 ? 45 : rem == 2 ? 51 : rem == 3 ? 57 : rem == 4 ? 64 : 72;
+    int v = 72;
+    v = rem == 4 ? 64 : v;
+    v = rem == 3 ? 57 : v;
+    v = rem == 2 ? 51 : v;
+    v = rem == 1 ? 45 : v;
+    v = rem == 0 ? 40 : v;
+    return v;
 }
 
 // LDS exchange among the lanes of one wavefront: orders this lane's LDS
@@ -114,6 +127,115 @@ __device__ __forceinline__ int group_max(int v)
         v = o > v ? o : v;
     }
     return v;
+}
+
+// The candidate search of signBitHidingHDQ (quant.cpp:313-366) over one CG in
+// scan order, branch-free: qv / cv = quantized / DCT coefficients of scan
+// positions 0..15, mask = their significance bits, top = the highest
+// candidate position, signbit = the parity target.  Returns the position and
+// the +-1 change of the cheapest candidate (first minimum from the top, as the
+// reference's strict `<` keeps it).
+__device__ __forceinline__ void sbh_pick(const int (&qv)[16], const int (&cv)[16], uint32_t mask, int top, int signbit,
+                                         int qscale, int qadd, int qbits, int& min_n, int& change)
+{
+    const int qbits8 = qbits - 8;
+    int min_cost = 0x7fffffff;
+    min_n = 0;
+    change = 0;
+#pragma unroll
+    for (int n = 15; n >= 0; n--)
+    {
+        const int c = cv[n], q = qv[n];
+        const int tmp = (c < 0 ? -c : c) * qscale;
+        const int du = (tmp - (((tmp + qadd) >> qbits) << qbits)) >> qbits8;   // deltaU (quant_c)
+        const bool below = (mask & ((1u << n) - 1)) != 0;   // a significant coefficient before n
+        const bool one = q == 1 || q == -1;
+        const int adu = du < 0 ? -du : du;
+        // significant: +1 if deltaU > 0, else -1 (never zeroing the first significant one)
+        // not significant: +1 (before the first significant one only with the matching sign)
+        const bool blocked = q ? (!below && one && du <= 0) : (!below && (int)(c < 0) != signbit);
+        const int cost = blocked ? 0x7fffffff : (q ? -adu : -du);
+        const int ch = (q && du <= 0) ? -1 : 1;
+        const bool take = n <= top && cost < min_cost;
+        min_cost = take ? cost : min_cost;
+        change = take ? ch : change;
+        min_n = take ? n : min_n;
+    }
+}
+
+// Position of scan index n inside a 4x4 coefficient group, as a raster offset in
+// a TU of pitch N (the 4x4 scans of make_scan, folded to immediates).
+template <int N>
+__device__ __forceinline__ int cg_offset(int type, int n)
+{
+    constexpr int diag[16] = { 0, 4, 1, 8, 5, 2, 12, 9, 6, 3, 13, 10, 7, 14, 11, 15 };
+    const int v = type == 1 ? n : type == 2 ? (n & 3) * 4 + (n >> 2) : diag[n];
+    return (v >> 2) * N + (v & 3);
+}
+
+// Quant::signBitHidingHDQ (quant.cpp:247-393) over one N x N TU held in LDS by
+// a G-lane group (G >= number of coefficient groups): Q = quantized
+// coefficients (raster, modified in place), C = DCT coefficients (raster,
+// pitch N; deltaU is recomputed from them exactly as quant_c computes it),
+// lane `lane` owns the CG of scan index `lane`.  CGs are independent (each
+// decision reads and changes only its own 16 coefficients); the only TU-wide
+// input is the last significant scan position (a group max).  All 16 values
+// of a CG are loaded at once (the CG's corner from the scan table, the
+// positions inside it are immediates), so there is no serial load chain.
+// Returns the change of numSig (group-reduced, valid in every lane).
+template <int N, int G>
+__device__ __forceinline__ int sign_hide(int16_t* Q, const int16_t* C, const uint16_t* scan, int type, int lane,
+                                         int qscale, int qadd, int qbits)
+{
+    constexpr int NCG = N * N / 16;
+    static_assert(NCG <= G, "one coefficient group per lane");
+    const bool has = lane < NCG;
+    const int cg = has ? lane : 0;
+    const int corner = scan[cg * 16];            // position 0 of every 4x4 scan is the CG's corner
+    int qv[16];
+    uint32_t mask = 0;
+#pragma unroll
+    for (int n = 0; n < 16; n++)
+    {
+        qv[n] = Q[corner + cg_offset<N>(type, n)];
+        mask |= (uint32_t)(qv[n] != 0) << n;
+    }
+    if (!has) mask = 0;
+    const int last = group_max<G>(mask ? cg * 16 + 31 - __builtin_clz(mask) : -1);
+    int dsig = 0;
+    const int first = __builtin_ctz(mask | 0x10000), lastnz = 31 - __builtin_clz(mask | 1);
+    // CGs after the last significant one are all zero; the last CG's mask already
+    // stops at the last significant position (quant.cpp:264-268)
+    if (has && cg <= (last >> 4) && mask && lastnz - first >= 4)   // SBH_THRESHOLD (common.h:273)
+    {
+        int sum = 0, fq = 0;
+#pragma unroll
+        for (int n = 0; n < 16; n++)
+        {
+            sum += qv[n];
+            fq = n == first ? qv[n] : fq;
+        }
+        const int signbit = fq > 0 ? 0 : 1;
+        if (signbit != (sum & 1))
+        {
+            const int top = cg == (last >> 4) ? (last & 15) : 15;
+            int cv[16];
+#pragma unroll
+            for (int n = 0; n < 16; n++) cv[n] = C[corner + cg_offset<N>(type, n)];
+            int min_n, change;
+            sbh_pick(qv, cv, mask, top, signbit, qscale, qadd, qbits, min_n, change);
+            int qm = 0, cm = 0;
+#pragma unroll
+            for (int n = 0; n < 16; n++)
+                if (n == min_n) { qm = qv[n]; cm = cv[n]; }
+            if (qm == 32767 || qm == -32768) change = -1;
+            if (!qm) dsig++;
+            else if (change == -1 && (qm == 1 || qm == -1)) dsig--;
+            const int sm = cm < 0 ? -1 : 0;
+            Q[corner + cg_offset<N>(type, min_n)] = (int16_t)(qm + ((change ^ sm) - sm));
+        }
+    }
+    return group_sum<G>(dsig);
 }
 
 template <typename P, int N>
@@ -246,73 +368,7 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_tu(const TuArgs a)
         wave_sync();
         const int st = a.scan ? a.scan[j] : 0;
         const uint16_t* scan = N == 4 ? c_scan.s4[st] : N == 8 ? c_scan.s8[st] : N == 16 ? c_scan.s16 : c_scan.s32;
-        int last = -1;
-        for (int cg = r; cg < NCG; cg += N)
-            for (int n = 15; n >= 0; n--)
-                if (Q[scan[cg * 16 + n]]) { last = last > cg * 16 + n ? last : cg * 16 + n; break; }
-        last = group_max<N>(last);
-        const int cg_last = last >> 4;
-        const int qbits8 = qbits - 8;
-        int dsig = 0;
-        for (int cg = r; cg <= cg_last; cg += N)
-        {
-            const int base = cg << 4, top = cg == cg_last ? (last & 15) : 15;
-            int qv[16], pos[16];
-            uint32_t mask = 0;
-#pragma unroll
-            for (int n = 0; n < 16; n++)
-            {
-                pos[n] = scan[base + n];
-                qv[n] = n <= top ? Q[pos[n]] : 0;
-                mask |= (uint32_t)(qv[n] != 0) << n;
-            }
-            if (!mask) continue;
-            const int first = __builtin_ctz(mask), lastnz = 31 - __builtin_clz(mask);
-            if (lastnz - first < 4) continue;               // SBH_THRESHOLD (common.h:273)
-            int sum = 0, fq = 0;
-#pragma unroll
-            for (int n = 0; n < 16; n++)
-            {
-                sum += qv[n];                               // zeros outside [first, lastnz]
-                fq = n == first ? qv[n] : fq;
-            }
-            const int signbit = fq > 0 ? 0 : 1;
-            if (signbit == (sum & 1)) continue;
-            int min_cost = 0x7fffffff, min_n = 0, change = 0;
-#pragma unroll
-            for (int n = 15; n >= 0; n--)
-            {
-                if (n > top) continue;
-                const int c = T[pos[n]];
-                const int tmp = (c < 0 ? -c : c) * qscale;
-                const int lvl = (tmp + qadd) >> qbits;
-                const int du = (tmp - (lvl << qbits)) >> qbits8;   // deltaU (quant_c)
-                const bool below = (mask & ((1u << n) - 1)) != 0;
-                int cost, ch = 1;
-                if (qv[n])
-                {
-                    if (du > 0) cost = -du;
-                    else if (!below && (qv[n] == 1 || qv[n] == -1)) cost = 0x7fffffff;
-                    else { cost = du; ch = -1; }
-                }
-                else if (!below)
-                    cost = ((c >= 0 ? 0 : 1) != signbit) ? 0x7fffffff : -du;
-                else
-                    cost = -du;
-                if (cost < min_cost) { min_cost = cost; change = ch; min_n = n; }
-            }
-            int qm = 0, p = 0, cm = 0;
-#pragma unroll
-            for (int n = 0; n < 16; n++)
-                if (n == min_n) { qm = qv[n]; p = pos[n]; }
-            cm = T[p];
-            if (qm == 32767 || qm == -32768) change = -1;
-            if (!qm) dsig++;
-            else if (change == -1 && (qm == 1 || qm == -1)) dsig--;
-            const int sm = cm < 0 ? -1 : 0;
-            Q[p] = (int16_t)(qm + ((change ^ sm) - sm));
-        }
-        num_sig += group_sum<N>(dsig);
+        num_sig += sign_hide<N, N>(Q, T, scan, st, r, qscale, qadd, qbits);
         wave_sync();
     }
 
@@ -393,6 +449,356 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_tu(const TuArgs a)
         store_n<int16_t, N>(a.resi + a.resi_off[j] + r * a.resi_stride, res);
 }
 
+// ---------------------------------------------------------------- 32x32 on the matrix cores
+// One wavefront per TU (grid-stride over TUs, constant fragments loaded once
+// per wave).  The four transform stages are the exact f16 MFMA products of
+// k_tr32_mfma (transform.hip): the residual rows are the A operand of the
+// forward stage 1, the stage-1 accumulator feeds stage 2 from registers, and
+// the coefficient accumulator (column r = l & 31, rows (i&3) + 8(i>>2) + 4h)
+// is quantized in registers.  Sign-bit hiding maps the 64 coefficient groups
+// of a 32x32 TU onto the 64 lanes, one CG each.  Coefficients, residual and
+// reconstruction leave through 16-element row segments (two lanes per row).
+constexpr int kTuWaves = X265AMD_BLOCK / 64;
+
+template <typename P>
+__global__ __launch_bounds__(X265AMD_BLOCK) void k_tu32_mfma(const TuArgs a)
+{
+    __shared__ int16_t lds_c[kTuWaves][32 * 32];   // DCT coefficients; later the inverse output
+    __shared__ int16_t lds_q[kTuWaves][32 * 32];   // quantized coefficients
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63, r = l & 31, h = l >> 5;
+    int16_t* Cs = lds_c[w];
+    int16_t* Q = lds_q[w];
+    const int depth = a.depth, maxv = (1 << depth) - 1;
+    const int fsh1 = 4 + depth - 8, fsh2 = 11, ish2 = 12 - (depth - 8);
+    const int tshift = 15 - depth - 5;
+    const int io_row = l >> 1, io_col = 16 * (l & 1);
+
+    // constant operands (as k_tr32_mfma): stage 1 in natural k order, stage 2 in accumulator order
+    f16x8 ft1[2], ft2[2], it1[2], it2[2];
+#pragma unroll
+    for (int st = 0; st < 2; st++)
+#pragma unroll
+        for (int j = 0; j < 8; j++)
+        {
+            const int kn = 16 * st + 8 * h + j, kp = 16 * st + 8 * (j >> 2) + 4 * h + (j & 3);
+            ft1[st][j] = (_Float16)c_t32.m[r][kn];
+            ft2[st][j] = (_Float16)c_t32.m[r][kp];
+            it1[st][j] = (_Float16)c_t32.m[kn][r];
+            it2[st][j] = (_Float16)c_t32.m[kp][r];
+        }
+
+    const int64_t step = (int64_t)gridDim.x * kTuWaves;
+    for (int64_t j = (int64_t)blockIdx.x * kTuWaves + w; j < a.n; j += step)
+    {
+        const P* pf = (const P*)a.fenc + a.fenc_off[j];
+        const P* pp = (const P*)a.pred + a.pred_off[j];
+        const int qp = a.qp[j], rem = qp % 6, per = qp / 6;
+
+        // ---- forward stage 1: A = residual rows (row r, columns 16 st + 8 h + 0..7)
+        int x[2][8];
+#pragma unroll
+        for (int st = 0; st < 2; st++)
+        {
+            int f[8], p[8];
+            load_row<P, 8>(pf + r * a.fenc_stride + 16 * st + 8 * h, f);
+            load_row<P, 8>(pp + r * a.pred_stride + 16 * st + 8 * h, p);
+#pragma unroll
+            for (int k = 0; k < 8; k++) x[st][k] = f[k] - p[k];
+        }
+        f32x16 lo = {}, hi = {};
+#pragma unroll
+        for (int st = 0; st < 2; st++)
+        {
+            f16x8 xl, xh;
+            split_hl<8>(x[st], xl, xh);
+            lo = __builtin_amdgcn_mfma_f32_32x32x16_f16(xl, ft1[st], lo, 0, 0, 0);
+            hi = __builtin_amdgcn_mfma_f32_32x32x16_f16(xh, ft1[st], hi, 0, 0, 0);
+        }
+        int v[16];
+#pragma unroll
+        for (int i = 0; i < 16; i++) v[i] = fwd_round((int)hi[i] * 2048 + (int)lo[i], fsh1);
+        // ---- forward stage 2 from registers: Dst = T * U'
+        lo = f32x16{};
+        hi = f32x16{};
+#pragma unroll
+        for (int st = 0; st < 2; st++)
+        {
+            int y[8];
+#pragma unroll
+            for (int k = 0; k < 8; k++) y[k] = v[8 * st + k];
+            f16x8 xl, xh;
+            split_hl<8>(y, xl, xh);
+            lo = __builtin_amdgcn_mfma_f32_32x32x16_f16(ft2[st], xl, lo, 0, 0, 0);
+            hi = __builtin_amdgcn_mfma_f32_32x32x16_f16(ft2[st], xh, hi, 0, 0, 0);
+        }
+
+        // ---- quant in registers: coefficient (row (i&3) + 8(i>>2) + 4h, column r)
+        const int qscale = quant_scale(rem);
+        const int qbits = 14 + per + tshift;
+        const int qadd = (a.i_slice ? 171 : 85) << (qbits - 9);
+        int cnt = 0;
+#pragma unroll
+        for (int i = 0; i < 16; i++)
+        {
+            const int c = fwd_round((int)hi[i] * 2048 + (int)lo[i], fsh2);
+            const int tmp = (c < 0 ? -c : c) * qscale;
+            int lvl = (tmp + qadd) >> qbits;
+            cnt += lvl != 0;
+            lvl = c < 0 ? -lvl : lvl;
+            const int pos = ((i & 3) + 8 * (i >> 2) + 4 * h) * 32 + r;
+            Cs[pos] = (int16_t)c;
+            Q[pos] = (int16_t)clip16(lvl);
+        }
+        int num_sig = group_sum<64>(cnt);
+        wave_sync();
+        if (a.sign_hide && num_sig >= 2)
+        {
+            num_sig += sign_hide<32, 64>(Q, Cs, c_scan.s32, 0, l, qscale, qadd, qbits);
+            wave_sync();
+        }
+
+        // ---- coefficients out (16-element row segments)
+        int16_t* pc = a.coeff + a.coeff_off[j] + io_row * 32 + io_col;
+        stu<uint4>(pc, ldu<uint4>(&Q[io_row * 32 + io_col]));
+        stu<uint4>(pc + 8, ldu<uint4>(&Q[io_row * 32 + io_col + 8]));
+        if (l == 0) a.num_sig[j] = (uint32_t)num_sig;
+
+        // ---- reconstruction
+        int f[16], p[16], res[16];
+        load_row<P, 16>(pf + io_row * a.fenc_stride + io_col, f);
+        load_row<P, 16>(pp + io_row * a.pred_stride + io_col, p);
+        if (num_sig == 0)
+        {
+#pragma unroll
+            for (int k = 0; k < 16; k++) res[k] = f[k] - p[k];
+        }
+        else
+        {
+            const int scale = inv_quant_scale(rem) << per;
+            const int dsh = 20 - 14 - tshift, dadd = 1 << (dsh - 1);
+            const int q0 = Q[0];
+            if (num_sig == 1 && q0 != 0)
+            {
+                const int dq0 = clip16((q0 * scale + dadd) >> dsh);
+                const int sh2 = 12 - (depth - 8) - 3;
+                const int dc = (int16_t)((((dq0 + 1) >> 1) * 8 + (1 << (sh2 - 1))) >> sh2);
+#pragma unroll
+                for (int k = 0; k < 16; k++) res[k] = dc;
+            }
+            else
+            {
+                // inverse stage 1: A = dequantized coefficient column r (rows 16 st + 8 h + 0..7)
+                lo = f32x16{};
+                hi = f32x16{};
+#pragma unroll
+                for (int st = 0; st < 2; st++)
+                {
+                    int c[8];
+#pragma unroll
+                    for (int k = 0; k < 8; k++) c[k] = clip16((Q[(16 * st + 8 * h + k) * 32 + r] * scale + dadd) >> dsh);
+                    f16x8 xl, xh;
+                    split_hl<8>(c, xl, xh);
+                    lo = __builtin_amdgcn_mfma_f32_32x32x16_f16(xl, it1[st], lo, 0, 0, 0);
+                    hi = __builtin_amdgcn_mfma_f32_32x32x16_f16(xh, it1[st], hi, 0, 0, 0);
+                }
+#pragma unroll
+                for (int i = 0; i < 16; i++) v[i] = inv_round((int)hi[i] * 2048 + (int)lo[i], 7);
+                lo = f32x16{};
+                hi = f32x16{};
+#pragma unroll
+                for (int st = 0; st < 2; st++)
+                {
+                    int y[8];
+#pragma unroll
+                    for (int k = 0; k < 8; k++) y[k] = v[8 * st + k];
+                    f16x8 xl, xh;
+                    split_hl<8>(y, xl, xh);
+                    lo = __builtin_amdgcn_mfma_f32_32x32x16_f16(xl, it2[st], lo, 0, 0, 0);
+                    hi = __builtin_amdgcn_mfma_f32_32x32x16_f16(xh, it2[st], hi, 0, 0, 0);
+                }
+                // residual (row (i&3) + 8(i>>2) + 4h, column r) -> LDS -> row segments
+#pragma unroll
+                for (int i = 0; i < 16; i++)
+                    Cs[((i & 3) + 8 * (i >> 2) + 4 * h) * 32 + r] = (int16_t)inv_round((int)hi[i] * 2048 + (int)lo[i], ish2);
+                wave_sync();
+                load_row16<16>(&Cs[io_row * 32 + io_col], res);
+            }
+        }
+        int rec[16];
+#pragma unroll
+        for (int k = 0; k < 16; k++)
+        {
+            const int t = num_sig ? p[k] + res[k] : p[k];
+            rec[k] = t < 0 ? 0 : (t > maxv ? maxv : t);
+        }
+        store_row<P, 16>((P*)a.recon + a.recon_off[j] + io_row * a.recon_stride + io_col, rec);
+        if (a.resi) store_n<int16_t, 16>(a.resi + a.resi_off[j] + io_row * a.resi_stride + io_col, res);
+        wave_sync();                                 // LDS reuse by the next TU of this wave
+    }
+}
+
+// ---------------------------------------------------------------- 4x4: one lane per TU
+// The whole chain in registers (no LDS, no cross-lane traffic): 4x4 TUs are
+// the most frequent residual blocks and too small to share between lanes.
+// Sign-bit hiding works on the single coefficient group in scan order, the
+// scan type selecting between three immediate permutations per position.
+template <typename P>
+__global__ __launch_bounds__(X265AMD_BLOCK) void k_tu4(const TuArgs a)
+{
+    const int64_t j = (int64_t)xcd_block() * X265AMD_BLOCK + threadIdx.x;
+    if (j >= a.n) return;
+    const int depth = a.depth, maxv = (1 << depth) - 1;
+    const int qp = a.qp[j], rem = qp % 6, per = qp / 6;
+    const bool use_dst = a.is_luma && a.is_intra;
+    const int tshift = 15 - depth - 2;
+    const P* pf = (const P*)a.fenc + a.fenc_off[j];
+    const P* pp = (const P*)a.pred + a.pred_off[j];
+    int f[4][4], p[4][4], m[4][4], t[4][4];
+#pragma unroll
+    for (int r = 0; r < 4; r++)
+    {
+        load_row<P, 4>(pf + r * a.fenc_stride, f[r]);
+        load_row<P, 4>(pp + r * a.pred_stride, p[r]);
+#pragma unroll
+        for (int c = 0; c < 4; c++) m[r][c] = f[r][c] - p[r][c];
+    }
+    // forward: row i -> column i of t; row i of t -> column i of the coefficients (k_tr4)
+    const int sh1 = 1 + depth - 8;
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+    {
+        int y[4];
+        if (use_dst) dst_fwd(m[i], y); else fwd_1d<4>(m[i], y);
+#pragma unroll
+        for (int k = 0; k < 4; k++) t[k][i] = fwd_round(y[k], sh1);
+    }
+    int cf[16];                                   // DCT coefficients, raster
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+    {
+        int y[4];
+        if (use_dst) dst_fwd(t[i], y); else fwd_1d<4>(t[i], y);
+#pragma unroll
+        for (int k = 0; k < 4; k++) cf[k * 4 + i] = fwd_round(y[k], 8);
+    }
+    const int qscale = quant_scale(rem);
+    const int qbits = 14 + per + tshift;
+    const int qadd = (a.i_slice ? 171 : 85) << (qbits - 9);
+    int q[16];
+    int num_sig = 0;
+#pragma unroll
+    for (int i = 0; i < 16; i++)
+    {
+        const int c = cf[i];
+        int lvl = ((c < 0 ? -c : c) * qscale + qadd) >> qbits;
+        num_sig += lvl != 0;
+        q[i] = clip16(c < 0 ? -lvl : lvl);
+    }
+    if (a.sign_hide && num_sig >= 2)
+    {
+        constexpr int diag[16] = { 0, 4, 1, 8, 5, 2, 12, 9, 6, 3, 13, 10, 7, 14, 11, 15 };
+        constexpr int ver[16] = { 0, 4, 8, 12, 1, 5, 9, 13, 2, 6, 10, 14, 3, 7, 11, 15 };
+        const int type = a.scan ? a.scan[j] : 0;
+        int qv[16], cv[16];
+        uint32_t mask = 0;
+#pragma unroll
+        for (int n = 0; n < 16; n++)
+        {
+            qv[n] = type == 1 ? q[n] : type == 2 ? q[ver[n]] : q[diag[n]];
+            cv[n] = type == 1 ? cf[n] : type == 2 ? cf[ver[n]] : cf[diag[n]];
+            mask |= (uint32_t)(qv[n] != 0) << n;
+        }
+        const int first = __builtin_ctz(mask), top = 31 - __builtin_clz(mask);
+        int sum = 0, fq = 0;
+#pragma unroll
+        for (int n = 0; n < 16; n++) { sum += qv[n]; fq = n == first ? qv[n] : fq; }
+        const int signbit = fq > 0 ? 0 : 1;
+        if (top - first >= 4 && signbit != (sum & 1))   // SBH_THRESHOLD; parity mismatch
+        {
+            int min_n, change;
+            sbh_pick(qv, cv, mask, top, signbit, qscale, qadd, qbits, min_n, change);
+            int qm = 0, cm = 0;
+#pragma unroll
+            for (int n = 0; n < 16; n++)
+                if (n == min_n) { qm = qv[n]; cm = cv[n]; }
+            if (qm == 32767 || qm == -32768) change = -1;
+            if (!qm) num_sig++;
+            else if (change == -1 && (qm == 1 || qm == -1)) num_sig--;
+            const int sm = cm < 0 ? -1 : 0;
+            const int nv = (int16_t)(qm + ((change ^ sm) - sm));
+            const int pos = type == 1 ? min_n : type == 2 ? (min_n & 3) * 4 + (min_n >> 2) : 0;
+            int dpos = 0;
+#pragma unroll
+            for (int n = 0; n < 16; n++) dpos = n == min_n ? diag[n] : dpos;
+            const int at = type == 0 ? dpos : pos;
+#pragma unroll
+            for (int i = 0; i < 16; i++) q[i] = i == at ? nv : q[i];
+        }
+    }
+    {
+        int16_t* pc = a.coeff + a.coeff_off[j];
+        int r0[8], r1[8];
+#pragma unroll
+        for (int i = 0; i < 8; i++) { r0[i] = q[i]; r1[i] = q[8 + i]; }
+        store_row<int16_t, 8>(pc, r0);
+        store_row<int16_t, 8>(pc + 8, r1);
+        a.num_sig[j] = (uint32_t)num_sig;
+    }
+    // reconstruction: m <- residual rows
+    if (num_sig)
+    {
+        const int scale = inv_quant_scale(rem) << per;
+        const int dsh = 20 - 14 - tshift, dadd = 1 << (dsh - 1);
+        if (num_sig == 1 && q[0] != 0 && !use_dst)
+        {
+            const int dq0 = clip16((q[0] * scale + dadd) >> dsh);
+            const int sh2 = 12 - (depth - 8) - 3;
+            const int dc = (int16_t)((((dq0 + 1) >> 1) * 8 + (1 << (sh2 - 1))) >> sh2);
+#pragma unroll
+            for (int r = 0; r < 4; r++)
+#pragma unroll
+                for (int c = 0; c < 4; c++) m[r][c] = dc;
+        }
+        else
+        {
+            int d[4][4];
+#pragma unroll
+            for (int i = 0; i < 16; i++) d[i >> 2][i & 3] = clip16((q[i] * scale + dadd) >> dsh);
+            // inverse: column jx of d -> row jx of t; column jx of t -> row jx of the residual (k_tr4)
+#pragma unroll
+            for (int jx = 0; jx < 4; jx++)
+            {
+                int c[4] = { d[0][jx], d[1][jx], d[2][jx], d[3][jx] }, y[4];
+                if (use_dst) dst_inv(c, y); else inv_1d<4>(c, y);
+#pragma unroll
+                for (int k = 0; k < 4; k++) t[jx][k] = inv_round(y[k], 7);
+            }
+            const int ish2 = 12 - (depth - 8);
+#pragma unroll
+            for (int jx = 0; jx < 4; jx++)
+            {
+                int c[4] = { t[0][jx], t[1][jx], t[2][jx], t[3][jx] }, y[4];
+                if (use_dst) dst_inv(c, y); else inv_1d<4>(c, y);
+#pragma unroll
+                for (int k = 0; k < 4; k++) m[jx][k] = inv_round(y[k], ish2);
+            }
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; r++)
+    {
+        int rec[4];
+#pragma unroll
+        for (int c = 0; c < 4; c++)
+        {
+            const int v = num_sig ? p[r][c] + m[r][c] : p[r][c];
+            rec[c] = v < 0 ? 0 : (v > maxv ? maxv : v);
+        }
+        store_row<P, 4>((P*)a.recon + a.recon_off[j] + r * a.recon_stride, rec);
+        if (a.resi) store_row<int16_t, 4>(a.resi + a.resi_off[j] + r * a.resi_stride, m[r]);
+    }
+}
+
 template <typename P>
 static int launch_tu(int log2, const TuArgs& a, hipStream_t st)
 {
@@ -400,10 +806,19 @@ static int launch_tu(int log2, const TuArgs& a, hipStream_t st)
     const uint32_t blocks = (uint32_t)((a.n + X265AMD_BLOCK / N - 1) / (X265AMD_BLOCK / N));
     switch (log2)
     {
-    case 2: hipLaunchKernelGGL((k_tu<P, 4>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, a); break;
+    case 2:
+        hipLaunchKernelGGL((k_tu4<P>), dim3((uint32_t)((a.n + X265AMD_BLOCK - 1) / X265AMD_BLOCK)), dim3(X265AMD_BLOCK),
+                           0, st, a);
+        break;
     case 3: hipLaunchKernelGGL((k_tu<P, 8>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, a); break;
     case 4: hipLaunchKernelGGL((k_tu<P, 16>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, a); break;
-    case 5: hipLaunchKernelGGL((k_tu<P, 32>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, a); break;
+    case 5:
+    {
+        // one wavefront per TU, enough waves to fill the chip, each looping over TUs
+        const int64_t want = ((int64_t)a.n + kTuWaves - 1) / kTuWaves;
+        hipLaunchKernelGGL((k_tu32_mfma<P>), dim3((uint32_t)(want < 4096 ? want : 4096)), dim3(X265AMD_BLOCK), 0, st, a);
+        break;
+    }
     default: return X265AMD_EINVAL;
     }
     return (int)hipGetLastError();
