@@ -238,6 +238,34 @@ __device__ __forceinline__ int sign_hide(int16_t* Q, const int16_t* C, const uin
     return group_sum<G>(dsig);
 }
 
+// A row segment of N pixels kept packed in registers (loaded once, unpacked
+// twice: for the residual and again for the reconstruction).
+template <typename P, int N>
+struct PixRow
+{
+    static constexpr int W = (N * (int)sizeof(P) + 3) / 4;
+    uint32_t w[W];
+    __device__ __forceinline__ void load(const P* p)
+    {
+        if constexpr (W == 1) w[0] = ldu<uint32_t>(p);
+        else if constexpr (W == 2) { const uint2 v = ldu<uint2>(p); w[0] = v.x; w[1] = v.y; }
+        else
+        {
+#pragma unroll
+            for (int i = 0; i < W; i += 4)
+            {
+                const uint4 v = ldu<uint4>((const char*)p + 4 * i);
+                w[i] = v.x; w[i + 1] = v.y; w[i + 2] = v.z; w[i + 3] = v.w;
+            }
+        }
+    }
+    __device__ __forceinline__ int get(int i) const
+    {
+        if constexpr (sizeof(P) == 1) return (int)((w[i >> 2] >> (8 * (i & 3))) & 0xff);
+        else return (int)((w[i >> 1] >> (16 * (i & 1))) & 0xffff);
+    }
+};
+
 template <typename P, int N>
 __device__ __forceinline__ void load_n(const P* p, int (&o)[N])
 {
@@ -310,13 +338,11 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_tu(const TuArgs a)
     const P* pp = (const P*)a.pred + a.pred_off[j] + r * a.pred_stride;
 
     int x[N], y[N];
-    {
-        int f[N], p[N];
-        load_n<P, N>(pf, f);
-        load_n<P, N>(pp, p);
+    PixRow<P, N> frow, prow;                  // kept packed for the reconstruction
+    frow.load(pf);
+    prow.load(pp);
 #pragma unroll
-        for (int i = 0; i < N; i++) x[i] = f[i] - p[i];
-    }
+    for (int i = 0; i < N; i++) x[i] = frow.get(i) - prow.get(i);
 
     // ---- forward transform: row r -> column r of T, then row r of T -> column r of the coefficients
     const int fsh1 = LOG2 - 1 + depth - 8, fsh2 = LOG2 + 6;
@@ -388,8 +414,8 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_tu(const TuArgs a)
 
     // ---- reconstruction (invtransformNxN + add_ps, or copy_pp)
     int f[N], p[N], res[N];
-    load_n<P, N>(pf, f);                      // second touch of the TU rows: served by L2
-    load_n<P, N>(pp, p);
+#pragma unroll
+    for (int i = 0; i < N; i++) { f[i] = frow.get(i); p[i] = prow.get(i); }
     if (num_sig == 0)
     {
 #pragma unroll
@@ -493,6 +519,10 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_tu32_mfma(const TuArgs a)
         const P* pf = (const P*)a.fenc + a.fenc_off[j];
         const P* pp = (const P*)a.pred + a.pred_off[j];
         const int qp = a.qp[j], rem = qp % 6, per = qp / 6;
+        // the reconstruction's row segments, loaded with the residual's (one global round trip per TU)
+        PixRow<P, 16> fio, pio;
+        fio.load(pf + io_row * a.fenc_stride + io_col);
+        pio.load(pp + io_row * a.pred_stride + io_col);
 
         // ---- forward stage 1: A = residual rows (row r, columns 16 st + 8 h + 0..7)
         int x[2][8];
@@ -565,8 +595,8 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_tu32_mfma(const TuArgs a)
 
         // ---- reconstruction
         int f[16], p[16], res[16];
-        load_row<P, 16>(pf + io_row * a.fenc_stride + io_col, f);
-        load_row<P, 16>(pp + io_row * a.pred_stride + io_col, p);
+#pragma unroll
+        for (int k = 0; k < 16; k++) { f[k] = fio.get(k); p[k] = pio.get(k); }
         if (num_sig == 0)
         {
 #pragma unroll
