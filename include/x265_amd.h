@@ -351,6 +351,56 @@ typedef struct
 } x265amd_tu_batch;
 int x265amd_tu_pipeline(int depth, int count, const x265amd_tu_batch* batches, void* stream);
 
+/* ------------------------------------------------------------------- f1
+ * Lookahead lowres pipeline: the parts that depend only on
+ * the source pictures, batched over n frames.
+ *
+ * x265amd_lowres_init — Lowres::init's plane generation (lowres.cpp:151-162):
+ * frameInitLowres (frame_init_lowres_core, pixel.cpp:549-573) writes the four
+ * half-pel lowres planes, then extendPicBorder (pixel.cpp:908-922) pads each by
+ * margin_x / margin_y (left/right margins replicate the edge pixel, margin rows
+ * copy the extended first/last row over the whole stride).  width / lines are
+ * the lowres size rounded up to the 8x8 CU grid as Lowres::create rounds it
+ * (lowres.cpp:34-45); src_off[i] is frame i's full-resolution luma origin
+ * (PicYuv::m_picOrg[0]), plane_off[4 i + k] the origin of its lowresPlane[k]. */
+typedef struct
+{
+    int n;
+    int width, lines;
+    int margin_x, margin_y;
+    const void* src;
+    intptr_t src_stride;
+    const int64_t* src_off;
+    void* planes;
+    intptr_t lowres_stride;
+    const int64_t* plane_off;
+} x265amd_lowres_batch;
+int x265amd_lowres_init(int depth, const x265amd_lowres_batch* batch, void* stream);
+
+/* x265amd_lowres_intra — LookaheadTLD::lowresIntraEstimate (slicetype.cpp:230-330)
+ * for every 8x8 CU of n frames: intra_cost / intra_mode / lowres_cost
+ * (Lowres::intraCost, intraMode, lowresCosts[0][0]) per CU, row_satd
+ * (rowSatds[0][0]) per CU row, cost_est[2 i] / [2 i + 1] = costEst[0][0] /
+ * costEstAq[0][0] of frame i.  plane_off[i] = origin of frame i's border-extended
+ * lowresPlane[0]; inv_qscale = per-CU invQscaleFactor (AQ) or NULL.  Arrays are
+ * n * width_cu * height_cu (per CU, frame-major) / n * height_cu / 2 n; row_satd
+ * and cost_est are overwritten. */
+typedef struct
+{
+    int n;
+    int width_cu, height_cu;
+    const void* planes;
+    intptr_t lowres_stride;
+    const int64_t* plane_off;
+    const int32_t* inv_qscale;
+    int32_t* intra_cost;
+    uint8_t* intra_mode;
+    uint16_t* lowres_cost;
+    int32_t* row_satd;
+    int64_t* cost_est;
+} x265amd_lowres_intra_batch;
+int x265amd_lowres_intra(int depth, const x265amd_lowres_intra_batch* batch, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -62,6 +62,9 @@ typedef struct
     uint32_t (*tu)(int, int, int, int, int, int, int, const void*, intptr_t, const void*, intptr_t,
                    int16_t*, intptr_t, int16_t*, void*, intptr_t);
     void (*scan)(int, int, uint16_t*);
+    void (*lr_init)(int, int, const void*, intptr_t, void*, void*, void*, void*, intptr_t, int, int);
+    void (*lr_intra)(int, int, const void*, intptr_t, const int32_t*, int32_t*, uint8_t*, uint16_t*, int32_t*,
+                     int64_t*);
 } Lib;
 
 #define SYM(field, name)                                                     \
@@ -90,6 +93,7 @@ void* cb_open(const char* path)
     SYM(copy_cnt, "xo_copy_cnt"); SYM(transpose, "xo_transpose");
     SYM(denoise, "xo_denoise_dct");
     SYM(tu, "xo_tu_pipeline"); SYM(scan, "xo_scan_table");
+    SYM(lr_init, "xo_lowres_init"); SYM(lr_intra, "xo_lowres_intra");
     return L;
 }
 
@@ -491,4 +495,23 @@ int cb_tu(void* h, int64_t n, int log2, int luma, int intra, int islice, int sh,
 void cb_scan_table(void* h, int type, int log2, uint16_t* out)
 {
     ((Lib*)h)->scan(type, log2, out);
+}
+
+/* f1 lookahead lowres: per frame, plane generation then the intra estimate (x265amd_lowres_init +
+ * x265amd_lowres_intra); offsets in pixels of the library's depth */
+int cb_lowres(void* h, int n, int width, int lines, int mx, int my, const void* src, intptr_t ss, const int64_t* so,
+              void* planes, intptr_t ls, const int64_t* po, int wcu, int hcu, const int32_t* inv_q, int32_t* ic,
+              uint8_t* im, uint16_t* lc, int32_t* rs, int64_t* ce)
+{
+    Lib* L = (Lib*)h;
+    const int b = L->depth > 8 ? 2 : 1, ncu = wcu * hcu;
+    for (int f = 0; f < n; f++)
+    {
+        char* pl = (char*)planes;
+        L->lr_init(width, lines, (const char*)src + so[f] * b, ss, pl + po[4 * f] * b, pl + po[4 * f + 1] * b,
+                   pl + po[4 * f + 2] * b, pl + po[4 * f + 3] * b, ls, mx, my);
+        L->lr_intra(wcu, hcu, pl + po[4 * f] * b, ls, inv_q ? inv_q + (int64_t)f * ncu : NULL, ic + (int64_t)f * ncu,
+                    im + (int64_t)f * ncu, lc + (int64_t)f * ncu, rs + (int64_t)f * hcu, ce + 2 * f);
+    }
+    return 0;
 }

@@ -105,6 +105,10 @@ class CpuOracle:
                       _p(po), _p(r), _ip(rs), _p(ro), _p(c), _p(co), _p(rc), _ip(rcs), _p(rco), _p(sig), _p(qp),
                       _p(scan), self.nthreads)
 
+    def lowres(self, n, width, lines, mx, my, src, ss, so, planes, ls, po, wcu, hcu, inv_q, ic, im, lc, rs, ce):
+        self.cb.cb_lowres(_vp(self.h), n, width, lines, mx, my, _p(src), _ip(ss), _p(so), _p(planes), _ip(ls), _p(po),
+                          wcu, hcu, _p(inv_q), _p(ic), _p(im), _p(lc), _p(rs), _p(ce))
+
     def scan_table(self, typ, log2):
         out = np.zeros(1 << (2 * log2), np.uint16)
         self.cb.cb_scan_table(_vp(self.h), typ, log2, _p(out))

@@ -19,6 +19,8 @@
 #include "slice.h"
 #include "scalinglist.h"
 #include "entropy.h"
+#include "lowres.h"
+#include "slicetype.h"
 #include "x265_oracle.h"
 
 #include <pthread.h>
@@ -499,6 +501,42 @@ uint32_t xo_tu_pipeline(int log2, int is_luma, int is_intra, int i_slice, int si
         }
     memcpy(coeff, c, sizeof(coeff_t) * n * n);
     return numSig;
+}
+
+/* f1: the reference's own lowres plane generation — the two calls Lowres::init makes
+ * (lowres.cpp:151-162) on the planes of a Lowres allocated like Lowres::create */
+void xo_lowres_init(int width, int lines, const void* src, intptr_t ss, void* p0, void* p1, void* p2, void* p3,
+                    intptr_t ls, int mx, int my)
+{
+    pthread_once(&g_prim_once, init_global_prims);
+    primitives.frameInitLowres((const pixel*)src, (pixel*)p0, (pixel*)p1, (pixel*)p2, (pixel*)p3, ss, ls, width, lines);
+    extendPicBorder((pixel*)p0, ls, width, lines, mx, my);
+    extendPicBorder((pixel*)p1, ls, width, lines, mx, my);
+    extendPicBorder((pixel*)p2, ls, width, lines, mx, my);
+    extendPicBorder((pixel*)p3, ls, width, lines, mx, my);
+}
+
+/* f1: the reference's own LookaheadTLD::lowresIntraEstimate (slicetype.cpp:230-330) on a
+ * Lowres whose fields it reads / writes point at the caller's buffers */
+void xo_lowres_intra(int wcu, int hcu, const void* plane0, intptr_t ls, const int32_t* inv_q, int32_t* intra_cost,
+                     uint8_t* intra_mode, uint16_t* lowres_cost, int32_t* row_satd, int64_t* cost_est)
+{
+    pthread_once(&g_prim_once, init_global_prims);
+    static __thread LookaheadTLD* tld = NULL;
+    if (!tld) tld = new LookaheadTLD();
+    tld->init(wcu, hcu, wcu * hcu);
+    Lowres* lr = (Lowres*)calloc(1, sizeof(Lowres));
+    lr->lowresPlane[0] = (pixel*)plane0;
+    lr->lumaStride = ls;
+    lr->intraCost = intra_cost;
+    lr->intraMode = intra_mode;
+    lr->lowresCosts[0][0] = lowres_cost;
+    lr->rowSatds[0][0] = row_satd;
+    lr->invQscaleFactor = (int*)inv_q;
+    tld->lowresIntraEstimate(*lr);
+    cost_est[0] = lr->costEst[0][0];
+    cost_est[1] = lr->costEstAq[0][0];
+    free(lr);
 }
 
 void xo_scan_table(int type, int log2, uint16_t* out)

@@ -891,3 +891,116 @@ uint32_t xo_tu_pipeline(int log2, int is_luma, int is_intra, int i_slice, int si
     xo_add_ps(n, n, recon, rcs, pred, resi, ps, rs);
     return numSig;
 }
+
+/* ===================================================================== f1
+ * Lookahead lowres pipeline, the parts that are pure
+ * functions of the source picture: Lowres::init's plane generation and
+ * LookaheadTLD::lowresIntraEstimate. */
+
+/* g_intraFilterFlags (constants.cpp:550-556): bit N set = mode uses the filtered samples at TU size N */
+static const uint8_t kIntraFilterFlags[35] = { 0x38, 0x00, 0x38, 0x30, 0x30, 0x30, 0x30, 0x30, 0x30, 0x20, 0x00, 0x20,
+                                               0x30, 0x30, 0x30, 0x30, 0x30, 0x30, 0x38, 0x30, 0x30, 0x30, 0x30, 0x30,
+                                               0x30, 0x20, 0x00, 0x20, 0x30, 0x30, 0x30, 0x30, 0x30, 0x30, 0x38 };
+#define kIntraFilterFlags8(m) (kIntraFilterFlags[m] & 8)
+
+static void extend_border(pix* pic, intptr_t stride, int width, int height, int mx, int my)
+{
+    /* extendPicBorder (pixel.cpp:908-922) = extendRowBorder (ipfilter.cpp:59-77) + row copies */
+    for (int y = 0; y < height; y++)
+        for (int x = 0; x < mx; x++)
+        {
+            pic[y * stride - mx + x] = pic[y * stride];
+            pic[y * stride + width + x] = pic[y * stride + width - 1];
+        }
+    pix* top = pic - mx;
+    for (int y = 0; y < my; y++) memcpy(top - (y + 1) * stride, top, stride * sizeof(pix));
+    pix* bot = pic - mx + (height - 1) * stride;
+    for (int y = 0; y < my; y++) memcpy(bot + (y + 1) * stride, bot, stride * sizeof(pix));
+}
+
+void xo_lowres_init(int width, int lines, const void* src_, intptr_t ss, void* p0_, void* p1_, void* p2_, void* p3_,
+                    intptr_t ls, int mx, int my)
+{
+    /* frame_init_lowres_core (pixel.cpp:549-573): four half-pel phases of a 2:1 box downscale */
+    const pix* src = (const pix*)src_;
+    pix* d[4] = { (pix*)p0_, (pix*)p1_, (pix*)p2_, (pix*)p3_ };
+#define XO_AVG4(a, b, c, e) ((((a) + (b) + 1) >> 1) + (((c) + (e) + 1) >> 1) + 1) >> 1
+    for (int y = 0; y < lines; y++)
+    {
+        const pix* r0 = src + 2 * y * ss;
+        const pix* r1 = r0 + ss;
+        const pix* r2 = r1 + ss;
+        for (int x = 0; x < width; x++)
+        {
+            d[0][y * ls + x] = (pix)(XO_AVG4(r0[2 * x], r1[2 * x], r0[2 * x + 1], r1[2 * x + 1]));
+            d[1][y * ls + x] = (pix)(XO_AVG4(r0[2 * x + 1], r1[2 * x + 1], r0[2 * x + 2], r1[2 * x + 2]));
+            d[2][y * ls + x] = (pix)(XO_AVG4(r1[2 * x], r2[2 * x], r1[2 * x + 1], r2[2 * x + 1]));
+            d[3][y * ls + x] = (pix)(XO_AVG4(r1[2 * x + 1], r2[2 * x + 1], r1[2 * x + 2], r2[2 * x + 2]));
+        }
+    }
+#undef XO_AVG4
+    for (int k = 0; k < 4; k++) extend_border(d[k], ls, width, lines, mx, my);
+}
+
+/* slicetype.cpp:230-330 (LookaheadTLD::lowresIntraEstimate) over one frame's 8x8 lowres CUs.
+ * inv_q may be NULL (no AQ).  cost_est[0] = costEst[0][0], cost_est[1] = costEstAq[0][0]. */
+void xo_lowres_intra(int wcu, int hcu, const void* plane_, intptr_t ls, const int32_t* inv_q, int32_t* intra_cost,
+                     uint8_t* intra_mode, uint16_t* lowres_cost, int32_t* row_satd, int64_t* cost_est)
+{
+    const pix* plane = (const pix*)plane_;
+    /* (int)x265_lambda_tab[X265_LOOKAHEAD_QP], X265_LOOKAHEAD_QP = 12 + QP_BD_OFFSET (common.h:208):
+     * lambda_tab[q] = 2^(q/6 - 2) * 2^(depth - 8) (constants.cpp:31-151) -> 1 (8-bit), 16 (10-bit), 256 (12-bit) */
+    const int lambda = XO_DEPTH == 8 ? 1 : XO_DEPTH == 10 ? 16 : 256;
+    const int intra_penalty = 5 * lambda, lowres_penalty = 4;
+    int64_t est = 0, est_aq = 0;
+    pix fenc[64], pred[64], samples[33], filtered[33];
+    for (int cy = 0; cy < hcu; cy++)
+    {
+        row_satd[cy] = 0;
+        for (int cx = 0; cx < wcu; cx++)
+        {
+            const int xy = cx + cy * wcu;
+            const pix* cur = plane + 8 * cx + 8 * cy * ls;
+            for (int y = 0; y < 8; y++) memcpy(fenc + 8 * y, cur + y * ls, 8 * sizeof(pix));
+            const pix* nb = cur - ls - 1;
+            memcpy(samples, nb, 17 * sizeof(pix));
+            for (int i = 1; i <= 16; i++) samples[16 + i] = nb[i * ls];
+            xo_intra_filter(8, samples, filtered);
+            int icost = 0x7fffffff, imode = 0, cost;
+            xo_intra_pred(8, 1, pred, 8, samples, 1);                  /* DC, edge filter (8 <= 16) */
+            cost = xo_satd(8, 8, fenc, 8, pred, 8);
+            if (cost < icost) { icost = cost; imode = 1; }
+            xo_intra_pred(8, 0, pred, 8, filtered, 0);                 /* planar from the filtered samples */
+            cost = xo_satd(8, 8, fenc, 8, pred, 8);
+            if (cost < icost) { icost = cost; imode = 0; }
+            int acost = 0x7fffffff, amode = 4;
+            for (int m = 5; m < 35; m += 5)
+            {
+                xo_intra_pred(8, m, pred, 8, (kIntraFilterFlags8(m) ? filtered : samples), 1);
+                cost = xo_satd(8, 8, fenc, 8, pred, 8);
+                if (cost < acost) { acost = cost; amode = m; }
+            }
+            for (int dist = 2; dist >= 1; dist--)
+            {
+                const int lo = amode - dist, hi = amode + dist;
+                xo_intra_pred(8, lo, pred, 8, (kIntraFilterFlags8(lo) ? filtered : samples), 1);
+                cost = xo_satd(8, 8, fenc, 8, pred, 8);
+                if (cost < acost) { acost = cost; amode = lo; }
+                xo_intra_pred(8, hi, pred, 8, (kIntraFilterFlags8(hi) ? filtered : samples), 1);
+                cost = xo_satd(8, 8, fenc, 8, pred, 8);
+                if (cost < acost) { acost = cost; amode = hi; }
+            }
+            if (acost < icost) { icost = acost; imode = amode; }
+            icost += intra_penalty + lowres_penalty;
+            lowres_cost[xy] = (uint16_t)(icost < 0x3fff ? icost : 0x3fff);   /* LOWRES_COST_MASK, shift 0 */
+            intra_cost[xy] = icost;
+            intra_mode[xy] = (uint8_t)imode;
+            const int scored = (cx > 0 && cx < wcu - 1 && cy > 0 && cy < hcu - 1) || wcu <= 2 || hcu <= 2;
+            const int icost_aq = (scored && inv_q) ? ((icost * inv_q[xy] + 128) >> 8) : icost;
+            if (scored) { est += icost; est_aq += icost_aq; }
+            row_satd[cy] += icost_aq;
+        }
+    }
+    cost_est[0] = est;
+    cost_est[1] = est_aq;
+}

@@ -103,6 +103,18 @@ void     xo_denoise_dct(int16_t* coef, uint32_t* resSum, const uint16_t* offset,
 uint32_t xo_tu_pipeline(int log2, int is_luma, int is_intra, int i_slice, int sign_hide, int qp, int scan,
                         const void* fenc, intptr_t fs, const void* pred, intptr_t ps,
                         int16_t* resi, intptr_t rs, int16_t* coeff, void* recon, intptr_t rcs);
+/* f1 lookahead lowres (lowres.cpp:151-162): frameInitLowres (pixel.cpp:549-573) into the 4
+ * half-pel planes p0..p3 (stride ls, lowres width x lines, multiples of 8) then
+ * extendPicBorder (pixel.cpp:908-922) of each with margins mx, my. */
+void     xo_lowres_init(int width, int lines, const void* src, intptr_t ss, void* p0, void* p1, void* p2, void* p3,
+                        intptr_t ls, int mx, int my);
+/* LookaheadTLD::lowresIntraEstimate (slicetype.cpp:230-330) over a wcu x hcu grid of 8x8
+ * lowres CUs of plane0 (border-extended).  inv_q: per-CU invQscaleFactor or NULL.
+ * Writes intra_cost / intra_mode / lowres_cost (lowresCosts[0][0]) per CU, row_satd
+ * (rowSatds[0][0]) per CU row and cost_est[0..1] = costEst[0][0], costEstAq[0][0]. */
+void     xo_lowres_intra(int wcu, int hcu, const void* plane0, intptr_t ls, const int32_t* inv_q,
+                         int32_t* intra_cost, uint8_t* intra_mode, uint16_t* lowres_cost, int32_t* row_satd,
+                         int64_t* cost_est);
 /* g_scanOrder[type][log2 - 2] (constants.cpp:445-450): scan position -> raster position */
 void     xo_scan_table(int type, int log2, uint16_t* out);
 

@@ -346,4 +346,32 @@ __device__ __forceinline__ void store_row(P* p, const int (&v)[UW])
     }
 }
 
+// A row segment of N pixels kept packed in registers (loaded once, unpacked
+// twice: for the residual and again for the reconstruction).
+template <typename P, int N>
+struct PixRow
+{
+    static constexpr int W = (N * (int)sizeof(P) + 3) / 4;
+    uint32_t w[W];
+    __device__ __forceinline__ void load(const P* p)
+    {
+        if constexpr (W == 1) w[0] = ldu<uint32_t>(p);
+        else if constexpr (W == 2) { const uint2 v = ldu<uint2>(p); w[0] = v.x; w[1] = v.y; }
+        else
+        {
+#pragma unroll
+            for (int i = 0; i < W; i += 4)
+            {
+                const uint4 v = ldu<uint4>((const char*)p + 4 * i);
+                w[i] = v.x; w[i + 1] = v.y; w[i + 2] = v.z; w[i + 3] = v.w;
+            }
+        }
+    }
+    __device__ __forceinline__ int get(int i) const
+    {
+        if constexpr (sizeof(P) == 1) return (int)((w[i >> 2] >> (8 * (i & 3))) & 0xff);
+        else return (int)((w[i >> 1] >> (16 * (i & 1))) & 0xffff);
+    }
+};
+
 } // namespace x265amd

@@ -44,6 +44,18 @@ class TuBatch(C.Structure):
                 ("num_sig", _vp), ("qp", _vp), ("scan", _vp)]
 
 
+class LowresBatch(C.Structure):
+    _fields_ = [("n", _int), ("width", _int), ("lines", _int), ("margin_x", _int), ("margin_y", _int),
+                ("src", _vp), ("src_stride", _ip), ("src_off", _vp), ("planes", _vp), ("lowres_stride", _ip),
+                ("plane_off", _vp)]
+
+
+class LowresIntraBatch(C.Structure):
+    _fields_ = [("n", _int), ("width_cu", _int), ("height_cu", _int), ("planes", _vp), ("lowres_stride", _ip),
+                ("plane_off", _vp), ("inv_qscale", _vp), ("intra_cost", _vp), ("intra_mode", _vp),
+                ("lowres_cost", _vp), ("row_satd", _vp), ("cost_est", _vp)]
+
+
 def _addr(t):
     return None if t is None else t.data_ptr()
 
@@ -205,3 +217,13 @@ class Primitives:
 
     def tu_pipeline_grouped(self, depth, arr, stream=None):
         self._check(self.lib.x265amd_tu_pipeline(depth, len(arr), arr, stream or _stream()), "tu_pipeline")
+
+    # -- f1 lookahead lowres pipeline
+    def lowres_init(self, depth, n, width, lines, mx, my, src, ss, so, planes, ls, po, stream=None):
+        b = LowresBatch(n, width, lines, mx, my, _addr(src), ss, _addr(so), _addr(planes), ls, _addr(po))
+        self._check(self.lib.x265amd_lowres_init(depth, C.byref(b), stream or _stream()), "lowres_init")
+
+    def lowres_intra(self, depth, n, wcu, hcu, planes, ls, p0, inv_q, ic, im, lc, rs, ce, stream=None):
+        b = LowresIntraBatch(n, wcu, hcu, _addr(planes), ls, _addr(p0), _addr(inv_q), _addr(ic), _addr(im), _addr(lc),
+                             _addr(rs), _addr(ce))
+        self._check(self.lib.x265amd_lowres_intra(depth, C.byref(b), stream or _stream()), "lowres_intra")

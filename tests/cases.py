@@ -444,6 +444,61 @@ def tu_cases(depth: int, n: int = 48):
     return out
 
 
+def lowres_geometry(W: int, H: int, mx: int = 96, my: int = 80) -> dict:
+    """Lowres::create (lowres.cpp:34-45): lowres size rounded up to the 8x8 CU grid, stride =
+    W/2 + 2 margin_x rounded up to 32 (margins as PicYuv's, 64 + 32 and 64 + 16)"""
+    w2, l2 = W // 2, H // 2
+    ls = w2 + 2 * mx
+    if ls & 31:
+        ls += 32 - (ls & 31)
+    wcu, hcu = (w2 + 7) // 8, (l2 + 7) // 8
+    return dict(width=wcu * 8, lines=hcu * 8, ls=ls, wcu=wcu, hcu=hcu, mx=mx, my=my)
+
+
+def case_lowres(W: int, H: int, nframes: int, aq: bool, depth: int, seed: int) -> Case:
+    """f1: lowres planes + lowres intra estimate of `nframes` pictures W x H.  Frame content
+    alternates between uniform noise and a smoothed (box-filtered) texture so that every
+    prediction mode family wins somewhere; the whole picture buffer (margins included, which
+    the downscale of the rounded-up lowres size reads) is filled."""
+    det = Det(seed)
+    g = lowres_geometry(W, H)
+    pmax = (1 << depth) - 1
+    pdt = pixel_dtype(depth)
+    ss = 2 * g["width"] + 2 * 16
+    srows = 2 * g["lines"] + 4
+    fsize = ss * srows
+    src = np.empty(nframes * fsize, pdt)
+    for f in range(nframes):
+        v = det.ints(0, pmax + 1, fsize).reshape(srows, ss)
+        if f % 2:
+            k = np.ones(5) / 5
+            v = np.apply_along_axis(lambda r: np.convolve(r, k, mode="same"), 1, v.astype(np.float64))
+            v = np.apply_along_axis(lambda c: np.convolve(c, k, mode="same"), 0, v)
+            v = np.clip(np.rint(v), 0, pmax)
+        src[f * fsize:(f + 1) * fsize] = v.reshape(-1).astype(pdt)
+    so = np.array([f * fsize + 16 for f in range(nframes)], np.int64)
+    psize = g["ls"] * (g["lines"] + 2 * g["my"])
+    planes = np.empty(4 * nframes * psize, pdt)
+    planes.view(np.uint8)[:] = 0xCD
+    org = g["my"] * g["ls"] + g["mx"]
+    po = np.array([(4 * f + k) * psize + org for f in range(nframes) for k in range(4)], np.int64)
+    ncu = g["wcu"] * g["hcu"]
+    inv_q = det.ints(64, 512, nframes * ncu).astype(np.int32) if aq else None
+    bufs = dict(src=src, ss=ss, so=so, planes=planes, po=po, inv_q=inv_q,
+                ic=np.full(nframes * ncu, -1, np.int32), im=np.full(nframes * ncu, 0xCD, np.uint8),
+                lc=np.full(nframes * ncu, 0xCDCD, np.uint16), rs=np.full(nframes * g["hcu"], -1, np.int32),
+                ce=np.full(2 * nframes, -1, np.int64))
+    return Case("lowres", dict(W=W, H=H, n=nframes, aq=int(aq), depth=depth, seed=seed, **g), bufs,
+                ["planes", "ic", "im", "lc", "rs", "ce"])
+
+
+def lowres_cases(depth: int):
+    return [case_lowres(64, 32, 1, False, depth, seed_of(depth, "lr", 0)),
+            case_lowres(136, 72, 2, True, depth, seed_of(depth, "lr", 1)),
+            case_lowres(200, 120, 2, False, depth, seed_of(depth, "lr", 2)),
+            case_lowres(352, 288, 2, True, depth, seed_of(depth, "lr", 3))]
+
+
 # ---------------------------------------------------------------- catalogue
 def blockop_sizes(op: int):
     if op in (SUB_PS, ADD_PS, COPY_SP, COPY_PS, COPY_SS):
@@ -514,6 +569,7 @@ def all_cases(depth: int, n: int = 6, quick: bool = False):
     for size in TU_SQ:
         cases.append(case_denoise(size, depth, n, s("dn", size)))
     cases += tu_cases(depth)
+    cases += lowres_cases(depth)
     return cases
 
 
@@ -547,6 +603,9 @@ def run_cpu(case: Case, orc) -> dict:
         orc.count_nonzero(p["size"], b["c"], b["co"], b["r"], b["rs"], b["ro"], b["cnt"])
     elif f == "denoise":
         orc.denoise(p["size"] ** 2, b["c"], b["co"], b["rs"], b["off"])
+    elif f == "lowres":
+        orc.lowres(p["n"], p["width"], p["lines"], p["mx"], p["my"], b["src"], b["ss"], b["so"], b["planes"], p["ls"],
+                   b["po"], p["wcu"], p["hcu"], b["inv_q"], b["ic"], b["im"], b["lc"], b["rs"], b["ce"])
     elif f == "tu":
         orc.tu(p["log2"], p["luma"], p["intra"], p["islice"], p["sh"], b["f"], b["fs"], b["fo"], b["p"], b["ps"],
                b["po"], b["r"], b["rs"], b["ro"], b["c"], b["co"], b["rc"], b["rcs"], b["rco"], b["sig"], b["qp"],
@@ -600,6 +659,11 @@ def run_gpu(case: Case, prims, device="cuda") -> dict:
         prims.count_nonzero(p["size"], b["c"], b["co"], b["r"], b["rs"], b["ro"], b["cnt"])
     elif f == "denoise":
         prims.denoise_dct(p["size"] ** 2, b["c"], b["co"], b["rs"], b["off"])
+    elif f == "lowres":
+        prims.lowres_init(d, p["n"], p["width"], p["lines"], p["mx"], p["my"], b["src"], b["ss"], b["so"], b["planes"],
+                          p["ls"], b["po"])
+        prims.lowres_intra(d, p["n"], p["wcu"], p["hcu"], b["planes"], p["ls"], b["po"][0::4].contiguous(), b["inv_q"],
+                           b["ic"], b["im"], b["lc"], b["rs"], b["ce"])
     elif f == "tu":
         prims.tu_pipeline(d, p["log2"], p["luma"], p["intra"], p["islice"], p["sh"], b["f"], b["fs"], b["fo"], b["p"],
                           b["ps"], b["po"], b["r"], b["rs"], b["ro"], b["c"], b["co"], b["rc"], b["rcs"], b["rco"],
