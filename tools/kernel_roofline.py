@@ -287,6 +287,69 @@ def main():
         results.append(r)
         print(json.dumps(r), flush=True)
         del F, P, off, R, RC, CO, coff, SIG, QP, SC, DC, DQ, DL, QT, qo, qb, ad, dsc, dsh
+    # ---------------------------------------------------------------- f1 lookahead lowres
+    # 8 frames per call.  lowres_init is HBM-bound: algorithmic bytes = the source rows it reads
+    # (2 lines + 1 rows of 2 width + 1 pixels) + the four padded planes it writes.  lowres_intra is
+    # compute-bound (12 predictions + 8x8 SATDs per 8x8 CU): reported as CUs/s and frames/s, with
+    # the reference's own lowresIntraEstimate (oracle/_ref) timed on one host core beside it.
+    for (Wf, Hf) in ((1920, 1080), (3840, 2160)):
+        name = f"lowres_{Hf}p"
+        if not want(name):
+            continue
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        from cases import lowres_geometry
+        g = lowres_geometry(Wf, Hf)
+        nf = 8
+        ss = 2 * g["width"] + 32
+        fsize = ss * (2 * g["lines"] + 4)
+        SRC = rand_u8(nf * fsize)
+        so = torch.arange(nf, dtype=torch.int64, device=dev) * fsize + 16
+        psize = g["ls"] * (g["lines"] + 2 * g["my"])
+        PL = torch.empty(4 * nf * psize, dtype=torch.uint8, device=dev)
+        org = g["my"] * g["ls"] + g["mx"]
+        po = torch.arange(4 * nf, dtype=torch.int64, device=dev) * psize + org
+        ncu = g["wcu"] * g["hcu"]
+        IC = torch.empty(nf * ncu, dtype=torch.int32, device=dev)
+        IM = torch.empty(nf * ncu, dtype=torch.uint8, device=dev)
+        LC = torch.empty(nf * ncu, dtype=torch.int16, device=dev)
+        RS = torch.empty(nf * g["hcu"], dtype=torch.int32, device=dev)
+        CE = torch.empty(2 * nf, dtype=torch.int64, device=dev)
+        IQ = torch.randint(128, 384, (nf * ncu,), dtype=torch.int32, device=dev)
+        ms_init = timeit(lambda: prims.lowres_init(8, nf, g["width"], g["lines"], g["mx"], g["my"], SRC, ss, so, PL,
+                                                   g["ls"], po))
+        init_bytes = nf * ((2 * g["lines"] + 1) * (2 * g["width"] + 1) + 4 * psize)
+        record(f"lowres_init_{Hf}p_x8", init_bytes, ms_init, nf)
+        p0 = po[0::4].contiguous()
+        ms_intra = timeit(lambda: prims.lowres_intra(8, nf, g["wcu"], g["hcu"], PL, g["ls"], p0, IQ, IC, IM, LC, RS,
+                                                     CE))
+        r = {"kernel": f"lowres_intra_{Hf}p_x8", "jobs": nf * ncu, "ms": round(ms_intra, 4),
+             "cu_per_s": round(nf * ncu / (ms_intra * 1e-3), 1), "frames_per_s": round(nf / (ms_intra * 1e-3), 1),
+             "bound": "valu (12 predictions + 8x8 SATD per CU)"}
+        try:
+            import time as _t
+
+            import numpy as _np
+            from pyoracle import CpuOracle, available
+            if available("ref", 8):
+                ref = CpuOracle("ref", 8)
+                pl = PL[:psize].cpu().numpy()
+                ic, im = _np.empty(ncu, _np.int32), _np.empty(ncu, _np.uint8)
+                lc, rs_, ce = _np.empty(ncu, _np.uint16), _np.empty(g["hcu"], _np.int32), _np.empty(2, _np.int64)
+                import ctypes as _C
+                lib = _C.CDLL(os.path.join(ROOT, "oracle", "_ref", "libx265ref8.so"))
+                t0 = _t.perf_counter()
+                lib.xo_lowres_intra(g["wcu"], g["hcu"], _C.c_void_p(pl.ctypes.data + org), _C.c_ssize_t(g["ls"]),
+                                    None, _C.c_void_p(ic.ctypes.data), _C.c_void_p(im.ctypes.data),
+                                    _C.c_void_p(lc.ctypes.data), _C.c_void_p(rs_.ctypes.data),
+                                    _C.c_void_p(ce.ctypes.data))
+                dt = _t.perf_counter() - t0
+                r["cpu_reference_1core_frames_per_s"] = round(1.0 / dt, 2)
+        except Exception as ex:  # the CPU leg is informational
+            r["cpu_reference_error"] = str(ex)
+        results.append(r)
+        print(json.dumps(r), flush=True)
+        del SRC, PL, IC, IM, LC, RS, CE, IQ
     if a.out:
         with open(a.out, "w") as f:
             json.dump({"hbm_peak_GBps": HBM, "working_set_GB": a.gb, "results": results}, f, indent=1)
