@@ -401,6 +401,43 @@ typedef struct
 } x265amd_lowres_intra_batch;
 int x265amd_lowres_intra(int depth, const x265amd_lowres_intra_batch* batch, void* stream);
 
+/* x265amd_lowres_pcost — CostEstimateGroup::estimateFrameCost for n P estimates
+ * (b == p1, list 0: slicetype.cpp:1977-2066) = estimateCUCost (slicetype.cpp:2068-2225)
+ * for every 8x8 CU: MVP from the right / below neighbours by SATD, the lowres HEX motion
+ * search with sub-pel refine of MotionEstimate::motionEstimate at subme 1 (motion.cpp:
+ * 571-1172) and the inter / intra choice.  CUs are visited in the reference's order
+ * inside each coop slice (rows_per_slice / num_slices as Lookahead::create sets them,
+ * slicetype.cpp:546-557; num_slices <= 1: the whole frame as one slice), so results are
+ * identical to the serial reference for that slicing.
+ * Per estimate i: fenc_off[i] = lowresPlane[0] of frame b; ref_off[4 i + k] =
+ * lowresPlane[k] of p0 (or its weighted planes); intra_cost / inv_qscale = frame b's
+ * Lowres::intraCost / invQscaleFactor (n * ncu, inv_qscale may be NULL).  mvcost points at
+ * the centre (difference 0) of the BitCost table for X265_LOOKAHEAD_QP (uint16 per qpel
+ * MV component difference, bitcost.cpp) and must cover every difference the search
+ * forms.  Outputs: mvs (2 int16 per CU: lowresMvs, qpel), mv_costs (lowresMvCosts),
+ * lowres_costs (lowresCosts[b-p0][p1-b]), row_satd (rowSatds), cost_est[2 i .. 2 i + 1]
+ * (costEst / costEstAq), intra_mbs[i] (intraMbs[b - p0]).  Slices of at most 512 rows. */
+typedef struct
+{
+    int n;
+    int width_cu, height_cu;
+    int rows_per_slice, num_slices;
+    const void* planes;
+    intptr_t lowres_stride;
+    const int64_t* fenc_off;
+    const int64_t* ref_off;
+    const int32_t* intra_cost;
+    const int32_t* inv_qscale;
+    const uint16_t* mvcost;
+    int16_t* mvs;
+    int32_t* mv_costs;
+    uint16_t* lowres_costs;
+    int32_t* row_satd;
+    int64_t* cost_est;
+    int32_t* intra_mbs;
+} x265amd_lowres_pcost_batch;
+int x265amd_lowres_pcost(int depth, const x265amd_lowres_pcost_batch* batch, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -65,6 +65,10 @@ typedef struct
     void (*lr_init)(int, int, const void*, intptr_t, void*, void*, void*, void*, intptr_t, int, int);
     void (*lr_intra)(int, int, const void*, intptr_t, const int32_t*, int32_t*, uint8_t*, uint16_t*, int32_t*,
                      int64_t*);
+    void (*lr_pcost)(int, int, int, int, const void*, const void*, const void*, const void*, const void*, intptr_t,
+                     const int32_t*, const int32_t*, const uint16_t*, int16_t*, int32_t*, uint16_t*, int32_t*, int64_t*,
+                     int32_t*);
+    void (*mvtab)(int, uint16_t*);
 } Lib;
 
 #define SYM(field, name)                                                     \
@@ -94,6 +98,7 @@ void* cb_open(const char* path)
     SYM(denoise, "xo_denoise_dct");
     SYM(tu, "xo_tu_pipeline"); SYM(scan, "xo_scan_table");
     SYM(lr_init, "xo_lowres_init"); SYM(lr_intra, "xo_lowres_intra");
+    SYM(lr_pcost, "xo_lowres_pcost"); SYM(mvtab, "xo_mvcost_table");
     return L;
 }
 
@@ -515,3 +520,21 @@ int cb_lowres(void* h, int n, int width, int lines, int mx, int my, const void* 
     }
     return 0;
 }
+
+/* f1 P-frame cost estimates (x265amd_lowres_pcost), one estimate after another */
+int cb_lowres_pcost(void* h, int n, int wcu, int hcu, int rps, int ns, const void* planes, intptr_t ls,
+                    const int64_t* fo, const int64_t* ro, const int32_t* ic, const int32_t* iq, const uint16_t* tab,
+                    int16_t* mvs, int32_t* mc, uint16_t* lc, int32_t* rs, int64_t* ce, int32_t* mbs)
+{
+    Lib* L = (Lib*)h;
+    const int b = L->depth > 8 ? 2 : 1, ncu = wcu * hcu;
+    const char* pl = (const char*)planes;
+    for (int e = 0; e < n; e++)
+        L->lr_pcost(wcu, hcu, rps, ns, pl + fo[e] * b, pl + ro[4 * e] * b, pl + ro[4 * e + 1] * b,
+                    pl + ro[4 * e + 2] * b, pl + ro[4 * e + 3] * b, ls, ic + (int64_t)e * ncu,
+                    iq ? iq + (int64_t)e * ncu : NULL, tab, mvs + 2 * (int64_t)e * ncu, mc + (int64_t)e * ncu,
+                    lc + (int64_t)e * ncu, rs + (int64_t)e * hcu, ce + 2 * e, mbs + e);
+    return 0;
+}
+
+void cb_mvcost_table(void* h, int range, uint16_t* out) { ((Lib*)h)->mvtab(range, out); }

@@ -109,6 +109,15 @@ class CpuOracle:
         self.cb.cb_lowres(_vp(self.h), n, width, lines, mx, my, _p(src), _ip(ss), _p(so), _p(planes), _ip(ls), _p(po),
                           wcu, hcu, _p(inv_q), _p(ic), _p(im), _p(lc), _p(rs), _p(ce))
 
+    def lowres_pcost(self, n, wcu, hcu, rps, ns, planes, ls, fo, ro, ic, iq, tab_centre_ptr, mvs, mc, lc, rs, ce, mbs):
+        self.cb.cb_lowres_pcost(_vp(self.h), n, wcu, hcu, rps, ns, _p(planes), _ip(ls), _p(fo), _p(ro), _p(ic), _p(iq),
+                                _vp(tab_centre_ptr), _p(mvs), _p(mc), _p(lc), _p(rs), _p(ce), _p(mbs))
+
+    def mvcost_table(self, rng):
+        out = np.zeros(2 * rng + 1, np.uint16)
+        self.cb.cb_mvcost_table(_vp(self.h), rng, _p(out))
+        return out
+
     def scan_table(self, typ, log2):
         out = np.zeros(1 << (2 * log2), np.uint16)
         self.cb.cb_scan_table(_vp(self.h), typ, log2, _p(out))

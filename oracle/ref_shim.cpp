@@ -21,6 +21,7 @@
 #include "entropy.h"
 #include "lowres.h"
 #include "slicetype.h"
+#include "bitcost.h"
 #include "x265_oracle.h"
 
 #include <pthread.h>
@@ -537,6 +538,124 @@ void xo_lowres_intra(int wcu, int hcu, const void* plane0, intptr_t ls, const in
     cost_est[0] = lr->costEst[0][0];
     cost_est[1] = lr->costEstAq[0][0];
     free(lr);
+}
+
+} // extern "C"
+
+namespace {
+struct TabBitCost : public BitCost
+{
+    const uint16_t* table(unsigned qp) { setQP(qp); return m_cost; }
+};
+struct CostGroup : public CostEstimateGroup
+{
+    CostGroup(Lookahead& l, Lowres** f) : CostEstimateGroup(l, f) {}
+    void cu(LookaheadTLD& tld, int cx, int cy, int p0, int p1, int b, bool* ds, bool last, int slice)
+    {
+        estimateCUCost(tld, cx, cy, p0, p1, b, ds, last, slice);
+    }
+    Slice& slice(int i) { return m_slice[i]; }
+};
+} // namespace
+
+extern "C" {
+
+/* the reference's BitCost table for X265_LOOKAHEAD_QP (what LookaheadTLD's MotionEstimate uses) */
+void xo_mvcost_table(int range, uint16_t* out)
+{
+    TabBitCost bc;
+    const uint16_t* c = bc.table(X265_LOOKAHEAD_QP);
+    for (int d = -range; d <= range; d++) out[range + d] = c[d];
+}
+
+/* f1: a P estimate (p0 = 0, b = p1 = 1) through the reference's own
+ * CostEstimateGroup::estimateCUCost (slicetype.cpp:2068-2225, motion search included), in the
+ * CU order and slice accounting of estimateFrameCost / processTasks (slicetype.cpp:1957-1972,
+ * 2029-2050); weighted prediction off (the caller passes the planes to search). */
+void xo_lowres_pcost(int wcu, int hcu, int rows_per_slice, int num_slices, const void* fenc_plane0,
+                     const void* r0, const void* r1, const void* r2, const void* r3, intptr_t ls,
+                     const int32_t* intra_cost, const int32_t* inv_q, const uint16_t* mvcost_centre,
+                     int16_t* mvs, int32_t* mv_costs, uint16_t* lowres_costs, int32_t* row_satd, int64_t* cost_est,
+                     int32_t* intra_mbs)
+{
+    (void)mvcost_centre;   /* the reference uses its own BitCost table */
+    pthread_once(&g_prim_once, init_global_prims);
+    x265_param* param = x265_param_alloc();
+    x265_param_default(param);
+    param->sourceWidth = 16 * wcu;
+    param->sourceHeight = 16 * hcu;
+    param->lookaheadSlices = 0;
+    param->bEnableWeightedPred = 0;
+    Lookahead* la = new Lookahead(param, NULL);
+    LookaheadTLD* tld = new LookaheadTLD();
+    tld->init(wcu, hcu, wcu * hcu);
+
+    Lowres* ref = (Lowres*)calloc(1, sizeof(Lowres));
+    Lowres* cur = (Lowres*)calloc(1, sizeof(Lowres));
+    const void* rp[4] = { r0, r1, r2, r3 };
+    for (int k = 0; k < 4; k++) ref->lowresPlane[k] = (pixel*)rp[k];
+    ref->fpelPlane[0] = ref->lowresPlane[0];
+    ref->lumaStride = ls;
+    ref->isLowres = true;
+    cur->lowresPlane[0] = (pixel*)fenc_plane0;
+    cur->fpelPlane[0] = cur->lowresPlane[0];
+    cur->lumaStride = ls;
+    cur->isLowres = true;
+    cur->intraCost = (int32_t*)intra_cost;
+    cur->invQscaleFactor = (int*)inv_q;
+    cur->lowresMvs[0][0] = (MV*)mvs;
+    cur->lowresMvCosts[0][0] = mv_costs;
+    cur->lowresCosts[1][0] = lowres_costs;
+    cur->rowSatds[1][0] = row_satd;
+    Lowres* frames[2] = { ref, cur };
+    CostGroup g(*la, frames);
+    bool ds[2] = { true, false };
+    const int p0 = 0, b = 1, p1 = 1;
+    if (num_slices < 1) { num_slices = 1; rows_per_slice = hcu; }
+    if (num_slices == 1)
+    {
+        /* serial whole-frame path: sums go straight to the frame */
+        cur->costEst[1][0] = cur->costEstAq[1][0] = 0;
+        bool last = true;
+        for (int cy = hcu - 1; cy >= 0; cy--)
+        {
+            row_satd[cy] = 0;
+            for (int cx = wcu - 1; cx >= 0; cx--) g.cu(*tld, cx, cy, p0, p1, b, ds, last, -1);
+            last = false;
+        }
+        cost_est[0] = cur->costEst[1][0];
+        cost_est[1] = cur->costEstAq[1][0];
+        *intra_mbs = cur->intraMbs[1];
+    }
+    else
+    {
+        int64_t est = 0, est_aq = 0;
+        int mbs = 0;
+        for (int i = 0; i < num_slices; i++)
+        {
+            memset(&g.slice(i), 0, sizeof(g.slice(i)));
+            const int first = rows_per_slice * i;
+            const int lastY = i == num_slices - 1 ? hcu - 1 : rows_per_slice * (i + 1) - 1;
+            bool last = true;
+            for (int cy = lastY; cy >= first; cy--)
+            {
+                row_satd[cy] = 0;
+                for (int cx = wcu - 1; cx >= 0; cx--) g.cu(*tld, cx, cy, p0, p1, b, ds, last, i);
+                last = false;
+            }
+            est += g.slice(i).costEst;
+            est_aq += g.slice(i).costEstAq;
+            mbs += g.slice(i).intraMbs;
+        }
+        cost_est[0] = est;
+        cost_est[1] = est_aq;
+        *intra_mbs = mbs;
+    }
+    free(ref);
+    free(cur);
+    delete tld;
+    delete la;
+    x265_param_free(param);
 }
 
 void xo_scan_table(int type, int log2, uint16_t* out)

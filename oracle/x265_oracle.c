@@ -16,6 +16,7 @@
  */
 #include "x265_oracle.h"
 
+#include <math.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -1003,4 +1004,253 @@ void xo_lowres_intra(int wcu, int hcu, const void* plane_, intptr_t ls, const in
     }
     cost_est[0] = est;
     cost_est[1] = est_aq;
+}
+
+/* ---------------------------------------------------------------- f1: lowres motion search
+ * CostEstimateGroup::estimateFrameCost / estimateCUCost for a P estimate (b == p1, list 0
+ * only: slicetype.cpp:1977-2066, 2068-2225) with MotionEstimate::motionEstimate's lowres HEX
+ * path at subpel level 1 (motion.cpp:571-1172; LookaheadTLD sets X265_HEX_SEARCH and subme 1,
+ * slicetype.h:61-64) and BitCost's MV cost (bitcost.h:45, bitcost.cpp). */
+
+typedef struct { int x, y; } xmv;
+
+/* BitCost::setQP(X265_LOOKAHEAD_QP) table, centre at index 0: s_costs[qp][i] =
+ * min(s_bitsizes[i] * lambda + 0.5f, 2^15 - 1), s_bitsizes[i] = log(i + 1) * 2 / log(2) + 1.718f
+ * (float), s_bitsizes[0] = 0.718f (bitcost.cpp:41-86).  out has 2 * range + 1 entries. */
+void xo_mvcost_table(int range, uint16_t* out)
+{
+    const double lambda = XO_DEPTH == 8 ? 1.0 : XO_DEPTH == 10 ? 16.0 : 256.0;   /* lambda_tab[12 + QP_BD_OFFSET] */
+    const float log2_2 = 2.0f / logf(2.0f);
+    for (int i = 0; i <= range; i++)
+    {
+        const float bits = i ? logf((float)(i + 1)) * log2_2 + 1.718f : 0.718f;
+        double v = bits * lambda + 0.5f;
+        if (v > (1 << 15) - 1) v = (1 << 15) - 1;
+        out[range + i] = out[range - i] = (uint16_t)v;
+    }
+}
+
+typedef struct
+{
+    const pix* fenc;          /* 8x8 block, stride 8 */
+    const pix* ref[4];        /* lowres planes of the reference at the block origin */
+    intptr_t ls;
+    const uint16_t* tab;      /* mv cost table centre */
+    xmv mvp;
+} XoMe;
+
+static int xo_mvcost(const XoMe* m, xmv q)
+{
+    return (uint16_t)(m->tab[q.x - m->mvp.x] + m->tab[q.y - m->mvp.y]);
+}
+
+static int xo_fpel_sad(const XoMe* m, int x, int y)
+{
+    return xo_sad(8, 8, m->fenc, 8, m->ref[0] + x + y * m->ls, m->ls);
+}
+
+/* ReferencePlanes::lowresQPelCost / lowresMC (lowres.h:57-104): hpel plane or the rounded
+ * average of the two hpel planes around a qpel position */
+static int xo_qpel_cost(const XoMe* m, xmv q, int use_satd)
+{
+    pix buf[64];
+    const pix* p;
+    intptr_t ps;
+    if ((q.x | q.y) & 1)
+    {
+        const int ha = (q.y & 2) | ((q.x & 2) >> 1);
+        const pix* a = m->ref[ha] + (q.x >> 2) + (q.y >> 2) * m->ls;
+        const int qx = q.x + (q.x & 1), qy = q.y + (q.y & 1);
+        const int hb = (qy & 2) | ((qx & 2) >> 1);
+        const pix* b = m->ref[hb] + (qx >> 2) + (qy >> 2) * m->ls;
+        xo_pixelavg(8, 8, buf, 8, a, m->ls, b, m->ls);
+        p = buf;
+        ps = 8;
+    }
+    else
+    {
+        p = m->ref[(q.y & 2) | ((q.x & 2) >> 1)] + (q.x >> 2) + (q.y >> 2) * m->ls;
+        ps = m->ls;
+    }
+    return use_satd ? xo_satd(8, 8, m->fenc, 8, p, ps) : xo_sad(8, 8, m->fenc, 8, p, ps);
+}
+
+static xmv xo_clip(xmv v, xmv lo, xmv hi)
+{
+    xmv r = v;
+    if (r.x > hi.x) r.x = hi.x;
+    if (r.y > hi.y) r.y = hi.y;
+    if (r.x < lo.x) r.x = lo.x;
+    if (r.y < lo.y) r.y = lo.y;
+    return r;
+}
+
+static int xo_in_range(xmv v, xmv lo, xmv hi) { return v.x >= lo.x && v.x <= hi.x && v.y >= lo.y && v.y <= hi.y; }
+
+/* MotionEstimate::motionEstimate, lowres reference, no extra candidates, HEX search, subme 1 */
+static int xo_me_lowres(XoMe* m, xmv mvmin, xmv mvmax, xmv qmvp, int merange, xmv* out)
+{
+    static const xmv hex2[8] = { { -1, -2 }, { -2, 0 }, { -1, 2 }, { 1, 2 }, { 2, 0 }, { 1, -2 }, { -1, -2 }, { -2, 0 } };
+    static const int mod6m1[8] = { 5, 0, 1, 2, 3, 4, 5, 0 };
+    static const xmv square1[9] = { { 0, 0 }, { 0, -1 }, { 0, 1 }, { -1, 0 }, { 1, 0 }, { -1, -1 }, { -1, 1 }, { 1, -1 }, { 1, 1 } };
+    m->mvp = qmvp;
+    const xmv qmin = { mvmin.x * 4, mvmin.y * 4 }, qmax = { mvmax.x * 4, mvmax.y * 4 };
+    xmv pmv = xo_clip(qmvp, qmin, qmax);
+    const xmv bestpre = pmv;
+    const int bprecost = xo_qpel_cost(m, pmv, 0);                 /* no MV cost (motion.cpp:606) */
+    xmv bmv = { (pmv.x + 2) >> 2, (pmv.y + 2) >> 2 };
+    int bcost = bprecost;
+    if ((pmv.x | pmv.y) & 3)
+        bcost = xo_fpel_sad(m, bmv.x, bmv.y) + xo_mvcost(m, (xmv){ bmv.x * 4, bmv.y * 4 });
+    if (pmv.x || pmv.y)
+    {
+        const int c = xo_fpel_sad(m, 0, 0) + xo_mvcost(m, (xmv){ 0, 0 });
+        if (c < bcost) { bcost = c; bmv.x = bmv.y = 0; }
+    }
+    /* hexagon, radius 2 (motion.cpp:681-730), costs packed with the direction in 3 low bits */
+#define XO_HEXC(dx, dy) (xo_fpel_sad(m, bmv.x + (dx), bmv.y + (dy)) + \
+                         xo_mvcost(m, (xmv){ (bmv.x + (dx)) * 4, (bmv.y + (dy)) * 4 }))
+    {
+        int c0 = XO_HEXC(-2, 0), c1 = XO_HEXC(-1, 2), c2 = XO_HEXC(1, 2);
+        bcost <<= 3;
+        if ((c0 << 3) + 2 < bcost) bcost = (c0 << 3) + 2;
+        if ((c1 << 3) + 3 < bcost) bcost = (c1 << 3) + 3;
+        if ((c2 << 3) + 4 < bcost) bcost = (c2 << 3) + 4;
+        c0 = XO_HEXC(2, 0); c1 = XO_HEXC(1, -2); c2 = XO_HEXC(-1, -2);
+        if ((c0 << 3) + 5 < bcost) bcost = (c0 << 3) + 5;
+        if ((c1 << 3) + 6 < bcost) bcost = (c1 << 3) + 6;
+        if ((c2 << 3) + 7 < bcost) bcost = (c2 << 3) + 7;
+        if (bcost & 7)
+        {
+            int dir = (bcost & 7) - 2;
+            bmv.x += hex2[dir + 1].x; bmv.y += hex2[dir + 1].y;
+            for (int i = (merange >> 1) - 1; i > 0 && xo_in_range(bmv, mvmin, mvmax); i--)
+            {
+                c0 = XO_HEXC(hex2[dir + 0].x, hex2[dir + 0].y);
+                c1 = XO_HEXC(hex2[dir + 1].x, hex2[dir + 1].y);
+                c2 = XO_HEXC(hex2[dir + 2].x, hex2[dir + 2].y);
+                bcost &= ~7;
+                if ((c0 << 3) + 1 < bcost) bcost = (c0 << 3) + 1;
+                if ((c1 << 3) + 2 < bcost) bcost = (c1 << 3) + 2;
+                if ((c2 << 3) + 3 < bcost) bcost = (c2 << 3) + 3;
+                if (!(bcost & 7)) break;
+                dir += (bcost & 7) - 2;
+                dir = mod6m1[dir + 1];
+                bmv.x += hex2[dir + 1].x; bmv.y += hex2[dir + 1].y;
+            }
+        }
+        bcost >>= 3;
+        /* square refine */
+        int dir = 0;
+        for (int k = 1; k <= 8; k++)
+        {
+            const int c = XO_HEXC(square1[k].x, square1[k].y);
+            if (c < bcost) { bcost = c; dir = k; }
+        }
+        bmv.x += square1[dir].x; bmv.y += square1[dir].y;
+    }
+#undef XO_HEXC
+    if (bprecost < bcost) { bmv = bestpre; bcost = bprecost; }
+    else { bmv.x *= 4; bmv.y *= 4; }
+    if (!bcost)
+        bcost = xo_mvcost(m, bmv);
+    else
+    {
+        /* workload[1]: 4 SAD half-pel, then 4 SATD quarter-pel (motion.cpp:1095-1116) */
+        int bdir = 0;
+        for (int i = 1; i <= 4; i++)
+        {
+            const xmv q = { bmv.x + square1[i].x * 2, bmv.y + square1[i].y * 2 };
+            const int c = xo_qpel_cost(m, q, 0) + xo_mvcost(m, q);
+            if (c < bcost) { bcost = c; bdir = i; }
+        }
+        bmv.x += square1[bdir].x * 2; bmv.y += square1[bdir].y * 2;
+        bcost = xo_qpel_cost(m, bmv, 1) + xo_mvcost(m, bmv);
+        bdir = 0;
+        for (int i = 1; i <= 4; i++)
+        {
+            const xmv q = { bmv.x + square1[i].x, bmv.y + square1[i].y };
+            const int c = xo_qpel_cost(m, q, 1) + xo_mvcost(m, q);
+            if (c < bcost) { bcost = c; bdir = i; }
+        }
+        bmv.x += square1[bdir].x; bmv.y += square1[bdir].y;
+    }
+    *out = bmv;
+    return bcost;
+}
+
+void xo_lowres_pcost(int wcu, int hcu, int rows_per_slice, int num_slices, const void* fenc_plane0,
+                     const void* r0, const void* r1, const void* r2, const void* r3, intptr_t ls,
+                     const int32_t* intra_cost, const int32_t* inv_q, const uint16_t* mvcost_centre,
+                     int16_t* mvs, int32_t* mv_costs, uint16_t* lowres_costs, int32_t* row_satd, int64_t* cost_est,
+                     int32_t* intra_mbs)
+{
+    const pix* fp = (const pix*)fenc_plane0;
+    const pix* rp[4] = { (const pix*)r0, (const pix*)r1, (const pix*)r2, (const pix*)r3 };
+    if (num_slices < 1) { num_slices = 1; rows_per_slice = hcu; }
+    int64_t est = 0, est_aq = 0;
+    int mbs = 0;
+    for (int s = 0; s < num_slices; s++)
+    {
+        /* CostEstimateGroup::processTasks (slicetype.cpp:1957-1972) / the serial loop (:2041-2050) */
+        const int first = rows_per_slice * s;
+        const int last = s == num_slices - 1 ? hcu - 1 : rows_per_slice * (s + 1) - 1;
+        int last_row = 1;
+        for (int cy = last; cy >= first; cy--)
+        {
+            row_satd[cy] = 0;
+            for (int cx = wcu - 1; cx >= 0; cx--)
+            {
+                const int xy = cx + cy * wcu;
+                const intptr_t off = 8 * cx + 8 * cy * ls;
+                pix fenc[64];
+                for (int y = 0; y < 8; y++) memcpy(fenc + 8 * y, fp + off + y * ls, 8 * sizeof(pix));
+                XoMe m = { fenc, { rp[0] + off, rp[1] + off, rp[2] + off, rp[3] + off }, ls, mvcost_centre, { 0, 0 } };
+                const xmv mvmin = { -cx * 8 - 8, -cy * 8 - 8 };
+                const xmv mvmax = { (wcu - cx - 1) * 8 + 8, (hcu - cy - 1) * 8 + 8 };
+                xmv mvc[4];
+                int numc = 0;
+                if (cx < wcu - 1) { mvc[numc].x = mvs[2 * (xy + 1)]; mvc[numc++].y = mvs[2 * (xy + 1) + 1]; }
+                if (!last_row)
+                {
+                    mvc[numc].x = mvs[2 * (xy + wcu)]; mvc[numc++].y = mvs[2 * (xy + wcu) + 1];
+                    if (cx > 0) { mvc[numc].x = mvs[2 * (xy + wcu - 1)]; mvc[numc++].y = mvs[2 * (xy + wcu - 1) + 1]; }
+                    if (cx < wcu - 1) { mvc[numc].x = mvs[2 * (xy + wcu + 1)]; mvc[numc++].y = mvs[2 * (xy + wcu + 1) + 1]; }
+                }
+                xmv mvp = { 0, 0 };
+                if (numc)
+                {
+                    int mvpcost = 1 << 28;                                 /* MotionEstimate::COST_MAX */
+                    for (int i = 0; i < numc; i++)
+                    {
+                        const int c = xo_qpel_cost(&m, mvc[i], 1);         /* bufSATD(lowresMC(mvc)) */
+                        if (c < mvpcost) { mvpcost = c; mvp = mvc[i]; }
+                    }
+                }
+                xmv out;
+                const int fcost = xo_me_lowres(&m, mvmin, mvmax, mvp, 16, &out);   /* s_merange = 16 */
+                mvs[2 * xy] = (int16_t)out.x;
+                mvs[2 * xy + 1] = (int16_t)out.y;
+                mv_costs[xy] = fcost;
+                int bcost = 1 << 28, listused = 0;
+                if (fcost < bcost) { bcost = fcost; listused = 1; }
+                bcost += 4;                                                /* lowresPenalty */
+                if (intra_cost[xy] < bcost) { bcost = intra_cost[xy]; listused = 0; }
+                const int scored = (cx > 0 && cx < wcu - 1 && cy > 0 && cy < hcu - 1) || wcu <= 2 || hcu <= 2;
+                const int bcost_aq = (scored && inv_q) ? ((bcost * inv_q[xy] + 128) >> 8) : bcost;
+                if (scored)
+                {
+                    est += bcost;
+                    est_aq += bcost_aq;
+                    if (!listused) mbs++;
+                }
+                row_satd[cy] += bcost_aq;
+                lowres_costs[xy] = (uint16_t)((bcost < 0x3fff ? bcost : 0x3fff) | (listused << 14));
+            }
+            last_row = 0;
+        }
+    }
+    cost_est[0] = est;
+    cost_est[1] = est_aq;
+    *intra_mbs = mbs;
 }

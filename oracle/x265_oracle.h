@@ -115,6 +115,23 @@ void     xo_lowres_init(int width, int lines, const void* src, intptr_t ss, void
 void     xo_lowres_intra(int wcu, int hcu, const void* plane0, intptr_t ls, const int32_t* inv_q,
                          int32_t* intra_cost, uint8_t* intra_mode, uint16_t* lowres_cost, int32_t* row_satd,
                          int64_t* cost_est);
+/* BitCost table for X265_LOOKAHEAD_QP (bitcost.cpp): out[range + d] = cost of an MV
+ * component difference d (qpel), |d| <= range */
+void     xo_mvcost_table(int range, uint16_t* out);
+/* CostEstimateGroup::estimateFrameCost for a P estimate (b == p1, list 0): per 8x8 lowres CU
+ * the MVP choice, the lowres HEX motion search with sub-pel refine (MotionEstimate::
+ * motionEstimate) and the inter / intra decision of estimateCUCost (slicetype.cpp:2068-2225),
+ * in the reference's CU order: coefficient rows bottom-up, right to left, per coop slice
+ * (rows_per_slice / num_slices as Lookahead::create sets them; num_slices <= 1 = whole frame).
+ * fenc_plane0 = lowresPlane[0] of b; r0..r3 = the (weighted) lowres planes of p0; mvcost_centre
+ * = the BitCost table of X265_LOOKAHEAD_QP at difference 0.  Outputs per CU: mvs (qpel x, y:
+ * lowresMvs), mv_costs (lowresMvCosts), lowres_costs (lowresCosts[b-p0][p1-b]); per row
+ * row_satd; cost_est[0..1] = costEst / costEstAq; intra_mbs = intraMbs[b - p0]. */
+void     xo_lowres_pcost(int wcu, int hcu, int rows_per_slice, int num_slices, const void* fenc_plane0,
+                         const void* r0, const void* r1, const void* r2, const void* r3, intptr_t ls,
+                         const int32_t* intra_cost, const int32_t* inv_q, const uint16_t* mvcost_centre,
+                         int16_t* mvs, int32_t* mv_costs, uint16_t* lowres_costs, int32_t* row_satd,
+                         int64_t* cost_est, int32_t* intra_mbs);
 /* g_scanOrder[type][log2 - 2] (constants.cpp:445-450): scan position -> raster position */
 void     xo_scan_table(int type, int log2, uint16_t* out);
 

@@ -29,6 +29,15 @@
 
 namespace x265amd {
 
+// orders LDS writes of this wavefront before its later LDS reads (no s_barrier:
+// the pcost kernel is one wavefront per workgroup)
+__device__ __forceinline__ void wave_sync_lds()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 struct LowresArgs
 {
     const void* src;
@@ -287,6 +296,346 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_lowres_intra(const LowresIntr
     }
 }
 
+// ---------------------------------------------------------------- P-frame cost estimate
+// CostEstimateGroup::estimateFrameCost for a P estimate (b == p1, list 0 only;
+// slicetype.cpp:1977-2066) = estimateCUCost (slicetype.cpp:2068-2225) for every
+// 8x8 lowres CU: the MVP is the candidate of the right / below / below-left /
+// below-right neighbours (already searched) with the lowest SATD, then
+// MotionEstimate::motionEstimate's lowres HEX search with sub-pel refine at
+// subme 1 (motion.cpp:571-1172), then the inter / intra decision.
+//
+// The neighbour dependency (right and the row below, CUs visited bottom-up and
+// right to left within each coop slice) makes a wavefront: with x' = W-1-cx and
+// y' = (slice's last row) - cy, CU (x', y') only needs CUs of steps before
+// x' + 2 y'.  One wavefront owns one (estimate, slice); lane l owns rows
+// y' = l, l + 64, ... and at step t searches CU x' = t - 2 y' of each.  The
+// motion search itself runs inside the lane, exactly in the reference's order,
+// on packed 8-bit (v_sad_u8) / 16-bit (v_sad_u16) rows; the four MVs a row
+// needs from the row below live in a 4-entry LDS ring per row.
+constexpr int kPcostMaxRows = 512;
+
+struct PcostArgs
+{
+    const void* planes;
+    int64_t ls;
+    const int64_t* fenc_off;      // per estimate: lowresPlane[0] of b
+    const int64_t* ref_off;       // 4 per estimate: lowresPlane[0..3] of p0
+    const int32_t* intra_cost;
+    const int32_t* inv_q;
+    const uint16_t* mvcost;       // BitCost table centre (difference 0)
+    int16_t* mvs;
+    int32_t* mv_costs;
+    uint16_t* lowres_costs;
+    int32_t* row_satd;
+    int64_t* cost_est;
+    int32_t* intra_mbs;
+    int n, wcu, hcu, rps, nslices;
+};
+
+// an 8x8 block of pixels packed into dwords (2 per row at 8-bit, 4 at 16-bit)
+template <typename P>
+struct Blk8
+{
+    static constexpr int W = 8 * (int)sizeof(P) / 4;
+    uint32_t r[8][W];
+    __device__ __forceinline__ void load(const P* p, int64_t ls)
+    {
+#pragma unroll
+        for (int y = 0; y < 8; y++)
+        {
+            if constexpr (W == 2) { const uint2 v = ldu<uint2>(p + y * ls); r[y][0] = v.x; r[y][1] = v.y; }
+            else { const uint4 v = ldu<uint4>(p + y * ls); r[y][0] = v.x; r[y][1] = v.y; r[y][2] = v.z; r[y][3] = v.w; }
+        }
+    }
+    __device__ __forceinline__ int get(int y, int x) const
+    {
+        if constexpr (W == 2) return (int)((r[y][x >> 2] >> (8 * (x & 3))) & 0xff);
+        else return (int)((r[y][x >> 1] >> (16 * (x & 1))) & 0xffff);
+    }
+};
+
+template <typename P>
+__device__ __forceinline__ uint32_t sad_packed(uint32_t a, uint32_t b, uint32_t acc)
+{
+    if constexpr (sizeof(P) == 1) return __builtin_amdgcn_sad_u8(a, b, acc);
+    else return __builtin_amdgcn_sad_u16(a, b, acc);
+}
+
+// SAD of the fenc block against 8 rows at p (fullpel or half-pel plane)
+template <typename P>
+__device__ __forceinline__ int sad8_mem(const Blk8<P>& fe, const P* p, int64_t ls)
+{
+    Blk8<P> b;
+    b.load(p, ls);
+    uint32_t s = 0;
+#pragma unroll
+    for (int y = 0; y < 8; y++)
+#pragma unroll
+        for (int w = 0; w < Blk8<P>::W; w++) s = sad_packed<P>(fe.r[y][w], b.r[y][w], s);
+    return (int)s;
+}
+
+template <typename P>
+__device__ __forceinline__ int sad8_blk(const Blk8<P>& fe, const Blk8<P>& b)
+{
+    uint32_t s = 0;
+#pragma unroll
+    for (int y = 0; y < 8; y++)
+#pragma unroll
+        for (int w = 0; w < Blk8<P>::W; w++) s = sad_packed<P>(fe.r[y][w], b.r[y][w], s);
+    return (int)s;
+}
+
+template <typename P>
+__device__ __forceinline__ int satd8_blk(const Blk8<P>& fe, const Blk8<P>& b)
+{
+    int sum = 0;
+#pragma unroll
+    for (int qy = 0; qy < 8; qy += 4)
+#pragma unroll
+        for (int qx = 0; qx < 8; qx += 4)
+        {
+            int d[4][4];
+#pragma unroll
+            for (int r = 0; r < 4; r++)
+#pragma unroll
+                for (int c = 0; c < 4; c++) d[r][c] = fe.get(qy + r, qx + c) - b.get(qy + r, qx + c);
+#pragma unroll
+            for (int r = 0; r < 4; r++) had4(d[r][0], d[r][1], d[r][2], d[r][3]);
+#pragma unroll
+            for (int c = 0; c < 4; c++)
+            {
+                had4(d[0][c], d[1][c], d[2][c], d[3][c]);
+#pragma unroll
+                for (int r = 0; r < 4; r++) sum += d[r][c] < 0 ? -d[r][c] : d[r][c];
+            }
+        }
+    return sum >> 1;
+}
+
+// ReferencePlanes::lowresMC (lowres.h:57-80): the block at quarter-pel q, the
+// rounded average of two half-pel planes when q is a quarter position
+template <typename P>
+__device__ __forceinline__ void qpel_block(const P* const (&ref)[4], int64_t ls, int qx, int qy, Blk8<P>& out)
+{
+    const int ha = (qy & 2) | ((qx & 2) >> 1);
+    out.load(ref[ha] + (qx >> 2) + (qy >> 2) * ls, ls);
+    if ((qx | qy) & 1)
+    {
+        const int bx = qx + (qx & 1), by = qy + (qy & 1);
+        const int hb = (by & 2) | ((bx & 2) >> 1);
+        Blk8<P> b;
+        b.load(ref[hb] + (bx >> 2) + (by >> 2) * ls, ls);
+        constexpr uint32_t M = sizeof(P) == 1 ? 0x7f7f7f7fu : 0x7fff7fffu;
+#pragma unroll
+        for (int y = 0; y < 8; y++)
+#pragma unroll
+            for (int w = 0; w < Blk8<P>::W; w++)
+            {
+                const uint32_t x = out.r[y][w], z = b.r[y][w];
+                out.r[y][w] = (x | z) - (((x ^ z) >> 1) & M);     // (a + b + 1) >> 1 per element
+            }
+    }
+}
+
+template <typename P>
+__device__ __forceinline__ int qpel_cost(const Blk8<P>& fe, const P* const (&ref)[4], int64_t ls, int qx, int qy,
+                                         bool satd)
+{
+    Blk8<P> b;
+    qpel_block<P>(ref, ls, qx, qy, b);
+    return satd ? satd8_blk<P>(fe, b) : sad8_blk<P>(fe, b);
+}
+
+struct MvCost
+{
+    const uint16_t* tab;
+    int px, py;
+    __device__ __forceinline__ int operator()(int qx, int qy) const
+    {
+        return (uint16_t)(tab[qx - px] + tab[qy - py]);
+    }
+};
+
+// MotionEstimate::motionEstimate, lowres reference, HEX search, subme 1
+template <typename P>
+__device__ int me_lowres(const Blk8<P>& fe, const P* const (&ref)[4], int64_t ls, const MvCost& mc, int minx,
+                         int miny, int maxx, int maxy, int mvpx, int mvpy, int& outx, int& outy)
+{
+    constexpr int hx[8] = { -1, -2, -1, 1, 2, 1, -1, -2 }, hy[8] = { -2, 0, 2, 2, 0, -2, -2, 0 };   // hex2
+    constexpr int sx[9] = { 0, 0, 0, -1, 1, -1, -1, 1, 1 }, sy[9] = { 0, -1, 1, 0, 0, -1, 1, -1, 1 };  // square1
+    const int pmx = mvpx > 4 * maxx ? 4 * maxx : (mvpx < 4 * minx ? 4 * minx : mvpx);
+    const int pmy = mvpy > 4 * maxy ? 4 * maxy : (mvpy < 4 * miny ? 4 * miny : mvpy);
+    const int bprecost = qpel_cost<P>(fe, ref, ls, pmx, pmy, false);          // no MV cost (motion.cpp:606)
+    int bx = (pmx + 2) >> 2, by = (pmy + 2) >> 2;
+    int bcost = bprecost;
+    const P* f0 = ref[0];
+    if ((pmx | pmy) & 3) bcost = sad8_mem<P>(fe, f0 + bx + by * ls, ls) + mc(4 * bx, 4 * by);
+    if (pmx | pmy)
+    {
+        const int c = sad8_mem<P>(fe, f0, ls) + mc(0, 0);
+        if (c < bcost) { bcost = c; bx = by = 0; }
+    }
+    auto cand = [&](int dx, int dy) {
+        return sad8_mem<P>(fe, f0 + (bx + dx) + (by + dy) * ls, ls) + mc(4 * (bx + dx), 4 * (by + dy));
+    };
+    {
+        int c0 = cand(-2, 0), c1 = cand(-1, 2), c2 = cand(1, 2);
+        bcost <<= 3;
+        if ((c0 << 3) + 2 < bcost) bcost = (c0 << 3) + 2;
+        if ((c1 << 3) + 3 < bcost) bcost = (c1 << 3) + 3;
+        if ((c2 << 3) + 4 < bcost) bcost = (c2 << 3) + 4;
+        c0 = cand(2, 0); c1 = cand(1, -2); c2 = cand(-1, -2);
+        if ((c0 << 3) + 5 < bcost) bcost = (c0 << 3) + 5;
+        if ((c1 << 3) + 6 < bcost) bcost = (c1 << 3) + 6;
+        if ((c2 << 3) + 7 < bcost) bcost = (c2 << 3) + 7;
+        if (bcost & 7)
+        {
+            int dir = (bcost & 7) - 2;
+            bx += hx[dir + 1]; by += hy[dir + 1];
+            for (int i = (16 >> 1) - 1; i > 0 && bx >= minx && bx <= maxx && by >= miny && by <= maxy; i--)
+            {
+                c0 = cand(hx[dir], hy[dir]);
+                c1 = cand(hx[dir + 1], hy[dir + 1]);
+                c2 = cand(hx[dir + 2], hy[dir + 2]);
+                bcost &= ~7;
+                if ((c0 << 3) + 1 < bcost) bcost = (c0 << 3) + 1;
+                if ((c1 << 3) + 2 < bcost) bcost = (c1 << 3) + 2;
+                if ((c2 << 3) + 3 < bcost) bcost = (c2 << 3) + 3;
+                if (!(bcost & 7)) break;
+                dir += (bcost & 7) - 2;
+                dir = dir < 0 ? dir + 6 : (dir > 5 ? dir - 6 : dir);   // mod6m1[dir + 1] = dir mod 6
+                bx += hx[dir + 1]; by += hy[dir + 1];
+            }
+        }
+        bcost >>= 3;
+        int sdir = 0;
+#pragma unroll
+        for (int k = 1; k <= 8; k++)
+        {
+            const int c = cand(sx[k], sy[k]);
+            if (c < bcost) { bcost = c; sdir = k; }
+        }
+        bx += sx[sdir]; by += sy[sdir];
+    }
+    int qx, qy;
+    if (bprecost < bcost) { qx = pmx; qy = pmy; bcost = bprecost; }
+    else { qx = 4 * bx; qy = 4 * by; }
+    if (!bcost)
+        bcost = mc(qx, qy);
+    else
+    {
+        int bdir = 0;
+#pragma unroll
+        for (int k = 1; k <= 4; k++)
+        {
+            const int c = qpel_cost<P>(fe, ref, ls, qx + 2 * sx[k], qy + 2 * sy[k], false) + mc(qx + 2 * sx[k], qy + 2 * sy[k]);
+            if (c < bcost) { bcost = c; bdir = k; }
+        }
+        qx += 2 * sx[bdir]; qy += 2 * sy[bdir];
+        bcost = qpel_cost<P>(fe, ref, ls, qx, qy, true) + mc(qx, qy);
+        bdir = 0;
+#pragma unroll
+        for (int k = 1; k <= 4; k++)
+        {
+            const int c = qpel_cost<P>(fe, ref, ls, qx + sx[k], qy + sy[k], true) + mc(qx + sx[k], qy + sy[k]);
+            if (c < bcost) { bcost = c; bdir = k; }
+        }
+        qx += sx[bdir]; qy += sy[bdir];
+    }
+    outx = qx;
+    outy = qy;
+    return bcost;
+}
+
+template <typename P>
+__global__ __launch_bounds__(64) void k_lowres_pcost(const PcostArgs a)
+{
+    __shared__ uint32_t ring[kPcostMaxRows][4];   // per row: MVs of its last four CUs (x' & 3), packed x | y << 16
+    __shared__ int32_t rowsum[kPcostMaxRows];
+    const int lane = threadIdx.x;
+    const int e = blockIdx.x / a.nslices, sl = blockIdx.x % a.nslices;
+    const int first = a.rps * sl;
+    const int last = sl == a.nslices - 1 ? a.hcu - 1 : a.rps * (sl + 1) - 1;
+    const int R = last - first + 1, W = a.wcu;
+    const int ncu = W * a.hcu;
+    const P* planes = (const P*)a.planes;
+    const int64_t ls = a.ls;
+    const P* fenc0 = planes + a.fenc_off[e];
+    const P* const rbase[4] = { planes + a.ref_off[4 * e], planes + a.ref_off[4 * e + 1], planes + a.ref_off[4 * e + 2],
+                                planes + a.ref_off[4 * e + 3] };
+    const int64_t cub = (int64_t)e * ncu;
+    for (int y = lane; y < R; y += 64) rowsum[y] = 0;
+    wave_sync_lds();
+    int64_t est = 0, est_aq = 0;
+    int mbs = 0;
+    const int steps = W + 2 * (R - 1);
+    for (int t = 0; t < steps; t++)
+    {
+        for (int yp = lane; yp < R; yp += 64)
+        {
+            const int xp = t - 2 * yp;
+            if (xp < 0 || xp >= W) continue;
+            const int cx = W - 1 - xp, cy = last - yp;
+            const int xy = cx + cy * W;
+            const int64_t off = 8 * cx + 8 * (int64_t)cy * ls;
+            Blk8<P> fe;
+            fe.load(fenc0 + off, ls);
+            const P* const ref[4] = { rbase[0] + off, rbase[1] + off, rbase[2] + off, rbase[3] + off };
+            // MVP: right, below, below-left, below-right (slicetype.cpp:2116-2150)
+            int candx[4], candy[4], numc = 0;
+            if (cx < W - 1) { const uint32_t m = ring[yp][(xp - 1) & 3]; candx[numc] = (int16_t)m; candy[numc++] = (int16_t)(m >> 16); }
+            if (yp > 0)
+            {
+                const uint32_t mb = ring[yp - 1][xp & 3];
+                candx[numc] = (int16_t)mb; candy[numc++] = (int16_t)(mb >> 16);
+                if (cx > 0) { const uint32_t m = ring[yp - 1][(xp + 1) & 3]; candx[numc] = (int16_t)m; candy[numc++] = (int16_t)(m >> 16); }
+                if (cx < W - 1) { const uint32_t m = ring[yp - 1][(xp - 1) & 3]; candx[numc] = (int16_t)m; candy[numc++] = (int16_t)(m >> 16); }
+            }
+            int mvpx = 0, mvpy = 0;
+            if (numc)
+            {
+                int best = 1 << 28;                                  // MotionEstimate::COST_MAX
+                for (int i = 0; i < numc; i++)
+                {
+                    const int c = qpel_cost<P>(fe, ref, ls, candx[i], candy[i], true);
+                    if (c < best) { best = c; mvpx = candx[i]; mvpy = candy[i]; }
+                }
+            }
+            const MvCost mc{ a.mvcost, mvpx, mvpy };
+            int ox, oy;
+            const int fcost = me_lowres<P>(fe, ref, ls, mc, -cx * 8 - 8, -cy * 8 - 8, (W - cx - 1) * 8 + 8,
+                                           (a.hcu - cy - 1) * 8 + 8, mvpx, mvpy, ox, oy);
+            ring[yp][xp & 3] = (uint32_t)(uint16_t)ox | ((uint32_t)(uint16_t)oy << 16);
+            a.mvs[2 * (cub + xy)] = (int16_t)ox;
+            a.mvs[2 * (cub + xy) + 1] = (int16_t)oy;
+            a.mv_costs[cub + xy] = fcost;
+            int bcost = 1 << 28, listused = 0;
+            if (fcost < bcost) { bcost = fcost; listused = 1; }
+            bcost += 4;                                              // lowresPenalty
+            const int ic = a.intra_cost[cub + xy];
+            if (ic < bcost) { bcost = ic; listused = 0; }
+            const bool scored = (cx > 0 && cx < W - 1 && cy > 0 && cy < a.hcu - 1) || W <= 2 || a.hcu <= 2;
+            const int bcost_aq = (scored && a.inv_q) ? ((bcost * a.inv_q[cub + xy] + 128) >> 8) : bcost;
+            if (scored) { est += bcost; est_aq += bcost_aq; mbs += !listused; }
+            rowsum[yp] += bcost_aq;
+            a.lowres_costs[cub + xy] = (uint16_t)((bcost < 0x3fff ? bcost : 0x3fff) | (listused << 14));
+        }
+        wave_sync_lds();
+    }
+    for (int yp = lane; yp < R; yp += 64) a.row_satd[(int64_t)e * a.hcu + last - yp] = rowsum[yp];
+    // slice totals into the estimate's (integer sums: order-independent)
+    est = (int64_t)group_sum64<64>((uint64_t)est);
+    est_aq = (int64_t)group_sum64<64>((uint64_t)est_aq);
+    mbs = group_sum<64>(mbs);
+    if (lane == 0)
+    {
+        atomicAdd((unsigned long long*)&a.cost_est[2 * e], (unsigned long long)est);
+        atomicAdd((unsigned long long*)&a.cost_est[2 * e + 1], (unsigned long long)est_aq);
+        atomicAdd(&a.intra_mbs[e], mbs);
+    }
+}
+
 template <typename P>
 static int launch_lowres_init(const LowresArgs& a, hipStream_t st)
 {
@@ -346,5 +695,30 @@ extern "C" int x265amd_lowres_intra(int depth, const x265amd_lowres_intra_batch*
     const uint32_t blocks = (uint32_t)((threads + X265AMD_BLOCK - 1) / X265AMD_BLOCK);
     if (depth == 8) hipLaunchKernelGGL((k_lowres_intra<uint8_t>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, a);
     else hipLaunchKernelGGL((k_lowres_intra<uint16_t>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, a);
+    return (int)hipGetLastError();
+}
+
+extern "C" int x265amd_lowres_pcost(int depth, const x265amd_lowres_pcost_batch* b, void* stream)
+{
+    if ((depth != 8 && depth != 10 && depth != 12) || !b) return X265AMD_EINVAL;
+    if (b->n < 0 || b->width_cu <= 0 || b->height_cu <= 0) return X265AMD_EINVAL;
+    int rps = b->rows_per_slice, ns = b->num_slices;
+    if (ns <= 1) { ns = 1; rps = b->height_cu; }
+    if (rps <= 0 || (int64_t)rps * (ns - 1) >= b->height_cu) return X265AMD_EINVAL;
+    if (b->height_cu - rps * (ns - 1) > kPcostMaxRows || rps > kPcostMaxRows) return X265AMD_EINVAL;
+    if (!b->n) return 0;
+    if (!b->planes || !b->fenc_off || !b->ref_off || !b->intra_cost || !b->mvcost || !b->mvs || !b->mv_costs ||
+        !b->lowres_costs || !b->row_satd || !b->cost_est || !b->intra_mbs)
+        return X265AMD_EINVAL;
+    hipStream_t st = (hipStream_t)stream;
+    hipError_t err = hipMemsetAsync(b->cost_est, 0, sizeof(int64_t) * 2 * (size_t)b->n, st);
+    if (err == hipSuccess) err = hipMemsetAsync(b->intra_mbs, 0, sizeof(int32_t) * (size_t)b->n, st);
+    if (err != hipSuccess) return (int)err;
+    PcostArgs a{ b->planes, (int64_t)b->lowres_stride, b->fenc_off, b->ref_off, b->intra_cost, b->inv_qscale,
+                 b->mvcost, b->mvs, b->mv_costs, b->lowres_costs, b->row_satd, b->cost_est, b->intra_mbs, b->n,
+                 b->width_cu, b->height_cu, rps, ns };
+    const uint32_t blocks = (uint32_t)(b->n * ns);
+    if (depth == 8) hipLaunchKernelGGL((k_lowres_pcost<uint8_t>), dim3(blocks), dim3(64), 0, st, a);
+    else hipLaunchKernelGGL((k_lowres_pcost<uint16_t>), dim3(blocks), dim3(64), 0, st, a);
     return (int)hipGetLastError();
 }

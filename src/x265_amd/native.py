@@ -56,6 +56,13 @@ class LowresIntraBatch(C.Structure):
                 ("lowres_cost", _vp), ("row_satd", _vp), ("cost_est", _vp)]
 
 
+class LowresPcostBatch(C.Structure):
+    _fields_ = [("n", _int), ("width_cu", _int), ("height_cu", _int), ("rows_per_slice", _int), ("num_slices", _int),
+                ("planes", _vp), ("lowres_stride", _ip), ("fenc_off", _vp), ("ref_off", _vp), ("intra_cost", _vp),
+                ("inv_qscale", _vp), ("mvcost", _vp), ("mvs", _vp), ("mv_costs", _vp), ("lowres_costs", _vp),
+                ("row_satd", _vp), ("cost_est", _vp), ("intra_mbs", _vp)]
+
+
 def _addr(t):
     return None if t is None else t.data_ptr()
 
@@ -227,3 +234,9 @@ class Primitives:
         b = LowresIntraBatch(n, wcu, hcu, _addr(planes), ls, _addr(p0), _addr(inv_q), _addr(ic), _addr(im), _addr(lc),
                              _addr(rs), _addr(ce))
         self._check(self.lib.x265amd_lowres_intra(depth, C.byref(b), stream or _stream()), "lowres_intra")
+
+    def lowres_pcost(self, depth, n, wcu, hcu, rps, ns, planes, ls, fo, ro, ic, iq, tab_centre_ptr, mvs, mc, lc, rs, ce,
+                     mbs, stream=None):
+        b = LowresPcostBatch(n, wcu, hcu, rps, ns, _addr(planes), ls, _addr(fo), _addr(ro), _addr(ic), _addr(iq),
+                             tab_centre_ptr, _addr(mvs), _addr(mc), _addr(lc), _addr(rs), _addr(ce), _addr(mbs))
+        self._check(self.lib.x265amd_lowres_pcost(depth, C.byref(b), stream or _stream()), "lowres_pcost")

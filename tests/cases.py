@@ -492,6 +492,80 @@ def case_lowres(W: int, H: int, nframes: int, aq: bool, depth: int, seed: int) -
                 ["planes", "ic", "im", "lc", "rs", "ce"])
 
 
+MVCOST_RANGE = 1 << 14
+
+
+def mvcost_table(depth: int) -> np.ndarray:
+    """BitCost table for X265_LOOKAHEAD_QP, generated from the REFERENCE by make_golden.py
+    (tests/golden/mvcost_lookahead_d{8,10}.npy, entries -2^14 .. 2^14)"""
+    import os
+
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", f"mvcost_lookahead_d{depth}.npy")
+    return np.load(path)
+
+
+def _lowres_planes_np(y: np.ndarray, g: dict, pdt) -> np.ndarray:
+    """the four border-extended lowres planes of a luma picture (frame_init_lowres_core +
+    extendPicBorder in numpy; test input generation only)"""
+    H2, W2 = 2 * g["lines"] + 2, 2 * g["width"] + 2
+    src = np.pad(y.astype(np.int64), ((0, max(0, H2 - y.shape[0])), (0, max(0, W2 - y.shape[1]))), mode="edge")
+    f = lambda a, b, c, d: ((((a + b + 1) >> 1) + ((c + d + 1) >> 1) + 1) >> 1)
+    r0, r1, r2 = src[0:2 * g["lines"]:2], src[1:2 * g["lines"] + 1:2], src[2:2 * g["lines"] + 2:2]
+    e = slice(0, 2 * g["width"], 2)
+    o = slice(1, 2 * g["width"] + 1, 2)
+    o2 = slice(2, 2 * g["width"] + 2, 2)
+    planes = [f(r0[:, e], r1[:, e], r0[:, o], r1[:, o]), f(r0[:, o], r1[:, o], r0[:, o2], r1[:, o2]),
+              f(r1[:, e], r2[:, e], r1[:, o], r2[:, o]), f(r1[:, o], r2[:, o], r1[:, o2], r2[:, o2])]
+    out = []
+    for pl in planes:
+        ext = np.pad(pl, ((g["my"], g["my"]), (g["mx"], g["ls"] - g["width"] - g["mx"])), mode="edge")
+        out.append(ext.astype(pdt).reshape(-1))
+    return np.concatenate(out)
+
+
+def case_lowres_pcost(W: int, H: int, n: int, rps: int, ns: int, aq: bool, depth: int, seed: int) -> Case:
+    """f1: n P estimates (frame i+1 against frame i) of the synthetic sequence (src/x265_amd/synth.py:
+    panning texture, a moving object, noise) with one band of each frame replaced by uniform noise so
+    intra wins there; intra costs drawn around the inter cost range."""
+    import os
+    import sys
+
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from src.x265_amd.synth import SyntheticSource
+
+    det = Det(seed)
+    g = lowres_geometry(W, H)
+    pmax = (1 << depth) - 1
+    pdt = pixel_dtype(depth)
+    src = SyntheticSource(W, H, n + 1, depth, seed=seed % 100000)
+    psize = g["ls"] * (g["lines"] + 2 * g["my"])
+    planes = []
+    for f in range(n + 1):
+        y = src.frame(f)[0].astype(np.int64)
+        band = slice(H // 3, H // 3 + max(16, H // 10))
+        y[band] = det.ints(0, pmax + 1, y[band].size).reshape(y[band].shape)
+        planes.append(_lowres_planes_np(y, g, pdt))
+    planes = np.concatenate(planes)
+    org = g["my"] * g["ls"] + g["mx"]
+    fo = np.array([4 * (f + 1) * psize + org for f in range(n)], np.int64)
+    ro = np.array([(4 * f + k) * psize + org for f in range(n) for k in range(4)], np.int64)
+    ncu = g["wcu"] * g["hcu"]
+    ic = det.ints(60, 1500, n * ncu).astype(np.int32) << (depth - 8)
+    iq = det.ints(64, 512, n * ncu).astype(np.int32) if aq else None
+    bufs = dict(planes=planes, fo=fo, ro=ro, ic=ic, iq=iq, tab=mvcost_table(depth),
+                mvs=np.full(2 * n * ncu, -21846, np.int16), mc=np.full(n * ncu, -1, np.int32),
+                lc=np.full(n * ncu, 0xCDCD, np.uint16), rs=np.full(n * g["hcu"], -1, np.int32),
+                ce=np.full(2 * n, -1, np.int64), mbs=np.full(n, -1, np.int32))
+    return Case("lowres_pcost", dict(W=W, H=H, n=n, rps=rps, ns=ns, aq=int(aq), depth=depth, seed=seed, **g), bufs,
+                ["mvs", "mc", "lc", "rs", "ce", "mbs"])
+
+
+def lowres_pcost_cases(depth: int):
+    return [case_lowres_pcost(256, 160, 2, 0, 0, True, depth, seed_of(depth, "lp", 0)),
+            case_lowres_pcost(480, 272, 1, 4, 2, False, depth, seed_of(depth, "lp", 1)),
+            case_lowres_pcost(640, 360, 1, 10, 2, True, depth, seed_of(depth, "lp", 2))]
+
+
 def lowres_cases(depth: int):
     return [case_lowres(64, 32, 1, False, depth, seed_of(depth, "lr", 0)),
             case_lowres(136, 72, 2, True, depth, seed_of(depth, "lr", 1)),
@@ -570,6 +644,7 @@ def all_cases(depth: int, n: int = 6, quick: bool = False):
         cases.append(case_denoise(size, depth, n, s("dn", size)))
     cases += tu_cases(depth)
     cases += lowres_cases(depth)
+    cases += lowres_pcost_cases(depth)
     return cases
 
 
@@ -606,6 +681,10 @@ def run_cpu(case: Case, orc) -> dict:
     elif f == "lowres":
         orc.lowres(p["n"], p["width"], p["lines"], p["mx"], p["my"], b["src"], b["ss"], b["so"], b["planes"], p["ls"],
                    b["po"], p["wcu"], p["hcu"], b["inv_q"], b["ic"], b["im"], b["lc"], b["rs"], b["ce"])
+    elif f == "lowres_pcost":
+        orc.lowres_pcost(p["n"], p["wcu"], p["hcu"], p["rps"], p["ns"], b["planes"], p["ls"], b["fo"], b["ro"], b["ic"],
+                         b["iq"], b["tab"].ctypes.data + 2 * MVCOST_RANGE, b["mvs"], b["mc"], b["lc"], b["rs"], b["ce"],
+                         b["mbs"])
     elif f == "tu":
         orc.tu(p["log2"], p["luma"], p["intra"], p["islice"], p["sh"], b["f"], b["fs"], b["fo"], b["p"], b["ps"],
                b["po"], b["r"], b["rs"], b["ro"], b["c"], b["co"], b["rc"], b["rcs"], b["rco"], b["sig"], b["qp"],
@@ -664,6 +743,10 @@ def run_gpu(case: Case, prims, device="cuda") -> dict:
                           p["ls"], b["po"])
         prims.lowres_intra(d, p["n"], p["wcu"], p["hcu"], b["planes"], p["ls"], b["po"][0::4].contiguous(), b["inv_q"],
                            b["ic"], b["im"], b["lc"], b["rs"], b["ce"])
+    elif f == "lowres_pcost":
+        prims.lowres_pcost(d, p["n"], p["wcu"], p["hcu"], p["rps"], p["ns"], b["planes"], p["ls"], b["fo"], b["ro"],
+                           b["ic"], b["iq"], b["tab"].data_ptr() + 2 * MVCOST_RANGE, b["mvs"], b["mc"], b["lc"], b["rs"],
+                           b["ce"], b["mbs"])
     elif f == "tu":
         prims.tu_pipeline(d, p["log2"], p["luma"], p["intra"], p["islice"], p["sh"], b["f"], b["fs"], b["fo"], b["p"],
                           b["ps"], b["po"], b["r"], b["rs"], b["ro"], b["c"], b["co"], b["rc"], b["rcs"], b["rco"],

@@ -30,10 +30,16 @@ from pyoracle import CpuOracle, available  # noqa: E402
 
 
 def main() -> None:
+    import numpy as np
+
+    from cases import MVCOST_RANGE
+
     for depth in (8, 10):
         if not available("ref", depth):
             raise SystemExit("reference library missing: run `make -C oracle ref cpubatch` first")
         ref = CpuOracle("ref", depth)
+        # the lookahead's BitCost table (input of the lowres P-estimate cases), from the reference
+        np.save(os.path.join(HERE, f"mvcost_lookahead_d{depth}.npy"), ref.mvcost_table(MVCOST_RANGE))
         entries = []
         for c in all_cases(depth):
             outs = run_cpu(c, ref)
