@@ -349,7 +349,69 @@ def main():
             r["cpu_reference_error"] = str(ex)
         results.append(r)
         print(json.dumps(r), flush=True)
-        del SRC, PL, IC, IM, LC, RS, CE, IQ
+        # P estimates of frame f+1 against frame f for the 8 frames' planes (7 estimates), coop slices as
+        # Lookahead::create sets them for --lookahead-slices 8 (medium), and the whole-frame variant
+        from cases import MVCOST_RANGE, mvcost_table
+        TAB = torch.from_numpy(mvcost_table(8)).to(dev)
+        ne = nf - 1
+        fo = po[4::4].contiguous()
+        ro = po[:4 * ne].contiguous()
+        rps = max(g["hcu"] // 8, 10)
+        ns = g["hcu"] // rps
+        MVS = torch.empty(2 * ne * ncu, dtype=torch.int16, device=dev)
+        MC = torch.empty(ne * ncu, dtype=torch.int32, device=dev)
+        PLC = torch.empty(ne * ncu, dtype=torch.int16, device=dev)
+        PRS = torch.empty(ne * g["hcu"], dtype=torch.int32, device=dev)
+        PCE = torch.empty(2 * ne, dtype=torch.int64, device=dev)
+        MB = torch.empty(ne, dtype=torch.int32, device=dev)
+        for (rr, nn, tag) in ((rps, ns, f"slices{ns}"), (0, 0, "whole")):
+            ms_p = timeit(lambda: prims.lowres_pcost(8, ne, g["wcu"], g["hcu"], rr, nn, PL, g["ls"], fo, ro,
+                                                     IC[:ne * ncu], IQ[:ne * ncu], TAB.data_ptr() + 2 * MVCOST_RANGE,
+                                                     MVS, MC, PLC, PRS, PCE, MB))
+            r = {"kernel": f"lowres_pcost_{Hf}p_x{ne}_{tag}", "jobs": ne * ncu, "ms": round(ms_p, 4),
+                 "estimates_per_s": round(ne / (ms_p * 1e-3), 1),
+                 "bound": "latency (serial CU wavefront per slice, one wavefront per slice)"}
+            try:
+                import ctypes as _C
+                import time as _t
+
+                import numpy as _np
+                lib = _C.CDLL(os.path.join(ROOT, "oracle", "_ref", "libx265ref8.so"))
+                plh = PL[:8 * psize].cpu().numpy()
+                ich = IC[:ncu].cpu().numpy()
+                o = [_np.empty(2 * ncu, _np.int16), _np.empty(ncu, _np.int32), _np.empty(ncu, _np.uint16),
+                     _np.empty(g["hcu"], _np.int32), _np.empty(2, _np.int64), _np.empty(1, _np.int32)]
+                vp = lambda arr, off=0: _C.c_void_p(arr.ctypes.data + off * arr.itemsize)
+                t0 = _t.perf_counter()
+                lib.xo_lowres_pcost(g["wcu"], g["hcu"], rr, nn, vp(plh, 4 * psize + org),
+                                    *[vp(plh, k * psize + org) for k in range(4)], _C.c_ssize_t(g["ls"]), vp(ich),
+                                    None, None, *[vp(x) for x in o])
+                r["cpu_reference_1core_estimates_per_s"] = round(1.0 / (_t.perf_counter() - t0), 2)
+            except Exception as ex:
+                r["cpu_reference_error"] = str(ex)
+            results.append(r)
+            print(json.dumps(r), flush=True)
+        # throughput with a lookahead-sized batch: 56 estimates (each frame against each of the 7 others)
+        pairs = [(b_, p_) for b_ in range(nf) for p_ in range(nf) if p_ != b_]
+        nb = len(pairs)
+        fo56 = torch.tensor([4 * b_ * psize + org for b_, _ in pairs], dtype=torch.int64, device=dev)
+        ro56 = torch.tensor([(4 * p_ + k) * psize + org for _, p_ in pairs for k in range(4)], dtype=torch.int64,
+                            device=dev)
+        IC56 = IC[:ncu].repeat(nb)
+        MVS = torch.empty(2 * nb * ncu, dtype=torch.int16, device=dev)
+        MC = torch.empty(nb * ncu, dtype=torch.int32, device=dev)
+        PLC = torch.empty(nb * ncu, dtype=torch.int16, device=dev)
+        PRS = torch.empty(nb * g["hcu"], dtype=torch.int32, device=dev)
+        PCE = torch.empty(2 * nb, dtype=torch.int64, device=dev)
+        MB = torch.empty(nb, dtype=torch.int32, device=dev)
+        ms_p = timeit(lambda: prims.lowres_pcost(8, nb, g["wcu"], g["hcu"], rps, ns, PL, g["ls"], fo56, ro56, IC56, None,
+                                                 TAB.data_ptr() + 2 * MVCOST_RANGE, MVS, MC, PLC, PRS, PCE, MB))
+        r = {"kernel": f"lowres_pcost_{Hf}p_x{nb}_slices{ns}", "jobs": nb * ncu, "ms": round(ms_p, 4),
+             "estimates_per_s": round(nb / (ms_p * 1e-3), 1),
+             "bound": "latency (serial CU wavefront per slice, one wavefront per slice)"}
+        results.append(r)
+        print(json.dumps(r), flush=True)
+        del SRC, PL, IC, IM, LC, RS, CE, IQ, MVS, MC, PLC, PRS, PCE, MB
     if a.out:
         with open(a.out, "w") as f:
             json.dump({"hbm_peak_GBps": HBM, "working_set_GB": a.gb, "results": results}, f, indent=1)
