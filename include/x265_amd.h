@@ -438,6 +438,43 @@ typedef struct
 } x265amd_lowres_pcost_batch;
 int x265amd_lowres_pcost(int depth, const x265amd_lowres_pcost_batch* batch, void* stream);
 
+/* ------------------------------------------------------------------- f2
+ * Full-resolution motion search.  Job i is one
+ * MotionEstimate::motionEstimate call (motion.cpp:571-1172) on a full-resolution
+ * luma reference, as Search::predInterSearch makes it (search.cpp:2024, 2112):
+ * the clipped MVP measured at sub-pel (SAD, no MV cost), the num_cand[i] extra
+ * candidates (AMVP list), DIA (method 0) or HEX (method 1) integer search within
+ * merange, then the sub-pel refine of workload[subme] for subme 0..2 (luma only;
+ * levels >= 3 add chroma SATD).  fenc_off[i] / ref_off[i] = the PU origin in the
+ * source / reference plane (the reference is border-extended as PicYuv is);
+ * mv_range[4 i ..] = mvmin.x, mvmin.y, mvmax.x, mvmax.y (full-pel); mvp[2 i ..]
+ * and the candidates mvc[2 (i max_cand + k) ..] are quarter-pel; mvcost +
+ * mvcost_off[i] is the centre (difference 0) of the BitCost table of the job's
+ * QP (BitCost::setQP; uint16 per MV component difference), which must cover
+ * every difference the search forms.  Outputs: out_mv[2 i ..] (outQMv, qpel)
+ * and out_cost[i] (the returned cost).  PU sizes: the 25 luma PU shapes. */
+typedef struct
+{
+    int w, h, n;
+    int method, subme, merange;
+    int max_cand;
+    const void* fenc;
+    intptr_t fenc_stride;
+    const int64_t* fenc_off;
+    const void* ref;
+    intptr_t ref_stride;
+    const int64_t* ref_off;
+    const int16_t* mv_range;
+    const int16_t* mvp;
+    const int16_t* mvc;
+    const uint8_t* num_cand;
+    const uint16_t* mvcost;
+    const int64_t* mvcost_off;
+    int16_t* out_mv;
+    int32_t* out_cost;
+} x265amd_me_batch;
+int x265amd_motion_search(int depth, int count, const x265amd_me_batch* batches, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

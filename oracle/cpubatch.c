@@ -69,6 +69,9 @@ typedef struct
                      const int32_t*, const int32_t*, const uint16_t*, int16_t*, int32_t*, uint16_t*, int32_t*, int64_t*,
                      int32_t*);
     void (*mvtab)(int, uint16_t*);
+    int (*me)(int, int, int, int, int, const void*, intptr_t, const void*, intptr_t, int, int, int, int, int, int, int,
+              const int16_t*, const uint16_t*, int16_t*);
+    void (*set_me_qp)(int);   /* reference shim only: its BitCost QP (the restatement reads the table) */
 } Lib;
 
 #define SYM(field, name)                                                     \
@@ -99,6 +102,8 @@ void* cb_open(const char* path)
     SYM(tu, "xo_tu_pipeline"); SYM(scan, "xo_scan_table");
     SYM(lr_init, "xo_lowres_init"); SYM(lr_intra, "xo_lowres_intra");
     SYM(lr_pcost, "xo_lowres_pcost"); SYM(mvtab, "xo_mvcost_table");
+    SYM(me, "xo_motion_search");
+    *(void**)&L->set_me_qp = dlsym(L->dl, "xo_set_me_qp");
     return L;
 }
 
@@ -538,3 +543,23 @@ int cb_lowres_pcost(void* h, int n, int wcu, int hcu, int rps, int ns, const voi
 }
 
 void cb_mvcost_table(void* h, int range, uint16_t* out) { ((Lib*)h)->mvtab(range, out); }
+
+/* f2 full-resolution motion search batch (x265amd_me_batch); qp[i] selects the reference shim's
+ * BitCost QP, tab + tab_off[i] is the same table for the restatement */
+int cb_motion_search(void* h, int64_t n, int w, int hh, int method, int subme, int merange, int max_cand,
+                     const void* fenc, intptr_t fs, const int64_t* fo, const void* ref, intptr_t rs, const int64_t* ro,
+                     const int16_t* range, const int16_t* mvp, const int16_t* mvc, const uint8_t* numc,
+                     const uint16_t* tab, const int64_t* tab_off, const uint8_t* qp, int16_t* out_mv, int32_t* out_cost)
+{
+    Lib* L = (Lib*)h;
+    const int b = L->depth > 8 ? 2 : 1;
+    for (int64_t i = 0; i < n; i++)
+    {
+        if (L->set_me_qp) L->set_me_qp(qp[i]);
+        out_cost[i] = L->me(w, hh, method, subme, merange, (const char*)fenc + fo[i] * b, fs,
+                            (const char*)ref + ro[i] * b, rs, range[4 * i], range[4 * i + 1], range[4 * i + 2],
+                            range[4 * i + 3], mvp[2 * i], mvp[2 * i + 1], numc ? numc[i] : 0,
+                            mvc + 2 * i * max_cand, tab + tab_off[i], out_mv + 2 * i);
+    }
+    return 0;
+}

@@ -118,6 +118,12 @@ class CpuOracle:
         self.cb.cb_mvcost_table(_vp(self.h), rng, _p(out))
         return out
 
+    def motion_search(self, w, h, method, subme, merange, max_cand, f, fs, fo, r, rs, ro, rng, mvp, mvc, numc, tab,
+                      tab_off, qp, out_mv, out_cost):
+        self.cb.cb_motion_search(_vp(self.h), _i64(len(fo)), w, h, method, subme, merange, max_cand, _p(f), _ip(fs),
+                                 _p(fo), _p(r), _ip(rs), _p(ro), _p(rng), _p(mvp), _p(mvc), _p(numc), _p(tab),
+                                 _p(tab_off), _p(qp), _p(out_mv), _p(out_cost))
+
     def scan_table(self, typ, log2):
         out = np.zeros(1 << (2 * log2), np.uint16)
         self.cb.cb_scan_table(_vp(self.h), typ, log2, _p(out))

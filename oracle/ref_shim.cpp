@@ -22,6 +22,7 @@
 #include "lowres.h"
 #include "slicetype.h"
 #include "bitcost.h"
+#include "motion.h"
 #include "x265_oracle.h"
 
 #include <pthread.h>
@@ -427,6 +428,7 @@ struct TuContext
 };
 
 pthread_once_t g_prim_once = PTHREAD_ONCE_INIT;
+__thread int g_me_qp = 32;
 void init_global_prims()
 {
     /* Quant calls through the process-global table, as in the encoder */
@@ -547,6 +549,10 @@ struct TabBitCost : public BitCost
 {
     const uint16_t* table(unsigned qp) { setQP(qp); return m_cost; }
 };
+struct SearchME : public MotionEstimate
+{
+    void configure(int method, int refine) { searchMethod = method; subpelRefine = refine; }
+};
 struct CostGroup : public CostEstimateGroup
 {
     CostGroup(Lookahead& l, Lowres** f) : CostEstimateGroup(l, f) {}
@@ -657,6 +663,47 @@ void xo_lowres_pcost(int wcu, int hcu, int rows_per_slice, int num_slices, const
     delete la;
     x265_param_free(param);
 }
+
+void xo_mvcost_table_qp(int qp, int range, uint16_t* out)
+{
+    TabBitCost bc;
+    const uint16_t* c = bc.table((unsigned)qp);
+    for (int d = -range; d <= range; d++) out[range + d] = c[d];
+}
+
+/* f2: the reference's own MotionEstimate::motionEstimate on a full-resolution reference
+ * (fpelPlane[0] at the PU origin, no PicYuv: ctuAddr stays -1 so blockOffset = 0, luma only) */
+int xo_motion_search(int w, int h, int method, int subme, int merange, const void* fenc, intptr_t fs, const void* ref,
+                     intptr_t rs, int minx, int miny, int maxx, int maxy, int mvpx, int mvpy, int numc,
+                     const int16_t* mvc, const uint16_t* tab_centre, int16_t* out)
+{
+    (void)tab_centre;    /* the reference uses its own BitCost table: the caller sets the QP below */
+    pthread_once(&g_prim_once, init_global_prims);
+    static __thread SearchME* me = NULL;
+    if (!me)
+    {
+        MotionEstimate::initScales();
+        me = new SearchME();
+        me->init(X265_HEX_SEARCH, 2, X265_CSP_I400);   /* allocates the fenc PU buffer once */
+    }
+    me->configure(method == 0 ? X265_DIA_SEARCH : X265_HEX_SEARCH, subme);
+    me->setQP(g_me_qp);
+    me->setSourcePU((pixel*)fenc, fs, 0, w, h);
+    ReferencePlanes rp;
+    rp.fpelPlane[0] = (pixel*)ref;
+    rp.lumaStride = rs;
+    rp.isLowres = false;
+    MV mvs[16];
+    for (int i = 0; i < numc && i < 16; i++) mvs[i] = MV(mvc[2 * i], mvc[2 * i + 1]);
+    MV outmv;
+    const int cost = me->motionEstimate(&rp, MV(minx, miny), MV(maxx, maxy), MV(mvpx, mvpy), numc, mvs, merange, outmv);
+    out[0] = outmv.x;
+    out[1] = outmv.y;
+    return cost;
+}
+
+/* QP used by xo_motion_search's BitCost (the restatement receives the table instead) */
+void xo_set_me_qp(int qp) { g_me_qp = qp; }
 
 void xo_scan_table(int type, int log2, uint16_t* out)
 {

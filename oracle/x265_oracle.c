@@ -1254,3 +1254,184 @@ void xo_lowres_pcost(int wcu, int hcu, int rows_per_slice, int num_slices, const
     cost_est[1] = est_aq;
     *intra_mbs = mbs;
 }
+
+/* ---------------------------------------------------------------- f2: full-resolution motion search
+ * MotionEstimate::motionEstimate (motion.cpp:571-1172) for one PU on a full-resolution
+ * reference: clipped MVP measured at sub-pel with SAD, the extra MV candidates, DIA or HEX
+ * integer search, then the sub-pel refine of workload[subme] for subme 0..2 (luma only:
+ * chroma SATD starts at subme 3, motion.cpp:197).  Sub-pel blocks come from the 8-tap luma
+ * filters exactly as subpelCompare (motion.cpp:1174-1203) builds them. */
+
+typedef struct
+{
+    int w, h;
+    const pix* fenc; intptr_t fs;
+    const pix* ref; intptr_t rs;        /* reference at the PU origin */
+    const uint16_t* tab;
+    xmv mvp;
+} XoMeF;
+
+static int xo_f_mvcost(const XoMeF* m, int qx, int qy)
+{
+    return (uint16_t)(m->tab[qx - m->mvp.x] + m->tab[qy - m->mvp.y]);
+}
+
+static int xo_f_fpel_sad(const XoMeF* m, int x, int y)
+{
+    return xo_sad(m->w, m->h, m->fenc, m->fs, m->ref + x + y * m->rs, m->rs);
+}
+
+static int xo_subpel_compare(const XoMeF* m, int qx, int qy, int use_satd)
+{
+    const pix* fr = m->ref + (qx >> 2) + (qy >> 2) * m->rs;
+    const int xf = qx & 3, yf = qy & 3;
+    const pix* p = fr;
+    intptr_t ps = m->rs;
+    pix buf[64 * 64];
+    if (xf | yf)
+    {
+        if (!yf) xo_interp(XO_HPP, 8, m->w, m->h, fr, m->rs, buf, 64, xf, 0);
+        else if (!xf) xo_interp(XO_VPP, 8, m->w, m->h, fr, m->rs, buf, 64, yf, 0);
+        else xo_interp(XO_HVPP, 8, m->w, m->h, fr, m->rs, buf, 64, xf, yf);
+        p = buf;
+        ps = 64;
+    }
+    return use_satd ? xo_satd(m->w, m->h, m->fenc, m->fs, p, ps) : xo_sad(m->w, m->h, m->fenc, m->fs, p, ps);
+}
+
+int xo_motion_search(int w, int h, int method, int subme, int merange, const void* fenc, intptr_t fs, const void* ref,
+                     intptr_t rs, int minx, int miny, int maxx, int maxy, int mvpx, int mvpy, int numc,
+                     const int16_t* mvc, const uint16_t* tab_centre, int16_t* out)
+{
+    static const xmv hex2[8] = { { -1, -2 }, { -2, 0 }, { -1, 2 }, { 1, 2 }, { 2, 0 }, { 1, -2 }, { -1, -2 }, { -2, 0 } };
+    static const int mod6m1[8] = { 5, 0, 1, 2, 3, 4, 5, 0 };
+    static const xmv square1[9] = { { 0, 0 }, { 0, -1 }, { 0, 1 }, { -1, 0 }, { 1, 0 }, { -1, -1 }, { -1, 1 }, { 1, -1 }, { 1, 1 } };
+    /* workload[] (motion.cpp:48-58): hpel_iters, hpel_dirs, qpel_iters, qpel_dirs, hpel_satd */
+    static const int wl[3][5] = { { 1, 4, 0, 4, 0 }, { 1, 4, 1, 4, 0 }, { 1, 4, 1, 4, 1 } };
+    XoMeF m = { w, h, (const pix*)fenc, fs, (const pix*)ref, rs, tab_centre, { mvpx, mvpy } };
+    const xmv qmin = { minx * 4, miny * 4 }, qmax = { maxx * 4, maxy * 4 };
+    const xmv mvmin = { minx, miny }, mvmax = { maxx, maxy };
+    xmv pmv = xo_clip((xmv){ mvpx, mvpy }, qmin, qmax);
+    xmv bestpre = pmv;
+    int bprecost = xo_subpel_compare(&m, pmv.x, pmv.y, 0);            /* no MV cost (motion.cpp:609) */
+    xmv bmv = { (pmv.x + 2) >> 2, (pmv.y + 2) >> 2 };
+    int bcost = bprecost;
+    if ((pmv.x | pmv.y) & 3)
+        bcost = xo_f_fpel_sad(&m, bmv.x, bmv.y) + xo_f_mvcost(&m, bmv.x * 4, bmv.y * 4);
+    if (pmv.x || pmv.y)
+    {
+        const int c = xo_f_fpel_sad(&m, 0, 0) + xo_f_mvcost(&m, 0, 0);
+        if (c < bcost) { bcost = c; bmv.x = bmv.y = 0; }
+    }
+    for (int i = 0; i < numc; i++)
+    {
+        const xmv c = xo_clip((xmv){ mvc[2 * i], mvc[2 * i + 1] }, qmin, qmax);
+        if ((c.x || c.y) && (c.x != pmv.x || c.y != pmv.y) && (c.x != bestpre.x || c.y != bestpre.y))
+        {
+            const int cost = xo_subpel_compare(&m, c.x, c.y, 0) + xo_f_mvcost(&m, c.x, c.y);
+            if (cost < bprecost) { bprecost = cost; bestpre = c; }
+        }
+    }
+#define XO_FC(dx, dy) (xo_f_fpel_sad(&m, bmv.x + (dx), bmv.y + (dy)) + \
+                       xo_f_mvcost(&m, (bmv.x + (dx)) * 4, (bmv.y + (dy)) * 4))
+    if (method == 0)
+    {
+        /* diamond, radius 1 (motion.cpp:654-676) */
+        bcost <<= 4;
+        int i = merange;
+        do
+        {
+            const int c0 = XO_FC(0, -1), c1 = XO_FC(0, 1), c2 = XO_FC(-1, 0), c3 = XO_FC(1, 0);
+            if ((c0 << 4) + 1 < bcost) bcost = (c0 << 4) + 1;
+            if ((c1 << 4) + 3 < bcost) bcost = (c1 << 4) + 3;
+            if ((c2 << 4) + 4 < bcost) bcost = (c2 << 4) + 4;
+            if ((c3 << 4) + 12 < bcost) bcost = (c3 << 4) + 12;
+            if (!(bcost & 15)) break;
+            bmv.x -= (int32_t)((uint32_t)bcost << 28) >> 30;
+            bmv.y -= (int32_t)((uint32_t)bcost << 30) >> 30;
+            bcost &= ~15;
+        } while (--i && xo_in_range(bmv, mvmin, mvmax));
+        bcost >>= 4;
+    }
+    else
+    {
+        int c0 = XO_FC(-2, 0), c1 = XO_FC(-1, 2), c2 = XO_FC(1, 2);
+        bcost <<= 3;
+        if ((c0 << 3) + 2 < bcost) bcost = (c0 << 3) + 2;
+        if ((c1 << 3) + 3 < bcost) bcost = (c1 << 3) + 3;
+        if ((c2 << 3) + 4 < bcost) bcost = (c2 << 3) + 4;
+        c0 = XO_FC(2, 0); c1 = XO_FC(1, -2); c2 = XO_FC(-1, -2);
+        if ((c0 << 3) + 5 < bcost) bcost = (c0 << 3) + 5;
+        if ((c1 << 3) + 6 < bcost) bcost = (c1 << 3) + 6;
+        if ((c2 << 3) + 7 < bcost) bcost = (c2 << 3) + 7;
+        if (bcost & 7)
+        {
+            int dir = (bcost & 7) - 2;
+            bmv.x += hex2[dir + 1].x; bmv.y += hex2[dir + 1].y;
+            for (int i = (merange >> 1) - 1; i > 0 && xo_in_range(bmv, mvmin, mvmax); i--)
+            {
+                c0 = XO_FC(hex2[dir + 0].x, hex2[dir + 0].y);
+                c1 = XO_FC(hex2[dir + 1].x, hex2[dir + 1].y);
+                c2 = XO_FC(hex2[dir + 2].x, hex2[dir + 2].y);
+                bcost &= ~7;
+                if ((c0 << 3) + 1 < bcost) bcost = (c0 << 3) + 1;
+                if ((c1 << 3) + 2 < bcost) bcost = (c1 << 3) + 2;
+                if ((c2 << 3) + 3 < bcost) bcost = (c2 << 3) + 3;
+                if (!(bcost & 7)) break;
+                dir += (bcost & 7) - 2;
+                dir = mod6m1[dir + 1];
+                bmv.x += hex2[dir + 1].x; bmv.y += hex2[dir + 1].y;
+            }
+        }
+        bcost >>= 3;
+        int dir = 0;
+        for (int k = 1; k <= 8; k++)
+        {
+            const int c = XO_FC(square1[k].x, square1[k].y);
+            if (c < bcost) { bcost = c; dir = k; }
+        }
+        bmv.x += square1[dir].x; bmv.y += square1[dir].y;
+    }
+#undef XO_FC
+    if (bprecost < bcost) { bmv = bestpre; bcost = bprecost; }
+    else { bmv.x *= 4; bmv.y *= 4; }
+    const int* W = wl[subme];
+    if (!bcost)
+        bcost = xo_f_mvcost(&m, bmv.x, bmv.y);
+    else
+    {
+        int hsatd = W[4];
+        if (hsatd) bcost = xo_subpel_compare(&m, bmv.x, bmv.y, 1) + xo_f_mvcost(&m, bmv.x, bmv.y);
+        for (int it = 0; it < W[0]; it++)
+        {
+            int bdir = 0;
+            for (int i = 1; i <= W[1]; i++)
+            {
+                const int qx = bmv.x + square1[i].x * 2, qy = bmv.y + square1[i].y * 2;
+                const int c = xo_subpel_compare(&m, qx, qy, hsatd) + xo_f_mvcost(&m, qx, qy);
+                if (c < bcost) { bcost = c; bdir = i; }
+            }
+            if (bdir) { bmv.x += square1[bdir].x * 2; bmv.y += square1[bdir].y * 2; }
+            else break;
+        }
+        if (!hsatd) bcost = xo_subpel_compare(&m, bmv.x, bmv.y, 1) + xo_f_mvcost(&m, bmv.x, bmv.y);
+        for (int it = 0; it < W[2]; it++)
+        {
+            int bdir = 0;
+            for (int i = 1; i <= W[3]; i++)
+            {
+                const int qx = bmv.x + square1[i].x, qy = bmv.y + square1[i].y;
+                const int c = xo_subpel_compare(&m, qx, qy, 1) + xo_f_mvcost(&m, qx, qy);
+                if (c < bcost) { bcost = c; bdir = i; }
+            }
+            if (bdir) { bmv.x += square1[bdir].x; bmv.y += square1[bdir].y; }
+            else break;
+        }
+    }
+    out[0] = (int16_t)bmv.x;
+    out[1] = (int16_t)bmv.y;
+    return bcost;
+}
+
+/* BitCost::setQP(qp) table: out[range + d] for |d| <= range.  Restated only for the lookahead QP
+ * (xo_mvcost_table); for other QPs the reference's table is the fixture (lambda_tab is data). */

@@ -374,4 +374,12 @@ struct PixRow
     }
 };
 
+// MotionEstimate direction tables (motion.cpp:61-63) as packed nibbles, so a
+// run-time index is a shift and mask instead of a private-memory array load:
+// hex2[i] = (HEX_DX(i), HEX_DY(i)) for i = 0..7, square1[i] = (SQ_DX(i), SQ_DY(i)) for i = 0..8
+__device__ __forceinline__ int hex_dx(int i) { return (int)((0x1343101ull >> (4 * i)) & 15) - 2; }
+__device__ __forceinline__ int hex_dy(int i) { return (int)((0x20024420ull >> (4 * i)) & 15) - 2; }
+__device__ __forceinline__ int sq_dx(int i) { return (int)((0x220020111ull >> (4 * i)) & 15) - 1; }
+__device__ __forceinline__ int sq_dy(int i) { return (int)((0x202011201ull >> (4 * i)) & 15) - 1; }
+
 } // namespace x265amd

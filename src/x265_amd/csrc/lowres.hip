@@ -462,8 +462,6 @@ template <typename P>
 __device__ int me_lowres(const Blk8<P>& fe, const P* const (&ref)[4], int64_t ls, const MvCost& mc, int minx,
                          int miny, int maxx, int maxy, int mvpx, int mvpy, int& outx, int& outy)
 {
-    constexpr int hx[8] = { -1, -2, -1, 1, 2, 1, -1, -2 }, hy[8] = { -2, 0, 2, 2, 0, -2, -2, 0 };   // hex2
-    constexpr int sx[9] = { 0, 0, 0, -1, 1, -1, -1, 1, 1 }, sy[9] = { 0, -1, 1, 0, 0, -1, 1, -1, 1 };  // square1
     const int pmx = mvpx > 4 * maxx ? 4 * maxx : (mvpx < 4 * minx ? 4 * minx : mvpx);
     const int pmy = mvpy > 4 * maxy ? 4 * maxy : (mvpy < 4 * miny ? 4 * miny : mvpy);
     const int bprecost = qpel_cost<P>(fe, ref, ls, pmx, pmy, false);          // no MV cost (motion.cpp:606)
@@ -492,12 +490,12 @@ __device__ int me_lowres(const Blk8<P>& fe, const P* const (&ref)[4], int64_t ls
         if (bcost & 7)
         {
             int dir = (bcost & 7) - 2;
-            bx += hx[dir + 1]; by += hy[dir + 1];
+            bx += hex_dx(dir + 1); by += hex_dy(dir + 1);
             for (int i = (16 >> 1) - 1; i > 0 && bx >= minx && bx <= maxx && by >= miny && by <= maxy; i--)
             {
-                c0 = cand(hx[dir], hy[dir]);
-                c1 = cand(hx[dir + 1], hy[dir + 1]);
-                c2 = cand(hx[dir + 2], hy[dir + 2]);
+                c0 = cand(hex_dx(dir), hex_dy(dir));
+                c1 = cand(hex_dx(dir + 1), hex_dy(dir + 1));
+                c2 = cand(hex_dx(dir + 2), hex_dy(dir + 2));
                 bcost &= ~7;
                 if ((c0 << 3) + 1 < bcost) bcost = (c0 << 3) + 1;
                 if ((c1 << 3) + 2 < bcost) bcost = (c1 << 3) + 2;
@@ -505,7 +503,7 @@ __device__ int me_lowres(const Blk8<P>& fe, const P* const (&ref)[4], int64_t ls
                 if (!(bcost & 7)) break;
                 dir += (bcost & 7) - 2;
                 dir = dir < 0 ? dir + 6 : (dir > 5 ? dir - 6 : dir);   // mod6m1[dir + 1] = dir mod 6
-                bx += hx[dir + 1]; by += hy[dir + 1];
+                bx += hex_dx(dir + 1); by += hex_dy(dir + 1);
             }
         }
         bcost >>= 3;
@@ -513,10 +511,10 @@ __device__ int me_lowres(const Blk8<P>& fe, const P* const (&ref)[4], int64_t ls
 #pragma unroll
         for (int k = 1; k <= 8; k++)
         {
-            const int c = cand(sx[k], sy[k]);
+            const int c = cand(sq_dx(k), sq_dy(k));
             if (c < bcost) { bcost = c; sdir = k; }
         }
-        bx += sx[sdir]; by += sy[sdir];
+        bx += sq_dx(sdir); by += sq_dy(sdir);
     }
     int qx, qy;
     if (bprecost < bcost) { qx = pmx; qy = pmy; bcost = bprecost; }
@@ -529,19 +527,19 @@ __device__ int me_lowres(const Blk8<P>& fe, const P* const (&ref)[4], int64_t ls
 #pragma unroll
         for (int k = 1; k <= 4; k++)
         {
-            const int c = qpel_cost<P>(fe, ref, ls, qx + 2 * sx[k], qy + 2 * sy[k], false) + mc(qx + 2 * sx[k], qy + 2 * sy[k]);
+            const int c = qpel_cost<P>(fe, ref, ls, qx + 2 * sq_dx(k), qy + 2 * sq_dy(k), false) + mc(qx + 2 * sq_dx(k), qy + 2 * sq_dy(k));
             if (c < bcost) { bcost = c; bdir = k; }
         }
-        qx += 2 * sx[bdir]; qy += 2 * sy[bdir];
+        qx += 2 * sq_dx(bdir); qy += 2 * sq_dy(bdir);
         bcost = qpel_cost<P>(fe, ref, ls, qx, qy, true) + mc(qx, qy);
         bdir = 0;
 #pragma unroll
         for (int k = 1; k <= 4; k++)
         {
-            const int c = qpel_cost<P>(fe, ref, ls, qx + sx[k], qy + sy[k], true) + mc(qx + sx[k], qy + sy[k]);
+            const int c = qpel_cost<P>(fe, ref, ls, qx + sq_dx(k), qy + sq_dy(k), true) + mc(qx + sq_dx(k), qy + sq_dy(k));
             if (c < bcost) { bcost = c; bdir = k; }
         }
-        qx += sx[bdir]; qy += sy[bdir];
+        qx += sq_dx(bdir); qy += sq_dy(bdir);
     }
     outx = qx;
     outy = qy;

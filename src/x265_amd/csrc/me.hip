@@ -1,0 +1,453 @@
+// me.hip — batched full-resolution motion search.
+//
+// One job = one MotionEstimate::motionEstimate call (motion.cpp:571-1172) for a
+// PU on a full-resolution reference, luma only (subme 0..2, the levels that
+// never add chroma SATD, motion.cpp:197): the clipped MVP measured at sub-pel
+// with SAD, the caller's extra MV candidates, DIA or HEX integer search, then
+// the sub-pel refine of workload[subme] whose blocks come from the 8-tap luma
+// filters exactly as subpelCompare builds them (motion.cpp:1174-1203;
+// ipfilter.cpp interp_horiz_pp / interp_vert_pp / interp_hv_pp).
+//
+// Work mapping: a PU is owned by a group of G lanes (G = the PU's 4x4 units
+// rounded up to a power of two, at most 64); every lane keeps the fenc pixels
+// of its units in registers and evaluates its units of every candidate block
+// — full-pel rows straight from the reference, sub-pel rows through the
+// horizontal / vertical / 2-D 8-tap filter computed per unit — and the group
+// sums SAD / SATD partials with shuffles.  Every decision is then identical
+// in all lanes of the group, so the search runs in lockstep in the reference's
+// candidate order (the packed-cost tie rules of the DIA / HEX loops included).
+#include "common.h"
+#include "../../../include/x265_amd.h"
+
+namespace x265amd {
+
+struct MeArgs
+{
+    const void* fenc;
+    const int64_t* fenc_off;
+    int64_t fs;
+    const void* ref;
+    const int64_t* ref_off;
+    int64_t rs;
+    const int16_t* mv_range;
+    const int16_t* mvp;
+    const int16_t* mvc;
+    const uint8_t* num_cand;
+    const uint16_t* mvcost;
+    const int64_t* mvcost_off;
+    int16_t* out_mv;
+    int32_t* out_cost;
+    int w, h, n, lg, method, subme, merange, max_cand, depth;
+};
+
+constexpr int kMeMaxUnits = 4;    // 4x4 units per lane (64x64 PU over 64 lanes)
+
+template <typename P>
+struct MeState
+{
+    const MeArgs* a;
+    const P* ref;           // reference at the PU origin
+    int64_t rs;
+    const uint16_t* tab;
+    int mvpx, mvpy;
+    int nu, lane, G, uw;    // units of this lane, lane in group, group size, units per PU row
+    const P* fenc;          // source PU origin (re-read per evaluation: L1-resident, no dynamic register indexing)
+    int64_t fs;
+
+    __device__ __forceinline__ void unit_xy(int k, int& ux, int& uy) const
+    {
+        const int u = lane + k * G;
+        ux = 4 * (u % uw);
+        uy = 4 * (u / uw);
+    }
+    __device__ __forceinline__ int mvcost(int qx, int qy) const
+    {
+        return (uint16_t)(tab[qx - mvpx] + tab[qy - mvpy]);
+    }
+};
+
+template <typename P>
+__device__ __forceinline__ void load4(const P* p, uint32_t (&w)[sizeof(P) == 1 ? 1 : 2])
+{
+    if constexpr (sizeof(P) == 1) w[0] = ldu<uint32_t>(p);
+    else { const uint2 v = ldu<uint2>(p); w[0] = v.x; w[1] = v.y; }
+}
+
+template <typename P>
+__device__ __forceinline__ uint32_t sad4(const uint32_t (&a)[sizeof(P) == 1 ? 1 : 2],
+                                         const uint32_t (&b)[sizeof(P) == 1 ? 1 : 2], uint32_t acc)
+{
+    if constexpr (sizeof(P) == 1) return __builtin_amdgcn_sad_u8(a[0], b[0], acc);
+    else return __builtin_amdgcn_sad_u16(a[1], b[1], __builtin_amdgcn_sad_u16(a[0], b[0], acc));
+}
+
+template <typename P>
+__device__ __forceinline__ int px(const uint32_t (&w)[sizeof(P) == 1 ? 1 : 2], int i)
+{
+    if constexpr (sizeof(P) == 1) return (int)((w[0] >> (8 * i)) & 0xff);
+    else return (int)((w[i >> 1] >> (16 * (i & 1))) & 0xffff);
+}
+
+__device__ __forceinline__ void had4m(int& a, int& b, int& c, int& d)
+{
+    const int s0 = a + b, s1 = a - b, s2 = c + d, s3 = c - d;
+    a = s0 + s2; b = s1 + s3; c = s0 - s2; d = s1 - s3;
+}
+
+// full-pel SAD of the PU at integer displacement (dx, dy), group-reduced
+template <typename P, int G>
+__device__ __forceinline__ int fpel_sad(const MeState<P>& s, int dx, int dy)
+{
+    uint32_t acc = 0;
+    for (int k = 0; k < s.nu; k++)
+    {
+        int ux, uy;
+        s.unit_xy(k, ux, uy);
+        const P* p = s.ref + (ux + dx) + (int64_t)(uy + dy) * s.rs;
+        const P* f = s.fenc + ux + (int64_t)uy * s.fs;
+#pragma unroll
+        for (int r = 0; r < 4; r++)
+        {
+            uint32_t w[sizeof(P) == 1 ? 1 : 2], e[sizeof(P) == 1 ? 1 : 2];
+            load4<P>(p + r * s.rs, w);
+            load4<P>(f + r * s.fs, e);
+            acc = sad4<P>(e, w, acc);
+        }
+    }
+    return group_sum<G>((int)acc);
+}
+
+// subpelCompare (motion.cpp:1174-1203): the block at quarter-pel (qx, qy), built by
+// luma_hpp / luma_vpp / luma_hvpp when fractional, compared with SAD or SATD
+template <typename P, int G>
+__device__ int subpel_cost(const MeState<P>& s, int qx, int qy, bool satd)
+{
+    const int xf = qx & 3, yf = qy & 3;
+    const P* base = s.ref + (qx >> 2) + (int64_t)(qy >> 2) * s.rs;
+    const int maxv = (1 << s.a->depth) - 1;
+    const int head = 14 - s.a->depth;
+    int cx[8], cy[8];
+#pragma unroll
+    for (int t = 0; t < 8; t++) { cx[t] = c_luma.c[xf][t]; cy[t] = c_luma.c[yf][t]; }
+    int acc = 0;
+    for (int k = 0; k < s.nu; k++)
+    {
+        int ux, uy;
+        s.unit_xy(k, ux, uy);
+        const P* p = base + ux + (int64_t)uy * s.rs;
+        int blk[4][4];
+        if (!(xf | yf))
+        {
+#pragma unroll
+            for (int r = 0; r < 4; r++)
+#pragma unroll
+                for (int c = 0; c < 4; c++) blk[r][c] = p[r * s.rs + c];
+        }
+        else if (!yf)
+        {
+            // interp_horiz_pp: (int16)((sum + 32) >> 6) clipped
+#pragma unroll
+            for (int r = 0; r < 4; r++)
+            {
+                int v[11];
+#pragma unroll
+                for (int i = 0; i < 11; i++) v[i] = p[r * s.rs + i - 3];
+#pragma unroll
+                for (int c = 0; c < 4; c++)
+                {
+                    int sum = 0;
+#pragma unroll
+                    for (int t = 0; t < 8; t++) sum += cx[t] * v[c + t];
+                    const int val = (int16_t)((sum + 32) >> 6);
+                    blk[r][c] = val < 0 ? 0 : (val > maxv ? maxv : val);
+                }
+            }
+        }
+        else if (!xf)
+        {
+            // interp_vert_pp
+            int v[11][4];
+#pragma unroll
+            for (int i = 0; i < 11; i++)
+#pragma unroll
+                for (int c = 0; c < 4; c++) v[i][c] = p[(i - 3) * s.rs + c];
+#pragma unroll
+            for (int r = 0; r < 4; r++)
+#pragma unroll
+                for (int c = 0; c < 4; c++)
+                {
+                    int sum = 0;
+#pragma unroll
+                    for (int t = 0; t < 8; t++) sum += cy[t] * v[r + t][c];
+                    const int val = (int16_t)((sum + 32) >> 6);
+                    blk[r][c] = val < 0 ? 0 : (val > maxv ? maxv : val);
+                }
+        }
+        else
+        {
+            // interp_hv_pp: horizontal ps over 11 rows (int16), then vertical sp
+            const int ps_shift = 6 - head, ps_off = -8192 * (1 << ps_shift);
+            const int sp_shift = 6 + head, sp_off = (1 << (sp_shift - 1)) + (8192 << 6);
+            int m[11][4];
+#pragma unroll
+            for (int i = 0; i < 11; i++)
+            {
+                int v[11];
+#pragma unroll
+                for (int j = 0; j < 11; j++) v[j] = p[(i - 3) * s.rs + j - 3];
+#pragma unroll
+                for (int c = 0; c < 4; c++)
+                {
+                    int sum = 0;
+#pragma unroll
+                    for (int t = 0; t < 8; t++) sum += cx[t] * v[c + t];
+                    m[i][c] = (int16_t)((sum + ps_off) >> ps_shift);
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < 4; r++)
+#pragma unroll
+                for (int c = 0; c < 4; c++)
+                {
+                    int sum = 0;
+#pragma unroll
+                    for (int t = 0; t < 8; t++) sum += cy[t] * m[r + t][c];
+                    const int val = (int16_t)((sum + sp_off) >> sp_shift);
+                    blk[r][c] = val < 0 ? 0 : (val > maxv ? maxv : val);
+                }
+        }
+        uint32_t fe[4][sizeof(P) == 1 ? 1 : 2];
+#pragma unroll
+        for (int r = 0; r < 4; r++) load4<P>(s.fenc + ux + (int64_t)(uy + r) * s.fs, fe[r]);
+        if (satd)
+        {
+            int d[4][4];
+#pragma unroll
+            for (int r = 0; r < 4; r++)
+#pragma unroll
+                for (int c = 0; c < 4; c++) d[r][c] = px<P>(fe[r], c) - blk[r][c];
+#pragma unroll
+            for (int r = 0; r < 4; r++) had4m(d[r][0], d[r][1], d[r][2], d[r][3]);
+            int sum = 0;
+#pragma unroll
+            for (int c = 0; c < 4; c++)
+            {
+                had4m(d[0][c], d[1][c], d[2][c], d[3][c]);
+#pragma unroll
+                for (int r = 0; r < 4; r++) sum += d[r][c] < 0 ? -d[r][c] : d[r][c];
+            }
+            acc += sum >> 1;          // each 4x4 raw sum is even (SURVEY note a7): any tiling gives satd
+        }
+        else
+        {
+#pragma unroll
+            for (int r = 0; r < 4; r++)
+#pragma unroll
+                for (int c = 0; c < 4; c++)
+                {
+                    const int d = px<P>(fe[r], c) - blk[r][c];
+                    acc += d < 0 ? -d : d;
+                }
+        }
+    }
+    return group_sum<G>(acc);
+}
+
+template <typename P, int G>
+__global__ __launch_bounds__(X265AMD_BLOCK) void k_motion_search(const MeArgs a)
+{
+    const int64_t j = (int64_t)xcd_block() * (X265AMD_BLOCK / G) + threadIdx.x / G;
+    if (j >= a.n) return;                               // whole groups
+    MeState<P> s;
+    s.a = &a;
+    s.lane = threadIdx.x & (G - 1);
+    s.G = G;
+    s.uw = a.w >> 2;
+    const int units = s.uw * (a.h >> 2);
+    s.nu = s.lane < units ? (units - s.lane + G - 1) / G : 0;
+    s.ref = (const P*)a.ref + a.ref_off[j];
+    s.rs = a.rs;
+    s.tab = a.mvcost + a.mvcost_off[j];
+    s.fenc = (const P*)a.fenc + a.fenc_off[j];
+    s.fs = a.fs;
+    const int minx = a.mv_range[4 * j], miny = a.mv_range[4 * j + 1];
+    const int maxx = a.mv_range[4 * j + 2], maxy = a.mv_range[4 * j + 3];
+    s.mvpx = a.mvp[2 * j];
+    s.mvpy = a.mvp[2 * j + 1];
+    auto clipq = [&](int& x, int& y) {
+        x = x > 4 * maxx ? 4 * maxx : x; y = y > 4 * maxy ? 4 * maxy : y;
+        x = x < 4 * minx ? 4 * minx : x; y = y < 4 * miny ? 4 * miny : y;
+    };
+    int pmx = s.mvpx, pmy = s.mvpy;
+    clipq(pmx, pmy);
+    int bpx = pmx, bpy = pmy;                          // bestpre
+    int bprecost = subpel_cost<P, G>(s, pmx, pmy, false);   // no MV cost (motion.cpp:609)
+    int bx = (pmx + 2) >> 2, by = (pmy + 2) >> 2;
+    int bcost = bprecost;
+    if ((pmx | pmy) & 3) bcost = fpel_sad<P, G>(s, bx, by) + s.mvcost(4 * bx, 4 * by);
+    if (pmx | pmy)
+    {
+        const int c = fpel_sad<P, G>(s, 0, 0) + s.mvcost(0, 0);
+        if (c < bcost) { bcost = c; bx = by = 0; }
+    }
+    const int nc = a.num_cand ? a.num_cand[j] : 0;
+    for (int i = 0; i < nc; i++)
+    {
+        int cx = a.mvc[2 * (j * a.max_cand + i)], cy = a.mvc[2 * (j * a.max_cand + i) + 1];
+        clipq(cx, cy);
+        if ((cx | cy) && (cx != pmx || cy != pmy) && (cx != bpx || cy != bpy))
+        {
+            const int c = subpel_cost<P, G>(s, cx, cy, false) + s.mvcost(cx, cy);
+            if (c < bprecost) { bprecost = c; bpx = cx; bpy = cy; }
+        }
+    }
+    auto fc = [&](int dx, int dy) { return fpel_sad<P, G>(s, bx + dx, by + dy) + s.mvcost(4 * (bx + dx), 4 * (by + dy)); };
+    if (a.method == 0)
+    {
+        // diamond, radius 1 (motion.cpp:654-676)
+        bcost <<= 4;
+        int i = a.merange;
+        do
+        {
+            const int c0 = fc(0, -1), c1 = fc(0, 1), c2 = fc(-1, 0), c3 = fc(1, 0);
+            if ((c0 << 4) + 1 < bcost) bcost = (c0 << 4) + 1;
+            if ((c1 << 4) + 3 < bcost) bcost = (c1 << 4) + 3;
+            if ((c2 << 4) + 4 < bcost) bcost = (c2 << 4) + 4;
+            if ((c3 << 4) + 12 < bcost) bcost = (c3 << 4) + 12;
+            if (!(bcost & 15)) break;
+            bx -= (int32_t)((uint32_t)bcost << 28) >> 30;
+            by -= (int32_t)((uint32_t)bcost << 30) >> 30;
+            bcost &= ~15;
+        } while (--i && bx >= minx && bx <= maxx && by >= miny && by <= maxy);
+        bcost >>= 4;
+    }
+    else
+    {
+        int c0 = fc(-2, 0), c1 = fc(-1, 2), c2 = fc(1, 2);
+        bcost <<= 3;
+        if ((c0 << 3) + 2 < bcost) bcost = (c0 << 3) + 2;
+        if ((c1 << 3) + 3 < bcost) bcost = (c1 << 3) + 3;
+        if ((c2 << 3) + 4 < bcost) bcost = (c2 << 3) + 4;
+        c0 = fc(2, 0); c1 = fc(1, -2); c2 = fc(-1, -2);
+        if ((c0 << 3) + 5 < bcost) bcost = (c0 << 3) + 5;
+        if ((c1 << 3) + 6 < bcost) bcost = (c1 << 3) + 6;
+        if ((c2 << 3) + 7 < bcost) bcost = (c2 << 3) + 7;
+        if (bcost & 7)
+        {
+            int dir = (bcost & 7) - 2;
+            bx += hex_dx(dir + 1); by += hex_dy(dir + 1);
+            for (int i = (a.merange >> 1) - 1; i > 0 && bx >= minx && bx <= maxx && by >= miny && by <= maxy; i--)
+            {
+                c0 = fc(hex_dx(dir), hex_dy(dir));
+                c1 = fc(hex_dx(dir + 1), hex_dy(dir + 1));
+                c2 = fc(hex_dx(dir + 2), hex_dy(dir + 2));
+                bcost &= ~7;
+                if ((c0 << 3) + 1 < bcost) bcost = (c0 << 3) + 1;
+                if ((c1 << 3) + 2 < bcost) bcost = (c1 << 3) + 2;
+                if ((c2 << 3) + 3 < bcost) bcost = (c2 << 3) + 3;
+                if (!(bcost & 7)) break;
+                dir += (bcost & 7) - 2;
+                dir = dir < 0 ? dir + 6 : (dir > 5 ? dir - 6 : dir);   // mod6m1[dir + 1]
+                bx += hex_dx(dir + 1); by += hex_dy(dir + 1);
+            }
+        }
+        bcost >>= 3;
+        int sdir = 0;
+        for (int k = 1; k <= 8; k++)
+        {
+            const int c = fc(sq_dx(k), sq_dy(k));
+            if (c < bcost) { bcost = c; sdir = k; }
+        }
+        bx += sq_dx(sdir); by += sq_dy(sdir);
+    }
+    int qx, qy;
+    if (bprecost < bcost) { qx = bpx; qy = bpy; bcost = bprecost; }
+    else { qx = 4 * bx; qy = 4 * by; }
+    // workload[subme] (motion.cpp:48-58): hpel_iters 1, dirs 4; qpel_iters 0/1/1, dirs 4; hpel_satd at 2
+    const bool hsatd = a.subme >= 2;
+    const int qiters = a.subme >= 1 ? 1 : 0;
+    if (!bcost)
+        bcost = s.mvcost(qx, qy);
+    else
+    {
+        if (hsatd) bcost = subpel_cost<P, G>(s, qx, qy, true) + s.mvcost(qx, qy);
+        {
+            int bdir = 0;
+            for (int i = 1; i <= 4; i++)
+            {
+                const int tx = qx + 2 * sq_dx(i), ty = qy + 2 * sq_dy(i);
+                const int c = subpel_cost<P, G>(s, tx, ty, hsatd) + s.mvcost(tx, ty);
+                if (c < bcost) { bcost = c; bdir = i; }
+            }
+            qx += 2 * sq_dx(bdir); qy += 2 * sq_dy(bdir);
+        }
+        if (!hsatd) bcost = subpel_cost<P, G>(s, qx, qy, true) + s.mvcost(qx, qy);
+        for (int it = 0; it < qiters; it++)
+        {
+            int bdir = 0;
+            for (int i = 1; i <= 4; i++)
+            {
+                const int tx = qx + sq_dx(i), ty = qy + sq_dy(i);
+                const int c = subpel_cost<P, G>(s, tx, ty, true) + s.mvcost(tx, ty);
+                if (c < bcost) { bcost = c; bdir = i; }
+            }
+            if (!bdir) break;
+            qx += sq_dx(bdir); qy += sq_dy(bdir);
+        }
+    }
+    if (s.lane == 0)
+    {
+        a.out_mv[2 * j] = (int16_t)qx;
+        a.out_mv[2 * j + 1] = (int16_t)qy;
+        a.out_cost[j] = bcost;
+    }
+}
+
+template <typename P>
+static int launch_me(const MeArgs& a, hipStream_t st)
+{
+    const int G = 1 << a.lg;
+    const uint32_t blocks = (uint32_t)((a.n + X265AMD_BLOCK / G - 1) / (X265AMD_BLOCK / G));
+#define L(g) case g: hipLaunchKernelGGL((k_motion_search<P, g>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, a); break;
+    switch (G)
+    {
+        L(1) L(2) L(4) L(8) L(16) L(32) L(64)
+    default: return X265AMD_EINVAL;
+    }
+#undef L
+    return (int)hipGetLastError();
+}
+
+} // namespace x265amd
+
+using namespace x265amd;
+
+extern "C" int x265amd_motion_search(int depth, int count, const x265amd_me_batch* bt, void* stream)
+{
+    if ((depth != 8 && depth != 10 && depth != 12) || count < 0 || (count && !bt)) return X265AMD_EINVAL;
+    for (int i = 0; i < count; i++)
+    {
+        const x265amd_me_batch& b = bt[i];
+        if (b.n < 0 || b.w < 4 || b.h < 4 || b.w > 64 || b.h > 64 || (b.w & 3) || (b.h & 3)) return X265AMD_EINVAL;
+        if (b.method < 0 || b.method > 1 || b.subme < 0 || b.subme > 2 || b.merange < 1) return X265AMD_EINVAL;
+        if (b.n && (!b.fenc || !b.fenc_off || !b.ref || !b.ref_off || !b.mv_range || !b.mvp || !b.mvcost ||
+                    !b.mvcost_off || !b.out_mv || !b.out_cost || (b.num_cand && (!b.mvc || b.max_cand < 1))))
+            return X265AMD_EINVAL;
+    }
+    hipStream_t st = (hipStream_t)stream;
+    for (int i = 0; i < count; i++)
+    {
+        const x265amd_me_batch& b = bt[i];
+        if (!b.n) continue;
+        const int units = (b.w / 4) * (b.h / 4);
+        int g = 1, lg = 0;
+        while (g < units && g < 64) { g <<= 1; lg++; }
+        if ((units + g - 1) / g > kMeMaxUnits) return X265AMD_EINVAL;
+        MeArgs a{ b.fenc, b.fenc_off, (int64_t)b.fenc_stride, b.ref, b.ref_off, (int64_t)b.ref_stride, b.mv_range,
+                  b.mvp, b.mvc, b.num_cand, b.mvcost, b.mvcost_off, b.out_mv, b.out_cost, b.w, b.h, b.n, lg, b.method,
+                  b.subme, b.merange, b.max_cand, depth };
+        const int rc = depth == 8 ? launch_me<uint8_t>(a, st) : launch_me<uint16_t>(a, st);
+        if (rc) return rc;
+    }
+    return 0;
+}

@@ -63,6 +63,13 @@ class LowresPcostBatch(C.Structure):
                 ("row_satd", _vp), ("cost_est", _vp), ("intra_mbs", _vp)]
 
 
+class MeBatch(C.Structure):
+    _fields_ = [("w", _int), ("h", _int), ("n", _int), ("method", _int), ("subme", _int), ("merange", _int),
+                ("max_cand", _int), ("fenc", _vp), ("fenc_stride", _ip), ("fenc_off", _vp), ("ref", _vp),
+                ("ref_stride", _ip), ("ref_off", _vp), ("mv_range", _vp), ("mvp", _vp), ("mvc", _vp), ("num_cand", _vp),
+                ("mvcost", _vp), ("mvcost_off", _vp), ("out_mv", _vp), ("out_cost", _vp)]
+
+
 def _addr(t):
     return None if t is None else t.data_ptr()
 
@@ -240,3 +247,12 @@ class Primitives:
         b = LowresPcostBatch(n, wcu, hcu, rps, ns, _addr(planes), ls, _addr(fo), _addr(ro), _addr(ic), _addr(iq),
                              tab_centre_ptr, _addr(mvs), _addr(mc), _addr(lc), _addr(rs), _addr(ce), _addr(mbs))
         self._check(self.lib.x265amd_lowres_pcost(depth, C.byref(b), stream or _stream()), "lowres_pcost")
+
+    # -- f2 full-resolution motion search
+    def motion_search(self, depth, w, h, method, subme, merange, max_cand, f, fs, fo, r, rs, ro, rng, mvp, mvc, numc,
+                      tab, tab_off, out_mv, out_cost, stream=None):
+        arr = (MeBatch * 1)()
+        arr[0] = MeBatch(w, h, fo.numel(), method, subme, merange, max_cand, _addr(f), fs, _addr(fo), _addr(r), rs,
+                         _addr(ro), _addr(rng), _addr(mvp), _addr(mvc), _addr(numc), _addr(tab), _addr(tab_off),
+                         _addr(out_mv), _addr(out_cost))
+        self._check(self.lib.x265amd_motion_search(depth, 1, arr, stream or _stream()), "motion_search")

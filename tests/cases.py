@@ -566,6 +566,66 @@ def lowres_pcost_cases(depth: int):
             case_lowres_pcost(640, 360, 1, 10, 2, True, depth, seed_of(depth, "lp", 2))]
 
 
+ME_QPS = (22, 27, 32, 37)
+ME_TAB_RANGE = 2048
+
+
+def me_tables(depth: int) -> np.ndarray:
+    """the reference's BitCost tables for ME_QPS (tests/golden/mvcost_qp_d{8,10}.npy, made by make_golden.py),
+    concatenated: table q spans [q * (2R + 1), (q + 1) * (2R + 1)), centre at + R"""
+    import os
+
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", f"mvcost_qp_d{depth}.npy")
+    return np.load(path).reshape(-1)
+
+
+def case_me(w: int, h: int, method: int, subme: int, merange: int, depth: int, n: int, seed: int) -> Case:
+    """f2: n PUs of the synthetic sequence (frame 1 searched in frame 0; pan (+2, +1) px/frame, moving object,
+    noise), both planes edge-padded by 96 px like PicYuv.  MVP = the true pan +- a few quarter-pels, 0..3 AMVP-like
+    candidates nearby, per-PU QP from ME_QPS, MV range = the picture + 24 px (the search stays inside the padding)."""
+    import os
+    import sys
+
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from src.x265_amd.synth import SyntheticSource
+
+    det = Det(seed)
+    W, H, M = 256, 160, 96
+    pdt = pixel_dtype(depth)
+    src = SyntheticSource(W, H, 2, depth, seed=seed % 100000)
+    pad = lambda y: np.pad(y.astype(np.int64), M, mode="edge").astype(pdt).reshape(-1)
+    f1, f0 = pad(src.frame(1)[0]), pad(src.frame(0)[0])
+    st = W + 2 * M
+    xs, ys = det.ints(0, W - w + 1, n), det.ints(0, H - h + 1, n)
+    fo = np.array([(int(y) + M) * st + int(x) + M for x, y in zip(xs, ys)], np.int64)
+    rng = np.array([[-int(x) - 24, -int(y) - 24, W - int(x) - w + 24, H - int(y) - h + 24] for x, y in zip(xs, ys)],
+                   np.int16).reshape(-1)
+    mvp = np.stack([-8 + det.ints(-6, 7, n), -4 + det.ints(-6, 7, n)], 1).astype(np.int16).reshape(-1)
+    max_cand = 3
+    numc = det.ints(0, max_cand + 1, n).astype(np.uint8)
+    mvc = det.ints(-48, 49, 2 * max_cand * n).astype(np.int16)
+    qi = det.ints(0, len(ME_QPS), n)
+    R = ME_TAB_RANGE
+    tab_off = (qi * (2 * R + 1) + R).astype(np.int64)
+    qp = np.array([ME_QPS[i] for i in qi], np.uint8)
+    bufs = dict(f=f1, fs=st, fo=fo, r=f0, rs=st, ro=fo.copy(), rng=rng, mvp=mvp, mvc=mvc, numc=numc,
+                tab=me_tables(depth), tab_off=tab_off, qp=qp, out_mv=np.full(2 * n, -21846, np.int16),
+                out_cost=np.full(n, -1, np.int32))
+    return Case("me", dict(w=w, h=h, method=method, subme=subme, merange=merange, max_cand=max_cand, depth=depth,
+                           n=n, seed=seed), bufs, ["out_mv", "out_cost"])
+
+
+def me_cases(depth: int, n: int = 24):
+    out = []
+    for (w, h) in LUMA_PU[1:]:
+        out.append(case_me(w, h, 1, 2, 57, depth, n, seed_of(depth, "me", w, h)))
+    for (w, h) in ((8, 8), (16, 16), (32, 32), (64, 64)):
+        for method, subme in ((0, 0), (0, 1), (1, 1), (0, 2)):
+            out.append(case_me(w, h, method, subme, 16 if method == 0 else 57, depth, n,
+                               seed_of(depth, "me-m", w, h, method, subme)))
+    return out
+
+
 def lowres_cases(depth: int):
     return [case_lowres(64, 32, 1, False, depth, seed_of(depth, "lr", 0)),
             case_lowres(136, 72, 2, True, depth, seed_of(depth, "lr", 1)),
@@ -645,6 +705,7 @@ def all_cases(depth: int, n: int = 6, quick: bool = False):
     cases += tu_cases(depth)
     cases += lowres_cases(depth)
     cases += lowres_pcost_cases(depth)
+    cases += me_cases(depth)
     return cases
 
 
@@ -685,6 +746,10 @@ def run_cpu(case: Case, orc) -> dict:
         orc.lowres_pcost(p["n"], p["wcu"], p["hcu"], p["rps"], p["ns"], b["planes"], p["ls"], b["fo"], b["ro"], b["ic"],
                          b["iq"], b["tab"].ctypes.data + 2 * MVCOST_RANGE, b["mvs"], b["mc"], b["lc"], b["rs"], b["ce"],
                          b["mbs"])
+    elif f == "me":
+        orc.motion_search(p["w"], p["h"], p["method"], p["subme"], p["merange"], p["max_cand"], b["f"], b["fs"], b["fo"],
+                          b["r"], b["rs"], b["ro"], b["rng"], b["mvp"], b["mvc"], b["numc"], b["tab"], b["tab_off"],
+                          b["qp"], b["out_mv"], b["out_cost"])
     elif f == "tu":
         orc.tu(p["log2"], p["luma"], p["intra"], p["islice"], p["sh"], b["f"], b["fs"], b["fo"], b["p"], b["ps"],
                b["po"], b["r"], b["rs"], b["ro"], b["c"], b["co"], b["rc"], b["rcs"], b["rco"], b["sig"], b["qp"],
@@ -747,6 +812,10 @@ def run_gpu(case: Case, prims, device="cuda") -> dict:
         prims.lowres_pcost(d, p["n"], p["wcu"], p["hcu"], p["rps"], p["ns"], b["planes"], p["ls"], b["fo"], b["ro"],
                            b["ic"], b["iq"], b["tab"].data_ptr() + 2 * MVCOST_RANGE, b["mvs"], b["mc"], b["lc"], b["rs"],
                            b["ce"], b["mbs"])
+    elif f == "me":
+        prims.motion_search(d, p["w"], p["h"], p["method"], p["subme"], p["merange"], p["max_cand"], b["f"], b["fs"],
+                            b["fo"], b["r"], b["rs"], b["ro"], b["rng"], b["mvp"], b["mvc"], b["numc"], b["tab"],
+                            b["tab_off"], b["out_mv"], b["out_cost"])
     elif f == "tu":
         prims.tu_pipeline(d, p["log2"], p["luma"], p["intra"], p["islice"], p["sh"], b["f"], b["fs"], b["fo"], b["p"],
                           b["ps"], b["po"], b["r"], b["rs"], b["ro"], b["c"], b["co"], b["rc"], b["rcs"], b["rco"],

@@ -40,6 +40,14 @@ def main() -> None:
         ref = CpuOracle("ref", depth)
         # the lookahead's BitCost table (input of the lowres P-estimate cases), from the reference
         np.save(os.path.join(HERE, f"mvcost_lookahead_d{depth}.npy"), ref.mvcost_table(MVCOST_RANGE))
+        # BitCost tables of the motion-search cases' QPs (lambda_tab is reference data, taken as input)
+        import ctypes as C
+        from cases import ME_QPS, ME_TAB_RANGE
+        lib = C.CDLL(os.path.join(ROOT, "oracle", "_ref", f"libx265ref{depth}.so"))
+        tabs = np.zeros((len(ME_QPS), 2 * ME_TAB_RANGE + 1), np.uint16)
+        for k, qp in enumerate(ME_QPS):
+            lib.xo_mvcost_table_qp(qp, ME_TAB_RANGE, C.c_void_p(tabs[k].ctypes.data))
+        np.save(os.path.join(HERE, f"mvcost_qp_d{depth}.npy"), tabs)
         entries = []
         for c in all_cases(depth):
             outs = run_cpu(c, ref)

@@ -1,0 +1,50 @@
+"""f2 full-resolution motion search (x265amd_motion_search).
+
+Parity chain: the reference's own MotionEstimate::motionEstimate (motion.cpp:571-1172,
+driven through oracle/ref_shim.cpp with its own BitCost tables) -> golden hashes (the `me`
+cases of cases.all_cases: every luma PU shape with HEX / subme 2 as at --preset medium,
+DIA and subme 0 / 1 on the square sizes) -> oracle restatement (xo_motion_search) [CPU]
+-> gfx950 kernel k_motion_search [GPU].  Output MVs and costs bit-exact.
+"""
+import numpy as np
+import pytest
+
+from cases import LUMA_PU, case_me, me_cases, run_cpu, run_gpu, seed_of
+from pyoracle import CpuOracle, available
+
+
+@pytest.mark.skipif(not available("ref", 8), reason="reference library oracle/_ref not built")
+@pytest.mark.parametrize("depth", [8, 10])
+def test_me_oracle_matches_reference(oracle_libs, depth):
+    orc, ref = CpuOracle("oracle", depth), CpuOracle("ref", depth)
+    for (w, h) in ((8, 8), (16, 16), (64, 64), (32, 8), (12, 16)):
+        for method, subme in ((1, 2), (0, 1)):
+            c = case_me(w, h, method, subme, 57 if method else 16, depth, 64, seed_of("me-r", depth, w, h, method))
+            a, b = run_cpu(c, orc), run_cpu(c, ref)
+            for k in c.outs:
+                assert np.array_equal(a[k], b[k]), (c.key(), k)
+
+
+@pytest.mark.parametrize("depth", [8, 10])
+def test_me_cases_exercise_search(oracle_libs, depth):
+    """results include quarter-pel, half-pel and full-pel MVs and MVs away from the MVP"""
+    orc = CpuOracle("oracle", depth)
+    mvs = np.concatenate([run_cpu(c, orc)["out_mv"].reshape(-1, 2) for c in me_cases(depth)[:8]])
+    frac = mvs & 3
+    assert (frac == 1).any() or (frac == 3).any()
+    assert (frac == 2).any() and (frac == 0).all(axis=1).any()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("depth", [8, 10])
+def test_me_gpu_matches_oracle(gpu_prims, oracle_libs, depth):
+    orc = CpuOracle("oracle", depth)
+    cases = me_cases(depth) + [case_me(w, h, 1, 2, 57, depth, 512, seed_of("me-g", depth, w, h))
+                               for (w, h) in ((8, 8), (16, 16), (32, 32), (64, 64))]
+    bad = []
+    for c in cases:
+        got, exp = run_gpu(c, gpu_prims), run_cpu(c, orc)
+        for k in c.outs:
+            if not np.array_equal(got[k], exp[k]):
+                bad.append((c.key(), k, int((got[k] != exp[k]).sum())))
+    assert not bad, bad[:6]

@@ -412,6 +412,61 @@ def main():
         results.append(r)
         print(json.dumps(r), flush=True)
         del SRC, PL, IC, IM, LC, RS, CE, IQ, MVS, MC, PLC, PRS, PCE, MB
+    # ---------------------------------------------------------------- f2 motion search
+    # HEX + subme 2 + merange 57 (--preset medium) on the synthetic 1080p pair (pan +2/+1, object, noise):
+    # every 2Nx2N PU of the frame at 8 / 16 / 32 / 64 (one batch per size), MVP = true pan +- jitter,
+    # 2 candidates, QP 32.  Search-bound (serial dependent SAD rounds per PU); reported as PUs/s with
+    # the reference's MotionEstimate::motionEstimate timed on one host core on the same jobs.
+    for s_ in (8, 16, 32, 64):
+        name = f"me_hex_{s_}x{s_}"
+        if not want(name):
+            continue
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        from cases import ME_TAB_RANGE, me_tables
+        from src.x265_amd.synth import SyntheticSource
+        Wf, Hf, M = 1920, 1080, 96
+        syn = SyntheticSource(Wf, Hf, 2, 8)
+        padf = lambda y: np.pad(y, M, mode="edge").reshape(-1)
+        f1, f0 = padf(syn.frame(1)[0]), padf(syn.frame(0)[0])
+        st = Wf + 2 * M
+        xs, ys = np.meshgrid(np.arange(0, Wf - s_ + 1, s_), np.arange(0, Hf - s_ + 1, s_))
+        xs, ys = xs.reshape(-1), ys.reshape(-1)
+        n = xs.size
+        rng_ = np.random.default_rng(s_)
+        fo_h = ((ys + M) * st + xs + M).astype(np.int64)
+        rng_h = np.stack([-xs - 24, -ys - 24, Wf - xs - s_ + 24, Hf - ys - s_ + 24], 1).astype(np.int16).reshape(-1)
+        mvp_h = np.stack([-8 + rng_.integers(-4, 5, n), -4 + rng_.integers(-4, 5, n)], 1).astype(np.int16).reshape(-1)
+        mvc_h = rng_.integers(-16, 17, 2 * 2 * n).astype(np.int16)
+        numc_h = np.full(n, 2, np.uint8)
+        tabs = me_tables(8)
+        toff_h = np.full(n, 2 * (2 * ME_TAB_RANGE + 1) + ME_TAB_RANGE, np.int64)   # ME_QPS[2] = 32
+        T = lambda x: torch.from_numpy(np.ascontiguousarray(x)).to(dev)
+        F1, F0, FO, RG, MP, MC2, NC, TB, TO = (T(f1), T(f0), T(fo_h), T(rng_h), T(mvp_h), T(mvc_h), T(numc_h),
+                                               T(tabs), T(toff_h))
+        OM = torch.empty(2 * n, dtype=torch.int16, device=dev)
+        OC = torch.empty(n, dtype=torch.int32, device=dev)
+        ms_me = timeit(lambda: prims.motion_search(8, s_, s_, 1, 2, 57, 2, F1, st, FO, F0, st, FO, RG, MP, MC2, NC, TB,
+                                                   TO, OM, OC))
+        r = {"kernel": name, "jobs": n, "ms": round(ms_me, 4), "pu_per_s": round(n / (ms_me * 1e-3), 1),
+             "bound": "latency (serial SAD rounds per PU)"}
+        try:
+            from pyoracle import CpuOracle, available
+            if available("ref", 8):
+                import time as _t
+                ref = CpuOracle("ref", 8)
+                k = min(n, 2000)
+                om, oc = np.empty(2 * k, np.int16), np.empty(k, np.int32)
+                t0 = _t.perf_counter()
+                ref.motion_search(s_, s_, 1, 2, 57, 2, f1, st, fo_h[:k], f0, st, fo_h[:k], rng_h[:4 * k], mvp_h[:2 * k],
+                                  mvc_h[:4 * k], numc_h[:k], tabs, toff_h[:k], np.full(k, 32, np.uint8), om, oc)
+                r["cpu_reference_1core_pu_per_s"] = round(k / (_t.perf_counter() - t0), 1)
+                r["gpu_matches_reference_on_sample"] = bool(np.array_equal(om, OM[:2 * k].cpu().numpy()) and
+                                                            np.array_equal(oc, OC[:k].cpu().numpy()))
+        except Exception as ex:
+            r["cpu_reference_error"] = str(ex)
+        results.append(r)
+        print(json.dumps(r), flush=True)
     if a.out:
         with open(a.out, "w") as f:
             json.dump({"hbm_peak_GBps": HBM, "working_set_GB": a.gb, "results": results}, f, indent=1)
