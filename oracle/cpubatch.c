@@ -70,7 +70,8 @@ typedef struct
                      int32_t*);
     void (*mvtab)(int, uint16_t*);
     int (*me)(int, int, int, int, int, const void*, intptr_t, const void*, intptr_t, int, int, int, int, int, int, int,
-              const int16_t*, const uint16_t*, int16_t*);
+              const int16_t*, const uint16_t*, int16_t*, const void*, const void*, intptr_t, const void*, const void*,
+              intptr_t);
     void (*set_me_qp)(int);   /* reference shim only: its BitCost QP (the restatement reads the table) */
 } Lib;
 
@@ -549,17 +550,22 @@ void cb_mvcost_table(void* h, int range, uint16_t* out) { ((Lib*)h)->mvtab(range
 int cb_motion_search(void* h, int64_t n, int w, int hh, int method, int subme, int merange, int max_cand,
                      const void* fenc, intptr_t fs, const int64_t* fo, const void* ref, intptr_t rs, const int64_t* ro,
                      const int16_t* range, const int16_t* mvp, const int16_t* mvc, const uint8_t* numc,
-                     const uint16_t* tab, const int64_t* tab_off, const uint8_t* qp, int16_t* out_mv, int32_t* out_cost)
+                     const uint16_t* tab, const int64_t* tab_off, const uint8_t* qp, int16_t* out_mv, int32_t* out_cost,
+                     const void* fcb, const void* fcr, intptr_t fcs, const int64_t* fco, const void* rcb, const void* rcr,
+                     intptr_t rcs, const int64_t* rco)
 {
     Lib* L = (Lib*)h;
     const int b = L->depth > 8 ? 2 : 1;
     for (int64_t i = 0; i < n; i++)
     {
         if (L->set_me_qp) L->set_me_qp(qp[i]);
+        const int ch = fcb != NULL;
         out_cost[i] = L->me(w, hh, method, subme, merange, (const char*)fenc + fo[i] * b, fs,
                             (const char*)ref + ro[i] * b, rs, range[4 * i], range[4 * i + 1], range[4 * i + 2],
                             range[4 * i + 3], mvp[2 * i], mvp[2 * i + 1], numc ? numc[i] : 0,
-                            mvc + 2 * i * max_cand, tab + tab_off[i], out_mv + 2 * i);
+                            mvc + 2 * i * max_cand, tab + tab_off[i], out_mv + 2 * i,
+                            ch ? (const char*)fcb + fco[i] * b : NULL, ch ? (const char*)fcr + fco[i] * b : NULL, fcs,
+                            ch ? (const char*)rcb + rco[i] * b : NULL, ch ? (const char*)rcr + rco[i] * b : NULL, rcs);
     }
     return 0;
 }

@@ -119,10 +119,12 @@ class CpuOracle:
         return out
 
     def motion_search(self, w, h, method, subme, merange, max_cand, f, fs, fo, r, rs, ro, rng, mvp, mvc, numc, tab,
-                      tab_off, qp, out_mv, out_cost):
+                      tab_off, qp, out_mv, out_cost, fcb=None, fcr=None, fcs=0, fco=None, rcb=None, rcr=None, rcs=0,
+                      rco=None):
         self.cb.cb_motion_search(_vp(self.h), _i64(len(fo)), w, h, method, subme, merange, max_cand, _p(f), _ip(fs),
                                  _p(fo), _p(r), _ip(rs), _p(ro), _p(rng), _p(mvp), _p(mvc), _p(numc), _p(tab),
-                                 _p(tab_off), _p(qp), _p(out_mv), _p(out_cost))
+                                 _p(tab_off), _p(qp), _p(out_mv), _p(out_cost), _p(fcb), _p(fcr), _ip(fcs), _p(fco),
+                                 _p(rcb), _p(rcr), _ip(rcs), _p(rco))
 
     def scan_table(self, typ, log2):
         out = np.zeros(1 << (2 * log2), np.uint16)

@@ -552,6 +552,8 @@ struct TabBitCost : public BitCost
 struct SearchME : public MotionEstimate
 {
     void configure(int method, int refine) { searchMethod = method; subpelRefine = refine; }
+    void chroma(pixelcmp_t cs) { chromaSatd = cs; bChromaSATD = subpelRefine > 2 && cs; }
+    void at_ctu0() { ctuAddr = 0; absPartIdx = 0; }   /* chroma addressing goes through the PicYuv offsets */
 };
 struct CostGroup : public CostEstimateGroup
 {
@@ -675,7 +677,8 @@ void xo_mvcost_table_qp(int qp, int range, uint16_t* out)
  * (fpelPlane[0] at the PU origin, no PicYuv: ctuAddr stays -1 so blockOffset = 0, luma only) */
 int xo_motion_search(int w, int h, int method, int subme, int merange, const void* fenc, intptr_t fs, const void* ref,
                      intptr_t rs, int minx, int miny, int maxx, int maxy, int mvpx, int mvpy, int numc,
-                     const int16_t* mvc, const uint16_t* tab_centre, int16_t* out)
+                     const int16_t* mvc, const uint16_t* tab_centre, int16_t* out,
+                     const void* fcb, const void* fcr, intptr_t fcs, const void* rcb, const void* rcr, intptr_t rcs)
 {
     (void)tab_centre;    /* the reference uses its own BitCost table: the caller sets the QP below */
     pthread_once(&g_prim_once, init_global_prims);
@@ -684,19 +687,46 @@ int xo_motion_search(int w, int h, int method, int subme, int merange, const voi
     {
         MotionEstimate::initScales();
         me = new SearchME();
-        me->init(X265_HEX_SEARCH, 2, X265_CSP_I400);   /* allocates the fenc PU buffer once */
+        me->init(X265_HEX_SEARCH, 2, X265_CSP_I420);   /* allocates the 4:2:0 fenc PU buffers once */
     }
-    me->configure(method == 0 ? X265_DIA_SEARCH : X265_HEX_SEARCH, subme);
+    me->configure(method == 0 ? X265_DIA_SEARCH : method == 1 ? X265_HEX_SEARCH : X265_STAR_SEARCH, subme);
     me->setQP(g_me_qp);
     me->setSourcePU((pixel*)fenc, fs, 0, w, h);
+    /* chroma PU as Yuv::copyPUFromYuv would place it, and bChromaSATD as the encoder's setSourcePU
+     * sets it (motion.cpp:183-197) */
+    pixelcmp_t cs = fcb ? primitives.chroma[X265_CSP_I420].pu[me->partEnum].satd : NULL;
+    me->chroma(cs);
+    static intptr_t zero_off[2] = { 0, 0 };
+    PicYuv* pic = (PicYuv*)calloc(1, sizeof(PicYuv));
     ReferencePlanes rp;
     rp.fpelPlane[0] = (pixel*)ref;
     rp.lumaStride = rs;
     rp.isLowres = false;
+    if (me->bChromaSATD)
+    {
+        for (int y = 0; y < (h >> 1); y++)
+            for (int x = 0; x < (w >> 1); x++)
+            {
+                me->fencPUYuv.m_buf[1][y * me->fencPUYuv.m_csize + x] = ((const pixel*)fcb)[y * fcs + x];
+                me->fencPUYuv.m_buf[2][y * me->fencPUYuv.m_csize + x] = ((const pixel*)fcr)[y * fcs + x];
+            }
+        /* chroma addresses come from reconPic's CU / block offsets (lowres.h:52-54): address the PU as
+         * CTU 0 / part 0 of a picture whose offsets are all 0, so blockOffset stays 0 (motion.cpp:582) */
+        pic->m_cuOffsetY = zero_off;
+        pic->m_buOffsetY = zero_off;
+        pic->m_cuOffsetC = zero_off;
+        pic->m_buOffsetC = zero_off;
+        pic->m_strideC = rcs;
+        me->at_ctu0();
+        rp.fpelPlane[1] = (pixel*)rcb;
+        rp.fpelPlane[2] = (pixel*)rcr;
+        rp.reconPic = pic;
+    }
     MV mvs[16];
     for (int i = 0; i < numc && i < 16; i++) mvs[i] = MV(mvc[2 * i], mvc[2 * i + 1]);
     MV outmv;
     const int cost = me->motionEstimate(&rp, MV(minx, miny), MV(maxx, maxy), MV(mvpx, mvpy), numc, mvs, merange, outmv);
+    free(pic);
     out[0] = outmv.x;
     out[1] = outmv.y;
     return cost;

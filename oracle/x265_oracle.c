@@ -1269,6 +1269,9 @@ typedef struct
     const pix* ref; intptr_t rs;        /* reference at the PU origin */
     const uint16_t* tab;
     xmv mvp;
+    int chroma;                         /* bChromaSATD (subme > 2 and a 4:2:0 chroma satd entry exists) */
+    const pix* fc[2]; intptr_t fcs;     /* source Cb / Cr at the PU's chroma origin */
+    const pix* rc[2]; intptr_t rcs;     /* reference Cb / Cr at the PU's chroma origin */
 } XoMeF;
 
 static int xo_f_mvcost(const XoMeF* m, int qx, int qy)
@@ -1296,19 +1299,153 @@ static int xo_subpel_compare(const XoMeF* m, int qx, int qy, int use_satd)
         p = buf;
         ps = 64;
     }
-    return use_satd ? xo_satd(m->w, m->h, m->fenc, m->fs, p, ps) : xo_sad(m->w, m->h, m->fenc, m->fs, p, ps);
+    int cost = use_satd ? xo_satd(m->w, m->h, m->fenc, m->fs, p, ps) : xo_sad(m->w, m->h, m->fenc, m->fs, p, ps);
+    if (m->chroma)
+    {
+        /* chroma SATD at the 1/8-pel chroma position (motion.cpp:1205-1266, 4:2:0) */
+        const int cw = m->w >> 1, chh = m->h >> 1;
+        const intptr_t off = (qx >> 3) + (qy >> 3) * m->rcs;
+        const int cxf = qx & 7, cyf = qy & 7;
+        for (int k = 0; k < 2; k++)
+        {
+            const pix* rc = m->rc[k] + off;
+            if (!(cxf | cyf))
+                cost += xo_satd(cw, chh, m->fc[k], m->fcs, rc, m->rcs);
+            else
+            {
+                pix cb[64 * 32];
+                if (!cyf) xo_interp(XO_HPP, 4, cw, chh, rc, m->rcs, cb, 64, cxf, 0);
+                else if (!cxf) xo_interp(XO_VPP, 4, cw, chh, rc, m->rcs, cb, 64, cyf, 0);
+                else
+                {
+                    int16_t immed[32 * (32 + 3)];
+                    xo_interp(XO_HPS, 4, cw, chh, rc, m->rcs, immed, cw, cxf, 1);
+                    xo_interp(XO_VSP, 4, cw, chh, immed + cw, cw, cb, 64, cyf, 0);
+                }
+                cost += xo_satd(cw, chh, m->fc[k], m->fcs, cb, 64);
+            }
+        }
+    }
+    return cost;
+}
+
+/* MotionEstimate::StarPatternSearch (motion.cpp:328-569) */
+static void xo_star(XoMeF* m, xmv mvmin, xmv mvmax, xmv* bmv, int* bcost, int* bPointNr, int* bDistance,
+                    int earlyExitIters, int merange)
+{
+    const xmv omv = *bmv;
+    int saved = *bcost, rounds = 0;
+#define PT(mx, my, pt, dd) do { \
+        const int c_ = xo_f_fpel_sad(m, (mx), (my)) + xo_f_mvcost(m, (mx) * 4, (my) * 4); \
+        if (c_ < *bcost) { *bcost = c_; bmv->x = (mx); bmv->y = (my); *bPointNr = (pt); *bDistance = (dd); } } while (0)
+    {
+        const int dist = 1;
+        const int top = omv.y - dist, bottom = omv.y + dist, left = omv.x - dist, right = omv.x + dist;
+        if (top >= mvmin.y && left >= mvmin.x && right <= mvmax.x && bottom <= mvmax.y)
+        {
+            PT(omv.x, top, 2, dist); PT(left, omv.y, 4, dist); PT(right, omv.y, 5, dist); PT(omv.x, bottom, 7, dist);
+        }
+        else
+        {
+            if (top >= mvmin.y) PT(omv.x, top, 2, dist);
+            if (left >= mvmin.x) PT(left, omv.y, 4, dist);
+            if (right <= mvmax.x) PT(right, omv.y, 5, dist);
+            if (bottom <= mvmax.y) PT(omv.x, bottom, 7, dist);
+        }
+        if (*bcost < saved) rounds = 0;
+        else if (++rounds >= earlyExitIters) return;
+    }
+    for (int dist = 2; dist <= 8; dist <<= 1)
+    {
+        const int top = omv.y - dist, bottom = omv.y + dist, left = omv.x - dist, right = omv.x + dist;
+        const int top2 = omv.y - (dist >> 1), bottom2 = omv.y + (dist >> 1);
+        const int left2 = omv.x - (dist >> 1), right2 = omv.x + (dist >> 1);
+        saved = *bcost;
+        if (top >= mvmin.y && left >= mvmin.x && right <= mvmax.x && bottom <= mvmax.y)
+        {
+            PT(omv.x, top, 2, dist); PT(left2, top2, 1, dist >> 1); PT(right2, top2, 3, dist >> 1);
+            PT(left, omv.y, 4, dist);
+            PT(right, omv.y, 5, dist); PT(left2, bottom2, 6, dist >> 1); PT(right2, bottom2, 8, dist >> 1);
+            PT(omv.x, bottom, 7, dist);
+        }
+        else
+        {
+            if (top >= mvmin.y) PT(omv.x, top, 2, dist);
+            if (top2 >= mvmin.y)
+            {
+                if (left2 >= mvmin.x) PT(left2, top2, 1, dist >> 1);
+                if (right2 <= mvmax.x) PT(right2, top2, 3, dist >> 1);
+            }
+            if (left >= mvmin.x) PT(left, omv.y, 4, dist);
+            if (right <= mvmax.x) PT(right, omv.y, 5, dist);
+            if (bottom2 <= mvmax.y)
+            {
+                if (left2 >= mvmin.x) PT(left2, bottom2, 6, dist >> 1);
+                if (right2 <= mvmax.x) PT(right2, bottom2, 8, dist >> 1);
+            }
+            if (bottom <= mvmax.y) PT(omv.x, bottom, 7, dist);
+        }
+        if (*bcost < saved) rounds = 0;
+        else if (++rounds >= earlyExitIters) return;
+    }
+    for (int dist = 16; dist <= merange; dist <<= 1)
+    {
+        const int top = omv.y - dist, bottom = omv.y + dist, left = omv.x - dist, right = omv.x + dist;
+        saved = *bcost;
+        if (top >= mvmin.y && left >= mvmin.x && right <= mvmax.x && bottom <= mvmax.y)
+        {
+            PT(omv.x, top, 0, dist); PT(left, omv.y, 0, dist); PT(right, omv.y, 0, dist); PT(omv.x, bottom, 0, dist);
+            for (int index = 1; index < 4; index++)
+            {
+                const int yt = top + ((dist >> 2) * index), yb = bottom - ((dist >> 2) * index);
+                const int xl = omv.x - ((dist >> 2) * index), xr = omv.x + ((dist >> 2) * index);
+                PT(xl, yt, 0, dist); PT(xr, yt, 0, dist); PT(xl, yb, 0, dist); PT(xr, yb, 0, dist);
+            }
+        }
+        else
+        {
+            if (top >= mvmin.y) PT(omv.x, top, 0, dist);
+            if (left >= mvmin.x) PT(left, omv.y, 0, dist);
+            if (right <= mvmax.x) PT(right, omv.y, 0, dist);
+            if (bottom <= mvmax.y) PT(omv.x, bottom, 0, dist);
+            for (int index = 1; index < 4; index++)
+            {
+                const int yt = top + ((dist >> 2) * index), yb = bottom - ((dist >> 2) * index);
+                const int xl = omv.x - ((dist >> 2) * index), xr = omv.x + ((dist >> 2) * index);
+                if (yt >= mvmin.y)
+                {
+                    if (xl >= mvmin.x) PT(xl, yt, 0, dist);
+                    if (xr <= mvmax.x) PT(xr, yt, 0, dist);
+                }
+                if (yb <= mvmax.y)
+                {
+                    if (xl >= mvmin.x) PT(xl, yb, 0, dist);
+                    if (xr <= mvmax.x) PT(xr, yb, 0, dist);
+                }
+            }
+        }
+        if (*bcost < saved) rounds = 0;
+        else if (++rounds >= earlyExitIters) return;
+    }
+#undef PT
 }
 
 int xo_motion_search(int w, int h, int method, int subme, int merange, const void* fenc, intptr_t fs, const void* ref,
                      intptr_t rs, int minx, int miny, int maxx, int maxy, int mvpx, int mvpy, int numc,
-                     const int16_t* mvc, const uint16_t* tab_centre, int16_t* out)
+                     const int16_t* mvc, const uint16_t* tab_centre, int16_t* out,
+                     const void* fcb, const void* fcr, intptr_t fcs, const void* rcb, const void* rcr, intptr_t rcs)
 {
     static const xmv hex2[8] = { { -1, -2 }, { -2, 0 }, { -1, 2 }, { 1, 2 }, { 2, 0 }, { 1, -2 }, { -1, -2 }, { -2, 0 } };
     static const int mod6m1[8] = { 5, 0, 1, 2, 3, 4, 5, 0 };
     static const xmv square1[9] = { { 0, 0 }, { 0, -1 }, { 0, 1 }, { -1, 0 }, { 1, 0 }, { -1, -1 }, { -1, 1 }, { 1, -1 }, { 1, 1 } };
     /* workload[] (motion.cpp:48-58): hpel_iters, hpel_dirs, qpel_iters, qpel_dirs, hpel_satd */
-    static const int wl[3][5] = { { 1, 4, 0, 4, 0 }, { 1, 4, 1, 4, 0 }, { 1, 4, 1, 4, 1 } };
-    XoMeF m = { w, h, (const pix*)fenc, fs, (const pix*)ref, rs, tab_centre, { mvpx, mvpy } };
+    static const int wl[4][5] = { { 1, 4, 0, 4, 0 }, { 1, 4, 1, 4, 0 }, { 1, 4, 1, 4, 1 }, { 2, 4, 1, 4, 1 } };
+    static const xmv offs[16] = { { -1, 0 }, { 0, -1 }, { -1, -1 }, { 1, -1 }, { -1, 0 }, { 1, 0 }, { -1, 1 }, { -1, -1 },
+                                  { 1, -1 }, { 1, 1 }, { -1, 0 }, { 0, 1 }, { -1, 1 }, { 1, 1 }, { 1, 0 }, { 0, 1 } };
+    XoMeF m = { w, h, (const pix*)fenc, fs, (const pix*)ref, rs, tab_centre, { mvpx, mvpy }, 0,
+                { (const pix*)fcb, (const pix*)fcr }, fcs, { (const pix*)rcb, (const pix*)rcr }, rcs };
+    /* bChromaSATD = subpelRefine > 2 && the 4:2:0 chroma satd entry exists (both chroma dims % 4 == 0) */
+    m.chroma = subme > 2 && fcb && ((w >> 1) & 3) == 0 && ((h >> 1) & 3) == 0;
     const xmv qmin = { minx * 4, miny * 4 }, qmax = { maxx * 4, maxy * 4 };
     const xmv mvmin = { minx, miny }, mvmax = { maxx, maxy };
     xmv pmv = xo_clip((xmv){ mvpx, mvpy }, qmin, qmax);
@@ -1352,6 +1489,89 @@ int xo_motion_search(int w, int h, int method, int subme, int merange, const voi
             bcost &= ~15;
         } while (--i && xo_in_range(bmv, mvmin, mvmax));
         bcost >>= 4;
+    }
+    else if (method == 2)
+    {
+        /* STAR (motion.cpp:929-1034) */
+        int bPointNr = 0, bDistance = 0;
+        int done = 0;
+        xo_star(&m, mvmin, mvmax, &bmv, &bcost, &bPointNr, &bDistance, 3, merange);
+        if (bDistance == 1)
+        {
+            if (bPointNr)
+            {
+                const int saved = bcost;
+                const xmv m1 = { bmv.x + offs[(bPointNr - 1) * 2].x, bmv.y + offs[(bPointNr - 1) * 2].y };
+                const xmv m2 = { bmv.x + offs[(bPointNr - 1) * 2 + 1].x, bmv.y + offs[(bPointNr - 1) * 2 + 1].y };
+                if (xo_in_range(m1, mvmin, mvmax))
+                {
+                    const int c = xo_f_fpel_sad(&m, m1.x, m1.y) + xo_f_mvcost(&m, m1.x * 4, m1.y * 4);
+                    if (c < bcost) { bcost = c; bmv = m1; }
+                }
+                if (xo_in_range(m2, mvmin, mvmax))
+                {
+                    const int c = xo_f_fpel_sad(&m, m2.x, m2.y) + xo_f_mvcost(&m, m2.x * 4, m2.y * 4);
+                    if (c < bcost) { bcost = c; bmv = m2; }
+                }
+                if (bcost == saved) done = 1;
+            }
+            else
+                done = 1;
+        }
+        if (!done)
+        {
+            if (bDistance > 5)
+            {
+                /* raster refinement; the 4th sad_x4 lane's MV cost uses tmv << 3 in the reference (motion.cpp:993) */
+                for (int ty = mvmin.y; ty <= mvmax.y; ty += 5)
+                    for (int tx = mvmin.x; tx <= mvmax.x; tx += 5)
+                    {
+                        if (tx + 15 <= mvmax.x)
+                        {
+                            int c;
+                            c = xo_f_fpel_sad(&m, tx, ty) + xo_f_mvcost(&m, tx * 4, ty * 4);
+                            if (c < bcost) { bcost = c; bmv.x = tx; bmv.y = ty; }
+                            tx += 5;
+                            c = xo_f_fpel_sad(&m, tx, ty) + xo_f_mvcost(&m, tx * 4, ty * 4);
+                            if (c < bcost) { bcost = c; bmv.x = tx; bmv.y = ty; }
+                            tx += 5;
+                            c = xo_f_fpel_sad(&m, tx, ty) + xo_f_mvcost(&m, tx * 4, ty * 4);
+                            if (c < bcost) { bcost = c; bmv.x = tx; bmv.y = ty; }
+                            tx += 5;
+                            c = xo_f_fpel_sad(&m, tx, ty) + xo_f_mvcost(&m, tx * 8, ty * 8);
+                            if (c < bcost) { bcost = c; bmv.x = tx; bmv.y = ty; }
+                        }
+                        else
+                        {
+                            const int c = xo_f_fpel_sad(&m, tx, ty) + xo_f_mvcost(&m, tx * 4, ty * 4);
+                            if (c < bcost) { bcost = c; bmv.x = tx; bmv.y = ty; }
+                        }
+                    }
+            }
+            while (bDistance > 0)
+            {
+                bDistance = 0;
+                bPointNr = 0;
+                xo_star(&m, mvmin, mvmax, &bmv, &bcost, &bPointNr, &bDistance, 32, merange);
+                if (bDistance == 1)
+                {
+                    if (!bPointNr) break;
+                    const xmv m1 = { bmv.x + offs[(bPointNr - 1) * 2].x, bmv.y + offs[(bPointNr - 1) * 2].y };
+                    const xmv m2 = { bmv.x + offs[(bPointNr - 1) * 2 + 1].x, bmv.y + offs[(bPointNr - 1) * 2 + 1].y };
+                    if (xo_in_range(m1, mvmin, mvmax))
+                    {
+                        const int c = xo_f_fpel_sad(&m, m1.x, m1.y) + xo_f_mvcost(&m, m1.x * 4, m1.y * 4);
+                        if (c < bcost) { bcost = c; bmv = m1; }
+                    }
+                    if (xo_in_range(m2, mvmin, mvmax))
+                    {
+                        const int c = xo_f_fpel_sad(&m, m2.x, m2.y) + xo_f_mvcost(&m, m2.x * 4, m2.y * 4);
+                        if (c < bcost) { bcost = c; bmv = m2; }
+                    }
+                    break;
+                }
+            }
+        }
     }
     else
     {

@@ -133,13 +133,17 @@ void     xo_lowres_pcost(int wcu, int hcu, int rows_per_slice, int num_slices, c
                          int16_t* mvs, int32_t* mv_costs, uint16_t* lowres_costs, int32_t* row_satd,
                          int64_t* cost_est, int32_t* intra_mbs);
 /* f2: MotionEstimate::motionEstimate (motion.cpp:571-1172) for one w x h PU on a full-resolution
- * reference (luma): method 0 = DIA, 1 = HEX; subme 0..2; fenc / ref at the PU origin; mvmin /
+ * reference: method 0 = DIA, 1 = HEX, 2 = STAR; subme 0..3 (at 3 the 4:2:0 chroma SATD of
+ * subpelCompare is added when fcb != NULL and the chroma PU has a satd entry: fcb / fcr, rcb / rcr =
+ * source / reference Cb, Cr at the PU's chroma origin); fenc / ref at the PU origin; mvmin /
  * mvmax full-pel; mvp and the numc candidates mvc (x, y pairs) quarter-pel; tab_centre = the
  * BitCost table of the CU's QP at difference 0.  Writes the quarter-pel MV to out[0..1] and
  * returns the cost motionEstimate returns. */
 int      xo_motion_search(int w, int h, int method, int subme, int merange, const void* fenc, intptr_t fs,
                           const void* ref, intptr_t rs, int minx, int miny, int maxx, int maxy, int mvpx, int mvpy,
-                          int numc, const int16_t* mvc, const uint16_t* tab_centre, int16_t* out);
+                          int numc, const int16_t* mvc, const uint16_t* tab_centre, int16_t* out,
+                          const void* fcb, const void* fcr, intptr_t fcs, const void* rcb, const void* rcr,
+                          intptr_t rcs);
 /* the reference's BitCost table for any QP (ref_shim only: the restatement takes it as data) */
 void     xo_mvcost_table_qp(int qp, int range, uint16_t* out);
 /* g_scanOrder[type][log2 - 2] (constants.cpp:445-450): scan position -> raster position */

@@ -37,6 +37,14 @@ struct MeArgs
     const int64_t* mvcost_off;
     int16_t* out_mv;
     int32_t* out_cost;
+    const void* fcb;              // chroma (4:2:0) for subme 3; NULL = none
+    const void* fcr;
+    int64_t fcs;
+    const int64_t* fcoff;
+    const void* rcb;
+    const void* rcr;
+    int64_t rcs;
+    const int64_t* rcoff;
     int w, h, n, lg, method, subme, merange, max_cand, depth;
 };
 
@@ -53,6 +61,10 @@ struct MeState
     int nu, lane, G, uw;    // units of this lane, lane in group, group size, units per PU row
     const P* fenc;          // source PU origin (re-read per evaluation: L1-resident, no dynamic register indexing)
     int64_t fs;
+    bool chroma;            // bChromaSATD
+    const P* fc[2];         // source Cb / Cr at the PU's chroma origin
+    const P* rc[2];         // reference Cb / Cr at the PU's chroma origin
+    int64_t fcs, rcs;
 
     __device__ __forceinline__ void unit_xy(int k, int& ux, int& uy) const
     {
@@ -95,6 +107,13 @@ __device__ __forceinline__ void had4m(int& a, int& b, int& c, int& d)
 }
 
 // full-pel SAD of the PU at integer displacement (dx, dy), group-reduced
+// sum over the G lanes of a group (G = 1..64, a power of two, known at run time)
+__device__ __forceinline__ int group_sum_rt(int v, int G)
+{
+    for (int m = G >> 1; m > 0; m >>= 1) v += __shfl_xor(v, m, 64);
+    return v;
+}
+
 template <typename P, int G>
 __device__ __forceinline__ int fpel_sad(const MeState<P>& s, int dx, int dy)
 {
@@ -117,10 +136,119 @@ __device__ __forceinline__ int fpel_sad(const MeState<P>& s, int dx, int dy)
     return group_sum<G>((int)acc);
 }
 
+// the 4:2:0 chroma SATD subpelCompare adds at subme 3 (motion.cpp:1205-1266): the chroma block at
+// the 1/8-pel position (qx, qy) (4-tap pp filters; hps + vsp for 2-D), satd against the source
+// chroma, over this lane's 4x4 chroma units (not group-reduced)
+template <typename P>
+__device__ __forceinline__ int chroma_satd(const MeState<P>& s, int qx, int qy)
+{
+    const int cw = s.a->w >> 1, ch = s.a->h >> 1;
+    const int cuw = cw >> 2, units = cuw * (ch >> 2);
+    const int xf = qx & 7, yf = qy & 7;
+    const int64_t off = (qx >> 3) + (int64_t)(qy >> 3) * s.rcs;
+    const int maxv = (1 << s.a->depth) - 1;
+    const int head = 14 - s.a->depth;
+    int cx[4], cy[4];
+#pragma unroll
+    for (int t = 0; t < 4; t++) { cx[t] = c_chroma.c[xf][t]; cy[t] = c_chroma.c[yf][t]; }
+    int acc = 0;
+    for (int u = s.lane; u < units; u += s.G)
+    {
+        const int ux = 4 * (u % cuw), uy = 4 * (u / cuw);
+#pragma unroll
+        for (int pl = 0; pl < 2; pl++)
+        {
+            const P* p = s.rc[pl] + off + ux + (int64_t)uy * s.rcs;
+            int blk[4][4];
+            if (!(xf | yf))
+            {
+#pragma unroll
+                for (int r = 0; r < 4; r++)
+#pragma unroll
+                    for (int c = 0; c < 4; c++) blk[r][c] = p[r * s.rcs + c];
+            }
+            else if (!yf)
+            {
+#pragma unroll
+                for (int r = 0; r < 4; r++)
+#pragma unroll
+                    for (int c = 0; c < 4; c++)
+                    {
+                        int sum = 0;
+#pragma unroll
+                        for (int t = 0; t < 4; t++) sum += cx[t] * p[r * s.rcs + c + t - 1];
+                        const int val = (int16_t)((sum + 32) >> 6);
+                        blk[r][c] = val < 0 ? 0 : (val > maxv ? maxv : val);
+                    }
+            }
+            else if (!xf)
+            {
+#pragma unroll
+                for (int r = 0; r < 4; r++)
+#pragma unroll
+                    for (int c = 0; c < 4; c++)
+                    {
+                        int sum = 0;
+#pragma unroll
+                        for (int t = 0; t < 4; t++) sum += cy[t] * p[(r + t - 1) * s.rcs + c];
+                        const int val = (int16_t)((sum + 32) >> 6);
+                        blk[r][c] = val < 0 ? 0 : (val > maxv ? maxv : val);
+                    }
+            }
+            else
+            {
+                // filter_hps (isRowExt: rows -1 .. +2 beyond the unit) then filter_vsp
+                const int ps_shift = 6 - head, ps_off = -8192 * (1 << ps_shift);
+                const int sp_shift = 6 + head, sp_off = (1 << (sp_shift - 1)) + (8192 << 6);
+                int m[7][4];
+#pragma unroll
+                for (int i = 0; i < 7; i++)
+#pragma unroll
+                    for (int c = 0; c < 4; c++)
+                    {
+                        int sum = 0;
+#pragma unroll
+                        for (int t = 0; t < 4; t++) sum += cx[t] * p[(i - 1) * s.rcs + c + t - 1];
+                        m[i][c] = (int16_t)((sum + ps_off) >> ps_shift);
+                    }
+#pragma unroll
+                for (int r = 0; r < 4; r++)
+#pragma unroll
+                    for (int c = 0; c < 4; c++)
+                    {
+                        int sum = 0;
+#pragma unroll
+                        for (int t = 0; t < 4; t++) sum += cy[t] * m[r + t][c];
+                        const int val = (int16_t)((sum + sp_off) >> sp_shift);
+                        blk[r][c] = val < 0 ? 0 : (val > maxv ? maxv : val);
+                    }
+            }
+            int d[4][4];
+            const P* f = s.fc[pl] + ux + (int64_t)uy * s.fcs;
+#pragma unroll
+            for (int r = 0; r < 4; r++)
+#pragma unroll
+                for (int c = 0; c < 4; c++) d[r][c] = (int)f[r * s.fcs + c] - blk[r][c];
+#pragma unroll
+            for (int r = 0; r < 4; r++) had4m(d[r][0], d[r][1], d[r][2], d[r][3]);
+            int sum = 0;
+#pragma unroll
+            for (int c = 0; c < 4; c++)
+            {
+                had4m(d[0][c], d[1][c], d[2][c], d[3][c]);
+#pragma unroll
+                for (int r = 0; r < 4; r++) sum += d[r][c] < 0 ? -d[r][c] : d[r][c];
+            }
+            acc += sum >> 1;
+        }
+    }
+    return acc;
+}
+
 // subpelCompare (motion.cpp:1174-1203): the block at quarter-pel (qx, qy), built by
 // luma_hpp / luma_vpp / luma_hvpp when fractional, compared with SAD or SATD
 template <typename P, int G>
-__device__ int subpel_cost(const MeState<P>& s, int qx, int qy, bool satd)
+__device__ __noinline__ int subpel_cost(const MeState<P>& s, int qx, int qy, bool satd)
 {
     const int xf = qx & 3, yf = qy & 3;
     const P* base = s.ref + (qx >> 2) + (int64_t)(qy >> 2) * s.rs;
@@ -250,6 +378,8 @@ __device__ int subpel_cost(const MeState<P>& s, int qx, int qy, bool satd)
                 }
         }
     }
+    if (s.chroma)
+        acc += chroma_satd<P>(s, qx, qy);
     return group_sum<G>(acc);
 }
 
@@ -270,6 +400,14 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_motion_search(const MeArgs a)
     s.tab = a.mvcost + a.mvcost_off[j];
     s.fenc = (const P*)a.fenc + a.fenc_off[j];
     s.fs = a.fs;
+    // bChromaSATD = subpelRefine > 2 && the 4:2:0 chroma satd entry exists (chroma dims % 4 == 0)
+    s.chroma = a.subme > 2 && a.fcb && ((a.w >> 1) & 3) == 0 && ((a.h >> 1) & 3) == 0;
+    if (s.chroma)
+    {
+        s.fc[0] = (const P*)a.fcb + a.fcoff[j]; s.fc[1] = (const P*)a.fcr + a.fcoff[j];
+        s.rc[0] = (const P*)a.rcb + a.rcoff[j]; s.rc[1] = (const P*)a.rcr + a.rcoff[j];
+        s.fcs = a.fcs; s.rcs = a.rcs;
+    }
     const int minx = a.mv_range[4 * j], miny = a.mv_range[4 * j + 1];
     const int maxx = a.mv_range[4 * j + 2], maxy = a.mv_range[4 * j + 3];
     s.mvpx = a.mvp[2 * j];
@@ -321,6 +459,139 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_motion_search(const MeArgs a)
         } while (--i && bx >= minx && bx <= maxx && by >= miny && by <= maxy);
         bcost >>= 4;
     }
+    else if (a.method == 2)
+    {
+        // STAR (motion.cpp:929-1034, StarPatternSearch :328-569)
+        int bpn = 0, bdist = 0;
+        // one candidate point (every point the reference tests is range-checked; the origin is in range,
+        // so the full check equals the reference's per-side checks)
+        auto pt = [&](int mx, int my, int pn, int dd) {
+            if (mx < minx || mx > maxx || my < miny || my > maxy) return;
+            const int c = fpel_sad<P, G>(s, mx, my) + s.mvcost(4 * mx, 4 * my);
+            if (c < bcost) { bcost = c; bx = mx; by = my; bpn = pn; bdist = dd; }
+        };
+        auto star = [&](int early) {
+            const int ox = bx, oy = by;
+            int saved = bcost, rounds = 0;
+            // distance 1: points 2, 4, 5, 7
+#pragma unroll 1
+            for (int k = 0; k < 4; k++)
+            {
+                const int dx = k == 1 ? -1 : k == 2 ? 1 : 0, dy = k == 0 ? -1 : k == 3 ? 1 : 0;
+                pt(ox + dx, oy + dy, (int)((0x7542u >> (4 * k)) & 15), 1);
+            }
+            if (bcost < saved) rounds = 0;
+            else if (++rounds >= early) return;
+            // distances 2, 4, 8: points 2, 1, 3, 4, 5, 6, 8, 7 (1, 3, 6, 8 at half distance)
+            for (int dist = 2; dist <= 8; dist <<= 1)
+            {
+                const int h2 = dist >> 1;
+                saved = bcost;
+#pragma unroll 1
+                for (int k = 0; k < 8; k++)
+                {
+                    const int ux = (int)((0x23140312u >> (4 * k)) & 15) - 2;   // x in half-distance units
+                    const int uy = (int)((0x43322110u >> (4 * k)) & 15) - 2;   // y in half-distance units
+                    const bool half = k == 1 || k == 2 || k == 5 || k == 6;
+                    pt(ox + ux * h2, oy + uy * h2, (int)((0x78654312u >> (4 * k)) & 15), half ? h2 : dist);
+                }
+                if (bcost < saved) rounds = 0;
+                else if (++rounds >= early) return;
+            }
+            // distances 16 .. merange: the four axis points, then three diamonds of four
+            for (int dist = 16; dist <= a.merange; dist <<= 1)
+            {
+                saved = bcost;
+                const int q = dist >> 2;
+#pragma unroll 1
+                for (int k = 0; k < 16; k++)
+                {
+                    int dx, dy;
+                    if (k < 4)
+                    {
+                        dx = k == 1 ? -dist : k == 2 ? dist : 0;
+                        dy = k == 0 ? -dist : k == 3 ? dist : 0;
+                    }
+                    else
+                    {
+                        const int index = (k >> 2), c = k & 3;
+                        dx = (c & 1 ? 1 : -1) * q * index;
+                        dy = c < 2 ? -dist + q * index : dist - q * index;
+                    }
+                    pt(ox + dx, oy + dy, 0, dist);
+                }
+                if (bcost < saved) rounds = 0;
+                else if (++rounds >= early) return;
+            }
+        };
+        // two-point check around a distance-1 best (offsets[], motion.cpp:74-84)
+        auto two_points = [&]() {
+            constexpr uint64_t OX = 0x1220102200202010ull, OY = 0x2122212002110001ull;   // offsets[] + 1, nibbles
+            const int i0 = (bpn - 1) * 2, i1 = i0 + 1;
+            const int m1x = bx + (int)((OX >> (4 * i0)) & 15) - 1, m1y = by + (int)((OY >> (4 * i0)) & 15) - 1;
+            const int m2x = bx + (int)((OX >> (4 * i1)) & 15) - 1, m2y = by + (int)((OY >> (4 * i1)) & 15) - 1;
+            if (m1x >= minx && m1x <= maxx && m1y >= miny && m1y <= maxy)
+            {
+                const int c = fpel_sad<P, G>(s, m1x, m1y) + s.mvcost(4 * m1x, 4 * m1y);
+                if (c < bcost) { bcost = c; bx = m1x; by = m1y; }
+            }
+            if (m2x >= minx && m2x <= maxx && m2y >= miny && m2y <= maxy)
+            {
+                const int c = fpel_sad<P, G>(s, m2x, m2y) + s.mvcost(4 * m2x, 4 * m2y);
+                if (c < bcost) { bcost = c; bx = m2x; by = m2y; }
+            }
+        };
+        star(3);
+        bool done = false;
+        if (bdist == 1)
+        {
+            if (bpn)
+            {
+                const int saved = bcost;
+                two_points();
+                done = bcost == saved;
+            }
+            else
+                done = true;
+        }
+        if (!done)
+        {
+            if (bdist > 5)
+            {
+                // raster refinement; the 4th lane of each sad_x4 costs its MV with tmv << 3 (motion.cpp:993)
+                for (int ty = miny; ty <= maxy; ty += 5)
+                    for (int tx = minx; tx <= maxx; tx += 5)
+                    {
+                        if (tx + 15 <= maxx)
+                        {
+#pragma unroll
+                            for (int q = 0; q < 4; q++)
+                            {
+                                const int c = fpel_sad<P, G>(s, tx, ty) + s.mvcost((q == 3 ? 8 : 4) * tx, (q == 3 ? 8 : 4) * ty);
+                                if (c < bcost) { bcost = c; bx = tx; by = ty; }
+                                if (q < 3) tx += 5;
+                            }
+                        }
+                        else
+                        {
+                            const int c = fpel_sad<P, G>(s, tx, ty) + s.mvcost(4 * tx, 4 * ty);
+                            if (c < bcost) { bcost = c; bx = tx; by = ty; }
+                        }
+                    }
+            }
+            while (bdist > 0)
+            {
+                bdist = 0;
+                bpn = 0;
+                star(32);
+                if (bdist == 1)
+                {
+                    if (bpn) two_points();
+                    break;
+                }
+            }
+        }
+    }
     else
     {
         int c0 = fc(-2, 0), c1 = fc(-1, 2), c2 = fc(1, 2);
@@ -363,14 +634,17 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_motion_search(const MeArgs a)
     int qx, qy;
     if (bprecost < bcost) { qx = bpx; qy = bpy; bcost = bprecost; }
     else { qx = 4 * bx; qy = 4 * by; }
-    // workload[subme] (motion.cpp:48-58): hpel_iters 1, dirs 4; qpel_iters 0/1/1, dirs 4; hpel_satd at 2
+    // workload[subme] (motion.cpp:48-58): hpel_iters 1 (2 at subme 3), dirs 4; qpel_iters 0/1/1/1, dirs 4;
+    // hpel_satd from subme 2
     const bool hsatd = a.subme >= 2;
     const int qiters = a.subme >= 1 ? 1 : 0;
+    const int hiters = a.subme >= 3 ? 2 : 1;
     if (!bcost)
         bcost = s.mvcost(qx, qy);
     else
     {
         if (hsatd) bcost = subpel_cost<P, G>(s, qx, qy, true) + s.mvcost(qx, qy);
+        for (int it = 0; it < hiters; it++)
         {
             int bdir = 0;
             for (int i = 1; i <= 4; i++)
@@ -379,6 +653,7 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_motion_search(const MeArgs a)
                 const int c = subpel_cost<P, G>(s, tx, ty, hsatd) + s.mvcost(tx, ty);
                 if (c < bcost) { bcost = c; bdir = i; }
             }
+            if (!bdir) break;
             qx += 2 * sq_dx(bdir); qy += 2 * sq_dy(bdir);
         }
         if (!hsatd) bcost = subpel_cost<P, G>(s, qx, qy, true) + s.mvcost(qx, qy);
@@ -411,7 +686,7 @@ static int launch_me(const MeArgs& a, hipStream_t st)
 #define L(g) case g: hipLaunchKernelGGL((k_motion_search<P, g>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, a); break;
     switch (G)
     {
-        L(1) L(2) L(4) L(8) L(16) L(32) L(64)
+        L(4) L(8) L(16) L(32) L(64)
     default: return X265AMD_EINVAL;
     }
 #undef L
@@ -429,7 +704,9 @@ extern "C" int x265amd_motion_search(int depth, int count, const x265amd_me_batc
     {
         const x265amd_me_batch& b = bt[i];
         if (b.n < 0 || b.w < 4 || b.h < 4 || b.w > 64 || b.h > 64 || (b.w & 3) || (b.h & 3)) return X265AMD_EINVAL;
-        if (b.method < 0 || b.method > 1 || b.subme < 0 || b.subme > 2 || b.merange < 1) return X265AMD_EINVAL;
+        if (b.method < 0 || b.method > 2 || b.subme < 0 || b.subme > 3 || b.merange < 1) return X265AMD_EINVAL;
+        if (b.n && b.fenc_cb && (!b.fenc_cr || !b.fenc_coff || !b.ref_cb || !b.ref_cr || !b.ref_coff))
+            return X265AMD_EINVAL;
         if (b.n && (!b.fenc || !b.fenc_off || !b.ref || !b.ref_off || !b.mv_range || !b.mvp || !b.mvcost ||
                     !b.mvcost_off || !b.out_mv || !b.out_cost || (b.num_cand && (!b.mvc || b.max_cand < 1))))
             return X265AMD_EINVAL;
@@ -440,12 +717,13 @@ extern "C" int x265amd_motion_search(int depth, int count, const x265amd_me_batc
         const x265amd_me_batch& b = bt[i];
         if (!b.n) continue;
         const int units = (b.w / 4) * (b.h / 4);
-        int g = 1, lg = 0;
+        int g = 4, lg = 2;                               // groups of at least 4 lanes (fewer kernel variants)
         while (g < units && g < 64) { g <<= 1; lg++; }
         if ((units + g - 1) / g > kMeMaxUnits) return X265AMD_EINVAL;
         MeArgs a{ b.fenc, b.fenc_off, (int64_t)b.fenc_stride, b.ref, b.ref_off, (int64_t)b.ref_stride, b.mv_range,
-                  b.mvp, b.mvc, b.num_cand, b.mvcost, b.mvcost_off, b.out_mv, b.out_cost, b.w, b.h, b.n, lg, b.method,
-                  b.subme, b.merange, b.max_cand, depth };
+                  b.mvp, b.mvc, b.num_cand, b.mvcost, b.mvcost_off, b.out_mv, b.out_cost, b.fenc_cb, b.fenc_cr,
+                  (int64_t)b.fenc_cstride, b.fenc_coff, b.ref_cb, b.ref_cr, (int64_t)b.ref_cstride, b.ref_coff,
+                  b.w, b.h, b.n, lg, b.method, b.subme, b.merange, b.max_cand, depth };
         const int rc = depth == 8 ? launch_me<uint8_t>(a, st) : launch_me<uint16_t>(a, st);
         if (rc) return rc;
     }

@@ -67,7 +67,9 @@ class MeBatch(C.Structure):
     _fields_ = [("w", _int), ("h", _int), ("n", _int), ("method", _int), ("subme", _int), ("merange", _int),
                 ("max_cand", _int), ("fenc", _vp), ("fenc_stride", _ip), ("fenc_off", _vp), ("ref", _vp),
                 ("ref_stride", _ip), ("ref_off", _vp), ("mv_range", _vp), ("mvp", _vp), ("mvc", _vp), ("num_cand", _vp),
-                ("mvcost", _vp), ("mvcost_off", _vp), ("out_mv", _vp), ("out_cost", _vp)]
+                ("mvcost", _vp), ("mvcost_off", _vp), ("out_mv", _vp), ("out_cost", _vp), ("fenc_cb", _vp),
+                ("fenc_cr", _vp), ("fenc_cstride", _ip), ("fenc_coff", _vp), ("ref_cb", _vp), ("ref_cr", _vp),
+                ("ref_cstride", _ip), ("ref_coff", _vp)]
 
 
 def _addr(t):
@@ -250,9 +252,11 @@ class Primitives:
 
     # -- f2 full-resolution motion search
     def motion_search(self, depth, w, h, method, subme, merange, max_cand, f, fs, fo, r, rs, ro, rng, mvp, mvc, numc,
-                      tab, tab_off, out_mv, out_cost, stream=None):
+                      tab, tab_off, out_mv, out_cost, fcb=None, fcr=None, fcs=0, fco=None, rcb=None, rcr=None, rcs=0,
+                      rco=None, stream=None):
         arr = (MeBatch * 1)()
         arr[0] = MeBatch(w, h, fo.numel(), method, subme, merange, max_cand, _addr(f), fs, _addr(fo), _addr(r), rs,
                          _addr(ro), _addr(rng), _addr(mvp), _addr(mvc), _addr(numc), _addr(tab), _addr(tab_off),
-                         _addr(out_mv), _addr(out_cost))
+                         _addr(out_mv), _addr(out_cost), _addr(fcb), _addr(fcr), fcs, _addr(fco), _addr(rcb),
+                         _addr(rcr), rcs, _addr(rco))
         self._check(self.lib.x265amd_motion_search(depth, 1, arr, stream or _stream()), "motion_search")

@@ -593,9 +593,12 @@ def case_me(w: int, h: int, method: int, subme: int, merange: int, depth: int, n
     W, H, M = 256, 160, 96
     pdt = pixel_dtype(depth)
     src = SyntheticSource(W, H, 2, depth, seed=seed % 100000)
-    pad = lambda y: np.pad(y.astype(np.int64), M, mode="edge").astype(pdt).reshape(-1)
-    f1, f0 = pad(src.frame(1)[0]), pad(src.frame(0)[0])
+    pad = lambda y, m: np.pad(y.astype(np.int64), m, mode="edge").astype(pdt).reshape(-1)
+    fr1, fr0 = src.frame(1), src.frame(0)
+    f1, f0 = pad(fr1[0], M), pad(fr0[0], M)
     st = W + 2 * M
+    MC = M // 2
+    cst = W // 2 + 2 * MC
     xs, ys = det.ints(0, W - w + 1, n), det.ints(0, H - h + 1, n)
     fo = np.array([(int(y) + M) * st + int(x) + M for x, y in zip(xs, ys)], np.int64)
     rng = np.array([[-int(x) - 24, -int(y) - 24, W - int(x) - w + 24, H - int(y) - h + 24] for x, y in zip(xs, ys)],
@@ -610,7 +613,13 @@ def case_me(w: int, h: int, method: int, subme: int, merange: int, depth: int, n
     qp = np.array([ME_QPS[i] for i in qi], np.uint8)
     bufs = dict(f=f1, fs=st, fo=fo, r=f0, rs=st, ro=fo.copy(), rng=rng, mvp=mvp, mvc=mvc, numc=numc,
                 tab=me_tables(depth), tab_off=tab_off, qp=qp, out_mv=np.full(2 * n, -21846, np.int16),
-                out_cost=np.full(n, -1, np.int32))
+                out_cost=np.full(n, -1, np.int32), fcb=None, fcr=None, fcs=0, fco=None, rcb=None, rcr=None, rcs=0,
+                rco=None)
+    if subme >= 3:
+        # 4:2:0 chroma planes of both pictures, padded by 48 px; PU chroma origin = luma origin / 2
+        fco = np.array([(int(y) // 2 + MC) * cst + int(x) // 2 + MC for x, y in zip(xs, ys)], np.int64)
+        bufs.update(fcb=pad(fr1[1], MC), fcr=pad(fr1[2], MC), fcs=cst, fco=fco, rcb=pad(fr0[1], MC),
+                    rcr=pad(fr0[2], MC), rcs=cst, rco=fco.copy())
     return Case("me", dict(w=w, h=h, method=method, subme=subme, merange=merange, max_cand=max_cand, depth=depth,
                            n=n, seed=seed), bufs, ["out_mv", "out_cost"])
 
@@ -623,6 +632,9 @@ def me_cases(depth: int, n: int = 24):
         for method, subme in ((0, 0), (0, 1), (1, 1), (0, 2)):
             out.append(case_me(w, h, method, subme, 16 if method == 0 else 57, depth, n,
                                seed_of(depth, "me-m", w, h, method, subme)))
+    # --preset slow: STAR search, subme 3 (chroma SATD in the sub-pel compare), every luma PU shape
+    for (w, h) in LUMA_PU[1:]:
+        out.append(case_me(w, h, 2, 3, 57, depth, n // 2, seed_of(depth, "me-star", w, h)))
     return out
 
 
@@ -749,7 +761,8 @@ def run_cpu(case: Case, orc) -> dict:
     elif f == "me":
         orc.motion_search(p["w"], p["h"], p["method"], p["subme"], p["merange"], p["max_cand"], b["f"], b["fs"], b["fo"],
                           b["r"], b["rs"], b["ro"], b["rng"], b["mvp"], b["mvc"], b["numc"], b["tab"], b["tab_off"],
-                          b["qp"], b["out_mv"], b["out_cost"])
+                          b["qp"], b["out_mv"], b["out_cost"], b["fcb"], b["fcr"], b["fcs"], b["fco"], b["rcb"],
+                          b["rcr"], b["rcs"], b["rco"])
     elif f == "tu":
         orc.tu(p["log2"], p["luma"], p["intra"], p["islice"], p["sh"], b["f"], b["fs"], b["fo"], b["p"], b["ps"],
                b["po"], b["r"], b["rs"], b["ro"], b["c"], b["co"], b["rc"], b["rcs"], b["rco"], b["sig"], b["qp"],
@@ -815,7 +828,8 @@ def run_gpu(case: Case, prims, device="cuda") -> dict:
     elif f == "me":
         prims.motion_search(d, p["w"], p["h"], p["method"], p["subme"], p["merange"], p["max_cand"], b["f"], b["fs"],
                             b["fo"], b["r"], b["rs"], b["ro"], b["rng"], b["mvp"], b["mvc"], b["numc"], b["tab"],
-                            b["tab_off"], b["out_mv"], b["out_cost"])
+                            b["tab_off"], b["out_mv"], b["out_cost"], b["fcb"], b["fcr"], b["fcs"], b["fco"], b["rcb"],
+                            b["rcr"], b["rcs"], b["rco"])
     elif f == "tu":
         prims.tu_pipeline(d, p["log2"], p["luma"], p["intra"], p["islice"], p["sh"], b["f"], b["fs"], b["fo"], b["p"],
                           b["ps"], b["po"], b["r"], b["rs"], b["ro"], b["c"], b["co"], b["rc"], b["rcs"], b["rco"],

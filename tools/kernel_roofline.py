@@ -435,8 +435,12 @@ def main():
         n = xs.size
         rng_ = np.random.default_rng(s_)
         fo_h = ((ys + M) * st + xs + M).astype(np.int64)
-        rng_h = np.stack([-xs - 24, -ys - 24, Wf - xs - s_ + 24, Hf - ys - s_ + 24], 1).astype(np.int16).reshape(-1)
-        mvp_h = np.stack([-8 + rng_.integers(-4, 5, n), -4 + rng_.integers(-4, 5, n)], 1).astype(np.int16).reshape(-1)
+        mvp_xy = np.stack([-8 + rng_.integers(-4, 5, n), -4 + rng_.integers(-4, 5, n)], 1)
+        mvp_h = mvp_xy.astype(np.int16).reshape(-1)
+        # Search::setSearchRange: MVP +- merange (57) in full-pel, clipped to the picture + 40 px of padding
+        rng_h = np.stack([np.maximum(-xs - 40, (mvp_xy[:, 0] >> 2) - 57), np.maximum(-ys - 40, (mvp_xy[:, 1] >> 2) - 57),
+                          np.minimum(Wf - xs - s_ + 40, (mvp_xy[:, 0] >> 2) + 57),
+                          np.minimum(Hf - ys - s_ + 40, (mvp_xy[:, 1] >> 2) + 57)], 1).astype(np.int16).reshape(-1)
         mvc_h = rng_.integers(-16, 17, 2 * 2 * n).astype(np.int16)
         numc_h = np.full(n, 2, np.uint8)
         tabs = me_tables(8)
@@ -460,6 +464,35 @@ def main():
                 t0 = _t.perf_counter()
                 ref.motion_search(s_, s_, 1, 2, 57, 2, f1, st, fo_h[:k], f0, st, fo_h[:k], rng_h[:4 * k], mvp_h[:2 * k],
                                   mvc_h[:4 * k], numc_h[:k], tabs, toff_h[:k], np.full(k, 32, np.uint8), om, oc)
+                r["cpu_reference_1core_pu_per_s"] = round(k / (_t.perf_counter() - t0), 1)
+                r["gpu_matches_reference_on_sample"] = bool(np.array_equal(om, OM[:2 * k].cpu().numpy()) and
+                                                            np.array_equal(oc, OC[:k].cpu().numpy()))
+        except Exception as ex:
+            r["cpu_reference_error"] = str(ex)
+        results.append(r)
+        print(json.dumps(r), flush=True)
+        # --preset slow: STAR search, subme 3 with the 4:2:0 chroma SATD
+        MCp = M // 2
+        padc = lambda y: np.pad(y, MCp, mode="edge").reshape(-1)
+        fr1, fr0 = syn.frame(1), syn.frame(0)
+        cst = Wf // 2 + 2 * MCp
+        co_h = ((ys // 2 + MCp) * cst + xs // 2 + MCp).astype(np.int64)
+        FCB, FCR, RCB, RCR, CO = T(padc(fr1[1])), T(padc(fr1[2])), T(padc(fr0[1])), T(padc(fr0[2])), T(co_h)
+        ms_st = timeit(lambda: prims.motion_search(8, s_, s_, 2, 3, 57, 2, F1, st, FO, F0, st, FO, RG, MP, MC2, NC, TB,
+                                                   TO, OM, OC, FCB, FCR, cst, CO, RCB, RCR, cst, CO))
+        r = {"kernel": f"me_star_subme3_{s_}x{s_}", "jobs": n, "ms": round(ms_st, 4),
+             "pu_per_s": round(n / (ms_st * 1e-3), 1), "bound": "latency (serial SAD rounds per PU)"}
+        try:
+            from pyoracle import CpuOracle, available
+            if available("ref", 8):
+                import time as _t
+                ref = CpuOracle("ref", 8)
+                k = min(n, 1000)
+                om, oc = np.empty(2 * k, np.int16), np.empty(k, np.int32)
+                t0 = _t.perf_counter()
+                ref.motion_search(s_, s_, 2, 3, 57, 2, f1, st, fo_h[:k], f0, st, fo_h[:k], rng_h[:4 * k], mvp_h[:2 * k],
+                                  mvc_h[:4 * k], numc_h[:k], tabs, toff_h[:k], np.full(k, 32, np.uint8), om, oc,
+                                  padc(fr1[1]), padc(fr1[2]), cst, co_h[:k], padc(fr0[1]), padc(fr0[2]), cst, co_h[:k])
                 r["cpu_reference_1core_pu_per_s"] = round(k / (_t.perf_counter() - t0), 1)
                 r["gpu_matches_reference_on_sample"] = bool(np.array_equal(om, OM[:2 * k].cpu().numpy()) and
                                                             np.array_equal(oc, OC[:k].cpu().numpy()))
