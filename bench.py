@@ -285,6 +285,13 @@ def main():
             # algorithmic bytes exceed what reaches HBM; this is the HBM rate the PMC bytes imply
             roofline["traffic_over_algorithmic"] = round(traffic / dominant.bytes, 3)
             roofline["hbm_GBps_from_traffic"] = round(traffic / (dom_ms * 1e-3) / 1e9, 1)
+        caller = None
+        if world == 1:
+            try:
+                from src.x265_amd.caller_bench import caller_rates
+                caller = caller_rates(prims, args.width, args.height, args.depth, dev=f"cuda:{local}")
+            except Exception as e:   # informational: never fails the bench line
+                caller = {"error": str(e)}
         cpu = None
         if world == 1 and not args.no_cpu:
             try:
@@ -318,6 +325,7 @@ def main():
             "step_GBps_algorithmic": round(step_bytes * world / (elapsed / args.steps) / 1e9, 1),
             "roofline": roofline,
             "cpu_baseline": cpu,
+            "caller_level_rates": caller,
             "cpu_excluded_calls_per_frame": round(sum(v for v in wb.skipped.values()) / F),
         }
         if args.breakdown:

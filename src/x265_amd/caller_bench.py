@@ -1,0 +1,139 @@
+"""Caller-level rates for bench.py on the bench's own
+resolution and synthetic source: how fast the GPU runs, per frame, the lookahead's lowres
+pipeline (plane init, intra estimate, one P estimate), the main encoder's 2Nx2N motion search
+(HEX, subme 2, merange 57: --preset medium; every PU of 8x8 .. 64x64 against one reference) and
+the fused residual-coding chain for a frame's worth of TUs.  Informational: the census replay
+stays the headline workload.  Product path only (no oracle)."""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import torch
+
+from .synth import SyntheticSource
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def _t(x, dev):
+    return torch.from_numpy(np.ascontiguousarray(x)).to(dev)
+
+
+def _time(fn, reps=5):
+    for _ in range(2):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+def caller_rates(prims, width: int, height: int, depth: int = 8, dev: str = "cuda") -> dict:
+    if depth != 8:
+        return {}
+    out = {}
+    syn = SyntheticSource(width, height, 9, depth)
+    frames = [syn.frame(i) for i in range(9)]
+    # ---- f1: lowres planes + intra estimate for 8 frames, P estimates of frames 1..8 against their predecessor
+    mx, my = 96, 80
+    w2, l2 = width // 2, height // 2
+    ls = w2 + 2 * mx
+    ls += (32 - ls % 32) % 32
+    wcu, hcu = (w2 + 7) // 8, (l2 + 7) // 8
+    lw, ll = wcu * 8, hcu * 8
+    ss = 2 * lw + 32
+    srows = 2 * ll + 4
+    nf = 9
+    src = np.zeros((nf, srows, ss), np.uint8)
+    for i, f in enumerate(frames):
+        y = np.pad(f[0], ((0, srows - height), (0, ss - width)), mode="edge")
+        src[i] = y
+    S = _t(src.reshape(-1), dev)
+    so = _t(np.arange(nf, dtype=np.int64) * srows * ss, dev)
+    psize = ls * (ll + 2 * my)
+    org = my * ls + mx
+    PL = torch.empty(4 * nf * psize, dtype=torch.uint8, device=dev)
+    po = _t(np.arange(4 * nf, dtype=np.int64) * psize + org, dev)
+    ncu = wcu * hcu
+    IC = torch.empty(nf * ncu, dtype=torch.int32, device=dev)
+    IM = torch.empty(nf * ncu, dtype=torch.uint8, device=dev)
+    LC = torch.empty(nf * ncu, dtype=torch.int16, device=dev)
+    RS = torch.empty(nf * hcu, dtype=torch.int32, device=dev)
+    CE = torch.empty(2 * nf, dtype=torch.int64, device=dev)
+    tab = np.load(os.path.join(ROOT, "tests", "golden", "mvcost_lookahead_d8.npy"))
+    TAB = _t(tab, dev)
+    ne = nf - 1
+    rps = max(hcu // 8, 10)
+    ns = max(1, hcu // rps)
+    MV = torch.empty(2 * ne * ncu, dtype=torch.int16, device=dev)
+    MC = torch.empty(ne * ncu, dtype=torch.int32, device=dev)
+    PLC = torch.empty(ne * ncu, dtype=torch.int16, device=dev)
+    PRS = torch.empty(ne * hcu, dtype=torch.int32, device=dev)
+    PCE = torch.empty(2 * ne, dtype=torch.int64, device=dev)
+    MB = torch.empty(ne, dtype=torch.int32, device=dev)
+    p0 = po[0::4].contiguous()
+    fo = po[4::4].contiguous()
+    ro = po[:4 * ne].contiguous()
+
+    def lookahead():
+        prims.lowres_init(8, nf, lw, ll, mx, my, S, ss, so, PL, ls, po)
+        prims.lowres_intra(8, nf, wcu, hcu, PL, ls, p0, None, IC, IM, LC, RS, CE)
+        prims.lowres_pcost(8, ne, wcu, hcu, rps, ns, PL, ls, fo, ro, IC[ncu:], None, TAB.data_ptr() + 2 * (1 << 14),
+                           MV, MC, PLC, PRS, PCE, MB)
+    ms = _time(lookahead)
+    out["lookahead_lowres_frames_per_s"] = round(ne / (ms * 1e-3), 1)
+    out["lookahead_note"] = (f"{nf} frames: lowres planes + intra estimate, {ne} P estimates "
+                             f"({ns} coop slices of {rps} rows)")
+    # ---- f2: every 2Nx2N PU of one frame (8 .. 64) against the previous frame, HEX / subme 2 / merange 57
+    M = 96
+    st = width + 2 * M
+    f1 = np.pad(frames[1][0], M, mode="edge").reshape(-1)
+    f0 = np.pad(frames[0][0], M, mode="edge").reshape(-1)
+    F1, F0 = _t(f1, dev), _t(f0, dev)
+    tq = np.load(os.path.join(ROOT, "tests", "golden", "mvcost_qp_d8.npy"))
+    TQ = _t(tq.reshape(-1), dev)
+    R = (tq.shape[1] - 1) // 2
+    jobs = []
+    rng = np.random.default_rng(5)
+    for s_ in (8, 16, 32, 64):
+        xs, ys = np.meshgrid(np.arange(0, width - s_ + 1, s_), np.arange(0, height - s_ + 1, s_))
+        xs, ys = xs.reshape(-1), ys.reshape(-1)
+        n = xs.size
+        mvp = np.stack([-8 + rng.integers(-4, 5, n), -4 + rng.integers(-4, 5, n)], 1)
+        rg = np.stack([np.maximum(-xs - 40, (mvp[:, 0] >> 2) - 57), np.maximum(-ys - 40, (mvp[:, 1] >> 2) - 57),
+                       np.minimum(width - xs - s_ + 40, (mvp[:, 0] >> 2) + 57),
+                       np.minimum(height - ys - s_ + 40, (mvp[:, 1] >> 2) + 57)], 1)
+        jobs.append(dict(s=s_, n=n, fo=_t(((ys + M) * st + xs + M).astype(np.int64), dev),
+                         rg=_t(rg.astype(np.int16).reshape(-1), dev), mvp=_t(mvp.astype(np.int16).reshape(-1), dev),
+                         mvc=_t(rng.integers(-16, 17, 4 * n).astype(np.int16), dev),
+                         nc=_t(np.full(n, 2, np.uint8), dev),
+                         to=_t(np.full(n, 2 * (2 * R + 1) + R, np.int64), dev),
+                         om=torch.empty(2 * n, dtype=torch.int16, device=dev),
+                         oc=torch.empty(n, dtype=torch.int32, device=dev)))
+
+    def me():
+        for j in jobs:
+            prims.motion_search(8, j["s"], j["s"], 1, 2, 57, 2, F1, st, j["fo"], F0, st, j["fo"], j["rg"], j["mvp"],
+                                j["mvc"], j["nc"], TQ, j["to"], j["om"], j["oc"])
+    ms = _time(me)
+    out["me_2Nx2N_frames_per_s"] = round(1.0 / (ms * 1e-3), 1)
+    out["me_pus_per_frame"] = int(sum(j["n"] for j in jobs))
+    # ---- f3: a frame's worth of 8x8 luma TUs through the fused residual-coding chain
+    xs, ys = np.meshgrid(np.arange(0, width - 7, 8), np.arange(0, height - 7, 8))
+    n = xs.size
+    off = _t(((ys.reshape(-1) + M) * st + xs.reshape(-1) + M).astype(np.int64), dev)
+    RES = torch.empty(f1.size, dtype=torch.int16, device=dev)
+    REC = torch.empty(f1.size, dtype=torch.uint8, device=dev)
+    CO = torch.empty(64 * n, dtype=torch.int16, device=dev)
+    coff = torch.arange(n, dtype=torch.int64, device=dev) * 64
+    SIG = torch.empty(n, dtype=torch.int32, device=dev)
+    QP = torch.full((n,), 32, dtype=torch.uint8, device=dev)
+    ms = _time(lambda: prims.tu_pipeline(8, 3, 1, 0, 0, 1, F1, st, off, F0, st, off, RES, st, off, CO, coff, REC, st,
+                                         off, SIG, QP, None))
+    out["tu_pipeline_8x8_tus_per_s"] = round(n / (ms * 1e-3), 1)
+    return out
