@@ -487,6 +487,105 @@ typedef struct
 } x265amd_me_batch;
 int x265amd_motion_search(int depth, int count, const x265amd_me_batch* batches, void* stream);
 
+/* ------------------------------------------------------------------- f4
+ * In-loop filters and border extension of device-resident 4:2:0 recon frames
+ * (SURVEY.md §8(f) f4), frame-parallel: what FrameFilter::processRow does row by
+ * row (framefilter.cpp:223-520) as whole-frame passes.  One descriptor = one
+ * frame; a call takes `count` frames (any mix of sizes).  Planes are addressed
+ * at the picture origin with element strides and must be readable at least 16
+ * pixels around the picture (x265's PicYuv margins are 64 + 32 / 64 + 16,
+ * picyuv.cpp:62-80).  Widths and heights are multiples of 8 (the minimum CU).
+ * ctu_log2 = log2 of the CTU size (g_maxCUSize) 4..6; CTUs in raster order. */
+
+/* SaoCtuParam (common.h:336-355) after merge resolution: type -1 off, 0..3 EO_0..EO_3,
+ * 4 BO; band = bandPos; offset[0..3] */
+typedef struct
+{
+    int8_t type;
+    uint8_t band;
+    int8_t offset[4];
+} x265amd_sao_param;
+
+/* SAO::processSaoUnitCuLuma / processSaoUnitCuChroma -> processSaoCu (sao.cpp:278-760) for
+ * every CTU of the frame, as FrameFilter drives them after deblocking (framefilter.cpp:
+ * 176-210, 300-430).  The reference works in place, keeping deblocked copies of the
+ * neighbour lines (m_tmpU / m_tmpL); here src (deblocked) and dst (output) are two
+ * buffers (must not overlap) and dst receives every picture pixel.  params[p * nctu + c]
+ * for plane p; Cr is processed with Cb's type (sao.cpp:755; HEVC shares it).  luma_on /
+ * chroma_on = SAOParam::bSaoFlag[0 / 1]. */
+typedef struct
+{
+    int width, height, ctu_log2;
+    int luma_on, chroma_on;
+    const void* src[3];
+    void* dst[3];
+    int64_t stride, cstride;
+    const x265amd_sao_param* params;
+} x265amd_sao_frame;
+int x265amd_sao_apply(int depth, int count, const x265amd_sao_frame* frames, void* stream);
+
+/* SAO::calcSaoStatsCu (sao.cpp:772-943) for every CTU and plane: per CTU, plane, SAO type
+ * (EO_0..EO_3, BO) and class 0..32 the sum of (source - deblocked) and the pixel count
+ * (m_offsetOrg / m_count), into stats / count[((ctu * 3 + plane) * 5 + type) * 33 + class]
+ * (every entry written).  non_deblocked = --sao-non-deblock (bSaoNonDeblocked). */
+typedef struct
+{
+    int width, height, ctu_log2, non_deblocked;
+    const void* fenc[3];
+    int64_t fenc_stride, fenc_cstride;
+    const void* rec[3];
+    int64_t rec_stride, rec_cstride;
+    int32_t* stats;
+    int32_t* count;
+} x265amd_sao_stats_frame;
+int x265amd_sao_stats(int depth, int count, const x265amd_sao_stats_frame* frames, void* stream);
+
+/* The CUData fields deblocking reads, per 4x4 luma unit (raster, unit_stride units per
+ * row): the device-resident CU description (16 bytes per unit). */
+typedef struct
+{
+    uint8_t cu_log2;     /* m_log2CUSize */
+    uint8_t tu_log2;     /* log2 luma TU size = m_log2CUSize - m_tuDepth */
+    uint8_t part;        /* m_partSize (PartSize, cudata.h:39-50) */
+    uint8_t flags;       /* 1 intra (m_predMode), 2 luma cbf of the unit's TU, 4 m_tqBypass */
+    int8_t qp;           /* m_qp */
+    int8_t ref_idx[2];   /* m_refIdx[list], -1 = unused */
+    uint8_t pad;
+    int16_t mv[2][2];    /* m_mv[list] x, y (quarter-pel) */
+} x265amd_deblock_unit;
+
+/* Deblock::deblockCTU (deblock.cpp:37-536) for every CTU of the frame, in place: the edge
+ * marks of deblockCU (CU / TU edges 2, PU splits 1), getBoundaryStrength, the luma strong /
+ * weak filters and the 4:2:0 chroma filter, vertical edges of the frame before horizontal
+ * ones (the order FrameFilter's per-CTU interleave is equivalent to).  ref_poc[list][i] =
+ * identity of the slice's m_refFrameList[list][i] (equal POC = same picture); is_p = P
+ * slice; pps fields deblockingFilter{Beta,Tc}OffsetDiv2, chromaQpOffset[0..1],
+ * bTransquantBypassEnabled. */
+typedef struct
+{
+    int width, height;
+    void* plane[3];
+    int64_t stride, cstride;
+    const x265amd_deblock_unit* units;
+    int64_t unit_stride;
+    int is_p;
+    int beta_offset_div2, tc_offset_div2, cb_qp_offset, cr_qp_offset, tq_bypass_enabled;
+    int32_t ref_poc[2][16];
+} x265amd_deblock_frame;
+int x265amd_deblock(int depth, int count, const x265amd_deblock_frame* frames, void* stream);
+
+/* extendPicBorder (pixel.cpp:908-922): fill margin_x columns left / right of every row with
+ * the edge pixel, then margin_y full-stride rows above / below with the extended first /
+ * last row — the finished-frame result of FrameFilter::processPostCu's row-wise extension
+ * (framefilter.cpp:223-297). */
+typedef struct
+{
+    void* plane;
+    int64_t stride;
+    int width, height, margin_x, margin_y;
+} x265amd_border_plane;
+int x265amd_extend_border(int depth, int count, const x265amd_border_plane* planes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -200,3 +200,65 @@ class CpuPrims:
         n = self._n
         self.orc.tu(log2, luma, intra, islice, sh, n(f), fs, n(fo), n(p), ps, n(po), n(r), rs, n(ro), n(c), n(co),
                     n(rc), rcs, n(rco), n(sig), n(qp), n(scan))
+
+
+# ---------------------------------------------------------------- f4 loop filters (frame level)
+# numpy layouts of xo_sao_param / xo_deblock_unit (x265_oracle.h) == x265amd_sao_param /
+# x265amd_deblock_unit (include/x265_amd.h)
+SAO_PARAM = np.dtype([("type", np.int8), ("band", np.uint8), ("offset", np.int8, 4)])
+DEBLOCK_UNIT = np.dtype([("cu_log2", np.uint8), ("tu_log2", np.uint8), ("part", np.uint8), ("flags", np.uint8),
+                         ("qp", np.int8), ("ref_idx", np.int8, 2), ("pad", np.uint8), ("mv", np.int16, (2, 2))])
+assert SAO_PARAM.itemsize == 6 and DEBLOCK_UNIT.itemsize == 16
+
+
+class DeblockParams(C.Structure):
+    _fields_ = [("is_p", C.c_int), ("beta_offset_div2", C.c_int), ("tc_offset_div2", C.c_int),
+                ("cb_qp_offset", C.c_int), ("cr_qp_offset", C.c_int), ("tq_bypass_enabled", C.c_int),
+                ("ref_poc", (C.c_int32 * 16) * 2)]
+
+
+class FrameFilters:
+    """xo_sao_apply / xo_sao_stats / xo_deblock / xo_extend_border of one oracle library."""
+
+    def __init__(self, kind: str, depth: int):
+        self.depth = depth
+        self.lib = C.CDLL(lib_path(kind, depth))
+        L = self.lib
+        L.xo_sao_apply.argtypes = [C.c_int, C.c_int, C.c_int, _vp, _vp, _vp, _ip, _ip, _vp, C.c_int, C.c_int]
+        L.xo_sao_stats.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, _vp, _vp, _vp, _ip, _ip, _vp, _vp, _vp, _ip,
+                                   _ip, _vp, _vp]
+        L.xo_deblock.argtypes = [C.c_int, C.c_int, C.c_int, _vp, _vp, _vp, _ip, _ip, _vp, _ip, C.POINTER(DeblockParams)]
+        L.xo_extend_border.argtypes = [_vp, _ip, C.c_int, C.c_int, C.c_int, C.c_int]
+
+    @staticmethod
+    def _org(buf, margin, stride):
+        return buf.ctypes.data + (margin * stride + margin) * buf.itemsize
+
+    def sao_apply(self, width, height, ctu_log2, planes, margin, params, luma_on=1, chroma_on=1):
+        """planes: (Y, Cb, Cr) padded 2-D arrays with `margin` pixels on every side; in place."""
+        y, cb, cr = planes
+        self.lib.xo_sao_apply(width, height, ctu_log2, self._org(y, margin, y.shape[1]),
+                              self._org(cb, margin, cb.shape[1]), self._org(cr, margin, cr.shape[1]), y.shape[1],
+                              cb.shape[1], params.ctypes.data, luma_on, chroma_on)
+
+    def sao_stats(self, width, height, ctu_log2, fenc, rec, margin, non_deblocked=0):
+        ctu = 1 << ctu_log2
+        nctu = ((width + ctu - 1) // ctu) * ((height + ctu - 1) // ctu)
+        stats = np.zeros((nctu, 3, 5, 33), np.int32)
+        count = np.zeros((nctu, 3, 5, 33), np.int32)
+        f = [self._org(p, margin, p.shape[1]) for p in fenc]
+        r = [self._org(p, margin, p.shape[1]) for p in rec]
+        self.lib.xo_sao_stats(width, height, ctu_log2, non_deblocked, f[0], f[1], f[2], fenc[0].shape[1],
+                              fenc[1].shape[1], r[0], r[1], r[2], rec[0].shape[1], rec[1].shape[1],
+                              stats.ctypes.data, count.ctypes.data)
+        return stats, count
+
+    def deblock(self, width, height, ctu_log2, planes, margin, units, prm: DeblockParams):
+        y, cb, cr = planes
+        self.lib.xo_deblock(width, height, ctu_log2, self._org(y, margin, y.shape[1]),
+                            self._org(cb, margin, cb.shape[1]), self._org(cr, margin, cr.shape[1]), y.shape[1],
+                            cb.shape[1], units.ctypes.data, units.shape[1], C.byref(prm))
+
+    def extend_border(self, plane, margin_x, margin_y, width, height):
+        self.lib.xo_extend_border(plane.ctypes.data + (margin_y * plane.shape[1] + margin_x) * plane.itemsize,
+                                  plane.shape[1], width, height, margin_x, margin_y)

@@ -23,6 +23,11 @@
 #include "slicetype.h"
 #include "bitcost.h"
 #include "motion.h"
+#include "picyuv.h"
+#include "frame.h"
+#include "framedata.h"
+#include "deblock.h"
+#include "sao.h"
 #include "x265_oracle.h"
 
 #include <pthread.h>
@@ -738,6 +743,316 @@ void xo_set_me_qp(int qp) { g_me_qp = qp; }
 void xo_scan_table(int type, int log2, uint16_t* out)
 {
     memcpy(out, g_scanOrder[type][log2 - 2], sizeof(uint16_t) << (2 * log2));
+}
+
+} // extern "C"
+
+/* ======================================================= f4 loop filters
+ * The reference's own SAO (sao.cpp) and Deblock (deblock.cpp) run on a frame built from the
+ * caller's planes: PicYuv::create / createOffsets for the recon (and source) pictures, one CUData
+ * per CTU, and the process globals x265_set_globals would set for the CTU size (param.cpp:1242-1255). */
+namespace {
+
+void set_ctu_globals(int ctu_log2)
+{
+    g_maxCUSize = 1u << ctu_log2;
+    g_maxLog2CUSize = ctu_log2;
+    g_maxCUDepth = ctu_log2 - 3;
+    g_unitSizeDepth = ctu_log2 - LOG2_UNIT_SIZE;
+    uint32_t* tmp = &g_zscanToRaster[0];
+    initZscanToRaster(g_unitSizeDepth, 1, 0, tmp);
+    initRasterToZscan(g_unitSizeDepth);
+    CUData::s_numPartInCUSize = 1u << g_unitSizeDepth;
+}
+
+struct FrameShell
+{
+    SPS sps;
+    PPS pps;
+    Slice slice;
+    FrameData* fd;
+    Frame* frame;
+    PicYuv* recon;
+    PicYuv* fenc;
+    CUData* ctus;
+    CUDataMemPool pool;
+    int wc, hc;
+
+    FrameShell(int width, int height, bool with_fenc, bool with_cudata)
+    {
+        memset(&sps, 0, sizeof(sps));
+        memset(&pps, 0, sizeof(pps));
+        wc = (width + g_maxCUSize - 1) / g_maxCUSize;
+        hc = (height + g_maxCUSize - 1) / g_maxCUSize;
+        sps.numCuInWidth = wc;
+        sps.numCuInHeight = hc;
+        sps.numPartInCUSize = 1u << g_unitSizeDepth;
+        sps.picWidthInLumaSamples = width;
+        sps.picHeightInLumaSamples = height;
+        slice.m_sps = &sps;
+        slice.m_pps = &pps;
+        recon = new PicYuv;
+        recon->create(width, height, X265_CSP_I420);
+        recon->createOffsets(sps);
+        fenc = NULL;
+        if (with_fenc)
+        {
+            fenc = new PicYuv;
+            fenc->create(width, height, X265_CSP_I420);
+            fenc->createOffsets(sps);
+        }
+        fd = (FrameData*)calloc(1, sizeof(FrameData));
+        fd->m_slice = &slice;
+        fd->m_reconPic = recon;
+        frame = (Frame*)calloc(1, sizeof(Frame));
+        frame->m_encData = fd;
+        frame->m_reconPic = recon;
+        frame->m_fencPic = fenc;
+        ctus = new CUData[wc * hc];
+        if (with_cudata) pool.create(0, X265_CSP_I420, wc * hc);
+        for (int i = 0; i < wc * hc; i++)
+        {
+            CUData& cu = ctus[i];
+            if (with_cudata) cu.initialize(pool, 0, X265_CSP_I420, i);
+            cu.m_encData = fd;
+            cu.m_slice = &slice;
+            cu.m_cuAddr = i;
+            cu.m_cuPelX = (i % wc) << g_maxLog2CUSize;
+            cu.m_cuPelY = (i / wc) << g_maxLog2CUSize;
+            cu.m_absIdxInCTU = 0;
+            cu.m_numPartitions = NUM_4x4_PARTITIONS;
+            cu.m_chromaFormat = X265_CSP_I420;
+            cu.m_hChromaShift = cu.m_vChromaShift = 1;
+            cu.m_cuLeft = (i % wc) ? &ctus[i - 1] : NULL;
+            cu.m_cuAbove = (i / wc) ? &ctus[i - wc] : NULL;
+        }
+        fd->m_picCTU = ctus;
+    }
+    ~FrameShell()
+    {
+        if (pool.charMemBlock) pool.destroy();
+        /* CUData arrays belong to the pool; the CUData objects themselves are plain */
+        delete[] ctus;
+        recon->destroy();
+        delete recon;
+        if (fenc) { fenc->destroy(); delete fenc; }
+        free(fd);
+        free(frame);
+    }
+};
+
+/* caller plane (plus a one-pixel ring) <-> PicYuv plane */
+void load_plane(PicYuv* pic, int plane, const void* src, intptr_t ss, int w, int h)
+{
+    const intptr_t ps = plane ? pic->m_strideC : pic->m_stride;
+    for (int y = -1; y <= h; y++)
+        memcpy(pic->m_picOrg[plane] + y * ps - 1, (const pixel*)src + y * ss - 1, sizeof(pixel) * (w + 2));
+}
+void store_plane(const PicYuv* pic, int plane, void* dst, intptr_t ds, int w, int h)
+{
+    const intptr_t ps = plane ? pic->m_strideC : pic->m_stride;
+    for (int y = 0; y < h; y++)
+        memcpy((pixel*)dst + y * ds, pic->m_picOrg[plane] + y * ps, sizeof(pixel) * w);
+}
+
+struct ShimSao : public SAO
+{
+    void tmpU_from(const PicYuv* snap, int row, int col)
+    {
+        /* FrameFilter::ParallelFilter::copySaoAboveRef (framefilter.cpp:176-199) on the deblocked,
+         * not yet SAO-processed picture */
+        const uint32_t addr = row * m_numCuInWidth + col;
+        for (int p = 0; p < 3; p++)
+        {
+            const int cw = p ? g_maxCUSize >> 1 : g_maxCUSize;
+            const intptr_t st = p ? snap->m_strideC : snap->m_stride;
+            const pixel* r = snap->getPlaneAddr(p, addr) - (row == 0 ? 0 : st);
+            memcpy(&m_tmpU[p][col * cw], r, cw * sizeof(pixel));
+        }
+    }
+    void clear_stats() { memset(m_offsetOrg, 0, sizeof(m_offsetOrg)); memset(m_count, 0, sizeof(m_count)); }
+    const int32_t* org(int p, int t) const { return m_offsetOrg[p][t]; }
+    const int32_t* cnt(int p, int t) const { return m_count[p][t]; }
+};
+
+void sao_param_defaults(x265_param* prm, int width, int height, int non_deblocked)
+{
+    x265_param_default(prm);
+    prm->sourceWidth = width;
+    prm->sourceHeight = height;
+    prm->internalCsp = X265_CSP_I420;
+    prm->maxCUSize = g_maxCUSize;
+    prm->bSaoNonDeblocked = non_deblocked;
+}
+
+} // namespace
+
+extern "C" {
+
+void xo_sao_apply(int width, int height, int ctu_log2, void* y, void* cb, void* cr, intptr_t stride,
+                  intptr_t cstride, const xo_sao_param* params, int luma_on, int chroma_on)
+{
+    pthread_once(&g_prim_once, init_global_prims);
+    set_ctu_globals(ctu_log2);
+    FrameShell fs(width, height, false, false);
+    FrameShell snap(width, height, false, false);
+    void* planes[3] = { y, cb, cr };
+    for (int p = 0; p < 3; p++)
+    {
+        const int w = p ? width >> 1 : width, h = p ? height >> 1 : height;
+        load_plane(fs.recon, p, planes[p], p ? cstride : stride, w, h);
+        load_plane(snap.recon, p, planes[p], p ? cstride : stride, w, h);
+    }
+    x265_param prm;
+    sao_param_defaults(&prm, width, height, 0);
+    ShimSao sao;
+    sao.create(&prm, 1);
+    sao.m_frame = fs.frame;
+    const int nctu = fs.wc * fs.hc;
+    SaoCtuParam* cp[3];
+    for (int p = 0; p < 3; p++)
+    {
+        cp[p] = new SaoCtuParam[nctu];
+        for (int c = 0; c < nctu; c++)
+        {
+            const xo_sao_param& q = params[p * nctu + c];
+            cp[p][c].mergeMode = SAO_MERGE_NONE;
+            cp[p][c].typeIdx = q.type;
+            cp[p][c].bandPos = q.band;
+            for (int i = 0; i < 4; i++) cp[p][c].offset[i] = q.offset[i];
+        }
+    }
+    for (int row = 0; row < fs.hc; row++)
+    {
+        for (int col = 0; col < fs.wc; col++) sao.tmpU_from(snap.recon, row, col);
+        for (int col = 0; col < fs.wc; col++)
+        {
+            if (luma_on) sao.processSaoUnitCuLuma(cp[0], row, col);
+            if (chroma_on) sao.processSaoUnitCuChroma(cp, row, col);
+        }
+    }
+    for (int p = 0; p < 3; p++)
+    {
+        store_plane(fs.recon, p, planes[p], p ? cstride : stride, p ? width >> 1 : width, p ? height >> 1 : height);
+        delete[] cp[p];
+    }
+    sao.destroy(1);
+}
+
+void xo_sao_stats(int width, int height, int ctu_log2, int non_deblocked, const void* fy, const void* fcb,
+                  const void* fcr, intptr_t fstride, intptr_t fcstride, const void* ry, const void* rcb,
+                  const void* rcr, intptr_t rstride, intptr_t rcstride, int32_t* stats, int32_t* count)
+{
+    pthread_once(&g_prim_once, init_global_prims);
+    set_ctu_globals(ctu_log2);
+    FrameShell fs(width, height, true, false);
+    const void* fp[3] = { fy, fcb, fcr };
+    const void* rp[3] = { ry, rcb, rcr };
+    for (int p = 0; p < 3; p++)
+    {
+        const int w = p ? width >> 1 : width, h = p ? height >> 1 : height;
+        load_plane(fs.fenc, p, fp[p], p ? fcstride : fstride, w, h);
+        load_plane(fs.recon, p, rp[p], p ? rcstride : rstride, w, h);
+    }
+    x265_param prm;
+    sao_param_defaults(&prm, width, height, non_deblocked);
+    ShimSao sao;
+    sao.create(&prm, 1);
+    sao.m_frame = fs.frame;
+    const int nctu = fs.wc * fs.hc;
+    for (int c = 0; c < nctu; c++)
+        for (int p = 0; p < 3; p++)
+        {
+            sao.clear_stats();
+            sao.calcSaoStatsCu(c, p);
+            for (int t = 0; t < 5; t++)
+            {
+                memcpy(stats + ((c * 3 + p) * 5 + t) * 33, sao.org(p, t), 33 * sizeof(int32_t));
+                memcpy(count + ((c * 3 + p) * 5 + t) * 33, sao.cnt(p, t), 33 * sizeof(int32_t));
+            }
+        }
+    sao.destroy(1);
+}
+
+void xo_deblock(int width, int height, int ctu_log2, void* y, void* cb, void* cr, intptr_t stride,
+                intptr_t cstride, const xo_deblock_unit* units, intptr_t us, const xo_deblock_params* prm)
+{
+    pthread_once(&g_prim_once, init_global_prims);
+    set_ctu_globals(ctu_log2);
+    FrameShell fs(width, height, false, true);
+    fs.pps.deblockingFilterBetaOffsetDiv2 = prm->beta_offset_div2;
+    fs.pps.deblockingFilterTcOffsetDiv2 = prm->tc_offset_div2;
+    fs.pps.chromaQpOffset[0] = prm->cb_qp_offset;
+    fs.pps.chromaQpOffset[1] = prm->cr_qp_offset;
+    fs.pps.bTransquantBypassEnabled = !!prm->tq_bypass_enabled;
+    fs.slice.m_sliceType = prm->is_p ? P_SLICE : B_SLICE;
+    /* reference identity: one distinct (never dereferenced) Frame address per POC */
+    static char poc_space[1 << 16];
+    for (int l = 0; l < 2; l++)
+        for (int i = 0; i < 16; i++)
+            fs.slice.m_refFrameList[l][i] = (Frame*)(poc_space + ((prm->ref_poc[l][i] & 0x3fff) << 2));
+    void* planes[3] = { y, cb, cr };
+    for (int p = 0; p < 3; p++)
+        load_plane(fs.recon, p, planes[p], p ? cstride : stride, p ? width >> 1 : width, p ? height >> 1 : height);
+
+    /* the CU tree, per 4x4 partition in z-order */
+    const int ctu = g_maxCUSize, npart = NUM_4x4_PARTITIONS;
+    for (int c = 0; c < fs.wc * fs.hc; c++)
+    {
+        CUData& cu = fs.ctus[c];
+        for (int z = 0; z < npart; z++)
+        {
+            const int px = cu.m_cuPelX + g_zscanToPelX[z], py = cu.m_cuPelY + g_zscanToPelY[z];
+            if (px >= width || py >= height)
+            {
+                cu.m_predMode[z] = MODE_NONE;
+                cu.m_cuDepth[z] = g_maxCUDepth;
+                cu.m_log2CUSize[z] = 3;
+                continue;
+            }
+            const xo_deblock_unit& u = units[(py >> 2) * us + (px >> 2)];
+            cu.m_predMode[z] = (u.flags & 1) ? MODE_INTRA : MODE_INTER;
+            cu.m_partSize[z] = u.part;
+            cu.m_cuDepth[z] = ctu_log2 - u.cu_log2;
+            cu.m_log2CUSize[z] = u.cu_log2;
+            cu.m_tuDepth[z] = u.cu_log2 - u.tu_log2;
+            cu.m_cbf[0][z] = (u.flags & 2) ? (uint8_t)(1 << cu.m_tuDepth[z]) : 0;
+            cu.m_qp[z] = u.qp;
+            cu.m_tqBypass[z] = (u.flags & 4) ? 1 : 0;
+            for (int l = 0; l < 2; l++)
+            {
+                cu.m_refIdx[l][z] = u.ref_idx[l];
+                cu.m_mv[l][z] = MV(u.mv[l][0], u.mv[l][1]);
+            }
+        }
+    }
+    CUGeom* geoms = new CUGeom[fs.wc * fs.hc * CUGeom::MAX_GEOMS];
+    for (int c = 0; c < fs.wc * fs.hc; c++)
+    {
+        const int cw = X265_MIN(ctu, width - (c % fs.wc) * ctu), ch = X265_MIN(ctu, height - (c / fs.wc) * ctu);
+        CUData::calcCTUGeoms(cw, ch, ctu, 8, geoms + c * CUGeom::MAX_GEOMS);
+    }
+    /* FrameFilter::ParallelFilter::processTasks order (framefilter.cpp:312-330, 386-392) */
+    for (int row = 0; row < fs.hc; row++)
+    {
+        for (int col = 0; col < fs.wc; col++)
+        {
+            const int a = row * fs.wc + col;
+            Deblock::deblockCTU(&fs.ctus[a], geoms[a * CUGeom::MAX_GEOMS], Deblock::EDGE_VER);
+            if (col >= 1)
+                Deblock::deblockCTU(&fs.ctus[a - 1], geoms[(a - 1) * CUGeom::MAX_GEOMS], Deblock::EDGE_HOR);
+        }
+        const int a = row * fs.wc + fs.wc - 1;
+        Deblock::deblockCTU(&fs.ctus[a], geoms[a * CUGeom::MAX_GEOMS], Deblock::EDGE_HOR);
+    }
+    delete[] geoms;
+    for (int p = 0; p < 3; p++)
+        store_plane(fs.recon, p, planes[p], p ? cstride : stride, p ? width >> 1 : width, p ? height >> 1 : height);
+}
+
+void xo_extend_border(void* plane, intptr_t stride, int width, int height, int mx, int my)
+{
+    extendPicBorder((pixel*)plane, stride, width, height, mx, my);
 }
 
 } // extern "C"

@@ -1655,3 +1655,329 @@ int xo_motion_search(int w, int h, int method, int subme, int merange, const voi
 
 /* BitCost::setQP(qp) table: out[range + d] for |d| <= range.  Restated only for the lookahead QP
  * (xo_mvcost_table); for other QPs the reference's table is the fixture (lambda_tab is data). */
+
+/* ======================================================= f4 loop filters */
+
+void xo_extend_border(void* plane, intptr_t stride, int width, int height, int mx, int my)
+{
+    extend_border((pix*)plane, stride, width, height, mx, my);
+}
+
+static int sgn(int v) { return (v > 0) - (v < 0); }
+
+/* SAO::s_eoTable (sao.cpp:65-72): edge type (sign sum + 2) -> EO class */
+static const int kEoClass[5] = { 1, 2, 0, 3, 4 };
+
+/* the two neighbour offsets of EO class direction t (sao.cpp:321-560): -, |, 135, 45 degrees */
+static void eo_dirs(int t, int* dx0, int* dy0, int* dx1, int* dy1)
+{
+    static const int d[4][4] = { { -1, 0, 1, 0 }, { 0, -1, 0, 1 }, { -1, -1, 1, 1 }, { 1, -1, -1, 1 } };
+    *dx0 = d[t][0]; *dy0 = d[t][1]; *dx1 = d[t][2]; *dy1 = d[t][3];
+}
+
+/* processSaoCu semantics (sao.cpp:278-597): every output pixel is computed from deblocked (pre-SAO)
+ * neighbours (the m_tmpU / m_tmpL copies keep them), EO skips the picture's outermost column / row
+ * in its direction, BO maps bands (bandPos + i) & 31 to offset[i]. */
+void xo_sao_apply(int width, int height, int ctu_log2, void* y_, void* cb_, void* cr_, intptr_t stride,
+                  intptr_t cstride, const xo_sao_param* params, int luma_on, int chroma_on)
+{
+    const int ctu = 1 << ctu_log2;
+    const int wc = (width + ctu - 1) >> ctu_log2, hc = (height + ctu - 1) >> ctu_log2, nctu = wc * hc;
+    pix* planes[3] = { (pix*)y_, (pix*)cb_, (pix*)cr_ };
+    for (int p = 0; p < 3; p++)
+    {
+        if (p == 0 ? !luma_on : !chroma_on) continue;
+        const intptr_t s = p ? cstride : stride;
+        const int pw = p ? width >> 1 : width, ph = p ? height >> 1 : height, cs = p ? ctu >> 1 : ctu;
+        /* the deblocked plane plus a one-pixel ring, as the processing reads it */
+        const int sw = pw + 2, sh = ph + 2;
+        pix* snap = (pix*)malloc(sizeof(pix) * sw * sh);
+        for (int yy = -1; yy <= ph; yy++)
+            for (int xx = -1; xx <= pw; xx++) snap[(yy + 1) * sw + xx + 1] = planes[p][yy * s + xx];
+#define SN(xx, yy) ((int)snap[((yy) + 1) * sw + (xx) + 1])
+        for (int c = 0; c < nctu; c++)
+        {
+            const xo_sao_param* prm = &params[p * nctu + c];
+            int type = prm->type;
+            if (p == 2 && type >= 0) type = params[nctu + c].type;   /* processSaoCu(addr, typeIdxCb, 2) */
+            if (type < 0) continue;
+            const int x0 = (c % wc) * cs, y0 = (c / wc) * cs;
+            const int x1 = x0 + cs < pw ? x0 + cs : pw, y1 = y0 + cs < ph ? y0 + cs : ph;
+            if (type == 4)
+            {
+                int8_t tab[32] = { 0 };
+                for (int i = 0; i < 4; i++) tab[(prm->band + i) & 31] = prm->offset[i];
+                for (int yy = y0; yy < y1; yy++)
+                    for (int xx = x0; xx < x1; xx++)
+                        planes[p][yy * s + xx] = (pix)clipp(SN(xx, yy) + tab[SN(xx, yy) >> (XO_DEPTH - 5)]);
+                continue;
+            }
+            const int off[5] = { 0, prm->offset[0], prm->offset[1], prm->offset[2], prm->offset[3] };
+            int dx0, dy0, dx1, dy1;
+            eo_dirs(type, &dx0, &dy0, &dx1, &dy1);
+            const int xs = (type != 1 && x0 == 0) ? 1 : x0, xe = (type != 1 && x1 == pw) ? pw - 1 : x1;
+            const int ys = (type != 0 && y0 == 0) ? 1 : y0, ye = (type != 0 && y1 == ph) ? ph - 1 : y1;
+            for (int yy = ys; yy < ye; yy++)
+                for (int xx = xs; xx < xe; xx++)
+                {
+                    const int v = SN(xx, yy);
+                    const int e = sgn(v - SN(xx + dx0, yy + dy0)) + sgn(v - SN(xx + dx1, yy + dy1)) + 2;
+                    planes[p][yy * s + xx] = (pix)clipp(v + off[kEoClass[e]]);
+                }
+        }
+#undef SN
+        free(snap);
+    }
+}
+
+/* calcSaoStatsCu (sao.cpp:772-943) with saoCuStats{BO,E0..E3}_c (sao.cpp:1748-1916): per class the
+ * sum of (source - deblocked) and the pixel count, over regions that leave out the not yet
+ * deblocked right / bottom lines (skipR / skipB) unless the CTU touches the picture edge (E0 keeps
+ * its bottom skip even there, sao.cpp:852) */
+void xo_sao_stats(int width, int height, int ctu_log2, int non_deblocked, const void* fy, const void* fcb,
+                  const void* fcr, intptr_t fstride, intptr_t fcstride, const void* ry, const void* rcb,
+                  const void* rcr, intptr_t rstride, intptr_t rcstride, int32_t* stats, int32_t* count)
+{
+    const int ctu = 1 << ctu_log2;
+    const int wc = (width + ctu - 1) >> ctu_log2, hc = (height + ctu - 1) >> ctu_log2, nctu = wc * hc;
+    const pix* fp[3] = { (const pix*)fy, (const pix*)fcb, (const pix*)fcr };
+    const pix* rp[3] = { (const pix*)ry, (const pix*)rcb, (const pix*)rcr };
+    /* (skipB, skipR) per type: E0..E3, BO (sao.cpp:825-925) */
+    static const int kSkip[2][5][2] = { { { 4, 5 }, { 4, 5 }, { 4, 5 }, { 4, 5 }, { 4, 5 } },
+                                        { { 3, 5 }, { 4, 4 }, { 4, 5 }, { 4, 5 }, { 3, 4 } } };
+    memset(stats, 0, sizeof(int32_t) * nctu * 3 * 5 * 33);
+    memset(count, 0, sizeof(int32_t) * nctu * 3 * 5 * 33);
+    for (int c = 0; c < nctu; c++)
+        for (int p = 0; p < 3; p++)
+        {
+            const intptr_t fs = p ? fcstride : fstride, rs = p ? rcstride : rstride;
+            const int pw = p ? width >> 1 : width, ph = p ? height >> 1 : height, cs = p ? ctu >> 1 : ctu;
+            const int po = p ? 2 : 0;
+            const int x0 = (c % wc) * cs, y0 = (c / wc) * cs;
+            const int cw = (x0 + cs < pw ? x0 + cs : pw) - x0, ch = (y0 + cs < ph ? y0 + cs : ph) - y0;
+            const int right = x0 + cw == pw, bottom = y0 + ch == ph;
+            const pix* f = fp[p] + y0 * fs + x0;
+            const pix* r = rp[p] + y0 * rs + x0;
+            int32_t* st = stats + (c * 3 + p) * 5 * 33;
+            int32_t* cn = count + (c * 3 + p) * 5 * 33;
+            for (int t = 0; t < 5; t++)
+            {
+                const int sb = kSkip[!!non_deblocked][t][0], sr = kSkip[!!non_deblocked][t][1];
+                int xs, xe, ys, ye;
+                if (t == 4) { xs = 0; xe = right ? cw : cw - sr + po; ys = 0; ye = bottom ? ch : ch - sb + po; }
+                else if (t == 0) { xs = !x0; xe = right ? cw - 1 : cw - sr + po; ys = 0; ye = ch - sb + po; }
+                else if (t == 1) { xs = 0; xe = right ? cw : cw - sr + po; ys = !y0; ye = bottom ? ch - 1 : ch - sb + po; }
+                else { xs = !x0; xe = right ? cw - 1 : cw - sr + po; ys = !y0; ye = bottom ? ch - 1 : ch - sb + po; }
+                int dx0 = 0, dy0 = 0, dx1 = 0, dy1 = 0;
+                if (t < 4) eo_dirs(t, &dx0, &dy0, &dx1, &dy1);
+                for (int yy = ys; yy < ye; yy++)
+                    for (int xx = xs; xx < xe; xx++)
+                    {
+                        const int v = r[yy * rs + xx];
+                        const int d = (int)f[yy * fs + xx] - v;
+                        int k;
+                        if (t == 4)
+                            k = 1 + (v >> (XO_DEPTH - 5));
+                        else
+                            k = kEoClass[sgn(v - r[(yy + dy0) * rs + xx + dx0]) + sgn(v - r[(yy + dy1) * rs + xx + dx1]) + 2];
+                        st[t * 33 + k] += d;
+                        cn[t * 33 + k]++;
+                    }
+            }
+        }
+}
+
+/* Deblock::s_tcTable / s_betaTable (deblock.cpp:523-535), g_chromaScale (constants.cpp:335-339) */
+static const uint8_t kTc[54] = { 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 1, 1, 1, 1, 1, 2,
+                                 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 5, 5, 6, 6, 7, 8, 9, 10, 11, 13, 14, 16, 18, 20, 22, 24 };
+static const uint8_t kBeta[52] = { 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15,
+                                   16, 17, 18, 20, 22, 24, 26, 28, 30, 32, 34, 36, 38, 40, 42, 44, 46, 48, 50, 52, 54,
+                                   56, 58, 60, 62, 64 };
+static const uint8_t kChromaScale[70] = { 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20,
+                                          21, 22, 23, 24, 25, 26, 27, 28, 29, 29, 30, 31, 32, 33, 33, 34, 34, 35, 35,
+                                          36, 36, 37, 37, 38, 39, 40, 41, 42, 43, 44, 45, 46, 47, 48, 49, 50, 51, 51,
+                                          51, 51, 51, 51, 51, 51, 51, 51, 51, 51, 51 };
+
+static int clip3i(int lo, int hi, int v) { return v < lo ? lo : (v > hi ? hi : v); }
+
+/* the edge marks deblockCU leaves in blockStrength before the bS decision (deblock.cpp:72-191):
+ * the CU's own left / top edge bsCuEdge (2 inside the picture), its TU edges 2, its PU split 1 */
+static int edge_mark(const xo_deblock_unit* u, int dir, int px, int py)
+{
+    const int pos = dir ? py : px;
+    const int cu = 1 << u->cu_log2, tu = 1 << u->tu_log2;
+    const int rel = pos & (cu - 1);
+    if (!rel) return pos > 0 ? 2 : 0;
+    if (!(pos & (tu - 1))) return 2;
+    int pu = -1;
+    switch (u->part)
+    {
+    case 1: if (dir) pu = cu >> 1; break;              /* 2NxN */
+    case 2: if (!dir) pu = cu >> 1; break;             /* Nx2N */
+    case 3: pu = cu >> 1; break;                       /* NxN */
+    case 4: if (dir) pu = cu >> 2; break;              /* 2NxnU */
+    case 5: if (dir) pu = cu - (cu >> 2); break;       /* 2NxnD */
+    case 6: if (!dir) pu = cu >> 2; break;             /* nLx2N */
+    case 7: if (!dir) pu = cu - (cu >> 2); break;      /* nRx2N */
+    }
+    return rel == pu ? 1 : 0;
+}
+
+/* Deblock::getBoundaryStrength (deblock.cpp:193-252).  m_refFrameList[0][-1] is the Slice's m_pps
+ * (a non-null pointer no reference equals, MV kept); m_refFrameList[1][-1] is
+ * m_refFrameList[0][MAX_NUM_REF] = NULL (MV zeroed). */
+#define XO_KEY_L0_NONE ((int64_t)1 << 40)
+#define XO_KEY_NULL ((int64_t)1 << 41)
+static int64_t ref_key(const xo_deblock_params* prm, int list, int idx)
+{
+    return idx < 0 ? (list ? XO_KEY_NULL : XO_KEY_L0_NONE) : (int64_t)prm->ref_poc[list][idx];
+}
+
+static int mvdiff(const int16_t* a, const int16_t* b) { return abs(a[0] - b[0]) >= 4 || abs(a[1] - b[1]) >= 4; }
+
+static int boundary_strength(const xo_deblock_unit* P, const xo_deblock_unit* Q, int mark, const xo_deblock_params* prm)
+{
+    if ((P->flags & 1) || (Q->flags & 1)) return 2;
+    if (mark > 1 && ((Q->flags & 2) || (P->flags & 2))) return 1;
+    static const int16_t zero[2] = { 0, 0 };
+    const int64_t p0 = ref_key(prm, 0, P->ref_idx[0]), q0 = ref_key(prm, 0, Q->ref_idx[0]);
+    const int16_t* mp0 = p0 != XO_KEY_NULL ? P->mv[0] : zero;
+    const int16_t* mq0 = q0 != XO_KEY_NULL ? Q->mv[0] : zero;
+    if (prm->is_p) return (p0 != q0 || mvdiff(mq0, mp0)) ? 1 : 0;
+    const int64_t p1 = ref_key(prm, 1, P->ref_idx[1]), q1 = ref_key(prm, 1, Q->ref_idx[1]);
+    const int16_t* mp1 = p1 != XO_KEY_NULL ? P->mv[1] : zero;
+    const int16_t* mq1 = q1 != XO_KEY_NULL ? Q->mv[1] : zero;
+    if ((p0 == q0 && p1 == q1) || (p0 == q1 && p1 == q0))
+    {
+        if (p0 != p1)
+        {
+            if (p0 == q0) return (mvdiff(mq0, mp0) || mvdiff(mq1, mp1)) ? 1 : 0;
+            return (mvdiff(mq1, mp0) || mvdiff(mq0, mp1)) ? 1 : 0;
+        }
+        return ((mvdiff(mq0, mp0) || mvdiff(mq1, mp1)) && (mvdiff(mq1, mp0) || mvdiff(mq0, mp1))) ? 1 : 0;
+    }
+    return 1;
+}
+
+/* edgeFilterLuma (deblock.cpp:343-441) for one 4-line segment; src at line 0 on the Q side, `off`
+ * across the edge, `step` along it.  pelFilterLumaStrong_c (loopfilter.cpp:141-162), pelFilterLuma
+ * (deblock.cpp:283-326). */
+static void filter_luma_seg(pix* src, intptr_t step, intptr_t off, int bs, int qp, int maskP, int maskQ,
+                            const xo_deblock_params* prm)
+{
+    const int bd = XO_DEPTH - 8;
+    const int beta = kBeta[clip3i(0, 51, qp + prm->beta_offset_div2 * 2)] << bd;
+#define PX(l, k) ((int)src[(l) * step + (k) * off])
+    const int dp0 = abs(PX(0, -3) - 2 * PX(0, -2) + PX(0, -1)), dq0 = abs(PX(0, 0) - 2 * PX(0, 1) + PX(0, 2));
+    const int dp3 = abs(PX(3, -3) - 2 * PX(3, -2) + PX(3, -1)), dq3 = abs(PX(3, 0) - 2 * PX(3, 1) + PX(3, 2));
+    const int d0 = dp0 + dq0, d3 = dp3 + dq3;
+    if (d0 + d3 >= beta) return;
+    const int tc = kTc[clip3i(0, 53, qp + 2 * (bs - 1) + prm->tc_offset_div2 * 2)] << bd;
+    int sw = 2 * d0 < (beta >> 2) && 2 * d3 < (beta >> 2);
+    for (int l = 0; l < 4 && sw; l += 3)
+        sw = abs(PX(l, -4) - PX(l, -1)) + abs(PX(l, 3) - PX(l, 0)) < (beta >> 3) &&
+             abs(PX(l, -1) - PX(l, 0)) < ((tc * 5 + 1) >> 1);
+    if (sw)
+    {
+        const int tcP = (2 * tc) & maskP, tcQ = (2 * tc) & maskQ;
+        for (int l = 0; l < 4; l++)
+        {
+            pix* s = src + l * step;
+            const int m0 = s[-4 * off], m1 = s[-3 * off], m2 = s[-2 * off], m3 = s[-off], m4 = s[0], m5 = s[off],
+                      m6 = s[2 * off], m7 = s[3 * off];
+            s[-3 * off] = (pix)(clip3i(-tcP, tcP, ((2 * m0 + 3 * m1 + m2 + m3 + m4 + 4) >> 3) - m1) + m1);
+            s[-2 * off] = (pix)(clip3i(-tcP, tcP, ((m1 + m2 + m3 + m4 + 2) >> 2) - m2) + m2);
+            s[-off] = (pix)(clip3i(-tcP, tcP, ((m1 + 2 * m2 + 2 * m3 + 2 * m4 + m5 + 4) >> 3) - m3) + m3);
+            s[0] = (pix)(clip3i(-tcQ, tcQ, ((m2 + 2 * m3 + 2 * m4 + 2 * m5 + m6 + 4) >> 3) - m4) + m4);
+            s[off] = (pix)(clip3i(-tcQ, tcQ, ((m3 + m4 + m5 + m6 + 2) >> 2) - m5) + m5);
+            s[2 * off] = (pix)(clip3i(-tcQ, tcQ, ((m3 + m4 + m5 + 3 * m6 + 2 * m7 + 4) >> 3) - m6) + m6);
+        }
+        return;
+    }
+    const int side = (beta + (beta >> 1)) >> 3;
+    const int mP1 = (dp0 + dp3 < side ? -1 : 0) & maskP, mQ1 = (dq0 + dq3 < side ? -1 : 0) & maskQ;
+    const int thr = tc * 10, tc2 = tc >> 1;
+    for (int l = 0; l < 4; l++)
+    {
+        pix* s = src + l * step;
+        const int m2 = s[-2 * off], m3 = s[-off], m4 = s[0], m5 = s[off];
+        int delta = (9 * (m4 - m3) - 3 * (m5 - m2) + 8) >> 4;
+        if (abs(delta) >= thr) continue;
+        delta = clip3i(-tc, tc, delta);
+        s[-off] = (pix)clipp(m3 + (delta & maskP));
+        s[0] = (pix)clipp(m4 - (delta & maskQ));
+        if (mP1)
+        {
+            const int m1 = s[-3 * off];
+            s[-2 * off] = (pix)clipp(m2 + clip3i(-tc2, tc2, (((m1 + m3 + 1) >> 1) - m2 + delta) >> 1));
+        }
+        if (mQ1)
+        {
+            const int m6 = s[2 * off];
+            s[off] = (pix)clipp(m5 + clip3i(-tc2, tc2, (((m6 + m4 + 1) >> 1) - m5 - delta) >> 1));
+        }
+    }
+#undef PX
+}
+
+/* edgeFilterChroma (deblock.cpp:443-521) for one 4-line chroma segment of Cb and Cr (bS 2 only) */
+static void filter_chroma_seg(pix* const cbcr[2], intptr_t step, intptr_t off, int qpA, int maskP, int maskQ,
+                              const xo_deblock_params* prm)
+{
+    const int bd = XO_DEPTH - 8;
+    for (int k = 0; k < 2; k++)
+    {
+        int qp = qpA + (k ? prm->cr_qp_offset : prm->cb_qp_offset);
+        if (qp >= 30) qp = kChromaScale[qp];
+        const int tc = kTc[clip3i(0, 53, qp + 2 + prm->tc_offset_div2 * 2)] << bd;
+        for (int l = 0; l < 4; l++)
+        {
+            pix* s = cbcr[k] + l * step;
+            const int m2 = s[-2 * off], m3 = s[-off], m4 = s[0], m5 = s[off];
+            const int delta = clip3i(-tc, tc, (((m4 - m3) * 4) + m2 - m5 + 4) >> 3);
+            s[-off] = (pix)clipp(m3 + (delta & maskP));
+            s[0] = (pix)clipp(m4 - (delta & maskQ));
+        }
+    }
+}
+
+void xo_deblock(int width, int height, int ctu_log2, void* y_, void* cb_, void* cr_, intptr_t stride,
+                intptr_t cstride, const xo_deblock_unit* units, intptr_t us, const xo_deblock_params* prm)
+{
+    (void)ctu_log2;   /* the per-CTU order of the reference is equivalent to all-vertical-then-all-horizontal */
+    pix* Y = (pix*)y_;
+    pix* C[2] = { (pix*)cb_, (pix*)cr_ };
+    const int wu = width >> 2, hu = height >> 2;
+    for (int dir = 0; dir < 2; dir++)
+    {
+        /* luma: every 4-line segment of an edge on the 8x8 grid */
+        for (int uy = 0; uy < hu; uy++)
+            for (int ux = 0; ux < wu; ux++)
+            {
+                if (dir ? (uy & 1) : (ux & 1)) continue;
+                const xo_deblock_unit* Q = &units[uy * us + ux];
+                const int mark = edge_mark(Q, dir, 4 * ux, 4 * uy);
+                if (!mark) continue;
+                const xo_deblock_unit* P = dir ? Q - us : Q - 1;
+                const int bs = boundary_strength(P, Q, mark, prm);
+                int maskP = -1, maskQ = -1;
+                if (prm->tq_bypass_enabled)
+                {
+                    maskP = (P->flags & 4) ? 0 : -1;
+                    maskQ = (Q->flags & 4) ? 0 : -1;
+                    if (!(maskP | maskQ)) continue;
+                }
+                const int qp = (P->qp + Q->qp + 1) >> 1;
+                if (bs)
+                    filter_luma_seg(Y + 4 * uy * stride + 4 * ux, dir ? 1 : stride, dir ? stride : 1, bs, qp, maskP,
+                                    maskQ, prm);
+                /* chroma: edges on the 8x8 chroma grid, 4 chroma lines per second luma unit */
+                if (bs == 2 && !((dir ? uy : ux) & 3) && !((dir ? ux : uy) & 1))
+                {
+                    const intptr_t o = (intptr_t)(2 * uy) * cstride + 2 * ux;
+                    pix* const cbcr[2] = { C[0] + o, C[1] + o };
+                    filter_chroma_seg(cbcr, dir ? 1 : cstride, dir ? cstride : 1, qp, maskP, maskQ, prm);
+                }
+            }
+    }
+}

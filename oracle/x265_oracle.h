@@ -149,6 +149,55 @@ void     xo_mvcost_table_qp(int qp, int range, uint16_t* out);
 /* g_scanOrder[type][log2 - 2] (constants.cpp:445-450): scan position -> raster position */
 void     xo_scan_table(int type, int log2, uint16_t* out);
 
+/* ------------------------------------------------------------ f4 loop filters (4:2:0)
+ * Planes: y (width x height), cb / cr (width/2 x height/2); every plane readable one pixel
+ * outside the picture on each side (the recon PicYuv margins, picyuv.cpp:62-80).
+ * ctu_log2 = log2 of the CTU size (g_maxCUSize), 4..6; CTUs in raster order. */
+typedef struct
+{
+    int8_t  type;        /* SaoCtuParam.typeIdx after merge resolution: -1 off, 0..3 EO_0..EO_3, 4 BO */
+    uint8_t band;        /* bandPos (BO) */
+    int8_t  offset[4];   /* offset[0..3] */
+} xo_sao_param;
+
+/* per 4x4 luma unit (raster, unit_stride units per row): the CUData fields deblocking reads */
+typedef struct
+{
+    uint8_t cu_log2;     /* log2 CU size (m_log2CUSize) */
+    uint8_t tu_log2;     /* log2 luma TU size (m_log2CUSize - m_tuDepth) */
+    uint8_t part;        /* PartSize (cudata.h:39-50) */
+    uint8_t flags;       /* 1 intra, 2 luma cbf of the unit's TU, 4 transquant bypass */
+    int8_t  qp;          /* m_qp */
+    int8_t  ref_idx[2];  /* m_refIdx[list] (-1 = not used) */
+    uint8_t pad;
+    int16_t mv[2][2];    /* m_mv[list] (x, y), quarter-pel */
+} xo_deblock_unit;
+
+typedef struct
+{
+    int is_p;                   /* P slice: list 0 only (slice.h isInterP); else B */
+    int beta_offset_div2, tc_offset_div2, cb_qp_offset, cr_qp_offset, tq_bypass_enabled;
+    int32_t ref_poc[2][16];     /* identity of m_refFrameList[list][refIdx] */
+} xo_deblock_params;
+
+/* SAO::processSaoUnitCuLuma / processSaoUnitCuChroma -> processSaoCu (sao.cpp:278-760) for every
+ * CTU, as FrameFilter drives them on a deblocked frame (framefilter.cpp:176-210, 300-430).  In
+ * place.  params[plane * nctu + ctu]; Cr takes Cb's type (processSaoUnitCuChroma, sao.cpp:755). */
+void     xo_sao_apply(int width, int height, int ctu_log2, void* y, void* cb, void* cr, intptr_t stride,
+                      intptr_t cstride, const xo_sao_param* params, int luma_on, int chroma_on);
+/* SAO::calcSaoStatsCu (sao.cpp:772-943) for every CTU and plane: stats / count
+ * [ctu][plane][type 0..4][class 0..32] (m_offsetOrg / m_count of the CTU). */
+void     xo_sao_stats(int width, int height, int ctu_log2, int non_deblocked, const void* fy, const void* fcb,
+                      const void* fcr, intptr_t fstride, intptr_t fcstride, const void* ry, const void* rcb,
+                      const void* rcr, intptr_t rstride, intptr_t rcstride, int32_t* stats, int32_t* count);
+/* Deblock::deblockCTU (deblock.cpp:37-536) over the frame, vertical edges of every CTU before
+ * the horizontal ones (framefilter.cpp:312-330 order), CU tree given as 4x4 units.  In place. */
+void     xo_deblock(int width, int height, int ctu_log2, void* y, void* cb, void* cr, intptr_t stride,
+                    intptr_t cstride, const xo_deblock_unit* units, intptr_t unit_stride,
+                    const xo_deblock_params* prm);
+/* extendPicBorder (pixel.cpp:908-922) of one plane: width x height, margins mx, my */
+void     xo_extend_border(void* plane, intptr_t stride, int width, int height, int mx, int my);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,892 @@
+// loopfilter.hip — f4: the in-loop filters and border extension of
+// device-resident 4:2:0 recon frames, as whole-frame passes instead of FrameFilter's CTU-row
+// pipeline (framefilter.cpp:223-520):
+//
+//   x265amd_deblock        Deblock::deblockCTU (deblock.cpp:37-536): edge marks, boundary
+//                          strength, luma strong / weak and chroma filters.  Two launches per
+//                          call: every vertical edge of every frame, then every horizontal one
+//                          (HEVC's order; x265's per-CTU V(c) / H(c-1) interleave is equivalent
+//                          because a filter reads 4 and writes 3 pixels each side of an edge
+//                          and edges are 8 apart).  One lane per 4-line edge segment: it
+//                          derives the edge mark and bS from the two 16-byte CU units on either
+//                          side, loads its 4 x 8 pixel window, filters in registers and stores
+//                          the window back (windows tile the plane, so lanes never overlap).
+//   x265amd_sao_apply      SAO::processSaoCu (sao.cpp:278-597): one lane per 8-pixel row segment
+//                          of a plane; neighbours come from the deblocked source buffer and the
+//                          result goes to a second buffer, which is what the reference's
+//                          m_tmpU / m_tmpL copies emulate in place.
+//   x265amd_sao_stats      SAO::calcSaoStatsCu (sao.cpp:772-943): one workgroup per CTU, all
+//                          three planes; per pixel the five SAO types' classes; edge-offset
+//                          classes accumulate in registers and reduce across the wavefront,
+//                          band classes go to LDS as packed (count << 40) + sum 64-bit adds.
+//   x265amd_extend_border  extendPicBorder (pixel.cpp:908-922): side margins, then full-stride
+//                          margin rows (second launch, so corners copy extended rows).
+//
+// All four are HBM-bound byte work: no MFMA, vector loads of whole row windows, the neighbour
+// rows of a segment come from L2.
+#include "common.h"
+#include "../../../include/x265_amd.h"
+
+#include <cstring>
+
+namespace x265amd {
+
+// Deblock::s_tcTable / s_betaTable (deblock.cpp:523-535), g_chromaScale (constants.cpp:335-339)
+__constant__ uint8_t c_tc[54] = { 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 1, 1, 1, 1, 1,
+                                  2, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 5, 5, 6, 6, 7, 8, 9, 10, 11, 13, 14, 16, 18, 20,
+                                  22, 24 };
+__constant__ uint8_t c_beta[52] = { 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 6, 7, 8, 9, 10, 11, 12, 13, 14,
+                                    15, 16, 17, 18, 20, 22, 24, 26, 28, 30, 32, 34, 36, 38, 40, 42, 44, 46, 48, 50,
+                                    52, 54, 56, 58, 60, 62, 64 };
+__constant__ uint8_t c_chroma_scale[70] = { 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19,
+                                            20, 21, 22, 23, 24, 25, 26, 27, 28, 29, 29, 30, 31, 32, 33, 33, 34, 34,
+                                            35, 35, 36, 36, 37, 37, 38, 39, 40, 41, 42, 43, 44, 45, 46, 47, 48, 49,
+                                            50, 51, 51, 51, 51, 51, 51, 51, 51, 51, 51, 51, 51, 51 };
+
+constexpr int kMaxFrames = 8;   // frame descriptors per launch (they travel in the kernarg segment)
+
+__device__ __forceinline__ int clip3(int lo, int hi, int v) { return v < lo ? lo : (v > hi ? hi : v); }
+__device__ __forceinline__ int sgn(int v) { return (v > 0) - (v < 0); }
+__device__ __forceinline__ int iabs(int v) { return v < 0 ? -v : v; }
+
+// which frame of the launch a logical block belongs to (uniform scan, as group_sub)
+template <typename L>
+__device__ __forceinline__ int frame_of(const L& l, uint32_t b)
+{
+    int f = 0;
+#pragma unroll
+    for (int i = 1; i < kMaxFrames; i++)
+        if (i < l.count && l.f[i].block0 <= b) f = i;
+    return f;
+}
+
+// ================================================================ deblocking
+struct DbkFrame
+{
+    void* plane[3];
+    int64_t stride, cstride;
+    const x265amd_deblock_unit* units;
+    int64_t us;
+    int wu, hu;                       // picture size in 4x4 units
+    int is_p, beta2, tc2, cbqp, crqp, tqb;
+    int32_t poc[2][16];
+    uint32_t block0, nluma, nseg;     // first block; luma / all segments of this pass
+};
+struct DbkLaunch
+{
+    DbkFrame f[kMaxFrames];
+    int count, maxv;
+};
+
+struct Unit
+{
+    int cu_log2, tu_log2, part, flags, qp, ref0, ref1, mv0x, mv0y, mv1x, mv1y;
+    __device__ __forceinline__ Unit(const x265amd_deblock_unit* p)
+    {
+        const uint4 v = *(const uint4*)p;
+        cu_log2 = v.x & 0xff; tu_log2 = (v.x >> 8) & 0xff; part = (v.x >> 16) & 0xff; flags = v.x >> 24;
+        qp = (int8_t)(v.y & 0xff); ref0 = (int8_t)((v.y >> 8) & 0xff); ref1 = (int8_t)((v.y >> 16) & 0xff);
+        mv0x = (int16_t)(v.z & 0xffff); mv0y = (int16_t)(v.z >> 16);
+        mv1x = (int16_t)(v.w & 0xffff); mv1y = (int16_t)(v.w >> 16);
+    }
+};
+
+// deblockCU's marks (deblock.cpp:72-191): CU edge bsCuEdge (2 inside the picture), TU edge 2,
+// PU split 1 (setEdgefilterPU), in that priority
+__device__ __forceinline__ int edge_mark(const Unit& u, int dir, int pos)
+{
+    const int cu = 1 << u.cu_log2;
+    const int rel = pos & (cu - 1);
+    if (!rel) return pos > 0 ? 2 : 0;
+    if (!(pos & ((1 << u.tu_log2) - 1))) return 2;
+    int pu = -1;
+    switch (u.part)
+    {
+    case 1: pu = dir ? cu >> 1 : -1; break;
+    case 2: pu = dir ? -1 : cu >> 1; break;
+    case 3: pu = cu >> 1; break;
+    case 4: pu = dir ? cu >> 2 : -1; break;
+    case 5: pu = dir ? cu - (cu >> 2) : -1; break;
+    case 6: pu = dir ? -1 : cu >> 2; break;
+    case 7: pu = dir ? -1 : cu - (cu >> 2); break;
+    default: break;
+    }
+    return rel == pu ? 1 : 0;
+}
+
+// m_refFrameList[list][refIdx] identity: refIdx -1 reads m_refFrameList[0][-1] = the Slice's m_pps
+// (non-null, equal to no picture, MV kept) or m_refFrameList[1][-1] = m_refFrameList[0][MAX_NUM_REF]
+// = NULL (MV zeroed) — slice.h:320-338
+constexpr int64_t kKeyL0None = (int64_t)1 << 40;
+constexpr int64_t kKeyNull = (int64_t)1 << 41;
+
+__device__ __forceinline__ bool mvd(int ax, int ay, int bx, int by) { return iabs(ax - bx) >= 4 || iabs(ay - by) >= 4; }
+
+// Deblock::getBoundaryStrength (deblock.cpp:193-252)
+__device__ __forceinline__ int boundary_strength(const DbkFrame& f, const Unit& P, const Unit& Q, int mark)
+{
+    if ((P.flags | Q.flags) & 1) return 2;
+    if (mark > 1 && ((P.flags | Q.flags) & 2)) return 1;
+    const int64_t p0 = P.ref0 < 0 ? kKeyL0None : (int64_t)f.poc[0][P.ref0 & 15];
+    const int64_t q0 = Q.ref0 < 0 ? kKeyL0None : (int64_t)f.poc[0][Q.ref0 & 15];
+    const int mp0x = P.mv0x, mp0y = P.mv0y, mq0x = Q.mv0x, mq0y = Q.mv0y;
+    if (f.is_p) return (p0 != q0 || mvd(mq0x, mq0y, mp0x, mp0y)) ? 1 : 0;
+    const int64_t p1 = P.ref1 < 0 ? kKeyNull : (int64_t)f.poc[1][P.ref1 & 15];
+    const int64_t q1 = Q.ref1 < 0 ? kKeyNull : (int64_t)f.poc[1][Q.ref1 & 15];
+    const int mp1x = p1 != kKeyNull ? P.mv1x : 0, mp1y = p1 != kKeyNull ? P.mv1y : 0;
+    const int mq1x = q1 != kKeyNull ? Q.mv1x : 0, mq1y = q1 != kKeyNull ? Q.mv1y : 0;
+    if ((p0 == q0 && p1 == q1) || (p0 == q1 && p1 == q0))
+    {
+        const bool same = mvd(mq0x, mq0y, mp0x, mp0y) || mvd(mq1x, mq1y, mp1x, mp1y);
+        const bool cross = mvd(mq1x, mq1y, mp0x, mp0y) || mvd(mq0x, mq0y, mp1x, mp1y);
+        if (p0 != p1) return (p0 == q0 ? same : cross) ? 1 : 0;
+        return (same && cross) ? 1 : 0;
+    }
+    return 1;
+}
+
+// the 4 lines x 8 pixels across one luma edge (v[l][i] = pixel i - 4 across the edge on line l)
+template <typename P, int DIR>
+__device__ __forceinline__ void load_window(const P* q, int64_t s, int (&v)[4][8])
+{
+    if constexpr (DIR == 0)
+    {
+#pragma unroll
+        for (int l = 0; l < 4; l++) load_row<P, 8>(q + l * s - 4, v[l]);
+    }
+    else
+    {
+#pragma unroll
+        for (int i = 0; i < 8; i++)
+        {
+            int r[4];
+            load_row<P, 4>(q + (i - 4) * s, r);
+#pragma unroll
+            for (int l = 0; l < 4; l++) v[l][i] = r[l];
+        }
+    }
+}
+
+template <typename P, int DIR>
+__device__ __forceinline__ void store_window(P* q, int64_t s, const int (&v)[4][8])
+{
+    if constexpr (DIR == 0)
+    {
+#pragma unroll
+        for (int l = 0; l < 4; l++) store_row<P, 8>(q + l * s - 4, v[l]);
+    }
+    else
+    {
+#pragma unroll
+        for (int i = 1; i < 7; i++)
+        {
+            const int r[4] = { v[0][i], v[1][i], v[2][i], v[3][i] };
+            store_row<P, 4>(q + (i - 4) * s, r);
+        }
+    }
+}
+
+// Deblock::edgeFilterLuma's per-segment body (deblock.cpp:388-440) with pelFilterLumaStrong_c
+// (loopfilter.cpp:141-162) and pelFilterLuma (deblock.cpp:283-326); returns false if untouched
+__device__ __forceinline__ bool filter_luma(int (&v)[4][8], int bs, int qp, int maskP, int maskQ, int beta2,
+                                            int tc2, int bd, int maxv)
+{
+    const int beta = (int)c_beta[clip3(0, 51, qp + beta2)] << bd;
+    const int dp0 = iabs(v[0][1] - 2 * v[0][2] + v[0][3]), dq0 = iabs(v[0][4] - 2 * v[0][5] + v[0][6]);
+    const int dp3 = iabs(v[3][1] - 2 * v[3][2] + v[3][3]), dq3 = iabs(v[3][4] - 2 * v[3][5] + v[3][6]);
+    const int d0 = dp0 + dq0, d3 = dp3 + dq3;
+    if (d0 + d3 >= beta) return false;
+    const int tc = (int)c_tc[clip3(0, 53, qp + 2 * (bs - 1) + tc2)] << bd;
+    const bool sw = 2 * d0 < (beta >> 2) && 2 * d3 < (beta >> 2) &&
+                    iabs(v[0][0] - v[0][3]) + iabs(v[0][7] - v[0][4]) < (beta >> 3) &&
+                    iabs(v[0][3] - v[0][4]) < ((tc * 5 + 1) >> 1) &&
+                    iabs(v[3][0] - v[3][3]) + iabs(v[3][7] - v[3][4]) < (beta >> 3) &&
+                    iabs(v[3][3] - v[3][4]) < ((tc * 5 + 1) >> 1);
+    if (sw)
+    {
+        const int tcP = (2 * tc) & maskP, tcQ = (2 * tc) & maskQ;
+#pragma unroll
+        for (int l = 0; l < 4; l++)
+        {
+            const int m0 = v[l][0], m1 = v[l][1], m2 = v[l][2], m3 = v[l][3], m4 = v[l][4], m5 = v[l][5],
+                      m6 = v[l][6], m7 = v[l][7];
+            v[l][1] = clip3(-tcP, tcP, ((2 * m0 + 3 * m1 + m2 + m3 + m4 + 4) >> 3) - m1) + m1;
+            v[l][2] = clip3(-tcP, tcP, ((m1 + m2 + m3 + m4 + 2) >> 2) - m2) + m2;
+            v[l][3] = clip3(-tcP, tcP, ((m1 + 2 * m2 + 2 * m3 + 2 * m4 + m5 + 4) >> 3) - m3) + m3;
+            v[l][4] = clip3(-tcQ, tcQ, ((m2 + 2 * m3 + 2 * m4 + 2 * m5 + m6 + 4) >> 3) - m4) + m4;
+            v[l][5] = clip3(-tcQ, tcQ, ((m3 + m4 + m5 + m6 + 2) >> 2) - m5) + m5;
+            v[l][6] = clip3(-tcQ, tcQ, ((m3 + m4 + m5 + 3 * m6 + 2 * m7 + 4) >> 3) - m6) + m6;
+        }
+        return true;
+    }
+    const int side = (beta + (beta >> 1)) >> 3;
+    const int mP1 = (dp0 + dp3 < side ? -1 : 0) & maskP, mQ1 = (dq0 + dq3 < side ? -1 : 0) & maskQ;
+    const int thr = tc * 10, tch = tc >> 1;
+#pragma unroll
+    for (int l = 0; l < 4; l++)
+    {
+        const int m1 = v[l][1], m2 = v[l][2], m3 = v[l][3], m4 = v[l][4], m5 = v[l][5], m6 = v[l][6];
+        int delta = (9 * (m4 - m3) - 3 * (m5 - m2) + 8) >> 4;
+        if (iabs(delta) >= thr) continue;
+        delta = clip3(-tc, tc, delta);
+        v[l][3] = clip3(0, maxv, m3 + (delta & maskP));
+        v[l][4] = clip3(0, maxv, m4 - (delta & maskQ));
+        if (mP1) v[l][2] = clip3(0, maxv, m2 + clip3(-tch, tch, (((m1 + m3 + 1) >> 1) - m2 + delta) >> 1));
+        if (mQ1) v[l][5] = clip3(0, maxv, m5 + clip3(-tch, tch, (((m6 + m4 + 1) >> 1) - m5 - delta) >> 1));
+    }
+    return true;
+}
+
+// one segment = one 4-line piece of an edge.  Luma: VER edges at x = 8k (4 rows), HOR at y = 8k
+// (4 columns).  Chroma (4:2:0): edges on the 8x8 chroma grid, 4 chroma lines per second luma unit
+// of the edge (edgeFilterChroma's idx << chromaShift), Cb and Cr together, bS 2 only.
+template <typename P, int DIR>
+__global__ __launch_bounds__(X265AMD_BLOCK) void k_deblock(const DbkLaunch L)
+{
+    const uint32_t b = xcd_block();
+    const DbkFrame& f = L.f[frame_of(L, b)];
+    const uint32_t s = (b - f.block0) * X265AMD_BLOCK + threadIdx.x;
+    if (s >= f.nseg) return;
+    const bool luma = s < f.nluma;
+    int ux, uy;
+    if (luma)
+    {
+        if (DIR == 0) { const int n = f.wu >> 1; uy = (int)(s / n); ux = 2 * (int)(s % n); }
+        else { ux = (int)(s % f.wu); uy = 2 * (int)(s / f.wu); }
+    }
+    else
+    {
+        const uint32_t c = s - f.nluma;
+        if (DIR == 0) { const int n = (f.wu + 3) >> 2; uy = 2 * (int)(c / n); ux = 4 * (int)(c % n); }
+        else { const int n = f.wu >> 1; ux = 2 * (int)(c % n); uy = 4 * (int)(c / n); }
+    }
+    const x265amd_deblock_unit* qu = f.units + uy * f.us + ux;
+    const Unit Q(qu);
+    const int mark = edge_mark(Q, DIR, DIR ? 4 * uy : 4 * ux);
+    if (!mark) return;
+    const Unit Pn(DIR ? qu - f.us : qu - 1);
+    const int bs = boundary_strength(f, Pn, Q, mark);
+    if (!bs || (!luma && bs < 2)) return;
+    int maskP = -1, maskQ = -1;
+    if (f.tqb)
+    {
+        maskP = (Pn.flags & 4) ? 0 : -1;
+        maskQ = (Q.flags & 4) ? 0 : -1;
+        if (!(maskP | maskQ)) return;
+    }
+    const int qp = (Pn.qp + Q.qp + 1) >> 1;
+    const int bd = sizeof(P) == 1 ? 0 : (L.maxv == 1023 ? 2 : 4);
+    if (luma)
+    {
+        P* q = (P*)f.plane[0] + (int64_t)(4 * uy) * f.stride + 4 * ux;
+        int v[4][8];
+        load_window<P, DIR>(q, f.stride, v);
+        if (filter_luma(v, bs, qp, maskP, maskQ, f.beta2, f.tc2, bd, L.maxv)) store_window<P, DIR>(q, f.stride, v);
+        return;
+    }
+    // edgeFilterChroma (deblock.cpp:443-521)
+#pragma unroll
+    for (int k = 0; k < 2; k++)
+    {
+        int qpc = qp + (k ? f.crqp : f.cbqp);
+        if (qpc >= 30) qpc = c_chroma_scale[qpc];
+        const int tc = (int)c_tc[clip3(0, 53, qpc + 2 + f.tc2)] << bd;
+        P* q = (P*)f.plane[1 + k] + (int64_t)(2 * uy) * f.cstride + 2 * ux;
+        int w[4][4];
+        if (DIR == 0)
+        {
+#pragma unroll
+            for (int l = 0; l < 4; l++) load_row<P, 4>(q + l * f.cstride - 2, w[l]);
+        }
+        else
+        {
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+            {
+                int r[4];
+                load_row<P, 4>(q + (i - 2) * f.cstride, r);
+#pragma unroll
+                for (int l = 0; l < 4; l++) w[l][i] = r[l];
+            }
+        }
+#pragma unroll
+        for (int l = 0; l < 4; l++)
+        {
+            const int m2 = w[l][0], m3 = w[l][1], m4 = w[l][2], m5 = w[l][3];
+            const int delta = clip3(-tc, tc, ((((m4 - m3) * 4) + m2 - m5 + 4) >> 3));
+            w[l][1] = clip3(0, L.maxv, m3 + (delta & maskP));
+            w[l][2] = clip3(0, L.maxv, m4 - (delta & maskQ));
+        }
+        if (DIR == 0)
+        {
+#pragma unroll
+            for (int l = 0; l < 4; l++) store_row<P, 4>(q + l * f.cstride - 2, w[l]);
+        }
+        else
+        {
+#pragma unroll
+            for (int i = 1; i < 3; i++)
+            {
+                const int r[4] = { w[0][i], w[1][i], w[2][i], w[3][i] };
+                store_row<P, 4>(q + (i - 2) * f.cstride, r);
+            }
+        }
+    }
+}
+
+// ================================================================ SAO apply
+struct SaoFrame
+{
+    const void* src[3];
+    void* dst[3];
+    int64_t stride, cstride;
+    const x265amd_sao_param* params;
+    int w, h, ctu_log2, wc, nctu, luma_on, chroma_on;
+    uint32_t block0, nseg, nluma, nchroma;   // segments: all, luma, per chroma plane
+};
+struct SaoLaunch
+{
+    SaoFrame f[kMaxFrames];
+    int count, maxv, bo_shift;
+};
+
+template <typename P>
+__global__ __launch_bounds__(X265AMD_BLOCK) void k_sao_apply(const SaoLaunch L)
+{
+    const uint32_t b = xcd_block();
+    const SaoFrame& f = L.f[frame_of(L, b)];
+    const uint32_t s = (b - f.block0) * X265AMD_BLOCK + threadIdx.x;
+    if (s >= f.nseg) return;
+    int p;
+    uint32_t r;
+    if (s < f.nluma) { p = 0; r = s; }
+    else { r = s - f.nluma; p = 1 + (r >= f.nchroma); r -= p == 2 ? f.nchroma : 0; }
+    const int pw = p ? f.w >> 1 : f.w, ph = p ? f.h >> 1 : f.h;
+    const int segs = (pw + 7) >> 3;
+    const int y = (int)(r / segs), x0 = 8 * (int)(r % segs);
+    const int n = pw - x0 < 8 ? pw - x0 : 8;         // 8, or 4 at a right edge of width 8k + 4
+    const int64_t st = p ? f.cstride : f.stride;
+    const P* src = (const P*)f.src[p] + y * st + x0;
+    P* dst = (P*)f.dst[p] + y * st + x0;
+    const int cl = f.ctu_log2 - (p ? 1 : 0);
+    const int c = (y >> cl) * f.wc + (x0 >> cl);
+    const x265amd_sao_param* prm = f.params + p * f.nctu + c;
+    int type = (int)prm->type;
+    if (p == 2 && type >= 0) type = (int)f.params[f.nctu + c].type;   // processSaoCu(addr, typeIdxCb, 2)
+    if (!(p ? f.chroma_on : f.luma_on)) type = -1;
+    int v[8];
+    load_row<P, 8>(src, v);
+    int o[8];
+    if (type == 4)
+    {
+        // m_offsetBo: offset[i] at band (bandPos + i) & 31 (sao.cpp:637-640)
+        const int band = prm->band;
+        const int o0 = prm->offset[0], o1 = prm->offset[1], o2 = prm->offset[2], o3 = prm->offset[3];
+#pragma unroll
+        for (int i = 0; i < 8; i++)
+        {
+            const int k = ((v[i] >> L.bo_shift) - band) & 31;
+            const int off = k == 0 ? o0 : k == 1 ? o1 : k == 2 ? o2 : k == 3 ? o3 : 0;
+            o[i] = clip3(0, L.maxv, v[i] + off);
+        }
+    }
+    else if (type >= 0)
+    {
+        // m_offsetEo via s_eoTable (sao.cpp:65-72, 644-650): edge type 0, 1, 3, 4 -> offset[0..3], 2 -> 0
+        const int e0 = prm->offset[0], e1 = prm->offset[1], e3 = prm->offset[2], e4 = prm->offset[3];
+        const int dy0 = type == 0 ? 0 : -1, dy1 = -dy0;
+        const int dx0 = type == 1 ? 0 : (type == 3 ? 1 : -1), dx1 = -dx0;
+        int a[10], bb[10];
+        {
+            const P* r0 = src + dy0 * st;
+            const P* r1 = src + dy1 * st;
+            int t[8];
+            load_row<P, 8>(r0, t);
+#pragma unroll
+            for (int i = 0; i < 8; i++) a[i + 1] = t[i];
+            a[0] = r0[-1]; a[9] = r0[8];
+            load_row<P, 8>(r1, t);
+#pragma unroll
+            for (int i = 0; i < 8; i++) bb[i + 1] = t[i];
+            bb[0] = r1[-1]; bb[9] = r1[8];
+        }
+        // EO leaves the picture's outermost column (not EO_1) / row (not EO_0) untouched
+        const bool skip_row = type != 0 && (y == 0 || y == ph - 1);
+#pragma unroll
+        for (int i = 0; i < 8; i++)
+        {
+            const int x = x0 + i;
+            const int na = dx0 == -1 ? a[i] : (dx0 == 1 ? a[i + 2] : a[i + 1]);
+            const int nb = dx1 == -1 ? bb[i] : (dx1 == 1 ? bb[i + 2] : bb[i + 1]);
+            const int e = sgn(v[i] - na) + sgn(v[i] - nb) + 2;
+            const int off = e == 0 ? e0 : e == 1 ? e1 : e == 3 ? e3 : e == 4 ? e4 : 0;
+            const bool skip = skip_row || (type != 1 && (x == 0 || x == pw - 1));
+            o[i] = skip ? v[i] : clip3(0, L.maxv, v[i] + off);
+        }
+    }
+    else
+    {
+#pragma unroll
+        for (int i = 0; i < 8; i++) o[i] = v[i];
+    }
+    if (n == 8) store_row<P, 8>(dst, o);
+    else
+    {
+        const int o4[4] = { o[0], o[1], o[2], o[3] };
+        store_row<P, 4>(dst, o4);
+    }
+}
+
+// ================================================================ SAO statistics
+struct StatFrame
+{
+    const void* fenc[3];
+    const void* rec[3];
+    int64_t fs, fcs, rs, rcs;
+    int32_t* stats;
+    int32_t* count;
+    int w, h, ctu_log2, wc, nd;
+    uint32_t block0, nctu;
+};
+struct StatLaunch
+{
+    StatFrame f[kMaxFrames];
+    int count, bo_shift;
+};
+
+template <typename P>
+__global__ __launch_bounds__(X265AMD_BLOCK) void k_sao_stats(const StatLaunch L)
+{
+    __shared__ int32_t eo_sum[3][4][5], eo_cnt[3][4][5];
+    __shared__ unsigned long long bo[3][32];
+    const uint32_t b = xcd_block();
+    const StatFrame& f = L.f[frame_of(L, b)];
+    const uint32_t c = b - f.block0;
+    const int tid = threadIdx.x;
+    for (int i = tid; i < 3 * 4 * 5; i += X265AMD_BLOCK)
+    {
+        (&eo_sum[0][0][0])[i] = 0;
+        (&eo_cnt[0][0][0])[i] = 0;
+    }
+    for (int i = tid; i < 3 * 32; i += X265AMD_BLOCK) (&bo[0][0])[i] = 0;
+    __syncthreads();
+    const int cxi = (int)(c % f.wc), cyi = (int)(c / f.wc);
+    for (int p = 0; p < 3; p++)
+    {
+        const int pw = p ? f.w >> 1 : f.w, ph = p ? f.h >> 1 : f.h;
+        const int cs = (1 << f.ctu_log2) >> (p ? 1 : 0);
+        const int x0 = cxi * cs, y0 = cyi * cs;
+        const int cw = (x0 + cs < pw ? x0 + cs : pw) - x0, ch = (y0 + cs < ph ? y0 + cs : ph) - y0;
+        const bool right = x0 + cw == pw, bottom = y0 + ch == ph;
+        const int po = p ? 2 : 0;
+        // regions per type (sao.cpp:825-925): EO_0, EO_1, EO_2, EO_3, BO; EO_0 keeps its bottom
+        // skip at the picture edge (sao.cpp:852)
+        int xs[5], xe[5], ys[5], ye[5];
+#pragma unroll
+        for (int t = 0; t < 5; t++)
+        {
+            const int sb = f.nd ? (t == 0 || t == 4 ? 3 : 4) : 4;
+            const int sr = f.nd ? (t == 1 || t == 4 ? 4 : 5) : 5;
+            const bool eox = t == 0 || t == 2 || t == 3, eoy = t >= 1 && t <= 3;
+            xs[t] = eox ? (x0 == 0) : 0;
+            xe[t] = right ? (eox ? cw - 1 : cw) : cw - sr + po;
+            ys[t] = eoy ? (y0 == 0) : 0;
+            ye[t] = t == 0 ? ch - sb + po : (bottom ? (eoy ? ch - 1 : ch) : ch - sb + po);
+        }
+        const int64_t rs = p ? f.rcs : f.rs, fs = p ? f.fcs : f.fs;
+        const P* rec = (const P*)f.rec[p] + (int64_t)y0 * rs + x0;
+        const P* fen = (const P*)f.fenc[p] + (int64_t)y0 * fs + x0;
+        const int segs = (cw + 7) >> 3, nseg = segs * ch;
+        const int nround = (nseg + 63) & ~63;                 // whole wavefronts per plane
+        int acc_s[4][5], acc_c[4][5];
+#pragma unroll
+        for (int t = 0; t < 4; t++)
+#pragma unroll
+            for (int k = 0; k < 5; k++) acc_s[t][k] = acc_c[t][k] = 0;
+        for (int sg = tid; sg < nround; sg += X265AMD_BLOCK)
+        {
+            if (sg < nseg)
+            {
+                const int ly = sg / segs, lx0 = 8 * (sg % segs);
+                const P* r1 = rec + (int64_t)ly * rs + lx0;
+                int up[10], mid[10], dn[10], fe[8];
+                {
+                    int t[8];
+                    load_row<P, 8>(r1 - rs, t);
+#pragma unroll
+                    for (int i = 0; i < 8; i++) up[i + 1] = t[i];
+                    load_row<P, 8>(r1, t);
+#pragma unroll
+                    for (int i = 0; i < 8; i++) mid[i + 1] = t[i];
+                    load_row<P, 8>(r1 + rs, t);
+#pragma unroll
+                    for (int i = 0; i < 8; i++) dn[i + 1] = t[i];
+                    up[0] = r1[-rs - 1]; up[9] = r1[-rs + 8];
+                    mid[0] = r1[-1]; mid[9] = r1[8];
+                    dn[0] = r1[rs - 1]; dn[9] = r1[rs + 8];
+                    load_row<P, 8>(fen + (int64_t)ly * fs + lx0, fe);
+                }
+#pragma unroll
+                for (int i = 0; i < 8; i++)
+                {
+                    const int lx = lx0 + i;
+                    const int v = mid[i + 1], d = fe[i] - v;
+                    const int e[4] = { sgn(v - mid[i]) + sgn(v - mid[i + 2]), sgn(v - up[i + 1]) + sgn(v - dn[i + 1]),
+                                       sgn(v - up[i]) + sgn(v - dn[i + 2]), sgn(v - up[i + 2]) + sgn(v - dn[i]) };
+#pragma unroll
+                    for (int t = 0; t < 4; t++)
+                    {
+                        const bool in = lx >= xs[t] && lx < xe[t] && ly >= ys[t] && ly < ye[t];
+                        const int k = e[t] == 0 ? 0 : (e[t] < 0 ? e[t] + 3 : e[t] + 2);   // s_eoTable[e + 2]
+#pragma unroll
+                        for (int kk = 0; kk < 5; kk++)
+                        {
+                            const bool hit = in && k == kk;
+                            acc_s[t][kk] += hit ? d : 0;
+                            acc_c[t][kk] += hit ? 1 : 0;
+                        }
+                    }
+                    if (lx >= xs[4] && lx < xe[4] && ly >= ys[4] && ly < ye[4])
+                        atomicAdd(&bo[p][v >> L.bo_shift], (1ull << 40) + (unsigned long long)(int64_t)d);
+                }
+            }
+        }
+        // wavefront reduction of the edge classes, one LDS add per wave
+#pragma unroll
+        for (int t = 0; t < 4; t++)
+#pragma unroll
+            for (int k = 0; k < 5; k++)
+            {
+                int vs = acc_s[t][k], vc = acc_c[t][k];
+#pragma unroll
+                for (int m = 32; m > 0; m >>= 1)
+                {
+                    vs += __shfl_xor(vs, m, 64);
+                    vc += __shfl_xor(vc, m, 64);
+                }
+                if ((tid & 63) == 0 && vc)
+                {
+                    atomicAdd(&eo_sum[p][t][k], vs);
+                    atomicAdd(&eo_cnt[p][t][k], vc);
+                }
+            }
+    }
+    __syncthreads();
+    // every entry of the CTU's [3][5][33] block
+    int32_t* os = f.stats + (int64_t)c * 3 * 5 * 33;
+    int32_t* oc = f.count + (int64_t)c * 3 * 5 * 33;
+    for (int i = tid; i < 3 * 5 * 33; i += X265AMD_BLOCK)
+    {
+        const int p = i / 165, t = (i % 165) / 33, k = i % 33;
+        int sv = 0, cv = 0;
+        if (t < 4)
+        {
+            if (k < 5) { sv = eo_sum[p][t][k]; cv = eo_cnt[p][t][k]; }
+        }
+        else if (k >= 1)
+        {
+            const long long tot = (long long)bo[p][k - 1];
+            const long long lo = (long long)((unsigned long long)tot << 24) >> 24;   // sign-extend 40 bits
+            sv = (int)lo;
+            cv = (int)((tot - lo) >> 40);
+        }
+        os[i] = sv;
+        oc[i] = cv;
+    }
+}
+
+// ================================================================ border extension
+struct BorderPlane
+{
+    void* p;
+    int64_t stride;
+    int w, h, mx, my;
+    uint32_t block0_lr, block0_tb;
+};
+constexpr int kMaxPlanes = 16;
+struct BorderLaunch
+{
+    BorderPlane f[kMaxPlanes];
+    int count;
+};
+
+// extendRowBorder (ipfilter.cpp:59-77): one lane per (row, side)
+template <typename P>
+__global__ __launch_bounds__(X265AMD_BLOCK) void k_border_lr(const BorderLaunch L)
+{
+    const uint32_t b = xcd_block();
+    int i = 0;
+#pragma unroll
+    for (int k = 1; k < kMaxPlanes; k++)
+        if (k < L.count && L.f[k].block0_lr <= b) i = k;
+    const BorderPlane& f = L.f[i];
+    const int64_t t = (int64_t)(b - f.block0_lr) * X265AMD_BLOCK + threadIdx.x;
+    if (t >= 2 * (int64_t)f.h) return;
+    const bool right = t >= f.h;
+    const int y = (int)(right ? t - f.h : t);
+    P* row = (P*)f.p + y * f.stride;
+    const P v = right ? row[f.w - 1] : row[0];
+    P* d = right ? row + f.w : row - f.mx;
+    int x = 0;
+    if constexpr (sizeof(P) == 1)
+    {
+        const uint32_t w = 0x01010101u * (uint32_t)v;
+        for (; x + 16 <= f.mx; x += 16) stu<uint4>(d + x, make_uint4(w, w, w, w));
+        for (; x + 4 <= f.mx; x += 4) stu<uint32_t>(d + x, w);
+    }
+    else
+    {
+        const uint32_t w = 0x00010001u * (uint32_t)v;
+        for (; x + 8 <= f.mx; x += 8) stu<uint4>(d + x, make_uint4(w, w, w, w));
+        for (; x + 2 <= f.mx; x += 2) stu<uint32_t>(d + x, w);
+    }
+    for (; x < f.mx; x++) d[x] = v;
+}
+
+// the margin rows: full-stride copies of the extended first / last row, 16 bytes per lane
+template <typename P>
+__global__ __launch_bounds__(X265AMD_BLOCK) void k_border_tb(const BorderLaunch L)
+{
+    constexpr int C = 16 / sizeof(P);
+    const uint32_t b = xcd_block();
+    int i = 0;
+#pragma unroll
+    for (int k = 1; k < kMaxPlanes; k++)
+        if (k < L.count && L.f[k].block0_tb <= b) i = k;
+    const BorderPlane& f = L.f[i];
+    const int64_t chunks = (f.stride + C - 1) / C;
+    const int64_t t = (int64_t)(b - f.block0_tb) * X265AMD_BLOCK + threadIdx.x;
+    if (t >= 2 * (int64_t)f.my * chunks) return;
+    const int r = (int)(t / chunks), c = (int)(t % chunks);
+    const bool bottom = r >= f.my;
+    const int yd = bottom ? f.h + (r - f.my) : -1 - r;
+    const int ys = bottom ? f.h - 1 : 0;
+    const P* s = (const P*)f.p - f.mx + ys * f.stride + c * C;
+    P* d = (P*)f.p - f.mx + yd * f.stride + c * C;
+    if ((c + 1) * C <= f.stride) stu<uint4>(d, ldu<uint4>(s));
+    else
+        for (int x = 0; x < f.stride - c * C; x++) d[x] = s[x];
+}
+
+} // namespace x265amd
+
+using namespace x265amd;
+
+static bool bd_ok(int depth) { return depth == 8 || depth == 10 || depth == 12; }
+static uint32_t nblocks(uint64_t n) { return (uint32_t)((n + X265AMD_BLOCK - 1) / X265AMD_BLOCK); }
+
+extern "C" int x265amd_deblock(int depth, int count, const x265amd_deblock_frame* frames, void* stream)
+{
+    if (!bd_ok(depth) || count < 0 || (count && !frames)) return X265AMD_EINVAL;
+    for (int i = 0; i < count; i++)
+    {
+        const x265amd_deblock_frame& a = frames[i];
+        if (a.width <= 0 || a.height <= 0 || (a.width & 7) || (a.height & 7) || !a.plane[0] || !a.plane[1] ||
+            !a.plane[2] || !a.units || a.unit_stride < a.width / 4 || a.stride < a.width || a.cstride < a.width / 2)
+            return X265AMD_EINVAL;
+    }
+    hipStream_t st = (hipStream_t)stream;
+    for (int dir = 0; dir < 2; dir++)
+        for (int i0 = 0; i0 < count; i0 += kMaxFrames)
+        {
+            DbkLaunch L;
+            memset(&L, 0, sizeof(L));
+            L.count = count - i0 < kMaxFrames ? count - i0 : kMaxFrames;
+            L.maxv = (1 << depth) - 1;
+            uint32_t blocks = 0;
+            for (int k = 0; k < L.count; k++)
+            {
+                const x265amd_deblock_frame& a = frames[i0 + k];
+                DbkFrame& f = L.f[k];
+                for (int p = 0; p < 3; p++) f.plane[p] = a.plane[p];
+                f.stride = a.stride;
+                f.cstride = a.cstride;
+                f.units = a.units;
+                f.us = a.unit_stride;
+                f.wu = a.width >> 2;
+                f.hu = a.height >> 2;
+                f.is_p = a.is_p;
+                f.beta2 = 2 * a.beta_offset_div2;
+                f.tc2 = 2 * a.tc_offset_div2;
+                f.cbqp = a.cb_qp_offset;
+                f.crqp = a.cr_qp_offset;
+                f.tqb = a.tq_bypass_enabled;
+                memcpy(f.poc, a.ref_poc, sizeof(f.poc));
+                if (dir == 0)
+                {
+                    f.nluma = (uint32_t)((f.wu >> 1) * f.hu);
+                    f.nseg = f.nluma + (uint32_t)(((f.wu + 3) >> 2) * (f.hu >> 1));
+                }
+                else
+                {
+                    f.nluma = (uint32_t)(f.wu * (f.hu >> 1));
+                    f.nseg = f.nluma + (uint32_t)((f.wu >> 1) * ((f.hu + 3) >> 2));
+                }
+                f.block0 = blocks;
+                blocks += nblocks(f.nseg);
+            }
+            if (!blocks) continue;
+            if (depth == 8)
+            {
+                if (dir == 0) hipLaunchKernelGGL((k_deblock<uint8_t, 0>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, L);
+                else hipLaunchKernelGGL((k_deblock<uint8_t, 1>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, L);
+            }
+            else
+            {
+                if (dir == 0) hipLaunchKernelGGL((k_deblock<uint16_t, 0>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, L);
+                else hipLaunchKernelGGL((k_deblock<uint16_t, 1>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, L);
+            }
+            const hipError_t e = hipGetLastError();
+            if (e != hipSuccess) return (int)e;
+        }
+    return 0;
+}
+
+extern "C" int x265amd_sao_apply(int depth, int count, const x265amd_sao_frame* frames, void* stream)
+{
+    if (!bd_ok(depth) || count < 0 || (count && !frames)) return X265AMD_EINVAL;
+    for (int i = 0; i < count; i++)
+    {
+        const x265amd_sao_frame& a = frames[i];
+        if (a.width <= 0 || a.height <= 0 || (a.width & 7) || (a.height & 7) || a.ctu_log2 < 4 || a.ctu_log2 > 6 ||
+            !a.params || a.stride < a.width || a.cstride < a.width / 2)
+            return X265AMD_EINVAL;
+        for (int p = 0; p < 3; p++)
+            if (!a.src[p] || !a.dst[p] || a.src[p] == a.dst[p]) return X265AMD_EINVAL;
+    }
+    hipStream_t st = (hipStream_t)stream;
+    for (int i0 = 0; i0 < count; i0 += kMaxFrames)
+    {
+        SaoLaunch L;
+        memset(&L, 0, sizeof(L));
+        L.count = count - i0 < kMaxFrames ? count - i0 : kMaxFrames;
+        L.maxv = (1 << depth) - 1;
+        L.bo_shift = depth - 5;
+        uint32_t blocks = 0;
+        for (int k = 0; k < L.count; k++)
+        {
+            const x265amd_sao_frame& a = frames[i0 + k];
+            SaoFrame& f = L.f[k];
+            for (int p = 0; p < 3; p++) { f.src[p] = a.src[p]; f.dst[p] = a.dst[p]; }
+            f.stride = a.stride;
+            f.cstride = a.cstride;
+            f.params = a.params;
+            f.w = a.width;
+            f.h = a.height;
+            f.ctu_log2 = a.ctu_log2;
+            const int ctu = 1 << a.ctu_log2;
+            f.wc = (a.width + ctu - 1) >> a.ctu_log2;
+            f.nctu = f.wc * ((a.height + ctu - 1) >> a.ctu_log2);
+            f.luma_on = a.luma_on;
+            f.chroma_on = a.chroma_on;
+            f.nluma = (uint32_t)(((a.width + 7) >> 3) * a.height);
+            f.nchroma = (uint32_t)(((a.width / 2 + 7) >> 3) * (a.height / 2));
+            f.nseg = f.nluma + 2 * f.nchroma;
+            f.block0 = blocks;
+            blocks += nblocks(f.nseg);
+        }
+        if (!blocks) continue;
+        if (depth == 8) hipLaunchKernelGGL((k_sao_apply<uint8_t>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, L);
+        else hipLaunchKernelGGL((k_sao_apply<uint16_t>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, L);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return (int)e;
+    }
+    return 0;
+}
+
+extern "C" int x265amd_sao_stats(int depth, int count, const x265amd_sao_stats_frame* frames, void* stream)
+{
+    if (!bd_ok(depth) || count < 0 || (count && !frames)) return X265AMD_EINVAL;
+    for (int i = 0; i < count; i++)
+    {
+        const x265amd_sao_stats_frame& a = frames[i];
+        if (a.width <= 0 || a.height <= 0 || (a.width & 7) || (a.height & 7) || a.ctu_log2 < 4 || a.ctu_log2 > 6 ||
+            !a.stats || !a.count)
+            return X265AMD_EINVAL;
+        for (int p = 0; p < 3; p++)
+            if (!a.fenc[p] || !a.rec[p]) return X265AMD_EINVAL;
+    }
+    hipStream_t st = (hipStream_t)stream;
+    for (int i0 = 0; i0 < count; i0 += kMaxFrames)
+    {
+        StatLaunch L;
+        memset(&L, 0, sizeof(L));
+        L.count = count - i0 < kMaxFrames ? count - i0 : kMaxFrames;
+        L.bo_shift = depth - 5;
+        uint32_t blocks = 0;
+        for (int k = 0; k < L.count; k++)
+        {
+            const x265amd_sao_stats_frame& a = frames[i0 + k];
+            StatFrame& f = L.f[k];
+            for (int p = 0; p < 3; p++) { f.fenc[p] = a.fenc[p]; f.rec[p] = a.rec[p]; }
+            f.fs = a.fenc_stride;
+            f.fcs = a.fenc_cstride;
+            f.rs = a.rec_stride;
+            f.rcs = a.rec_cstride;
+            f.stats = a.stats;
+            f.count = a.count;
+            f.w = a.width;
+            f.h = a.height;
+            f.ctu_log2 = a.ctu_log2;
+            f.nd = a.non_deblocked;
+            const int ctu = 1 << a.ctu_log2;
+            f.wc = (a.width + ctu - 1) >> a.ctu_log2;
+            f.nctu = (uint32_t)(f.wc * ((a.height + ctu - 1) >> a.ctu_log2));
+            f.block0 = blocks;
+            blocks += f.nctu;
+        }
+        if (depth == 8) hipLaunchKernelGGL((k_sao_stats<uint8_t>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, L);
+        else hipLaunchKernelGGL((k_sao_stats<uint16_t>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, L);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return (int)e;
+    }
+    return 0;
+}
+
+extern "C" int x265amd_extend_border(int depth, int count, const x265amd_border_plane* planes, void* stream)
+{
+    if (!bd_ok(depth) || count < 0 || (count && !planes)) return X265AMD_EINVAL;
+    for (int i = 0; i < count; i++)
+    {
+        const x265amd_border_plane& a = planes[i];
+        if (!a.plane || a.width <= 0 || a.height <= 0 || a.margin_x < 0 || a.margin_y < 0 ||
+            a.stride < a.width + 2 * a.margin_x)
+            return X265AMD_EINVAL;
+    }
+    hipStream_t st = (hipStream_t)stream;
+    for (int i0 = 0; i0 < count; i0 += kMaxPlanes)
+    {
+        BorderLaunch L;
+        memset(&L, 0, sizeof(L));
+        L.count = count - i0 < kMaxPlanes ? count - i0 : kMaxPlanes;
+        uint32_t blr = 0, btb = 0;
+        const int C = depth == 8 ? 16 : 8;
+        for (int k = 0; k < L.count; k++)
+        {
+            const x265amd_border_plane& a = planes[i0 + k];
+            BorderPlane& f = L.f[k];
+            f.p = a.plane;
+            f.stride = a.stride;
+            f.w = a.width;
+            f.h = a.height;
+            f.mx = a.margin_x;
+            f.my = a.margin_y;
+            f.block0_lr = blr;
+            f.block0_tb = btb;
+            blr += nblocks(2 * (uint64_t)a.height);
+            btb += nblocks(2 * (uint64_t)a.margin_y * (uint64_t)((a.stride + C - 1) / C));
+        }
+        if (depth == 8) hipLaunchKernelGGL((k_border_lr<uint8_t>), dim3(blr), dim3(X265AMD_BLOCK), 0, st, L);
+        else hipLaunchKernelGGL((k_border_lr<uint16_t>), dim3(blr), dim3(X265AMD_BLOCK), 0, st, L);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return (int)e;
+        if (btb)
+        {
+            if (depth == 8) hipLaunchKernelGGL((k_border_tb<uint8_t>), dim3(btb), dim3(X265AMD_BLOCK), 0, st, L);
+            else hipLaunchKernelGGL((k_border_tb<uint16_t>), dim3(btb), dim3(X265AMD_BLOCK), 0, st, L);
+            e = hipGetLastError();
+            if (e != hipSuccess) return (int)e;
+        }
+    }
+    return 0;
+}

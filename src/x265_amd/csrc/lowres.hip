@@ -207,9 +207,14 @@ __device__ __forceinline__ int lowres_mode_cost(int m, const int (&smp)[33], con
     // DC: raw samples with the edge filter; planar: filtered samples, no edge filter;
     // angular: g_intraFilterFlags[mode] & 8 selects the filtered samples, edge filter on (N <= 16)
     const bool use_flt = m == 0 || (m >= 2 && (c_intra.filter_flags[m] & 8));
+    // a masked blend, kept opaque: a plain `use_flt ? flt[i] : smp[i]` is
+    // rewritten into a select of the two arrays' addresses, which puts both
+    // arrays in scratch
+    int mk = use_flt ? -1 : 0;
+    asm volatile("" : "+v"(mk));
     int nb[33];
 #pragma unroll
-    for (int i = 0; i < 33; i++) nb[i] = use_flt ? flt[i] : smp[i];
+    for (int i = 0; i < 33; i++) nb[i] = smp[i] ^ ((smp[i] ^ flt[i]) & mk);
     int v[8][8];
     const ModeInfo mi = intra_lane_predict<8>(nb, m, m != 0, maxv, D, v);
     return satd8<P>(fe, v, mi.hor);
@@ -221,8 +226,10 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_lowres_intra(const LowresIntr
     __shared__ uint32_t D[24][X265AMD_BLOCK];          // intra_lane_predict's per-lane LDS column (3N, N = 8)
     const int lane = threadIdx.x & 7;
     const int ncu = a.wcu * a.hcu;
-    const int64_t g = ((int64_t)xcd_block() * X265AMD_BLOCK + threadIdx.x) >> 3;
-    if (g >= (int64_t)a.n * ncu) return;                // whole 8-lane groups
+    const int64_t total = (int64_t)a.n * ncu;
+    const int64_t graw = ((int64_t)xcd_block() * X265AMD_BLOCK + threadIdx.x) >> 3;
+    const bool valid = graw < total;                    // whole 8-lane groups; the wave stays
+    const int64_t g = valid ? graw : total - 1;         // converged for the sums below
     const int f = (int)(g / ncu), xy = (int)(g % ncu);
     const int cx = xy % a.wcu, cy = xy / a.wcu;
     const P* cur = (const P*)a.planes + a.plane_off[f] + 8 * cx + 8 * cy * a.ls;
@@ -278,21 +285,47 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_lowres_intra(const LowresIntr
     if (acost < icost) { icost = acost; imode = amode; }
     icost += a.penalty;
 
-    if (lane == 0)
+    const int64_t o = (int64_t)f * ncu + xy;
+    if (lane == 0 && valid)
     {
-        const int64_t o = (int64_t)f * ncu + xy;
         a.intra_cost[o] = icost;
         a.intra_mode[o] = (uint8_t)imode;
         a.lowres_cost[o] = (uint16_t)(icost < 0x3fff ? icost : 0x3fff);   // LOWRES_COST_MASK, shift 0
-        const bool scored = (cx > 0 && cx < a.wcu - 1 && cy > 0 && cy < a.hcu - 1) || a.wcu <= 2 || a.hcu <= 2;
-        const int icost_aq = (scored && a.inv_q) ? ((icost * a.inv_q[o] + 128) >> 8) : icost;
-        // integer sums: order-independent, so atomics reproduce the serial totals
-        atomicAdd(&a.row_satd[(int64_t)f * a.hcu + cy], icost_aq);
-        if (scored)
+    }
+    const bool scored = (cx > 0 && cx < a.wcu - 1 && cy > 0 && cy < a.hcu - 1) || a.wcu <= 2 || a.hcu <= 2;
+    const int icost_aq = (scored && a.inv_q) ? ((icost * a.inv_q[o] + 128) >> 8) : icost;
+
+    // integer sums: order-independent, so atomics reproduce the serial totals.
+    // The wave's eight CUs are consecutive: when they share a frame (and a
+    // row) one atomic per wave replaces eight contended ones.
+    const bool lead = lane == 0 && valid;
+    int r_aq = lead ? icost_aq : 0;
+    int s_c = lead && scored ? icost : 0, s_aq = lead && scored ? icost_aq : 0;
+#pragma unroll
+    for (int m = 8; m < 64; m <<= 1)
+    {
+        r_aq += __shfl_xor(r_aq, m, 64);
+        s_c += __shfl_xor(s_c, m, 64);
+        s_aq += __shfl_xor(s_aq, m, 64);
+    }
+    const int wl = threadIdx.x & 63;
+    const int row_key = f * a.hcu + cy;
+    const int f0 = __shfl(f, 0, 64), f7 = __shfl(f, 56, 64);
+    const int k0 = __shfl(row_key, 0, 64), k7 = __shfl(row_key, 56, 64);
+    if (k0 == k7 ? wl == 0 : lead)
+        atomicAdd(&a.row_satd[row_key], k0 == k7 ? r_aq : icost_aq);
+    if (f0 == f7)
+    {
+        if (wl == 0)
         {
-            atomicAdd((unsigned long long*)&a.cost_est[2 * f], (unsigned long long)(int64_t)icost);
-            atomicAdd((unsigned long long*)&a.cost_est[2 * f + 1], (unsigned long long)(int64_t)icost_aq);
+            atomicAdd((unsigned long long*)&a.cost_est[2 * f], (unsigned long long)(int64_t)s_c);
+            atomicAdd((unsigned long long*)&a.cost_est[2 * f + 1], (unsigned long long)(int64_t)s_aq);
         }
+    }
+    else if (lead && scored)
+    {
+        atomicAdd((unsigned long long*)&a.cost_est[2 * f], (unsigned long long)(int64_t)icost);
+        atomicAdd((unsigned long long*)&a.cost_est[2 * f + 1], (unsigned long long)(int64_t)icost_aq);
     }
 }
 

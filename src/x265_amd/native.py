@@ -72,6 +72,33 @@ class MeBatch(C.Structure):
                 ("ref_cstride", _ip), ("ref_coff", _vp)]
 
 
+# f4 frame descriptors (include/x265_amd.h): device addresses of the plane origins
+_i64 = C.c_int64
+
+
+class SaoFrame(C.Structure):
+    _fields_ = [("width", _int), ("height", _int), ("ctu_log2", _int), ("luma_on", _int), ("chroma_on", _int),
+                ("src", _vp * 3), ("dst", _vp * 3), ("stride", _i64), ("cstride", _i64), ("params", _vp)]
+
+
+class SaoStatsFrame(C.Structure):
+    _fields_ = [("width", _int), ("height", _int), ("ctu_log2", _int), ("non_deblocked", _int), ("fenc", _vp * 3),
+                ("fenc_stride", _i64), ("fenc_cstride", _i64), ("rec", _vp * 3), ("rec_stride", _i64),
+                ("rec_cstride", _i64), ("stats", _vp), ("count", _vp)]
+
+
+class DeblockFrame(C.Structure):
+    _fields_ = [("width", _int), ("height", _int), ("plane", _vp * 3), ("stride", _i64), ("cstride", _i64),
+                ("units", _vp), ("unit_stride", _i64), ("is_p", _int), ("beta_offset_div2", _int),
+                ("tc_offset_div2", _int), ("cb_qp_offset", _int), ("cr_qp_offset", _int), ("tq_bypass_enabled", _int),
+                ("ref_poc", (C.c_int32 * 16) * 2)]
+
+
+class BorderPlane(C.Structure):
+    _fields_ = [("plane", _vp), ("stride", _i64), ("width", _int), ("height", _int), ("margin_x", _int),
+                ("margin_y", _int)]
+
+
 def _addr(t):
     return None if t is None else t.data_ptr()
 
@@ -260,3 +287,21 @@ class Primitives:
                          _addr(out_mv), _addr(out_cost), _addr(fcb), _addr(fcr), fcs, _addr(fco), _addr(rcb),
                          _addr(rcr), rcs, _addr(rco))
         self._check(self.lib.x265amd_motion_search(depth, 1, arr, stream or _stream()), "motion_search")
+
+    # -- f4 loop filters and border extension (frame descriptors: SaoFrame, SaoStatsFrame,
+    #    DeblockFrame, BorderPlane with device addresses)
+    def _frames(self, entry, what, depth, frames, stream):
+        arr = (type(frames[0]) * len(frames))(*frames)
+        self._check(getattr(self.lib, entry)(depth, len(frames), arr, stream or _stream()), what)
+
+    def sao_apply(self, depth, frames, stream=None):
+        self._frames("x265amd_sao_apply", "sao_apply", depth, frames, stream)
+
+    def sao_stats(self, depth, frames, stream=None):
+        self._frames("x265amd_sao_stats", "sao_stats", depth, frames, stream)
+
+    def deblock(self, depth, frames, stream=None):
+        self._frames("x265amd_deblock", "deblock", depth, frames, stream)
+
+    def extend_border(self, depth, planes, stream=None):
+        self._frames("x265amd_extend_border", "extend_border", depth, planes, stream)

@@ -1,0 +1,241 @@
+"""f4 loop filters: SAO apply, SAO statistics, deblocking, border extension.
+
+CPU tests pin the restatement (oracle/x265_oracle.c) to the reference's own SAO / Deblock classes
+run by oracle/ref_shim.cpp on the same frames; GPU tests hold the gfx950 kernels to the oracle,
+bit-exact.
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+import f4cases as F
+import pyoracle as po
+
+SIZES = [(200, 136, 6), (128, 64, 5), (96, 48, 4), (256, 128, 6)]
+DEPTHS = [8, 10]
+
+
+def _libs(depth):
+    if not po.available("ref", depth):
+        pytest.skip("reference library not built (make -C oracle ref)")
+    return po.FrameFilters("oracle", depth), po.FrameFilters("ref", depth)
+
+
+@pytest.mark.parametrize("depth", DEPTHS)
+@pytest.mark.parametrize("size", SIZES)
+def test_sao_apply_oracle_vs_reference(oracle_libs, depth, size):
+    W, H, cl = size
+    O, R = _libs(depth)
+    rng = np.random.default_rng(W + H + depth + cl)
+    pl = F.frame_planes(W, H, depth, rng)
+    prm = F.sao_params(W, H, cl, depth, rng)
+    for on in ((1, 1), (1, 0), (0, 1)):
+        a, b = F.copy_planes(pl), F.copy_planes(pl)
+        O.sao_apply(W, H, cl, a, F.MARGIN, prm, *on)
+        R.sao_apply(W, H, cl, b, F.MARGIN, prm, *on)
+        for x, y in zip(a, b):
+            np.testing.assert_array_equal(x, y)
+    assert sum(int((x != y).sum()) for x, y in zip(b, pl)) > 0
+
+
+@pytest.mark.parametrize("depth", DEPTHS)
+@pytest.mark.parametrize("size", SIZES)
+@pytest.mark.parametrize("non_deblocked", [0, 1])
+def test_sao_stats_oracle_vs_reference(oracle_libs, depth, size, non_deblocked):
+    W, H, cl = size
+    O, R = _libs(depth)
+    rng = np.random.default_rng(7 * W + H + depth + cl)
+    rec = F.frame_planes(W, H, depth, rng)
+    fenc = F.frame_planes(W, H, depth, rng)
+    s1, c1 = O.sao_stats(W, H, cl, fenc, rec, F.MARGIN, non_deblocked)
+    s2, c2 = R.sao_stats(W, H, cl, fenc, rec, F.MARGIN, non_deblocked)
+    np.testing.assert_array_equal(c1, c2)
+    np.testing.assert_array_equal(s1, s2)
+
+
+@pytest.mark.parametrize("depth", DEPTHS)
+@pytest.mark.parametrize("size", SIZES)
+@pytest.mark.parametrize("slice_type", ["I", "P", "B"])
+@pytest.mark.parametrize("tq", [0, 1])
+def test_deblock_oracle_vs_reference(oracle_libs, depth, size, slice_type, tq):
+    W, H, cl = size
+    O, R = _libs(depth)
+    rng = np.random.default_rng(13 * W + H + depth + cl + ord(slice_type) + tq)
+    pl = F.frame_planes(W, H, depth, rng)
+    U = F.deblock_units(W, H, cl, depth, rng, slice_type, 0.2 if tq else 0.0)
+    dp = F.deblock_params(rng, slice_type, tq)
+    a, b = F.copy_planes(pl), F.copy_planes(pl)
+    O.deblock(W, H, cl, a, F.MARGIN, U, dp)
+    R.deblock(W, H, cl, b, F.MARGIN, U, dp)
+    for x, y in zip(a, b):
+        np.testing.assert_array_equal(x, y)
+    assert int((b[0] != pl[0]).sum()) > 0
+
+
+@pytest.mark.parametrize("depth", DEPTHS)
+def test_extend_border_oracle_vs_reference(oracle_libs, depth):
+    O, R = _libs(depth)
+    rng = np.random.default_rng(depth)
+    W, H, mx, my = 200, 136, 96, 80
+    dt = np.uint8 if depth == 8 else np.uint16
+    p = rng.integers(0, 1 << depth, size=(H + 2 * my, W + 2 * mx)).astype(dt)
+    a, b = p.copy(), p.copy()
+    O.extend_border(a, mx, my, W, H)
+    R.extend_border(b, mx, my, W, H)
+    np.testing.assert_array_equal(a, b)
+
+
+# ---------------------------------------------------------------- GPU: gfx950 kernels vs the oracle
+GPU_SIZES = [(200, 136, 6), (128, 64, 5), (96, 48, 4), (1920, 1080, 6)]
+
+
+def _dev(planes):
+    import torch
+
+    return tuple(torch.from_numpy(p.view(np.int16) if p.dtype == np.uint16 else p).cuda() for p in planes)
+
+
+def _host(t, dtype):
+    a = t.cpu().numpy()
+    return a.view(np.uint16) if dtype == np.uint16 else a
+
+
+def _org(t, margin=F.MARGIN):
+    return t.data_ptr() + (margin * t.shape[1] + margin) * t.element_size()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("depth", DEPTHS)
+def test_gpu_deblock(gpu_prims, depth):
+    import torch
+    from src.x265_amd.native import DeblockFrame
+
+    O = po.FrameFilters("oracle", depth)
+    frames, keep, expect = [], [], []
+    for i, (W, H, cl) in enumerate(GPU_SIZES):
+        for st in ("I", "P", "B"):
+            tq = int(st == "B" and i == 0)
+            rng = np.random.default_rng(100 * i + ord(st) + depth)
+            pl = F.frame_planes(W, H, depth, rng)
+            U = F.deblock_units(W, H, cl, depth, rng, st, 0.2 if tq else 0.0)
+            dp = F.deblock_params(rng, st, tq)
+            ref = F.copy_planes(pl)
+            O.deblock(W, H, cl, ref, F.MARGIN, U, dp)
+            d = _dev(pl)
+            du = torch.from_numpy(U.view(np.uint8).reshape(U.shape[0], -1)).cuda()
+            fr = DeblockFrame()
+            fr.width, fr.height = W, H
+            for p in range(3):
+                fr.plane[p] = _org(d[p])
+            fr.stride, fr.cstride = d[0].shape[1], d[1].shape[1]
+            fr.units, fr.unit_stride = du.data_ptr(), U.shape[1]
+            fr.is_p, fr.beta_offset_div2, fr.tc_offset_div2 = dp.is_p, dp.beta_offset_div2, dp.tc_offset_div2
+            fr.cb_qp_offset, fr.cr_qp_offset, fr.tq_bypass_enabled = dp.cb_qp_offset, dp.cr_qp_offset, tq
+            for lst in range(2):
+                for k in range(16):
+                    fr.ref_poc[lst][k] = dp.ref_poc[lst][k]
+            frames.append(fr)
+            keep.append((d, du))
+            expect.append((ref, pl))
+    gpu_prims.deblock(depth, frames)          # 12 frames of four sizes: two launches per direction
+    torch.cuda.synchronize()
+    for (d, _), (ref, pl) in zip(keep, expect):
+        for p in range(3):
+            np.testing.assert_array_equal(_host(d[p], pl[p].dtype), ref[p])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("depth", DEPTHS)
+def test_gpu_sao_apply(gpu_prims, depth):
+    import torch
+    from src.x265_amd.native import SaoFrame
+
+    O = po.FrameFilters("oracle", depth)
+    frames, keep = [], []
+    for i, (W, H, cl) in enumerate(GPU_SIZES):
+        for on in ((1, 1), (1, 0), (0, 1)):
+            rng = np.random.default_rng(10 * i + depth + on[0])
+            pl = F.frame_planes(W, H, depth, rng)
+            prm = F.sao_params(W, H, cl, depth, rng)
+            ref = F.copy_planes(pl)
+            O.sao_apply(W, H, cl, ref, F.MARGIN, prm, *on)
+            src, dst = _dev(pl), _dev(tuple(np.zeros_like(p) for p in pl))
+            dprm = torch.from_numpy(prm.view(np.uint8)).cuda()
+            fr = SaoFrame()
+            fr.width, fr.height, fr.ctu_log2, fr.luma_on, fr.chroma_on = W, H, cl, on[0], on[1]
+            for p in range(3):
+                fr.src[p], fr.dst[p] = _org(src[p]), _org(dst[p])
+            fr.stride, fr.cstride = src[0].shape[1], src[1].shape[1]
+            fr.params = dprm.data_ptr()
+            frames.append(fr)
+            keep.append((src, dst, dprm, ref, pl))
+    gpu_prims.sao_apply(depth, frames)
+    torch.cuda.synchronize()
+    M = F.MARGIN
+    for (src, dst, _, ref, pl) in keep:
+        for p in range(3):
+            got = _host(dst[p], pl[p].dtype)[M:-M, M:-M]
+            np.testing.assert_array_equal(got, ref[p][M:-M, M:-M])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("depth", DEPTHS)
+def test_gpu_sao_stats(gpu_prims, depth):
+    import torch
+    from src.x265_amd.native import SaoStatsFrame
+
+    O = po.FrameFilters("oracle", depth)
+    frames, keep = [], []
+    for i, (W, H, cl) in enumerate(GPU_SIZES):
+        for nd in (0, 1):
+            rng = np.random.default_rng(31 * i + depth + nd)
+            rec = F.frame_planes(W, H, depth, rng)
+            fenc = F.frame_planes(W, H, depth, rng)
+            s_ref, c_ref = O.sao_stats(W, H, cl, fenc, rec, F.MARGIN, nd)
+            dr, df = _dev(rec), _dev(fenc)
+            st = torch.full(s_ref.shape, -7, dtype=torch.int32, device="cuda")
+            ct = torch.full(c_ref.shape, -7, dtype=torch.int32, device="cuda")
+            fr = SaoStatsFrame()
+            fr.width, fr.height, fr.ctu_log2, fr.non_deblocked = W, H, cl, nd
+            for p in range(3):
+                fr.fenc[p], fr.rec[p] = _org(df[p]), _org(dr[p])
+            fr.fenc_stride, fr.fenc_cstride = df[0].shape[1], df[1].shape[1]
+            fr.rec_stride, fr.rec_cstride = dr[0].shape[1], dr[1].shape[1]
+            fr.stats, fr.count = st.data_ptr(), ct.data_ptr()
+            frames.append(fr)
+            keep.append((dr, df, st, ct, s_ref, c_ref))
+    gpu_prims.sao_stats(depth, frames)
+    torch.cuda.synchronize()
+    for (_, _, st, ct, s_ref, c_ref) in keep:
+        np.testing.assert_array_equal(ct.cpu().numpy(), c_ref)
+        np.testing.assert_array_equal(st.cpu().numpy(), s_ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("depth", DEPTHS)
+def test_gpu_extend_border(gpu_prims, depth):
+    import torch
+    from src.x265_amd.native import BorderPlane
+
+    O = po.FrameFilters("oracle", depth)
+    dt = np.uint8 if depth == 8 else np.uint16
+    planes, keep = [], []
+    # recon PicYuv geometry (picyuv.cpp:62-80) at CTU 64: luma 96 / 80, chroma 96 / 40
+    for i, (W, H, mx, my) in enumerate([(1920, 1080, 96, 80), (960, 540, 96, 40), (200, 136, 96, 80),
+                                        (100, 68, 96, 40), (64, 8, 3, 5)]):
+        rng = np.random.default_rng(i + depth)
+        stride = ((W + 63) // 64) * 64 + 2 * mx
+        p = rng.integers(0, 1 << depth, size=(H + 2 * my, stride)).astype(dt)
+        ref = p.copy()
+        O.extend_border(ref, mx, my, W, H)
+        d = torch.from_numpy(p.view(np.int16) if dt == np.uint16 else p).cuda()
+        bp = BorderPlane()
+        bp.plane = d.data_ptr() + (my * stride + mx) * d.element_size()
+        bp.stride, bp.width, bp.height, bp.margin_x, bp.margin_y = stride, W, H, mx, my
+        planes.append(bp)
+        keep.append((d, ref))
+    gpu_prims.extend_border(depth, planes)
+    torch.cuda.synchronize()
+    for d, ref in keep:
+        np.testing.assert_array_equal(_host(d, dt), ref)

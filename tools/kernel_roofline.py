@@ -500,6 +500,113 @@ def main():
             r["cpu_reference_error"] = str(ex)
         results.append(r)
         print(json.dumps(r), flush=True)
+    # ---------------------------------------------------------------- f4 loop filters
+    # Whole frames, >= --gb of distinct frame buffers per call (8 frames per launch).  Algorithmic
+    # bytes per frame: deblock = the picture read once and written once + its 16-byte CU units
+    # (a fused one-pass lower bound; the kernel makes two passes, V then H); sao_apply = the
+    # deblocked picture read + the output written; sao_stats = source + deblocked pictures read;
+    # extend_border = the margin area written.  CPU: the reference's own Deblock / SAO / extendPicBorder
+    # (oracle/_ref via ref_shim, one core, frame setup included).
+    for Hf in (1080, 2160):
+        if not want(f"f4_{Hf}p"):
+            continue
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import f4cases as F4
+        from src.x265_amd.native import BorderPlane, DeblockFrame, SaoFrame, SaoStatsFrame
+        import pyoracle as po4
+        Wf = 3840 if Hf == 2160 else 1920
+        M = F4.MARGIN
+        rng = np.random.default_rng(Hf)
+        pl = F4.frame_planes(Wf, Hf, 8, rng)
+        U = F4.deblock_units(Wf, Hf, 6, 8, rng, "B")
+        dp = F4.deblock_params(rng, "B", 0)
+        prm = F4.sao_params(Wf, Hf, 6, 8, rng)
+        fbytes = Wf * Hf * 3 // 2
+        nfr = max(8, int(a.gb * 1e9 / (2 * sum(p.nbytes for p in pl) + U.nbytes)))
+        nfr = (nfr + 7) // 8 * 8
+        src = [torch.from_numpy(p).cuda().unsqueeze(0).repeat(nfr, 1, 1).contiguous() for p in pl]
+        dst = [torch.empty_like(s) for s in src]
+        du = torch.from_numpy(U.view(np.uint8).reshape(U.shape[0], -1)).cuda().unsqueeze(0).repeat(nfr, 1, 1).contiguous()
+        dprm = torch.from_numpy(prm.view(np.uint8)).cuda()
+
+        def org(t, i):
+            return t[i].data_ptr() + (M * t.shape[2] + M) * t.element_size()
+
+        dbk, sao, sst, bor = [], [], [], []
+        nctu = ((Wf + 63) // 64) * ((Hf + 63) // 64)
+        stats = torch.empty(nfr * nctu * 3 * 5 * 33, dtype=torch.int32, device=dev)
+        count = torch.empty_like(stats)
+        for i in range(nfr):
+            fr = DeblockFrame()
+            fr.width, fr.height = Wf, Hf
+            for p in range(3):
+                fr.plane[p] = org(dst[p], i)
+            fr.stride, fr.cstride = src[0].shape[2], src[1].shape[2]
+            fr.units, fr.unit_stride = du[i].data_ptr(), U.shape[1]
+            fr.is_p, fr.beta_offset_div2, fr.tc_offset_div2 = 0, dp.beta_offset_div2, dp.tc_offset_div2
+            fr.cb_qp_offset, fr.cr_qp_offset = dp.cb_qp_offset, dp.cr_qp_offset
+            for lst in range(2):
+                for k in range(16):
+                    fr.ref_poc[lst][k] = dp.ref_poc[lst][k]
+            dbk.append(fr)
+            sf = SaoFrame()
+            sf.width, sf.height, sf.ctu_log2, sf.luma_on, sf.chroma_on = Wf, Hf, 6, 1, 1
+            for p in range(3):
+                sf.src[p], sf.dst[p] = org(src[p], i), org(dst[p], i)
+            sf.stride, sf.cstride, sf.params = src[0].shape[2], src[1].shape[2], dprm.data_ptr()
+            sao.append(sf)
+            tf = SaoStatsFrame()
+            tf.width, tf.height, tf.ctu_log2, tf.non_deblocked = Wf, Hf, 6, 0
+            for p in range(3):
+                tf.fenc[p], tf.rec[p] = org(src[p], i), org(dst[p], i)
+            tf.fenc_stride, tf.fenc_cstride, tf.rec_stride, tf.rec_cstride = (src[0].shape[2], src[1].shape[2],
+                                                                              src[0].shape[2], src[1].shape[2])
+            tf.stats = stats.data_ptr() + i * nctu * 3 * 5 * 33 * 4
+            tf.count = count.data_ptr() + i * nctu * 3 * 5 * 33 * 4
+            sst.append(tf)
+            for p in range(3):
+                bp = BorderPlane()
+                bp.plane = org(dst[p], i) + 0
+                w_, h_ = (Wf, Hf) if p == 0 else (Wf // 2, Hf // 2)
+                bp.stride, bp.width, bp.height, bp.margin_x, bp.margin_y = src[p].shape[2], w_, h_, M, M
+                bor.append(bp)
+        for d_, s_ in zip(dst, src):
+            d_.copy_(s_)
+        ms_d = timeit(lambda: prims.deblock(8, dbk))
+        ms_a = timeit(lambda: prims.sao_apply(8, sao))
+        ms_s = timeit(lambda: prims.sao_stats(8, sst))
+        ms_b = timeit(lambda: prims.extend_border(8, bor))
+        border_bytes = sum((s.shape[2] * s.shape[1] - (w_ * h_)) for s, (w_, h_) in
+                           zip(src, ((Wf, Hf), (Wf // 2, Hf // 2), (Wf // 2, Hf // 2))))
+        cpu = {}
+        try:
+            if po4.available("ref", 8):
+                import time as _t
+                R = po4.FrameFilters("ref", 8)
+                reps = 2 if Hf == 1080 else 1
+                for nm, fn in (("deblock", lambda q: R.deblock(Wf, Hf, 6, q, M, U, dp)),
+                               ("sao_apply", lambda q: R.sao_apply(Wf, Hf, 6, q, M, prm)),
+                               ("sao_stats", lambda q: R.sao_stats(Wf, Hf, 6, pl, q, M, 0))):
+                    q = F4.copy_planes(pl)
+                    t0 = _t.perf_counter()
+                    for _ in range(reps):
+                        fn(q)
+                    cpu[nm] = round(reps / (_t.perf_counter() - t0), 2)
+        except Exception as ex:
+            cpu["error"] = str(ex)
+        for nm, ms, nbytes in (("deblock", ms_d, nfr * (2 * fbytes + U.nbytes)), ("sao_apply", ms_a, nfr * 2 * fbytes),
+                               ("sao_stats", ms_s, nfr * 2 * fbytes), ("extend_border", ms_b, nfr * border_bytes)):
+            gbs = nbytes / (ms * 1e-3) / 1e9
+            r = {"kernel": f"f4_{nm}_{Hf}p_x{nfr}", "jobs": nfr, "bytes_per_launch": int(nbytes), "ms": round(ms, 4),
+                 "frames_per_s": round(nfr / (ms * 1e-3), 1), "achieved_GBps": round(gbs, 1),
+                 "frac_of_8TBps": round(gbs / HBM, 3)}
+            if nm in cpu:
+                r["cpu_reference_1core_frames_per_s"] = cpu[nm]
+            results.append(r)
+            print(json.dumps(r), flush=True)
+        del src, dst, du, stats, count
+        torch.cuda.empty_cache()
     if a.out:
         with open(a.out, "w") as f:
             json.dump({"hbm_peak_GBps": HBM, "working_set_GB": a.gb, "results": results}, f, indent=1)
