@@ -11,12 +11,12 @@
 //                          derives the edge mark and bS from the two 16-byte CU units on either
 //                          side, loads its 4 x 8 pixel window, filters in registers and stores
 //                          the window back (windows tile the plane, so lanes never overlap).
-//   x265amd_sao_apply      SAO::processSaoCu (sao.cpp:278-597): one lane per 8-pixel row segment
-//                          of a plane; neighbours come from the deblocked source buffer and the
+//   x265amd_sao_apply      SAO::processSaoCu (sao.cpp:278-597): one wavefront per plane CTU, one
+//                          lane per 8-pixel wide strip of it; neighbours come from the deblocked source buffer and the
 //                          result goes to a second buffer, which is what the reference's
 //                          m_tmpU / m_tmpL copies emulate in place.
-//   x265amd_sao_stats      SAO::calcSaoStatsCu (sao.cpp:772-943): one workgroup per CTU, all
-//                          three planes; per pixel the five SAO types' classes; edge-offset
+//   x265amd_sao_stats      SAO::calcSaoStatsCu (sao.cpp:772-943): one wavefront per CTU, one lane
+//                          per 8x8 strip; per pixel the five SAO types' classes; edge-offset
 //                          classes accumulate in registers and reduce across the wavefront,
 //                          band classes go to LDS as packed (count << 40) + sum 64-bit adds.
 //   x265amd_extend_border  extendPicBorder (pixel.cpp:908-922): side margins, then full-stride
@@ -43,19 +43,23 @@ __constant__ uint8_t c_chroma_scale[70] = { 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11
                                             35, 35, 36, 36, 37, 37, 38, 39, 40, 41, 42, 43, 44, 45, 46, 47, 48, 49,
                                             50, 51, 51, 51, 51, 51, 51, 51, 51, 51, 51, 51, 51, 51 };
 
-constexpr int kMaxFrames = 8;   // frame descriptors per launch (they travel in the kernarg segment)
+// frame descriptors per launch: they travel in the kernarg segment (<= 4 KiB), so a launch covers
+// as many frames as fit and a call of many frames costs few launches
+constexpr int kMaxFrames = 32;
+constexpr int kDbkFrames = 16;
+constexpr int kStatFrames = 24;
 
 __device__ __forceinline__ int clip3(int lo, int hi, int v) { return v < lo ? lo : (v > hi ? hi : v); }
 __device__ __forceinline__ int sgn(int v) { return (v > 0) - (v < 0); }
 __device__ __forceinline__ int iabs(int v) { return v < 0 ? -v : v; }
 
 // which frame of the launch a logical block belongs to (uniform scan, as group_sub)
-template <typename L>
+template <int N, typename L>
 __device__ __forceinline__ int frame_of(const L& l, uint32_t b)
 {
     int f = 0;
 #pragma unroll
-    for (int i = 1; i < kMaxFrames; i++)
+    for (int i = 1; i < N; i++)
         if (i < l.count && l.f[i].block0 <= b) f = i;
     return f;
 }
@@ -74,7 +78,7 @@ struct DbkFrame
 };
 struct DbkLaunch
 {
-    DbkFrame f[kMaxFrames];
+    DbkFrame f[kDbkFrames];
     int count, maxv;
 };
 
@@ -244,7 +248,7 @@ template <typename P, int DIR>
 __global__ __launch_bounds__(X265AMD_BLOCK) void k_deblock(const DbkLaunch L)
 {
     const uint32_t b = xcd_block();
-    const DbkFrame& f = L.f[frame_of(L, b)];
+    const DbkFrame& f = L.f[frame_of<kDbkFrames>(L, b)];
     const uint32_t s = (b - f.block0) * X265AMD_BLOCK + threadIdx.x;
     if (s >= f.nseg) return;
     const bool luma = s < f.nluma;
@@ -334,6 +338,28 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_deblock(const DbkLaunch L)
     }
 }
 
+// o[i] = p[i - 1], i = 0..9: a row segment with its left / right neighbour in one (8-bit) or
+// two (16-bit) 16-byte loads; planes are readable 16 pixels around the picture
+template <typename P>
+__device__ __forceinline__ void load_row10(const P* p, int (&o)[10])
+{
+    if constexpr (sizeof(P) == 1)
+    {
+        const uint4 v = ldu<uint4>(p - 4);
+        const uint32_t w[4] = { v.x, v.y, v.z, v.w };
+#pragma unroll
+        for (int i = 0; i < 10; i++) o[i] = (int)((w[(i + 3) >> 2] >> (8 * ((i + 3) & 3))) & 0xff);
+    }
+    else
+    {
+        const uint4 a = ldu<uint4>(p - 2), b = ldu<uint4>(p + 6);
+        const uint32_t w[8] = { a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w };
+#pragma unroll
+        for (int i = 0; i < 10; i++)   // element i + 1 of the window p - 2 .. p + 13
+            o[i] = (int)((w[(i + 1) >> 1] >> (16 * ((i + 1) & 1))) & 0xffff);
+    }
+}
+
 // ================================================================ SAO apply
 struct SaoFrame
 {
@@ -342,7 +368,7 @@ struct SaoFrame
     int64_t stride, cstride;
     const x265amd_sao_param* params;
     int w, h, ctu_log2, wc, nctu, luma_on, chroma_on;
-    uint32_t block0, nseg, nluma, nchroma;   // segments: all, luma, per chroma plane
+    uint32_t block0;                         // first block (one per plane and CTU)
 };
 struct SaoLaunch
 {
@@ -350,90 +376,90 @@ struct SaoLaunch
     int count, maxv, bo_shift;
 };
 
+// One wavefront per (plane, CTU), so the SAO type is uniform across it: lane = an 8-pixel wide
+// strip of sh rows (sh = 8 for 64x64, 2 for 32x32, 1 below); the row above, the current row and
+// the row below slide down the strip, one new 16-byte load per output row.
 template <typename P>
-__global__ __launch_bounds__(X265AMD_BLOCK) void k_sao_apply(const SaoLaunch L)
+__global__ __launch_bounds__(64) void k_sao_apply(const SaoLaunch L)
 {
     const uint32_t b = xcd_block();
-    const SaoFrame& f = L.f[frame_of(L, b)];
-    const uint32_t s = (b - f.block0) * X265AMD_BLOCK + threadIdx.x;
-    if (s >= f.nseg) return;
-    int p;
-    uint32_t r;
-    if (s < f.nluma) { p = 0; r = s; }
-    else { r = s - f.nluma; p = 1 + (r >= f.nchroma); r -= p == 2 ? f.nchroma : 0; }
+    const SaoFrame& f = L.f[frame_of<kMaxFrames>(L, b)];
+    const uint32_t u = b - f.block0;                 // plane-major: [3][nctu]
+    const int p = (int)(u / f.nctu), c = (int)(u % f.nctu);
+    const int lane = threadIdx.x;
     const int pw = p ? f.w >> 1 : f.w, ph = p ? f.h >> 1 : f.h;
-    const int segs = (pw + 7) >> 3;
-    const int y = (int)(r / segs), x0 = 8 * (int)(r % segs);
-    const int n = pw - x0 < 8 ? pw - x0 : 8;         // 8, or 4 at a right edge of width 8k + 4
+    const int cl = f.ctu_log2 - (p ? 1 : 0), cs = 1 << cl;
+    const int nsx = cs >> 3, sh = cs * cs >= 512 ? (cs * cs) >> 9 : 1;
+    const int cx0 = (c % f.wc) * cs, cy0 = (c / f.wc) * cs;
+    const int x0 = cx0 + 8 * (lane % nsx), y0 = cy0 + sh * (lane / nsx);
+    const int yend = min(min(y0 + sh, cy0 + cs), ph);
+    if (x0 >= pw || y0 >= yend) return;
+    const bool full = pw - x0 >= 8;                  // else 4 pixels (a right edge of width 8k + 4)
     const int64_t st = p ? f.cstride : f.stride;
-    const P* src = (const P*)f.src[p] + y * st + x0;
-    P* dst = (P*)f.dst[p] + y * st + x0;
-    const int cl = f.ctu_log2 - (p ? 1 : 0);
-    const int c = (y >> cl) * f.wc + (x0 >> cl);
+    const P* src = (const P*)f.src[p] + y0 * st + x0;
+    P* dst = (P*)f.dst[p] + y0 * st + x0;
     const x265amd_sao_param* prm = f.params + p * f.nctu + c;
     int type = (int)prm->type;
     if (p == 2 && type >= 0) type = (int)f.params[f.nctu + c].type;   // processSaoCu(addr, typeIdxCb, 2)
     if (!(p ? f.chroma_on : f.luma_on)) type = -1;
-    int v[8];
-    load_row<P, 8>(src, v);
-    int o[8];
-    if (type == 4)
-    {
-        // m_offsetBo: offset[i] at band (bandPos + i) & 31 (sao.cpp:637-640)
-        const int band = prm->band;
-        const int o0 = prm->offset[0], o1 = prm->offset[1], o2 = prm->offset[2], o3 = prm->offset[3];
+    const int band = prm->band;
+    const int o0 = prm->offset[0], o1 = prm->offset[1], o2 = prm->offset[2], o3 = prm->offset[3];
+    // EO neighbour directions (sao.cpp:321-560): EO_0 -, EO_1 |, EO_2 135 deg, EO_3 45 deg
+    const int dxa = type == 1 ? 0 : (type == 3 ? 1 : -1), dxb = -dxa;   // above / below
+    int up[10], mid[10], dn[10];
+    load_row10<P>(src - st, up);
+    load_row10<P>(src, mid);
 #pragma unroll
-        for (int i = 0; i < 8; i++)
+    for (int yy = 0; yy < 8; yy++)
+    {
+        const int y = y0 + yy;
+        if (y >= yend) break;
+        load_row10<P>(src + (yy + 1) * st, dn);
+        int o[8];
+        if (type == 4)
         {
-            const int k = ((v[i] >> L.bo_shift) - band) & 31;
-            const int off = k == 0 ? o0 : k == 1 ? o1 : k == 2 ? o2 : k == 3 ? o3 : 0;
-            o[i] = clip3(0, L.maxv, v[i] + off);
+            // m_offsetBo: offset[i] at band (bandPos + i) & 31 (sao.cpp:637-640)
+#pragma unroll
+            for (int i = 0; i < 8; i++)
+            {
+                const int v = mid[i + 1];
+                const int k = ((v >> L.bo_shift) - band) & 31;
+                const int off = k == 0 ? o0 : k == 1 ? o1 : k == 2 ? o2 : k == 3 ? o3 : 0;
+                o[i] = clip3(0, L.maxv, v + off);
+            }
         }
-    }
-    else if (type >= 0)
-    {
-        // m_offsetEo via s_eoTable (sao.cpp:65-72, 644-650): edge type 0, 1, 3, 4 -> offset[0..3], 2 -> 0
-        const int e0 = prm->offset[0], e1 = prm->offset[1], e3 = prm->offset[2], e4 = prm->offset[3];
-        const int dy0 = type == 0 ? 0 : -1, dy1 = -dy0;
-        const int dx0 = type == 1 ? 0 : (type == 3 ? 1 : -1), dx1 = -dx0;
-        int a[10], bb[10];
+        else if (type >= 0)
         {
-            const P* r0 = src + dy0 * st;
-            const P* r1 = src + dy1 * st;
-            int t[8];
-            load_row<P, 8>(r0, t);
+            // m_offsetEo via s_eoTable (sao.cpp:65-72, 644-650): edge type 0, 1, 3, 4 -> offset[0..3], 2 -> 0;
+            // EO leaves the picture's outermost column (not EO_1) / row (not EO_0) untouched
+            const bool skip_row = type != 0 && (y == 0 || y == ph - 1);
 #pragma unroll
-            for (int i = 0; i < 8; i++) a[i + 1] = t[i];
-            a[0] = r0[-1]; a[9] = r0[8];
-            load_row<P, 8>(r1, t);
-#pragma unroll
-            for (int i = 0; i < 8; i++) bb[i + 1] = t[i];
-            bb[0] = r1[-1]; bb[9] = r1[8];
+            for (int i = 0; i < 8; i++)
+            {
+                const int v = mid[i + 1];
+                const int na = type == 0 ? mid[i] : (dxa < 0 ? up[i] : (dxa > 0 ? up[i + 2] : up[i + 1]));
+                const int nb = type == 0 ? mid[i + 2] : (dxb < 0 ? dn[i] : (dxb > 0 ? dn[i + 2] : dn[i + 1]));
+                const int e = sgn(v - na) + sgn(v - nb) + 2;
+                const int off = e == 0 ? o0 : e == 1 ? o1 : e == 3 ? o2 : e == 4 ? o3 : 0;
+                const int x = x0 + i;
+                const bool skip = skip_row || (type != 1 && (x == 0 || x == pw - 1));
+                o[i] = skip ? v : clip3(0, L.maxv, v + off);
+            }
         }
-        // EO leaves the picture's outermost column (not EO_1) / row (not EO_0) untouched
-        const bool skip_row = type != 0 && (y == 0 || y == ph - 1);
-#pragma unroll
-        for (int i = 0; i < 8; i++)
+        else
         {
-            const int x = x0 + i;
-            const int na = dx0 == -1 ? a[i] : (dx0 == 1 ? a[i + 2] : a[i + 1]);
-            const int nb = dx1 == -1 ? bb[i] : (dx1 == 1 ? bb[i + 2] : bb[i + 1]);
-            const int e = sgn(v[i] - na) + sgn(v[i] - nb) + 2;
-            const int off = e == 0 ? e0 : e == 1 ? e1 : e == 3 ? e3 : e == 4 ? e4 : 0;
-            const bool skip = skip_row || (type != 1 && (x == 0 || x == pw - 1));
-            o[i] = skip ? v[i] : clip3(0, L.maxv, v[i] + off);
-        }
-    }
-    else
-    {
 #pragma unroll
-        for (int i = 0; i < 8; i++) o[i] = v[i];
-    }
-    if (n == 8) store_row<P, 8>(dst, o);
-    else
-    {
-        const int o4[4] = { o[0], o[1], o[2], o[3] };
-        store_row<P, 4>(dst, o4);
+            for (int i = 0; i < 8; i++) o[i] = mid[i + 1];
+        }
+        P* d = dst + yy * st;
+        if (full) store_row<P, 8>(d, o);
+        else
+        {
+            const int o4[4] = { o[0], o[1], o[2], o[3] };
+            store_row<P, 4>(d, o4);
+        }
+#pragma unroll
+        for (int i = 0; i < 10; i++) { up[i] = mid[i]; mid[i] = dn[i]; }
     }
 }
 
@@ -450,29 +476,32 @@ struct StatFrame
 };
 struct StatLaunch
 {
-    StatFrame f[kMaxFrames];
+    StatFrame f[kStatFrames];
     int count, bo_shift;
 };
 
+// One wavefront per CTU.  Pass 0: luma, lane = 8x8 strip of the CTU (<= 64 strips); pass 1: Cb on
+// lanes 0-31, Cr on lanes 32-63 (<= 16 strips each).  A lane walks its strip row by row (one new
+// 16-byte load per row) and keeps, per EO type and edge class, (sum << 7) + count in one int32
+// (<= 64 pixels of <= 12 bits: no overflow); band classes merge runs of equal band and add them to
+// LDS as (count << 40) + sum.  The lanes' totals then reduce across the wave (or half-wave).
 template <typename P>
-__global__ __launch_bounds__(X265AMD_BLOCK) void k_sao_stats(const StatLaunch L)
+__global__ __launch_bounds__(64) void k_sao_stats(const StatLaunch L)
 {
     __shared__ int32_t eo_sum[3][4][5], eo_cnt[3][4][5];
     __shared__ unsigned long long bo[3][32];
     const uint32_t b = xcd_block();
-    const StatFrame& f = L.f[frame_of(L, b)];
+    const StatFrame& f = L.f[frame_of<kStatFrames>(L, b)];
     const uint32_t c = b - f.block0;
-    const int tid = threadIdx.x;
-    for (int i = tid; i < 3 * 4 * 5; i += X265AMD_BLOCK)
-    {
-        (&eo_sum[0][0][0])[i] = 0;
-        (&eo_cnt[0][0][0])[i] = 0;
-    }
-    for (int i = tid; i < 3 * 32; i += X265AMD_BLOCK) (&bo[0][0])[i] = 0;
+    const int lane = threadIdx.x;
+    for (int i = lane; i < 3 * 32; i += 64) (&bo[0][0])[i] = 0;
     __syncthreads();
     const int cxi = (int)(c % f.wc), cyi = (int)(c / f.wc);
-    for (int p = 0; p < 3; p++)
+#pragma unroll 1
+    for (int pass = 0; pass < 2; pass++)
     {
+        const int p = pass ? 1 + (lane >> 5) : 0;
+        const int sl = pass ? lane & 31 : lane;
         const int pw = p ? f.w >> 1 : f.w, ph = p ? f.h >> 1 : f.h;
         const int cs = (1 << f.ctu_log2) >> (p ? 1 : 0);
         const int x0 = cxi * cs, y0 = cyi * cs;
@@ -493,81 +522,97 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_sao_stats(const StatLaunch L)
             ys[t] = eoy ? (y0 == 0) : 0;
             ye[t] = t == 0 ? ch - sb + po : (bottom ? (eoy ? ch - 1 : ch) : ch - sb + po);
         }
-        const int64_t rs = p ? f.rcs : f.rs, fs = p ? f.fcs : f.fs;
-        const P* rec = (const P*)f.rec[p] + (int64_t)y0 * rs + x0;
-        const P* fen = (const P*)f.fenc[p] + (int64_t)y0 * fs + x0;
-        const int segs = (cw + 7) >> 3, nseg = segs * ch;
-        const int nround = (nseg + 63) & ~63;                 // whole wavefronts per plane
-        int acc_s[4][5], acc_c[4][5];
+        const int nsx = (cw + 7) >> 3, nsy = (ch + 7) >> 3;
+        int acc[4][5];
 #pragma unroll
         for (int t = 0; t < 4; t++)
 #pragma unroll
-            for (int k = 0; k < 5; k++) acc_s[t][k] = acc_c[t][k] = 0;
-        for (int sg = tid; sg < nround; sg += X265AMD_BLOCK)
+            for (int k = 0; k < 5; k++) acc[t][k] = 0;
+        if (sl < nsx * nsy)
         {
-            if (sg < nseg)
+            const int lx0 = 8 * (sl % nsx), ly0 = 8 * (sl / nsx);
+            const int rows = ch - ly0 < 8 ? ch - ly0 : 8;
+            uint32_t xm[5];
+#pragma unroll
+            for (int t = 0; t < 5; t++)
             {
-                const int ly = sg / segs, lx0 = 8 * (sg % segs);
-                const P* r1 = rec + (int64_t)ly * rs + lx0;
-                int up[10], mid[10], dn[10], fe[8];
-                {
-                    int t[8];
-                    load_row<P, 8>(r1 - rs, t);
+                const int lo = clip3(0, 8, xs[t] - lx0), hi = clip3(0, 8, xe[t] - lx0);
+                xm[t] = hi > lo ? ((1u << hi) - 1) & ~((1u << lo) - 1) : 0u;
+            }
+            const int64_t rs = p ? f.rcs : f.rs, fs = p ? f.fcs : f.fs;
+            const P* r = (const P*)f.rec[p] + (int64_t)(y0 + ly0) * rs + x0 + lx0;
+            const P* fe = (const P*)f.fenc[p] + (int64_t)(y0 + ly0) * fs + x0 + lx0;
+            int up[10], mid[10], dn[10];
+            load_row10<P>(r - rs, up);
+            load_row10<P>(r, mid);
 #pragma unroll
-                    for (int i = 0; i < 8; i++) up[i + 1] = t[i];
-                    load_row<P, 8>(r1, t);
+            for (int yy = 0; yy < 8; yy++)
+            {
+                if (yy >= rows) break;
+                load_row10<P>(r + (yy + 1) * rs, dn);
+                int fv[8];
+                load_row<P, 8>(fe + yy * fs, fv);
+                const int ly = ly0 + yy;
+                uint32_t m[5];
 #pragma unroll
-                    for (int i = 0; i < 8; i++) mid[i + 1] = t[i];
-                    load_row<P, 8>(r1 + rs, t);
-#pragma unroll
-                    for (int i = 0; i < 8; i++) dn[i + 1] = t[i];
-                    up[0] = r1[-rs - 1]; up[9] = r1[-rs + 8];
-                    mid[0] = r1[-1]; mid[9] = r1[8];
-                    dn[0] = r1[rs - 1]; dn[9] = r1[rs + 8];
-                    load_row<P, 8>(fen + (int64_t)ly * fs + lx0, fe);
-                }
+                for (int t = 0; t < 5; t++) m[t] = (ly >= ys[t] && ly < ye[t]) ? xm[t] : 0u;
+                int run_band = -1;
+                unsigned long long run = 0;
 #pragma unroll
                 for (int i = 0; i < 8; i++)
                 {
-                    const int lx = lx0 + i;
-                    const int v = mid[i + 1], d = fe[i] - v;
+                    const int v = mid[i + 1], d = fv[i] - v;
+                    const int val = (d << 7) + 1;
                     const int e[4] = { sgn(v - mid[i]) + sgn(v - mid[i + 2]), sgn(v - up[i + 1]) + sgn(v - dn[i + 1]),
                                        sgn(v - up[i]) + sgn(v - dn[i + 2]), sgn(v - up[i + 2]) + sgn(v - dn[i]) };
 #pragma unroll
                     for (int t = 0; t < 4; t++)
                     {
-                        const bool in = lx >= xs[t] && lx < xe[t] && ly >= ys[t] && ly < ye[t];
-                        const int k = e[t] == 0 ? 0 : (e[t] < 0 ? e[t] + 3 : e[t] + 2);   // s_eoTable[e + 2]
-#pragma unroll
-                        for (int kk = 0; kk < 5; kk++)
-                        {
-                            const bool hit = in && k == kk;
-                            acc_s[t][kk] += hit ? d : 0;
-                            acc_c[t][kk] += hit ? 1 : 0;
-                        }
+                        const int vin = (m[t] >> i) & 1 ? val : 0;
+                        acc[t][0] += e[t] == -2 ? vin : 0;
+                        acc[t][1] += e[t] == -1 ? vin : 0;
+                        acc[t][2] += e[t] == 0 ? vin : 0;
+                        acc[t][3] += e[t] == 1 ? vin : 0;
+                        acc[t][4] += e[t] == 2 ? vin : 0;
                     }
-                    if (lx >= xs[4] && lx < xe[4] && ly >= ys[4] && ly < ye[4])
-                        atomicAdd(&bo[p][v >> L.bo_shift], (1ull << 40) + (unsigned long long)(int64_t)d);
+                    if ((m[4] >> i) & 1)
+                    {
+                        const int band = v >> L.bo_shift;
+                        if (band != run_band)
+                        {
+                            if (run_band >= 0) atomicAdd(&bo[p][run_band], run);
+                            run_band = band;
+                            run = 0;
+                        }
+                        run += (1ull << 40) + (unsigned long long)(int64_t)d;
+                    }
                 }
+                if (run_band >= 0) atomicAdd(&bo[p][run_band], run);
+#pragma unroll
+                for (int i = 0; i < 10; i++) { up[i] = mid[i]; mid[i] = dn[i]; }
             }
         }
-        // wavefront reduction of the edge classes, one LDS add per wave
+        // wave (pass 0) / half-wave (pass 1) totals; edge type j = e + 2 -> class s_eoTable[j]
+        // (sao.cpp:65-72): 1, 2, 0, 3, 4
 #pragma unroll
         for (int t = 0; t < 4; t++)
 #pragma unroll
-            for (int k = 0; k < 5; k++)
+            for (int j = 0; j < 5; j++)
             {
-                int vs = acc_s[t][k], vc = acc_c[t][k];
+                const int cn = acc[t][j] & 127;
+                int vs = (acc[t][j] - cn) >> 7, vc = cn;
 #pragma unroll
-                for (int m = 32; m > 0; m >>= 1)
+                for (int mm = 1; mm < 64; mm <<= 1)
                 {
-                    vs += __shfl_xor(vs, m, 64);
-                    vc += __shfl_xor(vc, m, 64);
+                    if (pass && mm == 32) break;
+                    vs += __shfl_xor(vs, mm, 64);
+                    vc += __shfl_xor(vc, mm, 64);
                 }
-                if ((tid & 63) == 0 && vc)
+                const int k = j == 0 ? 1 : j == 1 ? 2 : j == 2 ? 0 : j;
+                if ((lane & 31) == 0 && (pass || lane == 0))
                 {
-                    atomicAdd(&eo_sum[p][t][k], vs);
-                    atomicAdd(&eo_cnt[p][t][k], vc);
+                    eo_sum[p][t][k] = vs;
+                    eo_cnt[p][t][k] = vc;
                 }
             }
     }
@@ -575,7 +620,7 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_sao_stats(const StatLaunch L)
     // every entry of the CTU's [3][5][33] block
     int32_t* os = f.stats + (int64_t)c * 3 * 5 * 33;
     int32_t* oc = f.count + (int64_t)c * 3 * 5 * 33;
-    for (int i = tid; i < 3 * 5 * 33; i += X265AMD_BLOCK)
+    for (int i = lane; i < 3 * 5 * 33; i += 64)
     {
         const int p = i / 165, t = (i % 165) / 33, k = i % 33;
         int sv = 0, cv = 0;
@@ -687,11 +732,11 @@ extern "C" int x265amd_deblock(int depth, int count, const x265amd_deblock_frame
     }
     hipStream_t st = (hipStream_t)stream;
     for (int dir = 0; dir < 2; dir++)
-        for (int i0 = 0; i0 < count; i0 += kMaxFrames)
+        for (int i0 = 0; i0 < count; i0 += kDbkFrames)
         {
             DbkLaunch L;
             memset(&L, 0, sizeof(L));
-            L.count = count - i0 < kMaxFrames ? count - i0 : kMaxFrames;
+            L.count = count - i0 < kDbkFrames ? count - i0 : kDbkFrames;
             L.maxv = (1 << depth) - 1;
             uint32_t blocks = 0;
             for (int k = 0; k < L.count; k++)
@@ -779,15 +824,12 @@ extern "C" int x265amd_sao_apply(int depth, int count, const x265amd_sao_frame* 
             f.nctu = f.wc * ((a.height + ctu - 1) >> a.ctu_log2);
             f.luma_on = a.luma_on;
             f.chroma_on = a.chroma_on;
-            f.nluma = (uint32_t)(((a.width + 7) >> 3) * a.height);
-            f.nchroma = (uint32_t)(((a.width / 2 + 7) >> 3) * (a.height / 2));
-            f.nseg = f.nluma + 2 * f.nchroma;
             f.block0 = blocks;
-            blocks += nblocks(f.nseg);
+            blocks += 3 * (uint32_t)f.nctu;
         }
         if (!blocks) continue;
-        if (depth == 8) hipLaunchKernelGGL((k_sao_apply<uint8_t>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, L);
-        else hipLaunchKernelGGL((k_sao_apply<uint16_t>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, L);
+        if (depth == 8) hipLaunchKernelGGL((k_sao_apply<uint8_t>), dim3(blocks), dim3(64), 0, st, L);
+        else hipLaunchKernelGGL((k_sao_apply<uint16_t>), dim3(blocks), dim3(64), 0, st, L);
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return (int)e;
     }
@@ -807,11 +849,11 @@ extern "C" int x265amd_sao_stats(int depth, int count, const x265amd_sao_stats_f
             if (!a.fenc[p] || !a.rec[p]) return X265AMD_EINVAL;
     }
     hipStream_t st = (hipStream_t)stream;
-    for (int i0 = 0; i0 < count; i0 += kMaxFrames)
+    for (int i0 = 0; i0 < count; i0 += kStatFrames)
     {
         StatLaunch L;
         memset(&L, 0, sizeof(L));
-        L.count = count - i0 < kMaxFrames ? count - i0 : kMaxFrames;
+        L.count = count - i0 < kStatFrames ? count - i0 : kStatFrames;
         L.bo_shift = depth - 5;
         uint32_t blocks = 0;
         for (int k = 0; k < L.count; k++)
@@ -835,8 +877,8 @@ extern "C" int x265amd_sao_stats(int depth, int count, const x265amd_sao_stats_f
             f.block0 = blocks;
             blocks += f.nctu;
         }
-        if (depth == 8) hipLaunchKernelGGL((k_sao_stats<uint8_t>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, L);
-        else hipLaunchKernelGGL((k_sao_stats<uint16_t>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, L);
+        if (depth == 8) hipLaunchKernelGGL((k_sao_stats<uint8_t>), dim3(blocks), dim3(64), 0, st, L);
+        else hipLaunchKernelGGL((k_sao_stats<uint16_t>), dim3(blocks), dim3(64), 0, st, L);
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return (int)e;
     }
@@ -890,3 +932,9 @@ extern "C" int x265amd_extend_border(int depth, int count, const x265amd_border_
     }
     return 0;
 }
+
+// the launch descriptors must fit the 4 KiB kernarg segment
+static_assert(sizeof(x265amd::DbkLaunch) <= 4096, "DbkLaunch exceeds the kernarg segment");
+static_assert(sizeof(x265amd::SaoLaunch) <= 4096, "SaoLaunch exceeds the kernarg segment");
+static_assert(sizeof(x265amd::StatLaunch) <= 4096, "StatLaunch exceeds the kernarg segment");
+static_assert(sizeof(x265amd::BorderLaunch) <= 4096, "BorderLaunch exceeds the kernarg segment");
