@@ -136,4 +136,87 @@ def caller_rates(prims, width: int, height: int, depth: int = 8, dev: str = "cud
     ms = _time(lambda: prims.tu_pipeline(8, 3, 1, 0, 0, 1, F1, st, off, F0, st, off, RES, st, off, CO, coff, REC, st,
                                          off, SIG, QP, None))
     out["tu_pipeline_8x8_tus_per_s"] = round(n / (ms * 1e-3), 1)
+    out.update(_loop_filter_rate(prims, frames[1:], width, height, dev))
     return out
+
+
+# x265amd_deblock_unit / x265amd_sao_param (include/x265_amd.h)
+_UNIT = np.dtype([("cu_log2", np.uint8), ("tu_log2", np.uint8), ("part", np.uint8), ("flags", np.uint8),
+                  ("qp", np.int8), ("ref_idx", np.int8, 2), ("pad", np.uint8), ("mv", np.int16, (2, 2))])
+_SAO = np.dtype([("type", np.int8), ("band", np.uint8), ("offset", np.int8, 4)])
+
+
+def _loop_filter_rate(prims, frames, width, height, dev):
+    """f4: deblock -> SAO statistics -> SAO apply -> border extension of 8 recon frames per call
+    (a synthetic CU layout: 16x16 CUs of 8x8 TUs, a quarter intra, P-slice MVs)."""
+    from .native import BorderPlane, DeblockFrame, SaoFrame, SaoStatsFrame
+
+    rng = np.random.default_rng(9)
+    hu, wu = height // 4, width // 4
+    U = np.zeros((hu, wu), _UNIT)
+    cu = rng.random((hu // 4 + 1, wu // 4 + 1)) < 0.25
+    U["cu_log2"], U["tu_log2"], U["qp"] = 4, 3, 32
+    U["flags"] = np.repeat(np.repeat(cu, 4, 0), 4, 1)[:hu, :wu].astype(np.uint8) | (rng.random((hu, wu)) < 0.5) * 2
+    U["ref_idx"][..., 0], U["ref_idx"][..., 1] = 0, -1
+    mv = np.repeat(np.repeat(rng.integers(-6, 7, (hu // 4 + 1, wu // 4 + 1, 2)), 4, 0), 4, 1)[:hu, :wu]
+    U["mv"][..., 0, :] = mv
+    ctu = 64
+    nctu = ((width + ctu - 1) // ctu) * ((height + ctu - 1) // ctu)
+    prm = np.zeros(3 * nctu, _SAO)
+    prm["type"] = rng.integers(-1, 5, 3 * nctu)
+    prm["type"][2 * nctu:] = prm["type"][nctu:2 * nctu]
+    prm["band"] = rng.integers(0, 32, 3 * nctu)
+    prm["offset"] = rng.integers(-3, 4, (3 * nctu, 4))
+    M = 16
+    planes, recs = [], []
+    for f in frames:
+        planes.append([_t(np.pad(p, M, mode="edge"), dev) for p in f[:3]])
+        recs.append([p.clone() for p in planes[-1]])
+    outs = [[torch.empty_like(p) for p in pl] for pl in planes]
+    du = _t(U.view(np.uint8).reshape(hu, -1), dev)
+    dprm = _t(prm.view(np.uint8), dev)
+    stats = torch.empty(len(frames) * nctu * 3 * 5 * 33, dtype=torch.int32, device=dev)
+    count = torch.empty_like(stats)
+
+    def org(t):
+        return t.data_ptr() + (M * t.shape[1] + M) * t.element_size()
+
+    dbk, sst, sao, bor = [], [], [], []
+    for i, (src, rec, dst) in enumerate(zip(planes, recs, outs)):
+        d = DeblockFrame()
+        d.width, d.height, d.is_p = width, height, 1
+        for p in range(3):
+            d.plane[p] = org(rec[p])
+        d.stride, d.cstride, d.units, d.unit_stride = rec[0].shape[1], rec[1].shape[1], du.data_ptr(), wu
+        d.ref_poc[0][0] = 0
+        dbk.append(d)
+        s = SaoStatsFrame()
+        s.width, s.height, s.ctu_log2 = width, height, 6
+        for p in range(3):
+            s.fenc[p], s.rec[p] = org(src[p]), org(rec[p])
+        s.fenc_stride, s.fenc_cstride, s.rec_stride, s.rec_cstride = (src[0].shape[1], src[1].shape[1],
+                                                                      rec[0].shape[1], rec[1].shape[1])
+        s.stats = stats.data_ptr() + i * nctu * 3 * 5 * 33 * 4
+        s.count = count.data_ptr() + i * nctu * 3 * 5 * 33 * 4
+        sst.append(s)
+        a = SaoFrame()
+        a.width, a.height, a.ctu_log2, a.luma_on, a.chroma_on = width, height, 6, 1, 1
+        for p in range(3):
+            a.src[p], a.dst[p] = org(rec[p]), org(dst[p])
+        a.stride, a.cstride, a.params = rec[0].shape[1], rec[1].shape[1], dprm.data_ptr()
+        sao.append(a)
+        for p in range(3):
+            b = BorderPlane()
+            b.plane, b.stride = org(dst[p]), dst[p].shape[1]
+            b.width, b.height = (width, height) if p == 0 else (width // 2, height // 2)
+            b.margin_x = b.margin_y = M
+            bor.append(b)
+
+    def chain():
+        prims.deblock(8, dbk)
+        prims.sao_stats(8, sst)
+        prims.sao_apply(8, sao)
+        prims.extend_border(8, bor)
+    ms = _time(chain)
+    return {"loop_filter_frames_per_s": round(len(frames) / (ms * 1e-3), 1),
+            "loop_filter_note": f"{len(frames)} frames per call: deblock, SAO statistics, SAO apply, border extension"}
