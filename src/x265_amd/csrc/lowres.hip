@@ -29,15 +29,6 @@
 
 namespace x265amd {
 
-// orders LDS writes of this wavefront before its later LDS reads (no s_barrier:
-// the pcost kernel is one wavefront per workgroup)
-__device__ __forceinline__ void wave_sync_lds()
-{
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
 struct LowresArgs
 {
     const void* src;
@@ -340,11 +331,15 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_lowres_intra(const LowresIntr
 // The neighbour dependency (right and the row below, CUs visited bottom-up and
 // right to left within each coop slice) makes a wavefront: with x' = W-1-cx and
 // y' = (slice's last row) - cy, CU (x', y') only needs CUs of steps before
-// x' + 2 y'.  One wavefront owns one (estimate, slice); lane l owns rows
-// y' = l, l + 64, ... and at step t searches CU x' = t - 2 y' of each.  The
-// motion search itself runs inside the lane, exactly in the reference's order,
-// on packed 8-bit (v_sad_u8) / 16-bit (v_sad_u16) rows; the four MVs a row
-// needs from the row below live in a 4-entry LDS ring per row.
+// x' + 2 y'.  One workgroup owns one (estimate, slice), with a 4-lane quad per
+// row of the slice (up to 16 wavefronts, a barrier per step); quad g owns rows
+// y' = g, g + nquads, ... and at step t searches CU x' = t - 2 y' of each.  The
+// motion search runs on the quad, exactly in the reference's order: each lane
+// scores its 4x4 quadrant of every candidate on packed 8-bit (v_sad_u8) /
+// 16-bit (v_sad_u16) rows and the quad sums by DPP, so a step's dependent
+// chain of candidate rounds costs a quarter of the instructions of a
+// lane-per-CU search; the four MVs a row needs from the row below live in a
+// 4-entry LDS ring per row.
 constexpr int kPcostMaxRows = 512;
 
 struct PcostArgs
@@ -365,27 +360,37 @@ struct PcostArgs
     int n, wcu, hcu, rps, nslices;
 };
 
-// an 8x8 block of pixels packed into dwords (2 per row at 8-bit, 4 at 16-bit)
+// A CU's search runs on a 4-lane group (a quad): lane q owns the 4x4 quadrant (x 4(q & 1),
+// y 4(q >> 1)) of the 8x8 block, evaluates its quadrant of every candidate (SAD on packed rows,
+// or one 4x4 Hadamard) and the quad sums by two DPP quad_perm adds, so every lane of the group
+// holds the same cost and takes the same decisions, in the reference's order.
 template <typename P>
-struct Blk8
+struct Quad
 {
-    static constexpr int W = 8 * (int)sizeof(P) / 4;
-    uint32_t r[8][W];
+    static constexpr int W = (int)sizeof(P);     // dwords per 4-pixel row
+    uint32_t r[4][W];
     __device__ __forceinline__ void load(const P* p, int64_t ls)
     {
 #pragma unroll
-        for (int y = 0; y < 8; y++)
+        for (int y = 0; y < 4; y++)
         {
-            if constexpr (W == 2) { const uint2 v = ldu<uint2>(p + y * ls); r[y][0] = v.x; r[y][1] = v.y; }
-            else { const uint4 v = ldu<uint4>(p + y * ls); r[y][0] = v.x; r[y][1] = v.y; r[y][2] = v.z; r[y][3] = v.w; }
+            if constexpr (W == 1) r[y][0] = ldu<uint32_t>(p + y * ls);
+            else { const uint2 v = ldu<uint2>(p + y * ls); r[y][0] = v.x; r[y][1] = v.y; }
         }
     }
     __device__ __forceinline__ int get(int y, int x) const
     {
-        if constexpr (W == 2) return (int)((r[y][x >> 2] >> (8 * (x & 3))) & 0xff);
+        if constexpr (W == 1) return (int)((r[y][0] >> (8 * x)) & 0xff);
         else return (int)((r[y][x >> 1] >> (16 * (x & 1))) & 0xffff);
     }
 };
+
+__device__ __forceinline__ int quad_sum(int v)
+{
+    v += __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false);   // quad_perm [1, 0, 3, 2]
+    v += __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, false);   // quad_perm [2, 3, 0, 1]
+    return v;
+}
 
 template <typename P>
 __device__ __forceinline__ uint32_t sad_packed(uint32_t a, uint32_t b, uint32_t acc)
@@ -394,62 +399,53 @@ __device__ __forceinline__ uint32_t sad_packed(uint32_t a, uint32_t b, uint32_t 
     else return __builtin_amdgcn_sad_u16(a, b, acc);
 }
 
-// SAD of the fenc block against 8 rows at p (fullpel or half-pel plane)
 template <typename P>
-__device__ __forceinline__ int sad8_mem(const Blk8<P>& fe, const P* p, int64_t ls)
+__device__ __forceinline__ int sad_quad(const Quad<P>& fe, const Quad<P>& b)
 {
-    Blk8<P> b;
+    uint32_t s = 0;
+#pragma unroll
+    for (int y = 0; y < 4; y++)
+#pragma unroll
+        for (int w = 0; w < Quad<P>::W; w++) s = sad_packed<P>(fe.r[y][w], b.r[y][w], s);
+    return quad_sum((int)s);
+}
+
+// SAD of the CU against the full-pel block at p (the lane's quadrant origin)
+template <typename P>
+__device__ __forceinline__ int sad8_mem(const Quad<P>& fe, const P* p, int64_t ls)
+{
+    Quad<P> b;
     b.load(p, ls);
-    uint32_t s = 0;
-#pragma unroll
-    for (int y = 0; y < 8; y++)
-#pragma unroll
-        for (int w = 0; w < Blk8<P>::W; w++) s = sad_packed<P>(fe.r[y][w], b.r[y][w], s);
-    return (int)s;
+    return sad_quad<P>(fe, b);
 }
 
+// satd 8x8 = (sum of the four raw 4x4 Hadamard sums) >> 1 (each raw sum is even, so this equals
+// satd8's per-8x4 halving, SURVEY note a7)
 template <typename P>
-__device__ __forceinline__ int sad8_blk(const Blk8<P>& fe, const Blk8<P>& b)
+__device__ __forceinline__ int satd_quad(const Quad<P>& fe, const Quad<P>& b)
 {
-    uint32_t s = 0;
+    int d[4][4];
 #pragma unroll
-    for (int y = 0; y < 8; y++)
+    for (int r = 0; r < 4; r++)
 #pragma unroll
-        for (int w = 0; w < Blk8<P>::W; w++) s = sad_packed<P>(fe.r[y][w], b.r[y][w], s);
-    return (int)s;
-}
-
-template <typename P>
-__device__ __forceinline__ int satd8_blk(const Blk8<P>& fe, const Blk8<P>& b)
-{
+        for (int c = 0; c < 4; c++) d[r][c] = fe.get(r, c) - b.get(r, c);
+#pragma unroll
+    for (int r = 0; r < 4; r++) had4(d[r][0], d[r][1], d[r][2], d[r][3]);
     int sum = 0;
 #pragma unroll
-    for (int qy = 0; qy < 8; qy += 4)
+    for (int c = 0; c < 4; c++)
+    {
+        had4(d[0][c], d[1][c], d[2][c], d[3][c]);
 #pragma unroll
-        for (int qx = 0; qx < 8; qx += 4)
-        {
-            int d[4][4];
-#pragma unroll
-            for (int r = 0; r < 4; r++)
-#pragma unroll
-                for (int c = 0; c < 4; c++) d[r][c] = fe.get(qy + r, qx + c) - b.get(qy + r, qx + c);
-#pragma unroll
-            for (int r = 0; r < 4; r++) had4(d[r][0], d[r][1], d[r][2], d[r][3]);
-#pragma unroll
-            for (int c = 0; c < 4; c++)
-            {
-                had4(d[0][c], d[1][c], d[2][c], d[3][c]);
-#pragma unroll
-                for (int r = 0; r < 4; r++) sum += d[r][c] < 0 ? -d[r][c] : d[r][c];
-            }
-        }
-    return sum >> 1;
+        for (int r = 0; r < 4; r++) sum += d[r][c] < 0 ? -d[r][c] : d[r][c];
+    }
+    return quad_sum(sum) >> 1;
 }
 
-// ReferencePlanes::lowresMC (lowres.h:57-80): the block at quarter-pel q, the
-// rounded average of two half-pel planes when q is a quarter position
+// ReferencePlanes::lowresMC (lowres.h:57-80): the block at quarter-pel q, the rounded average of
+// two half-pel planes when q is a quarter position (ref[] = the lane's quadrant origins)
 template <typename P>
-__device__ __forceinline__ void qpel_block(const P* const (&ref)[4], int64_t ls, int qx, int qy, Blk8<P>& out)
+__device__ __forceinline__ void qpel_block(const P* const (&ref)[4], int64_t ls, int qx, int qy, Quad<P>& out)
 {
     const int ha = (qy & 2) | ((qx & 2) >> 1);
     out.load(ref[ha] + (qx >> 2) + (qy >> 2) * ls, ls);
@@ -457,13 +453,13 @@ __device__ __forceinline__ void qpel_block(const P* const (&ref)[4], int64_t ls,
     {
         const int bx = qx + (qx & 1), by = qy + (qy & 1);
         const int hb = (by & 2) | ((bx & 2) >> 1);
-        Blk8<P> b;
+        Quad<P> b;
         b.load(ref[hb] + (bx >> 2) + (by >> 2) * ls, ls);
         constexpr uint32_t M = sizeof(P) == 1 ? 0x7f7f7f7fu : 0x7fff7fffu;
 #pragma unroll
-        for (int y = 0; y < 8; y++)
+        for (int y = 0; y < 4; y++)
 #pragma unroll
-            for (int w = 0; w < Blk8<P>::W; w++)
+            for (int w = 0; w < Quad<P>::W; w++)
             {
                 const uint32_t x = out.r[y][w], z = b.r[y][w];
                 out.r[y][w] = (x | z) - (((x ^ z) >> 1) & M);     // (a + b + 1) >> 1 per element
@@ -472,12 +468,12 @@ __device__ __forceinline__ void qpel_block(const P* const (&ref)[4], int64_t ls,
 }
 
 template <typename P>
-__device__ __forceinline__ int qpel_cost(const Blk8<P>& fe, const P* const (&ref)[4], int64_t ls, int qx, int qy,
+__device__ __forceinline__ int qpel_cost(const Quad<P>& fe, const P* const (&ref)[4], int64_t ls, int qx, int qy,
                                          bool satd)
 {
-    Blk8<P> b;
+    Quad<P> b;
     qpel_block<P>(ref, ls, qx, qy, b);
-    return satd ? satd8_blk<P>(fe, b) : sad8_blk<P>(fe, b);
+    return satd ? satd_quad<P>(fe, b) : sad_quad<P>(fe, b);
 }
 
 struct MvCost
@@ -490,9 +486,9 @@ struct MvCost
     }
 };
 
-// MotionEstimate::motionEstimate, lowres reference, HEX search, subme 1
+// MotionEstimate::motionEstimate, lowres reference, HEX search, subme 1 (motion.cpp:571-1172)
 template <typename P>
-__device__ int me_lowres(const Blk8<P>& fe, const P* const (&ref)[4], int64_t ls, const MvCost& mc, int minx,
+__device__ int me_lowres(const Quad<P>& fe, const P* const (&ref)[4], int64_t ls, const MvCost& mc, int minx,
                          int miny, int maxx, int maxy, int mvpx, int mvpy, int& outx, int& outy)
 {
     const int pmx = mvpx > 4 * maxx ? 4 * maxx : (mvpx < 4 * minx ? 4 * minx : mvpx);
@@ -579,12 +575,15 @@ __device__ int me_lowres(const Blk8<P>& fe, const P* const (&ref)[4], int64_t ls
     return bcost;
 }
 
+// one workgroup per (estimate, coop slice) of nw wavefronts (enough quads for the slice's rows,
+// up to 16 wavefronts); quad g = threadIdx.x >> 2 owns rows y' = g, g + 16 nw, ...
 template <typename P>
-__global__ __launch_bounds__(64) void k_lowres_pcost(const PcostArgs a)
+__global__ __launch_bounds__(1024) void k_lowres_pcost(const PcostArgs a)
 {
     __shared__ uint32_t ring[kPcostMaxRows][4];   // per row: MVs of its last four CUs (x' & 3), packed x | y << 16
     __shared__ int32_t rowsum[kPcostMaxRows];
-    const int lane = threadIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, g = tid >> 2, q = tid & 3, nq = blockDim.x >> 2;
+    const bool lead = q == 0;
     const int e = blockIdx.x / a.nslices, sl = blockIdx.x % a.nslices;
     const int first = a.rps * sl;
     const int last = sl == a.nslices - 1 ? a.hcu - 1 : a.rps * (sl + 1) - 1;
@@ -592,25 +591,26 @@ __global__ __launch_bounds__(64) void k_lowres_pcost(const PcostArgs a)
     const int ncu = W * a.hcu;
     const P* planes = (const P*)a.planes;
     const int64_t ls = a.ls;
-    const P* fenc0 = planes + a.fenc_off[e];
-    const P* const rbase[4] = { planes + a.ref_off[4 * e], planes + a.ref_off[4 * e + 1], planes + a.ref_off[4 * e + 2],
-                                planes + a.ref_off[4 * e + 3] };
+    const int64_t qoff = 4 * (q & 1) + 4 * (q >> 1) * ls;   // the lane's quadrant
+    const P* fenc0 = planes + a.fenc_off[e] + qoff;
+    const P* const rbase[4] = { planes + a.ref_off[4 * e] + qoff, planes + a.ref_off[4 * e + 1] + qoff,
+                                planes + a.ref_off[4 * e + 2] + qoff, planes + a.ref_off[4 * e + 3] + qoff };
     const int64_t cub = (int64_t)e * ncu;
-    for (int y = lane; y < R; y += 64) rowsum[y] = 0;
-    wave_sync_lds();
+    for (int y = tid; y < R; y += blockDim.x) rowsum[y] = 0;
+    __syncthreads();
     int64_t est = 0, est_aq = 0;
     int mbs = 0;
     const int steps = W + 2 * (R - 1);
     for (int t = 0; t < steps; t++)
     {
-        for (int yp = lane; yp < R; yp += 64)
+        for (int yp = g; yp < R; yp += nq)
         {
             const int xp = t - 2 * yp;
             if (xp < 0 || xp >= W) continue;
             const int cx = W - 1 - xp, cy = last - yp;
             const int xy = cx + cy * W;
             const int64_t off = 8 * cx + 8 * (int64_t)cy * ls;
-            Blk8<P> fe;
+            Quad<P> fe;
             fe.load(fenc0 + off, ls);
             const P* const ref[4] = { rbase[0] + off, rbase[1] + off, rbase[2] + off, rbase[3] + off };
             // MVP: right, below, below-left, below-right (slicetype.cpp:2116-2150)
@@ -637,10 +637,6 @@ __global__ __launch_bounds__(64) void k_lowres_pcost(const PcostArgs a)
             int ox, oy;
             const int fcost = me_lowres<P>(fe, ref, ls, mc, -cx * 8 - 8, -cy * 8 - 8, (W - cx - 1) * 8 + 8,
                                            (a.hcu - cy - 1) * 8 + 8, mvpx, mvpy, ox, oy);
-            ring[yp][xp & 3] = (uint32_t)(uint16_t)ox | ((uint32_t)(uint16_t)oy << 16);
-            a.mvs[2 * (cub + xy)] = (int16_t)ox;
-            a.mvs[2 * (cub + xy) + 1] = (int16_t)oy;
-            a.mv_costs[cub + xy] = fcost;
             int bcost = 1 << 28, listused = 0;
             if (fcost < bcost) { bcost = fcost; listused = 1; }
             bcost += 4;                                              // lowresPenalty
@@ -648,13 +644,20 @@ __global__ __launch_bounds__(64) void k_lowres_pcost(const PcostArgs a)
             if (ic < bcost) { bcost = ic; listused = 0; }
             const bool scored = (cx > 0 && cx < W - 1 && cy > 0 && cy < a.hcu - 1) || W <= 2 || a.hcu <= 2;
             const int bcost_aq = (scored && a.inv_q) ? ((bcost * a.inv_q[cub + xy] + 128) >> 8) : bcost;
-            if (scored) { est += bcost; est_aq += bcost_aq; mbs += !listused; }
-            rowsum[yp] += bcost_aq;
-            a.lowres_costs[cub + xy] = (uint16_t)((bcost < 0x3fff ? bcost : 0x3fff) | (listused << 14));
+            if (lead)
+            {
+                ring[yp][xp & 3] = (uint32_t)(uint16_t)ox | ((uint32_t)(uint16_t)oy << 16);
+                a.mvs[2 * (cub + xy)] = (int16_t)ox;
+                a.mvs[2 * (cub + xy) + 1] = (int16_t)oy;
+                a.mv_costs[cub + xy] = fcost;
+                if (scored) { est += bcost; est_aq += bcost_aq; mbs += !listused; }
+                rowsum[yp] += bcost_aq;
+                a.lowres_costs[cub + xy] = (uint16_t)((bcost < 0x3fff ? bcost : 0x3fff) | (listused << 14));
+            }
         }
-        wave_sync_lds();
+        __syncthreads();
     }
-    for (int yp = lane; yp < R; yp += 64) a.row_satd[(int64_t)e * a.hcu + last - yp] = rowsum[yp];
+    for (int yp = tid; yp < R; yp += blockDim.x) a.row_satd[(int64_t)e * a.hcu + last - yp] = rowsum[yp];
     // slice totals into the estimate's (integer sums: order-independent)
     est = (int64_t)group_sum64<64>((uint64_t)est);
     est_aq = (int64_t)group_sum64<64>((uint64_t)est_aq);
@@ -749,7 +752,11 @@ extern "C" int x265amd_lowres_pcost(int depth, const x265amd_lowres_pcost_batch*
                  b->mvcost, b->mvs, b->mv_costs, b->lowres_costs, b->row_satd, b->cost_est, b->intra_mbs, b->n,
                  b->width_cu, b->height_cu, rps, ns };
     const uint32_t blocks = (uint32_t)(b->n * ns);
-    if (depth == 8) hipLaunchKernelGGL((k_lowres_pcost<uint8_t>), dim3(blocks), dim3(64), 0, st, a);
-    else hipLaunchKernelGGL((k_lowres_pcost<uint16_t>), dim3(blocks), dim3(64), 0, st, a);
+    // enough 4-lane quads for the tallest slice, up to 16 wavefronts (rows beyond take turns)
+    const int rmax = b->height_cu - rps * (ns - 1) > rps ? b->height_cu - rps * (ns - 1) : rps;
+    int nw = (rmax + 15) / 16;
+    nw = nw < 1 ? 1 : (nw > 16 ? 16 : nw);
+    if (depth == 8) hipLaunchKernelGGL((k_lowres_pcost<uint8_t>), dim3(blocks), dim3(64 * nw), 0, st, a);
+    else hipLaunchKernelGGL((k_lowres_pcost<uint16_t>), dim3(blocks), dim3(64 * nw), 0, st, a);
     return (int)hipGetLastError();
 }

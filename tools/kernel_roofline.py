@@ -370,7 +370,7 @@ def main():
                                                      MVS, MC, PLC, PRS, PCE, MB))
             r = {"kernel": f"lowres_pcost_{Hf}p_x{ne}_{tag}", "jobs": ne * ncu, "ms": round(ms_p, 4),
                  "estimates_per_s": round(ne / (ms_p * 1e-3), 1),
-                 "bound": "latency (serial CU wavefront per slice, one wavefront per slice)"}
+                 "bound": "latency (serial CU wavefront per slice; one workgroup per slice, a 4-lane quad per CU row)"}
             try:
                 import ctypes as _C
                 import time as _t
@@ -408,7 +408,7 @@ def main():
                                                  TAB.data_ptr() + 2 * MVCOST_RANGE, MVS, MC, PLC, PRS, PCE, MB))
         r = {"kernel": f"lowres_pcost_{Hf}p_x{nb}_slices{ns}", "jobs": nb * ncu, "ms": round(ms_p, 4),
              "estimates_per_s": round(nb / (ms_p * 1e-3), 1),
-             "bound": "latency (serial CU wavefront per slice, one wavefront per slice)"}
+             "bound": "latency (serial CU wavefront per slice; one workgroup per slice, a 4-lane quad per CU row)"}
         results.append(r)
         print(json.dumps(r), flush=True)
         del SRC, PL, IC, IM, LC, RS, CE, IQ, MVS, MC, PLC, PRS, PCE, MB
