@@ -17,7 +17,7 @@
 //                          m_tmpU / m_tmpL copies emulate in place.
 //   x265amd_sao_stats      SAO::calcSaoStatsCu (sao.cpp:772-943): one wavefront per CTU, one lane
 //                          per 8x8 strip; per pixel the five SAO types' classes; edge-offset
-//                          classes accumulate in registers and reduce across the wavefront,
+//                          classes accumulate in per-lane LDS bins, reduced across the wavefront,
 //                          band classes go to LDS as packed (count << 40) + sum 64-bit adds.
 //   x265amd_extend_border  extendPicBorder (pixel.cpp:908-922): side margins, then full-stride
 //                          margin rows (second launch, so corners copy extended rows).
@@ -482,14 +482,16 @@ struct StatLaunch
 
 // One wavefront per CTU.  Pass 0: luma, lane = 8x8 strip of the CTU (<= 64 strips); pass 1: Cb on
 // lanes 0-31, Cr on lanes 32-63 (<= 16 strips each).  A lane walks its strip row by row (one new
-// 16-byte load per row) and keeps, per EO type and edge class, (sum << 7) + count in one int32
-// (<= 64 pixels of <= 12 bits: no overflow); band classes merge runs of equal band and add them to
-// LDS as (count << 40) + sum.  The lanes' totals then reduce across the wave (or half-wave).
+// 16-byte load per row) and adds, per EO type, (d << 7) + 1 to its private LDS bin of the pixel's
+// edge class (<= 64 pixels of <= 12 bits per lane: no overflow; a conflict-free ds_add instead of a
+// five-way select chain); band classes merge runs of equal band and add them to LDS as
+// (count << 40) + sum.  The lanes' bins then reduce across the wave (or half-wave).
 template <typename P>
 __global__ __launch_bounds__(64) void k_sao_stats(const StatLaunch L)
 {
     __shared__ int32_t eo_sum[3][4][5], eo_cnt[3][4][5];
     __shared__ unsigned long long bo[3][32];
+    __shared__ int32_t bins[64][21];              // per lane: [EO type][edge type] (sum << 7) + count
     const uint32_t b = xcd_block();
     const StatFrame& f = L.f[frame_of<kStatFrames>(L, b)];
     const uint32_t c = b - f.block0;
@@ -523,11 +525,8 @@ __global__ __launch_bounds__(64) void k_sao_stats(const StatLaunch L)
             ye[t] = t == 0 ? ch - sb + po : (bottom ? (eoy ? ch - 1 : ch) : ch - sb + po);
         }
         const int nsx = (cw + 7) >> 3, nsy = (ch + 7) >> 3;
-        int acc[4][5];
 #pragma unroll
-        for (int t = 0; t < 4; t++)
-#pragma unroll
-            for (int k = 0; k < 5; k++) acc[t][k] = 0;
+        for (int k = 0; k < 20; k++) bins[lane][k] = 0;
         if (sl < nsx * nsy)
         {
             const int lx0 = 8 * (sl % nsx), ly0 = 8 * (sl / nsx);
@@ -567,14 +566,7 @@ __global__ __launch_bounds__(64) void k_sao_stats(const StatLaunch L)
                                        sgn(v - up[i]) + sgn(v - dn[i + 2]), sgn(v - up[i + 2]) + sgn(v - dn[i]) };
 #pragma unroll
                     for (int t = 0; t < 4; t++)
-                    {
-                        const int vin = (m[t] >> i) & 1 ? val : 0;
-                        acc[t][0] += e[t] == -2 ? vin : 0;
-                        acc[t][1] += e[t] == -1 ? vin : 0;
-                        acc[t][2] += e[t] == 0 ? vin : 0;
-                        acc[t][3] += e[t] == 1 ? vin : 0;
-                        acc[t][4] += e[t] == 2 ? vin : 0;
-                    }
+                        if ((m[t] >> i) & 1) atomicAdd(&bins[lane][5 * t + e[t] + 2], val);
                     if ((m[4] >> i) & 1)
                     {
                         const int band = v >> L.bo_shift;
@@ -592,29 +584,27 @@ __global__ __launch_bounds__(64) void k_sao_stats(const StatLaunch L)
                 for (int i = 0; i < 10; i++) { up[i] = mid[i]; mid[i] = dn[i]; }
             }
         }
-        // wave (pass 0) / half-wave (pass 1) totals; edge type j = e + 2 -> class s_eoTable[j]
-        // (sao.cpp:65-72): 1, 2, 0, 3, 4
-#pragma unroll
-        for (int t = 0; t < 4; t++)
-#pragma unroll
-            for (int j = 0; j < 5; j++)
+        __syncthreads();
+        // wave (pass 0) / half-wave (pass 1) totals: lane r < 20 of each half sums bin r over the
+        // lanes of its plane; edge type j = e + 2 -> class s_eoTable[j] (sao.cpp:65-72): 1, 2, 0, 3, 4
+        const int r = pass ? lane & 31 : lane;
+        if (r < 20)
+        {
+            const int l0 = pass ? lane & 32 : 0, nl = pass ? 32 : 64;
+            int vs = 0, vc = 0;
+            for (int l = 0; l < nl; l++)
             {
-                const int cn = acc[t][j] & 127;
-                int vs = (acc[t][j] - cn) >> 7, vc = cn;
-#pragma unroll
-                for (int mm = 1; mm < 64; mm <<= 1)
-                {
-                    if (pass && mm == 32) break;
-                    vs += __shfl_xor(vs, mm, 64);
-                    vc += __shfl_xor(vc, mm, 64);
-                }
-                const int k = j == 0 ? 1 : j == 1 ? 2 : j == 2 ? 0 : j;
-                if ((lane & 31) == 0 && (pass || lane == 0))
-                {
-                    eo_sum[p][t][k] = vs;
-                    eo_cnt[p][t][k] = vc;
-                }
+                const int v = bins[l0 + l][r];
+                const int cn = v & 127;
+                vc += cn;
+                vs += (v - cn) >> 7;
             }
+            const int t = r / 5, j = r % 5;
+            const int k = j == 0 ? 1 : j == 1 ? 2 : j == 2 ? 0 : j;
+            eo_sum[p][t][k] = vs;
+            eo_cnt[p][t][k] = vc;
+        }
+        __syncthreads();
     }
     __syncthreads();
     // every entry of the CTU's [3][5][33] block
