@@ -51,6 +51,7 @@ def parse():
     ap.add_argument("--preset", default="medium", choices=("medium", "slow"),
                     help="selects the census of that x265 preset (tests/golden/census_<H>p_<preset>[_main10].json)")
     ap.add_argument("--no-graph", action="store_true", help="launch eagerly instead of replaying a hipGraph")
+    ap.add_argument("--streams", type=int, default=8, help="HIP streams the step's independent launches spread over")
     ap.add_argument("--no-group", action="store_true", help="one launch per batch instead of grouped multi-shape launches")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample duration")
     ap.add_argument("--no-cpu", action="store_true")
@@ -200,9 +201,31 @@ def main():
     ring = RefRing(world, rank)
     ref_send, ref_recv = fs.planes(F - 1), fs.planes(F)
 
+    # independent launches spread over S streams (forked from and joined back into the current
+    # stream, so a captured graph gets S parallel branches): small launches and launch tails overlap
+    import ctypes
+    nstreams = max(1, args.streams)
+    side = [torch.cuda.Stream() for _ in range(nstreams)] if nstreams > 1 else []
+    lanes = [[] for _ in range(nstreams)]
+    load = [0.0] * nstreams
+    for b in launches:                 # largest first: greedy balance by algorithmic bytes
+        i = min(range(nstreams), key=lambda k: load[k])
+        lanes[i].append(b)
+        load[i] += b.bytes
+
     def kernels():
-        for b in launches:
-            b.run(prims)
+        if not side:
+            for b in launches:
+                b.run(prims)
+            return
+        cur = torch.cuda.current_stream()
+        for s_, lst in zip(side, lanes):
+            s_.wait_stream(cur)
+            h = ctypes.c_void_p(s_.cuda_stream)
+            for b in lst:
+                b.run(prims, h)
+        for s_ in side:
+            cur.wait_stream(s_)
 
     def exchange():
         # frame-parallel dependency: my first frame predicts from rank-1's last frame
@@ -319,7 +342,7 @@ def main():
                 "calls_per_step_per_gpu": calls, "batches_per_step": len(batches),
                 "launches_per_step": len(launches),
                 "algorithmic_GB_per_step_per_gpu": round(step_bytes / 1e9, 3),
-                "hipgraph": graph is not None, "parallelism": f"frame-shard x{world}",
+                "hipgraph": graph is not None, "streams": nstreams, "parallelism": f"frame-shard x{world}",
             },
             "mpix_per_s": round(fps * args.width * args.height / 1e6, 1),
             "step_GBps_algorithmic": round(step_bytes * world / (elapsed / args.steps) / 1e9, 1),
