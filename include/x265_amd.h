@@ -438,6 +438,36 @@ typedef struct
 } x265amd_lowres_pcost_batch;
 int x265amd_lowres_pcost(int depth, const x265amd_lowres_pcost_batch* batch, void* stream);
 
+/* f1 B estimates: CostEstimateGroup::estimateFrameCost for p0 < b < p1 (estimateCUCost with
+ * bBidir, slicetype.cpp:2068-2225): per list the search when do_search[2 i + l] (bDoSearch[l]) —
+ * MVP choice incl. the zero-MVP skip cost, lowres HEX search from p0 (list 0) / p1 (list 1) —
+ * else the stored lowresMvCosts / lowresMvs are reused; then the bidir and co-located averages.
+ * Same slice geometry, MV-cost table and sums as x265amd_lowres_pcost (no intra, no intraMbs).
+ * mvs0 / mv_costs0 = lowresMvs[0][b-p0-1] / lowresMvCosts[0][b-p0-1] of b (ncu per estimate; read when
+ * not searched, written when searched), mvs1 / mv_costs1 = lowresMvs[1][p1-b-1] / ...;
+ * lowres_costs = lowresCosts[b-p0][p1-b]; row_satd = rowSatds[b-p0][p1-b]; cost_est = costEst /
+ * costEstAq[b-p0][p1-b].  Weighted prediction of p0 (wfref0) is not applied. */
+typedef struct
+{
+    int n, width_cu, height_cu, rows_per_slice, num_slices;
+    const void* planes;
+    intptr_t lowres_stride;
+    const int64_t* fenc_off;      /* per estimate: lowresPlane[0] of b */
+    const int64_t* ref0_off;      /* 4 per estimate: lowresPlane[0..3] of p0 */
+    const int64_t* ref1_off;      /* 4 per estimate: lowresPlane[0..3] of p1 */
+    const uint8_t* do_search;     /* 2 per estimate */
+    const int32_t* inv_qscale;    /* per estimate: frame b's invQscaleFactor (ncu), or NULL */
+    const uint16_t* mvcost;       /* BitCost table of X265_LOOKAHEAD_QP at difference 0 */
+    int16_t* mvs0;
+    int32_t* mv_costs0;
+    int16_t* mvs1;
+    int32_t* mv_costs1;
+    uint16_t* lowres_costs;
+    int32_t* row_satd;
+    int64_t* cost_est;
+} x265amd_lowres_bcost_batch;
+int x265amd_lowres_bcost(int depth, const x265amd_lowres_bcost_batch* batch, void* stream);
+
 /* ------------------------------------------------------------------- f2
  * Full-resolution motion search.  Job i is one
  * MotionEstimate::motionEstimate call (motion.cpp:571-1172) on a full-resolution

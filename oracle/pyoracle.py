@@ -262,3 +262,21 @@ class FrameFilters:
     def extend_border(self, plane, margin_x, margin_y, width, height):
         self.lib.xo_extend_border(plane.ctypes.data + (margin_y * plane.shape[1] + margin_x) * plane.itemsize,
                                   plane.shape[1], width, height, margin_x, margin_y)
+
+
+class LowresB:
+    """xo_lowres_bcost of one oracle library (one B estimate per call)."""
+
+    def __init__(self, kind: str, depth: int):
+        self.lib = C.CDLL(lib_path(kind, depth))
+        self.lib.xo_lowres_bcost.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, _vp, C.POINTER(_vp), C.POINTER(_vp),
+                                             _ip, _vp, _vp, C.c_int, C.c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp]
+
+    def bcost(self, wcu, hcu, rps, ns, planes, ls, fo, r0o, r1o, iq, tab_centre_ptr, ds0, ds1, mvs0, mc0, mvs1, mc1, lc,
+              rs, ce):
+        """planes: the frames' lowres planes (numpy); fo / r0o[4] / r1o[4]: element offsets"""
+        base, esz = planes.ctypes.data, planes.itemsize
+        r0 = (_vp * 4)(*[base + int(o) * esz for o in r0o])
+        r1 = (_vp * 4)(*[base + int(o) * esz for o in r1o])
+        self.lib.xo_lowres_bcost(wcu, hcu, rps, ns, base + int(fo) * esz, r0, r1, ls, _p(iq), tab_centre_ptr, ds0, ds1,
+                                 _p(mvs0), _p(mc0), _p(mvs1), _p(mc1), _p(lc), _p(rs), _p(ce))

@@ -671,6 +671,93 @@ void xo_lowres_pcost(int wcu, int hcu, int rows_per_slice, int num_slices, const
     x265_param_free(param);
 }
 
+/* f1: a B estimate (p0 = 0, b = 1, p1 = 2) through the reference's own estimateCUCost with
+ * bBidir, in the CU order and slice accounting of estimateFrameCost / processTasks */
+void xo_lowres_bcost(int wcu, int hcu, int rows_per_slice, int num_slices, const void* fenc_plane0,
+                     const void* const* ref0, const void* const* ref1, intptr_t ls, const int32_t* inv_q,
+                     const uint16_t* mvcost_centre, int do_search0, int do_search1, int16_t* mvs0,
+                     int32_t* mv_costs0, int16_t* mvs1, int32_t* mv_costs1, uint16_t* lowres_costs,
+                     int32_t* row_satd, int64_t* cost_est)
+{
+    (void)mvcost_centre;
+    pthread_once(&g_prim_once, init_global_prims);
+    x265_param* param = x265_param_alloc();
+    x265_param_default(param);
+    param->sourceWidth = 16 * wcu;
+    param->sourceHeight = 16 * hcu;
+    param->lookaheadSlices = 0;
+    param->bEnableWeightedPred = 0;
+    Lookahead* la = new Lookahead(param, NULL);
+    LookaheadTLD* tld = new LookaheadTLD();
+    tld->init(wcu, hcu, wcu * hcu);
+
+    Lowres* r0 = (Lowres*)calloc(1, sizeof(Lowres));
+    Lowres* r1 = (Lowres*)calloc(1, sizeof(Lowres));
+    Lowres* cur = (Lowres*)calloc(1, sizeof(Lowres));
+    for (int k = 0; k < 4; k++)
+    {
+        r0->lowresPlane[k] = (pixel*)ref0[k];
+        r1->lowresPlane[k] = (pixel*)ref1[k];
+    }
+    Lowres* lr[3] = { r0, cur, r1 };
+    for (int i = 0; i < 3; i++)
+    {
+        lr[i]->fpelPlane[0] = lr[i]->lowresPlane[0];
+        lr[i]->lumaStride = ls;
+        lr[i]->isLowres = true;
+    }
+    cur->lowresPlane[0] = cur->fpelPlane[0] = (pixel*)fenc_plane0;
+    cur->invQscaleFactor = (int*)inv_q;
+    cur->lowresMvs[0][0] = (MV*)mvs0;
+    cur->lowresMvCosts[0][0] = mv_costs0;
+    cur->lowresMvs[1][0] = (MV*)mvs1;
+    cur->lowresMvCosts[1][0] = mv_costs1;
+    cur->lowresCosts[1][1] = lowres_costs;
+    cur->rowSatds[1][1] = row_satd;
+    CostGroup g(*la, lr);
+    bool ds[2] = { !!do_search0, !!do_search1 };
+    const int p0 = 0, b = 1, p1 = 2;
+    if (num_slices < 1) { num_slices = 1; rows_per_slice = hcu; }
+    int64_t est = 0, est_aq = 0;
+    if (num_slices == 1)
+    {
+        cur->costEst[1][1] = cur->costEstAq[1][1] = 0;
+        bool last = true;
+        for (int cy = hcu - 1; cy >= 0; cy--)
+        {
+            row_satd[cy] = 0;
+            for (int cx = wcu - 1; cx >= 0; cx--) g.cu(*tld, cx, cy, p0, p1, b, ds, last, -1);
+            last = false;
+        }
+        est = cur->costEst[1][1];
+        est_aq = cur->costEstAq[1][1];
+    }
+    else
+        for (int i = 0; i < num_slices; i++)
+        {
+            memset(&g.slice(i), 0, sizeof(g.slice(i)));
+            const int first = rows_per_slice * i;
+            const int lastY = i == num_slices - 1 ? hcu - 1 : rows_per_slice * (i + 1) - 1;
+            bool last = true;
+            for (int cy = lastY; cy >= first; cy--)
+            {
+                row_satd[cy] = 0;
+                for (int cx = wcu - 1; cx >= 0; cx--) g.cu(*tld, cx, cy, p0, p1, b, ds, last, i);
+                last = false;
+            }
+            est += g.slice(i).costEst;
+            est_aq += g.slice(i).costEstAq;
+        }
+    cost_est[0] = est;
+    cost_est[1] = est_aq;
+    free(r0);
+    free(r1);
+    free(cur);
+    delete tld;
+    delete la;
+    x265_param_free(param);
+}
+
 void xo_mvcost_table_qp(int qp, int range, uint16_t* out)
 {
     TabBitCost bc;

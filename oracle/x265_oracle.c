@@ -1255,6 +1255,131 @@ void xo_lowres_pcost(int wcu, int hcu, int rows_per_slice, int num_slices, const
     *intra_mbs = mbs;
 }
 
+/* ReferencePlanes::lowresMC (lowres.h:57-80) into an 8x8 buffer (stride 8) */
+static void xo_lowres_mc(const pix* const ref[4], intptr_t ls, xmv q, pix* out)
+{
+    if ((q.x | q.y) & 1)
+    {
+        const int ha = (q.y & 2) | ((q.x & 2) >> 1);
+        const pix* a = ref[ha] + (q.x >> 2) + (q.y >> 2) * ls;
+        const int qx = q.x + (q.x & 1), qy = q.y + (q.y & 1);
+        const int hb = (qy & 2) | ((qx & 2) >> 1);
+        const pix* b = ref[hb] + (qx >> 2) + (qy >> 2) * ls;
+        xo_pixelavg(8, 8, out, 8, a, ls, b, ls);
+    }
+    else
+    {
+        const pix* p = ref[(q.y & 2) | ((q.x & 2) >> 1)] + (q.x >> 2) + (q.y >> 2) * ls;
+        for (int y = 0; y < 8; y++) memcpy(out + 8 * y, p + y * ls, 8 * sizeof(pix));
+    }
+}
+
+/* CostEstimateGroup::estimateFrameCost for a B estimate (p0 < b < p1) = estimateCUCost
+ * (slicetype.cpp:2068-2225) with bBidir: per list i with bDoSearch[i] the MVP choice (incl. the
+ * skipCost of a zero MVP), the lowres HEX search from fref0 (list 0) / fref1 (list 1) and the
+ * zero-MV skip override; lists not searched reuse lowresMvCosts; then the bidir average of the two
+ * lists' predictions and the co-located average, each scored by SATD.  Weighted prediction off. */
+void xo_lowres_bcost(int wcu, int hcu, int rows_per_slice, int num_slices, const void* fenc_plane0,
+                     const void* const* ref0, const void* const* ref1, intptr_t ls, const int32_t* inv_q,
+                     const uint16_t* mvcost_centre, int do_search0, int do_search1, int16_t* mvs0,
+                     int32_t* mv_costs0, int16_t* mvs1, int32_t* mv_costs1, uint16_t* lowres_costs,
+                     int32_t* row_satd, int64_t* cost_est)
+{
+    const pix* fp = (const pix*)fenc_plane0;
+    const pix* rp[2][4];
+    for (int k = 0; k < 4; k++) { rp[0][k] = (const pix*)ref0[k]; rp[1][k] = (const pix*)ref1[k]; }
+    int16_t* mvs[2] = { mvs0, mvs1 };
+    int32_t* mcost[2] = { mv_costs0, mv_costs1 };
+    const int ds[2] = { do_search0, do_search1 };
+    if (num_slices < 1) { num_slices = 1; rows_per_slice = hcu; }
+    int64_t est = 0, est_aq = 0;
+    for (int s = 0; s < num_slices; s++)
+    {
+        const int first = rows_per_slice * s;
+        const int last = s == num_slices - 1 ? hcu - 1 : rows_per_slice * (s + 1) - 1;
+        int last_row = 1;
+        for (int cy = last; cy >= first; cy--)
+        {
+            row_satd[cy] = 0;
+            for (int cx = wcu - 1; cx >= 0; cx--)
+            {
+                const int xy = cx + cy * wcu;
+                const intptr_t off = 8 * cx + 8 * cy * ls;
+                pix fenc[64];
+                for (int y = 0; y < 8; y++) memcpy(fenc + 8 * y, fp + off + y * ls, 8 * sizeof(pix));
+                const xmv mvmin = { -cx * 8 - 8, -cy * 8 - 8 };
+                const xmv mvmax = { (wcu - cx - 1) * 8 + 8, (hcu - cy - 1) * 8 + 8 };
+                int bcost = 1 << 28, listused = 0;
+                for (int i = 0; i < 2; i++)
+                {
+                    if (!ds[i])
+                    {
+                        if (mcost[i][xy] < bcost) { bcost = mcost[i][xy]; listused = i + 1; }
+                        continue;
+                    }
+                    int16_t* mv = mvs[i];
+                    XoMe m = { fenc, { rp[i][0] + off, rp[i][1] + off, rp[i][2] + off, rp[i][3] + off }, ls,
+                               mvcost_centre, { 0, 0 } };
+                    xmv mvc[4];
+                    int numc = 0;
+                    if (cx < wcu - 1) { mvc[numc].x = mv[2 * (xy + 1)]; mvc[numc++].y = mv[2 * (xy + 1) + 1]; }
+                    if (!last_row)
+                    {
+                        mvc[numc].x = mv[2 * (xy + wcu)]; mvc[numc++].y = mv[2 * (xy + wcu) + 1];
+                        if (cx > 0) { mvc[numc].x = mv[2 * (xy + wcu - 1)]; mvc[numc++].y = mv[2 * (xy + wcu - 1) + 1]; }
+                        if (cx < wcu - 1) { mvc[numc].x = mv[2 * (xy + wcu + 1)]; mvc[numc++].y = mv[2 * (xy + wcu + 1) + 1]; }
+                    }
+                    xmv mvp = { 0, 0 };
+                    int skip = 0x7fffffff;                                  /* INT_MAX */
+                    if (numc)
+                    {
+                        int mvpcost = 1 << 28;
+                        for (int k = 0; k < numc; k++)
+                        {
+                            const int c = xo_qpel_cost(&m, mvc[k], 1);
+                            if (c < mvpcost) { mvpcost = c; mvp = mvc[k]; }
+                            if (!mvp.x && !mvp.y) skip = c;                 /* the candidate's cost, as written */
+                        }
+                    }
+                    xmv out;
+                    int fcost = xo_me_lowres(&m, mvmin, mvmax, mvp, 16, &out);
+                    if (skip < 64 && skip < fcost) { fcost = skip; out.x = out.y = 0; }
+                    mv[2 * xy] = (int16_t)out.x;
+                    mv[2 * xy + 1] = (int16_t)out.y;
+                    mcost[i][xy] = fcost;
+                    if (fcost < bcost) { bcost = fcost; listused = i + 1; }
+                }
+                /* bidir: avg(l0 prediction, l1 prediction), then the co-located average */
+                pix b0[64], b1[64], avg[64];
+                const pix* r0o[4] = { rp[0][0] + off, rp[0][1] + off, rp[0][2] + off, rp[0][3] + off };
+                const pix* r1o[4] = { rp[1][0] + off, rp[1][1] + off, rp[1][2] + off, rp[1][3] + off };
+                const xmv m0 = { mvs0[2 * xy], mvs0[2 * xy + 1] }, m1 = { mvs1[2 * xy], mvs1[2 * xy + 1] };
+                xo_lowres_mc(r0o, ls, m0, b0);
+                xo_lowres_mc(r1o, ls, m1, b1);
+                xo_pixelavg(8, 8, avg, 8, b0, 8, b1, 8);
+                int bicost = xo_satd(8, 8, fenc, 8, avg, 8);
+                if (bicost < bcost) { bcost = bicost; listused = 3; }
+                xo_pixelavg(8, 8, avg, 8, rp[0][0] + off, ls, rp[1][0] + off, ls);
+                bicost = xo_satd(8, 8, fenc, 8, avg, 8);
+                if (bicost < bcost) { bcost = bicost; listused = 3; }
+                bcost += 4;                                                /* lowresPenalty */
+                const int scored = (cx > 0 && cx < wcu - 1 && cy > 0 && cy < hcu - 1) || wcu <= 2 || hcu <= 2;
+                const int bcost_aq = (scored && inv_q) ? ((bcost * inv_q[xy] + 128) >> 8) : bcost;
+                if (scored)
+                {
+                    est += bcost;
+                    est_aq += bcost_aq;
+                }
+                row_satd[cy] += bcost_aq;
+                lowres_costs[xy] = (uint16_t)((bcost < 0x3fff ? bcost : 0x3fff) | (listused << 14));
+            }
+            last_row = 0;
+        }
+    }
+    cost_est[0] = est;
+    cost_est[1] = est_aq;
+}
+
 /* ---------------------------------------------------------------- f2: full-resolution motion search
  * MotionEstimate::motionEstimate (motion.cpp:571-1172) for one PU on a full-resolution
  * reference: clipped MVP measured at sub-pel with SAD, the extra MV candidates, DIA or HEX

@@ -132,6 +132,16 @@ void     xo_lowres_pcost(int wcu, int hcu, int rows_per_slice, int num_slices, c
                          const int32_t* intra_cost, const int32_t* inv_q, const uint16_t* mvcost_centre,
                          int16_t* mvs, int32_t* mv_costs, uint16_t* lowres_costs, int32_t* row_satd,
                          int64_t* cost_est, int32_t* intra_mbs);
+/* f1: CostEstimateGroup::estimateFrameCost for a B estimate (p0 < b < p1, slicetype.cpp:2068-2225
+ * with bBidir): ref0 / ref1 = the four lowres planes of p0 / p1; do_search0 / 1 = bDoSearch[0 / 1]
+ * (a list not searched reuses mvs / mv_costs as given); mvs0 / mv_costs0 = lowresMvs[0][b-p0-1] /
+ * lowresMvCosts[0][b-p0-1] of b, mvs1 / mv_costs1 = lowresMvs[1][p1-b-1] / ...; outputs
+ * lowres_costs (lowresCosts[b-p0][p1-b]), row_satd, cost_est[0..1].  Weighted prediction off. */
+void     xo_lowres_bcost(int wcu, int hcu, int rows_per_slice, int num_slices, const void* fenc_plane0,
+                         const void* const* ref0, const void* const* ref1, intptr_t ls, const int32_t* inv_q,
+                         const uint16_t* mvcost_centre, int do_search0, int do_search1, int16_t* mvs0,
+                         int32_t* mv_costs0, int16_t* mvs1, int32_t* mv_costs1, uint16_t* lowres_costs,
+                         int32_t* row_satd, int64_t* cost_est);
 /* f2: MotionEstimate::motionEstimate (motion.cpp:571-1172) for one w x h PU on a full-resolution
  * reference: method 0 = DIA, 1 = HEX, 2 = STAR; subme 0..3 (at 3 the 4:2:0 chroma SATD of
  * subpelCompare is added when fcb != NULL and the chroma PU has a satd entry: fcb / fcr, rcb / rcr =

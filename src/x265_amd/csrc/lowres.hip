@@ -670,6 +670,170 @@ __global__ __launch_bounds__(1024) void k_lowres_pcost(const PcostArgs a)
     }
 }
 
+// ---------------------------------------------------------------- B-frame cost estimate
+// estimateCUCost with bBidir (p0 < b < p1, slicetype.cpp:2068-2225): per list i with bDoSearch[i]
+// the MVP choice (and the skipCost of a zero MVP), the lowres HEX search from p0 (list 0) or p1
+// (list 1) and the zero-MV skip override; a list not searched reuses its stored cost and MV; then
+// the bidir average of the two lists' predictions and the co-located average, scored by SATD.
+// Same wavefront schedule and quad mapping as the P estimate, one MV ring per list.
+struct BcostArgs
+{
+    const void* planes;
+    int64_t ls;
+    const int64_t* fenc_off;      // per estimate: lowresPlane[0] of b
+    const int64_t* ref_off[2];    // 4 per estimate: lowresPlane[0..3] of p0 / p1
+    const uint8_t* do_search;     // 2 per estimate
+    const int32_t* inv_q;
+    const uint16_t* mvcost;
+    int16_t* mvs[2];
+    int32_t* mv_costs[2];
+    uint16_t* lowres_costs;
+    int32_t* row_satd;
+    int64_t* cost_est;
+    int n, wcu, hcu, rps, nslices;
+};
+
+template <typename P>
+__global__ __launch_bounds__(1024) void k_lowres_bcost(const BcostArgs a)
+{
+    __shared__ uint32_t ring[2][kPcostMaxRows][4];
+    __shared__ int32_t rowsum[kPcostMaxRows];
+    const int tid = threadIdx.x, lane = tid & 63, g = tid >> 2, q = tid & 3, nq = blockDim.x >> 2;
+    const bool lead = q == 0;
+    const int e = blockIdx.x / a.nslices, sl = blockIdx.x % a.nslices;
+    const int first = a.rps * sl;
+    const int last = sl == a.nslices - 1 ? a.hcu - 1 : a.rps * (sl + 1) - 1;
+    const int R = last - first + 1, W = a.wcu;
+    const int ncu = W * a.hcu;
+    const P* planes = (const P*)a.planes;
+    const int64_t ls = a.ls;
+    const int64_t qoff = 4 * (q & 1) + 4 * (q >> 1) * ls;   // the lane's quadrant
+    const P* fenc0 = planes + a.fenc_off[e] + qoff;
+    const P* rb[2][4];
+#pragma unroll
+    for (int i = 0; i < 2; i++)
+#pragma unroll
+        for (int k = 0; k < 4; k++) rb[i][k] = planes + a.ref_off[i][4 * e + k] + qoff;
+    const bool ds[2] = { a.do_search[2 * e] != 0, a.do_search[2 * e + 1] != 0 };
+    const int64_t cub = (int64_t)e * ncu;
+    for (int y = tid; y < R; y += blockDim.x) rowsum[y] = 0;
+    __syncthreads();
+    int64_t est = 0, est_aq = 0;
+    const int steps = W + 2 * (R - 1);
+    for (int t = 0; t < steps; t++)
+    {
+        for (int yp = g; yp < R; yp += nq)
+        {
+            const int xp = t - 2 * yp;
+            if (xp < 0 || xp >= W) continue;
+            const int cx = W - 1 - xp, cy = last - yp;
+            const int xy = cx + cy * W;
+            const int64_t off = 8 * cx + 8 * (int64_t)cy * ls;
+            Quad<P> fe;
+            fe.load(fenc0 + off, ls);
+            int bcost = 1 << 28, listused = 0;
+            int mx[2], my[2];
+#pragma unroll
+            for (int i = 0; i < 2; i++)
+            {
+                if (!ds[i])
+                {
+                    const int c = a.mv_costs[i][cub + xy];
+                    mx[i] = a.mvs[i][2 * (cub + xy)];
+                    my[i] = a.mvs[i][2 * (cub + xy) + 1];
+                    if (c < bcost) { bcost = c; listused = i + 1; }
+                    continue;
+                }
+                const P* const ref[4] = { rb[i][0] + off, rb[i][1] + off, rb[i][2] + off, rb[i][3] + off };
+                int candx[4], candy[4], numc = 0;
+                if (cx < W - 1) { const uint32_t m = ring[i][yp][(xp - 1) & 3]; candx[numc] = (int16_t)m; candy[numc++] = (int16_t)(m >> 16); }
+                if (yp > 0)
+                {
+                    const uint32_t mb = ring[i][yp - 1][xp & 3];
+                    candx[numc] = (int16_t)mb; candy[numc++] = (int16_t)(mb >> 16);
+                    if (cx > 0) { const uint32_t m = ring[i][yp - 1][(xp + 1) & 3]; candx[numc] = (int16_t)m; candy[numc++] = (int16_t)(m >> 16); }
+                    if (cx < W - 1) { const uint32_t m = ring[i][yp - 1][(xp - 1) & 3]; candx[numc] = (int16_t)m; candy[numc++] = (int16_t)(m >> 16); }
+                }
+                int mvpx = 0, mvpy = 0, skip = 0x7fffffff;
+                if (numc)
+                {
+                    int best = 1 << 28;                              // MotionEstimate::COST_MAX
+                    for (int k = 0; k < numc; k++)
+                    {
+                        const int c = qpel_cost<P>(fe, ref, ls, candx[k], candy[k], true);
+                        if (c < best) { best = c; mvpx = candx[k]; mvpy = candy[k]; }
+                        if (!mvpx && !mvpy) skip = c;                // slicetype.cpp:2150-2151, as written
+                    }
+                }
+                const MvCost mc{ a.mvcost, mvpx, mvpy };
+                int ox, oy;
+                int fcost = me_lowres<P>(fe, ref, ls, mc, -cx * 8 - 8, -cy * 8 - 8, (W - cx - 1) * 8 + 8,
+                                         (a.hcu - cy - 1) * 8 + 8, mvpx, mvpy, ox, oy);
+                if (skip < 64 && skip < fcost) { fcost = skip; ox = oy = 0; }
+                mx[i] = ox;
+                my[i] = oy;
+                if (lead)
+                {
+                    ring[i][yp][xp & 3] = (uint32_t)(uint16_t)ox | ((uint32_t)(uint16_t)oy << 16);
+                    a.mvs[i][2 * (cub + xy)] = (int16_t)ox;
+                    a.mvs[i][2 * (cub + xy) + 1] = (int16_t)oy;
+                    a.mv_costs[i][cub + xy] = fcost;
+                }
+                if (fcost < bcost) { bcost = fcost; listused = i + 1; }
+            }
+            // bidir: avg(l0 prediction, l1 prediction), then the co-located average (pixelavg_pp, bufSATD)
+            constexpr uint32_t M = sizeof(P) == 1 ? 0x7f7f7f7fu : 0x7fff7fffu;
+            {
+                const P* const r0[4] = { rb[0][0] + off, rb[0][1] + off, rb[0][2] + off, rb[0][3] + off };
+                const P* const r1[4] = { rb[1][0] + off, rb[1][1] + off, rb[1][2] + off, rb[1][3] + off };
+                Quad<P> b0, b1;
+                qpel_block<P>(r0, ls, mx[0], my[0], b0);
+                qpel_block<P>(r1, ls, mx[1], my[1], b1);
+#pragma unroll
+                for (int y = 0; y < 4; y++)
+#pragma unroll
+                    for (int w = 0; w < Quad<P>::W; w++)
+                    {
+                        const uint32_t x = b0.r[y][w], z = b1.r[y][w];
+                        b0.r[y][w] = (x | z) - (((x ^ z) >> 1) & M);
+                    }
+                const int bi = satd_quad<P>(fe, b0);
+                if (bi < bcost) { bcost = bi; listused = 3; }
+                b0.load(r0[0], ls);
+                b1.load(r1[0], ls);
+#pragma unroll
+                for (int y = 0; y < 4; y++)
+#pragma unroll
+                    for (int w = 0; w < Quad<P>::W; w++)
+                    {
+                        const uint32_t x = b0.r[y][w], z = b1.r[y][w];
+                        b0.r[y][w] = (x | z) - (((x ^ z) >> 1) & M);
+                    }
+                const int co = satd_quad<P>(fe, b0);
+                if (co < bcost) { bcost = co; listused = 3; }
+            }
+            bcost += 4;                                              // lowresPenalty
+            const bool scored = (cx > 0 && cx < W - 1 && cy > 0 && cy < a.hcu - 1) || W <= 2 || a.hcu <= 2;
+            const int bcost_aq = (scored && a.inv_q) ? ((bcost * a.inv_q[cub + xy] + 128) >> 8) : bcost;
+            if (lead)
+            {
+                if (scored) { est += bcost; est_aq += bcost_aq; }
+                rowsum[yp] += bcost_aq;
+                a.lowres_costs[cub + xy] = (uint16_t)((bcost < 0x3fff ? bcost : 0x3fff) | (listused << 14));
+            }
+        }
+        __syncthreads();
+    }
+    for (int yp = tid; yp < R; yp += blockDim.x) a.row_satd[(int64_t)e * a.hcu + last - yp] = rowsum[yp];
+    est = (int64_t)group_sum64<64>((uint64_t)est);
+    est_aq = (int64_t)group_sum64<64>((uint64_t)est_aq);
+    if (lane == 0)
+    {
+        atomicAdd((unsigned long long*)&a.cost_est[2 * e], (unsigned long long)est);
+        atomicAdd((unsigned long long*)&a.cost_est[2 * e + 1], (unsigned long long)est_aq);
+    }
+}
+
 template <typename P>
 static int launch_lowres_init(const LowresArgs& a, hipStream_t st)
 {
@@ -758,5 +922,32 @@ extern "C" int x265amd_lowres_pcost(int depth, const x265amd_lowres_pcost_batch*
     nw = nw < 1 ? 1 : (nw > 16 ? 16 : nw);
     if (depth == 8) hipLaunchKernelGGL((k_lowres_pcost<uint8_t>), dim3(blocks), dim3(64 * nw), 0, st, a);
     else hipLaunchKernelGGL((k_lowres_pcost<uint16_t>), dim3(blocks), dim3(64 * nw), 0, st, a);
+    return (int)hipGetLastError();
+}
+
+extern "C" int x265amd_lowres_bcost(int depth, const x265amd_lowres_bcost_batch* b, void* stream)
+{
+    if ((depth != 8 && depth != 10 && depth != 12) || !b) return X265AMD_EINVAL;
+    if (b->n < 0 || b->width_cu <= 0 || b->height_cu <= 0) return X265AMD_EINVAL;
+    int rps = b->rows_per_slice, ns = b->num_slices;
+    if (ns <= 1) { ns = 1; rps = b->height_cu; }
+    if (rps <= 0 || (int64_t)rps * (ns - 1) >= b->height_cu) return X265AMD_EINVAL;
+    if (b->height_cu - rps * (ns - 1) > kPcostMaxRows || rps > kPcostMaxRows) return X265AMD_EINVAL;
+    if (!b->n) return 0;
+    if (!b->planes || !b->fenc_off || !b->ref0_off || !b->ref1_off || !b->do_search || !b->mvcost || !b->mvs0 ||
+        !b->mv_costs0 || !b->mvs1 || !b->mv_costs1 || !b->lowres_costs || !b->row_satd || !b->cost_est)
+        return X265AMD_EINVAL;
+    hipStream_t st = (hipStream_t)stream;
+    const hipError_t err = hipMemsetAsync(b->cost_est, 0, sizeof(int64_t) * 2 * (size_t)b->n, st);
+    if (err != hipSuccess) return (int)err;
+    BcostArgs a{ b->planes, (int64_t)b->lowres_stride, b->fenc_off, { b->ref0_off, b->ref1_off }, b->do_search,
+                 b->inv_qscale, b->mvcost, { b->mvs0, b->mvs1 }, { b->mv_costs0, b->mv_costs1 }, b->lowres_costs,
+                 b->row_satd, b->cost_est, b->n, b->width_cu, b->height_cu, rps, ns };
+    const uint32_t blocks = (uint32_t)(b->n * ns);
+    const int rmax = b->height_cu - rps * (ns - 1) > rps ? b->height_cu - rps * (ns - 1) : rps;
+    int nw = (rmax + 15) / 16;
+    nw = nw < 1 ? 1 : (nw > 16 ? 16 : nw);
+    if (depth == 8) hipLaunchKernelGGL((k_lowres_bcost<uint8_t>), dim3(blocks), dim3(64 * nw), 0, st, a);
+    else hipLaunchKernelGGL((k_lowres_bcost<uint16_t>), dim3(blocks), dim3(64 * nw), 0, st, a);
     return (int)hipGetLastError();
 }

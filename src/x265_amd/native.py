@@ -63,6 +63,13 @@ class LowresPcostBatch(C.Structure):
                 ("row_satd", _vp), ("cost_est", _vp), ("intra_mbs", _vp)]
 
 
+class LowresBcostBatch(C.Structure):
+    _fields_ = [("n", _int), ("width_cu", _int), ("height_cu", _int), ("rows_per_slice", _int), ("num_slices", _int),
+                ("planes", _vp), ("lowres_stride", _ip), ("fenc_off", _vp), ("ref0_off", _vp), ("ref1_off", _vp),
+                ("do_search", _vp), ("inv_qscale", _vp), ("mvcost", _vp), ("mvs0", _vp), ("mv_costs0", _vp),
+                ("mvs1", _vp), ("mv_costs1", _vp), ("lowres_costs", _vp), ("row_satd", _vp), ("cost_est", _vp)]
+
+
 class MeBatch(C.Structure):
     _fields_ = [("w", _int), ("h", _int), ("n", _int), ("method", _int), ("subme", _int), ("merange", _int),
                 ("max_cand", _int), ("fenc", _vp), ("fenc_stride", _ip), ("fenc_off", _vp), ("ref", _vp),
@@ -276,6 +283,13 @@ class Primitives:
         b = LowresPcostBatch(n, wcu, hcu, rps, ns, _addr(planes), ls, _addr(fo), _addr(ro), _addr(ic), _addr(iq),
                              tab_centre_ptr, _addr(mvs), _addr(mc), _addr(lc), _addr(rs), _addr(ce), _addr(mbs))
         self._check(self.lib.x265amd_lowres_pcost(depth, C.byref(b), stream or _stream()), "lowres_pcost")
+
+    def lowres_bcost(self, depth, n, wcu, hcu, rps, ns, planes, ls, fo, r0o, r1o, ds, iq, tab_centre_ptr, mvs0, mc0,
+                     mvs1, mc1, lc, rs, ce, stream=None):
+        b = LowresBcostBatch(n, wcu, hcu, rps, ns, _addr(planes), ls, _addr(fo), _addr(r0o), _addr(r1o), _addr(ds),
+                             _addr(iq), tab_centre_ptr, _addr(mvs0), _addr(mc0), _addr(mvs1), _addr(mc1), _addr(lc),
+                             _addr(rs), _addr(ce))
+        self._check(self.lib.x265amd_lowres_bcost(depth, C.byref(b), stream or _stream()), "lowres_bcost")
 
     # -- f2 full-resolution motion search
     def motion_search(self, depth, w, h, method, subme, merange, max_cand, f, fs, fo, r, rs, ro, rng, mvp, mvc, numc,
