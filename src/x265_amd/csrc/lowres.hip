@@ -675,7 +675,7 @@ __global__ __launch_bounds__(1024) void k_lowres_pcost(const PcostArgs a)
 // the MVP choice (and the skipCost of a zero MVP), the lowres HEX search from p0 (list 0) or p1
 // (list 1) and the zero-MV skip override; a list not searched reuses its stored cost and MV; then
 // the bidir average of the two lists' predictions and the co-located average, scored by SATD.
-// Same wavefront schedule and quad mapping as the P estimate, one MV ring per list.
+// Same wavefront schedule as the P estimate, one MV ring per list.
 struct BcostArgs
 {
     const void* planes;
@@ -693,12 +693,16 @@ struct BcostArgs
     int n, wcu, hcu, rps, nslices;
 };
 
+// Two quads per CU (8 lanes): quad li searches list li, the two run concurrently and exchange
+// their MV and cost by a lane ^ 4 swizzle; then quad 0 scores the bidir average and quad 1 the
+// co-located average, and both apply the reference's decision order.
 template <typename P>
 __global__ __launch_bounds__(1024) void k_lowres_bcost(const BcostArgs a)
 {
     __shared__ uint32_t ring[2][kPcostMaxRows][4];
     __shared__ int32_t rowsum[kPcostMaxRows];
-    const int tid = threadIdx.x, lane = tid & 63, g = tid >> 2, q = tid & 3, nq = blockDim.x >> 2;
+    const int tid = threadIdx.x, lane = tid & 63, g = tid >> 3, li = (tid >> 2) & 1, q = tid & 3;
+    const int nq = blockDim.x >> 3;
     const bool lead = q == 0;
     const int e = blockIdx.x / a.nslices, sl = blockIdx.x % a.nslices;
     const int first = a.rps * sl;
@@ -714,7 +718,9 @@ __global__ __launch_bounds__(1024) void k_lowres_bcost(const BcostArgs a)
     for (int i = 0; i < 2; i++)
 #pragma unroll
         for (int k = 0; k < 4; k++) rb[i][k] = planes + a.ref_off[i][4 * e + k] + qoff;
-    const bool ds[2] = { a.do_search[2 * e] != 0, a.do_search[2 * e + 1] != 0 };
+    const bool search = a.do_search[2 * e + li] != 0;
+    int16_t* const mvs = a.mvs[li];
+    int32_t* const mvc = a.mv_costs[li];
     const int64_t cub = (int64_t)e * ncu;
     for (int y = tid; y < R; y += blockDim.x) rowsum[y] = 0;
     __syncthreads();
@@ -731,28 +737,25 @@ __global__ __launch_bounds__(1024) void k_lowres_bcost(const BcostArgs a)
             const int64_t off = 8 * cx + 8 * (int64_t)cy * ls;
             Quad<P> fe;
             fe.load(fenc0 + off, ls);
-            int bcost = 1 << 28, listused = 0;
-            int mx[2], my[2];
-#pragma unroll
-            for (int i = 0; i < 2; i++)
+            // ---- this quad's list
+            int cost, ox, oy;
+            if (!search)
             {
-                if (!ds[i])
-                {
-                    const int c = a.mv_costs[i][cub + xy];
-                    mx[i] = a.mvs[i][2 * (cub + xy)];
-                    my[i] = a.mvs[i][2 * (cub + xy) + 1];
-                    if (c < bcost) { bcost = c; listused = i + 1; }
-                    continue;
-                }
-                const P* const ref[4] = { rb[i][0] + off, rb[i][1] + off, rb[i][2] + off, rb[i][3] + off };
+                cost = mvc[cub + xy];
+                ox = mvs[2 * (cub + xy)];
+                oy = mvs[2 * (cub + xy) + 1];
+            }
+            else
+            {
+                const P* const ref[4] = { rb[li][0] + off, rb[li][1] + off, rb[li][2] + off, rb[li][3] + off };
                 int candx[4], candy[4], numc = 0;
-                if (cx < W - 1) { const uint32_t m = ring[i][yp][(xp - 1) & 3]; candx[numc] = (int16_t)m; candy[numc++] = (int16_t)(m >> 16); }
+                if (cx < W - 1) { const uint32_t m = ring[li][yp][(xp - 1) & 3]; candx[numc] = (int16_t)m; candy[numc++] = (int16_t)(m >> 16); }
                 if (yp > 0)
                 {
-                    const uint32_t mb = ring[i][yp - 1][xp & 3];
+                    const uint32_t mb = ring[li][yp - 1][xp & 3];
                     candx[numc] = (int16_t)mb; candy[numc++] = (int16_t)(mb >> 16);
-                    if (cx > 0) { const uint32_t m = ring[i][yp - 1][(xp + 1) & 3]; candx[numc] = (int16_t)m; candy[numc++] = (int16_t)(m >> 16); }
-                    if (cx < W - 1) { const uint32_t m = ring[i][yp - 1][(xp - 1) & 3]; candx[numc] = (int16_t)m; candy[numc++] = (int16_t)(m >> 16); }
+                    if (cx > 0) { const uint32_t m = ring[li][yp - 1][(xp + 1) & 3]; candx[numc] = (int16_t)m; candy[numc++] = (int16_t)(m >> 16); }
+                    if (cx < W - 1) { const uint32_t m = ring[li][yp - 1][(xp - 1) & 3]; candx[numc] = (int16_t)m; candy[numc++] = (int16_t)(m >> 16); }
                 }
                 int mvpx = 0, mvpy = 0, skip = 0x7fffffff;
                 if (numc)
@@ -766,56 +769,57 @@ __global__ __launch_bounds__(1024) void k_lowres_bcost(const BcostArgs a)
                     }
                 }
                 const MvCost mc{ a.mvcost, mvpx, mvpy };
-                int ox, oy;
-                int fcost = me_lowres<P>(fe, ref, ls, mc, -cx * 8 - 8, -cy * 8 - 8, (W - cx - 1) * 8 + 8,
-                                         (a.hcu - cy - 1) * 8 + 8, mvpx, mvpy, ox, oy);
-                if (skip < 64 && skip < fcost) { fcost = skip; ox = oy = 0; }
-                mx[i] = ox;
-                my[i] = oy;
+                cost = me_lowres<P>(fe, ref, ls, mc, -cx * 8 - 8, -cy * 8 - 8, (W - cx - 1) * 8 + 8,
+                                    (a.hcu - cy - 1) * 8 + 8, mvpx, mvpy, ox, oy);
+                if (skip < 64 && skip < cost) { cost = skip; ox = oy = 0; }
                 if (lead)
                 {
-                    ring[i][yp][xp & 3] = (uint32_t)(uint16_t)ox | ((uint32_t)(uint16_t)oy << 16);
-                    a.mvs[i][2 * (cub + xy)] = (int16_t)ox;
-                    a.mvs[i][2 * (cub + xy) + 1] = (int16_t)oy;
-                    a.mv_costs[i][cub + xy] = fcost;
+                    ring[li][yp][xp & 3] = (uint32_t)(uint16_t)ox | ((uint32_t)(uint16_t)oy << 16);
+                    mvs[2 * (cub + xy)] = (int16_t)ox;
+                    mvs[2 * (cub + xy) + 1] = (int16_t)oy;
+                    mvc[cub + xy] = cost;
                 }
-                if (fcost < bcost) { bcost = fcost; listused = i + 1; }
             }
-            // bidir: avg(l0 prediction, l1 prediction), then the co-located average (pixelavg_pp, bufSATD)
+            // ---- the other list's result (lane ^ 4 is the same quadrant of the partner quad)
+            const int pcost = __shfl_xor(cost, 4, 64), pox = __shfl_xor(ox, 4, 64), poy = __shfl_xor(oy, 4, 64);
+            const int c0 = li ? pcost : cost, c1 = li ? cost : pcost;
+            const int m0x = li ? pox : ox, m0y = li ? poy : oy, m1x = li ? ox : pox, m1y = li ? oy : poy;
+            int bcost = 1 << 28, listused = 0;
+            if (c0 < bcost) { bcost = c0; listused = 1; }
+            if (c1 < bcost) { bcost = c1; listused = 2; }
+            // ---- bidir (quad 0): avg of the two lists' lowresMC blocks; co-located (quad 1): avg of the
+            // full-pel planes (pixelavg_pp + bufSATD)
             constexpr uint32_t M = sizeof(P) == 1 ? 0x7f7f7f7fu : 0x7fff7fffu;
+            const P* const r0[4] = { rb[0][0] + off, rb[0][1] + off, rb[0][2] + off, rb[0][3] + off };
+            const P* const r1[4] = { rb[1][0] + off, rb[1][1] + off, rb[1][2] + off, rb[1][3] + off };
+            Quad<P> b0, b1;
+            if (li == 0)
             {
-                const P* const r0[4] = { rb[0][0] + off, rb[0][1] + off, rb[0][2] + off, rb[0][3] + off };
-                const P* const r1[4] = { rb[1][0] + off, rb[1][1] + off, rb[1][2] + off, rb[1][3] + off };
-                Quad<P> b0, b1;
-                qpel_block<P>(r0, ls, mx[0], my[0], b0);
-                qpel_block<P>(r1, ls, mx[1], my[1], b1);
-#pragma unroll
-                for (int y = 0; y < 4; y++)
-#pragma unroll
-                    for (int w = 0; w < Quad<P>::W; w++)
-                    {
-                        const uint32_t x = b0.r[y][w], z = b1.r[y][w];
-                        b0.r[y][w] = (x | z) - (((x ^ z) >> 1) & M);
-                    }
-                const int bi = satd_quad<P>(fe, b0);
-                if (bi < bcost) { bcost = bi; listused = 3; }
+                qpel_block<P>(r0, ls, m0x, m0y, b0);
+                qpel_block<P>(r1, ls, m1x, m1y, b1);
+            }
+            else
+            {
                 b0.load(r0[0], ls);
                 b1.load(r1[0], ls);
-#pragma unroll
-                for (int y = 0; y < 4; y++)
-#pragma unroll
-                    for (int w = 0; w < Quad<P>::W; w++)
-                    {
-                        const uint32_t x = b0.r[y][w], z = b1.r[y][w];
-                        b0.r[y][w] = (x | z) - (((x ^ z) >> 1) & M);
-                    }
-                const int co = satd_quad<P>(fe, b0);
-                if (co < bcost) { bcost = co; listused = 3; }
             }
+#pragma unroll
+            for (int y = 0; y < 4; y++)
+#pragma unroll
+                for (int w = 0; w < Quad<P>::W; w++)
+                {
+                    const uint32_t x = b0.r[y][w], z = b1.r[y][w];
+                    b0.r[y][w] = (x | z) - (((x ^ z) >> 1) & M);
+                }
+            const int mine = satd_quad<P>(fe, b0);
+            const int other = __shfl_xor(mine, 4, 64);
+            const int bi = li ? other : mine, co = li ? mine : other;
+            if (bi < bcost) { bcost = bi; listused = 3; }
+            if (co < bcost) { bcost = co; listused = 3; }
             bcost += 4;                                              // lowresPenalty
             const bool scored = (cx > 0 && cx < W - 1 && cy > 0 && cy < a.hcu - 1) || W <= 2 || a.hcu <= 2;
             const int bcost_aq = (scored && a.inv_q) ? ((bcost * a.inv_q[cub + xy] + 128) >> 8) : bcost;
-            if (lead)
+            if (lead && li == 0)
             {
                 if (scored) { est += bcost; est_aq += bcost_aq; }
                 rowsum[yp] += bcost_aq;
@@ -945,7 +949,7 @@ extern "C" int x265amd_lowres_bcost(int depth, const x265amd_lowres_bcost_batch*
                  b->row_satd, b->cost_est, b->n, b->width_cu, b->height_cu, rps, ns };
     const uint32_t blocks = (uint32_t)(b->n * ns);
     const int rmax = b->height_cu - rps * (ns - 1) > rps ? b->height_cu - rps * (ns - 1) : rps;
-    int nw = (rmax + 15) / 16;
+    int nw = (rmax + 7) / 8;                      // 8 lanes (two quads) per CU row
     nw = nw < 1 ? 1 : (nw > 16 ? 16 : nw);
     if (depth == 8) hipLaunchKernelGGL((k_lowres_bcost<uint8_t>), dim3(blocks), dim3(64 * nw), 0, st, a);
     else hipLaunchKernelGGL((k_lowres_bcost<uint16_t>), dim3(blocks), dim3(64 * nw), 0, st, a);

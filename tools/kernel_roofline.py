@@ -411,6 +411,50 @@ def main():
              "bound": "latency (serial CU wavefront per slice; one workgroup per slice, a 4-lane quad per CU row)"}
         results.append(r)
         print(json.dumps(r), flush=True)
+        # B estimates (p0, b, p1) = (f, f+1, f+2), both lists searched: 6 per call, and a b-adapt-2
+        # sized batch of 48 (every b between two frames up to 4 apart, repeated)
+        for nbb in (6, 48):
+            trip = [(f, f + 1, f + 2) for f in range(nf - 2)]
+            trip = (trip * ((nbb + len(trip) - 1) // len(trip)))[:nbb]
+            fob = torch.tensor([4 * b_ * psize + org for _, b_, _ in trip], dtype=torch.int64, device=dev)
+            r0b = torch.tensor([(4 * p_ + k) * psize + org for p_, _, _ in trip for k in range(4)], dtype=torch.int64,
+                               device=dev)
+            r1b = torch.tensor([(4 * p_ + k) * psize + org for _, _, p_ in trip for k in range(4)], dtype=torch.int64,
+                               device=dev)
+            DS = torch.ones(2 * nbb, dtype=torch.uint8, device=dev)
+            BM0 = torch.empty(2 * nbb * ncu, dtype=torch.int16, device=dev)
+            BM1 = torch.empty_like(BM0)
+            BC0 = torch.empty(nbb * ncu, dtype=torch.int32, device=dev)
+            BC1 = torch.empty_like(BC0)
+            BLC = torch.empty(nbb * ncu, dtype=torch.int16, device=dev)
+            BRS = torch.empty(nbb * g["hcu"], dtype=torch.int32, device=dev)
+            BCE = torch.empty(2 * nbb, dtype=torch.int64, device=dev)
+            ms_b = timeit(lambda: prims.lowres_bcost(8, nbb, g["wcu"], g["hcu"], rps, ns, PL, g["ls"], fob, r0b, r1b, DS,
+                                                     None, TAB.data_ptr() + 2 * MVCOST_RANGE, BM0, BC0, BM1, BC1, BLC,
+                                                     BRS, BCE))
+            r = {"kernel": f"lowres_bcost_{Hf}p_x{nbb}_slices{ns}", "jobs": nbb * ncu, "ms": round(ms_b, 4),
+                 "estimates_per_s": round(nbb / (ms_b * 1e-3), 1),
+                 "bound": "latency (serial CU wavefront per slice; two quads per CU search the two lists concurrently)"}
+            if nbb == 6:
+                try:
+                    import time as _t
+                    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+                    import pyoracle as _po
+                    RB = _po.LowresB("ref", 8)
+                    plh = PL[:12 * psize].cpu().numpy()
+                    tabh = TAB.cpu().numpy()
+                    z = lambda k, dt: np.zeros(k, dt)
+                    t0 = _t.perf_counter()
+                    RB.bcost(g["wcu"], g["hcu"], rps, ns, plh, g["ls"], 4 * psize + org,
+                             [k * psize + org for k in range(4)], [(8 + k) * psize + org for k in range(4)], None,
+                             tabh.ctypes.data + 2 * MVCOST_RANGE, 1, 1, z(2 * ncu, np.int16), z(ncu, np.int32),
+                             z(2 * ncu, np.int16), z(ncu, np.int32), z(ncu, np.uint16), z(g["hcu"], np.int32),
+                             z(2, np.int64))
+                    r["cpu_reference_1core_estimates_per_s"] = round(1.0 / (_t.perf_counter() - t0), 2)
+                except Exception as ex:
+                    r["cpu_reference_error"] = str(ex)
+            results.append(r)
+            print(json.dumps(r), flush=True)
         del SRC, PL, IC, IM, LC, RS, CE, IQ, MVS, MC, PLC, PRS, PCE, MB
     # ---------------------------------------------------------------- f2 motion search
     # HEX + subme 2 + merange 57 (--preset medium) on the synthetic 1080p pair (pan +2/+1, object, noise):
