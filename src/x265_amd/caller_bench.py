@@ -1,6 +1,6 @@
 """Caller-level rates for bench.py on the bench's own
 resolution and synthetic source: how fast the GPU runs, per frame, the lookahead's lowres
-pipeline (plane init, intra estimate, one P estimate), the main encoder's 2Nx2N motion search
+pipeline (plane init, intra estimate, one P estimate; B estimates separately), the main encoder's 2Nx2N motion search
 (HEX, subme 2, merange 57: --preset medium; every PU of 8x8 .. 64x64 against one reference) and
 the fused residual-coding chain for a frame's worth of TUs.  Informational: the census replay
 stays the headline workload.  Product path only (no oracle)."""
@@ -89,6 +89,20 @@ def caller_rates(prims, width: int, height: int, depth: int = 8, dev: str = "cud
     out["lookahead_lowres_frames_per_s"] = round(ne / (ms * 1e-3), 1)
     out["lookahead_note"] = (f"{nf} frames: lowres planes + intra estimate, {ne} P estimates "
                              f"({ns} coop slices of {rps} rows)")
+    # B estimates (p0, b, p1) = (f, f+1, f+2) on the same planes, both lists searched
+    nb = nf - 2
+    fob = po[4:4 * (nb + 1):4].contiguous()
+    r0b = po[:4 * nb].contiguous()
+    r1b = po[8:8 + 4 * nb].contiguous()
+    DS = torch.ones(2 * nb, dtype=torch.uint8, device=dev)
+    BM = [torch.empty(2 * nb * ncu, dtype=torch.int16, device=dev) for _ in range(2)]
+    BC = [torch.empty(nb * ncu, dtype=torch.int32, device=dev) for _ in range(2)]
+    BLC = torch.empty(nb * ncu, dtype=torch.int16, device=dev)
+    BRS = torch.empty(nb * hcu, dtype=torch.int32, device=dev)
+    BCE = torch.empty(2 * nb, dtype=torch.int64, device=dev)
+    ms = _time(lambda: prims.lowres_bcost(8, nb, wcu, hcu, rps, ns, PL, ls, fob, r0b, r1b, DS, None,
+                                          TAB.data_ptr() + 2 * (1 << 14), BM[0], BC[0], BM[1], BC[1], BLC, BRS, BCE))
+    out["lookahead_b_estimates_per_s"] = round(nb / (ms * 1e-3), 1)
     # ---- f2: every 2Nx2N PU of one frame (8 .. 64) against the previous frame, HEX / subme 2 / merange 57
     M = 96
     st = width + 2 * M
