@@ -40,17 +40,19 @@ using namespace X265_NS;
 namespace {
 
 EncoderPrimitives g_tab;
-bool g_init = false;
+pthread_once_t g_tab_once = PTHREAD_ONCE_INIT;
 
+void init_tab()
+{
+    memset(&g_tab, 0, sizeof(g_tab));
+    setupCPrimitives(g_tab);
+    setupAliasPrimitives(g_tab);
+}
+
+/* filled once, thread-safely: the CPU baseline calls in from many host threads at once */
 EncoderPrimitives& tab()
 {
-    if (!g_init)
-    {
-        memset(&g_tab, 0, sizeof(g_tab));
-        setupCPrimitives(g_tab);
-        setupAliasPrimitives(g_tab);
-        g_init = true;
-    }
+    pthread_once(&g_tab_once, init_tab);
     return g_tab;
 }
 
