@@ -130,11 +130,10 @@ def caller_rates(prims, width: int, height: int, depth: int = 8, dev: str = "cud
                          om=torch.empty(2 * n, dtype=torch.int16, device=dev),
                          oc=torch.empty(n, dtype=torch.int32, device=dev)))
 
-    def me():
-        for j in jobs:
-            prims.motion_search(8, j["s"], j["s"], 1, 2, 57, 2, F1, st, j["fo"], F0, st, j["fo"], j["rg"], j["mvp"],
-                                j["mvc"], j["nc"], TQ, j["to"], j["om"], j["oc"])
-    ms = _time(me)
+    multi = [dict(w=j["s"], h=j["s"], method=1, subme=2, merange=57, max_cand=2, f=F1, fs=st, fo=j["fo"], r=F0, rs=st,
+                  ro=j["fo"], rng=j["rg"], mvp=j["mvp"], mvc=j["mvc"], numc=j["nc"], tab=TQ, tab_off=j["to"],
+                  out_mv=j["om"], out_cost=j["oc"]) for j in jobs]
+    ms = _time(lambda: prims.motion_search_multi(8, multi))     # the four PU sizes in one call
     out["me_2Nx2N_frames_per_s"] = round(1.0 / (ms * 1e-3), 1)
     out["me_pus_per_frame"] = int(sum(j["n"] for j in jobs))
     # ---- f3: a frame's worth of 8x8 luma TUs through the fused residual-coding chain

@@ -170,6 +170,60 @@ inline int launch_grouped(int count, const int* cls, const BatchGroup& proto, Fi
     return 0;
 }
 
+// ---------------------------------------------------------------- fork / join
+// A call carrying several independent batches spreads their launches over up to kForkStreams
+// internal streams: they wait on an event recorded on the caller's stream, and the caller's stream
+// waits on their completion events, so stream order (and hipGraph capture) is preserved.  Streams
+// and events are created once per host thread and device.
+constexpr int kForkStreams = 4;
+
+struct ForkJoin
+{
+    hipStream_t origin = nullptr;
+    hipStream_t sub[kForkStreams] = {};
+    hipEvent_t fork = nullptr, done[kForkStreams] = {};
+    int n = 0;
+    hipError_t err = hipSuccess;
+
+    ForkJoin(hipStream_t st, int want)
+    {
+        origin = st;
+        if (want <= 1) return;                      // nothing to overlap: launch on the caller's stream
+        n = want > kForkStreams ? kForkStreams : want;
+        int dev = 0;
+        err = hipGetDevice(&dev);
+        struct Cache { hipStream_t s[kForkStreams]; hipEvent_t f, d[kForkStreams]; bool ok; };
+        static thread_local Cache cache[16] = {};
+        if (err != hipSuccess || dev < 0 || dev >= 16) { n = 0; return; }
+        Cache& c = cache[dev];
+        if (!c.ok)
+        {
+            for (int i = 0; i < kForkStreams && err == hipSuccess; i++)
+            {
+                err = hipStreamCreateWithFlags(&c.s[i], hipStreamNonBlocking);
+                if (err == hipSuccess) err = hipEventCreateWithFlags(&c.d[i], hipEventDisableTiming);
+            }
+            if (err == hipSuccess) err = hipEventCreateWithFlags(&c.f, hipEventDisableTiming);
+            if (err != hipSuccess) { n = 0; return; }
+            c.ok = true;
+        }
+        fork = c.f;
+        for (int i = 0; i < kForkStreams; i++) { sub[i] = c.s[i]; done[i] = c.d[i]; }
+        err = hipEventRecord(fork, origin);
+        for (int i = 0; i < n && err == hipSuccess; i++) err = hipStreamWaitEvent(sub[i], fork, 0);
+    }
+    hipStream_t stream(int k) const { return n ? sub[k % n] : origin; }
+    hipError_t join()
+    {
+        for (int i = 0; i < n && err == hipSuccess; i++)
+        {
+            err = hipEventRecord(done[i], sub[i]);
+            if (err == hipSuccess) err = hipStreamWaitEvent(origin, done[i], 0);
+        }
+        return err;
+    }
+};
+
 // ---------------------------------------------------------------- loads
 // Unaligned little-endian loads (gfx950 runs HSA in unaligned mode: these
 // lower to single global_load_dword{,x2,x4}).

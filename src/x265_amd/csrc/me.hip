@@ -712,10 +712,18 @@ extern "C" int x265amd_motion_search(int depth, int count, const x265amd_me_batc
             return X265AMD_EINVAL;
     }
     hipStream_t st = (hipStream_t)stream;
+    int live = 0;
+    for (int i = 0; i < count; i++) live += bt[i].n > 0;
+    // batches of different PU sizes are independent: they run concurrently on internal streams
+    // joined back into `stream` (a latency-bound 64x64 search overlaps the small-PU batches)
+    ForkJoin fj(st, live);
+    if (fj.err != hipSuccess) return (int)fj.err;
+    int k = 0;
     for (int i = 0; i < count; i++)
     {
         const x265amd_me_batch& b = bt[i];
         if (!b.n) continue;
+        const hipStream_t bs = fj.stream(k++);
         const int units = (b.w / 4) * (b.h / 4);
         int g = 4, lg = 2;                               // groups of at least 4 lanes (fewer kernel variants)
         while (g < units && g < 64) { g <<= 1; lg++; }
@@ -724,8 +732,8 @@ extern "C" int x265amd_motion_search(int depth, int count, const x265amd_me_batc
                   b.mvp, b.mvc, b.num_cand, b.mvcost, b.mvcost_off, b.out_mv, b.out_cost, b.fenc_cb, b.fenc_cr,
                   (int64_t)b.fenc_cstride, b.fenc_coff, b.ref_cb, b.ref_cr, (int64_t)b.ref_cstride, b.ref_coff,
                   b.w, b.h, b.n, lg, b.method, b.subme, b.merange, b.max_cand, depth };
-        const int rc = depth == 8 ? launch_me<uint8_t>(a, st) : launch_me<uint16_t>(a, st);
-        if (rc) return rc;
+        const int rc = depth == 8 ? launch_me<uint8_t>(a, bs) : launch_me<uint16_t>(a, bs);
+        if (rc) { fj.join(); return rc; }
     }
-    return 0;
+    return (int)fj.join();
 }

@@ -302,6 +302,18 @@ class Primitives:
                          _addr(rcr), rcs, _addr(rco))
         self._check(self.lib.x265amd_motion_search(depth, 1, arr, stream or _stream()), "motion_search")
 
+    def motion_search_multi(self, depth, jobs, stream=None):
+        """several batches (one per PU size) in ONE call: they run concurrently on the library's
+        internal streams, joined back into `stream`.  jobs: dicts of motion_search's arguments."""
+        arr = (MeBatch * len(jobs))()
+        for i, j in enumerate(jobs):
+            arr[i] = MeBatch(j["w"], j["h"], j["fo"].numel(), j["method"], j["subme"], j["merange"], j["max_cand"],
+                             _addr(j["f"]), j["fs"], _addr(j["fo"]), _addr(j["r"]), j["rs"], _addr(j["ro"]),
+                             _addr(j["rng"]), _addr(j["mvp"]), _addr(j["mvc"]), _addr(j["numc"]), _addr(j["tab"]),
+                             _addr(j["tab_off"]), _addr(j["out_mv"]), _addr(j["out_cost"]), None, None, 0, None, None,
+                             None, 0, None)
+        self._check(self.lib.x265amd_motion_search(depth, len(jobs), arr, stream or _stream()), "motion_search")
+
     # -- f4 loop filters and border extension (frame descriptors: SaoFrame, SaoStatsFrame,
     #    DeblockFrame, BorderPlane with device addresses)
     def _frames(self, entry, what, depth, frames, stream):

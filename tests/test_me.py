@@ -48,3 +48,31 @@ def test_me_gpu_matches_oracle(gpu_prims, oracle_libs, depth):
             if not np.array_equal(got[k], exp[k]):
                 bad.append((c.key(), k, int((got[k] != exp[k]).sum())))
     assert not bad, bad[:6]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("depth", [8, 10])
+def test_me_gpu_multi_batch_call(gpu_prims, oracle_libs, depth):
+    """Several PU sizes in ONE x265amd_motion_search call (they run concurrently on the library's
+    internal streams, joined back into the caller's stream): every batch equals the oracle."""
+    import torch
+
+    orc = CpuOracle("oracle", depth)
+    cases = [case_me(w, h, m, 2, 57, depth, 384, seed_of("me-m", depth, w, h, m))
+             for (w, h, m) in ((8, 8, 1), (16, 16, 0), (32, 32, 1), (64, 64, 2), (12, 16, 1), (64, 16, 1))]
+    dv = lambda v: torch.from_numpy(np.ascontiguousarray(v)).cuda() if isinstance(v, np.ndarray) else v
+    jobs, keep = [], []
+    for c in cases:
+        b = {k: dv(v) for k, v in c.bufs.items()}
+        p = c.params
+        jobs.append(dict(w=p["w"], h=p["h"], method=p["method"], subme=p["subme"], merange=p["merange"],
+                         max_cand=p["max_cand"], f=b["f"], fs=b["fs"], fo=b["fo"], r=b["r"], rs=b["rs"], ro=b["ro"],
+                         rng=b["rng"], mvp=b["mvp"], mvc=b["mvc"], numc=b["numc"], tab=b["tab"], tab_off=b["tab_off"],
+                         out_mv=b["out_mv"], out_cost=b["out_cost"]))
+        keep.append(b)
+    gpu_prims.motion_search_multi(depth, jobs)
+    torch.cuda.synchronize()
+    for c, b in zip(cases, keep):
+        exp = run_cpu(c, orc)
+        for k in c.outs:
+            np.testing.assert_array_equal(b[k].cpu().numpy(), exp[k])
