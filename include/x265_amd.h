@@ -475,8 +475,8 @@ int x265amd_lowres_bcost(int depth, const x265amd_lowres_bcost_batch* batch, voi
  * the clipped MVP measured at sub-pel (SAD, no MV cost), the num_cand[i] extra
  * candidates (AMVP list), DIA (method 0), HEX (method 1, --preset medium) or STAR
  * (method 2, --preset slow) integer search within merange, then the sub-pel refine
- * of workload[subme] for subme 0..3 (subme 3 adds the 4:2:0 chroma SATD when the
- * chroma planes are given).  fenc_off[i] / ref_off[i] = the PU origin in the
+ * of workload[subme] for subme 0..7 (motion.cpp:48-58; from subme 3 the 4:2:0
+ * chroma SATD is added when the chroma planes are given).  fenc_off[i] / ref_off[i] = the PU origin in the
  * source / reference plane (the reference is border-extended as PicYuv is);
  * mv_range[4 i ..] = mvmin.x, mvmin.y, mvmax.x, mvmax.y (full-pel); mvp[2 i ..]
  * and the candidates mvc[2 (i max_cand + k) ..] are quarter-pel; mvcost +
@@ -503,7 +503,7 @@ typedef struct
     const int64_t* mvcost_off;
     int16_t* out_mv;
     int32_t* out_cost;
-    /* subme 3 only: 4:2:0 chroma of source and reference (NULL = luma only); *_coff[i] = the
+    /* subme >= 3 only: 4:2:0 chroma of source and reference (NULL = luma only); *_coff[i] = the
      * PU's chroma origin.  Chroma SATD is added exactly where bChromaSATD adds it
      * (motion.cpp:183-197, 1205-1266): chroma PU dims multiples of 4. */
     const void* fenc_cb;

@@ -1383,8 +1383,8 @@ void xo_lowres_bcost(int wcu, int hcu, int rows_per_slice, int num_slices, const
 /* ---------------------------------------------------------------- f2: full-resolution motion search
  * MotionEstimate::motionEstimate (motion.cpp:571-1172) for one PU on a full-resolution
  * reference: clipped MVP measured at sub-pel with SAD, the extra MV candidates, DIA or HEX
- * integer search, then the sub-pel refine of workload[subme] for subme 0..2 (luma only:
- * chroma SATD starts at subme 3, motion.cpp:197).  Sub-pel blocks come from the 8-tap luma
+ * integer search, then the sub-pel refine of workload[subme] for subme 0..7 (motion.cpp:48-58;
+ * chroma SATD from subme 3, motion.cpp:197).  Sub-pel blocks come from the 8-tap luma
  * filters exactly as subpelCompare (motion.cpp:1174-1203) builds them. */
 
 typedef struct
@@ -1564,7 +1564,8 @@ int xo_motion_search(int w, int h, int method, int subme, int merange, const voi
     static const int mod6m1[8] = { 5, 0, 1, 2, 3, 4, 5, 0 };
     static const xmv square1[9] = { { 0, 0 }, { 0, -1 }, { 0, 1 }, { -1, 0 }, { 1, 0 }, { -1, -1 }, { -1, 1 }, { 1, -1 }, { 1, 1 } };
     /* workload[] (motion.cpp:48-58): hpel_iters, hpel_dirs, qpel_iters, qpel_dirs, hpel_satd */
-    static const int wl[4][5] = { { 1, 4, 0, 4, 0 }, { 1, 4, 1, 4, 0 }, { 1, 4, 1, 4, 1 }, { 2, 4, 1, 4, 1 } };
+    static const int wl[8][5] = { { 1, 4, 0, 4, 0 }, { 1, 4, 1, 4, 0 }, { 1, 4, 1, 4, 1 }, { 2, 4, 1, 4, 1 },
+                                  { 2, 4, 2, 4, 1 }, { 1, 8, 1, 8, 1 }, { 2, 8, 1, 8, 1 }, { 2, 8, 2, 8, 1 } };
     static const xmv offs[16] = { { -1, 0 }, { 0, -1 }, { -1, -1 }, { 1, -1 }, { -1, 0 }, { 1, 0 }, { -1, 1 }, { -1, -1 },
                                   { 1, -1 }, { 1, 1 }, { -1, 0 }, { 0, 1 }, { -1, 1 }, { 1, 1 }, { 1, 0 }, { 0, 1 } };
     XoMeF m = { w, h, (const pix*)fenc, fs, (const pix*)ref, rs, tab_centre, { mvpx, mvpy }, 0,

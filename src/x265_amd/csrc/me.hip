@@ -1,9 +1,9 @@
 // me.hip — batched full-resolution motion search.
 //
 // One job = one MotionEstimate::motionEstimate call (motion.cpp:571-1172) for a
-// PU on a full-resolution reference, luma only (subme 0..2, the levels that
-// never add chroma SATD, motion.cpp:197): the clipped MVP measured at sub-pel
-// with SAD, the caller's extra MV candidates, DIA or HEX integer search, then
+// PU on a full-resolution reference at subme 0..7 (from subme 3 the sub-pel
+// compare adds the 4:2:0 chroma SATD, motion.cpp:197): the clipped MVP measured at sub-pel
+// with SAD, the caller's extra MV candidates, DIA / HEX / STAR integer search, then
 // the sub-pel refine of workload[subme] whose blocks come from the 8-tap luma
 // filters exactly as subpelCompare builds them (motion.cpp:1174-1203;
 // ipfilter.cpp interp_horiz_pp / interp_vert_pp / interp_hv_pp).
@@ -383,6 +383,15 @@ __device__ __noinline__ int subpel_cost(const MeState<P>& s, int qx, int qy, boo
     return group_sum<G>(acc);
 }
 
+// workload[subme] of motion.cpp:48-58 as {hpel_iters, hpel_dirs, qpel_iters, qpel_dirs}, one
+// nibble each per level (subme is wave-uniform: a batch has one level)
+__device__ __forceinline__ int4 subpel_workload(int subme)
+{
+    constexpr uint32_t kTab[8] = { 0x4041, 0x4141, 0x4141, 0x4142, 0x4242, 0x8181, 0x8182, 0x8282 };
+    const uint32_t v = kTab[subme & 7];
+    return make_int4(v & 15, (v >> 4) & 15, (v >> 8) & 15, v >> 12);
+}
+
 template <typename P, int G>
 __global__ __launch_bounds__(X265AMD_BLOCK) void k_motion_search(const MeArgs a)
 {
@@ -634,20 +643,18 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_motion_search(const MeArgs a)
     int qx, qy;
     if (bprecost < bcost) { qx = bpx; qy = bpy; bcost = bprecost; }
     else { qx = 4 * bx; qy = 4 * by; }
-    // workload[subme] (motion.cpp:48-58): hpel_iters 1 (2 at subme 3), dirs 4; qpel_iters 0/1/1/1, dirs 4;
-    // hpel_satd from subme 2
+    // workload[subme] (motion.cpp:48-58): {hpel_iters, hpel_dirs, qpel_iters, qpel_dirs, hpel_satd}
+    const int4 wl = subpel_workload(a.subme);
     const bool hsatd = a.subme >= 2;
-    const int qiters = a.subme >= 1 ? 1 : 0;
-    const int hiters = a.subme >= 3 ? 2 : 1;
     if (!bcost)
         bcost = s.mvcost(qx, qy);
     else
     {
         if (hsatd) bcost = subpel_cost<P, G>(s, qx, qy, true) + s.mvcost(qx, qy);
-        for (int it = 0; it < hiters; it++)
+        for (int it = 0; it < wl.x; it++)
         {
             int bdir = 0;
-            for (int i = 1; i <= 4; i++)
+            for (int i = 1; i <= wl.y; i++)
             {
                 const int tx = qx + 2 * sq_dx(i), ty = qy + 2 * sq_dy(i);
                 const int c = subpel_cost<P, G>(s, tx, ty, hsatd) + s.mvcost(tx, ty);
@@ -657,10 +664,10 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_motion_search(const MeArgs a)
             qx += 2 * sq_dx(bdir); qy += 2 * sq_dy(bdir);
         }
         if (!hsatd) bcost = subpel_cost<P, G>(s, qx, qy, true) + s.mvcost(qx, qy);
-        for (int it = 0; it < qiters; it++)
+        for (int it = 0; it < wl.z; it++)
         {
             int bdir = 0;
-            for (int i = 1; i <= 4; i++)
+            for (int i = 1; i <= wl.w; i++)
             {
                 const int tx = qx + sq_dx(i), ty = qy + sq_dy(i);
                 const int c = subpel_cost<P, G>(s, tx, ty, true) + s.mvcost(tx, ty);
@@ -704,7 +711,7 @@ extern "C" int x265amd_motion_search(int depth, int count, const x265amd_me_batc
     {
         const x265amd_me_batch& b = bt[i];
         if (b.n < 0 || b.w < 4 || b.h < 4 || b.w > 64 || b.h > 64 || (b.w & 3) || (b.h & 3)) return X265AMD_EINVAL;
-        if (b.method < 0 || b.method > 2 || b.subme < 0 || b.subme > 3 || b.merange < 1) return X265AMD_EINVAL;
+        if (b.method < 0 || b.method > 2 || b.subme < 0 || b.subme > 7 || b.merange < 1) return X265AMD_EINVAL;
         if (b.n && b.fenc_cb && (!b.fenc_cr || !b.fenc_coff || !b.ref_cb || !b.ref_cr || !b.ref_coff))
             return X265AMD_EINVAL;
         if (b.n && (!b.fenc || !b.fenc_off || !b.ref || !b.ref_off || !b.mv_range || !b.mvp || !b.mvcost ||

@@ -635,6 +635,10 @@ def me_cases(depth: int, n: int = 24):
     # --preset slow: STAR search, subme 3 (chroma SATD in the sub-pel compare), every luma PU shape
     for (w, h) in LUMA_PU[1:]:
         out.append(case_me(w, h, 2, 3, 57, depth, n // 2, seed_of(depth, "me-star", w, h)))
+    # --preset slower / veryslow / placebo sub-pel levels: 2x4 qpel, 8-direction square refine
+    for (w, h) in ((8, 8), (16, 8), (32, 32), (64, 16)):
+        for method, subme in ((2, 4), (1, 5), (2, 6), (2, 7)):
+            out.append(case_me(w, h, method, subme, 57, depth, n // 2, seed_of(depth, "me-sub", w, h, subme)))
     return out
 
 

@@ -18,7 +18,7 @@ from pyoracle import CpuOracle, available
 def test_me_oracle_matches_reference(oracle_libs, depth):
     orc, ref = CpuOracle("oracle", depth), CpuOracle("ref", depth)
     for (w, h) in ((8, 8), (16, 16), (64, 64), (32, 8), (12, 16)):
-        for method, subme in ((1, 2), (0, 1)):
+        for method, subme in ((1, 2), (0, 1), (2, 3), (2, 4), (1, 5), (2, 6), (2, 7)):
             c = case_me(w, h, method, subme, 57 if method else 16, depth, 64, seed_of("me-r", depth, w, h, method))
             a, b = run_cpu(c, orc), run_cpu(c, ref)
             for k in c.outs:
