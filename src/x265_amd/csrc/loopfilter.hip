@@ -50,7 +50,16 @@ constexpr int kDbkFrames = 16;
 constexpr int kStatFrames = 24;
 
 __device__ __forceinline__ int clip3(int lo, int hi, int v) { return v < lo ? lo : (v > hi ? hi : v); }
-__device__ __forceinline__ int sgn(int v) { return (v > 0) - (v < 0); }
+// sign as one v_med3_i32 (clamp to [-1, 1]); written as asm because the compiler turns
+// (v > 0) - (v < 0) and min / max of a difference back into two compares and selects
+__device__ __forceinline__ int sgn(int v)
+{
+    int r;
+    asm("v_med3_i32 %0, %1, -1, 1" : "=v"(r) : "v"(v));
+    return r;
+}
+// the compare form, kept where it measured faster (SAO apply: its selects fold into the offset pick)
+__device__ __forceinline__ int sgn_cmp(int v) { return (v > 0) - (v < 0); }
 __device__ __forceinline__ int iabs(int v) { return v < 0 ? -v : v; }
 
 // which frame of the launch a logical block belongs to (uniform scan, as group_sub)
@@ -439,7 +448,7 @@ __global__ __launch_bounds__(64) void k_sao_apply(const SaoLaunch L)
                 const int v = mid[i + 1];
                 const int na = type == 0 ? mid[i] : (dxa < 0 ? up[i] : (dxa > 0 ? up[i + 2] : up[i + 1]));
                 const int nb = type == 0 ? mid[i + 2] : (dxb < 0 ? dn[i] : (dxb > 0 ? dn[i + 2] : dn[i + 1]));
-                const int e = sgn(v - na) + sgn(v - nb) + 2;
+                const int e = sgn_cmp(v - na) + sgn_cmp(v - nb) + 2;
                 const int off = e == 0 ? o0 : e == 1 ? o1 : e == 3 ? o2 : e == 4 ? o3 : 0;
                 const int x = x0 + i;
                 const bool skip = skip_row || (type != 1 && (x == 0 || x == pw - 1));
@@ -491,7 +500,7 @@ __global__ __launch_bounds__(64) void k_sao_stats(const StatLaunch L)
 {
     __shared__ int32_t eo_sum[3][4][5], eo_cnt[3][4][5];
     __shared__ unsigned long long bo[3][32];
-    __shared__ int32_t bins[64][21];              // per lane: [EO type][edge type] (sum << 7) + count
+    __shared__ int32_t bins[64][21];              // per lane: [EO type][edge type] (sum << 7) + count; [20] sink
     const uint32_t b = xcd_block();
     const StatFrame& f = L.f[frame_of<kStatFrames>(L, b)];
     const uint32_t c = b - f.block0;
@@ -544,11 +553,27 @@ __global__ __launch_bounds__(64) void k_sao_stats(const StatLaunch L)
             int up[10], mid[10], dn[10];
             load_row10<P>(r - rs, up);
             load_row10<P>(r, mid);
+            // signs against the row above for EO_1 / EO_2 / EO_3: after the first row they are the
+            // negated signs against the row below of the previous row (sao.cpp's signUp buffers)
+            int u1[8], u2[8], u3[8];
+#pragma unroll
+            for (int i = 0; i < 8; i++)
+            {
+                u1[i] = sgn(mid[i + 1] - up[i + 1]);
+                u2[i] = sgn(mid[i + 1] - up[i]);
+                u3[i] = sgn(mid[i + 1] - up[i + 2]);
+            }
 #pragma unroll
             for (int yy = 0; yy < 8; yy++)
             {
                 if (yy >= rows) break;
                 load_row10<P>(r + (yy + 1) * rs, dn);
+                int h[9];                 // EO_0: sign of each pixel against its left neighbour
+#pragma unroll
+                for (int k = 0; k < 9; k++) h[k] = sgn(mid[k + 1] - mid[k]);
+                int n1[8], n2[8], n3[8];
+                n2[0] = sgn(dn[1] - mid[0]);
+                n3[7] = sgn(dn[8] - mid[9]);
                 int fv[8];
                 load_row<P, 8>(fe + yy * fs, fv);
                 const int ly = ly0 + yy;
@@ -562,11 +587,18 @@ __global__ __launch_bounds__(64) void k_sao_stats(const StatLaunch L)
                 {
                     const int v = mid[i + 1], d = fv[i] - v;
                     const int val = (d << 7) + 1;
-                    const int e[4] = { sgn(v - mid[i]) + sgn(v - mid[i + 2]), sgn(v - up[i + 1]) + sgn(v - dn[i + 1]),
-                                       sgn(v - up[i]) + sgn(v - dn[i + 2]), sgn(v - up[i + 2]) + sgn(v - dn[i]) };
+                    const int d1 = sgn(v - dn[i + 1]), d2 = sgn(v - dn[i + 2]), d3 = sgn(v - dn[i]);
+                    const int e[4] = { h[i] - h[i + 1], u1[i] + d1, u2[i] + d2, u3[i] + d3 };
+                    n1[i] = -d1;
+                    if (i < 7) n2[i + 1] = -d2;
+                    if (i > 0) n3[i - 1] = -d3;
 #pragma unroll
                     for (int t = 0; t < 4; t++)
-                        if ((m[t] >> i) & 1) atomicAdd(&bins[lane][5 * t + e[t] + 2], val);
+                    {
+                        // masked-off pixels go to the sink bin 20: no branch around the ds_add
+                        const int bi = ((m[t] >> i) & 1) ? 5 * t + e[t] + 2 : 20;
+                        atomicAdd(&bins[lane][bi], val);
+                    }
                     if ((m[4] >> i) & 1)
                     {
                         const int band = v >> L.bo_shift;
@@ -581,7 +613,9 @@ __global__ __launch_bounds__(64) void k_sao_stats(const StatLaunch L)
                 }
                 if (run_band >= 0) atomicAdd(&bo[p][run_band], run);
 #pragma unroll
-                for (int i = 0; i < 10; i++) { up[i] = mid[i]; mid[i] = dn[i]; }
+                for (int i = 0; i < 8; i++) { u1[i] = n1[i]; u2[i] = n2[i]; u3[i] = n3[i]; }
+#pragma unroll
+                for (int i = 0; i < 10; i++) mid[i] = dn[i];
             }
         }
         __syncthreads();
