@@ -1,0 +1,56 @@
+/* hip_encoder_main.cpp — TEST/MEASUREMENT INFRASTRUCTURE: the reference x265 1.9
+ * CLI and encoder (compiled where they lie under /root/reference, see
+ * oracle/Makefile x265hip) with the MI355X provider installed in the global
+ * primitive table, i.e. the INTEGRATION.md §1 patch applied from outside:
+ *
+ *   x265_setup_primitives (primitives.cpp:228-249) = setupCPrimitives, allangs
+ *   NULL, [asm providers], setupAliasPrimitives, guarded by
+ *   `if (!primitives.pu[0].sad)` (primitives.cpp:230).
+ *
+ * Before the CLI's main runs, this fills `x265::primitives` the same way with
+ * the MI355X provider (x265amd_setup_primitives, include/x265_amd.h) in the
+ * place of the assembly providers; the encoder's own once-only guard then leaves
+ * the table alone, so x265_encoder_open / x265_encoder_encode (api.cpp:182) run
+ * every primitive the provider implements on the GPU.
+ *
+ *   X265AMD_PROVIDER=c    keeps the plain C table (same binary, CPU reference)
+ *   X265AMD_PROVIDER=hip  (default) MI355X provider
+ *
+ * Prints "[x265hip] provider=<c|hip> entries=<n>" on stderr before encoding.
+ */
+#include "common.h"
+#include "primitives.h"
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+
+extern "C" int x265amd_setup_primitives(void* table, int depth, int* overridden);
+extern "C" const char* x265amd_strerror(int status);
+
+using namespace X265_NS;
+
+int x265_cli_main(int argc, char** argv);
+
+int main(int argc, char** argv)
+{
+    const char* which = getenv("X265AMD_PROVIDER");
+    const bool hip = !(which && !strcmp(which, "c"));
+    EncoderPrimitives& p = primitives;
+    setupCPrimitives(p);
+    for (int i = 0; i < NUM_TR_SIZE; i++)
+        p.cu[i].intra_pred_allangs = NULL;
+    int n = 0;
+    if (hip)
+    {
+        int rc = x265amd_setup_primitives(&p, X265_DEPTH, &n);
+        if (rc)
+        {
+            fprintf(stderr, "[x265hip] x265amd_setup_primitives failed: %s\n", x265amd_strerror(rc));
+            return 3;
+        }
+    }
+    setupAliasPrimitives(p);
+    fprintf(stderr, "[x265hip] provider=%s entries=%d depth=%d\n", hip ? "hip" : "c", n, X265_DEPTH);
+    return x265_cli_main(argc, argv);
+}

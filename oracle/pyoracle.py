@@ -17,6 +17,8 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
+# X265AMD_ORACLE_DIR=_build_asan selects the ASan/UBSan build (oracle/Makefile asan)
+BUILD = os.environ.get("X265AMD_ORACLE_DIR", "_build")
 
 _vp, _i64, _ip = C.c_void_p, C.c_int64, C.c_ssize_t
 
@@ -24,14 +26,14 @@ _vp, _i64, _ip = C.c_void_p, C.c_int64, C.c_ssize_t
 def lib_path(kind: str, depth: int) -> str:
     d = 8 if depth == 8 else 10
     if kind == "oracle":
-        return os.path.join(HERE, "_build", f"liboracle{d}.so")
+        return os.path.join(HERE, BUILD, f"liboracle{d}.so")
     if kind == "ref":
         return os.path.join(HERE, "_ref", f"libx265ref{d}.so")
     raise ValueError(kind)
 
 
 def available(kind: str, depth: int = 8) -> bool:
-    return os.path.exists(lib_path(kind, depth)) and os.path.exists(os.path.join(HERE, "_build", "libcpubatch.so"))
+    return os.path.exists(lib_path(kind, depth)) and os.path.exists(os.path.join(HERE, BUILD, "libcpubatch.so"))
 
 
 def _p(a):
@@ -43,7 +45,7 @@ class CpuOracle:
 
     def __init__(self, kind: str, depth: int):
         if CpuOracle._cb is None:
-            cb = C.CDLL(os.path.join(HERE, "_build", "libcpubatch.so"))
+            cb = C.CDLL(os.path.join(HERE, BUILD, "libcpubatch.so"))
             cb.cb_open.restype = _vp
             cb.cb_open.argtypes = [C.c_char_p]
             CpuOracle._cb = cb

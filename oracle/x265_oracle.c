@@ -20,6 +20,11 @@
 #include <stdlib.h>
 #include <string.h>
 
+/* the reference's int arithmetic, defined for every input: two's-complement wrap
+   of the product, and << of a negative value as the arithmetic shift g++ emits */
+static inline int32_t mul_wrap(int32_t a, int32_t b) { return (int32_t)((uint32_t)a * (uint32_t)b); }
+static inline int32_t shl_wrap(int32_t a, int s) { return (int32_t)((uint32_t)a << s); }
+
 #ifndef XO_DEPTH
 #define XO_DEPTH 8
 #endif
@@ -344,7 +349,7 @@ void xo_interp(int op, int taps, int w, int h, const void* src_, intptr_t ss, vo
         for (int y = 0; y < h; y++, sp += ss, d16 += ds)
             for (int x = 0; x < w; x++)
             {
-                int16_t v = (int16_t)(sp[x] << head);
+                int16_t v = (int16_t)shl_wrap(sp[x], head);
                 d16[x] = (int16_t)(v - (int16_t)IF_OFFS);
             }
         return;
@@ -477,6 +482,7 @@ void xo_dequant_normal(const int16_t* q, int16_t* coef, int num, int scale, int 
     for (int i = 0; i < num; i++) coef[i] = (int16_t)clip16((q[i] * scale + add) >> shift);
 }
 
+
 /* dct.cpp:636-662 */
 void xo_dequant_scaling(const int16_t* q, const int32_t* dq, int16_t* coef, int num, int per, int shift)
 {
@@ -484,10 +490,10 @@ void xo_dequant_scaling(const int16_t* q, const int32_t* dq, int16_t* coef, int 
     if (shift > per)
     {
         const int add = 1 << (shift - per - 1);
-        for (int i = 0; i < num; i++) coef[i] = (int16_t)clip16((q[i] * dq[i] + add) >> (shift - per));
+        for (int i = 0; i < num; i++) coef[i] = (int16_t)clip16((int32_t)((uint32_t)mul_wrap(q[i], dq[i]) + (uint32_t)add) >> (shift - per));
     }
     else
-        for (int i = 0; i < num; i++) coef[i] = (int16_t)clip16(clip16(q[i] * dq[i]) << (per - shift));
+        for (int i = 0; i < num; i++) coef[i] = (int16_t)clip16(shl_wrap(clip16(mul_wrap(q[i], dq[i])), per - shift));
 }
 
 /* ======================================================= intra */
@@ -694,7 +700,7 @@ void xo_blockfill_s(int n, int16_t* d, intptr_t ds, int16_t v)
 void xo_cpy2Dto1D_shl(int n, int16_t* d, const int16_t* s, intptr_t ss, int shift)
 {
     for (int y = 0; y < n; y++)
-        for (int x = 0; x < n; x++) d[y * n + x] = (int16_t)(s[y * ss + x] << shift);
+        for (int x = 0; x < n; x++) d[y * n + x] = (int16_t)shl_wrap(s[y * ss + x], shift);
 }
 
 void xo_cpy2Dto1D_shr(int n, int16_t* d, const int16_t* s, intptr_t ss, int shift)
@@ -707,7 +713,7 @@ void xo_cpy2Dto1D_shr(int n, int16_t* d, const int16_t* s, intptr_t ss, int shif
 void xo_cpy1Dto2D_shl(int n, int16_t* d, const int16_t* s, intptr_t ds, int shift)
 {
     for (int y = 0; y < n; y++)
-        for (int x = 0; x < n; x++) d[y * ds + x] = (int16_t)(s[y * n + x] << shift);
+        for (int x = 0; x < n; x++) d[y * ds + x] = (int16_t)shl_wrap(s[y * n + x], shift);
 }
 
 void xo_cpy1Dto2D_shr(int n, int16_t* d, const int16_t* s, intptr_t ds, int shift)

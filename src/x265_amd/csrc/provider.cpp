@@ -300,9 +300,15 @@ void denoise(int16_t* coef, uint32_t* res_sum, const uint16_t* offset, int num)
 }
 
 // ------------------------------------------------------------------ intra
-template <int N>
+// SLOT: the table slot's mode (0 planar, 1 DC) or -1 for the angular slots.  The
+// reference's planar_pred_c / intra_pred_dc_c ignore the dirMode argument
+// (intrapred.cpp:69,87: TestBench passes 0 to the DC slot, intrapredharness.cpp:62)
+// and planar ignores bFilter too; intra_pred_ang_c uses the dirMode it is given.
+template <int N, int SLOT>
 void intra_pred(pixel* dst, intptr_t ds, const pixel* src, int mode, int bFilter)
 {
+    if (SLOT >= 0) mode = SLOT;
+    if (SLOT == 0) bFilter = 0;
     Ctx& c = ctx();
     c.reset();
     const size_t z = stage_value<int64_t>(c, 0);
@@ -496,7 +502,9 @@ void luma_cu(EncoderPrimitives::CU& u)
         put(u.dct, &dct<N>);
         put(u.idct, &idct<N>);
         put(u.intra_filter, &intra_filter<N>);
-        for (int m = 0; m < NUM_INTRA_MODE; m++) put(u.intra_pred[m], &intra_pred<N>);
+        put(u.intra_pred[0], &intra_pred<N, 0>);
+        put(u.intra_pred[1], &intra_pred<N, 1>);
+        for (int m = 2; m < NUM_INTRA_MODE; m++) put(u.intra_pred[m], &intra_pred<N, -1>);
         constexpr int L = N == 4 ? 2 : N == 8 ? 3 : N == 16 ? 4 : 5;
         put(u.intra_pred_allangs, &allangs<L>);
         put(u.count_nonzero, &count_nonzero<N>);
