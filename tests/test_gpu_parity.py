@@ -72,21 +72,31 @@ def test_gpu_matches_oracle_random(prims, oracle_libs, depth):
     assert not bad, bad[:10]
 
 
-def test_gpu_fullsize_frame_batch(prims, oracle_libs):
-    """Bench-sized batch on 1080p planes: sampled exact parity + properties."""
+CENSUSES = [("census_1080p_medium.json", 1920, 1080, 8), ("census_2160p_medium.json", 3840, 2160, 8),
+            ("census_2160p_slow.json", 3840, 2160, 8), ("census_2160p_medium_main10.json", 3840, 2160, 10)]
+
+
+@pytest.mark.parametrize("census_file,width,height,depth", CENSUSES, ids=[c[0][7:-5] for c in CENSUSES])
+def test_gpu_fullsize_frame_batch(prims, oracle_libs, census_file, width, height, depth):
+    """Every batch of a recorded census (BASELINE configs 2, 3 and 5: 1080p medium, 2160p
+    medium, 2160p slow with rect PUs / nquant, 2160p Main10) on full-size planes, issued
+    through the bench's grouped launches: sampled exact parity of every batch against the
+    oracle + properties."""
     import torch
 
-    from src.x265_amd.workload import FrameSet, census_batches
+    from src.x265_amd.workload import FrameSet, census_batches, group_launches, load_census
 
-    fs = FrameSet(1920, 1080, nframes=2, depth=8, device="cuda")
-    orc = CpuOracle("oracle", 8)
+    census = load_census(os.path.join(os.path.dirname(__file__), "golden", census_file))
+    fs = FrameSet(width, height, nframes=2, depth=depth, device="cuda")
+    orc = CpuOracle("oracle", depth)
     orc.nthreads = 8
-    batches, wb = census_batches(fs, frames=2, scale=1.0)
+    batches, wb = census_batches(fs, frames=2, census=census)
     assert len(batches) > 100
+    for g in group_launches(batches):
+        g.run(prims)
+    torch.cuda.synchronize()
     bad = []
     for b in batches:
-        b.run(prims)
-        torch.cuda.synchronize()
         mism = b.verify_sample(orc, fs.host, b.sample(48))
         if mism:
             bad.append((b.name, mism))

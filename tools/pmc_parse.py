@@ -23,7 +23,7 @@ import os
 
 def dispatches(d: str, counter: str):
     rows = []
-    for path in glob.glob(os.path.join(d, "*counter_collection.csv")):
+    for path in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         with open(path) as f:
             for r in csv.DictReader(f):
                 if r["Counter_Name"] == counter and "x265amd::" in r["Kernel_Name"]:
