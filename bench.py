@@ -10,8 +10,19 @@ in this design (CABAC estimation, SAO, lowres init, ...) are excluded and
 listed in the output.  `value` is frames per second of that primitive
 workload over all ranks; Mpixel/s is reported beside it.
 
-Multi-GPU: one process per GPU (torch.distributed.run), every rank works on
-its own frames (frame-parallel shard, weak scaling); no data-path collective.
+Modes (one process per GPU under torch.distributed.run; weak scaling, F frames
+per rank per step):
+  replay (default)  every rank replays the census of its own F frames as one set
+                    of grouped launches — independent closed-GOP shards, no
+                    data-path collective;
+  pipeline          the frame-parallel shard of SURVEY §8(e): frame i of a
+                    G*F-frame sequence on rank i mod G, encoded band by band of
+                    CTU rows; a band waits until the reference frame's owner has
+                    published the rows it reads (refLagRows); finished rows
+                    (deblock, SAO, border extension) go point to point over RCCL
+                    to the owner of the next frame (src/x265_amd/pipeline.py,
+                    DESIGN.md §6).  At N = 1 its rate is reported beside the
+                    replay line (`frame_parallel_pipeline`).
 Timing: W warmup steps, then K steps bracketed by barrier + device sync, max
 over ranks.
 
@@ -63,6 +74,14 @@ def parse():
     ap.add_argument("--preset", default="medium", choices=("medium", "slow"),
                     help="selects the census of that x265 preset (tests/golden/census_<H>p_<preset>[_main10].json)")
     ap.add_argument("--no-graph", action="store_true", help="launch eagerly instead of replaying a hipGraph")
+    ap.add_argument("--mode", default="replay", choices=("pipeline", "replay"),
+                    help="pipeline: frame-parallel shard, frames encoded band by band with the reference-row "
+                         "dependencies and RCCL row exchange (src/x265_amd/pipeline.py); replay: the census of "
+                         "this rank's frames as one set of independent grouped launches")
+    ap.add_argument("--band-rows", type=int, default=4, help="CTU rows per pipeline band")
+    ap.add_argument("--no-pipeline-check", action="store_true",
+                    help="skip the N=1 measurement of the frame-parallel pipeline beside a replay run")
+    ap.add_argument("--one-graph", action="store_true", help="pipeline on one rank: the whole step as one hipGraph")
     ap.add_argument("--streams", type=int, default=8, help="HIP streams the step's independent launches spread over")
     ap.add_argument("--no-group", action="store_true", help="one launch per batch instead of grouped multi-shape launches")
     ap.add_argument("--census-cpu-seconds", type=float, default=5.0,
@@ -288,6 +307,33 @@ def census_replay_cpu(args, census):
             "mpix_per_s": round(fps * args.width * args.height / 1e6, 3)}
 
 
+def pipeline_rates(prims, args, census, local):
+    """The frame-parallel step (--mode pipeline) on this one GPU: frames encoded in order, band by
+    band, with the reference-row waits, loop filters and row publications (local copies at N=1)."""
+    import torch
+
+    from src.x265_amd.frame_pipeline import GpuFramePipeline
+
+    pipe = GpuFramePipeline(prims, args.width, args.height, args.depth, args.frames, 1, 0, census=census,
+                            band_rows=args.band_rows, streams=args.streams, device=f"cuda:{local}")
+    out = {"frames_per_step": args.frames}
+    for br in (args.band_rows, pipe.fs.ph // 64):
+        pipe.set_band_rows(br)
+        pipe.build(graphs=True)
+        for _ in range(2):
+            pipe.step()
+        torch.cuda.synchronize()
+        n = 10
+        t0 = time.perf_counter()
+        for _ in range(n):
+            pipe.step()
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / n
+        out[f"band_rows_{br}"] = {"fps": round(args.frames / dt, 1), "ms_per_step": round(dt * 1e3, 3),
+                                  "bands_per_frame": pipe.plan.nbands, "launches_per_step": pipe.launches_per_step}
+    return out
+
+
 def main():
     args = parse()
     import torch
@@ -296,29 +342,35 @@ def main():
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs the MI355X (no CPU fallback)")
     from src.x265_amd import Primitives
-    from src.x265_amd.workload import FrameSet, WorkloadBuilder, census_batches, group_launches, load_census
-
-    from src.x265_amd.shard import RefRing
+    from src.x265_amd.workload import FrameSet, WorkloadBuilder, census_batches, group_launches
 
     prims = Primitives(device=local)
     census, census_name = pick_census(args)
     F = args.frames
-    # GOP shard: rank r encodes frames [r*F, (r+1)*F) of the sequence
-    fs = FrameSet(args.width, args.height, F, args.depth, device=f"cuda:{local}", first_frame=rank * F)
-    batches, wb = census_batches(fs, frames=F, census=census, builder=WorkloadBuilder(fs, seed=11 + rank))
+    import ctypes
+    nstreams = max(1, args.streams)
+    pipe = None
+    if args.mode == "pipeline":
+        # frame-parallel shard: rank r encodes frames i = k*G + r of a G*F-frame sequence, band by
+        # band of CTU rows, waiting on / publishing reconstructed rows (src/x265_amd/pipeline.py)
+        from src.x265_amd.frame_pipeline import GpuFramePipeline
+
+        pipe = GpuFramePipeline(prims, args.width, args.height, args.depth, F, world, rank, census=census,
+                                band_rows=args.band_rows, streams=nstreams, device=f"cuda:{local}")
+        batches, wb = pipe.batches, pipe.wb
+    else:
+        # independent replay: this rank's F frames' census as one set of grouped launches
+        fs = FrameSet(args.width, args.height, F, args.depth, device=f"cuda:{local}", first_frame=rank * F)
+        batches, wb = census_batches(fs, frames=F, census=census, builder=WorkloadBuilder(fs, seed=11 + rank))
     # one launch per kernel class: batches of different block shapes share a grouped launch
     launches = list(batches) if args.no_group else group_launches(batches)
     step_bytes = sum(b.bytes for b in batches)
     calls = sum(b.n for b in batches)
-    ring = RefRing(world, rank)
-    ref_send, ref_recv = fs.planes(F - 1), fs.planes(F)
 
-    # independent launches spread over S streams (forked from and joined back into the current
-    # stream, so a captured graph gets S parallel branches): small launches and launch tails overlap
-    # The launch the roofline reports runs alone first (not overlapped), so its duration inside
-    # the step equals its isolated duration and the rocprof summary of this command agrees.
-    import ctypes
-    nstreams = max(1, args.streams)
+    # replay mode: independent launches spread over S streams (forked from and joined back into the
+    # current stream, so a captured graph gets S parallel branches): small launches and launch tails
+    # overlap.  The launch the roofline reports runs alone first (not overlapped), so its duration
+    # inside the step equals its isolated duration and the rocprof summary of this command agrees.
     side = [torch.cuda.Stream() for _ in range(nstreams)] if nstreams > 1 else []
     solo = []
     lanes = [[] for _ in range(nstreams)]
@@ -354,46 +406,43 @@ def main():
         for s_ in side:
             cur.wait_stream(s_)
 
-    def exchange():
-        # frame-parallel dependency: my first frame predicts from rank-1's last frame
-        if world > 1:
-            ring.exchange(list(ref_send), list(ref_recv))
-
-    def step():
-        exchange()
-        kernels()
-
-    # warmup (also JIT-free: the code objects are prebuilt) + per-kernel timing to find the dominant batch
+    # per-kernel timing (eager, whole-frame launches) to find the dominant launch
     for _ in range(max(1, args.warmup)):
-        step()
+        kernels()
     torch.cuda.synchronize()
     ktimes = kernel_times(launches, prims)
     dominant = max(launches, key=lambda b: ktimes[b.name])
     assign(dominant)
 
     graph = None
-    if not args.no_graph:
-        try:
-            s = torch.cuda.Stream()
-            s.wait_stream(torch.cuda.current_stream())
-            with torch.cuda.stream(s):
-                kernels()
-            torch.cuda.current_stream().wait_stream(s)
-            graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(graph):
-                kernels()
-            graph.replay()
-            torch.cuda.synchronize()
-        except Exception as e:  # capture unsupported: measure eager launches instead
-            print(f"[bench] hipGraph capture failed ({e}); eager launches", file=sys.stderr)
-            graph = None
+    if pipe is not None:
+        pipe.build(graphs=not args.no_graph, one_graph=args.one_graph)
+        graph = bool(pipe.graphs) or None
 
-    def run():
-        exchange()                     # P2P over RCCL, outside the captured graph
-        if graph is not None:
-            graph.replay()
-        else:
-            kernels()
+        def run():
+            pipe.step()
+    else:
+        if not args.no_graph:
+            try:
+                s = torch.cuda.Stream()
+                s.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(s):
+                    kernels()
+                torch.cuda.current_stream().wait_stream(s)
+                graph = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(graph):
+                    kernels()
+                graph.replay()
+                torch.cuda.synchronize()
+            except Exception as e:  # capture unsupported: measure eager launches instead
+                print(f"[bench] hipGraph capture failed ({e}); eager launches", file=sys.stderr)
+                graph = None
+
+        def run():
+            if graph is not None:
+                graph.replay()
+            else:
+                kernels()
     for _ in range(args.warmup):
         run()
     barrier(world)
@@ -469,6 +518,12 @@ def main():
                 caller = caller_rates(prims, args.width, args.height, args.depth, dev=f"cuda:{local}")
             except Exception as e:   # informational: never fails the bench line
                 caller = {"error": str(e)}
+        frame_parallel = None
+        if world == 1 and pipe is None and not args.no_pipeline_check:
+            try:
+                frame_parallel = pipeline_rates(prims, args, census, local)
+            except Exception as e:   # informational
+                frame_parallel = {"error": str(e)}
         cpu, replay, enc = None, None, None
         if world == 1 and not args.no_cpu:
             try:
@@ -509,9 +564,14 @@ def main():
                             "serially dependent); CPU-side entries (CABAC estimates, SAO, lowres init) excluded",
                 "resolution": f"{args.width}x{args.height}", "depth": args.depth, "frames_per_step_per_gpu": F,
                 "calls_per_step_per_gpu": calls, "batches_per_step": len(batches),
-                "launches_per_step": len(launches),
+                "launches_per_step": pipe.launches_per_step if pipe is not None else len(launches),
                 "algorithmic_GB_per_step_per_gpu": round(step_bytes / 1e9, 3),
-                "hipgraph": graph is not None, "streams": nstreams, "parallelism": f"frame-shard x{world}",
+                "hipgraph": graph is not None, "streams": nstreams, "mode": args.mode,
+                "parallelism": (f"frame-parallel x{world}: frame i on rank i mod {world}, CTU-row bands of "
+                                f"{args.band_rows}, reference rows published after deblock/SAO/border and sent "
+                                f"over {'RCCL' if world > 1 else 'a local copy'}" if pipe is not None else
+                                f"independent replay x{world}"),
+                "frames_per_step_total": world * F,
             },
             "mpix_per_s": round(fps * args.width * args.height / 1e6, 1),
             "timed_region_s": round(elapsed, 4),
@@ -521,6 +581,7 @@ def main():
             "roofline": roofline,
             "cpu_baseline": cpu,
             "encoder_level": enc,
+            "frame_parallel_pipeline": frame_parallel,
             "caller_level_rates": caller,
             "cpu_excluded_calls_per_frame": round(sum(v for v in wb.skipped.values()) / F),
         }

@@ -616,6 +616,25 @@ typedef struct
 } x265amd_border_plane;
 int x265amd_extend_border(int depth, int count, const x265amd_border_plane* planes, void* stream);
 
+/* Row-band forms of the loop filters — the CTU-row pipeline of FrameFilter
+ * (framefilter.cpp:300-430, processRow / processPostRow) that the frame-parallel
+ * shard publishes reconstructed rows from.  Per frame / plane a band
+ * of rows; running the bands of a frame top to bottom, deblocking band b before the
+ * SAO of band b - 1 (whose last rows deblocking band b modifies), gives the whole-frame
+ * result bit-exactly.
+ *   deblock_rows:       rows[2i], rows[2i+1] = luma pixel rows [y0, y1) of frame i,
+ *                       y0 % 16 == 0, (y1 - y0) % 8 == 0, y1 <= height: the vertical edges
+ *                       inside the band and the horizontal edges at y0 <= y < y1 (y > 0);
+ *   sao_apply_rows:     ctu_rows[2i], ctu_rows[2i+1] = CTU rows [r0, r1) of frame i;
+ *   extend_border_rows: rows[4i..4i+3] = y0, y1, top, bottom: the side margins of picture
+ *                       rows [y0, y1) and, when set, the margin rows above / below. */
+int x265amd_deblock_rows(int depth, int count, const x265amd_deblock_frame* frames, const int32_t* rows,
+                         void* stream);
+int x265amd_sao_apply_rows(int depth, int count, const x265amd_sao_frame* frames, const int32_t* ctu_rows,
+                           void* stream);
+int x265amd_extend_border_rows(int depth, int count, const x265amd_border_plane* planes, const int32_t* rows,
+                               void* stream);
+
 #ifdef __cplusplus
 }
 #endif

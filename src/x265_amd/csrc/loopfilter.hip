@@ -80,7 +80,8 @@ struct DbkFrame
     int64_t stride, cstride;
     const x265amd_deblock_unit* units;
     int64_t us;
-    int wu, hu;                       // picture size in 4x4 units
+    int wu, hu;                       // picture width / band height in 4x4 units
+    int uy0;                          // first unit row of the band (0: whole picture)
     int is_p, beta2, tc2, cbqp, crqp, tqb;
     int32_t poc[2][16];
     uint32_t block0, nluma, nseg;     // first block; luma / all segments of this pass
@@ -273,6 +274,7 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_deblock(const DbkLaunch L)
         if (DIR == 0) { const int n = (f.wu + 3) >> 2; uy = 2 * (int)(c / n); ux = 4 * (int)(c % n); }
         else { const int n = f.wu >> 1; ux = 2 * (int)(c % n); uy = 4 * (int)(c / n); }
     }
+    uy += f.uy0;
     const x265amd_deblock_unit* qu = f.units + uy * f.us + ux;
     const Unit Q(qu);
     const int mark = edge_mark(Q, DIR, DIR ? 4 * uy : 4 * ux);
@@ -377,6 +379,7 @@ struct SaoFrame
     int64_t stride, cstride;
     const x265amd_sao_param* params;
     int w, h, ctu_log2, wc, nctu, luma_on, chroma_on;
+    int c0, nctu_all;                        // first CTU of the band, CTUs of the picture (params stride)
     uint32_t block0;                         // first block (one per plane and CTU)
 };
 struct SaoLaunch
@@ -394,7 +397,7 @@ __global__ __launch_bounds__(64) void k_sao_apply(const SaoLaunch L)
     const uint32_t b = xcd_block();
     const SaoFrame& f = L.f[frame_of<kMaxFrames>(L, b)];
     const uint32_t u = b - f.block0;                 // plane-major: [3][nctu]
-    const int p = (int)(u / f.nctu), c = (int)(u % f.nctu);
+    const int p = (int)(u / f.nctu), c = f.c0 + (int)(u % f.nctu);
     const int lane = threadIdx.x;
     const int pw = p ? f.w >> 1 : f.w, ph = p ? f.h >> 1 : f.h;
     const int cl = f.ctu_log2 - (p ? 1 : 0), cs = 1 << cl;
@@ -407,9 +410,9 @@ __global__ __launch_bounds__(64) void k_sao_apply(const SaoLaunch L)
     const int64_t st = p ? f.cstride : f.stride;
     const P* src = (const P*)f.src[p] + y0 * st + x0;
     P* dst = (P*)f.dst[p] + y0 * st + x0;
-    const x265amd_sao_param* prm = f.params + p * f.nctu + c;
+    const x265amd_sao_param* prm = f.params + p * f.nctu_all + c;
     int type = (int)prm->type;
-    if (p == 2 && type >= 0) type = (int)f.params[f.nctu + c].type;   // processSaoCu(addr, typeIdxCb, 2)
+    if (p == 2 && type >= 0) type = (int)f.params[f.nctu_all + c].type;   // processSaoCu(addr, typeIdxCb, 2)
     if (!(p ? f.chroma_on : f.luma_on)) type = -1;
     const int band = prm->band;
     const int o0 = prm->offset[0], o1 = prm->offset[1], o2 = prm->offset[2], o3 = prm->offset[3];
@@ -670,6 +673,7 @@ struct BorderPlane
     void* p;
     int64_t stride;
     int w, h, mx, my;
+    int y0, nr, top, bottom;                 // side margins of rows [y0, y0 + nr); which margin rows
     uint32_t block0_lr, block0_tb;
 };
 constexpr int kMaxPlanes = 16;
@@ -690,9 +694,9 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_border_lr(const BorderLaunch 
         if (k < L.count && L.f[k].block0_lr <= b) i = k;
     const BorderPlane& f = L.f[i];
     const int64_t t = (int64_t)(b - f.block0_lr) * X265AMD_BLOCK + threadIdx.x;
-    if (t >= 2 * (int64_t)f.h) return;
-    const bool right = t >= f.h;
-    const int y = (int)(right ? t - f.h : t);
+    if (t >= 2 * (int64_t)f.nr) return;
+    const bool right = t >= f.nr;
+    const int y = f.y0 + (int)(right ? t - f.nr : t);
     P* row = (P*)f.p + y * f.stride;
     const P v = right ? row[f.w - 1] : row[0];
     P* d = right ? row + f.w : row - f.mx;
@@ -725,10 +729,12 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_border_tb(const BorderLaunch 
     const BorderPlane& f = L.f[i];
     const int64_t chunks = (f.stride + C - 1) / C;
     const int64_t t = (int64_t)(b - f.block0_tb) * X265AMD_BLOCK + threadIdx.x;
-    if (t >= 2 * (int64_t)f.my * chunks) return;
-    const int r = (int)(t / chunks), c = (int)(t % chunks);
-    const bool bottom = r >= f.my;
-    const int yd = bottom ? f.h + (r - f.my) : -1 - r;
+    if (t >= (int64_t)(f.top + f.bottom) * f.my * chunks) return;
+    int r = (int)(t / chunks);
+    const int c = (int)(t % chunks);
+    const bool bottom = !f.top || r >= f.my;
+    if (f.top && bottom) r -= f.my;
+    const int yd = bottom ? f.h + r : -1 - r;
     const int ys = bottom ? f.h - 1 : 0;
     const P* s = (const P*)f.p - f.mx + ys * f.stride + c * C;
     P* d = (P*)f.p - f.mx + yd * f.stride + c * C;
@@ -744,7 +750,7 @@ using namespace x265amd;
 static bool bd_ok(int depth) { return depth == 8 || depth == 10 || depth == 12; }
 static uint32_t nblocks(uint64_t n) { return (uint32_t)((n + X265AMD_BLOCK - 1) / X265AMD_BLOCK); }
 
-extern "C" int x265amd_deblock(int depth, int count, const x265amd_deblock_frame* frames, void* stream)
+static int deblock_impl(int depth, int count, const x265amd_deblock_frame* frames, const int32_t* rows, void* stream)
 {
     if (!bd_ok(depth) || count < 0 || (count && !frames)) return X265AMD_EINVAL;
     for (int i = 0; i < count; i++)
@@ -752,6 +758,9 @@ extern "C" int x265amd_deblock(int depth, int count, const x265amd_deblock_frame
         const x265amd_deblock_frame& a = frames[i];
         if (a.width <= 0 || a.height <= 0 || (a.width & 7) || (a.height & 7) || !a.plane[0] || !a.plane[1] ||
             !a.plane[2] || !a.units || a.unit_stride < a.width / 4 || a.stride < a.width || a.cstride < a.width / 2)
+            return X265AMD_EINVAL;
+        if (rows && (rows[2 * i] < 0 || (rows[2 * i] & 15) || rows[2 * i + 1] <= rows[2 * i] ||
+                     rows[2 * i + 1] > a.height || ((rows[2 * i + 1] - rows[2 * i]) & 7)))
             return X265AMD_EINVAL;
     }
     hipStream_t st = (hipStream_t)stream;
@@ -773,7 +782,8 @@ extern "C" int x265amd_deblock(int depth, int count, const x265amd_deblock_frame
                 f.units = a.units;
                 f.us = a.unit_stride;
                 f.wu = a.width >> 2;
-                f.hu = a.height >> 2;
+                f.uy0 = rows ? rows[2 * (i0 + k)] >> 2 : 0;
+                f.hu = rows ? (rows[2 * (i0 + k) + 1] - rows[2 * (i0 + k)]) >> 2 : a.height >> 2;
                 f.is_p = a.is_p;
                 f.beta2 = 2 * a.beta_offset_div2;
                 f.tc2 = 2 * a.tc_offset_div2;
@@ -811,7 +821,18 @@ extern "C" int x265amd_deblock(int depth, int count, const x265amd_deblock_frame
     return 0;
 }
 
-extern "C" int x265amd_sao_apply(int depth, int count, const x265amd_sao_frame* frames, void* stream)
+extern "C" int x265amd_deblock(int depth, int count, const x265amd_deblock_frame* frames, void* stream)
+{
+    return deblock_impl(depth, count, frames, nullptr, stream);
+}
+
+extern "C" int x265amd_deblock_rows(int depth, int count, const x265amd_deblock_frame* frames, const int32_t* rows,
+                                    void* stream)
+{
+    return rows ? deblock_impl(depth, count, frames, rows, stream) : X265AMD_EINVAL;
+}
+
+static int sao_apply_impl(int depth, int count, const x265amd_sao_frame* frames, const int32_t* ctu_rows, void* stream)
 {
     if (!bd_ok(depth) || count < 0 || (count && !frames)) return X265AMD_EINVAL;
     for (int i = 0; i < count; i++)
@@ -819,6 +840,9 @@ extern "C" int x265amd_sao_apply(int depth, int count, const x265amd_sao_frame* 
         const x265amd_sao_frame& a = frames[i];
         if (a.width <= 0 || a.height <= 0 || (a.width & 7) || (a.height & 7) || a.ctu_log2 < 4 || a.ctu_log2 > 6 ||
             !a.params || a.stride < a.width || a.cstride < a.width / 2)
+            return X265AMD_EINVAL;
+        const int hc = (a.height + (1 << a.ctu_log2) - 1) >> a.ctu_log2;
+        if (ctu_rows && (ctu_rows[2 * i] < 0 || ctu_rows[2 * i + 1] <= ctu_rows[2 * i] || ctu_rows[2 * i + 1] > hc))
             return X265AMD_EINVAL;
         for (int p = 0; p < 3; p++)
             if (!a.src[p] || !a.dst[p] || a.src[p] == a.dst[p]) return X265AMD_EINVAL;
@@ -845,7 +869,9 @@ extern "C" int x265amd_sao_apply(int depth, int count, const x265amd_sao_frame* 
             f.ctu_log2 = a.ctu_log2;
             const int ctu = 1 << a.ctu_log2;
             f.wc = (a.width + ctu - 1) >> a.ctu_log2;
-            f.nctu = f.wc * ((a.height + ctu - 1) >> a.ctu_log2);
+            f.nctu_all = f.wc * ((a.height + ctu - 1) >> a.ctu_log2);
+            f.c0 = ctu_rows ? ctu_rows[2 * (i0 + k)] * f.wc : 0;
+            f.nctu = ctu_rows ? (ctu_rows[2 * (i0 + k) + 1] - ctu_rows[2 * (i0 + k)]) * f.wc : f.nctu_all;
             f.luma_on = a.luma_on;
             f.chroma_on = a.chroma_on;
             f.block0 = blocks;
@@ -858,6 +884,17 @@ extern "C" int x265amd_sao_apply(int depth, int count, const x265amd_sao_frame* 
         if (e != hipSuccess) return (int)e;
     }
     return 0;
+}
+
+extern "C" int x265amd_sao_apply(int depth, int count, const x265amd_sao_frame* frames, void* stream)
+{
+    return sao_apply_impl(depth, count, frames, nullptr, stream);
+}
+
+extern "C" int x265amd_sao_apply_rows(int depth, int count, const x265amd_sao_frame* frames, const int32_t* ctu_rows,
+                                      void* stream)
+{
+    return ctu_rows ? sao_apply_impl(depth, count, frames, ctu_rows, stream) : X265AMD_EINVAL;
 }
 
 extern "C" int x265amd_sao_stats(int depth, int count, const x265amd_sao_stats_frame* frames, void* stream)
@@ -909,7 +946,7 @@ extern "C" int x265amd_sao_stats(int depth, int count, const x265amd_sao_stats_f
     return 0;
 }
 
-extern "C" int x265amd_extend_border(int depth, int count, const x265amd_border_plane* planes, void* stream)
+static int border_impl(int depth, int count, const x265amd_border_plane* planes, const int32_t* rows, void* stream)
 {
     if (!bd_ok(depth) || count < 0 || (count && !planes)) return X265AMD_EINVAL;
     for (int i = 0; i < count; i++)
@@ -917,6 +954,8 @@ extern "C" int x265amd_extend_border(int depth, int count, const x265amd_border_
         const x265amd_border_plane& a = planes[i];
         if (!a.plane || a.width <= 0 || a.height <= 0 || a.margin_x < 0 || a.margin_y < 0 ||
             a.stride < a.width + 2 * a.margin_x)
+            return X265AMD_EINVAL;
+        if (rows && (rows[4 * i] < 0 || rows[4 * i + 1] < rows[4 * i] || rows[4 * i + 1] > a.height))
             return X265AMD_EINVAL;
     }
     hipStream_t st = (hipStream_t)stream;
@@ -937,15 +976,24 @@ extern "C" int x265amd_extend_border(int depth, int count, const x265amd_border_
             f.h = a.height;
             f.mx = a.margin_x;
             f.my = a.margin_y;
+            const int* r = rows ? rows + 4 * (i0 + k) : nullptr;
+            f.y0 = r ? r[0] : 0;
+            f.nr = r ? r[1] - r[0] : a.height;
+            f.top = r ? (r[2] != 0) : 1;
+            f.bottom = r ? (r[3] != 0) : 1;
             f.block0_lr = blr;
             f.block0_tb = btb;
-            blr += nblocks(2 * (uint64_t)a.height);
-            btb += nblocks(2 * (uint64_t)a.margin_y * (uint64_t)((a.stride + C - 1) / C));
+            blr += nblocks(2 * (uint64_t)f.nr);
+            btb += nblocks((uint64_t)(f.top + f.bottom) * a.margin_y * (uint64_t)((a.stride + C - 1) / C));
         }
-        if (depth == 8) hipLaunchKernelGGL((k_border_lr<uint8_t>), dim3(blr), dim3(X265AMD_BLOCK), 0, st, L);
-        else hipLaunchKernelGGL((k_border_lr<uint16_t>), dim3(blr), dim3(X265AMD_BLOCK), 0, st, L);
-        hipError_t e = hipGetLastError();
-        if (e != hipSuccess) return (int)e;
+        hipError_t e;
+        if (blr)
+        {
+            if (depth == 8) hipLaunchKernelGGL((k_border_lr<uint8_t>), dim3(blr), dim3(X265AMD_BLOCK), 0, st, L);
+            else hipLaunchKernelGGL((k_border_lr<uint16_t>), dim3(blr), dim3(X265AMD_BLOCK), 0, st, L);
+            e = hipGetLastError();
+            if (e != hipSuccess) return (int)e;
+        }
         if (btb)
         {
             if (depth == 8) hipLaunchKernelGGL((k_border_tb<uint8_t>), dim3(btb), dim3(X265AMD_BLOCK), 0, st, L);
@@ -955,6 +1003,17 @@ extern "C" int x265amd_extend_border(int depth, int count, const x265amd_border_
         }
     }
     return 0;
+}
+
+extern "C" int x265amd_extend_border(int depth, int count, const x265amd_border_plane* planes, void* stream)
+{
+    return border_impl(depth, count, planes, nullptr, stream);
+}
+
+extern "C" int x265amd_extend_border_rows(int depth, int count, const x265amd_border_plane* planes, const int32_t* rows,
+                                          void* stream)
+{
+    return rows ? border_impl(depth, count, planes, rows, stream) : X265AMD_EINVAL;
 }
 
 // the launch descriptors must fit the 4 KiB kernarg segment

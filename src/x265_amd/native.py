@@ -331,3 +331,20 @@ class Primitives:
 
     def extend_border(self, depth, planes, stream=None):
         self._frames("x265amd_extend_border", "extend_border", depth, planes, stream)
+
+    # row-band forms (the frame-parallel pipeline): rows is a flat list of ints per frame / plane
+    def _rows(self, entry, what, depth, frames, rows, per, stream):
+        if len(rows) != per * len(frames):
+            raise ValueError(f"{what}: {per} row values per frame expected")
+        arr = (type(frames[0]) * len(frames))(*frames)
+        r = (C.c_int32 * len(rows))(*rows)
+        self._check(getattr(self.lib, entry)(depth, len(frames), arr, r, stream or _stream()), what)
+
+    def deblock_rows(self, depth, frames, rows, stream=None):
+        self._rows("x265amd_deblock_rows", "deblock_rows", depth, frames, rows, 2, stream)
+
+    def sao_apply_rows(self, depth, frames, ctu_rows, stream=None):
+        self._rows("x265amd_sao_apply_rows", "sao_apply_rows", depth, frames, ctu_rows, 2, stream)
+
+    def extend_border_rows(self, depth, planes, rows, stream=None):
+        self._rows("x265amd_extend_border_rows", "extend_border_rows", depth, planes, rows, 4, stream)

@@ -62,7 +62,7 @@ class FrameSet:
     """F padded frames (luma + 4:2:0 chroma) plus int16 residual planes, on one device."""
 
     def __init__(self, width: int, height: int, nframes: int, depth: int = 8, device: str = "cuda", ctu: int = 64,
-                 first_frame: int = 0):
+                 first_frame: int = 0, frame_ids: list | None = None):
         import torch
 
         self.w, self.h, self.F, self.depth, self.device = width, height, nframes, depth, device
@@ -74,19 +74,28 @@ class FrameSet:
         self.cmx, self.cmy = self.mx, self.my // 2          # picyuv.cpp:71-73 (4:2:0)
         self.cstride = self.pw // 2 + 2 * self.cmx
         self.crows = self.ph // 2 + 2 * self.cmy
-        # stored frames 0..F-1 are the chunk being encoded (synthetic frames
+        # Default: stored frames 0..F-1 are the chunk being encoded (synthetic frames
         # first+1 .. first+F); stored frame F is the REFERENCE SLOT holding the
         # picture before the chunk (synthetic frame `first`), which frame 0
-        # predicts from.  Under frame sharding the slot is refilled each step
-        # with the previous rank's last frame (shard.RefRing).
-        src = SyntheticSource(width, height, nframes + 1 + first_frame, depth)
+        # predicts from; frame f > 0 predicts from stored frame f - 1.
+        # frame_ids (the frame-parallel pipeline, pipeline.py): stored frame k is synthetic
+        # frame frame_ids[k] and stored frame F + k its own reference slot, which the row
+        # exchange fills with the reconstruction of frame frame_ids[k] - 1 (initially the
+        # synthetic frame frame_ids[k] - 1).
+        self.per_frame_refs = frame_ids is not None
+        if self.per_frame_refs:
+            assert len(frame_ids) == nframes
+            ids = list(frame_ids) + [max(0, i - 1) for i in frame_ids]
+        else:
+            ids = [first_frame + i + 1 for i in range(nframes)] + [first_frame]
+        src = SyntheticSource(width, height, max(ids) + 1, depth)
         dt = np.uint8 if depth == 8 else np.uint16
-        S = nframes + 1
+        S = len(ids)
         Y = np.zeros((S, self.rows, self.stride), dt)
         U = np.zeros((S, self.crows, self.cstride), dt)
         V = np.zeros((S, self.crows, self.cstride), dt)
         for i in range(S):
-            y, u, v = src.frame(first_frame + (i + 1 if i < nframes else 0))
+            y, u, v = src.frame(ids[i])
             Y[i] = self._pad(y, self.mx, self.my, self.rows, self.stride)
             U[i] = self._pad(u, self.cmx, self.cmy, self.crows, self.cstride)
             V[i] = self._pad(v, self.cmx, self.cmy, self.crows, self.cstride)
@@ -100,7 +109,10 @@ class FrameSet:
         self.cplane_size = self.crows * self.cstride
 
     def ref_of(self, f):
-        """reference frame of stored frame f: the previous frame, or the reference slot for frame 0"""
+        """reference frame of stored frame f: the previous frame, or the reference slot for frame 0
+        (per-frame reference slots: stored frame F + f)"""
+        if self.per_frame_refs:
+            return np.asarray(f) % self.F + self.F if not np.isscalar(f) else f % self.F + self.F
         return np.where(np.asarray(f) == 0, self.F, np.asarray(f) - 1) if not np.isscalar(f) else (self.F if f == 0 else f - 1)
 
     def planes(self, f: int):

@@ -239,3 +239,74 @@ def test_gpu_extend_border(gpu_prims, depth):
     torch.cuda.synchronize()
     for d, ref in keep:
         np.testing.assert_array_equal(_host(d, dt), ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("depth", DEPTHS)
+def test_gpu_loop_filter_row_bands_equal_whole_frame(gpu_prims, depth):
+    """The CTU-row pipeline the frame-parallel shard publishes rows from: deblock
+    band b, then SAO + border extension of band b - 1, top to bottom (x265amd_*_rows), equals
+    the whole-frame deblock -> SAO -> border of the oracle bit-exactly, margins included."""
+    import torch
+    from src.x265_amd.native import BorderPlane, DeblockFrame, SaoFrame
+
+    O = po.FrameFilters("oracle", depth)
+    M = F.MARGIN
+    for i, (W, H, cl) in enumerate(GPU_SIZES):
+        rng = np.random.default_rng(700 + i + depth)
+        pl = F.frame_planes(W, H, depth, rng)
+        U = F.deblock_units(W, H, cl, depth, rng, "P")
+        dp = F.deblock_params(rng, "P", 0)
+        prm = F.sao_params(W, H, cl, depth, rng)
+        # oracle: whole frame
+        dbk = F.copy_planes(pl)
+        O.deblock(W, H, cl, dbk, M, U, dp)
+        ref = F.copy_planes(dbk)
+        O.sao_apply(W, H, cl, ref, M, prm, 1, 1)
+        for p in range(3):
+            O.extend_border(ref[p], M, M, W if p == 0 else W // 2, H if p == 0 else H // 2)
+        # GPU: row bands
+        d = _dev(pl)
+        out = _dev(tuple(np.zeros_like(p) for p in pl))
+        du = torch.from_numpy(U.view(np.uint8).reshape(U.shape[0], -1)).cuda()
+        dprm = torch.from_numpy(prm.view(np.uint8)).cuda()
+        fr = DeblockFrame()
+        fr.width, fr.height = W, H
+        for p in range(3):
+            fr.plane[p] = _org(d[p])
+        fr.stride, fr.cstride = d[0].shape[1], d[1].shape[1]
+        fr.units, fr.unit_stride = du.data_ptr(), U.shape[1]
+        fr.is_p, fr.beta_offset_div2, fr.tc_offset_div2 = dp.is_p, dp.beta_offset_div2, dp.tc_offset_div2
+        fr.cb_qp_offset, fr.cr_qp_offset = dp.cb_qp_offset, dp.cr_qp_offset
+        for lst in range(2):
+            for k in range(16):
+                fr.ref_poc[lst][k] = dp.ref_poc[lst][k]
+        sf = SaoFrame()
+        sf.width, sf.height, sf.ctu_log2, sf.luma_on, sf.chroma_on = W, H, cl, 1, 1
+        for p in range(3):
+            sf.src[p], sf.dst[p] = _org(d[p]), _org(out[p])
+        sf.stride, sf.cstride, sf.params = d[0].shape[1], d[1].shape[1], dprm.data_ptr()
+        bps = []
+        for p in range(3):
+            bp = BorderPlane()
+            bp.plane, bp.stride = _org(out[p]), out[p].shape[1]
+            bp.width, bp.height = (W, H) if p == 0 else (W // 2, H // 2)
+            bp.margin_x = bp.margin_y = M
+            bps.append(bp)
+        ctu = 1 << cl
+        rows = (H + ctu - 1) // ctu
+
+        def finish(b):
+            gpu_prims.sao_apply_rows(depth, [sf], [b, b + 1])
+            y0, y1 = b * ctu, min((b + 1) * ctu, H)
+            gpu_prims.extend_border_rows(depth, bps, [y0, y1, b == 0, b == rows - 1] +
+                                         [y0 // 2, y1 // 2, b == 0, b == rows - 1] * 2)
+
+        for b in range(rows):
+            gpu_prims.deblock_rows(depth, [fr], [b * ctu, min((b + 1) * ctu, H)])
+            if b:
+                finish(b - 1)
+        finish(rows - 1)
+        torch.cuda.synchronize()
+        for p in range(3):
+            np.testing.assert_array_equal(_host(out[p], pl[p].dtype), ref[p], err_msg=f"{W}x{H} plane {p}")
