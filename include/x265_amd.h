@@ -468,6 +468,39 @@ typedef struct
 } x265amd_lowres_bcost_batch;
 int x265amd_lowres_bcost(int depth, const x265amd_lowres_bcost_batch* batch, void* stream);
 
+/* f1 cuTree: Lookahead::estimateCUPropagate (slicetype.cpp:1738-1836) with the
+ * propagateCost primitive (pixel.cpp:846-872), one call of it per batch, batches in order.
+ * For every lowres CU of frame b: the amount
+ *   (int)((propagate_in + intra * inv_qscale * fps_factor / 256) * (intra - inter) / intra + 0.5)
+ * in IEEE double (no contraction; out-of-range -> INT_MIN as x86-64), and where it is > 0 its
+ * share follows the list-0 / list-1 MV (bipred-weighted when both lists are used) onto the
+ * (up to) four overlapped CUs of frames p0 / p1, added into ref_costs[l] saturating at 65535.
+ *   propagate_in   frames[b]->propagateCost (uint16 per CU), NULL for a non-referenced b (zeros;
+ *                  the reference then also zeroes that array's first row — the caller's business)
+ *   intra_cost     frames[b]->intraCost;  lowres_costs = frames[b]->lowresCosts[b-p0][p1-b]
+ *   inv_qscale     frames[b]->invQscaleFactor
+ *   mvs[l]         frames[b]->lowresMvs[l][listDist[l]] (MV: int16 x, y; NULL if list l unused)
+ *   fps_factor     CLIP_DURATION(fpsDenom / fpsNum) / CLIP_DURATION(averageDuration)
+ *   bipred_weight  bipredWeights[0..1] of estimateCUPropagate
+ *   ref_costs[l]   frames[p0 / p1]->propagateCost (in / out)
+ *   scratch        2 * width_cu * height_cu int64 of device memory (contents ignored)
+ * Exact when every propagated share is >= 0 (amounts below 2^21: the reference's int
+ * products do not wrap), which makes the saturating adds order-free. */
+typedef struct
+{
+    int width_cu, height_cu;
+    const uint16_t* propagate_in;
+    const int32_t* intra_cost;
+    const uint16_t* lowres_costs;
+    const int32_t* inv_qscale;
+    const int32_t* mvs[2];
+    double fps_factor;
+    int bipred_weight[2];
+    uint16_t* ref_costs[2];
+    int64_t* scratch;
+} x265amd_propagate_batch;
+int x265amd_cutree_propagate(int count, const x265amd_propagate_batch* batches, void* stream);
+
 /* ------------------------------------------------------------------- f2
  * Full-resolution motion search.  Job i is one
  * MotionEstimate::motionEstimate call (motion.cpp:571-1172) on a full-resolution

@@ -282,3 +282,18 @@ class LowresB:
         r1 = (_vp * 4)(*[base + int(o) * esz for o in r1o])
         self.lib.xo_lowres_bcost(wcu, hcu, rps, ns, base + int(fo) * esz, r0, r1, ls, _p(iq), tab_centre_ptr, ds0, ds1,
                                  _p(mvs0), _p(mc0), _p(mvs1), _p(mc1), _p(lc), _p(rs), _p(ce))
+
+
+class CuTree:
+    """xo_cutree_propagate of one library: Lookahead::estimateCUPropagate (slicetype.cpp:1738-1836)."""
+
+    def __init__(self, kind: str, depth: int = 8):
+        self.lib = C.CDLL(lib_path(kind, depth))
+        self.lib.xo_cutree_propagate.argtypes = [C.c_int] * 8 + [C.c_double] + [_vp] * 8
+
+    def propagate(self, wcu, hcu, b_p0, p1_b, referenced, weighted_bipred, fps_num, fps_den, avg_duration,
+                  prop_b, intra, lowres_costs, inv_q, mvs0, mvs1, ref0, ref1):
+        """in place on prop_b (first row zeroed when not referenced), ref0, ref1 (numpy arrays)"""
+        self.lib.xo_cutree_propagate(wcu, hcu, b_p0, p1_b, referenced, weighted_bipred, fps_num, fps_den,
+                                     avg_duration, _p(prop_b), _p(intra), _p(lowres_costs), _p(inv_q), _p(mvs0),
+                                     _p(mvs1), _p(ref0), _p(ref1))

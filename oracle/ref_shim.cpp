@@ -562,6 +562,15 @@ struct SearchME : public MotionEstimate
     void chroma(pixelcmp_t cs) { chromaSatd = cs; bChromaSATD = subpelRefine > 2 && cs; }
     void at_ctu0() { ctuAddr = 0; absPartIdx = 0; }   /* chroma addressing goes through the PicYuv offsets */
 };
+struct PropLookahead : public Lookahead
+{
+    PropLookahead(x265_param* p) : Lookahead(p, NULL) { m_scratch = (int*)calloc(m_8x8Width + 1, sizeof(int)); }
+    ~PropLookahead() { free(m_scratch); m_scratch = NULL; }
+    void propagate(Lowres** frames, double avg, int p0, int p1, int b, int referenced)
+    {
+        estimateCUPropagate(frames, avg, p0, p1, b, referenced);
+    }
+};
 struct CostGroup : public CostEstimateGroup
 {
     CostGroup(Lookahead& l, Lowres** f) : CostEstimateGroup(l, f) {}
@@ -669,6 +678,40 @@ void xo_lowres_pcost(int wcu, int hcu, int rows_per_slice, int num_slices, const
     free(ref);
     free(cur);
     delete tld;
+    delete la;
+    x265_param_free(param);
+}
+
+/* f1 cuTree: the reference's own Lookahead::estimateCUPropagate (slicetype.cpp:1738-1836) for
+ * (p0, b, p1) = (0, b_p0, b_p0 + p1_b) on Lowres frames wired to the caller's arrays */
+void xo_cutree_propagate(int wcu, int hcu, int b_p0, int p1_b, int referenced, int weighted_bipred,
+                         int fps_num, int fps_den, double avg_duration, uint16_t* propagate_b,
+                         const int32_t* intra_cost, const uint16_t* lowres_costs, const int32_t* inv_q,
+                         const int32_t* mvs0, const int32_t* mvs1, uint16_t* ref0, uint16_t* ref1)
+{
+    pthread_once(&g_prim_once, init_global_prims);
+    x265_param* param = x265_param_alloc();
+    x265_param_default(param);
+    param->sourceWidth = 16 * wcu;
+    param->sourceHeight = 16 * hcu;
+    param->fpsNum = fps_num;
+    param->fpsDenom = fps_den;
+    param->bEnableWeightedBiPred = weighted_bipred;
+    param->rc.vbvBufferSize = 0;
+    PropLookahead* la = new PropLookahead(param);
+    const int p0 = 0, b = b_p0, p1 = b_p0 + p1_b;
+    Lowres* fr[X265_BFRAME_MAX + 2];
+    for (int i = 0; i <= p1; i++) fr[i] = (Lowres*)calloc(1, sizeof(Lowres));
+    fr[p0]->propagateCost = ref0;
+    fr[p1]->propagateCost = p1 == b ? propagate_b : ref1;
+    fr[b]->propagateCost = propagate_b;
+    fr[b]->intraCost = (int32_t*)intra_cost;
+    fr[b]->invQscaleFactor = (int*)inv_q;
+    fr[b]->lowresCosts[b - p0][p1 - b] = (uint16_t*)lowres_costs;
+    fr[b]->lowresMvs[0][b - p0 - 1] = (MV*)mvs0;
+    if (p1 > b) fr[b]->lowresMvs[1][p1 - b - 1] = (MV*)mvs1;
+    la->propagate(fr, avg_duration, p0, p1, b, referenced);
+    for (int i = 0; i <= p1; i++) free(fr[i]);
     delete la;
     x265_param_free(param);
 }

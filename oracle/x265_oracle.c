@@ -17,6 +17,7 @@
 #include "x265_oracle.h"
 
 #include <math.h>
+#include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -2112,4 +2113,94 @@ void xo_deblock(int width, int height, int ctu_log2, void* y_, void* cb_, void* 
                 }
             }
     }
+}
+
+/* ======================================================= f1 cuTree propagation */
+
+/* (int) of a double as x86-64 cvttsd2si: truncation, INT_MIN when out of range or NaN */
+static int xo_cvt_trunc(double v)
+{
+    if (!(v > -2147483649.0 && v < 2147483648.0)) return INT32_MIN;
+    return (int)v;
+}
+
+/* pixel.cpp:846-872 estimateCUPropagateCost (the C propagateCost primitive) */
+static void xo_propagate_cost_row(int* dst, const uint16_t* in, const int32_t* intra, const uint16_t* inter,
+                                  const int32_t* invq, double fps_factor, int len)
+{
+    const double fps = fps_factor / 256;
+    for (int i = 0; i < len; i++)
+    {
+        const int intraCost = intra[i];
+        const int ic = inter[i] & ((1 << 14) - 1);
+        const int interCost = intra[i] < ic ? intra[i] : ic;
+        const double propagateIntra = (double)mul_wrap(intraCost, invq[i]);
+        const double amount = (double)in[i] + propagateIntra * fps;
+        const double num = (double)(intraCost - interCost);
+        const double denom = (double)intraCost;
+        dst[i] = xo_cvt_trunc(amount * num / denom + 0.5);
+    }
+}
+
+static double xo_clip_duration(double f) { return f < 0.01 ? 0.01 : f > 1.00 ? 1.00 : f; }   /* ratecontrol.h:45-47 */
+
+static void xo_clip_add(uint16_t* s, int x)
+{
+    const int v = (int)*s + x;
+    *s = (uint16_t)(v < 65535 ? v : 65535);
+}
+
+/* slicetype.cpp:1738-1836 */
+void xo_cutree_propagate(int wcu, int hcu, int b_p0, int p1_b, int referenced, int weighted_bipred,
+                         int fps_num, int fps_den, double avg_duration, uint16_t* propagate_b,
+                         const int32_t* intra_cost, const uint16_t* lowres_costs, const int32_t* inv_q,
+                         const int32_t* mvs0, const int32_t* mvs1, uint16_t* ref0, uint16_t* ref1)
+{
+    const int p0 = 0, b = b_p0, p1 = b_p0 + p1_b;
+    uint16_t* refCosts[2] = { ref0, ref1 };
+    const int32_t distScale = (((b - p0) << 8) + ((p1 - p0) >> 1)) / (p1 - p0);
+    const int32_t bw = weighted_bipred ? 64 - (distScale >> 2) : 32;
+    const int32_t bipredWeights[2] = { bw, 64 - bw };
+    const int32_t* mvs[2] = { mvs0, mvs1 };
+    const double fpsFactor = xo_clip_duration((double)fps_den / fps_num) / xo_clip_duration(avg_duration);
+    int* scratch = (int*)calloc((size_t)wcu, sizeof(int));
+    if (!referenced) memset(propagate_b, 0, (size_t)wcu * sizeof(uint16_t));
+    const uint16_t* prop = propagate_b;
+    for (int by = 0; by < hcu; by++)
+    {
+        int cu = by * wcu;
+        xo_propagate_cost_row(scratch, prop, intra_cost + cu, lowres_costs + cu, inv_q + cu, fpsFactor, wcu);
+        if (referenced) prop += wcu;
+        for (int bx = 0; bx < wcu; bx++, cu++)
+        {
+            const int amount = scratch[bx];
+            if (amount <= 0) continue;
+            const int used = lowres_costs[cu] >> 14;
+            for (int l = 0; l < 2; l++)
+            {
+                if (!((used >> l) & 1)) continue;
+                int la = amount;
+                if (used == 3) la = (int32_t)((uint32_t)mul_wrap(la, bipredWeights[l]) + 32u) >> 6;
+                const int32_t mv = mvs[l][cu];
+                if (!mv)
+                {
+                    xo_clip_add(&refCosts[l][cu], la);
+                    continue;
+                }
+                const int x = (int16_t)(mv & 0xffff), y = (int16_t)((uint32_t)mv >> 16);
+                const int cux = (x >> 5) + bx, cuy = (y >> 5) + by;
+                const int i0 = cux + cuy * wcu, fx = x & 31, fy = y & 31;
+                const int w[4] = { (32 - fy) * (32 - fx), (32 - fy) * fx, fy * (32 - fx), fy * fx };
+                const int dx[4] = { 0, 1, 0, 1 }, dy[4] = { 0, 0, 1, 1 };
+                for (int k = 0; k < 4; k++)
+                {
+                    const int cx = cux + dx[k], cy = cuy + dy[k];
+                    if (cx < wcu && cy < hcu && cx >= 0 && cy >= 0)
+                        xo_clip_add(&refCosts[l][i0 + dx[k] + dy[k] * wcu],
+                                    (int32_t)((uint32_t)mul_wrap(la, w[k]) + 512u) >> 10);
+                }
+            }
+        }
+    }
+    free(scratch);
 }

@@ -142,6 +142,17 @@ void     xo_lowres_bcost(int wcu, int hcu, int rows_per_slice, int num_slices, c
                          const uint16_t* mvcost_centre, int do_search0, int do_search1, int16_t* mvs0,
                          int32_t* mv_costs0, int16_t* mvs1, int32_t* mv_costs1, uint16_t* lowres_costs,
                          int32_t* row_satd, int64_t* cost_est);
+/* f1 cuTree: Lookahead::estimateCUPropagate (slicetype.cpp:1738-1836) with the propagateCost
+ * primitive (pixel.cpp:846-872) for one (p0, b, p1) = (0, b_p0, b_p0 + p1_b): reads frame b's
+ * propagate_b (referenced; with referenced = 0 its first row is zeroed and re-read, as the
+ * reference does), intra_cost, lowres_costs (= lowresCosts[b - p0][p1 - b]), inv_q, the list-0 /
+ * list-1 MVs (lowresMvs[l][listDist[l]], x / y int16 pairs), and adds the propagated amounts into
+ * ref0 / ref1 (frames[p0 / p1]->propagateCost, saturating uint16).  fps_num / fps_den and
+ * avg_duration as x265_param / cuTree's averageDuration; weighted_bipred = bEnableWeightedBiPred. */
+void     xo_cutree_propagate(int wcu, int hcu, int b_p0, int p1_b, int referenced, int weighted_bipred,
+                             int fps_num, int fps_den, double avg_duration, uint16_t* propagate_b,
+                             const int32_t* intra_cost, const uint16_t* lowres_costs, const int32_t* inv_q,
+                             const int32_t* mvs0, const int32_t* mvs1, uint16_t* ref0, uint16_t* ref1);
 /* f2: MotionEstimate::motionEstimate (motion.cpp:571-1172) for one w x h PU on a full-resolution
  * reference: method 0 = DIA, 1 = HEX, 2 = STAR; subme 0..3 (at 3 the 4:2:0 chroma SATD of
  * subpelCompare is added when fcb != NULL and the chroma PU has a satd entry: fcb / fcr, rcb / rcr =

@@ -955,3 +955,107 @@ extern "C" int x265amd_lowres_bcost(int depth, const x265amd_lowres_bcost_batch*
     else hipLaunchKernelGGL((k_lowres_bcost<uint16_t>), dim3(blocks), dim3(64 * nw), 0, st, a);
     return (int)hipGetLastError();
 }
+
+// ================================================================ f1 cuTree propagation
+namespace x265amd {
+
+// (int) of a double the way x86-64 cvttsd2si converts it (INT_MIN when out of range / NaN)
+__device__ __forceinline__ int cvt_trunc_x86(double v)
+{
+    return (v > -2147483649.0 && v < 2147483648.0) ? (int)v : INT32_MIN;
+}
+
+// estimateCUPropagateCost (pixel.cpp:846-872), no FMA contraction: the reference's double
+// multiply / add / divide sequence rounded step by step
+__device__ __forceinline__ int propagate_amount(int in, int intra, int inter_raw, int invq, double fps)
+{
+    const int ic = inter_raw & ((1 << 14) - 1);
+    const int inter = intra < ic ? intra : ic;
+    const double pintra = (double)(int)((uint32_t)intra * (uint32_t)invq);
+    const double amount = __dadd_rn((double)in, __dmul_rn(pintra, fps));
+    const double r = __dadd_rn(__ddiv_rn(__dmul_rn(amount, (double)(intra - inter)), (double)intra), 0.5);
+    return cvt_trunc_x86(r);
+}
+
+// one thread per CU: shares onto the reference frames' CUs, accumulated in int64
+__global__ __launch_bounds__(X265AMD_BLOCK) void k_propagate(const x265amd_propagate_batch b)
+{
+    const int n = b.width_cu * b.height_cu;
+    const int cu = (int)(blockIdx.x * X265AMD_BLOCK + threadIdx.x);
+    if (cu >= n) return;
+    const int in = b.propagate_in ? (int)b.propagate_in[cu] : 0;
+    const int lc = (int)b.lowres_costs[cu];
+    const int amount = propagate_amount(in, b.intra_cost[cu], lc, b.inv_qscale[cu], b.fps_factor / 256);
+    if (amount <= 0) return;
+    const int used = lc >> 14;
+    const int bx = cu % b.width_cu, by = cu / b.width_cu;
+    for (int l = 0; l < 2; l++)
+    {
+        if (!((used >> l) & 1)) continue;
+        int la = amount;
+        if (used == 3) la = (int)((uint32_t)la * (uint32_t)b.bipred_weight[l] + 32u) >> 6;
+        unsigned long long* acc = (unsigned long long*)b.scratch + (size_t)l * n;
+        const int32_t mv = b.mvs[l][cu];
+        if (!mv)
+        {
+            atomicAdd(acc + cu, (unsigned long long)la);
+            continue;
+        }
+        const int x = (int16_t)(mv & 0xffff), y = (int16_t)((uint32_t)mv >> 16);
+        const int cux = (x >> 5) + bx, cuy = (y >> 5) + by, fx = x & 31, fy = y & 31;
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+        {
+            const int dx = k & 1, dy = k >> 1;
+            const int cx = cux + dx, cy = cuy + dy;
+            if (cx < 0 || cy < 0 || cx >= b.width_cu || cy >= b.height_cu) continue;
+            const int w = (dy ? fy : 32 - fy) * (dx ? fx : 32 - fx);
+            const int share = (int)((uint32_t)la * (uint32_t)w + 512u) >> 10;
+            atomicAdd(acc + cy * b.width_cu + cx, (unsigned long long)share);
+        }
+    }
+}
+
+// CLIP_ADD of the accumulated shares (order-free for non-negative shares)
+__global__ __launch_bounds__(X265AMD_BLOCK) void k_propagate_finish(const x265amd_propagate_batch b)
+{
+    const int n = b.width_cu * b.height_cu;
+    const int t = (int)(blockIdx.x * X265AMD_BLOCK + threadIdx.x);
+    if (t >= 2 * n) return;
+    const int l = t / n, cu = t % n;
+    if (!b.ref_costs[l]) return;
+    const unsigned long long a = ((const unsigned long long*)b.scratch)[t];
+    if (!a) return;
+    const unsigned long long v = (unsigned long long)b.ref_costs[l][cu] + a;
+    b.ref_costs[l][cu] = (uint16_t)(v < 65535ull ? v : 65535ull);
+}
+
+} // namespace x265amd
+
+extern "C" int x265amd_cutree_propagate(int count, const x265amd_propagate_batch* batches, void* stream)
+{
+    using namespace x265amd;
+    if (count < 0 || (count && !batches)) return X265AMD_EINVAL;
+    for (int i = 0; i < count; i++)
+    {
+        const x265amd_propagate_batch& b = batches[i];
+        if (b.width_cu <= 0 || b.height_cu <= 0 || !b.intra_cost || !b.lowres_costs || !b.inv_qscale || !b.scratch ||
+            !b.mvs[0] || !b.ref_costs[0])
+            return X265AMD_EINVAL;
+    }
+    hipStream_t st = (hipStream_t)stream;
+    for (int i = 0; i < count; i++)
+    {
+        const x265amd_propagate_batch& b = batches[i];
+        const size_t n = (size_t)b.width_cu * b.height_cu;
+        hipError_t e = hipMemsetAsync(b.scratch, 0, 2 * n * sizeof(int64_t), st);
+        if (e != hipSuccess) return (int)e;
+        hipLaunchKernelGGL(k_propagate, dim3((unsigned)((n + X265AMD_BLOCK - 1) / X265AMD_BLOCK)), dim3(X265AMD_BLOCK),
+                           0, st, b);
+        hipLaunchKernelGGL(k_propagate_finish, dim3((unsigned)((2 * n + X265AMD_BLOCK - 1) / X265AMD_BLOCK)),
+                           dim3(X265AMD_BLOCK), 0, st, b);
+        e = hipGetLastError();
+        if (e != hipSuccess) return (int)e;
+    }
+    return 0;
+}

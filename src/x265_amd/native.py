@@ -101,6 +101,12 @@ class DeblockFrame(C.Structure):
                 ("ref_poc", (C.c_int32 * 16) * 2)]
 
 
+class PropagateBatch(C.Structure):
+    _fields_ = [("width_cu", _int), ("height_cu", _int), ("propagate_in", _vp), ("intra_cost", _vp),
+                ("lowres_costs", _vp), ("inv_qscale", _vp), ("mvs", _vp * 2), ("fps_factor", C.c_double),
+                ("bipred_weight", _int * 2), ("ref_costs", _vp * 2), ("scratch", _vp)]
+
+
 class BorderPlane(C.Structure):
     _fields_ = [("plane", _vp), ("stride", _i64), ("width", _int), ("height", _int), ("margin_x", _int),
                 ("margin_y", _int)]
@@ -331,6 +337,21 @@ class Primitives:
 
     def extend_border(self, depth, planes, stream=None):
         self._frames("x265amd_extend_border", "extend_border", depth, planes, stream)
+
+    # -- f1 cuTree propagation (x265amd_cutree_propagate): one estimateCUPropagate per dict, in order
+    def cutree_propagate(self, jobs, stream=None):
+        arr = (PropagateBatch * len(jobs))()
+        for i, j in enumerate(jobs):
+            b = arr[i]
+            b.width_cu, b.height_cu = j["wcu"], j["hcu"]
+            b.propagate_in, b.intra_cost = _addr(j["prop"]), _addr(j["intra"])
+            b.lowres_costs, b.inv_qscale = _addr(j["lowres"]), _addr(j["invq"])
+            b.mvs[0], b.mvs[1] = _addr(j["mvs"][0]), _addr(j["mvs"][1])
+            b.fps_factor = float(j["fps_factor"])
+            b.bipred_weight[0], b.bipred_weight[1] = int(j["weights"][0]), int(j["weights"][1])
+            b.ref_costs[0], b.ref_costs[1] = _addr(j["refs"][0]), _addr(j["refs"][1])
+            b.scratch = _addr(j["scratch"])
+        self._check(self.lib.x265amd_cutree_propagate(len(jobs), arr, stream or _stream()), "cutree_propagate")
 
     # row-band forms (the frame-parallel pipeline): rows is a flat list of ints per frame / plane
     def _rows(self, entry, what, depth, frames, rows, per, stream):
