@@ -501,6 +501,35 @@ typedef struct
 } x265amd_propagate_batch;
 int x265amd_cutree_propagate(int count, const x265amd_propagate_batch* batches, void* stream);
 
+/* f1 weightp: LookaheadTLD::weightsAnalyse (slicetype.cpp:391-495) for one (fenc, ref) lowres
+ * pair: the weight_pp primitive (pixel.cpp:463-488) over the padded planes and the
+ * weightCostLuma passes (Σ min(satd 8x8, intraCost), slicetype.cpp:338-368) on the device; the
+ * reference's float decisions (guess scale, offset, denominator reduction, 0.998 threshold) on
+ * the host between them, so the call is synchronous on `stream` (two 4-byte read-backs).
+ * Geometry as Lowres::create (lowres.cpp:30-60): width / lines multiples of 8, stride,
+ * padded_lines = planesize / stride, pad_offset = lowresPlane - buffer.  fenc_plane =
+ * fenc.lowresPlane[0]; ref_buf[4] = ref.buffer[]; wbuf[4] = the weighted planes' buffers (the
+ * LookaheadTLD wbuffer: plane 0 is written by the weighted cost pass, all four when a weight is
+ * chosen); scratch = one device uint32.  Outputs: weighted (weightedRef.isWeighted), the chosen
+ * scale / denom / offset (WeightParam inputWeight / log2WeightDenom / inputOffset) and
+ * cost_delta (weightedCostDelta[frame distance], set when weighted). */
+typedef struct
+{
+    int width, lines;
+    int64_t stride;
+    int padded_lines;
+    int64_t pad_offset;
+    const void* fenc_plane;
+    const void* ref_buf[4];
+    const int32_t* intra_cost;
+    void* wbuf[4];
+    uint32_t* scratch;
+    uint64_t fenc_ssd, ref_ssd, fenc_sum, ref_sum;
+    int weighted, scale, denom, offset;
+    double cost_delta;
+} x265amd_weights_batch;
+int x265amd_weights_analyse(int depth, x265amd_weights_batch* batch, void* stream);
+
 /* ------------------------------------------------------------------- f2
  * Full-resolution motion search.  Job i is one
  * MotionEstimate::motionEstimate call (motion.cpp:571-1172) on a full-resolution

@@ -297,3 +297,27 @@ class CuTree:
         self.lib.xo_cutree_propagate(wcu, hcu, b_p0, p1_b, referenced, weighted_bipred, fps_num, fps_den,
                                      avg_duration, _p(prop_b), _p(intra), _p(lowres_costs), _p(inv_q), _p(mvs0),
                                      _p(mvs1), _p(ref0), _p(ref1))
+
+
+class Weights:
+    """xo_weights_analyse of one library: LookaheadTLD::weightsAnalyse (slicetype.cpp:391-495)."""
+
+    def __init__(self, kind: str, depth: int = 8):
+        self.lib = C.CDLL(lib_path(kind, depth))
+        self.lib.xo_weights_analyse.argtypes = [C.c_int, C.c_int, _ip, C.c_int, _ip, _vp, C.POINTER(_vp), _vp,
+                                                C.POINTER(_vp), C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, _vp,
+                                                C.POINTER(C.c_double)]
+
+    def analyse(self, width, lines, stride, padded_lines, pad_offset, fenc_buf, ref_buf, intra, wbuf, fssd, rssd,
+                fsum, rsum):
+        """fenc_buf / ref_buf / wbuf: contiguous (4, planesize) numpy arrays; returns (out[4], cost_delta)"""
+        ps = ref_buf.shape[1]
+        es = ref_buf.itemsize
+        rb = (_vp * 4)(*[ref_buf.ctypes.data + i * ps * es for i in range(4)])
+        wb = (_vp * 4)(*[wbuf.ctypes.data + i * ps * es for i in range(4)])
+        out = np.zeros(4, np.int32)
+        delta = C.c_double(-1.0)
+        self.lib.xo_weights_analyse(width, lines, stride, padded_lines, pad_offset,
+                                    fenc_buf.ctypes.data + pad_offset * es, rb, _p(intra), wb, int(fssd), int(rssd),
+                                    int(fsum), int(rsum), _p(out), C.byref(delta))
+        return out, delta.value

@@ -682,6 +682,51 @@ void xo_lowres_pcost(int wcu, int hcu, int rows_per_slice, int num_slices, const
     x265_param_free(param);
 }
 
+/* f1 weightp: the reference's own LookaheadTLD::weightsAnalyse (slicetype.cpp:391-495) on Lowres
+ * frames wired to the caller's contiguous 4-plane buffers (as Lowres::create allocates them) */
+void xo_weights_analyse(int width, int lines, intptr_t stride, int padded_lines, intptr_t pad_offset,
+                        const void* fenc_plane, const void* const* ref_buf, const int32_t* intra_cost,
+                        void* const* wbuf, uint64_t fenc_ssd, uint64_t ref_ssd, uint64_t fenc_sum,
+                        uint64_t ref_sum, int* out, double* cost_delta)
+{
+    pthread_once(&g_prim_once, init_global_prims);
+    const size_t planesize = (size_t)stride * padded_lines;
+    Lowres* fenc = (Lowres*)calloc(1, sizeof(Lowres));
+    Lowres* ref = (Lowres*)calloc(1, sizeof(Lowres));
+    /* weightsAnalyse reads only fenc's plane 0 but sizes its buffers from fenc.buffer[1] - buffer[0] */
+    pixel* fbuf = (pixel*)fenc_plane - pad_offset;
+    for (int i = 0; i < 4; i++)
+    {
+        fenc->buffer[i] = fbuf + i * planesize;
+        fenc->lowresPlane[i] = fenc->buffer[i] + pad_offset;
+        ref->buffer[i] = (pixel*)ref_buf[i];
+        ref->lowresPlane[i] = ref->buffer[i] + pad_offset;
+    }
+    fenc->fpelPlane[0] = fenc->lowresPlane[0];
+    ref->fpelPlane[0] = ref->lowresPlane[0];
+    fenc->lumaStride = ref->lumaStride = stride;
+    fenc->width = ref->width = width;
+    fenc->lines = ref->lines = lines;
+    fenc->isLowres = ref->isLowres = true;
+    fenc->frameNum = 1;
+    ref->frameNum = 0;
+    fenc->intraCost = (int32_t*)intra_cost;
+    fenc->wp_ssd[0] = fenc_ssd;
+    ref->wp_ssd[0] = ref_ssd;
+    fenc->wp_sum[0] = fenc_sum;
+    ref->wp_sum[0] = ref_sum;
+    LookaheadTLD* tld = new LookaheadTLD();
+    tld->weightsAnalyse(*fenc, *ref);
+    ReferencePlanes& wr = fenc->weightedRef[1];
+    out[0] = wr.isWeighted ? 1 : 0;
+    if (tld->wbuffer[0])
+        for (int i = 0; i < 4; i++) memcpy(wbuf[i], tld->wbuffer[i], planesize * sizeof(pixel));
+    if (wr.isWeighted) *cost_delta = fenc->weightedCostDelta[1];
+    free(fenc);
+    free(ref);
+    delete tld;
+}
+
 /* f1 cuTree: the reference's own Lookahead::estimateCUPropagate (slicetype.cpp:1738-1836) for
  * (p0, b, p1) = (0, b_p0, b_p0 + p1_b) on Lowres frames wired to the caller's arrays */
 void xo_cutree_propagate(int wcu, int hcu, int b_p0, int p1_b, int referenced, int weighted_bipred,

@@ -2204,3 +2204,92 @@ void xo_cutree_propagate(int wcu, int hcu, int b_p0, int p1_b, int referenced, i
     }
     free(scratch);
 }
+
+/* ======================================================= f1 weighted-prediction analysis */
+
+/* pixel.cpp:463-488 weight_pp_c */
+static void xo_weight_pp(const pix* src, pix* dst, intptr_t stride, int width, int height, int w0, int round,
+                         int shift, int offset)
+{
+    const int correction = 14 - XO_DEPTH;
+    for (int y = 0; y < height; y++, src += stride, dst += stride)
+        for (int x = 0; x < width; x++)
+        {
+            const int16_t val = (int16_t)shl_wrap(src[x], correction);
+            const int v = ((w0 * val + round) >> shift) + offset;
+            dst[x] = (pix)(v < 0 ? 0 : v > PMAX ? PMAX : v);
+        }
+}
+
+/* slicetype.cpp:338-368 weightCostLuma */
+static uint32_t xo_weight_cost_luma(int width, int lines, intptr_t stride, int padded_lines, intptr_t padoff,
+                                    const pix* fenc, const pix* ref_buf0, const int32_t* intra, pix* wbuf0,
+                                    int present, int w0, int denom, int offset)
+{
+    const pix* src = ref_buf0 + padoff;
+    if (present)
+    {
+        const int off = offset << (XO_DEPTH - 8), round = denom ? 1 << (denom - 1) : 0, corr = 14 - XO_DEPTH;
+        xo_weight_pp(ref_buf0, wbuf0, stride, (int)stride, padded_lines, w0, round << corr, denom + corr, off);
+        src = wbuf0 + padoff;
+    }
+    uint32_t cost = 0;
+    int mb = 0;
+    for (int y = 0; y < lines; y += 8)
+        for (int x = 0; x < width; x += 8, mb++)
+        {
+            const int satd = xo_satd(8, 8, src + y * stride + x, stride, fenc + y * stride + x, stride);
+            cost += (uint32_t)(satd < intra[mb] ? satd : intra[mb]);
+        }
+    return cost;
+}
+
+/* slicetype.cpp:391-495 */
+void xo_weights_analyse(int width, int lines, intptr_t stride, int padded_lines, intptr_t pad_offset,
+                        const void* fenc_plane, const void* const* ref_buf, const int32_t* intra_cost,
+                        void* const* wbuf, uint64_t fenc_ssd, uint64_t ref_ssd, uint64_t fenc_sum,
+                        uint64_t ref_sum, int* out, double* cost_delta)
+{
+    const float epsilon = 1.f / 128.f;
+    const pix* fenc = (const pix*)fenc_plane;
+    out[0] = 0;
+    float guessScale;
+    if (fenc_ssd && ref_ssd) guessScale = sqrtf((float)fenc_ssd / ref_ssd);
+    else guessScale = 1.0f;
+    const float fencMean = (float)fenc_sum / (lines * width) / (1 << (XO_DEPTH - 8));
+    const float refMean = (float)ref_sum / (lines * width) / (1 << (XO_DEPTH - 8));
+    if (fabsf(refMean - fencMean) < 0.5f && fabsf(1.f - guessScale) < epsilon) return;
+
+    /* WeightParam::setFromWeightAndOffset(w, 0, 7, true) (slice.h:293-305) */
+    int mindenom = 7, minscale = (int)(guessScale * 128 + 0.5f);
+    while (mindenom > 0 && minscale > 127) { mindenom--; minscale >>= 1; }
+    if (minscale > 127) minscale = 127;
+    int minoff = 0, found = 0;
+    unsigned int minscore, origscore;
+    origscore = minscore = xo_weight_cost_luma(width, lines, stride, padded_lines, pad_offset, fenc,
+                                               (const pix*)ref_buf[0], intra_cost, (pix*)wbuf[0], 0, 0, 0, 0);
+    if (!minscore) return;
+    int curScale = minscale;
+    int curOffset = (int)(fencMean - refMean * curScale / (1 << mindenom) + 0.5f);
+    if (curOffset < -128 || curOffset > 127)
+    {
+        curOffset = curOffset < -128 ? -128 : 127;
+        curScale = (int)((1 << mindenom) * (fencMean - curOffset) / refMean + 0.5f);
+        curScale = curScale < 0 ? 0 : curScale > 127 ? 127 : curScale;
+    }
+    const unsigned int s = xo_weight_cost_luma(width, lines, stride, padded_lines, pad_offset, fenc,
+                                               (const pix*)ref_buf[0], intra_cost, (pix*)wbuf[0], 1, curScale,
+                                               mindenom, curOffset);
+    if (s < minscore) { minscore = s; minscale = curScale; minoff = curOffset; found = 1; }
+    while (mindenom > 0 && !(minscale & 1)) { mindenom--; minscale >>= 1; }
+    if (!found || (minscale == 1 << mindenom && minoff == 0) || (float)minscore / origscore > 0.998f) return;
+    *cost_delta = minscore / origscore;
+    const int off = minoff << (XO_DEPTH - 8), round = mindenom ? 1 << (mindenom - 1) : 0, corr = 14 - XO_DEPTH;
+    for (int i = 0; i < 4; i++)
+        xo_weight_pp((const pix*)ref_buf[i], (pix*)wbuf[i], stride, (int)stride, padded_lines, minscale,
+                     round << corr, mindenom + corr, off);
+    out[0] = 1;
+    out[1] = minscale;
+    out[2] = mindenom;
+    out[3] = minoff;
+}

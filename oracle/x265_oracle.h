@@ -153,6 +153,18 @@ void     xo_cutree_propagate(int wcu, int hcu, int b_p0, int p1_b, int reference
                              int fps_num, int fps_den, double avg_duration, uint16_t* propagate_b,
                              const int32_t* intra_cost, const uint16_t* lowres_costs, const int32_t* inv_q,
                              const int32_t* mvs0, const int32_t* mvs1, uint16_t* ref0, uint16_t* ref1);
+/* f1 weightp: LookaheadTLD::weightsAnalyse (slicetype.cpp:391-495) with weightCostLuma
+ * (:338-368) and the weight_pp primitive (pixel.cpp:463-488).  Lowres geometry as Lowres::create
+ * (lowres.cpp:30-60): width / lines (multiples of 8), stride, padded_lines = planesize / stride,
+ * pad_offset = lowresPlane - buffer.  fenc_plane = fenc.lowresPlane[0]; ref_buf[4] = ref.buffer[];
+ * wbuf[4] = the weighted planes' buffers (written: plane 0 by the cost passes, all four when a
+ * weight is chosen); *_ssd / *_sum = Lowres wp_ssd[0] / wp_sum[0].  out[0] = isWeighted,
+ * out[1..3] = inputWeight, log2WeightDenom, inputOffset of the chosen weight;
+ * *cost_delta = weightedCostDelta (set only when weighted). */
+void     xo_weights_analyse(int width, int lines, intptr_t stride, int padded_lines, intptr_t pad_offset,
+                            const void* fenc_plane, const void* const* ref_buf, const int32_t* intra_cost,
+                            void* const* wbuf, uint64_t fenc_ssd, uint64_t ref_ssd, uint64_t fenc_sum,
+                            uint64_t ref_sum, int* out, double* cost_delta);
 /* f2: MotionEstimate::motionEstimate (motion.cpp:571-1172) for one w x h PU on a full-resolution
  * reference: method 0 = DIA, 1 = HEX, 2 = STAR; subme 0..3 (at 3 the 4:2:0 chroma SATD of
  * subpelCompare is added when fcb != NULL and the chroma PU has a satd entry: fcb / fcr, rcb / rcr =

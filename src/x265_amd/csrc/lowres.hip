@@ -1059,3 +1059,188 @@ extern "C" int x265amd_cutree_propagate(int count, const x265amd_propagate_batch
     }
     return 0;
 }
+
+// ================================================================ f1 weighted-prediction analysis
+namespace x265amd {
+
+// weight_pp_c (pixel.cpp:463-488) over a whole padded plane, C pixels per thread
+template <typename P>
+__global__ __launch_bounds__(X265AMD_BLOCK) void k_weight_pp(const P* __restrict__ src, P* __restrict__ dst,
+                                                             int64_t n, int w0, int round, int shift, int offset,
+                                                             int maxv)
+{
+    constexpr int C = 16 / sizeof(P);
+    const int64_t i0 = ((int64_t)blockIdx.x * X265AMD_BLOCK + threadIdx.x) * C;
+    if (i0 >= n) return;
+    const int corr = 14 - (sizeof(P) == 1 ? 8 : (maxv == 1023 ? 10 : 12));
+    if (i0 + C <= n)
+    {
+        int v[C];
+        load_row<P, C>(src + i0, v);
+#pragma unroll
+        for (int k = 0; k < C; k++)
+        {
+            const int16_t val = (int16_t)(v[k] << corr);
+            const int r = ((w0 * val + round) >> shift) + offset;
+            v[k] = r < 0 ? 0 : (r > maxv ? maxv : r);
+        }
+        store_row<P, C>(dst + i0, v);
+        return;
+    }
+    for (int64_t i = i0; i < n; i++)
+    {
+        const int16_t val = (int16_t)((int)src[i] << corr);
+        const int r = ((w0 * val + round) >> shift) + offset;
+        dst[i] = (P)(r < 0 ? 0 : (r > maxv ? maxv : r));
+    }
+}
+
+// weightCostLuma's sum (slicetype.cpp:359-365): one thread per 8x8 block, satd 8x8 as four 4x4
+// Hadamard sums (>> 1 once: SURVEY note a7), min with intraCost, uint32 sum (order-free)
+template <typename P>
+__global__ __launch_bounds__(X265AMD_BLOCK) void k_weight_cost(const P* __restrict__ src, const P* __restrict__ fenc,
+                                                               int64_t stride, int wcu, int hcu,
+                                                               const int32_t* __restrict__ intra, uint32_t* cost)
+{
+    const int mb = (int)(blockIdx.x * X265AMD_BLOCK + threadIdx.x);
+    int c = 0;
+    if (mb < wcu * hcu)
+    {
+        const int64_t off = (int64_t)(mb / wcu) * 8 * stride + (mb % wcu) * 8;
+        int d[8][8];
+#pragma unroll
+        for (int r = 0; r < 8; r++)
+        {
+            int a[8], b[8];
+            load_row<P, 8>(src + off + r * stride, a);
+            load_row<P, 8>(fenc + off + r * stride, b);
+#pragma unroll
+            for (int x = 0; x < 8; x++) d[r][x] = a[x] - b[x];
+        }
+        int sum = 0;
+#pragma unroll
+        for (int qy = 0; qy < 8; qy += 4)
+#pragma unroll
+            for (int qx = 0; qx < 8; qx += 4)
+            {
+#pragma unroll
+                for (int r = 0; r < 4; r++) had4(d[qy + r][qx], d[qy + r][qx + 1], d[qy + r][qx + 2], d[qy + r][qx + 3]);
+#pragma unroll
+                for (int x = 0; x < 4; x++)
+                {
+                    had4(d[qy][qx + x], d[qy + 1][qx + x], d[qy + 2][qx + x], d[qy + 3][qx + x]);
+#pragma unroll
+                    for (int r = 0; r < 4; r++) sum += d[qy + r][qx + x] < 0 ? -d[qy + r][qx + x] : d[qy + r][qx + x];
+                }
+            }
+        const int satd = sum >> 1;
+        c = satd < intra[mb] ? satd : intra[mb];
+    }
+    // wave sum, one atomic per wave
+#pragma unroll
+    for (int o = 32; o; o >>= 1) c += __shfl_xor(c, o);
+    if ((threadIdx.x & 63) == 0 && c) atomicAdd(cost, (uint32_t)c);
+}
+
+template <typename P>
+static int weight_pp_plane(const void* src, void* dst, int64_t n, int w0, int round, int shift, int offset, int maxv,
+                           hipStream_t st)
+{
+    constexpr int C = 16 / sizeof(P);
+    const int64_t threads = (n + C - 1) / C;
+    hipLaunchKernelGGL(k_weight_pp<P>, dim3((unsigned)((threads + X265AMD_BLOCK - 1) / X265AMD_BLOCK)),
+                       dim3(X265AMD_BLOCK), 0, st, (const P*)src, (P*)dst, n, w0, round, shift, offset, maxv);
+    return (int)hipGetLastError();
+}
+
+// weightCostLuma (slicetype.cpp:338-368): weighted (present) or plain reference vs fenc
+template <typename P>
+static int weight_cost(const x265amd_weights_batch& b, int depth, bool present, int w0, int denom, int offset,
+                       uint32_t* out, hipStream_t st)
+{
+    const P* src = (const P*)b.ref_buf[0] + b.pad_offset;
+    const int maxv = (1 << depth) - 1;
+    if (present)
+    {
+        const int off = offset << (depth - 8), round = denom ? 1 << (denom - 1) : 0, corr = 14 - depth;
+        int rc = weight_pp_plane<P>(b.ref_buf[0], b.wbuf[0], b.stride * b.padded_lines, w0, round << corr,
+                                    denom + corr, off, maxv, st);
+        if (rc) return rc;
+        src = (const P*)b.wbuf[0] + b.pad_offset;
+    }
+    hipError_t e = hipMemsetAsync(b.scratch, 0, 4, st);
+    if (e != hipSuccess) return (int)e;
+    const int wcu = b.width / 8, hcu = b.lines / 8;
+    hipLaunchKernelGGL(k_weight_cost<P>, dim3((unsigned)((wcu * hcu + X265AMD_BLOCK - 1) / X265AMD_BLOCK)),
+                       dim3(X265AMD_BLOCK), 0, st, src, (const P*)b.fenc_plane, b.stride, wcu, hcu, b.intra_cost,
+                       b.scratch);
+    e = hipGetLastError();
+    if (e != hipSuccess) return (int)e;
+    e = hipMemcpyAsync(out, b.scratch, 4, hipMemcpyDeviceToHost, st);
+    if (e != hipSuccess) return (int)e;
+    return (int)hipStreamSynchronize(st);
+}
+
+// LookaheadTLD::weightsAnalyse (slicetype.cpp:391-495); the host float arithmetic is the
+// reference's, statement for statement
+template <typename P>
+static int weights_analyse(int depth, x265amd_weights_batch& b, hipStream_t st)
+{
+    const float epsilon = 1.f / 128.f;
+    b.weighted = 0;
+    float guessScale;
+    if (b.fenc_ssd && b.ref_ssd) guessScale = sqrtf((float)b.fenc_ssd / b.ref_ssd);
+    else guessScale = 1.0f;
+    const float fencMean = (float)b.fenc_sum / (b.lines * b.width) / (1 << (depth - 8));
+    const float refMean = (float)b.ref_sum / (b.lines * b.width) / (1 << (depth - 8));
+    if (fabsf(refMean - fencMean) < 0.5f && fabsf(1.f - guessScale) < epsilon) return 0;
+    int mindenom = 7, minscale = (int)(guessScale * 128 + 0.5f);          // setFromWeightAndOffset
+    while (mindenom > 0 && minscale > 127) { mindenom--; minscale >>= 1; }
+    if (minscale > 127) minscale = 127;
+    int minoff = 0, found = 0;
+    uint32_t minscore = 0, origscore = 0, s = 0;
+    int rc = weight_cost<P>(b, depth, false, 0, 0, 0, &origscore, st);
+    if (rc) return rc;
+    minscore = origscore;
+    if (!minscore) return 0;
+    int curScale = minscale;
+    int curOffset = (int)(fencMean - refMean * curScale / (1 << mindenom) + 0.5f);
+    if (curOffset < -128 || curOffset > 127)
+    {
+        curOffset = curOffset < -128 ? -128 : 127;
+        curScale = (int)((1 << mindenom) * (fencMean - curOffset) / refMean + 0.5f);
+        curScale = curScale < 0 ? 0 : (curScale > 127 ? 127 : curScale);
+    }
+    rc = weight_cost<P>(b, depth, true, curScale, mindenom, curOffset, &s, st);
+    if (rc) return rc;
+    if (s < minscore) { minscore = s; minscale = curScale; minoff = curOffset; found = 1; }
+    while (mindenom > 0 && !(minscale & 1)) { mindenom--; minscale >>= 1; }
+    if (!found || (minscale == 1 << mindenom && minoff == 0) || (float)minscore / origscore > 0.998f) return 0;
+    b.cost_delta = minscore / origscore;
+    const int off = minoff << (depth - 8), round = mindenom ? 1 << (mindenom - 1) : 0, corr = 14 - depth;
+    for (int i = 0; i < 4; i++)
+    {
+        rc = weight_pp_plane<P>(b.ref_buf[i], b.wbuf[i], b.stride * b.padded_lines, minscale, round << corr,
+                                mindenom + corr, off, (1 << depth) - 1, st);
+        if (rc) return rc;
+    }
+    b.weighted = 1;
+    b.scale = minscale;
+    b.denom = mindenom;
+    b.offset = minoff;
+    return 0;
+}
+
+} // namespace x265amd
+
+extern "C" int x265amd_weights_analyse(int depth, x265amd_weights_batch* b, void* stream)
+{
+    using namespace x265amd;
+    if (!b || (depth != 8 && depth != 10 && depth != 12) || b->width <= 0 || b->lines <= 0 || (b->width & 7) ||
+        (b->lines & 7) || b->stride < b->width || !b->fenc_plane || !b->intra_cost || !b->scratch)
+        return X265AMD_EINVAL;
+    for (int i = 0; i < 4; i++)
+        if (!b->ref_buf[i] || !b->wbuf[i]) return X265AMD_EINVAL;
+    hipStream_t st = (hipStream_t)stream;
+    return depth == 8 ? weights_analyse<uint8_t>(depth, *b, st) : weights_analyse<uint16_t>(depth, *b, st);
+}

@@ -107,6 +107,14 @@ class PropagateBatch(C.Structure):
                 ("bipred_weight", _int * 2), ("ref_costs", _vp * 2), ("scratch", _vp)]
 
 
+class WeightsBatch(C.Structure):
+    _fields_ = [("width", _int), ("lines", _int), ("stride", _i64), ("padded_lines", _int), ("pad_offset", _i64),
+                ("fenc_plane", _vp), ("ref_buf", _vp * 4), ("intra_cost", _vp), ("wbuf", _vp * 4),
+                ("scratch", _vp), ("fenc_ssd", C.c_uint64), ("ref_ssd", C.c_uint64), ("fenc_sum", C.c_uint64),
+                ("ref_sum", C.c_uint64), ("weighted", _int), ("scale", _int), ("denom", _int), ("offset", _int),
+                ("cost_delta", C.c_double)]
+
+
 class BorderPlane(C.Structure):
     _fields_ = [("plane", _vp), ("stride", _i64), ("width", _int), ("height", _int), ("margin_x", _int),
                 ("margin_y", _int)]
@@ -352,6 +360,29 @@ class Primitives:
             b.ref_costs[0], b.ref_costs[1] = _addr(j["refs"][0]), _addr(j["refs"][1])
             b.scratch = _addr(j["scratch"])
         self._check(self.lib.x265amd_cutree_propagate(len(jobs), arr, stream or _stream()), "cutree_propagate")
+
+    # -- f1 weightp (x265amd_weights_analyse): synchronous on the stream
+    def weights_analyse(self, depth, width, lines, stride, padded_lines, pad_offset, fenc_buf, ref_buf, intra, wbuf,
+                        fenc_ssd, ref_ssd, fenc_sum, ref_sum, stream=None):
+        """fenc_buf / ref_buf / wbuf: device tensors holding 4 contiguous padded lowres planes
+        (Lowres::create); returns the decision dict"""
+        import torch
+
+        b = WeightsBatch()
+        b.width, b.lines, b.stride, b.padded_lines, b.pad_offset = width, lines, stride, padded_lines, pad_offset
+        es = ref_buf.element_size()
+        ps = stride * padded_lines
+        b.fenc_plane = fenc_buf.data_ptr() + pad_offset * es
+        for i in range(4):
+            b.ref_buf[i] = ref_buf.data_ptr() + i * ps * es
+            b.wbuf[i] = wbuf.data_ptr() + i * ps * es
+        b.intra_cost = intra.data_ptr()
+        scratch = torch.zeros(1, dtype=torch.int32, device=ref_buf.device)
+        b.scratch = scratch.data_ptr()
+        b.fenc_ssd, b.ref_ssd, b.fenc_sum, b.ref_sum = int(fenc_ssd), int(ref_ssd), int(fenc_sum), int(ref_sum)
+        self._check(self.lib.x265amd_weights_analyse(depth, C.byref(b), stream or _stream()), "weights_analyse")
+        return {"weighted": b.weighted, "scale": b.scale, "denom": b.denom, "offset": b.offset,
+                "cost_delta": b.cost_delta}
 
     # row-band forms (the frame-parallel pipeline): rows is a flat list of ints per frame / plane
     def _rows(self, entry, what, depth, frames, rows, per, stream):
