@@ -231,35 +231,39 @@ class FrameFilters:
                                    _ip, _vp, _vp]
         L.xo_deblock.argtypes = [C.c_int, C.c_int, C.c_int, _vp, _vp, _vp, _ip, _ip, _vp, _ip, C.POINTER(DeblockParams)]
         L.xo_extend_border.argtypes = [_vp, _ip, C.c_int, C.c_int, C.c_int, C.c_int]
+        L.xo_sao_apply_csp.argtypes = L.xo_sao_apply.argtypes + [C.c_int]
+        L.xo_sao_stats_csp.argtypes = L.xo_sao_stats.argtypes + [C.c_int]
+        L.xo_deblock_csp.argtypes = L.xo_deblock.argtypes + [C.c_int]
 
     @staticmethod
     def _org(buf, margin, stride):
         return buf.ctypes.data + (margin * stride + margin) * buf.itemsize
 
-    def sao_apply(self, width, height, ctu_log2, planes, margin, params, luma_on=1, chroma_on=1):
-        """planes: (Y, Cb, Cr) padded 2-D arrays with `margin` pixels on every side; in place."""
+    def sao_apply(self, width, height, ctu_log2, planes, margin, params, luma_on=1, chroma_on=1, csp=1):
+        """planes: (Y, Cb, Cr) padded 2-D arrays with `margin` pixels on every side; in place.
+        csp: 1 = 4:2:0, 2 = 4:2:2, 3 = 4:4:4"""
         y, cb, cr = planes
-        self.lib.xo_sao_apply(width, height, ctu_log2, self._org(y, margin, y.shape[1]),
-                              self._org(cb, margin, cb.shape[1]), self._org(cr, margin, cr.shape[1]), y.shape[1],
-                              cb.shape[1], params.ctypes.data, luma_on, chroma_on)
+        self.lib.xo_sao_apply_csp(width, height, ctu_log2, self._org(y, margin, y.shape[1]),
+                                  self._org(cb, margin, cb.shape[1]), self._org(cr, margin, cr.shape[1]), y.shape[1],
+                                  cb.shape[1], params.ctypes.data, luma_on, chroma_on, csp)
 
-    def sao_stats(self, width, height, ctu_log2, fenc, rec, margin, non_deblocked=0):
+    def sao_stats(self, width, height, ctu_log2, fenc, rec, margin, non_deblocked=0, csp=1):
         ctu = 1 << ctu_log2
         nctu = ((width + ctu - 1) // ctu) * ((height + ctu - 1) // ctu)
         stats = np.zeros((nctu, 3, 5, 33), np.int32)
         count = np.zeros((nctu, 3, 5, 33), np.int32)
         f = [self._org(p, margin, p.shape[1]) for p in fenc]
         r = [self._org(p, margin, p.shape[1]) for p in rec]
-        self.lib.xo_sao_stats(width, height, ctu_log2, non_deblocked, f[0], f[1], f[2], fenc[0].shape[1],
-                              fenc[1].shape[1], r[0], r[1], r[2], rec[0].shape[1], rec[1].shape[1],
-                              stats.ctypes.data, count.ctypes.data)
+        self.lib.xo_sao_stats_csp(width, height, ctu_log2, non_deblocked, f[0], f[1], f[2], fenc[0].shape[1],
+                                  fenc[1].shape[1], r[0], r[1], r[2], rec[0].shape[1], rec[1].shape[1],
+                                  stats.ctypes.data, count.ctypes.data, csp)
         return stats, count
 
-    def deblock(self, width, height, ctu_log2, planes, margin, units, prm: DeblockParams):
+    def deblock(self, width, height, ctu_log2, planes, margin, units, prm: DeblockParams, csp=1):
         y, cb, cr = planes
-        self.lib.xo_deblock(width, height, ctu_log2, self._org(y, margin, y.shape[1]),
-                            self._org(cb, margin, cb.shape[1]), self._org(cr, margin, cr.shape[1]), y.shape[1],
-                            cb.shape[1], units.ctypes.data, units.shape[1], C.byref(prm))
+        self.lib.xo_deblock_csp(width, height, ctu_log2, self._org(y, margin, y.shape[1]),
+                                self._org(cb, margin, cb.shape[1]), self._org(cr, margin, cr.shape[1]), y.shape[1],
+                                cb.shape[1], units.ctypes.data, units.shape[1], C.byref(prm), csp)
 
     def extend_border(self, plane, margin_x, margin_y, width, height):
         self.lib.xo_extend_border(plane.ctypes.data + (margin_y * plane.shape[1] + margin_x) * plane.itemsize,

@@ -955,7 +955,8 @@ struct FrameShell
     CUDataMemPool pool;
     int wc, hc;
 
-    FrameShell(int width, int height, bool with_fenc, bool with_cudata)
+    int csp;
+    FrameShell(int width, int height, bool with_fenc, bool with_cudata, int csp_ = X265_CSP_I420) : csp(csp_)
     {
         memset(&sps, 0, sizeof(sps));
         memset(&pps, 0, sizeof(pps));
@@ -969,13 +970,13 @@ struct FrameShell
         slice.m_sps = &sps;
         slice.m_pps = &pps;
         recon = new PicYuv;
-        recon->create(width, height, X265_CSP_I420);
+        recon->create(width, height, csp);
         recon->createOffsets(sps);
         fenc = NULL;
         if (with_fenc)
         {
             fenc = new PicYuv;
-            fenc->create(width, height, X265_CSP_I420);
+            fenc->create(width, height, csp);
             fenc->createOffsets(sps);
         }
         fd = (FrameData*)calloc(1, sizeof(FrameData));
@@ -986,11 +987,11 @@ struct FrameShell
         frame->m_reconPic = recon;
         frame->m_fencPic = fenc;
         ctus = new CUData[wc * hc];
-        if (with_cudata) pool.create(0, X265_CSP_I420, wc * hc);
+        if (with_cudata) pool.create(0, csp, wc * hc);
         for (int i = 0; i < wc * hc; i++)
         {
             CUData& cu = ctus[i];
-            if (with_cudata) cu.initialize(pool, 0, X265_CSP_I420, i);
+            if (with_cudata) cu.initialize(pool, 0, csp, i);
             cu.m_encData = fd;
             cu.m_slice = &slice;
             cu.m_cuAddr = i;
@@ -998,8 +999,9 @@ struct FrameShell
             cu.m_cuPelY = (i / wc) << g_maxLog2CUSize;
             cu.m_absIdxInCTU = 0;
             cu.m_numPartitions = NUM_4x4_PARTITIONS;
-            cu.m_chromaFormat = X265_CSP_I420;
-            cu.m_hChromaShift = cu.m_vChromaShift = 1;
+            cu.m_chromaFormat = csp;
+            cu.m_hChromaShift = CHROMA_H_SHIFT(csp);
+            cu.m_vChromaShift = CHROMA_V_SHIFT(csp);
             cu.m_cuLeft = (i % wc) ? &ctus[i - 1] : NULL;
             cu.m_cuAbove = (i / wc) ? &ctus[i - wc] : NULL;
         }
@@ -1041,7 +1043,7 @@ struct ShimSao : public SAO
         const uint32_t addr = row * m_numCuInWidth + col;
         for (int p = 0; p < 3; p++)
         {
-            const int cw = p ? g_maxCUSize >> 1 : g_maxCUSize;
+            const int cw = p ? g_maxCUSize >> m_hChromaShift : g_maxCUSize;
             const intptr_t st = p ? snap->m_strideC : snap->m_stride;
             const pixel* r = snap->getPlaneAddr(p, addr) - (row == 0 ? 0 : st);
             memcpy(&m_tmpU[p][col * cw], r, cw * sizeof(pixel));
@@ -1052,12 +1054,12 @@ struct ShimSao : public SAO
     const int32_t* cnt(int p, int t) const { return m_count[p][t]; }
 };
 
-void sao_param_defaults(x265_param* prm, int width, int height, int non_deblocked)
+void sao_param_defaults(x265_param* prm, int width, int height, int non_deblocked, int csp = X265_CSP_I420)
 {
     x265_param_default(prm);
     prm->sourceWidth = width;
     prm->sourceHeight = height;
-    prm->internalCsp = X265_CSP_I420;
+    prm->internalCsp = csp;
     prm->maxCUSize = g_maxCUSize;
     prm->bSaoNonDeblocked = non_deblocked;
 }
@@ -1066,22 +1068,23 @@ void sao_param_defaults(x265_param* prm, int width, int height, int non_deblocke
 
 extern "C" {
 
-void xo_sao_apply(int width, int height, int ctu_log2, void* y, void* cb, void* cr, intptr_t stride,
-                  intptr_t cstride, const xo_sao_param* params, int luma_on, int chroma_on)
+void xo_sao_apply_csp(int width, int height, int ctu_log2, void* y, void* cb, void* cr, intptr_t stride,
+                      intptr_t cstride, const xo_sao_param* params, int luma_on, int chroma_on, int csp)
 {
     pthread_once(&g_prim_once, init_global_prims);
     set_ctu_globals(ctu_log2);
-    FrameShell fs(width, height, false, false);
-    FrameShell snap(width, height, false, false);
+    const int hs = CHROMA_H_SHIFT(csp), vs = CHROMA_V_SHIFT(csp);
+    FrameShell fs(width, height, false, false, csp);
+    FrameShell snap(width, height, false, false, csp);
     void* planes[3] = { y, cb, cr };
     for (int p = 0; p < 3; p++)
     {
-        const int w = p ? width >> 1 : width, h = p ? height >> 1 : height;
+        const int w = p ? width >> hs : width, h = p ? height >> vs : height;
         load_plane(fs.recon, p, planes[p], p ? cstride : stride, w, h);
         load_plane(snap.recon, p, planes[p], p ? cstride : stride, w, h);
     }
     x265_param prm;
-    sao_param_defaults(&prm, width, height, 0);
+    sao_param_defaults(&prm, width, height, 0, csp);
     ShimSao sao;
     sao.create(&prm, 1);
     sao.m_frame = fs.frame;
@@ -1110,29 +1113,36 @@ void xo_sao_apply(int width, int height, int ctu_log2, void* y, void* cb, void* 
     }
     for (int p = 0; p < 3; p++)
     {
-        store_plane(fs.recon, p, planes[p], p ? cstride : stride, p ? width >> 1 : width, p ? height >> 1 : height);
+        store_plane(fs.recon, p, planes[p], p ? cstride : stride, p ? width >> hs : width, p ? height >> vs : height);
         delete[] cp[p];
     }
     sao.destroy(1);
 }
 
-void xo_sao_stats(int width, int height, int ctu_log2, int non_deblocked, const void* fy, const void* fcb,
-                  const void* fcr, intptr_t fstride, intptr_t fcstride, const void* ry, const void* rcb,
-                  const void* rcr, intptr_t rstride, intptr_t rcstride, int32_t* stats, int32_t* count)
+void xo_sao_apply(int width, int height, int ctu_log2, void* y, void* cb, void* cr, intptr_t stride,
+                  intptr_t cstride, const xo_sao_param* params, int luma_on, int chroma_on)
+{
+    xo_sao_apply_csp(width, height, ctu_log2, y, cb, cr, stride, cstride, params, luma_on, chroma_on, X265_CSP_I420);
+}
+
+void xo_sao_stats_csp(int width, int height, int ctu_log2, int non_deblocked, const void* fy, const void* fcb,
+                      const void* fcr, intptr_t fstride, intptr_t fcstride, const void* ry, const void* rcb,
+                      const void* rcr, intptr_t rstride, intptr_t rcstride, int32_t* stats, int32_t* count, int csp)
 {
     pthread_once(&g_prim_once, init_global_prims);
     set_ctu_globals(ctu_log2);
-    FrameShell fs(width, height, true, false);
+    const int hs = CHROMA_H_SHIFT(csp), vs = CHROMA_V_SHIFT(csp);
+    FrameShell fs(width, height, true, false, csp);
     const void* fp[3] = { fy, fcb, fcr };
     const void* rp[3] = { ry, rcb, rcr };
     for (int p = 0; p < 3; p++)
     {
-        const int w = p ? width >> 1 : width, h = p ? height >> 1 : height;
+        const int w = p ? width >> hs : width, h = p ? height >> vs : height;
         load_plane(fs.fenc, p, fp[p], p ? fcstride : fstride, w, h);
         load_plane(fs.recon, p, rp[p], p ? rcstride : rstride, w, h);
     }
     x265_param prm;
-    sao_param_defaults(&prm, width, height, non_deblocked);
+    sao_param_defaults(&prm, width, height, non_deblocked, csp);
     ShimSao sao;
     sao.create(&prm, 1);
     sao.m_frame = fs.frame;
@@ -1151,12 +1161,21 @@ void xo_sao_stats(int width, int height, int ctu_log2, int non_deblocked, const 
     sao.destroy(1);
 }
 
-void xo_deblock(int width, int height, int ctu_log2, void* y, void* cb, void* cr, intptr_t stride,
-                intptr_t cstride, const xo_deblock_unit* units, intptr_t us, const xo_deblock_params* prm)
+void xo_sao_stats(int width, int height, int ctu_log2, int non_deblocked, const void* fy, const void* fcb,
+                  const void* fcr, intptr_t fstride, intptr_t fcstride, const void* ry, const void* rcb,
+                  const void* rcr, intptr_t rstride, intptr_t rcstride, int32_t* stats, int32_t* count)
+{
+    xo_sao_stats_csp(width, height, ctu_log2, non_deblocked, fy, fcb, fcr, fstride, fcstride, ry, rcb, rcr, rstride,
+                     rcstride, stats, count, X265_CSP_I420);
+}
+
+void xo_deblock_csp(int width, int height, int ctu_log2, void* y, void* cb, void* cr, intptr_t stride,
+                    intptr_t cstride, const xo_deblock_unit* units, intptr_t us, const xo_deblock_params* prm, int csp)
 {
     pthread_once(&g_prim_once, init_global_prims);
     set_ctu_globals(ctu_log2);
-    FrameShell fs(width, height, false, true);
+    const int hs = CHROMA_H_SHIFT(csp), vs = CHROMA_V_SHIFT(csp);
+    FrameShell fs(width, height, false, true, csp);
     fs.pps.deblockingFilterBetaOffsetDiv2 = prm->beta_offset_div2;
     fs.pps.deblockingFilterTcOffsetDiv2 = prm->tc_offset_div2;
     fs.pps.chromaQpOffset[0] = prm->cb_qp_offset;
@@ -1170,7 +1189,7 @@ void xo_deblock(int width, int height, int ctu_log2, void* y, void* cb, void* cr
             fs.slice.m_refFrameList[l][i] = (Frame*)(poc_space + ((prm->ref_poc[l][i] & 0x3fff) << 2));
     void* planes[3] = { y, cb, cr };
     for (int p = 0; p < 3; p++)
-        load_plane(fs.recon, p, planes[p], p ? cstride : stride, p ? width >> 1 : width, p ? height >> 1 : height);
+        load_plane(fs.recon, p, planes[p], p ? cstride : stride, p ? width >> hs : width, p ? height >> vs : height);
 
     /* the CU tree, per 4x4 partition in z-order */
     const int ctu = g_maxCUSize, npart = NUM_4x4_PARTITIONS;
@@ -1224,7 +1243,13 @@ void xo_deblock(int width, int height, int ctu_log2, void* y, void* cb, void* cr
     }
     delete[] geoms;
     for (int p = 0; p < 3; p++)
-        store_plane(fs.recon, p, planes[p], p ? cstride : stride, p ? width >> 1 : width, p ? height >> 1 : height);
+        store_plane(fs.recon, p, planes[p], p ? cstride : stride, p ? width >> hs : width, p ? height >> vs : height);
+}
+
+void xo_deblock(int width, int height, int ctu_log2, void* y, void* cb, void* cr, intptr_t stride,
+                intptr_t cstride, const xo_deblock_unit* units, intptr_t us, const xo_deblock_params* prm)
+{
+    xo_deblock_csp(width, height, ctu_log2, y, cb, cr, stride, cstride, units, us, prm, X265_CSP_I420);
 }
 
 void xo_extend_border(void* plane, intptr_t stride, int width, int height, int mx, int my)

@@ -1811,9 +1811,10 @@ static void eo_dirs(int t, int* dx0, int* dy0, int* dx1, int* dy1)
 /* processSaoCu semantics (sao.cpp:278-597): every output pixel is computed from deblocked (pre-SAO)
  * neighbours (the m_tmpU / m_tmpL copies keep them), EO skips the picture's outermost column / row
  * in its direction, BO maps bands (bandPos + i) & 31 to offset[i]. */
-void xo_sao_apply(int width, int height, int ctu_log2, void* y_, void* cb_, void* cr_, intptr_t stride,
-                  intptr_t cstride, const xo_sao_param* params, int luma_on, int chroma_on)
+void xo_sao_apply_csp(int width, int height, int ctu_log2, void* y_, void* cb_, void* cr_, intptr_t stride,
+                      intptr_t cstride, const xo_sao_param* params, int luma_on, int chroma_on, int csp)
 {
+    const int hs = csp == 3 ? 0 : 1, vs = csp == 1 ? 1 : 0;   /* CHROMA_H/V_SHIFT (x265.h) */
     const int ctu = 1 << ctu_log2;
     const int wc = (width + ctu - 1) >> ctu_log2, hc = (height + ctu - 1) >> ctu_log2, nctu = wc * hc;
     pix* planes[3] = { (pix*)y_, (pix*)cb_, (pix*)cr_ };
@@ -1821,7 +1822,8 @@ void xo_sao_apply(int width, int height, int ctu_log2, void* y_, void* cb_, void
     {
         if (p == 0 ? !luma_on : !chroma_on) continue;
         const intptr_t s = p ? cstride : stride;
-        const int pw = p ? width >> 1 : width, ph = p ? height >> 1 : height, cs = p ? ctu >> 1 : ctu;
+        const int pw = p ? width >> hs : width, ph = p ? height >> vs : height;
+        const int csw = p ? ctu >> hs : ctu, csh = p ? ctu >> vs : ctu;
         /* the deblocked plane plus a one-pixel ring, as the processing reads it */
         const int sw = pw + 2, sh = ph + 2;
         pix* snap = (pix*)malloc(sizeof(pix) * sw * sh);
@@ -1834,8 +1836,8 @@ void xo_sao_apply(int width, int height, int ctu_log2, void* y_, void* cb_, void
             int type = prm->type;
             if (p == 2 && type >= 0) type = params[nctu + c].type;   /* processSaoCu(addr, typeIdxCb, 2) */
             if (type < 0) continue;
-            const int x0 = (c % wc) * cs, y0 = (c / wc) * cs;
-            const int x1 = x0 + cs < pw ? x0 + cs : pw, y1 = y0 + cs < ph ? y0 + cs : ph;
+            const int x0 = (c % wc) * csw, y0 = (c / wc) * csh;
+            const int x1 = x0 + csw < pw ? x0 + csw : pw, y1 = y0 + csh < ph ? y0 + csh : ph;
             if (type == 4)
             {
                 int8_t tab[32] = { 0 };
@@ -1863,14 +1865,21 @@ void xo_sao_apply(int width, int height, int ctu_log2, void* y_, void* cb_, void
     }
 }
 
+void xo_sao_apply(int width, int height, int ctu_log2, void* y_, void* cb_, void* cr_, intptr_t stride,
+                  intptr_t cstride, const xo_sao_param* params, int luma_on, int chroma_on)
+{
+    xo_sao_apply_csp(width, height, ctu_log2, y_, cb_, cr_, stride, cstride, params, luma_on, chroma_on, 1);
+}
+
 /* calcSaoStatsCu (sao.cpp:772-943) with saoCuStats{BO,E0..E3}_c (sao.cpp:1748-1916): per class the
  * sum of (source - deblocked) and the pixel count, over regions that leave out the not yet
  * deblocked right / bottom lines (skipR / skipB) unless the CTU touches the picture edge (E0 keeps
  * its bottom skip even there, sao.cpp:852) */
-void xo_sao_stats(int width, int height, int ctu_log2, int non_deblocked, const void* fy, const void* fcb,
-                  const void* fcr, intptr_t fstride, intptr_t fcstride, const void* ry, const void* rcb,
-                  const void* rcr, intptr_t rstride, intptr_t rcstride, int32_t* stats, int32_t* count)
+void xo_sao_stats_csp(int width, int height, int ctu_log2, int non_deblocked, const void* fy, const void* fcb,
+                      const void* fcr, intptr_t fstride, intptr_t fcstride, const void* ry, const void* rcb,
+                      const void* rcr, intptr_t rstride, intptr_t rcstride, int32_t* stats, int32_t* count, int csp)
 {
+    const int hs = csp == 3 ? 0 : 1, vs = csp == 1 ? 1 : 0;
     const int ctu = 1 << ctu_log2;
     const int wc = (width + ctu - 1) >> ctu_log2, hc = (height + ctu - 1) >> ctu_log2, nctu = wc * hc;
     const pix* fp[3] = { (const pix*)fy, (const pix*)fcb, (const pix*)fcr };
@@ -1884,10 +1893,11 @@ void xo_sao_stats(int width, int height, int ctu_log2, int non_deblocked, const 
         for (int p = 0; p < 3; p++)
         {
             const intptr_t fs = p ? fcstride : fstride, rs = p ? rcstride : rstride;
-            const int pw = p ? width >> 1 : width, ph = p ? height >> 1 : height, cs = p ? ctu >> 1 : ctu;
+            const int pw = p ? width >> hs : width, ph = p ? height >> vs : height;
+            const int csw = p ? ctu >> hs : ctu, csh = p ? ctu >> vs : ctu;
             const int po = p ? 2 : 0;
-            const int x0 = (c % wc) * cs, y0 = (c / wc) * cs;
-            const int cw = (x0 + cs < pw ? x0 + cs : pw) - x0, ch = (y0 + cs < ph ? y0 + cs : ph) - y0;
+            const int x0 = (c % wc) * csw, y0 = (c / wc) * csh;
+            const int cw = (x0 + csw < pw ? x0 + csw : pw) - x0, ch = (y0 + csh < ph ? y0 + csh : ph) - y0;
             const int right = x0 + cw == pw, bottom = y0 + ch == ph;
             const pix* f = fp[p] + y0 * fs + x0;
             const pix* r = rp[p] + y0 * rs + x0;
@@ -1918,6 +1928,14 @@ void xo_sao_stats(int width, int height, int ctu_log2, int non_deblocked, const 
                     }
             }
         }
+}
+
+void xo_sao_stats(int width, int height, int ctu_log2, int non_deblocked, const void* fy, const void* fcb,
+                  const void* fcr, intptr_t fstride, intptr_t fcstride, const void* ry, const void* rcb,
+                  const void* rcr, intptr_t rstride, intptr_t rcstride, int32_t* stats, int32_t* count)
+{
+    xo_sao_stats_csp(width, height, ctu_log2, non_deblocked, fy, fcb, fcr, fstride, fcstride, ry, rcb, rcr, rstride,
+                     rcstride, stats, count, 1);
 }
 
 /* Deblock::s_tcTable / s_betaTable (deblock.cpp:523-535), g_chromaScale (constants.cpp:335-339) */
@@ -2055,13 +2073,13 @@ static void filter_luma_seg(pix* src, intptr_t step, intptr_t off, int bs, int q
 
 /* edgeFilterChroma (deblock.cpp:443-521) for one 4-line chroma segment of Cb and Cr (bS 2 only) */
 static void filter_chroma_seg(pix* const cbcr[2], intptr_t step, intptr_t off, int qpA, int maskP, int maskQ,
-                              const xo_deblock_params* prm)
+                              const xo_deblock_params* prm, int csp)
 {
     const int bd = XO_DEPTH - 8;
     for (int k = 0; k < 2; k++)
     {
         int qp = qpA + (k ? prm->cr_qp_offset : prm->cb_qp_offset);
-        if (qp >= 30) qp = kChromaScale[qp];
+        if (qp >= 30) qp = csp == 1 ? kChromaScale[qp] : (qp < 51 ? qp : 51);   /* QP_MAX_SPEC */
         const int tc = kTc[clip3i(0, 53, qp + 2 + prm->tc_offset_div2 * 2)] << bd;
         for (int l = 0; l < 4; l++)
         {
@@ -2074,9 +2092,10 @@ static void filter_chroma_seg(pix* const cbcr[2], intptr_t step, intptr_t off, i
     }
 }
 
-void xo_deblock(int width, int height, int ctu_log2, void* y_, void* cb_, void* cr_, intptr_t stride,
-                intptr_t cstride, const xo_deblock_unit* units, intptr_t us, const xo_deblock_params* prm)
+void xo_deblock_csp(int width, int height, int ctu_log2, void* y_, void* cb_, void* cr_, intptr_t stride,
+                    intptr_t cstride, const xo_deblock_unit* units, intptr_t us, const xo_deblock_params* prm, int csp)
 {
+    const int hs = csp == 3 ? 0 : 1, vs = csp == 1 ? 1 : 0;
     (void)ctu_log2;   /* the per-CTU order of the reference is equivalent to all-vertical-then-all-horizontal */
     pix* Y = (pix*)y_;
     pix* C[2] = { (pix*)cb_, (pix*)cr_ };
@@ -2104,15 +2123,23 @@ void xo_deblock(int width, int height, int ctu_log2, void* y_, void* cb_, void* 
                 if (bs)
                     filter_luma_seg(Y + 4 * uy * stride + 4 * ux, dir ? 1 : stride, dir ? stride : 1, bs, qp, maskP,
                                     maskQ, prm);
-                /* chroma: edges on the 8x8 chroma grid, 4 chroma lines per second luma unit */
-                if (bs == 2 && !((dir ? uy : ux) & 3) && !((dir ? ux : uy) & 1))
+                /* chroma (deblock.cpp:104-113, 443-521): edges on the 8x8 grid of the chroma plane; one
+                   4-line chroma segment per (1 << shift along the edge) luma units */
+                const int across = dir ? vs : hs, along = dir ? hs : vs;
+                if (bs == 2 && !(((4 * (dir ? uy : ux)) >> across) & 7) && !((dir ? ux : uy) & ((1 << along) - 1)))
                 {
-                    const intptr_t o = (intptr_t)(2 * uy) * cstride + 2 * ux;
+                    const intptr_t o = (intptr_t)((4 * uy) >> vs) * cstride + ((4 * ux) >> hs);
                     pix* const cbcr[2] = { C[0] + o, C[1] + o };
-                    filter_chroma_seg(cbcr, dir ? 1 : cstride, dir ? cstride : 1, qp, maskP, maskQ, prm);
+                    filter_chroma_seg(cbcr, dir ? 1 : cstride, dir ? cstride : 1, qp, maskP, maskQ, prm, csp);
                 }
             }
     }
+}
+
+void xo_deblock(int width, int height, int ctu_log2, void* y_, void* cb_, void* cr_, intptr_t stride,
+                intptr_t cstride, const xo_deblock_unit* units, intptr_t us, const xo_deblock_params* prm)
+{
+    xo_deblock_csp(width, height, ctu_log2, y_, cb_, cr_, stride, cstride, units, us, prm, 1);
 }
 
 /* ======================================================= f1 cuTree propagation */

@@ -216,6 +216,18 @@ typedef struct
 /* SAO::processSaoUnitCuLuma / processSaoUnitCuChroma -> processSaoCu (sao.cpp:278-760) for every
  * CTU, as FrameFilter drives them on a deblocked frame (framefilter.cpp:176-210, 300-430).  In
  * place.  params[plane * nctu + ctu]; Cr takes Cb's type (processSaoUnitCuChroma, sao.cpp:755). */
+/* the same for chroma format csp (1 = 4:2:0, 2 = 4:2:2, 3 = 4:4:4): chroma planes are
+ * (width >> hshift) x (height >> vshift), chroma CTUs (ctu >> hshift) x (ctu >> vshift)
+ * (sao.cpp:289-298, 786-794; deblock.cpp:104-113, 443-521) */
+void     xo_sao_apply_csp(int width, int height, int ctu_log2, void* y, void* cb, void* cr, intptr_t stride,
+                          intptr_t cstride, const xo_sao_param* params, int luma_on, int chroma_on, int csp);
+void     xo_sao_stats_csp(int width, int height, int ctu_log2, int non_deblocked, const void* fy, const void* fcb,
+                          const void* fcr, intptr_t fstride, intptr_t fcstride, const void* ry, const void* rcb,
+                          const void* rcr, intptr_t rstride, intptr_t rcstride, int32_t* stats, int32_t* count,
+                          int csp);
+void     xo_deblock_csp(int width, int height, int ctu_log2, void* y, void* cb, void* cr, intptr_t stride,
+                        intptr_t cstride, const xo_deblock_unit* units, intptr_t us, const xo_deblock_params* prm,
+                        int csp);
 void     xo_sao_apply(int width, int height, int ctu_log2, void* y, void* cb, void* cr, intptr_t stride,
                       intptr_t cstride, const xo_sao_param* params, int luma_on, int chroma_on);
 /* SAO::calcSaoStatsCu (sao.cpp:772-943) for every CTU and plane: stats / count

@@ -17,6 +17,7 @@
 // each source row is loaded once per unit; hv_pp recomputes the horizontal
 // int16 intermediate for the UH+7 rows its unit needs, entirely on-chip.
 #include <algorithm>
+#include <stdlib.h>
 
 #include "common.h"
 #include "../../../include/x265_amd.h"
@@ -575,15 +576,32 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_hvpp(const BatchGroup g)
 
 // -------------------------------------------------------------- dispatch
 
+// unit-height override for tuning runs (X265AMD_UH_<op>=1|2|4|16; 0 = built-in choice)
+static int uh_override(int op)
+{
+    static int v[8] = {-1, -1, -1, -1, -1, -1, -1, -1};
+    if (op < 0 || op > 7) return 0;
+    if (v[op] < 0)
+    {
+        static const char* names[8] = {"X265AMD_UH_HPP", "X265AMD_UH_HPS", "X265AMD_UH_VPP", "X265AMD_UH_VPS",
+                                       "X265AMD_UH_VSP", "X265AMD_UH_VSS", "X265AMD_UH_HVPP", "X265AMD_UH_P2S"};
+        const char* e = getenv(names[op]);
+        v[op] = e ? atoi(e) : 0;
+    }
+    return v[op];
+}
+
 // kernel class of a batch: unit width x unit height, packed as uw * 32 + uh
 template <int OP, int TAPS>
 static int interp_class(int w, int h, int rowext, bool pk8)
 {
     if (w < 2 || h < 2 || w > 64 || h > 64) return -X265AMD_EINVAL;
+    const int ov = uh_override(OP);
     if constexpr (OP == X265AMD_HVPP)
     {
         if (w % 4) return -X265AMD_EINVAL;
-        return (w % 8 == 0 ? 8 : 4) * 32 + (h % 4 == 0 ? 4 : 1);
+        const int uh = (ov == 1 || ov == 2 || ov == 4) && h % ov == 0 ? ov : (h % 4 == 0 ? 4 : 1);
+        return (w % 8 == 0 ? 8 : 4) * 32 + uh;
     }
     const int rows = (OP == X265AMD_HPS && rowext) ? h + TAPS - 1 : h;
     // vertical filters take 16-row units on blocks of 16+ rows: UH + taps - 1
@@ -591,7 +609,9 @@ static int interp_class(int w, int h, int rowext, bool pk8)
     // rows per output row (measured, 8-bit vpp: 64x64 40% -> 55% of HBM peak,
     // 16x16 36.5% -> 37.7%; 8-row units were worse on 8x8 and 16x16)
     // (the packed 8-bit vpp / vps path only: its accumulators are half-size)
-    const int uh = (pk8 && rows % 16 == 0 && w % 4 == 0) ? 16 : rows % 4 ? 1 : 4;
+    int uh = (pk8 && rows % 16 == 0 && w % 4 == 0) ? 16 : rows % 4 ? 1 : 4;
+    if (ov && rows % ov == 0 && (ov != 16 || (pk8 && w % 4 == 0)) && (ov == 1 || ov == 2 || ov == 4 || ov == 16))
+        uh = ov;
     if (w % 8 == 0) return 8 * 32 + uh;
     if (w % 4 == 0) return 4 * 32 + uh;
     // 2-wide units: the chroma filters and the vertical / p2s luma paths
@@ -627,7 +647,7 @@ static int launch_interp(int cls, const BatchGroup& g, uint32_t blocks, hipStrea
         return (int)hipGetLastError(); \
     }
     constexpr bool PK8 = sizeof(S) == 1 && (OP == X265AMD_VPP || OP == X265AMD_VPS);
-    L(8, 16) L(4, 16) L(8, 4) L(8, 1) L(4, 4) L(4, 1) L(2, 4) L(2, 1)
+    L(8, 16) L(4, 16) L(8, 4) L(8, 2) L(8, 1) L(4, 4) L(4, 2) L(4, 1) L(2, 4) L(2, 1)
 #undef L
     return X265AMD_EINVAL;
 }

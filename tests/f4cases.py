@@ -12,13 +12,19 @@ import pyoracle as po
 MARGIN = 16
 
 
-def frame_planes(width, height, depth, rng, margin=MARGIN):
+def chroma_shift(csp):
+    """(hshift, vshift) of a chroma format: 1 = 4:2:0, 2 = 4:2:2, 3 = 4:4:4 (x265.h CHROMA_*_SHIFT)"""
+    return (0 if csp == 3 else 1), (1 if csp == 1 else 0)
+
+
+def frame_planes(width, height, depth, rng, margin=MARGIN, csp=1):
     """(Y, Cb, Cr) as padded 2-D arrays (margin on every side), the margins filled too."""
+    hs, vs = chroma_shift(csp)
     dt = np.uint8 if depth == 8 else np.uint16
     maxv = (1 << depth) - 1
     out = []
     for p in range(3):
-        w, h = (width, height) if p == 0 else (width // 2, height // 2)
+        w, h = (width, height) if p == 0 else (width >> hs, height >> vs)
         yy, xx = np.mgrid[0:h + 2 * margin, 0:w + 2 * margin]
         base = rng.integers(0, maxv + 1, size=((h + 2 * margin) // 8 + 1, (w + 2 * margin) // 8 + 1))
         blocks = base[yy // 8, xx // 8].astype(np.int64)

@@ -86,6 +86,42 @@ def test_extend_border_oracle_vs_reference(oracle_libs, depth):
     np.testing.assert_array_equal(a, b)
 
 
+# 4:2:2 / 4:4:4 (SAO chroma CTUs (ctu >> hshift) x (ctu >> vshift), deblocking on the chroma
+# plane's 8x8 grid with QP clamped instead of g_chromaScale, deblock.cpp:104-113, 443-521)
+CSPS = [2, 3]
+
+
+@pytest.mark.parametrize("csp", CSPS)
+@pytest.mark.parametrize("depth", DEPTHS)
+@pytest.mark.parametrize("size", SIZES)
+def test_f4_chroma_formats_oracle_vs_reference(oracle_libs, csp, depth, size):
+    W, H, cl = size
+    O, R = _libs(depth)
+    rng = np.random.default_rng(31 * W + H + depth + cl + csp)
+    pl = F.frame_planes(W, H, depth, rng, csp=csp)
+    prm = F.sao_params(W, H, cl, depth, rng)
+    a, b = F.copy_planes(pl), F.copy_planes(pl)
+    O.sao_apply(W, H, cl, a, F.MARGIN, prm, 1, 1, csp=csp)
+    R.sao_apply(W, H, cl, b, F.MARGIN, prm, 1, 1, csp=csp)
+    for x, y in zip(a, b):
+        np.testing.assert_array_equal(x, y)
+    fenc = F.frame_planes(W, H, depth, rng, csp=csp)
+    for nd in (0, 1):
+        s1, c1 = O.sao_stats(W, H, cl, fenc, pl, F.MARGIN, nd, csp=csp)
+        s2, c2 = R.sao_stats(W, H, cl, fenc, pl, F.MARGIN, nd, csp=csp)
+        np.testing.assert_array_equal(c1, c2)
+        np.testing.assert_array_equal(s1, s2)
+    for st in ("I", "P", "B"):
+        U = F.deblock_units(W, H, cl, depth, rng, st, 0.2 if st == "B" else 0.0)
+        dp = F.deblock_params(rng, st, int(st == "B"))
+        a, b = F.copy_planes(pl), F.copy_planes(pl)
+        O.deblock(W, H, cl, a, F.MARGIN, U, dp, csp=csp)
+        R.deblock(W, H, cl, b, F.MARGIN, U, dp, csp=csp)
+        for x, y in zip(a, b):
+            np.testing.assert_array_equal(x, y)
+        assert int((b[1] != pl[1]).sum()) > 0
+
+
 # ---------------------------------------------------------------- GPU: gfx950 kernels vs the oracle
 GPU_SIZES = [(200, 136, 6), (128, 64, 5), (96, 48, 4), (1920, 1080, 6)]
 
