@@ -613,6 +613,7 @@ typedef struct
     void* dst[3];
     int64_t stride, cstride;
     const x265amd_sao_param* params;
+    int chroma_format;   /* 0 or 1 = 4:2:0, 2 = 4:2:2, 3 = 4:4:4 (chroma CTU (ctu >> hshift) x (ctu >> vshift)) */
 } x265amd_sao_frame;
 int x265amd_sao_apply(int depth, int count, const x265amd_sao_frame* frames, void* stream);
 
@@ -629,6 +630,7 @@ typedef struct
     int64_t rec_stride, rec_cstride;
     int32_t* stats;
     int32_t* count;
+    int chroma_format;   /* as x265amd_sao_frame */
 } x265amd_sao_stats_frame;
 int x265amd_sao_stats(int depth, int count, const x265amd_sao_stats_frame* frames, void* stream);
 
@@ -663,6 +665,8 @@ typedef struct
     int is_p;
     int beta_offset_div2, tc_offset_div2, cb_qp_offset, cr_qp_offset, tq_bypass_enabled;
     int32_t ref_poc[2][16];
+    int chroma_format;   /* 0 or 1 = 4:2:0, 2 = 4:2:2, 3 = 4:4:4: chroma edges on the chroma plane's 8x8
+                            grid (deblock.cpp:104-113); non-4:2:0 chroma QP min(qp, 51) (:505-506) */
 } x265amd_deblock_frame;
 int x265amd_deblock(int depth, int count, const x265amd_deblock_frame* frames, void* stream);
 

@@ -600,7 +600,10 @@ static int interp_class(int w, int h, int rowext, bool pk8)
     if constexpr (OP == X265AMD_HVPP)
     {
         if (w % 4) return -X265AMD_EINVAL;
-        const int uh = (ov == 1 || ov == 2 || ov == 4) && h % ov == 0 ? ov : (h % 4 == 0 ? 4 : 1);
+        // 2-row units up to 16 rows: more lanes per job for the latency-bound small blocks (measured,
+        // profiles/r02/interp_uh_sweep.txt: 8x8 0.25 -> 0.35, 16x16 0.25 -> 0.31 of HBM peak)
+        const int uh = (ov == 1 || ov == 2 || ov == 4) && h % ov == 0 ? ov
+                       : (h <= 16 && h % 2 == 0 ? 2 : (h % 4 == 0 ? 4 : 1));
         return (w % 8 == 0 ? 8 : 4) * 32 + uh;
     }
     const int rows = (OP == X265AMD_HPS && rowext) ? h + TAPS - 1 : h;

@@ -82,6 +82,7 @@ struct DbkFrame
     int64_t us;
     int wu, hu;                       // picture width / band height in 4x4 units
     int uy0;                          // first unit row of the band (0: whole picture)
+    int hs, vs;                       // chroma shifts (4:2:0 1/1, 4:2:2 1/0, 4:4:4 0/0)
     int is_p, beta2, tc2, cbqp, crqp, tqb;
     int32_t poc[2][16];
     uint32_t block0, nluma, nseg;     // first block; luma / all segments of this pass
@@ -270,9 +271,21 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_deblock(const DbkLaunch L)
     }
     else
     {
+        // chroma edges on the chroma plane's 8x8 grid, one 4-line chroma segment per (1 << shift
+        // along the edge) luma units (deblock.cpp:104-113, 479-480)
         const uint32_t c = s - f.nluma;
-        if (DIR == 0) { const int n = (f.wu + 3) >> 2; uy = 2 * (int)(c / n); ux = 4 * (int)(c % n); }
-        else { const int n = f.wu >> 1; ux = 2 * (int)(c % n); uy = 4 * (int)(c / n); }
+        if (DIR == 0)
+        {
+            const int sx = 2 << f.hs, n = (f.wu + sx - 1) / sx;
+            uy = (int)(c / n) << f.vs;
+            ux = sx * (int)(c % n);
+        }
+        else
+        {
+            const int n = f.wu >> f.hs;
+            ux = (int)(c % n) << f.hs;
+            uy = (2 << f.vs) * (int)(c / n);
+        }
     }
     uy += f.uy0;
     const x265amd_deblock_unit* qu = f.units + uy * f.us + ux;
@@ -304,9 +317,9 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_deblock(const DbkLaunch L)
     for (int k = 0; k < 2; k++)
     {
         int qpc = qp + (k ? f.crqp : f.cbqp);
-        if (qpc >= 30) qpc = c_chroma_scale[qpc];
+        if (qpc >= 30) qpc = (f.hs & f.vs) ? c_chroma_scale[qpc] : min(qpc, 51);
         const int tc = (int)c_tc[clip3(0, 53, qpc + 2 + f.tc2)] << bd;
-        P* q = (P*)f.plane[1 + k] + (int64_t)(2 * uy) * f.cstride + 2 * ux;
+        P* q = (P*)f.plane[1 + k] + (int64_t)((4 * uy) >> f.vs) * f.cstride + ((4 * ux) >> f.hs);
         int w[4][4];
         if (DIR == 0)
         {
@@ -380,6 +393,7 @@ struct SaoFrame
     const x265amd_sao_param* params;
     int w, h, ctu_log2, wc, nctu, luma_on, chroma_on;
     int c0, nctu_all;                        // first CTU of the band, CTUs of the picture (params stride)
+    int hs, vs;                              // chroma shifts
     uint32_t block0;                         // first block (one per plane and CTU)
 };
 struct SaoLaunch
@@ -399,12 +413,12 @@ __global__ __launch_bounds__(64) void k_sao_apply(const SaoLaunch L)
     const uint32_t u = b - f.block0;                 // plane-major: [3][nctu]
     const int p = (int)(u / f.nctu), c = f.c0 + (int)(u % f.nctu);
     const int lane = threadIdx.x;
-    const int pw = p ? f.w >> 1 : f.w, ph = p ? f.h >> 1 : f.h;
-    const int cl = f.ctu_log2 - (p ? 1 : 0), cs = 1 << cl;
-    const int nsx = cs >> 3, sh = cs * cs >= 512 ? (cs * cs) >> 9 : 1;
-    const int cx0 = (c % f.wc) * cs, cy0 = (c / f.wc) * cs;
+    const int pw = p ? f.w >> f.hs : f.w, ph = p ? f.h >> f.vs : f.h;
+    const int csw = (1 << f.ctu_log2) >> (p ? f.hs : 0), csh = (1 << f.ctu_log2) >> (p ? f.vs : 0);
+    const int nsx = csw >> 3, sh = csw * csh >= 512 ? (csw * csh) >> 9 : 1;
+    const int cx0 = (c % f.wc) * csw, cy0 = (c / f.wc) * csh;
     const int x0 = cx0 + 8 * (lane % nsx), y0 = cy0 + sh * (lane / nsx);
-    const int yend = min(min(y0 + sh, cy0 + cs), ph);
+    const int yend = min(min(y0 + sh, cy0 + csh), ph);
     if (x0 >= pw || y0 >= yend) return;
     const bool full = pw - x0 >= 8;                  // else 4 pixels (a right edge of width 8k + 4)
     const int64_t st = p ? f.cstride : f.stride;
@@ -484,6 +498,7 @@ struct StatFrame
     int32_t* stats;
     int32_t* count;
     int w, h, ctu_log2, wc, nd;
+    int hs, vs;                              // chroma shifts
     uint32_t block0, nctu;
 };
 struct StatLaunch
@@ -509,17 +524,18 @@ __global__ __launch_bounds__(64) void k_sao_stats(const StatLaunch L)
     const uint32_t c = b - f.block0;
     const int lane = threadIdx.x;
     for (int i = lane; i < 3 * 32; i += 64) (&bo[0][0])[i] = 0;
+    for (int i = lane; i < 3 * 4 * 5; i += 64) { (&eo_sum[0][0][0])[i] = 0; (&eo_cnt[0][0][0])[i] = 0; }
     __syncthreads();
     const int cxi = (int)(c % f.wc), cyi = (int)(c / f.wc);
 #pragma unroll 1
     for (int pass = 0; pass < 2; pass++)
     {
         const int p = pass ? 1 + (lane >> 5) : 0;
-        const int sl = pass ? lane & 31 : lane;
-        const int pw = p ? f.w >> 1 : f.w, ph = p ? f.h >> 1 : f.h;
-        const int cs = (1 << f.ctu_log2) >> (p ? 1 : 0);
-        const int x0 = cxi * cs, y0 = cyi * cs;
-        const int cw = (x0 + cs < pw ? x0 + cs : pw) - x0, ch = (y0 + cs < ph ? y0 + cs : ph) - y0;
+        const int sl = pass ? lane & 31 : lane, nl = pass ? 32 : 64;
+        const int pw = p ? f.w >> f.hs : f.w, ph = p ? f.h >> f.vs : f.h;
+        const int csw = (1 << f.ctu_log2) >> (p ? f.hs : 0), csh = (1 << f.ctu_log2) >> (p ? f.vs : 0);
+        const int x0 = cxi * csw, y0 = cyi * csh;
+        const int cw = (x0 + csw < pw ? x0 + csw : pw) - x0, ch = (y0 + csh < ph ? y0 + csh : ph) - y0;
         const bool right = x0 + cw == pw, bottom = y0 + ch == ph;
         const int po = p ? 2 : 0;
         // regions per type (sao.cpp:825-925): EO_0, EO_1, EO_2, EO_3, BO; EO_0 keeps its bottom
@@ -537,111 +553,119 @@ __global__ __launch_bounds__(64) void k_sao_stats(const StatLaunch L)
             ye[t] = t == 0 ? ch - sb + po : (bottom ? (eoy ? ch - 1 : ch) : ch - sb + po);
         }
         const int nsx = (cw + 7) >> 3, nsy = (ch + 7) >> 3;
-#pragma unroll
-        for (int k = 0; k < 20; k++) bins[lane][k] = 0;
-        if (sl < nsx * nsy)
+        // chroma strips per plane: 16 (4:2:0), 32 (4:2:2), 64 (4:4:4) over 32 lanes; Cb and Cr have the
+        // same geometry, so the round count is uniform over the wave
+        const int rounds = (nsx * nsy + nl - 1) / nl;
+#pragma unroll 1
+        for (int round = 0; round < rounds; round++)
         {
-            const int lx0 = 8 * (sl % nsx), ly0 = 8 * (sl / nsx);
-            const int rows = ch - ly0 < 8 ? ch - ly0 : 8;
-            uint32_t xm[5];
 #pragma unroll
-            for (int t = 0; t < 5; t++)
+            for (int k = 0; k < 20; k++) bins[lane][k] = 0;
+            const int strip = sl + round * nl;
+            if (strip < nsx * nsy)
             {
-                const int lo = clip3(0, 8, xs[t] - lx0), hi = clip3(0, 8, xe[t] - lx0);
-                xm[t] = hi > lo ? ((1u << hi) - 1) & ~((1u << lo) - 1) : 0u;
-            }
-            const int64_t rs = p ? f.rcs : f.rs, fs = p ? f.fcs : f.fs;
-            const P* r = (const P*)f.rec[p] + (int64_t)(y0 + ly0) * rs + x0 + lx0;
-            const P* fe = (const P*)f.fenc[p] + (int64_t)(y0 + ly0) * fs + x0 + lx0;
-            int up[10], mid[10], dn[10];
-            load_row10<P>(r - rs, up);
-            load_row10<P>(r, mid);
-            // signs against the row above for EO_1 / EO_2 / EO_3: after the first row they are the
-            // negated signs against the row below of the previous row (sao.cpp's signUp buffers)
-            int u1[8], u2[8], u3[8];
+                const int lx0 = 8 * (strip % nsx), ly0 = 8 * (strip / nsx);
+                const int rows = ch - ly0 < 8 ? ch - ly0 : 8;
+                uint32_t xm[5];
 #pragma unroll
-            for (int i = 0; i < 8; i++)
-            {
-                u1[i] = sgn(mid[i + 1] - up[i + 1]);
-                u2[i] = sgn(mid[i + 1] - up[i]);
-                u3[i] = sgn(mid[i + 1] - up[i + 2]);
-            }
-#pragma unroll
-            for (int yy = 0; yy < 8; yy++)
-            {
-                if (yy >= rows) break;
-                load_row10<P>(r + (yy + 1) * rs, dn);
-                int h[9];                 // EO_0: sign of each pixel against its left neighbour
-#pragma unroll
-                for (int k = 0; k < 9; k++) h[k] = sgn(mid[k + 1] - mid[k]);
-                int n1[8], n2[8], n3[8];
-                n2[0] = sgn(dn[1] - mid[0]);
-                n3[7] = sgn(dn[8] - mid[9]);
-                int fv[8];
-                load_row<P, 8>(fe + yy * fs, fv);
-                const int ly = ly0 + yy;
-                uint32_t m[5];
-#pragma unroll
-                for (int t = 0; t < 5; t++) m[t] = (ly >= ys[t] && ly < ye[t]) ? xm[t] : 0u;
-                int run_band = -1;
-                unsigned long long run = 0;
+                for (int t = 0; t < 5; t++)
+                {
+                    const int lo = clip3(0, 8, xs[t] - lx0), hi = clip3(0, 8, xe[t] - lx0);
+                    xm[t] = hi > lo ? ((1u << hi) - 1) & ~((1u << lo) - 1) : 0u;
+                }
+                const int64_t rs = p ? f.rcs : f.rs, fs = p ? f.fcs : f.fs;
+                const P* r = (const P*)f.rec[p] + (int64_t)(y0 + ly0) * rs + x0 + lx0;
+                const P* fe = (const P*)f.fenc[p] + (int64_t)(y0 + ly0) * fs + x0 + lx0;
+                int up[10], mid[10], dn[10];
+                load_row10<P>(r - rs, up);
+                load_row10<P>(r, mid);
+                // signs against the row above for EO_1 / EO_2 / EO_3: after the first row they are the
+                // negated signs against the row below of the previous row (sao.cpp's signUp buffers)
+                int u1[8], u2[8], u3[8];
 #pragma unroll
                 for (int i = 0; i < 8; i++)
                 {
-                    const int v = mid[i + 1], d = fv[i] - v;
-                    const int val = (d << 7) + 1;
-                    const int d1 = sgn(v - dn[i + 1]), d2 = sgn(v - dn[i + 2]), d3 = sgn(v - dn[i]);
-                    const int e[4] = { h[i] - h[i + 1], u1[i] + d1, u2[i] + d2, u3[i] + d3 };
-                    n1[i] = -d1;
-                    if (i < 7) n2[i + 1] = -d2;
-                    if (i > 0) n3[i - 1] = -d3;
-#pragma unroll
-                    for (int t = 0; t < 4; t++)
-                    {
-                        // masked-off pixels go to the sink bin 20: no branch around the ds_add
-                        const int bi = ((m[t] >> i) & 1) ? 5 * t + e[t] + 2 : 20;
-                        atomicAdd(&bins[lane][bi], val);
-                    }
-                    if ((m[4] >> i) & 1)
-                    {
-                        const int band = v >> L.bo_shift;
-                        if (band != run_band)
-                        {
-                            if (run_band >= 0) atomicAdd(&bo[p][run_band], run);
-                            run_band = band;
-                            run = 0;
-                        }
-                        run += (1ull << 40) + (unsigned long long)(int64_t)d;
-                    }
+                    u1[i] = sgn(mid[i + 1] - up[i + 1]);
+                    u2[i] = sgn(mid[i + 1] - up[i]);
+                    u3[i] = sgn(mid[i + 1] - up[i + 2]);
                 }
-                if (run_band >= 0) atomicAdd(&bo[p][run_band], run);
 #pragma unroll
-                for (int i = 0; i < 8; i++) { u1[i] = n1[i]; u2[i] = n2[i]; u3[i] = n3[i]; }
+                for (int yy = 0; yy < 8; yy++)
+                {
+                    if (yy >= rows) break;
+                    load_row10<P>(r + (yy + 1) * rs, dn);
+                    int h[9];                 // EO_0: sign of each pixel against its left neighbour
 #pragma unroll
-                for (int i = 0; i < 10; i++) mid[i] = dn[i];
+                    for (int k = 0; k < 9; k++) h[k] = sgn(mid[k + 1] - mid[k]);
+                    int n1[8], n2[8], n3[8];
+                    n2[0] = sgn(dn[1] - mid[0]);
+                    n3[7] = sgn(dn[8] - mid[9]);
+                    int fv[8];
+                    load_row<P, 8>(fe + yy * fs, fv);
+                    const int ly = ly0 + yy;
+                    uint32_t m[5];
+#pragma unroll
+                    for (int t = 0; t < 5; t++) m[t] = (ly >= ys[t] && ly < ye[t]) ? xm[t] : 0u;
+                    int run_band = -1;
+                    unsigned long long run = 0;
+#pragma unroll
+                    for (int i = 0; i < 8; i++)
+                    {
+                        const int v = mid[i + 1], d = fv[i] - v;
+                        const int val = (d << 7) + 1;
+                        const int d1 = sgn(v - dn[i + 1]), d2 = sgn(v - dn[i + 2]), d3 = sgn(v - dn[i]);
+                        const int e[4] = { h[i] - h[i + 1], u1[i] + d1, u2[i] + d2, u3[i] + d3 };
+                        n1[i] = -d1;
+                        if (i < 7) n2[i + 1] = -d2;
+                        if (i > 0) n3[i - 1] = -d3;
+#pragma unroll
+                        for (int t = 0; t < 4; t++)
+                        {
+                            // masked-off pixels go to the sink bin 20: no branch around the ds_add
+                            const int bi = ((m[t] >> i) & 1) ? 5 * t + e[t] + 2 : 20;
+                            atomicAdd(&bins[lane][bi], val);
+                        }
+                        if ((m[4] >> i) & 1)
+                        {
+                            const int band = v >> L.bo_shift;
+                            if (band != run_band)
+                            {
+                                if (run_band >= 0) atomicAdd(&bo[p][run_band], run);
+                                run_band = band;
+                                run = 0;
+                            }
+                            run += (1ull << 40) + (unsigned long long)(int64_t)d;
+                        }
+                    }
+                    if (run_band >= 0) atomicAdd(&bo[p][run_band], run);
+#pragma unroll
+                    for (int i = 0; i < 8; i++) { u1[i] = n1[i]; u2[i] = n2[i]; u3[i] = n3[i]; }
+#pragma unroll
+                    for (int i = 0; i < 10; i++) mid[i] = dn[i];
+                }
             }
-        }
-        __syncthreads();
-        // wave (pass 0) / half-wave (pass 1) totals: lane r < 20 of each half sums bin r over the
-        // lanes of its plane; edge type j = e + 2 -> class s_eoTable[j] (sao.cpp:65-72): 1, 2, 0, 3, 4
-        const int r = pass ? lane & 31 : lane;
-        if (r < 20)
-        {
-            const int l0 = pass ? lane & 32 : 0, nl = pass ? 32 : 64;
-            int vs = 0, vc = 0;
-            for (int l = 0; l < nl; l++)
+            __syncthreads();
+            // wave (pass 0) / half-wave (pass 1) totals: lane r < 20 of each half sums bin r over the
+            // lanes of its plane; edge type j = e + 2 -> class s_eoTable[j] (sao.cpp:65-72): 1, 2, 0, 3, 4
+            const int r = pass ? lane & 31 : lane;
+            if (r < 20)
             {
-                const int v = bins[l0 + l][r];
-                const int cn = v & 127;
-                vc += cn;
-                vs += (v - cn) >> 7;
+                const int l0 = pass ? lane & 32 : 0;
+                int vsum = 0, vc = 0;
+                for (int l = 0; l < nl; l++)
+                {
+                    const int v = bins[l0 + l][r];
+                    const int cn = v & 127;
+                    vc += cn;
+                    vsum += (v - cn) >> 7;
+                }
+                const int t = r / 5, j = r % 5;
+                const int k = j == 0 ? 1 : j == 1 ? 2 : j == 2 ? 0 : j;
+                eo_sum[p][t][k] += vsum;
+                eo_cnt[p][t][k] += vc;
             }
-            const int t = r / 5, j = r % 5;
-            const int k = j == 0 ? 1 : j == 1 ? 2 : j == 2 ? 0 : j;
-            eo_sum[p][t][k] = vs;
-            eo_cnt[p][t][k] = vc;
+            __syncthreads();
         }
-        __syncthreads();
     }
     __syncthreads();
     // every entry of the CTU's [3][5][33] block
@@ -757,7 +781,8 @@ static int deblock_impl(int depth, int count, const x265amd_deblock_frame* frame
     {
         const x265amd_deblock_frame& a = frames[i];
         if (a.width <= 0 || a.height <= 0 || (a.width & 7) || (a.height & 7) || !a.plane[0] || !a.plane[1] ||
-            !a.plane[2] || !a.units || a.unit_stride < a.width / 4 || a.stride < a.width || a.cstride < a.width / 2)
+            !a.plane[2] || !a.units || a.unit_stride < a.width / 4 || a.stride < a.width ||
+            a.cstride < (a.chroma_format == 3 ? a.width : a.width / 2) || a.chroma_format < 0 || a.chroma_format > 3)
             return X265AMD_EINVAL;
         if (rows && (rows[2 * i] < 0 || (rows[2 * i] & 15) || rows[2 * i + 1] <= rows[2 * i] ||
                      rows[2 * i + 1] > a.height || ((rows[2 * i + 1] - rows[2 * i]) & 7)))
@@ -790,16 +815,20 @@ static int deblock_impl(int depth, int count, const x265amd_deblock_frame* frame
                 f.cbqp = a.cb_qp_offset;
                 f.crqp = a.cr_qp_offset;
                 f.tqb = a.tq_bypass_enabled;
+                f.hs = a.chroma_format == 3 ? 0 : 1;
+                f.vs = a.chroma_format == 2 || a.chroma_format == 3 ? 0 : 1;
                 memcpy(f.poc, a.ref_poc, sizeof(f.poc));
                 if (dir == 0)
                 {
+                    const int sx = 2 << f.hs;
                     f.nluma = (uint32_t)((f.wu >> 1) * f.hu);
-                    f.nseg = f.nluma + (uint32_t)(((f.wu + 3) >> 2) * (f.hu >> 1));
+                    f.nseg = f.nluma + (uint32_t)(((f.wu + sx - 1) / sx) * (f.hu >> f.vs));
                 }
                 else
                 {
+                    const int sy = 2 << f.vs;
                     f.nluma = (uint32_t)(f.wu * (f.hu >> 1));
-                    f.nseg = f.nluma + (uint32_t)((f.wu >> 1) * ((f.hu + 3) >> 2));
+                    f.nseg = f.nluma + (uint32_t)((f.wu >> f.hs) * ((f.hu + sy - 1) / sy));
                 }
                 f.block0 = blocks;
                 blocks += nblocks(f.nseg);
@@ -839,7 +868,8 @@ static int sao_apply_impl(int depth, int count, const x265amd_sao_frame* frames,
     {
         const x265amd_sao_frame& a = frames[i];
         if (a.width <= 0 || a.height <= 0 || (a.width & 7) || (a.height & 7) || a.ctu_log2 < 4 || a.ctu_log2 > 6 ||
-            !a.params || a.stride < a.width || a.cstride < a.width / 2)
+            !a.params || a.stride < a.width || a.cstride < (a.chroma_format == 3 ? a.width : a.width / 2) ||
+            a.chroma_format < 0 || a.chroma_format > 3)
             return X265AMD_EINVAL;
         const int hc = (a.height + (1 << a.ctu_log2) - 1) >> a.ctu_log2;
         if (ctu_rows && (ctu_rows[2 * i] < 0 || ctu_rows[2 * i + 1] <= ctu_rows[2 * i] || ctu_rows[2 * i + 1] > hc))
@@ -874,6 +904,8 @@ static int sao_apply_impl(int depth, int count, const x265amd_sao_frame* frames,
             f.nctu = ctu_rows ? (ctu_rows[2 * (i0 + k) + 1] - ctu_rows[2 * (i0 + k)]) * f.wc : f.nctu_all;
             f.luma_on = a.luma_on;
             f.chroma_on = a.chroma_on;
+            f.hs = a.chroma_format == 3 ? 0 : 1;
+            f.vs = a.chroma_format == 2 || a.chroma_format == 3 ? 0 : 1;
             f.block0 = blocks;
             blocks += 3 * (uint32_t)f.nctu;
         }
@@ -904,7 +936,7 @@ extern "C" int x265amd_sao_stats(int depth, int count, const x265amd_sao_stats_f
     {
         const x265amd_sao_stats_frame& a = frames[i];
         if (a.width <= 0 || a.height <= 0 || (a.width & 7) || (a.height & 7) || a.ctu_log2 < 4 || a.ctu_log2 > 6 ||
-            !a.stats || !a.count)
+            !a.stats || !a.count || a.chroma_format < 0 || a.chroma_format > 3)
             return X265AMD_EINVAL;
         for (int p = 0; p < 3; p++)
             if (!a.fenc[p] || !a.rec[p]) return X265AMD_EINVAL;
@@ -932,6 +964,8 @@ extern "C" int x265amd_sao_stats(int depth, int count, const x265amd_sao_stats_f
             f.h = a.height;
             f.ctu_log2 = a.ctu_log2;
             f.nd = a.non_deblocked;
+            f.hs = a.chroma_format == 3 ? 0 : 1;
+            f.vs = a.chroma_format == 2 || a.chroma_format == 3 ? 0 : 1;
             const int ctu = 1 << a.ctu_log2;
             f.wc = (a.width + ctu - 1) >> a.ctu_log2;
             f.nctu = (uint32_t)(f.wc * ((a.height + ctu - 1) >> a.ctu_log2));

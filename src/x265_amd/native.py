@@ -85,20 +85,21 @@ _i64 = C.c_int64
 
 class SaoFrame(C.Structure):
     _fields_ = [("width", _int), ("height", _int), ("ctu_log2", _int), ("luma_on", _int), ("chroma_on", _int),
-                ("src", _vp * 3), ("dst", _vp * 3), ("stride", _i64), ("cstride", _i64), ("params", _vp)]
+                ("src", _vp * 3), ("dst", _vp * 3), ("stride", _i64), ("cstride", _i64), ("params", _vp),
+                ("chroma_format", _int)]
 
 
 class SaoStatsFrame(C.Structure):
     _fields_ = [("width", _int), ("height", _int), ("ctu_log2", _int), ("non_deblocked", _int), ("fenc", _vp * 3),
                 ("fenc_stride", _i64), ("fenc_cstride", _i64), ("rec", _vp * 3), ("rec_stride", _i64),
-                ("rec_cstride", _i64), ("stats", _vp), ("count", _vp)]
+                ("rec_cstride", _i64), ("stats", _vp), ("count", _vp), ("chroma_format", _int)]
 
 
 class DeblockFrame(C.Structure):
     _fields_ = [("width", _int), ("height", _int), ("plane", _vp * 3), ("stride", _i64), ("cstride", _i64),
                 ("units", _vp), ("unit_stride", _i64), ("is_p", _int), ("beta_offset_div2", _int),
                 ("tc_offset_div2", _int), ("cb_qp_offset", _int), ("cr_qp_offset", _int), ("tq_bypass_enabled", _int),
-                ("ref_poc", (C.c_int32 * 16) * 2)]
+                ("ref_poc", (C.c_int32 * 16) * 2), ("chroma_format", _int)]
 
 
 class PropagateBatch(C.Structure):

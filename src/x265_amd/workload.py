@@ -276,6 +276,8 @@ def launch_class(b: Batch):
             rows = h
         pk8 = b.op in (VPP, VPS) and b.depth == 8     # csrc/interp.hip: packed 8-bit vertical path
         uh = 16 if pk8 and rows % 16 == 0 and w % 4 == 0 else 4 if rows % 4 == 0 else 1
+        if b.op == HVPP and h <= 16 and h % 2 == 0:
+            uh = 2                                      # csrc/interp.hip interp_class: 2-row hv units
         return ("interp", b.op, taps, b.depth, 8 if w % 8 == 0 else 4 if w % 4 == 0 else 2, uh)
     return None
 

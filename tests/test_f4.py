@@ -346,3 +346,71 @@ def test_gpu_loop_filter_row_bands_equal_whole_frame(gpu_prims, depth):
         torch.cuda.synchronize()
         for p in range(3):
             np.testing.assert_array_equal(_host(out[p], pl[p].dtype), ref[p], err_msg=f"{W}x{H} plane {p}")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("csp", [2, 3])
+@pytest.mark.parametrize("depth", DEPTHS)
+def test_gpu_f4_chroma_formats(gpu_prims, csp, depth):
+    """4:2:2 / 4:4:4 (chroma_format 2 / 3): deblocking, SAO apply and SAO statistics of the
+    gfx950 kernels equal the oracle (itself equal to the reference's classes on the CPU)."""
+    import torch
+    from src.x265_amd.native import DeblockFrame, SaoFrame, SaoStatsFrame
+
+    O = po.FrameFilters("oracle", depth)
+    for i, (W, H, cl) in enumerate(GPU_SIZES):
+        rng = np.random.default_rng(500 + 10 * i + depth + csp)
+        pl = F.frame_planes(W, H, depth, rng, csp=csp)
+        # deblocking (B slice, lossless CUs on)
+        U = F.deblock_units(W, H, cl, depth, rng, "B", 0.2)
+        dp = F.deblock_params(rng, "B", 1)
+        ref = F.copy_planes(pl)
+        O.deblock(W, H, cl, ref, F.MARGIN, U, dp, csp=csp)
+        d = _dev(pl)
+        du = torch.from_numpy(U.view(np.uint8).reshape(U.shape[0], -1)).cuda()
+        fr = DeblockFrame()
+        fr.width, fr.height, fr.chroma_format = W, H, csp
+        for p in range(3):
+            fr.plane[p] = _org(d[p])
+        fr.stride, fr.cstride = d[0].shape[1], d[1].shape[1]
+        fr.units, fr.unit_stride = du.data_ptr(), U.shape[1]
+        fr.is_p, fr.beta_offset_div2, fr.tc_offset_div2 = dp.is_p, dp.beta_offset_div2, dp.tc_offset_div2
+        fr.cb_qp_offset, fr.cr_qp_offset, fr.tq_bypass_enabled = dp.cb_qp_offset, dp.cr_qp_offset, 1
+        for lst in range(2):
+            for k in range(16):
+                fr.ref_poc[lst][k] = dp.ref_poc[lst][k]
+        gpu_prims.deblock(depth, [fr])
+        # SAO apply on the deblocked picture
+        prm = F.sao_params(W, H, cl, depth, rng)
+        sref = F.copy_planes(ref)
+        O.sao_apply(W, H, cl, sref, F.MARGIN, prm, 1, 1, csp=csp)
+        out = _dev(tuple(np.zeros_like(p) for p in pl))
+        dprm = torch.from_numpy(prm.view(np.uint8)).cuda()
+        sf = SaoFrame()
+        sf.width, sf.height, sf.ctu_log2, sf.luma_on, sf.chroma_on, sf.chroma_format = W, H, cl, 1, 1, csp
+        for p in range(3):
+            sf.src[p], sf.dst[p] = _org(d[p]), _org(out[p])
+        sf.stride, sf.cstride, sf.params = d[0].shape[1], d[1].shape[1], dprm.data_ptr()
+        gpu_prims.sao_apply(depth, [sf])
+        # SAO statistics of a source against the deblocked picture
+        fenc = F.frame_planes(W, H, depth, rng, csp=csp)
+        s_ref, c_ref = O.sao_stats(W, H, cl, fenc, ref, F.MARGIN, 0, csp=csp)
+        df = _dev(fenc)
+        st = torch.full(s_ref.shape, -7, dtype=torch.int32, device="cuda")
+        ct = torch.full(c_ref.shape, -7, dtype=torch.int32, device="cuda")
+        tf = SaoStatsFrame()
+        tf.width, tf.height, tf.ctu_log2, tf.non_deblocked, tf.chroma_format = W, H, cl, 0, csp
+        for p in range(3):
+            tf.fenc[p], tf.rec[p] = _org(df[p]), _org(d[p])
+        tf.fenc_stride, tf.fenc_cstride = df[0].shape[1], df[1].shape[1]
+        tf.rec_stride, tf.rec_cstride = d[0].shape[1], d[1].shape[1]
+        tf.stats, tf.count = st.data_ptr(), ct.data_ptr()
+        gpu_prims.sao_stats(depth, [tf])
+        torch.cuda.synchronize()
+        M = F.MARGIN
+        for p in range(3):
+            np.testing.assert_array_equal(_host(d[p], pl[p].dtype), ref[p], err_msg=f"deblock {W}x{H} p{p}")
+            np.testing.assert_array_equal(_host(out[p], pl[p].dtype)[M:-M, M:-M], sref[p][M:-M, M:-M],
+                                          err_msg=f"sao {W}x{H} p{p}")
+        np.testing.assert_array_equal(ct.cpu().numpy(), c_ref)
+        np.testing.assert_array_equal(st.cpu().numpy(), s_ref)
