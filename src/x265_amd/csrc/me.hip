@@ -59,8 +59,9 @@ struct MeState
     const uint16_t* tab;
     int mvpx, mvpy;
     int nu, lane, G, uw;    // units of this lane, lane in group, group size, units per PU row
-    const P* fenc;          // source PU origin (re-read per evaluation: L1-resident, no dynamic register indexing)
+    const P* fenc;          // source PU origin
     int64_t fs;
+    uint32_t fe[kMeMaxUnits][4][sizeof(P) == 1 ? 1 : 2];   // this lane's fenc units, loaded once
     bool chroma;            // bChromaSATD
     const P* fc[2];         // source Cb / Cr at the PU's chroma origin
     const P* rc[2];         // reference Cb / Cr at the PU's chroma origin
@@ -114,24 +115,24 @@ __device__ __forceinline__ int group_sum_rt(int v, int G)
     return v;
 }
 
+// fenc from registers (loaded once per PU); the unit loop unrolled to kMeMaxUnits with a guard, so
+// every reference row load of a candidate is issued before the first SAD
 template <typename P, int G>
 __device__ __forceinline__ int fpel_sad(const MeState<P>& s, int dx, int dy)
 {
     uint32_t acc = 0;
-    for (int k = 0; k < s.nu; k++)
+#pragma unroll
+    for (int k = 0; k < kMeMaxUnits; k++)
     {
+        if (k >= s.nu) break;
         int ux, uy;
         s.unit_xy(k, ux, uy);
         const P* p = s.ref + (ux + dx) + (int64_t)(uy + dy) * s.rs;
-        const P* f = s.fenc + ux + (int64_t)uy * s.fs;
+        uint32_t w[4][sizeof(P) == 1 ? 1 : 2];
 #pragma unroll
-        for (int r = 0; r < 4; r++)
-        {
-            uint32_t w[sizeof(P) == 1 ? 1 : 2], e[sizeof(P) == 1 ? 1 : 2];
-            load4<P>(p + r * s.rs, w);
-            load4<P>(f + r * s.fs, e);
-            acc = sad4<P>(e, w, acc);
-        }
+        for (int r = 0; r < 4; r++) load4<P>(p + r * s.rs, w[r]);
+#pragma unroll
+        for (int r = 0; r < 4; r++) acc = sad4<P>(s.fe[k][r], w[r], acc);
     }
     return group_sum<G>((int)acc);
 }
@@ -409,6 +410,15 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_motion_search(const MeArgs a)
     s.tab = a.mvcost + a.mvcost_off[j];
     s.fenc = (const P*)a.fenc + a.fenc_off[j];
     s.fs = a.fs;
+#pragma unroll
+    for (int k = 0; k < kMeMaxUnits; k++)
+    {
+        if (k >= s.nu) break;
+        int ux, uy;
+        s.unit_xy(k, ux, uy);
+#pragma unroll
+        for (int r = 0; r < 4; r++) load4<P>(s.fenc + ux + (int64_t)(uy + r) * s.fs, s.fe[k][r]);
+    }
     // bChromaSATD = subpelRefine > 2 && the 4:2:0 chroma satd entry exists (chroma dims % 4 == 0)
     s.chroma = a.subme > 2 && a.fcb && ((a.w >> 1) & 3) == 0 && ((a.h >> 1) & 3) == 0;
     if (s.chroma)

@@ -544,6 +544,38 @@ def main():
             r["cpu_reference_error"] = str(ex)
         results.append(r)
         print(json.dumps(r), flush=True)
+        # batched: R independent (current, reference) frame pairs in ONE launch (the searches of several
+        # reference frames / lists or of several frames whose references are final): the latency-bound
+        # search needs many PUs in flight to fill 256 CUs
+        R = 8
+        synR = SyntheticSource(Wf, Hf, R + 1, 8)
+        curs = np.concatenate([padf(synR.frame(q + 1)[0]) for q in range(R)])
+        refs = np.concatenate([padf(synR.frame(q)[0]) for q in range(R)])
+        psz = f1.size
+        foR = (fo_h[None, :] + psz * np.arange(R)[:, None]).reshape(-1)
+        tile = lambda x, per: np.tile(x.reshape(n, per), (R, 1)).reshape(-1)
+        FR, RR, FOR = T(curs), T(refs), T(foR)
+        RGR, MPR, MCR, NCR, TOR = (T(tile(rng_h, 4)), T(tile(mvp_h, 2)), T(tile(mvc_h, 4)), T(tile(numc_h, 1)),
+                                   T(tile(toff_h, 1)))
+        OMR = torch.empty(2 * n * R, dtype=torch.int16, device=dev)
+        OCR = torch.empty(n * R, dtype=torch.int32, device=dev)
+        for meth, sub, tag in ((1, 2, "hex"), (2, 3, "star_subme3")):
+            if meth == 2:
+                cR = np.concatenate([padc(synR.frame(q + 1)[1]) for q in range(R)])
+                crR = np.concatenate([padc(synR.frame(q + 1)[2]) for q in range(R)])
+                rR = np.concatenate([padc(synR.frame(q)[1]) for q in range(R)])
+                rrR = np.concatenate([padc(synR.frame(q)[2]) for q in range(R)])
+                coR = T((co_h[None, :] + padc(fr1[1]).size * np.arange(R)[:, None]).reshape(-1))
+                chroma = (T(cR), T(crR), cst, coR, T(rR), T(rrR), cst, coR)
+            else:
+                chroma = ()
+            ms_b = timeit(lambda: prims.motion_search(8, s_, s_, meth, sub, 57, 2, FR, st, FOR, RR, st, FOR, RGR, MPR,
+                                                      MCR, NCR, TB, TOR, OMR, OCR, *chroma))
+            r = {"kernel": f"me_{tag}_{s_}x{s_}_x{R}", "jobs": n * R, "ms": round(ms_b, 4),
+                 "pu_per_s": round(n * R / (ms_b * 1e-3), 1),
+                 "note": f"{R} (current, reference) frame pairs of 1080p PUs in one launch"}
+            results.append(r)
+            print(json.dumps(r), flush=True)
     # ---------------------------------------------------------------- f4 loop filters
     # Whole frames, >= --gb of distinct frame buffers per call (8 frames per launch).  Algorithmic
     # bytes per frame: deblock = the picture read once and written once + its 16-byte CU units
