@@ -24,6 +24,8 @@
 
 namespace x265amd {
 
+typedef unsigned short pair16 __attribute__((ext_vector_type(2)));
+
 template <typename P, int N>
 __global__ __launch_bounds__(X265AMD_BLOCK) void k_intra_pred(int n, int maxv,
     P* __restrict__ dst, intptr_t ds, const int64_t* __restrict__ doff,
@@ -35,13 +37,17 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_intra_pred(int n, int maxv,
     constexpr int N2 = 2 * N;
     constexpr int LG2 = N == 4 ? 2 : N == 8 ? 3 : N == 16 ? 4 : 5;
     constexpr int SLOT = 4 * N + 4;                  // R: 3N+1, L: N+1, padded
+    constexpr int PW = 3 * N;                        // pairs D[j] = (R[j], R[j + 1]), j = -N .. 2N-1
     __shared__ int16_t sh[JOBS][SLOT];
+    __shared__ int16_t raw[JOBS][4 * N + 2];         // the 4N+1 neighbours as loaded
+    __shared__ uint32_t Dp[JOBS][PW];
     const int slot = threadIdx.x / N, r = threadIdx.x % N;
     const int64_t job = (int64_t)xcd_block() * JOBS + slot;
     const bool live = job < n;
     const int64_t jj = live ? job : 0;
     int16_t* R = sh[slot] + N;                       // R[j], j = -N .. 2N
     int16_t* L = sh[slot] + 3 * N + 2;               // L[y], y = 0 .. N
+    uint32_t* D = Dp[slot] + N;                      // D[j], j = -N .. 2N-1
 
     int m, bf;
     const P* src;
@@ -64,16 +70,29 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_intra_pred(int n, int maxv,
     }
     const ModeInfo mi = decode_mode(m);
 
-    // ---- stage: R[j] = s'[1 + j] for j = -1 .. 2N-1, L[y] = s'[2N + 1 + y] for y = 0 .. N
+    // ---- neighbours: lane r loads pixels 4r .. 4r+3 with one vector load (lane 0 also pixel 4N)
+    {
+        int t[4];
+        load_row<P, 4>(src + 4 * r, t);
+#pragma unroll
+        for (int k = 0; k < 4; k++) raw[slot][4 * r + k] = (int16_t)t[k];
+        if (r == 0) raw[slot][4 * N] = (int16_t)src[4 * N];
+    }
+    __syncthreads();
+    const int16_t* sr = raw[slot];
+    // ---- R[j] = s'[1 + j] for j = -1 .. 2N-1, L[y] = s'[2N + 1 + y] for y = 0 .. N
     //      (s' = neighbours in the mode's frame), R[-2-k] = projected left samples
-    for (int e = r; e < N2 + 1; e += N) R[e - 1] = (int16_t)src[flip_index(e, N2, mi.hor)];
-    for (int y = r; y <= N; y += N) L[y] = (int16_t)src[flip_index(N2 + 1 + y, N2, mi.hor)];
+    for (int e = r; e < N2 + 1; e += N) R[e - 1] = sr[flip_index(e, N2, mi.hor)];
+    for (int y = r; y <= N; y += N) L[y] = sr[flip_index(N2 + 1 + y, N2, mi.hor)];
     if (mi.angle < 0)
     {
         const int nproj = -((N * mi.angle) >> 5) - 1;     // intrapred.cpp:154-164
         for (int k = r; k < nproj; k += N)
-            R[-2 - k] = (int16_t)src[flip_index(N2 + ((128 + (k + 1) * mi.inv) >> 8), N2, mi.hor)];
+            R[-2 - k] = sr[flip_index(N2 + ((128 + (k + 1) * mi.inv) >> 8), N2, mi.hor)];
     }
+    __syncthreads();
+    // pairs for the angular interpolation: one ds_read_b32 + one v_dot2 per pixel
+    for (int j = r - N; j < 2 * N; j += N) D[j] = (uint32_t)(uint16_t)R[j] | ((uint32_t)(uint16_t)R[j + 1] << 16);
     __syncthreads();
     if (!live) return;
 
@@ -121,9 +140,11 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_intra_pred(int n, int maxv,
         }
         else
         {
-            const int16_t* row = R + off;
+            const pair16 wt = {(unsigned short)(32 - f), (unsigned short)f};
+            const uint32_t* row = D + off;
 #pragma unroll
-            for (int x = 0; x < N; x++) v[x] = ((32 - f) * row[x] + f * row[x + 1] + 16) >> 5;
+            for (int x = 0; x < N; x++)
+                v[x] = (int)(__builtin_amdgcn_udot2(__builtin_bit_cast(pair16, row[x]), wt, 16u, false) >> 5);
         }
     }
     else
@@ -150,8 +171,8 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_intra_pred(int n, int maxv,
             for (int c = 0; c < N; c++)
             {
                 const int sum = (c + 1) * mi.angle, off = sum >> 5, f = sum & 31;
-                const int a = R[off + r], b = R[off + r + 1];
-                v[c] = ((32 - f) * a + f * b + 16) >> 5;
+                const pair16 wt = {(unsigned short)(32 - f), (unsigned short)f};
+                v[c] = (int)(__builtin_amdgcn_udot2(__builtin_bit_cast(pair16, D[off + r]), wt, 16u, false) >> 5);
             }
         }
     }
@@ -185,9 +206,16 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_intra_lane(int n, int maxv,
     const P* __restrict__ filt, const int64_t* __restrict__ filtoff,
     const uint8_t* __restrict__ mode, const uint8_t* __restrict__ bfilter, int allangs)
 {
-    __shared__ uint32_t D[3 * N][X265AMD_BLOCK];     // D[j + N][lane], j = -N .. 2N-1
+    // D[j + N][lane], j = -N .. 2N-1; after the prediction the same LDS holds the 8x8 blocks of the
+    // block's 256 jobs for the coalesced store (N == 8)
+    constexpr int NB = N * N * (int)sizeof(P);                 // output bytes per job
+    constexpr int DW = 3 * N * X265AMD_BLOCK;                  // dwords of D
+    constexpr int SW = N == 8 ? NB * X265AMD_BLOCK / 4 : 0;    // dwords of the output staging
+    __shared__ uint32_t lds[DW > SW ? DW : SW];
+    uint32_t (*D)[X265AMD_BLOCK] = (uint32_t (*)[X265AMD_BLOCK])lds;
     const int64_t job = (int64_t)xcd_block() * X265AMD_BLOCK + threadIdx.x;
-    if (job >= n) return;
+    const bool live = job < n;
+    const int64_t jj = live ? job : 0;
 
     int m, bf;
     const P* src;
@@ -195,8 +223,8 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_intra_lane(int n, int maxv,
     intptr_t os;
     if (allangs)
     {
-        const int64_t tu = job / 33;
-        m = 2 + (int)(job % 33);
+        const int64_t tu = jj / 33;
+        m = 2 + (int)(jj % 33);
         bf = bfilter[tu];
         src = (c_intra.filter_flags[m] & N) ? filt + filtoff[tu] : nb + nboff[tu];
         out = dst + doff[tu] + (int64_t)(m - 2) * N * N;
@@ -204,10 +232,10 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_intra_lane(int n, int maxv,
     }
     else
     {
-        m = mode[job];
-        bf = bfilter[job];
-        src = nb + nboff[job];
-        out = dst + doff[job];
+        m = mode[jj];
+        bf = bfilter[jj];
+        src = nb + nboff[jj];
+        out = dst + doff[jj];
         os = ds;
     }
     int s[4 * N + 1], v[N][N];
@@ -216,14 +244,79 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_intra_lane(int n, int maxv,
 
     // horizontal modes are transposed back, except in all-angles output
     const bool tr = mi.hor && !allangs;
+    int o[N][N];
 #pragma unroll
     for (int r = 0; r < N; r++)
-    {
-        int o[N];
 #pragma unroll
-        for (int c = 0; c < N; c++) o[c] = tr ? v[c][r] : v[r][c];
-        store_row<P, N>(out + (int64_t)r * os, o);
+        for (int c = 0; c < N; c++) o[r][c] = tr ? v[c][r] : v[r][c];
+
+    // compact blocks (stride N) of consecutive jobs at consecutive addresses: the wave's outputs are one
+    // contiguous run, written with coalesced 16-byte stores instead of one short row per lane
+    const int lane = threadIdx.x & 63;
+    const P* out0 = (const P*)__shfl((long long)(intptr_t)out, 0, 64);
+    const bool run = os == N && (!live || out == out0 + (int64_t)lane * N * N);
+    const bool wave_run = __all(run);
+    if constexpr (N == 4)
+    {
+        if (!live) return;
+        if (os == 4)
+        {
+            uint32_t w[NB / 4];
+#pragma unroll
+            for (int r = 0; r < 4; r++)
+            {
+                if constexpr (sizeof(P) == 1)
+                    w[r] = (uint32_t)o[r][0] | ((uint32_t)o[r][1] << 8) | ((uint32_t)o[r][2] << 16) | ((uint32_t)o[r][3] << 24);
+                else
+                {
+                    w[2 * r] = (uint32_t)o[r][0] | ((uint32_t)o[r][1] << 16);
+                    w[2 * r + 1] = (uint32_t)o[r][2] | ((uint32_t)o[r][3] << 16);
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < NB / 16; q++)
+                stu<uint4>((uint8_t*)out + 16 * q, make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]));
+            return;
+        }
     }
+    else
+    {
+        const int wv = threadIdx.x >> 6;
+        // block-uniform decision (every lane has left D once the barrier returns)
+        if (__syncthreads_and(wave_run))
+        {
+            uint8_t* stg = (uint8_t*)lds + (size_t)wv * 64 * NB;
+            uint32_t* mine = (uint32_t*)(stg + lane * NB);
+#pragma unroll
+            for (int r = 0; r < N; r++)
+            {
+                if constexpr (sizeof(P) == 1)
+                {
+                    mine[2 * r] = (uint32_t)o[r][0] | ((uint32_t)o[r][1] << 8) | ((uint32_t)o[r][2] << 16) | ((uint32_t)o[r][3] << 24);
+                    mine[2 * r + 1] = (uint32_t)o[r][4] | ((uint32_t)o[r][5] << 8) | ((uint32_t)o[r][6] << 16) | ((uint32_t)o[r][7] << 24);
+                }
+                else
+                {
+#pragma unroll
+                    for (int q = 0; q < 4; q++) mine[4 * r + q] = (uint32_t)o[r][2 * q] | ((uint32_t)o[r][2 * q + 1] << 16);
+                }
+            }
+            __syncthreads();
+            const int64_t live_jobs = (int64_t)n - (job - lane);
+            const int64_t lim = (live_jobs < 64 ? live_jobs : 64) * NB;    // bytes of the wave's live jobs
+            uint8_t* base = (uint8_t*)out0;
+#pragma unroll
+            for (int q = 0; q < NB / 16; q++)
+            {
+                const int off = (q * 64 + lane) * 16;
+                if (off < lim) stu<uint4>(base + off, *(const uint4*)(stg + off));
+            }
+            return;
+        }
+        if (!live) return;
+    }
+#pragma unroll
+    for (int r = 0; r < N; r++) store_row<P, N>(out + (int64_t)r * os, o[r]);
 }
 
 template <typename P>
