@@ -535,8 +535,9 @@ int x265amd_weights_analyse(int depth, x265amd_weights_batch* batch, void* strea
  * MotionEstimate::motionEstimate call (motion.cpp:571-1172) on a full-resolution
  * luma reference, as Search::predInterSearch makes it (search.cpp:2024, 2112):
  * the clipped MVP measured at sub-pel (SAD, no MV cost), the num_cand[i] extra
- * candidates (AMVP list), DIA (method 0), HEX (method 1, --preset medium) or STAR
- * (method 2, --preset slow) integer search within merange, then the sub-pel refine
+ * candidates (AMVP list), DIA (method 0), HEX (method 1, --preset medium), STAR
+ * (method 2, --preset slow) or UMH (method 3, --me umh: adaptive range, early
+ * termination, hexagon grid) integer search within merange, then the sub-pel refine
  * of workload[subme] for subme 0..7 (motion.cpp:48-58; from subme 3 the 4:2:0
  * chroma SATD is added when the chroma planes are given).  fenc_off[i] / ref_off[i] = the PU origin in the
  * source / reference plane (the reference is border-extended as PicYuv is);

@@ -1708,6 +1708,139 @@ int xo_motion_search(int w, int h, int method, int subme, int merange, const voi
     }
     else
     {
+    int do_hex = 1;
+    if (method == 3)
+    {
+        /* UMH (motion.cpp:744-926); ends either by leaving the search (`break`: do_hex = 0) or by
+           continuing with the hexagon search at me_hex2 when the result is in range */
+        static const xmv hex4[16] = { { 0, -4 }, { 0, 4 }, { -2, -3 }, { 2, -3 }, { -4, -2 }, { 4, -2 }, { -4, -1 },
+                                      { 4, -1 }, { -4, 0 }, { 4, 0 }, { -4, 1 }, { 4, 1 }, { -4, 2 }, { 4, 2 },
+                                      { -2, 3 }, { 2, 3 } };
+        static const uint8_t range_mul[4][4] = { { 3, 3, 4, 4 }, { 3, 4, 4, 4 }, { 4, 4, 4, 5 }, { 4, 4, 5, 6 } };
+        const int scale = (h * h) >> 4;                      /* sizeScale[partEnum] (motion.cpp:121-150) */
+#define XO_SAD_THRESH(v) (bcost < (((v) >> 4) * scale))
+#define XO_COST_MV(mx, my) do { const int _x = (mx), _y = (my); \
+            const int _c = xo_f_fpel_sad(&m, _x, _y) + xo_f_mvcost(&m, _x * 4, _y * 4); \
+            if (_c < bcost) { bcost = _c; bmv.x = _x; bmv.y = _y; } } while (0)
+#define XO_COST_MV_X4(a0, b0, a1, b1, a2, b2, a3, b3) do { \
+            const int _c0 = xo_f_fpel_sad(&m, omv.x + (a0), omv.y + (b0)) + xo_f_mvcost(&m, (omv.x + (a0)) * 4, (omv.y + (b0)) * 4); \
+            const int _c1 = xo_f_fpel_sad(&m, omv.x + (a1), omv.y + (b1)) + xo_f_mvcost(&m, (omv.x + (a1)) * 4, (omv.y + (b1)) * 4); \
+            const int _c2 = xo_f_fpel_sad(&m, omv.x + (a2), omv.y + (b2)) + xo_f_mvcost(&m, (omv.x + (a2)) * 4, (omv.y + (b2)) * 4); \
+            const int _c3 = xo_f_fpel_sad(&m, omv.x + (a3), omv.y + (b3)) + xo_f_mvcost(&m, (omv.x + (a3)) * 4, (omv.y + (b3)) * 4); \
+            if (_c0 < bcost) { bcost = _c0; bmv.x = omv.x + (a0); bmv.y = omv.y + (b0); } \
+            if (_c1 < bcost) { bcost = _c1; bmv.x = omv.x + (a1); bmv.y = omv.y + (b1); } \
+            if (_c2 < bcost) { bcost = _c2; bmv.x = omv.x + (a2); bmv.y = omv.y + (b2); } \
+            if (_c3 < bcost) { bcost = _c3; bmv.x = omv.x + (a3); bmv.y = omv.y + (b3); } } while (0)
+#define XO_DIA1(mx, my) do { omv.x = (mx); omv.y = (my); XO_COST_MV_X4(0, -1, 0, 1, -1, 0, 1, 0); } while (0)
+#define XO_CROSS(start, x_max, y_max) do { \
+            int _i = (start); const int _xm = (x_max), _ym = (y_max); \
+            if (_xm <= XO_MIN2(mvmax.x - omv.x, omv.x - mvmin.x)) \
+                for (; _i < _xm - 2; _i += 4) XO_COST_MV_X4(_i, 0, -_i, 0, _i + 2, 0, -_i - 2, 0); \
+            for (; _i < _xm; _i += 2) { \
+                if (omv.x + _i <= mvmax.x) XO_COST_MV(omv.x + _i, omv.y); \
+                if (omv.x - _i >= mvmin.x) XO_COST_MV(omv.x - _i, omv.y); } \
+            _i = (start); \
+            if (_ym <= XO_MIN2(mvmax.y - omv.y, omv.y - mvmin.y)) \
+                for (; _i < _ym - 2; _i += 4) XO_COST_MV_X4(0, _i, 0, -_i, 0, _i + 2, 0, -_i - 2); \
+            for (; _i < _ym; _i += 2) { \
+                if (omv.y + _i <= mvmax.y) XO_COST_MV(omv.x, omv.y + _i); \
+                if (omv.y - _i >= mvmin.y) XO_COST_MV(omv.x, omv.y - _i); } } while (0)
+#define XO_MIN2(a, b) ((a) < (b) ? (a) : (b))
+        const xmv fpmv = { (pmv.x + 2) >> 2, (pmv.y + 2) >> 2 };       /* pmv.roundToFPel() (motion.cpp:645) */
+        xmv omv = bmv;
+        int cross_start = 1, range = merange;
+        const int ucost1 = bcost;
+        XO_DIA1(fpmv.x, fpmv.y);
+        if (fpmv.x || fpmv.y) XO_DIA1(0, 0);
+        const int ucost2 = bcost;
+        if ((bmv.x || bmv.y) && (bmv.x != fpmv.x || bmv.y != fpmv.y)) XO_DIA1(bmv.x, bmv.y);
+        if (bcost == ucost2) cross_start = 3;
+        omv = bmv;
+        do_hex = -1;
+        if (bcost == ucost2 && XO_SAD_THRESH(2000))
+        {
+            XO_COST_MV_X4(0, -2, -1, -1, 1, -1, -2, 0);
+            XO_COST_MV_X4(2, 0, -1, 1, 1, 1, 0, 2);
+            if (bcost == ucost1 && XO_SAD_THRESH(500)) do_hex = 0;
+            else if (bcost == ucost2)
+            {
+                const int r = (merange >> 1) | 1;
+                XO_CROSS(3, r, r);
+                XO_COST_MV_X4(-1, -2, 1, -2, -2, -1, 2, -1);
+                XO_COST_MV_X4(-2, 1, 2, 1, -1, 2, 1, 2);
+                if (bcost == ucost2) do_hex = 0;
+                else cross_start = r + 2;
+            }
+        }
+        if (do_hex)
+        {
+            if (numc)
+            {
+                /* adaptive range from the candidates' agreement (motion.cpp:785-834) */
+                int mvd, denom = 1;
+                const int is64 = w == 64 && h == 64;
+                if (numc == 1)
+                    mvd = is64 ? 25 : abs(mvpx - mvc[0]) + abs(mvpy - mvc[1]);
+                else
+                {
+                    denom = numc - 1;
+                    mvd = 0;
+                    if (!is64)
+                    {
+                        mvd = abs(mvpx - mvc[0]) + abs(mvpy - mvc[1]);
+                        denom++;
+                    }
+                    for (int k = 0; k < numc - 1; k++)     /* predictorDifference (motion.cpp:87-98) */
+                        mvd += abs(mvc[2 * k] - mvc[2 * k + 2]) + abs(mvc[2 * k + 1] - mvc[2 * k + 3]);
+                }
+                const int sad_ctx = XO_SAD_THRESH(1000) ? 0 : XO_SAD_THRESH(2000) ? 1 : XO_SAD_THRESH(4000) ? 2 : 3;
+                const int mvd_ctx = mvd < 10 * denom ? 0 : mvd < 20 * denom ? 1 : mvd < 40 * denom ? 2 : 3;
+                range = (range * range_mul[mvd_ctx][sad_ctx]) >> 2;
+            }
+            merange = range;                     /* the reference rescales merange itself: me_hex2 sees it */
+            XO_CROSS(cross_start, range, range >> 1);
+            XO_COST_MV_X4(-2, -2, -2, 2, 2, -2, 2, 2);
+            /* hexagon grid (motion.cpp:866-921) */
+            omv = bmv;
+            int gi = 1;
+            do
+            {
+                const int lim = XO_MIN2(XO_MIN2(mvmax.x - omv.x, omv.x - mvmin.x), XO_MIN2(mvmax.y - omv.y, omv.y - mvmin.y));
+                if (4 * gi > lim)
+                {
+                    for (int k = 0; k < 16; k++)
+                    {
+                        const xmv c = { omv.x + hex4[k].x * gi, omv.y + hex4[k].y * gi };
+                        if (xo_in_range(c, mvmin, mvmax)) XO_COST_MV(c.x, c.y);
+                    }
+                }
+                else
+                {
+                    int dir = 0;
+                    for (int k = 0; k < 16; k++)
+                    {
+                        const int c = xo_f_fpel_sad(&m, omv.x + hex4[k].x * gi, omv.y + hex4[k].y * gi) +
+                                      xo_f_mvcost(&m, (omv.x + hex4[k].x * gi) * 4, (omv.y + hex4[k].y * gi) * 4);
+                        if (c < bcost) { bcost = c; dir = hex4[k].x * 16 + (hex4[k].y & 15); }
+                    }
+                    if (dir)
+                    {
+                        bmv.x = omv.x + gi * (dir >> 4);
+                        bmv.y = omv.y + gi * ((int32_t)((uint32_t)dir << 28) >> 28);
+                    }
+                }
+            } while (++gi <= range >> 2);
+            do_hex = xo_in_range(bmv, mvmin, mvmax);
+        }
+#undef XO_SAD_THRESH
+#undef XO_COST_MV
+#undef XO_COST_MV_X4
+#undef XO_DIA1
+#undef XO_CROSS
+#undef XO_MIN2
+    }
+    if (do_hex)
+    {
         int c0 = XO_FC(-2, 0), c1 = XO_FC(-1, 2), c2 = XO_FC(1, 2);
         bcost <<= 3;
         if ((c0 << 3) + 2 < bcost) bcost = (c0 << 3) + 2;
@@ -1744,6 +1877,7 @@ int xo_motion_search(int w, int h, int method, int subme, int merange, const voi
             if (c < bcost) { bcost = c; dir = k; }
         }
         bmv.x += square1[dir].x; bmv.y += square1[dir].y;
+    }
     }
 #undef XO_FC
     if (bprecost < bcost) { bmv = bestpre; bcost = bprecost; }

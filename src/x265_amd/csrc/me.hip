@@ -613,6 +613,143 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_motion_search(const MeArgs a)
     }
     else
     {
+    bool do_hex = true;
+    int hex_range = a.merange;            // UMH rescales merange before its goto me_hex2
+    if (a.method == 3)
+    {
+        // UMH (motion.cpp:744-926), in lockstep on the group; `break`s of the reference leave the
+        // search (do_hex = false), its `goto me_hex2` continues with the hexagon search below
+        auto ca = [&](int x, int y) { return fpel_sad<P, G>(s, x, y) + s.mvcost(4 * x, 4 * y); };
+        auto cost_mv = [&](int x, int y) {
+            const int c = ca(x, y);
+            if (c < bcost) { bcost = c; bx = x; by = y; }
+        };
+        int ox = bx, oy = by;
+        auto cost_x4 = [&](int a0, int b0, int a1, int b1, int a2, int b2, int a3, int b3) {
+            const int c0 = ca(ox + a0, oy + b0), c1 = ca(ox + a1, oy + b1);
+            const int c2 = ca(ox + a2, oy + b2), c3 = ca(ox + a3, oy + b3);
+            if (c0 < bcost) { bcost = c0; bx = ox + a0; by = oy + b0; }
+            if (c1 < bcost) { bcost = c1; bx = ox + a1; by = oy + b1; }
+            if (c2 < bcost) { bcost = c2; bx = ox + a2; by = oy + b2; }
+            if (c3 < bcost) { bcost = c3; bx = ox + a3; by = oy + b3; }
+        };
+        auto dia1 = [&](int mx, int my) { ox = mx; oy = my; cost_x4(0, -1, 0, 1, -1, 0, 1, 0); };
+        auto cross = [&](int start, int xm, int ym) {
+            int i = start;
+            if (xm <= min(maxx - ox, ox - minx))
+                for (; i < xm - 2; i += 4) cost_x4(i, 0, -i, 0, i + 2, 0, -i - 2, 0);
+            for (; i < xm; i += 2)
+            {
+                if (ox + i <= maxx) cost_mv(ox + i, oy);
+                if (ox - i >= minx) cost_mv(ox - i, oy);
+            }
+            i = start;
+            if (ym <= min(maxy - oy, oy - miny))
+                for (; i < ym - 2; i += 4) cost_x4(0, i, 0, -i, 0, i + 2, 0, -i - 2);
+            for (; i < ym; i += 2)
+            {
+                if (oy + i <= maxy) cost_mv(ox, oy + i);
+                if (oy - i >= miny) cost_mv(ox, oy - i);
+            }
+        };
+        const int scale = (a.h * a.h) >> 4;                 // sizeScale[partEnum] (motion.cpp:121-150)
+        auto thresh = [&](int v) { return bcost < ((v >> 4) * scale); };
+        const int fpx = (pmx + 2) >> 2, fpy = (pmy + 2) >> 2;   // pmv.roundToFPel()
+        int cross_start = 1, merange = a.merange;
+        const int ucost1 = bcost;
+        dia1(fpx, fpy);
+        if (fpx | fpy) dia1(0, 0);
+        const int ucost2 = bcost;
+        if ((bx | by) && (bx != fpx || by != fpy)) dia1(bx, by);
+        if (bcost == ucost2) cross_start = 3;
+        ox = bx; oy = by;
+        bool go = true;
+        if (bcost == ucost2 && thresh(2000))
+        {
+            cost_x4(0, -2, -1, -1, 1, -1, -2, 0);
+            cost_x4(2, 0, -1, 1, 1, 1, 0, 2);
+            if (bcost == ucost1 && thresh(500)) go = false;
+            else if (bcost == ucost2)
+            {
+                const int r = (merange >> 1) | 1;
+                cross(3, r, r);
+                cost_x4(-1, -2, 1, -2, -2, -1, 2, -1);
+                cost_x4(-2, 1, 2, 1, -1, 2, 1, 2);
+                if (bcost == ucost2) go = false;
+                else cross_start = r + 2;
+            }
+        }
+        if (go)
+        {
+            if (nc)
+            {
+                // adaptive range from the candidates' agreement (motion.cpp:785-834)
+                const int qmx = s.mvpx, qmy = s.mvpy;
+                const int16_t* mc = a.mvc + 2 * j * a.max_cand;
+                const bool is64 = a.w == 64 && a.h == 64;
+                int mvd, denom = 1;
+                if (nc == 1)
+                    mvd = is64 ? 25 : abs(qmx - mc[0]) + abs(qmy - mc[1]);
+                else
+                {
+                    denom = nc - 1;
+                    mvd = 0;
+                    if (!is64)
+                    {
+                        mvd = abs(qmx - mc[0]) + abs(qmy - mc[1]);
+                        denom++;
+                    }
+                    for (int k = 0; k < nc - 1; k++)
+                        mvd += abs(mc[2 * k] - mc[2 * k + 2]) + abs(mc[2 * k + 1] - mc[2 * k + 3]);
+                }
+                const int sad_ctx = thresh(1000) ? 0 : thresh(2000) ? 1 : thresh(4000) ? 2 : 3;
+                const int mvd_ctx = mvd < 10 * denom ? 0 : mvd < 20 * denom ? 1 : mvd < 40 * denom ? 2 : 3;
+                // range_mul[4][4] = {{3,3,4,4},{3,4,4,4},{4,4,4,5},{4,4,5,6}} as nibbles
+                constexpr uint64_t RM = 0x6544544444434433ull;
+                merange = (merange * (int)((RM >> (4 * (4 * mvd_ctx + sad_ctx))) & 15)) >> 2;
+            }
+            cross(cross_start, merange, merange >> 1);
+            cost_x4(-2, -2, -2, 2, 2, -2, 2, 2);
+            // hexagon grid (motion.cpp:866-921): hex4[k] as nibbles (value + 4)
+            constexpr uint64_t HX = 0x6280808080806244ull, HY = 0x7766554433221180ull;
+            ox = bx; oy = by;
+            int gi = 1;
+            do
+            {
+                const int lim = min(min(maxx - ox, ox - minx), min(maxy - oy, oy - miny));
+                if (4 * gi > lim)
+                {
+                    for (int k = 0; k < 16; k++)
+                    {
+                        const int cx = ox + ((int)((HX >> (4 * k)) & 15) - 4) * gi;
+                        const int cy = oy + ((int)((HY >> (4 * k)) & 15) - 4) * gi;
+                        if (cx >= minx && cx <= maxx && cy >= miny && cy <= maxy) cost_mv(cx, cy);
+                    }
+                }
+                else
+                {
+                    int dir = 0;
+                    for (int k = 0; k < 16; k++)
+                    {
+                        const int hx = (int)((HX >> (4 * k)) & 15) - 4, hy = (int)((HY >> (4 * k)) & 15) - 4;
+                        const int c = ca(ox + hx * gi, oy + hy * gi);
+                        if (c < bcost) { bcost = c; dir = hx * 16 + (hy & 15); }
+                    }
+                    if (dir)
+                    {
+                        bx = ox + gi * (dir >> 4);
+                        by = oy + gi * ((int)((uint32_t)dir << 28) >> 28);
+                    }
+                }
+            } while (++gi <= merange >> 2);
+            do_hex = bx >= minx && bx <= maxx && by >= miny && by <= maxy;
+            hex_range = merange;
+        }
+        else
+            do_hex = false;
+    }
+    if (do_hex)
+    {
         int c0 = fc(-2, 0), c1 = fc(-1, 2), c2 = fc(1, 2);
         bcost <<= 3;
         if ((c0 << 3) + 2 < bcost) bcost = (c0 << 3) + 2;
@@ -626,7 +763,7 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_motion_search(const MeArgs a)
         {
             int dir = (bcost & 7) - 2;
             bx += hex_dx(dir + 1); by += hex_dy(dir + 1);
-            for (int i = (a.merange >> 1) - 1; i > 0 && bx >= minx && bx <= maxx && by >= miny && by <= maxy; i--)
+            for (int i = (hex_range >> 1) - 1; i > 0 && bx >= minx && bx <= maxx && by >= miny && by <= maxy; i--)
             {
                 c0 = fc(hex_dx(dir), hex_dy(dir));
                 c1 = fc(hex_dx(dir + 1), hex_dy(dir + 1));
@@ -649,6 +786,7 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_motion_search(const MeArgs a)
             if (c < bcost) { bcost = c; sdir = k; }
         }
         bx += sq_dx(sdir); by += sq_dy(sdir);
+    }
     }
     int qx, qy;
     if (bprecost < bcost) { qx = bpx; qy = bpy; bcost = bprecost; }
@@ -721,7 +859,7 @@ extern "C" int x265amd_motion_search(int depth, int count, const x265amd_me_batc
     {
         const x265amd_me_batch& b = bt[i];
         if (b.n < 0 || b.w < 4 || b.h < 4 || b.w > 64 || b.h > 64 || (b.w & 3) || (b.h & 3)) return X265AMD_EINVAL;
-        if (b.method < 0 || b.method > 2 || b.subme < 0 || b.subme > 7 || b.merange < 1) return X265AMD_EINVAL;
+        if (b.method < 0 || b.method > 3 || b.subme < 0 || b.subme > 7 || b.merange < 1) return X265AMD_EINVAL;
         if (b.n && b.fenc_cb && (!b.fenc_cr || !b.fenc_coff || !b.ref_cb || !b.ref_cr || !b.ref_coff))
             return X265AMD_EINVAL;
         if (b.n && (!b.fenc || !b.fenc_off || !b.ref || !b.ref_off || !b.mv_range || !b.mvp || !b.mvcost ||

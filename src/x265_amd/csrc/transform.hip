@@ -32,13 +32,24 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_tr4(int n, int depth,
     const int16_t* ps = src + soff[job];
     int16_t* pd = dst + doff[job];
     int m[4][4], t[4][4];
-#pragma unroll
-    for (int r = 0; r < 4; r++)
+    if (ss == 4)
     {
-        int v[4];
-        load_row16<4>(ps + r * ss, v);
+        // compact block (coefficients, compact residuals): 32 contiguous bytes, two 16-byte loads
+        const uint4 a = ldu<uint4>(ps), b = ldu<uint4>(ps + 8);
+        const uint32_t w[8] = { a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w };
 #pragma unroll
-        for (int c = 0; c < 4; c++) m[r][c] = v[c];
+        for (int i = 0; i < 16; i++) m[i >> 2][i & 3] = (int)(int16_t)(w[i >> 1] >> (16 * (i & 1)));
+    }
+    else
+    {
+#pragma unroll
+        for (int r = 0; r < 4; r++)
+        {
+            int v[4];
+            load_row16<4>(ps + r * ss, v);
+#pragma unroll
+            for (int c = 0; c < 4; c++) m[r][c] = v[c];
+        }
     }
     const bool fwd = KIND == X265AMD_DCT || KIND == X265AMD_DST;
     const int sh1 = fwd ? 1 + depth - 8 : 7, sh2 = fwd ? 8 : 12 - (depth - 8);
@@ -81,6 +92,16 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_tr4(int n, int depth,
 #pragma unroll
             for (int k = 0; k < 4; k++) m[j][k] = inv_round(y[k], sh2);
         }
+    }
+    if (ds == 4)
+    {
+        uint32_t w[8];
+#pragma unroll
+        for (int i = 0; i < 8; i++)
+            w[i] = (uint32_t)(uint16_t)m[(2 * i) >> 2][(2 * i) & 3] | ((uint32_t)(uint16_t)m[(2 * i + 1) >> 2][(2 * i + 1) & 3] << 16);
+        stu<uint4>(pd, make_uint4(w[0], w[1], w[2], w[3]));
+        stu<uint4>(pd + 8, make_uint4(w[4], w[5], w[6], w[7]));
+        return;
     }
 #pragma unroll
     for (int r = 0; r < 4; r++)

@@ -3,7 +3,8 @@
 Parity chain: the reference's own MotionEstimate::motionEstimate (motion.cpp:571-1172,
 driven through oracle/ref_shim.cpp with its own BitCost tables) -> golden hashes (the `me`
 cases of cases.all_cases: every luma PU shape with HEX / subme 2 as at --preset medium,
-DIA and subme 0 / 1 on the square sizes) -> oracle restatement (xo_motion_search) [CPU]
+DIA and subme 0 / 1 on the square sizes; STAR / UMH and subme 3-7 checked by the oracle
+against the reference here and by the GPU against the oracle) -> oracle restatement (xo_motion_search) [CPU]
 -> gfx950 kernel k_motion_search [GPU].  Output MVs and costs bit-exact.
 """
 import numpy as np
@@ -18,7 +19,7 @@ from pyoracle import CpuOracle, available
 def test_me_oracle_matches_reference(oracle_libs, depth):
     orc, ref = CpuOracle("oracle", depth), CpuOracle("ref", depth)
     for (w, h) in ((8, 8), (16, 16), (64, 64), (32, 8), (12, 16)):
-        for method, subme in ((1, 2), (0, 1), (2, 3), (2, 4), (1, 5), (2, 6), (2, 7)):
+        for method, subme in ((1, 2), (0, 1), (2, 3), (2, 4), (1, 5), (2, 6), (2, 7), (3, 2), (3, 3)):
             c = case_me(w, h, method, subme, 57 if method else 16, depth, 64, seed_of("me-r", depth, w, h, method))
             a, b = run_cpu(c, orc), run_cpu(c, ref)
             for k in c.outs:
@@ -41,6 +42,10 @@ def test_me_gpu_matches_oracle(gpu_prims, oracle_libs, depth):
     orc = CpuOracle("oracle", depth)
     cases = me_cases(depth) + [case_me(w, h, 1, 2, 57, depth, 512, seed_of("me-g", depth, w, h))
                                for (w, h) in ((8, 8), (16, 16), (32, 32), (64, 64))]
+    # --me umh (method 3): every luma PU shape, plus the sub-pel levels with chroma SATD
+    cases += [case_me(w, h, 3, 2, 57, depth, 48, seed_of("me-umh", depth, w, h)) for (w, h) in LUMA_PU[1:]]
+    cases += [case_me(w, h, 3, s, 57, depth, 128, seed_of("me-umh-s", depth, w, h, s))
+              for (w, h) in ((8, 8), (32, 32), (64, 64)) for s in (3, 5)]
     bad = []
     for c in cases:
         got, exp = run_gpu(c, gpu_prims), run_cpu(c, orc)
