@@ -536,8 +536,10 @@ int x265amd_weights_analyse(int depth, x265amd_weights_batch* batch, void* strea
  * luma reference, as Search::predInterSearch makes it (search.cpp:2024, 2112):
  * the clipped MVP measured at sub-pel (SAD, no MV cost), the num_cand[i] extra
  * candidates (AMVP list), DIA (method 0), HEX (method 1, --preset medium), STAR
- * (method 2, --preset slow) or UMH (method 3, --me umh: adaptive range, early
- * termination, hexagon grid) integer search within merange, then the sub-pel refine
+ * (method 2, --preset slow), UMH (method 3, --me umh: adaptive range, early
+ * termination, hexagon grid) or FULL (method 4, --me full: every MV of mv_range, the
+ * first raster-order minimum; out_mv / out_cost double as its scratch) integer search
+ * within merange, then the sub-pel refine
  * of workload[subme] for subme 0..7 (motion.cpp:48-58; from subme 3 the 4:2:0
  * chroma SATD is added when the chroma planes are given).  fenc_off[i] / ref_off[i] = the PU origin in the
  * source / reference plane (the reference is border-extended as PicYuv is);

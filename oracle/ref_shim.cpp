@@ -871,7 +871,7 @@ int xo_motion_search(int w, int h, int method, int subme, int merange, const voi
         me = new SearchME();
         me->init(X265_HEX_SEARCH, 2, X265_CSP_I420);   /* allocates the 4:2:0 fenc PU buffers once */
     }
-    me->configure(method == 0 ? X265_DIA_SEARCH : method == 1 ? X265_HEX_SEARCH : method == 3 ? X265_UMH_SEARCH : X265_STAR_SEARCH, subme);
+    me->configure(method == 0 ? X265_DIA_SEARCH : method == 1 ? X265_HEX_SEARCH : method == 3 ? X265_UMH_SEARCH : method == 4 ? X265_FULL_SEARCH : X265_STAR_SEARCH, subme);
     me->setQP(g_me_qp);
     me->setSourcePU((pixel*)fenc, fs, 0, w, h);
     /* chroma PU as Yuv::copyPUFromYuv would place it, and bChromaSATD as the encoder's setSourcePU

@@ -1709,7 +1709,19 @@ int xo_motion_search(int w, int h, int method, int subme, int merange, const voi
     else
     {
     int do_hex = 1;
-    if (method == 3)
+    if (method == 4)
+    {
+        /* FULL (motion.cpp:1039-1074): every integer MV of the range in raster order; the sad_x4
+           grouping of the reference changes nothing (each candidate's cost is SAD + mvcost(tmv << 2)) */
+        for (int ty = mvmin.y; ty <= mvmax.y; ty++)
+            for (int tx = mvmin.x; tx <= mvmax.x; tx++)
+            {
+                const int c = xo_f_fpel_sad(&m, tx, ty) + xo_f_mvcost(&m, tx * 4, ty * 4);
+                if (c < bcost) { bcost = c; bmv.x = tx; bmv.y = ty; }
+            }
+        do_hex = 0;
+    }
+    else if (method == 3)
     {
         /* UMH (motion.cpp:744-926); ends either by leaving the search (`break`: do_hex = 0) or by
            continuing with the hexagon search at me_hex2 when the result is in range */

@@ -166,7 +166,7 @@ void     xo_weights_analyse(int width, int lines, intptr_t stride, int padded_li
                             void* const* wbuf, uint64_t fenc_ssd, uint64_t ref_ssd, uint64_t fenc_sum,
                             uint64_t ref_sum, int* out, double* cost_delta);
 /* f2: MotionEstimate::motionEstimate (motion.cpp:571-1172) for one w x h PU on a full-resolution
- * reference: method 0 = DIA, 1 = HEX, 2 = STAR; subme 0..3 (at 3 the 4:2:0 chroma SATD of
+ * reference: method 0 = DIA, 1 = HEX, 2 = STAR, 3 = UMH, 4 = FULL; subme 0..7 (from 3 the 4:2:0 chroma SATD of
  * subpelCompare is added when fcb != NULL and the chroma PU has a satd entry: fcb / fcr, rcb / rcr =
  * source / reference Cb, Cr at the PU's chroma origin); fenc / ref at the PU origin; mvmin /
  * mvmax full-pel; mvp and the numc candidates mvc (x, y pairs) quarter-pel; tab_centre = the

@@ -16,6 +16,8 @@
 // sums SAD / SATD partials with shuffles.  Every decision is then identical
 // in all lanes of the group, so the search runs in lockstep in the reference's
 // candidate order (the packed-cost tie rules of the DIA / HEX loops included).
+// FULL search is the one data-parallel integer search: k_full_search (below) runs it as a
+// block-per-PU argmin before the lockstep kernel refines its result.
 #include "common.h"
 #include "../../../include/x265_amd.h"
 
@@ -615,7 +617,14 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_motion_search(const MeArgs a)
     {
     bool do_hex = true;
     int hex_range = a.merange;            // UMH rescales merange before its goto me_hex2
-    if (a.method == 3)
+    if (a.method == 4)
+    {
+        // FULL: k_full_search left the first raster-order minimum of the range in out_mv / out_cost
+        const int fcost = a.out_cost[j];
+        if (fcost < bcost) { bcost = fcost; bx = a.out_mv[2 * j]; by = a.out_mv[2 * j + 1]; }
+        do_hex = false;
+    }
+    else if (a.method == 3)
     {
         // UMH (motion.cpp:744-926), in lockstep on the group; `break`s of the reference leave the
         // search (do_hex = false), its `goto me_hex2` continues with the hexagon search below
@@ -833,9 +842,129 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_motion_search(const MeArgs a)
     }
 }
 
+// FULL search (motion.cpp:1039-1074) as a data-parallel argmin: one block per PU over candidate
+// tiles of kFsTx x kFsTy integer MVs.  The tile's reference window and the PU's source block are
+// staged in LDS; each thread costs 4 horizontally adjacent MVs of one row (v_sad_u8 / v_sad_u16 on
+// byte-aligned windows of two / four LDS dwords).  The block keeps the minimum of (cost, raster
+// index) — the first raster-order minimum, which is what the reference's strict-less scan leaves —
+// and writes it to out_mv / out_cost, where k_motion_search picks it up against the predictors.
+constexpr int kFsTx = 64, kFsTy = 16;
+
+template <typename P>
+__global__ __launch_bounds__(256) void k_full_search(const MeArgs a)
+{
+    constexpr int WSMAX = kFsTx + 64 + 4;
+    __shared__ uint32_t win[(kFsTy + 63) * WSMAX * sizeof(P) / 4];
+    __shared__ uint32_t fen[64 * 64 * sizeof(P) / 4];
+    __shared__ uint32_t red[8];
+    const int j = blockIdx.x, t = threadIdx.x;
+    const int w = a.w, h = a.h;
+    const P* ref = (const P*)a.ref + a.ref_off[j];
+    const P* fenc = (const P*)a.fenc + a.fenc_off[j];
+    const uint16_t* tab = a.mvcost + a.mvcost_off[j];
+    const int mvpx = a.mvp[2 * j], mvpy = a.mvp[2 * j + 1];
+    const int minx = a.mv_range[4 * j], miny = a.mv_range[4 * j + 1];
+    const int ncx = a.mv_range[4 * j + 2] - minx + 1, ncy = a.mv_range[4 * j + 3] - miny + 1;
+    const int WS = kFsTx + w + 4;                       // window row stride (pixels, multiple of 4)
+    P* fl = (P*)fen;
+    P* wl = (P*)win;
+    for (int i = t; i < w * h; i += 256) fl[i] = fenc[(int64_t)(i / w) * a.fs + i % w];
+    const int q = t & 15, r = t >> 4;
+    uint32_t bkey_hi = 0xffffffffu, bkey_lo = 0xffffffffu;   // (cost, raster index)
+    for (int ty0 = 0; ty0 < ncy; ty0 += kFsTy)
+        for (int tx0 = 0; tx0 < ncx; tx0 += kFsTx)
+        {
+            const int wr = min(kFsTy, ncy - ty0) + h - 1, wc = min(kFsTx, ncx - tx0) + w - 1;
+            const P* src = ref + (minx + tx0) + (int64_t)(miny + ty0) * a.rs;
+            __syncthreads();
+            for (int i = t; i < wr * wc; i += 256)
+            {
+                const int y = i / wc, x = i - y * wc;
+                wl[y * WS + x] = src[x + (int64_t)y * a.rs];
+            }
+            __syncthreads();
+            const int cy = ty0 + r, cx = tx0 + 4 * q;
+            if (cy >= ncy || cx >= ncx) continue;
+            uint32_t acc[4] = { 0, 0, 0, 0 };
+            if constexpr (sizeof(P) == 1)
+            {
+                for (int rr = 0; rr < h; rr++)
+                {
+                    const uint32_t* wp = win + ((r + rr) * WS + 4 * q) / 4;
+                    const uint32_t* fp = fen + rr * (w / 4);
+                    uint32_t d0 = wp[0];
+                    for (int c = 0; c < w / 4; c++)
+                    {
+                        const uint32_t d1 = wp[c + 1], f = fp[c];
+                        acc[0] = __builtin_amdgcn_sad_u8(f, d0, acc[0]);
+                        acc[1] = __builtin_amdgcn_sad_u8(f, __builtin_amdgcn_alignbyte(d1, d0, 1), acc[1]);
+                        acc[2] = __builtin_amdgcn_sad_u8(f, __builtin_amdgcn_alignbyte(d1, d0, 2), acc[2]);
+                        acc[3] = __builtin_amdgcn_sad_u8(f, __builtin_amdgcn_alignbyte(d1, d0, 3), acc[3]);
+                        d0 = d1;
+                    }
+                }
+            }
+            else
+            {
+                for (int rr = 0; rr < h; rr++)
+                {
+                    const uint32_t* wp = win + ((r + rr) * WS + 4 * q) / 2;
+                    const uint32_t* fp = fen + rr * (w / 2);
+                    uint32_t e0 = wp[0], e1 = wp[1];
+                    for (int c = 0; c < w / 4; c++)
+                    {
+                        const uint32_t e2 = wp[2 * c + 2], e3 = wp[2 * c + 3], f0 = fp[2 * c], f1 = fp[2 * c + 1];
+                        const uint32_t g1 = __builtin_amdgcn_alignbyte(e1, e0, 2), g2 = __builtin_amdgcn_alignbyte(e2, e1, 2);
+                        const uint32_t g3 = __builtin_amdgcn_alignbyte(e3, e2, 2);
+                        acc[0] = __builtin_amdgcn_sad_u16(f1, e1, __builtin_amdgcn_sad_u16(f0, e0, acc[0]));
+                        acc[1] = __builtin_amdgcn_sad_u16(f1, g2, __builtin_amdgcn_sad_u16(f0, g1, acc[1]));
+                        acc[2] = __builtin_amdgcn_sad_u16(f1, e2, __builtin_amdgcn_sad_u16(f0, e1, acc[2]));
+                        acc[3] = __builtin_amdgcn_sad_u16(f1, g3, __builtin_amdgcn_sad_u16(f0, g2, acc[3]));
+                        e0 = e2; e1 = e3;
+                    }
+                }
+            }
+            const int my = 4 * (miny + cy) - mvpy;
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+            {
+                if (cx + k >= ncx) break;
+                const uint32_t cost = acc[k] + (uint16_t)(tab[4 * (minx + cx + k) - mvpx] + tab[my]);
+                const uint32_t idx = (uint32_t)(cy * ncx + cx + k);
+                if (cost < bkey_hi || (cost == bkey_hi && idx < bkey_lo)) { bkey_hi = cost; bkey_lo = idx; }
+            }
+        }
+    // block argmin of (cost, index): wave shuffles, then the 4 waves through LDS
+    for (int m = 32; m > 0; m >>= 1)
+    {
+        const uint32_t oh = __shfl_xor(bkey_hi, m, 64), ol = __shfl_xor(bkey_lo, m, 64);
+        if (oh < bkey_hi || (oh == bkey_hi && ol < bkey_lo)) { bkey_hi = oh; bkey_lo = ol; }
+    }
+    if ((t & 63) == 0) { red[2 * (t >> 6)] = bkey_hi; red[2 * (t >> 6) + 1] = bkey_lo; }
+    __syncthreads();
+    if (t == 0)
+    {
+        for (int k = 1; k < 4; k++)
+            if (red[2 * k] < bkey_hi || (red[2 * k] == bkey_hi && red[2 * k + 1] < bkey_lo))
+            {
+                bkey_hi = red[2 * k]; bkey_lo = red[2 * k + 1];
+            }
+        if (bkey_hi == 0xffffffffu)
+            a.out_cost[j] = 0x7fffffff;                  // empty range: the predictors stand
+        else
+        {
+            a.out_mv[2 * j] = (int16_t)(minx + (int)(bkey_lo % (uint32_t)ncx));
+            a.out_mv[2 * j + 1] = (int16_t)(miny + (int)(bkey_lo / (uint32_t)ncx));
+            a.out_cost[j] = (int32_t)bkey_hi;
+        }
+    }
+}
+
 template <typename P>
 static int launch_me(const MeArgs& a, hipStream_t st)
 {
+    if (a.method == 4)
+        hipLaunchKernelGGL((k_full_search<P>), dim3(a.n), dim3(256), 0, st, a);
     const int G = 1 << a.lg;
     const uint32_t blocks = (uint32_t)((a.n + X265AMD_BLOCK / G - 1) / (X265AMD_BLOCK / G));
 #define L(g) case g: hipLaunchKernelGGL((k_motion_search<P, g>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, a); break;
@@ -859,7 +988,7 @@ extern "C" int x265amd_motion_search(int depth, int count, const x265amd_me_batc
     {
         const x265amd_me_batch& b = bt[i];
         if (b.n < 0 || b.w < 4 || b.h < 4 || b.w > 64 || b.h > 64 || (b.w & 3) || (b.h & 3)) return X265AMD_EINVAL;
-        if (b.method < 0 || b.method > 3 || b.subme < 0 || b.subme > 7 || b.merange < 1) return X265AMD_EINVAL;
+        if (b.method < 0 || b.method > 4 || b.subme < 0 || b.subme > 7 || b.merange < 1) return X265AMD_EINVAL;
         if (b.n && b.fenc_cb && (!b.fenc_cr || !b.fenc_coff || !b.ref_cb || !b.ref_cr || !b.ref_coff))
             return X265AMD_EINVAL;
         if (b.n && (!b.fenc || !b.fenc_off || !b.ref || !b.ref_off || !b.mv_range || !b.mvp || !b.mvcost ||

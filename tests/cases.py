@@ -579,10 +579,12 @@ def me_tables(depth: int) -> np.ndarray:
     return np.load(path).reshape(-1)
 
 
-def case_me(w: int, h: int, method: int, subme: int, merange: int, depth: int, n: int, seed: int) -> Case:
+def case_me(w: int, h: int, method: int, subme: int, merange: int, depth: int, n: int, seed: int,
+            box: int = 0) -> Case:
     """f2: n PUs of the synthetic sequence (frame 1 searched in frame 0; pan (+2, +1) px/frame, moving object,
     noise), both planes edge-padded by 96 px like PicYuv.  MVP = the true pan +- a few quarter-pels, 0..3 AMVP-like
-    candidates nearby, per-PU QP from ME_QPS, MV range = the picture + 24 px (the search stays inside the padding)."""
+    candidates nearby, per-PU QP from ME_QPS, MV range = the picture + 24 px (the search stays inside the padding);
+    box > 0 also limits it to the full-pel MVP +- box, as Search::setSearchRange does with merange."""
     import os
     import sys
 
@@ -604,6 +606,12 @@ def case_me(w: int, h: int, method: int, subme: int, merange: int, depth: int, n
     rng = np.array([[-int(x) - 24, -int(y) - 24, W - int(x) - w + 24, H - int(y) - h + 24] for x, y in zip(xs, ys)],
                    np.int16).reshape(-1)
     mvp = np.stack([-8 + det.ints(-6, 7, n), -4 + det.ints(-6, 7, n)], 1).astype(np.int16).reshape(-1)
+    if box:
+        r4 = rng.reshape(-1, 4).astype(np.int64)
+        fp = (mvp.reshape(-1, 2).astype(np.int64) + 2) >> 2
+        r4[:, :2] = np.maximum(r4[:, :2], fp - box)
+        r4[:, 2:] = np.minimum(r4[:, 2:], fp + box)
+        rng = r4.astype(np.int16).reshape(-1)
     max_cand = 3
     numc = det.ints(0, max_cand + 1, n).astype(np.uint8)
     mvc = det.ints(-48, 49, 2 * max_cand * n).astype(np.int16)
@@ -620,8 +628,10 @@ def case_me(w: int, h: int, method: int, subme: int, merange: int, depth: int, n
         fco = np.array([(int(y) // 2 + MC) * cst + int(x) // 2 + MC for x, y in zip(xs, ys)], np.int64)
         bufs.update(fcb=pad(fr1[1], MC), fcr=pad(fr1[2], MC), fcs=cst, fco=fco, rcb=pad(fr0[1], MC),
                     rcr=pad(fr0[2], MC), rcs=cst, rco=fco.copy())
-    return Case("me", dict(w=w, h=h, method=method, subme=subme, merange=merange, max_cand=max_cand, depth=depth,
-                           n=n, seed=seed), bufs, ["out_mv", "out_cost"])
+    prm = dict(w=w, h=h, method=method, subme=subme, merange=merange, max_cand=max_cand, depth=depth, n=n, seed=seed)
+    if box:
+        prm["box"] = box
+    return Case("me", prm, bufs, ["out_mv", "out_cost"])
 
 
 def me_cases(depth: int, n: int = 24):

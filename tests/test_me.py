@@ -26,6 +26,23 @@ def test_me_oracle_matches_reference(oracle_libs, depth):
                 assert np.array_equal(a[k], b[k]), (c.key(), k)
 
 
+def full_cases(depth, n=16):
+    """--me full (method 4) over MVP +- 16 (the exhaustive search is slow on the CPU), every luma PU shape,
+    subme 2 and (with chroma SATD) 3"""
+    return [case_me(w, h, 4, 2 + (i & 1), 16, depth, n, seed_of("me-full", depth, w, h), box=16)
+            for i, (w, h) in enumerate(LUMA_PU[1:])]
+
+
+@pytest.mark.skipif(not available("ref", 8), reason="reference library oracle/_ref not built")
+@pytest.mark.parametrize("depth", [8, 10])
+def test_me_full_oracle_matches_reference(oracle_libs, depth):
+    orc, ref = CpuOracle("oracle", depth), CpuOracle("ref", depth)
+    for c in full_cases(depth):
+        a, b = run_cpu(c, orc), run_cpu(c, ref)
+        for k in c.outs:
+            assert np.array_equal(a[k], b[k]), (c.key(), k)
+
+
 @pytest.mark.parametrize("depth", [8, 10])
 def test_me_cases_exercise_search(oracle_libs, depth):
     """results include quarter-pel, half-pel and full-pel MVs and MVs away from the MVP"""
@@ -46,6 +63,10 @@ def test_me_gpu_matches_oracle(gpu_prims, oracle_libs, depth):
     cases += [case_me(w, h, 3, 2, 57, depth, 48, seed_of("me-umh", depth, w, h)) for (w, h) in LUMA_PU[1:]]
     cases += [case_me(w, h, 3, s, 57, depth, 128, seed_of("me-umh-s", depth, w, h, s))
               for (w, h) in ((8, 8), (32, 32), (64, 64)) for s in (3, 5)]
+    # --me full (method 4): the exhaustive search kernel, then the lockstep refine
+    cases += full_cases(depth, 32)
+    cases += [case_me(w, h, 4, 2, 57, depth, 24, seed_of("me-full-g", depth, w, h), box=57)
+              for (w, h) in ((8, 8), (64, 64), (24, 32))]
     bad = []
     for c in cases:
         got, exp = run_gpu(c, gpu_prims), run_cpu(c, orc)

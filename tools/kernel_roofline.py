@@ -576,6 +576,37 @@ def main():
                  "note": f"{R} (current, reference) frame pairs of 1080p PUs in one launch"}
             results.append(r)
             print(json.dumps(r), flush=True)
+        # --me umh and --me full (subme 2) on the single-frame batch; FULL is the one data-parallel
+        # integer search: its unit of work is one pixel of one candidate (w h per MV, (2 merange + 1)^2
+        # MVs per PU when the range is not clipped), bounded by v_sad throughput, not HBM
+        for meth, tag, kcpu in ((3, "umh", 1000), (4, "full", max(2, 4096 // (s_ * s_) * 4))):
+            ms_x = timeit(lambda: prims.motion_search(8, s_, s_, meth, 2, 57, 2, F1, st, FO, F0, st, FO, RG, MP, MC2,
+                                                      NC, TB, TO, OM, OC))
+            r = {"kernel": f"me_{tag}_{s_}x{s_}", "jobs": n, "ms": round(ms_x, 4),
+                 "pu_per_s": round(n / (ms_x * 1e-3), 1)}
+            if meth == 4:
+                rg4 = rng_h.reshape(-1, 4).astype(np.int64)
+                pxc = float(((rg4[:, 2] - rg4[:, 0] + 1) * (rg4[:, 3] - rg4[:, 1] + 1)).sum() * s_ * s_)
+                r["pixel_candidates_per_s"] = round(pxc / (ms_x * 1e-3), 1)
+                r["bound"] = "valu (v_sad_u8: 4 pixel-candidates per lane op)"
+            try:
+                from pyoracle import CpuOracle, available
+                if available("ref", 8):
+                    import time as _t
+                    ref = CpuOracle("ref", 8)
+                    k = min(n, kcpu)
+                    om, oc = np.empty(2 * k, np.int16), np.empty(k, np.int32)
+                    t0 = _t.perf_counter()
+                    ref.motion_search(s_, s_, meth, 2, 57, 2, f1, st, fo_h[:k], f0, st, fo_h[:k], rng_h[:4 * k],
+                                      mvp_h[:2 * k], mvc_h[:4 * k], numc_h[:k], tabs, toff_h[:k],
+                                      np.full(k, 32, np.uint8), om, oc)
+                    r["cpu_reference_1core_pu_per_s"] = round(k / (_t.perf_counter() - t0), 2)
+                    r["gpu_matches_reference_on_sample"] = bool(np.array_equal(om, OM[:2 * k].cpu().numpy()) and
+                                                                np.array_equal(oc, OC[:k].cpu().numpy()))
+            except Exception as ex:
+                r["cpu_reference_error"] = str(ex)
+            results.append(r)
+            print(json.dumps(r), flush=True)
     # ---------------------------------------------------------------- f4 loop filters
     # Whole frames, >= --gb of distinct frame buffers per call (8 frames per launch).  Algorithmic
     # bytes per frame: deblock = the picture read once and written once + its 16-byte CU units
