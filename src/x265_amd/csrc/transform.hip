@@ -15,6 +15,8 @@
 // job per N-lane group, lane r owning row r (forward) or column r (inverse)
 // in stage 1, with the int16 intermediate staged through LDS (row pitch N+2
 // to spread banks) for stage 2.
+#include <stdlib.h>
+
 #include "common.h"
 #include "transform1d.h"
 #include "../../../include/x265_amd.h"
@@ -393,9 +395,85 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_tr16_mfma(int n, int depth,
 }
 
 // --------------------------------------------------------------- quant family
-// one job per G-lane group (G = num/8, at most 64); a lane handles 8
-// coefficients per iteration
-template <bool NQUANT>
+// A job's chunks of CW coefficients (CW = 4 or 8) go to a group of
+// G = min(64, num / CW) lanes; each lane carries CPJ chunks of each of JPG jobs.
+// Step k of a block covers jobs block0 + k NG + g (NG groups per block), chunk
+// c = lane + i G, so every wave-instruction reads / writes contiguous bytes of
+// consecutive jobs, and all loads of a lane are issued before the first chunk is
+// quantized.  (CW, JPG) per size class were set by measurement
+// (tools/coef_tune.sh; X265AMD_COEF_CW / X265AMD_COEF_JPG override them).
+template <int CPJ, int JPG>
+struct CoefMap
+{
+    int G, NG, g, lane, nch;
+    int64_t job[JPG];
+    bool live[JPG];
+    __device__ __forceinline__ CoefMap(int n, int num, int lg, int cw)
+    {
+        G = 1 << lg;
+        NG = X265AMD_BLOCK >> lg;
+        g = threadIdx.x >> lg;
+        lane = threadIdx.x & (G - 1);
+        nch = num / cw;
+        const int64_t b0 = (int64_t)xcd_block() * NG * JPG;
+#pragma unroll
+        for (int k = 0; k < JPG; k++)
+        {
+            const int64_t j = b0 + (int64_t)k * NG + g;
+            live[k] = j < n;
+            job[k] = live[k] ? j : 0;
+        }
+    }
+    // chunk index of slot i of job slot k (-1: none)
+    __device__ __forceinline__ int chunk(int k, int i, int c0) const
+    {
+        const int c = c0 + i * G;
+        return live[k] && c < nch ? c : -1;
+    }
+};
+
+// CW int16 / int32 values as packed words
+template <int CW>
+struct Chunk16 { uint32_t w[CW / 2]; };
+template <int CW>
+struct Chunk32 { int w[CW]; };
+
+template <int CW>
+__device__ __forceinline__ Chunk16<CW> ld16(const int16_t* p)
+{
+    Chunk16<CW> c;
+    if constexpr (CW == 8) { const uint4 v = ldu<uint4>(p); c.w[0] = v.x; c.w[1] = v.y; c.w[2] = v.z; c.w[3] = v.w; }
+    else { const uint2 v = ldu<uint2>(p); c.w[0] = v.x; c.w[1] = v.y; }
+    return c;
+}
+template <int CW>
+__device__ __forceinline__ Chunk32<CW> ld32(const int32_t* p)
+{
+    Chunk32<CW> c;
+#pragma unroll
+    for (int q = 0; q < CW / 4; q++)
+    {
+        const int4 v = ldu<int4>(p + 4 * q);
+        c.w[4 * q] = v.x; c.w[4 * q + 1] = v.y; c.w[4 * q + 2] = v.z; c.w[4 * q + 3] = v.w;
+    }
+    return c;
+}
+template <int CW>
+__device__ __forceinline__ void st16(int16_t* p, const int (&o)[CW])
+{
+    uint32_t w[CW / 2];
+#pragma unroll
+    for (int e = 0; e < CW / 2; e++) w[e] = (uint32_t)(o[2 * e] & 0xffff) | ((uint32_t)o[2 * e + 1] << 16);
+    if constexpr (CW == 8) stu<uint4>(p, make_uint4(w[0], w[1], w[2], w[3]));
+    else stu<uint2>(p, make_uint2(w[0], w[1]));
+}
+template <int CW>
+__device__ __forceinline__ int c16(const Chunk16<CW>& c, int e)
+{
+    return (int16_t)(e & 1 ? c.w[e >> 1] >> 16 : c.w[e >> 1] & 0xffff);
+}
+
+template <bool NQUANT, int CW, int CPJ, int JPG>
 __global__ __launch_bounds__(X265AMD_BLOCK) void k_quant(int n, int num, int lg,
     const int16_t* __restrict__ coef, const int64_t* __restrict__ coff,
     const int32_t* __restrict__ qtab, const int64_t* __restrict__ qoff,
@@ -403,99 +481,157 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_quant(int n, int num, int lg,
     int16_t* __restrict__ qout, const int64_t* __restrict__ ooff,
     const int32_t* __restrict__ qbits, const int32_t* __restrict__ add, uint32_t* __restrict__ numsig)
 {
-    const int G = 1 << lg;
-    const int64_t job0 = (int64_t)xcd_block() * (X265AMD_BLOCK >> lg) + (threadIdx.x >> lg);
-    const int lane = threadIdx.x & (G - 1);
-    const bool live = job0 < n;
-    const int64_t job = live ? job0 : 0;
-    const int16_t* pc = coef + coff[job];
-    const int32_t* pq = qtab + qoff[job];
-    int16_t* po = qout + ooff[job];
-    int32_t* pdl = NQUANT ? nullptr : delta + doff[job];
-    const int qb = qbits[job], ad = add[job], qb8 = qb - 8;
-    uint32_t sig = 0;
-    for (int i = lane * 8; live && i < num; i += G * 8)
-    {
-        int c[8], o[8];
-        load_row16<8>(pc + i, c);
-        const int4 q0 = ldu<int4>(pq + i), q1 = ldu<int4>(pq + i + 4);
-        const int qv[8] = { q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w };
-        int dl[8];
+    const CoefMap<CPJ, JPG> m(n, num, lg, CW);
+    const int16_t* pc[JPG];
+    const int32_t* pq[JPG];
+    int16_t* po[JPG];
+    int32_t* pdl[JPG];
+    int qb[JPG], ad[JPG];
+    uint32_t sig[JPG];
 #pragma unroll
-        for (int k = 0; k < 8; k++)
-        {
-            const int lv = c[k];
-            // int32 products/sums wrap exactly as the reference's int arithmetic (dct.cpp:676-678)
-            const uint32_t tmp = (uint32_t)abs(lv) * (uint32_t)qv[k];
-            int level = (int)(tmp + (uint32_t)ad) >> qb;
-            dl[k] = (int)(tmp - ((uint32_t)level << qb)) >> qb8;
-            sig += level != 0;
-            if (lv < 0) level = -level;
-            level = clip16(level);
-            o[k] = NQUANT ? abs(level) : level;
-        }
-        store_row<int16_t, 8>(po + i, o);
-        if (!NQUANT)
-        {
-            stu<int4>(pdl + i, make_int4(dl[0], dl[1], dl[2], dl[3]));
-            stu<int4>(pdl + i + 4, make_int4(dl[4], dl[5], dl[6], dl[7]));
-        }
+    for (int k = 0; k < JPG; k++)
+    {
+        pc[k] = coef + coff[m.job[k]];
+        pq[k] = qtab + qoff[m.job[k]];
+        po[k] = qout + ooff[m.job[k]];
+        pdl[k] = NQUANT ? nullptr : delta + doff[m.job[k]];
+        qb[k] = qbits[m.job[k]];
+        ad[k] = add[m.job[k]];
+        sig[k] = 0;
     }
-    for (int m = G >> 1; m > 0; m >>= 1) sig += __shfl_xor(sig, m, 64);
-    if (live && lane == 0) numsig[job] = sig;
+    for (int c0 = m.lane; c0 < m.nch; c0 += CPJ * m.G)
+    {
+        Chunk16<CW> cv[JPG][CPJ];
+        Chunk32<CW> qv[JPG][CPJ];
+#pragma unroll
+        for (int k = 0; k < JPG; k++)
+#pragma unroll
+            for (int i = 0; i < CPJ; i++)
+            {
+                const int c = m.chunk(k, i, c0);
+                if (c < 0) continue;
+                cv[k][i] = ld16<CW>(pc[k] + CW * c);
+                qv[k][i] = ld32<CW>(pq[k] + CW * c);
+            }
+#pragma unroll
+        for (int k = 0; k < JPG; k++)
+#pragma unroll
+            for (int i = 0; i < CPJ; i++)
+            {
+                const int c = m.chunk(k, i, c0);
+                if (c < 0) continue;
+                int o[CW], dl[CW];
+#pragma unroll
+                for (int e = 0; e < CW; e++)
+                {
+                    const int lv = c16<CW>(cv[k][i], e);
+                    // int32 products/sums wrap exactly as the reference's int arithmetic (dct.cpp:676-678)
+                    const uint32_t tmp = (uint32_t)abs(lv) * (uint32_t)qv[k][i].w[e];
+                    int level = (int)(tmp + (uint32_t)ad[k]) >> qb[k];
+                    dl[e] = (int)(tmp - ((uint32_t)level << qb[k])) >> (qb[k] - 8);
+                    sig[k] += level != 0;
+                    if (lv < 0) level = -level;
+                    level = clip16(level);
+                    o[e] = NQUANT ? abs(level) : level;
+                }
+                st16<CW>(po[k] + CW * c, o);
+                if (!NQUANT)
+                {
+#pragma unroll
+                    for (int q = 0; q < CW / 4; q++)
+                        stu<int4>(pdl[k] + CW * c + 4 * q, make_int4(dl[4 * q], dl[4 * q + 1], dl[4 * q + 2], dl[4 * q + 3]));
+                }
+            }
+    }
+#pragma unroll
+    for (int k = 0; k < JPG; k++)
+    {
+        uint32_t v = sig[k];
+        for (int mm = m.G >> 1; mm > 0; mm >>= 1) v += __shfl_xor(v, mm, 64);
+        if (m.live[k] && m.lane == 0) numsig[m.job[k]] = v;
+    }
 }
 
-template <bool SCALING>
+template <bool SCALING, int CW, int CPJ, int JPG>
 __global__ __launch_bounds__(X265AMD_BLOCK) void k_dequant(int n, int num, int lg,
     const int16_t* __restrict__ q, const int64_t* __restrict__ qoff,
     const int32_t* __restrict__ dq, const int64_t* __restrict__ dqoff,
     int16_t* __restrict__ out, const int64_t* __restrict__ ooff,
     const int32_t* __restrict__ p0, const int32_t* __restrict__ p1)
 {
-    const int G = 1 << lg;
-    const int64_t job = (int64_t)xcd_block() * (X265AMD_BLOCK >> lg) + (threadIdx.x >> lg);
-    const int lane = threadIdx.x & (G - 1);
-    if (job >= n) return;
-    const int16_t* pq = q + qoff[job];
-    int16_t* po = out + ooff[job];
-    for (int i = lane * 8; i < num; i += G * 8)
+    // the chunk / job mapping of k_quant
+    const CoefMap<CPJ, JPG> m(n, num, lg, CW);
+    const int16_t* pq[JPG];
+    const int32_t* pd[JPG];
+    int16_t* po[JPG];
+    int a0[JPG], a1[JPG];
+#pragma unroll
+    for (int k = 0; k < JPG; k++)
     {
-        int v[8], o[8];
-        load_row16<8>(pq + i, v);
-        if (!SCALING)
-        {
-            const int scale = p0[job], shift = p1[job], ad = 1 << (shift - 1);
+        pq[k] = q + qoff[m.job[k]];
+        pd[k] = SCALING ? dq + dqoff[m.job[k]] : nullptr;
+        po[k] = out + ooff[m.job[k]];
+        a0[k] = p0[m.job[k]];
+        a1[k] = p1[m.job[k]];
+    }
+    for (int c0 = m.lane; c0 < m.nch; c0 += CPJ * m.G)
+    {
+        Chunk16<CW> v[JPG][CPJ];
+        Chunk32<CW> d[JPG][CPJ];
 #pragma unroll
-            for (int k = 0; k < 8; k++) o[k] = clip16((v[k] * scale + ad) >> shift);
-        }
-        else
-        {
-            const int per = p0[job], shift = p1[job] + 4;
-            const int32_t* pd = dq + dqoff[job] + i;
-            const int4 d0 = ldu<int4>(pd), d1 = ldu<int4>(pd + 4);
-            const int dv[8] = { d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w };
-            if (shift > per)
+        for (int k = 0; k < JPG; k++)
+#pragma unroll
+            for (int i = 0; i < CPJ; i++)
             {
-                const int ad = 1 << (shift - per - 1);
-#pragma unroll
-                for (int k = 0; k < 8; k++) o[k] = clip16((v[k] * dv[k] + ad) >> (shift - per));
+                const int c = m.chunk(k, i, c0);
+                if (c < 0) continue;
+                v[k][i] = ld16<CW>(pq[k] + CW * c);
+                if (SCALING) d[k][i] = ld32<CW>(pd[k] + CW * c);
             }
-            else
+#pragma unroll
+        for (int k = 0; k < JPG; k++)
+#pragma unroll
+            for (int i = 0; i < CPJ; i++)
             {
+                const int c = m.chunk(k, i, c0);
+                if (c < 0) continue;
+                int o[CW];
+                if (!SCALING)
+                {
+                    const int scale = a0[k], shift = a1[k], ad = 1 << (shift - 1);
 #pragma unroll
-                for (int k = 0; k < 8; k++) o[k] = clip16(clip16(v[k] * dv[k]) << (per - shift));
+                    for (int e = 0; e < CW; e++) o[e] = clip16((c16<CW>(v[k][i], e) * scale + ad) >> shift);
+                }
+                else
+                {
+                    const int per = a0[k], shift = a1[k] + 4;
+                    if (shift > per)
+                    {
+                        const int ad = 1 << (shift - per - 1);
+#pragma unroll
+                        for (int e = 0; e < CW; e++)
+                            o[e] = clip16((c16<CW>(v[k][i], e) * d[k][i].w[e] + ad) >> (shift - per));
+                    }
+                    else
+                    {
+#pragma unroll
+                        for (int e = 0; e < CW; e++)
+                            o[e] = clip16(clip16(c16<CW>(v[k][i], e) * d[k][i].w[e]) << (per - shift));
+                    }
+                }
+                st16<CW>(po[k] + CW * c, o);
             }
-        }
-        store_row<int16_t, 8>(po + i, o);
     }
 }
 
-// count_nonzero (res == nullptr) / copy_cnt
+// count_nonzero (res == nullptr) / copy_cnt: CW coefficients per lane per step
+// (8 from 8x8 up: one 16-byte load / store, the shape the quant family measured best)
 template <int N>
 __global__ __launch_bounds__(X265AMD_BLOCK) void k_count(int n, int16_t* __restrict__ coeff, const int64_t* __restrict__ coff,
     const int16_t* __restrict__ res, intptr_t rs, const int64_t* __restrict__ roff, uint32_t* __restrict__ cnt)
 {
-    constexpr int G = N * N / 4 < 64 ? N * N / 4 : 64;   // 4 coefficients per lane per step
+    constexpr int CW = N >= 8 ? 8 : 4;
+    constexpr int G = N * N / CW < 64 ? N * N / CW : 64;
     const int64_t job = (int64_t)xcd_block() * (X265AMD_BLOCK / G) + threadIdx.x / G;
     const int lane = threadIdx.x & (G - 1);
     const bool live = job < n;
@@ -503,18 +639,25 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_count(int n, int16_t* __restr
     if (live)
     {
         int16_t* pc = coeff + coff[job];
-        for (int i = lane * 4; i < N * N; i += G * 4)
+        const int16_t* pr = res ? res + roff[job] : nullptr;
+        for (int i = lane * CW; i < N * N; i += G * CW)
         {
-            int v[4];
-            if (res)
+            uint32_t w[CW / 2];
+            const int16_t* src = res ? pr + (i / N) * rs + i % N : pc + i;
+            if constexpr (CW == 8)
             {
-                const int y = i / N, x = i % N;
-                load_row16<4>(res + roff[job] + y * rs + x, v);
-                store_row<int16_t, 4>(pc + i, v);
+                const uint4 v = ldu<uint4>(src);
+                w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+                if (res) stu<uint4>(pc + i, v);
             }
             else
-                load_row16<4>(pc + i, v);
-            c += (v[0] != 0) + (v[1] != 0) + (v[2] != 0) + (v[3] != 0);
+            {
+                const uint2 v = ldu<uint2>(src);
+                w[0] = v.x; w[1] = v.y;
+                if (res) stu<uint2>(pc + i, v);
+            }
+#pragma unroll
+            for (int e = 0; e < CW / 2; e++) c += ((w[e] & 0xffffu) != 0) + ((w[e] >> 16) != 0);
         }
     }
     for (int m = G >> 1; m > 0; m >>= 1) c += __shfl_xor(c, m, 64);
@@ -569,14 +712,54 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_denoise(int n, int num, int16
     }
 }
 
-// lanes per coefficient job: 8 coefficients per lane, at most one wavefront
-static inline int coef_lanes_log2(int num)
+// chunk width / jobs per lane group of the coefficient kernels (measured,
+// tools/coef_tune.sh); X265AMD_COEF_CW = 4 | 8 and
+// X265AMD_COEF_JPG = 1 | 2 | 4 override them for tuning runs
+struct CoefShape
 {
-    int g = num / 8, lg = 0;
-    if (g > 64) g = 64;
+    int cw, jpg, cpj, lg;
+};
+static CoefShape coef_shape(int num, bool quant)
+{
+    static int cw_env = -1, jpg_env = -1;
+    if (cw_env < 0)
+    {
+        const char* e = getenv("X265AMD_COEF_CW");
+        cw_env = e ? atoi(e) : 0;
+        e = getenv("X265AMD_COEF_JPG");
+        jpg_env = e ? atoi(e) : 0;
+    }
+    CoefShape c;
+    // measured (profiles/r02/coef_tune.txt): 8-coefficient chunks of one job per lane, except
+    // quant 32x32 which prefers four 4-coefficient chunks per lane (0.55 -> 0.61 of HBM peak)
+    c.cw = cw_env == 4 || cw_env == 8 ? cw_env : (quant && num > 256 ? 4 : 8);
+    if (num % (c.cw * 2)) c.cw = 4;         // num = 8 (dequant only) or odd multiples
+    const int nch = num / c.cw;
+    int g = nch > 64 ? 64 : nch, lg = 0;
     while ((1 << lg) < g) lg++;
-    return lg;
+    c.lg = lg;
+    c.cpj = nch > 64 ? (nch + 63) / 64 : 1;
+    if (c.cpj > 1) c.cpj = c.cw == 8 ? 2 : 4;
+    c.jpg = c.cpj > 1 ? 1 : (jpg_env == 1 || jpg_env == 2 || jpg_env == 4 ? jpg_env : 1);
+    return c;
 }
+
+// dispatch (CW, CPJ, JPG) to a kernel instantiation: CW 4 / 8, CPJ 1 with JPG 1 / 2 / 4, or
+// the 32x32 shapes (CW 8, CPJ 2) / (CW 4, CPJ 4)
+#define X265AMD_COEF_DISPATCH(c, LAUNCH)                                                              \
+    do                                                                                                \
+    {                                                                                                 \
+        if (c.cw == 8)                                                                                \
+        {                                                                                             \
+            if (c.cpj > 1) LAUNCH(8, 2, 1); else if (c.jpg == 1) LAUNCH(8, 1, 1);                     \
+            else if (c.jpg == 2) LAUNCH(8, 1, 2); else LAUNCH(8, 1, 4);                               \
+        }                                                                                             \
+        else                                                                                          \
+        {                                                                                             \
+            if (c.cpj > 1) LAUNCH(4, 4, 1); else if (c.jpg == 1) LAUNCH(4, 1, 1);                     \
+            else if (c.jpg == 2) LAUNCH(4, 1, 2); else LAUNCH(4, 1, 4);                               \
+        }                                                                                             \
+    } while (0)
 
 } // namespace x265amd
 
@@ -641,15 +824,20 @@ extern "C" int x265amd_quant(int n, int num, const int16_t* coef, const int64_t*
 {
     if (n <= 0) return 0;
     if (num <= 0 || num % 16 || num > 1024) return X265AMD_EINVAL;
-    const int lg = coef_lanes_log2(num);
-    const dim3 grid((n + (X265AMD_BLOCK >> lg) - 1) / (X265AMD_BLOCK >> lg));
+    const CoefShape c = coef_shape(num, true);
+    const int per_block = (X265AMD_BLOCK >> c.lg) * c.jpg;
+    const dim3 grid((n + per_block - 1) / per_block);
     hipStream_t st = (hipStream_t)stream;
-    if (delta_u)
-        hipLaunchKernelGGL(k_quant<false>, grid, dim3(X265AMD_BLOCK), 0, st, n, num, lg, coef, coef_off, qtab, qtab_off,
-                           delta_u, delta_off, qcoef, qcoef_off, qbits, add, num_sig);
-    else
-        hipLaunchKernelGGL(k_quant<true>, grid, dim3(X265AMD_BLOCK), 0, st, n, num, lg, coef, coef_off, qtab, qtab_off,
-                           delta_u, delta_off, qcoef, qcoef_off, qbits, add, num_sig);
+    const int lg = c.lg;
+#define Q(NQ, CW, C, J) hipLaunchKernelGGL((k_quant<NQ, CW, C, J>), grid, dim3(X265AMD_BLOCK), 0, st, n, num, lg, coef, \
+                                           coef_off, qtab, qtab_off, delta_u, delta_off, qcoef, qcoef_off, qbits, add, num_sig)
+#define QF(CW, C, J) Q(false, CW, C, J)
+#define QT(CW, C, J) Q(true, CW, C, J)
+    if (delta_u) X265AMD_COEF_DISPATCH(c, QF);
+    else X265AMD_COEF_DISPATCH(c, QT);
+#undef QT
+#undef QF
+#undef Q
     return (int)hipGetLastError();
 }
 
@@ -659,10 +847,14 @@ extern "C" int x265amd_dequant_normal(int n, int num, const int16_t* q, const in
 {
     if (n <= 0) return 0;
     if (num <= 0 || num % 8 || num > 1024) return X265AMD_EINVAL;
-    const int lg = coef_lanes_log2(num);
-    hipLaunchKernelGGL(k_dequant<false>, dim3((n + (X265AMD_BLOCK >> lg) - 1) / (X265AMD_BLOCK >> lg)),
-                       dim3(X265AMD_BLOCK), 0, (hipStream_t)stream, n, num, lg, q, q_off,
-                       (const int32_t*)nullptr, (const int64_t*)nullptr, coef, coef_off, scale, shift);
+    const CoefShape c = coef_shape(num, false);
+    const int per_block = (X265AMD_BLOCK >> c.lg) * c.jpg;
+    const dim3 grid((n + per_block - 1) / per_block);
+    const int lg = c.lg;
+#define D(CW, C, J) hipLaunchKernelGGL((k_dequant<false, CW, C, J>), grid, dim3(X265AMD_BLOCK), 0, (hipStream_t)stream, n, \
+                                       num, lg, q, q_off, (const int32_t*)nullptr, (const int64_t*)nullptr, coef, coef_off, scale, shift)
+    X265AMD_COEF_DISPATCH(c, D);
+#undef D
     return (int)hipGetLastError();
 }
 
@@ -673,10 +865,14 @@ extern "C" int x265amd_dequant_scaling(int n, int num, const int16_t* q, const i
 {
     if (n <= 0) return 0;
     if (num <= 0 || num % 8 || num > 1024) return X265AMD_EINVAL;
-    const int lg = coef_lanes_log2(num);
-    hipLaunchKernelGGL(k_dequant<true>, dim3((n + (X265AMD_BLOCK >> lg) - 1) / (X265AMD_BLOCK >> lg)),
-                       dim3(X265AMD_BLOCK), 0, (hipStream_t)stream, n, num, lg, q, q_off,
-                       dq, dq_off, coef, coef_off, per, shift);
+    const CoefShape c = coef_shape(num, false);
+    const int per_block = (X265AMD_BLOCK >> c.lg) * c.jpg;
+    const dim3 grid((n + per_block - 1) / per_block);
+    const int lg = c.lg;
+#define D(CW, C, J) hipLaunchKernelGGL((k_dequant<true, CW, C, J>), grid, dim3(X265AMD_BLOCK), 0, (hipStream_t)stream, n, \
+                                       num, lg, q, q_off, dq, dq_off, coef, coef_off, per, shift)
+    X265AMD_COEF_DISPATCH(c, D);
+#undef D
     return (int)hipGetLastError();
 }
 
@@ -698,7 +894,7 @@ extern "C" int x265amd_count_nonzero(int size, int n, int16_t* coeff, const int6
     hipStream_t st = (hipStream_t)stream;
 #define C(N)                                                                                          \
     {                                                                                                 \
-        constexpr int G = N * N / 4 < 64 ? N * N / 4 : 64;                                            \
+        constexpr int CW = N >= 8 ? 8 : 4, G = N * N / CW < 64 ? N * N / CW : 64;                     \
         const int per = X265AMD_BLOCK / G;                                                            \
         hipLaunchKernelGGL(k_count<N>, dim3((n + per - 1) / per), dim3(X265AMD_BLOCK), 0, st, n, coeff, \
                            coeff_off, res, res_stride, res_off, count);                               \

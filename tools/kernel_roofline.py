@@ -71,10 +71,14 @@ def main():
         torch.cuda.synchronize()
         return sum(x.elapsed_time(y) for x, y in evs) / len(evs)
 
-    def record(name, nbytes, ms, n):
+    def record(name, nbytes, ms, n, desc=0):
         gbs = nbytes / (ms * 1e-3) / 1e9
         r = {"kernel": name, "jobs": n, "bytes_per_launch": int(nbytes), "ms": round(ms, 4),
              "achieved_GBps": round(gbs, 1), "frac_of_8TBps": round(gbs / HBM, 3)}
+        if desc:
+            # the C ABI's per-job descriptors (int64 offsets, per-job scalars) the kernel must also read
+            r["descriptor_bytes_per_job"] = desc
+            r["frac_incl_descriptors"] = round((nbytes + desc * n) / (ms * 1e-3) / 1e9 / HBM, 3)
         results.append(r)
         print(json.dumps(r), flush=True)
 
@@ -98,7 +102,7 @@ def main():
             wide = op == SSE_PP
             out = torch.empty(n, dtype=torch.int64 if wide else torch.int32, device=dev)
             ms = timeit(lambda: prims.pixelcmp(op, 8, s, s, A, W, off, B, W, off, out))
-            record(name, n * (2 * s * s + (8 if wide else 4)), ms, n)
+            record(name, n * (2 * s * s + (8 if wide else 4)), ms, n, desc=16)
             del A, B, off, out
     # ---------------------------------------------------------------- sad_x4
     for s in (8, 16, 64):
@@ -114,7 +118,7 @@ def main():
         roff = torch.from_numpy(y4 * W + x4).to(dev)
         out = torch.empty(4 * n, dtype=torch.int32, device=dev)
         ms = timeit(lambda: prims.sad_multi(4, 8, s, s, F, W, foff, R, W, roff, out))
-        record(name, n * (5 * s * s + 16), ms, n)
+        record(name, n * (5 * s * s + 16), ms, n, desc=40)
         del F, R, foff, roff, out
     # ---------------------------------------------------------------- luma interp
     for op, opname in ((HPP, "luma_hpp"), (VPP, "luma_vpp"), (HVPP, "luma_hvpp")):
@@ -134,7 +138,7 @@ def main():
             if op == HVPP:
                 coeff = coeff | (torch.randint(1, 4, (n,), dtype=torch.uint8, device=dev) << 4)
             ms = timeit(lambda: prims.interp(op, 8, 8, s, s, S, W, soff, D, s, doff, coeff))
-            record(name, n * ((s + ext_w) * (s + ext_h) + s * s), ms, n)
+            record(name, n * ((s + ext_w) * (s + ext_h) + s * s), ms, n, desc=17)
             del S, soff, D, doff, coeff
     # ---------------------------------------------------------------- block ops
     # sources tiled in planes (as frame blocks), destinations in compact slots
@@ -161,7 +165,7 @@ def main():
             D = torch.empty(n * s * s, dtype=torch.int16 if d16 else torch.uint8, device=dev)
             doff = torch.arange(n, dtype=torch.int64, device=dev) * (s * s)
             ms = timeit(lambda: prims.blockop(op, 8, s, s, D, s, doff, A, W, off, B, W, off if B is not None else None))
-            record(name, n * (esz_a + esz_b + esz_d) * s * s, ms, n)
+            record(name, n * (esz_a + esz_b + esz_d) * s * s, ms, n, desc=16 if B is None else 24)
             del A, B, D, off, doff
     # ---------------------------------------------------------------- transforms
     for kind, kname in ((DCT, "dct"), (IDCT, "idct")):
@@ -174,7 +178,7 @@ def main():
             Dr = torch.empty(n * s * s, dtype=torch.int16, device=dev)
             offs = torch.arange(n, dtype=torch.int64, device=dev) * (s * s)
             ms = timeit(lambda: prims.transform(kind, 8, s, Sr, s, offs, Dr, s, offs))
-            record(name, n * 4 * s * s, ms, n)
+            record(name, n * 4 * s * s, ms, n, desc=16)
             if s >= 16:
                 # matrix-core path (csrc/transform.hip k_tr16/32_mfma): two stages, each an
                 # N x N x N product issued twice (hi / lo f16 halves of every int16 operand)
@@ -200,7 +204,21 @@ def main():
         ad = torch.full((n,), 85 << 11, dtype=torch.int32, device=dev)
         sig = torch.empty(n, dtype=torch.int32, device=dev)
         ms = timeit(lambda: prims.quant(num, C, offs, Q, qo, DL, offs, O, offs, qb, ad, sig))
-        record(name, n * (8 * num + 4), ms, n)
+        record(name, n * (8 * num + 4), ms, n, desc=40)
+        if want(f"copy_cnt_{s}x{s}"):
+            # copy_cnt: the residual block (in a plane) -> compact coefficients + count
+            x, y, rows = tiled_offsets(n, s, s, s, s, W)
+            R = torch.randint(-3, 4, (rows * W,), dtype=torch.int16, device=dev)
+            roff = torch.from_numpy(y * W + x).to(dev)
+            ms = timeit(lambda: prims.count_nonzero(s, O, offs, R, W, roff, sig))
+            record(f"copy_cnt_{s}x{s}", n * (4 * num + 4), ms, n, desc=16)
+            del R, roff
+        if want(f"dequant_{s}x{s}"):
+            dsc = torch.full((n,), 40 * 4, dtype=torch.int32, device=dev)
+            dsh = torch.full((n,), 3, dtype=torch.int32, device=dev)
+            ms = timeit(lambda: prims.dequant_normal(num, C, offs, O, offs, dsc, dsh))
+            record(f"dequant_{s}x{s}", n * 4 * num, ms, n, desc=24)
+            del dsc, dsh
         del C, offs, qo, DL, O, qb, ad, sig
     # ---------------------------------------------------------------- intra
     for s in (4, 8, 16, 32):
@@ -216,7 +234,7 @@ def main():
         mode = torch.from_numpy(np.sort(np.random.default_rng(1).integers(2, 35, n)).astype(np.uint8)).to(dev)
         bf = torch.ones(n, dtype=torch.uint8, device=dev)
         ms = timeit(lambda: prims.intra_pred(8, s, D, s, doff, NB, nbo, mode, bf))
-        record(name, n * (m + s * s), ms, n)
+        record(name, n * (m + s * s), ms, n, desc=18)
         del NB, nbo, D, doff, mode, bf
     # ---------------------------------------------------------------- f3 fused TU pipeline
     # TUs tiled through disjoint fenc / pred / recon / residual planes; pred = fenc + noise in
