@@ -14,7 +14,8 @@
 // Work mapping: N = 4 transforms run one job per lane; N = 8/16/32 run one
 // job per N-lane group, lane r owning row r (forward) or column r (inverse)
 // in stage 1, with the int16 intermediate staged through LDS (row pitch N+2
-// to spread banks) for stage 2.
+// to spread banks) for stage 2; global memory is only touched by rows (16-byte
+// loads / stores), the column sides of both directions go through LDS.
 #include <stdlib.h>
 
 #include "common.h"
@@ -24,16 +25,15 @@
 namespace x265amd {
 
 // --------------------------------------------------------------- 4x4: lane per job
+// Each lane takes kTr4Jobs jobs (jobs b + k * 256 + t: every wave-instruction still
+// covers consecutive jobs) and issues the descriptor and block loads of all of them
+// before the first transform, so one dependent offset -> block round trip serves
+// several jobs.
+constexpr int kTr4Jobs = 2;
+
 template <int KIND>
-__global__ __launch_bounds__(X265AMD_BLOCK) void k_tr4(int n, int depth,
-    const int16_t* __restrict__ src, intptr_t ss, const int64_t* __restrict__ soff,
-    int16_t* __restrict__ dst, intptr_t ds, const int64_t* __restrict__ doff)
+__device__ __forceinline__ void tr4_load(const int16_t* ps, intptr_t ss, int (&m)[4][4])
 {
-    const int64_t job = (int64_t)xcd_block() * X265AMD_BLOCK + threadIdx.x;
-    if (job >= n) return;
-    const int16_t* ps = src + soff[job];
-    int16_t* pd = dst + doff[job];
-    int m[4][4], t[4][4];
     if (ss == 4)
     {
         // compact block (coefficients, compact residuals): 32 contiguous bytes, two 16-byte loads
@@ -53,6 +53,12 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_tr4(int n, int depth,
             for (int c = 0; c < 4; c++) m[r][c] = v[c];
         }
     }
+}
+
+template <int KIND>
+__device__ __forceinline__ void tr4_apply(int depth, int (&m)[4][4])
+{
+    int t[4][4];
     const bool fwd = KIND == X265AMD_DCT || KIND == X265AMD_DST;
     const int sh1 = fwd ? 1 + depth - 8 : 7, sh2 = fwd ? 8 : 12 - (depth - 8);
     if (fwd)
@@ -95,6 +101,10 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_tr4(int n, int depth,
             for (int k = 0; k < 4; k++) m[j][k] = inv_round(y[k], sh2);
         }
     }
+}
+
+__device__ __forceinline__ void tr4_store(int16_t* pd, intptr_t ds, const int (&m)[4][4])
+{
     if (ds == 4)
     {
         uint32_t w[8];
@@ -110,6 +120,34 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_tr4(int n, int depth,
     {
         int v[4] = { m[r][0], m[r][1], m[r][2], m[r][3] };
         store_row<int16_t, 4>(pd + r * ds, v);
+    }
+}
+
+template <int KIND>
+__global__ __launch_bounds__(X265AMD_BLOCK) void k_tr4(int n, int depth,
+    const int16_t* __restrict__ src, intptr_t ss, const int64_t* __restrict__ soff,
+    int16_t* __restrict__ dst, intptr_t ds, const int64_t* __restrict__ doff)
+{
+    const int64_t b = (int64_t)xcd_block() * X265AMD_BLOCK * kTr4Jobs + threadIdx.x;
+    int m[kTr4Jobs][4][4];
+    int64_t dof[kTr4Jobs];
+#pragma unroll
+    for (int k = 0; k < kTr4Jobs; k++)
+    {
+        const int64_t job = b + (int64_t)k * X265AMD_BLOCK;
+        if (job < n)
+        {
+            dof[k] = doff[job];
+            tr4_load<KIND>(src + soff[job], ss, m[k]);
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < kTr4Jobs; k++)
+    {
+        const int64_t job = b + (int64_t)k * X265AMD_BLOCK;
+        if (job >= n) break;
+        tr4_apply<KIND>(depth, m[k]);
+        tr4_store(dst + dof[k], ds, m[k]);
     }
 }
 
@@ -154,21 +192,48 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_trN(int n, int depth,
             x[i + 1] = (int16_t)(v >> 16);
         }
         fwd_1d<N>(x, y);
+        // column r of the output -> LDS, then row r -> one 16-byte store per 8 coefficients
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < N; k++) L[k * P + r] = (int16_t)fwd_round(y[k], sh2);
+        __syncthreads();
         if (live)
         {
-            int16_t* pd = dst + doff[jj];
+            int16_t* pd = dst + doff[jj] + r * ds;
 #pragma unroll
-            for (int k = 0; k < N; k++) pd[k * ds + r] = (int16_t)fwd_round(y[k], sh2);
+            for (int i = 0; i < N; i += 8)
+            {
+                uint32_t w[4];
+#pragma unroll
+                for (int q = 0; q < 4; q++) w[q] = *(const uint32_t*)&L[r * P + i + 2 * q];
+                stu<uint4>(pd + i, make_uint4(w[0], w[1], w[2], w[3]));
+            }
         }
     }
     else
     {
         const int sh1 = 7, sh2 = 12 - (depth - 8);
         int c[N], y[N];
-        const int16_t* col = src + soff[jj] + r;
+        // row r of the coefficients by 16-byte loads, transposed through LDS into column r
+        const int16_t* row = src + soff[jj] + r * ss;
 #pragma unroll
-        for (int k = 0; k < N; k++) c[k] = col[k * ss];
+        for (int i = 0; i < N; i += 8)
+        {
+            int t[8];
+            load_row16<8>(row + i, t);
+#pragma unroll
+            for (int k = 0; k < 8; k++) L[(i + k) * P + r] = (int16_t)t[k];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < N; i += 2)
+        {
+            const uint32_t v = *(const uint32_t*)&L[r * P + i];
+            c[i] = (int16_t)(v & 0xffff);
+            c[i + 1] = (int16_t)(v >> 16);
+        }
         inv_1d<N>(c, y);
+        __syncthreads();
 #pragma unroll
         for (int k = 0; k < N; k++) L[r * P + k] = (int16_t)inv_round(y[k], sh1);
         __syncthreads();
@@ -776,7 +841,7 @@ extern "C" int x265amd_transform(int kind, int depth, int size, int n,
     if (kind == X265AMD_DST || kind == X265AMD_IDST || size == 4)
     {
         if (size != 4) return X265AMD_EINVAL;
-        const dim3 grid((n + X265AMD_BLOCK - 1) / X265AMD_BLOCK);
+        const dim3 grid((n + X265AMD_BLOCK * kTr4Jobs - 1) / (X265AMD_BLOCK * kTr4Jobs));
         switch (kind)
         {
         case X265AMD_DCT: hipLaunchKernelGGL(k_tr4<X265AMD_DCT>, grid, dim3(X265AMD_BLOCK), 0, st, n, depth, src, src_stride, src_off, dst, dst_stride, dst_off); break;

@@ -91,6 +91,20 @@ __global__ __launch_bounds__(256) void k_dshape(const v2u* __restrict__ s, v2u* 
     }
 }
 
+// each lane copies 32 (64) contiguous bytes as two (four) 16-B loads: the 4x4-transform
+// lane-per-job shape (wave-instructions at a 32-B / 64-B lane stride)
+template <int PER>
+__global__ __launch_bounds__(256) void k_copy_lane(const v4u* __restrict__ s, v4u* __restrict__ d, size_t n)
+{
+    const size_t b = ((size_t)blockIdx.x * 256 + threadIdx.x) * PER;
+    if (b + PER > n) return;
+    v4u v[PER];
+#pragma unroll
+    for (int k = 0; k < PER; k++) v[k] = s[b + k];
+#pragma unroll
+    for (int k = 0; k < PER; k++) d[b + k] = v[k];
+}
+
 static float time_ms(void (*launch)(void*), void* arg, int reps)
 {
     hipEvent_t e0, e1;
@@ -127,6 +141,13 @@ static void L_copy(void* p)
     hipLaunchKernelGGL((k_copy<K, NT>), dim3((n + 256 * K - 1) / (256 * K)), dim3(256), 0, 0, (const v4u*)B->a,
                        (v4u*)B->b, n);
 }
+template <int PER>
+static void L_lane(void* p)
+{
+    Bufs* B = (Bufs*)p;
+    const size_t n = B->bytes / 2 / 16;
+    hipLaunchKernelGGL((k_copy_lane<PER>), dim3((n / PER + 255) / 256), dim3(256), 0, 0, (const v4u*)B->a, (v4u*)B->b, n);
+}
 template <int K, bool NT>
 static void L_q(void* p)
 {
@@ -155,7 +176,7 @@ int main()
     struct V { const char* name; void (*f)(void*); };
     const V vs[] = {
         {"copy16_k1", L_copy<1, false>}, {"copy16_k2", L_copy<2, false>}, {"copy16_k4", L_copy<4, false>},
-        {"copy16_k8", L_copy<8, false>}, {"copy16_k4_nt", L_copy<4, true>}, {"copy16_k8_nt", L_copy<8, true>},
+        {"copy16_k8", L_copy<8, false>}, {"copy_lane32", L_lane<2>}, {"copy_lane64", L_lane<4>}, {"copy16_k4_nt", L_copy<4, true>}, {"copy16_k8_nt", L_copy<8, true>},
         {"quant_k1", L_q<1, false>}, {"quant_k2", L_q<2, false>}, {"quant_k4", L_q<4, false>}, {"quant_k8", L_q<8, false>},
         {"quant_k4_nt", L_q<4, true>}, {"quant_k8_nt", L_q<8, true>},
         {"deq_k1", L_d<1, false>}, {"deq_k4", L_d<4, false>}, {"deq_k8", L_d<8, false>}, {"deq_k4_nt", L_d<4, true>},
