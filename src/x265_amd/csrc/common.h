@@ -224,6 +224,17 @@ struct ForkJoin
     }
 };
 
+// LDS exchange among the lanes of one wavefront: orders this lane's LDS
+// writes before the other lanes' later reads (LDS executes a wavefront's
+// instructions in order; the fences keep the compiler from moving accesses
+// across).  No s_barrier: groups never span wavefronts.
+__device__ __forceinline__ void wave_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // ---------------------------------------------------------------- loads
 // Unaligned little-endian loads (gfx950 runs HSA in unaligned mode: these
 // lower to single global_load_dword{,x2,x4}).

@@ -106,17 +106,6 @@ __device__ __forceinline__ int inv_quant_scale(int rem)
     return v;
 }
 
-// LDS exchange among the lanes of one wavefront: orders this lane's LDS
-// writes before the other lanes' later reads (LDS executes a wavefront's
-// instructions in order; the fences keep the compiler from moving accesses
-// across).  No s_barrier: groups never span wavefronts.
-__device__ __forceinline__ void wave_sync()
-{
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
 template <int G>
 __device__ __forceinline__ int group_max(int v)
 {

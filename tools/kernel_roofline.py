@@ -129,7 +129,9 @@ def main():
             ext_w = 7 if op in (HPP, HVPP) else 0
             ext_h = 7 if op in (VPP, HVPP) else 0
             n = int(a.gb * 1e9 / ((s + ext_w) * (s + ext_h) + s * s))
-            x, y, rows = tiled_offsets(n, s, s, s + 8, s + 8, W, margin=8)
+            # windows tiled densely and disjointly: (s + 7) x s for hpp, s x (s + 7) for vpp, (s + 7)^2 for hvpp
+            # (a pitch of s + 8 in a direction with no filter extension would leave unread gaps in every line)
+            x, y, rows = tiled_offsets(n, s, s, s + (8 if ext_w else 0), s + (8 if ext_h else 0), W, margin=8)
             S = rand_u8(rows * W)
             soff = torch.from_numpy(y * W + x).to(dev)
             D = torch.empty(n * s * s, dtype=torch.uint8, device=dev)
