@@ -319,25 +319,35 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_intra_lane(int n, int maxv,
     for (int r = 0; r < N; r++) store_row<P, N>(out + (int64_t)r * os, o[r]);
 }
 
+// intraFilter (intrapred.cpp:31-51): N lanes per job, lane l filters pixels 4l .. 4l+3 of the
+// 4N+1 neighbours from one vector load plus its two outer neighbours (lane 0 also copies
+// pixel 4N); 256 / N jobs per block
 template <typename P>
 __global__ __launch_bounds__(X265AMD_BLOCK) void k_intra_filter(int N, int n, const P* __restrict__ src,
     const int64_t* __restrict__ soff, P* __restrict__ dst, const int64_t* __restrict__ doff)
 {
-    const int64_t job = (int64_t)xcd_block() * (X265AMD_BLOCK / 64) + threadIdx.x / 64;
-    const int lane = threadIdx.x & 63;
+    const int lg = N == 4 ? 2 : N == 8 ? 3 : N == 16 ? 4 : 5;
+    const int64_t job = (int64_t)xcd_block() * (X265AMD_BLOCK >> lg) + (threadIdx.x >> lg);
+    const int l = threadIdx.x & (N - 1);
     if (job >= n) return;
     const P* s = src + soff[job];
     P* d = dst + doff[job];
-    const int n2 = 2 * N, n4 = 4 * N;
-    for (int i = lane; i <= n4; i += 64)
+    const int n2 = 2 * N, i0 = 4 * l;
+    int v[4], o[4];
+    load_row<P, 4>(s + i0, v);
+    const int left = l ? (int)s[i0 - 1] : (int)s[n2 + 1];        // pixel 0's other neighbour is s[2N + 1]
+    const int right = s[i0 + 4];
+#pragma unroll
+    for (int k = 0; k < 4; k++)
     {
-        int v;
-        if (i == n2 || i == n4) v = s[i];
-        else if (i == 0) v = (2 * s[0] + s[1] + s[n2 + 1] + 2) >> 2;
-        else if (i == n2 + 1) v = (2 * s[n2 + 1] + s[0] + s[n2 + 2] + 2) >> 2;
-        else v = (2 * s[i] + s[i - 1] + s[i + 1] + 2) >> 2;
-        d[i] = (P)v;
+        const int i = i0 + k;
+        const int a = k ? v[k - 1] : left, b = k < 3 ? v[k + 1] : right;
+        if (i == n2) o[k] = v[k];                                   // top-left-most above-right end
+        else if (i == n2 + 1) o[k] = (2 * v[k] + (int)s[0] + b + 2) >> 2;
+        else o[k] = (2 * v[k] + a + b + 2) >> 2;
     }
+    store_row<P, 4>(d + i0, o);
+    if (l == 0) d[4 * N] = s[4 * N];
 }
 
 template <typename P>
@@ -373,7 +383,8 @@ extern "C" int x265amd_intra_filter(int depth, int size, int n, const void* src,
     if (n <= 0) return 0;
     if (!valid_tu(size)) return X265AMD_EINVAL;
     hipStream_t st = (hipStream_t)stream;
-    const dim3 grid((n + 3) / 4);
+    const int per = X265AMD_BLOCK / size;
+    const dim3 grid((n + per - 1) / per);
     if (depth == 8)
         hipLaunchKernelGGL(k_intra_filter<uint8_t>, grid, dim3(X265AMD_BLOCK), 0, st, size, n, (const uint8_t*)src, src_off, (uint8_t*)dst, dst_off);
     else if (depth == 10 || depth == 12)
