@@ -574,6 +574,98 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_hvpp(const BatchGroup g)
     }
 }
 
+
+// hv_pp without the LDS round trip (ipfilter.cpp:322-372): hps with row extension
+// then filterVertical_sp, streamed through registers.  A lane owns an SW-column strip
+// of one job and walks its h + 7 source rows top to bottom: the row's horizontal sums
+// (v_dot4 at 8 bit), the int16 intermediate I[r] = (int16)((S + ps_off) >> ps_shift)
+// exactly as hps writes it, the vertical pairs P[r - 1] = (I[r - 1], I[r]) packed in
+// one dword, and every output row y = r - 7 as four v_dot2_i32_i16 per column against
+// (c_v[2k], c_v[2k+1]) over P[y], P[y+2], P[y+4], P[y+6] — each pair is formed once and
+// serves four output rows — then the sp rounding, int16 truncation and clamp.  The last
+// eight pairs live in a ring indexed by r & 7, compile-time inside a body unrolled over
+// eight rows.
+template <typename P, int SW>
+__global__ __launch_bounds__(X265AMD_BLOCK) void k_hvpp_stream(const BatchGroup g)
+{
+    const uint32_t gb = xcd_block();
+    const SubBatch& sub = group_sub(g, gb);
+    const int w = sub.w, h = sub.h, n = sub.n, lg = sub.lg;
+    const intptr_t ss = sub.sa, ds = sub.ds;
+    const int G = 1 << lg;
+    const int64_t job = (int64_t)(gb - sub.block0) * (X265AMD_BLOCK >> lg) + (threadIdx.x >> lg);
+    const int lane = threadIdx.x & (G - 1);
+    if (job >= n || SW * lane >= w) return;
+    const IfConst K(g.depth);
+    const int cidx = ((const uint8_t*)sub.b)[job];
+    constexpr bool DOT = sizeof(P) == 1;
+    int cp[2], cx[8], cy[8];
+    if constexpr (DOT) pack_taps<8>(cidx & 15, cp);
+    else get_taps<8>(cidx & 15, cx);
+    get_taps<8>(cidx >> 4, cy);
+    s16x2 cv[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) cv[k] = s16x2{ (short)cy[2 * k], (short)cy[2 * k + 1] };
+    const int x0 = SW * lane;
+    const P* ps = (const P*)sub.a + sub.aoff[job] - 3 * ss + x0;
+    P* pd = (P*)sub.d + sub.doff[job] + x0;
+    const int R = h + 7;
+    // 8 bit: I = S - 8192 exactly (shift 0, |S| <= 88 * 255), and the sp offset adds 8192 * 64
+    // back, so the raw sums S are paired and the output is (t + 2048) >> 12
+    auto inter = [&](const P* row, int (&I)[SW]) {
+        if constexpr (DOT) hfilter_dot<8, SW>((const uint8_t*)row, cp, I);
+        else
+        {
+            int S[SW];
+            hfilter<P, 8, SW>(row, cx, S);
+#pragma unroll
+            for (int x = 0; x < SW; x++) I[x] = (int)(int16_t)((S[x] + K.ps_off) >> K.ps_shift);
+        }
+    };
+    uint32_t Pr[8][SW];                  // ring of vertical pairs: Pr[r & 7][x] = (I[r][x], I[r + 1][x])
+    int Iprev[SW];
+    inter(ps, Iprev);
+    for (int r0 = 1; r0 < R; r0 += 8)
+    {
+#pragma unroll
+        for (int i = 0; i < 8; i++)
+        {
+            const int r = r0 + i;                        // row whose intermediate is formed now
+            if (r >= R) break;
+            int I[SW];
+            inter(ps + (intptr_t)r * ss, I);
+            // P[r - 1] goes to ring slot (r - 1) & 7 = i (r0 = 1 mod 8): compile-time
+#pragma unroll
+            for (int x = 0; x < SW; x++)
+            {
+                Pr[i][x] = __builtin_amdgcn_perm((uint32_t)I[x], (uint32_t)Iprev[x], 0x05040100u);
+                Iprev[x] = I[x];
+            }
+            const int y = r - 7;                         // output row ready once P[y + 6] exists
+            if (y >= 0)
+            {
+                int o[SW];
+#pragma unroll
+                for (int x = 0; x < SW; x++)
+                {
+                    int t = 0;
+#pragma unroll
+                    for (int k = 0; k < 4; k++)
+                        t = __builtin_amdgcn_sdot2(__builtin_bit_cast(s16x2, Pr[(i + 2 + 2 * k) & 7][x]), cv[k], t, false);
+                    if constexpr (DOT)
+                    {
+                        const int v = (t + 2048) >> 12;
+                        o[x] = v < 0 ? 0 : (v > 255 ? 255 : v);
+                    }
+                    else
+                        o[x] = clampp((t + K.sp_off) >> K.sp_shift, K.maxv);
+                }
+                store_row<P, SW>(pd + (intptr_t)y * ds, o);
+            }
+        }
+    }
+}
+
 // -------------------------------------------------------------- dispatch
 
 // unit-height override for tuning runs (X265AMD_UH_<op>=1|2|4|16; 0 = built-in choice)
@@ -630,9 +722,19 @@ static int hvpp_lg(int w, int h, int uw, int uh)
     return lg;
 }
 
+// classes of the streaming hv_pp (k_hvpp_stream): 8- / 4-wide strips, no LDS
+constexpr int kHvppStream = 8 * 32 + 31, kHvppStream4 = 4 * 32 + 31;
+
 template <typename P, typename S, typename D, int OP, int TAPS>
 static int launch_interp(int cls, const BatchGroup& g, uint32_t blocks, hipStream_t st)
 {
+    if constexpr (OP == X265AMD_HVPP)
+        if (cls == kHvppStream || cls == kHvppStream4)
+        {
+            if (cls == kHvppStream) hipLaunchKernelGGL((k_hvpp_stream<P, 8>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, g);
+            else hipLaunchKernelGGL((k_hvpp_stream<P, 4>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, g);
+            return (int)hipGetLastError();
+        }
     size_t lds = 0;
     if constexpr (OP == X265AMD_HVPP)
         for (int i = 0; i < g.count; i++)
@@ -667,6 +769,17 @@ static int grouped_interp(int depth, int count, const x265amd_interp_batch* bt, 
         cls[i] = interp_class<OP, TAPS>(bt[i].w, bt[i].h, bt[i].is_row_ext,
                                         sizeof(S) == 1 && (OP == X265AMD_VPP || OP == X265AMD_VPS));
         if (cls[i] < 0) return -cls[i];
+        // hv_pp streams its rows through registers on 8-wide strips at 8 bit (4-wide for 4-wide blocks
+        // and for 16-bit pixels, whose int32 window doubles the registers;
+        // measured, profiles/r02/hvpp_stream.txt); X265AMD_HVPP_LDS=1 selects the two-pass LDS
+        // kernel, X265AMD_HVPP_SW=4 the 4-wide strips everywhere (tuning runs)
+        static const bool hv_lds = getenv("X265AMD_HVPP_LDS") && atoi(getenv("X265AMD_HVPP_LDS"));
+        static const int hv_sw = getenv("X265AMD_HVPP_SW") ? atoi(getenv("X265AMD_HVPP_SW")) : 8;
+        if (OP == X265AMD_HVPP && !hv_lds)
+        {
+            if (sizeof(P) == 1 && bt[i].w % 8 == 0 && hv_sw != 4) cls[i] = kHvppStream;
+            else if (bt[i].w % 4 == 0) cls[i] = kHvppStream4;
+        }
     }
     BatchGroup proto{};
     proto.depth = depth;
@@ -681,7 +794,8 @@ static int grouped_interp(int depth, int count, const x265amd_interp_batch* bt, 
             s.param = OP == X265AMD_HPS ? b.is_row_ext : 0;
             const int uw = cls[i] / 32, uh = cls[i] % 32;
             if constexpr (OP == X265AMD_HVPP)
-                s.lg = hvpp_lg(b.w, b.h, uw, uh);
+                s.lg = cls[i] == kHvppStream ? lanes_log2(b.w / 8, 1)
+                       : cls[i] == kHvppStream4 ? lanes_log2(b.w / 4, 1) : hvpp_lg(b.w, b.h, uw, uh);
             else
             {
                 const int rows = (OP == X265AMD_HPS && s.param) ? b.h + TAPS - 1 : b.h;
