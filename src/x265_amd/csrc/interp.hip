@@ -668,7 +668,7 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_hvpp_stream(const BatchGroup 
 
 // -------------------------------------------------------------- dispatch
 
-// unit-height override for tuning runs (X265AMD_UH_<op>=1|2|4|16; 0 = built-in choice)
+// unit-height override for tuning runs (X265AMD_UH_<op>=1|2|4|8|16; 0 = built-in choice)
 static int uh_override(int op)
 {
     static int v[8] = {-1, -1, -1, -1, -1, -1, -1, -1};
@@ -705,7 +705,7 @@ static int interp_class(int w, int h, int rowext, bool pk8)
     // 16x16 36.5% -> 37.7%; 8-row units were worse on 8x8 and 16x16)
     // (the packed 8-bit vpp / vps path only: its accumulators are half-size)
     int uh = (pk8 && rows % 16 == 0 && w % 4 == 0) ? 16 : rows % 4 ? 1 : 4;
-    if (ov && rows % ov == 0 && (ov != 16 || (pk8 && w % 4 == 0)) && (ov == 1 || ov == 2 || ov == 4 || ov == 16))
+    if (ov && rows % ov == 0 && (ov != 16 || (pk8 && w % 4 == 0)) && (ov == 1 || ov == 2 || ov == 4 || ov == 8 || ov == 16))
         uh = ov;
     if (w % 8 == 0) return 8 * 32 + uh;
     if (w % 4 == 0) return 4 * 32 + uh;
@@ -747,12 +747,12 @@ static int launch_interp(int cls, const BatchGroup& g, uint32_t blocks, hipStrea
             if constexpr (UW >= 4) \
                 hipLaunchKernelGGL((k_hvpp<P, UW, UH>), dim3(blocks), dim3(X265AMD_BLOCK), lds, st, g); \
         } \
-        else if constexpr ((UW >= 4 || TAPS == 4 || (OP != X265AMD_HPP && OP != X265AMD_HPS)) && (UH < 8 || PK8)) \
+        else if constexpr ((UW >= 4 || TAPS == 4 || (OP != X265AMD_HPP && OP != X265AMD_HPS)) && (UH <= 8 || PK8)) \
             hipLaunchKernelGGL((k_interp<P, S, D, OP, TAPS, UW, UH>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, g); \
         return (int)hipGetLastError(); \
     }
     constexpr bool PK8 = sizeof(S) == 1 && (OP == X265AMD_VPP || OP == X265AMD_VPS);
-    L(8, 16) L(4, 16) L(8, 4) L(8, 2) L(8, 1) L(4, 4) L(4, 2) L(4, 1) L(2, 4) L(2, 1)
+    L(8, 16) L(4, 16) L(8, 8) L(8, 4) L(8, 2) L(8, 1) L(4, 4) L(4, 2) L(4, 1) L(2, 4) L(2, 1)
 #undef L
     return X265AMD_EINVAL;
 }
