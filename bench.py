@@ -332,6 +332,23 @@ def pipeline_rates(prims, args, census, local):
         dt = (time.perf_counter() - t0) / n
         out[f"band_rows_{br}"] = {"fps": round(args.frames / dt, 1), "ms_per_step": round(dt * 1e3, 3),
                                   "bands_per_frame": pipe.plan.nbands, "launches_per_step": pipe.launches_per_step}
+    # the same frames and bands in the wavefront schedule (frame k's band b at step k * d + b: one set
+    # of grouped launches per step for every frame in it, the sequence as one hipGraph)
+    for br in (args.band_rows, 1):
+        pipe.set_band_rows(br)
+        pipe.build_wave()
+        for _ in range(2):
+            pipe.step()
+        torch.cuda.synchronize()
+        n = 10
+        t0 = time.perf_counter()
+        for _ in range(n):
+            pipe.step()
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / n
+        out[f"wavefront_band_rows_{br}"] = {"fps": round(args.frames / dt, 1), "ms_per_step": round(dt * 1e3, 3),
+                                            "bands_per_frame": pipe.plan.nbands, "frame_delay_bands": pipe.d,
+                                            "steps": pipe.nsteps, "launches_per_step": pipe.wave_launches_per_step()}
     return out
 
 

@@ -104,6 +104,35 @@ def band_slices(batches, fs: FrameSet, plan: BandPlan, ctu: int = 64):
     return out
 
 
+def wave_delay(plan: BandPlan) -> int:
+    """bands by which frame k + 1 trails frame k in the single-rank wavefront: its band b needs
+    reference band need(b), which frame k publishes in the step of band need(b) + 1 (after that
+    band's deblocking) or, for the last band, in its own step; the publication must come from an
+    earlier step, so d > need(b) + 1 - b for every b"""
+    return max(min(plan.need(b) + 1, plan.nbands - 1) + 1 - b for b in range(plan.nbands))
+
+
+def step_slices(batches, fs: FrameSet, plan: BandPlan, d: int, ctu: int = 64):
+    """{step: [batch slices]} of the wavefront schedule, step = frame * d + band: the (frame, band)
+    pairs of one step are independent, so each census batch contributes ONE slice per step"""
+    out = {}
+    nsteps = (fs.F - 1) * d + plan.nbands
+    for b in batches:
+        frame, y = job_rows(b, fs)
+        band = np.minimum(y // ctu, plan.ctu_rows - 1) // plan.band_rows
+        key = frame * d + band
+        if np.any(np.diff(key) < 0):
+            order = np.argsort(key, kind="stable")
+            b = _take(b, idx=order)
+            key = key[order]
+        bounds = np.searchsorted(key, np.arange(nsteps + 1))
+        for st in range(nsteps):
+            lo, hi = int(bounds[st]), int(bounds[st + 1])
+            if hi > lo:
+                out.setdefault(st, []).append(_take(b, lo=lo, hi=hi))
+    return out
+
+
 def check_reference_reach(slices, fs: FrameSet, plan: BandPlan, ctu: int = 64, taps: int = 8):
     """every reference read of band b's jobs lies in CTU rows <= rows(b)[1] - 1 + lag"""
     bad = []
@@ -337,8 +366,102 @@ class GpuFramePipeline:
     def _eager_step(self):
         run_frames(self.ex, self.F, self.band_work, lambda k, b: None, lambda k, b: None)
 
+    # ---------------------------------------------------------------- single-rank wavefront
+    def build_wave(self):
+        """Single rank: schedule (frame k, band b) at step k * d + b (d = wave_delay) — the bands of
+        consecutive frames that x265's frame threads run concurrently — so one step's census work
+        of every frame goes out as one set of grouped launches and its loop filters as one call per
+        kernel, and capture the whole sequence as ONE hipGraph.  Same results as step()."""
+        import torch
+
+        assert self.world == 1
+        self.d = wave_delay(self.plan)
+        self.nsteps = (self.F - 1) * self.d + self.plan.nbands
+        self.wslices = step_slices(self.batches, self.fs, self.plan, self.d)
+        self._wgroups = {st: group_launches(bs) for st, bs in self.wslices.items()}
+        for gs in self._wgroups.values():
+            for g in gs:
+                g.run(self.prims)
+        torch.cuda.synchronize()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            self._wave_all()
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._wave_all()
+        self.graphs = {"wave": g}
+        torch.cuda.synchronize()
+
+    def _wave_all(self):
+        for st in range(self.nsteps):
+            self._wave_step(st)
+
+    def _wave_step(self, st):
+        import torch
+
+        plan, nb = self.plan, self.plan.nbands
+        pairs = [(k, st - k * self.d) for k in range(self.F) if 0 <= st - k * self.d < nb]
+        cur = torch.cuda.current_stream()
+        groups = self._wgroups.get(st, [])
+        if self.streams:
+            lanes = [[] for _ in self.streams]
+            load = [0.0] * len(self.streams)
+            for g in groups:
+                i = min(range(len(self.streams)), key=lambda j: load[j])
+                lanes[i].append(g)
+                load[i] += g.bytes
+            for s_, lst in zip(self.streams, lanes):
+                if not lst:
+                    continue
+                s_.wait_stream(cur)
+                h = ctypes.c_void_p(s_.cuda_stream)
+                for g in lst:
+                    g.run(self.prims, h)
+            for s_, lst in zip(self.streams, lanes):
+                if lst:
+                    cur.wait_stream(s_)
+        else:
+            for g in groups:
+                g.run(self.prims)
+        fs = self.fs
+        for k, b in pairs:                       # the bands' reconstruction (stand-in: source pixels)
+            y0, y1 = self._rows_px(b)
+            for p in range(3):
+                stride, my, sh = (fs.stride, fs.my, 0) if p == 0 else (fs.cstride, fs.cmy, 1)
+                s0, e0 = (my + (y0 >> sh)) * stride, (my + (y1 >> sh)) * stride
+                src = self.src_planes[p][k * self._sizes[p]:(k + 1) * self._sizes[p]]
+                self.frame_planes(self.work, k)[p][s0:e0].copy_(src[s0:e0])
+        h = ctypes.c_void_p(cur.cuda_stream)
+        rows = []
+        for k, b in pairs:
+            rows += list(self._rows_px(b))
+        self.prims.deblock_rows(self.depth, [self.dbk[k] for k, _ in pairs], rows, h)
+        # bands finished in this step: b - 1 of every pair, and b itself when it is the last band
+        done = [(k, b - 1) for k, b in pairs if b] + [(k, b) for k, b in pairs if b == nb - 1]
+        if done:
+            self.prims.sao_apply_rows(self.depth, [self.sao[k] for k, _ in done],
+                                      [r for _, c in done for r in plan.rows(c)], h)
+            planes, brows = [], []
+            for k, c in done:
+                y0, y1 = self._rows_px(c)
+                first, last = int(c == 0), int(c == nb - 1)
+                planes += self.bor[k]
+                brows += [y0, y1, first, last] + [y0 // 2, y1 // 2, first, last] * 2
+            self.prims.extend_border_rows(self.depth, planes, brows, h)
+            for k, c in done:
+                self.ex.publish(k, c)
+
+    def wave_launches_per_step(self):
+        return sum(len(v) for v in self._wgroups.values()) + 3 * self.nsteps
+
     def step(self):
         """one sequence of G * F frames: this rank's F frames with the row exchange"""
+        if "wave" in self.graphs:
+            self.graphs["wave"].replay()
+            return
         if "step" in self.graphs:
             self.graphs["step"].replay()
             return

@@ -6,7 +6,9 @@ frame's final reconstruction equals the whole-frame deblock -> SAO -> border cha
 (x265amd_deblock / _sao_apply / _extend_border, themselves bit-exact vs the
 reference's Deblock / SAO classes in test_f4.py) on the same picture; every
 reference slot holds the previous frame's final reconstruction, margins included;
-and every census batch still matches the oracle on sampled jobs after the band split.
+and every census batch still matches the oracle on sampled jobs after the band split
+(a job that read a reference row before it was published would not).  Both schedules:
+frame by frame, and the single-rank wavefront.
 """
 import numpy as np
 import pytest
@@ -14,8 +16,10 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("band_rows", [1, 3])
-def test_gpu_pipeline_rows_equal_whole_frame(gpu_prims, oracle_libs, band_rows):
+@pytest.mark.parametrize("band_rows,wave", [(1, False), (3, False), (1, True), (4, True)])
+def test_gpu_pipeline_rows_equal_whole_frame(gpu_prims, oracle_libs, band_rows, wave):
+    """wave=True: the single-rank wavefront schedule (frame k's band b at step k * d + b, one set
+    of grouped launches per step, the whole sequence one hipGraph) must give the same frames"""
     import torch
 
     from pyoracle import CpuOracle
@@ -23,7 +27,10 @@ def test_gpu_pipeline_rows_equal_whole_frame(gpu_prims, oracle_libs, band_rows):
 
     W, H, F = 416, 240, 4
     pipe = GpuFramePipeline(gpu_prims, W, H, 8, F, 1, 0, band_rows=band_rows, streams=4, device="cuda")
-    pipe.build(graphs=True)
+    if wave:
+        pipe.build_wave()
+    else:
+        pipe.build(graphs=True)
     pipe.step()
     torch.cuda.synchronize()
     fs = pipe.fs
