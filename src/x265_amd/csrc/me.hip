@@ -396,7 +396,10 @@ __device__ __forceinline__ int4 subpel_workload(int subme)
 }
 
 template <typename P, int G>
-__global__ __launch_bounds__(X265AMD_BLOCK) void k_motion_search(const MeArgs a)
+#ifndef X265AMD_ME_WAVES
+#define X265AMD_ME_WAVES 1
+#endif
+__global__ __launch_bounds__(X265AMD_BLOCK, X265AMD_ME_WAVES) void k_motion_search(const MeArgs a)
 {
     const int64_t j = (int64_t)xcd_block() * (X265AMD_BLOCK / G) + threadIdx.x / G;
     if (j >= a.n) return;                               // whole groups

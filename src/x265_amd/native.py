@@ -10,7 +10,7 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libx265amd.so")
+LIB_PATH = os.environ.get("X265AMD_LIB") or os.path.join(HERE, "libx265amd.so")   # override: A/B tuning builds
 
 _vp, _ip, _int = C.c_void_p, C.c_ssize_t, C.c_int
 
