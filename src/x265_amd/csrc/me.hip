@@ -139,6 +139,35 @@ __device__ __forceinline__ int fpel_sad(const MeState<P>& s, int dx, int dy)
     return group_sum<G>((int)acc);
 }
 
+
+// N consecutive pixels from p as ints, by vector loads that stay inside [p, p + N)
+// (N = 4, 7 or 11; overlapping loads cover the odd widths)
+template <typename P, int N>
+__device__ __forceinline__ void load_px(const P* p, int (&v)[N])
+{
+    if constexpr (N == 4)
+        load_row<P, 4>(p, v);
+    else if constexpr (N == 7)
+    {
+        int a[4], b[4];
+        load_row<P, 4>(p, a);
+        load_row<P, 4>(p + 3, b);
+#pragma unroll
+        for (int i = 0; i < 4; i++) { v[i] = a[i]; v[3 + i] = b[i]; }
+    }
+    else
+    {
+        static_assert(N == 11, "window");
+        int a[8], b[4];
+        load_row<P, 8>(p, a);
+        load_row<P, 4>(p + 7, b);
+#pragma unroll
+        for (int i = 0; i < 8; i++) v[i] = a[i];
+#pragma unroll
+        for (int i = 0; i < 4; i++) v[7 + i] = b[i];
+    }
+}
+
 // the 4:2:0 chroma SATD subpelCompare adds at subme 3 (motion.cpp:1205-1266): the chroma block at
 // the 1/8-pel position (qx, qy) (4-tap pp filters; hps + vsp for 2-D), satd against the source
 // chroma, over this lane's 4x4 chroma units (not group-reduced)
@@ -166,26 +195,31 @@ __device__ __forceinline__ int chroma_satd(const MeState<P>& s, int qx, int qy)
             if (!(xf | yf))
             {
 #pragma unroll
-                for (int r = 0; r < 4; r++)
-#pragma unroll
-                    for (int c = 0; c < 4; c++) blk[r][c] = p[r * s.rcs + c];
+                for (int r = 0; r < 4; r++) load_px<P, 4>(p + r * s.rcs, blk[r]);
             }
             else if (!yf)
             {
 #pragma unroll
                 for (int r = 0; r < 4; r++)
+                {
+                    int w7[7];
+                    load_px<P, 7>(p + r * s.rcs - 1, w7);
 #pragma unroll
                     for (int c = 0; c < 4; c++)
                     {
                         int sum = 0;
 #pragma unroll
-                        for (int t = 0; t < 4; t++) sum += cx[t] * p[r * s.rcs + c + t - 1];
+                        for (int t = 0; t < 4; t++) sum += cx[t] * w7[c + t];
                         const int val = (int16_t)((sum + 32) >> 6);
                         blk[r][c] = val < 0 ? 0 : (val > maxv ? maxv : val);
                     }
+                }
             }
             else if (!xf)
             {
+                int w4[7][4];
+#pragma unroll
+                for (int i = 0; i < 7; i++) load_px<P, 4>(p + (i - 1) * s.rcs, w4[i]);
 #pragma unroll
                 for (int r = 0; r < 4; r++)
 #pragma unroll
@@ -193,7 +227,7 @@ __device__ __forceinline__ int chroma_satd(const MeState<P>& s, int qx, int qy)
                     {
                         int sum = 0;
 #pragma unroll
-                        for (int t = 0; t < 4; t++) sum += cy[t] * p[(r + t - 1) * s.rcs + c];
+                        for (int t = 0; t < 4; t++) sum += cy[t] * w4[r + t][c];
                         const int val = (int16_t)((sum + 32) >> 6);
                         blk[r][c] = val < 0 ? 0 : (val > maxv ? maxv : val);
                     }
@@ -206,14 +240,18 @@ __device__ __forceinline__ int chroma_satd(const MeState<P>& s, int qx, int qy)
                 int m[7][4];
 #pragma unroll
                 for (int i = 0; i < 7; i++)
+                {
+                    int w7[7];
+                    load_px<P, 7>(p + (i - 1) * s.rcs - 1, w7);
 #pragma unroll
                     for (int c = 0; c < 4; c++)
                     {
                         int sum = 0;
 #pragma unroll
-                        for (int t = 0; t < 4; t++) sum += cx[t] * p[(i - 1) * s.rcs + c + t - 1];
+                        for (int t = 0; t < 4; t++) sum += cx[t] * w7[c + t];
                         m[i][c] = (int16_t)((sum + ps_off) >> ps_shift);
                     }
+                }
 #pragma unroll
                 for (int r = 0; r < 4; r++)
 #pragma unroll
@@ -270,9 +308,7 @@ __device__ __noinline__ int subpel_cost(const MeState<P>& s, int qx, int qy, boo
         if (!(xf | yf))
         {
 #pragma unroll
-            for (int r = 0; r < 4; r++)
-#pragma unroll
-                for (int c = 0; c < 4; c++) blk[r][c] = p[r * s.rs + c];
+            for (int r = 0; r < 4; r++) load_px<P, 4>(p + r * s.rs, blk[r]);
         }
         else if (!yf)
         {
@@ -281,8 +317,7 @@ __device__ __noinline__ int subpel_cost(const MeState<P>& s, int qx, int qy, boo
             for (int r = 0; r < 4; r++)
             {
                 int v[11];
-#pragma unroll
-                for (int i = 0; i < 11; i++) v[i] = p[r * s.rs + i - 3];
+                load_px<P, 11>(p + r * s.rs - 3, v);
 #pragma unroll
                 for (int c = 0; c < 4; c++)
                 {
@@ -299,9 +334,7 @@ __device__ __noinline__ int subpel_cost(const MeState<P>& s, int qx, int qy, boo
             // interp_vert_pp
             int v[11][4];
 #pragma unroll
-            for (int i = 0; i < 11; i++)
-#pragma unroll
-                for (int c = 0; c < 4; c++) v[i][c] = p[(i - 3) * s.rs + c];
+            for (int i = 0; i < 11; i++) load_px<P, 4>(p + (i - 3) * s.rs, v[i]);
 #pragma unroll
             for (int r = 0; r < 4; r++)
 #pragma unroll
@@ -324,8 +357,7 @@ __device__ __noinline__ int subpel_cost(const MeState<P>& s, int qx, int qy, boo
             for (int i = 0; i < 11; i++)
             {
                 int v[11];
-#pragma unroll
-                for (int j = 0; j < 11; j++) v[j] = p[(i - 3) * s.rs + j - 3];
+                load_px<P, 11>(p + (i - 3) * s.rs - 3, v);
 #pragma unroll
                 for (int c = 0; c < 4; c++)
                 {
