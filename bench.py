@@ -511,11 +511,16 @@ def main():
         # so its algorithmic bytes exceed what reaches HBM and algorithmic/time can
         # exceed the HBM peak.  The HBM fraction is therefore taken from the calibrated PMC bytes
         # of the same launch (FETCH_SIZE / WRITE_SIZE passes); without them it is the algorithmic rate.
-        achieved = traffic / (dom_ms * 1e-3) / 1e9 if traffic else algo_gbps
-        roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+        # Without a PMC record (non-default configurations) there is no HBM figure to divide: the
+        # algorithmic rate of a census launch counts cache-resident re-reads and can exceed the peak,
+        # so it is reported beside a null frac instead of as one.
+        achieved = traffic / (dom_ms * 1e-3) / 1e9 if traffic else None
+        roofline = {"bound": "hbm", "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
+                    "traffic": traffic,
                     "basis": "PMC HBM bytes per launch / launch time" if traffic else
-                             "algorithmic bytes per launch / launch time (no PMC record for this launch)",
+                             "no PMC record for this configuration (profiles/pmc_traffic.json holds the default "
+                             "1080p medium 8-frame step); see achieved_algorithmic",
                     "achieved_algorithmic": round(algo_gbps, 1),
                     "kernel": kname, "kernel_ms": round(dom_ms, 4), "bytes_per_launch": int(dominant.bytes),
                     "launch_jobs": dominant.n,
