@@ -233,7 +233,7 @@ def reference_encoder_baseline(args):
     if args.depth != 8 or not os.path.exists(exe):
         return None
     cores = host_cores()
-    n_all = 32 if args.width * args.height <= 1920 * 1080 else 8
+    n_all = 64 if args.width * args.height <= 1920 * 1080 else 16     # BASELINE config 0: 64 frames at 1080p
     n_one = 4 if args.width * args.height <= 1920 * 1080 else 2
     with tempfile.TemporaryDirectory() as td:
         src = os.path.join(td, "src.yuv")
