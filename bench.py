@@ -146,11 +146,18 @@ def kernel_times(batches, prims, reps=2):
     return {k: sum(a.elapsed_time(c) for a, c in v) / len(v) for k, v in out.items()}
 
 
-def pmc_traffic(launch_name: str):
-    """per-launch HBM bytes of `launch_name` from the committed PMC summary
-    (profiles/pmc_traffic.json: tools/pmc_workload.py + tools/pmc_parse.py, FETCH_SIZE and
-    WRITE_SIZE in separate rocprofv3 passes, calibrated on known-byte kernels), if any"""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+def pmc_traffic_path(args) -> str:
+    """the PMC traffic table of this configuration (F = 8 frames per step): profiles/pmc_traffic.json
+    for the default 1080p medium 8-bit step, profiles/pmc_traffic_<h>p_<preset>_<depth>bit.json else"""
+    default = (args.width, args.height, args.depth, args.preset) == (1920, 1080, 8, "medium")
+    name = "pmc_traffic.json" if default else f"pmc_traffic_{args.height}p_{args.preset}_{args.depth}bit.json"
+    return os.path.join(ROOT, "profiles", name)
+
+
+def pmc_traffic(launch_name: str, path: str):
+    """per-launch HBM bytes of `launch_name` from a committed PMC summary
+    (tools/pmc_workload.py + tools/pmc_parse.py, FETCH_SIZE and WRITE_SIZE in separate
+    rocprofv3 passes, calibrated on known-byte kernels), if any"""
     if not os.path.exists(path):
         return None
     try:
@@ -505,8 +512,9 @@ def main():
         algo_gbps = dominant.bytes / (dom_ms * 1e-3) / 1e9
         kname = f"{dominant.kind}:{dominant.name}"
         # the committed PMC summary (profiles/pmc_traffic.json) was recorded on the default configuration
-        default_cfg = (args.width, args.height, args.depth, args.preset, F) == (1920, 1080, 8, "medium", 8)
-        traffic = pmc_traffic(dominant.name) if default_cfg else None
+        # the committed PMC summaries were recorded with 8 frames per step
+        ppath = pmc_traffic_path(args) if F == 8 else ""
+        traffic = pmc_traffic(dominant.name, ppath) if ppath else None
         # A census launch re-reads blocks many times (x265 scores many candidates per fenc block),
         # so its algorithmic bytes exceed what reaches HBM and algorithmic/time can
         # exceed the HBM peak.  The HBM fraction is therefore taken from the calibrated PMC bytes
@@ -519,15 +527,15 @@ def main():
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
                     "traffic": traffic,
                     "basis": "PMC HBM bytes per launch / launch time" if traffic else
-                             "no PMC record for this configuration (profiles/pmc_traffic.json holds the default "
-                             "1080p medium 8-frame step); see achieved_algorithmic",
+                             "no PMC record for this launch in " + (os.path.relpath(ppath, ROOT) if ppath else
+                             "profiles/ (recorded with 8 frames per step)") + "; see achieved_algorithmic",
                     "achieved_algorithmic": round(algo_gbps, 1),
                     "kernel": kname, "kernel_ms": round(dom_ms, 4), "bytes_per_launch": int(dominant.bytes),
                     "launch_jobs": dominant.n,
                     "share_of_step": round(ktimes[dominant.name] / max(1e-9, sum(ktimes.values())), 3)}
         if traffic:
             roofline["traffic_over_algorithmic"] = round(traffic / dominant.bytes, 3)
-        step_traffic = [pmc_traffic(b.name) for b in launches] if default_cfg else []
+        step_traffic = [pmc_traffic(b.name, ppath) for b in launches] if ppath else []
         step_hbm = None
         if step_traffic and all(t is not None for t in step_traffic):
             tb = sum(step_traffic)

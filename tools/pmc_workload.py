@@ -12,6 +12,8 @@ order to --order so tools/pmc_parse.py can attribute the dispatch rows.
     (again with --pmc WRITE_SIZE into gpurun_out/pmc_write)
     python3 tools/pmc_parse.py gpurun_out/pmc_fetch gpurun_out/pmc_write gpurun_out/pmc_order.json \
         --out profiles/pmc_traffic.json
+Other configurations (--width / --height / --depth / --preset, as bench.py) go to
+profiles/pmc_traffic_<height>p_<preset>_<depth>bit.json, which bench.py reads for them.
 """
 from __future__ import annotations
 
@@ -29,6 +31,10 @@ def main():
     ap.add_argument("--frames", type=int, default=8)
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--order", required=True)
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--depth", type=int, default=8)
+    ap.add_argument("--preset", default="medium")
     a = ap.parse_args()
 
     import torch
@@ -37,8 +43,11 @@ def main():
     from src.x265_amd.workload import FrameSet, WorkloadBuilder, census_batches, group_launches, load_census
 
     prims = Primitives(device=0)
-    fs = FrameSet(1920, 1080, a.frames, 8, device="cuda:0")
-    batches, _ = census_batches(fs, frames=a.frames, census=load_census(), builder=WorkloadBuilder(fs, seed=11))
+    import bench
+
+    census, _ = bench.pick_census(a)            # the census bench.py uses for this configuration
+    fs = FrameSet(a.width, a.height, a.frames, a.depth, device="cuda:0")
+    batches, _ = census_batches(fs, frames=a.frames, census=census, builder=WorkloadBuilder(fs, seed=11))
     launches = group_launches(batches)
     for _ in range(a.steps):
         for g in launches:
