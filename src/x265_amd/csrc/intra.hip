@@ -199,6 +199,8 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_intra_pred(int n, int maxv,
 // reference array to a private LDS column as PAIRS D[j] = (R[j], R[j+1]) of
 // u16: every angular pixel is then one ds_read_b32 and one v_dot2_u32_u16
 // against the row weights (32 - f, f):  ((32-f)·a + f·b + 16) >> 5.
+constexpr int kIntraLaneJobs = 2;     // 4x4 jobs per lane
+
 template <typename P, int N>
 __global__ __launch_bounds__(X265AMD_BLOCK) void k_intra_lane(int n, int maxv,
     P* __restrict__ dst, intptr_t ds, const int64_t* __restrict__ doff,
@@ -213,6 +215,77 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_intra_lane(int n, int maxv,
     constexpr int SW = N == 8 ? NB * X265AMD_BLOCK / 4 : 0;    // dwords of the output staging
     __shared__ uint32_t lds[DW > SW ? DW : SW];
     uint32_t (*D)[X265AMD_BLOCK] = (uint32_t (*)[X265AMD_BLOCK])lds;
+    if constexpr (N == 4)
+    {
+        // 4x4: kIntraLaneJobs jobs per lane (jobs b + k * 256 + t), the descriptors and neighbour
+        // loads of all of them issued before the first prediction; the lane's LDS column is reused
+        // job after job (private to the lane: no barrier)
+        const int64_t base = (int64_t)xcd_block() * X265AMD_BLOCK * kIntraLaneJobs + threadIdx.x;
+        int mk[kIntraLaneJobs], bfk[kIntraLaneJobs], sk[kIntraLaneJobs][4 * N + 1];
+        P* outk[kIntraLaneJobs];
+        bool livek[kIntraLaneJobs];
+#pragma unroll
+        for (int k = 0; k < kIntraLaneJobs; k++)
+        {
+            const int64_t job = base + (int64_t)k * X265AMD_BLOCK;
+            livek[k] = job < n;
+            const int64_t jj = livek[k] ? job : 0;
+            const P* src;
+            if (allangs)
+            {
+                const int64_t tu = jj / 33;
+                mk[k] = 2 + (int)(jj % 33);
+                bfk[k] = bfilter[tu];
+                src = (c_intra.filter_flags[mk[k]] & N) ? filt + filtoff[tu] : nb + nboff[tu];
+                outk[k] = dst + doff[tu] + (int64_t)(mk[k] - 2) * N * N;
+            }
+            else
+            {
+                mk[k] = mode[jj];
+                bfk[k] = bfilter[jj];
+                src = nb + nboff[jj];
+                outk[k] = dst + doff[jj];
+            }
+            intra_lane_load<P, N>(src, sk[k]);
+        }
+        const intptr_t os = allangs ? N : ds;
+#pragma unroll
+        for (int k = 0; k < kIntraLaneJobs; k++)
+        {
+            if (!livek[k]) continue;
+            int v[N][N], o[N][N];
+            const ModeInfo mi = intra_lane_predict<N>(sk[k], mk[k], bfk[k], maxv, D, v);
+            const bool tr = mi.hor && !allangs;
+#pragma unroll
+            for (int r = 0; r < N; r++)
+#pragma unroll
+                for (int c = 0; c < N; c++) o[r][c] = tr ? v[c][r] : v[r][c];
+            if (os == 4)
+            {
+                uint32_t w[NB / 4];
+#pragma unroll
+                for (int r = 0; r < 4; r++)
+                {
+                    if constexpr (sizeof(P) == 1)
+                        w[r] = (uint32_t)o[r][0] | ((uint32_t)o[r][1] << 8) | ((uint32_t)o[r][2] << 16) | ((uint32_t)o[r][3] << 24);
+                    else
+                    {
+                        w[2 * r] = (uint32_t)o[r][0] | ((uint32_t)o[r][1] << 16);
+                        w[2 * r + 1] = (uint32_t)o[r][2] | ((uint32_t)o[r][3] << 16);
+                    }
+                }
+#pragma unroll
+                for (int q = 0; q < NB / 16; q++)
+                    stu<uint4>((uint8_t*)outk[k] + 16 * q, make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]));
+            }
+            else
+            {
+#pragma unroll
+                for (int r = 0; r < N; r++) store_row<P, N>(outk[k] + (int64_t)r * os, o[r]);
+            }
+        }
+        return;
+    }
     const int64_t job = (int64_t)xcd_block() * X265AMD_BLOCK + threadIdx.x;
     const bool live = job < n;
     const int64_t jj = live ? job : 0;
@@ -355,7 +428,7 @@ static int launch_pred(int N, int n, int depth, void* dst, intptr_t ds, const in
                        const int64_t* nboff, const void* filt, const int64_t* filtoff, const uint8_t* mode,
                        const uint8_t* bfilter, int allangs, hipStream_t st)
 {
-    const int per = N <= 8 ? X265AMD_BLOCK : X265AMD_BLOCK / N;    // lane per job up to 8x8
+    const int per = N == 4 ? X265AMD_BLOCK * kIntraLaneJobs : N <= 8 ? X265AMD_BLOCK : X265AMD_BLOCK / N;
     const dim3 grid((n + per - 1) / per);
 #define L(K, NN) hipLaunchKernelGGL((K<P, NN>), grid, dim3(X265AMD_BLOCK), 0, st, n, (1 << depth) - 1, \
                                     (P*)dst, ds, doff, (const P*)nb, nboff, (const P*)filt, filtoff, mode, bfilter, allangs)
