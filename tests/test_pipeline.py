@@ -185,3 +185,27 @@ def test_frame_parallel_rows_gloo(world, band_rows):
                 # the reference slot holds the producer's final frame i - 1, byte for byte (margins too)
                 np.testing.assert_array_equal(refs[i][p], finals[i - 1][p], err_msg=f"ref of frame {i} plane {p}")
                 assert refs[i][p].min() >= 0
+
+
+@pytest.mark.parametrize("ctu_rows", [4, 17, 34])
+@pytest.mark.parametrize("band_rows", [1, 2, 3, 4, 17])
+def test_wavefront_schedule_respects_row_dependencies(ctu_rows, band_rows):
+    """The single-rank wavefront (frame_pipeline.wave_delay): frame k's band b runs at step k*d + b.
+    Every (frame, band) runs exactly once, and every reference band a band needs (BandPlan.need) was
+    published in an EARLIER step by the previous frame — band c is published in the step of band
+    c + 1 (its SAO needs the next band's deblocking), the last band in its own step."""
+    from src.x265_amd.frame_pipeline import wave_delay
+
+    plan = BandPlan(ctu_rows=ctu_rows, band_rows=band_rows)
+    nb, d, F = plan.nbands, wave_delay(plan), 6
+    step = {(k, b): k * d + b for k in range(F) for b in range(nb)}
+    pub = {(k, c): step[(k, min(c + 1, nb - 1))] for k in range(F) for c in range(nb)}
+    assert len(set(step.items())) == F * nb
+    for k in range(1, F):
+        for b in range(nb):
+            assert pub[(k - 1, plan.need(b))] < step[(k, b)], (k, b, d)
+    # and d is the smallest such delay
+    if d > 1:
+        d2 = d - 1
+        assert any(k * d2 + b <= (k - 1) * d2 + min(plan.need(b) + 1, nb - 1)
+                   for k in range(1, F) for b in range(nb))
