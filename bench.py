@@ -366,7 +366,7 @@ def main():
     world, rank, local = dist_setup(args)
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs the MI355X (no CPU fallback)")
-    from src.x265_amd import Primitives
+    from src.x265_amd import Primitives, capture_graph
     from src.x265_amd.workload import FrameSet, WorkloadBuilder, census_batches, group_launches
 
     prims = Primitives(device=local)
@@ -455,7 +455,7 @@ def main():
                     kernels()
                 torch.cuda.current_stream().wait_stream(s)
                 graph = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(graph):
+                with capture_graph(graph):
                     kernels()
                 graph.replay()
                 torch.cuda.synchronize()

@@ -45,7 +45,8 @@ enum
 {
     X265AMD_OK = 0,
     X265AMD_EINVAL = 1000,   /* unsupported op / shape / depth */
-    X265AMD_ENODEV = 1001    /* no gfx950 device */
+    X265AMD_ENODEV = 1001,   /* no gfx950 device */
+    X265AMD_ENOMEM = 1002    /* device / pinned staging allocation failed */
 };
 
 /* ----------------------------------------------------------------- runtime */

@@ -268,6 +268,16 @@ extern "C" {
 int x265amd_setup_primitives(void* table, int depth, int* overridden);
 /* sizeof(EncoderPrimitives) this library was built with (15008 on x86-64) */
 size_t x265amd_primitives_size(void);
+/* Sticky status of the per-call provider.  x265's primitives have no error
+ * channel (primitives.h:113-199 return void / a value), so the provider records
+ * the FIRST failure of any call it served (a HIP status of a copy, launch or
+ * synchronisation, or X265AMD_ENOMEM for a host thread whose staging buffers
+ * could not be allocated), returns zeroed outputs from then on, and the caller
+ * maps a non-zero status onto x265_encoder_encode() < 0 (x265.h:1351-1359), as
+ * oracle/hip_encoder_main.cpp does.  0 while every call succeeded. */
+int x265amd_provider_status(void);
+/* Clears the sticky status (tests). */
+void x265amd_provider_clear_status(void);
 }
 
 #endif /* X265_AMD_PRIMITIVES_H */

@@ -17,6 +17,14 @@
  *   X265AMD_PROVIDER=hip  (default) MI355X provider
  *
  * Prints "[x265hip] provider=<c|hip> entries=<n>" on stderr before encoding.
+ *
+ * Error channel: the provider keeps the first failure of any call in a sticky
+ * status (x265amd_provider_status, include/x265_amd_primitives.h).  The CLI gets
+ * its API table from x265_api_get (x265.cpp:219-223); this binary is linked with
+ * -Wl,--wrap=x265_api_get_79, so the table it gets is the reference's with
+ * encoder_encode wrapped: a non-zero provider status turns the call into the
+ * documented failure, x265_encoder_encode() < 0 (x265.h:1351-1359), and the CLI
+ * aborts with exit code 4 (x265.cpp:643-649, 677-681).
  */
 #include "common.h"
 #include "primitives.h"
@@ -27,6 +35,37 @@
 
 extern "C" int x265amd_setup_primitives(void* table, int depth, int* overridden);
 extern "C" const char* x265amd_strerror(int status);
+extern "C" int x265amd_provider_status(void);
+
+extern "C" const x265_api* __real_x265_api_get_79(int bitDepth);
+
+namespace {
+x265_api g_api;
+int (*g_encode)(x265_encoder*, x265_nal**, uint32_t*, x265_picture*, x265_picture*);
+
+int checked_encode(x265_encoder* enc, x265_nal** pp_nal, uint32_t* pi_nal, x265_picture* in, x265_picture* out)
+{
+    int n = g_encode(enc, pp_nal, pi_nal, in, out);
+    int st = x265amd_provider_status();
+    if (st)
+    {
+        fprintf(stderr, "[x265hip] MI355X provider failed: %s (status %d); x265_encoder_encode -> -1\n",
+                x265amd_strerror(st), st);
+        return -1;
+    }
+    return n;
+}
+}
+
+extern "C" const x265_api* __wrap_x265_api_get_79(int bitDepth)
+{
+    const x265_api* api = __real_x265_api_get_79(bitDepth);
+    if (!api) return api;
+    g_api = *api;
+    g_encode = api->encoder_encode;
+    g_api.encoder_encode = checked_encode;
+    return &g_api;
+}
 
 using namespace X265_NS;
 

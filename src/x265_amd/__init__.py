@@ -3,4 +3,4 @@
 The product is the C-ABI shared library libx265amd.so (include/x265_amd.h)
 built from csrc/*.hip; this package only builds and binds it.
 """
-from .native import LIB_PATH, Primitives, X265AmdError  # noqa: F401
+from .native import LIB_PATH, Primitives, X265AmdError, capture_graph  # noqa: F401

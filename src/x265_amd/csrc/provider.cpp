@@ -10,10 +10,22 @@
 // (batch of one, zero offsets), and the outputs are copied back into the
 // caller's strided buffers.  Staging and the stream are per host thread, since
 // x265 calls primitives concurrently from its worker pools.
+//
+// Errors: x265's primitives have no error channel, so every HIP status of a
+// round trip (the two copies, the launch's own status, the synchronisation) is
+// checked and the first failure is kept in a sticky process-wide status
+// (x265amd_provider_status); a failed call returns zeroed outputs instead of
+// whatever the staging buffer held, and every later call fails fast.  The
+// caller turns the status into x265_encoder_encode() < 0 (x265.h:1351-1359;
+// oracle/hip_encoder_main.cpp).  Test hooks, read once per process:
+//   X265AMD_FAULT=alloc     every host thread's staging allocation fails
+//   X265AMD_FAULT_AFTER=N   round trip N+1 onwards reports a failed copy
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
+#include <atomic>
 #include <new>
 
 #include "../../../include/x265_amd.h"
@@ -24,6 +36,49 @@ namespace {
 
 constexpr int kDepth = X265_DEPTH;
 constexpr size_t kStage = 4u << 20;
+
+} // namespace
+} // namespace X265_NS
+
+namespace x265amd_provider {
+// one status for both depth builds of the provider (this file is compiled twice)
+#if X265_DEPTH == 8
+std::atomic<int> g_status{0};
+std::atomic<long> g_trips{0};
+#else
+extern std::atomic<int> g_status;
+extern std::atomic<long> g_trips;
+#endif
+
+inline void fail(int st)
+{
+    int zero = 0;
+    g_status.compare_exchange_strong(zero, st);
+}
+
+struct FaultHooks
+{
+    bool alloc = false;
+    long after = -1;
+    FaultHooks()
+    {
+        const char* f = getenv("X265AMD_FAULT");
+        alloc = f && !strcmp(f, "alloc");
+        const char* a = getenv("X265AMD_FAULT_AFTER");
+        if (a) after = atol(a);
+    }
+};
+
+inline const FaultHooks& hooks()
+{
+    static const FaultHooks h;
+    return h;
+}
+} // namespace x265amd_provider
+
+namespace X265_NS {
+namespace {
+using x265amd_provider::fail;
 
 struct Ctx
 {
@@ -36,9 +91,15 @@ struct Ctx
     // never destroyed: thread-exit order against the HIP runtime's own teardown is unspecified
     Ctx()
     {
-        ok = hipStreamCreateWithFlags(&st, hipStreamNonBlocking) == hipSuccess &&
+        ok = !x265amd_provider::hooks().alloc && hipStreamCreateWithFlags(&st, hipStreamNonBlocking) == hipSuccess &&
              hipMalloc((void**)&dev, kStage) == hipSuccess &&
              hipHostMalloc((void**)&host, kStage, hipHostMallocDefault) == hipSuccess;
+        if (!ok)
+        {
+            // a failed thread still answers calls (with zeroed outputs) from a plain host buffer
+            host = (uint8_t*)calloc(1, kStage);
+            fail(X265AMD_ENOMEM);
+        }
     }
     void reset() { used = 0; }
     size_t alloc(size_t bytes)
@@ -75,14 +136,26 @@ size_t stage_value(Ctx& c, T v)
     return off;
 }
 
-// upload everything staged so far, run `launch`, download [out_off, out_off+out_bytes)
+// upload everything staged so far, run `launch` (returns the C ABI status), download
+// [out_off, out_off+out_bytes).  On any failure — or once an earlier call failed — the
+// output window is zeroed and the first failure stays in the sticky status.
 template <typename F>
 void round_trip(Ctx& c, F launch, size_t out_off, size_t out_bytes)
 {
-    (void)hipMemcpyAsync(c.dev, c.host, c.used, hipMemcpyHostToDevice, c.st);
-    launch();
-    (void)hipMemcpyAsync(c.host + out_off, c.dev + out_off, out_bytes, hipMemcpyDeviceToHost, c.st);
-    (void)hipStreamSynchronize(c.st);
+    using namespace x265amd_provider;
+    int st = g_status.load(std::memory_order_relaxed);
+    if (!st && !c.ok) st = X265AMD_ENOMEM;
+    if (!st && hooks().after >= 0 && g_trips.fetch_add(1) >= hooks().after) st = (int)hipErrorInvalidValue;
+    if (!st) st = (int)hipMemcpyAsync(c.dev, c.host, c.used, hipMemcpyHostToDevice, c.st);
+    if (!st) st = launch();
+    if (!st) st = (int)hipMemcpyAsync(c.host + out_off, c.dev + out_off, out_bytes, hipMemcpyDeviceToHost, c.st);
+    if (!st) st = (int)hipStreamSynchronize(c.st);
+    if (st)
+    {
+        fail(st);
+        if (c.ok) (void)hipStreamSynchronize(c.st);   // nothing of this call may still be in flight
+        memset(c.host + out_off, 0, out_bytes);
+    }
 }
 
 template <typename T>
@@ -103,7 +176,7 @@ int64_t cmp_call(const T* a, intptr_t sa, const T* b, intptr_t sb)
     const size_t ob = b ? stage(c, b, sb, W, H) : oa;
     const size_t out = c.alloc(8);
     round_trip(c, [&] {
-        x265amd_pixelcmp(OP, kDepth, W, H, 1, c.d<T>(oa), W, c.d<int64_t>(z), c.d<T>(ob), W, c.d<int64_t>(z),
+        return x265amd_pixelcmp(OP, kDepth, W, H, 1, c.d<T>(oa), W, c.d<int64_t>(z), c.d<T>(ob), W, c.d<int64_t>(z),
                          c.dev + out, c.st);
     }, out, 8);
     const bool wide = OP == X265AMD_SSE_PP || OP == X265AMD_SSE_SS || OP == X265AMD_SSD_S || OP == X265AMD_VAR;
@@ -146,7 +219,7 @@ void sad_multi(const pixel* f, const pixel* const* r, intptr_t rs, int32_t* res)
     for (int k = 0; k < NREF; k++) c.h<int64_t>(ro)[k] = (int64_t)k * W * H;
     const size_t out = c.alloc(4 * NREF);
     round_trip(c, [&] {
-        x265amd_sad_multi(NREF, kDepth, W, H, 1, c.d<pixel>(of), W, c.d<int64_t>(z), c.d<pixel>(refs), W,
+        return x265amd_sad_multi(NREF, kDepth, W, H, 1, c.d<pixel>(of), W, c.d<int64_t>(z), c.d<pixel>(refs), W,
                           c.d<int64_t>(ro), c.d<int32_t>(out), c.st);
     }, out, 4 * NREF);
     memcpy(res, c.h<int32_t>(out), 4 * NREF);
@@ -186,7 +259,7 @@ void filt_call(const S* src, intptr_t ss, D* dst, intptr_t ds, int W, int H, int
     const size_t os = stage(c, src - ly * ss - lx, ss, sw, sh);
     const size_t od = c.alloc(sizeof(D) * W * oh);
     round_trip(c, [&] {
-        x265amd_interp(OP, N, kDepth, W, H, 1, c.d<S>(os), sw, c.d<int64_t>(z), c.d<D>(od), W, c.d<int64_t>(zd),
+        return x265amd_interp(OP, N, kDepth, W, H, 1, c.d<S>(os), sw, c.d<int64_t>(z), c.d<D>(od), W, c.d<int64_t>(zd),
                        c.d<uint8_t>(cf), rowext, c.st);
     }, od, sizeof(D) * W * oh);
     // hps with row extension writes H+N-1 rows starting at dst, the first of them being source
@@ -214,7 +287,7 @@ void tr_call(const int16_t* src, int16_t* dst, intptr_t stride)
     const size_t os = fwd ? stage(c, src, stride, N, N) : stage(c, src, N, N, N);
     const size_t od = c.alloc(2 * N * N);
     round_trip(c, [&] {
-        x265amd_transform(KIND, kDepth, N, 1, c.d<int16_t>(os), N, c.d<int64_t>(z), c.d<int16_t>(od), N,
+        return x265amd_transform(KIND, kDepth, N, 1, c.d<int16_t>(os), N, c.d<int64_t>(z), c.d<int16_t>(od), N,
                           c.d<int64_t>(z), c.st);
     }, od, 2 * N * N);
     scatter(c, od, dst, fwd ? N : stride, N, N);
@@ -235,7 +308,7 @@ uint32_t quant_call(const int16_t* coef, const int32_t* qc, int32_t* deltaU, int
     const size_t out = c.alloc(2 * num + 4 * num + 4);
     const size_t odl = out + 2 * num, osig = out + 6 * num;
     round_trip(c, [&] {
-        x265amd_quant(1, num, c.d<int16_t>(oc), c.d<int64_t>(z), c.d<int32_t>(oq), c.d<int64_t>(z),
+        return x265amd_quant(1, num, c.d<int16_t>(oc), c.d<int64_t>(z), c.d<int32_t>(oq), c.d<int64_t>(z),
                       deltaU ? c.d<int32_t>(odl) : nullptr, c.d<int64_t>(z), c.d<int16_t>(out), c.d<int64_t>(z),
                       c.d<int32_t>(qb), c.d<int32_t>(ad), c.d<uint32_t>(osig), c.st);
     }, out, 6 * num + 4);
@@ -263,7 +336,7 @@ void dequant_normal(const int16_t* q, int16_t* coef, int num, int scale, int shi
     const size_t oq = stage(c, q, num, num, 1);
     const size_t out = c.alloc(2 * num);
     round_trip(c, [&] {
-        x265amd_dequant_normal(1, num, c.d<int16_t>(oq), c.d<int64_t>(z), c.d<int16_t>(out), c.d<int64_t>(z),
+        return x265amd_dequant_normal(1, num, c.d<int16_t>(oq), c.d<int64_t>(z), c.d<int16_t>(out), c.d<int64_t>(z),
                                c.d<int32_t>(sc), c.d<int32_t>(sh), c.st);
     }, out, 2 * num);
     memcpy(coef, c.h<int16_t>(out), 2 * num);
@@ -278,7 +351,7 @@ void dequant_scaling(const int16_t* q, const int32_t* dq, int16_t* coef, int num
     const size_t oq = stage(c, q, num, num, 1), od = stage(c, dq, num, num, 1);
     const size_t out = c.alloc(2 * num);
     round_trip(c, [&] {
-        x265amd_dequant_scaling(1, num, c.d<int16_t>(oq), c.d<int64_t>(z), c.d<int32_t>(od), c.d<int64_t>(z),
+        return x265amd_dequant_scaling(1, num, c.d<int16_t>(oq), c.d<int64_t>(z), c.d<int32_t>(od), c.d<int64_t>(z),
                                 c.d<int16_t>(out), c.d<int64_t>(z), c.d<int32_t>(pp), c.d<int32_t>(sh), c.st);
     }, out, 2 * num);
     memcpy(coef, c.h<int16_t>(out), 2 * num);
@@ -293,7 +366,7 @@ void denoise(int16_t* coef, uint32_t* res_sum, const uint16_t* offset, int num)
     const size_t oc = stage(c, (const int16_t*)coef, num, num, 1);
     const size_t orr = stage(c, (const uint32_t*)res_sum, num, num, 1);
     round_trip(c, [&] {
-        x265amd_denoise_dct(1, num, c.d<int16_t>(oc), c.d<int64_t>(z), c.d<uint32_t>(orr), c.d<uint16_t>(oo), c.st);
+        return x265amd_denoise_dct(1, num, c.d<int16_t>(oc), c.d<int64_t>(z), c.d<uint32_t>(orr), c.d<uint16_t>(oo), c.st);
     }, oc, orr + 4 * num - oc);
     memcpy(coef, c.h<int16_t>(oc), 2 * num);
     memcpy(res_sum, c.h<uint32_t>(orr), 4 * num);
@@ -316,7 +389,7 @@ void intra_pred(pixel* dst, intptr_t ds, const pixel* src, int mode, int bFilter
     const size_t on = stage(c, src, 4 * N + 1, 4 * N + 1, 1);
     const size_t od = c.alloc(sizeof(pixel) * N * N);
     round_trip(c, [&] {
-        x265amd_intra_pred(kDepth, N, 1, c.d<pixel>(od), N, c.d<int64_t>(z), c.d<pixel>(on), c.d<int64_t>(z),
+        return x265amd_intra_pred(kDepth, N, 1, c.d<pixel>(od), N, c.d<int64_t>(z), c.d<pixel>(on), c.d<int64_t>(z),
                            c.d<uint8_t>(om), c.d<uint8_t>(ob), c.st);
     }, od, sizeof(pixel) * N * N);
     scatter(c, od, dst, ds, N, N);
@@ -331,7 +404,7 @@ void intra_filter(const pixel* src, pixel* filt)
     const size_t on = stage(c, src, 4 * N + 1, 4 * N + 1, 1);
     const size_t od = c.alloc(sizeof(pixel) * (4 * N + 1));
     round_trip(c, [&] {
-        x265amd_intra_filter(kDepth, N, 1, c.d<pixel>(on), c.d<int64_t>(z), c.d<pixel>(od), c.d<int64_t>(z), c.st);
+        return x265amd_intra_filter(kDepth, N, 1, c.d<pixel>(on), c.d<int64_t>(z), c.d<pixel>(od), c.d<int64_t>(z), c.st);
     }, od, sizeof(pixel) * (4 * N + 1));
     memcpy(filt, c.h<pixel>(od), sizeof(pixel) * (4 * N + 1));
 }
@@ -348,7 +421,7 @@ void allangs(pixel* dst, pixel* ref, pixel* filt, int bLuma)
     const size_t oft = stage(c, (const pixel*)filt, 4 * N + 1, 4 * N + 1, 1);
     const size_t od = c.alloc(sizeof(pixel) * 33 * N * N);
     round_trip(c, [&] {
-        x265amd_intra_allangs(kDepth, N, 1, c.d<pixel>(od), c.d<int64_t>(z), c.d<pixel>(orf), c.d<int64_t>(z),
+        return x265amd_intra_allangs(kDepth, N, 1, c.d<pixel>(od), c.d<int64_t>(z), c.d<pixel>(orf), c.d<int64_t>(z),
                               c.d<pixel>(oft), c.d<int64_t>(z), c.d<uint8_t>(ob), c.st);
     }, od, sizeof(pixel) * 33 * N * N);
     memcpy(dst, c.h<pixel>(od), sizeof(pixel) * 33 * N * N);
@@ -367,7 +440,7 @@ void bo_call(D* dst, intptr_t ds, const A* a, intptr_t sa, const B* b, intptr_t 
     const size_t ob = b ? stage(c, b, sb, W, H) : z;
     const size_t od = c.alloc(sizeof(D) * W * H);
     round_trip(c, [&] {
-        x265amd_blockop(OP, kDepth, W, H, 1, c.d<D>(od), W, c.d<int64_t>(z), a ? c.d<A>(oa) : nullptr, W,
+        return x265amd_blockop(OP, kDepth, W, H, 1, c.d<D>(od), W, c.d<int64_t>(z), a ? c.d<A>(oa) : nullptr, W,
                         c.d<int64_t>(z), b ? c.d<B>(ob) : nullptr, W, c.d<int64_t>(z), param, c.st);
     }, od, sizeof(D) * W * H);
     scatter(c, od, dst, ds, W, H);
@@ -430,7 +503,7 @@ uint32_t count_call(int16_t* coeff, const int16_t* res, intptr_t rs)
     const size_t orr = res ? stage(c, res, rs, N, N) : z;
     const size_t out = c.alloc(4);
     round_trip(c, [&] {
-        x265amd_count_nonzero(N, 1, c.d<int16_t>(oc), c.d<int64_t>(z), res ? c.d<int16_t>(orr) : nullptr, N,
+        return x265amd_count_nonzero(N, 1, c.d<int16_t>(oc), c.d<int64_t>(z), res ? c.d<int16_t>(orr) : nullptr, N,
                               c.d<int64_t>(z), c.d<uint32_t>(out), c.st);
     }, oc, out + 4 - oc);
     if (res) memcpy(coeff, c.h<int16_t>(oc), 2 * N * N);
@@ -560,7 +633,9 @@ void chroma_cu(EncoderPrimitives::Chroma::CUChroma& u)
 void setupHipPrimitives(EncoderPrimitives& p, int /*cpuMask*/)
 {
     g_count = 0;
-    if (x265amd_set_device(0) != 0 || !ctx().ok) return;
+    // staging is per host thread and created on a thread's first call; a thread whose staging
+    // cannot be allocated records X265AMD_ENOMEM in the sticky status (see round_trip)
+    if (x265amd_set_device(0) != 0) return;
     enum { I420 = 1, I422 = 2, I444 = 3 };
 #define X(P, W, H)                                                     \
     luma_pu<W, H>(p.pu[P]);                                            \
@@ -629,5 +704,16 @@ extern "C" int x265amd_setup_primitives(void* table, int depth, int* overridden)
 extern "C" size_t x265amd_primitives_size(void)
 {
     return sizeof(x265::EncoderPrimitives);
+}
+
+extern "C" int x265amd_provider_status(void)
+{
+    return x265amd_provider::g_status.load();
+}
+
+extern "C" void x265amd_provider_clear_status(void)
+{
+    x265amd_provider::g_status.store(0);
+    x265amd_provider::g_trips.store(0);
 }
 #endif

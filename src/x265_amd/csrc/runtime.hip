@@ -39,6 +39,7 @@ extern "C" const char* x265amd_strerror(int status)
     case X265AMD_OK: return "success";
     case X265AMD_EINVAL: return "x265amd: unsupported primitive, block shape or bit depth";
     case X265AMD_ENODEV: return "x265amd: no gfx950 (MI355X) device";
+    case X265AMD_ENOMEM: return "x265amd: device or pinned staging allocation failed";
     default: return hipGetErrorString((hipError_t)status);
     }
 }

@@ -29,6 +29,7 @@ import ctypes
 
 import numpy as np
 
+from .native import capture_graph
 from .pipeline import BandPlan, RowExchange, run_frames
 from .workload import (CENSUS_1080P, FrameSet, WorkloadBuilder, census_batches, group_launches, load_census)
 
@@ -350,7 +351,7 @@ class GpuFramePipeline:
         torch.cuda.synchronize()
         if one_graph and self.world == 1:
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
+            with capture_graph(g):
                 self._eager_step()
             self.graphs["step"] = g
             torch.cuda.synchronize()
@@ -358,7 +359,7 @@ class GpuFramePipeline:
         for k in range(self.F):
             for b in range(self.plan.nbands):
                 g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g):
+                with capture_graph(g):
                     self.band_work(k, b)
                 self.graphs[(k, b)] = g
         torch.cuda.synchronize()
@@ -390,7 +391,7 @@ class GpuFramePipeline:
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        with capture_graph(g):
             self._wave_all()
         self.graphs = {"wave": g}
         torch.cuda.synchronize()

@@ -121,6 +121,37 @@ class BorderPlane(C.Structure):
                 ("margin_y", _int)]
 
 
+
+class capture_graph:
+    """torch.cuda.graph(g) with Python's cyclic GC held off for the capture.
+
+    A dead reference cycle that owns CUDA graphs or tensors (e.g. a discarded
+    GpuFramePipeline, whose lambdas reference itself) must not be collected while a
+    stream is capturing: freeing a graph's private pool there calls hipFree inside
+    the capture and aborts the process.  Collect first, then capture with GC off."""
+
+    def __init__(self, g):
+        import torch
+
+        self._ctx = torch.cuda.graph(g)
+
+    def __enter__(self):
+        import gc
+
+        gc.collect()
+        self._was = gc.isenabled()
+        gc.disable()
+        return self._ctx.__enter__()
+
+    def __exit__(self, *exc):
+        import gc
+
+        try:
+            return self._ctx.__exit__(*exc)
+        finally:
+            if self._was:
+                gc.enable()
+
 def _addr(t):
     return None if t is None else t.data_ptr()
 

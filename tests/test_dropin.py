@@ -115,3 +115,38 @@ def test_reference_encoder_on_hip_provider_is_bit_exact(tmp_path, depth):
           f"MI355X per-call provider {h_fps} fps; bitstream md5 {h_bs}")
     assert h_bs == c_bs, "bitstream differs between the C table and the MI355X provider"
     assert h_rec == c_rec, "reconstructed frames differ"
+
+
+def _run_enc(exe, src, depth, out_dir, env_extra, timeout=600):
+    env = dict(os.environ, **env_extra)
+    cmd = [exe, "--input", str(src), "--input-res", f"{W}x{H}", "--input-depth", str(depth), "--frames",
+           str(FRAMES), *ENC_ARGS, "-o", str(out_dir / "o.hevc")]
+    return subprocess.run(cmd, capture_output=True, text=True, env=env, timeout=timeout)
+
+
+def test_encoder_fails_loudly_without_device(tmp_path):
+    """(no GPU) the provider cannot be installed: the encoder refuses to run (non-zero exit,
+    the library's message) instead of silently encoding on the C table"""
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("a device is present")
+    src = _source(tmp_path, 8)
+    r = _run_enc(_bin("x265hip8"), src, 8, tmp_path, {"X265AMD_PROVIDER": "hip"})
+    assert r.returncode != 0
+    assert "x265amd_setup_primitives failed" in r.stderr, r.stderr[-2000:]
+    assert not (tmp_path / "o.hevc").exists() or (tmp_path / "o.hevc").stat().st_size == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fault", [{"X265AMD_FAULT": "alloc"}, {"X265AMD_FAULT_AFTER": "2000"}],
+                         ids=["staging-alloc", "copy-after-2000-calls"])
+def test_provider_failure_fails_the_encode(tmp_path, fault):
+    """A failing staging allocation / device copy inside the per-call provider must surface as
+    x265_encoder_encode() < 0 (x265.h:1351-1359), i.e. the CLI's exit code 4
+    (x265.cpp:643-649), not as garbage primitive results in a 'successful' encode"""
+    src = _source(tmp_path, 8)
+    r = _run_enc(_bin("x265hip8"), src, 8, tmp_path, dict(fault, X265AMD_PROVIDER="hip"), timeout=900)
+    assert r.returncode == 4, (r.returncode, r.stderr[-3000:])
+    assert "MI355X provider failed" in r.stderr, r.stderr[-2000:]
+    assert "x265_encoder_encode -> -1" in r.stderr

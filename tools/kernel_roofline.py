@@ -49,7 +49,7 @@ def main():
 
     import torch
 
-    from src.x265_amd import Primitives
+    from src.x265_amd import Primitives, capture_graph
 
     prims = Primitives(device=0)
     dev = "cuda"
@@ -706,7 +706,7 @@ def main():
             fn()
             torch.cuda.synchronize()
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
+            with capture_graph(g):
                 fn()
             return timeit(g.replay)
 
