@@ -469,6 +469,55 @@ typedef struct
 } x265amd_lowres_bcost_batch;
 int x265amd_lowres_bcost(int depth, const x265amd_lowres_bcost_batch* batch, void* stream);
 
+/* f1 encoder session: the lookahead cost estimates of a RUNNING x265 encoder on the device
+ * (the reference-side hook is integration/gpu_lookahead.cpp).  Unlike the
+ * entries above, these take HOST pointers and are synchronous: they sit under
+ *   LookaheadTLD::lowresIntraEstimate(Lowres&)                      slicetype.cpp:230-336
+ *   CostEstimateGroup::estimateFrameCost(tld, p0, p1, b, penalty)   slicetype.cpp:1977-2066
+ * whose results the encoder reads right after the call.  A session owns device slots for the
+ * pictures' lowres planes: x265amd_la_load uploads a Lowres buffer (lowres.cpp:30-163 layout:
+ * 4 planes of `planesize` pixels, lowresPlane[k] = buffer + k * planesize + padoffset) once, keyed
+ * by any unique host address (the Lowres*), and every later estimate that reads the picture uses
+ * the device copy; the intra estimate keeps the picture's intraCost on the device for its P
+ * estimates.  Thread-safe: x265 calls them from its pre-lookahead and batch workers at once; each
+ * host thread gets its own stream, scratch and weighted-plane slot.  Errors are returned and
+ * recorded in the backend's sticky status (x265amd_provider_status). */
+typedef struct x265amd_la x265amd_la;
+typedef struct
+{
+    int depth;
+    int width_cu, height_cu;       /* Lowres::maxBlocksInRow / maxBlocksInCol */
+    intptr_t lowres_stride;        /* Lowres::lumaStride */
+    int64_t planesize, padoffset;  /* elements */
+    int max_frames;                /* device picture slots (distinct keys) */
+    int max_threads;               /* distinct host threads calling the session */
+    const uint16_t* mvcost;        /* HOST BitCost table of X265_LOOKAHEAD_QP at difference 0 */
+    int mvcost_range;              /* entries [-range, range] are copied */
+} x265amd_la_config;
+int  x265amd_la_create(const x265amd_la_config* cfg, x265amd_la** out);
+void x265amd_la_destroy(x265amd_la* la);
+/* (re)load picture `key` (generation gen = Lowres::frameNum): its 4 planes and, with AQ, its
+ * invQscaleFactor (ncu int32; NULL without AQ) */
+int x265amd_la_load(x265amd_la* la, const void* key, int gen, const void* buffer, const int32_t* inv_qscale);
+/* lowresIntraEstimate of a loaded picture: intraCost, intraMode, lowresCosts[0][0], rowSatds[0][0],
+ * cost_est[0..1] = costEst[0][0] / costEstAq[0][0] */
+int x265amd_la_intra(x265amd_la* la, const void* key, int32_t* intra_cost, uint8_t* intra_mode,
+                     uint16_t* lowres_cost, int32_t* row_satd, int64_t* cost_est);
+/* P estimate (b == p1) of picture fenc from ref (list-0 search always on): weighted_buffer = the
+ * 4-plane weighted reference of weightsAnalyse (LookaheadTLD::wbuffer[0]) or NULL; coop-slice
+ * geometry as estimateFrameCost chooses it (num_slices <= 1: the whole frame).  Outputs as
+ * x265amd_lowres_pcost: lowresMvs[0][b-p0-1], lowresMvCosts[0][b-p0-1], lowresCosts[b-p0][0],
+ * rowSatds[b-p0][0], the raw sums costEst / costEstAq, and the count of intra CUs. */
+int x265amd_la_pcost(x265amd_la* la, const void* fenc, const void* ref, const void* weighted_buffer,
+                     int rows_per_slice, int num_slices, int16_t* mvs, int32_t* mv_costs, uint16_t* lowres_costs,
+                     int32_t* row_satd, int64_t* cost_est, int32_t* intra_mbs);
+/* B estimate (p0 < b < p1): a list is searched when do_search<l>, else its mvs / mv_costs are
+ * read; outputs as x265amd_lowres_bcost (searched lists' mvs / mv_costs written back). */
+int x265amd_la_bcost(x265amd_la* la, const void* fenc, const void* ref0, const void* ref1, int do_search0,
+                     int do_search1, int rows_per_slice, int num_slices, int16_t* mvs0, int32_t* mv_costs0,
+                     int16_t* mvs1, int32_t* mv_costs1, uint16_t* lowres_costs, int32_t* row_satd,
+                     int64_t* cost_est);
+
 /* f1 cuTree: Lookahead::estimateCUPropagate (slicetype.cpp:1738-1836) with the
  * propagateCost primitive (pixel.cpp:846-872), one call of it per batch, batches in order.
  * For every lowres CU of frame b: the amount

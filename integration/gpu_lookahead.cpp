@@ -1,0 +1,403 @@
+/* gpu_lookahead.cpp — reference-side binding: x265 1.9's lookahead cost estimates run on
+ * the MI355X through the f1 session entries of include/x265_amd.h (x265amd_la_*).
+ *
+ * This is the hook a maintainer adds to the encoder.  It replaces two
+ * functions of encoder/slicetype.cpp; oracle/Makefile links the reference encoder with a
+ * copy of slicetype.o in which exactly those two symbols are weak (objcopy -W) and the
+ * original code stays reachable under an alias (objcopy --add-symbol), so every call site —
+ * PreLookaheadGroup::processTasks, CostEstimateGroup::singleCost / processTasks, all through
+ * the PLT (the Makefile checks the relocations) — lands here:
+ *
+ *   LookaheadTLD::lowresIntraEstimate(Lowres&)                          slicetype.cpp:230-336
+ *     -> x265amd_la_load (the picture's 4 lowres planes + invQscaleFactor, once) and
+ *        x265amd_la_intra, outputs written into the Lowres;
+ *   CostEstimateGroup::estimateFrameCost(tld, p0, p1, b, bIntraPenalty) slicetype.cpp:1977-2066
+ *     -> the reference's control flow unchanged (cost cache test, bDoSearch from the
+ *        lowresMvs sentinel, weightsAnalyse on the host, the coop-slice geometry of
+ *        m_numRowsPerSlice / m_numCoopSlices in non-batch mode, the B-frame bias and the
+ *        intra penalty); the per-CU work (estimateCUCost over the frame, :2068-2225) is ONE
+ *        device call, x265amd_la_pcost (b == p1) or x265amd_la_bcost.
+ *
+ * Two cases the device estimate does not cover run the reference's own estimateCUCost on
+ * the calling thread, in the reference's CU and slice order: a P estimate whose list-0 MVs
+ * already exist (bDoSearch[0] false) and a B estimate whose list-0 reference was weighted
+ * (the device B estimate reads p0 unweighted).  Results are bit-identical either way, so the
+ * bitstream equals the reference encoder's (tests/test_encoder_lookahead.py).
+ *
+ *   X265AMD_LOOKAHEAD=cpu    every call goes to the reference's original functions (same binary)
+ *   X265AMD_LOOKAHEAD=host   this hook's control flow with the CPU per-CU loops only (no device):
+ *                            checks the restated control flow against the reference on a CPU host
+ *
+ * Errors: a failing device call is recorded in the backend's sticky status; the returned
+ * estimate is then meaningless and the encoder binding (hip_encoder_main.cpp) turns the status
+ * into x265_encoder_encode() < 0.
+ */
+#include "common.h"
+#include "primitives.h"
+#include "lowres.h"
+#include "slicetype.h"
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <pthread.h>
+
+#include "../include/x265_amd.h"
+
+using namespace X265_NS;
+
+/* the reference's own implementations (aliases of the weakened symbols, see oracle/Makefile) */
+extern "C" void x265ref_lowresIntraEstimate(LookaheadTLD* self, Lowres* fenc);
+extern "C" int64_t x265ref_estimateFrameCost(CostEstimateGroup* self, LookaheadTLD* tld, int p0, int p1, int b,
+                                             bool bIntraPenalty);
+
+namespace {
+
+struct TabBitCost : public BitCost
+{
+    const uint16_t* table(unsigned qp) { setQP(qp); return m_cost; }
+};
+
+enum { MODE_GPU = 0, MODE_CPU = 1, MODE_HOST = 2, MODE_CHECK = 3 };
+
+int g_mode = MODE_GPU;
+x265amd_la* g_la = NULL;
+int g_la_status = 0;
+pthread_mutex_t g_mu = PTHREAD_MUTEX_INITIALIZER;
+pthread_once_t g_mode_once = PTHREAD_ONCE_INIT;
+
+void print_check_summary();
+
+void read_mode()
+{
+    const char* m = getenv("X265AMD_LOOKAHEAD");
+    g_mode = (m && !strcmp(m, "cpu")) ? MODE_CPU : (m && !strcmp(m, "host")) ? MODE_HOST :
+             (m && !strcmp(m, "check")) ? MODE_CHECK : MODE_GPU;
+    fprintf(stderr, "[x265la] lookahead estimates on %s\n", g_mode == MODE_CPU ? "the CPU (reference functions)" :
+            g_mode == MODE_HOST ? "the CPU (hook control flow)" :
+            g_mode == MODE_CHECK ? "the MI355X, each checked against the CPU" : "the MI355X");
+    if (g_mode == MODE_CHECK)
+        atexit(print_check_summary);
+}
+
+/* the session, created on the first call from the first Lowres (all pictures of an encoder
+ * share the geometry) */
+x265amd_la* session(const Lowres& f)
+{
+    pthread_mutex_lock(&g_mu);
+    if (!g_la && !g_la_status)
+    {
+        x265amd_la_config c;
+        memset(&c, 0, sizeof(c));
+        c.depth = X265_DEPTH;
+        c.width_cu = (int)f.maxBlocksInRow;
+        c.height_cu = (int)f.maxBlocksInCol;
+        c.lowres_stride = f.lumaStride;
+        c.planesize = f.buffer[1] - f.buffer[0];
+        c.padoffset = f.lowresPlane[0] - f.buffer[0];
+        c.max_frames = 256;          // distinct Lowres objects of one encoder (its Frame pool)
+        c.max_threads = 128;         // pool workers + API / lookahead threads
+        TabBitCost bc;
+        c.mvcost = bc.table(X265_LOOKAHEAD_QP);
+        c.mvcost_range = 1 << 14;    // > every qpel MV difference of a 2160p lowres search
+        g_la_status = x265amd_la_create(&c, &g_la);
+        if (g_la_status)
+            fprintf(stderr, "[x265la] x265amd_la_create failed: %s\n", x265amd_strerror(g_la_status));
+    }
+    x265amd_la* la = g_la;
+    pthread_mutex_unlock(&g_mu);
+    return la;
+}
+
+void report(const char* what, int st)
+{
+    if (st) fprintf(stderr, "[x265la] %s failed: %s\n", what, x265amd_strerror(st));
+}
+
+int g_mismatches = 0;
+
+int ncu_of(const Lowres& f) { return (int)(f.maxBlocksInRow * f.maxBlocksInCol); }
+
+void print_check_summary()
+{
+    fprintf(stderr, "[x265la] check: %d mismatching estimates\n", g_mismatches);
+}
+
+/* X265AMD_LOOKAHEAD=check: scratch outputs of one device estimate and their comparison with the
+ * reference's results in the Lowres (first mismatches printed, count kept) */
+struct CheckBufs
+{
+    int ncu = 0, hcu = 0;
+    MV* mvs[2] = { NULL, NULL };
+    int32_t* mvc[2] = { NULL, NULL };
+    uint16_t* lc = NULL;
+    int32_t* rs = NULL;
+    void init(int n, int h, MV* const src_mvs[2], int32_t* const src_mvc[2])
+    {
+        ncu = n;
+        hcu = h;
+        for (int l = 0; l < 2; l++)
+        {
+            mvs[l] = (MV*)malloc(sizeof(MV) * n);
+            mvc[l] = (int32_t*)malloc(sizeof(int32_t) * n);
+            if (src_mvs[l]) memcpy(mvs[l], src_mvs[l], sizeof(MV) * n);   /* inputs of an unsearched list */
+            if (src_mvc[l]) memcpy(mvc[l], src_mvc[l], sizeof(int32_t) * n);
+        }
+        lc = (uint16_t*)malloc(2 * n);
+        rs = (int32_t*)malloc(4 * h);
+    }
+    ~CheckBufs()
+    {
+        for (int l = 0; l < 2; l++) { free(mvs[l]); free(mvc[l]); }
+        free(lc);
+        free(rs);
+    }
+    void compare(int p0, int p1, int b, int ns, const bool ds[2], Lowres* f, const int64_t ce[2], int mbs, int ref_mbs)
+    {
+        char what[256] = "";
+        int first = -1;
+        for (int l = 0; l < 2 && first < 0; l++)
+        {
+            if (!ds[l]) continue;
+            const MV* r = f->lowresMvs[l][l ? p1 - b - 1 : b - p0 - 1];
+            const int32_t* rc = f->lowresMvCosts[l][l ? p1 - b - 1 : b - p0 - 1];
+            for (int i = 0; i < ncu && first < 0; i++)
+                if (r[i].word != mvs[l][i].word || rc[i] != mvc[l][i])
+                {
+                    first = i;
+                    snprintf(what, sizeof(what), "list %d mv/cost at cu %d: ref (%d,%d)/%d dev (%d,%d)/%d", l, i, r[i].x,
+                             r[i].y, rc[i], mvs[l][i].x, mvs[l][i].y, mvc[l][i]);
+                }
+        }
+        const uint16_t* rl = f->lowresCosts[b - p0][p1 - b];
+        for (int i = 0; i < ncu && first < 0; i++)
+            if (rl[i] != lc[i])
+            {
+                first = i;
+                snprintf(what, sizeof(what), "lowresCosts at cu %d: ref %d dev %d", i, rl[i], lc[i]);
+            }
+        const int32_t* rr = f->rowSatds[b - p0][p1 - b];
+        for (int i = 0; i < hcu && first < 0; i++)
+            if (rr[i] != rs[i])
+            {
+                first = i;
+                snprintf(what, sizeof(what), "rowSatds at row %d: ref %d dev %d", i, rr[i], rs[i]);
+            }
+        if (first < 0 && (f->costEst[b - p0][p1 - b] != ce[0] || f->costEstAq[b - p0][p1 - b] != ce[1]))
+        {
+            first = 0;
+            snprintf(what, sizeof(what), "costEst ref %lld/%lld dev %lld/%lld", (long long)f->costEst[b - p0][p1 - b],
+                     (long long)f->costEstAq[b - p0][p1 - b], (long long)ce[0], (long long)ce[1]);
+        }
+        if (first < 0 && p1 == b && mbs != ref_mbs)
+        {
+            first = 0;
+            snprintf(what, sizeof(what), "intraMbs ref %d dev %d", ref_mbs, mbs);
+        }
+        if (first >= 0)
+        {
+            int n = __sync_add_and_fetch(&g_mismatches, 1);
+            if (n <= 20)
+                fprintf(stderr, "[x265la] CHECK MISMATCH estimate (p0 %d, p1 %d, b %d) frame %d, slices %d, search %d/%d: %s\n",
+                        p0, p1, b, f->frameNum, ns, ds[0], ds[1], what);
+        }
+    }
+};
+
+} // namespace
+
+namespace X265_NS {
+
+void LookaheadTLD::lowresIntraEstimate(Lowres& fenc)
+{
+    pthread_once(&g_mode_once, read_mode);
+    if (g_mode == MODE_CPU || g_mode == MODE_HOST)
+    {
+        x265ref_lowresIntraEstimate(this, &fenc);
+        return;
+    }
+    x265amd_la* la = session(fenc);
+    int st = la ? x265amd_la_load(la, &fenc, fenc.frameNum, fenc.buffer[0], fenc.invQscaleFactor) : -1;
+    if (la) report("x265amd_la_load", st);
+    int64_t ce[2];
+    if (!st && g_mode == MODE_CHECK)
+    {
+        const int ncu = ncu_of(fenc), hcu = (int)fenc.maxBlocksInCol;
+        int32_t* ic = (int32_t*)malloc(4 * ncu);
+        uint8_t* im = (uint8_t*)malloc(ncu);
+        uint16_t* lc = (uint16_t*)malloc(2 * ncu);
+        int32_t* rs = (int32_t*)malloc(4 * hcu);
+        st = x265amd_la_intra(la, &fenc, ic, im, lc, rs, ce);
+        report("x265amd_la_intra", st);
+        x265ref_lowresIntraEstimate(this, &fenc);
+        if (!st && (memcmp(ic, fenc.intraCost, 4 * ncu) || memcmp(im, fenc.intraMode, ncu) ||
+                    memcmp(lc, fenc.lowresCosts[0][0], 2 * ncu) || memcmp(rs, fenc.rowSatds[0][0], 4 * hcu) ||
+                    ce[0] != fenc.costEst[0][0] || ce[1] != fenc.costEstAq[0][0]))
+        {
+            __sync_add_and_fetch(&g_mismatches, 1);
+            fprintf(stderr, "[x265la] CHECK MISMATCH intra estimate of frame %d\n", fenc.frameNum);
+        }
+        free(ic); free(im); free(lc); free(rs);
+        return;
+    }
+    if (!st)
+    {
+        st = x265amd_la_intra(la, &fenc, fenc.intraCost, fenc.intraMode, fenc.lowresCosts[0][0], fenc.rowSatds[0][0],
+                              ce);
+        report("x265amd_la_intra", st);
+    }
+    if (st)
+    {
+        /* status recorded: the encode fails; keep the encoder's state valid until it stops */
+        x265ref_lowresIntraEstimate(this, &fenc);
+        return;
+    }
+    fenc.costEst[0][0] = ce[0];
+    fenc.costEstAq[0][0] = ce[1];
+}
+
+int64_t CostEstimateGroup::estimateFrameCost(LookaheadTLD& tld, int p0, int p1, int b, bool bIntraPenalty)
+{
+    pthread_once(&g_mode_once, read_mode);
+    if (g_mode == MODE_CPU)
+        return x265ref_estimateFrameCost(this, &tld, p0, p1, b, bIntraPenalty);
+
+    Lowres*     fenc  = m_frames[b];
+    x265_param* param = m_lookahead.m_param;
+    int64_t     score = 0;
+
+    if (fenc->costEst[b - p0][p1 - b] >= 0 && fenc->rowSatds[b - p0][p1 - b][0] != -1)
+        score = fenc->costEst[b - p0][p1 - b];
+    else
+    {
+        bool bDoSearch[2];
+        bDoSearch[0] = p0 < b && fenc->lowresMvs[0][b - p0 - 1][0].x == 0x7FFF;
+        bDoSearch[1] = p1 > b && fenc->lowresMvs[1][p1 - b - 1][0].x == 0x7FFF;
+
+        fenc->weightedRef[b - p0].isWeighted = false;
+        if (param->bEnableWeightedPred && bDoSearch[0])
+            tld.weightsAnalyse(*m_frames[b], *m_frames[p0]);
+
+        fenc->costEst[b - p0][p1 - b] = 0;
+        fenc->costEstAq[b - p0][p1 - b] = 0;
+
+        /* the reference's choice between cooperative slices and one serial pass (:2007) */
+        const bool coop = !m_batchMode && m_lookahead.m_numCoopSlices > 1 && ((p1 > b) || bDoSearch[0] || bDoSearch[1]);
+        const int rps = coop ? m_lookahead.m_numRowsPerSlice : m_lookahead.m_8x8Height;
+        const int ns = coop ? m_lookahead.m_numCoopSlices : 1;
+        const bool weighted = fenc->weightedRef[b - p0].isWeighted;
+        x265amd_la* la = (g_mode == MODE_GPU || g_mode == MODE_CHECK) ? session(*fenc) : NULL;
+        const bool device = la && ((p1 == b && bDoSearch[0]) || (p1 > b && !weighted));
+
+        /* X265AMD_LOOKAHEAD=check: the device estimate goes to scratch copies, the host loops below
+         * produce the reference's results in the Lowres, and the two are compared */
+        const bool check = g_mode == MODE_CHECK;
+        const int ncu = tld.ncu, hcu = m_lookahead.m_8x8Height;
+        const int d0 = b - p0 - 1, d1 = p1 - b - 1;
+        MV* mvs[2] = { p0 < b ? fenc->lowresMvs[0][d0] : NULL, p1 > b ? fenc->lowresMvs[1][d1] : NULL };
+        int32_t* mvc[2] = { p0 < b ? fenc->lowresMvCosts[0][d0] : NULL, p1 > b ? fenc->lowresMvCosts[1][d1] : NULL };
+        uint16_t* lc = fenc->lowresCosts[b - p0][p1 - b];
+        int32_t* rs = fenc->rowSatds[b - p0][p1 - b];
+        CheckBufs cb;
+        if (check && device)
+        {
+            cb.init(ncu, hcu, mvs, mvc);
+            for (int l = 0; l < 2; l++)
+            {
+                mvs[l] = cb.mvs[l];
+                mvc[l] = cb.mvc[l];
+            }
+            lc = cb.lc;
+            rs = cb.rs;
+        }
+        bool done = false;
+        int64_t ce[2] = { 0, 0 };
+        int32_t mbs = 0;
+        if (device)
+        {
+            /* outputs reach the Lowres only when the device call succeeded; on a failure the
+             * status is recorded (the encode will fail) and the estimate is computed on the host
+             * so the encoder's state stays valid until it stops */
+            int st;
+            if (p1 == b)
+            {
+                st = x265amd_la_pcost(la, fenc, m_frames[p0], weighted ? tld.wbuffer[0] : NULL, rps, ns,
+                                      (int16_t*)mvs[0], mvc[0], lc, rs, ce, &mbs);
+                report("x265amd_la_pcost", st);
+            }
+            else
+            {
+                st = x265amd_la_bcost(la, fenc, m_frames[p0], m_frames[p1], bDoSearch[0], bDoSearch[1], rps, ns,
+                                      (int16_t*)mvs[0], mvc[0], (int16_t*)mvs[1], mvc[1], lc, rs, ce);
+                report("x265amd_la_bcost", st);
+            }
+            if (!st && !check)
+            {
+                if (p1 == b)
+                    fenc->intraMbs[b - p0] += mbs;
+                fenc->costEst[b - p0][p1 - b] = ce[0];
+                fenc->costEstAq[b - p0][p1 - b] = ce[1];
+                done = true;
+            }
+        }
+        const int mbs_before = fenc->intraMbs[b - p0];
+        if (done)
+            ;
+        else if (coop)
+        {
+            /* the reference's cooperative slices (:2012-2037), run here one after another:
+             * slices are independent and their sums commute */
+            memset(&m_slice, 0, sizeof(Slice) * ns);
+            for (int i = 0; i < ns; i++)
+            {
+                const int firstY = rps * i;
+                const int lastY = (i == ns - 1) ? m_lookahead.m_8x8Height - 1 : rps * (i + 1) - 1;
+                bool lastRow = true;
+                for (int cuY = lastY; cuY >= firstY; cuY--)
+                {
+                    fenc->rowSatds[b - p0][p1 - b][cuY] = 0;
+                    for (int cuX = m_lookahead.m_8x8Width - 1; cuX >= 0; cuX--)
+                        estimateCUCost(tld, cuX, cuY, p0, p1, b, bDoSearch, lastRow, i);
+                    lastRow = false;
+                }
+            }
+            for (int i = 0; i < ns; i++)
+            {
+                fenc->costEst[b - p0][p1 - b] += m_slice[i].costEst;
+                fenc->costEstAq[b - p0][p1 - b] += m_slice[i].costEstAq;
+                if (p1 == b)
+                    fenc->intraMbs[b - p0] += m_slice[i].intraMbs;
+            }
+        }
+        else
+        {
+            /* the reference's serial pass (:2041-2050) */
+            bool lastRow = true;
+            for (int cuY = m_lookahead.m_8x8Height - 1; cuY >= 0; cuY--)
+            {
+                fenc->rowSatds[b - p0][p1 - b][cuY] = 0;
+                for (int cuX = m_lookahead.m_8x8Width - 1; cuX >= 0; cuX--)
+                    estimateCUCost(tld, cuX, cuY, p0, p1, b, bDoSearch, lastRow, -1);
+                lastRow = false;
+            }
+        }
+
+        if (check && device)
+            cb.compare(p0, p1, b, ns, bDoSearch, fenc, ce, mbs, fenc->intraMbs[b - p0] - mbs_before);
+
+        score = fenc->costEst[b - p0][p1 - b];
+
+        if (b != p1)
+            score = score * 100 / (130 + param->bFrameBias);
+
+        fenc->costEst[b - p0][p1 - b] = score;
+    }
+
+    if (bIntraPenalty)
+        // arbitrary penalty for I-blocks after B-frames
+        score += score * fenc->intraMbs[b - p0] / (tld.ncu * 8);
+
+    return score;
+}
+
+} // namespace X265_NS

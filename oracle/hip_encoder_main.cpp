@@ -74,7 +74,12 @@ int x265_cli_main(int argc, char** argv);
 int main(int argc, char** argv)
 {
     const char* which = getenv("X265AMD_PROVIDER");
+#ifdef X265AMD_DEFAULT_PROVIDER_C
+    /* x265la: the C table unless the per-call provider is asked for */
+    const bool hip = which && !strcmp(which, "hip");
+#else
     const bool hip = !(which && !strcmp(which, "c"));
+#endif
     EncoderPrimitives& p = primitives;
     setupCPrimitives(p);
     for (int i = 0; i < NUM_TR_SIZE; i++)

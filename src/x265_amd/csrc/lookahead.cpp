@@ -1,0 +1,397 @@
+// lookahead.cpp — f1 encoder session: the lookahead cost estimates of a running x265
+// encoder on the MI355X (include/x265_amd.h, x265amd_la_*).
+//
+// x265's lookahead keeps one Lowres per picture (lowres.cpp:30-163: one host buffer of
+// four half-pel planes, `planesize` pixels each, lowresPlane[k] = buffer + k * planesize
+// + padoffset) and asks for per-picture intra estimates (LookaheadTLD::lowresIntraEstimate,
+// slicetype.cpp:230-336) and per-(p0, p1, b) inter estimates
+// (CostEstimateGroup::estimateFrameCost -> estimateCUCost, slicetype.cpp:1977-2225) from
+// its pre-lookahead and batch worker threads.  A session holds:
+//   * device frame slots — a picture's four planes are uploaded once (x265amd_la_load) and
+//     reused by every estimate that reads it; the intra estimate leaves the picture's
+//     intraCost on the device for its P estimates;
+//   * one arena for all slots, so every batch entry addresses planes as offsets from one
+//     base (the batched x265amd_lowres_* entries' convention);
+//   * per host thread: a non-blocking stream, device scratch for one estimate's outputs,
+//     pinned staging, and an arena slot for weighted reference planes (weightsAnalyse's
+//     wbuffer, slicetype.cpp:391-495, which lives on the calling thread's LookaheadTLD).
+// Every entry is synchronous on the calling thread's stream: the outputs are in the
+// caller's host arrays when it returns.  A failure is returned AND recorded in the
+// backend's sticky status (x265amd_provider_status), which the encoder binding turns into
+// x265_encoder_encode() < 0.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <atomic>
+#include <mutex>
+#include <new>
+#include <unordered_map>
+#include <vector>
+
+#include "../../../include/x265_amd.h"
+
+namespace x265amd_provider {
+extern std::atomic<int> g_status;
+}
+
+namespace {
+
+int record(int st)
+{
+    if (st)
+    {
+        int zero = 0;
+        x265amd_provider::g_status.compare_exchange_strong(zero, st);
+    }
+    return st;
+}
+
+#define LA_TRY(expr)                                   \
+    do                                                 \
+    {                                                  \
+        int st_ = (int)(expr);                         \
+        if (st_) return record(st_);                   \
+    } while (0)
+
+} // namespace
+
+struct x265amd_la_thread
+{
+    hipStream_t st = nullptr;
+    uint8_t* dev = nullptr;     // scratch: outputs / inputs of one estimate
+    uint8_t* host = nullptr;    // pinned staging of the same size
+    int wslot = -1;             // arena slot for this thread's weighted reference planes
+};
+
+struct x265amd_la
+{
+    x265amd_la_config cfg;
+    size_t pix = 1;             // bytes per pixel
+    size_t frame_bytes = 0;     // 4 planes
+    int ncu = 0;
+    int slots = 0;              // frame slots + thread slots
+    uint8_t* arena = nullptr;   // slots * frame_bytes
+    int32_t* intra = nullptr;   // slots * ncu: intraCost of each slot's picture
+    int32_t* invq = nullptr;    // slots * ncu: invQscaleFactor (when AQ is on)
+    uint16_t* mvcost = nullptr; // centre of the device BitCost table
+    uint16_t* mvcost_base = nullptr;
+    size_t scratch = 0;
+
+    std::mutex mu;
+    struct Slot { int index; int gen; bool has_invq; };
+    std::unordered_map<const void*, Slot> frames;
+    int next_frame = 0, next_thread = 0;
+    std::vector<x265amd_la_thread*> threads;
+};
+
+namespace {
+
+struct TlsEntry { const x265amd_la* la; x265amd_la_thread* t; };
+thread_local std::vector<TlsEntry> tls;
+
+int thread_ctx(x265amd_la* la, x265amd_la_thread** out)
+{
+    for (auto& e : tls)
+        if (e.la == la)
+        {
+            *out = e.t;
+            return 0;
+        }
+    auto* t = new (std::nothrow) x265amd_la_thread();
+    if (!t) return X265AMD_ENOMEM;
+    {
+        std::lock_guard<std::mutex> g(la->mu);
+        if (la->next_thread >= la->cfg.max_threads)
+        {
+            delete t;
+            return X265AMD_ENOMEM;
+        }
+        t->wslot = la->cfg.max_frames + la->next_thread++;
+        la->threads.push_back(t);
+    }
+    if (hipStreamCreateWithFlags(&t->st, hipStreamNonBlocking) != hipSuccess ||
+        hipMalloc((void**)&t->dev, la->scratch) != hipSuccess ||
+        hipHostMalloc((void**)&t->host, la->scratch, hipHostMallocDefault) != hipSuccess)
+        return X265AMD_ENOMEM;
+    tls.push_back({ la, t });
+    *out = t;
+    return 0;
+}
+
+// scratch layout of one estimate (byte offsets, 256-aligned)
+struct Layout
+{
+    size_t mvs0, mvc0, mvs1, mvc1, lc, rs, ce, mbs, offs, ds, end;
+    Layout(int ncu, int hcu)
+    {
+        size_t o = 0;
+        auto take = [&](size_t b) { size_t r = o; o = (o + b + 255) & ~(size_t)255; return r; };
+        mvs0 = take(4 * (size_t)ncu);
+        mvc0 = take(4 * (size_t)ncu);
+        mvs1 = take(4 * (size_t)ncu);
+        mvc1 = take(4 * (size_t)ncu);
+        lc = take(2 * (size_t)ncu);
+        rs = take(4 * (size_t)hcu);
+        ce = take(16);
+        mbs = take(4);
+        offs = take(8 * 9);
+        ds = take(2);
+        end = o;
+    }
+};
+
+int find_slot(x265amd_la* la, const void* key, int* index)
+{
+    std::lock_guard<std::mutex> g(la->mu);
+    auto it = la->frames.find(key);
+    if (it == la->frames.end()) return X265AMD_EINVAL;     // estimate of a picture never loaded
+    *index = it->second.index;
+    return 0;
+}
+
+int64_t plane_off(const x265amd_la* la, int slot, int k)
+{
+    return (int64_t)slot * 4 * la->cfg.planesize + (int64_t)k * la->cfg.planesize + la->cfg.padoffset;
+}
+
+} // namespace
+
+extern "C" int x265amd_la_create(const x265amd_la_config* cfg, x265amd_la** out)
+{
+    if (!cfg || !out) return X265AMD_EINVAL;
+    *out = nullptr;
+    if ((cfg->depth != 8 && cfg->depth != 10 && cfg->depth != 12) || cfg->width_cu <= 0 || cfg->height_cu <= 0 ||
+        cfg->planesize <= 0 || cfg->padoffset < 0 || cfg->max_frames <= 0 || cfg->max_threads <= 0 || !cfg->mvcost ||
+        cfg->mvcost_range <= 0)
+        return X265AMD_EINVAL;
+    auto* la = new (std::nothrow) x265amd_la();
+    if (!la) return record(X265AMD_ENOMEM);
+    la->cfg = *cfg;
+    la->pix = cfg->depth > 8 ? 2 : 1;
+    la->frame_bytes = 4 * (size_t)cfg->planesize * la->pix;
+    la->ncu = cfg->width_cu * cfg->height_cu;
+    la->slots = cfg->max_frames + cfg->max_threads;
+    la->scratch = Layout(la->ncu, cfg->height_cu).end;
+    const size_t tab = 2 * (size_t)cfg->mvcost_range + 1;
+    if (hipMalloc((void**)&la->arena, la->frame_bytes * la->slots) != hipSuccess ||
+        hipMalloc((void**)&la->intra, sizeof(int32_t) * la->ncu * la->slots) != hipSuccess ||
+        hipMalloc((void**)&la->invq, sizeof(int32_t) * la->ncu * la->slots) != hipSuccess ||
+        hipMalloc((void**)&la->mvcost_base, sizeof(uint16_t) * tab) != hipSuccess ||
+        hipMemcpy(la->mvcost_base, cfg->mvcost - cfg->mvcost_range, sizeof(uint16_t) * tab, hipMemcpyHostToDevice) !=
+            hipSuccess)
+    {
+        x265amd_la_destroy(la);
+        return record(X265AMD_ENOMEM);
+    }
+    la->mvcost = la->mvcost_base + cfg->mvcost_range;
+    *out = la;
+    return 0;
+}
+
+extern "C" void x265amd_la_destroy(x265amd_la* la)
+{
+    if (!la) return;
+    for (auto* t : la->threads)
+    {
+        if (t->st) (void)hipStreamSynchronize(t->st);
+        (void)hipFree(t->dev);
+        (void)hipHostFree(t->host);
+        if (t->st) (void)hipStreamDestroy(t->st);
+        delete t;
+    }
+    (void)hipFree(la->arena);
+    (void)hipFree(la->intra);
+    (void)hipFree(la->invq);
+    (void)hipFree(la->mvcost_base);
+    delete la;
+}
+
+extern "C" int x265amd_la_load(x265amd_la* la, const void* key, int gen, const void* buffer,
+                               const int32_t* inv_qscale)
+{
+    if (!la || !key || !buffer) return record(X265AMD_EINVAL);
+    x265amd_la_thread* t;
+    LA_TRY(thread_ctx(la, &t));
+    int slot;
+    {
+        std::lock_guard<std::mutex> g(la->mu);
+        auto it = la->frames.find(key);
+        if (it == la->frames.end())
+        {
+            if (la->next_frame >= la->cfg.max_frames) return record(X265AMD_ENOMEM);
+            it = la->frames.emplace(key, x265amd_la::Slot{ la->next_frame++, gen, false }).first;
+        }
+        it->second.gen = gen;
+        it->second.has_invq = inv_qscale != nullptr;
+        slot = it->second.index;
+    }
+    // x265 reuses a Lowres for a new picture only after every estimate that read it is done
+    LA_TRY(hipMemcpyAsync(la->arena + (size_t)slot * la->frame_bytes, buffer, la->frame_bytes,
+                          hipMemcpyHostToDevice, t->st));
+    if (inv_qscale)
+        LA_TRY(hipMemcpyAsync(la->invq + (size_t)slot * la->ncu, inv_qscale, sizeof(int32_t) * la->ncu,
+                              hipMemcpyHostToDevice, t->st));
+    return record((int)hipStreamSynchronize(t->st));
+}
+
+extern "C" int x265amd_la_intra(x265amd_la* la, const void* key, int32_t* intra_cost, uint8_t* intra_mode,
+                                uint16_t* lowres_cost, int32_t* row_satd, int64_t* cost_est)
+{
+    if (!la || !key || !intra_cost || !intra_mode || !lowres_cost || !row_satd || !cost_est)
+        return record(X265AMD_EINVAL);
+    x265amd_la_thread* t;
+    LA_TRY(thread_ctx(la, &t));
+    int slot;
+    bool has_invq;
+    {
+        std::lock_guard<std::mutex> g(la->mu);
+        auto it = la->frames.find(key);
+        if (it == la->frames.end()) return record(X265AMD_EINVAL);
+        slot = it->second.index;
+        has_invq = it->second.has_invq;
+    }
+    const int ncu = la->ncu, hcu = la->cfg.height_cu;
+    const Layout L(ncu, hcu);
+    int64_t* off = (int64_t*)(t->host + L.offs);
+    off[0] = plane_off(la, slot, 0);
+    LA_TRY(hipMemcpyAsync(t->dev + L.offs, off, 8, hipMemcpyHostToDevice, t->st));
+    int32_t* dic = la->intra + (size_t)slot * ncu;
+    x265amd_lowres_intra_batch b{ 1, la->cfg.width_cu, hcu, la->arena, la->cfg.lowres_stride,
+                                  (const int64_t*)(t->dev + L.offs),
+                                  has_invq ? la->invq + (size_t)slot * ncu : nullptr, dic,
+                                  (uint8_t*)(t->dev + L.mvs0), (uint16_t*)(t->dev + L.lc), (int32_t*)(t->dev + L.rs),
+                                  (int64_t*)(t->dev + L.ce) };
+    LA_TRY(x265amd_lowres_intra(la->cfg.depth, &b, t->st));
+    LA_TRY(hipMemcpyAsync(t->host + L.mvc0, dic, 4 * (size_t)ncu, hipMemcpyDeviceToHost, t->st));
+    LA_TRY(hipMemcpyAsync(t->host + L.mvs0, t->dev + L.mvs0, ncu, hipMemcpyDeviceToHost, t->st));
+    LA_TRY(hipMemcpyAsync(t->host + L.lc, t->dev + L.lc, L.rs - L.lc + 4 * (size_t)hcu, hipMemcpyDeviceToHost, t->st));
+    LA_TRY(hipMemcpyAsync(t->host + L.ce, t->dev + L.ce, 16, hipMemcpyDeviceToHost, t->st));
+    LA_TRY(hipStreamSynchronize(t->st));
+    memcpy(intra_cost, t->host + L.mvc0, 4 * (size_t)ncu);
+    memcpy(intra_mode, t->host + L.mvs0, ncu);
+    memcpy(lowres_cost, t->host + L.lc, 2 * (size_t)ncu);
+    memcpy(row_satd, t->host + L.rs, 4 * (size_t)hcu);
+    memcpy(cost_est, t->host + L.ce, 16);
+    return 0;
+}
+
+extern "C" int x265amd_la_pcost(x265amd_la* la, const void* fenc, const void* ref, const void* weighted_buffer,
+                                int rows_per_slice, int num_slices, int16_t* mvs, int32_t* mv_costs,
+                                uint16_t* lowres_costs, int32_t* row_satd, int64_t* cost_est, int32_t* intra_mbs)
+{
+    if (!la || !fenc || !ref || !mvs || !mv_costs || !lowres_costs || !row_satd || !cost_est || !intra_mbs)
+        return record(X265AMD_EINVAL);
+    x265amd_la_thread* t;
+    LA_TRY(thread_ctx(la, &t));
+    int sf, sr;
+    LA_TRY(find_slot(la, fenc, &sf));
+    LA_TRY(find_slot(la, ref, &sr));
+    bool has_invq;
+    {
+        std::lock_guard<std::mutex> g(la->mu);
+        has_invq = la->frames[fenc].has_invq;
+    }
+    const int ncu = la->ncu, hcu = la->cfg.height_cu;
+    const Layout L(ncu, hcu);
+    if (weighted_buffer)
+    {
+        // weightsAnalyse's planes (the calling thread's LookaheadTLD wbuffer, same layout)
+        LA_TRY(hipMemcpyAsync(la->arena + (size_t)t->wslot * la->frame_bytes, weighted_buffer, la->frame_bytes,
+                              hipMemcpyHostToDevice, t->st));
+        sr = t->wslot;
+    }
+    int64_t* off = (int64_t*)(t->host + L.offs);
+    off[0] = plane_off(la, sf, 0);
+    for (int k = 0; k < 4; k++) off[1 + k] = plane_off(la, sr, k);
+    LA_TRY(hipMemcpyAsync(t->dev + L.offs, off, 8 * 5, hipMemcpyHostToDevice, t->st));
+    const int64_t* doff = (const int64_t*)(t->dev + L.offs);
+    x265amd_lowres_pcost_batch b{ 1, la->cfg.width_cu, hcu, rows_per_slice, num_slices, la->arena,
+                                  la->cfg.lowres_stride, doff, doff + 1, la->intra + (size_t)sf * ncu,
+                                  has_invq ? la->invq + (size_t)sf * ncu : nullptr, la->mvcost,
+                                  (int16_t*)(t->dev + L.mvs0), (int32_t*)(t->dev + L.mvc0), (uint16_t*)(t->dev + L.lc),
+                                  (int32_t*)(t->dev + L.rs), (int64_t*)(t->dev + L.ce), (int32_t*)(t->dev + L.mbs) };
+    LA_TRY(x265amd_lowres_pcost(la->cfg.depth, &b, t->st));
+    // mvs0 .. mbs are contiguous in the layout: one download
+    LA_TRY(hipMemcpyAsync(t->host + L.mvs0, t->dev + L.mvs0, L.mvs1 - L.mvs0, hipMemcpyDeviceToHost, t->st));
+    LA_TRY(hipMemcpyAsync(t->host + L.lc, t->dev + L.lc, L.offs - L.lc, hipMemcpyDeviceToHost, t->st));
+    LA_TRY(hipStreamSynchronize(t->st));
+    memcpy(mvs, t->host + L.mvs0, 4 * (size_t)ncu);
+    memcpy(mv_costs, t->host + L.mvc0, 4 * (size_t)ncu);
+    memcpy(lowres_costs, t->host + L.lc, 2 * (size_t)ncu);
+    memcpy(row_satd, t->host + L.rs, 4 * (size_t)hcu);
+    memcpy(cost_est, t->host + L.ce, 16);
+    memcpy(intra_mbs, t->host + L.mbs, 4);
+    return 0;
+}
+
+extern "C" int x265amd_la_bcost(x265amd_la* la, const void* fenc, const void* ref0, const void* ref1, int do_search0,
+                                int do_search1, int rows_per_slice, int num_slices, int16_t* mvs0, int32_t* mv_costs0,
+                                int16_t* mvs1, int32_t* mv_costs1, uint16_t* lowres_costs, int32_t* row_satd,
+                                int64_t* cost_est)
+{
+    if (!la || !fenc || !ref0 || !ref1 || !mvs0 || !mv_costs0 || !mvs1 || !mv_costs1 || !lowres_costs || !row_satd ||
+        !cost_est)
+        return record(X265AMD_EINVAL);
+    x265amd_la_thread* t;
+    LA_TRY(thread_ctx(la, &t));
+    int sf, s0, s1;
+    LA_TRY(find_slot(la, fenc, &sf));
+    LA_TRY(find_slot(la, ref0, &s0));
+    LA_TRY(find_slot(la, ref1, &s1));
+    bool has_invq;
+    {
+        std::lock_guard<std::mutex> g(la->mu);
+        has_invq = la->frames[fenc].has_invq;
+    }
+    const int ncu = la->ncu, hcu = la->cfg.height_cu;
+    const Layout L(ncu, hcu);
+    int64_t* off = (int64_t*)(t->host + L.offs);
+    off[0] = plane_off(la, sf, 0);
+    for (int k = 0; k < 4; k++)
+    {
+        off[1 + k] = plane_off(la, s0, k);
+        off[5 + k] = plane_off(la, s1, k);
+    }
+    uint8_t* ds = t->host + L.ds;
+    ds[0] = (uint8_t)!!do_search0;
+    ds[1] = (uint8_t)!!do_search1;
+    LA_TRY(hipMemcpyAsync(t->dev + L.offs, off, L.end - L.offs, hipMemcpyHostToDevice, t->st));
+    // a list that is not searched reuses the stored lowresMvs / lowresMvCosts (slicetype.cpp:2105-2109, 2171-2172)
+    if (!do_search0)
+    {
+        memcpy(t->host + L.mvs0, mvs0, 4 * (size_t)ncu);
+        memcpy(t->host + L.mvc0, mv_costs0, 4 * (size_t)ncu);
+        LA_TRY(hipMemcpyAsync(t->dev + L.mvs0, t->host + L.mvs0, L.mvs1 - L.mvs0, hipMemcpyHostToDevice, t->st));
+    }
+    if (!do_search1)
+    {
+        memcpy(t->host + L.mvs1, mvs1, 4 * (size_t)ncu);
+        memcpy(t->host + L.mvc1, mv_costs1, 4 * (size_t)ncu);
+        LA_TRY(hipMemcpyAsync(t->dev + L.mvs1, t->host + L.mvs1, L.lc - L.mvs1, hipMemcpyHostToDevice, t->st));
+    }
+    const int64_t* doff = (const int64_t*)(t->dev + L.offs);
+    x265amd_lowres_bcost_batch b{ 1, la->cfg.width_cu, hcu, rows_per_slice, num_slices, la->arena,
+                                  la->cfg.lowres_stride, doff, doff + 1, doff + 5, t->dev + L.ds,
+                                  has_invq ? la->invq + (size_t)sf * ncu : nullptr, la->mvcost,
+                                  (int16_t*)(t->dev + L.mvs0), (int32_t*)(t->dev + L.mvc0),
+                                  (int16_t*)(t->dev + L.mvs1), (int32_t*)(t->dev + L.mvc1),
+                                  (uint16_t*)(t->dev + L.lc), (int32_t*)(t->dev + L.rs), (int64_t*)(t->dev + L.ce) };
+    LA_TRY(x265amd_lowres_bcost(la->cfg.depth, &b, t->st));
+    LA_TRY(hipMemcpyAsync(t->host + L.mvs0, t->dev + L.mvs0, L.offs - L.mvs0, hipMemcpyDeviceToHost, t->st));
+    LA_TRY(hipStreamSynchronize(t->st));
+    if (do_search0)
+    {
+        memcpy(mvs0, t->host + L.mvs0, 4 * (size_t)ncu);
+        memcpy(mv_costs0, t->host + L.mvc0, 4 * (size_t)ncu);
+    }
+    if (do_search1)
+    {
+        memcpy(mvs1, t->host + L.mvs1, 4 * (size_t)ncu);
+        memcpy(mv_costs1, t->host + L.mvc1, 4 * (size_t)ncu);
+    }
+    memcpy(lowres_costs, t->host + L.lc, 2 * (size_t)ncu);
+    memcpy(row_satd, t->host + L.rs, 4 * (size_t)hcu);
+    memcpy(cost_est, t->host + L.ce, 16);
+    return 0;
+}
