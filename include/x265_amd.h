@@ -518,6 +518,39 @@ int x265amd_la_bcost(x265amd_la* la, const void* fenc, const void* ref0, const v
                      int16_t* mvs1, int32_t* mv_costs1, uint16_t* lowres_costs, int32_t* row_satd,
                      int64_t* cost_est);
 
+/* Several estimates in ONE device launch (CostEstimateGroup::finishBatch's batch: estimates of
+ * one batch are independent, slicetype.cpp:1231-1298).  Per job the same inputs / outputs as the
+ * single-estimate entries; cost_est / intra_mbs are returned in the job.  weighted_buffer must be
+ * NULL when n > 1 (one weighted slot per thread). */
+typedef struct
+{
+    const void* fenc;
+    const void* ref;
+    const void* weighted_buffer;
+    int16_t* mvs;
+    int32_t* mv_costs;
+    uint16_t* lowres_costs;
+    int32_t* row_satd;
+    int64_t cost_est[2];
+    int32_t intra_mbs;
+} x265amd_la_pjob;
+typedef struct
+{
+    const void* fenc;
+    const void* ref0;
+    const void* ref1;
+    int do_search0, do_search1;
+    int16_t* mvs0;
+    int32_t* mv_costs0;
+    int16_t* mvs1;
+    int32_t* mv_costs1;
+    uint16_t* lowres_costs;
+    int32_t* row_satd;
+    int64_t cost_est[2];
+} x265amd_la_bjob;
+int x265amd_la_pcost_n(x265amd_la* la, int n, x265amd_la_pjob* jobs, int rows_per_slice, int num_slices);
+int x265amd_la_bcost_n(x265amd_la* la, int n, x265amd_la_bjob* jobs, int rows_per_slice, int num_slices);
+
 /* f1 cuTree: Lookahead::estimateCUPropagate (slicetype.cpp:1738-1836) with the
  * propagateCost primitive (pixel.cpp:846-872), one call of it per batch, batches in order.
  * For every lowres CU of frame b: the amount

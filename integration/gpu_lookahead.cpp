@@ -40,13 +40,16 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <ctime>
 #include <pthread.h>
+#include <vector>
 
 #include "../include/x265_amd.h"
 
 using namespace X265_NS;
 
 /* the reference's own implementations (aliases of the weakened symbols, see oracle/Makefile) */
+extern "C" void x265ref_finishBatch(CostEstimateGroup* self);
 extern "C" void x265ref_lowresIntraEstimate(LookaheadTLD* self, Lowres* fenc);
 extern "C" int64_t x265ref_estimateFrameCost(CostEstimateGroup* self, LookaheadTLD* tld, int p0, int p1, int b,
                                              bool bIntraPenalty);
@@ -67,6 +70,8 @@ pthread_mutex_t g_mu = PTHREAD_MUTEX_INITIALIZER;
 pthread_once_t g_mode_once = PTHREAD_ONCE_INIT;
 
 void print_check_summary();
+void print_stats();
+extern bool g_stats_on;
 
 void read_mode()
 {
@@ -78,6 +83,10 @@ void read_mode()
             g_mode == MODE_CHECK ? "the MI355X, each checked against the CPU" : "the MI355X");
     if (g_mode == MODE_CHECK)
         atexit(print_check_summary);
+    const char* st = getenv("X265AMD_LA_STATS");
+    g_stats_on = st && *st && strcmp(st, "0");
+    if (g_stats_on)
+        atexit(print_stats);
 }
 
 /* the session, created on the first call from the first Lowres (all pictures of an encoder
@@ -115,6 +124,39 @@ void report(const char* what, int st)
 }
 
 int g_mismatches = 0;
+
+/* X265AMD_LA_STATS=1: calls and wall time per kind, printed at exit */
+enum { ST_INTRA, ST_P, ST_B, ST_BATCH_P, ST_BATCH_B, ST_HOST, ST_N };
+const char* const st_name[ST_N] = { "intra", "P single", "B single", "P batched", "B batched", "host loops" };
+struct Stat { long calls, jobs; double sec; };
+Stat g_stat[ST_N];
+bool g_stats_on = false;
+
+double now_s()
+{
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return ts.tv_sec + 1e-9 * ts.tv_nsec;
+}
+
+void stat_add(int k, long jobs, double t0)
+{
+    if (!g_stats_on) return;
+    const double dt = now_s() - t0;
+    pthread_mutex_lock(&g_mu);
+    g_stat[k].calls++;
+    g_stat[k].jobs += jobs;
+    g_stat[k].sec += dt;
+    pthread_mutex_unlock(&g_mu);
+}
+
+void print_stats()
+{
+    for (int k = 0; k < ST_N; k++)
+        if (g_stat[k].calls)
+            fprintf(stderr, "[x265la] stats %-10s calls %6ld estimates %6ld  %8.1f ms  (%.3f ms/call)\n", st_name[k],
+                    g_stat[k].calls, g_stat[k].jobs, 1e3 * g_stat[k].sec, 1e3 * g_stat[k].sec / g_stat[k].calls);
+}
 
 int ncu_of(const Lowres& f) { return (int)(f.maxBlocksInRow * f.maxBlocksInCol); }
 
@@ -242,9 +284,11 @@ void LookaheadTLD::lowresIntraEstimate(Lowres& fenc)
     }
     if (!st)
     {
+        const double t0 = now_s();
         st = x265amd_la_intra(la, &fenc, fenc.intraCost, fenc.intraMode, fenc.lowresCosts[0][0], fenc.rowSatds[0][0],
                               ce);
         report("x265amd_la_intra", st);
+        stat_add(ST_INTRA, 1, t0);
     }
     if (st)
     {
@@ -292,7 +336,7 @@ int64_t CostEstimateGroup::estimateFrameCost(LookaheadTLD& tld, int p0, int p1, 
         /* X265AMD_LOOKAHEAD=check: the device estimate goes to scratch copies, the host loops below
          * produce the reference's results in the Lowres, and the two are compared */
         const bool check = g_mode == MODE_CHECK;
-        const int ncu = tld.ncu, hcu = m_lookahead.m_8x8Height;
+        const int ncu = m_lookahead.m_8x8Width * m_lookahead.m_8x8Height, hcu = m_lookahead.m_8x8Height;
         const int d0 = b - p0 - 1, d1 = p1 - b - 1;
         MV* mvs[2] = { p0 < b ? fenc->lowresMvs[0][d0] : NULL, p1 > b ? fenc->lowresMvs[1][d1] : NULL };
         int32_t* mvc[2] = { p0 < b ? fenc->lowresMvCosts[0][d0] : NULL, p1 > b ? fenc->lowresMvCosts[1][d1] : NULL };
@@ -319,17 +363,20 @@ int64_t CostEstimateGroup::estimateFrameCost(LookaheadTLD& tld, int p0, int p1, 
              * status is recorded (the encode will fail) and the estimate is computed on the host
              * so the encoder's state stays valid until it stops */
             int st;
+            const double t0 = now_s();
             if (p1 == b)
             {
                 st = x265amd_la_pcost(la, fenc, m_frames[p0], weighted ? tld.wbuffer[0] : NULL, rps, ns,
                                       (int16_t*)mvs[0], mvc[0], lc, rs, ce, &mbs);
                 report("x265amd_la_pcost", st);
+                stat_add(ST_P, 1, t0);
             }
             else
             {
                 st = x265amd_la_bcost(la, fenc, m_frames[p0], m_frames[p1], bDoSearch[0], bDoSearch[1], rps, ns,
                                       (int16_t*)mvs[0], mvc[0], (int16_t*)mvs[1], mvc[1], lc, rs, ce);
                 report("x265amd_la_bcost", st);
+                stat_add(ST_B, 1, t0);
             }
             if (!st && !check)
             {
@@ -341,6 +388,7 @@ int64_t CostEstimateGroup::estimateFrameCost(LookaheadTLD& tld, int p0, int p1, 
             }
         }
         const int mbs_before = fenc->intraMbs[b - p0];
+        const double th = now_s();
         if (done)
             ;
         else if (coop)
@@ -382,6 +430,8 @@ int64_t CostEstimateGroup::estimateFrameCost(LookaheadTLD& tld, int p0, int p1, 
             }
         }
 
+        if (!done)
+            stat_add(ST_HOST, 1, th);
         if (check && device)
             cb.compare(p0, p1, b, ns, bDoSearch, fenc, ce, mbs, fenc->intraMbs[b - p0] - mbs_before);
 
@@ -398,6 +448,147 @@ int64_t CostEstimateGroup::estimateFrameCost(LookaheadTLD& tld, int p0, int p1, 
         score += score * fenc->intraMbs[b - p0] / (tld.ncu * 8);
 
     return score;
+}
+
+/* CostEstimateGroup::finishBatch (slicetype.cpp:1919-1926): the reference hands the batch's
+ * estimates to its bonded workers, one estimateFrameCost each; the estimates of a batch are
+ * independent (slicetype.cpp:1231-1298 builds them so), so here every device-eligible estimate of
+ * the batch goes out in ONE launch per kind — the motion-search batch's P / B searches, the
+ * frame-cost batch's B estimates on stored MVs — after each one's estimateFrameCost preamble
+ * (cost cache, bDoSearch, weightsAnalyse) on this thread.  A weighted estimate runs through
+ * estimateFrameCost alone (its weighted planes live in this thread's wbuffer), a P estimate on
+ * stored MVs through the host loop (no search: a few operations per CU). */
+void CostEstimateGroup::finishBatch()
+{
+    pthread_once(&g_mode_once, read_mode);
+    if (g_mode != MODE_GPU)
+    {
+        x265ref_finishBatch(this);
+        return;
+    }
+    LookaheadTLD& tld = m_lookahead.m_tld[m_lookahead.m_pool ? m_lookahead.m_pool->m_numWorkers : 0];
+    x265_param* param = m_lookahead.m_param;
+    std::vector<x265amd_la_pjob> pj;
+    std::vector<x265amd_la_bjob> bj;
+    std::vector<int> pidx, bidx, host;
+    x265amd_la* la = NULL;
+    for (int i = 0; i < m_jobTotal; i++)
+    {
+        const Estimate& e = m_estimates[i];
+        const int p0 = e.p0, p1 = e.p1, b = e.b;
+        Lowres* fenc = m_frames[b];
+        if (fenc->costEst[b - p0][p1 - b] >= 0 && fenc->rowSatds[b - p0][p1 - b][0] != -1)
+            continue;
+        bool bDoSearch[2];
+        bDoSearch[0] = p0 < b && fenc->lowresMvs[0][b - p0 - 1][0].x == 0x7FFF;
+        bDoSearch[1] = p1 > b && fenc->lowresMvs[1][p1 - b - 1][0].x == 0x7FFF;
+        fenc->weightedRef[b - p0].isWeighted = false;
+        if (param->bEnableWeightedPred && bDoSearch[0])
+            tld.weightsAnalyse(*m_frames[b], *m_frames[p0]);
+        if (fenc->weightedRef[b - p0].isWeighted)
+        {
+            estimateFrameCost(tld, p0, p1, b, false);   /* analyses again (same result) and runs alone */
+            continue;
+        }
+        if (!la)
+            la = session(*fenc);
+        fenc->costEst[b - p0][p1 - b] = 0;
+        fenc->costEstAq[b - p0][p1 - b] = 0;
+        if (la && p1 == b && bDoSearch[0])
+        {
+            x265amd_la_pjob j;
+            memset(&j, 0, sizeof(j));
+            j.fenc = fenc;
+            j.ref = m_frames[p0];
+            j.mvs = (int16_t*)fenc->lowresMvs[0][b - p0 - 1];
+            j.mv_costs = fenc->lowresMvCosts[0][b - p0 - 1];
+            j.lowres_costs = fenc->lowresCosts[b - p0][p1 - b];
+            j.row_satd = fenc->rowSatds[b - p0][p1 - b];
+            pj.push_back(j);
+            pidx.push_back(i);
+        }
+        else if (la && p1 > b)
+        {
+            x265amd_la_bjob j;
+            memset(&j, 0, sizeof(j));
+            j.fenc = fenc;
+            j.ref0 = m_frames[p0];
+            j.ref1 = m_frames[p1];
+            j.do_search0 = bDoSearch[0];
+            j.do_search1 = bDoSearch[1];
+            j.mvs0 = (int16_t*)fenc->lowresMvs[0][b - p0 - 1];
+            j.mv_costs0 = fenc->lowresMvCosts[0][b - p0 - 1];
+            j.mvs1 = (int16_t*)fenc->lowresMvs[1][p1 - b - 1];
+            j.mv_costs1 = fenc->lowresMvCosts[1][p1 - b - 1];
+            j.lowres_costs = fenc->lowresCosts[b - p0][p1 - b];
+            j.row_satd = fenc->rowSatds[b - p0][p1 - b];
+            bj.push_back(j);
+            bidx.push_back(i);
+        }
+        else
+            host.push_back(i);
+    }
+    const int rows = m_lookahead.m_8x8Height;
+    int st = 0;
+    if (!pj.empty())
+    {
+        const double t0 = now_s();
+        st = x265amd_la_pcost_n(la, (int)pj.size(), &pj[0], rows, 1);
+        report("x265amd_la_pcost_n", st);
+        stat_add(ST_BATCH_P, (long)pj.size(), t0);
+        if (st)
+            host.insert(host.end(), pidx.begin(), pidx.end());
+    }
+    if (!bj.empty())
+    {
+        const double t0 = now_s();
+        const int stb = x265amd_la_bcost_n(la, (int)bj.size(), &bj[0], rows, 1);
+        report("x265amd_la_bcost_n", stb);
+        stat_add(ST_BATCH_B, (long)bj.size(), t0);
+        if (stb)
+            host.insert(host.end(), bidx.begin(), bidx.end());
+        st = st ? st : stb;
+    }
+    for (size_t k = 0; k < pj.size() && !st; k++)
+    {
+        const Estimate& e = m_estimates[pidx[k]];
+        Lowres* fenc = m_frames[e.b];
+        fenc->costEst[e.b - e.p0][0] = pj[k].cost_est[0];
+        fenc->costEstAq[e.b - e.p0][0] = pj[k].cost_est[1];
+        fenc->intraMbs[e.b - e.p0] += pj[k].intra_mbs;
+    }
+    for (size_t k = 0; k < bj.size() && !st; k++)
+    {
+        const Estimate& e = m_estimates[bidx[k]];
+        Lowres* fenc = m_frames[e.b];
+        fenc->costEst[e.b - e.p0][e.p1 - e.b] = bj[k].cost_est[0] * 100 / (130 + param->bFrameBias);
+        fenc->costEstAq[e.b - e.p0][e.p1 - e.b] = bj[k].cost_est[1];
+    }
+    /* the rest: the reference's serial pass of batch mode (:2041-2050) on this thread */
+    for (size_t k = 0; k < host.size(); k++)
+    {
+        const Estimate& e = m_estimates[host[k]];
+        const int p0 = e.p0, p1 = e.p1, b = e.b;
+        Lowres* fenc = m_frames[b];
+        const double th = now_s();
+        bool bDoSearch[2];
+        bDoSearch[0] = p0 < b && fenc->lowresMvs[0][b - p0 - 1][0].x == 0x7FFF;
+        bDoSearch[1] = p1 > b && fenc->lowresMvs[1][p1 - b - 1][0].x == 0x7FFF;
+        fenc->costEst[b - p0][p1 - b] = 0;
+        fenc->costEstAq[b - p0][p1 - b] = 0;
+        bool lastRow = true;
+        for (int cuY = m_lookahead.m_8x8Height - 1; cuY >= 0; cuY--)
+        {
+            fenc->rowSatds[b - p0][p1 - b][cuY] = 0;
+            for (int cuX = m_lookahead.m_8x8Width - 1; cuX >= 0; cuX--)
+                estimateCUCost(tld, cuX, cuY, p0, p1, b, bDoSearch, lastRow, -1);
+            lastRow = false;
+        }
+        if (b != p1)
+            fenc->costEst[b - p0][p1 - b] = fenc->costEst[b - p0][p1 - b] * 100 / (130 + param->bFrameBias);
+        stat_add(ST_HOST, 1, th);
+    }
+    m_jobTotal = m_jobAcquired = 0;
 }
 
 } // namespace X265_NS

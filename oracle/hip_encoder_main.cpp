@@ -29,9 +29,12 @@
 #include "common.h"
 #include "primitives.h"
 
+#include <csignal>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <execinfo.h>
+#include <unistd.h>
 
 extern "C" int x265amd_setup_primitives(void* table, int depth, int* overridden);
 extern "C" const char* x265amd_strerror(int status);
@@ -71,8 +74,21 @@ using namespace X265_NS;
 
 int x265_cli_main(int argc, char** argv);
 
+/* a crash names its place (binaries are linked with -rdynamic) */
+static void on_fatal(int sig)
+{
+    void* bt[64];
+    int n = backtrace(bt, 64);
+    fprintf(stderr, "[x265hip] fatal signal %d, backtrace:\n", sig);
+    backtrace_symbols_fd(bt, n, 2);
+    signal(sig, SIG_DFL);
+    raise(sig);
+}
+
 int main(int argc, char** argv)
 {
+    signal(SIGSEGV, on_fatal);
+    signal(SIGBUS, on_fatal);
     const char* which = getenv("X265AMD_PROVIDER");
 #ifdef X265AMD_DEFAULT_PROVIDER_C
     /* x265la: the C table unless the per-call provider is asked for */

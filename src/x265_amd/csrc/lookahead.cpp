@@ -12,7 +12,7 @@
 //     intraCost on the device for its P estimates;
 //   * one arena for all slots, so every batch entry addresses planes as offsets from one
 //     base (the batched x265amd_lowres_* entries' convention);
-//   * per host thread: a non-blocking stream, device scratch for one estimate's outputs,
+//   * per host thread: a non-blocking stream, device scratch for a batch of estimates,
 //     pinned staging, and an arena slot for weighted reference planes (weightsAnalyse's
 //     wbuffer, slicetype.cpp:391-495, which lives on the calling thread's LookaheadTLD).
 // Every entry is synchronous on the calling thread's stream: the outputs are in the
@@ -62,6 +62,7 @@ struct x265amd_la_thread
     uint8_t* dev = nullptr;     // scratch: outputs / inputs of one estimate
     uint8_t* host = nullptr;    // pinned staging of the same size
     int wslot = -1;             // arena slot for this thread's weighted reference planes
+    size_t cap = 0;             // bytes of dev / host scratch
 };
 
 struct x265amd_la
@@ -79,7 +80,7 @@ struct x265amd_la
     size_t scratch = 0;
 
     std::mutex mu;
-    struct Slot { int index; int gen; bool has_invq; };
+    struct Slot { int index; int gen; bool has_invq; const void* pinned; };
     std::unordered_map<const void*, Slot> frames;
     int next_frame = 0, next_thread = 0;
     std::vector<x265amd_la_thread*> threads;
@@ -89,6 +90,46 @@ namespace {
 
 struct TlsEntry { const x265amd_la* la; x265amd_la_thread* t; };
 thread_local std::vector<TlsEntry> tls;
+
+// scratch layout of n estimates (byte offsets, 256-aligned), field-major as the batched
+// x265amd_lowres_* entries index them (estimate e's CU arrays at e * ncu)
+struct Layout
+{
+    size_t mvs0, mvc0, mvs1, mvc1, lc, rs, ce, mbs, offs, ds, end;
+    Layout(int ncu, int hcu, int n = 1)
+    {
+        size_t o = 0;
+        auto take = [&](size_t b) { size_t r = o; o = (o + b + 255) & ~(size_t)255; return r; };
+        const size_t cus = (size_t)ncu * n;
+        mvs0 = take(4 * cus);
+        mvc0 = take(4 * cus);
+        mvs1 = take(4 * cus);
+        mvc1 = take(4 * cus);
+        lc = take(2 * cus);
+        rs = take(4 * (size_t)hcu * n);
+        ce = take(16 * (size_t)n);
+        mbs = take(4 * (size_t)n);
+        offs = take(8 * 9 * (size_t)n);
+        ds = take(2 * (size_t)n);
+        end = o;
+    }
+};
+
+// grow the calling thread's scratch to hold `bytes`
+int reserve(x265amd_la_thread* t, size_t bytes)
+{
+    if (bytes <= t->cap) return 0;
+    if (t->st) (void)hipStreamSynchronize(t->st);
+    (void)hipFree(t->dev);
+    (void)hipHostFree(t->host);
+    t->dev = t->host = nullptr;
+    t->cap = 0;
+    if (hipMalloc((void**)&t->dev, bytes) != hipSuccess ||
+        hipHostMalloc((void**)&t->host, bytes, hipHostMallocDefault) != hipSuccess)
+        return X265AMD_ENOMEM;
+    t->cap = bytes;
+    return 0;
+}
 
 int thread_ctx(x265amd_la* la, x265amd_la_thread** out)
 {
@@ -110,36 +151,12 @@ int thread_ctx(x265amd_la* la, x265amd_la_thread** out)
         t->wslot = la->cfg.max_frames + la->next_thread++;
         la->threads.push_back(t);
     }
-    if (hipStreamCreateWithFlags(&t->st, hipStreamNonBlocking) != hipSuccess ||
-        hipMalloc((void**)&t->dev, la->scratch) != hipSuccess ||
-        hipHostMalloc((void**)&t->host, la->scratch, hipHostMallocDefault) != hipSuccess)
+    if (hipStreamCreateWithFlags(&t->st, hipStreamNonBlocking) != hipSuccess || reserve(t, la->scratch))
         return X265AMD_ENOMEM;
     tls.push_back({ la, t });
     *out = t;
     return 0;
 }
-
-// scratch layout of one estimate (byte offsets, 256-aligned)
-struct Layout
-{
-    size_t mvs0, mvc0, mvs1, mvc1, lc, rs, ce, mbs, offs, ds, end;
-    Layout(int ncu, int hcu)
-    {
-        size_t o = 0;
-        auto take = [&](size_t b) { size_t r = o; o = (o + b + 255) & ~(size_t)255; return r; };
-        mvs0 = take(4 * (size_t)ncu);
-        mvc0 = take(4 * (size_t)ncu);
-        mvs1 = take(4 * (size_t)ncu);
-        mvc1 = take(4 * (size_t)ncu);
-        lc = take(2 * (size_t)ncu);
-        rs = take(4 * (size_t)hcu);
-        ce = take(16);
-        mbs = take(4);
-        offs = take(8 * 9);
-        ds = take(2);
-        end = o;
-    }
-};
 
 int find_slot(x265amd_la* la, const void* key, int* index)
 {
@@ -200,6 +217,8 @@ extern "C" void x265amd_la_destroy(x265amd_la* la)
         if (t->st) (void)hipStreamDestroy(t->st);
         delete t;
     }
+    for (auto& f : la->frames)
+        if (f.second.pinned) (void)hipHostUnregister((void*)f.second.pinned);
     (void)hipFree(la->arena);
     (void)hipFree(la->intra);
     (void)hipFree(la->invq);
@@ -220,11 +239,21 @@ extern "C" int x265amd_la_load(x265amd_la* la, const void* key, int gen, const v
         if (it == la->frames.end())
         {
             if (la->next_frame >= la->cfg.max_frames) return record(X265AMD_ENOMEM);
-            it = la->frames.emplace(key, x265amd_la::Slot{ la->next_frame++, gen, false }).first;
+            it = la->frames.emplace(key, x265amd_la::Slot{ la->next_frame++, gen, false, nullptr }).first;
         }
         it->second.gen = gen;
         it->second.has_invq = inv_qscale != nullptr;
         slot = it->second.index;
+        // page-lock the picture's host buffer once (x265 keeps a Frame's Lowres buffer for the life of
+        // the encoder and reuses it for later pictures), so every upload is a direct DMA; a buffer that
+        // cannot be registered is copied pageable
+        if (it->second.pinned != buffer)
+        {
+            if (it->second.pinned) (void)hipHostUnregister((void*)it->second.pinned);
+            it->second.pinned =
+                hipHostRegister((void*)buffer, la->frame_bytes, hipHostRegisterDefault) == hipSuccess ? buffer : nullptr;
+            (void)hipGetLastError();
+        }
     }
     // x265 reuses a Lowres for a new picture only after every estimate that read it is done
     LA_TRY(hipMemcpyAsync(la->arena + (size_t)slot * la->frame_bytes, buffer, la->frame_bytes,
@@ -276,53 +305,177 @@ extern "C" int x265amd_la_intra(x265amd_la* la, const void* key, int32_t* intra_
     return 0;
 }
 
+extern "C" int x265amd_la_pcost_n(x265amd_la* la, int n, x265amd_la_pjob* jobs, int rows_per_slice, int num_slices)
+{
+    if (!la || n < 0 || (n && !jobs)) return record(X265AMD_EINVAL);
+    if (!n) return 0;
+    for (int e = 0; e < n; e++)
+    {
+        const x265amd_la_pjob& j = jobs[e];
+        if (!j.fenc || !j.ref || !j.mvs || !j.mv_costs || !j.lowres_costs || !j.row_satd || (j.weighted_buffer && n > 1))
+            return record(X265AMD_EINVAL);
+    }
+    x265amd_la_thread* t;
+    LA_TRY(thread_ctx(la, &t));
+    const int ncu = la->ncu, hcu = la->cfg.height_cu;
+    const Layout L(ncu, hcu, n);
+    LA_TRY(reserve(t, L.end));
+    int64_t* off = (int64_t*)(t->host + L.offs);
+    bool has_invq = false;
+    for (int e = 0; e < n; e++)
+    {
+        int sf, sr;
+        LA_TRY(find_slot(la, jobs[e].fenc, &sf));
+        LA_TRY(find_slot(la, jobs[e].ref, &sr));
+        if (e == 0)
+        {
+            std::lock_guard<std::mutex> g(la->mu);
+            has_invq = la->frames[jobs[0].fenc].has_invq;
+        }
+        if (jobs[e].weighted_buffer)
+        {
+            // weightsAnalyse's planes (the calling thread's LookaheadTLD wbuffer, same layout)
+            LA_TRY(hipMemcpyAsync(la->arena + (size_t)t->wslot * la->frame_bytes, jobs[e].weighted_buffer,
+                                  la->frame_bytes, hipMemcpyHostToDevice, t->st));
+            sr = t->wslot;
+        }
+        off[e] = plane_off(la, sf, 0);
+        for (int k = 0; k < 4; k++) off[n + 4 * e + k] = plane_off(la, sr, k);
+        // per-estimate intraCost / invQscaleFactor, gathered from the pictures' slots into the
+        // scratch's (unused by a P estimate) list-1 arrays
+        LA_TRY(hipMemcpyAsync(t->dev + L.mvs1 + 4 * (size_t)ncu * e, la->intra + (size_t)sf * ncu, 4 * (size_t)ncu,
+                              hipMemcpyDeviceToDevice, t->st));
+        if (has_invq)
+            LA_TRY(hipMemcpyAsync(t->dev + L.mvc1 + 4 * (size_t)ncu * e, la->invq + (size_t)sf * ncu, 4 * (size_t)ncu,
+                                  hipMemcpyDeviceToDevice, t->st));
+    }
+    LA_TRY(hipMemcpyAsync(t->dev + L.offs, off, 8 * 5 * (size_t)n, hipMemcpyHostToDevice, t->st));
+    const int64_t* doff = (const int64_t*)(t->dev + L.offs);
+    x265amd_lowres_pcost_batch b{ n, la->cfg.width_cu, hcu, rows_per_slice, num_slices, la->arena,
+                                  la->cfg.lowres_stride, doff, doff + n, (const int32_t*)(t->dev + L.mvs1),
+                                  has_invq ? (const int32_t*)(t->dev + L.mvc1) : nullptr, la->mvcost,
+                                  (int16_t*)(t->dev + L.mvs0), (int32_t*)(t->dev + L.mvc0), (uint16_t*)(t->dev + L.lc),
+                                  (int32_t*)(t->dev + L.rs), (int64_t*)(t->dev + L.ce), (int32_t*)(t->dev + L.mbs) };
+    LA_TRY(x265amd_lowres_pcost(la->cfg.depth, &b, t->st));
+    LA_TRY(hipMemcpyAsync(t->host + L.mvs0, t->dev + L.mvs0, L.mvs1 - L.mvs0, hipMemcpyDeviceToHost, t->st));
+    LA_TRY(hipMemcpyAsync(t->host + L.lc, t->dev + L.lc, L.offs - L.lc, hipMemcpyDeviceToHost, t->st));
+    LA_TRY(hipStreamSynchronize(t->st));
+    for (int e = 0; e < n; e++)
+    {
+        x265amd_la_pjob& j = jobs[e];
+        memcpy(j.mvs, t->host + L.mvs0 + 4 * (size_t)ncu * e, 4 * (size_t)ncu);
+        memcpy(j.mv_costs, t->host + L.mvc0 + 4 * (size_t)ncu * e, 4 * (size_t)ncu);
+        memcpy(j.lowres_costs, t->host + L.lc + 2 * (size_t)ncu * e, 2 * (size_t)ncu);
+        memcpy(j.row_satd, t->host + L.rs + 4 * (size_t)hcu * e, 4 * (size_t)hcu);
+        memcpy(j.cost_est, t->host + L.ce + 16 * (size_t)e, 16);
+        memcpy(&j.intra_mbs, t->host + L.mbs + 4 * (size_t)e, 4);
+    }
+    return 0;
+}
+
+extern "C" int x265amd_la_bcost_n(x265amd_la* la, int n, x265amd_la_bjob* jobs, int rows_per_slice, int num_slices)
+{
+    if (!la || n < 0 || (n && !jobs)) return record(X265AMD_EINVAL);
+    if (!n) return 0;
+    for (int e = 0; e < n; e++)
+    {
+        const x265amd_la_bjob& j = jobs[e];
+        if (!j.fenc || !j.ref0 || !j.ref1 || !j.mvs0 || !j.mv_costs0 || !j.mvs1 || !j.mv_costs1 || !j.lowres_costs ||
+            !j.row_satd)
+            return record(X265AMD_EINVAL);
+    }
+    x265amd_la_thread* t;
+    LA_TRY(thread_ctx(la, &t));
+    const int ncu = la->ncu, hcu = la->cfg.height_cu;
+    const Layout L(ncu, hcu, n);
+    LA_TRY(reserve(t, L.end));
+    // per-estimate invQscaleFactor goes in a device array of its own (after the layout)
+    bool has_invq = false;
+    {
+        std::lock_guard<std::mutex> g(la->mu);
+        has_invq = la->frames.count(jobs[0].fenc) && la->frames[jobs[0].fenc].has_invq;
+    }
+    const size_t iq = (L.end + 255) & ~(size_t)255;
+    if (has_invq) LA_TRY(reserve(t, iq + 4 * (size_t)ncu * n));
+    int64_t* off = (int64_t*)(t->host + L.offs);
+    uint8_t* ds = t->host + L.ds;
+    for (int e = 0; e < n; e++)
+    {
+        const x265amd_la_bjob& j = jobs[e];
+        int sf, s0, s1;
+        LA_TRY(find_slot(la, j.fenc, &sf));
+        LA_TRY(find_slot(la, j.ref0, &s0));
+        LA_TRY(find_slot(la, j.ref1, &s1));
+        off[e] = plane_off(la, sf, 0);
+        for (int k = 0; k < 4; k++)
+        {
+            off[n + 4 * e + k] = plane_off(la, s0, k);
+            off[5 * n + 4 * e + k] = plane_off(la, s1, k);
+        }
+        ds[2 * e] = (uint8_t)!!j.do_search0;
+        ds[2 * e + 1] = (uint8_t)!!j.do_search1;
+        if (has_invq)
+            LA_TRY(hipMemcpyAsync(t->dev + iq + 4 * (size_t)ncu * e, la->invq + (size_t)sf * ncu, 4 * (size_t)ncu,
+                                  hipMemcpyDeviceToDevice, t->st));
+        // a list that is not searched reuses the stored lowresMvs / lowresMvCosts (slicetype.cpp:2105-2109, 2171-2172)
+        if (!j.do_search0)
+        {
+            memcpy(t->host + L.mvs0 + 4 * (size_t)ncu * e, j.mvs0, 4 * (size_t)ncu);
+            memcpy(t->host + L.mvc0 + 4 * (size_t)ncu * e, j.mv_costs0, 4 * (size_t)ncu);
+        }
+        if (!j.do_search1)
+        {
+            memcpy(t->host + L.mvs1 + 4 * (size_t)ncu * e, j.mvs1, 4 * (size_t)ncu);
+            memcpy(t->host + L.mvc1 + 4 * (size_t)ncu * e, j.mv_costs1, 4 * (size_t)ncu);
+        }
+    }
+    // inputs: the stored MVs / costs (all four arrays at once), descriptors, search flags
+    LA_TRY(hipMemcpyAsync(t->dev + L.mvs0, t->host + L.mvs0, L.lc - L.mvs0, hipMemcpyHostToDevice, t->st));
+    LA_TRY(hipMemcpyAsync(t->dev + L.offs, t->host + L.offs, L.end - L.offs, hipMemcpyHostToDevice, t->st));
+    const int64_t* doff = (const int64_t*)(t->dev + L.offs);
+    x265amd_lowres_bcost_batch b{ n, la->cfg.width_cu, hcu, rows_per_slice, num_slices, la->arena,
+                                  la->cfg.lowres_stride, doff, doff + n, doff + 5 * n, t->dev + L.ds,
+                                  has_invq ? (const int32_t*)(t->dev + iq) : nullptr, la->mvcost,
+                                  (int16_t*)(t->dev + L.mvs0), (int32_t*)(t->dev + L.mvc0),
+                                  (int16_t*)(t->dev + L.mvs1), (int32_t*)(t->dev + L.mvc1),
+                                  (uint16_t*)(t->dev + L.lc), (int32_t*)(t->dev + L.rs), (int64_t*)(t->dev + L.ce) };
+    LA_TRY(x265amd_lowres_bcost(la->cfg.depth, &b, t->st));
+    LA_TRY(hipMemcpyAsync(t->host + L.mvs0, t->dev + L.mvs0, L.offs - L.mvs0, hipMemcpyDeviceToHost, t->st));
+    LA_TRY(hipStreamSynchronize(t->st));
+    for (int e = 0; e < n; e++)
+    {
+        x265amd_la_bjob& j = jobs[e];
+        if (j.do_search0)
+        {
+            memcpy(j.mvs0, t->host + L.mvs0 + 4 * (size_t)ncu * e, 4 * (size_t)ncu);
+            memcpy(j.mv_costs0, t->host + L.mvc0 + 4 * (size_t)ncu * e, 4 * (size_t)ncu);
+        }
+        if (j.do_search1)
+        {
+            memcpy(j.mvs1, t->host + L.mvs1 + 4 * (size_t)ncu * e, 4 * (size_t)ncu);
+            memcpy(j.mv_costs1, t->host + L.mvc1 + 4 * (size_t)ncu * e, 4 * (size_t)ncu);
+        }
+        memcpy(j.lowres_costs, t->host + L.lc + 2 * (size_t)ncu * e, 2 * (size_t)ncu);
+        memcpy(j.row_satd, t->host + L.rs + 4 * (size_t)hcu * e, 4 * (size_t)hcu);
+        memcpy(j.cost_est, t->host + L.ce + 16 * (size_t)e, 16);
+    }
+    return 0;
+}
+
 extern "C" int x265amd_la_pcost(x265amd_la* la, const void* fenc, const void* ref, const void* weighted_buffer,
                                 int rows_per_slice, int num_slices, int16_t* mvs, int32_t* mv_costs,
                                 uint16_t* lowres_costs, int32_t* row_satd, int64_t* cost_est, int32_t* intra_mbs)
 {
-    if (!la || !fenc || !ref || !mvs || !mv_costs || !lowres_costs || !row_satd || !cost_est || !intra_mbs)
-        return record(X265AMD_EINVAL);
-    x265amd_la_thread* t;
-    LA_TRY(thread_ctx(la, &t));
-    int sf, sr;
-    LA_TRY(find_slot(la, fenc, &sf));
-    LA_TRY(find_slot(la, ref, &sr));
-    bool has_invq;
+    if (!cost_est || !intra_mbs) return record(X265AMD_EINVAL);
+    x265amd_la_pjob j{ fenc, ref, weighted_buffer, mvs, mv_costs, lowres_costs, row_satd, { 0, 0 }, 0 };
+    const int st = x265amd_la_pcost_n(la, 1, &j, rows_per_slice, num_slices);
+    if (!st)
     {
-        std::lock_guard<std::mutex> g(la->mu);
-        has_invq = la->frames[fenc].has_invq;
+        cost_est[0] = j.cost_est[0];
+        cost_est[1] = j.cost_est[1];
+        *intra_mbs = j.intra_mbs;
     }
-    const int ncu = la->ncu, hcu = la->cfg.height_cu;
-    const Layout L(ncu, hcu);
-    if (weighted_buffer)
-    {
-        // weightsAnalyse's planes (the calling thread's LookaheadTLD wbuffer, same layout)
-        LA_TRY(hipMemcpyAsync(la->arena + (size_t)t->wslot * la->frame_bytes, weighted_buffer, la->frame_bytes,
-                              hipMemcpyHostToDevice, t->st));
-        sr = t->wslot;
-    }
-    int64_t* off = (int64_t*)(t->host + L.offs);
-    off[0] = plane_off(la, sf, 0);
-    for (int k = 0; k < 4; k++) off[1 + k] = plane_off(la, sr, k);
-    LA_TRY(hipMemcpyAsync(t->dev + L.offs, off, 8 * 5, hipMemcpyHostToDevice, t->st));
-    const int64_t* doff = (const int64_t*)(t->dev + L.offs);
-    x265amd_lowres_pcost_batch b{ 1, la->cfg.width_cu, hcu, rows_per_slice, num_slices, la->arena,
-                                  la->cfg.lowres_stride, doff, doff + 1, la->intra + (size_t)sf * ncu,
-                                  has_invq ? la->invq + (size_t)sf * ncu : nullptr, la->mvcost,
-                                  (int16_t*)(t->dev + L.mvs0), (int32_t*)(t->dev + L.mvc0), (uint16_t*)(t->dev + L.lc),
-                                  (int32_t*)(t->dev + L.rs), (int64_t*)(t->dev + L.ce), (int32_t*)(t->dev + L.mbs) };
-    LA_TRY(x265amd_lowres_pcost(la->cfg.depth, &b, t->st));
-    // mvs0 .. mbs are contiguous in the layout: one download
-    LA_TRY(hipMemcpyAsync(t->host + L.mvs0, t->dev + L.mvs0, L.mvs1 - L.mvs0, hipMemcpyDeviceToHost, t->st));
-    LA_TRY(hipMemcpyAsync(t->host + L.lc, t->dev + L.lc, L.offs - L.lc, hipMemcpyDeviceToHost, t->st));
-    LA_TRY(hipStreamSynchronize(t->st));
-    memcpy(mvs, t->host + L.mvs0, 4 * (size_t)ncu);
-    memcpy(mv_costs, t->host + L.mvc0, 4 * (size_t)ncu);
-    memcpy(lowres_costs, t->host + L.lc, 2 * (size_t)ncu);
-    memcpy(row_satd, t->host + L.rs, 4 * (size_t)hcu);
-    memcpy(cost_est, t->host + L.ce, 16);
-    memcpy(intra_mbs, t->host + L.mbs, 4);
-    return 0;
+    return st;
 }
 
 extern "C" int x265amd_la_bcost(x265amd_la* la, const void* fenc, const void* ref0, const void* ref1, int do_search0,
@@ -330,68 +483,14 @@ extern "C" int x265amd_la_bcost(x265amd_la* la, const void* fenc, const void* re
                                 int16_t* mvs1, int32_t* mv_costs1, uint16_t* lowres_costs, int32_t* row_satd,
                                 int64_t* cost_est)
 {
-    if (!la || !fenc || !ref0 || !ref1 || !mvs0 || !mv_costs0 || !mvs1 || !mv_costs1 || !lowres_costs || !row_satd ||
-        !cost_est)
-        return record(X265AMD_EINVAL);
-    x265amd_la_thread* t;
-    LA_TRY(thread_ctx(la, &t));
-    int sf, s0, s1;
-    LA_TRY(find_slot(la, fenc, &sf));
-    LA_TRY(find_slot(la, ref0, &s0));
-    LA_TRY(find_slot(la, ref1, &s1));
-    bool has_invq;
+    if (!cost_est) return record(X265AMD_EINVAL);
+    x265amd_la_bjob j{ fenc, ref0, ref1, do_search0, do_search1, mvs0, mv_costs0, mvs1, mv_costs1, lowres_costs,
+                       row_satd, { 0, 0 } };
+    const int st = x265amd_la_bcost_n(la, 1, &j, rows_per_slice, num_slices);
+    if (!st)
     {
-        std::lock_guard<std::mutex> g(la->mu);
-        has_invq = la->frames[fenc].has_invq;
+        cost_est[0] = j.cost_est[0];
+        cost_est[1] = j.cost_est[1];
     }
-    const int ncu = la->ncu, hcu = la->cfg.height_cu;
-    const Layout L(ncu, hcu);
-    int64_t* off = (int64_t*)(t->host + L.offs);
-    off[0] = plane_off(la, sf, 0);
-    for (int k = 0; k < 4; k++)
-    {
-        off[1 + k] = plane_off(la, s0, k);
-        off[5 + k] = plane_off(la, s1, k);
-    }
-    uint8_t* ds = t->host + L.ds;
-    ds[0] = (uint8_t)!!do_search0;
-    ds[1] = (uint8_t)!!do_search1;
-    LA_TRY(hipMemcpyAsync(t->dev + L.offs, off, L.end - L.offs, hipMemcpyHostToDevice, t->st));
-    // a list that is not searched reuses the stored lowresMvs / lowresMvCosts (slicetype.cpp:2105-2109, 2171-2172)
-    if (!do_search0)
-    {
-        memcpy(t->host + L.mvs0, mvs0, 4 * (size_t)ncu);
-        memcpy(t->host + L.mvc0, mv_costs0, 4 * (size_t)ncu);
-        LA_TRY(hipMemcpyAsync(t->dev + L.mvs0, t->host + L.mvs0, L.mvs1 - L.mvs0, hipMemcpyHostToDevice, t->st));
-    }
-    if (!do_search1)
-    {
-        memcpy(t->host + L.mvs1, mvs1, 4 * (size_t)ncu);
-        memcpy(t->host + L.mvc1, mv_costs1, 4 * (size_t)ncu);
-        LA_TRY(hipMemcpyAsync(t->dev + L.mvs1, t->host + L.mvs1, L.lc - L.mvs1, hipMemcpyHostToDevice, t->st));
-    }
-    const int64_t* doff = (const int64_t*)(t->dev + L.offs);
-    x265amd_lowres_bcost_batch b{ 1, la->cfg.width_cu, hcu, rows_per_slice, num_slices, la->arena,
-                                  la->cfg.lowres_stride, doff, doff + 1, doff + 5, t->dev + L.ds,
-                                  has_invq ? la->invq + (size_t)sf * ncu : nullptr, la->mvcost,
-                                  (int16_t*)(t->dev + L.mvs0), (int32_t*)(t->dev + L.mvc0),
-                                  (int16_t*)(t->dev + L.mvs1), (int32_t*)(t->dev + L.mvc1),
-                                  (uint16_t*)(t->dev + L.lc), (int32_t*)(t->dev + L.rs), (int64_t*)(t->dev + L.ce) };
-    LA_TRY(x265amd_lowres_bcost(la->cfg.depth, &b, t->st));
-    LA_TRY(hipMemcpyAsync(t->host + L.mvs0, t->dev + L.mvs0, L.offs - L.mvs0, hipMemcpyDeviceToHost, t->st));
-    LA_TRY(hipStreamSynchronize(t->st));
-    if (do_search0)
-    {
-        memcpy(mvs0, t->host + L.mvs0, 4 * (size_t)ncu);
-        memcpy(mv_costs0, t->host + L.mvc0, 4 * (size_t)ncu);
-    }
-    if (do_search1)
-    {
-        memcpy(mvs1, t->host + L.mvs1, 4 * (size_t)ncu);
-        memcpy(mv_costs1, t->host + L.mvc1, 4 * (size_t)ncu);
-    }
-    memcpy(lowres_costs, t->host + L.lc, 2 * (size_t)ncu);
-    memcpy(row_satd, t->host + L.rs, 4 * (size_t)hcu);
-    memcpy(cost_est, t->host + L.ce, 16);
-    return 0;
+    return st;
 }

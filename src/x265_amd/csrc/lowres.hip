@@ -725,12 +725,16 @@ __global__ __launch_bounds__(1024) void k_lowres_bcost(const BcostArgs a)
     for (int y = tid; y < R; y += blockDim.x) rowsum[y] = 0;
     __syncthreads();
     int64_t est = 0, est_aq = 0;
-    const int steps = W + 2 * (R - 1);
+    // without a search in either list no CU depends on another (the MVPs are only for searching):
+    // every CU of the slice in one flat pass instead of the slope-2 wavefront
+    const bool wave = a.do_search[2 * e] || a.do_search[2 * e + 1];
+    const int steps = wave ? W + 2 * (R - 1) : 1;
     for (int t = 0; t < steps; t++)
     {
-        for (int yp = g; yp < R; yp += nq)
+        for (int it = g; it < (wave ? R : R * W); it += nq)
         {
-            const int xp = t - 2 * yp;
+            const int yp = wave ? it : it / W;
+            const int xp = wave ? t - 2 * yp : it % W;
             if (xp < 0 || xp >= W) continue;
             const int cx = W - 1 - xp, cy = last - yp;
             const int xy = cx + cy * W;
@@ -822,7 +826,7 @@ __global__ __launch_bounds__(1024) void k_lowres_bcost(const BcostArgs a)
             if (lead && li == 0)
             {
                 if (scored) { est += bcost; est_aq += bcost_aq; }
-                rowsum[yp] += bcost_aq;
+                atomicAdd(&rowsum[yp], bcost_aq);           // flat pass: several groups per row
                 a.lowres_costs[cub + xy] = (uint16_t)((bcost < 0x3fff ? bcost : 0x3fff) | (listused << 14));
             }
         }
