@@ -551,6 +551,38 @@ typedef struct
 int x265amd_la_pcost_n(x265amd_la* la, int n, x265amd_la_pjob* jobs, int rows_per_slice, int num_slices);
 int x265amd_la_bcost_n(x265amd_la* la, int n, x265amd_la_bjob* jobs, int rows_per_slice, int num_slices);
 
+/* ------------------------------------------------------------------ (e)
+ * Frame-parallel schedule, host only: the GOP model of --preset medium
+ * (bframes 4, b-pyramid, 3 references, L1 <= 2; param.cpp:145-174, dpb.cpp:149-150,
+ * slicetype.cpp:993-1078) over closed segments of segment_frames pictures, frame j (encode order)
+ * on rank j mod world (encoder.cpp:649-650), and the earliest step of every CTU-row band: after the
+ * frame's previous band and after every reference has published the band holding row
+ * r1 - 2 + lag (frameencoder.cpp:516-531; a band is published in the step of the next band's
+ * deblocking, the last band in its own).  step[j * nbands + b]; *nsteps = last step + 1. */
+enum { X265AMD_FRAME_I = 0, X265AMD_FRAME_P = 1, X265AMD_FRAME_BREF = 2, X265AMD_FRAME_B = 3 };
+typedef struct
+{
+    int frames;            /* pictures in encode order, all segments */
+    int segment_frames;    /* pictures per closed segment (each starts with an I picture) */
+    int bframes;           /* 4 at --preset medium */
+    int b_pyramid;         /* 1 */
+    int max_refs;          /* maxNumReferences: 3 */
+    int max_refs_l1;       /* 2 with b-pyramid */
+    int ctu_rows, band_rows;
+    int lag;               /* refLagRows: 2 at --preset medium (frameencoder.cpp:114-119) */
+    int world;
+} x265amd_sched_config;
+typedef struct
+{
+    int poc;               /* display order over the whole sequence */
+    int type;              /* X265AMD_FRAME_* */
+    int is_ref;            /* I / P / B-ref */
+    int rank;
+    int nrefs, nrefs_l0;   /* refs[0 .. nrefs_l0) = L0 (nearest first), then L1 */
+    int refs[6];           /* encode indices */
+} x265amd_sched_frame;
+int x265amd_schedule(const x265amd_sched_config* config, x265amd_sched_frame* frames, int* step, int* nsteps);
+
 /* f1 cuTree: Lookahead::estimateCUPropagate (slicetype.cpp:1738-1836) with the
  * propagateCost primitive (pixel.cpp:846-872), one call of it per batch, batches in order.
  * For every lowres CU of frame b: the amount

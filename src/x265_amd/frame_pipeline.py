@@ -1,27 +1,25 @@
 """The frame-parallel GPU step (bench.py --mode pipeline).
 
-Per rank: the frames i = k * G + rank (k < F) of a G * F frame sequence, each
-encoded band by band of CTU rows with the row dependencies of x265's frame
-threads (pipeline.py): band b of frame i runs once the reference (frame i - 1,
-encoded by rank (i - 1) mod G) has published the rows band b's motion search
-reads; after it, band b is deblocked and band b - 1 SAO-filtered,
-border-extended and published to the owner of frame i + 1 over RCCL.
+Per rank: the frames j with j mod G == rank of a G * F frame sequence (closed segments of the
+--preset medium GOP, pipeline.Schedule), each encoded band by band of CTU rows in the steps the
+schedule gives: a band runs once every reference it reads has published the rows it needs;
+after it the band is deblocked and the bands that became final are SAO-filtered,
+border-extended and sent to the reference stores of every rank that owns a frame referencing
+them (RCCL P2P; a local copy for the rank's own consumers).
 
-The per-band work is the recorded x265 primitive census of the frame
-(census_batches), its jobs split by the CTU row they belong to (`band_slices`),
-followed by the f4 loop filters on the band (x265amd_deblock_rows /
-_sao_apply_rows / _extend_border_rows).  Each (frame, band) is one captured
-hipGraph (its launches spread over several streams); the exchange runs between
-graph replays (an RCCL receive is a stream wait, not a host block).
+The per-band work is the recorded x265 primitive census of the frame (census_batches), its jobs
+split by the (frame, band) they belong to and regrouped per STEP: every census batch contributes
+one slice per step (all frames and bands the step holds), so a step is one set of grouped
+launches whatever the number of frames in it, followed by the f4 loop filters of the step
+(x265amd_deblock_rows / _sao_apply_rows / _extend_border_rows, one call per kernel for all its
+bands).  Census jobs of a frame read its references (L0 and L1) from the rank's reference store;
+`check_reference_reach` verifies that no job reads a reference row beyond refLagRows.
 
-The census jobs of band b read the reference slot of their frame only inside
-rows <= r1 - 1 + refLagRows (CTU rows): the motion vectors of the census
-workload stay within +-MV_RANGE (48) + 2 px plus the 8-tap window, less than the
-57 + 7 px that refLagRows = 2 covers (frameencoder.cpp:114-119);
-`check_reference_reach` verifies it on the built batches.
+On one rank the whole sequence (steps + local reference copies) is ONE hipGraph; with several
+ranks each step is a graph replay followed by the step's exchange.
 
-The reconstruction a real encoder writes (prediction + residual) is stood in for
-by the band's source pixels, copied into the recon buffer before the loop filters.
+The reconstruction a real encoder writes (prediction + residual) is stood in for by the band's
+source pixels, copied into the recon buffer before the loop filters.
 """
 from __future__ import annotations
 
@@ -30,8 +28,8 @@ import ctypes
 import numpy as np
 
 from .native import capture_graph
-from .pipeline import BandPlan, RowExchange, run_frames
-from .workload import (CENSUS_1080P, FrameSet, WorkloadBuilder, census_batches, group_launches, load_census)
+from .pipeline import BandPlan, RefExchange, Schedule
+from .workload import CENSUS_1080P, FrameSet, WorkloadBuilder, census_batches, group_launches, load_census
 
 # per-job device tensors of a Batch (everything else — planes, pools, slot buffers — is shared)
 PER_JOB = {"aoff", "boff", "foff", "roff", "soff", "doff", "coeff", "co", "qo", "oo", "dlo", "nbo", "mode", "bf",
@@ -39,22 +37,12 @@ PER_JOB = {"aoff", "boff", "foff", "roff", "soff", "doff", "coeff", "co", "qo", 
 
 
 def job_rows(b, fs: FrameSet):
-    """(stored frame, luma picture row) of every job of batch b, from the offset of its
-    block in a frame plane; jobs of pool-based batches (coefficients, intra
-    neighbours) are spread evenly over the frames and rows in job order."""
-    d = b.dev
-    key = {"pixelcmp": ("a", "aoff"), "sad_multi": ("f", "foff"), "interp": ("s", "soff"),
-           "blockop": ("a", "aoff"), "transform": ("s", "soff")}.get(b.kind)
-    plane = d.get(key[0]) if key else None
-    if plane is not None and (plane is fs.luma or plane is fs.resid or plane is fs.cb or plane is fs.cr):
-        off = d[key[1]].cpu().numpy().astype(np.int64)
-        per = len(off) // b.n
-        off = off.reshape(b.n, per)[:, 0]
-        chroma = plane is fs.cb or plane is fs.cr
-        psize, stride, my = (fs.cplane_size, fs.cstride, fs.cmy) if chroma else (fs.plane_size, fs.stride, fs.my)
-        frame = (off // psize) % fs.F
-        y = (off % psize) // stride - my
-        return frame, np.clip(y * (2 if chroma else 1), 0, fs.ph - 1)
+    """(stored frame, luma picture row) of every job of batch b: the block the job codes (recorded
+    by the workload builder); jobs of pool-based batches (coefficients, intra neighbours) are
+    spread evenly over the frames and rows in job order"""
+    if b.pos is not None:
+        f, y = b.pos
+        return np.asarray(f, np.int64), np.clip(np.asarray(y, np.int64), 0, fs.ph - 1)
     j = np.arange(b.n, dtype=np.int64)
     frame = j * fs.F // b.n
     start = (frame * b.n + fs.F - 1) // fs.F
@@ -81,64 +69,41 @@ def _take(b, idx=None, lo=None, hi=None):
         else:
             dev[k] = t
     n = b.n if idx is not None else hi - lo
-    out = replace(b, n=n, dev=dev)
+    pos = None
+    if b.pos is not None:
+        pos = tuple(np.asarray(a)[idx] if idx is not None else np.asarray(a)[lo:hi] for a in b.pos)
+    out = replace(b, n=n, dev=dev, pos=pos)
     out.bytes = b.bytes * n / b.n
     return out
 
 
-def band_slices(batches, fs: FrameSet, plan: BandPlan, ctu: int = 64):
-    """{(frame, band): [batch slices]} — every job of every batch in exactly one slice"""
+def keyed_slices(batches, fs: FrameSet, key_of, nkeys: int, ctu: int, plan: BandPlan):
+    """{key: [batch slices]}: every job of every batch in exactly one slice; key_of(frame, band)
+    (numpy arrays) gives the job's key"""
     out = {}
     for b in batches:
         frame, y = job_rows(b, fs)
         band = np.minimum(y // ctu, plan.ctu_rows - 1) // plan.band_rows
-        key = frame * plan.nbands + band
+        key = key_of(frame, band)
         if np.any(np.diff(key) < 0):
             order = np.argsort(key, kind="stable")
             b = _take(b, idx=order)
             key = key[order]
-        bounds = np.searchsorted(key, np.arange(fs.F * plan.nbands + 1))
-        for kk in range(fs.F * plan.nbands):
+        bounds = np.searchsorted(key, np.arange(nkeys + 1))
+        for kk in range(nkeys):
             lo, hi = int(bounds[kk]), int(bounds[kk + 1])
             if hi > lo:
-                out.setdefault(divmod(kk, plan.nbands), []).append(_take(b, lo=lo, hi=hi))
+                out.setdefault(kk, []).append(_take(b, lo=lo, hi=hi))
     return out
 
 
-def wave_delay(plan: BandPlan) -> int:
-    """bands by which frame k + 1 trails frame k in the single-rank wavefront: its band b needs
-    reference band need(b), which frame k publishes in the step of band need(b) + 1 (after that
-    band's deblocking) or, for the last band, in its own step; the publication must come from an
-    earlier step, so d > need(b) + 1 - b for every b"""
-    return max(min(plan.need(b) + 1, plan.nbands - 1) + 1 - b for b in range(plan.nbands))
-
-
-def step_slices(batches, fs: FrameSet, plan: BandPlan, d: int, ctu: int = 64):
-    """{step: [batch slices]} of the wavefront schedule, step = frame * d + band: the (frame, band)
-    pairs of one step are independent, so each census batch contributes ONE slice per step"""
-    out = {}
-    nsteps = (fs.F - 1) * d + plan.nbands
-    for b in batches:
-        frame, y = job_rows(b, fs)
-        band = np.minimum(y // ctu, plan.ctu_rows - 1) // plan.band_rows
-        key = frame * d + band
-        if np.any(np.diff(key) < 0):
-            order = np.argsort(key, kind="stable")
-            b = _take(b, idx=order)
-            key = key[order]
-        bounds = np.searchsorted(key, np.arange(nsteps + 1))
-        for st in range(nsteps):
-            lo, hi = int(bounds[st]), int(bounds[st + 1])
-            if hi > lo:
-                out.setdefault(st, []).append(_take(b, lo=lo, hi=hi))
-    return out
-
-
-def check_reference_reach(slices, fs: FrameSet, plan: BandPlan, ctu: int = 64, taps: int = 8):
-    """every reference read of band b's jobs lies in CTU rows <= rows(b)[1] - 1 + lag"""
+def check_reference_reach(slices_by_fb, fs: FrameSet, plan: BandPlan, ctu: int = 64, taps: int = 8):
+    """every reference read of band b's jobs lies in CTU rows < rows(b)[1] - 1 + lag, i.e. within
+    the rows frameencoder.cpp:526-527 lets row r1 - 1 see; reads of the rank's own pictures (an I
+    frame's jobs) are not reference reads and are skipped entry by entry"""
     bad = []
-    for (k, band), bs in slices.items():
-        limit = (plan.rows(band)[1] + plan.lag) * ctu          # first luma row that is not yet published
+    for (k, band), bs in slices_by_fb.items():
+        limit = plan.reach_rows(band) * ctu                    # first luma row not yet published
         for b in bs:
             for key, plane_key in (("boff", "b"), ("roff", "r"), ("soff", "s")):
                 t = b.dev.get(key)
@@ -149,9 +114,10 @@ def check_reference_reach(slices, fs: FrameSet, plan: BandPlan, ctu: int = 64, t
                 chroma = pl is not fs.luma
                 psize, stride, my = (fs.cplane_size, fs.cstride, fs.cmy) if chroma else (fs.plane_size, fs.stride, fs.my)
                 stored = off // psize
-                if not np.all(stored >= fs.F):
-                    continue                                       # not a reference-slot read
-                last = (off % psize) // stride - my + b.h + taps // 2   # last row the block (+ filter taps) reads
+                sel = stored >= fs.F                               # entries that read the reference store
+                if not sel.any():
+                    continue
+                last = (off[sel] % psize) // stride - my + b.h + taps // 2   # last row the block (+ filter taps) reads
                 if chroma:
                     last = 2 * last + 1
                 if last.max() >= limit:
@@ -160,26 +126,37 @@ def check_reference_reach(slices, fs: FrameSet, plan: BandPlan, ctu: int = 64, t
 
 
 class GpuFramePipeline:
-    def __init__(self, prims, width, height, depth, frames_local, world, rank, census=None, band_rows=1,
-                 streams=8, device="cuda", seed=11):
+    def __init__(self, prims, width, height, depth, frames_local, world, rank, census=None, band_rows=None,
+                 segment_frames=None, streams=8, device="cuda", seed=11):
         import torch
 
         self.prims, self.world, self.rank, self.depth = prims, world, rank, depth
         self.F = frames_local
         self.total = frames_local * world
-        ids = [k * world + rank for k in range(frames_local)]
-        self.fs = fs = FrameSet(width, height, frames_local, depth, device=device, frame_ids=ids)
         ctu = 64
-        self.plan = plan = BandPlan(ctu_rows=fs.ph // ctu, band_rows=band_rows)
+        ph = (height + ctu - 1) // ctu * ctu
+        self.plan = plan = BandPlan(ctu_rows=ph // ctu, band_rows=band_rows or ph // ctu)
+        self.segment_frames = segment_frames or frames_local
+        self.sched = s = Schedule(self.total, world, plan, segment_frames=self.segment_frames)
+        self.local = s.local_frames(rank)
+        assert len(self.local) == frames_local
+        self.kof = {j: k for k, j in enumerate(self.local)}
+        self.store = s.store_frames(rank)
+        self.sof = {r: frames_local + i for i, r in enumerate(self.store)}
+        self.fs = fs = FrameSet(width, height, frames_local, depth, device=device,
+                                frame_ids=[s.poc[j] for j in self.local], store_ids=[s.poc[r] for r in self.store],
+                                ref_slots=[[self.sof[r] for r in s.refs[j]] for j in self.local])
         census = census or load_census(CENSUS_1080P)
         self.batches, self.wb = census_batches(fs, frames=frames_local, census=census,
                                                builder=WorkloadBuilder(fs, seed=seed + rank))
-        self.slices = band_slices(self.batches, fs, plan, ctu)
+        nb = plan.nbands
+        self.slices = {divmod(kk, nb): v for kk, v in
+                       keyed_slices(self.batches, fs, lambda f, b: f * nb + b, frames_local * nb, ctu, plan).items()}
         bad = check_reference_reach(self.slices, fs, plan, ctu)
         if bad:
             raise RuntimeError(f"census jobs read reference rows beyond refLagRows: {bad[:4]}")
         # recon buffers: work (deblocked in place) and final (SAO output, border-extended), per local frame
-        mk = lambda ref: torch.empty_like(ref)
+        mk = lambda ref: torch.empty_like(ref[:frames_local * (ref.numel() // fs.stored)])
         self.work = [mk(fs.luma), mk(fs.cb), mk(fs.cr)]
         self.final = [mk(fs.luma), mk(fs.cb), mk(fs.cr)]
         for t in self.work + self.final:
@@ -191,7 +168,7 @@ class GpuFramePipeline:
             return [bufs[p][k * sizes[p]:(k + 1) * sizes[p]] for p in range(3)]
 
         self.frame_planes = frame_planes
-        src_planes = [fs.luma, fs.cb, fs.cr]
+        self.src_planes = src_planes = [fs.luma, fs.cb, fs.cr]
         regions = []
         for p in range(3):
             rows, stride, my = (fs.rows, fs.stride, fs.my) if p == 0 else (fs.crows, fs.cstride, fs.cmy)
@@ -199,15 +176,13 @@ class GpuFramePipeline:
                 stride * r for r in self.plan.region(b, ctu, my, rows, shift=int(p > 0))))
         self.regions = regions
 
-        def planes_of(kind, k):
-            return frame_planes(self.final, k) if kind == "final" else frame_planes(src_planes, self.F + k)
+        def planes_of(kind, j):
+            return frame_planes(self.final, self.kof[j]) if kind == "final" else frame_planes(src_planes, self.sof[j])
 
-        self._planes_of = planes_of
-        self.ex = RowExchange(world, rank, plan, planes_of, regions, self.total)
+        self.ex = RefExchange(s, rank, planes_of, regions)
         self._f4_setup(width, height, device)
         self.streams = [torch.cuda.Stream() for _ in range(max(1, streams))] if streams > 1 else []
         self.graphs = {}
-        self.src_planes = src_planes
 
     # ---------------------------------------------------------------- f4 descriptors
     def _f4_setup(self, width, height, device):
@@ -266,147 +241,60 @@ class GpuFramePipeline:
             self.bor.append(bps)
         self.W, self.H = width, height
 
-    # ---------------------------------------------------------------- per-band work
+    # ---------------------------------------------------------------- steps
     def _rows_px(self, b):
         r0, r1 = self.plan.rows(b)
         return r0 * 64, min(r1 * 64, self.H)
 
-    def _finish(self, k, b, stream):
-        y0, y1 = self._rows_px(b)
-        last = b == self.plan.nbands - 1
-        self.prims.sao_apply_rows(self.depth, [self.sao[k]], [self.plan.rows(b)[0], self.plan.rows(b)[1]], stream)
-        self.prims.extend_border_rows(self.depth, self.bor[k], [y0, y1, b == 0, last] +
-                                      [y0 // 2, y1 // 2, b == 0, last] * 2, stream)
-
-    def band_work(self, k, b):
-        """launch the whole work of (frame k, band b) on the current stream (graph-capturable)"""
+    def build(self, graphs=True):
+        """regroup the census slices per step (one slice per census batch per step, grouped launches),
+        and capture the work: one graph for the whole sequence on one rank, one per step otherwise"""
         import torch
 
-        cur = torch.cuda.current_stream()
-        groups = self._groups.get((k, b), [])
-        if self.streams:
-            lanes = [[] for _ in self.streams]
-            load = [0.0] * len(self.streams)
-            for g in groups:
-                i = min(range(len(self.streams)), key=lambda j: load[j])
-                lanes[i].append(g)
-                load[i] += g.bytes
-            for s_, lst in zip(self.streams, lanes):
-                if not lst:
-                    continue
-                s_.wait_stream(cur)
-                h = ctypes.c_void_p(s_.cuda_stream)
-                for g in lst:
-                    g.run(self.prims, h)
-            for s_, lst in zip(self.streams, lanes):
-                if lst:
-                    cur.wait_stream(s_)
-        else:
-            for g in groups:
-                g.run(self.prims)
-        # the reconstruction of the band (stand-in: its source pixels) into the recon buffer
-        y0, y1 = self._rows_px(b)
-        fs = self.fs
-        for p in range(3):
-            stride, my, sh = (fs.stride, fs.my, 0) if p == 0 else (fs.cstride, fs.cmy, 1)
-            s, e = (my + (y0 >> sh)) * stride, (my + (y1 >> sh)) * stride
-            src = self.src_planes[p][k * self._sizes[p]:(k + 1) * self._sizes[p]]
-            self.frame_planes(self.work, k)[p][s:e].copy_(src[s:e])
-        h = ctypes.c_void_p(cur.cuda_stream)
-        self.prims.deblock_rows(self.depth, [self.dbk[k]], [y0, y1], h)
-        if b:
-            self._finish(k, b - 1, h)
-        if b == self.plan.nbands - 1:
-            self._finish(k, b, h)
-
-    def set_band_rows(self, band_rows: int):
-        """re-slice the same census batches into bands of another height (single rank);
-        call build() again afterwards"""
-        assert self.world == 1
-        self.plan = BandPlan(ctu_rows=self.fs.ph // 64, band_rows=band_rows)
-        self.slices = band_slices(self.batches, self.fs, self.plan, 64)
-        self.ex = RowExchange(1, 0, self.plan, self._planes_of, self.regions, self.total)
-        self.graphs = {}
-
-    def build(self, graphs=True, one_graph=False):
-        """group each (frame, band)'s slices into launches and capture one hipGraph per band
-        (one_graph, single rank only: the whole step — every band and the local row
-        publications — as ONE graph)"""
-        import torch
-
-        self._groups = {kb: group_launches(bs) for kb, bs in self.slices.items()}
-        for kb, gs in self._groups.items():
+        s, nb = self.sched, self.plan.nbands
+        step_of = np.array([[s.step[j, b] for b in range(nb)] for j in self.local], np.int64)
+        self.step_slices = keyed_slices(self.batches, self.fs, lambda f, b: step_of[f, b], s.nsteps, 64, self.plan)
+        self._sgroups = {st: group_launches(bs) for st, bs in self.step_slices.items()}
+        for gs in self._sgroups.values():
             for g in gs:
                 g.run(self.prims)       # build grouped descriptor tables outside any capture
         torch.cuda.synchronize()
+        self.graphs = {}
         if not graphs:
             return
-        s = torch.cuda.Stream()
-        s.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(s):
-            for k in range(self.F):
-                for b in range(self.plan.nbands):
-                    self.band_work(k, b)
-        torch.cuda.current_stream().wait_stream(s)
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):                        # warm-up pass (allocations, descriptor uploads)
+            self._run_all(exchange=self.world == 1)
+        torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
-        if one_graph and self.world == 1:
+        if self.world == 1:
             g = torch.cuda.CUDAGraph()
             with capture_graph(g):
-                self._eager_step()
-            self.graphs["step"] = g
-            torch.cuda.synchronize()
-            return
-        for k in range(self.F):
-            for b in range(self.plan.nbands):
+                self._run_all(exchange=True)                 # exchange = local copies: capturable
+            self.graphs["all"] = g
+        else:
+            for st in range(s.nsteps):
                 g = torch.cuda.CUDAGraph()
                 with capture_graph(g):
-                    self.band_work(k, b)
-                self.graphs[(k, b)] = g
+                    self._step_work(st)
+                self.graphs[st] = g
         torch.cuda.synchronize()
 
-    def _eager_step(self):
-        run_frames(self.ex, self.F, self.band_work, lambda k, b: None, lambda k, b: None)
+    def _run_all(self, exchange):
+        for st in range(self.sched.nsteps):
+            self._step_work(st)
+            if exchange:
+                self.ex.exchange(st)
 
-    # ---------------------------------------------------------------- single-rank wavefront
-    def build_wave(self):
-        """Single rank: schedule (frame k, band b) at step k * d + b (d = wave_delay) — the bands of
-        consecutive frames that x265's frame threads run concurrently — so one step's census work
-        of every frame goes out as one set of grouped launches and its loop filters as one call per
-        kernel, and capture the whole sequence as ONE hipGraph.  Same results as step()."""
+    def _step_work(self, st):
+        """launch the whole work of step st on the current stream (graph-capturable)"""
         import torch
 
-        assert self.world == 1
-        self.d = wave_delay(self.plan)
-        self.nsteps = (self.F - 1) * self.d + self.plan.nbands
-        self.wslices = step_slices(self.batches, self.fs, self.plan, self.d)
-        self._wgroups = {st: group_launches(bs) for st, bs in self.wslices.items()}
-        for gs in self._wgroups.values():
-            for g in gs:
-                g.run(self.prims)
-        torch.cuda.synchronize()
-        s = torch.cuda.Stream()
-        s.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(s):
-            self._wave_all()
-        torch.cuda.current_stream().wait_stream(s)
-        torch.cuda.synchronize()
-        g = torch.cuda.CUDAGraph()
-        with capture_graph(g):
-            self._wave_all()
-        self.graphs = {"wave": g}
-        torch.cuda.synchronize()
-
-    def _wave_all(self):
-        for st in range(self.nsteps):
-            self._wave_step(st)
-
-    def _wave_step(self, st):
-        import torch
-
-        plan, nb = self.plan, self.plan.nbands
-        pairs = [(k, st - k * self.d) for k in range(self.F) if 0 <= st - k * self.d < nb]
+        s, plan = self.sched, self.plan
+        items = s.items(self.rank, st)
         cur = torch.cuda.current_stream()
-        groups = self._wgroups.get(st, [])
+        groups = self._sgroups.get(st, [])
         if self.streams:
             lanes = [[] for _ in self.streams]
             load = [0.0] * len(self.streams)
@@ -428,7 +316,8 @@ class GpuFramePipeline:
             for g in groups:
                 g.run(self.prims)
         fs = self.fs
-        for k, b in pairs:                       # the bands' reconstruction (stand-in: source pixels)
+        for j, b in items:                       # the bands' reconstruction (stand-in: source pixels)
+            k = self.kof[j]
             y0, y1 = self._rows_px(b)
             for p in range(3):
                 stride, my, sh = (fs.stride, fs.my, 0) if p == 0 else (fs.cstride, fs.cmy, 1)
@@ -436,48 +325,54 @@ class GpuFramePipeline:
                 src = self.src_planes[p][k * self._sizes[p]:(k + 1) * self._sizes[p]]
                 self.frame_planes(self.work, k)[p][s0:e0].copy_(src[s0:e0])
         h = ctypes.c_void_p(cur.cuda_stream)
-        rows = []
-        for k, b in pairs:
-            rows += list(self._rows_px(b))
-        self.prims.deblock_rows(self.depth, [self.dbk[k] for k, _ in pairs], rows, h)
-        # bands finished in this step: b - 1 of every pair, and b itself when it is the last band
-        done = [(k, b - 1) for k, b in pairs if b] + [(k, b) for k, b in pairs if b == nb - 1]
+        if items:
+            rows = []
+            for j, b in items:
+                rows += list(self._rows_px(b))
+            self.prims.deblock_rows(self.depth, [self.dbk[self.kof[j]] for j, _ in items], rows, h)
+        done = s.finals(self.rank, st)           # bands that became final in this step
         if done:
-            self.prims.sao_apply_rows(self.depth, [self.sao[k] for k, _ in done],
+            self.prims.sao_apply_rows(self.depth, [self.sao[self.kof[j]] for j, _ in done],
                                       [r for _, c in done for r in plan.rows(c)], h)
             planes, brows = [], []
-            for k, c in done:
+            nb = plan.nbands
+            for j, c in done:
                 y0, y1 = self._rows_px(c)
                 first, last = int(c == 0), int(c == nb - 1)
-                planes += self.bor[k]
+                planes += self.bor[self.kof[j]]
                 brows += [y0, y1, first, last] + [y0 // 2, y1 // 2, first, last] * 2
             self.prims.extend_border_rows(self.depth, planes, brows, h)
-            for k, c in done:
-                self.ex.publish(k, c)
 
-    def wave_launches_per_step(self):
-        return sum(len(v) for v in self._wgroups.values()) + 3 * self.nsteps
+    def reset_stores(self):
+        """put the reference stores back to the unfiltered source pictures they start with (tests: a
+        job that reads a reference before its publication then sees different pixels)"""
+        import torch
+
+        fs = self.fs
+        for dev, key, size in ((fs.luma, "Y", fs.plane_size), (fs.cb, "U", fs.cplane_size), (fs.cr, "V", fs.cplane_size)):
+            lo = self.F * size
+            dev[lo:].copy_(torch.from_numpy(fs.host[key][lo:]).to(dev.device))
+        torch.cuda.synchronize()
 
     def step(self):
-        """one sequence of G * F frames: this rank's F frames with the row exchange"""
-        if "wave" in self.graphs:
-            self.graphs["wave"].replay()
+        """one sequence: this rank's frames in the schedule's steps, with the reference exchange"""
+        if "all" in self.graphs:
+            self.graphs["all"].replay()
             return
-        if "step" in self.graphs:
-            self.graphs["step"].replay()
-            return
-
-        def encode(k, b):
-            g = self.graphs.get((k, b))
+        for st in range(self.sched.nsteps):
+            g = self.graphs.get(st)
             if g is not None:
                 g.replay()
             else:
-                self.band_work(k, b)
-        run_frames(self.ex, self.F, encode, lambda k, b: None, lambda k, b: None)
+                self._step_work(st)
+            self.ex.exchange(st)
 
     @property
     def launches_per_step(self):
-        return sum(len(v) for v in self._groups.values()) + self.F * (2 * self.plan.nbands + 2 * self.plan.nbands)
+        s = self.sched
+        filt = sum((1 if s.items(self.rank, st) else 0) + 2 * (1 if s.finals(self.rank, st) else 0)
+                   for st in range(s.nsteps))
+        return sum(len(v) for v in self._sgroups.values()) + filt
 
     @property
     def calls(self):

@@ -1,47 +1,40 @@
-"""Frame-parallel shard with reconstructed-row exchange (BASELINE config 4).
+"""Frame-parallel GOP shard with reconstructed-reference exchange (BASELINE config 4).
 
-x265 runs frames in parallel on FrameEncoders assigned round robin
-(encoder.cpp:649-650).  Frames share nothing but reconstructed reference rows:
-FrameFilter publishes a CTU row once it is deblocked, SAO-filtered and
-border-extended (m_reconRowCount, framefilter.cpp:520), and a frame encoding CTU
-row r waits until its reference has published r + refLagRows rows
-(frameencoder.cpp:516-531; refLagRows = 1 + ceil((merange + 1 + 4 + 2) / 64) = 2 at
---preset medium, frameencoder.cpp:114-119).  Across GPUs the same structure is:
+x265 runs frames in parallel on FrameEncoders assigned round robin (encoder.cpp:649-650).
+Frames share nothing but reconstructed reference rows: FrameFilter publishes a CTU row once it
+is deblocked, SAO-filtered and border-extended (m_reconRowCount, framefilter.cpp:520), and a
+frame encoding CTU row r waits until EACH of its references has published r + refLagRows rows
+(frameencoder.cpp:516-531; refLagRows = 2 at --preset medium, frameencoder.cpp:114-119).
+Across GPUs the same structure is:
 
-  * frame i is encoded by rank i mod G (`owner`);
-  * a frame is processed in bands of CTU rows; band b is encoded once the
-    reference frame has published the bands covering rows up to
-    r1 - 1 + refLagRows (`BandPlan.need`);
-  * FrameFilter's row order: deblocking band b changes the last rows of band
-    b - 1 (a horizontal edge filter writes 3 rows on each side), so band b - 1
-    is SAO-filtered, border-extended and published after band b is deblocked
-    (the last band right after its own deblocking);
-  * a published band (full-stride rows, plus the margin rows above band 0 and
-    below the last band) goes to the owner of frame i + 1 — point-to-point over
-    RCCL / xGMI on the GPU (gloo in the CPU tests), on one 2-rank communicator
-    per ring link so that every communicator carries traffic in one direction
-    only (a rank's sends can never queue behind its own receives).  With G = 1
-    the band is copied into the local reference slot.
+  * the GOP of --preset medium (bframes 4, b-pyramid, 3 references; x265amd_schedule in
+    csrc/schedule.cpp restates the mini-GOP and reference-list rules) over closed segments;
+    frame j (encode order) is encoded by rank j mod G;
+  * a frame is processed in bands of CTU rows; the schedule gives every (frame, band) the
+    earliest STEP after its previous band and after each reference published the band that
+    holds row r1 - 2 + refLagRows (BandPlan.need);
+  * FrameFilter's row order: deblocking band b changes the last rows of band b - 1, so band
+    b - 1 becomes final (SAO, border extension) in band b's step, the last band in its own;
+  * a final band of a REFERENCE picture goes to every rank that owns a frame referencing it
+    (fan-out up to the pictures' L0 + L1 users; non-reference b pictures publish nothing),
+    point to point over RCCL / xGMI on the GPU (torch.distributed P2P; gloo in the CPU tests),
+    into that rank's reference store; a rank's own consumers get a local copy.
 
-Nothing else crosses ranks.  The pipeline is generic over the per-band work
-(`encode`, `deblock`, `finish` callbacks); bench.py plugs in the census
-primitive workload and the f4 loop-filter kernels, tests/test_pipeline.py a
-CPU stand-in with the same row dependencies.
+Each rank runs the steps in order: its (frame, band) work of the step, then the step's
+exchange (one batch of sends and receives, identical order on both sides of every link).
+The pipeline is generic over the per-band work (`encode`, `deblock`, `finish` callbacks);
+bench.py plugs in the census primitive workload and the f4 loop-filter kernels
+(frame_pipeline.py), tests/test_pipeline.py a CPU stand-in with the same row dependencies.
 """
 from __future__ import annotations
 
+import ctypes
 from dataclasses import dataclass
 
+import numpy as np
+
 REF_LAG_ROWS_MEDIUM = 2   # frameencoder.cpp:114-119 with merange 57
-
-
-def owner(i: int, world: int) -> int:
-    """Rank that encodes frame i (encoder.cpp:649-650 round robin over FrameEncoders)."""
-    return i % world
-
-
-def owned_frames(total: int, rank: int, world: int) -> list:
-    return list(range(rank, total, world))
+FRAME_I, FRAME_P, FRAME_BREF, FRAME_B = range(4)
 
 
 @dataclass
@@ -63,9 +56,14 @@ class BandPlan:
         return min(row, self.ctu_rows - 1) // self.band_rows
 
     def need(self, b: int) -> int:
-        """last reference band that must be published before band b is encoded:
-        the band holding CTU row r1 - 1 + lag (frameencoder.cpp:516-531)"""
-        return self.band_of(self.rows(b)[1] - 1 + self.lag)
+        """last reference band that must be published before band b is encoded: row r of the band
+        waits for rows 0 .. r + lag - 1 (frameencoder.cpp:526-527), so the last row r1 - 1 needs
+        the band holding row r1 - 2 + lag"""
+        return self.band_of(self.rows(b)[1] - 2 + self.lag)
+
+    def reach_rows(self, b: int) -> int:
+        """CTU rows of every reference that band b may read: rows 0 .. r1 - 2 + lag"""
+        return self.rows(b)[1] - 1 + self.lag
 
     def region(self, b: int, ctu: int, margin_rows: int, rows_total: int, shift: int = 0):
         """buffer rows [start, end) of band b in a padded plane (full stride): the
@@ -78,110 +76,165 @@ class BandPlan:
         return start, end
 
 
-class RowExchange:
-    """Publishes bands of final reconstructed frames to the owner of the next frame.
+class _SchedConfig(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int) for n in ("frames", "segment_frames", "bframes", "b_pyramid", "max_refs",
+                                            "max_refs_l1", "ctu_rows", "band_rows", "lag", "world")]
 
-    planes_of(kind, k) -> list of flat per-plane tensors of local frame k, kind in
-    {"final", "ref"}; regions[p](b) -> (start, end) element range of band b in plane p.
-    """
 
-    def __init__(self, world: int, rank: int, plan: BandPlan, planes_of, regions, total_frames: int):
-        self.world, self.rank, self.plan = world, rank, plan
-        self.planes_of, self.regions, self.total = planes_of, regions, total_frames
-        self.recv_works = {}
-        self.send_works = []
-        self.avail = {}           # local frame k -> last reference band known to be in place
-        self.g_out = self.g_in = None
-        if world > 1:
-            import torch.distributed as dist
+class _SchedFrame(ctypes.Structure):
+    _fields_ = [("poc", ctypes.c_int), ("type", ctypes.c_int), ("is_ref", ctypes.c_int), ("rank", ctypes.c_int),
+                ("nrefs", ctypes.c_int), ("nrefs_l0", ctypes.c_int), ("refs", ctypes.c_int * 6)]
 
-            # one communicator per ring link j -> j+1: rank r sends only on link r, receives only on link r-1
-            groups = [dist.new_group([j, (j + 1) % world]) for j in range(world)]
-            self.g_out, self.g_in = groups[rank], groups[(rank - 1) % world]
 
-    def _band(self, kind, k, b):
+def _lib():
+    from .native import LIB_PATH
+
+    lib = ctypes.CDLL(LIB_PATH)
+    lib.x265amd_schedule.restype = ctypes.c_int
+    return lib
+
+
+class Schedule:
+    """The plan every rank computes identically (x265amd_schedule, csrc/schedule.cpp): per frame its
+    type, references and rank; per (frame, band) its step; per step the bands published and where
+    they go."""
+
+    def __init__(self, frames: int, world: int, plan: BandPlan, segment_frames: int | None = None, bframes: int = 4,
+                 b_pyramid: bool = True, max_refs: int = 3, max_refs_l1: int = 2):
+        self.frames, self.world, self.plan = frames, world, plan
+        self.segment_frames = segment_frames or frames
+        cfg = _SchedConfig(frames, self.segment_frames, bframes, int(b_pyramid), max_refs,
+                           max_refs_l1 if b_pyramid else 1, plan.ctu_rows, plan.band_rows, plan.lag, world)
+        fr = (_SchedFrame * frames)()
+        nb = plan.nbands
+        step = (ctypes.c_int * (frames * nb))()
+        nsteps = ctypes.c_int()
+        rc = _lib().x265amd_schedule(ctypes.byref(cfg), fr, step, ctypes.byref(nsteps))
+        if rc:
+            raise ValueError(f"x265amd_schedule: status {rc}")
+        self.nsteps = nsteps.value
+        self.type = [f.type for f in fr]
+        self.poc = [f.poc for f in fr]
+        self.is_ref = [bool(f.is_ref) for f in fr]
+        self.rank = [f.rank for f in fr]
+        self.refs = [list(f.refs[:f.nrefs]) for f in fr]
+        self.nrefs_l0 = [f.nrefs_l0 for f in fr]
+        self.step = np.frombuffer(step, dtype=np.int32).reshape(frames, nb).copy()
+        self.users = [[] for _ in range(frames)]              # frames that reference frame j
+        for j, rs in enumerate(self.refs):
+            for r in rs:
+                self.users[r].append(j)
+
+    # ---- derived plans
+    def pub_step(self, j: int, c: int) -> int:
+        """step in which band c of frame j becomes final"""
+        nb = self.plan.nbands
+        return int(self.step[j, min(c + 1, nb - 1)])
+
+    def local_frames(self, rank: int) -> list:
+        return [j for j in range(self.frames) if self.rank[j] == rank]
+
+    def store_frames(self, rank: int) -> list:
+        """reference pictures rank keeps a copy of: every reference of its frames"""
+        return sorted({r for j in self.local_frames(rank) for r in self.refs[j]})
+
+    def dest_ranks(self, j: int) -> list:
+        """ranks that receive the reference picture j (owners of its users)"""
+        return sorted({self.rank[u] for u in self.users[j]})
+
+    def items(self, rank: int, step: int) -> list:
+        """(frame, band) pairs rank encodes in step, frames in encode order"""
+        nb = self.plan.nbands
+        return [(j, b) for j in self.local_frames(rank) for b in range(nb) if self.step[j, b] == step]
+
+    def finals(self, rank: int, step: int) -> list:
+        """(frame, band) pairs of rank's frames that become final in step (SAO + border)"""
+        nb = self.plan.nbands
         out = []
-        for p, t in enumerate(self.planes_of(kind, k)):
-            s, e = self.regions[p](b)
+        for j in self.local_frames(rank):
+            for c in range(nb):
+                if self.pub_step(j, c) == step:
+                    out.append((j, c))
+        return out
+
+    def transfers(self, step: int) -> list:
+        """(frame j, band c, src rank, dst rank) of every band published in step, canonical order"""
+        nb = self.plan.nbands
+        out = []
+        for j in range(self.frames):
+            if not self.is_ref[j] or not self.users[j]:
+                continue
+            for c in range(nb):
+                if self.pub_step(j, c) == step:
+                    for d in self.dest_ranks(j):
+                        out.append((j, c, self.rank[j], d))
+        return out
+
+    def check(self):
+        """every band needed from every reference is published strictly before it is used"""
+        plan = self.plan
+        for j in range(self.frames):
+            for b in range(plan.nbands):
+                for r in self.refs[j]:
+                    assert self.pub_step(r, plan.need(b)) < self.step[j, b], (j, b, r)
+                if b:
+                    assert self.step[j, b - 1] < self.step[j, b]
+
+
+class RefExchange:
+    """Moves final bands of reference pictures into the reference stores of the ranks that read them.
+
+    planes_of(kind, idx) -> list of flat per-plane tensors: kind "final" with a frame index owned by
+    this rank (its finished reconstruction), kind "store" with a reference frame index in this rank's
+    store; regions[p](b) -> (start, end) element range of band b in plane p."""
+
+    def __init__(self, sched: Schedule, rank: int, planes_of, regions):
+        self.s, self.rank, self.planes_of, self.regions = sched, rank, planes_of, regions
+        self.world = sched.world
+        self.store = set(sched.store_frames(rank))
+        self.plans = [[t for t in sched.transfers(st) if rank in (t[2], t[3])] for st in range(sched.nsteps)]
+
+    def _band(self, kind, j, c):
+        out = []
+        for p, t in enumerate(self.planes_of(kind, j)):
+            s, e = self.regions[p](c)
             out.append(t[s:e])
         return out
 
-    def frame_index(self, k: int) -> int:
-        return k * self.world + self.rank
-
-    def start_frame(self, k: int):
-        """post the receives of every band of frame i - 1 into local frame k's reference slot"""
-        i = self.frame_index(k)
-        self.avail[k] = -1
-        if i == 0:
-            self.avail[k] = self.plan.nbands - 1      # first frame of the sequence: no reference
-            return
-        if self.world == 1:
-            return                                     # filled by the local publication of frame k - 1
-        import torch.distributed as dist
-
-        src = owner(i - 1, self.world)
-        self.recv_works[k] = [[dist.irecv(t, src=src, group=self.g_in) for t in self._band("ref", k, b)]
-                              for b in range(self.plan.nbands)]
-
-    def wait(self, k: int, band: int):
-        """make the work issued next wait until reference bands 0..band of local frame k are in place
-        (NCCL: a stream wait, no host block; gloo: a host wait)"""
-        if self.avail[k] >= band:
-            return
-        if self.world == 1:          # published by frame k - 1, which the stream has already ordered
-            self.avail[k] = band
-            return
-        for b in range(self.avail[k] + 1, band + 1):
-            for w in self.recv_works[k][b]:
-                w.wait()
-        self.avail[k] = band
-
-    def publish(self, k: int, b: int):
-        """band b of local frame k is final: send it to the owner of frame i + 1"""
-        i = self.frame_index(k)
-        if i + 1 >= self.total:
-            return
-        if self.world == 1:
-            for s, d in zip(self._band("final", k, b), self._band("ref", k + 1, b)):
-                d.copy_(s)
+    def exchange(self, step: int):
+        """after step's work: local copies, then this rank's sends and receives of the step (NCCL:
+        enqueued on the communicator's stream and waited on by the current stream; gloo: host waits)"""
+        ops = []
+        for j, c, src, dst in self.plans[step]:
+            if src == dst == self.rank:
+                for s_, d_ in zip(self._band("final", j, c), self._band("store", j, c)):
+                    d_.copy_(s_)
+            elif src == self.rank:
+                ops += [("send", t, dst) for t in self._band("final", j, c)]
+            else:
+                ops += [("recv", t, src) for t in self._band("store", j, c)]
+        if not ops:
             return
         import torch.distributed as dist
 
-        dst = owner(i + 1, self.world)
-        self.send_works += [dist.isend(t, dst=dst, group=self.g_out) for t in self._band("final", k, b)]
-
-    def finish_frame(self, k: int):
-        self.recv_works.pop(k, None)
-
-    def drain(self):
-        """wait for every outstanding send (its buffer may be rewritten afterwards)"""
-        for w in self.send_works:
+        p2p = [dist.P2POp(dist.isend if k == "send" else dist.irecv, t, peer) for k, t, peer in ops]
+        for w in dist.batch_isend_irecv(p2p):
             w.wait()
-        self.send_works = []
 
 
-def run_frames(ex: RowExchange, nlocal: int, encode, deblock, finish):
-    """Encode this rank's frames in order, band by band, with FrameFilter's row order.
+def run_steps(sched: Schedule, rank: int, ex: RefExchange, encode, deblock, finish, steps=None):
+    """This rank's share of the schedule, step by step: each (frame, band) of the step is encoded and
+    deblocked (encode order), then the bands that became final are SAO-filtered / border-extended
+    (finish), then the step's exchange runs.
 
-    encode(k, b): the band's encoder work (reads reference rows <= rows(b)[1] - 1 + lag)
-    deblock(k, b): deblocking of band b (changes the last rows of band b - 1)
-    finish(k, b): SAO + border extension of band b (reads one row of band b + 1)
+    encode(j, b): the band's encoder work (reads reference rows < reach_rows(b) CTU rows)
+    deblock(j, b): deblocking of band b (changes the last rows of band b - 1)
+    finish(j, c): SAO + border extension of band c (reads one row of band c + 1)
     """
-    plan = ex.plan
-    nb = plan.nbands
-    for k in range(nlocal):
-        if ex.frame_index(k) >= ex.total:
-            break
-        ex.start_frame(k)
-        for b in range(nb):
-            ex.wait(k, plan.need(b))
-            encode(k, b)
-            deblock(k, b)
-            if b:
-                finish(k, b - 1)
-                ex.publish(k, b - 1)
-        finish(k, nb - 1)
-        ex.publish(k, nb - 1)
-        ex.finish_frame(k)
-    ex.drain()
+    for st in (range(sched.nsteps) if steps is None else steps):
+        for j, b in sched.items(rank, st):
+            encode(j, b)
+            deblock(j, b)
+        for j, c in sched.finals(rank, st):
+            finish(j, c)
+        ex.exchange(st)

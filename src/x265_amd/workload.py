@@ -62,7 +62,8 @@ class FrameSet:
     """F padded frames (luma + 4:2:0 chroma) plus int16 residual planes, on one device."""
 
     def __init__(self, width: int, height: int, nframes: int, depth: int = 8, device: str = "cuda", ctu: int = 64,
-                 first_frame: int = 0, frame_ids: list | None = None):
+                 first_frame: int = 0, frame_ids: list | None = None, store_ids: list | None = None,
+                 ref_slots: list | None = None):
         import torch
 
         self.w, self.h, self.F, self.depth, self.device = width, height, nframes, depth, device
@@ -78,19 +79,21 @@ class FrameSet:
         # first+1 .. first+F); stored frame F is the REFERENCE SLOT holding the
         # picture before the chunk (synthetic frame `first`), which frame 0
         # predicts from; frame f > 0 predicts from stored frame f - 1.
-        # frame_ids (the frame-parallel pipeline, pipeline.py): stored frame k is synthetic
-        # frame frame_ids[k] and stored frame F + k its own reference slot, which the row
-        # exchange fills with the reconstruction of frame frame_ids[k] - 1 (initially the
-        # synthetic frame frame_ids[k] - 1).
-        self.per_frame_refs = frame_ids is not None
-        if self.per_frame_refs:
-            assert len(frame_ids) == nframes
-            ids = list(frame_ids) + [max(0, i - 1) for i in frame_ids]
+        # Frame-parallel pipeline (pipeline.py): stored frames 0..F-1 are this rank's frames
+        # (synthetic frames frame_ids), stored frames F.. its REFERENCE STORE (synthetic frames
+        # store_ids until the exchange overwrites them with the producers' reconstructions);
+        # ref_slots[k] lists the stored indices of local frame k's references (L0 then L1; empty
+        # for an I frame, whose inter-shaped census jobs then read its own picture).
+        self.ref_slots = ref_slots
+        if ref_slots is not None:
+            assert frame_ids is not None and len(frame_ids) == nframes and len(ref_slots) == nframes
+            ids = list(frame_ids) + list(store_ids or [])
         else:
             ids = [first_frame + i + 1 for i in range(nframes)] + [first_frame]
         src = SyntheticSource(width, height, max(ids) + 1, depth)
         dt = np.uint8 if depth == 8 else np.uint16
         S = len(ids)
+        self.stored = S
         Y = np.zeros((S, self.rows, self.stride), dt)
         U = np.zeros((S, self.crows, self.cstride), dt)
         V = np.zeros((S, self.crows, self.cstride), dt)
@@ -99,8 +102,8 @@ class FrameSet:
             Y[i] = self._pad(y, self.mx, self.my, self.rows, self.stride)
             U[i] = self._pad(u, self.cmx, self.cmy, self.crows, self.cstride)
             V[i] = self._pad(v, self.cmx, self.cmy, self.crows, self.cstride)
-        # residual planes: frame f minus its reference (int16), same layout as luma
-        ref_idx = [self.ref_of(f) for f in range(S)]
+        # residual planes: frame f minus its (first) reference (int16), same layout as luma
+        ref_idx = [self.ref_of(f) if f < nframes else f for f in range(S)]
         R = (Y.astype(np.int32) - Y[ref_idx].astype(np.int32)).astype(np.int16)
         self.host = dict(Y=Y.reshape(-1), U=U.reshape(-1), V=V.reshape(-1), R=R.reshape(-1))
         t = lambda a: torch.from_numpy(a).to(device)
@@ -108,11 +111,17 @@ class FrameSet:
         self.plane_size = self.rows * self.stride
         self.cplane_size = self.crows * self.cstride
 
-    def ref_of(self, f):
-        """reference frame of stored frame f: the previous frame, or the reference slot for frame 0
-        (per-frame reference slots: stored frame F + f)"""
-        if self.per_frame_refs:
-            return np.asarray(f) % self.F + self.F if not np.isscalar(f) else f % self.F + self.F
+    def ref_of(self, f, sel=None):
+        """stored index of the reference a job of stored frame f reads: the previous frame (or the
+        reference slot for frame 0); with reference stores, entry sel mod n of f's reference list"""
+        if self.ref_slots is not None:
+            fa = np.atleast_1d(np.asarray(f))
+            sa = np.zeros_like(fa) if sel is None else np.broadcast_to(np.asarray(sel), fa.shape)
+            out = np.empty(fa.shape, np.int64)
+            for i, (ff, ss) in enumerate(zip(fa.tolist(), sa.tolist())):
+                rs = self.ref_slots[ff]
+                out[i] = rs[ss % len(rs)] if rs else ff
+            return out if not np.isscalar(f) else int(out[0])
         return np.where(np.asarray(f) == 0, self.F, np.asarray(f) - 1) if not np.isscalar(f) else (self.F if f == 0 else f - 1)
 
     def planes(self, f: int):
@@ -153,6 +162,7 @@ class Batch:
     host_src: dict = field(default_factory=dict)   # name -> host array key for inputs shared with the FrameSet
     outs: dict = field(default_factory=dict)       # out name -> ("scalar", per_job) | ("slot", elems_per_job)
     bytes: float = 0.0                             # algorithmic bytes per launch
+    pos: tuple | None = None                       # (stored frame, luma row) of each job's coded block, if any
 
     def run(self, prims, stream=None):
         d, p = self.dev, self.params
@@ -363,6 +373,7 @@ class WorkloadBuilder:
         self.rng = np.random.default_rng(seed)
         self.skipped = {}
         self._pools = {}
+        self._pos = None
 
     # ---- shared pools ------------------------------------------------------------
     def pool(self, name, make):
@@ -417,7 +428,10 @@ class WorkloadBuilder:
     def _fenc_ref_offsets(self, n, w, h, chroma=False, nref=1):
         fs = self.fs
         f, x, y, cand = self._positions(n, w, h, chroma)
-        r = fs.ref_of(f)
+        if self._pos is None:                  # the batch's jobs: frame and luma row of the block coded
+            self._pos = (f, y * (2 if chroma else 1))
+        # the reference a job reads: one entry of its frame's list (a PU's candidates search one picture)
+        r = fs.ref_of(f, (x // max(w, 1)) * 7 + (y // max(h, 1)) * 13 + cand // 5)
         off = fs.chroma_off if chroma else fs.luma_off
         a = off(f, x, y)
         refs = []
@@ -440,6 +454,13 @@ class WorkloadBuilder:
 
     # ---- batch factories ----------------------------------------------------------
     def batch(self, key: str, count: float):
+        self._pos = None
+        b = self._batch(key, count)
+        if b is not None:
+            b.pos = self._pos
+        return b
+
+    def _batch(self, key: str, count: float):
         import torch
 
         fs = self.fs

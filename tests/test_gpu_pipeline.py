@@ -1,14 +1,14 @@
 """The frame-parallel GPU step (src/x265_amd/frame_pipeline.py) on one GPU.
 
-Frames are encoded band by band (census primitive work per band + the f4 row-band
-loop filters) and published into the next frame's reference slot.  Checked: every
-frame's final reconstruction equals the whole-frame deblock -> SAO -> border chain
-(x265amd_deblock / _sao_apply / _extend_border, themselves bit-exact vs the
-reference's Deblock / SAO classes in test_f4.py) on the same picture; every
-reference slot holds the previous frame's final reconstruction, margins included;
-and every census batch still matches the oracle on sampled jobs after the band split
-(a job that read a reference row before it was published would not).  Both schedules:
-frame by frame, and the single-rank wavefront.
+The pictures of a --preset medium GOP (pipeline.Schedule: I, P, B-ref and b pictures with their
+L0 / L1 references) are encoded step by step (census primitive work per band + the f4 row-band
+loop filters) and every final band of a reference picture is copied into the reference store.
+Checked: every picture's final reconstruction equals the whole-frame deblock -> SAO -> border
+chain (x265amd_deblock / _sao_apply / _extend_border, themselves bit-exact vs the reference's
+Deblock / SAO classes in test_f4.py) on the same picture; every store slot holds its producer's
+final reconstruction, margins included; and every census batch still matches the oracle on
+sampled jobs read against the FINAL stores — the stores start out holding the unfiltered source,
+so a job that read a reference before its rows were published would not match.
 """
 import numpy as np
 import pytest
@@ -16,26 +16,22 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("band_rows,wave", [(1, False), (3, False), (1, True), (4, True)])
-def test_gpu_pipeline_rows_equal_whole_frame(gpu_prims, oracle_libs, band_rows, wave):
-    """wave=True: the single-rank wavefront schedule (frame k's band b at step k * d + b, one set
-    of grouped launches per step, the whole sequence one hipGraph) must give the same frames"""
+@pytest.mark.parametrize("band_rows,frames", [(1, 8), (2, 6), (None, 11)])
+def test_gpu_pipeline_gop_equals_whole_frame_chain(gpu_prims, oracle_libs, band_rows, frames):
     import torch
 
     from pyoracle import CpuOracle
     from src.x265_amd.frame_pipeline import GpuFramePipeline
 
-    W, H, F = 416, 240, 4
-    pipe = GpuFramePipeline(gpu_prims, W, H, 8, F, 1, 0, band_rows=band_rows, streams=4, device="cuda")
-    if wave:
-        pipe.build_wave()
-    else:
-        pipe.build(graphs=True)
+    W, H = 416, 240
+    pipe = GpuFramePipeline(gpu_prims, W, H, 8, frames, 1, 0, band_rows=band_rows, streams=4, device="cuda")
+    pipe.build(graphs=True)
+    pipe.reset_stores()                  # the build's warm-up pass already filled them
     pipe.step()
     torch.cuda.synchronize()
-    fs = pipe.fs
-    # whole-frame f4 chain on a copy of each frame's source (the pipeline's stand-in reconstruction)
-    work = [t.clone() for t in (fs.luma, fs.cb, fs.cr)]
+    fs, F = pipe.fs, pipe.F
+    # whole-frame f4 chain on a copy of each picture's source (the pipeline's stand-in reconstruction)
+    work = [t[:F * (t.numel() // fs.stored)].clone() for t in (fs.luma, fs.cb, fs.cr)]
     final = [torch.zeros_like(t) for t in work]
     saved = (pipe.work, pipe.final)
     pipe.work, pipe.final = work, final
@@ -48,17 +44,20 @@ def test_gpu_pipeline_rows_equal_whole_frame(gpu_prims, oracle_libs, band_rows, 
     for k in range(F):
         got, want = pipe.frame_planes(pipe.final, k), pipe.frame_planes(final, k)
         for p in range(3):
-            assert torch.equal(got[p], want[p]), f"frame {k} plane {p}: band pipeline != whole-frame chain"
-        if k + 1 < F:
-            ref = pipe.frame_planes([fs.luma, fs.cb, fs.cr], F + k + 1)
-            for p in range(3):
-                assert torch.equal(ref[p], got[p]), f"reference slot of frame {k + 1} plane {p}"
+            assert torch.equal(got[p], want[p]), f"picture {k} plane {p}: band pipeline != whole-frame chain"
+    for r, slot in pipe.sof.items():
+        st = pipe.frame_planes([fs.luma, fs.cb, fs.cr], slot)
+        fin = pipe.frame_planes(pipe.final, pipe.kof[r])
+        for p in range(3):
+            assert torch.equal(st[p], fin[p]), f"reference store of picture {r} plane {p}"
+    assert len(pipe.store) >= 2 and any(len(pipe.sched.refs[j]) >= 3 for j in pipe.local)
     orc = CpuOracle("oracle", 8)
     orc.nthreads = 8
     bad = []
+    host = {"Y": fs.luma.cpu().numpy(), "U": fs.cb.cpu().numpy(), "V": fs.cr.cpu().numpy(),
+            "R": fs.resid.cpu().numpy()}
     for b in pipe.batches:
-        m = b.verify_sample(orc, {"Y": fs.luma.cpu().numpy(), "U": fs.cb.cpu().numpy(), "V": fs.cr.cpu().numpy(),
-                                  "R": fs.resid.cpu().numpy()}, b.sample(16))
+        m = b.verify_sample(orc, host, b.sample(16))
         if m:
             bad.append((b.name, m))
     assert not bad, bad[:5]

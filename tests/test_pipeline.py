@@ -1,17 +1,21 @@
-"""Frame-parallel shard with reconstructed-row exchange (src/x265_amd/pipeline.py), on CPU.
+"""Frame-parallel GOP shard with reconstructed-reference exchange (src/x265_amd/pipeline.py,
+csrc/schedule.cpp), on CPU.
 
-Multi-process gloo runs at world 1, 2 and 4 of the same pipeline bench.py drives
-over RCCL, with a CPU stand-in for the per-band work that has the encoder's row
+The schedule (x265amd_schedule, the C ABI every rank computes the plan with) is checked against
+the mini-GOP and reference-list rules of x265 1.9 --preset medium, and the row dependencies of
+frameencoder.cpp:516-531.  Then multi-process gloo runs at world 1, 2 and 4 of the same pipeline
+bench.py drives over RCCL, with a CPU stand-in for the per-band work that has the encoder's row
 dependencies:
 
-  encode(k, b)  reads reference rows up to r1 - 1 + refLagRows CTU rows (ME window);
-  deblock(k, b) rewrites the 3 rows on each side of the band's top edge;
-  finish(k, b)  reads one row of band b + 1 (SAO), then extends the borders.
+  encode(j, b)  reads every reference of frame j (L0 and L1) up to refLagRows rows below the
+                band (the motion-search window), 2 px beyond the sides;
+  deblock(j, b) rewrites the 3 rows on each side of the band's top edge;
+  finish(j, c)  reads one row of band c + 1 (SAO), then extends the borders.
 
-Checked: every rank's reference slots hold, byte for byte, the producer's final
-frames (margins included); no band is encoded before the reference rows it reads
-are in place (reference slots start poisoned with -1, and the encoder asserts it
-never sees one); and every frame's output equals a one-rank run.
+Checked: every rank's reference store holds, byte for byte, the producer's final pictures
+(margins included) for every reference its frames use; no band is encoded before the reference
+rows it reads are in place (stores start poisoned with -1, the encoder asserts it never sees one);
+non-reference b pictures are never sent; and every picture equals the one-rank run.
 """
 import os
 import socket
@@ -22,10 +26,9 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from src.x265_amd.pipeline import BandPlan, RowExchange, owned_frames, owner, run_frames
+from src.x265_amd.pipeline import FRAME_B, FRAME_BREF, FRAME_I, FRAME_P, BandPlan, RefExchange, Schedule, run_steps
 
 CTU, W, H, M = 16, 96, 88, 8            # 6 CTU rows (the last one partial), margins 8 / 4
-TOTAL = 8
 
 
 def _geom(p):
@@ -49,27 +52,27 @@ def _source(i):
 class StandIn:
     """Per-rank buffers and the CPU stand-in band work."""
 
-    def __init__(self, world, rank, band_rows):
+    def __init__(self, world, rank, band_rows, total, segment):
         self.world, self.rank = world, rank
-        self.frames = [i for i in owned_frames(TOTAL, rank, world)]
         self.plan = BandPlan(ctu_rows=-(-H // CTU), band_rows=band_rows)
-        n = len(self.frames)
-        self.src = [[torch.from_numpy(a) for a in _source(i)] for i in self.frames]
-        self.ref = [[torch.full_like(t, -1) for t in s] for s in self.src]
-        self.work = [[torch.zeros_like(t) for t in s] for s in self.src]
-        self.final = [[torch.zeros_like(t) for t in s] for s in self.src]
-        self.planes = {"ref": self.ref, "final": self.final}
+        self.s = Schedule(total, world, self.plan, segment_frames=segment)
+        self.frames = self.s.local_frames(rank)
+        self.src = {j: [torch.from_numpy(a) for a in _source(j)] for j in self.frames}
+        self.store = {j: [torch.full_like(t, -1) for t in self.src[self.frames[0]]] for j in self.s.store_frames(rank)}
+        self.work = {j: [torch.zeros_like(t) for t in self.src[j]] for j in self.frames}
+        self.final = {j: [torch.zeros_like(t) for t in self.src[j]] for j in self.frames}
         regions = []
         for p in range(3):
             _, _, m, stride, rows = _geom(p)
             regions.append(lambda b, p=p, m=m, stride=stride, rows=rows: tuple(
                 stride * r for r in self.plan.region(b, CTU, m, rows, shift=int(p > 0))))
-        self.ex = RowExchange(world, rank, self.plan, lambda kind, k: self.planes[kind][k], regions, TOTAL)
-        assert n == len(self.src)
+        self.ex = RefExchange(self.s, rank, lambda kind, j: (self.final if kind == "final" else self.store)[j],
+                              regions)
+        self.received = set()
 
-    def view(self, bufs, k, p):
+    def view(self, bufs, j, p):
         w, h, m, stride, rows = _geom(p)
-        return bufs[k][p].view(rows, stride)
+        return bufs[j][p].view(rows, stride)
 
     def band_px(self, b, p):
         r0, r1 = self.plan.rows(b)
@@ -77,40 +80,39 @@ class StandIn:
         h = _geom(p)[1]
         return r0 * c, min(r1 * c, h)
 
-    def encode(self, k, b):
-        i = self.frames[k]
-        assert self.ex.avail[k] >= self.plan.need(b), "band encoded before its reference rows were published"
+    def encode(self, j, b):
         for p in range(3):
             w, h, m, _, _ = _geom(p)
             y0, y1 = self.band_px(b, p)
-            src, wk = self.view(self.src, k, p), self.view(self.work, k, p)
-            if i == 0:
-                wk[m + y0:m + y1, m:m + w] = src[m + y0:m + y1, m:m + w]
-                continue
-            ref = self.view(self.ref, k, p)
-            lag = self.plan.lag * (CTU >> (p > 0))
+            src, wk = self.view(self.src, j, p), self.view(self.work, j, p)
+            acc = src[m + y0:m + y1, m:m + w].clone()
             ys = torch.arange(y0, y1)
-            far = ref[m + torch.clamp(ys + lag, max=h - 1), m - 2:m + w + 2]   # motion window: +lag rows, 2 px
-            near = ref[m + ys, m:m + w]
-            assert int(far.min()) >= 0 and int(near.min()) >= 0, "read a reference row before it was published"
-            wk[m + y0:m + y1, m:m + w] = (src[m + y0:m + y1, m:m + w] + 3 * far[:, 2:-2] + (near >> 1)
-                                         + far[:, :-4] - far[:, 4:]) & 255
+            # rows r of the band may read reference rows < (r // CTU + lag) * CTU (frameencoder.cpp:526)
+            reach = torch.clamp(((ys // (CTU >> (p > 0))) + self.plan.lag) * (CTU >> (p > 0)) - 1, max=h - 1)
+            for k, r in enumerate(self.s.refs[j]):
+                ref = self.view(self.store, r, p)
+                far = ref[m + reach, m - 2:m + w + 2]                  # motion window: lag rows below, 2 px out
+                near = ref[m + ys, m:m + w]
+                assert int(far.min()) >= 0 and int(near.min()) >= 0, \
+                    f"frame {j} band {b} read reference {r} before it was published"
+                acc += (k + 1) * far[:, 2:-2] + (near >> 1) + far[:, :-4] - far[:, 4:]
+            wk[m + y0:m + y1, m:m + w] = acc & 255
 
-    def deblock(self, k, b):
+    def deblock(self, j, b):
         for p in range(3):
             w, h, m, _, _ = _geom(p)
             y0, _ = self.band_px(b, p)
             if y0 == 0:
                 continue
-            wk = self.view(self.work, k, p)
+            wk = self.view(self.work, j, p)
             a = wk[m + y0 - 3:m + y0 + 3, m:m + w].clone()
             wk[m + y0 - 3:m + y0 + 3, m:m + w] = (a + a.flip(0) + 1) >> 1
 
-    def finish(self, k, b):
+    def finish(self, j, b):
         for p in range(3):
             w, h, m, stride, rows = _geom(p)
             y0, y1 = self.band_px(b, p)
-            wk, fin = self.view(self.work, k, p), self.view(self.final, k, p)
+            wk, fin = self.view(self.work, j, p), self.view(self.final, j, p)
             ys = torch.arange(y0, y1)
             up, dn = m + torch.clamp(ys - 1, min=0), m + torch.clamp(ys + 1, max=h - 1)
             fin[m + y0:m + y1, m:m + w] = (wk[up, m:m + w] + 2 * wk[m + ys, m:m + w] + wk[dn, m:m + w] + 2) >> 2
@@ -122,9 +124,9 @@ class StandIn:
                 fin[m + h:] = fin[m + h - 1:m + h]
 
     def run(self):
-        run_frames(self.ex, len(self.frames), self.encode, self.deblock, self.finish)
-        return ({i: [t.numpy().copy() for t in self.final[k]] for k, i in enumerate(self.frames)},
-                {i: [t.numpy().copy() for t in self.ref[k]] for k, i in enumerate(self.frames)})
+        run_steps(self.s, self.rank, self.ex, self.encode, self.deblock, self.finish)
+        return ({j: [t.numpy().copy() for t in self.final[j]] for j in self.frames},
+                {j: [t.numpy().copy() for t in self.store[j]] for j in self.store})
 
 
 def _free_port():
@@ -133,79 +135,114 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, band_rows, q):
+def _worker(rank, world, port, args, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        q.put((rank,) + StandIn(world, rank, band_rows).run())
+        q.put((rank,) + StandIn(world, rank, *args).run())
         dist.barrier()
     finally:
         dist.destroy_process_group()
 
 
-def _run(world, band_rows):
+def _run(world, band_rows, total, segment):
     if world == 1:
-        return StandIn(1, 0, band_rows).run()
+        return StandIn(1, 0, band_rows, total, segment).run()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, band_rows, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, (band_rows, total, segment), q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = [q.get(timeout=180) for _ in procs]
+    res = [q.get(timeout=240) for _ in procs]
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    finals, refs = {}, {}
-    for _, f, r in res:
+    finals, stores = {}, []
+    for _, f, s in res:
         finals.update(f)
-        refs.update(r)
-    return finals, refs
+        stores.append(s)
+    return finals, stores
 
 
+# ---------------------------------------------------------------- the schedule
 def test_band_plan_matches_ref_lag():
+    """row r waits for reference rows 0 .. r + lag - 1 (frameencoder.cpp:526-527)"""
     plan = BandPlan(ctu_rows=17, band_rows=1, lag=2)          # 1080p, --preset medium
-    assert plan.nbands == 17 and [plan.need(b) for b in (0, 1, 14, 15, 16)] == [2, 3, 16, 16, 16]
+    assert plan.nbands == 17 and [plan.need(b) for b in (0, 1, 14, 15, 16)] == [1, 2, 15, 16, 16]
     plan = BandPlan(ctu_rows=17, band_rows=4, lag=2)
     assert plan.nbands == 5 and [plan.need(b) for b in range(5)] == [1, 2, 3, 4, 4]
-    assert plan.region(0, 64, 80, 1240) == (0, 80 + 4 * 64) and plan.region(4, 64, 80, 1240) == (80 + 16 * 64, 1240)
-    assert [owner(i, 4) for i in range(6)] == [0, 1, 2, 3, 0, 1] and owned_frames(8, 1, 4) == [1, 5]
+    plan = BandPlan(ctu_rows=17, band_rows=17, lag=2)
+    assert plan.nbands == 1 and plan.need(0) == 0
+    assert plan.region(0, 64, 80, 1240) == (0, 1240)
 
 
-@pytest.mark.parametrize("world,band_rows", [(2, 1), (4, 1), (2, 2), (4, 3)])
-def test_frame_parallel_rows_gloo(world, band_rows):
-    ref_finals, ref_refs = _run(1, band_rows)
-    finals, refs = _run(world, band_rows)
-    assert sorted(finals) == list(range(TOTAL))
-    for i in range(TOTAL):
-        for p in range(3):
-            # output identical to the one-rank run
-            np.testing.assert_array_equal(finals[i][p], ref_finals[i][p], err_msg=f"frame {i} plane {p}")
-            if i:
-                # the reference slot holds the producer's final frame i - 1, byte for byte (margins too)
-                np.testing.assert_array_equal(refs[i][p], finals[i - 1][p], err_msg=f"ref of frame {i} plane {p}")
-                assert refs[i][p].min() >= 0
+def test_medium_gop_structure_and_references():
+    """mini-GOP of --preset medium: encode order P, B-ref, b, b, b (slicetype.cpp:993-996,
+    1050-1078); L0 = the 3 nearest earlier-coded reference pictures before it, L1 (B only) = the
+    2 nearest after it (dpb.cpp:149-150, 188-207, dpb.h:57-58)"""
+    s = Schedule(11, 1, BandPlan(ctu_rows=4, band_rows=4))
+    assert s.poc == [0, 5, 3, 1, 2, 4, 10, 8, 6, 7, 9]
+    T = {FRAME_I: "I", FRAME_P: "P", FRAME_BREF: "Bref", FRAME_B: "b"}
+    assert [T[t] for t in s.type] == ["I", "P", "Bref", "b", "b", "b", "P", "Bref", "b", "b", "b"]
+    assert s.refs == [[], [0], [0, 1], [0, 2, 1], [0, 2, 1], [2, 0, 1], [1, 2, 0], [1, 2, 0, 6], [1, 2, 0, 7, 6],
+                      [1, 2, 0, 7, 6], [7, 1, 2, 6]]
+    assert [s.is_ref[j] for j in range(11)] == [True, True, True] + [False] * 3 + [True, True] + [False] * 3
+    # segments are closed: each starts with an I picture and references nothing before it
+    s2 = Schedule(20, 2, BandPlan(ctu_rows=4, band_rows=4), segment_frames=10)
+    assert s2.type[10] == FRAME_I and all(r >= 10 for j in range(10, 20) for r in s2.refs[j])
+    assert s2.rank == [j % 2 for j in range(20)]
 
 
 @pytest.mark.parametrize("ctu_rows", [4, 17, 34])
-@pytest.mark.parametrize("band_rows", [1, 2, 3, 4, 17])
-def test_wavefront_schedule_respects_row_dependencies(ctu_rows, band_rows):
-    """The single-rank wavefront (frame_pipeline.wave_delay): frame k's band b runs at step k*d + b.
-    Every (frame, band) runs exactly once, and every reference band a band needs (BandPlan.need) was
-    published in an EARLIER step by the previous frame — band c is published in the step of band
-    c + 1 (its SAO needs the next band's deblocking), the last band in its own step."""
-    from src.x265_amd.frame_pipeline import wave_delay
-
+@pytest.mark.parametrize("band_rows", [1, 2, 4, 17])
+def test_schedule_respects_row_dependencies(ctu_rows, band_rows):
+    """every (frame, band) runs after its previous band and after every reference band it needs
+    was published in an EARLIER step; and at the earliest such step"""
     plan = BandPlan(ctu_rows=ctu_rows, band_rows=band_rows)
-    nb, d, F = plan.nbands, wave_delay(plan), 6
-    step = {(k, b): k * d + b for k in range(F) for b in range(nb)}
-    pub = {(k, c): step[(k, min(c + 1, nb - 1))] for k in range(F) for c in range(nb)}
-    assert len(set(step.items())) == F * nb
-    for k in range(1, F):
-        for b in range(nb):
-            assert pub[(k - 1, plan.need(b))] < step[(k, b)], (k, b, d)
-    # and d is the smallest such delay
-    if d > 1:
-        d2 = d - 1
-        assert any(k * d2 + b <= (k - 1) * d2 + min(plan.need(b) + 1, nb - 1)
-                   for k in range(1, F) for b in range(nb))
+    s = Schedule(24, 4, plan, segment_frames=12)
+    s.check()
+    for j in range(24):
+        for b in range(plan.nbands):
+            lo = s.step[j, b - 1] + 1 if b else 0
+            for r in s.refs[j]:
+                lo = max(lo, s.pub_step(r, plan.need(b)) + 1)
+            assert s.step[j, b] == lo
+    # the non-reference b pictures' bands are never sent; reference pictures reach every user's rank
+    sent = {(j, d) for st in range(s.nsteps) for (j, c, src, d) in s.transfers(st)}
+    assert all(s.is_ref[j] for j, _ in sent)
+    for j in range(24):
+        for u in s.users[j]:
+            assert (j, s.rank[u]) in sent
+
+
+def test_schedule_overlaps_frames():
+    """whole-frame bands: the next mini-GOP's P runs beside the previous mini-GOP's b pictures (the
+    critical path is P -> B-ref -> next P, two steps per mini-GOP: a P references the previous
+    B-ref), so a 32-frame segment needs far fewer steps than frames"""
+    s = Schedule(32, 1, BandPlan(ctu_rows=17, band_rows=17))
+    assert s.nsteps <= 2 * (32 // 5) + 3
+    assert max(len(s.items(0, st)) for st in range(s.nsteps)) >= 4
+
+
+# ---------------------------------------------------------------- the exchange
+@pytest.mark.parametrize("world,band_rows,total,segment", [(2, 1, 11, 11), (4, 2, 16, 8), (2, 6, 12, 6),
+                                                           (4, 3, 12, 12)])
+def test_frame_parallel_exchange_gloo(world, band_rows, total, segment):
+    ref_finals, ref_stores = _run(1, band_rows, total, segment)
+    finals, stores = _run(world, band_rows, total, segment)
+    assert sorted(finals) == list(range(total))
+    s = Schedule(total, world, BandPlan(ctu_rows=-(-H // CTU), band_rows=band_rows), segment_frames=segment)
+    fanout = max(len(s.dest_ranks(j)) for j in range(total))
+    if world == 4:
+        assert fanout >= 2, "no reference picture was sent to more than one rank"
+    for j in range(total):
+        for p in range(3):
+            # output identical to the one-rank run
+            np.testing.assert_array_equal(finals[j][p], ref_finals[j][p], err_msg=f"frame {j} plane {p}")
+    # every store slot holds the producer's final picture, byte for byte (margins too)
+    for st in stores:
+        for r, planes in st.items():
+            for p in range(3):
+                np.testing.assert_array_equal(planes[p], finals[r][p], err_msg=f"store copy of frame {r} plane {p}")
+                assert planes[p].min() >= 0
