@@ -68,21 +68,24 @@ def parse():
     # default K: >= 1 s of timed steps at the measured ~2.2 ms per 8-frame step
     ap.add_argument("--steps", type=int, default=500)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--frames", type=int, default=8, help="frames per step per GPU")
+    ap.add_argument("--frames", type=int, default=0,
+                    help="frames per step per GPU (default: 8 in replay mode, 32 in pipeline mode)")
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--depth", type=int, default=8)
     ap.add_argument("--preset", default="medium", choices=("medium", "slow"),
                     help="selects the census of that x265 preset (tests/golden/census_<H>p_<preset>[_main10].json)")
     ap.add_argument("--no-graph", action="store_true", help="launch eagerly instead of replaying a hipGraph")
-    ap.add_argument("--mode", default="replay", choices=("pipeline", "replay"),
-                    help="pipeline: frame-parallel shard, frames encoded band by band with the reference-row "
-                         "dependencies and RCCL row exchange (src/x265_amd/pipeline.py); replay: the census of "
-                         "this rank's frames as one set of independent grouped launches")
-    ap.add_argument("--band-rows", type=int, default=4, help="CTU rows per pipeline band")
+    ap.add_argument("--mode", default="", choices=("", "pipeline", "replay"),
+                    help="pipeline: frame-parallel GOP shard, pictures encoded band by band with the reference-row "
+                         "dependencies and the RCCL reference exchange (src/x265_amd/pipeline.py); replay: the census "
+                         "of this rank's frames as one set of independent grouped launches.  Default: replay at N = 1, "
+                         "pipeline at N > 1")
+    ap.add_argument("--band-rows", type=int, default=0, help="CTU rows per pipeline band (default: whole pictures)")
+    ap.add_argument("--segment-frames", type=int, default=0,
+                    help="pictures per closed GOP segment in pipeline mode (default: the frames per rank)")
     ap.add_argument("--no-pipeline-check", action="store_true",
                     help="skip the N=1 measurement of the frame-parallel pipeline beside a replay run")
-    ap.add_argument("--one-graph", action="store_true", help="pipeline on one rank: the whole step as one hipGraph")
     ap.add_argument("--streams", type=int, default=8, help="HIP streams the step's independent launches spread over")
     ap.add_argument("--no-group", action="store_true", help="one launch per batch instead of grouped multi-shape launches")
     ap.add_argument("--census-cpu-seconds", type=float, default=5.0,
@@ -93,10 +96,26 @@ def parse():
     return ap.parse_args()
 
 
+def spawn_ranks(args) -> int:
+    """--gpus N without a launcher: start N ranks with torch.distributed.run (a child process, before
+    this process initialises the GPU) and return their exit status"""
+    import socket
+    import subprocess
+
+    with socket.socket() as s_:
+        s_.bind(("127.0.0.1", 0))
+        port = s_.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *sys.argv[1:]]
+    return subprocess.call(cmd, env=dict(os.environ))
+
+
 def dist_setup(args):
     import torch
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py --gpus {args.gpus} but WORLD_SIZE={world}")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
@@ -316,17 +335,18 @@ def census_replay_cpu(args, census):
 
 
 def pipeline_rates(prims, args, census, local):
-    """The frame-parallel step (--mode pipeline) on this one GPU: frames encoded in order, band by
-    band, with the reference-row waits, loop filters and row publications (local copies at N=1)."""
+    """The frame-parallel step (--mode pipeline) on this one GPU: one closed GOP of F pictures (F = the
+    pipeline default of 32 frames), steps of x265amd_schedule, reference bands copied (in place) into the
+    reference store; whole-picture bands and 4-CTU-row bands."""
     import torch
 
     from src.x265_amd.frame_pipeline import GpuFramePipeline
 
-    pipe = GpuFramePipeline(prims, args.width, args.height, args.depth, args.frames, 1, 0, census=census,
-                            band_rows=args.band_rows, streams=args.streams, device=f"cuda:{local}")
-    out = {"frames_per_step": args.frames}
-    for br in (args.band_rows, pipe.fs.ph // 64):
-        pipe.set_band_rows(br)
+    F = 32
+    out = {"frames_per_step": F}
+    for br in (0, 4):
+        pipe = GpuFramePipeline(prims, args.width, args.height, args.depth, F, 1, 0, census=census,
+                                band_rows=br or None, streams=args.streams, device=f"cuda:{local}")
         pipe.build(graphs=True)
         for _ in range(2):
             pipe.step()
@@ -337,30 +357,22 @@ def pipeline_rates(prims, args, census, local):
             pipe.step()
         torch.cuda.synchronize()
         dt = (time.perf_counter() - t0) / n
-        out[f"band_rows_{br}"] = {"fps": round(args.frames / dt, 1), "ms_per_step": round(dt * 1e3, 3),
-                                  "bands_per_frame": pipe.plan.nbands, "launches_per_step": pipe.launches_per_step}
-    # the same frames and bands in the wavefront schedule (frame k's band b at step k * d + b: one set
-    # of grouped launches per step for every frame in it, the sequence as one hipGraph)
-    for br in (args.band_rows, 1):
-        pipe.set_band_rows(br)
-        pipe.build_wave()
-        for _ in range(2):
-            pipe.step()
+        out[f"band_rows_{br or pipe.plan.band_rows}"] = {
+            "fps": round(F / dt, 1), "ms_per_step": round(dt * 1e3, 3), "bands_per_frame": pipe.plan.nbands,
+            "schedule_steps": pipe.sched.nsteps, "launches_per_step": pipe.launches_per_step}
+        del pipe
         torch.cuda.synchronize()
-        n = 10
-        t0 = time.perf_counter()
-        for _ in range(n):
-            pipe.step()
-        torch.cuda.synchronize()
-        dt = (time.perf_counter() - t0) / n
-        out[f"wavefront_band_rows_{br}"] = {"fps": round(args.frames / dt, 1), "ms_per_step": round(dt * 1e3, 3),
-                                            "bands_per_frame": pipe.plan.nbands, "frame_delay_bands": pipe.d,
-                                            "steps": pipe.nsteps, "launches_per_step": pipe.wave_launches_per_step()}
     return out
 
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        raise SystemExit(spawn_ranks(args))
+    if not args.mode:
+        args.mode = "pipeline" if args.gpus > 1 else "replay"
+    if not args.frames:
+        args.frames = 32 if args.mode == "pipeline" else 8
     import torch
 
     world, rank, local = dist_setup(args)
@@ -381,7 +393,8 @@ def main():
         from src.x265_amd.frame_pipeline import GpuFramePipeline
 
         pipe = GpuFramePipeline(prims, args.width, args.height, args.depth, F, world, rank, census=census,
-                                band_rows=args.band_rows, streams=nstreams, device=f"cuda:{local}")
+                                band_rows=args.band_rows or None, segment_frames=args.segment_frames or None,
+                                streams=nstreams, device=f"cuda:{local}")
         batches, wb = pipe.batches, pipe.wb
     else:
         # independent replay: this rank's F frames' census as one set of grouped launches
@@ -441,7 +454,7 @@ def main():
 
     graph = None
     if pipe is not None:
-        pipe.build(graphs=not args.no_graph, one_graph=args.one_graph)
+        pipe.build(graphs=not args.no_graph)
         graph = bool(pipe.graphs) or None
 
         def run():
@@ -598,9 +611,12 @@ def main():
                 "launches_per_step": pipe.launches_per_step if pipe is not None else len(launches),
                 "algorithmic_GB_per_step_per_gpu": round(step_bytes / 1e9, 3),
                 "hipgraph": graph is not None, "streams": nstreams, "mode": args.mode,
-                "parallelism": (f"frame-parallel x{world}: frame i on rank i mod {world}, CTU-row bands of "
-                                f"{args.band_rows}, reference rows published after deblock/SAO/border and sent "
-                                f"over {'RCCL' if world > 1 else 'a local copy'}" if pipe is not None else
+                "parallelism": (f"frame-parallel GOP shard x{world}: {world * F // pipe.segment_frames} closed "
+                                f"--preset medium GOPs of {pipe.segment_frames} pictures (I/P/B-ref/b, 3 refs, L1<=2), "
+                                f"picture j on rank j mod {world}, bands of {pipe.plan.band_rows} CTU rows in "
+                                f"{pipe.sched.nsteps} schedule steps, final reference bands (deblock/SAO/border) sent "
+                                f"to every rank that reads them over "
+                                f"{'RCCL P2P' if world > 1 else 'in-place stores (one rank)'}" if pipe is not None else
                                 f"independent replay x{world}"),
                 "frames_per_step_total": world * F,
             },

@@ -77,17 +77,34 @@ def _take(b, idx=None, lo=None, hi=None):
     return out
 
 
+def reads_store(b, fs: FrameSet) -> np.ndarray:
+    """per job of batch b: does it read a reference picture (the rank's reference store)?"""
+    out = np.zeros(b.n, bool)
+    for key, plane_key in (("aoff", "a"), ("boff", "b"), ("roff", "r"), ("soff", "s"), ("foff", "f")):
+        t, pl = b.dev.get(key), b.dev.get(plane_key)
+        if t is None or pl is None or not (pl is fs.luma or pl is fs.cb or pl is fs.cr):
+            continue
+        psize = fs.plane_size if pl is fs.luma else fs.cplane_size
+        off = t.cpu().numpy().astype(np.int64)
+        per = len(off) // b.n
+        out |= (off.reshape(b.n, per) // psize >= fs.F).any(axis=1)
+    return out
+
+
 def keyed_slices(batches, fs: FrameSet, key_of, nkeys: int, ctu: int, plan: BandPlan):
-    """{key: [batch slices]}: every job of every batch in exactly one slice; key_of(frame, band)
-    (numpy arrays) gives the job's key"""
+    """{key: [batch slices]}: every job of every batch in exactly one slice; key_of(batch, frame, band)
+    (numpy arrays per job) gives the job's key"""
     out = {}
     for b in batches:
         frame, y = job_rows(b, fs)
         band = np.minimum(y // ctu, plan.ctu_rows - 1) // plan.band_rows
-        key = key_of(frame, band)
+        key = key_of(b, frame, band)
         if np.any(np.diff(key) < 0):
+            # reorder the batch's own jobs (descriptors AND per-job outputs), so the slices below are
+            # views of it and their results land in the batch's outputs, where verification reads them
             order = np.argsort(key, kind="stable")
-            b = _take(b, idx=order)
+            p = _take(b, idx=order)
+            b.dev, b.pos = p.dev, p.pos
             key = key[order]
         bounds = np.searchsorted(key, np.arange(nkeys + 1))
         for kk in range(nkeys):
@@ -127,9 +144,10 @@ def check_reference_reach(slices_by_fb, fs: FrameSet, plan: BandPlan, ctu: int =
 
 class GpuFramePipeline:
     def __init__(self, prims, width, height, depth, frames_local, world, rank, census=None, band_rows=None,
-                 segment_frames=None, streams=8, device="cuda", seed=11):
+                 segment_frames=None, streams=8, device="cuda", seed=11, early_independent=True):
         import torch
 
+        self.early_independent = early_independent
         self.prims, self.world, self.rank, self.depth = prims, world, rank, depth
         self.F = frames_local
         self.total = frames_local * world
@@ -141,7 +159,10 @@ class GpuFramePipeline:
         self.local = s.local_frames(rank)
         assert len(self.local) == frames_local
         self.kof = {j: k for k, j in enumerate(self.local)}
-        self.store = s.store_frames(rank)
+        # the reference store: every picture this rank's frames reference, plus this rank's own reference
+        # pictures, whose final reconstruction is written straight into their store slot (local users
+        # then read it in place: no copy)
+        self.store = sorted(set(s.store_frames(rank)) | {j for j in self.local if s.is_ref[j]})
         self.sof = {r: frames_local + i for i, r in enumerate(self.store)}
         self.fs = fs = FrameSet(width, height, frames_local, depth, device=device,
                                 frame_ids=[s.poc[j] for j in self.local], store_ids=[s.poc[r] for r in self.store],
@@ -151,7 +172,8 @@ class GpuFramePipeline:
                                                builder=WorkloadBuilder(fs, seed=seed + rank))
         nb = plan.nbands
         self.slices = {divmod(kk, nb): v for kk, v in
-                       keyed_slices(self.batches, fs, lambda f, b: f * nb + b, frames_local * nb, ctu, plan).items()}
+                       keyed_slices(self.batches, fs, lambda bt, f, b: f * nb + b, frames_local * nb, ctu,
+                                    plan).items()}
         bad = check_reference_reach(self.slices, fs, plan, ctu)
         if bad:
             raise RuntimeError(f"census jobs read reference rows beyond refLagRows: {bad[:4]}")
@@ -177,15 +199,25 @@ class GpuFramePipeline:
         self.regions = regions
 
         def planes_of(kind, j):
-            return frame_planes(self.final, self.kof[j]) if kind == "final" else frame_planes(src_planes, self.sof[j])
+            return self.final_planes(self.kof[j]) if kind == "final" else frame_planes(src_planes, self.sof[j])
 
         self.ex = RefExchange(s, rank, planes_of, regions)
         self._f4_setup(width, height, device)
         self.streams = [torch.cuda.Stream() for _ in range(max(1, streams))] if streams > 1 else []
         self.graphs = {}
 
+    def final_planes(self, k, final=None):
+        """where local frame k's final reconstruction lives: its store slot for a reference picture,
+        else the frame's own final buffer"""
+        j = self.local[k]
+        if final is None and j in self.sof:
+            return self.frame_planes(self.src_planes, self.sof[j])
+        return self.frame_planes(self.final if final is None else final, k)
+
     # ---------------------------------------------------------------- f4 descriptors
-    def _f4_setup(self, width, height, device):
+    def _f4_setup(self, width, height, device, work=None, final=None):
+        """loop-filter descriptors of every local frame: deblock in place in `work`, SAO into the final
+        planes (final_planes, or `final` for every frame when given), border extension there"""
         import torch
 
         from .caller_bench import _SAO, _UNIT
@@ -217,7 +249,7 @@ class GpuFramePipeline:
 
         self.dbk, self.sao, self.bor = [], [], []
         for k in range(self.F):
-            wk, fin = self.frame_planes(self.work, k), self.frame_planes(self.final, k)
+            wk, fin = self.frame_planes(work if work is not None else self.work, k), self.final_planes(k, final)
             d = DeblockFrame()
             d.width, d.height, d.is_p = width, height, 1
             for p in range(3):
@@ -253,7 +285,15 @@ class GpuFramePipeline:
 
         s, nb = self.sched, self.plan.nbands
         step_of = np.array([[s.step[j, b] for b in range(nb)] for j in self.local], np.int64)
-        self.step_slices = keyed_slices(self.batches, self.fs, lambda f, b: step_of[f, b], s.nsteps, 64, self.plan)
+        # a job waits for its band's step only if it reads a reference picture: x265's frame threads wait
+        # on reference rows and on nothing else (frameencoder.cpp:516-531); the census jobs that read no
+        # reference (transforms, quant, intra, residual and current-picture block ops, an I picture's
+        # jobs) carry no cross-frame dependency and go out with the first step
+        if self.early_independent:
+            key_of = lambda bt, f, b: np.where(reads_store(bt, self.fs), step_of[f, b], 0)
+        else:
+            key_of = lambda bt, f, b: step_of[f, b]
+        self.step_slices = keyed_slices(self.batches, self.fs, key_of, s.nsteps, 64, self.plan)
         self._sgroups = {st: group_launches(bs) for st, bs in self.step_slices.items()}
         for gs in self._sgroups.values():
             for g in gs:
@@ -315,15 +355,12 @@ class GpuFramePipeline:
         else:
             for g in groups:
                 g.run(self.prims)
-        fs = self.fs
-        for j, b in items:                       # the bands' reconstruction (stand-in: source pixels)
-            k = self.kof[j]
-            y0, y1 = self._rows_px(b)
+        if st == 0:
+            # the reconstruction of every band (stand-in: the source pixels), written before any band is
+            # deblocked: one copy per plane for all local frames
             for p in range(3):
-                stride, my, sh = (fs.stride, fs.my, 0) if p == 0 else (fs.cstride, fs.cmy, 1)
-                s0, e0 = (my + (y0 >> sh)) * stride, (my + (y1 >> sh)) * stride
-                src = self.src_planes[p][k * self._sizes[p]:(k + 1) * self._sizes[p]]
-                self.frame_planes(self.work, k)[p][s0:e0].copy_(src[s0:e0])
+                n = self.F * self._sizes[p]
+                self.work[p][:n].copy_(self.src_planes[p][:n])
         h = ctypes.c_void_p(cur.cuda_stream)
         if items:
             rows = []

@@ -208,7 +208,8 @@ class RefExchange:
         for j, c, src, dst in self.plans[step]:
             if src == dst == self.rank:
                 for s_, d_ in zip(self._band("final", j, c), self._band("store", j, c)):
-                    d_.copy_(s_)
+                    if s_.data_ptr() != d_.data_ptr():         # a final written in place in the store: nothing to do
+                        d_.copy_(s_)
             elif src == self.rank:
                 ops += [("send", t, dst) for t in self._band("final", j, c)]
             else:

@@ -244,8 +244,13 @@ class Batch:
                 if not np.array_equal(cpu[k], gpu_outs[k]):
                     bad.append(k)
             else:
-                g, c = gpu_outs[k].reshape(self.n, per), cpu[k].reshape(self.n, per)
-                if not np.array_equal(g[idx], c[idx]):
+                # a job's slot is where its own output offset points (jobs may have been reordered)
+                okey = {"d": "doff", "o": "oo", "dl": "dlo"}.get(k)
+                rows = idx
+                if okey in self.dev:
+                    rows = self.dev[okey].cpu().numpy().astype(np.int64)[idx] // per
+                g, c = gpu_outs[k].reshape(-1, per), cpu[k].reshape(-1, per)
+                if not np.array_equal(g[rows], c[rows]):
                     bad.append(k)
         return bad
 

@@ -43,13 +43,14 @@ def main():
         print(json.dumps({"mode": "replay-eager-1stream", "frames": F, "fps": round(F / dt, 1), "launches": len(ls)}),
               flush=True)
         del fs, bs, ls
-        for br in (int(x) for x in a.band_rows.split(",")):
+        for br, early in [(int(x), e) for x in a.band_rows.split(",") for e in (True, False)]:
             t0 = time.perf_counter()
-            pipe = GpuFramePipeline(prims, 1920, 1080, 8, F, 1, 0, band_rows=br, streams=8, device="cuda")
+            pipe = GpuFramePipeline(prims, 1920, 1080, 8, F, 1, 0, band_rows=br, streams=8, device="cuda",
+                                    early_independent=early)
             pipe.build(graphs=True)
             tb = time.perf_counter() - t0
             dt = timed(pipe.step, a.reps)
-            print(json.dumps({"mode": "pipeline", "frames": F, "band_rows": br, "fps": round(F / dt, 1),
+            print(json.dumps({"mode": "pipeline", "frames": F, "band_rows": br, "early_independent": early, "fps": round(F / dt, 1),
                               "ms_per_step": round(dt * 1e3, 3), "steps": pipe.sched.nsteps,
                               "launches": pipe.launches_per_step, "build_s": round(tb, 1)}), flush=True)
             del pipe
