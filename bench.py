@@ -38,9 +38,11 @@ Also reported (rank 0):
                  of the same resolution on the box's host-core share and on one
                  core (N = 1 only); beside it the reference's C primitives
                  replaying the same census descriptors (`census_replay`).
-  encoder_level — the reference encoder itself (x265_encoder_encode) on the
-                 MI355X per-call provider vs on its C table, small clip: fps of
-                 both and whether the bitstreams are identical.
+  encoder_level — BASELINE's metric on the encoder itself: encoded fps of the
+                 reference x265 encoder and of the same encoder with its lookahead
+                 cost estimates on the MI355X (integration/gpu_lookahead.cpp), 64
+                 synthetic frames at the bench resolution on the same host cores,
+                 bitstreams identical; plus the per-call provider on a small clip.
 
 `value` is frames/s of the PRIMITIVE WORKLOAD (the census replay), not of an
 end-to-end encode: the census's calls are replayed as independent batches,
@@ -277,28 +279,60 @@ def reference_encoder_baseline(args):
             "mpix_per_s": round(fps_all * args.width * args.height / 1e6, 3)}
 
 
-def encoder_level(seconds_cap=120):
-    """The reference encoder (x265_encoder_encode) on the MI355X per-call provider vs its C table
-    (oracle/_ref/x265hip8, tests/test_dropin.py): 416x240, 2 frames, --preset medium -F 2."""
+def encoder_level(args, reps=3):
+    """BASELINE's metric on the encoder itself: encoded fps of the reference x265 1.9 encoder
+    (oracle/_ref/x265ref8, C primitives) and of the same encoder with its lookahead cost estimates on
+    the MI355X (oracle/_ref/x265la8: integration/gpu_lookahead.cpp over the x265amd_la_* session,
+    tests/test_encoder_lookahead.py), on the same synthetic frames, the same host cores (--pools) and
+    the default frame threads, runs interleaved; median of `reps` each; bitstreams must be identical.
+    Beside it, the per-call provider (every primitive one synchronous device round trip) on a small clip."""
+    import statistics
     import tempfile
 
     from src.x265_amd.synth import SyntheticSource
 
-    exe = os.path.join(ROOT, "oracle", "_ref", "x265hip8")
-    if not os.path.exists(exe):
+    ref, la = (os.path.join(ROOT, "oracle", "_ref", b) for b in ("x265ref8", "x265la8"))
+    if args.depth != 8 or not (os.path.exists(ref) and os.path.exists(la)):
         return None
-    w, h, n = 416, 240, 2
-    extra = ["--preset", "medium", "-F", "2", "--pools", "8"]
+    cores = host_cores()
+    n = 64 if args.width * args.height <= 1920 * 1080 else 16
+    extra = ["--preset", args.preset, "--pools", str(cores)]
+    out = {"clip": f"{n} synthetic {args.width}x{args.height} 8-bit frames, --preset {args.preset}, --pools {cores}, "
+                   f"default frame threads", "cores": cores, "cpu_model": cpu_model()}
     with tempfile.TemporaryDirectory() as td:
         src = os.path.join(td, "src.yuv")
-        SyntheticSource(w, h, n, 8).write_yuv(src)
-        c_fps, c_md5, _ = _x265_run(exe, src, w, h, 8, n, extra, env=dict(os.environ, X265AMD_PROVIDER="c"))
-        g_fps, g_md5, _ = _x265_run(exe, src, w, h, 8, n, extra, env=dict(os.environ, X265AMD_PROVIDER="hip"),
-                                    timeout=seconds_cap)
-    return {"clip": f"{w}x{h} 8-bit, {n} frames, --preset medium -F 2", "c_table_fps": c_fps,
-            "mi355x_per_call_provider_fps": g_fps, "bitstreams_identical": c_md5 == g_md5,
-            "note": "every table call is one synchronous host->device->host round trip; the batched C ABI "
-                    "(value / caller_level_rates) is the throughput path"}
+        SyntheticSource(args.width, args.height, n, 8).write_yuv(src)
+        fr, fl, md5 = [], [], set()
+        for _ in range(reps):
+            f, m, _ = _x265_run(ref, src, args.width, args.height, 8, n, extra)
+            fr.append(f)
+            md5.add(("ref", m))
+            f, m, _ = _x265_run(la, src, args.width, args.height, 8, n, extra)
+            fl.append(f)
+            md5.add(("la", m))
+        digests = {m for _, m in md5}
+        out.update({"reference_fps": statistics.median(fr), "reference_fps_runs": fr,
+                    "mi355x_lookahead_fps": statistics.median(fl), "mi355x_lookahead_fps_runs": fl,
+                    "speedup": round(statistics.median(fl) / statistics.median(fr), 3),
+                    "mi355x_lookahead_mpix_per_s": round(statistics.median(fl) * args.width * args.height / 1e6, 2),
+                    "bitstreams_identical": len(digests) == 1,
+                    "what_runs_on_the_gpu": "LookaheadTLD::lowresIntraEstimate and every CostEstimateGroup "
+                                            "estimate (P / B, motion searches, batched per finishBatch); analysis, "
+                                            "RDO, CABAC, loop filters stay on the host cores"})
+    hip = os.path.join(ROOT, "oracle", "_ref", "x265hip8")
+    if os.path.exists(hip):
+        w, h, n2 = 416, 240, 2
+        small = ["--preset", "medium", "-F", "2", "--pools", "8"]
+        with tempfile.TemporaryDirectory() as td:
+            src = os.path.join(td, "src.yuv")
+            SyntheticSource(w, h, n2, 8).write_yuv(src)
+            c_fps, c_md5, _ = _x265_run(hip, src, w, h, 8, n2, small, env=dict(os.environ, X265AMD_PROVIDER="c"))
+            g_fps, g_md5, _ = _x265_run(hip, src, w, h, 8, n2, small, env=dict(os.environ, X265AMD_PROVIDER="hip"),
+                                        timeout=120)
+        out["per_call_provider"] = {"clip": f"{w}x{h} 8-bit, {n2} frames, --preset medium -F 2", "c_table_fps": c_fps,
+                                    "mi355x_per_call_provider_fps": g_fps, "bitstreams_identical": c_md5 == g_md5,
+                                    "note": "every table call is one synchronous host->device->host round trip"}
+    return out
 
 
 def census_replay_cpu(args, census):
@@ -584,7 +618,7 @@ def main():
                 cpu["census_replay"] = replay
         if world == 1 and not args.no_encoder_level:
             try:
-                enc = encoder_level()
+                enc = encoder_level(args)
             except Exception as e:
                 enc = {"error": str(e)}
         line = {
