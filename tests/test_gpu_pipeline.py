@@ -40,13 +40,18 @@ def test_gpu_pipeline_gop_equals_whole_frame_chain(gpu_prims, oracle_libs, band_
     gpu_prims.extend_border(8, [bp for bps in pipe.bor for bp in bps])
     torch.cuda.synchronize()
     pipe.dbk, pipe.sao, pipe.bor = saved
-    # the rows the chain defines: the picture and its margins (rows below the CTU-aligned plane's
-    # bottom margin are never written or read)
-    lim = [(2 * fs.my + H) * fs.stride, (2 * fs.cmy + H // 2) * fs.cstride, (2 * fs.cmy + H // 2) * fs.cstride]
+    # the area the chain defines: the picture and its margins (rows below the CTU-aligned plane's bottom
+    # margin and columns right of the right margin are never written or read)
+    geo = [(fs.stride, 2 * fs.my + H, 2 * fs.mx + W)] + [(fs.cstride, 2 * fs.cmy + H // 2, 2 * fs.cmx + W // 2)] * 2
+
+    def area(t, p):
+        stride, rows, cols = geo[p]
+        return t[:rows * stride].view(rows, stride)[:, :cols]
+
     for k in range(F):
         got, want = pipe.final_planes(k), pipe.frame_planes(final, k)
         for p in range(3):
-            assert torch.equal(got[p][:lim[p]], want[p][:lim[p]]), \
+            assert torch.equal(area(got[p], p), area(want[p], p)), \
                 f"picture {k} plane {p}: band pipeline != whole-frame chain"
     for r, slot in pipe.sof.items():
         st = pipe.frame_planes([fs.luma, fs.cb, fs.cr], slot)
