@@ -26,13 +26,62 @@ namespace x265amd {
 
 typedef unsigned short pair16 __attribute__((ext_vector_type(2)));
 
-// ---- shared steps of the N-lane-per-job kernels (lane r of a job owns output row r)
-// R[j] = s'[1 + j] for j = -1 .. 2N-1, L[y] = s'[2N + 1 + y] for y = 0 .. N (s' = neighbours in the
-// mode's frame), R[-2-k] = projected left samples (intrapred.cpp:111-164)
-template <int N>
-__device__ __forceinline__ void intra_refs(const int16_t* sr, int r, const ModeInfo& mi, int16_t* R, int16_t* L)
+template <typename P, int N>
+__global__ __launch_bounds__(X265AMD_BLOCK) void k_intra_pred(int n, int maxv,
+    P* __restrict__ dst, intptr_t ds, const int64_t* __restrict__ doff,
+    const P* __restrict__ nb, const int64_t* __restrict__ nboff,
+    const P* __restrict__ filt, const int64_t* __restrict__ filtoff,
+    const uint8_t* __restrict__ mode, const uint8_t* __restrict__ bfilter, int allangs)
 {
+    constexpr int JOBS = X265AMD_BLOCK / N;
     constexpr int N2 = 2 * N;
+    constexpr int LG2 = N == 4 ? 2 : N == 8 ? 3 : N == 16 ? 4 : 5;
+    constexpr int SLOT = 4 * N + 4;                  // R: 3N+1, L: N+1, padded
+    constexpr int PW = 3 * N;                        // pairs D[j] = (R[j], R[j + 1]), j = -N .. 2N-1
+    __shared__ int16_t sh[JOBS][SLOT];
+    __shared__ int16_t raw[JOBS][4 * N + 2];         // the 4N+1 neighbours as loaded
+    __shared__ uint32_t Dp[JOBS][PW];
+    const int slot = threadIdx.x / N, r = threadIdx.x % N;
+    const int64_t job = (int64_t)xcd_block() * JOBS + slot;
+    const bool live = job < n;
+    const int64_t jj = live ? job : 0;
+    int16_t* R = sh[slot] + N;                       // R[j], j = -N .. 2N
+    int16_t* L = sh[slot] + 3 * N + 2;               // L[y], y = 0 .. N
+    uint32_t* D = Dp[slot] + N;                      // D[j], j = -N .. 2N-1
+
+    int m, bf;
+    const P* src;
+    P* out;
+    if (allangs)
+    {
+        // job = tu * 33 + (mode - 2); filtered or unfiltered neighbours per g_intraFilterFlags
+        const int64_t tu = jj / 33;
+        m = 2 + (int)(jj % 33);
+        bf = bfilter[tu];
+        src = (c_intra.filter_flags[m] & N) ? filt + filtoff[tu] : nb + nboff[tu];
+        out = dst + doff[tu] + (int64_t)(m - 2) * N * N;
+    }
+    else
+    {
+        m = mode[jj];
+        bf = bfilter[jj];
+        src = nb + nboff[jj];
+        out = dst + doff[jj];
+    }
+    const ModeInfo mi = decode_mode(m);
+
+    // ---- neighbours: lane r loads pixels 4r .. 4r+3 with one vector load (lane 0 also pixel 4N)
+    {
+        int t[4];
+        load_row<P, 4>(src + 4 * r, t);
+#pragma unroll
+        for (int k = 0; k < 4; k++) raw[slot][4 * r + k] = (int16_t)t[k];
+        if (r == 0) raw[slot][4 * N] = (int16_t)src[4 * N];
+    }
+    __syncthreads();
+    const int16_t* sr = raw[slot];
+    // ---- R[j] = s'[1 + j] for j = -1 .. 2N-1, L[y] = s'[2N + 1 + y] for y = 0 .. N
+    //      (s' = neighbours in the mode's frame), R[-2-k] = projected left samples
     for (int e = r; e < N2 + 1; e += N) R[e - 1] = sr[flip_index(e, N2, mi.hor)];
     for (int y = r; y <= N; y += N) L[y] = sr[flip_index(N2 + 1 + y, N2, mi.hor)];
     if (mi.angle < 0)
@@ -41,21 +90,13 @@ __device__ __forceinline__ void intra_refs(const int16_t* sr, int r, const ModeI
         for (int k = r; k < nproj; k += N)
             R[-2 - k] = sr[flip_index(N2 + ((128 + (k + 1) * mi.inv) >> 8), N2, mi.hor)];
     }
-}
-
-// pairs D[j] = (R[j], R[j + 1]) for the angular interpolation: one ds_read_b32 + one v_dot2 per pixel
-template <int N>
-__device__ __forceinline__ void intra_pairs(int r, const int16_t* R, uint32_t* D)
-{
+    __syncthreads();
+    // pairs for the angular interpolation: one ds_read_b32 + one v_dot2 per pixel
     for (int j = r - N; j < 2 * N; j += N) D[j] = (uint32_t)(uint16_t)R[j] | ((uint32_t)(uint16_t)R[j + 1] << 16);
-}
+    __syncthreads();
+    if (!live) return;
 
-// output row r of mode m (vframe: horizontal modes stored in the vertical frame, as all-angles does)
-template <int N>
-__device__ __forceinline__ void intra_row(int m, int bf, int r, int maxv, bool vframe, const ModeInfo& mi,
-                                          const int16_t* R, const int16_t* L, const uint32_t* D, int (&v)[N])
-{
-    constexpr int LG2 = N == 4 ? 2 : N == 8 ? 3 : N == 16 ? 4 : 5;
+    int v[N];
     if (m == 0)   // planar (intrapred.cpp:87-100), unflipped: above = R[0..N], left = L[0..N]
     {
         const int lr = L[r], bl = L[N], tr = R[N];
@@ -68,7 +109,7 @@ __device__ __forceinline__ void intra_row(int m, int bf, int r, int maxv, bool v
         int t = N;
 #pragma unroll
         for (int i = 0; i < N; i++) t += R[i] + L[i];
-        const int dc = t / (2 * N);
+        const int dc = t / N2;
 #pragma unroll
         for (int x = 0; x < N; x++) v[x] = dc;
         if (bf)
@@ -83,7 +124,7 @@ __device__ __forceinline__ void intra_row(int m, int bf, int r, int maxv, bool v
                 v[0] = (L[r] + 3 * dc + 2) >> 2;
         }
     }
-    else if (!mi.hor || vframe)
+    else if (!mi.hor || allangs)
     {
         // output row r is vertical-frame row y = r: one (offset, fraction) for the whole row
         const int sum = (r + 1) * mi.angle, off = sum >> 5, f = sum & 31;
@@ -135,155 +176,19 @@ __device__ __forceinline__ void intra_row(int m, int bf, int r, int maxv, bool v
             }
         }
     }
-}
-
-// one output row as 16-byte stores
-template <typename P, int N>
-__device__ __forceinline__ void intra_store(P* orow, const int (&v)[N])
-{
-    constexpr int C = sizeof(P) == 1 ? 16 : 8;       // pixels per 16-byte store
-    if constexpr (N < C)
-        store_row<P, N>(orow, v);
+    P* orow = out + (int64_t)r * (allangs ? N : ds);
+    if constexpr (N == 4)
+        store_row<P, 4>(orow, v);
     else
     {
 #pragma unroll
-        for (int x = 0; x < N; x += C)
+        for (int x = 0; x < N; x += 8)
         {
-            int t[C];
+            int t[8];
 #pragma unroll
-            for (int k = 0; k < C; k++) t[k] = v[x + k];
-            store_row<P, C>(orow + x, t);
+            for (int k = 0; k < 8; k++) t[k] = v[x + k];
+            store_row<P, 8>(orow + x, t);
         }
-    }
-}
-
-// all-angles (and the block-per-256-lanes form): one (TU, mode) job per N-lane group, block barriers
-template <typename P, int N>
-__global__ __launch_bounds__(X265AMD_BLOCK) void k_intra_pred(int n, int maxv,
-    P* __restrict__ dst, intptr_t ds, const int64_t* __restrict__ doff,
-    const P* __restrict__ nb, const int64_t* __restrict__ nboff,
-    const P* __restrict__ filt, const int64_t* __restrict__ filtoff,
-    const uint8_t* __restrict__ mode, const uint8_t* __restrict__ bfilter, int allangs)
-{
-    constexpr int JOBS = X265AMD_BLOCK / N;
-    constexpr int SLOT = 4 * N + 4;                  // R: 3N+1, L: N+1, padded
-    constexpr int PW = 3 * N;                        // pairs D[j] = (R[j], R[j + 1]), j = -N .. 2N-1
-    __shared__ int16_t sh[JOBS][SLOT];
-    __shared__ int16_t raw[JOBS][4 * N + 2];         // the 4N+1 neighbours as loaded
-    __shared__ uint32_t Dp[JOBS][PW];
-    const int slot = threadIdx.x / N, r = threadIdx.x % N;
-    const int64_t job = (int64_t)xcd_block() * JOBS + slot;
-    const bool live = job < n;
-    const int64_t jj = live ? job : 0;
-    int16_t* R = sh[slot] + N;                       // R[j], j = -N .. 2N
-    int16_t* L = sh[slot] + 3 * N + 2;               // L[y], y = 0 .. N
-    uint32_t* D = Dp[slot] + N;                      // D[j], j = -N .. 2N-1
-
-    int m, bf;
-    const P* src;
-    P* out;
-    if (allangs)
-    {
-        // job = tu * 33 + (mode - 2); filtered or unfiltered neighbours per g_intraFilterFlags
-        const int64_t tu = jj / 33;
-        m = 2 + (int)(jj % 33);
-        bf = bfilter[tu];
-        src = (c_intra.filter_flags[m] & N) ? filt + filtoff[tu] : nb + nboff[tu];
-        out = dst + doff[tu] + (int64_t)(m - 2) * N * N;
-    }
-    else
-    {
-        m = mode[jj];
-        bf = bfilter[jj];
-        src = nb + nboff[jj];
-        out = dst + doff[jj];
-    }
-    const ModeInfo mi = decode_mode(m);
-
-    // ---- neighbours: lane r loads pixels 4r .. 4r+3 with one vector load (lane 0 also pixel 4N)
-    {
-        int t[4];
-        load_row<P, 4>(src + 4 * r, t);
-#pragma unroll
-        for (int k = 0; k < 4; k++) raw[slot][4 * r + k] = (int16_t)t[k];
-        if (r == 0) raw[slot][4 * N] = (int16_t)src[4 * N];
-    }
-    __syncthreads();
-    intra_refs<N>(raw[slot], r, mi, R, L);
-    __syncthreads();
-    intra_pairs<N>(r, R, D);
-    __syncthreads();
-    if (!live) return;
-    int v[N];
-    intra_row<N>(m, bf, r, maxv, allangs, mi, R, L, D, v);
-    intra_store<P, N>(out + (int64_t)r * (allangs ? N : ds), v);
-}
-
-// intra_pred of the 16x16 / 32x32 TUs: every wave works on its own jobs (64 / N at a time, lane r
-// of a job owns output row r) with wave-local LDS and wave-level ordering only, persistent over the
-// batch; the next jobs' neighbours, modes and offsets are loaded before the current jobs' LDS work
-// and stores, so a wave always has its next loads in flight
-template <typename P, int N>
-__global__ __launch_bounds__(X265AMD_BLOCK) void k_intra_wave(int n, int maxv,
-    P* __restrict__ dst, intptr_t ds, const int64_t* __restrict__ doff,
-    const P* __restrict__ nb, const int64_t* __restrict__ nboff,
-    const uint8_t* __restrict__ mode, const uint8_t* __restrict__ bfilter)
-{
-    constexpr int JPW = 64 / N;                      // jobs per wave iteration
-    constexpr int WPB = X265AMD_BLOCK / 64;
-    constexpr int SLOT = 4 * N + 4;
-    constexpr int PW = 3 * N;
-    __shared__ int16_t sh[WPB][JPW][SLOT];
-    __shared__ int16_t raw[WPB][JPW][4 * N + 2];
-    __shared__ uint32_t Dp[WPB][JPW][PW];
-    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int slot = lane / N, r = lane % N;
-    int16_t* R = sh[wv][slot] + N;
-    int16_t* L = sh[wv][slot] + 3 * N + 2;
-    uint32_t* D = Dp[wv][slot] + N;
-    int16_t* sr = raw[wv][slot];
-    const int64_t groups = ((int64_t)n + JPW - 1) / JPW;
-    const int64_t step = (int64_t)gridDim.x * WPB;
-    int64_t g = (int64_t)xcd_block() * WPB + wv;
-    // prefetched state of group g
-    int t[4], t4 = 0, m = 0, bf = 0;
-    int64_t oo = 0;
-    bool live = false;
-    auto fetch = [&](int64_t grp) {
-        const int64_t job = grp * JPW + slot;
-        live = job < n;
-        const int64_t jj = live ? job : (int64_t)n - 1;
-        const P* src = nb + nboff[jj];
-        load_row<P, 4>(src + 4 * r, t);
-        if (r == 0) t4 = src[4 * N];
-        m = mode[jj];
-        bf = bfilter[jj];
-        oo = doff[jj];
-    };
-    if (g < groups) fetch(g);
-    for (; g < groups; g += step)
-    {
-        int ct[4] = { t[0], t[1], t[2], t[3] };
-        const int ct4 = t4, cm = m, cbf = bf;
-        const int64_t coo = oo;
-        const bool clive = live;
-        if (g + step < groups) fetch(g + step);
-#pragma unroll
-        for (int k = 0; k < 4; k++) sr[4 * r + k] = (int16_t)ct[k];
-        if (r == 0) sr[4 * N] = (int16_t)ct4;
-        wave_sync();
-        const ModeInfo mi = decode_mode(cm);
-        intra_refs<N>(sr, r, mi, R, L);
-        wave_sync();
-        intra_pairs<N>(r, R, D);
-        wave_sync();
-        if (clive)
-        {
-            int v[N];
-            intra_row<N>(cm, cbf, r, maxv, false, mi, R, L, D, v);
-            intra_store<P, N>(dst + coo + (int64_t)r * ds, v);
-        }
-        wave_sync();                                 // the LDS of this group is read before it is rewritten
     }
 }
 
@@ -518,9 +423,6 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_intra_filter(int N, int n, co
     if (l == 0) d[4 * N] = s[4 * N];
 }
 
-// persistent intra_pred grid: 2048 blocks = 8 per CU of 256 (32 waves per CU in flight at most)
-constexpr int64_t kIntraWaveBlocks = 2048;
-
 template <typename P>
 static int launch_pred(int N, int n, int depth, void* dst, intptr_t ds, const int64_t* doff, const void* nb,
                        const int64_t* nboff, const void* filt, const int64_t* filtoff, const uint8_t* mode,
@@ -534,27 +436,8 @@ static int launch_pred(int N, int n, int depth, void* dst, intptr_t ds, const in
     {
     case 4: L(k_intra_lane, 4); break;
     case 8: L(k_intra_lane, 8); break;
-    case 16:
-    case 32:
-        if (!allangs)
-        {
-            // persistent waves: enough blocks for 4 per CU slot, each wave looping over its job groups
-            const int64_t groups = ((int64_t)n + 64 / N - 1) / (64 / N);
-            int64_t blocks = (groups + X265AMD_BLOCK / 64 - 1) / (X265AMD_BLOCK / 64);
-            blocks = blocks < kIntraWaveBlocks ? blocks : kIntraWaveBlocks;
-            const dim3 g2((uint32_t)(blocks > 0 ? blocks : 1));
-            if (N == 16)
-                hipLaunchKernelGGL((k_intra_wave<P, 16>), g2, dim3(X265AMD_BLOCK), 0, st, n, (1 << depth) - 1,
-                                   (P*)dst, ds, doff, (const P*)nb, nboff, mode, bfilter);
-            else
-                hipLaunchKernelGGL((k_intra_wave<P, 32>), g2, dim3(X265AMD_BLOCK), 0, st, n, (1 << depth) - 1,
-                                   (P*)dst, ds, doff, (const P*)nb, nboff, mode, bfilter);
-        }
-        else if (N == 16)
-            L(k_intra_pred, 16);
-        else
-            L(k_intra_pred, 32);
-        break;
+    case 16: L(k_intra_pred, 16); break;
+    case 32: L(k_intra_pred, 32); break;
     default: return X265AMD_EINVAL;
     }
 #undef L
