@@ -301,23 +301,52 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_tr32_mfma(int n, int depth,
             t2[st][j] = (_Float16)(FWD ? c_t32.m[r][kp] : c_t32.m[kp][r]);
         }
 
+    // software pipeline: the next transform's 2 KiB are loaded (into registers) before this one's
+    // MFMA chain and stores, so every wave keeps a transform's worth of loads in flight
     const int64_t step = (int64_t)gridDim.x * kTrWaves;
-    for (int64_t job = (int64_t)blockIdx.x * kTrWaves + w; job < n; job += step)
+    int64_t job = (int64_t)blockIdx.x * kTrWaves + w;
+    uint4 nx[2];                                     // forward: row r halves; inverse: the lane's 16-byte I/O chunks
+    auto fetch = [&](int64_t jb) {
+        const int16_t* s = src + soff[jb];
+        if constexpr (FWD)
+        {
+            nx[0] = ldu<uint4>(s + r * ss + 8 * h);
+            nx[1] = ldu<uint4>(s + r * ss + 16 + 8 * h);
+        }
+        else
+        {
+            nx[0] = ldu<uint4>(s + io_row * ss + io_col);
+            nx[1] = ldu<uint4>(s + io_row * ss + io_col + 8);
+        }
+    };
+    if (job < n) fetch(job);
+    for (; job < n; job += step)
     {
-        const int16_t* s = src + soff[job];
         int16_t* d = dst + doff[job];
+        const uint4 cx[2] = { nx[0], nx[1] };
+        if (job + step < n) fetch(job + step);
         // ---- stage 1: forward U = Src * T^T (A = source rows, 16-byte row loads);
         //      inverse M1 = C^T * T (A = coefficient columns, staged through the tile)
         int x[2][8];
         if constexpr (FWD)
         {
-            load_row16<8>(s + r * ss + 8 * h, x[0]);
-            load_row16<8>(s + r * ss + 16 + 8 * h, x[1]);
+#pragma unroll
+            for (int st = 0; st < 2; st++)
+            {
+                const uint32_t wv[4] = { cx[st].x, cx[st].y, cx[st].z, cx[st].w };
+#pragma unroll
+                for (int q = 0; q < 4; q++)
+                {
+                    x[st][2 * q] = (int16_t)(wv[q] & 0xffff);
+                    x[st][2 * q + 1] = (int16_t)(wv[q] >> 16);
+                }
+            }
         }
         else
         {
-#pragma unroll
-            for (int c = 0; c < 16; c += 8) stu<uint4>(&T[io_row * 32 + io_col + c], ldu<uint4>(s + io_row * ss + io_col + c));
+            stu<uint4>(&T[io_row * 32 + io_col], cx[0]);
+            stu<uint4>(&T[io_row * 32 + io_col + 8], cx[1]);
+            wave_sync();
 #pragma unroll
             for (int st = 0; st < 2; st++)
 #pragma unroll
@@ -367,8 +396,10 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_tr32_mfma(int n, int depth,
             const int a = (int)hi2[i] * 2048 + (int)lo2[i];
             T[((i & 3) + 8 * (i >> 2) + 4 * h) * 32 + r] = (int16_t)(FWD ? fwd_round(a, sh2) : inv_round(a, sh2));
         }
+        wave_sync();
 #pragma unroll
         for (int c = 0; c < 16; c += 8) stu<uint4>(d + io_row * ds + io_col + c, ldu<uint4>(&T[io_row * 32 + io_col + c]));
+        wave_sync();                                 // the tile is read out before the next transform rewrites it
     }
 }
 
@@ -393,21 +424,48 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_tr16_mfma(int n, int depth,
 #pragma unroll
     for (int j = 0; j < 4; j++) t[j] = (_Float16)(FWD ? c_t32.m[2 * r][4 * q + j] : c_t32.m[2 * (4 * q + j)][r]);
 
+    // software pipeline: the next iteration's JB transforms are loaded (into registers) before this
+    // iteration's MFMA chains and stores
     const int64_t step = (int64_t)gridDim.x * kTrWaves * JB;
-    for (int64_t job0 = ((int64_t)blockIdx.x * kTrWaves + w) * JB; job0 < n; job0 += step)
-    {
-        int16_t* d[JB];
-        int x[JB][4];
+    int64_t job0 = ((int64_t)blockIdx.x * kTrWaves + w) * JB;
+    uint2 nx[JB];
+    auto fetch = [&](int64_t j0) {
 #pragma unroll
         for (int b = 0; b < JB; b++)
         {
-            const int64_t job = job0 + b < n ? job0 + b : job0;   // a tail repeats the first (its result is not stored)
+            const int64_t job = j0 + b < n ? j0 + b : j0;   // a tail repeats the first (its result is not stored)
             const int16_t* s = src + soff[job];
-            d[b] = dst + doff[job];
-            int16_t* T = tile[w][b];
-            if constexpr (FWD) load_row16<4>(s + r * ss + 4 * q, x[b]);
-            else stu<uint2>(&T[io_row * 16 + io_col], ldu<uint2>(s + io_row * ss + io_col));
+            nx[b] = FWD ? ldu<uint2>(s + r * ss + 4 * q) : ldu<uint2>(s + io_row * ss + io_col);
         }
+    };
+    if (job0 < n) fetch(job0);
+    for (; job0 < n; job0 += step)
+    {
+        int16_t* d[JB];
+        int x[JB][4];
+        uint2 cx[JB];
+#pragma unroll
+        for (int b = 0; b < JB; b++)
+        {
+            cx[b] = nx[b];
+            d[b] = dst + doff[job0 + b < n ? job0 + b : job0];
+        }
+        if (job0 + step < n) fetch(job0 + step);
+#pragma unroll
+        for (int b = 0; b < JB; b++)
+        {
+            int16_t* T = tile[w][b];
+            if constexpr (FWD)
+            {
+                x[b][0] = (int16_t)(cx[b].x & 0xffff);
+                x[b][1] = (int16_t)(cx[b].x >> 16);
+                x[b][2] = (int16_t)(cx[b].y & 0xffff);
+                x[b][3] = (int16_t)(cx[b].y >> 16);
+            }
+            else
+                stu<uint2>(&T[io_row * 16 + io_col], cx[b]);
+        }
+        if constexpr (!FWD) wave_sync();
         f32x4 lo[JB], hi[JB];
 #pragma unroll
         for (int b = 0; b < JB; b++)
@@ -454,8 +512,10 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_tr16_mfma(int n, int depth,
                 const int a = (int)hi[b][i] * 2048 + (int)lo[b][i];
                 T[(4 * q + i) * 16 + r] = (int16_t)(FWD ? fwd_round(a, sh2) : inv_round(a, sh2));
             }
+            wave_sync();
             if (job0 + b < n) stu<uint2>(d[b] + io_row * ds + io_col, ldu<uint2>(&T[io_row * 16 + io_col]));
         }
+        wave_sync();                                 // tiles read out before the next iteration rewrites them
     }
 }
 
