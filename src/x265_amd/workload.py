@@ -402,7 +402,21 @@ class WorkloadBuilder:
         nblk = bx * by
         per = -(-n // fs.F)
         if per <= nblk:
-            blk = np.sort(rng.choice(nblk, size=per, replace=False))
+            # fewer calls than blocks: whole CTUs of blocks, the way CU analysis visits a CTU's blocks at
+            # each depth (analysis.cpp compressInterCU_rd*), CTUs in raster order and the blocks of a CTU
+            # in raster order inside it — neighbouring jobs share the CTU's rows and cache lines
+            ctu = 32 if chroma else 64
+            cw, ch = max(1, ctu // w), max(1, ctu // h)          # blocks per CTU across / down
+            ncx, ncy = -(-bx // cw), -(-by // ch)
+            k = -(-per // (cw * ch))
+            ctus = np.sort(rng.choice(ncx * ncy, size=min(k, ncx * ncy), replace=False))
+            ix = (ctus % ncx)[:, None] * cw + (np.arange(cw * ch) % cw)[None, :]
+            iy = (ctus // ncx)[:, None] * ch + (np.arange(cw * ch) // cw)[None, :]
+            ok = (ix < bx) & (iy < by)
+            blk = (iy * bx + ix)[ok][:per]
+            if len(blk) < per:                                 # partial CTUs at the picture edge
+                rest = np.setdiff1d(np.arange(nblk), blk)
+                blk = np.concatenate([blk, np.sort(rng.choice(rest, size=per - len(blk), replace=False))])
             cand = np.zeros(per, np.int64)
         else:
             reps = -(-per // nblk)
