@@ -403,13 +403,14 @@ class WorkloadBuilder:
         per = -(-n // fs.F)
         if per <= nblk:
             # fewer calls than blocks: whole CTUs of blocks, the way CU analysis visits a CTU's blocks at
-            # each depth (analysis.cpp compressInterCU_rd*), CTUs in raster order and the blocks of a CTU
-            # in raster order inside it — neighbouring jobs share the CTU's rows and cache lines
+            # each depth (analysis.cpp compressInterCU_rd*) — a run of consecutive CTUs (raster order,
+            # from a random start) and the blocks of a CTU in raster order inside it, so neighbouring
+            # jobs share the CTU's rows and cache lines, and so do neighbouring CTUs
             ctu = 32 if chroma else 64
             cw, ch = max(1, ctu // w), max(1, ctu // h)          # blocks per CTU across / down
             ncx, ncy = -(-bx // cw), -(-by // ch)
-            k = -(-per // (cw * ch))
-            ctus = np.sort(rng.choice(ncx * ncy, size=min(k, ncx * ncy), replace=False))
+            k = min(-(-per // (cw * ch)), ncx * ncy)
+            ctus = np.sort((int(rng.integers(0, ncx * ncy)) + np.arange(k)) % (ncx * ncy))
             ix = (ctus % ncx)[:, None] * cw + (np.arange(cw * ch) % cw)[None, :]
             iy = (ctus // ncx)[:, None] * ch + (np.arange(cw * ch) // cw)[None, :]
             ok = (ix < bx) & (iy < by)
