@@ -127,6 +127,9 @@ def dist_setup(args):
         if torch.cuda.is_available():
             torch.cuda.set_device(local)
         dist.init_process_group(backend=backend)
+        # the first collective of the group is one every rank joins (batch_isend_irecv, which only the
+        # ranks with transfers in a step call, must not be the first NCCL call of the group)
+        dist.barrier()
     elif torch.cuda.is_available():
         torch.cuda.set_device(local)
     return world, rank, local
