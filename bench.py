@@ -432,6 +432,9 @@ def main():
         pipe = GpuFramePipeline(prims, args.width, args.height, args.depth, F, world, rank, census=census,
                                 band_rows=args.band_rows or None, segment_frames=args.segment_frames or None,
                                 streams=nstreams, device=f"cuda:{local}")
+        # slice (and reorder) the census batches per step and capture the step graphs FIRST: every launch
+        # group below then builds its descriptor tables from the batches' final per-job tensors
+        pipe.build(graphs=not args.no_graph)
         batches, wb = pipe.batches, pipe.wb
     else:
         # independent replay: this rank's F frames' census as one set of grouped launches
@@ -491,7 +494,6 @@ def main():
 
     graph = None
     if pipe is not None:
-        pipe.build(graphs=not args.no_graph)
         graph = bool(pipe.graphs) or None
 
         def run():

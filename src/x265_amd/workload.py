@@ -337,6 +337,9 @@ class LaunchGroup:
             return self.members[0].run(prims, stream)
         if self._arr is None:
             self._arr = self._descriptors()   # device addresses are fixed for the life of the batches
+            # the table holds raw addresses: keep the tensors they point into alive with it (a batch
+            # whose per-job tensors are later replaced, e.g. reordered, must not leave it dangling)
+            self._keep = [dict(b.dev) for b in self.members]
         if self.kind == "pixelcmp":
             prims.pixelcmp_grouped(self.op, self.depth, self._arr, stream)
         elif self.kind == "sad_multi":
