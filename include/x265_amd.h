@@ -49,6 +49,10 @@ enum
     X265AMD_ENOMEM = 1002    /* device / pinned staging allocation failed */
 };
 
+/* loop-filter chroma layout value for a luma-only (4:0:0) picture; 0 / 1 = 4:2:0, 2 = 4:2:2,
+ * 3 = 4:4:4 (x265's X265_CSP_I400 is 0 — translate it, do not pass internalCsp through) */
+#define X265AMD_CSP_I400 4
+
 /* ----------------------------------------------------------------- runtime */
 int         x265amd_abi_version(void);
 /* Select the HIP device for this host thread; returns 0 or a hipError_t. */
@@ -731,7 +735,10 @@ typedef struct
     void* dst[3];
     int64_t stride, cstride;
     const x265amd_sao_param* params;
-    int chroma_format;   /* 0 or 1 = 4:2:0, 2 = 4:2:2, 3 = 4:4:4 (chroma CTU (ctu >> hshift) x (ctu >> vshift)) */
+    int chroma_format;   /* 0 or 1 = 4:2:0, 2 = 4:2:2, 3 = 4:4:4 (chroma CTU (ctu >> hshift) x (ctu >> vshift)),
+                            X265AMD_CSP_I400 = luma only (chroma planes unused, may be NULL).  NOT x265's
+                            internalCsp: there 0 is X265_CSP_I400, here 0 is 4:2:0 (zero-initialised
+                            descriptors) */
 } x265amd_sao_frame;
 int x265amd_sao_apply(int depth, int count, const x265amd_sao_frame* frames, void* stream);
 
@@ -784,7 +791,9 @@ typedef struct
     int beta_offset_div2, tc_offset_div2, cb_qp_offset, cr_qp_offset, tq_bypass_enabled;
     int32_t ref_poc[2][16];
     int chroma_format;   /* 0 or 1 = 4:2:0, 2 = 4:2:2, 3 = 4:4:4: chroma edges on the chroma plane's 8x8
-                            grid (deblock.cpp:104-113); non-4:2:0 chroma QP min(qp, 51) (:505-506) */
+                            grid (deblock.cpp:104-113); non-4:2:0 chroma QP min(qp, 51) (:505-506);
+                            X265AMD_CSP_I400: luma only (deblock.cpp:443 skips chroma), chroma planes may be
+                            NULL.  NOT x265's internalCsp (there 0 is 4:0:0) */
 } x265amd_deblock_frame;
 int x265amd_deblock(int depth, int count, const x265amd_deblock_frame* frames, void* stream);
 

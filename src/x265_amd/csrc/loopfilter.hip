@@ -391,7 +391,7 @@ struct SaoFrame
     void* dst[3];
     int64_t stride, cstride;
     const x265amd_sao_param* params;
-    int w, h, ctu_log2, wc, nctu, luma_on, chroma_on;
+    int w, h, ctu_log2, wc, nctu, luma_on, chroma_on, i400;
     int c0, nctu_all;                        // first CTU of the band, CTUs of the picture (params stride)
     int hs, vs;                              // chroma shifts
     uint32_t block0;                         // first block (one per plane and CTU)
@@ -421,6 +421,7 @@ __global__ __launch_bounds__(64) void k_sao_apply(const SaoLaunch L)
     const int yend = min(min(y0 + sh, cy0 + csh), ph);
     if (x0 >= pw || y0 >= yend) return;
     const bool full = pw - x0 >= 8;                  // else 4 pixels (a right edge of width 8k + 4)
+    if (p && f.i400) return;                         // 4:0:0: no chroma planes
     const int64_t st = p ? f.cstride : f.stride;
     const P* src = (const P*)f.src[p] + y0 * st + x0;
     P* dst = (P*)f.dst[p] + y0 * st + x0;
@@ -780,9 +781,11 @@ static int deblock_impl(int depth, int count, const x265amd_deblock_frame* frame
     for (int i = 0; i < count; i++)
     {
         const x265amd_deblock_frame& a = frames[i];
-        if (a.width <= 0 || a.height <= 0 || (a.width & 7) || (a.height & 7) || !a.plane[0] || !a.plane[1] ||
-            !a.plane[2] || !a.units || a.unit_stride < a.width / 4 || a.stride < a.width ||
-            a.cstride < (a.chroma_format == 3 ? a.width : a.width / 2) || a.chroma_format < 0 || a.chroma_format > 3)
+        const bool i400 = a.chroma_format == X265AMD_CSP_I400;
+        if (a.width <= 0 || a.height <= 0 || (a.width & 7) || (a.height & 7) || !a.plane[0] ||
+            (!i400 && (!a.plane[1] || !a.plane[2] || a.cstride < (a.chroma_format == 3 ? a.width : a.width / 2))) ||
+            !a.units || a.unit_stride < a.width / 4 || a.stride < a.width || a.chroma_format < 0 ||
+            a.chroma_format > X265AMD_CSP_I400)
             return X265AMD_EINVAL;
         if (rows && (rows[2 * i] < 0 || (rows[2 * i] & 15) || rows[2 * i + 1] <= rows[2 * i] ||
                      rows[2 * i + 1] > a.height || ((rows[2 * i + 1] - rows[2 * i]) & 7)))
@@ -822,13 +825,15 @@ static int deblock_impl(int depth, int count, const x265amd_deblock_frame* frame
                 {
                     const int sx = 2 << f.hs;
                     f.nluma = (uint32_t)((f.wu >> 1) * f.hu);
-                    f.nseg = f.nluma + (uint32_t)(((f.wu + sx - 1) / sx) * (f.hu >> f.vs));
+                    f.nseg = f.nluma + (a.chroma_format == X265AMD_CSP_I400 ? 0u :
+                                        (uint32_t)(((f.wu + sx - 1) / sx) * (f.hu >> f.vs)));
                 }
                 else
                 {
                     const int sy = 2 << f.vs;
                     f.nluma = (uint32_t)(f.wu * (f.hu >> 1));
-                    f.nseg = f.nluma + (uint32_t)((f.wu >> f.hs) * ((f.hu + sy - 1) / sy));
+                    f.nseg = f.nluma + (a.chroma_format == X265AMD_CSP_I400 ? 0u :
+                                        (uint32_t)((f.wu >> f.hs) * ((f.hu + sy - 1) / sy)));
                 }
                 f.block0 = blocks;
                 blocks += nblocks(f.nseg);
@@ -867,14 +872,15 @@ static int sao_apply_impl(int depth, int count, const x265amd_sao_frame* frames,
     for (int i = 0; i < count; i++)
     {
         const x265amd_sao_frame& a = frames[i];
+        const bool i400 = a.chroma_format == X265AMD_CSP_I400;
         if (a.width <= 0 || a.height <= 0 || (a.width & 7) || (a.height & 7) || a.ctu_log2 < 4 || a.ctu_log2 > 6 ||
-            !a.params || a.stride < a.width || a.cstride < (a.chroma_format == 3 ? a.width : a.width / 2) ||
-            a.chroma_format < 0 || a.chroma_format > 3)
+            !a.params || a.stride < a.width || (!i400 && a.cstride < (a.chroma_format == 3 ? a.width : a.width / 2)) ||
+            a.chroma_format < 0 || a.chroma_format > X265AMD_CSP_I400)
             return X265AMD_EINVAL;
         const int hc = (a.height + (1 << a.ctu_log2) - 1) >> a.ctu_log2;
         if (ctu_rows && (ctu_rows[2 * i] < 0 || ctu_rows[2 * i + 1] <= ctu_rows[2 * i] || ctu_rows[2 * i + 1] > hc))
             return X265AMD_EINVAL;
-        for (int p = 0; p < 3; p++)
+        for (int p = 0; p < (i400 ? 1 : 3); p++)
             if (!a.src[p] || !a.dst[p] || a.src[p] == a.dst[p]) return X265AMD_EINVAL;
     }
     hipStream_t st = (hipStream_t)stream;
@@ -904,6 +910,7 @@ static int sao_apply_impl(int depth, int count, const x265amd_sao_frame* frames,
             f.nctu = ctu_rows ? (ctu_rows[2 * (i0 + k) + 1] - ctu_rows[2 * (i0 + k)]) * f.wc : f.nctu_all;
             f.luma_on = a.luma_on;
             f.chroma_on = a.chroma_on;
+            f.i400 = a.chroma_format == X265AMD_CSP_I400;
             f.hs = a.chroma_format == 3 ? 0 : 1;
             f.vs = a.chroma_format == 2 || a.chroma_format == 3 ? 0 : 1;
             f.block0 = blocks;
@@ -936,7 +943,7 @@ extern "C" int x265amd_sao_stats(int depth, int count, const x265amd_sao_stats_f
     {
         const x265amd_sao_stats_frame& a = frames[i];
         if (a.width <= 0 || a.height <= 0 || (a.width & 7) || (a.height & 7) || a.ctu_log2 < 4 || a.ctu_log2 > 6 ||
-            !a.stats || !a.count || a.chroma_format < 0 || a.chroma_format > 3)
+            !a.stats || !a.count || a.chroma_format < 0 || a.chroma_format > 3)   /* 4:0:0 not supported */
             return X265AMD_EINVAL;
         for (int p = 0; p < 3; p++)
             if (!a.fenc[p] || !a.rec[p]) return X265AMD_EINVAL;

@@ -995,7 +995,9 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_propagate(const x265amd_propa
     const int bx = cu % b.width_cu, by = cu / b.width_cu;
     for (int l = 0; l < 2; l++)
     {
-        if (!((used >> l) & 1)) continue;
+        // a list without MVs or without a reference cost array contributes nothing (a NULL list is
+        // skipped, never dereferenced, even if a lowres cost claims it was used)
+        if (!((used >> l) & 1) || !b.mvs[l] || !b.ref_costs[l]) continue;
         int la = amount;
         if (used == 3) la = (int)((uint32_t)la * (uint32_t)b.bipred_weight[l] + 32u) >> 6;
         unsigned long long* acc = (unsigned long long*)b.scratch + (size_t)l * n;

@@ -414,3 +414,51 @@ def test_gpu_f4_chroma_formats(gpu_prims, csp, depth):
                                           err_msg=f"sao {W}x{H} p{p}")
         np.testing.assert_array_equal(ct.cpu().numpy(), c_ref)
         np.testing.assert_array_equal(st.cpu().numpy(), s_ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("depth", [8, 10])
+def test_gpu_loop_filters_luma_only_i400(gpu_prims, depth):
+    """X265AMD_CSP_I400 (x265's X265_CSP_I400 pictures: deblock.cpp:443 and sao.cpp skip chroma): the
+    chroma planes may be NULL and are never touched; the luma result equals the 4:2:0 run's luma"""
+    import torch
+    from src.x265_amd.native import DeblockFrame, SaoFrame
+
+    W, H, cl = GPU_SIZES[0]
+    rng = np.random.default_rng(7 + depth)
+    pl = F.frame_planes(W, H, depth, rng)
+    U = F.deblock_units(W, H, cl, depth, rng, "P", 0.0)
+    dp = F.deblock_params(rng, "P", 0)
+    du = torch.from_numpy(U.view(np.uint8).reshape(U.shape[0], -1)).cuda()
+    outs = []
+    for csp in (1, 4):
+        d = _dev(F.copy_planes(pl))
+        fr = DeblockFrame()
+        fr.width, fr.height, fr.chroma_format = W, H, csp
+        fr.plane[0] = _org(d[0])
+        if csp != 4:
+            fr.plane[1], fr.plane[2] = _org(d[1]), _org(d[2])
+        fr.stride, fr.cstride = d[0].shape[1], d[1].shape[1]
+        fr.units, fr.unit_stride = du.data_ptr(), U.shape[1]
+        fr.is_p, fr.beta_offset_div2, fr.tc_offset_div2 = dp.is_p, dp.beta_offset_div2, dp.tc_offset_div2
+        gpu_prims.deblock(depth, [fr])
+        torch.cuda.synchronize()
+        outs.append([t.cpu().numpy() for t in d])
+    np.testing.assert_array_equal(outs[0][0], outs[1][0])
+    np.testing.assert_array_equal(outs[1][1], _dev(pl)[1].cpu().numpy())     # chroma untouched
+    # SAO apply, luma only, NULL chroma planes: luma equals the 4:2:0 run's luma
+    prm = F.sao_params(W, H, cl, depth, rng)
+    dprm = torch.from_numpy(np.ascontiguousarray(prm).view(np.uint8).reshape(-1).copy()).cuda()
+    res = []
+    for csp in (1, 4):
+        src, dst = _dev(F.copy_planes(pl)), _dev(F.copy_planes(pl))
+        sf = SaoFrame()
+        sf.width, sf.height, sf.ctu_log2, sf.luma_on, sf.chroma_on, sf.chroma_format = W, H, cl, 1, 1, csp
+        sf.src[0], sf.dst[0] = _org(src[0]), _org(dst[0])
+        if csp != 4:
+            sf.src[1], sf.dst[1], sf.src[2], sf.dst[2] = _org(src[1]), _org(dst[1]), _org(src[2]), _org(dst[2])
+        sf.stride, sf.cstride, sf.params = src[0].shape[1], src[1].shape[1], dprm.data_ptr()
+        gpu_prims.sao_apply(depth, [sf])
+        torch.cuda.synchronize()
+        res.append(dst[0].cpu().numpy())
+    np.testing.assert_array_equal(res[0], res[1])
