@@ -27,6 +27,8 @@ def main():
     ap.add_argument("--frames", default="8,32")
     ap.add_argument("--band-rows", default="17,4")
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--segments", default="0", help="comma list of pictures per closed GOP segment (0: all frames)")
+    ap.add_argument("--no-replay", action="store_true")
     a = ap.parse_args()
     import torch
 
@@ -36,21 +38,23 @@ def main():
 
     prims = Primitives(device=0)
     for F in (int(x) for x in a.frames.split(",")):
-        fs = FrameSet(1920, 1080, F, 8, device="cuda")
-        bs, _ = census_batches(fs, frames=F, builder=WorkloadBuilder(fs, seed=11))
-        ls = group_launches(bs)
-        dt = timed(lambda: [b.run(prims) for b in ls], a.reps)
-        print(json.dumps({"mode": "replay-eager-1stream", "frames": F, "fps": round(F / dt, 1), "launches": len(ls)}),
-              flush=True)
-        del fs, bs, ls
-        for br, early in [(int(x), e) for x in a.band_rows.split(",") for e in (True, False)]:
+        if not a.no_replay:
+            fs = FrameSet(1920, 1080, F, 8, device="cuda")
+            bs, _ = census_batches(fs, frames=F, builder=WorkloadBuilder(fs, seed=11))
+            ls = group_launches(bs)
+            dt = timed(lambda: [b.run(prims) for b in ls], a.reps)
+            print(json.dumps({"mode": "replay-eager-1stream", "frames": F, "fps": round(F / dt, 1),
+                              "launches": len(ls)}), flush=True)
+            del fs, bs, ls
+        for br, seg in [(int(x), int(g)) for x in a.band_rows.split(",") for g in a.segments.split(",")]:
+            early = True
             t0 = time.perf_counter()
             pipe = GpuFramePipeline(prims, 1920, 1080, 8, F, 1, 0, band_rows=br, streams=8, device="cuda",
-                                    early_independent=early)
+                                    early_independent=early, segment_frames=seg or None)
             pipe.build(graphs=True)
             tb = time.perf_counter() - t0
             dt = timed(pipe.step, a.reps)
-            print(json.dumps({"mode": "pipeline", "frames": F, "band_rows": br, "early_independent": early, "fps": round(F / dt, 1),
+            print(json.dumps({"mode": "pipeline", "frames": F, "band_rows": br, "segment_frames": seg or F, "fps": round(F / dt, 1),
                               "ms_per_step": round(dt * 1e3, 3), "steps": pipe.sched.nsteps,
                               "launches": pipe.launches_per_step, "build_s": round(tb, 1)}), flush=True)
             del pipe
