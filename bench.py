@@ -86,6 +86,9 @@ def parse():
     ap.add_argument("--band-rows", type=int, default=0, help="CTU rows per pipeline band (default: whole pictures)")
     ap.add_argument("--segment-frames", type=int, default=0,
                     help="pictures per closed GOP segment in pipeline mode (default: the frames per rank)")
+    ap.add_argument("--exchange", default="torch", choices=("torch", "rccl"),
+                    help="pipeline reference exchange: torch.distributed P2P batches, or the native RCCL communicator "
+                         "of the C ABI (x265amd_exchange, csrc/exchange.cpp)")
     ap.add_argument("--no-pipeline-check", action="store_true",
                     help="skip the N=1 measurement of the frame-parallel pipeline beside a replay run")
     ap.add_argument("--streams", type=int, default=8, help="HIP streams the step's independent launches spread over")
@@ -431,7 +434,7 @@ def main():
 
         pipe = GpuFramePipeline(prims, args.width, args.height, args.depth, F, world, rank, census=census,
                                 band_rows=args.band_rows or None, segment_frames=args.segment_frames or None,
-                                streams=nstreams, device=f"cuda:{local}")
+                                streams=nstreams, device=f"cuda:{local}", exchange=args.exchange)
         # slice (and reorder) the census batches per step and capture the step graphs FIRST: every launch
         # group below then builds its descriptor tables from the batches' final per-job tensors
         pipe.build(graphs=not args.no_graph)
@@ -655,7 +658,8 @@ def main():
                                 f"picture j on rank j mod {world}, bands of {pipe.plan.band_rows} CTU rows in "
                                 f"{pipe.sched.nsteps} schedule steps, final reference bands (deblock/SAO/border) sent "
                                 f"to every rank that reads them over "
-                                f"{'RCCL P2P' if world > 1 else 'in-place stores (one rank)'}" if pipe is not None else
+                                f"{('RCCL P2P (' + args.exchange + ')') if world > 1 else 'in-place stores (one rank)'}"
+                                if pipe is not None else
                                 f"independent replay x{world}"),
                 "frames_per_step_total": world * F,
             },

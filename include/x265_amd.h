@@ -587,6 +587,30 @@ typedef struct
 } x265amd_sched_frame;
 int x265amd_schedule(const x265amd_sched_config* config, x265amd_sched_frame* frames, int* step, int* nsteps);
 
+/* Reference-row exchange of the frame-parallel shard (csrc/exchange.cpp): what FrameFilter's
+ * row publication (m_reconRowCount, framefilter.cpp:520) and the reference-row waits
+ * (frameencoder.cpp:516-531) are across GPUs.  One communicator per rank over RCCL (xGMI
+ * peer-to-peer), created from a 128-byte id made by rank 0 (x265amd_comm_unique_id) and handed to
+ * every rank by the caller; the device is the calling thread's current HIP device.
+ * x265amd_exchange enqueues one step's transfers on `stream` as one group (no host wait):
+ * xfers[i] sends (send = 1) or receives `bytes` bytes at device address buf to / from rank peer
+ * (peer may be the own rank: a loop-back pair).  Every pair of ranks must list the transfers
+ * between them in the same order (x265amd_schedule's canonical order does).  X265AMD_ENODEV when
+ * librccl is not loadable or a RCCL call fails. */
+#define X265AMD_COMM_ID_BYTES 128
+typedef struct x265amd_comm x265amd_comm;
+typedef struct
+{
+    void* buf;
+    size_t bytes;
+    int peer;
+    int send;
+} x265amd_transfer;
+int x265amd_comm_unique_id(uint8_t* id);
+int x265amd_comm_create(x265amd_comm** comm, const uint8_t* id, int nranks, int rank);
+int x265amd_comm_destroy(x265amd_comm* comm);
+int x265amd_exchange(x265amd_comm* comm, const x265amd_transfer* xfers, int count, void* stream);
+
 /* f1 cuTree: Lookahead::estimateCUPropagate (slicetype.cpp:1738-1836) with the
  * propagateCost primitive (pixel.cpp:846-872), one call of it per batch, batches in order.
  * For every lowres CU of frame b: the amount

@@ -20,7 +20,7 @@ LIB = os.path.join(HERE, "libx265amd.so")
 SOURCES = [("pixel.hip", "pixel.o", []), ("interp.hip", "interp.o", []), ("transform.hip", "transform.o", []),
            ("intra.hip", "intra.o", []), ("blockops.hip", "blockops.o", []), ("tu.hip", "tu.o", []), ("lowres.hip", "lowres.o", []), ("me.hip", "me.o", []), ("loopfilter.hip", "loopfilter.o", []),
            ("runtime.hip", "runtime.o", []), ("lookahead.cpp", "lookahead.o", []),
-           ("schedule.cpp", "schedule.o", []),
+           ("schedule.cpp", "schedule.o", []), ("exchange.cpp", "exchange.o", []),
            ("provider.cpp", "provider8.o", ["-DX265_DEPTH=8"]),
            ("provider.cpp", "provider10.o", ["-DX265_DEPTH=10"])]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")

@@ -391,9 +391,10 @@ struct SaoFrame
     void* dst[3];
     int64_t stride, cstride;
     const x265amd_sao_param* params;
-    int w, h, ctu_log2, wc, nctu, luma_on, chroma_on, i400;
+    int w, h, ctu_log2, wc, nctu;
     int c0, nctu_all;                        // first CTU of the band, CTUs of the picture (params stride)
-    int hs, vs;                              // chroma shifts
+    uint8_t luma_on, chroma_on, i400;
+    uint8_t hs, vs;                          // chroma shifts
     uint32_t block0;                         // first block (one per plane and CTU)
 };
 struct SaoLaunch

@@ -16,7 +16,9 @@ bands).  Census jobs of a frame read its references (L0 and L1) from the rank's 
 `check_reference_reach` verifies that no job reads a reference row beyond refLagRows.
 
 On one rank the whole sequence (steps + local reference copies) is ONE hipGraph; with several
-ranks each step is a graph replay followed by the step's exchange.
+ranks (or the native exchange) each step is a graph replay followed by the step's exchange:
+torch.distributed P2P batches, or one x265amd_exchange call (csrc/exchange.cpp, RCCL groups
+enqueued on the stream) with exchange="rccl".
 
 The reconstruction a real encoder writes (prediction + residual) is stood in for by the band's
 source pixels, copied into the recon buffer before the loop filters.
@@ -144,10 +146,16 @@ def check_reference_reach(slices_by_fb, fs: FrameSet, plan: BandPlan, ctu: int =
 
 class GpuFramePipeline:
     def __init__(self, prims, width, height, depth, frames_local, world, rank, census=None, band_rows=None,
-                 segment_frames=None, streams=8, device="cuda", seed=11, early_independent=True):
+                 segment_frames=None, streams=8, device="cuda", seed=11, early_independent=True, exchange="torch",
+                 inplace_store=True):
+        """exchange: "torch" (torch.distributed P2P batches; local copies on the stream) or "rccl" (the
+        native communicator, x265amd_exchange; with inplace_store=False a rank's own reference pictures
+        are finished in their own buffers and reach its store as loop-back transfers — the one-GPU check
+        of the native path)"""
         import torch
 
         self.early_independent = early_independent
+        self.exchange_kind, self.inplace_store = exchange, inplace_store
         self.prims, self.world, self.rank, self.depth = prims, world, rank, depth
         self.F = frames_local
         self.total = frames_local * world
@@ -201,7 +209,15 @@ class GpuFramePipeline:
         def planes_of(kind, j):
             return self.final_planes(self.kof[j]) if kind == "final" else frame_planes(src_planes, self.sof[j])
 
-        self.ex = RefExchange(s, rank, planes_of, regions)
+        if exchange == "rccl":
+            from .pipeline import Comm, RcclExchange
+
+            self.comm = Comm(world, rank)
+            self.ex = RcclExchange(s, rank, planes_of, regions, self.comm, loopback=not inplace_store)
+        elif exchange == "torch":
+            self.ex = RefExchange(s, rank, planes_of, regions)
+        else:
+            raise ValueError(f"exchange {exchange!r}")
         self._f4_setup(width, height, device)
         self.streams = [torch.cuda.Stream() for _ in range(max(1, streams))] if streams > 1 else []
         self.graphs = {}
@@ -210,7 +226,7 @@ class GpuFramePipeline:
         """where local frame k's final reconstruction lives: its store slot for a reference picture,
         else the frame's own final buffer"""
         j = self.local[k]
-        if final is None and j in self.sof:
+        if final is None and self.inplace_store and j in self.sof:
             return self.frame_planes(self.src_planes, self.sof[j])
         return self.frame_planes(self.final if final is None else final, k)
 
@@ -305,10 +321,10 @@ class GpuFramePipeline:
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):                        # warm-up pass (allocations, descriptor uploads)
-            self._run_all(exchange=self.world == 1)
+            self._run_all(exchange=self.world == 1 and self.exchange_kind == "torch")
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
-        if self.world == 1:
+        if self.world == 1 and self.exchange_kind == "torch":
             g = torch.cuda.CUDAGraph()
             with capture_graph(g):
                 self._run_all(exchange=True)                 # exchange = local copies: capturable

@@ -223,6 +223,95 @@ class RefExchange:
             w.wait()
 
 
+class _Transfer(ctypes.Structure):
+    _fields_ = [("buf", ctypes.c_void_p), ("bytes", ctypes.c_size_t), ("peer", ctypes.c_int), ("send", ctypes.c_int)]
+
+
+class Comm:
+    """A native RCCL communicator (x265amd_comm_*, csrc/exchange.cpp) on the current HIP device.  Rank 0
+    makes the 128-byte id; with world > 1 it reaches the other ranks over the torch.distributed group
+    (any channel would do: the id is plain bytes)."""
+
+    def __init__(self, world: int, rank: int):
+        self.lib = lib = _lib()
+        lib.x265amd_comm_create.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_char_p, ctypes.c_int,
+                                            ctypes.c_int]
+        lib.x265amd_comm_destroy.argtypes = [ctypes.c_void_p]
+        lib.x265amd_exchange.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
+        uid = ctypes.create_string_buffer(128)
+        if rank == 0:
+            rc = lib.x265amd_comm_unique_id(uid)
+            if rc:
+                raise RuntimeError(f"x265amd_comm_unique_id: status {rc} (librccl not loadable?)")
+        if world > 1:
+            import torch.distributed as dist
+
+            obj = [uid.raw if rank == 0 else None]
+            dist.broadcast_object_list(obj, src=0)
+            uid = ctypes.create_string_buffer(obj[0], 128)
+        self.handle = ctypes.c_void_p()
+        rc = lib.x265amd_comm_create(ctypes.byref(self.handle), uid, world, rank)
+        if rc:
+            raise RuntimeError(f"x265amd_comm_create: status {rc}")
+        self.world, self.rank = world, rank
+
+    def exchange(self, xfers, stream):
+        """xfers: a ctypes array of _Transfer; stream: a HIP stream handle (int)"""
+        rc = self.lib.x265amd_exchange(self.handle, ctypes.cast(xfers, ctypes.c_void_p), len(xfers),
+                                       ctypes.c_void_p(stream))
+        if rc:
+            raise RuntimeError(f"x265amd_exchange: status {rc}")
+
+    def close(self):
+        if self.handle:
+            self.lib.x265amd_comm_destroy(self.handle)
+            self.handle = ctypes.c_void_p()
+
+
+class RcclExchange(RefExchange):
+    """RefExchange through the native communicator: every step's sends and receives (and, with
+    loopback, the rank's local band copies as send / receive pairs to itself) are one
+    x265amd_exchange call enqueued on the current stream.  The transfer tables are built once: the
+    frame buffers never move."""
+
+    def __init__(self, sched: Schedule, rank: int, planes_of, regions, comm: Comm, loopback: bool = False):
+        super().__init__(sched, rank, planes_of, regions)
+        self.comm, self.loop_local = comm, loopback
+        self.tables = []
+        for st in range(sched.nsteps):
+            rows = []
+            for j, c, src, dst in self.plans[st]:
+                if src == dst == self.rank:
+                    if not loopback:
+                        continue
+                    pairs = list(zip(self._band("final", j, c), self._band("store", j, c)))
+                    if all(s_.data_ptr() == d_.data_ptr() for s_, d_ in pairs):
+                        continue
+                    for s_, d_ in pairs:
+                        rows += [(s_, self.rank, 1), (d_, self.rank, 0)]
+                elif src == self.rank:
+                    rows += [(t, dst, 1) for t in self._band("final", j, c)]
+                else:
+                    rows += [(t, src, 0) for t in self._band("store", j, c)]
+            tab = (_Transfer * len(rows))()
+            for i, (t, peer, send) in enumerate(rows):
+                tab[i] = _Transfer(t.data_ptr(), t.numel() * t.element_size(), peer, send)
+            self.tables.append(tab)
+
+    def exchange(self, step: int):
+        import torch
+
+        if not self.loop_local:
+            for j, c, src, dst in self.plans[step]:
+                if src == dst == self.rank:
+                    for s_, d_ in zip(self._band("final", j, c), self._band("store", j, c)):
+                        if s_.data_ptr() != d_.data_ptr():
+                            d_.copy_(s_)
+        if len(self.tables[step]):
+            stream = torch.cuda.current_stream().cuda_stream if torch.cuda.is_available() else 0
+            self.comm.exchange(self.tables[step], stream)
+
+
 def run_steps(sched: Schedule, rank: int, ex: RefExchange, encode, deblock, finish, steps=None):
     """This rank's share of the schedule, step by step: each (frame, band) of the step is encoded and
     deblocked (encode order), then the bands that became final are SAO-filtered / border-extended

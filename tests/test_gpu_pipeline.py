@@ -16,15 +16,45 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("band_rows,frames", [(1, 8), (2, 6), (None, 11)])
-def test_gpu_pipeline_gop_equals_whole_frame_chain(gpu_prims, oracle_libs, band_rows, frames):
+def test_gpu_native_exchange_loopback():
+    """x265amd_exchange (csrc/exchange.cpp) on one GPU: a group of send / receive pairs to the own rank
+    moves every byte, in the group's order, on the given stream"""
+    import torch
+
+    from src.x265_amd.pipeline import Comm, _Transfer
+
+    comm = Comm(1, 0)
+    try:
+        g = torch.Generator(device="cuda").manual_seed(3)
+        src = [torch.randint(0, 256, (n,), dtype=torch.uint8, device="cuda", generator=g) for n in (1, 4097, 1 << 20)]
+        dst = [torch.zeros_like(t) for t in src]
+        tab = (_Transfer * 6)()
+        for i, (a, b) in enumerate(zip(src, dst)):
+            tab[2 * i] = _Transfer(a.data_ptr(), a.numel(), 0, 1)
+            tab[2 * i + 1] = _Transfer(b.data_ptr(), b.numel(), 0, 0)
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        comm.exchange(tab, s.cuda_stream)
+        s.synchronize()
+        for a, b in zip(src, dst):
+            assert torch.equal(a, b)
+    finally:
+        comm.close()
+
+
+@pytest.mark.parametrize("band_rows,frames,exchange", [(1, 8, "torch"), (2, 6, "torch"), (None, 11, "torch"),
+                                                       (2, 8, "rccl")])
+def test_gpu_pipeline_gop_equals_whole_frame_chain(gpu_prims, oracle_libs, band_rows, frames, exchange):
+    """exchange "rccl": the rank's own reference pictures are finished in their own buffers and reach the
+    store through the native communicator (loop-back transfers, x265amd_exchange)"""
     import torch
 
     from pyoracle import CpuOracle
     from src.x265_amd.frame_pipeline import GpuFramePipeline
 
     W, H = 416, 240
-    pipe = GpuFramePipeline(gpu_prims, W, H, 8, frames, 1, 0, band_rows=band_rows, streams=4, device="cuda")
+    pipe = GpuFramePipeline(gpu_prims, W, H, 8, frames, 1, 0, band_rows=band_rows, streams=4, device="cuda",
+                            exchange=exchange, inplace_store=exchange == "torch")
     pipe.build(graphs=True)
     pipe.reset_stores()                  # the build's warm-up pass already filled them
     pipe.step()
@@ -71,3 +101,6 @@ def test_gpu_pipeline_gop_equals_whole_frame_chain(gpu_prims, oracle_libs, band_
         if m:
             bad.append((b.name, m))
     assert not bad, bad[:5]
+    if exchange == "rccl":
+        assert sum(len(t) for t in pipe.ex.tables) > 0
+        pipe.comm.close()

@@ -246,3 +246,79 @@ def test_frame_parallel_exchange_gloo(world, band_rows, total, segment):
             for p in range(3):
                 np.testing.assert_array_equal(planes[p], finals[r][p], err_msg=f"store copy of frame {r} plane {p}")
                 assert planes[p].min() >= 0
+
+
+class _LockstepComm:
+    """CPU stand-in of the native communicator (x265amd_exchange): records each rank's transfer table
+    of the step; `deliver` then matches them the way RCCL's point-to-point does (per ordered pair of
+    ranks, the k-th send to a peer with the peer's k-th receive from this rank, equal sizes)"""
+
+    def __init__(self):
+        self.pending = {}
+
+    def bind(self, rank):
+        comm = self
+
+        class _R:
+            def exchange(self, tab, stream):
+                comm.pending[rank] = list(tab)
+        return _R()
+
+    def deliver(self):
+        import ctypes
+
+        sends, recvs = {}, {}
+        for rank, tab in self.pending.items():
+            for t in tab:
+                (sends if t.send else recvs).setdefault((rank, t.peer) if t.send else (t.peer, rank), []).append(t)
+        assert sends.keys() == recvs.keys()
+        n = 0
+        for key in sends:
+            assert [t.bytes for t in sends[key]] == [t.bytes for t in recvs[key]], f"unmatched transfers {key}"
+            for s_, r_ in zip(sends[key], recvs[key]):
+                ctypes.memmove(r_.buf, s_.buf, s_.bytes)
+                n += 1
+        self.pending.clear()
+        return n
+
+
+@pytest.mark.parametrize("world,band_rows,total,segment", [(2, 1, 11, 11), (4, 2, 16, 8)])
+def test_native_exchange_tables_match_pairwise(world, band_rows, total, segment):
+    """the native exchange path (RcclExchange -> x265amd_exchange): every rank's per-step transfer table,
+    delivered with RCCL's pairing rule, reproduces the one-rank pictures and the producer-identical stores"""
+    from src.x265_amd.pipeline import RcclExchange
+
+    ref_finals, _ = _run(1, band_rows, total, segment)
+    lock = _LockstepComm()
+    ranks = [StandIn(world, r, band_rows, total, segment) for r in range(world)]
+    for r, st in enumerate(ranks):
+        st.ex = RcclExchange(st.s, r, st.ex.planes_of, st.ex.regions, lock.bind(r))
+    moved = 0
+    for step in range(ranks[0].s.nsteps):
+        for r, st in enumerate(ranks):
+            run_steps(st.s, r, st.ex, st.encode, st.deblock, st.finish, steps=[step])
+        moved += lock.deliver()
+    assert moved > 0
+    for st in ranks:
+        for j in st.frames:
+            for p in range(3):
+                np.testing.assert_array_equal(st.final[j][p].numpy(), ref_finals[j][p], err_msg=f"frame {j} plane {p}")
+        for r, planes in st.store.items():
+            owner = ranks[st.s.rank[r]]
+            for p in range(3):
+                np.testing.assert_array_equal(planes[p].numpy(), owner.final[r][p].numpy(), err_msg=f"store {r}")
+
+
+def test_native_exchange_argument_checks():
+    """x265amd_exchange / x265amd_comm_create reject bad arguments before touching RCCL or a device"""
+    import ctypes
+
+    from src.x265_amd.pipeline import _lib
+
+    lib = _lib()
+    assert lib.x265amd_exchange(None, None, 0, None) == 1000
+    h = ctypes.c_void_p()
+    uid = ctypes.create_string_buffer(128)
+    assert lib.x265amd_comm_create(ctypes.byref(h), uid, 0, 0) == 1000
+    assert lib.x265amd_comm_create(ctypes.byref(h), uid, 2, 2) == 1000
+    assert lib.x265amd_comm_destroy(None) == 0
