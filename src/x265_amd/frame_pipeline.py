@@ -93,6 +93,21 @@ def reads_store(b, fs: FrameSet) -> np.ndarray:
     return out
 
 
+def store_slots(b, fs: FrameSet) -> np.ndarray:
+    """per job of batch b and per read entry: the reference-store slot it reads (-1: not the store);
+    shape (n, entries)"""
+    cols = []
+    for key, plane_key in (("aoff", "a"), ("boff", "b"), ("roff", "r"), ("soff", "s"), ("foff", "f")):
+        t, pl = b.dev.get(key), b.dev.get(plane_key)
+        if t is None or pl is None or not (pl is fs.luma or pl is fs.cb or pl is fs.cr):
+            continue
+        psize = fs.plane_size if pl is fs.luma else fs.cplane_size
+        slot = t.cpu().numpy().astype(np.int64) // psize
+        slot = slot.reshape(b.n, -1)
+        cols.append(np.where(slot >= fs.F, slot, -1))
+    return np.concatenate(cols, axis=1) if cols else np.full((b.n, 1), -1, np.int64)
+
+
 def keyed_slices(batches, fs: FrameSet, key_of, nkeys: int, ctu: int, plan: BandPlan):
     """{key: [batch slices]}: every job of every batch in exactly one slice; key_of(batch, frame, band)
     (numpy arrays per job) gives the job's key"""
@@ -147,15 +162,18 @@ def check_reference_reach(slices_by_fb, fs: FrameSet, plan: BandPlan, ctu: int =
 class GpuFramePipeline:
     def __init__(self, prims, width, height, depth, frames_local, world, rank, census=None, band_rows=None,
                  segment_frames=None, streams=8, device="cuda", seed=11, early_independent=True, exchange="torch",
-                 inplace_store=True):
+                 inplace_store=True, job_wait="band"):
         """exchange: "torch" (torch.distributed P2P batches; local copies on the stream) or "rccl" (the
         native communicator, x265amd_exchange; with inplace_store=False a rank's own reference pictures
         are finished in their own buffers and reach its store as loop-back transfers — the one-GPU check
-        of the native path)"""
+        of the native path).
+        job_wait: "band" — a job that reads a reference waits for its band's step (x265: a CTU row waits
+        until every reference has published its rows, frameencoder.cpp:516-531); "reference" — it waits
+        only for the band of the ONE reference picture it reads (the data it actually depends on)"""
         import torch
 
         self.early_independent = early_independent
-        self.exchange_kind, self.inplace_store = exchange, inplace_store
+        self.exchange_kind, self.inplace_store, self.job_wait = exchange, inplace_store, job_wait
         self.prims, self.world, self.rank, self.depth = prims, world, rank, depth
         self.F = frames_local
         self.total = frames_local * world
@@ -305,7 +323,18 @@ class GpuFramePipeline:
         # on reference rows and on nothing else (frameencoder.cpp:516-531); the census jobs that read no
         # reference (transforms, quant, intra, residual and current-picture block ops, an I picture's
         # jobs) carry no cross-frame dependency and go out with the first step
-        if self.early_independent:
+        if self.job_wait == "reference":
+            # the step after the reference band the job reads was published (for band b: the band holding
+            # row r1 - 2 + lag of that reference, BandPlan.need)
+            need = np.array([self.plan.need(b) for b in range(nb)], np.int64)
+            pub = np.array([[s.pub_step(r, c) for c in range(nb)] for r in self.store], np.int64)
+            F = self.fs.F
+
+            def key_of(bt, f, b):
+                slots = store_slots(bt, self.fs)
+                k = np.where(slots >= 0, pub[np.clip(slots - F, 0, None), need[b][:, None]] + 1, 0).max(axis=1)
+                return np.minimum(k, step_of[f, b])
+        elif self.early_independent:
             key_of = lambda bt, f, b: np.where(reads_store(bt, self.fs), step_of[f, b], 0)
         else:
             key_of = lambda bt, f, b: step_of[f, b]

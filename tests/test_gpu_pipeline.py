@@ -42,11 +42,14 @@ def test_gpu_native_exchange_loopback():
         comm.close()
 
 
-@pytest.mark.parametrize("band_rows,frames,exchange", [(1, 8, "torch"), (2, 6, "torch"), (None, 11, "torch"),
-                                                       (2, 8, "rccl")])
-def test_gpu_pipeline_gop_equals_whole_frame_chain(gpu_prims, oracle_libs, band_rows, frames, exchange):
+@pytest.mark.parametrize("band_rows,frames,exchange,job_wait", [(1, 8, "torch", "band"), (2, 6, "torch", "band"),
+                                                                (None, 11, "torch", "band"), (2, 8, "rccl", "band"),
+                                                                (None, 11, "torch", "reference"),
+                                                                (2, 8, "torch", "reference")])
+def test_gpu_pipeline_gop_equals_whole_frame_chain(gpu_prims, oracle_libs, band_rows, frames, exchange, job_wait):
     """exchange "rccl": the rank's own reference pictures are finished in their own buffers and reach the
-    store through the native communicator (loop-back transfers, x265amd_exchange)"""
+    store through the native communicator (loop-back transfers, x265amd_exchange); job_wait "reference":
+    a job waits only for the reference picture it reads"""
     import torch
 
     from pyoracle import CpuOracle
@@ -54,7 +57,7 @@ def test_gpu_pipeline_gop_equals_whole_frame_chain(gpu_prims, oracle_libs, band_
 
     W, H = 416, 240
     pipe = GpuFramePipeline(gpu_prims, W, H, 8, frames, 1, 0, band_rows=band_rows, streams=4, device="cuda",
-                            exchange=exchange, inplace_store=exchange == "torch")
+                            exchange=exchange, inplace_store=exchange == "torch", job_wait=job_wait)
     pipe.build(graphs=True)
     pipe.reset_stores()                  # the build's warm-up pass already filled them
     pipe.step()
