@@ -21,6 +21,7 @@
 // x265_encoder_encode() < 0.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <atomic>
@@ -59,6 +60,7 @@ int record(int st)
 struct x265amd_la_thread
 {
     hipStream_t st = nullptr;
+    hipEvent_t ev = nullptr;    // blocking-sync event (X265AMD_LA_SYNC=block): the waiting thread sleeps
     uint8_t* dev = nullptr;     // scratch: outputs / inputs of one estimate
     uint8_t* host = nullptr;    // pinned staging of the same size
     int wslot = -1;             // arena slot for this thread's weighted reference planes
@@ -115,6 +117,18 @@ struct Layout
     }
 };
 
+// wait for the calling thread's stream: spin (hipStreamSynchronize) or, with X265AMD_LA_SYNC=block, sleep
+// on a blocking-sync event so the encoder's worker threads get the core while the device works
+int wait(x265amd_la_thread* t)
+{
+    if (t->ev)
+    {
+        const hipError_t e = hipEventRecord(t->ev, t->st);
+        return e != hipSuccess ? (int)e : (int)hipEventSynchronize(t->ev);
+    }
+    return (int)hipStreamSynchronize(t->st);
+}
+
 // grow the calling thread's scratch to hold `bytes`
 int reserve(x265amd_la_thread* t, size_t bytes)
 {
@@ -152,6 +166,10 @@ int thread_ctx(x265amd_la* la, x265amd_la_thread** out)
         la->threads.push_back(t);
     }
     if (hipStreamCreateWithFlags(&t->st, hipStreamNonBlocking) != hipSuccess || reserve(t, la->scratch))
+        return X265AMD_ENOMEM;
+    const char* sync = getenv("X265AMD_LA_SYNC");
+    if (sync && !strcmp(sync, "block") &&
+        hipEventCreateWithFlags(&t->ev, hipEventBlockingSync | hipEventDisableTiming) != hipSuccess)
         return X265AMD_ENOMEM;
     tls.push_back({ la, t });
     *out = t;
@@ -215,6 +233,7 @@ extern "C" void x265amd_la_destroy(x265amd_la* la)
         (void)hipFree(t->dev);
         (void)hipHostFree(t->host);
         if (t->st) (void)hipStreamDestroy(t->st);
+        if (t->ev) (void)hipEventDestroy(t->ev);
         delete t;
     }
     for (auto& f : la->frames)
@@ -261,7 +280,7 @@ extern "C" int x265amd_la_load(x265amd_la* la, const void* key, int gen, const v
     if (inv_qscale)
         LA_TRY(hipMemcpyAsync(la->invq + (size_t)slot * la->ncu, inv_qscale, sizeof(int32_t) * la->ncu,
                               hipMemcpyHostToDevice, t->st));
-    return record((int)hipStreamSynchronize(t->st));
+    return record(wait(t));
 }
 
 extern "C" int x265amd_la_intra(x265amd_la* la, const void* key, int32_t* intra_cost, uint8_t* intra_mode,
@@ -296,7 +315,7 @@ extern "C" int x265amd_la_intra(x265amd_la* la, const void* key, int32_t* intra_
     LA_TRY(hipMemcpyAsync(t->host + L.mvs0, t->dev + L.mvs0, ncu, hipMemcpyDeviceToHost, t->st));
     LA_TRY(hipMemcpyAsync(t->host + L.lc, t->dev + L.lc, L.rs - L.lc + 4 * (size_t)hcu, hipMemcpyDeviceToHost, t->st));
     LA_TRY(hipMemcpyAsync(t->host + L.ce, t->dev + L.ce, 16, hipMemcpyDeviceToHost, t->st));
-    LA_TRY(hipStreamSynchronize(t->st));
+    LA_TRY(wait(t));
     memcpy(intra_cost, t->host + L.mvc0, 4 * (size_t)ncu);
     memcpy(intra_mode, t->host + L.mvs0, ncu);
     memcpy(lowres_cost, t->host + L.lc, 2 * (size_t)ncu);
@@ -359,7 +378,7 @@ extern "C" int x265amd_la_pcost_n(x265amd_la* la, int n, x265amd_la_pjob* jobs, 
     LA_TRY(x265amd_lowres_pcost(la->cfg.depth, &b, t->st));
     LA_TRY(hipMemcpyAsync(t->host + L.mvs0, t->dev + L.mvs0, L.mvs1 - L.mvs0, hipMemcpyDeviceToHost, t->st));
     LA_TRY(hipMemcpyAsync(t->host + L.lc, t->dev + L.lc, L.offs - L.lc, hipMemcpyDeviceToHost, t->st));
-    LA_TRY(hipStreamSynchronize(t->st));
+    LA_TRY(wait(t));
     for (int e = 0; e < n; e++)
     {
         x265amd_la_pjob& j = jobs[e];
@@ -441,7 +460,7 @@ extern "C" int x265amd_la_bcost_n(x265amd_la* la, int n, x265amd_la_bjob* jobs, 
                                   (uint16_t*)(t->dev + L.lc), (int32_t*)(t->dev + L.rs), (int64_t*)(t->dev + L.ce) };
     LA_TRY(x265amd_lowres_bcost(la->cfg.depth, &b, t->st));
     LA_TRY(hipMemcpyAsync(t->host + L.mvs0, t->dev + L.mvs0, L.offs - L.mvs0, hipMemcpyDeviceToHost, t->st));
-    LA_TRY(hipStreamSynchronize(t->st));
+    LA_TRY(wait(t));
     for (int e = 0; e < n; e++)
     {
         x265amd_la_bjob& j = jobs[e];
