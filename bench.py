@@ -377,16 +377,18 @@ def census_replay_cpu(args, census):
 def pipeline_rates(prims, args, census, local):
     """The frame-parallel step (--mode pipeline) on this one GPU: one closed GOP of F pictures (F = the
     pipeline default of 32 frames), steps of x265amd_schedule, reference bands copied (in place) into the
-    reference store; whole-picture bands and 4-CTU-row bands."""
+    reference store; whole-picture bands and 4-CTU-row bands, and the 32 pictures as four closed GOPs of 8
+    (independent segments run side by side in the same steps)."""
     import torch
 
     from src.x265_amd.frame_pipeline import GpuFramePipeline
 
     F = 32
     out = {"frames_per_step": F}
-    for br in (0, 4):
+    for br, seg in ((0, 0), (4, 0), (0, 8)):
         pipe = GpuFramePipeline(prims, args.width, args.height, args.depth, F, 1, 0, census=census,
-                                band_rows=br or None, streams=args.streams, device=f"cuda:{local}")
+                                band_rows=br or None, segment_frames=seg or None, streams=args.streams,
+                                device=f"cuda:{local}")
         pipe.build(graphs=True)
         for _ in range(2):
             pipe.step()
@@ -397,7 +399,7 @@ def pipeline_rates(prims, args, census, local):
             pipe.step()
         torch.cuda.synchronize()
         dt = (time.perf_counter() - t0) / n
-        out[f"band_rows_{br or pipe.plan.band_rows}"] = {
+        out[f"band_rows_{br or pipe.plan.band_rows}" + (f"_segments_of_{seg}" if seg else "")] = {
             "fps": round(F / dt, 1), "ms_per_step": round(dt * 1e3, 3), "bands_per_frame": pipe.plan.nbands,
             "schedule_steps": pipe.sched.nsteps, "launches_per_step": pipe.launches_per_step}
         del pipe

@@ -162,18 +162,22 @@ def check_reference_reach(slices_by_fb, fs: FrameSet, plan: BandPlan, ctu: int =
 class GpuFramePipeline:
     def __init__(self, prims, width, height, depth, frames_local, world, rank, census=None, band_rows=None,
                  segment_frames=None, streams=8, device="cuda", seed=11, early_independent=True, exchange="torch",
-                 inplace_store=True, job_wait="band"):
+                 inplace_store=True, job_wait="band", background=True):
         """exchange: "torch" (torch.distributed P2P batches; local copies on the stream) or "rccl" (the
         native communicator, x265amd_exchange; with inplace_store=False a rank's own reference pictures
         are finished in their own buffers and reach its store as loop-back transfers — the one-GPU check
         of the native path).
         job_wait: "band" — a job that reads a reference waits for its band's step (x265: a CTU row waits
         until every reference has published its rows, frameencoder.cpp:516-531); "reference" — it waits
-        only for the band of the ONE reference picture it reads (the data it actually depends on)"""
+        only for the band of the ONE reference picture it reads (the data it actually depends on).
+        background (one rank, whole sequence in one graph): the jobs that read no reference run on
+        background streams from the start, in step order, and a step's loop filters wait only for the
+        background work of THAT step's pictures — instead of all reference-free work joining step 0"""
         import torch
 
         self.early_independent = early_independent
         self.exchange_kind, self.inplace_store, self.job_wait = exchange, inplace_store, job_wait
+        self.background = background
         self.prims, self.world, self.rank, self.depth = prims, world, rank, depth
         self.F = frames_local
         self.total = frames_local * world
@@ -238,6 +242,8 @@ class GpuFramePipeline:
             raise ValueError(f"exchange {exchange!r}")
         self._f4_setup(width, height, device)
         self.streams = [torch.cuda.Stream() for _ in range(max(1, streams))] if streams > 1 else []
+        self.bg_streams = []
+        self._bgroups, self._bg_events, self.bg = {}, {}, False
         self.graphs = {}
 
     def final_planes(self, k, final=None):
@@ -323,7 +329,17 @@ class GpuFramePipeline:
         # on reference rows and on nothing else (frameencoder.cpp:516-531); the census jobs that read no
         # reference (transforms, quant, intra, residual and current-picture block ops, an I picture's
         # jobs) carry no cross-frame dependency and go out with the first step
-        if self.job_wait == "reference":
+        one_graph = self.world == 1 and self.exchange_kind == "torch"
+        self.bg = self.background and one_graph and self.job_wait == "band" and graphs
+        if self.bg:
+            # reference-reading jobs keyed by their band's step (the step lanes), the others by
+            # nsteps + their band's step (the background streams)
+            key_of = lambda bt, f, b: np.where(reads_store(bt, self.fs), step_of[f, b], s.nsteps + step_of[f, b])
+            sl = keyed_slices(self.batches, self.fs, key_of, 2 * s.nsteps, 64, self.plan)
+            self.step_slices = {k: v for k, v in sl.items() if k < s.nsteps}
+            self._bgroups = {k - s.nsteps: group_launches(v) for k, v in sl.items() if k >= s.nsteps}
+            self.bg_streams = [torch.cuda.Stream() for _ in range(max(1, len(self.streams) // 2))]
+        elif self.job_wait == "reference":
             # the step after the reference band the job reads was published (for band b: the band holding
             # row r1 - 2 + lag of that reference, BandPlan.need)
             need = np.array([self.plan.need(b) for b in range(nb)], np.int64)
@@ -338,9 +354,10 @@ class GpuFramePipeline:
             key_of = lambda bt, f, b: np.where(reads_store(bt, self.fs), step_of[f, b], 0)
         else:
             key_of = lambda bt, f, b: step_of[f, b]
-        self.step_slices = keyed_slices(self.batches, self.fs, key_of, s.nsteps, 64, self.plan)
+        if not self.bg:
+            self.step_slices = keyed_slices(self.batches, self.fs, key_of, s.nsteps, 64, self.plan)
         self._sgroups = {st: group_launches(bs) for st, bs in self.step_slices.items()}
-        for gs in self._sgroups.values():
+        for gs in list(self._sgroups.values()) + list(self._bgroups.values()):
             for g in gs:
                 g.run(self.prims)       # build grouped descriptor tables outside any capture
         torch.cuda.synchronize()
@@ -367,10 +384,35 @@ class GpuFramePipeline:
         torch.cuda.synchronize()
 
     def _run_all(self, exchange):
+        import torch
+
+        cur = torch.cuda.current_stream()
+        self._bg_events = {}
+        if self.bg:
+            # every step's background work, in step order, spread over the background streams (balanced by
+            # bytes); one event per (step, stream) for the step's loop filters to wait on
+            load = [0.0] * len(self.bg_streams)
+            for s_ in self.bg_streams:
+                s_.wait_stream(cur)
+            for st in range(self.sched.nsteps):
+                used = set()
+                for g in self._bgroups.get(st, []):
+                    i = min(range(len(self.bg_streams)), key=lambda j: load[j])
+                    g.run(self.prims, ctypes.c_void_p(self.bg_streams[i].cuda_stream))
+                    load[i] += g.bytes
+                    used.add(i)
+                evs = []
+                for i in sorted(used):
+                    ev = torch.cuda.Event()
+                    ev.record(self.bg_streams[i])
+                    evs.append(ev)
+                self._bg_events[st] = evs
         for st in range(self.sched.nsteps):
             self._step_work(st)
             if exchange:
                 self.ex.exchange(st)
+        for s_ in self.bg_streams:
+            cur.wait_stream(s_)
 
     def _step_work(self, st):
         """launch the whole work of step st on the current stream (graph-capturable)"""
@@ -400,6 +442,8 @@ class GpuFramePipeline:
         else:
             for g in groups:
                 g.run(self.prims)
+        for ev in self._bg_events.get(st, []) if self.bg else []:
+            cur.wait_event(ev)
         if st == 0:
             # the reconstruction of every band (stand-in: the source pixels), written before any band is
             # deblocked: one copy per plane for all local frames
@@ -454,7 +498,7 @@ class GpuFramePipeline:
         s = self.sched
         filt = sum((1 if s.items(self.rank, st) else 0) + 2 * (1 if s.finals(self.rank, st) else 0)
                    for st in range(s.nsteps))
-        return sum(len(v) for v in self._sgroups.values()) + filt
+        return sum(len(v) for v in self._sgroups.values()) + sum(len(v) for v in self._bgroups.values()) + filt
 
     @property
     def calls(self):
