@@ -115,12 +115,17 @@ class FrameSet:
         """stored index of the reference a job of stored frame f reads: the previous frame (or the
         reference slot for frame 0); with reference stores, entry sel mod n of f's reference list"""
         if self.ref_slots is not None:
-            fa = np.atleast_1d(np.asarray(f))
-            sa = np.zeros_like(fa) if sel is None else np.broadcast_to(np.asarray(sel), fa.shape)
-            out = np.empty(fa.shape, np.int64)
-            for i, (ff, ss) in enumerate(zip(fa.tolist(), sa.tolist())):
-                rs = self.ref_slots[ff]
-                out[i] = rs[ss % len(rs)] if rs else ff
+            if getattr(self, "_ref_tab", None) is None:
+                # [frame, k] = k-th reference slot (an I frame: itself), and the list lengths
+                n = max(1, max(len(r) for r in self.ref_slots))
+                self._ref_tab = np.zeros((len(self.ref_slots), n), np.int64)
+                self._ref_len = np.array([len(r) for r in self.ref_slots], np.int64)
+                for i, rs in enumerate(self.ref_slots):
+                    self._ref_tab[i, :max(1, len(rs))] = rs if rs else i
+            fa = np.atleast_1d(np.asarray(f, np.int64))
+            sa = np.zeros_like(fa) if sel is None else np.broadcast_to(np.asarray(sel, np.int64), fa.shape)
+            ln = self._ref_len[fa]
+            out = np.where(ln > 0, self._ref_tab[fa, sa % np.maximum(ln, 1)], fa)
             return out if not np.isscalar(f) else int(out[0])
         return np.where(np.asarray(f) == 0, self.F, np.asarray(f) - 1) if not np.isscalar(f) else (self.F if f == 0 else f - 1)
 
