@@ -330,7 +330,7 @@ class GpuFramePipeline:
         # reference (transforms, quant, intra, residual and current-picture block ops, an I picture's
         # jobs) carry no cross-frame dependency and go out with the first step
         one_graph = self.world == 1 and self.exchange_kind == "torch"
-        self.bg = self.background and one_graph and self.job_wait == "band" and graphs
+        self.bg = self.background and self.job_wait == "band" and graphs
         if self.bg:
             # reference-reading jobs keyed by their band's step (the step lanes), the others by
             # nsteps + their band's step (the background streams)
@@ -375,12 +375,28 @@ class GpuFramePipeline:
             with capture_graph(g):
                 self._run_all(exchange=True)                 # exchange = local copies: capturable
             self.graphs["all"] = g
-        else:
+        elif not self.bg:
             for st in range(s.nsteps):
                 g = torch.cuda.CUDAGraph()
                 with capture_graph(g):
                     self._step_work(st)
                 self.graphs[st] = g
+        else:
+            # per step: the step's reference-reading work, its loop filters, and its background work as
+            # three graphs; step() replays the background graphs on their own stream and joins each into
+            # the main stream right before that step's filters
+            for st in range(s.nsteps):
+                for kind, fn, need in (("c", self._census_work, bool(self._sgroups.get(st))),
+                                       ("f", self._filter_work, st == 0 or bool(s.items(self.rank, st))
+                                        or bool(s.finals(self.rank, st))),
+                                       ("b", self._bg_graph_work, bool(self._bgroups.get(st)))):
+                    if need:
+                        g = torch.cuda.CUDAGraph()
+                        with capture_graph(g):
+                            fn(st)
+                        self.graphs[(kind, st)] = g
+            self._bg_main = torch.cuda.Stream()
+            self._bg_step_events = [torch.cuda.Event() for _ in range(s.nsteps)]
         torch.cuda.synchronize()
 
     def _run_all(self, exchange):
@@ -414,12 +430,38 @@ class GpuFramePipeline:
         for s_ in self.bg_streams:
             cur.wait_stream(s_)
 
+    def _bg_graph_work(self, st):
+        """step st's background work forked over the background streams and joined back into the current
+        stream (the body of one background graph)"""
+        import torch
+
+        cur = torch.cuda.current_stream()
+        load = [0.0] * len(self.bg_streams)
+        used = set()
+        for g in self._bgroups.get(st, []):
+            i = min(range(len(self.bg_streams)), key=lambda j: load[j])
+            if i not in used:
+                self.bg_streams[i].wait_stream(cur)
+                used.add(i)
+            g.run(self.prims, ctypes.c_void_p(self.bg_streams[i].cuda_stream))
+            load[i] += g.bytes
+        for i in used:
+            cur.wait_stream(self.bg_streams[i])
+
     def _step_work(self, st):
         """launch the whole work of step st on the current stream (graph-capturable)"""
         import torch
 
-        s, plan = self.sched, self.plan
-        items = s.items(self.rank, st)
+        self._census_work(st)
+        cur = torch.cuda.current_stream()
+        for ev in self._bg_events.get(st, []) if self.bg else []:
+            cur.wait_event(ev)
+        self._filter_work(st)
+
+    def _census_work(self, st):
+        """step st's census slices forked over the step lanes and joined into the current stream"""
+        import torch
+
         cur = torch.cuda.current_stream()
         groups = self._sgroups.get(st, [])
         if self.streams:
@@ -442,8 +484,15 @@ class GpuFramePipeline:
         else:
             for g in groups:
                 g.run(self.prims)
-        for ev in self._bg_events.get(st, []) if self.bg else []:
-            cur.wait_event(ev)
+
+    def _filter_work(self, st):
+        """step st's loop filters on the current stream: deblocking of the step's bands, SAO and border
+        extension of the bands that became final"""
+        import torch
+
+        s, plan = self.sched, self.plan
+        items = s.items(self.rank, st)
+        cur = torch.cuda.current_stream()
         if st == 0:
             # the reconstruction of every band (stand-in: the source pixels), written before any band is
             # deblocked: one copy per plane for all local frames
@@ -484,6 +533,27 @@ class GpuFramePipeline:
         """one sequence: this rank's frames in the schedule's steps, with the reference exchange"""
         if "all" in self.graphs:
             self.graphs["all"].replay()
+            return
+        if self.bg and self.graphs:
+            import torch
+
+            cur, bgs = torch.cuda.current_stream(), self._bg_main
+            bgs.wait_stream(cur)
+            with torch.cuda.stream(bgs):
+                for st in range(self.sched.nsteps):
+                    g = self.graphs.get(("b", st))
+                    if g is not None:
+                        g.replay()
+                    self._bg_step_events[st].record(bgs)
+            for st in range(self.sched.nsteps):
+                for kind in ("c", "f"):
+                    if kind == "f":
+                        cur.wait_event(self._bg_step_events[st])
+                    g = self.graphs.get((kind, st))
+                    if g is not None:
+                        g.replay()
+                self.ex.exchange(st)
+            cur.wait_stream(bgs)
             return
         for st in range(self.sched.nsteps):
             g = self.graphs.get(st)
