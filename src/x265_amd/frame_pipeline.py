@@ -162,7 +162,7 @@ def check_reference_reach(slices_by_fb, fs: FrameSet, plan: BandPlan, ctu: int =
 class GpuFramePipeline:
     def __init__(self, prims, width, height, depth, frames_local, world, rank, census=None, band_rows=None,
                  segment_frames=None, streams=8, device="cuda", seed=11, early_independent=True, exchange="torch",
-                 inplace_store=True, job_wait="band", background=True):
+                 inplace_store=True, job_wait="band", background=False):
         """exchange: "torch" (torch.distributed P2P batches; local copies on the stream) or "rccl" (the
         native communicator, x265amd_exchange; with inplace_store=False a rank's own reference pictures
         are finished in their own buffers and reach its store as loop-back transfers — the one-GPU check

@@ -30,7 +30,7 @@ def main():
     ap.add_argument("--segments", default="0", help="comma list of pictures per closed GOP segment (0: all frames)")
     ap.add_argument("--no-replay", action="store_true")
     ap.add_argument("--job-wait", default="band", help="comma list of band / reference")
-    ap.add_argument("--background", default="1", help="comma list of 1 / 0")
+    ap.add_argument("--background", default="0", help="comma list of 1 / 0")
     ap.add_argument("--exchange", default="torch",
                     help="comma list of torch / rccl (rccl at one rank: the multi-rank graph structure, per-step "
                          "graphs, with an empty native exchange)")
