@@ -42,14 +42,16 @@ def test_gpu_native_exchange_loopback():
         comm.close()
 
 
-@pytest.mark.parametrize("band_rows,frames,exchange,job_wait", [(1, 8, "torch", "band"), (2, 6, "torch", "band"),
-                                                                (None, 11, "torch", "band"), (2, 8, "rccl", "band"),
-                                                                (None, 11, "torch", "reference"),
-                                                                (2, 8, "torch", "reference")])
-def test_gpu_pipeline_gop_equals_whole_frame_chain(gpu_prims, oracle_libs, band_rows, frames, exchange, job_wait):
+@pytest.mark.parametrize("band_rows,frames,exchange,job_wait,background", [
+    (1, 8, "torch", "band", False), (2, 6, "torch", "band", False), (None, 11, "torch", "band", False),
+    (2, 8, "rccl", "band", False), (None, 11, "torch", "reference", False), (2, 8, "torch", "reference", False),
+    (None, 11, "torch", "band", True), (2, 8, "rccl", "band", True)])
+def test_gpu_pipeline_gop_equals_whole_frame_chain(gpu_prims, oracle_libs, band_rows, frames, exchange, job_wait,
+                                                   background):
     """exchange "rccl": the rank's own reference pictures are finished in their own buffers and reach the
     store through the native communicator (loop-back transfers, x265amd_exchange); job_wait "reference":
-    a job waits only for the reference picture it reads"""
+    a job waits only for the reference picture it reads; background: reference-free jobs on background
+    streams / graphs joined before each step's filters (one graph, or per-step graphs with "rccl")"""
     import torch
 
     from pyoracle import CpuOracle
@@ -57,7 +59,8 @@ def test_gpu_pipeline_gop_equals_whole_frame_chain(gpu_prims, oracle_libs, band_
 
     W, H = 416, 240
     pipe = GpuFramePipeline(gpu_prims, W, H, 8, frames, 1, 0, band_rows=band_rows, streams=4, device="cuda",
-                            exchange=exchange, inplace_store=exchange == "torch", job_wait=job_wait)
+                            exchange=exchange, inplace_store=exchange == "torch", job_wait=job_wait,
+                            background=background)
     pipe.build(graphs=True)
     pipe.reset_stores()                  # the build's warm-up pass already filled them
     pipe.step()
