@@ -64,9 +64,29 @@ def build(verbose: bool = True) -> str:
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
+    _build_hosts()
     if verbose:
         print(f"[x265amd] built {LIB}", file=sys.stderr)
     return LIB
+
+
+# C++ host programs over the C ABI (integration/): built next to their sources, linked to the library
+ROOT = os.path.dirname(os.path.dirname(HERE))
+HOSTS = [("frame_shard_host.cpp", "frame_shard_host")]
+
+
+def _build_hosts():
+    out_dir = os.path.join(ROOT, "integration", "_bin")
+    os.makedirs(out_dir, exist_ok=True)
+    for src, exe in HOSTS:
+        srcp, out = os.path.join(ROOT, "integration", src), os.path.join(out_dir, exe)
+        if _newer(out, [srcp, LIB] + _headers()):
+            continue
+        cmd = [HIPCC, "-O2", "-std=c++17", "-x", "hip", "--offload-arch=gfx950", srcp, "-o", out,
+               "-L" + HERE, "-lx265amd", "-Wl,-rpath,$ORIGIN/../../src/x265_amd"]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"hipcc failed for {src}:\n{r.stdout}\n{r.stderr}")
 
 
 if __name__ == "__main__":

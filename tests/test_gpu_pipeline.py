@@ -110,3 +110,22 @@ def test_gpu_pipeline_gop_equals_whole_frame_chain(gpu_prims, oracle_libs, band_
     if exchange == "rccl":
         assert sum(len(t) for t in pipe.ex.tables) > 0
         pipe.comm.close()
+
+
+@pytest.mark.parametrize("band_rows,frames,segment", [(1, 11, 11), (2, 16, 8)])
+def test_cpp_frame_shard_host_one_rank(tmp_path, band_rows, frames, segment):
+    """integration/frame_shard_host (C++ only: x265amd_schedule, the row-band loop filters and
+    x265amd_exchange loop-back transfers into the rank's reference stores): every picture equals the
+    whole-frame deblock -> SAO -> border chain and every store slot its producer's picture"""
+    import json
+    import os
+    import subprocess
+
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "integration", "_bin",
+                       "frame_shard_host")
+    assert os.path.exists(exe), "run __graft_entry__.build() first"
+    r = subprocess.run([exe, "416", "240", str(frames), str(band_rows), "1", "0", str(tmp_path / "id"), str(segment),
+                        "2"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["mismatches"] == 0 and out["transfers"] > 0 and out["stores"] >= 2, out

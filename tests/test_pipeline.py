@@ -322,3 +322,19 @@ def test_native_exchange_argument_checks():
     assert lib.x265amd_comm_create(ctypes.byref(h), uid, 0, 0) == 1000
     assert lib.x265amd_comm_create(ctypes.byref(h), uid, 2, 2) == 1000
     assert lib.x265amd_comm_destroy(None) == 0
+
+
+def test_cpp_frame_shard_host_built_and_needs_a_device(tmp_path):
+    """the C++ host of the frame-parallel shard is built by build() and, without a GPU, exits with
+    status 3 instead of running on anything else"""
+    import subprocess
+
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "integration", "_bin",
+                       "frame_shard_host")
+    if not os.path.exists(exe):
+        pytest.skip("not built (run __graft_entry__.build())")
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    r = subprocess.run([exe, "416", "240", "8", "1", "1", "0", str(tmp_path / "id")], capture_output=True, text=True,
+                       timeout=60)
+    assert r.returncode == 3 and "no device" in r.stderr
