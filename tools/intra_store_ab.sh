@@ -1,0 +1,11 @@
+# intra 16x16 / 32x32: 8-byte half-row stores (base build) vs 16-byte row pieces (current), twice each
+set -o pipefail
+mkdir -p gpurun_out
+for rep in 1 2; do
+for v in base cur; do
+  unset X265AMD_LIB
+  case $v in base) export X265AMD_LIB=$PWD/ablibs/libx265amd_base.so ;; esac
+  echo "== $v"
+  timeout -k 10 200 python3 -u tools/kernel_roofline.py --only intra_ang_16,intra_ang_32,intra_ang_8 2>/dev/null | grep "{" | cut -c1-160 || exit 1
+done
+done
