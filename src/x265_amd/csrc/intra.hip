@@ -702,6 +702,221 @@ staged:
     }
 }
 
+// 32x32: four lanes per (TU, mode) job, 16 jobs per wave, lane q producing rows q, q + 4, .. (a job's
+// four lanes write four consecutive rows: 128 contiguous bytes per pass).  The job's 4N+1 neighbours go
+// to LDS once (each lane loads a quarter), the four lanes build the job's reference pairs
+// D[j] = (R[j], R[j+1]) in the mode's frame (flip, projected left samples) together, and every angular
+// pixel is one ds_read_b32 + v_dot2.  Wave-private LDS (the wave's 16 jobs): wave-level ordering only,
+// no block barrier; the block-per-job kernel above keeps only 2 jobs per wave.
+template <typename P, int N>
+__global__ __launch_bounds__(X265AMD_BLOCK) void k_intra_quad(int n, int maxv,
+    P* __restrict__ dst, intptr_t ds, const int64_t* __restrict__ doff,
+    const P* __restrict__ nb, const int64_t* __restrict__ nboff,
+    const P* __restrict__ filt, const int64_t* __restrict__ filtoff,
+    const uint8_t* __restrict__ mode, const uint8_t* __restrict__ bfilter, int allangs)
+{
+    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+    constexpr int G = 4, JOBS = X265AMD_BLOCK / G;
+    constexpr int N2 = 2 * N, NS = 4 * N + 4, ND = 3 * N + 1;      // padded strides (u16 / dwords)
+    constexpr int LG2 = N == 32 ? 5 : 4;
+    __shared__ uint16_t S[JOBS][NS];                   // the neighbours as loaded
+    __shared__ uint32_t D[JOBS][ND];                   // reference pairs in the mode's frame
+    const int t = threadIdx.x, slot = t / G, q = t % G;
+    const int64_t job = (int64_t)xcd_block() * JOBS + slot;
+    const bool live = job < n;
+    const int64_t jj = live ? job : 0;
+
+    int m, bf;
+    const P* src;
+    P* out;
+    intptr_t os;
+    if (allangs)
+    {
+        const int64_t tu = jj / 33;
+        m = 2 + (int)(jj % 33);
+        bf = bfilter[tu];
+        src = (c_intra.filter_flags[m] & N) ? filt + filtoff[tu] : nb + nboff[tu];
+        out = dst + doff[tu] + (int64_t)(m - 2) * N * N;
+        os = N;
+    }
+    else
+    {
+        m = mode[jj];
+        bf = bfilter[jj];
+        src = nb + nboff[jj];
+        out = dst + doff[jj];
+        os = ds;
+    }
+    // neighbours: lane q loads pixels qN .. qN + N - 1 (lane G - 1 also pixel 4N)
+    {
+        int v[N];
+        load_row<P, 16>(src + q * N, *(int(*)[16])v);
+        load_row<P, 16>(src + q * N + 16, *(int(*)[16])(v + 16));
+#pragma unroll
+        for (int k = 0; k < N; k++) S[slot][q * N + k] = (uint16_t)v[k];
+        if (q == G - 1) S[slot][4 * N] = (uint16_t)src[4 * N];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const ModeInfo mi = decode_mode(m);
+    const bool fh = mi.hor && m >= 2;                  // the mode's frame is the flipped one
+    const uint16_t* sj = S[slot];
+    const int nproj = mi.angle < 0 ? -((N * mi.angle) >> 5) - 1 : 0;
+    // R[k], k = 0 .. 3N (R[N - 1] = top-left, R[N ..] = above in the mode's frame, below N - 1 the
+    // projected left samples of negative angles, intrapred.cpp:154-164)
+    auto Rv = [&](int k) -> uint32_t {
+        if (k >= N - 1)
+        {
+            const int e = k - N + 1;
+            if (e > N2) return 0;
+            return sj[flip_index(e, N2, fh)];
+        }
+        const int kk = N - 2 - k;                      // R[-2 - kk]
+        if (kk >= nproj) return 0;
+        const int i = (128 + (kk + 1) * mi.inv) >> 8;  // = L[i - 1] = s'[2N + i]
+        return sj[flip_index(N2 + i, N2, fh)];
+    };
+#pragma unroll
+    for (int i = 0; i < 3 * N / G; i++)
+    {
+        const int j = i * G + q;
+        D[slot][j] = Rv(j) | (Rv(j + 1) << 16);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (!live) return;
+    const uint32_t* Dj = D[slot];
+    const bool tr = fh && !allangs;
+    // unflipped neighbours for planar / DC: above[x] = s[1 + x], left[y] = s[2N + 1 + y]
+    if (m <= 1)
+    {
+        int above[N];
+#pragma unroll
+        for (int x = 0; x < N; x++) above[x] = sj[1 + x];
+        int dc = 0;
+        if (m == 1)
+        {
+            int sum = N;
+#pragma unroll
+            for (int i = 0; i < N; i++) sum += above[i] + sj[N2 + 1 + i];
+            dc = sum >> (LG2 + 1);
+        }
+        const int trr = sj[N + 1], bl = sj[N2 + 1 + N];
+#pragma unroll
+        for (int i = 0; i < N / G; i++)
+        {
+            const int r = i * G + q;
+            const int lr = sj[N2 + 1 + r];
+            int o[N];
+            if (m == 0)
+            {
+#pragma unroll
+                for (int x = 0; x < N; x++)
+                    o[x] = ((N - 1 - x) * lr + (N - 1 - r) * above[x] + (x + 1) * trr + (r + 1) * bl + N) >> (LG2 + 1);
+            }
+            else
+            {
+#pragma unroll
+                for (int x = 0; x < N; x++) o[x] = dc;
+                if (bf)
+                {
+                    if (r == 0)
+                    {
+                        o[0] = (above[0] + lr + 2 * dc + 2) >> 2;
+#pragma unroll
+                        for (int x = 1; x < N; x++) o[x] = (above[x] + 3 * dc + 2) >> 2;
+                    }
+                    else
+                        o[0] = (lr + 3 * dc + 2) >> 2;
+                }
+            }
+            store_row<P, 16>(out + (int64_t)r * os, *(const int(*)[16])o);
+            store_row<P, 16>(out + (int64_t)r * os + 16, *(const int(*)[16])(o + 16));
+        }
+        return;
+    }
+    const int Rn = (int)(Dj[N] & 0xffff), Rn1 = (int)(Dj[N - 1] & 0xffff);   // R[0], R[-1] of the frame
+    const bool edge = mi.angle == 0 && bf;
+    auto edge_px = [&](int l) {
+        const int e = (int16_t)(Rn + ((l - Rn1) >> 1));
+        return e < 0 ? 0 : (e > maxv ? maxv : e);
+    };
+    if (!tr && sizeof(P) == 1)
+    {
+        // 8 bit: two pixels of the row per packed-u16 multiply-add pair, v_perm to bytes
+        auto pmad = [](uint32_t a, uint32_t b, uint32_t c) -> uint32_t {
+            return __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, a) * __builtin_bit_cast(u16x2, b) +
+                                                    __builtin_bit_cast(u16x2, c));
+        };
+#pragma unroll
+        for (int i = 0; i < N / G; i++)
+        {
+            const int r = i * G + q;
+            const int sum = (r + 1) * mi.angle, f = sum & 31;
+            const uint32_t w0 = (uint32_t)(32 - f) * 0x10001u, w1 = (uint32_t)f * 0x10001u;
+            const uint32_t* row = Dj + N + (sum >> 5);
+            uint32_t pq[N / 2], w[N / 4];
+#pragma unroll
+            for (int k = 0; k < N / 2; k++)
+                pq[k] = __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, pmad(row[2 * k], w0, pmad(row[2 * k + 1], w1, 0x00100010u))) >> (u16x2){5, 5});
+#pragma unroll
+            for (int k = 0; k < N / 4; k++) w[k] = __builtin_amdgcn_perm(pq[2 * k + 1], pq[2 * k], 0x06040200u);
+            if (edge) w[0] = (w[0] & ~0xffu) | (uint32_t)edge_px(sj[flip_index(N2 + 1 + r, N2, fh)]);
+            uint8_t* o8 = (uint8_t*)(out + (int64_t)r * os);
+#pragma unroll
+            for (int k = 0; k < N / 16; k++) stu<uint4>(o8 + 16 * k, make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]));
+        }
+    }
+    else if (!tr)
+    {
+#pragma unroll
+        for (int i = 0; i < N / G; i++)
+        {
+            const int r = i * G + q;
+            const int sum = (r + 1) * mi.angle, f = sum & 31;
+            const u16x2 wt = {(unsigned short)(32 - f), (unsigned short)f};
+            const uint32_t* row = Dj + N + (sum >> 5);
+            int o[N];
+#pragma unroll
+            for (int x = 0; x < N; x++)
+                o[x] = (int)(__builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, row[x]), wt, 16u, false) >> 5);
+            if (edge) o[0] = edge_px(sj[flip_index(N2 + 1 + r, N2, fh)]);
+            store_row<P, 16>(out + (int64_t)r * os, *(const int(*)[16])o);
+            store_row<P, 16>(out + (int64_t)r * os + 16, *(const int(*)[16])(o + 16));
+        }
+    }
+    else
+    {
+        int offc[N];
+        u16x2 wc[N];
+#pragma unroll
+        for (int c = 0; c < N; c++)
+        {
+            const int sum = (c + 1) * mi.angle, f = sum & 31;
+            offc[c] = N + (sum >> 5);
+            wc[c] = u16x2{(unsigned short)(32 - f), (unsigned short)f};
+        }
+#pragma unroll
+        for (int i = 0; i < N / G; i++)
+        {
+            const int r = i * G + q;
+            int o[N];
+#pragma unroll
+            for (int c = 0; c < N; c++)
+                o[c] = (int)(__builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, Dj[offc[c] + r]), wc[c], 16u, false) >> 5);
+            if (edge && r == 0)
+            {
+#pragma unroll
+                for (int c = 0; c < N; c++) o[c] = edge_px(sj[flip_index(N2 + 1 + c, N2, fh)]);
+            }
+            store_row<P, 16>(out + (int64_t)r * os, *(const int(*)[16])o);
+            store_row<P, 16>(out + (int64_t)r * os + 16, *(const int(*)[16])(o + 16));
+        }
+    }
+}
+
 // intraFilter (intrapred.cpp:31-51): N lanes per job, lane l filters pixels 4l .. 4l+3 of the
 // 4N+1 neighbours from one vector load plus its two outer neighbours (lane 0 also copies
 // pixel 4N); 256 / N jobs per block
@@ -738,7 +953,7 @@ static int launch_pred(int N, int n, int depth, void* dst, intptr_t ds, const in
                        const int64_t* nboff, const void* filt, const int64_t* filtoff, const uint8_t* mode,
                        const uint8_t* bfilter, int allangs, hipStream_t st)
 {
-    const int per = N == 4 ? X265AMD_BLOCK * kIntraLaneJobs : N <= 16 ? X265AMD_BLOCK : X265AMD_BLOCK / N;
+    const int per = N == 4 ? X265AMD_BLOCK * kIntraLaneJobs : N <= 16 ? X265AMD_BLOCK : X265AMD_BLOCK / 4;
     const dim3 grid((n + per - 1) / per);
 #define L(K, NN) hipLaunchKernelGGL((K<P, NN>), grid, dim3(X265AMD_BLOCK), 0, st, n, (1 << depth) - 1, \
                                     (P*)dst, ds, doff, (const P*)nb, nboff, (const P*)filt, filtoff, mode, bfilter, allangs)
@@ -747,7 +962,7 @@ static int launch_pred(int N, int n, int depth, void* dst, intptr_t ds, const in
     case 4: L(k_intra_lane, 4); break;
     case 8: L(k_intra_lane, 8); break;
     case 16: L(k_intra_rows, 16); break;
-    case 32: L(k_intra_pred, 32); break;
+    case 32: L(k_intra_quad, 32); break;
     default: return X265AMD_EINVAL;
     }
 #undef L
