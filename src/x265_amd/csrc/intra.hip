@@ -750,8 +750,8 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_intra_quad(int n, int maxv,
     // neighbours: lane q loads pixels qN .. qN + N - 1 (lane G - 1 also pixel 4N)
     {
         int v[N];
-        load_row<P, 16>(src + q * N, *(int(*)[16])v);
-        load_row<P, 16>(src + q * N + 16, *(int(*)[16])(v + 16));
+#pragma unroll
+        for (int h = 0; h < N; h += 16) load_row<P, 16>(src + q * N + h, *(int(*)[16])(v + h));
 #pragma unroll
         for (int k = 0; k < N; k++) S[slot][q * N + k] = (uint16_t)v[k];
         if (q == G - 1) S[slot][4 * N] = (uint16_t)src[4 * N];
@@ -832,8 +832,8 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_intra_quad(int n, int maxv,
                         o[0] = (lr + 3 * dc + 2) >> 2;
                 }
             }
-            store_row<P, 16>(out + (int64_t)r * os, *(const int(*)[16])o);
-            store_row<P, 16>(out + (int64_t)r * os + 16, *(const int(*)[16])(o + 16));
+#pragma unroll
+            for (int h = 0; h < N; h += 16) store_row<P, 16>(out + (int64_t)r * os + h, *(const int(*)[16])(o + h));
         }
         return;
     }
@@ -883,8 +883,8 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_intra_quad(int n, int maxv,
             for (int x = 0; x < N; x++)
                 o[x] = (int)(__builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, row[x]), wt, 16u, false) >> 5);
             if (edge) o[0] = edge_px(sj[flip_index(N2 + 1 + r, N2, fh)]);
-            store_row<P, 16>(out + (int64_t)r * os, *(const int(*)[16])o);
-            store_row<P, 16>(out + (int64_t)r * os + 16, *(const int(*)[16])(o + 16));
+#pragma unroll
+            for (int h = 0; h < N; h += 16) store_row<P, 16>(out + (int64_t)r * os + h, *(const int(*)[16])(o + h));
         }
     }
     else
@@ -911,8 +911,8 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_intra_quad(int n, int maxv,
 #pragma unroll
                 for (int c = 0; c < N; c++) o[c] = edge_px(sj[flip_index(N2 + 1 + c, N2, fh)]);
             }
-            store_row<P, 16>(out + (int64_t)r * os, *(const int(*)[16])o);
-            store_row<P, 16>(out + (int64_t)r * os + 16, *(const int(*)[16])(o + 16));
+#pragma unroll
+            for (int h = 0; h < N; h += 16) store_row<P, 16>(out + (int64_t)r * os + h, *(const int(*)[16])(o + h));
         }
     }
 }
@@ -953,7 +953,7 @@ static int launch_pred(int N, int n, int depth, void* dst, intptr_t ds, const in
                        const int64_t* nboff, const void* filt, const int64_t* filtoff, const uint8_t* mode,
                        const uint8_t* bfilter, int allangs, hipStream_t st)
 {
-    const int per = N == 4 ? X265AMD_BLOCK * kIntraLaneJobs : N <= 16 ? X265AMD_BLOCK : X265AMD_BLOCK / 4;
+    const int per = N == 4 ? X265AMD_BLOCK * kIntraLaneJobs : N <= 8 ? X265AMD_BLOCK : X265AMD_BLOCK / 4;
     const dim3 grid((n + per - 1) / per);
 #define L(K, NN) hipLaunchKernelGGL((K<P, NN>), grid, dim3(X265AMD_BLOCK), 0, st, n, (1 << depth) - 1, \
                                     (P*)dst, ds, doff, (const P*)nb, nboff, (const P*)filt, filtoff, mode, bfilter, allangs)
@@ -961,7 +961,7 @@ static int launch_pred(int N, int n, int depth, void* dst, intptr_t ds, const in
     {
     case 4: L(k_intra_lane, 4); break;
     case 8: L(k_intra_lane, 8); break;
-    case 16: L(k_intra_rows, 16); break;
+    case 16: L(k_intra_quad, 16); break;
     case 32: L(k_intra_quad, 32); break;
     default: return X265AMD_EINVAL;
     }
