@@ -10,14 +10,11 @@
 // is x265_clip((int16_t)(top + ((left[y] - topLeft) >> 1))).  all-angles
 // stores horizontal modes UN-transposed (intrapred.cpp:219-233).
 //
-// Work mapping (template on the TU size N): one (TU, mode) job per N-lane
-// group, lane r producing output row r (N pixels, stored as full-row vector
-// stores).  The group builds the reference array of intra_pred_ang_c in LDS
-// exactly once per job, as one CONTIGUOUS int16 array R[-N .. 2N] (projected
-// left samples, top-left, the 2N above samples — all in the mode's flipped
-// frame) plus the N+1 samples of the other side L[0 .. N]; every angular
-// pixel is then two LDS reads and one blend.  The mode is decoded once per job
-// from packed register constants (no table loads).
+// Work mapping: 4x4 / 8x8 one (TU, mode) job per lane (k_intra_lane); 16x16 / 32x32 four lanes per
+// job (k_intra_quad).  Either way the reference array of intra_pred_ang_c is built once per job in the
+// mode's frame (projected left samples, top-left, the 2N above samples) as pairs (R[j], R[j+1]) in LDS,
+// so every angular pixel is one LDS read and one blend; the mode is decoded once per job from packed
+// register constants (no table loads).
 #include "common.h"
 #include "intra_lane.h"
 #include "../../../include/x265_amd.h"
@@ -25,175 +22,6 @@
 namespace x265amd {
 
 typedef unsigned short pair16 __attribute__((ext_vector_type(2)));
-
-template <typename P, int N>
-__global__ __launch_bounds__(X265AMD_BLOCK) void k_intra_pred(int n, int maxv,
-    P* __restrict__ dst, intptr_t ds, const int64_t* __restrict__ doff,
-    const P* __restrict__ nb, const int64_t* __restrict__ nboff,
-    const P* __restrict__ filt, const int64_t* __restrict__ filtoff,
-    const uint8_t* __restrict__ mode, const uint8_t* __restrict__ bfilter, int allangs)
-{
-    constexpr int JOBS = X265AMD_BLOCK / N;
-    constexpr int N2 = 2 * N;
-    constexpr int LG2 = N == 4 ? 2 : N == 8 ? 3 : N == 16 ? 4 : 5;
-    constexpr int SLOT = 4 * N + 4;                  // R: 3N+1, L: N+1, padded
-    constexpr int PW = 3 * N;                        // pairs D[j] = (R[j], R[j + 1]), j = -N .. 2N-1
-    __shared__ int16_t sh[JOBS][SLOT];
-    __shared__ int16_t raw[JOBS][4 * N + 2];         // the 4N+1 neighbours as loaded
-    __shared__ uint32_t Dp[JOBS][PW];
-    const int slot = threadIdx.x / N, r = threadIdx.x % N;
-    const int64_t job = (int64_t)xcd_block() * JOBS + slot;
-    const bool live = job < n;
-    const int64_t jj = live ? job : 0;
-    int16_t* R = sh[slot] + N;                       // R[j], j = -N .. 2N
-    int16_t* L = sh[slot] + 3 * N + 2;               // L[y], y = 0 .. N
-    uint32_t* D = Dp[slot] + N;                      // D[j], j = -N .. 2N-1
-
-    int m, bf;
-    const P* src;
-    P* out;
-    if (allangs)
-    {
-        // job = tu * 33 + (mode - 2); filtered or unfiltered neighbours per g_intraFilterFlags
-        const int64_t tu = jj / 33;
-        m = 2 + (int)(jj % 33);
-        bf = bfilter[tu];
-        src = (c_intra.filter_flags[m] & N) ? filt + filtoff[tu] : nb + nboff[tu];
-        out = dst + doff[tu] + (int64_t)(m - 2) * N * N;
-    }
-    else
-    {
-        m = mode[jj];
-        bf = bfilter[jj];
-        src = nb + nboff[jj];
-        out = dst + doff[jj];
-    }
-    const ModeInfo mi = decode_mode(m);
-
-    // ---- neighbours: lane r loads pixels 4r .. 4r+3 with one vector load (lane 0 also pixel 4N)
-    {
-        int t[4];
-        load_row<P, 4>(src + 4 * r, t);
-#pragma unroll
-        for (int k = 0; k < 4; k++) raw[slot][4 * r + k] = (int16_t)t[k];
-        if (r == 0) raw[slot][4 * N] = (int16_t)src[4 * N];
-    }
-    __syncthreads();
-    const int16_t* sr = raw[slot];
-    // ---- R[j] = s'[1 + j] for j = -1 .. 2N-1, L[y] = s'[2N + 1 + y] for y = 0 .. N
-    //      (s' = neighbours in the mode's frame), R[-2-k] = projected left samples
-    for (int e = r; e < N2 + 1; e += N) R[e - 1] = sr[flip_index(e, N2, mi.hor)];
-    for (int y = r; y <= N; y += N) L[y] = sr[flip_index(N2 + 1 + y, N2, mi.hor)];
-    if (mi.angle < 0)
-    {
-        const int nproj = -((N * mi.angle) >> 5) - 1;     // intrapred.cpp:154-164
-        for (int k = r; k < nproj; k += N)
-            R[-2 - k] = sr[flip_index(N2 + ((128 + (k + 1) * mi.inv) >> 8), N2, mi.hor)];
-    }
-    __syncthreads();
-    // pairs for the angular interpolation: one ds_read_b32 + one v_dot2 per pixel
-    for (int j = r - N; j < 2 * N; j += N) D[j] = (uint32_t)(uint16_t)R[j] | ((uint32_t)(uint16_t)R[j + 1] << 16);
-    __syncthreads();
-    if (!live) return;
-
-    int v[N];
-    if (m == 0)   // planar (intrapred.cpp:87-100), unflipped: above = R[0..N], left = L[0..N]
-    {
-        const int lr = L[r], bl = L[N], tr = R[N];
-#pragma unroll
-        for (int x = 0; x < N; x++)
-            v[x] = ((N - 1 - x) * lr + (N - 1 - r) * R[x] + (x + 1) * tr + (r + 1) * bl + N) >> (LG2 + 1);
-    }
-    else if (m == 1)   // DC (+ dcPredFilter, intrapred.cpp:53-85)
-    {
-        int t = N;
-#pragma unroll
-        for (int i = 0; i < N; i++) t += R[i] + L[i];
-        const int dc = t / N2;
-#pragma unroll
-        for (int x = 0; x < N; x++) v[x] = dc;
-        if (bf)
-        {
-            if (r == 0)
-            {
-                v[0] = (R[0] + L[0] + 2 * dc + 2) >> 2;
-#pragma unroll
-                for (int x = 1; x < N; x++) v[x] = (R[x] + 3 * dc + 2) >> 2;
-            }
-            else
-                v[0] = (L[r] + 3 * dc + 2) >> 2;
-        }
-    }
-    else if (!mi.hor || allangs)
-    {
-        // output row r is vertical-frame row y = r: one (offset, fraction) for the whole row
-        const int sum = (r + 1) * mi.angle, off = sum >> 5, f = sum & 31;
-        if (mi.angle == 0)
-        {
-#pragma unroll
-            for (int x = 0; x < N; x++) v[x] = R[x];
-            if (bf)
-            {
-                const int t = (int16_t)(R[0] + ((L[r] - R[-1]) >> 1));
-                v[0] = t < 0 ? 0 : (t > maxv ? maxv : t);
-            }
-        }
-        else
-        {
-            const pair16 wt = {(unsigned short)(32 - f), (unsigned short)f};
-            const uint32_t* row = D + off;
-#pragma unroll
-            for (int x = 0; x < N; x++)
-                v[x] = (int)(__builtin_amdgcn_udot2(__builtin_bit_cast(pair16, row[x]), wt, 16u, false) >> 5);
-        }
-    }
-    else
-    {
-        // horizontal mode, reference orientation: output (r, c) = vertical-frame (y = c, x = r)
-        if (mi.angle == 0)
-        {
-            // x = r: every pixel of the row is R[r], except column x = 0 of the vertical frame (row r = 0)
-#pragma unroll
-            for (int c = 0; c < N; c++)
-            {
-                int p = R[r];
-                if (bf && r == 0)
-                {
-                    const int t = (int16_t)(R[0] + ((L[c] - R[-1]) >> 1));
-                    p = t < 0 ? 0 : (t > maxv ? maxv : t);
-                }
-                v[c] = p;
-            }
-        }
-        else
-        {
-#pragma unroll
-            for (int c = 0; c < N; c++)
-            {
-                const int sum = (c + 1) * mi.angle, off = sum >> 5, f = sum & 31;
-                const pair16 wt = {(unsigned short)(32 - f), (unsigned short)f};
-                v[c] = (int)(__builtin_amdgcn_udot2(__builtin_bit_cast(pair16, D[off + r]), wt, 16u, false) >> 5);
-            }
-        }
-    }
-    P* orow = out + (int64_t)r * (allangs ? N : ds);
-    if constexpr (N == 4)
-        store_row<P, 4>(orow, v);
-    else if constexpr (N == 8)
-        store_row<P, 8>(orow, v);
-    else
-    {
-        // 16-pixel pieces: one 16-byte store per piece at 8 bit (two at 16 bit)
-#pragma unroll
-        for (int x = 0; x < N; x += 16)
-        {
-            int t[16];
-#pragma unroll
-            for (int k = 0; k < 16; k++) t[k] = v[x + k];
-            store_row<P, 16>(orow + x, t);
-        }
-    }
-}
 
 // Small TUs (4x4, 8x8): one (TU, mode) job per LANE.  The whole 4N+1
 // neighbour array is loaded with vector loads and flipped in registers
@@ -395,319 +223,14 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_intra_lane(int n, int maxv,
     for (int r = 0; r < N; r++) store_row<P, N>(out + (int64_t)r * os, o[r]);
 }
 
-// 16x16: one (TU, mode) job per LANE, 64 jobs per wave (the N-lane block kernel above keeps only 4 jobs
-// per wave in flight and is bound by their load -> barrier -> compute latency).  The lane's reference
-// array goes to its private LDS column as pairs D[j] = (R[j], R[j+1]) for every mode; the block is then
-// produced row by row (16 pixels in registers at a time, one 16-byte store per row): angular and pure
-// vertical / horizontal pixels are one ds_read_b32 + one v_dot2 (angle 0 reads (R[j], R[j+1]) against
-// weights (32, 0)), planar and DC come from registers.  Lane-private LDS: no barrier anywhere.
-template <typename P, int N>
-__global__ __launch_bounds__(X265AMD_BLOCK) void k_intra_rows(int n, int maxv,
-    P* __restrict__ dst, intptr_t ds, const int64_t* __restrict__ doff,
-    const P* __restrict__ nb, const int64_t* __restrict__ nboff,
-    const P* __restrict__ filt, const int64_t* __restrict__ filtoff,
-    const uint8_t* __restrict__ mode, const uint8_t* __restrict__ bfilter, int allangs)
-{
-    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
-    constexpr int N2 = 2 * N;
-    constexpr int LG2 = N == 16 ? 4 : 5;
-    constexpr int NW = N * N * (int)sizeof(P) / 4;            // dwords per output block
-    constexpr bool STAGE = sizeof(P) == 1;                   // 16-bit blocks would not fit the LDS
-    constexpr int ROWS = STAGE && NW > 3 * N ? NW : 3 * N;
-    // rows 0 .. 3N-1: the lanes' reference pairs; afterwards rows 0 .. NW-1 of the wave's columns stage
-    // the wave's 64 output blocks for coalesced stores
-    __shared__ uint32_t D[ROWS][X265AMD_BLOCK];
-    const int t = threadIdx.x;
-    const int64_t job = (int64_t)xcd_block() * X265AMD_BLOCK + t;
-    const bool live = job < n;
-    const int64_t jj = live ? job : 0;                 // dead lanes predict job 0 and store nothing
-
-    int m, bf;
-    const P* src;
-    P* out;
-    intptr_t os;
-    if (allangs)
-    {
-        const int64_t tu = jj / 33;
-        m = 2 + (int)(jj % 33);
-        bf = bfilter[tu];
-        src = (c_intra.filter_flags[m] & N) ? filt + filtoff[tu] : nb + nboff[tu];
-        out = dst + doff[tu] + (int64_t)(m - 2) * N * N;
-        os = N;
-    }
-    else
-    {
-        m = mode[jj];
-        bf = bfilter[jj];
-        src = nb + nboff[jj];
-        out = dst + doff[jj];
-        os = ds;
-    }
-    // the wave's 64 blocks are one contiguous run (compact outputs of consecutive jobs): stage them in LDS
-    // and write the run with coalesced 16-byte stores, else one row store per lane and row
-    const int lane = t & 63;
-    const P* out0 = (const P*)__shfl((long long)(intptr_t)out, 0, 64);
-    const bool wave_run = STAGE && __all(os == N && (!live || out == out0 + (int64_t)lane * N * N));
-    uint32_t pk[STAGE ? NW : 1];                       // the lane's block, packed (staged path)
-    int s[4 * N + 1];
-    intra_lane_load<P, N>(src, s);
-    const ModeInfo mi = decode_mode(m);
-    const bool frame_hor = mi.hor && m >= 2;
-
-    // the mode's frame: R[j + N], j = -N .. 2N (above row, top-left at j = -1), L[y] (left column)
-    int R[3 * N + 1], L[N + 1];
-#pragma unroll
-    for (int e = 0; e <= N2; e++) R[N + e - 1] = frame_hor ? s[e == 0 ? 0 : e + N2] : s[e];
-    R[3 * N] = 0;
-#pragma unroll
-    for (int y = 0; y <= N; y++) L[y] = frame_hor ? s[1 + y] : s[N2 + 1 + y];
-#pragma unroll
-    for (int k = 0; k < N - 1; k++) R[k] = 0;
-    if (mi.angle < 0)
-    {
-        // projected left samples R[-2-k] = L[i_k - 1], i_k = (128 + (k+1)·invAngle) >> 8
-        // (intrapred.cpp:154-164), gathered through the lane's LDS column
-#pragma unroll
-        for (int y = 0; y <= N; y++) D[y][t] = (uint32_t)L[y];
-        const int nproj = -((N * mi.angle) >> 5) - 1;
-#pragma unroll
-        for (int k = 0; k < N - 1; k++)
-            if (k < nproj) R[N - 2 - k] = (int)D[((128 + (k + 1) * mi.inv) >> 8) - 1][t];
-    }
-#pragma unroll
-    for (int j = 0; j < 3 * N; j++) D[j][t] = (uint32_t)R[j] | ((uint32_t)R[j + 1] << 16);
-
-    const bool tr = frame_hor && !allangs;           // horizontal modes are transposed back
-    // one output row: packed into the lane's block (staged path) or stored
-    auto emit = [&](int r, const int (&o)[N]) {
-        if constexpr (STAGE)
-        {
-            if (wave_run)
-            {
-#pragma unroll
-                for (int x = 0; x < N; x += 4)
-                    pk[(r * N + x) / 4] = (uint32_t)o[x] | ((uint32_t)o[x + 1] << 8) | ((uint32_t)o[x + 2] << 16) |
-                                          ((uint32_t)o[x + 3] << 24);
-                return;
-            }
-        }
-        if (live) store_row<P, N>(out + (int64_t)r * os, o);
-    };
-    // 8-bit staged angular / pure modes on packed u16 pairs: (32 - f)·(a, b) + f·(b, c) + 16 gives two
-    // neighbouring pixels per v_pk_mad pair, one v_pk_lshrrev and v_perm to bytes (vertical modes: two
-    // pixels of a row; transposed horizontal modes: the same column of two rows)
-    if constexpr (STAGE)
-    {
-        if (wave_run && m >= 2)
-        {
-            auto pmad = [](uint32_t a, uint32_t b, uint32_t c) -> uint32_t {
-                return __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, a) * __builtin_bit_cast(u16x2, b) +
-                                                        __builtin_bit_cast(u16x2, c));
-            };
-            auto pshr5 = [](uint32_t a) -> uint32_t {
-                return __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, a) >> (u16x2){5, 5});
-            };
-            constexpr uint32_t RND = 0x00100010u;
-            const bool edge = mi.angle == 0 && bf;
-            auto edge_px = [&](int l) {
-                const int e = (int16_t)(R[N] + ((l - R[N - 1]) >> 1));
-                return (uint32_t)(e < 0 ? 0 : (e > maxv ? maxv : e));
-            };
-            if (!tr)
-            {
-#pragma clang loop unroll(full)
-                for (int r = 0; r < N; r++)
-                {
-                    const int sum = (r + 1) * mi.angle, f = sum & 31;
-                    const uint32_t w0 = (uint32_t)(32 - f) * 0x10001u, w1 = (uint32_t)f * 0x10001u;
-                    const uint32_t* row = &D[N + (sum >> 5)][t];
-                    uint32_t q[N / 2];
-#pragma unroll
-                    for (int i = 0; i < N / 2; i++)
-                        q[i] = pshr5(pmad(row[(2 * i + 1) * X265AMD_BLOCK], w1, pmad(row[2 * i * X265AMD_BLOCK], w0, RND)));
-#pragma unroll
-                    for (int k = 0; k < N / 4; k++) pk[r * (N / 4) + k] = __builtin_amdgcn_perm(q[2 * k + 1], q[2 * k], 0x06040200u);
-                    if (edge) pk[r * (N / 4)] = (pk[r * (N / 4)] & ~0xffu) | edge_px(L[r]);
-                }
-            }
-            else
-            {
-                const uint32_t* col[N];
-                uint32_t w0[N], w1[N];
-#pragma unroll
-                for (int c = 0; c < N; c++)
-                {
-                    const int sum = (c + 1) * mi.angle, f = sum & 31;
-                    col[c] = &D[N + (sum >> 5)][t];
-                    w0[c] = (uint32_t)(32 - f) * 0x10001u;
-                    w1[c] = (uint32_t)f * 0x10001u;
-                }
-#pragma clang loop unroll(full)
-                for (int r = 0; r < N; r += 2)
-                {
-                    uint32_t q[N];                     // (pixel (r, c), pixel (r + 1, c))
-#pragma unroll
-                    for (int c = 0; c < N; c++)
-                        q[c] = pshr5(pmad(col[c][(r + 1) * X265AMD_BLOCK], w1[c], pmad(col[c][r * X265AMD_BLOCK], w0[c], RND)));
-#pragma unroll
-                    for (int k = 0; k < N / 4; k++)
-                    {
-                        const uint32_t t0 = __builtin_amdgcn_perm(q[4 * k + 1], q[4 * k], 0x06020400u);
-                        const uint32_t t1 = __builtin_amdgcn_perm(q[4 * k + 3], q[4 * k + 2], 0x06020400u);
-                        pk[r * (N / 4) + k] = __builtin_amdgcn_perm(t1, t0, 0x05040100u);
-                        pk[(r + 1) * (N / 4) + k] = __builtin_amdgcn_perm(t1, t0, 0x07060302u);
-                    }
-                }
-                if (edge)
-                {
-#pragma unroll
-                    for (int k = 0; k < N / 4; k++)
-                        pk[k] = edge_px(L[4 * k]) | (edge_px(L[4 * k + 1]) << 8) | (edge_px(L[4 * k + 2]) << 16) |
-                                (edge_px(L[4 * k + 3]) << 24);
-                }
-            }
-            goto staged;
-        }
-    }
-    // each mode class its own fully unrolled row loop (static indices into pk, no per-row branching)
-    if (m == 0)
-    {
-        const int tr_ = R[2 * N], bl = L[N];
-#pragma clang loop unroll(full)
-        for (int r = 0; r < N; r++)
-        {
-            int o[N];
-#pragma unroll
-            for (int x = 0; x < N; x++)
-                o[x] = ((N - 1 - x) * L[r] + (N - 1 - r) * R[N + x] + (x + 1) * tr_ + (r + 1) * bl + N) >> (LG2 + 1);
-            emit(r, o);
-        }
-    }
-    else if (m == 1)
-    {
-        int sum = N;
-#pragma unroll
-        for (int i = 0; i < N; i++) sum += R[N + i] + L[i];
-        const int dc = sum >> (LG2 + 1);
-#pragma clang loop unroll(full)
-        for (int r = 0; r < N; r++)
-        {
-            int o[N];
-#pragma unroll
-            for (int x = 0; x < N; x++) o[x] = dc;
-            if (bf)
-            {
-                if (r == 0)
-                {
-                    o[0] = (R[N] + L[0] + 2 * dc + 2) >> 2;
-#pragma unroll
-                    for (int x = 1; x < N; x++) o[x] = (R[N + x] + 3 * dc + 2) >> 2;
-                }
-                else
-                    o[0] = (L[r] + 3 * dc + 2) >> 2;
-            }
-            emit(r, o);
-        }
-    }
-    else if (!tr)
-    {
-        const bool edge = mi.angle == 0 && bf;
-#pragma clang loop unroll(full)
-        for (int r = 0; r < N; r++)
-        {
-            // mode-frame row y = r: one offset / fraction for the row
-            int o[N];
-            const int sum = (r + 1) * mi.angle, off = sum >> 5, f = sum & 31;
-            const u16x2 wt = {(unsigned short)(32 - f), (unsigned short)f};
-            const uint32_t* row = &D[N + off][t];
-#pragma unroll
-            for (int x = 0; x < N; x++)
-                o[x] = (int)(__builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, row[x * X265AMD_BLOCK]), wt, 16u, false) >> 5);
-            if (edge)
-            {
-                const int e = (int16_t)(R[N] + ((L[r] - R[N - 1]) >> 1));
-                o[0] = e < 0 ? 0 : (e > maxv ? maxv : e);
-            }
-            emit(r, o);
-        }
-    }
-    else
-    {
-        // output (r, c) = mode-frame (y = c, x = r): per column one offset / fraction, computed once
-        const uint32_t* col[N];
-        u16x2 wt[N];
-#pragma unroll
-        for (int c = 0; c < N; c++)
-        {
-            const int sum = (c + 1) * mi.angle, f = sum & 31;
-            col[c] = &D[N + (sum >> 5)][t];
-            wt[c] = u16x2{(unsigned short)(32 - f), (unsigned short)f};
-        }
-        const bool edge = mi.angle == 0 && bf;
-#pragma clang loop unroll(full)
-        for (int r = 0; r < N; r++)
-        {
-            int o[N];
-#pragma unroll
-            for (int c = 0; c < N; c++)
-                o[c] = (int)(__builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, col[c][r * X265AMD_BLOCK]), wt[c], 16u, false) >> 5);
-            if (edge && r == 0)
-            {
-#pragma unroll
-                for (int c = 0; c < N; c++)
-                {
-                    const int e = (int16_t)(R[N] + ((L[c] - R[N - 1]) >> 1));
-                    o[c] = e < 0 ? 0 : (e > maxv ? maxv : e);
-                }
-            }
-            emit(r, o);
-        }
-    }
-    if constexpr (!STAGE) return;
-    if (!wave_run) return;
-staged:
-    // staging: the wave's columns [w*64, w*64+64) of rows 0 .. NW-1 as one linear run of 64 * NW dwords
-    // (lane L's block at dwords L*NW ..), 16-byte chunks rotated by the lane so a chunk store hits 16 bank
-    // groups; the lane's own D column is no longer read by anyone (wave-private region)
-    const int w0 = t & ~63;
-    constexpr int CH = NW / 4;                         // 16-byte chunks per block
-    auto at = [&](int i) -> uint32_t* { return &D[i / 64][w0 + (i & 63)]; };   // linear dword i
-    __builtin_amdgcn_wave_barrier();
-#pragma unroll
-    for (int k = 0; k < CH; k++)
-    {
-        const int c = (k + lane) % CH;
-        uint32_t* p = at(lane * NW + 4 * c);
-        p[0] = pk[4 * k];
-        p[1] = pk[4 * k + 1];
-        p[2] = pk[4 * k + 2];
-        p[3] = pk[4 * k + 3];
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    const int64_t live_jobs = (int64_t)n - (job - lane);
-    const int64_t lim = (live_jobs < 64 ? live_jobs : 64) * CH;   // chunks of the wave's live jobs
-    uint8_t* base = (uint8_t*)out0;
-#pragma unroll
-    for (int i = 0; i < CH; i++)
-    {
-        const int q = i * 64 + lane;                   // chunk q of the run: job q / CH, chunk q % CH
-        if (q < lim)
-        {
-            const int jb = q / CH, c = (q % CH + jb) % CH;
-            const uint32_t* p = at(jb * NW + 4 * c);
-            stu<uint4>(base + (size_t)q * 16, make_uint4(p[0], p[1], p[2], p[3]));
-        }
-    }
-}
-
-// 32x32: four lanes per (TU, mode) job, 16 jobs per wave, lane q producing rows q, q + 4, .. (a job's
+// 16x16 / 32x32: four lanes per (TU, mode) job, 16 jobs per wave, lane q producing rows q, q + 4, .. (a job's
 // four lanes write four consecutive rows: 128 contiguous bytes per pass).  The job's 4N+1 neighbours go
 // to LDS once (each lane loads a quarter), the four lanes build the job's reference pairs
 // D[j] = (R[j], R[j+1]) in the mode's frame (flip, projected left samples) together, and every angular
-// pixel is one ds_read_b32 + v_dot2.  Wave-private LDS (the wave's 16 jobs): wave-level ordering only,
-// no block barrier; the block-per-job kernel above keeps only 2 jobs per wave.
+// pixel is one ds_read_b32 + v_dot2 (8-bit vertical modes: packed u16, (32 - f)·(a, b) + f·(b, c) gives two
+// neighbouring pixels per v_pk_mad pair).  Wave-private LDS (the wave's 16 jobs): wave-level ordering only,
+// no block barrier.  (Rounds 1-2 used N lanes per job and a block-wide LDS array: 1-4 jobs per wave in
+// flight, 0.28 / 0.34 of HBM peak at 16 / 32 against 0.43 / 0.43 here.)
 template <typename P, int N>
 __global__ __launch_bounds__(X265AMD_BLOCK) void k_intra_quad(int n, int maxv,
     P* __restrict__ dst, intptr_t ds, const int64_t* __restrict__ doff,
