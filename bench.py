@@ -378,14 +378,16 @@ def pipeline_rates(prims, args, census, local):
     """The frame-parallel step (--mode pipeline) on this one GPU: one closed GOP of F pictures (F = the
     pipeline default of 32 frames), steps of x265amd_schedule, reference bands copied (in place) into the
     reference store; whole-picture bands and 4-CTU-row bands, and the 32 pictures as four closed GOPs of 8
-    (independent segments run side by side in the same steps)."""
+    (independent segments run side by side in the same steps).  Segments of one picture (32 I pictures: no
+    references, one step) are the same 32 pictures through the same graph machinery without any
+    dependency: the like-for-like reference the dependent forms are measured against."""
     import torch
 
     from src.x265_amd.frame_pipeline import GpuFramePipeline
 
     F = 32
     out = {"frames_per_step": F}
-    for br, seg in ((0, 0), (4, 0), (0, 8)):
+    for br, seg in ((0, 0), (4, 0), (0, 8), (0, 1)):
         pipe = GpuFramePipeline(prims, args.width, args.height, args.depth, F, 1, 0, census=census,
                                 band_rows=br or None, segment_frames=seg or None, streams=args.streams,
                                 device=f"cuda:{local}")
