@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--no-replay", action="store_true")
     ap.add_argument("--job-wait", default="band", help="comma list of band / reference")
     ap.add_argument("--background", default="0", help="comma list of 1 / 0")
+    ap.add_argument("--streams", default="8", help="comma list of stream counts for the step lanes")
     ap.add_argument("--exchange", default="torch",
                     help="comma list of torch / rccl (rccl at one rank: the multi-rank graph structure, per-step "
                          "graphs, with an empty native exchange)")
@@ -51,18 +52,19 @@ def main():
             print(json.dumps({"mode": "replay-eager-1stream", "frames": F, "fps": round(F / dt, 1),
                               "launches": len(ls)}), flush=True)
             del fs, bs, ls
-        for br, seg, jw, bgv, ex in [(int(x), int(g), w, int(v), e) for x in a.band_rows.split(",")
-                                     for g in a.segments.split(",") for w in a.job_wait.split(",")
-                                     for v in a.background.split(",") for e in a.exchange.split(",")]:
+        for br, seg, jw, bgv, ex, nst in [(int(x), int(g), w, int(v), e, int(sn)) for x in a.band_rows.split(",")
+                                          for g in a.segments.split(",") for w in a.job_wait.split(",")
+                                          for v in a.background.split(",") for e in a.exchange.split(",")
+                                          for sn in a.streams.split(",")]:
             early = True
             t0 = time.perf_counter()
-            pipe = GpuFramePipeline(prims, 1920, 1080, 8, F, 1, 0, band_rows=br, streams=8, device="cuda",
+            pipe = GpuFramePipeline(prims, 1920, 1080, 8, F, 1, 0, band_rows=br, streams=nst, device="cuda",
                                     early_independent=early, segment_frames=seg or None, job_wait=jw,
                                     background=bool(bgv), exchange=ex)
             pipe.build(graphs=True)
             tb = time.perf_counter() - t0
             dt = timed(pipe.step, a.reps)
-            print(json.dumps({"mode": "pipeline", "frames": F, "band_rows": br, "segment_frames": seg or F, "job_wait": jw, "background": bgv, "exchange": ex, "fps": round(F / dt, 1),
+            print(json.dumps({"mode": "pipeline", "frames": F, "band_rows": br, "segment_frames": seg or F, "job_wait": jw, "background": bgv, "exchange": ex, "streams": nst, "fps": round(F / dt, 1),
                               "ms_per_step": round(dt * 1e3, 3), "steps": pipe.sched.nsteps,
                               "launches": pipe.launches_per_step, "build_s": round(tb, 1)}), flush=True)
             del pipe
