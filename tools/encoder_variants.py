@@ -28,13 +28,15 @@ def main():
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--variants", default="default;--no-cutree;--rc-lookahead 40;-F 8")
     ap.add_argument("--no-ref", action="store_true", help="only the la encoder")
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
     a = ap.parse_args()
     from bench import _x265_run, host_cores
     from src.x265_amd.synth import SyntheticSource
 
     ref, la = (os.path.join(ROOT, "oracle", "_ref", b) for b in ("x265ref8", "x265la8"))
     cores = host_cores()
-    w, h = 1920, 1080
+    w, h = a.width, a.height
     with tempfile.TemporaryDirectory() as td:
         src = os.path.join(td, "src.yuv")
         SyntheticSource(w, h, a.frames, 8).write_yuv(src)
