@@ -285,7 +285,7 @@ def reference_encoder_baseline(args):
             "mpix_per_s": round(fps_all * args.width * args.height / 1e6, 3)}
 
 
-def encoder_level(args, reps=3):
+def encoder_level(args, reps=3, width=None, height=None, frames=None, provider=True):
     """BASELINE's metric on the encoder itself: encoded fps of the reference x265 1.9 encoder
     (oracle/_ref/x265ref8, C primitives) and of the same encoder with its lookahead cost estimates on
     the MI355X (oracle/_ref/x265la8: integration/gpu_lookahead.cpp over the x265amd_la_* session,
@@ -301,32 +301,33 @@ def encoder_level(args, reps=3):
     if args.depth != 8 or not (os.path.exists(ref) and os.path.exists(la)):
         return None
     cores = host_cores()
-    n = 64 if args.width * args.height <= 1920 * 1080 else 16
+    W, H = width or args.width, height or args.height
+    n = frames or (64 if W * H <= 1920 * 1080 else 16)
     extra = ["--preset", args.preset, "--pools", str(cores)]
-    out = {"clip": f"{n} synthetic {args.width}x{args.height} 8-bit frames, --preset {args.preset}, --pools {cores}, "
+    out = {"clip": f"{n} synthetic {W}x{H} 8-bit frames, --preset {args.preset}, --pools {cores}, "
                    f"default frame threads", "cores": cores, "cpu_model": cpu_model()}
     with tempfile.TemporaryDirectory() as td:
         src = os.path.join(td, "src.yuv")
-        SyntheticSource(args.width, args.height, n, 8).write_yuv(src)
+        SyntheticSource(W, H, n, 8).write_yuv(src)
         fr, fl, md5 = [], [], set()
         for _ in range(reps):
-            f, m, _ = _x265_run(ref, src, args.width, args.height, 8, n, extra)
+            f, m, _ = _x265_run(ref, src, W, H, 8, n, extra, timeout=600)
             fr.append(f)
             md5.add(("ref", m))
-            f, m, _ = _x265_run(la, src, args.width, args.height, 8, n, extra)
+            f, m, _ = _x265_run(la, src, W, H, 8, n, extra, timeout=600)
             fl.append(f)
             md5.add(("la", m))
         digests = {m for _, m in md5}
         out.update({"reference_fps": statistics.median(fr), "reference_fps_runs": fr,
                     "mi355x_lookahead_fps": statistics.median(fl), "mi355x_lookahead_fps_runs": fl,
                     "speedup": round(statistics.median(fl) / statistics.median(fr), 3),
-                    "mi355x_lookahead_mpix_per_s": round(statistics.median(fl) * args.width * args.height / 1e6, 2),
+                    "mi355x_lookahead_mpix_per_s": round(statistics.median(fl) * W * H / 1e6, 2),
                     "bitstreams_identical": len(digests) == 1,
                     "what_runs_on_the_gpu": "LookaheadTLD::lowresIntraEstimate and every CostEstimateGroup "
                                             "estimate (P / B, motion searches, batched per finishBatch); analysis, "
                                             "RDO, CABAC, loop filters stay on the host cores"})
     hip = os.path.join(ROOT, "oracle", "_ref", "x265hip8")
-    if os.path.exists(hip):
+    if provider and os.path.exists(hip):
         w, h, n2 = 416, 240, 2
         small = ["--preset", "medium", "-F", "2", "--pools", "8"]
         with tempfile.TemporaryDirectory() as td:
@@ -631,6 +632,9 @@ def main():
         if world == 1 and not args.no_encoder_level:
             try:
                 enc = encoder_level(args)
+                if (args.width, args.height) == (1920, 1080) and args.preset == "medium":
+                    # BASELINE's 4K figure: 2160p medium, 64 frames (longer than the lookahead depth)
+                    enc["2160p"] = encoder_level(args, reps=2, width=3840, height=2160, frames=64, provider=False)
             except Exception as e:
                 enc = {"error": str(e)}
         line = {
