@@ -462,18 +462,21 @@ def main():
     lanes = [[] for _ in range(nstreams)]
     fork = [False]                     # one stream until the dominant launch is known
 
-    def assign(first=None):
+    def assign(first=None, weight=None):
+        """lanes by longest-processing-time: launches in decreasing weight (measured ms once known,
+        algorithmic bytes before), each onto the least-loaded stream"""
         fork[0] = first is not None
         solo[:] = [first] if first is not None else []
         load = [0.0] * nstreams
         for lst in lanes:
             lst.clear()
-        for b in launches:             # largest first: greedy balance by algorithmic bytes
+        wt = weight or (lambda b: b.bytes)
+        for b in sorted(launches, key=wt, reverse=True):
             if b is first:
                 continue
             i = min(range(nstreams), key=lambda k: load[k])
             lanes[i].append(b)
-            load[i] += b.bytes
+            load[i] += wt(b)
     assign()
 
     def kernels():
@@ -498,7 +501,8 @@ def main():
     torch.cuda.synchronize()
     ktimes = kernel_times(launches, prims)
     dominant = max(launches, key=lambda b: ktimes[b.name])
-    assign(dominant)
+    balance = os.environ.get("X265AMD_BENCH_BALANCE", "time")
+    assign(dominant, (lambda b: ktimes[b.name]) if balance == "time" else None)
 
     graph = None
     if pipe is not None:
