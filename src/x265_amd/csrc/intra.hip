@@ -15,6 +15,8 @@
 // mode's frame (projected left samples, top-left, the 2N above samples) as pairs (R[j], R[j+1]) in LDS,
 // so every angular pixel is one LDS read and one blend; the mode is decoded once per job from packed
 // register constants (no table loads).
+#include <stdlib.h>
+
 #include "common.h"
 #include "intra_lane.h"
 #include "../../../include/x265_amd.h"
@@ -231,7 +233,7 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_intra_lane(int n, int maxv,
 // neighbouring pixels per v_pk_mad pair).  Wave-private LDS (the wave's 16 jobs): wave-level ordering only,
 // no block barrier.  (Rounds 1-2 used N lanes per job and a block-wide LDS array: 1-4 jobs per wave in
 // flight, 0.28 / 0.34 of HBM peak at 16 / 32 against 0.43 / 0.43 here.)
-template <typename P, int N>
+template <typename P, int N, int G = 4>
 __global__ __launch_bounds__(X265AMD_BLOCK) void k_intra_quad(int n, int maxv,
     P* __restrict__ dst, intptr_t ds, const int64_t* __restrict__ doff,
     const P* __restrict__ nb, const int64_t* __restrict__ nboff,
@@ -239,7 +241,8 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_intra_quad(int n, int maxv,
     const uint8_t* __restrict__ mode, const uint8_t* __restrict__ bfilter, int allangs)
 {
     typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
-    constexpr int G = 4, JOBS = X265AMD_BLOCK / G;
+    constexpr int JOBS = X265AMD_BLOCK / G;
+    constexpr int PL = 4 * N / G;                      // neighbours loaded per lane
     constexpr int N2 = 2 * N, NS = 4 * N + 4, ND = 3 * N + 1;      // padded strides (u16 / dwords)
     constexpr int LG2 = N == 32 ? 5 : 4;
     __shared__ uint16_t S[JOBS][NS];                   // the neighbours as loaded
@@ -270,13 +273,14 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_intra_quad(int n, int maxv,
         out = dst + doff[jj];
         os = ds;
     }
-    // neighbours: lane q loads pixels qN .. qN + N - 1 (lane G - 1 also pixel 4N)
+    // neighbours: lane q loads pixels q·PL .. q·PL + PL - 1 (lane G - 1 also pixel 4N)
     {
-        int v[N];
+        static_assert(PL % 16 == 0, "16-pixel neighbour loads");
+        int v[PL];
 #pragma unroll
-        for (int h = 0; h < N; h += 16) load_row<P, 16>(src + q * N + h, *(int(*)[16])(v + h));
+        for (int h = 0; h < PL; h += 16) load_row<P, 16>(src + q * PL + h, *(int(*)[16])(v + h));
 #pragma unroll
-        for (int k = 0; k < N; k++) S[slot][q * N + k] = (uint16_t)v[k];
+        for (int k = 0; k < PL; k++) S[slot][q * PL + k] = (uint16_t)v[k];
         if (q == G - 1) S[slot][4 * N] = (uint16_t)src[4 * N];
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -476,18 +480,21 @@ static int launch_pred(int N, int n, int depth, void* dst, intptr_t ds, const in
                        const int64_t* nboff, const void* filt, const int64_t* filtoff, const uint8_t* mode,
                        const uint8_t* bfilter, int allangs, hipStream_t st)
 {
-    const int per = N == 4 ? X265AMD_BLOCK * kIntraLaneJobs : N <= 8 ? X265AMD_BLOCK : X265AMD_BLOCK / 4;
+    // lanes per job of the 16x16 / 32x32 kernel (X265AMD_INTRA_G16 / _G32 override for tuning runs)
+    auto env_int = [](const char* name, int dflt) { const char* e = getenv(name); return e ? atoi(e) : dflt; };
+    static const int g16 = env_int("X265AMD_INTRA_G16", 4), g32 = env_int("X265AMD_INTRA_G32", 4);
+    const int G = N == 16 ? g16 : N == 32 ? g32 : 1;
+    const int per = N == 4 ? X265AMD_BLOCK * kIntraLaneJobs : N <= 8 ? X265AMD_BLOCK : X265AMD_BLOCK / G;
     const dim3 grid((n + per - 1) / per);
-#define L(K, NN) hipLaunchKernelGGL((K<P, NN>), grid, dim3(X265AMD_BLOCK), 0, st, n, (1 << depth) - 1, \
-                                    (P*)dst, ds, doff, (const P*)nb, nboff, (const P*)filt, filtoff, mode, bfilter, allangs)
-    switch (N)
-    {
-    case 4: L(k_intra_lane, 4); break;
-    case 8: L(k_intra_lane, 8); break;
-    case 16: L(k_intra_quad, 16); break;
-    case 32: L(k_intra_quad, 32); break;
-    default: return X265AMD_EINVAL;
-    }
+#define L(K) hipLaunchKernelGGL(K, grid, dim3(X265AMD_BLOCK), 0, st, n, (1 << depth) - 1, \
+                                (P*)dst, ds, doff, (const P*)nb, nboff, (const P*)filt, filtoff, mode, bfilter, allangs)
+    if (N == 4) L((k_intra_lane<P, 4>));
+    else if (N == 8) L((k_intra_lane<P, 8>));
+    else if (N == 16 && G == 2) L((k_intra_quad<P, 16, 2>));
+    else if (N == 16 && G == 4) L((k_intra_quad<P, 16, 4>));
+    else if (N == 32 && G == 4) L((k_intra_quad<P, 32, 4>));
+    else if (N == 32 && G == 8) L((k_intra_quad<P, 32, 8>));
+    else return X265AMD_EINVAL;
 #undef L
     return (int)hipGetLastError();
 }
