@@ -233,6 +233,19 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_intra_lane(int n, int maxv,
 // neighbouring pixels per v_pk_mad pair).  Wave-private LDS (the wave's 16 jobs): wave-level ordering only,
 // no block barrier.  (Rounds 1-2 used N lanes per job and a block-wide LDS array: 1-4 jobs per wave in
 // flight, 0.28 / 0.34 of HBM peak at 16 / 32 against 0.43 / 0.43 here.)
+// one N-pixel output row (16-pixel pieces, or one 8-pixel store for N = 8)
+template <typename P, int N>
+__device__ __forceinline__ void store_quad_row(P* p, const int (&o)[N])
+{
+    if constexpr (N == 8)
+        store_row<P, 8>(p, o);
+    else
+    {
+#pragma unroll
+        for (int h = 0; h < N; h += 16) store_row<P, 16>(p + h, *(const int(*)[16])(o + h));
+    }
+}
+
 template <typename P, int N, int G = 4>
 __global__ __launch_bounds__(X265AMD_BLOCK) void k_intra_quad(int n, int maxv,
     P* __restrict__ dst, intptr_t ds, const int64_t* __restrict__ doff,
@@ -244,7 +257,7 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_intra_quad(int n, int maxv,
     constexpr int JOBS = X265AMD_BLOCK / G;
     constexpr int PL = 4 * N / G;                      // neighbours loaded per lane
     constexpr int N2 = 2 * N, NS = 4 * N + 4, ND = 3 * N + 1;      // padded strides (u16 / dwords)
-    constexpr int LG2 = N == 32 ? 5 : 4;
+    constexpr int LG2 = N == 8 ? 3 : N == 16 ? 4 : 5;
     __shared__ uint16_t S[JOBS][NS];                   // the neighbours as loaded
     __shared__ uint32_t D[JOBS][ND];                   // reference pairs in the mode's frame
     const int t = threadIdx.x, slot = t / G, q = t % G;
@@ -359,8 +372,7 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_intra_quad(int n, int maxv,
                         o[0] = (lr + 3 * dc + 2) >> 2;
                 }
             }
-#pragma unroll
-            for (int h = 0; h < N; h += 16) store_row<P, 16>(out + (int64_t)r * os + h, *(const int(*)[16])(o + h));
+            store_quad_row<P, N>(out + (int64_t)r * os, o);
         }
         return;
     }
@@ -392,8 +404,13 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_intra_quad(int n, int maxv,
             for (int k = 0; k < N / 4; k++) w[k] = __builtin_amdgcn_perm(pq[2 * k + 1], pq[2 * k], 0x06040200u);
             if (edge) w[0] = (w[0] & ~0xffu) | (uint32_t)edge_px(sj[flip_index(N2 + 1 + r, N2, fh)]);
             uint8_t* o8 = (uint8_t*)(out + (int64_t)r * os);
+            if constexpr (N == 8)
+                stu<uint2>(o8, make_uint2(w[0], w[1]));
+            else
+            {
 #pragma unroll
-            for (int k = 0; k < N / 16; k++) stu<uint4>(o8 + 16 * k, make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]));
+                for (int k = 0; k < N / 16; k++) stu<uint4>(o8 + 16 * k, make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]));
+            }
         }
     }
     else if (!tr)
@@ -410,8 +427,7 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_intra_quad(int n, int maxv,
             for (int x = 0; x < N; x++)
                 o[x] = (int)(__builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, row[x]), wt, 16u, false) >> 5);
             if (edge) o[0] = edge_px(sj[flip_index(N2 + 1 + r, N2, fh)]);
-#pragma unroll
-            for (int h = 0; h < N; h += 16) store_row<P, 16>(out + (int64_t)r * os + h, *(const int(*)[16])(o + h));
+            store_quad_row<P, N>(out + (int64_t)r * os, o);
         }
     }
     else
@@ -438,8 +454,7 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_intra_quad(int n, int maxv,
 #pragma unroll
                 for (int c = 0; c < N; c++) o[c] = edge_px(sj[flip_index(N2 + 1 + c, N2, fh)]);
             }
-#pragma unroll
-            for (int h = 0; h < N; h += 16) store_row<P, 16>(out + (int64_t)r * os + h, *(const int(*)[16])(o + h));
+            store_quad_row<P, N>(out + (int64_t)r * os, o);
         }
     }
 }
@@ -482,13 +497,15 @@ static int launch_pred(int N, int n, int depth, void* dst, intptr_t ds, const in
 {
     // lanes per job of the 16x16 / 32x32 kernel (X265AMD_INTRA_G16 / _G32 override for tuning runs)
     auto env_int = [](const char* name, int dflt) { const char* e = getenv(name); return e ? atoi(e) : dflt; };
+    static const int g8 = env_int("X265AMD_INTRA_G8", 0);     // 0: the lane-per-job kernel
     static const int g16 = env_int("X265AMD_INTRA_G16", 4), g32 = env_int("X265AMD_INTRA_G32", 4);
-    const int G = N == 16 ? g16 : N == 32 ? g32 : 1;
-    const int per = N == 4 ? X265AMD_BLOCK * kIntraLaneJobs : N <= 8 ? X265AMD_BLOCK : X265AMD_BLOCK / G;
+    const int G = N == 8 ? g8 : N == 16 ? g16 : N == 32 ? g32 : 0;
+    const int per = N == 4 ? X265AMD_BLOCK * kIntraLaneJobs : G ? X265AMD_BLOCK / G : X265AMD_BLOCK;
     const dim3 grid((n + per - 1) / per);
 #define L(K) hipLaunchKernelGGL(K, grid, dim3(X265AMD_BLOCK), 0, st, n, (1 << depth) - 1, \
                                 (P*)dst, ds, doff, (const P*)nb, nboff, (const P*)filt, filtoff, mode, bfilter, allangs)
     if (N == 4) L((k_intra_lane<P, 4>));
+    else if (N == 8 && G == 2) L((k_intra_quad<P, 8, 2>));
     else if (N == 8) L((k_intra_lane<P, 8>));
     else if (N == 16 && G == 2) L((k_intra_quad<P, 16, 2>));
     else if (N == 16 && G == 4) L((k_intra_quad<P, 16, 4>));
