@@ -326,7 +326,13 @@ __device__ __forceinline__ void vfilter_pk(const uint8_t* col, intptr_t ss, cons
 
 // Grouped launches (common.h): a = src, d = dst, b = per-job coeffIdx
 // (uint8), param = is_row_ext.
-template <typename P, typename S, typename D, int OP, int TAPS, int UW, int UH>
+//
+// STG (8-bit hpp / vpp into compact destinations, dst stride = w, power-of-two
+// w and h, one unit per lane): the wavefront's outputs are staged in
+// wave-private LDS in destination order and written back as 16-byte chunks, so
+// a store instruction covers whole 64-byte segments of four to sixteen jobs
+// instead of one 4-8-byte row piece per job.
+template <typename P, typename S, typename D, int OP, int TAPS, int UW, int UH, bool STG = false>
 __global__ __launch_bounds__(X265AMD_BLOCK) void k_interp(const BatchGroup g)
 {
     const uint32_t gb = xcd_block();
@@ -334,9 +340,22 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_interp(const BatchGroup g)
     const int w = sub.w, h = sub.h, n = sub.n, lg = sub.lg;
     const intptr_t ss = sub.sa, ds = sub.ds;
     const int G = 1 << lg;
-    const int64_t job = (int64_t)(gb - sub.block0) * (X265AMD_BLOCK >> lg) + (threadIdx.x >> lg);
+    const int64_t wjob0 = (int64_t)(gb - sub.block0) * (X265AMD_BLOCK >> lg) + ((threadIdx.x & ~63u) >> lg);
+    int64_t job = (int64_t)(gb - sub.block0) * (X265AMD_BLOCK >> lg) + (threadIdx.x >> lg);
     const int lane = threadIdx.x & (G - 1);
-    if (job >= n) return;
+    if constexpr (STG)
+    {
+        // the whole wavefront stays for the write-back; lanes past the batch compute a copy of
+        // the last job into LDS that is never written out
+        static_assert(sizeof(D) == 1 && sizeof(S) == 1 && (OP == X265AMD_HPP || OP == X265AMD_VPP), "staging");
+        if (wjob0 >= n) return;
+        if (job >= n) job = n - 1;
+    }
+    else if (job >= n)
+        return;
+    constexpr int STG_WAVE = STG ? 64 * UW * UH : 16;          // staged bytes per wavefront
+    __shared__ uint4 stg_lds[STG ? X265AMD_BLOCK / 64 * STG_WAVE / 16 : 1];
+    uint8_t* const stg = (uint8_t*)stg_lds + (threadIdx.x >> 6) * STG_WAVE + ((threadIdx.x & 63) >> lg) * w * h;
 
     const IfConst K(g.depth);
     const S* ps = (const S*)sub.a + sub.aoff[job];
@@ -376,7 +395,7 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_interp(const BatchGroup g)
                 else hfilter<P, TAPS, UW>((const P*)ps + (y0 + r) * ss + x, c, sum);
                 if constexpr (DOT && OP == X265AMD_HPP)
                 {
-                    store_pp8<UW>((uint8_t*)pd + (y0 + r) * ds + x, sum);
+                    store_pp8<UW>(STG ? stg + (y0 + r) * w + x : (uint8_t*)pd + (y0 + r) * ds + x, sum);
                     continue;
                 }
 #pragma unroll
@@ -424,7 +443,7 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_interp(const BatchGroup g)
                             v = v - (s16x2)8192;       // ps at 8-bit: shift 0, offset -IF_INTERNAL_OFFS
                         o[p] = __builtin_bit_cast(uint32_t, v);
                     }
-                    D* out = pd + (y0 + r) * ds + x;
+                    D* out = STG ? (D*)(stg + (y0 + r) * w + x) : pd + (y0 + r) * ds + x;
                     if constexpr (OP == X265AMD_VPP)
                     {
                         // two pairs -> four pixels per dword
@@ -488,6 +507,25 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_interp(const BatchGroup g)
                 }
                 store_row<D, UW>(pd + (y0 + r) * ds + x, o);
             }
+        }
+    }
+    if constexpr (STG)
+    {
+        // write-back: chunk c of the wavefront's staged bytes is bytes [16c, 16c + 16) of job
+        // (16c) / (w h), whose destination pointer comes from that job's first lane
+        wave_sync();
+        const uint8_t* wbase = (const uint8_t*)stg_lds + (threadIdx.x >> 6) * STG_WAVE;
+        const int lb = 31 - __builtin_clz(w * h);                   // log2 of a job's bytes
+        const int nch = (64 >> lg) << (lb - 4);
+        const int l64 = threadIdx.x & 63;
+#pragma unroll
+        for (int i = 0; i < STG_WAVE / 16 / 64; i++)
+        {
+            const int c = l64 + 64 * i;
+            const int jl = (c << 4) >> lb;
+            const long long dp = __shfl((long long)(intptr_t)pd, jl << lg, 64);
+            if (c < nch && wjob0 + jl < n)
+                stu<uint4>((uint8_t*)(intptr_t)dp + ((c << 4) & ((1 << lb) - 1)), *(const uint4*)(wbase + (c << 4)));
         }
     }
 }
@@ -724,6 +762,8 @@ static int hvpp_lg(int w, int h, int uw, int uh)
 
 // classes of the streaming hv_pp (k_hvpp_stream): 8- / 4-wide strips, no LDS
 constexpr int kHvppStream = 8 * 32 + 31, kHvppStream4 = 4 * 32 + 31;
+// class flag: outputs staged through LDS (k_interp STG)
+constexpr int kStaged = 2048;
 
 template <typename P, typename S, typename D, int OP, int TAPS>
 static int launch_interp(int cls, const BatchGroup& g, uint32_t blocks, hipStream_t st)
@@ -739,7 +779,14 @@ static int launch_interp(int cls, const BatchGroup& g, uint32_t blocks, hipStrea
     if constexpr (OP == X265AMD_HVPP)
         for (int i = 0; i < g.count; i++)
             lds = std::max(lds, (size_t)(X265AMD_BLOCK >> g.s[i].lg) * (g.s[i].h + 7) * g.s[i].w * sizeof(int16_t));
+    constexpr bool STGOK = sizeof(S) == 1 && sizeof(D) == 1 && (OP == X265AMD_HPP || OP == X265AMD_VPP);
 #define L(UW, UH) \
+    if constexpr (STGOK && UW * UH >= 16 && UW >= 4 && (UH <= 8 || PK8)) \
+        if (cls == (UW * 32 + UH | kStaged)) \
+        { \
+            hipLaunchKernelGGL((k_interp<P, S, D, OP, TAPS, UW, UH, true>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, g); \
+            return (int)hipGetLastError(); \
+        } \
     if (cls == UW * 32 + UH) \
     { \
         if constexpr (OP == X265AMD_HVPP) \
@@ -780,6 +827,16 @@ static int grouped_interp(int depth, int count, const x265amd_interp_batch* bt, 
             if (sizeof(P) == 1 && bt[i].w % 8 == 0 && hv_sw != 4) cls[i] = kHvppStream;
             else if (bt[i].w % 4 == 0) cls[i] = kHvppStream4;
         }
+        // 8-bit hpp / vpp into a compact destination (stride = width): stage the outputs in LDS
+        // when every lane holds exactly one unit of >= 16 bytes (X265AMD_INTERP_STAGE=0 disables)
+        static const bool stage = !getenv("X265AMD_INTERP_STAGE") || atoi(getenv("X265AMD_INTERP_STAGE"));
+        if (stage && sizeof(S) == 1 && sizeof(D) == 1 && (OP == X265AMD_HPP || OP == X265AMD_VPP))
+        {
+            const int w = bt[i].w, h = bt[i].h, uw = cls[i] / 32, uh = cls[i] % 32;
+            const bool p2 = (w & (w - 1)) == 0 && (h & (h - 1)) == 0;
+            if (p2 && bt[i].dst_stride == w && uw * uh >= 16 && uw >= 4 && (w / uw) * (h / uh) <= 64)
+                cls[i] |= kStaged;
+        }
     }
     BatchGroup proto{};
     proto.depth = depth;
@@ -792,7 +849,7 @@ static int grouped_interp(int depth, int count, const x265amd_interp_batch* bt, 
             s.b = OP == X265AMD_P2S ? nullptr : b.coeff;
             s.w = b.w; s.h = b.h; s.n = b.n;
             s.param = OP == X265AMD_HPS ? b.is_row_ext : 0;
-            const int uw = cls[i] / 32, uh = cls[i] % 32;
+            const int uw = (cls[i] & (kStaged - 1)) / 32, uh = cls[i] % 32;
             if constexpr (OP == X265AMD_HVPP)
                 s.lg = cls[i] == kHvppStream ? lanes_log2(b.w / 8, 1)
                        : cls[i] == kHvppStream4 ? lanes_log2(b.w / 4, 1) : hvpp_lg(b.w, b.h, uw, uh);

@@ -192,7 +192,10 @@ def case_sad_multi(nref: int, w: int, h: int, depth: int, n: int, seed: int) -> 
                 dict(f=fenc.data, fs=64, foff=foff, r=ref.data, rs=ref.stride, roff=roff, out=out), ["out"])
 
 
-def case_interp(op: int, taps: int, w: int, h: int, depth: int, n: int, seed: int, rowext: int = 0) -> Case:
+def case_interp(op: int, taps: int, w: int, h: int, depth: int, n: int, seed: int, rowext: int = 0,
+                compact: bool = False) -> Case:
+    """compact: destinations are w x rows slots at stride w with no padding (the census layout),
+    in a shuffled order over n + 5 slots so the untouched ones keep their sentinel"""
     det = Det(seed)
     pmax = (1 << depth) - 1
     pdt = pixel_dtype(depth)
@@ -210,8 +213,13 @@ def case_interp(op: int, taps: int, w: int, h: int, depth: int, n: int, seed: in
     else:
         coeff = det.ints(0, nidx, n).astype(np.uint8)
     rows = h + (taps - 1 if (op == HPS and rowext) else 0)
-    dst, ds, doff = out_slots(n, w, rows, np.int16 if dst16 else pdt)
-    return Case("interp", dict(op=op, taps=taps, w=w, h=h, depth=depth, n=n, seed=seed, rowext=rowext),
+    if compact:
+        dst, ds, _ = out_slots(n + 5, w, rows, np.int16 if dst16 else pdt, stride=w, pad=0)
+        doff = (np.argsort(det.ints(0, 1 << 30, n + 5), kind="stable")[:n] * (w * rows)).astype(np.int64)
+    else:
+        dst, ds, doff = out_slots(n, w, rows, np.int16 if dst16 else pdt)
+    return Case("interp", dict(op=op, taps=taps, w=w, h=h, depth=depth, n=n, seed=seed, rowext=rowext,
+                               **({"compact": True} if compact else {})),
                 dict(s=src.data, ss=stride, soff=soff, d=dst, ds=ds, doff=doff, coeff=coeff), ["d"])
 
 

@@ -72,6 +72,25 @@ def test_gpu_matches_oracle_random(prims, oracle_libs, depth):
     assert not bad, bad[:10]
 
 
+@pytest.mark.parametrize("depth", [8, 10])
+def test_gpu_interp_compact_destinations(prims, oracle_libs, depth):
+    """hpp / vpp into census-style compact slots (stride = width): the 8-bit LDS-staged
+    write-back (interp.hip k_interp STG) for power-of-two shapes, the direct stores otherwise;
+    77 jobs leave a partial last wavefront, the slot order is shuffled and five slots stay
+    untouched"""
+    orc = CpuOracle("oracle", depth)
+    bad = []
+    for op in (HPP, VPP):
+        for taps in (4, 8):
+            for (w, h) in ((4, 4), (8, 4), (4, 8), (8, 8), (16, 16), (32, 32), (64, 64), (16, 8), (8, 32), (32, 16),
+                           (16, 64), (64, 16), (12, 16), (24, 32), (16, 4)):
+                c = case_interp(op, taps, w, h, depth, 77, seed_of("gc", op, taps, depth, w, h), compact=True)
+                a, b = run_gpu(c, prims), run_cpu(c, orc)
+                if not np.array_equal(a["d"], b["d"]):
+                    bad.append(c.key())
+    assert not bad, bad[:10]
+
+
 CENSUSES = [("census_1080p_medium.json", 1920, 1080, 8), ("census_2160p_medium.json", 3840, 2160, 8),
             ("census_2160p_slow.json", 3840, 2160, 8), ("census_2160p_medium_main10.json", 3840, 2160, 10)]
 
