@@ -324,6 +324,31 @@ __device__ __forceinline__ void vfilter_pk(const uint8_t* col, intptr_t ss, cons
     }
 }
 
+// Write-back of a wavefront's outputs staged in LDS in destination order (the
+// STG kernels below): job jl of the wavefront (lanes jl << lg ...) owns bytes
+// [jl wh, (jl + 1) wh) of the staging area, wh a power of two >= 16.  Chunk c
+// = bytes [16c, 16c + 16) of job 16c / wh goes to that job's destination,
+// whose pointer comes from the job's first lane; a store instruction covers
+// whole 64-byte segments of several jobs instead of one row piece per job.
+template <int WAVE_BYTES>
+__device__ __forceinline__ void stage_writeback(const uint8_t* wbase, const void* pd, int lg, int wh, int64_t wjob0,
+                                                int n)
+{
+    wave_sync();
+    const int lb = 31 - __builtin_clz(wh);                      // log2 of a job's bytes
+    const int nch = (64 >> lg) << (lb - 4);
+    const int l64 = threadIdx.x & 63;
+#pragma unroll
+    for (int i = 0; i < WAVE_BYTES / 16 / 64; i++)
+    {
+        const int c = l64 + 64 * i;
+        const int jl = (c << 4) >> lb;
+        const long long dp = __shfl((long long)(intptr_t)pd, jl << lg, 64);
+        if (c < nch && wjob0 + jl < n)
+            stu<uint4>((uint8_t*)(intptr_t)dp + ((c << 4) & (wh - 1)), *(const uint4*)(wbase + (c << 4)));
+    }
+}
+
 // Grouped launches (common.h): a = src, d = dst, b = per-job coeffIdx
 // (uint8), param = is_row_ext.
 //
@@ -510,24 +535,7 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_interp(const BatchGroup g)
         }
     }
     if constexpr (STG)
-    {
-        // write-back: chunk c of the wavefront's staged bytes is bytes [16c, 16c + 16) of job
-        // (16c) / (w h), whose destination pointer comes from that job's first lane
-        wave_sync();
-        const uint8_t* wbase = (const uint8_t*)stg_lds + (threadIdx.x >> 6) * STG_WAVE;
-        const int lb = 31 - __builtin_clz(w * h);                   // log2 of a job's bytes
-        const int nch = (64 >> lg) << (lb - 4);
-        const int l64 = threadIdx.x & 63;
-#pragma unroll
-        for (int i = 0; i < STG_WAVE / 16 / 64; i++)
-        {
-            const int c = l64 + 64 * i;
-            const int jl = (c << 4) >> lb;
-            const long long dp = __shfl((long long)(intptr_t)pd, jl << lg, 64);
-            if (c < nch && wjob0 + jl < n)
-                stu<uint4>((uint8_t*)(intptr_t)dp + ((c << 4) & ((1 << lb) - 1)), *(const uint4*)(wbase + (c << 4)));
-        }
-    }
+        stage_writeback<STG_WAVE>((const uint8_t*)stg_lds + (threadIdx.x >> 6) * STG_WAVE, pd, lg, w * h, wjob0, n);
 }
 
 // hv_pp in two on-chip passes: the horizontal int16 intermediate of the
@@ -623,7 +631,10 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_hvpp(const BatchGroup g)
 // serves four output rows — then the sp rounding, int16 truncation and clamp.  The last
 // eight pairs live in a ring indexed by r & 7, compile-time inside a body unrolled over
 // eight rows.
-template <typename P, int SW>
+//
+// STG (8 bit, compact destinations, power-of-two w and h <= 16): the output
+// rows go to wave-private LDS and leave through stage_writeback.
+template <typename P, int SW, bool STG = false>
 __global__ __launch_bounds__(X265AMD_BLOCK) void k_hvpp_stream(const BatchGroup g)
 {
     const uint32_t gb = xcd_block();
@@ -631,9 +642,22 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_hvpp_stream(const BatchGroup 
     const int w = sub.w, h = sub.h, n = sub.n, lg = sub.lg;
     const intptr_t ss = sub.sa, ds = sub.ds;
     const int G = 1 << lg;
-    const int64_t job = (int64_t)(gb - sub.block0) * (X265AMD_BLOCK >> lg) + (threadIdx.x >> lg);
+    const int64_t wjob0 = (int64_t)(gb - sub.block0) * (X265AMD_BLOCK >> lg) + ((threadIdx.x & ~63u) >> lg);
+    int64_t job = (int64_t)(gb - sub.block0) * (X265AMD_BLOCK >> lg) + (threadIdx.x >> lg);
     const int lane = threadIdx.x & (G - 1);
-    if (job >= n || SW * lane >= w) return;
+    constexpr int STG_WAVE = STG ? 64 * SW * 16 : 16;
+    __shared__ uint4 stg_lds[STG ? X265AMD_BLOCK / 64 * STG_WAVE / 16 : 1];
+    if constexpr (STG)
+    {
+        // power-of-two w: every lane holds a strip; lanes past the batch compute a copy of the
+        // last job that is never written out
+        static_assert(sizeof(P) == 1, "staging");
+        if (wjob0 >= n) return;
+        if (job >= n) job = n - 1;
+    }
+    else if (job >= n || SW * lane >= w)
+        return;
+    uint8_t* const stg = (uint8_t*)stg_lds + (threadIdx.x >> 6) * STG_WAVE + ((threadIdx.x & 63) >> lg) * w * h;
     const IfConst K(g.depth);
     const int cidx = ((const uint8_t*)sub.b)[job];
     constexpr bool DOT = sizeof(P) == 1;
@@ -646,7 +670,7 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_hvpp_stream(const BatchGroup 
     for (int k = 0; k < 4; k++) cv[k] = s16x2{ (short)cy[2 * k], (short)cy[2 * k + 1] };
     const int x0 = SW * lane;
     const P* ps = (const P*)sub.a + sub.aoff[job] - 3 * ss + x0;
-    P* pd = (P*)sub.d + sub.doff[job] + x0;
+    P* pd = (P*)sub.d + sub.doff[job] + (STG ? 0 : x0);
     const int R = h + 7;
     // 8 bit: I = S - 8192 exactly (shift 0, |S| <= 88 * 255), and the sp offset adds 8192 * 64
     // back, so the raw sums S are paired and the output is (t + 2048) >> 12
@@ -698,10 +722,12 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_hvpp_stream(const BatchGroup 
                     else
                         o[x] = clampp((t + K.sp_off) >> K.sp_shift, K.maxv);
                 }
-                store_row<P, SW>(pd + (intptr_t)y * ds, o);
+                if constexpr (STG) store_row<P, SW>((P*)(stg + y * w + x0), o);
+                else store_row<P, SW>(pd + (intptr_t)y * ds, o);
             }
         }
     }
+    if constexpr (STG) stage_writeback<STG_WAVE>((const uint8_t*)stg_lds + (threadIdx.x >> 6) * STG_WAVE, pd, lg, w * h, wjob0, n);
 }
 
 // -------------------------------------------------------------- dispatch
@@ -769,9 +795,14 @@ template <typename P, typename S, typename D, int OP, int TAPS>
 static int launch_interp(int cls, const BatchGroup& g, uint32_t blocks, hipStream_t st)
 {
     if constexpr (OP == X265AMD_HVPP)
-        if (cls == kHvppStream || cls == kHvppStream4)
+        if (cls == kHvppStream || cls == kHvppStream4 || cls == (kHvppStream | kStaged))
         {
             if (cls == kHvppStream) hipLaunchKernelGGL((k_hvpp_stream<P, 8>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, g);
+            else if (cls == (kHvppStream | kStaged))
+            {
+                if constexpr (sizeof(P) == 1)
+                    hipLaunchKernelGGL((k_hvpp_stream<P, 8, true>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, g);
+            }
             else hipLaunchKernelGGL((k_hvpp_stream<P, 4>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, g);
             return (int)hipGetLastError();
         }
@@ -837,6 +868,12 @@ static int grouped_interp(int depth, int count, const x265amd_interp_batch* bt, 
             if (p2 && bt[i].dst_stride == w && uw * uh >= 16 && uw >= 4 && (w / uw) * (h / uh) <= 64)
                 cls[i] |= kStaged;
         }
+        if (stage && OP == X265AMD_HVPP && cls[i] == kHvppStream)
+        {
+            const int w = bt[i].w, h = bt[i].h;
+            if ((w & (w - 1)) == 0 && (h & (h - 1)) == 0 && h <= 16 && w * h >= 16 && bt[i].dst_stride == w)
+                cls[i] |= kStaged;
+        }
     }
     BatchGroup proto{};
     proto.depth = depth;
@@ -851,7 +888,7 @@ static int grouped_interp(int depth, int count, const x265amd_interp_batch* bt, 
             s.param = OP == X265AMD_HPS ? b.is_row_ext : 0;
             const int uw = (cls[i] & (kStaged - 1)) / 32, uh = cls[i] % 32;
             if constexpr (OP == X265AMD_HVPP)
-                s.lg = cls[i] == kHvppStream ? lanes_log2(b.w / 8, 1)
+                s.lg = (cls[i] & ~kStaged) == kHvppStream ? lanes_log2(b.w / 8, 1)
                        : cls[i] == kHvppStream4 ? lanes_log2(b.w / 4, 1) : hvpp_lg(b.w, b.h, uw, uh);
             else
             {
