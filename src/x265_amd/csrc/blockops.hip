@@ -11,6 +11,7 @@
 // Work mapping: one block per G-lane group, a lane handles UW (8/4/2)
 // contiguous elements of one row per step, loads and stores vectorised.
 #include <algorithm>
+#include <stdlib.h>
 
 #include "common.h"
 #include "../../../include/x265_amd.h"
@@ -54,7 +55,11 @@ struct RowRaw
 // offsets, then all their row loads, are issued before the first use, so a
 // wave keeps JPL times the bytes in flight across the dependent offset -> data
 // chain that bounds these small, latency-limited block copies.
-template <typename P, int OP, int UW, int UH, int JPL>
+//
+// STG (compact destinations, dst stride = w, power-of-two w and h, one unit per
+// lane): each job set's outputs are staged in wave-private LDS and leave
+// through stage_writeback (common.h) as 16-byte chunks.
+template <typename P, int OP, int UW, int UH, int JPL, bool STG = false>
 __global__ __launch_bounds__(X265AMD_BLOCK) void k_blockop(const BatchGroup g)
 {
     typedef typename OpTypes<P, OP>::d D;
@@ -69,8 +74,19 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_blockop(const BatchGroup g)
     const int G = 1 << lg;
     const int64_t per = X265AMD_BLOCK >> lg;
     const int64_t job0 = (int64_t)(gb - sub.block0) * per * JPL + (threadIdx.x >> lg);
+    const int64_t wjob0 = (int64_t)(gb - sub.block0) * per * JPL + ((threadIdx.x & ~63u) >> lg);
     const int lane = threadIdx.x & (G - 1);
-    if (job0 >= n) return;
+    constexpr int STG_LANE = UW * UH * (int)sizeof(D);        // staged bytes per lane and job set
+    constexpr int STG_WAVE = STG ? 64 * STG_LANE : 16;
+    __shared__ uint4 stg_lds[STG ? X265AMD_BLOCK / 64 * JPL * STG_WAVE / 16 : 1];
+    if constexpr (STG)
+    {
+        if (wjob0 >= n) return;                 // lanes past the batch stage copies never written out
+    }
+    else if (job0 >= n)
+        return;
+    const int wh = w * h * (int)sizeof(D);
+    uint8_t* const stg = (uint8_t*)stg_lds + (threadIdx.x >> 6) * JPL * STG_WAVE + ((threadIdx.x & 63) >> lg) * wh;
 
     D* pd[JPL];
     const A* pa[JPL];
@@ -81,7 +97,7 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_blockop(const BatchGroup g)
     {
         const int64_t job = job0 + k * per;
         live[k] = job < n;
-        const int64_t jj = live[k] ? job : job0;
+        const int64_t jj = live[k] ? job : (STG ? n - 1 : job0);
         pd[k] = (D*)sub.d + sub.doff[jj];
         pa[k] = OP == X265AMD_BLOCKFILL ? nullptr : (const A*)sub.a + sub.aoff[jj];
         pb[k] = TWO ? (const B*)sub.b + sub.boff[jj] : nullptr;
@@ -109,7 +125,7 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_blockop(const BatchGroup g)
 #pragma unroll
         for (int k = 0; k < JPL; k++)
         {
-            if (!live[k]) continue;
+            if (!STG && !live[k]) continue;
 #pragma unroll
             for (int r = 0; r < UH; r++)
             {
@@ -155,9 +171,17 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_blockop(const BatchGroup g)
                         }
                     }
                 }
-                store_row<D, UW>(pd[k] + y * ds + x, o);
+                if constexpr (STG) store_row<D, UW>((D*)(stg + k * STG_WAVE) + y * w + x, o);
+                else store_row<D, UW>(pd[k] + y * ds + x, o);
             }
         }
+    }
+    if constexpr (STG)
+    {
+#pragma unroll
+        for (int k = 0; k < JPL; k++)
+            stage_writeback<STG_WAVE>((const uint8_t*)stg_lds + (threadIdx.x >> 6) * JPL * STG_WAVE + k * STG_WAVE,
+                                      pd[k], lg, wh, wjob0 + k * per, n);
     }
 }
 
@@ -166,8 +190,10 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_blockop(const BatchGroup g)
 // measured on MI355X (tools/kernel_roofline.py, 8x8 and 16x16 blocks), 8-16 B
 // per lane leaves the chip issuing index math and 64+ B serialises each lane's
 // loads; wide int16 operands (addAvg, add_ps) want one row, pixel-only copies four.
+constexpr int kStagedBlock = 4096;
+
 template <typename P, int OP>
-static int blockop_class(int w, int h)
+static int blockop_class(int w, int h, int64_t ds)
 {
     if (w < 2 || h < 1 || w > 64 || h > 64 || (w % 2)) return -X265AMD_EINVAL;
     typedef typename OpTypes<P, OP>::a A;
@@ -179,7 +205,15 @@ static int blockop_class(int w, int h)
     const int uh = (want >= 4 && h % 4 == 0) ? 4 : (want >= 2 && h % 2 == 0) ? 2 : 1;
     // two jobs per lane group for the streaming ops (measured +2-10% on 8x8..64x64)
     const int jpl = ((TWO || OP == X265AMD_COPY_PP) && uw == 8) ? 2 : 1;
-    return jpl * 256 + uw * 16 + uh;
+    int cls = jpl * 256 + uw * 16 + uh;
+    // compact destination: stage the outputs in LDS when every lane holds exactly one unit of
+    // >= 16 bytes (X265AMD_BLOCK_STAGE=0 disables)
+    static const bool stage = !getenv("X265AMD_BLOCK_STAGE") || atoi(getenv("X265AMD_BLOCK_STAGE"));
+    typedef typename OpTypes<P, OP>::d D;
+    const bool p2 = (w & (w - 1)) == 0 && (h & (h - 1)) == 0;
+    if (stage && p2 && ds == w && uw * uh * (int)sizeof(D) >= 16 && (w / uw) * (h / uh) <= 64)
+        cls |= kStagedBlock;
+    return cls;
 }
 
 template <typename P, int OP>
@@ -188,6 +222,12 @@ static int launch_blockop(int cls, const BatchGroup& g, uint32_t blocks, hipStre
     constexpr bool MULTI = OP == X265AMD_SUB_PS || OP == X265AMD_ADD_PS || OP == X265AMD_ADDAVG ||
                            OP == X265AMD_PIXELAVG || OP == X265AMD_COPY_PP;
 #define L(UW, UH, J) \
+    if constexpr (UW * UH * sizeof(typename OpTypes<P, OP>::d) >= 16) \
+        if (cls == (J * 256 + UW * 16 + UH | kStagedBlock)) \
+        { \
+            hipLaunchKernelGGL((k_blockop<P, OP, UW, UH, J, true>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, g); \
+            return (int)hipGetLastError(); \
+        } \
     if (cls == J * 256 + UW * 16 + UH) \
     { \
         hipLaunchKernelGGL((k_blockop<P, OP, UW, UH, J>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, g); \
@@ -210,7 +250,7 @@ static int grouped_blockop(int depth, int count, const x265amd_block_batch* bt, 
     {
         if (bt[i].n < 0) return X265AMD_EINVAL;
         if (bt[i].n == 0) continue;
-        cls[i] = blockop_class<P, OP>(bt[i].w, bt[i].h);
+        cls[i] = blockop_class<P, OP>(bt[i].w, bt[i].h, bt[i].dst_stride);
         if (cls[i] < 0) return -cls[i];
     }
     BatchGroup proto{};
@@ -224,7 +264,7 @@ static int grouped_blockop(int depth, int count, const x265amd_block_batch* bt, 
             s.b = b.b; s.boff = b.b_off; s.sb = b.b_stride;
             s.w = b.w; s.h = b.h; s.n = b.n; s.param = b.param;
             const int uw = (cls[i] / 16) % 16, uh = cls[i] % 16;
-            s.jpl = cls[i] / 256;
+            s.jpl = (cls[i] & (kStagedBlock - 1)) / 256;
             s.lg = lanes_log2((b.w / uw) * (b.h / uh), 1);
         },
         [&](int c, const BatchGroup& g, uint32_t blocks) { return launch_blockop<P, OP>(c, g, blocks, st); });

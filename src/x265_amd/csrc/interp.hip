@@ -324,31 +324,6 @@ __device__ __forceinline__ void vfilter_pk(const uint8_t* col, intptr_t ss, cons
     }
 }
 
-// Write-back of a wavefront's outputs staged in LDS in destination order (the
-// STG kernels below): job jl of the wavefront (lanes jl << lg ...) owns bytes
-// [jl wh, (jl + 1) wh) of the staging area, wh a power of two >= 16.  Chunk c
-// = bytes [16c, 16c + 16) of job 16c / wh goes to that job's destination,
-// whose pointer comes from the job's first lane; a store instruction covers
-// whole 64-byte segments of several jobs instead of one row piece per job.
-template <int WAVE_BYTES>
-__device__ __forceinline__ void stage_writeback(const uint8_t* wbase, const void* pd, int lg, int wh, int64_t wjob0,
-                                                int n)
-{
-    wave_sync();
-    const int lb = 31 - __builtin_clz(wh);                      // log2 of a job's bytes
-    const int nch = (64 >> lg) << (lb - 4);
-    const int l64 = threadIdx.x & 63;
-#pragma unroll
-    for (int i = 0; i < WAVE_BYTES / 16 / 64; i++)
-    {
-        const int c = l64 + 64 * i;
-        const int jl = (c << 4) >> lb;
-        const long long dp = __shfl((long long)(intptr_t)pd, jl << lg, 64);
-        if (c < nch && wjob0 + jl < n)
-            stu<uint4>((uint8_t*)(intptr_t)dp + ((c << 4) & (wh - 1)), *(const uint4*)(wbase + (c << 4)));
-    }
-}
-
 // Grouped launches (common.h): a = src, d = dst, b = per-job coeffIdx
 // (uint8), param = is_row_ext.
 //

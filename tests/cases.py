@@ -310,7 +310,8 @@ def case_intra(kind: int, size: int, depth: int, n: int, seed: int, mode: int = 
                 dict(d=d, ds=ds, doff=doff, nb=nb.data, nbo=nbo, f=filt.data, fo=fo, mode=modes, bf=bf), ["d"])
 
 
-def case_blockop(op: int, w: int, h: int, depth: int, n: int, seed: int) -> Case:
+def case_blockop(op: int, w: int, h: int, depth: int, n: int, seed: int, compact: bool = False) -> Case:
+    """compact: shuffled stride-w destination slots, as case_interp"""
     det = Det(seed)
     pmax = (1 << depth) - 1
     pdt = pixel_dtype(depth)
@@ -334,7 +335,10 @@ def case_blockop(op: int, w: int, h: int, depth: int, n: int, seed: int) -> Case
         b = make_plane(det, pdt, stride, h + 8, 0, pmax, 0, pmax)
     aoff = job_offsets(det, a, n, w, h, 2)
     boff = job_offsets(det, b, n, w, h, 2)
-    if op in (CPY2D1D_SHL, CPY2D1D_SHR, TRANSPOSE):
+    if compact:
+        d, ds, _ = out_slots(n + 5, w, h, np.int16 if d16 else pdt, stride=w, pad=0)
+        doff = (np.argsort(det.ints(0, 1 << 30, n + 5), kind="stable")[:n] * (w * h)).astype(np.int64)
+    elif op in (CPY2D1D_SHL, CPY2D1D_SHR, TRANSPOSE):
         d, ds, doff = out_slots(n, w, h, np.int16 if d16 else pdt, stride=w, pad=0)
     else:
         d, ds, doff = out_slots(n, w, h, np.int16 if d16 else pdt)
@@ -355,7 +359,7 @@ def case_blockop(op: int, w: int, h: int, depth: int, n: int, seed: int) -> Case
     else:
         param = 0
     bdata = b.data if hasattr(b, "data") and not isinstance(b, np.ndarray) else b
-    return Case("blockop", dict(op=op, w=w, h=h, depth=depth, n=n, seed=seed),
+    return Case("blockop", dict(op=op, w=w, h=h, depth=depth, n=n, seed=seed, **({"compact": True} if compact else {})),
                 dict(d=d, ds=ds, doff=doff, a=a, sa=sa, aoff=aoff, b=bdata, sb=stride, boff=boff, param=param), ["d"])
 
 

@@ -92,6 +92,27 @@ def test_gpu_interp_compact_destinations(prims, oracle_libs, depth):
     assert not bad, bad[:10]
 
 
+@pytest.mark.parametrize("depth", [8, 10])
+def test_gpu_blockop_compact_destinations(prims, oracle_libs, depth):
+    """every block op into compact, shuffled stride-w slots: the LDS-staged write-back
+    (blockops.hip k_blockop STG) for power-of-two shapes, direct stores otherwise; 77 jobs
+    leave a partial last wavefront and partial two-job lane groups"""
+    from cases import (ADD_PS, ADDAVG, BLOCKFILL, COPY_PP, COPY_PS, COPY_SP, COPY_SS, CPY1D2D_SHL, CPY2D1D_SHR,
+                       PIXELAVG, SUB_PS, TRANSPOSE, case_blockop)
+    orc = CpuOracle("oracle", depth)
+    bad = []
+    for op in (SUB_PS, ADD_PS, ADDAVG, PIXELAVG, COPY_PP, COPY_SP, COPY_PS, COPY_SS, BLOCKFILL, CPY2D1D_SHR,
+               CPY1D2D_SHL, TRANSPOSE):
+        for (w, h) in ((4, 4), (8, 8), (16, 16), (32, 32), (64, 64), (16, 8), (8, 32), (12, 16), (16, 4), (8, 2)):
+            if op in (TRANSPOSE, CPY2D1D_SHR, CPY1D2D_SHL, BLOCKFILL) and w != h:
+                continue
+            c = case_blockop(op, w, h, depth, 77, seed_of("gbc", op, depth, w, h), compact=True)
+            a, b = run_gpu(c, prims), run_cpu(c, orc)
+            if not np.array_equal(a["d"], b["d"]):
+                bad.append(c.key())
+    assert not bad, bad[:10]
+
+
 CENSUSES = [("census_1080p_medium.json", 1920, 1080, 8), ("census_2160p_medium.json", 3840, 2160, 8),
             ("census_2160p_slow.json", 3840, 2160, 8), ("census_2160p_medium_main10.json", 3840, 2160, 10)]
 
