@@ -202,18 +202,22 @@ static int blockop_class(int w, int h, int64_t ds)
     constexpr int esz = OP == X265AMD_BLOCKFILL ? 2 : (int)sizeof(A) + (TWO ? (int)sizeof(B) : 0);
     const int uw = (w % 8 == 0) ? 8 : (w % 4 == 0) ? 4 : 2;
     const int want = std::max(1, 32 / (uw * esz));
-    const int uh = (want >= 4 && h % 4 == 0) ? 4 : (want >= 2 && h % 2 == 0) ? 2 : 1;
+    int uh = (want >= 4 && h % 4 == 0) ? 4 : (want >= 2 && h % 2 == 0) ? 2 : 1;
     // two jobs per lane group for the streaming ops (measured +2-10% on 8x8..64x64)
     const int jpl = ((TWO || OP == X265AMD_COPY_PP) && uw == 8) ? 2 : 1;
-    int cls = jpl * 256 + uw * 16 + uh;
     // compact destination: stage the outputs in LDS when every lane holds exactly one unit of
-    // >= 16 bytes (X265AMD_BLOCK_STAGE=0 disables)
+    // >= 16 bytes, two-row units for the one-row 8-byte ones (add_ps, addAvg at 8 bit)
+    // (X265AMD_BLOCK_STAGE=0 disables)
     static const bool stage = !getenv("X265AMD_BLOCK_STAGE") || atoi(getenv("X265AMD_BLOCK_STAGE"));
     typedef typename OpTypes<P, OP>::d D;
     const bool p2 = (w & (w - 1)) == 0 && (h & (h - 1)) == 0;
-    if (stage && p2 && ds == w && uw * uh * (int)sizeof(D) >= 16 && (w / uw) * (h / uh) <= 64)
-        cls |= kStagedBlock;
-    return cls;
+    bool stg = false;
+    if (stage && p2 && ds == w)
+    {
+        if (uw * uh * (int)sizeof(D) == 8 && uh == 1 && h % 2 == 0 && (w / uw) * (h / 2) <= 64) uh = 2;
+        stg = uw * uh * (int)sizeof(D) >= 16 && (w / uw) * (h / uh) <= 64;
+    }
+    return jpl * 256 + uw * 16 + uh + (stg ? kStagedBlock : 0);
 }
 
 template <typename P, int OP>

@@ -347,15 +347,15 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_interp(const BatchGroup g)
     {
         // the whole wavefront stays for the write-back; lanes past the batch compute a copy of
         // the last job into LDS that is never written out
-        static_assert(sizeof(D) == 1 && sizeof(S) == 1 && (OP == X265AMD_HPP || OP == X265AMD_VPP), "staging");
+        static_assert(OP != X265AMD_HVPP && UW * UH * sizeof(D) >= 16 && UW * UH * sizeof(D) <= 128, "staging");
         if (wjob0 >= n) return;
         if (job >= n) job = n - 1;
     }
     else if (job >= n)
         return;
-    constexpr int STG_WAVE = STG ? 64 * UW * UH : 16;          // staged bytes per wavefront
+    constexpr int STG_WAVE = STG ? 64 * UW * UH * (int)sizeof(D) : 16;          // staged bytes per wavefront
     __shared__ uint4 stg_lds[STG ? X265AMD_BLOCK / 64 * STG_WAVE / 16 : 1];
-    uint8_t* const stg = (uint8_t*)stg_lds + (threadIdx.x >> 6) * STG_WAVE + ((threadIdx.x & 63) >> lg) * w * h;
+    D* const stg = (D*)((uint8_t*)stg_lds + (threadIdx.x >> 6) * STG_WAVE) + ((threadIdx.x & 63) >> lg) * w * h;
 
     const IfConst K(g.depth);
     const S* ps = (const S*)sub.a + sub.aoff[job];
@@ -395,14 +395,14 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_interp(const BatchGroup g)
                 else hfilter<P, TAPS, UW>((const P*)ps + (y0 + r) * ss + x, c, sum);
                 if constexpr (DOT && OP == X265AMD_HPP)
                 {
-                    store_pp8<UW>(STG ? stg + (y0 + r) * w + x : (uint8_t*)pd + (y0 + r) * ds + x, sum);
+                    store_pp8<UW>((uint8_t*)(STG ? stg + (y0 + r) * w + x : pd + (y0 + r) * ds + x), sum);
                     continue;
                 }
 #pragma unroll
                 for (int i = 0; i < UW; i++)
                     o[i] = OP == X265AMD_HPP ? clampp((sum[i] + 32) >> 6, K.maxv)
                                              : (int)(int16_t)((sum[i] + K.ps_off) >> K.ps_shift);
-                store_row<D, UW>(pd + (y0 + r) * ds + x, o);
+                store_row<D, UW>(STG ? stg + (y0 + r) * w + x : pd + (y0 + r) * ds + x, o);
             }
         }
         else if constexpr (OP == X265AMD_P2S)
@@ -414,7 +414,7 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_interp(const BatchGroup g)
                 load_row<P, UW>((const P*)ps + (y0 + r) * ss + x, v);
 #pragma unroll
                 for (int i = 0; i < UW; i++) v[i] = (int)(int16_t)((int16_t)(v[i] << K.p2s_shift) - 8192);
-                store_row<D, UW>(pd + (y0 + r) * ds + x, v);
+                store_row<D, UW>(STG ? stg + (y0 + r) * w + x : pd + (y0 + r) * ds + x, v);
             }
         }
         else  // vertical: VPP, VPS, VSP, VSS
@@ -443,7 +443,7 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_interp(const BatchGroup g)
                             v = v - (s16x2)8192;       // ps at 8-bit: shift 0, offset -IF_INTERNAL_OFFS
                         o[p] = __builtin_bit_cast(uint32_t, v);
                     }
-                    D* out = STG ? (D*)(stg + (y0 + r) * w + x) : pd + (y0 + r) * ds + x;
+                    D* out = STG ? stg + (y0 + r) * w + x : pd + (y0 + r) * ds + x;
                     if constexpr (OP == X265AMD_VPP)
                     {
                         // two pairs -> four pixels per dword
@@ -492,7 +492,7 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_interp(const BatchGroup g)
             {
                 if constexpr (DOT && OP == X265AMD_VPP)
                 {
-                    store_pp8<UW>((uint8_t*)pd + (y0 + r) * ds + x, acc[r]);
+                    store_pp8<UW>((uint8_t*)(STG ? stg + (y0 + r) * w + x : pd + (y0 + r) * ds + x), acc[r]);
                     continue;
                 }
                 int o[UW];
@@ -505,12 +505,13 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_interp(const BatchGroup g)
                     else if constexpr (OP == X265AMD_VSP) o[i] = clampp((s + K.sp_off) >> K.sp_shift, K.maxv);
                     else o[i] = (int)(int16_t)(s >> 6);
                 }
-                store_row<D, UW>(pd + (y0 + r) * ds + x, o);
+                store_row<D, UW>(STG ? stg + (y0 + r) * w + x : pd + (y0 + r) * ds + x, o);
             }
         }
     }
     if constexpr (STG)
-        stage_writeback<STG_WAVE>((const uint8_t*)stg_lds + (threadIdx.x >> 6) * STG_WAVE, pd, lg, w * h, wjob0, n);
+        stage_writeback<STG_WAVE>((const uint8_t*)stg_lds + (threadIdx.x >> 6) * STG_WAVE, pd, lg,
+                                  w * h * (int)sizeof(D), wjob0, n);
 }
 
 // hv_pp in two on-chip passes: the horizontal int16 intermediate of the
@@ -785,9 +786,10 @@ static int launch_interp(int cls, const BatchGroup& g, uint32_t blocks, hipStrea
     if constexpr (OP == X265AMD_HVPP)
         for (int i = 0; i < g.count; i++)
             lds = std::max(lds, (size_t)(X265AMD_BLOCK >> g.s[i].lg) * (g.s[i].h + 7) * g.s[i].w * sizeof(int16_t));
-    constexpr bool STGOK = sizeof(S) == 1 && sizeof(D) == 1 && (OP == X265AMD_HPP || OP == X265AMD_VPP);
+    constexpr bool STGOK = OP != X265AMD_HVPP;
 #define L(UW, UH) \
-    if constexpr (STGOK && UW * UH >= 16 && UW >= 4 && (UH <= 8 || PK8)) \
+    if constexpr (STGOK && UW * UH * sizeof(D) >= 16 && UW * UH * sizeof(D) <= 128 && \
+                  (UW >= 4 || TAPS == 4 || (OP != X265AMD_HPP && OP != X265AMD_HPS)) && (UH <= 8 || PK8)) \
         if (cls == (UW * 32 + UH | kStaged)) \
         { \
             hipLaunchKernelGGL((k_interp<P, S, D, OP, TAPS, UW, UH, true>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, g); \
@@ -833,14 +835,15 @@ static int grouped_interp(int depth, int count, const x265amd_interp_batch* bt, 
             if (sizeof(P) == 1 && bt[i].w % 8 == 0 && hv_sw != 4) cls[i] = kHvppStream;
             else if (bt[i].w % 4 == 0) cls[i] = kHvppStream4;
         }
-        // 8-bit hpp / vpp into a compact destination (stride = width): stage the outputs in LDS
-        // when every lane holds exactly one unit of >= 16 bytes (X265AMD_INTERP_STAGE=0 disables)
+        // a compact destination (stride = width, power-of-two block): stage the outputs in LDS
+        // when every lane holds exactly one unit of 16..128 bytes (X265AMD_INTERP_STAGE=0 disables)
         static const bool stage = !getenv("X265AMD_INTERP_STAGE") || atoi(getenv("X265AMD_INTERP_STAGE"));
-        if (stage && sizeof(S) == 1 && sizeof(D) == 1 && (OP == X265AMD_HPP || OP == X265AMD_VPP))
+        if (stage && OP != X265AMD_HVPP && !(OP == X265AMD_HPS && bt[i].is_row_ext))
         {
             const int w = bt[i].w, h = bt[i].h, uw = cls[i] / 32, uh = cls[i] % 32;
+            const int ub = uw * uh * (int)sizeof(D);
             const bool p2 = (w & (w - 1)) == 0 && (h & (h - 1)) == 0;
-            if (p2 && bt[i].dst_stride == w && uw * uh >= 16 && uw >= 4 && (w / uw) * (h / uh) <= 64)
+            if (p2 && bt[i].dst_stride == w && ub >= 16 && ub <= 128 && (w / uw) * (h / uh) <= 64)
                 cls[i] |= kStaged;
         }
         if (stage && OP == X265AMD_HVPP && cls[i] == kHvppStream)

@@ -74,15 +74,16 @@ def test_gpu_matches_oracle_random(prims, oracle_libs, depth):
 
 @pytest.mark.parametrize("depth", [8, 10])
 def test_gpu_interp_compact_destinations(prims, oracle_libs, depth):
-    """hpp / vpp / hv_pp into census-style compact slots (stride = width): the 8-bit LDS-staged
+    """every interp op into census-style compact slots (stride = width): the 8-bit LDS-staged
     write-back (interp.hip k_interp / k_hvpp_stream STG) for power-of-two shapes, the direct
     stores otherwise;
     77 jobs leave a partial last wavefront, the slot order is shuffled and five slots stay
     untouched"""
     orc = CpuOracle("oracle", depth)
     bad = []
-    for op in (HPP, VPP, HVPP):
-        for taps in ((8,) if op == HVPP else (4, 8)):
+    from cases import HPS, P2S, VPS, VSP, VSS
+    for op in (HPP, HPS, VPP, VPS, VSP, VSS, P2S, HVPP):
+        for taps in ((8,) if op == HVPP else (4,) if op == P2S else (4, 8)):
             for (w, h) in ((4, 4), (8, 4), (4, 8), (8, 8), (16, 16), (32, 32), (64, 64), (16, 8), (8, 32), (32, 16),
                            (16, 64), (64, 16), (12, 16), (24, 32), (16, 4)):
                 c = case_interp(op, taps, w, h, depth, 77, seed_of("gc", op, taps, depth, w, h), compact=True)
