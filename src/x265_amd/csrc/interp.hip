@@ -610,12 +610,7 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_hvpp(const BatchGroup g)
 //
 // STG (8 bit, compact destinations, power-of-two w and h <= 16): the output
 // rows go to wave-private LDS and leave through stage_writeback.
-//
-// RB > 0: the block's rows are split into bands of RB output rows, one lane per
-// (strip, band), each band walking its own RB + 7 source rows — more lanes per job
-// and shorter dependent row chains for the horizontal pass's (RB + 7) / RB rows of
-// work per output row instead of (h + 7) / h.
-template <typename P, int SW, bool STG = false, int RB = 0>
+template <typename P, int SW, bool STG = false>
 __global__ __launch_bounds__(X265AMD_BLOCK) void k_hvpp_stream(const BatchGroup g)
 {
     const uint32_t gb = xcd_block();
@@ -636,7 +631,7 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_hvpp_stream(const BatchGroup 
         if (wjob0 >= n) return;
         if (job >= n) job = n - 1;
     }
-    else if (job >= n || lane >= (w / SW) * (RB ? h / RB : 1))
+    else if (job >= n || SW * lane >= w)
         return;
     uint8_t* const stg = (uint8_t*)stg_lds + (threadIdx.x >> 6) * STG_WAVE + ((threadIdx.x & 63) >> lg) * w * h;
     const IfConst K(g.depth);
@@ -649,12 +644,10 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_hvpp_stream(const BatchGroup 
     s16x2 cv[4];
 #pragma unroll
     for (int k = 0; k < 4; k++) cv[k] = s16x2{ (short)cy[2 * k], (short)cy[2 * k + 1] };
-    const int nstrip = w / SW;
-    const int x0 = SW * (RB ? lane % nstrip : lane);
-    const int yb = RB ? (lane / nstrip) * RB : 0;        // first output row of the lane's band
-    const P* ps = (const P*)sub.a + sub.aoff[job] + (intptr_t)(yb - 3) * ss + x0;
-    P* pd = (P*)sub.d + sub.doff[job] + (STG ? 0 : x0 + (intptr_t)yb * ds);
-    const int R = (RB ? RB : h) + 7;
+    const int x0 = SW * lane;
+    const P* ps = (const P*)sub.a + sub.aoff[job] - 3 * ss + x0;
+    P* pd = (P*)sub.d + sub.doff[job] + (STG ? 0 : x0);
+    const int R = h + 7;
     // 8 bit: I = S - 8192 exactly (shift 0, |S| <= 88 * 255), and the sp offset adds 8192 * 64
     // back, so the raw sums S are paired and the output is (t + 2048) >> 12
     auto inter = [&](const P* row, int (&I)[SW]) {
@@ -705,7 +698,7 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_hvpp_stream(const BatchGroup 
                     else
                         o[x] = clampp((t + K.sp_off) >> K.sp_shift, K.maxv);
                 }
-                if constexpr (STG) store_row<P, SW>((P*)(stg + (yb + y) * w + x0), o);
+                if constexpr (STG) store_row<P, SW>((P*)(stg + y * w + x0), o);
                 else store_row<P, SW>(pd + (intptr_t)y * ds, o);
             }
         }
@@ -778,24 +771,17 @@ template <typename P, typename S, typename D, int OP, int TAPS>
 static int launch_interp(int cls, const BatchGroup& g, uint32_t blocks, hipStream_t st)
 {
     if constexpr (OP == X265AMD_HVPP)
-    {
-        const int base = cls & ((1 << 12) - 1) & ~kStaged, rb = cls >> 12;
-        const bool stg = cls & kStaged;
-        if (base == kHvppStream || base == kHvppStream4)
+        if (cls == kHvppStream || cls == kHvppStream4 || cls == (kHvppStream | kStaged))
         {
-#define HS(SW, S, RB) \
-    if ((base == (SW == 8 ? kHvppStream : kHvppStream4)) && stg == S && rb == RB) \
-    { \
-        if constexpr (!S || sizeof(P) == 1) \
-            hipLaunchKernelGGL((k_hvpp_stream<P, SW, S, RB>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, g); \
-        return (int)hipGetLastError(); \
-    }
-            HS(8, false, 0) HS(8, true, 0) HS(4, false, 0) HS(4, true, 0)
-            HS(8, false, 4) HS(8, true, 4) HS(8, true, 8) HS(4, true, 8) HS(8, false, 8)
-#undef HS
-            return X265AMD_EINVAL;
+            if (cls == kHvppStream) hipLaunchKernelGGL((k_hvpp_stream<P, 8>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, g);
+            else if (cls == (kHvppStream | kStaged))
+            {
+                if constexpr (sizeof(P) == 1)
+                    hipLaunchKernelGGL((k_hvpp_stream<P, 8, true>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, g);
+            }
+            else hipLaunchKernelGGL((k_hvpp_stream<P, 4>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, g);
+            return (int)hipGetLastError();
         }
-    }
     size_t lds = 0;
     if constexpr (OP == X265AMD_HVPP)
         for (int i = 0; i < g.count; i++)
@@ -860,18 +846,12 @@ static int grouped_interp(int depth, int count, const x265amd_interp_batch* bt, 
             if (p2 && bt[i].dst_stride == w && ub >= 16 && ub <= 128 && (w / uw) * (h / uh) <= 64)
                 cls[i] |= kStaged;
         }
-        if (stage && OP == X265AMD_HVPP && (cls[i] == kHvppStream || (sizeof(P) == 1 && cls[i] == kHvppStream4)))
+        if (stage && OP == X265AMD_HVPP && cls[i] == kHvppStream)
         {
             const int w = bt[i].w, h = bt[i].h;
             if ((w & (w - 1)) == 0 && (h & (h - 1)) == 0 && h <= 16 && w * h >= 16 && bt[i].dst_stride == w)
                 cls[i] |= kStaged;
         }
-        // row bands of the streaming hv_pp (X265AMD_HVPP_RB=4|8: lanes per job x h / RB; tuning)
-        static const int hv_rb = getenv("X265AMD_HVPP_RB") ? atoi(getenv("X265AMD_HVPP_RB")) : 0;
-        if (OP == X265AMD_HVPP && (hv_rb == 4 || hv_rb == 8) && bt[i].h > hv_rb && bt[i].h % hv_rb == 0 &&
-            ((cls[i] & ~kStaged) == kHvppStream || cls[i] == (kHvppStream4 | kStaged)) &&
-            (hv_rb == 8 || (cls[i] & ~kStaged) == kHvppStream) && (bt[i].w / (cls[i] / 32 % 64 == 8 ? 8 : 4)) * (bt[i].h / hv_rb) <= 64)
-            cls[i] |= hv_rb << 12;
     }
     BatchGroup proto{};
     proto.depth = depth;
@@ -886,12 +866,8 @@ static int grouped_interp(int depth, int count, const x265amd_interp_batch* bt, 
             s.param = OP == X265AMD_HPS ? b.is_row_ext : 0;
             const int uw = (cls[i] & (kStaged - 1)) / 32, uh = cls[i] % 32;
             if constexpr (OP == X265AMD_HVPP)
-            {
-                const int base = cls[i] & ((1 << 12) - 1) & ~kStaged, rb = cls[i] >> 12;
-                const int bands = rb ? b.h / rb : 1;
-                s.lg = base == kHvppStream ? lanes_log2(b.w / 8 * bands, 1)
-                       : base == kHvppStream4 ? lanes_log2(b.w / 4 * bands, 1) : hvpp_lg(b.w, b.h, uw, uh);
-            }
+                s.lg = (cls[i] & ~kStaged) == kHvppStream ? lanes_log2(b.w / 8, 1)
+                       : cls[i] == kHvppStream4 ? lanes_log2(b.w / 4, 1) : hvpp_lg(b.w, b.h, uw, uh);
             else
             {
                 const int rows = (OP == X265AMD_HPS && s.param) ? b.h + TAPS - 1 : b.h;
