@@ -16,9 +16,12 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OBJ = os.path.join(HERE, "_obj")
 LIB = os.path.join(HERE, "libx265amd.so")
+# MFMA results in VGPRs, not AGPRs (no v_accvgpr_read per accumulator element; measured with the
+# MFMA transforms, profiles/r03/tr_split_ab.txt)
+MFMA_VGPR = ["-mllvm", "-amdgpu-mfma-vgpr-form"]
 # (source, object, extra flags): the EncoderPrimitives provider is built once per bit depth
-SOURCES = [("pixel.hip", "pixel.o", []), ("interp.hip", "interp.o", []), ("transform.hip", "transform.o", []),
-           ("intra.hip", "intra.o", []), ("blockops.hip", "blockops.o", []), ("tu.hip", "tu.o", []), ("lowres.hip", "lowres.o", []), ("me.hip", "me.o", []), ("loopfilter.hip", "loopfilter.o", []),
+SOURCES = [("pixel.hip", "pixel.o", []), ("interp.hip", "interp.o", []), ("transform.hip", "transform.o", MFMA_VGPR),
+           ("intra.hip", "intra.o", []), ("blockops.hip", "blockops.o", []), ("tu.hip", "tu.o", MFMA_VGPR), ("lowres.hip", "lowres.o", []), ("me.hip", "me.o", []), ("loopfilter.hip", "loopfilter.o", []),
            ("runtime.hip", "runtime.o", []), ("lookahead.cpp", "lookahead.o", []),
            ("schedule.cpp", "schedule.o", []), ("exchange.cpp", "exchange.o", []),
            ("provider.cpp", "provider8.o", ["-DX265_DEPTH=8"]),

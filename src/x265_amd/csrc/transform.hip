@@ -260,10 +260,15 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_trN(int n, int depth,
 // matrix cores with FP32 accumulation:  forward  Dst = T * (Src * T^T)^T,
 // inverse  Res = (C^T * T)^T * T  (each stage rounded / wrapped or clipped to
 // int16 exactly as partialButterfly*[Inverse]).  Exactness: every int16
-// operand is split x = hi * 2048 + lo with lo in [0, 2047] and hi in
-// [-16, 15] — both exact in f16 — and the two halves accumulate in separate
+// operand is split x = hi * 1024 + lo with lo in [0, 1023] and hi in
+// [-32, 31] — both exact in f16 — and the two halves accumulate in separate
 // FP32 tiles whose partial sums stay integers below 2^24 (|lo * t| summed over
-// K = 32 is < 2047 * 90 * 32), so hi * 2048 + lo reproduces the int32 sum.
+// K = 32 is < 1023 * 90 * 32), so hi * 1024 + lo reproduces the int32 sum.
+// The split works on packed int16 pairs with f16 bit patterns (transform1d.h
+// split10: v_and_or / packed shift / xor / packed f16 add, no conversions), and
+// the MFMA results stay in VGPRs (-amdgpu-mfma-vgpr-form, build.py): together
+// 499 -> 388 VALU instructions per 32x32 forward iteration, dct / idct 16 / 32
+// 0.46-0.52 -> 0.54-0.60 of HBM peak (profiles/r03/tr_split_ab.txt).
 // The first stage's accumulator tile feeds the second MFMA straight from
 // registers (column on the lane, rows in the registers: the second product
 // sums over its row index), so no LDS is used.
@@ -327,19 +332,13 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_tr32_mfma(int n, int depth,
         if (job + step < n) fetch(job + step);
         // ---- stage 1: forward U = Src * T^T (A = source rows, 16-byte row loads);
         //      inverse M1 = C^T * T (A = coefficient columns, staged through the tile)
-        int x[2][8];
+        uint32_t x[2][4];                            // int16 pairs in k order
         if constexpr (FWD)
         {
 #pragma unroll
             for (int st = 0; st < 2; st++)
             {
-                const uint32_t wv[4] = { cx[st].x, cx[st].y, cx[st].z, cx[st].w };
-#pragma unroll
-                for (int q = 0; q < 4; q++)
-                {
-                    x[st][2 * q] = (int16_t)(wv[q] & 0xffff);
-                    x[st][2 * q + 1] = (int16_t)(wv[q] >> 16);
-                }
+                x[st][0] = cx[st].x; x[st][1] = cx[st].y; x[st][2] = cx[st].z; x[st][3] = cx[st].w;
             }
         }
         else
@@ -350,14 +349,15 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_tr32_mfma(int n, int depth,
 #pragma unroll
             for (int st = 0; st < 2; st++)
 #pragma unroll
-                for (int j = 0; j < 8; j++) x[st][j] = T[(16 * st + 8 * h + j) * 32 + r];
+                for (int q = 0; q < 4; q++)
+                    x[st][q] = pack16(T[(16 * st + 8 * h + 2 * q) * 32 + r], T[(16 * st + 8 * h + 2 * q + 1) * 32 + r]);
         }
         f32x16 lo1 = {}, hi1 = {};
 #pragma unroll
         for (int st = 0; st < 2; st++)
         {
             f16x8 xl, xh;
-            split_hl<8>(x[st], xl, xh);
+            split10<4>(x[st], xl, xh);
             lo1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(xl, t1[st], lo1, 0, 0, 0);
             hi1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(xh, t1[st], hi1, 0, 0, 0);
         }
@@ -365,7 +365,7 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_tr32_mfma(int n, int depth,
 #pragma unroll
         for (int i = 0; i < 16; i++)
         {
-            const int a = (int)hi1[i] * 2048 + (int)lo1[i];
+            const int a = (int)hi1[i] * 1024 + (int)lo1[i];
             v[i] = FWD ? fwd_round(a, sh1) : inv_round(a, sh1);
         }
         // ---- stage 2 from registers: forward Dst = T * U' (U' as B); inverse Res = M1'^T * T (M1' as A)
@@ -373,11 +373,11 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_tr32_mfma(int n, int depth,
 #pragma unroll
         for (int st = 0; st < 2; st++)
         {
-            int y[8];
+            uint32_t y[4];
 #pragma unroll
-            for (int j = 0; j < 8; j++) y[j] = v[8 * st + j];
+            for (int q = 0; q < 4; q++) y[q] = pack16(v[8 * st + 2 * q], v[8 * st + 2 * q + 1]);
             f16x8 xl, xh;
-            split_hl<8>(y, xl, xh);
+            split10<4>(y, xl, xh);
             if constexpr (FWD)
             {
                 lo2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(t2[st], xl, lo2, 0, 0, 0);
@@ -393,7 +393,7 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_tr32_mfma(int n, int depth,
 #pragma unroll
         for (int i = 0; i < 16; i++)
         {
-            const int a = (int)hi2[i] * 2048 + (int)lo2[i];
+            const int a = (int)hi2[i] * 1024 + (int)lo2[i];
             T[((i & 3) + 8 * (i >> 2) + 4 * h) * 32 + r] = (int16_t)(FWD ? fwd_round(a, sh2) : inv_round(a, sh2));
         }
         wave_sync();
@@ -451,32 +451,30 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_tr16_mfma(int n, int depth,
             d[b] = dst + doff[job0 + b < n ? job0 + b : job0];
         }
         if (job0 + step < n) fetch(job0 + step);
-#pragma unroll
-        for (int b = 0; b < JB; b++)
+        if constexpr (!FWD)
         {
-            int16_t* T = tile[w][b];
-            if constexpr (FWD)
-            {
-                x[b][0] = (int16_t)(cx[b].x & 0xffff);
-                x[b][1] = (int16_t)(cx[b].x >> 16);
-                x[b][2] = (int16_t)(cx[b].y & 0xffff);
-                x[b][3] = (int16_t)(cx[b].y >> 16);
-            }
-            else
-                stu<uint2>(&T[io_row * 16 + io_col], cx[b]);
+#pragma unroll
+            for (int b = 0; b < JB; b++) stu<uint2>(&tile[w][b][io_row * 16 + io_col], cx[b]);
+            wave_sync();
         }
-        if constexpr (!FWD) wave_sync();
         f32x4 lo[JB], hi[JB];
 #pragma unroll
         for (int b = 0; b < JB; b++)
         {
-            if constexpr (!FWD)
+            uint32_t u[2];
+            if constexpr (FWD)
+            {
+                u[0] = cx[b].x;
+                u[1] = cx[b].y;
+            }
+            else
             {
 #pragma unroll
-                for (int j = 0; j < 4; j++) x[b][j] = tile[w][b][(4 * q + j) * 16 + r];
+                for (int p = 0; p < 2; p++)
+                    u[p] = pack16(tile[w][b][(4 * q + 2 * p) * 16 + r], tile[w][b][(4 * q + 2 * p + 1) * 16 + r]);
             }
             f16x4 xl, xh;
-            split_hl<4>(x[b], xl, xh);
+            split10<2>(u, xl, xh);
             lo[b] = __builtin_amdgcn_mfma_f32_16x16x16f16(xl, t, f32x4{}, 0, 0, 0);
             hi[b] = __builtin_amdgcn_mfma_f32_16x16x16f16(xh, t, f32x4{}, 0, 0, 0);
         }
@@ -486,11 +484,12 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_tr16_mfma(int n, int depth,
 #pragma unroll
             for (int i = 0; i < 4; i++)
             {
-                const int a = (int)hi[b][i] * 2048 + (int)lo[b][i];
+                const int a = (int)hi[b][i] * 1024 + (int)lo[b][i];
                 x[b][i] = FWD ? fwd_round(a, sh1) : inv_round(a, sh1);
             }
+            const uint32_t u[2] = { pack16(x[b][0], x[b][1]), pack16(x[b][2], x[b][3]) };
             f16x4 xl, xh;
-            split_hl<4>(x[b], xl, xh);
+            split10<2>(u, xl, xh);
             if constexpr (FWD)
             {
                 lo[b] = __builtin_amdgcn_mfma_f32_16x16x16f16(t, xl, f32x4{}, 0, 0, 0);
@@ -509,7 +508,7 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_tr16_mfma(int n, int depth,
 #pragma unroll
             for (int i = 0; i < 4; i++)
             {
-                const int a = (int)hi[b][i] * 2048 + (int)lo[b][i];
+                const int a = (int)hi[b][i] * 1024 + (int)lo[b][i];
                 T[(4 * q + i) * 16 + r] = (int16_t)(FWD ? fwd_round(a, sh2) : inv_round(a, sh2));
             }
             wave_sync();

@@ -117,4 +117,52 @@ __device__ __forceinline__ void split_hl(const int (&x)[K], V& lo, V& hi)
     }
 }
 
+// The same split on packed int16 pairs (x0 | x1 << 16) with 10-bit halves, built from
+// f16 bit patterns instead of conversions: 0x6400 | (x & 1023) is the f16 1024 + lo (one
+// v_and_or per pair) and ((x as uint16) >> 10) ^ 0x6420 is the f16 1056 + hi
+// (0x6400 | ((x >> 10) + 32): a packed shift and a xor per pair); one packed f16 add per
+// pair removes the 1024 / 1056 offsets exactly, leaving lo in [0, 1023] and hi in [-32, 31]
+// (x = 1024·hi + lo), so an MFMA sum over them stays as small as split_hl's.
+typedef unsigned short u16x2v __attribute__((ext_vector_type(2)));
+typedef _Float16 f16x2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t split10_lo(uint32_t u)
+{
+    uint32_t r;
+    asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(u), "v"(0x03FF03FFu), "v"(0x64006400u));
+    const f16x2v f = __builtin_bit_cast(f16x2v, r) - (f16x2v){(_Float16)1024, (_Float16)1024};
+    return __builtin_bit_cast(uint32_t, f);
+}
+__device__ __forceinline__ uint32_t split10_hi(uint32_t u)
+{
+    const u16x2v b = __builtin_bit_cast(u16x2v, u) >> (u16x2v){10, 10};
+    const f16x2v f = __builtin_bit_cast(f16x2v, __builtin_bit_cast(uint32_t, b) ^ 0x64206420u) -
+                     (f16x2v){(_Float16)1056, (_Float16)1056};
+    return __builtin_bit_cast(uint32_t, f);
+}
+// NP packed pairs -> 2·NP f16 operand lanes (element j = half j of the pairs)
+template <int NP, typename V>
+__device__ __forceinline__ void split10(const uint32_t (&u)[NP], V& lo, V& hi)
+{
+    uint32_t l[NP], h[NP];
+#pragma unroll
+    for (int i = 0; i < NP; i++)
+    {
+        l[i] = split10_lo(u[i]);
+        h[i] = split10_hi(u[i]);
+    }
+    lo = __builtin_bit_cast(V, l);
+    hi = __builtin_bit_cast(V, h);
+}
+// two int values (int16 range) packed as a pair
+__device__ __forceinline__ uint32_t pack16(int a, int b) { return __builtin_amdgcn_perm((uint32_t)b, (uint32_t)a, 0x05040100u); }
+// split10 of K int values (int16 range): packed in pairs first (one v_perm per pair)
+template <int K, typename V>
+__device__ __forceinline__ void split10i(const int (&x)[K], V& lo, V& hi)
+{
+    uint32_t u[K / 2];
+#pragma unroll
+    for (int i = 0; i < K / 2; i++) u[i] = pack16(x[2 * i], x[2 * i + 1]);
+    split10<K / 2>(u, lo, hi);
+}
+
 } // namespace x265amd

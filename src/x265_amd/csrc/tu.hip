@@ -501,13 +501,13 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_tu32_mfma(const TuArgs a)
         for (int st = 0; st < 2; st++)
         {
             f16x8 xl, xh;
-            split_hl<8>(x[st], xl, xh);
+            split10i<8>(x[st], xl, xh);
             lo = __builtin_amdgcn_mfma_f32_32x32x16_f16(xl, ft1[st], lo, 0, 0, 0);
             hi = __builtin_amdgcn_mfma_f32_32x32x16_f16(xh, ft1[st], hi, 0, 0, 0);
         }
         int v[16];
 #pragma unroll
-        for (int i = 0; i < 16; i++) v[i] = fwd_round((int)hi[i] * 2048 + (int)lo[i], fsh1);
+        for (int i = 0; i < 16; i++) v[i] = fwd_round((int)hi[i] * 1024 + (int)lo[i], fsh1);
         // ---- forward stage 2 from registers: Dst = T * U'
         lo = f32x16{};
         hi = f32x16{};
@@ -518,7 +518,7 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_tu32_mfma(const TuArgs a)
 #pragma unroll
             for (int k = 0; k < 8; k++) y[k] = v[8 * st + k];
             f16x8 xl, xh;
-            split_hl<8>(y, xl, xh);
+            split10i<8>(y, xl, xh);
             lo = __builtin_amdgcn_mfma_f32_32x32x16_f16(ft2[st], xl, lo, 0, 0, 0);
             hi = __builtin_amdgcn_mfma_f32_32x32x16_f16(ft2[st], xh, hi, 0, 0, 0);
         }
@@ -531,7 +531,7 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_tu32_mfma(const TuArgs a)
 #pragma unroll
         for (int i = 0; i < 16; i++)
         {
-            const int c = fwd_round((int)hi[i] * 2048 + (int)lo[i], fsh2);
+            const int c = fwd_round((int)hi[i] * 1024 + (int)lo[i], fsh2);
             const int tmp = (c < 0 ? -c : c) * qscale;
             int lvl = (tmp + qadd) >> qbits;
             cnt += lvl != 0;
@@ -588,12 +588,12 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_tu32_mfma(const TuArgs a)
 #pragma unroll
                     for (int k = 0; k < 8; k++) c[k] = clip16((Q[(16 * st + 8 * h + k) * 32 + r] * scale + dadd) >> dsh);
                     f16x8 xl, xh;
-                    split_hl<8>(c, xl, xh);
+                    split10i<8>(c, xl, xh);
                     lo = __builtin_amdgcn_mfma_f32_32x32x16_f16(xl, it1[st], lo, 0, 0, 0);
                     hi = __builtin_amdgcn_mfma_f32_32x32x16_f16(xh, it1[st], hi, 0, 0, 0);
                 }
 #pragma unroll
-                for (int i = 0; i < 16; i++) v[i] = inv_round((int)hi[i] * 2048 + (int)lo[i], 7);
+                for (int i = 0; i < 16; i++) v[i] = inv_round((int)hi[i] * 1024 + (int)lo[i], 7);
                 lo = f32x16{};
                 hi = f32x16{};
 #pragma unroll
@@ -603,14 +603,14 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_tu32_mfma(const TuArgs a)
 #pragma unroll
                     for (int k = 0; k < 8; k++) y[k] = v[8 * st + k];
                     f16x8 xl, xh;
-                    split_hl<8>(y, xl, xh);
+                    split10i<8>(y, xl, xh);
                     lo = __builtin_amdgcn_mfma_f32_32x32x16_f16(xl, it2[st], lo, 0, 0, 0);
                     hi = __builtin_amdgcn_mfma_f32_32x32x16_f16(xh, it2[st], hi, 0, 0, 0);
                 }
                 // residual (row (i&3) + 8(i>>2) + 4h, column r) -> LDS -> row segments
 #pragma unroll
                 for (int i = 0; i < 16; i++)
-                    Cs[((i & 3) + 8 * (i >> 2) + 4 * h) * 32 + r] = (int16_t)inv_round((int)hi[i] * 2048 + (int)lo[i], ish2);
+                    Cs[((i & 3) + 8 * (i >> 2) + 4 * h) * 32 + r] = (int16_t)inv_round((int)hi[i] * 1024 + (int)lo[i], ish2);
                 wave_sync();
                 load_row16<16>(&Cs[io_row * 32 + io_col], res);
             }
