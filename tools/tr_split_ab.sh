@@ -12,6 +12,6 @@ for rep in 1 2; do
 for v in old new; do
   unset X265AMD_LIB; test $v = new && export X265AMD_LIB=$NEWLIB
   echo "== $v"
-  timeout -k 10 200 python3 -u tools/kernel_roofline.py --only dct_16,dct_32,idct_16,idct_32 2>/dev/null | grep "{" | cut -c1-170 || exit 1
+  timeout -k 10 200 python3 -u tools/kernel_roofline.py --only ${ONLY:-dct_16,dct_32,idct_16,idct_32} 2>/dev/null | grep "{" | cut -c1-170 || exit 1
 done
 done
