@@ -15,21 +15,8 @@ primitive kernels use (SAD 64x64 for reads, copy_pp 64x64 for writes).
 from __future__ import annotations
 
 import argparse
-import csv
-import glob
 import json
 import os
-
-
-def dispatches(d: str, counter: str):
-    rows = []
-    for path in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
-        with open(path) as f:
-            for r in csv.DictReader(f):
-                if r["Counter_Name"] == counter and "x265amd::" in r["Kernel_Name"]:
-                    rows.append((int(r["Dispatch_Id"]), r["Kernel_Name"], float(r["Counter_Value"])))
-    rows.sort()
-    return rows
 
 
 def main():
@@ -41,29 +28,29 @@ def main():
     a = ap.parse_args()
     order = json.load(open(a.order))
     L, steps = order["launches"], order["steps"]
-    fe, wr = dispatches(a.fetch_dir, "FETCH_SIZE"), dispatches(a.write_dir, "WRITE_SIZE")
-    want = steps * len(L) + len(order["calibration"])
-    assert len(fe) == want and len(wr) == want, (len(fe), len(wr), want)
+    from pmc_segments import launch_groups
+
+    fe, cf = launch_groups(a.fetch_dir, order)
+    wr, cw = launch_groups(a.write_dir, order)
     kind_kernel = {"pixelcmp": "k_pixelcmp", "sad_multi": "k_sad_multi", "interp": ("k_interp", "k_hvpp"),
                    "blockop": "k_blockop", "transform": ("k_tr", "k_dst"), "quant": "k_quant",
                    "dequant": "k_dequant", "intra": "k_intra", "intra_filter": "k_intra_filter", "count": "k_count"}
     cal = order["calibration"]
-    cf, cw = fe[-len(cal):], wr[-len(cal):]
-    read_corr = cal[0]["read_bytes"] / (cf[0][2] * 1024)
-    write_corr = cal[1]["write_bytes"] / (cw[1][2] * 1024)
-    out = {"_units": "bytes per launch; hbm_bytes = FETCH_SIZE*1024*read_corr + WRITE_SIZE*1024*write_corr",
+    read_corr = cal[0]["read_bytes"] / (cf[0][2]["FETCH_SIZE"] * 1024)
+    write_corr = cal[1]["write_bytes"] / (cw[1][2]["WRITE_SIZE"] * 1024)
+    out = {"_units": "bytes per launch; hbm_bytes = FETCH_SIZE*1024*read_corr + WRITE_SIZE*1024*write_corr "
+                     "(summed over a launch's dispatches)",
            "_calibration": {"read_corr": round(read_corr, 4), "write_corr": round(write_corr, 4),
-                            "copy_read_corr_crosscheck": round(cal[1]["read_bytes"] / (cf[1][2] * 1024), 4),
+                            "copy_read_corr_crosscheck": round(cal[1]["read_bytes"] / (cf[1][2]["FETCH_SIZE"] * 1024), 4),
                             "kernels": [c["name"] for c in cal]}}
-    last_f = fe[(steps - 1) * len(L): steps * len(L)]
-    last_w = wr[(steps - 1) * len(L): steps * len(L)]
-    for g, f, w in zip(L, last_f, last_w):
+    for g, f, w in zip(L, fe, wr):
         kk = kind_kernel.get(g["kind"], "")
         kk = kk if isinstance(kk, tuple) else (kk,)
-        assert any(k in f[1] for k in kk), (g["name"], f[1])
-        hbm = f[2] * 1024 * read_corr + w[2] * 1024 * write_corr
-        out[g["name"]] = {"kernel": f[1].split("(")[0].replace("void ", ""), "fetch_kib": f[2], "write_kib": w[2],
-                          "hbm_bytes": int(hbm), "algorithmic_bytes": int(g["bytes"]),
+        assert any(k in f[0] for k in kk), (g["name"], f[0])
+        fk, wk = f[2]["FETCH_SIZE"], w[2]["WRITE_SIZE"]
+        hbm = fk * 1024 * read_corr + wk * 1024 * write_corr
+        out[g["name"]] = {"kernel": f[0].split("(")[0].replace("void ", ""), "dispatches": f[1], "fetch_kib": fk,
+                          "write_kib": wk, "hbm_bytes": int(hbm), "algorithmic_bytes": int(g["bytes"]),
                           "hbm_over_algorithmic": round(hbm / max(1.0, g["bytes"]), 3)}
     with open(a.out, "w") as fo:
         json.dump(out, fo, indent=1)

@@ -33,24 +33,13 @@ def main():
     a = ap.parse_args()
     order = json.load(open(a.order))
     L, steps = order["launches"], order["steps"]
-    rows = defaultdict(dict)
-    names = {}
-    for path in glob.glob(os.path.join(a.sq_dir, "**", "*counter_collection.csv"), recursive=True):
-        with open(path) as f:
-            for r in csv.DictReader(f):
-                if "x265amd::" not in r["Kernel_Name"]:
-                    continue
-                d = int(r["Dispatch_Id"])
-                rows[d][r["Counter_Name"]] = rows[d].get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
-                names[d] = r["Kernel_Name"].split("(")[0].replace("void ", "")
-    ids = sorted(rows)
-    want = steps * len(L) + len(order["calibration"])
-    assert len(ids) == want, (len(ids), want)
-    last = ids[(steps - 1) * len(L): steps * len(L)]
-    out = {"_counters": COUNTERS, "_derived": "valu_active_frac = SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES"}
-    for g, d in zip(L, last):
-        c = rows[d]
-        e = {"kernel": names[d], **{k: c.get(k) for k in COUNTERS}}
+    from pmc_segments import launch_groups
+
+    groups, _ = launch_groups(a.sq_dir, order)
+    out = {"_counters": COUNTERS, "_derived": "valu_active_frac = SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES "
+                                              "(counters summed over a launch's dispatches)"}
+    for g, (name, nd, c) in zip(L, groups):
+        e = {"kernel": name.split("(")[0].replace("void ", ""), "dispatches": nd, **{k: c.get(k) for k in COUNTERS}}
         if c.get("SQ_WAVE_CYCLES"):
             e["valu_active_frac"] = round(c.get("SQ_ACTIVE_INST_VALU", 0) / c["SQ_WAVE_CYCLES"], 4)
         if c.get("SQ_WAVES"):

@@ -49,9 +49,13 @@ def main():
     fs = FrameSet(a.width, a.height, a.frames, a.depth, device="cuda:0")
     batches, _ = census_batches(fs, frames=a.frames, census=census, builder=WorkloadBuilder(fs, seed=11))
     launches = group_launches(batches)
+    # a one-element fill after every launch marks its end (a launch may dispatch several kernels,
+    # tools/pmc_segments.py)
+    mark = torch.zeros(1, device="cuda")
     for _ in range(a.steps):
         for g in launches:
             g.run(prims)
+            mark.fill_(1.0)
     torch.cuda.synchronize()
 
     # calibration: disjoint 64x64 tiles through >= 1.5 GB (cache-cold)
@@ -71,7 +75,7 @@ def main():
     prims.blockop(4, 8, s, s, D, s, doff, A, W, off, None, 0, None)
     torch.cuda.synchronize()
 
-    order = {"steps": a.steps, "launches": [{"name": g.name, "kind": g.kind, "bytes": g.bytes, "jobs": g.n}
+    order = {"steps": a.steps, "marker": True, "launches": [{"name": g.name, "kind": g.kind, "bytes": g.bytes, "jobs": g.n}
                                             for g in launches],
              # known bytes: blocks + int64 job offsets (one offset array for both operands of the SAD)
              "calibration": [{"name": "cal_sad_64x64", "kind": "pixelcmp", "read_bytes": 2 * n * s * s + 8 * n,
