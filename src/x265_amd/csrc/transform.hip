@@ -278,8 +278,12 @@ constexpr int kTrWaves = X265AMD_BLOCK / 64;
 // each looping over transforms (the constant operands load once per wave)
 static inline uint32_t mfma_grid(int n)
 {
+    // workgroup cap: 16384 measured 0-3 % faster than 4096 and 1024 / 2048 5-8 % slower
+    // (profiles/r03/tr_grid_ab.txt); X265AMD_TR_GRID overrides it for tuning runs
+    static const int64_t cap = getenv("X265AMD_TR_GRID") && atoi(getenv("X265AMD_TR_GRID")) > 0
+                               ? atoi(getenv("X265AMD_TR_GRID")) : 16384;
     const int64_t want = ((int64_t)n + kTrWaves - 1) / kTrWaves;
-    return (uint32_t)(want < 4096 ? want : 4096);
+    return (uint32_t)(want < cap ? want : cap);
 }
 
 template <bool FWD>
