@@ -10,28 +10,25 @@ in this design (CABAC estimation, SAO, lowres init, ...) are excluded and
 listed in the output.  `value` is frames per second of that primitive
 workload over all ranks; Mpixel/s is reported beside it.
 
-Modes (one process per GPU under torch.distributed.run; weak scaling, F frames
+Modes (one process per GPU under torch.distributed.run; weak scaling, F pictures
 per rank per step):
-  replay (default)  every rank replays the census of its own F frames as one set
-                    of grouped launches — independent closed-GOP shards, no
-                    data-path collective;
-  pipeline          the frame-parallel shard of SURVEY §8(e): frame i of a
-                    G*F-frame sequence on rank i mod G, encoded band by band of
-                    CTU rows; a band waits until the reference frame's owner has
-                    published the rows it reads (refLagRows); finished rows
-                    (deblock, SAO, border extension) go point to point over RCCL
-                    to the owner of the next frame (src/x265_amd/pipeline.py,
-                    DESIGN.md §6).  At N = 1 its rate is reported beside the
-                    replay line (`frame_parallel_pipeline`).
+  pipeline (default, every N)  the frame-parallel shard of SURVEY §8(e): picture j
+                    of a G*F-picture sequence on rank j mod G, closed --preset medium
+                    GOPs of 8 pictures; every census job waits for the reference
+                    bands it reads; finished reference bands (deblock, SAO, border
+                    extension) go point to point over RCCL to every rank that reads
+                    them (src/x265_amd/pipeline.py).  The same step form
+                    at N = 1 and N > 1, so the driver's scaling ratio is like for like;
+  replay            the census of this rank's F frames as one set of independent
+                    grouped launches (no dependencies); at N = 1 its rate is
+                    reported beside the pipeline line (`frame_parallel_pipeline.replay`).
 Timing: W warmup steps, then K steps bracketed by barrier + device sync, max
 over ranks.
 
 Also reported (rank 0):
-  roofline     — dominant kernel (largest share of the step): algorithmic
-                 bytes per launch / its mean launch time,
-                 measured with HIP events on the launch stream inside the
-                 timed region, against the 8 TB/s HBM peak; traffic from the
-                 committed rocprofv3 PMC summary when one exists.
+  roofline     — dominant kernel of the replay step (largest share): its calibrated
+                 PMC HBM bytes per launch / its mean launch time, measured with HIP
+                 events on the launch stream, against the 8 TB/s HBM peak.
   cpu_baseline — the path north_star names: the reference x265 1.9 CLI
                  (`x265 --preset medium`, C primitives; oracle/_ref/x265ref8,
                  compiled from the reference sources) encoding synthetic frames
@@ -40,15 +37,16 @@ Also reported (rank 0):
                  replaying the same census descriptors (`census_replay`).
   encoder_level — BASELINE's metric on the encoder itself: encoded fps of the
                  reference x265 encoder and of the same encoder with its lookahead
-                 cost estimates on the MI355X (integration/gpu_lookahead.cpp), 64
-                 synthetic frames at the bench resolution on the same host cores,
-                 bitstreams identical; plus the per-call provider on a small clip.
+                 estimates and its large-PU motion searches on the MI355X
+                 (integration/gpu_lookahead.cpp, integration/gpu_me.cpp), 64 synthetic
+                 frames at 1080p and 2160p on the same host cores, 5 interleaved runs
+                 per arm (min / median / max), bitstreams identical; plus the
+                 per-call provider on a small clip.
 
-`value` is frames/s of the PRIMITIVE WORKLOAD (the census replay), not of an
-end-to-end encode: the census's calls are replayed as independent batches,
-while inside x265 they are serially dependent (HEX rounds, sub-pel early
-exits, intra neighbours), so it is an upper bound on what the table's work
-costs on the GPU, not an encoder frame rate (that is `encoder_level`).
+`value` is frames/s of the PRIMITIVE WORKLOAD, not of an end-to-end encode: the
+census's calls are batched per schedule step, while inside x265 they are serially
+dependent (HEX rounds, sub-pel early exits, intra neighbours), so it bounds what the
+table's work costs on the GPU; the encoder frame rate is `encoder_level`.
 """
 from __future__ import annotations
 
@@ -71,7 +69,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=500)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--frames", type=int, default=0,
-                    help="frames per step per GPU (default: 8 in replay mode, 32 in pipeline mode)")
+                    help="frames per step per GPU (default: 32 in pipeline mode, 8 in replay mode)")
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--depth", type=int, default=8)
@@ -79,13 +77,13 @@ def parse():
                     help="selects the census of that x265 preset (tests/golden/census_<H>p_<preset>[_main10].json)")
     ap.add_argument("--no-graph", action="store_true", help="launch eagerly instead of replaying a hipGraph")
     ap.add_argument("--mode", default="", choices=("", "pipeline", "replay"),
-                    help="pipeline: frame-parallel GOP shard, pictures encoded band by band with the reference-row "
-                         "dependencies and the RCCL reference exchange (src/x265_amd/pipeline.py); replay: the census "
-                         "of this rank's frames as one set of independent grouped launches.  Default: replay at N = 1, "
-                         "pipeline at N > 1")
+                    help="pipeline (default, every N): frame-parallel GOP shard, pictures encoded band by band with "
+                         "the reference-row dependencies and the RCCL reference exchange (src/x265_amd/pipeline.py), "
+                         "closed GOP segments of 8; replay: the census of this rank's frames as one set of "
+                         "independent grouped launches (reported beside the pipeline at N = 1)")
     ap.add_argument("--band-rows", type=int, default=0, help="CTU rows per pipeline band (default: whole pictures)")
     ap.add_argument("--segment-frames", type=int, default=0,
-                    help="pictures per closed GOP segment in pipeline mode (default: the frames per rank)")
+                    help="pictures per closed GOP segment in pipeline mode (default 8 with whole-picture bands)")
     ap.add_argument("--exchange", default="torch", choices=("torch", "rccl"),
                     help="pipeline reference exchange: torch.distributed P2P batches, or the native RCCL communicator "
                          "of the C ABI (x265amd_exchange, csrc/exchange.cpp)")
@@ -96,6 +94,8 @@ def parse():
     ap.add_argument("--census-cpu-seconds", type=float, default=5.0,
                     help="target duration of the census-replay CPU comparison")
     ap.add_argument("--no-encoder-level", action="store_true")
+    ap.add_argument("--encoder-reps", type=int, default=5,
+                    help="interleaved encoder runs per arm for encoder_level (SURVEY §8(d): median of >= 5)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--breakdown", type=str, default="", help="write per-batch timing JSON here")
     return ap.parse_args()
@@ -285,47 +285,70 @@ def reference_encoder_baseline(args):
             "mpix_per_s": round(fps_all * args.width * args.height / 1e6, 3)}
 
 
-def encoder_level(args, reps=3, width=None, height=None, frames=None, provider=True):
+ENCODER_ARMS = (
+    # (key, binary, extra environment, what runs on the MI355X)
+    ("reference", "x265ref8", {}, "nothing: the unmodified reference encoder on the host cores"),
+    ("mi355x_lookahead", "x265la8", {"X265AMD_ME": "cpu"},
+     "LookaheadTLD::lowresIntraEstimate and every CostEstimateGroup estimate (P / B, lowres motion searches, "
+     "batched per finishBatch)"),
+    ("mi355x_lookahead_me", "x265la8", {"X265AMD_ME": "gpu"},
+     "the lookahead estimates as above, plus the main encoder's motion searches of PUs >= 32x32 "
+     "(Search::predInterSearch's per-reference motionEstimate calls of a CU in one device batch, "
+     "integration/gpu_me.cpp)"),
+)
+
+
+def encoder_level(args, reps=5, width=None, height=None, frames=None, provider=True):
     """BASELINE's metric on the encoder itself: encoded fps of the reference x265 1.9 encoder
-    (oracle/_ref/x265ref8, C primitives) and of the same encoder with its lookahead cost estimates on
-    the MI355X (oracle/_ref/x265la8: integration/gpu_lookahead.cpp over the x265amd_la_* session,
-    tests/test_encoder_lookahead.py), on the same synthetic frames, the same host cores (--pools) and
-    the default frame threads, runs interleaved; median of `reps` each; bitstreams must be identical.
-    Beside it, the per-call provider (every primitive one synchronous device round trip) on a small clip."""
+    (oracle/_ref/x265ref8, C primitives) and of the same encoder with parts of its work on the MI355X
+    (oracle/_ref/x265la8: integration/gpu_lookahead.cpp and integration/gpu_me.cpp), on the same synthetic
+    frames, the same host cores (--pools) and the default frame threads; `reps` runs per arm, interleaved
+    arm by arm (median of >= 5, min / median / max reported); every bitstream must be
+    identical.  A speed-up is stated as significant only when the arm's slowest run beats the reference's
+    fastest.  Beside it, the per-call provider (every primitive one synchronous device round trip)."""
     import statistics
     import tempfile
 
     from src.x265_amd.synth import SyntheticSource
 
-    ref, la = (os.path.join(ROOT, "oracle", "_ref", b) for b in ("x265ref8", "x265la8"))
-    if args.depth != 8 or not (os.path.exists(ref) and os.path.exists(la)):
+    arms = [(k, os.path.join(ROOT, "oracle", "_ref", b), env, what) for k, b, env, what in ENCODER_ARMS]
+    if args.depth != 8 or not all(os.path.exists(exe) for _, exe, _, _ in arms):
         return None
+    if os.environ.get("X265AMD_BENCH_ARMS"):
+        keep = set(os.environ["X265AMD_BENCH_ARMS"].split(",")) | {"reference"}
+        arms = [a for a in arms if a[0] in keep]
     cores = host_cores()
     W, H = width or args.width, height or args.height
     n = frames or (64 if W * H <= 1920 * 1080 else 16)
     extra = ["--preset", args.preset, "--pools", str(cores)]
     out = {"clip": f"{n} synthetic {W}x{H} 8-bit frames, --preset {args.preset}, --pools {cores}, "
-                   f"default frame threads", "cores": cores, "cpu_model": cpu_model()}
+                   f"default frame threads", "cores": cores, "cpu_model": cpu_model(), "runs_per_arm": reps}
+    runs = {k: [] for k, _, _, _ in arms}
+    md5 = {}
     with tempfile.TemporaryDirectory() as td:
         src = os.path.join(td, "src.yuv")
         SyntheticSource(W, H, n, 8).write_yuv(src)
-        fr, fl, md5 = [], [], set()
         for _ in range(reps):
-            f, m, _ = _x265_run(ref, src, W, H, 8, n, extra, timeout=600)
-            fr.append(f)
-            md5.add(("ref", m))
-            f, m, _ = _x265_run(la, src, W, H, 8, n, extra, timeout=600)
-            fl.append(f)
-            md5.add(("la", m))
-        digests = {m for _, m in md5}
-        out.update({"reference_fps": statistics.median(fr), "reference_fps_runs": fr,
-                    "mi355x_lookahead_fps": statistics.median(fl), "mi355x_lookahead_fps_runs": fl,
-                    "speedup": round(statistics.median(fl) / statistics.median(fr), 3),
-                    "mi355x_lookahead_mpix_per_s": round(statistics.median(fl) * W * H / 1e6, 2),
-                    "bitstreams_identical": len(digests) == 1,
-                    "what_runs_on_the_gpu": "LookaheadTLD::lowresIntraEstimate and every CostEstimateGroup "
-                                            "estimate (P / B, motion searches, batched per finishBatch); analysis, "
-                                            "RDO, CABAC, loop filters stay on the host cores"})
+            for k, exe, env, _ in arms:
+                f, m, _ = _x265_run(exe, src, W, H, 8, n, extra, env=dict(os.environ, **env), timeout=600)
+                runs[k].append(f)
+                md5.setdefault(k, set()).add(m)
+    ref = runs["reference"]
+    digests = set().union(*md5.values())
+    for k, _, _, what in arms:
+        r = runs[k]
+        e = {"fps_min": min(r), "fps_median": statistics.median(r), "fps_max": max(r), "fps_runs": r,
+             "mpix_per_s_median": round(statistics.median(r) * W * H / 1e6, 2), "on_the_gpu": what}
+        if k != "reference":
+            e["speedup_median"] = round(statistics.median(r) / statistics.median(ref), 3)
+            e["speedup_significant"] = min(r) > max(ref)
+        out[k] = e
+    out["bitstreams_identical"] = len(digests) == 1
+    # round-3 field names (reference / lookahead medians), kept for continuity
+    out["reference_fps"] = statistics.median(ref)
+    if "mi355x_lookahead" in runs:
+        out["mi355x_lookahead_fps"] = statistics.median(runs["mi355x_lookahead"])
+    out["host_side"] = "CU analysis, RDO, CABAC, loop filters and the remaining motion searches stay on the host cores"
     hip = os.path.join(ROOT, "oracle", "_ref", "x265hip8")
     if provider and os.path.exists(hip):
         w, h, n2 = 416, 240, 2
@@ -375,13 +398,11 @@ def census_replay_cpu(args, census):
             "mpix_per_s": round(fps * args.width * args.height / 1e6, 3)}
 
 
-def pipeline_rates(prims, args, census, local):
-    """The frame-parallel step (--mode pipeline) on this one GPU: one closed GOP of F pictures (F = the
-    pipeline default of 32 frames), steps of x265amd_schedule, reference bands copied (in place) into the
-    reference store; whole-picture bands and 4-CTU-row bands, and the 32 pictures as four closed GOPs of 8
-    (independent segments run side by side in the same steps).  Segments of one picture (32 I pictures: no
-    references, one step) are the same 32 pictures through the same graph machinery without any
-    dependency: the like-for-like reference the dependent forms are measured against."""
+def pipeline_rates(prims, args, census, local, skip=()):
+    """Other forms of the frame-parallel step on this one GPU, beside `value` (N = 1): one open GOP of
+    F = 32 pictures with whole-picture and 4-CTU-row bands, and 32 one-picture segments (32 I pictures:
+    no references, one step) — the same pictures through the same graph machinery without any
+    dependency."""
     import torch
 
     from src.x265_amd.frame_pipeline import GpuFramePipeline
@@ -389,6 +410,8 @@ def pipeline_rates(prims, args, census, local):
     F = 32
     out = {"frames_per_step": F}
     for br, seg in ((0, 0), (4, 0), (0, 8), (0, 1)):
+        if (br, seg) in skip:
+            continue
         pipe = GpuFramePipeline(prims, args.width, args.height, args.depth, F, 1, 0, census=census,
                                 band_rows=br or None, segment_frames=seg or None, streams=args.streams,
                                 device=f"cuda:{local}")
@@ -410,107 +433,72 @@ def pipeline_rates(prims, args, census, local):
     return out
 
 
-def main():
-    args = parse()
-    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
-        raise SystemExit(spawn_ranks(args))
-    if not args.mode:
-        args.mode = "pipeline" if args.gpus > 1 else "replay"
-    if not args.frames:
-        args.frames = 32 if args.mode == "pipeline" else 8
-    import torch
+class ReplayStep:
+    """The census of F frames of this rank as one set of independent grouped launches (one launch per
+    kernel class), spread over S streams by measured launch time and captured in a hipGraph.  It gives
+    the dominant launch of the workload (the roofline kernel: the committed PMC table was recorded on
+    this step with F = 8) and the replay rate reported beside the pipeline `value`."""
 
-    world, rank, local = dist_setup(args)
-    if not torch.cuda.is_available():
-        raise SystemExit("bench.py needs the MI355X (no CPU fallback)")
-    from src.x265_amd import Primitives, capture_graph
-    from src.x265_amd.workload import FrameSet, WorkloadBuilder, census_batches, group_launches
+    def __init__(self, prims, args, census, local, rank, F=8):
+        import ctypes
 
-    prims = Primitives(device=local)
-    census, census_name = pick_census(args)
-    F = args.frames
-    import ctypes
-    nstreams = max(1, args.streams)
-    pipe = None
-    if args.mode == "pipeline":
-        # frame-parallel shard: rank r encodes frames i = k*G + r of a G*F-frame sequence, band by
-        # band of CTU rows, waiting on / publishing reconstructed rows (src/x265_amd/pipeline.py)
-        from src.x265_amd.frame_pipeline import GpuFramePipeline
+        import torch
 
-        pipe = GpuFramePipeline(prims, args.width, args.height, args.depth, F, world, rank, census=census,
-                                band_rows=args.band_rows or None, segment_frames=args.segment_frames or None,
-                                streams=nstreams, device=f"cuda:{local}", exchange=args.exchange)
-        # slice (and reorder) the census batches per step and capture the step graphs FIRST: every launch
-        # group below then builds its descriptor tables from the batches' final per-job tensors
-        pipe.build(graphs=not args.no_graph)
-        batches, wb = pipe.batches, pipe.wb
-    else:
-        # independent replay: this rank's F frames' census as one set of grouped launches
+        from src.x265_amd import capture_graph
+        from src.x265_amd.workload import FrameSet, WorkloadBuilder, census_batches, group_launches
+
+        self.prims, self.F = prims, F
         fs = FrameSet(args.width, args.height, F, args.depth, device=f"cuda:{local}", first_frame=rank * F)
-        batches, wb = census_batches(fs, frames=F, census=census, builder=WorkloadBuilder(fs, seed=11 + rank))
-    # one launch per kernel class: batches of different block shapes share a grouped launch
-    launches = list(batches) if args.no_group else group_launches(batches)
-    step_bytes = sum(b.bytes for b in batches)
-    calls = sum(b.n for b in batches)
+        self.batches, self.wb = census_batches(fs, frames=F, census=census, builder=WorkloadBuilder(fs, seed=11 + rank))
+        self.launches = launches = list(self.batches) if args.no_group else group_launches(self.batches)
+        self.bytes = sum(b.bytes for b in self.batches)
+        self.calls = sum(b.n for b in self.batches)
+        nstreams = max(1, args.streams)
+        side = [torch.cuda.Stream() for _ in range(nstreams)] if nstreams > 1 else []
+        solo, lanes, fork = [], [[] for _ in range(nstreams)], [False]
 
-    # replay mode: independent launches spread over S streams (forked from and joined back into the
-    # current stream, so a captured graph gets S parallel branches): small launches and launch tails
-    # overlap.  The launch the roofline reports runs alone first (not overlapped), so its duration
-    # inside the step equals its isolated duration and the rocprof summary of this command agrees.
-    side = [torch.cuda.Stream() for _ in range(nstreams)] if nstreams > 1 else []
-    solo = []
-    lanes = [[] for _ in range(nstreams)]
-    fork = [False]                     # one stream until the dominant launch is known
+        def assign(first=None, weight=None):
+            """lanes by longest-processing-time: launches in decreasing weight, each onto the least-loaded
+            stream; the dominant launch runs alone first (not overlapped), so its in-step duration is
+            its isolated duration and the rocprof summary of the same command agrees"""
+            fork[0] = first is not None
+            solo[:] = [first] if first is not None else []
+            load = [0.0] * nstreams
+            for lst in lanes:
+                lst.clear()
+            wt = weight or (lambda b: b.bytes)
+            for b in sorted(launches, key=wt, reverse=True):
+                if b is first:
+                    continue
+                i = min(range(nstreams), key=lambda k: load[k])
+                lanes[i].append(b)
+                load[i] += wt(b)
 
-    def assign(first=None, weight=None):
-        """lanes by longest-processing-time: launches in decreasing weight (measured ms once known,
-        algorithmic bytes before), each onto the least-loaded stream"""
-        fork[0] = first is not None
-        solo[:] = [first] if first is not None else []
-        load = [0.0] * nstreams
-        for lst in lanes:
-            lst.clear()
-        wt = weight or (lambda b: b.bytes)
-        for b in sorted(launches, key=wt, reverse=True):
-            if b is first:
-                continue
-            i = min(range(nstreams), key=lambda k: load[k])
-            lanes[i].append(b)
-            load[i] += wt(b)
-    assign()
-
-    def kernels():
-        if not side or not fork[0]:
-            for b in launches:
+        def kernels():
+            if not side or not fork[0]:
+                for b in launches:
+                    b.run(prims)
+                return
+            for b in solo:
                 b.run(prims)
-            return
-        for b in solo:
-            b.run(prims)
-        cur = torch.cuda.current_stream()
-        for s_, lst in zip(side, lanes):
-            s_.wait_stream(cur)
-            h = ctypes.c_void_p(s_.cuda_stream)
-            for b in lst:
-                b.run(prims, h)
-        for s_ in side:
-            cur.wait_stream(s_)
+            cur = torch.cuda.current_stream()
+            for s_, lst in zip(side, lanes):
+                s_.wait_stream(cur)
+                h = ctypes.c_void_p(s_.cuda_stream)
+                for b in lst:
+                    b.run(prims, h)
+            for s_ in side:
+                cur.wait_stream(s_)
 
-    # per-kernel timing (eager, whole-frame launches) to find the dominant launch
-    for _ in range(max(1, args.warmup)):
-        kernels()
-    torch.cuda.synchronize()
-    ktimes = kernel_times(launches, prims)
-    dominant = max(launches, key=lambda b: ktimes[b.name])
-    balance = os.environ.get("X265AMD_BENCH_BALANCE", "time")
-    assign(dominant, (lambda b: ktimes[b.name]) if balance == "time" else None)
-
-    graph = None
-    if pipe is not None:
-        graph = bool(pipe.graphs) or None
-
-        def run():
-            pipe.step()
-    else:
+        assign()
+        for _ in range(max(1, args.warmup)):
+            kernels()
+        torch.cuda.synchronize()
+        self.ktimes = kernel_times(launches, prims)
+        self.dominant = max(launches, key=lambda b: self.ktimes[b.name])
+        balance = os.environ.get("X265AMD_BENCH_BALANCE", "time")
+        assign(self.dominant, (lambda b: self.ktimes[b.name]) if balance == "time" else None)
+        self.kernels, self.graph = kernels, None
         if not args.no_graph:
             try:
                 s = torch.cuda.Stream()
@@ -518,20 +506,86 @@ def main():
                 with torch.cuda.stream(s):
                     kernels()
                 torch.cuda.current_stream().wait_stream(s)
-                graph = torch.cuda.CUDAGraph()
-                with capture_graph(graph):
+                g = torch.cuda.CUDAGraph()
+                with capture_graph(g):
                     kernels()
-                graph.replay()
+                g.replay()
                 torch.cuda.synchronize()
+                self.graph = g
             except Exception as e:  # capture unsupported: measure eager launches instead
                 print(f"[bench] hipGraph capture failed ({e}); eager launches", file=sys.stderr)
-                graph = None
 
-        def run():
-            if graph is not None:
-                graph.replay()
-            else:
-                kernels()
+    def run(self):
+        if self.graph is not None:
+            self.graph.replay()
+        else:
+            self.kernels()
+
+    def rate(self, seconds=1.0):
+        """frames/s of this step alone (>= `seconds` of timed steps after a warm-up)"""
+        import torch
+
+        for _ in range(5):
+            self.run()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        self.run()
+        torch.cuda.synchronize()
+        n = max(5, int(seconds / max(1e-5, time.perf_counter() - t0)))
+        t0 = time.perf_counter()
+        for _ in range(n):
+            self.run()
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / n
+        return {"fps": round(self.F / dt, 1), "ms_per_step": round(dt * 1e3, 3), "frames_per_step": self.F,
+                "steps": n, "launches_per_step": len(self.launches), "hipgraph": self.graph is not None}
+
+
+def main():
+    args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        raise SystemExit(spawn_ranks(args))
+    if not args.mode:
+        args.mode = "pipeline"
+    if not args.frames:
+        args.frames = 32 if args.mode == "pipeline" else 8
+    if args.mode == "pipeline" and not args.segment_frames and not args.band_rows:
+        # closed --preset medium GOP segments of 8 pictures: the same step form at every N
+        args.segment_frames = 8
+    import torch
+
+    world, rank, local = dist_setup(args)
+    if not torch.cuda.is_available():
+        raise SystemExit("bench.py needs the MI355X (no CPU fallback)")
+    from src.x265_amd import Primitives
+
+    prims = Primitives(device=local)
+    census, census_name = pick_census(args)
+    F = args.frames
+    nstreams = max(1, args.streams)
+    pipe = None
+    if args.mode == "pipeline":
+        # frame-parallel shard: picture j of a G*F-picture sequence on rank j mod G, band by band of CTU
+        # rows, waiting on / publishing reconstructed reference bands (src/x265_amd/pipeline.py)
+        from src.x265_amd.frame_pipeline import GpuFramePipeline
+
+        pipe = GpuFramePipeline(prims, args.width, args.height, args.depth, F, world, rank, census=census,
+                                band_rows=args.band_rows or None, segment_frames=args.segment_frames or None,
+                                streams=nstreams, device=f"cuda:{local}", exchange=args.exchange)
+        # slice (and reorder) the census batches per step and capture the step graphs FIRST
+        pipe.build(graphs=not args.no_graph)
+    # the replay step: the dominant launch for the roofline (and, in replay mode, the timed step)
+    rep = ReplayStep(prims, args, census, local, rank, F=8 if pipe is not None else F)
+    if pipe is not None:
+        batches, wb, graph = pipe.batches, pipe.wb, bool(pipe.graphs) or None
+        run = pipe.step
+    else:
+        batches, wb, graph = rep.batches, rep.wb, rep.graph
+        run = rep.run
+    step_bytes = sum(b.bytes for b in batches)
+    calls = sum(b.n for b in batches)
+    dominant, ktimes, launches = rep.dominant, rep.ktimes, rep.launches
+
     for _ in range(args.warmup):
         run()
     barrier(world)
@@ -575,17 +629,14 @@ def main():
     if rank == 0:
         algo_gbps = dominant.bytes / (dom_ms * 1e-3) / 1e9
         kname = f"{dominant.kind}:{dominant.name}"
-        # the committed PMC summary (profiles/pmc_traffic.json) was recorded on the default configuration
-        # the committed PMC summaries were recorded with 8 frames per step
-        ppath = pmc_traffic_path(args) if F == 8 else ""
+        # the committed PMC summaries were recorded on the replay step with 8 frames
+        ppath = pmc_traffic_path(args) if rep.F == 8 else ""
         traffic = pmc_traffic(dominant.name, ppath) if ppath else None
-        # A census launch re-reads blocks many times (x265 scores many candidates per fenc block),
-        # so its algorithmic bytes exceed what reaches HBM and algorithmic/time can
-        # exceed the HBM peak.  The HBM fraction is therefore taken from the calibrated PMC bytes
-        # of the same launch (FETCH_SIZE / WRITE_SIZE passes); without them it is the algorithmic rate.
-        # Without a PMC record (non-default configurations) there is no HBM figure to divide: the
-        # algorithmic rate of a census launch counts cache-resident re-reads and can exceed the peak,
-        # so it is reported beside a null frac instead of as one.
+        # A census launch re-reads blocks many times (x265 scores many candidates per fenc block), so its
+        # algorithmic bytes exceed what reaches HBM and algorithmic/time can exceed the HBM
+        # peak.  The HBM fraction is therefore taken from the calibrated PMC bytes of the same launch
+        # (FETCH_SIZE / WRITE_SIZE passes); without a PMC record the algorithmic rate is reported beside a
+        # null frac.
         achieved = traffic / (dom_ms * 1e-3) / 1e9 if traffic else None
         roofline = {"bound": "hbm", "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
@@ -596,16 +647,23 @@ def main():
                     "achieved_algorithmic": round(algo_gbps, 1),
                     "kernel": kname, "kernel_ms": round(dom_ms, 4), "bytes_per_launch": int(dominant.bytes),
                     "launch_jobs": dominant.n,
-                    "share_of_step": round(ktimes[dominant.name] / max(1e-9, sum(ktimes.values())), 3)}
+                    "share_of_step": round(ktimes[dominant.name] / max(1e-9, sum(ktimes.values())), 3),
+                    "workload": f"the census of {rep.F} frames as independent grouped launches (the replay step); "
+                                "the same kernels make up the pipeline's per-step slices"}
         if traffic:
             roofline["traffic_over_algorithmic"] = round(traffic / dominant.bytes, 3)
+        replay = None
+        if world == 1:
+            replay = rep.rate()
         step_traffic = [pmc_traffic(b.name, ppath) for b in launches] if ppath else []
         step_hbm = None
-        if step_traffic and all(t is not None for t in step_traffic):
+        rep_ms = replay["ms_per_step"] if replay else (ms_per_step if pipe is None else None)
+        if rep_ms and step_traffic and all(t is not None for t in step_traffic):
             tb = sum(step_traffic)
-            step_hbm = {"bytes_per_step": tb, "GBps": round(tb / (ms_per_step * 1e-3) / 1e9, 1),
-                        "frac": round(tb / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                        "basis": "sum of the step's launches' PMC HBM bytes / ms_per_step"}
+            step_hbm = {"bytes_per_step": tb, "GBps": round(tb / (rep_ms * 1e-3) / 1e9, 1),
+                        "frac": round(tb / (rep_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                        "basis": f"sum of the replay step's launches' PMC HBM bytes ({rep.F} frames) / its "
+                                 "ms_per_step"}
         caller = None
         if world == 1:
             try:
@@ -614,36 +672,52 @@ def main():
             except Exception as e:   # informational: never fails the bench line
                 caller = {"error": str(e)}
         frame_parallel = None
-        if world == 1 and pipe is None and not args.no_pipeline_check:
+        if world == 1 and not args.no_pipeline_check:
             try:
-                frame_parallel = pipeline_rates(prims, args, census, local)
+                skip = {(args.band_rows, args.segment_frames)} if pipe is not None else set()
+                frame_parallel = pipeline_rates(prims, args, census, local, skip=skip)
             except Exception as e:   # informational
                 frame_parallel = {"error": str(e)}
-        cpu, replay, enc = None, None, None
+            if replay is not None:
+                frame_parallel = dict(frame_parallel or {}, replay=replay)
+        cpu, creplay, enc = None, None, None
         if world == 1 and not args.no_cpu:
             try:
                 cpu = reference_encoder_baseline(args)
             except Exception as e:
                 cpu = {"value": None, "error": str(e)}
             try:
-                replay = census_replay_cpu(args, census)
+                creplay = census_replay_cpu(args, census)
             except Exception as e:
-                replay = {"value": None, "error": str(e)}
+                creplay = {"value": None, "error": str(e)}
             if cpu is None:
-                cpu = replay
+                cpu = creplay
             else:
-                cpu["census_replay"] = replay
+                cpu["census_replay"] = creplay
         if world == 1 and not args.no_encoder_level:
             try:
-                enc = encoder_level(args)
+                enc = encoder_level(args, reps=args.encoder_reps)
                 if (args.width, args.height) == (1920, 1080) and args.preset == "medium":
                     # BASELINE's 4K figure: 2160p medium, 64 frames (longer than the lookahead depth)
-                    enc["2160p"] = encoder_level(args, reps=2, width=3840, height=2160, frames=64, provider=False)
+                    enc["2160p"] = encoder_level(args, reps=args.encoder_reps, width=3840, height=2160, frames=64,
+                                                 provider=False)
             except Exception as e:
                 enc = {"error": str(e)}
+        if pipe is not None:
+            workload = (f"primitive-workload fps of the frame-parallel step: the x265-1.9 --preset {args.preset} "
+                        f"per-frame primitive census ({args.height}p, tests/golden/{census_name}) of {world * F} "
+                        f"pictures as closed GOPs of {pipe.segment_frames} (I/P/B-ref/b, 3 refs, L1<=2), every job "
+                        "waiting for the reference bands it reads (deblock/SAO/border final), batched gfx950 "
+                        "kernels per schedule step; CPU-side entries (CABAC estimates, SAO RDO, lowres init) "
+                        "excluded")
+        else:
+            workload = (f"primitive-workload fps: the x265-1.9 --preset {args.preset} per-frame primitive census "
+                        f"({args.height}p, tests/golden/{census_name}) replayed as independent batched gfx950 "
+                        "kernels; CPU-side entries (CABAC estimates, SAO RDO, lowres init) excluded")
         line = {
             "metric": f"primitive-workload fps (x265 1.9 --preset {args.preset} per-frame primitive census, "
-                      f"{args.height}p {args.depth}-bit; not an end-to-end encode) + Mpixels/s",
+                      f"{args.height}p {args.depth}-bit, frame-parallel GOP shard; not an end-to-end encode: "
+                      f"see encoder_level) + Mpixels/s",
             "value": round(fps, 2),
             "unit": "fps",
             "n_gpus": world,
@@ -656,10 +730,7 @@ def main():
             "dtype": "u8" if args.depth == 8 else "u16",
             "data": "synthetic (src/x265_amd/synth.py), HBM-resident",
             "config": {
-                "workload": f"primitive-workload fps: the x265-1.9 --preset {args.preset} per-frame primitive "
-                            f"census ({args.height}p, tests/golden/{census_name}) replayed as independent batched "
-                            "gfx950 kernels (an upper bound on the table's GPU cost: inside x265 the calls are "
-                            "serially dependent); CPU-side entries (CABAC estimates, SAO, lowres init) excluded",
+                "workload": workload,
                 "resolution": f"{args.width}x{args.height}", "depth": args.depth, "frames_per_step_per_gpu": F,
                 "calls_per_step_per_gpu": calls, "batches_per_step": len(batches),
                 "launches_per_step": pipe.launches_per_step if pipe is not None else len(launches),
@@ -687,6 +758,8 @@ def main():
             "caller_level_rates": caller,
             "cpu_excluded_calls_per_frame": round(sum(v for v in wb.skipped.values()) / F),
         }
+        if pipe is not None and getattr(pipe, "comm", None) is not None:
+            line["config"]["rccl_backend"] = getattr(pipe.comm, "backend", None)
         if args.breakdown:
             with open(args.breakdown, "w") as f:
                 json.dump({b.name: {"ms": ktimes[b.name], "jobs": b.n, "bytes": b.bytes,

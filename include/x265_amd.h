@@ -607,6 +607,9 @@ typedef struct
     int send;
 } x265amd_transfer;
 int x265amd_comm_unique_id(uint8_t* id);
+/* which RCCL the communicator entries bound (X265AMD_RCCL, the process's already-loaded copy, or
+ * ROCm's librccl.so.1 loaded by the library); NULL when no RCCL was found */
+const char* x265amd_comm_backend(void);
 int x265amd_comm_create(x265amd_comm** comm, const uint8_t* id, int nranks, int rank);
 int x265amd_comm_destroy(x265amd_comm* comm);
 int x265amd_exchange(x265amd_comm* comm, const x265amd_transfer* xfers, int count, void* stream);
@@ -724,6 +727,60 @@ typedef struct
     const int64_t* ref_coff;
 } x265amd_me_batch;
 int x265amd_motion_search(int depth, int count, const x265amd_me_batch* batches, void* stream);
+
+/* f2 in the running encoder: the searches of Search::predInterSearch (search.cpp:2050-2231)
+ * through a session, as the f1 session serves the lookahead.  Like the x265amd_la_* entries these
+ * take HOST pointers and are synchronous (the encoder reads each search's result right after the
+ * call); thread-safe (x265 searches from every WPP worker and frame encoder at once; each host
+ * thread gets its own stream and staging).  A session holds device copies of the reconstructed
+ * reference pictures' padded luma planes (PicYuv, picyuv.cpp:51-91: m_picBuf[0] of `plane_elems`
+ * elements, m_picOrg[0] at `org_offset`), uploaded CTU row by CTU row as the encoder makes them
+ * final (Frame::m_reconRowCount, framefilter.cpp:520), and the BitCost tables of the QPs in use
+ * (bitcost.cpp:31-57).  Errors are returned and recorded in the sticky status, except the
+ * capacity limits (ENOMEM from x265amd_mes_ref / _table), after which the caller searches that
+ * PU on the host. */
+typedef struct x265amd_mes x265amd_mes;
+typedef struct
+{
+    int depth;
+    intptr_t stride;               /* PicYuv::m_stride */
+    int64_t plane_elems;           /* m_stride * (maxHeight + 2 * m_lumaMarginY) */
+    int64_t org_offset;            /* m_picOrg[0] - m_picBuf[0] */
+    int margin_y;                  /* m_lumaMarginY */
+    int ctu_rows, ctu_size;        /* numCuInHeight, g_maxCUSize */
+    int max_pictures;              /* distinct reconstructed-picture buffers (keys) */
+    int max_threads;               /* distinct host threads calling the session */
+    int max_tables;                /* distinct BitCost tables (QPs) */
+    int mvcost_range;              /* table entries [-range, range] are copied (2 * BC_MAX_MV) */
+    int method, subme, merange;    /* x265_param searchMethod / subpelRefine / searchRange */
+    int max_cand;                  /* most MV candidates of one search (mvc[] of predInterSearch: 12) */
+} x265amd_mes_config;
+int  x265amd_mes_create(const x265amd_mes_config* cfg, x265amd_mes** out);
+void x265amd_mes_destroy(x265amd_mes* mes);
+/* make CTU rows [0, rows_final) of reference picture `key` (generation gen, e.g. its POC) resident
+ * on the device: uploads the rows not uploaded yet for this generation (the top margin with row 0,
+ * the bottom margin with the last row) from plane_buf = m_picBuf[0]; *slot = the picture's slot */
+int x265amd_mes_ref(x265amd_mes* mes, const void* key, int64_t gen, const void* plane_buf, int rows_final,
+                    int* slot);
+/* the device copy of a BitCost table (host pointer at difference 0); *index = its table number */
+int x265amd_mes_table(x265amd_mes* mes, const uint16_t* centre, int* index);
+/* one MotionEstimate::motionEstimate call (motion.cpp:571-1172) per job, all of one PU (w x h, the
+ * source block at `fenc` with stride fenc_stride = FENC_STRIDE), ONE device launch: job inputs as
+ * the call's arguments (block_off = the PU origin relative to m_picOrg[0], mv_range = mvmin.x,
+ * mvmin.y, mvmax.x, mvmax.y full-pel, mvp / mvc quarter-pel); outputs outQMv and the returned cost */
+typedef struct
+{
+    int slot, table;
+    int64_t block_off;
+    int16_t mv_range[4];
+    int16_t mvp[2];
+    int num_cand;
+    int16_t mvc[2 * 16];
+    int16_t out_mv[2];
+    int32_t out_cost;
+} x265amd_mes_job;
+int x265amd_mes_search(x265amd_mes* mes, int w, int h, const void* fenc, intptr_t fenc_stride, int n,
+                       x265amd_mes_job* jobs);
 
 /* ------------------------------------------------------------------- f4
  * In-loop filters and border extension of device-resident 4:2:0 recon frames

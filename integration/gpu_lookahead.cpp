@@ -64,7 +64,6 @@ struct TabBitCost : public BitCost
 enum { MODE_GPU = 0, MODE_CPU = 1, MODE_HOST = 2, MODE_CHECK = 3 };
 
 int g_mode = MODE_GPU;
-x265amd_la* g_la = NULL;
 int g_la_status = 0;
 pthread_mutex_t g_mu = PTHREAD_MUTEX_INITIALIZER;
 pthread_once_t g_mode_once = PTHREAD_ONCE_INIT;
@@ -89,31 +88,57 @@ void read_mode()
         atexit(print_stats);
 }
 
-/* the session, created on the first call from the first Lowres (all pictures of an encoder
- * share the geometry) */
+/* One session per picture geometry and bit depth (x265amd_la_config), created on the first call
+ * that needs it: every Lowres of one encoder shares its geometry, and a second encoder in the
+ * same process with another resolution gets a session of its own instead of having its pictures
+ * read with the first one's strides.  Sessions live until the process exits (the encoder has no
+ * teardown hook for the lookahead; x265amd_la_destroy is exercised by tests/test_la_session.py).
+ * Picture slots: a Lowres is uploaded into the slot of its key (the Lowres address) and x265
+ * reuses a Frame's Lowres for later pictures, so the slots needed are the distinct Lowres objects
+ * of the encoder's frame pool: rc-lookahead (<= 250, param.cpp X265_LOOKAHEAD_MAX) + bframes
+ * (<= 16) + frame threads (<= 16) + DPB (<= 16) + the pre-lookahead queue, below 320. */
+struct Session { x265amd_la_config cfg; x265amd_la* la; };
+std::vector<Session> g_sessions;
+enum { LA_MAX_FRAMES = 320 };
+
 x265amd_la* session(const Lowres& f)
 {
+    x265amd_la_config c;
+    memset(&c, 0, sizeof(c));
+    c.depth = X265_DEPTH;
+    c.width_cu = (int)f.maxBlocksInRow;
+    c.height_cu = (int)f.maxBlocksInCol;
+    c.lowres_stride = f.lumaStride;
+    c.planesize = f.buffer[1] - f.buffer[0];
+    c.padoffset = f.lowresPlane[0] - f.buffer[0];
+    c.max_frames = LA_MAX_FRAMES;
+    c.max_threads = 128;         // pool workers + API / lookahead threads
     pthread_mutex_lock(&g_mu);
-    if (!g_la && !g_la_status)
+    x265amd_la* la = NULL;
+    for (size_t i = 0; i < g_sessions.size() && !la; i++)
     {
-        x265amd_la_config c;
-        memset(&c, 0, sizeof(c));
-        c.depth = X265_DEPTH;
-        c.width_cu = (int)f.maxBlocksInRow;
-        c.height_cu = (int)f.maxBlocksInCol;
-        c.lowres_stride = f.lumaStride;
-        c.planesize = f.buffer[1] - f.buffer[0];
-        c.padoffset = f.lowresPlane[0] - f.buffer[0];
-        c.max_frames = 256;          // distinct Lowres objects of one encoder (its Frame pool)
-        c.max_threads = 128;         // pool workers + API / lookahead threads
+        const x265amd_la_config& s = g_sessions[i].cfg;
+        if (s.width_cu == c.width_cu && s.height_cu == c.height_cu && s.lowres_stride == c.lowres_stride &&
+            s.planesize == c.planesize && s.padoffset == c.padoffset)
+            la = g_sessions[i].la;
+    }
+    if (!la && !g_la_status)
+    {
         TabBitCost bc;
         c.mvcost = bc.table(X265_LOOKAHEAD_QP);
         c.mvcost_range = 1 << 14;    // > every qpel MV difference of a 2160p lowres search
-        g_la_status = x265amd_la_create(&c, &g_la);
+        g_la_status = x265amd_la_create(&c, &la);
         if (g_la_status)
+        {
             fprintf(stderr, "[x265la] x265amd_la_create failed: %s\n", x265amd_strerror(g_la_status));
+            la = NULL;
+        }
+        else
+        {
+            Session s = { c, la };
+            g_sessions.push_back(s);
+        }
     }
-    x265amd_la* la = g_la;
     pthread_mutex_unlock(&g_mu);
     return la;
 }
@@ -126,8 +151,9 @@ void report(const char* what, int st)
 int g_mismatches = 0;
 
 /* X265AMD_LA_STATS=1: calls and wall time per kind, printed at exit */
-enum { ST_INTRA, ST_P, ST_B, ST_BATCH_P, ST_BATCH_B, ST_HOST, ST_N };
-const char* const st_name[ST_N] = { "intra", "P single", "B single", "P batched", "B batched", "host loops" };
+enum { ST_INTRA, ST_P, ST_B, ST_BATCH_P, ST_BATCH_B, ST_HOST, ST_P_WEIGHTED, ST_HOST_WEIGHTED, ST_N };
+const char* const st_name[ST_N] = { "intra", "P single", "B single", "P batched", "B batched", "host loops",
+                                    "P weighted", "B weighted" };
 struct Stat { long calls, jobs; double sec; };
 Stat g_stat[ST_N];
 bool g_stats_on = false;
@@ -369,7 +395,7 @@ int64_t CostEstimateGroup::estimateFrameCost(LookaheadTLD& tld, int p0, int p1, 
                 st = x265amd_la_pcost(la, fenc, m_frames[p0], weighted ? tld.wbuffer[0] : NULL, rps, ns,
                                       (int16_t*)mvs[0], mvc[0], lc, rs, ce, &mbs);
                 report("x265amd_la_pcost", st);
-                stat_add(ST_P, 1, t0);
+                stat_add(weighted ? ST_P_WEIGHTED : ST_P, 1, t0);
             }
             else
             {
@@ -431,7 +457,7 @@ int64_t CostEstimateGroup::estimateFrameCost(LookaheadTLD& tld, int p0, int p1, 
         }
 
         if (!done)
-            stat_add(ST_HOST, 1, th);
+            stat_add(weighted && p1 > b ? ST_HOST_WEIGHTED : ST_HOST, 1, th);
         if (check && device)
             cb.compare(p0, p1, b, ns, bDoSearch, fenc, ce, mbs, fenc->intraMbs[b - p0] - mbs_before);
 
@@ -529,27 +555,29 @@ void CostEstimateGroup::finishBatch()
             host.push_back(i);
     }
     const int rows = m_lookahead.m_8x8Height;
-    int st = 0;
+    /* the P and B calls succeed or fail independently: the results of a successful call are
+     * applied, the estimates of a failed one go to the host loop below (the status is recorded,
+     * so the encode fails, but the encoder's state stays valid until it stops) */
+    int stp = 0, stb = 0;
     if (!pj.empty())
     {
         const double t0 = now_s();
-        st = x265amd_la_pcost_n(la, (int)pj.size(), &pj[0], rows, 1);
-        report("x265amd_la_pcost_n", st);
+        stp = x265amd_la_pcost_n(la, (int)pj.size(), &pj[0], rows, 1);
+        report("x265amd_la_pcost_n", stp);
         stat_add(ST_BATCH_P, (long)pj.size(), t0);
-        if (st)
+        if (stp)
             host.insert(host.end(), pidx.begin(), pidx.end());
     }
     if (!bj.empty())
     {
         const double t0 = now_s();
-        const int stb = x265amd_la_bcost_n(la, (int)bj.size(), &bj[0], rows, 1);
+        stb = x265amd_la_bcost_n(la, (int)bj.size(), &bj[0], rows, 1);
         report("x265amd_la_bcost_n", stb);
         stat_add(ST_BATCH_B, (long)bj.size(), t0);
         if (stb)
             host.insert(host.end(), bidx.begin(), bidx.end());
-        st = st ? st : stb;
     }
-    for (size_t k = 0; k < pj.size() && !st; k++)
+    for (size_t k = 0; k < pj.size() && !stp; k++)
     {
         const Estimate& e = m_estimates[pidx[k]];
         Lowres* fenc = m_frames[e.b];
@@ -557,7 +585,7 @@ void CostEstimateGroup::finishBatch()
         fenc->costEstAq[e.b - e.p0][0] = pj[k].cost_est[1];
         fenc->intraMbs[e.b - e.p0] += pj[k].intra_mbs;
     }
-    for (size_t k = 0; k < bj.size() && !st; k++)
+    for (size_t k = 0; k < bj.size() && !stb; k++)
     {
         const Estimate& e = m_estimates[bidx[k]];
         Lowres* fenc = m_frames[e.b];

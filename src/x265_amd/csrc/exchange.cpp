@@ -17,6 +17,7 @@
 // X265AMD_RCCL.  No RCCL type appears in the C ABI: the unique id is 128 opaque bytes the caller
 // distributes over any channel (torch.distributed, MPI, a file).
 #include <dlfcn.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -32,6 +33,7 @@ namespace {
 struct Rccl
 {
     bool ok = false;
+    const char* bound = nullptr;   // which library the symbols came from
     decltype(&ncclGetUniqueId) get_unique_id = nullptr;
     decltype(&ncclCommInitRank) init_rank = nullptr;
     decltype(&ncclCommDestroy) destroy = nullptr;
@@ -46,11 +48,23 @@ Rccl& rccl()
     static Rccl r;
     static std::once_flag once;
     std::call_once(once, [] {
+        // 1. an explicit library (X265AMD_RCCL); 2. RCCL already loaded in the process — PyTorch's copy
+        // is librccl.so.1 or a hashed name under torch/lib, so look the symbols up globally first and
+        // then by both sonames with RTLD_NOLOAD; 3. ROCm's librccl.so.1.  A second RCCL runtime next to
+        // the process's own would run its own communicators and proxy threads.
         void* h = nullptr;
-        if (const char* p = getenv("X265AMD_RCCL")) h = dlopen(p, RTLD_NOW | RTLD_LOCAL);
-        if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_NOLOAD);        // the process's copy, if any
-        if (!h) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
-        if (!h) return;
+        const char* how = nullptr;
+        bool global = false;           // RTLD_DEFAULT is a null handle: tracked separately
+        if (const char* p = getenv("X265AMD_RCCL"))
+            if ((h = dlopen(p, RTLD_NOW | RTLD_LOCAL))) how = p;
+        if (!h && dlsym(RTLD_DEFAULT, "ncclGetUniqueId")) { global = true; how = "already loaded (global lookup)"; }
+        if (!h && !global && (h = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD))) how = "already loaded (librccl.so.1)";
+        if (!h && !global && (h = dlopen("librccl.so", RTLD_NOW | RTLD_NOLOAD))) how = "already loaded (librccl.so)";
+        if (!h && !global && (h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL))) how = "librccl.so.1 (loaded here)";
+        if (!h && !global) return;
+        if (global) h = RTLD_DEFAULT;
+        if (getenv("X265AMD_RCCL_VERBOSE")) fprintf(stderr, "[x265amd] RCCL bound: %s\n", how);
+        r.bound = how;
         r.get_unique_id = (decltype(r.get_unique_id))dlsym(h, "ncclGetUniqueId");
         r.init_rank = (decltype(r.init_rank))dlsym(h, "ncclCommInitRank");
         r.destroy = (decltype(r.destroy))dlsym(h, "ncclCommDestroy");
@@ -72,6 +86,12 @@ struct x265amd_comm
 };
 
 static_assert(sizeof(ncclUniqueId) == X265AMD_COMM_ID_BYTES, "RCCL unique id size");
+
+extern "C" const char* x265amd_comm_backend(void)
+{
+    Rccl& r = rccl();
+    return r.ok ? r.bound : nullptr;
+}
 
 extern "C" int x265amd_comm_unique_id(uint8_t* id)
 {

@@ -81,6 +81,7 @@ struct x265amd_la
     uint16_t* mvcost_base = nullptr;
     size_t scratch = 0;
 
+    uint64_t id = 0;            // process-unique session number (a later session may reuse this address)
     std::mutex mu;
     struct Slot { int index; int gen; bool has_invq; const void* pinned; };
     std::unordered_map<const void*, Slot> frames;
@@ -90,8 +91,12 @@ struct x265amd_la
 
 namespace {
 
-struct TlsEntry { const x265amd_la* la; x265amd_la_thread* t; };
+// a thread's context of a session is found by (address, id): x265amd_la_destroy frees every
+// thread's context but cannot reach other threads' thread_local lists, and a later session can be
+// allocated at the same address, so an entry of a destroyed session must never match again
+struct TlsEntry { const x265amd_la* la; uint64_t id; x265amd_la_thread* t; };
 thread_local std::vector<TlsEntry> tls;
+std::atomic<uint64_t> g_next_id{ 1 };
 
 // scratch layout of n estimates (byte offsets, 256-aligned), field-major as the batched
 // x265amd_lowres_* entries index them (estimate e's CU arrays at e * ncu)
@@ -147,12 +152,22 @@ int reserve(x265amd_la_thread* t, size_t bytes)
 
 int thread_ctx(x265amd_la* la, x265amd_la_thread** out)
 {
-    for (auto& e : tls)
-        if (e.la == la)
+    for (size_t i = 0; i < tls.size();)
+    {
+        if (tls[i].la == la && tls[i].id == la->id)
         {
-            *out = e.t;
+            *out = tls[i].t;
             return 0;
         }
+        if (tls[i].la == la)
+        {
+            // a destroyed session's entry at a reused address: its context is already freed
+            tls[i] = tls.back();
+            tls.pop_back();
+            continue;
+        }
+        i++;
+    }
     auto* t = new (std::nothrow) x265amd_la_thread();
     if (!t) return X265AMD_ENOMEM;
     {
@@ -171,7 +186,7 @@ int thread_ctx(x265amd_la* la, x265amd_la_thread** out)
     if (sync && !strcmp(sync, "block") &&
         hipEventCreateWithFlags(&t->ev, hipEventBlockingSync | hipEventDisableTiming) != hipSuccess)
         return X265AMD_ENOMEM;
-    tls.push_back({ la, t });
+    tls.push_back({ la, la->id, t });
     *out = t;
     return 0;
 }
@@ -203,6 +218,7 @@ extern "C" int x265amd_la_create(const x265amd_la_config* cfg, x265amd_la** out)
     auto* la = new (std::nothrow) x265amd_la();
     if (!la) return record(X265AMD_ENOMEM);
     la->cfg = *cfg;
+    la->id = g_next_id.fetch_add(1);
     la->pix = cfg->depth > 8 ? 2 : 1;
     la->frame_bytes = 4 * (size_t)cfg->planesize * la->pix;
     la->ncu = cfg->width_cu * cfg->height_cu;

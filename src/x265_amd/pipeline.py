@@ -254,6 +254,9 @@ class Comm:
         if rc:
             raise RuntimeError(f"x265amd_comm_create: status {rc}")
         self.world, self.rank = world, rank
+        lib.x265amd_comm_backend.restype = ctypes.c_char_p
+        b = lib.x265amd_comm_backend()
+        self.backend = b.decode() if b else None    # which RCCL the C ABI bound (recorded by bench.py)
 
     def exchange(self, xfers, stream):
         """xfers: a ctypes array of _Transfer; stream: a HIP stream handle (int)"""

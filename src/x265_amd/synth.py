@@ -9,7 +9,9 @@ this repository runs on this generator:
   panned +2 px/frame horizontally and +1 px/frame vertically;
 * one 128x128 textured object moving (+7, +3) px/frame;
 * additive Gaussian noise sigma = 1 per frame;
-* chroma: 3-tap-smoothed noise in [64, 192] panned at half rate.
+* chroma: 3-tap-smoothed noise in [64, 192] panned at half rate;
+* optional luma fade (`fade` > 0): frame i's luma scaled by 1 - fade * i (a fade to black, the
+  case x265's weighted prediction analysis, slicetype.cpp:391-495, exists for).
 
 10-bit output is the 8-bit picture scaled by 4 (plus the same noise scaled),
 stored as little-endian uint16, as the survey's Main10 config describes.
@@ -46,9 +48,11 @@ def _box_fast(a: np.ndarray, taps: int) -> np.ndarray:
 class SyntheticSource:
     """Frame generator; frame(i) returns (Y, U, V) uint8 or uint16 planes."""
 
-    def __init__(self, width: int, height: int, nframes: int, depth: int = 8, seed: int | None = None):
+    def __init__(self, width: int, height: int, nframes: int, depth: int = 8, seed: int | None = None,
+                 fade: float = 0.0):
         assert width % 2 == 0 and height % 2 == 0
         self.w, self.h, self.n, self.depth = width, height, nframes, depth
+        self.fade = fade
         self.seed = _seed_for(width, height) if seed is None else seed
         rng = np.random.default_rng(self.seed)
         span_x = width + PAN_X * nframes + 8
@@ -74,6 +78,8 @@ class SyntheticSource:
         y[py:py + OBJ, px:px + OBJ] = self.obj[: min(OBJ, h - py), : min(OBJ, w - px)]
         rng = np.random.default_rng(self.seed * 1000 + i)
         y = y + rng.normal(0.0, 1.0, y.shape)
+        if self.fade:
+            y = y * max(0.05, 1.0 - self.fade * i)
         cw, ch = w // 2, h // 2
         cx, cy = (PAN_X * i) // 2, (PAN_Y * i) // 2
         u = self.ctex[0][cy:cy + ch, cx:cx + cw]

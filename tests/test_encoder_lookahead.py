@@ -44,12 +44,12 @@ def _bin(name):
     return p
 
 
-def _source(tmp_path, w, h, frames, depth=8):
+def _source(tmp_path, w, h, frames, depth=8, fade=0.0):
     from src.x265_amd.synth import SyntheticSource
 
-    path = tmp_path / f"src_{w}x{h}_{frames}_{depth}.yuv"
+    path = tmp_path / f"src_{w}x{h}_{frames}_{depth}_{fade}.yuv"
     if not path.exists():
-        SyntheticSource(w, h, frames, depth).write_yuv(str(path))
+        SyntheticSource(w, h, frames, depth, fade=fade).write_yuv(str(path))
     return path
 
 
@@ -80,6 +80,19 @@ def test_hooked_encoder_equals_reference_on_cpu(tmp_path, size, frames, mode):
     assert got == ref, f"X265AMD_LOOKAHEAD={mode}: bitstream differs from the reference encoder"
 
 
+def test_hooked_encoder_weighted_fade_equals_reference_on_cpu(tmp_path):
+    """a luma fade: weightsAnalyse picks weights, so the hook's weighted paths run (the weighted P
+    estimate on the thread's wbuffer, weighted B estimates on the host loop) — host control flow"""
+    w, h, n = 640, 360, 24
+    src = _source(tmp_path, w, h, n, fade=0.03)
+    rc, ref, _, err = encode(_bin("x265ref8"), src, w, h, n, tmp_path / "ref.hevc")
+    assert rc == 0, err[-2000:]
+    assert re.search(r"Weighted P-Frames: Y:[1-9]", err), "the fade clip must trigger weighted prediction"
+    rc, got, _, err = encode(_bin("x265la8"), src, w, h, n, tmp_path / "la.hevc", {"X265AMD_LOOKAHEAD": "host"})
+    assert rc == 0, err[-2000:]
+    assert got == ref
+
+
 def test_lookahead_encoder_fails_loudly_without_device(tmp_path):
     import torch
 
@@ -104,6 +117,23 @@ def test_gpu_lookahead_encode_1080p_medium_is_bit_exact(tmp_path):
     assert "[x265la] lookahead estimates on the MI355X" in err
     print(f"\n[x265la] 1080p medium {n} frames, --pools 16: reference {ref_fps} fps, MI355X lookahead {la_fps} fps")
     assert got == ref, "bitstream with the MI355X lookahead differs from the reference encoder"
+
+
+@pytest.mark.gpu
+def test_gpu_lookahead_weighted_fade_is_bit_exact(tmp_path):
+    """the weighted paths on the device — a luma fade makes weightsAnalyse choose weights, so
+    P estimates run on the thread's weighted planes (x265amd_la_pcost with weighted_buffer) and weighted
+    B estimates take the host loop; the encode equals the reference and the stats show both happened"""
+    w, h, n = 640, 360, 24
+    src = _source(tmp_path, w, h, n, fade=0.03)
+    rc, ref, _, err = encode(_bin("x265ref8"), src, w, h, n, tmp_path / "ref.hevc")
+    assert rc == 0, err[-2000:]
+    rc, got, _, err = encode(_bin("x265la8"), src, w, h, n, tmp_path / "la.hevc", {"X265AMD_LA_STATS": "1"})
+    assert rc == 0, err[-3000:]
+    assert re.search(r"Weighted P-Frames: Y:[1-9]", err)
+    m = re.search(r"stats P weighted\s+calls\s+(\d+)", err)
+    assert m and int(m.group(1)) > 0, err[-3000:]
+    assert got == ref, "weighted estimates on the device changed the bitstream"
 
 
 @pytest.mark.gpu

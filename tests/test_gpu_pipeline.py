@@ -25,6 +25,8 @@ def test_gpu_native_exchange_loopback():
 
     comm = Comm(1, 0)
     try:
+        # torch has RCCL loaded already: the C ABI must bind that copy, not load a second runtime
+        assert comm.backend and comm.backend.startswith("already loaded"), comm.backend
         g = torch.Generator(device="cuda").manual_seed(3)
         src = [torch.randint(0, 256, (n,), dtype=torch.uint8, device="cuda", generator=g) for n in (1, 4097, 1 << 20)]
         dst = [torch.zeros_like(t) for t in src]
