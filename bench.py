@@ -62,6 +62,11 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 
 
+def progress(msg: str) -> None:
+    """a progress line on stderr (long phases — the encoder runs — must not look hung)"""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -274,6 +279,7 @@ def reference_encoder_baseline(args):
         SyntheticSource(args.width, args.height, n_all, 8).write_yuv(src)
         fps_all, _, _ = _x265_run(exe, src, args.width, args.height, 8, n_all,
                                   ["--preset", args.preset, "--pools", str(cores)])
+        progress(f"cpu_baseline {cores} cores: {fps_all} fps")
         fps_one, _, _ = _x265_run(exe, src, args.width, args.height, 8, n_one,
                                   ["--preset", args.preset, "--pools", "1", "-F", "1"], one_core=True)
     return {"value": round(fps_all, 3), "unit": "fps", "cores": cores, "kind": "reference",
@@ -331,6 +337,7 @@ def encoder_level(args, reps=5, width=None, height=None, frames=None, provider=T
         for _ in range(reps):
             for k, exe, env, _ in arms:
                 f, m, _ = _x265_run(exe, src, W, H, 8, n, extra, env=dict(os.environ, **env), timeout=600)
+                progress(f"encoder_level {W}x{H} {k}: {f} fps")
                 runs[k].append(f)
                 md5.setdefault(k, set()).add(m)
     ref = runs["reference"]
@@ -412,6 +419,7 @@ def pipeline_rates(prims, args, census, local, skip=()):
     for br, seg in ((0, 0), (4, 0), (0, 8), (0, 1)):
         if (br, seg) in skip:
             continue
+        progress(f"pipeline form band_rows={br} segments={seg}")
         pipe = GpuFramePipeline(prims, args.width, args.height, args.depth, F, 1, 0, census=census,
                                 band_rows=br or None, segment_frames=seg or None, streams=args.streams,
                                 device=f"cuda:{local}")
@@ -586,6 +594,7 @@ def main():
     calls = sum(b.n for b in batches)
     dominant, ktimes, launches = rep.dominant, rep.ktimes, rep.launches
 
+    progress(f"timing {args.steps} steps ({args.mode})")
     for _ in range(args.warmup):
         run()
     barrier(world)
@@ -695,6 +704,7 @@ def main():
             else:
                 cpu["census_replay"] = creplay
         if world == 1 and not args.no_encoder_level:
+            progress("encoder_level runs")
             try:
                 enc = encoder_level(args, reps=args.encoder_reps)
                 if (args.width, args.height) == (1920, 1080) and args.preset == "medium":

@@ -167,23 +167,40 @@ __device__ __forceinline__ void load_win_dw(const uint8_t* p, uint32_t (&W)[(NB 
 }
 
 template <int TAPS, int UW>
+__device__ __forceinline__ void hfilter_dot(const uint8_t* src, const int (&cp)[TAPS / 4], int (&sum)[UW]);
+
+// the horizontal 8-bit filter split into its window load and its arithmetic, so a kernel can issue
+// the loads of several rows before the first row's sums (and before any store: a store between
+// two loads of possibly aliasing pointers pins the order, and gfx9's vmcnt counts both)
+template <int TAPS, int UW>
+struct HWin
+{
+    static constexpr int NB = UW + TAPS - 1, ND = (NB + 3) / 4;
+    uint32_t W[ND];
+    __device__ __forceinline__ void load(const uint8_t* src) { load_win_dw<NB>(src - (TAPS / 2 - 1), W); }
+    __device__ __forceinline__ void sums(const int (&cp)[TAPS / 4], int (&sum)[UW]) const
+    {
+#pragma unroll
+        for (int x = 0; x < UW; x++)
+        {
+            int s = 128 * 64;
+#pragma unroll
+            for (int k = 0; k < TAPS / 4; k++)
+            {
+                const int b = x + 4 * k;
+                s = __builtin_amdgcn_sdot4((int)alignb(W[(b >> 2) + ((b & 3) ? 1 : 0)], W[b >> 2], b & 3), cp[k], s, false);
+            }
+            sum[x] = s;
+        }
+    }
+};
+
+template <int TAPS, int UW>
 __device__ __forceinline__ void hfilter_dot(const uint8_t* src, const int (&cp)[TAPS / 4], int (&sum)[UW])
 {
-    constexpr int NB = UW + TAPS - 1;
-    uint32_t W[(NB + 3) / 4];
-    load_win_dw<NB>(src - (TAPS / 2 - 1), W);
-#pragma unroll
-    for (int x = 0; x < UW; x++)
-    {
-        int s = 128 * 64;
-#pragma unroll
-        for (int k = 0; k < TAPS / 4; k++)
-        {
-            const int b = x + 4 * k;
-            s = __builtin_amdgcn_sdot4((int)alignb(W[(b >> 2) + ((b & 3) ? 1 : 0)], W[b >> 2], b & 3), cp[k], s, false);
-        }
-        sum[x] = s;
-    }
+    HWin<TAPS, UW> w;
+    w.load(src);
+    w.sums(cp, sum);
 }
 
 typedef short s16x2 __attribute__((ext_vector_type(2)));
@@ -387,11 +404,18 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_interp(const BatchGroup g)
 
         if constexpr (OP == X265AMD_HPP || OP == X265AMD_HPS)
         {
+            // 8 bit: every row window of the unit loaded before the first sum / store
+            HWin<TAPS, DOT ? UW : 4> win[DOT ? UH : 1];
+            if constexpr (DOT)
+            {
+#pragma unroll
+                for (int r = 0; r < UH; r++) win[r].load((const uint8_t*)ps + (y0 + r) * ss + x);
+            }
 #pragma unroll
             for (int r = 0; r < UH; r++)
             {
                 int sum[UW], o[UW];
-                if constexpr (DOT) hfilter_dot<TAPS, UW>((const uint8_t*)ps + (y0 + r) * ss + x, cp, sum);
+                if constexpr (DOT) win[r].sums(cp, sum);
                 else hfilter<P, TAPS, UW>((const P*)ps + (y0 + r) * ss + x, c, sum);
                 if constexpr (DOT && OP == X265AMD_HPP)
                 {
@@ -610,7 +634,12 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_hvpp(const BatchGroup g)
 //
 // STG (8 bit, compact destinations, power-of-two w and h <= 16): the output
 // rows go to wave-private LDS and leave through stage_writeback.
-template <typename P, int SW, bool STG = false>
+//
+// PF (8 bit): the source windows of each 8-row body are loaded before its first sum — PF = 1 —
+// or one body ahead, while the current body is computed from registers — PF = 2 — so a lane has
+// 8 row loads in flight instead of one (rows past the block clamp to its last row; their
+// results are never used).
+template <typename P, int SW, bool STG = false, int PF = 0>
 __global__ __launch_bounds__(X265AMD_BLOCK) void k_hvpp_stream(const BatchGroup g)
 {
     const uint32_t gb = xcd_block();
@@ -637,6 +666,7 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_hvpp_stream(const BatchGroup 
     const IfConst K(g.depth);
     const int cidx = ((const uint8_t*)sub.b)[job];
     constexpr bool DOT = sizeof(P) == 1;
+    static_assert(!PF || DOT, "row prefetch: 8-bit path");
     int cp[2], cx[8], cy[8];
     if constexpr (DOT) pack_taps<8>(cidx & 15, cp);
     else get_taps<8>(cidx & 15, cx);
@@ -660,18 +690,38 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_hvpp_stream(const BatchGroup 
             for (int x = 0; x < SW; x++) I[x] = (int)(int16_t)((S[x] + K.ps_off) >> K.ps_shift);
         }
     };
+    using Win = HWin<8, SW>;
+    auto load_body = [&](int r0, Win (&wb)[8]) {
+#pragma unroll
+        for (int i = 0; i < 8; i++)
+        {
+            const int r = r0 + i < R ? r0 + i : R - 1;
+            wb[i].load((const uint8_t*)(ps + (intptr_t)r * ss));
+        }
+    };
     uint32_t Pr[8][SW];                  // ring of vertical pairs: Pr[r & 7][x] = (I[r][x], I[r + 1][x])
     int Iprev[SW];
+    Win wa[PF ? 8 : 1], wn[PF == 2 ? 8 : 1];
+    if constexpr (PF) load_body(1, wa);
     inter(ps, Iprev);
     for (int r0 = 1; r0 < R; r0 += 8)
     {
+        if constexpr (PF == 1)
+        {
+            if (r0 > 1) load_body(r0, wa);
+        }
+        else if constexpr (PF == 2)
+        {
+            if (r0 + 8 < R) load_body(r0 + 8, wn);
+        }
 #pragma unroll
         for (int i = 0; i < 8; i++)
         {
             const int r = r0 + i;                        // row whose intermediate is formed now
             if (r >= R) break;
             int I[SW];
-            inter(ps + (intptr_t)r * ss, I);
+            if constexpr (PF) wa[i].sums(cp, I);
+            else inter(ps + (intptr_t)r * ss, I);
             // P[r - 1] goes to ring slot (r - 1) & 7 = i (r0 = 1 mod 8): compile-time
 #pragma unroll
             for (int x = 0; x < SW; x++)
@@ -702,8 +752,26 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_hvpp_stream(const BatchGroup 
                 else store_row<P, SW>(pd + (intptr_t)y * ds, o);
             }
         }
+        if constexpr (PF == 2)
+        {
+#pragma unroll
+            for (int i = 0; i < 8; i++) wa[i] = wn[i];
+        }
     }
     if constexpr (STG) stage_writeback<STG_WAVE>((const uint8_t*)stg_lds + (threadIdx.x >> 6) * STG_WAVE, pd, lg, w * h, wjob0, n);
+}
+
+// row-prefetch variant of the 8-bit streaming hv_pp (X265AMD_HVPP_PF = 0 / 1 / 2; default below)
+static int hvpp_pf()
+{
+    static int v = -1;
+    if (v < 0)
+    {
+        const char* e = getenv("X265AMD_HVPP_PF");
+        v = e ? atoi(e) : 1;
+        if (v < 0 || v > 2) v = 1;
+    }
+    return v;
 }
 
 // -------------------------------------------------------------- dispatch
@@ -773,11 +841,25 @@ static int launch_interp(int cls, const BatchGroup& g, uint32_t blocks, hipStrea
     if constexpr (OP == X265AMD_HVPP)
         if (cls == kHvppStream || cls == kHvppStream4 || cls == (kHvppStream | kStaged))
         {
-            if (cls == kHvppStream) hipLaunchKernelGGL((k_hvpp_stream<P, 8>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, g);
+            const int pf = sizeof(P) == 1 ? hvpp_pf() : 0;
+            if (cls == kHvppStream)
+            {
+                if constexpr (sizeof(P) == 1)
+                {
+                    if (pf == 1) hipLaunchKernelGGL((k_hvpp_stream<P, 8, false, 1>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, g);
+                    else if (pf == 2) hipLaunchKernelGGL((k_hvpp_stream<P, 8, false, 2>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, g);
+                    else hipLaunchKernelGGL((k_hvpp_stream<P, 8>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, g);
+                }
+                else hipLaunchKernelGGL((k_hvpp_stream<P, 8>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, g);
+            }
             else if (cls == (kHvppStream | kStaged))
             {
                 if constexpr (sizeof(P) == 1)
-                    hipLaunchKernelGGL((k_hvpp_stream<P, 8, true>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, g);
+                {
+                    if (pf == 1) hipLaunchKernelGGL((k_hvpp_stream<P, 8, true, 1>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, g);
+                    else if (pf == 2) hipLaunchKernelGGL((k_hvpp_stream<P, 8, true, 2>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, g);
+                    else hipLaunchKernelGGL((k_hvpp_stream<P, 8, true>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, g);
+                }
             }
             else hipLaunchKernelGGL((k_hvpp_stream<P, 4>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, g);
             return (int)hipGetLastError();

@@ -407,6 +407,166 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_tr32_mfma(int n, int depth,
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// k_tr32_i8: the same two 32x32x32 products on the INTEGER matrix cores
+// (v_mfma_i32_32x32x32_i8: int8 operands, exact int32 accumulation, twice the K of the f16 form
+// per instruction).  Every int16 operand x is split into its bytes, x = 256 * hi + lo with
+// hi = x >> 8 in [-128, 127] (the high byte as stored) and lo = x & 255; lo enters the MFMA as the
+// signed byte lo - 128 (lo ^ 0x80), so
+//     sum_k c_k x_k = 256 * sum_k c_k hi_k + sum_k c_k (lo_k - 128) + 128 * sum_k c_k,
+// with the transform coefficients c (|c| <= 90) as the constant int8 operand.  The last term is a
+// constant of the output element: 128 x the row sum of the constant operand (forward: every row of
+// the DCT matrix but row 0 sums to 0, row 0 to 64 * 32) or its column sum (inverse), folded into
+// the rounding offset.  Recombination is one v_lshl_add per element, no float conversion; all
+// sums are exact in int32 (|256 * sum c hi| <= 256 * 32 * 90 * 128 < 2^31).
+// The k order inside a product only has to agree between its two operands: stage 1 takes the
+// 16 loaded values of a lane half as k = 16h + j, stage 2 takes the stage-1 accumulator registers
+// as they lie (register j of lane half h = row (j&3) + 8(j>>2) + 4h), with the constant operand
+// permuted to match — no data moves between the stages.
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x16 __attribute__((ext_vector_type(16)));
+
+// bytes of 8 packed int16 pairs (16 values in order) -> the lo fragment (biased) and hi fragment
+__device__ __forceinline__ void split_bytes(const uint32_t (&d)[8], i32x4& lo, i32x4& hi)
+{
+#pragma unroll
+    for (int q = 0; q < 4; q++)
+    {
+        lo[q] = (int)(__builtin_amdgcn_perm(d[2 * q + 1], d[2 * q], 0x06040200u) ^ 0x80808080u);
+        hi[q] = (int)__builtin_amdgcn_perm(d[2 * q + 1], d[2 * q], 0x07050301u);
+    }
+}
+
+template <bool FWD>
+__global__ __launch_bounds__(X265AMD_BLOCK) void k_tr32_i8(int n, int depth,
+    const int16_t* __restrict__ src, intptr_t ss, const int64_t* __restrict__ soff,
+    int16_t* __restrict__ dst, intptr_t ds, const int64_t* __restrict__ doff)
+{
+    __shared__ int16_t tile[kTrWaves][32 * 32];
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63, r = l & 31, h = l >> 5;
+    int16_t* T = tile[w];
+    const int sh1 = FWD ? 4 + depth - 8 : 7, sh2 = FWD ? 11 : 12 - (depth - 8);
+    const int io_row = l >> 1, io_col = 16 * (l & 1);
+
+    // constant int8 fragments: stage 1 in the natural k order of the lane half (k = 16h + j),
+    // stage 2 in the accumulator's row order (k = (j&3) + 8(j>>2) + 4h)
+    i32x4 c1, c2;
+    int csum = 0;                                    // 128 x the column sum of T at column r (inverse)
+#pragma unroll
+    for (int q = 0; q < 4; q++)
+    {
+        uint32_t a = 0, b = 0;
+#pragma unroll
+        for (int e = 0; e < 4; e++)
+        {
+            const int j = 4 * q + e, kn = 16 * h + j, kp = (j & 3) + 8 * (j >> 2) + 4 * h;
+            a |= (uint32_t)(uint8_t)(int8_t)(FWD ? c_t32.m[r][kn] : c_t32.m[kn][r]) << (8 * e);
+            b |= (uint32_t)(uint8_t)(int8_t)(FWD ? c_t32.m[r][kp] : c_t32.m[kp][r]) << (8 * e);
+        }
+        c1[q] = (int)a;
+        c2[q] = (int)b;
+    }
+#pragma unroll
+    for (int k = 0; k < 32; k++) csum += c_t32.m[k][r];
+    csum *= 128;
+    // bias + rounding offsets per stage: forward stage 1 (column r of U = X T^T: row r of T, zero
+    // sum unless r == 0), forward stage 2 (row 0 of T, register 0 of lane half 0 only), inverse
+    // (column sums of T at the lane's column, both stages)
+    const int k1 = (FWD ? (r == 0 ? 128 * 64 * 32 : 0) : csum) + (1 << (sh1 - 1));
+    const int k2 = FWD ? (1 << (sh2 - 1)) : csum + (1 << (sh2 - 1));
+    const int k20 = FWD && h == 0 ? 128 * 64 * 32 : 0;
+
+    const int64_t step = (int64_t)gridDim.x * kTrWaves;
+    int64_t job = (int64_t)blockIdx.x * kTrWaves + w;
+    uint4 nx[2];
+    auto fetch = [&](int64_t jb) {
+        const int16_t* s = src + soff[jb];
+        if constexpr (FWD)
+        {
+            nx[0] = ldu<uint4>(s + r * ss + 16 * h);
+            nx[1] = ldu<uint4>(s + r * ss + 16 * h + 8);
+        }
+        else
+        {
+            nx[0] = ldu<uint4>(s + io_row * ss + io_col);
+            nx[1] = ldu<uint4>(s + io_row * ss + io_col + 8);
+        }
+    };
+    if (job < n) fetch(job);
+    for (; job < n; job += step)
+    {
+        int16_t* d = dst + doff[job];
+        const uint4 cx[2] = { nx[0], nx[1] };
+        if (job + step < n) fetch(job + step);
+        // ---- stage 1: forward U = X T^T (A = source row r, k = 16h + j);
+        //      inverse M1 = C^T T (A = coefficient column r, staged through the tile)
+        uint32_t x[8];
+        if constexpr (FWD)
+        {
+            x[0] = cx[0].x; x[1] = cx[0].y; x[2] = cx[0].z; x[3] = cx[0].w;
+            x[4] = cx[1].x; x[5] = cx[1].y; x[6] = cx[1].z; x[7] = cx[1].w;
+        }
+        else
+        {
+            stu<uint4>(&T[io_row * 32 + io_col], cx[0]);
+            stu<uint4>(&T[io_row * 32 + io_col + 8], cx[1]);
+            wave_sync();
+#pragma unroll
+            for (int q = 0; q < 8; q++)
+                x[q] = pack16(T[(16 * h + 2 * q) * 32 + r], T[(16 * h + 2 * q + 1) * 32 + r]);
+        }
+        i32x4 xl, xh;
+        split_bytes(x, xl, xh);
+        i32x16 lo1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(xl, c1, (i32x16){}, 0, 0, 0);
+        i32x16 hi1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(xh, c1, (i32x16){}, 0, 0, 0);
+        int v[16];
+#pragma unroll
+        for (int i = 0; i < 16; i++)
+        {
+            const int a = (int)(((uint32_t)hi1[i] << 8) + (uint32_t)lo1[i]) + k1;
+            v[i] = FWD ? (a >> sh1) : clip16(a >> sh1);   // forward: the int16 wrap is the byte split below
+        }
+        // ---- stage 2 from registers: forward Dst = T U' (U' as B); inverse Res = M1'^T T (M1' as A)
+        uint32_t y[8];
+#pragma unroll
+        for (int q = 0; q < 8; q++) y[q] = pack16(v[2 * q], v[2 * q + 1]);
+        split_bytes(y, xl, xh);
+        i32x16 lo2, hi2;
+        if constexpr (FWD)
+        {
+            lo2 = __builtin_amdgcn_mfma_i32_32x32x32_i8(c2, xl, (i32x16){}, 0, 0, 0);
+            hi2 = __builtin_amdgcn_mfma_i32_32x32x32_i8(c2, xh, (i32x16){}, 0, 0, 0);
+        }
+        else
+        {
+            lo2 = __builtin_amdgcn_mfma_i32_32x32x32_i8(xl, c2, (i32x16){}, 0, 0, 0);
+            hi2 = __builtin_amdgcn_mfma_i32_32x32x32_i8(xh, c2, (i32x16){}, 0, 0, 0);
+        }
+#pragma unroll
+        for (int i = 0; i < 16; i++)
+        {
+            const int a = (int)(((uint32_t)hi2[i] << 8) + (uint32_t)lo2[i]) + k2 + (i == 0 ? k20 : 0);
+            T[((i & 3) + 8 * (i >> 2) + 4 * h) * 32 + r] = (int16_t)(FWD ? (a >> sh2) : clip16(a >> sh2));
+        }
+        wave_sync();
+#pragma unroll
+        for (int c = 0; c < 16; c += 8) stu<uint4>(d + io_row * ds + io_col + c, ldu<uint4>(&T[io_row * 32 + io_col + c]));
+        wave_sync();
+    }
+}
+
+// the integer-MFMA 32x32 transforms (X265AMD_TR_I8=0 selects the f16 split form)
+static bool tr_i8()
+{
+    static int v = -1;
+    if (v < 0)
+    {
+        const char* e = getenv("X265AMD_TR_I8");
+        v = e ? atoi(e) != 0 : 0;
+    }
+    return v != 0;
+}
+
 template <bool FWD>
 __global__ __launch_bounds__(X265AMD_BLOCK) void k_tr16_mfma(int n, int depth,
     const int16_t* __restrict__ src, intptr_t ss, const int64_t* __restrict__ soff,
@@ -921,7 +1081,8 @@ extern "C" int x265amd_transform(int kind, int depth, int size, int n,
         // matrix cores: one wavefront per transform
         const dim3 grid(mfma_grid(size == 16 ? (n + 3) / 4 : n));
 #define M(K) hipLaunchKernelGGL(K, grid, dim3(X265AMD_BLOCK), 0, st, n, depth, src, src_stride, src_off, dst, dst_stride, dst_off)
-        if (size == 32) { if (fwd) M(k_tr32_mfma<true>); else M(k_tr32_mfma<false>); }
+        if (size == 32 && tr_i8()) { if (fwd) M(k_tr32_i8<true>); else M(k_tr32_i8<false>); }
+        else if (size == 32) { if (fwd) M(k_tr32_mfma<true>); else M(k_tr32_mfma<false>); }
         else { if (fwd) M(k_tr16_mfma<true>); else M(k_tr16_mfma<false>); }
 #undef M
         return (int)hipGetLastError();
