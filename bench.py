@@ -298,7 +298,7 @@ ENCODER_ARMS = (
      "LookaheadTLD::lowresIntraEstimate and every CostEstimateGroup estimate (P / B, lowres motion searches, "
      "batched per finishBatch)"),
     ("mi355x_lookahead_me", "x265la8", {"X265AMD_ME": "gpu"},
-     "the lookahead estimates as above, plus the main encoder's motion searches of PUs >= 32x32 "
+     "the lookahead estimates as above, plus the main encoder's motion searches of 64x64 PUs "
      "(Search::predInterSearch's per-reference motionEstimate calls of a CU in one device batch, "
      "integration/gpu_me.cpp)"),
 )

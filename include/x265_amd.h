@@ -781,6 +781,14 @@ typedef struct
 } x265amd_mes_job;
 int x265amd_mes_search(x265amd_mes* mes, int w, int h, const void* fenc, intptr_t fenc_stride, int n,
                        x265amd_mes_job* jobs);
+/* the same searches without waiting: _submit enqueues them on the calling thread's stream (its own
+ * staging, separate from _search's) and returns; _collect waits for them and writes the outputs into
+ * `jobs` (n = the submitted count).  One outstanding submit per thread: the encoder issues a CTU's
+ * 64x64 searches when its analysis starts and collects them when Search::predInterSearch needs them,
+ * after the CTU's split recursion has run on the host meanwhile. */
+int x265amd_mes_submit(x265amd_mes* mes, int w, int h, const void* fenc, intptr_t fenc_stride, int n,
+                       const x265amd_mes_job* jobs);
+int x265amd_mes_collect(x265amd_mes* mes, int n, x265amd_mes_job* jobs);
 
 /* ------------------------------------------------------------------- f4
  * In-loop filters and border extension of device-resident 4:2:0 recon frames

@@ -8,7 +8,7 @@
  *   Search::predInterSearch(Mode&, const CUGeom&, bool, uint32_t[2])      search.cpp:2050-2420
  *     -> a PREFETCH, then the reference's own predInterSearch (x265ref_predInterSearch) unchanged.
  *        The prefetch forms, for the PU of a 2Nx2N CU of at least X265AMD_ME_MIN pixels
- *        (default 32x32), every search the unidirectional loop (:2181-2230) is about to make —
+ *        (default 64x64), every search the unidirectional loop (:2181-2230) is about to make —
  *        per (list, reference) allowed by refMasks: the AMVP candidates (getPMV), the lowres MV,
  *        and for EACH of the two AMVP predictors (selectMVP, :2199, picks one of them) its search
  *        range (setSearchRange) — and runs all of them in ONE device launch
@@ -46,6 +46,7 @@
 #include "picyuv.h"
 #include "slice.h"
 #include "search.h"
+#include "analysis.h"
 #include "motion.h"
 #include "reference.h"
 
@@ -65,6 +66,8 @@ extern "C" void x265ref_predInterSearch(Search* self, Mode& interMode, const CUG
                                         uint32_t refMasks[2]);
 extern "C" int x265ref_motionEstimate(MotionEstimate* self, ReferencePlanes* ref, const MV& mvmin, const MV& mvmax,
                                       const MV& qmvp, int numCandidates, const MV* mvc, int merange, MV& outQMv);
+extern "C" SplitData x265ref_compressInterCU_rd0_4(Analysis* self, const CUData& parentCTU, const CUGeom& cuGeom,
+                                                   int32_t qp);
 
 namespace {
 
@@ -77,7 +80,8 @@ struct CostPeek : public MotionEstimate
 
 enum { ME_GPU = 0, ME_CPU = 1, ME_HOST = 2, ME_CHECK = 3 };
 int g_mode = ME_GPU;
-int g_min_area = 32 * 32;
+bool g_async = true;           /* X265AMD_ME_ASYNC=0: no CTU-start submit, every search synchronous */
+int g_min_area = 64 * 64;      /* measured: 64x64 only beats 32x32 + 64x64 (profiles/r04/encoder_me_variants.txt) */
 bool g_stats_on = false;
 pthread_once_t g_once = PTHREAD_ONCE_INIT;
 pthread_mutex_t g_mu = PTHREAD_MUTEX_INITIALIZER;
@@ -112,6 +116,8 @@ void read_mode()
              (m && !strcmp(m, "check")) ? ME_CHECK : (m && !strcmp(m, "gpu")) ? ME_GPU : la_cpu ? ME_CPU : ME_GPU;
     if (const char* a = getenv("X265AMD_ME_MIN"))
         g_min_area = atoi(a);
+    if (const char* a = getenv("X265AMD_ME_ASYNC"))
+        g_async = atoi(a) != 0;
     const char* st = getenv("X265AMD_ME_STATS");
     g_stats_on = (st && *st && strcmp(st, "0")) || g_mode == ME_CHECK;
     fprintf(stderr, "[x265me] motion searches of PUs >= %d pixels on %s\n", g_min_area,
@@ -196,28 +202,37 @@ struct Memo
 };
 struct Prefetch
 {
-    const MotionEstimate* me;
+    const MotionEstimate* me;                /* the MotionEstimate the searches belong to (NULL: none ready) */
+    const uint16_t* cost;                    /* its BitCost table when they were formed */
     int n, nskip;
     Memo m[MAX_JOBS];
     const ReferencePlanes* skip[MAX_JOBS];   /* references left to the host (weighted) */
+    /* an asynchronous prefetch issued at the start of a CTU's analysis, collected by predInterSearch */
+    x265amd_mes* mes;
+    const Mode* mode;                        /* the Mode whose searches it holds */
+    x265amd_mes_job jobs[MAX_JOBS];
+    int pending;
+    double t0;
 };
+/* per thread: the synchronous prefetch of the PU being searched, and the asynchronous one submitted
+ * when the CTU's analysis started (collected by its 64x64 predInterSearch) */
 __thread Prefetch* t_pf = NULL;
+__thread Prefetch* t_apf = NULL;
 
-Prefetch* prefetch_buf()
+Prefetch* prefetch_buf(Prefetch*& p)
 {
-    if (!t_pf)
+    if (!p)
     {
-        t_pf = (Prefetch*)calloc(1, sizeof(Prefetch));
-        if (!t_pf) abort();
+        p = (Prefetch*)calloc(1, sizeof(Prefetch));
+        if (!p) abort();
     }
-    return t_pf;
+    return p;
 }
 
-const Memo* lookup(const MotionEstimate* me, const ReferencePlanes* ref, const MV& mvmin, const MV& mvmax,
-                   const MV& qmvp, int numc, const MV* mvc, int merange)
+const Memo* lookup1(const Prefetch* pf, const MotionEstimate* me, const uint16_t* cost, const ReferencePlanes* ref,
+                    const MV& mvmin, const MV& mvmax, const MV& qmvp, int numc, const MV* mvc, int merange)
 {
-    const Prefetch* pf = t_pf;
-    if (!pf || pf->me != me) return NULL;
+    if (!pf || pf->me != me || pf->cost != cost) return NULL;
     for (int i = 0; i < pf->n; i++)
     {
         const Memo& e = pf->m[i];
@@ -231,6 +246,28 @@ const Memo* lookup(const MotionEstimate* me, const ReferencePlanes* ref, const M
     return NULL;
 }
 
+const Memo* lookup(const MotionEstimate* me, const uint16_t* cost, const ReferencePlanes* ref, const MV& mvmin,
+                   const MV& mvmax, const MV& qmvp, int numc, const MV* mvc, int merange)
+{
+    const Memo* e = lookup1(t_pf, me, cost, ref, mvmin, mvmax, qmvp, numc, mvc, merange);
+    return e ? e : lookup1(t_apf, me, cost, ref, mvmin, mvmax, qmvp, numc, mvc, merange);
+}
+
+/* was a prefetch active for this MotionEstimate, and did it leave `ref` to the host */
+bool active_for(const MotionEstimate* me, const ReferencePlanes* ref, bool* skipped)
+{
+    bool act = false;
+    *skipped = false;
+    for (const Prefetch* pf : { (const Prefetch*)t_pf, (const Prefetch*)t_apf })
+        if (pf && pf->me == me)
+        {
+            act = true;
+            for (int i = 0; i < pf->nskip; i++)
+                *skipped |= pf->skip[i] == ref;
+        }
+    return act;
+}
+
 } // namespace
 
 namespace X265_NS {
@@ -238,16 +275,12 @@ namespace X265_NS {
 int MotionEstimate::motionEstimate(ReferencePlanes* ref, const MV& mvmin, const MV& mvmax, const MV& qmvp,
                                    int numCandidates, const MV* mvc, int merange, MV& outQMv)
 {
-    const Memo* e = lookup(this, ref, mvmin, mvmax, qmvp, numCandidates, mvc, merange);
+    const Memo* e = lookup(this, m_cost, ref, mvmin, mvmax, qmvp, numCandidates, mvc, merange);
     if (!e)
     {
-        if (t_pf && t_pf->me == this)
-        {
-            bool skipped = false;
-            for (int i = 0; i < t_pf->nskip; i++)
-                skipped |= t_pf->skip[i] == ref;
+        bool skipped;
+        if (active_for(this, ref, &skipped))
             stat_add(skipped ? &Stats::skipped : &Stats::misses, 1);
-        }
         return x265ref_motionEstimate(this, ref, mvmin, mvmax, qmvp, numCandidates, mvc, merange, outQMv);
     }
     stat_add(&Stats::hits, 1);
@@ -272,116 +305,189 @@ int MotionEstimate::motionEstimate(ReferencePlanes* ref, const MV& mvmin, const 
     return e->cost;
 }
 
+} // namespace X265_NS
+
+namespace {
+
+/* Form the searches the unidirectional loop of Search::predInterSearch (search.cpp:2181-2230) makes
+ * for PU 0 of interMode — per (list, reference) allowed by refMasks: getPMV, the lowres MV and, for each
+ * of the two AMVP predictors, setSearchRange — into pf->m[] (memo keys) and jobs[] (device
+ * descriptors), after making the reference rows the encoder has finished resident on the device.
+ * set_range forwards to the protected Search::setSearchRange.  Returns the number formed. */
+template <class SetRange>
+int form_searches(Search& S, Mode& interMode, const PredictionUnit& pu, const uint32_t refMasks[2], Prefetch* pf,
+                  x265amd_mes_job* jobs, x265amd_mes** mes_out, SetRange set_range)
+{
+    CUData& cu = interMode.cu;
+    const Slice* slice = S.m_slice;
+    const x265_param* param = S.m_param;
+    pf->me = NULL;
+    pf->n = pf->nskip = 0;
+    pf->cost = S.m_me.*CostPeek::member();
+    cu.getNeighbourMV(0, pu.puAbsPartIdx, interMode.interNeighbours);
+    const int numPredDir = slice->isInterP() ? 1 : 2;
+    x265amd_mes* mes = NULL;
+    int table = -1;
+    uint32_t refMask = refMasks[0] ? refMasks[0] : (uint32_t)-1;
+    for (int list = 0; list < numPredDir; list++, refMask >>= 16)
+        for (int ref = 0; ref < slice->m_numRefIdx[list]; ref++)
+        {
+            if (!(refMask & (1 << ref)))
+                continue;
+            MotionReference& mr = slice->m_mref[list][ref];
+            if (mr.isWeighted || !mr.reconPic || mr.fpelPlane[0] != mr.reconPic->m_picOrg[0])
+            {
+                pf->skip[pf->nskip++] = &mr;
+                continue;
+            }
+            int slot = 0;
+            if (g_mode != ME_HOST)
+            {
+                if (!mes && !(mes = session(*mr.reconPic, *param)))
+                    continue;
+                const Frame* rf = slice->m_refFrameList[list][ref];
+                if (x265amd_mes_ref(mes, mr.reconPic, rf->m_poc, mr.reconPic->m_picBuf[0],
+                                    const_cast<Frame*>(rf)->m_reconRowCount.get(), &slot))
+                {
+                    stat_add(&Stats::fallbacks, 1);
+                    continue;
+                }
+                if (table < 0 && x265amd_mes_table(mes, pf->cost, &table))
+                {
+                    table = -1;
+                    stat_add(&Stats::fallbacks, 1);
+                    continue;
+                }
+            }
+            MV mvc[MAX_CAND];
+            int numMvc = cu.getPMV(interMode.interNeighbours, list, ref, interMode.amvpCand[list][ref], mvc);
+            const MV* amvp = interMode.amvpCand[list][ref];
+            MV lmv = S.getLowresMV(cu, pu, list, ref);
+            if (lmv.notZero())
+                mvc[numMvc++] = lmv;
+            for (int c = 0; c < 2; c++)
+            {
+                if (c == 1 && amvp[1] == amvp[0])
+                    continue;
+                Memo& e = pf->m[pf->n];
+                e.ref = &mr;
+                set_range(cu, amvp[c], param->searchRange, e.mvmin, e.mvmax);
+                e.qmvp = amvp[c];
+                e.numc = numMvc;
+                for (int k = 0; k < numMvc; k++) e.mvc[k] = mvc[k];
+                e.merange = param->searchRange;
+                x265amd_mes_job& j = jobs[pf->n];
+                j.slot = slot;
+                j.table = table;
+                j.block_off = mr.reconPic->getLumaAddr(pu.ctuAddr, pu.cuAbsPartIdx + pu.puAbsPartIdx) -
+                              mr.reconPic->getLumaAddr(0);
+                j.mv_range[0] = e.mvmin.x;
+                j.mv_range[1] = e.mvmin.y;
+                j.mv_range[2] = e.mvmax.x;
+                j.mv_range[3] = e.mvmax.y;
+                j.mvp[0] = e.qmvp.x;
+                j.mvp[1] = e.qmvp.y;
+                j.num_cand = numMvc;
+                for (int k = 0; k < numMvc; k++)
+                {
+                    j.mvc[2 * k] = mvc[k].x;
+                    j.mvc[2 * k + 1] = mvc[k].y;
+                }
+                pf->n++;
+            }
+        }
+    *mes_out = mes;
+    return pf->n;
+}
+
+/* is a 2Nx2N PU of this CU searched on the device (large enough, the reference loop's plain path) */
+bool eligible(const Search& S, const CUGeom& cuGeom)
+{
+    const Slice* slice = S.m_slice;
+    return g_mode != ME_CPU && S.m_param->analysisMode != X265_ANALYSIS_LOAD && !S.m_param->bDistributeMotionEstimation &&
+           slice->isInterP() + slice->isInterB() > 0 && (1 << (2 * cuGeom.log2CUSize)) >= g_min_area;
+}
+
+void finish_stats(Prefetch* pf)
+{
+    if (!g_stats_on) return;
+    pthread_mutex_lock(&g_mu);
+    g_st.prefetch++;
+    g_st.searches += pf->n;
+    g_st.sec += now_s() - pf->t0;
+    pthread_mutex_unlock(&g_mu);
+}
+
+/* results of a submitted prefetch into its memo; false if the device call failed (the searches then run
+ * on the host) */
+bool collect(Prefetch* pf)
+{
+    if (!pf->mes)                              /* X265AMD_ME=host: computed when it was formed */
+    {
+        pf->pending = 0;
+        return true;
+    }
+    const int st = x265amd_mes_collect(pf->mes, pf->n, pf->jobs);
+    pf->pending = 0;
+    if (st)
+    {
+        fprintf(stderr, "[x265me] x265amd_mes_collect failed: %s\n", x265amd_strerror(st));
+        return false;
+    }
+    for (int i = 0; i < pf->n; i++)
+    {
+        pf->m[i].out = MV(pf->jobs[i].out_mv[0], pf->jobs[i].out_mv[1]);
+        pf->m[i].cost = pf->jobs[i].out_cost;
+    }
+    return true;
+}
+
+} // namespace
+
+namespace X265_NS {
+
 void Search::predInterSearch(Mode& interMode, const CUGeom& cuGeom, bool bChromaMC, uint32_t refMasks[2])
 {
     pthread_once(&g_once, read_mode);
-    CUData& cu = interMode.cu;
-    const Slice* slice = m_slice;
-    Prefetch* pf = NULL;
-    if (g_mode != ME_CPU && cu.getNumPartInter(0) == 1 && m_param->analysisMode != X265_ANALYSIS_LOAD &&
-        !m_param->bDistributeMotionEstimation && slice->isInterP() + slice->isInterB() > 0)
+    Prefetch* used = NULL;
+    if (interMode.cu.getNumPartInter(0) == 1 && eligible(*this, cuGeom))
     {
-        PredictionUnit pu(cu, cuGeom, 0);
-        if (pu.width * pu.height >= g_min_area)
+        PredictionUnit pu(interMode.cu, cuGeom, 0);
+        /* the same source block the reference loop sets up (search.cpp:2077) */
+        m_me.setSourcePU(*interMode.fencYuv, pu.ctuAddr, pu.cuAbsPartIdx, pu.puAbsPartIdx, pu.width, pu.height);
+        Prefetch* apf = t_apf;
+        if (m_me.bChromaSATD)
+            ;
+        else if (apf && apf->pending && apf->mode == &interMode)
         {
-            /* the same source block the reference loop sets up (search.cpp:2077) */
-            m_me.setSourcePU(*interMode.fencYuv, pu.ctuAddr, pu.cuAbsPartIdx, pu.puAbsPartIdx, pu.width, pu.height);
-            if (!m_me.bChromaSATD)
-                pf = prefetch_buf();
+            /* the searches submitted when this CTU's analysis started (compressInterCU_rd0_4 below) — every
+             * reference; the reference loop takes those its refMasks allow */
+            if (collect(apf))
+            {
+                apf->me = &m_me;
+                finish_stats(apf);
+                used = apf;
+            }
         }
-        if (pf)
+        else
         {
-            const double t0 = now_s();
-            pf->me = NULL;
-            pf->n = pf->nskip = 0;
-            cu.getNeighbourMV(0, pu.puAbsPartIdx, interMode.interNeighbours);
-            const int numPredDir = slice->isInterP() ? 1 : 2;
+            Prefetch* pf = prefetch_buf(t_pf);
+            pf->t0 = now_s();
             x265amd_mes* mes = NULL;
             x265amd_mes_job jobs[MAX_JOBS];
-            int table = -1;
-            uint32_t refMask = refMasks[0] ? refMasks[0] : (uint32_t)-1;
-            for (int list = 0; list < numPredDir; list++, refMask >>= 16)
-                for (int ref = 0; ref < slice->m_numRefIdx[list]; ref++)
-                {
-                    if (!(refMask & (1 << ref)))
-                        continue;
-                    MotionReference& mr = slice->m_mref[list][ref];
-                    if (mr.isWeighted || !mr.reconPic || mr.fpelPlane[0] != mr.reconPic->m_picOrg[0])
-                    {
-                        pf->skip[pf->nskip++] = &mr;
-                        continue;
-                    }
-                    int slot = 0;
-                    if (g_mode != ME_HOST)
-                    {
-                        if (!mes && !(mes = session(*mr.reconPic, *m_param)))
-                            continue;
-                        const Frame* rf = slice->m_refFrameList[list][ref];
-                        const int st = x265amd_mes_ref(mes, mr.reconPic, rf->m_poc, mr.reconPic->m_picBuf[0],
-                                                       const_cast<Frame*>(rf)->m_reconRowCount.get(), &slot);
-                        if (st)
-                        {
-                            stat_add(&Stats::fallbacks, 1);
-                            continue;
-                        }
-                        if (table < 0 && x265amd_mes_table(mes, m_me.*CostPeek::member(), &table))
-                        {
-                            table = -1;
-                            stat_add(&Stats::fallbacks, 1);
-                            break;
-                        }
-                    }
-                    /* the search inputs of search.cpp:2196-2206, for both AMVP predictors */
-                    MV mvc[MAX_CAND];
-                    int numMvc = cu.getPMV(interMode.interNeighbours, list, ref, interMode.amvpCand[list][ref], mvc);
-                    const MV* amvp = interMode.amvpCand[list][ref];
-                    MV lmv = getLowresMV(cu, pu, list, ref);
-                    if (lmv.notZero())
-                        mvc[numMvc++] = lmv;
-                    for (int c = 0; c < 2; c++)
-                    {
-                        if (c == 1 && amvp[1] == amvp[0])
-                            continue;
-                        Memo& e = pf->m[pf->n];
-                        e.ref = &mr;
-                        setSearchRange(cu, amvp[c], m_param->searchRange, e.mvmin, e.mvmax);
-                        e.qmvp = amvp[c];
-                        e.numc = numMvc;
-                        for (int k = 0; k < numMvc; k++) e.mvc[k] = mvc[k];
-                        e.merange = m_param->searchRange;
-                        x265amd_mes_job& j = jobs[pf->n];
-                        j.slot = slot;
-                        j.table = table;
-                        j.block_off = mr.reconPic->getLumaAddr(pu.ctuAddr, pu.cuAbsPartIdx + pu.puAbsPartIdx) -
-                                      mr.reconPic->getLumaAddr(0);
-                        j.mv_range[0] = e.mvmin.x;
-                        j.mv_range[1] = e.mvmin.y;
-                        j.mv_range[2] = e.mvmax.x;
-                        j.mv_range[3] = e.mvmax.y;
-                        j.mvp[0] = e.qmvp.x;
-                        j.mvp[1] = e.qmvp.y;
-                        j.num_cand = numMvc;
-                        for (int k = 0; k < numMvc; k++)
-                        {
-                            j.mvc[2 * k] = mvc[k].x;
-                            j.mvc[2 * k + 1] = mvc[k].y;
-                        }
-                        pf->n++;
-                    }
-                }
-            bool ok = pf->n > 0;
+            const int n = form_searches(*this, interMode, pu, refMasks, pf, jobs, &mes,
+                [this](const CUData& c, const MV& p, int r, MV& a, MV& b) { setSearchRange(c, p, r, a, b); });
+            bool ok = n > 0;
             if (ok && g_mode == ME_HOST)
-            {
-                for (int i = 0; i < pf->n; i++)
+                for (int i = 0; i < n; i++)
                 {
                     Memo& e = pf->m[i];
                     e.cost = x265ref_motionEstimate(&m_me, e.ref, e.mvmin, e.mvmax, e.qmvp, e.numc, e.mvc, e.merange,
                                                     e.out);
                 }
-            }
             else if (ok)
             {
-                const int st = x265amd_mes_search(mes, pu.width, pu.height, m_me.fencPUYuv.m_buf[0], FENC_STRIDE, pf->n,
+                const int st = x265amd_mes_search(mes, pu.width, pu.height, m_me.fencPUYuv.m_buf[0], FENC_STRIDE, n,
                                                   jobs);
                 if (st)
                 {
@@ -389,7 +495,7 @@ void Search::predInterSearch(Mode& interMode, const CUGeom& cuGeom, bool bChroma
                     ok = false;
                 }
                 else
-                    for (int i = 0; i < pf->n; i++)
+                    for (int i = 0; i < n; i++)
                     {
                         pf->m[i].out = MV(jobs[i].out_mv[0], jobs[i].out_mv[1]);
                         pf->m[i].cost = jobs[i].out_cost;
@@ -398,23 +504,86 @@ void Search::predInterSearch(Mode& interMode, const CUGeom& cuGeom, bool bChroma
             if (ok)
             {
                 pf->me = &m_me;
-                if (g_stats_on)
-                {
-                    pthread_mutex_lock(&g_mu);
-                    g_st.prefetch++;
-                    g_st.searches += pf->n;
-                    g_st.sec += now_s() - t0;
-                    pthread_mutex_unlock(&g_mu);
-                }
+                finish_stats(pf);
+                used = pf;
             }
         }
     }
     x265ref_predInterSearch(this, interMode, cuGeom, bChromaMC, refMasks);
-    if (pf)
+    if (used)
     {
-        pf->me = NULL;
-        pf->n = pf->nskip = 0;
+        used->me = NULL;
+        used->n = used->nskip = 0;
     }
+}
+
+/* Analysis::compressInterCU_rd0_4 (analysis.cpp:818-1100), --rd 0..4 (--preset medium: 3): the 64x64
+ * CU's 2Nx2N motion searches come last in its analysis (after the merge candidates and the whole split
+ * recursion, :945-953), but their inputs — the CU position, its neighbours' MVs (all in CTUs already
+ * coded), the lowres MVs, the QP's BitCost table — are known when the analysis starts.  So at depth 0
+ * the searches of EVERY reference are submitted to the device here (x265amd_mes_submit) and the host
+ * runs the reference analysis meanwhile; predInterSearch collects them, the reference loop takes those
+ * its refMasks allow.  The Mode's CU is initialised early exactly as :948 does it (nothing reads it
+ * before); inputs the reference call differs in (a changed QP table) miss the memo and run on the host. */
+SplitData Analysis::compressInterCU_rd0_4(const CUData& parentCTU, const CUGeom& cuGeom, int32_t qp)
+{
+    pthread_once(&g_once, read_mode);
+    if (cuGeom.depth == 0 && g_async && eligible(*this, cuGeom) &&
+        !(cuGeom.flags & CUGeom::SPLIT_MANDATORY))
+    {
+        Prefetch* pf = prefetch_buf(t_apf);
+        if (pf->pending)
+            (void)collect(pf);
+        Mode& im = m_modeDepth[0].pred[PRED_2Nx2N];
+        im.cu.initSubCU(parentCTU, cuGeom, qp);
+        PredictionUnit pu(im.cu, cuGeom, 0);
+        m_me.setSourcePU(*im.fencYuv, pu.ctuAddr, pu.cuAbsPartIdx, pu.puAbsPartIdx, pu.width, pu.height);
+        if (!m_me.bChromaSATD)
+        {
+            pf->t0 = now_s();
+            const uint32_t all[2] = { (uint32_t)-1, (uint32_t)-1 };
+            x265amd_mes* mes = NULL;
+            const int n = form_searches(*this, im, pu, all, pf, pf->jobs, &mes,
+                [this](const CUData& c, const MV& p, int r, MV& a, MV& b) { setSearchRange(c, p, r, a, b); });
+            pf->me = NULL;                     /* not usable before predInterSearch collects it */
+            if (n > 0 && g_mode == ME_HOST)
+            {
+                /* the CPU check of the early forming: the searches run here on the host, and the reference
+                 * loop must find every one it makes after the split recursion */
+                for (int i = 0; i < n; i++)
+                {
+                    Memo& e = pf->m[i];
+                    e.cost = x265ref_motionEstimate(&m_me, e.ref, e.mvmin, e.mvmax, e.qmvp, e.numc, e.mvc, e.merange,
+                                                    e.out);
+                }
+                pf->mes = NULL;
+                pf->mode = &im;
+                pf->pending = n;
+            }
+            else if (n > 0)
+            {
+                const int st = x265amd_mes_submit(mes, pu.width, pu.height, m_me.fencPUYuv.m_buf[0], FENC_STRIDE, n,
+                                                  pf->jobs);
+                if (st)
+                    fprintf(stderr, "[x265me] x265amd_mes_submit failed: %s\n", x265amd_strerror(st));
+                else
+                {
+                    pf->mes = mes;
+                    pf->mode = &im;
+                    pf->pending = n;
+                }
+            }
+        }
+    }
+    SplitData sd = x265ref_compressInterCU_rd0_4(this, parentCTU, cuGeom, qp);
+    if (cuGeom.depth == 0 && t_apf)
+    {
+        if (t_apf->pending)
+            (void)collect(t_apf);              /* the CU took a path without the 2Nx2N search */
+        t_apf->me = NULL;
+        t_apf->n = t_apf->nskip = 0;
+    }
+    return sd;
 }
 
 } // namespace X265_NS

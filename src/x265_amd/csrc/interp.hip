@@ -736,13 +736,13 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_hvpp_stream(const BatchGroup 
 #pragma unroll
                 for (int x = 0; x < SW; x++)
                 {
-                    int t = 0;
+                    int t = DOT ? 2048 : 0;        // 8 bit: the sp rounding offset as the accumulator's start
 #pragma unroll
                     for (int k = 0; k < 4; k++)
                         t = __builtin_amdgcn_sdot2(__builtin_bit_cast(s16x2, Pr[(i + 2 + 2 * k) & 7][x]), cv[k], t, false);
                     if constexpr (DOT)
                     {
-                        const int v = (t + 2048) >> 12;
+                        const int v = t >> 12;
                         o[x] = v < 0 ? 0 : (v > 255 ? 255 : v);
                     }
                     else
@@ -861,7 +861,15 @@ static int launch_interp(int cls, const BatchGroup& g, uint32_t blocks, hipStrea
                     else hipLaunchKernelGGL((k_hvpp_stream<P, 8, true>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, g);
                 }
             }
-            else hipLaunchKernelGGL((k_hvpp_stream<P, 4>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, g);
+            else
+            {
+                if constexpr (sizeof(P) == 1)
+                {
+                    if (pf) hipLaunchKernelGGL((k_hvpp_stream<P, 4, false, 1>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, g);
+                    else hipLaunchKernelGGL((k_hvpp_stream<P, 4>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, g);
+                }
+                else hipLaunchKernelGGL((k_hvpp_stream<P, 4>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, g);
+            }
             return (int)hipGetLastError();
         }
     size_t lds = 0;

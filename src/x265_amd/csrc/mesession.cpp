@@ -53,13 +53,22 @@ int record(int st)
 
 } // namespace
 
-struct x265amd_mes_thread
+struct x265amd_mes_stage
 {
-    hipStream_t st = nullptr;
-    hipEvent_t ev = nullptr;    // blocking-sync event: the waiting worker sleeps (X265AMD_MES_SYNC=spin: spin)
     uint8_t* dev = nullptr;
     uint8_t* host = nullptr;
     size_t cap = 0;
+};
+
+struct x265amd_mes_thread
+{
+    hipStream_t st = nullptr;
+    hipStream_t ast = nullptr;  // the outstanding x265amd_mes_submit's stream (never waited on by _search / _ref)
+    hipEvent_t ev = nullptr;    // blocking-sync event: the waiting worker sleeps (X265AMD_MES_SYNC=spin: spin)
+    hipEvent_t aev = nullptr;   // completion of the outstanding x265amd_mes_submit
+    x265amd_mes_stage sync, async;
+    int pending = 0;            // jobs of the outstanding submit (0: none)
+    size_t pend_out = 0;        // its output offset in the async staging
 };
 
 struct x265amd_mes
@@ -104,19 +113,20 @@ int wait(x265amd_mes_thread* t)
     return (int)hipStreamSynchronize(t->st);
 }
 
-int reserve(x265amd_mes_thread* t, size_t bytes)
+int reserve(x265amd_mes_thread* t, x265amd_mes_stage& g, size_t bytes)
 {
-    if (bytes <= t->cap) return 0;
+    if (bytes <= g.cap) return 0;
     bytes = (bytes + 65535) & ~(size_t)65535;
     if (t->st) (void)hipStreamSynchronize(t->st);
-    (void)hipFree(t->dev);
-    (void)hipHostFree(t->host);
-    t->dev = t->host = nullptr;
-    t->cap = 0;
-    if (hipMalloc((void**)&t->dev, bytes) != hipSuccess ||
-        hipHostMalloc((void**)&t->host, bytes, hipHostMallocDefault) != hipSuccess)
+    if (t->ast) (void)hipStreamSynchronize(t->ast);
+    (void)hipFree(g.dev);
+    (void)hipHostFree(g.host);
+    g.dev = g.host = nullptr;
+    g.cap = 0;
+    if (hipMalloc((void**)&g.dev, bytes) != hipSuccess ||
+        hipHostMalloc((void**)&g.host, bytes, hipHostMallocDefault) != hipSuccess)
         return X265AMD_ENOMEM;
-    t->cap = bytes;
+    g.cap = bytes;
     return 0;
 }
 
@@ -148,11 +158,14 @@ int thread_ctx(x265amd_mes* s, x265amd_mes_thread** out)
         }
         s->threads.push_back(t);
     }
-    if (hipStreamCreateWithFlags(&t->st, hipStreamNonBlocking) != hipSuccess || reserve(t, 1 << 16))
+    if (hipStreamCreateWithFlags(&t->st, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&t->ast, hipStreamNonBlocking) != hipSuccess || reserve(t, t->sync, 1 << 16) ||
+        reserve(t, t->async, 1 << 16))
         return X265AMD_ENOMEM;
     const char* sync = getenv("X265AMD_MES_SYNC");
-    if (!(sync && !strcmp(sync, "spin")) &&
-        hipEventCreateWithFlags(&t->ev, hipEventBlockingSync | hipEventDisableTiming) != hipSuccess)
+    const bool spin = sync && !strcmp(sync, "spin");
+    if ((!spin && hipEventCreateWithFlags(&t->ev, hipEventBlockingSync | hipEventDisableTiming) != hipSuccess) ||
+        hipEventCreateWithFlags(&t->aev, (spin ? 0 : hipEventBlockingSync) | hipEventDisableTiming) != hipSuccess)
         return X265AMD_ENOMEM;
     tls.push_back({ s, s->id, t });
     *out = t;
@@ -219,10 +232,16 @@ extern "C" void x265amd_mes_destroy(x265amd_mes* s)
     for (auto* t : s->threads)
     {
         if (t->st) (void)hipStreamSynchronize(t->st);
-        (void)hipFree(t->dev);
-        (void)hipHostFree(t->host);
+        for (x265amd_mes_stage* g : { &t->sync, &t->async })
+        {
+            (void)hipFree(g->dev);
+            (void)hipHostFree(g->host);
+        }
+        if (t->ast) (void)hipStreamSynchronize(t->ast);
         if (t->st) (void)hipStreamDestroy(t->st);
+        if (t->ast) (void)hipStreamDestroy(t->ast);
         if (t->ev) (void)hipEventDestroy(t->ev);
+        if (t->aev) (void)hipEventDestroy(t->aev);
         delete t;
     }
     for (auto& p : s->pics)
@@ -314,22 +333,23 @@ extern "C" int x265amd_mes_table(x265amd_mes* s, const uint16_t* centre, int* in
     return 0;
 }
 
-extern "C" int x265amd_mes_search(x265amd_mes* s, int w, int h, const void* fenc, intptr_t fenc_stride, int n,
-                                  x265amd_mes_job* jobs)
+namespace {
+
+// stage a batch of one PU's searches in g and enqueue upload, launch and download on the thread's
+// stream; *out = the outputs' offset in g.host
+int enqueue(x265amd_mes* s, x265amd_mes_thread* t, x265amd_mes_stage& g, hipStream_t st, int w, int h,
+            const void* fenc, intptr_t fenc_stride, int n, const x265amd_mes_job* jobs, size_t* out)
 {
     if (!s || n < 0 || (n && (!jobs || !fenc)) || w < 4 || h < 4 || w > 64 || h > 64 || fenc_stride < w)
-        return record(X265AMD_EINVAL);
-    if (!n) return 0;
+        return X265AMD_EINVAL;
     const int maxc = s->cfg.max_cand > 0 ? s->cfg.max_cand : 1;
     for (int i = 0; i < n; i++)
         if (jobs[i].slot < 0 || jobs[i].slot >= s->next_slot || jobs[i].table < 0 ||
             jobs[i].table >= s->cfg.max_tables || jobs[i].num_cand < 0 || jobs[i].num_cand > s->cfg.max_cand)
-            return record(X265AMD_EINVAL);
-    x265amd_mes_thread* t;
-    MES_TRY(thread_ctx(s, &t));
+            return X265AMD_EINVAL;
     const Layout L(n, h, (int)s->pix, maxc, fenc_stride);
-    MES_TRY(reserve(t, L.end));
-    uint8_t* H = t->host;
+    if (int rc = reserve(t, g, L.end)) return rc;
+    uint8_t* H = g.host;
     memcpy(H + L.fenc, fenc, (size_t)fenc_stride * h * s->pix);
     int64_t* foff = (int64_t*)(H + L.fenc_off);
     int64_t* roff = (int64_t*)(H + L.ref_off);
@@ -349,7 +369,7 @@ extern "C" int x265amd_mes_search(x265amd_mes* s, int w, int h, const void* fenc
         nc[i] = (uint8_t)j.num_cand;
         coff[i] = (int64_t)j.table * (int64_t)s->table_elems + s->cfg.mvcost_range;
     }
-    MES_TRY(hipMemcpyAsync(t->dev, H, L.out_mv, hipMemcpyHostToDevice, t->st));
+    if (hipError_t e = hipMemcpyAsync(g.dev, H, L.out_mv, hipMemcpyHostToDevice, st)) return (int)e;
     x265amd_me_batch b;
     memset(&b, 0, sizeof(b));
     b.w = w;
@@ -359,30 +379,80 @@ extern "C" int x265amd_mes_search(x265amd_mes* s, int w, int h, const void* fenc
     b.subme = s->cfg.subme;
     b.merange = s->cfg.merange;
     b.max_cand = maxc;
-    b.fenc = t->dev + L.fenc;
+    b.fenc = g.dev + L.fenc;
     b.fenc_stride = fenc_stride;
-    b.fenc_off = (const int64_t*)(t->dev + L.fenc_off);
+    b.fenc_off = (const int64_t*)(g.dev + L.fenc_off);
     b.ref = s->arena;
     b.ref_stride = s->cfg.stride;
-    b.ref_off = (const int64_t*)(t->dev + L.ref_off);
-    b.mv_range = (const int16_t*)(t->dev + L.range);
-    b.mvp = (const int16_t*)(t->dev + L.mvp);
-    b.mvc = (const int16_t*)(t->dev + L.mvc);
-    b.num_cand = t->dev + L.ncand;
+    b.ref_off = (const int64_t*)(g.dev + L.ref_off);
+    b.mv_range = (const int16_t*)(g.dev + L.range);
+    b.mvp = (const int16_t*)(g.dev + L.mvp);
+    b.mvc = (const int16_t*)(g.dev + L.mvc);
+    b.num_cand = g.dev + L.ncand;
     b.mvcost = s->tables;
-    b.mvcost_off = (const int64_t*)(t->dev + L.cost_off);
-    b.out_mv = (int16_t*)(t->dev + L.out_mv);
-    b.out_cost = (int32_t*)(t->dev + L.out_cost);
-    MES_TRY(x265amd_motion_search(s->cfg.depth, 1, &b, t->st));
-    MES_TRY(hipMemcpyAsync(H + L.out_mv, t->dev + L.out_mv, L.end - L.out_mv, hipMemcpyDeviceToHost, t->st));
-    MES_TRY(wait(t));
-    const int16_t* om = (const int16_t*)(H + L.out_mv);
-    const int32_t* oc = (const int32_t*)(H + L.out_cost);
+    b.mvcost_off = (const int64_t*)(g.dev + L.cost_off);
+    b.out_mv = (int16_t*)(g.dev + L.out_mv);
+    b.out_cost = (int32_t*)(g.dev + L.out_cost);
+    if (int rc = x265amd_motion_search(s->cfg.depth, 1, &b, st)) return rc;
+    if (hipError_t e = hipMemcpyAsync(H + L.out_mv, g.dev + L.out_mv, L.end - L.out_mv, hipMemcpyDeviceToHost, st))
+        return (int)e;
+    *out = L.out_mv;
+    return 0;
+}
+
+void unpack(const x265amd_mes_stage& g, size_t out, int n, x265amd_mes_job* jobs)
+{
+    const int16_t* om = (const int16_t*)(g.host + out);
+    const int32_t* oc = (const int32_t*)(g.host + out + (((size_t)4 * n + 255) & ~(size_t)255));
     for (int i = 0; i < n; i++)
     {
         jobs[i].out_mv[0] = om[2 * i];
         jobs[i].out_mv[1] = om[2 * i + 1];
         jobs[i].out_cost = oc[i];
     }
+}
+
+} // namespace
+
+extern "C" int x265amd_mes_search(x265amd_mes* s, int w, int h, const void* fenc, intptr_t fenc_stride, int n,
+                                  x265amd_mes_job* jobs)
+{
+    if (!s) return record(X265AMD_EINVAL);
+    if (!n) return 0;
+    x265amd_mes_thread* t;
+    MES_TRY(thread_ctx(s, &t));
+    size_t out = 0;
+    MES_TRY(enqueue(s, t, t->sync, t->st, w, h, fenc, fenc_stride, n, jobs, &out));
+    MES_TRY(wait(t));
+    unpack(t->sync, out, n, jobs);
+    return 0;
+}
+
+extern "C" int x265amd_mes_submit(x265amd_mes* s, int w, int h, const void* fenc, intptr_t fenc_stride, int n,
+                                  const x265amd_mes_job* jobs)
+{
+    if (!s || n <= 0) return record(X265AMD_EINVAL);
+    x265amd_mes_thread* t;
+    MES_TRY(thread_ctx(s, &t));
+    if (t->pending) return record(X265AMD_EINVAL);          // one outstanding submit per thread
+    size_t out = 0;
+    MES_TRY(enqueue(s, t, t->async, t->ast, w, h, fenc, fenc_stride, n, jobs, &out));
+    MES_TRY(hipEventRecord(t->aev, t->ast));
+    t->pending = n;
+    t->pend_out = out;
+    return 0;
+}
+
+extern "C" int x265amd_mes_collect(x265amd_mes* s, int n, x265amd_mes_job* jobs)
+{
+    if (!s || n < 0 || (n && !jobs)) return record(X265AMD_EINVAL);
+    x265amd_mes_thread* t;
+    MES_TRY(thread_ctx(s, &t));
+    if (!t->pending) return record(X265AMD_EINVAL);
+    const int pend = t->pending;
+    t->pending = 0;
+    MES_TRY(hipEventSynchronize(t->aev));
+    if (n != pend) return record(X265AMD_EINVAL);
+    unpack(t->async, t->pend_out, n, jobs);
     return 0;
 }

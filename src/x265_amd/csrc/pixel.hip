@@ -540,10 +540,24 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_sad_multi(const BatchGroup g)
 // kernel class of a batch: (op, unit width, unit height) packed in an int
 static inline int cmp_pack(int op, int uw, int uh) { return (op << 16) | (uw << 8) | uh; }
 
+// 8x8 SAD units (one lane per 8x8 block: twice the rows in flight per lane, each job's descriptors
+// loaded by one lane) instead of 8x4 ones; X265AMD_SAD_UH8=0 selects the 8x4 units
+static bool sad_uh8()
+{
+    static int v = -1;
+    if (v < 0)
+    {
+        const char* e = getenv("X265AMD_SAD_UH8");
+        v = e ? atoi(e) != 0 : 1;
+    }
+    return v != 0;
+}
+
 static int cmp_class(int op, int w, int h)
 {
     if ((w % 4) || (h % 4) || w > 64 || h > 64 || w < 4 || h < 4) return -X265AMD_EINVAL;
     const int uwd = (w % 8) ? 4 : 8;
+    if (op == X265AMD_SAD && w % 8 == 0 && h % 8 == 0 && sad_uh8()) return cmp_pack(op, 8, 8);
     switch (op)
     {
     case X265AMD_SAD: case X265AMD_SATD: case X265AMD_SSE_PP: case X265AMD_SSE_SS:
@@ -581,7 +595,7 @@ static int launch_cmp_class(int cls, const BatchGroup& g, uint32_t blocks, hipSt
     using S = int16_t;
 #define X265AMD_CMP(OPX, PX, W, H) \
     if (cls == cmp_pack(OPX, W, H)) return launch_cmp<OPX, PX, W, H>(g, blocks, st);
-    X265AMD_CMP(X265AMD_SAD, P, 8, 4)     X265AMD_CMP(X265AMD_SAD, P, 4, 4)
+    X265AMD_CMP(X265AMD_SAD, P, 8, 8)     X265AMD_CMP(X265AMD_SAD, P, 8, 4)     X265AMD_CMP(X265AMD_SAD, P, 4, 4)
     X265AMD_CMP(X265AMD_SATD, P, 8, 4)    X265AMD_CMP(X265AMD_SATD, P, 4, 4)
     X265AMD_CMP(X265AMD_SA8D, P, 16, 16)  X265AMD_CMP(X265AMD_SA8D, P, 8, 8)
     X265AMD_CMP(X265AMD_SSE_PP, P, 8, 4)  X265AMD_CMP(X265AMD_SSE_PP, P, 4, 4)
@@ -633,6 +647,7 @@ static int dispatch_cmp(int op, int count, const x265amd_cmp_batch* bt, hipStrea
 static int sad_multi_class(int, int w, int h)
 {
     if ((w % 4) || (h % 4) || w > 64 || h > 64 || w < 4 || h < 4) return -X265AMD_EINVAL;
+    if (w % 8 == 0 && h % 8 == 0 && sad_uh8()) return cmp_pack(X265AMD_SAD, 8, 8);
     return cmp_pack(X265AMD_SAD, (w % 8) ? 4 : 8, 4);
 }
 
@@ -644,7 +659,9 @@ static int dispatch_multi(int count, const x265amd_cmp_batch* bt, hipStream_t st
     return launch_grouped(count, cls.data(), BatchGroup{},
         [&](int i, SubBatch& s) { cmp_fill(bt[i], cls[i], s); },
         [&](int c, const BatchGroup& g, uint32_t blocks) {
-            if (((c >> 8) & 0xff) == 8)
+            if (((c >> 8) & 0xff) == 8 && (c & 0xff) == 8)
+                hipLaunchKernelGGL((k_sad_multi<P, NREF, 8, 8>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, g);
+            else if (((c >> 8) & 0xff) == 8)
                 hipLaunchKernelGGL((k_sad_multi<P, NREF, 8, 4>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, g);
             else
                 hipLaunchKernelGGL((k_sad_multi<P, NREF, 4, 4>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, g);

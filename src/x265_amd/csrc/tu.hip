@@ -628,6 +628,197 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_tu32_mfma(const TuArgs a)
     }
 }
 
+// ---------------------------------------------------------------- 32x32 on the integer matrix cores
+// k_tu32_mfma's chain with every transform stage as the int8 byte-split products of k_tr32_i8
+// (transform.hip): exact int32 sums, one v_lshl_add per element to recombine, a third of the
+// VALU work of the f16 split.  X265AMD_TU_I8=0 selects the f16 kernel.
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x16 __attribute__((ext_vector_type(16)));
+__device__ __forceinline__ void split_bytes(const uint32_t (&d)[8], i32x4& lo, i32x4& hi)
+{
+#pragma unroll
+    for (int q = 0; q < 4; q++)
+    {
+        lo[q] = (int)(__builtin_amdgcn_perm(d[2 * q + 1], d[2 * q], 0x06040200u) ^ 0x80808080u);
+        hi[q] = (int)__builtin_amdgcn_perm(d[2 * q + 1], d[2 * q], 0x07050301u);
+    }
+}
+struct ColSumsTu { int v[32]; };
+constexpr ColSumsTu make_colsums_tu()
+{
+    ColSumsTu c{};
+    for (int j = 0; j < 32; j++)
+        for (int k = 0; k < 32; k++) c.v[j] += 128 * kT32.m[k][j];
+    return c;
+}
+static __constant__ ColSumsTu c_colsum128_tu = make_colsums_tu();
+
+template <typename P>
+__global__ __launch_bounds__(X265AMD_BLOCK) void k_tu32_i8(const TuArgs a)
+{
+    __shared__ int16_t lds_c[kTuWaves][32 * 32];   // DCT coefficients; later the inverse output
+    __shared__ int16_t lds_q[kTuWaves][32 * 32];   // quantized coefficients
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63, r = l & 31, h = l >> 5;
+    int16_t* Cs = lds_c[w];
+    int16_t* Q = lds_q[w];
+    const int depth = a.depth, maxv = (1 << depth) - 1;
+    const int fsh1 = 4 + depth - 8, fsh2 = 11, ish2 = 12 - (depth - 8);
+    const int tshift = 15 - depth - 5;
+    const int io_row = l >> 1, io_col = 16 * (l & 1);
+
+    // constant int8 operands (as k_tr32_i8 in transform.hip): stage 1 in the lane half's natural k
+    // order (k = 16h + j), stage 2 in the accumulator's row order (k = (j&3) + 8(j>>2) + 4h)
+    i32x4 fc1, fc2, ic1, ic2;
+#pragma unroll
+    for (int q = 0; q < 4; q++)
+    {
+        uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
+#pragma unroll
+        for (int e = 0; e < 4; e++)
+        {
+            const int jj = 4 * q + e, kn = 16 * h + jj, kp = (jj & 3) + 8 * (jj >> 2) + 4 * h;
+            w0 |= (uint32_t)(uint8_t)(int8_t)c_t32.m[r][kn] << (8 * e);
+            w1 |= (uint32_t)(uint8_t)(int8_t)c_t32.m[r][kp] << (8 * e);
+            w2 |= (uint32_t)(uint8_t)(int8_t)c_t32.m[kn][r] << (8 * e);
+            w3 |= (uint32_t)(uint8_t)(int8_t)c_t32.m[kp][r] << (8 * e);
+        }
+        fc1[q] = (int)w0; fc2[q] = (int)w1; ic1[q] = (int)w2; ic2[q] = (int)w3;
+    }
+    // lo-byte bias corrections (k_tr32_i8): forward stage 1 on the lane's column (row sum of T: zero
+    // unless r == 0), forward stage 2 on output row 0 (register 0 of lane half 0), inverse stages on
+    // the lane's column (128 x the column sum of T at r)
+    const int fk1 = (r == 0 ? 128 * 64 * 32 : 0) + (1 << (fsh1 - 1));
+    const int fk2 = (1 << (fsh2 - 1)), fk20 = h == 0 ? 128 * 64 * 32 : 0;
+    const int icol = c_colsum128_tu.v[r];
+
+    const int64_t step = (int64_t)gridDim.x * kTuWaves;
+    for (int64_t j = (int64_t)blockIdx.x * kTuWaves + w; j < a.n; j += step)
+    {
+        const P* pf = (const P*)a.fenc + a.fenc_off[j];
+        const P* pp = (const P*)a.pred + a.pred_off[j];
+        const int qp = a.qp[j], rem = qp % 6, per = qp / 6;
+        // the reconstruction's row segments, loaded with the residual's (one global round trip per TU)
+        PixRow<P, 16> fio, pio;
+        fio.load(pf + io_row * a.fenc_stride + io_col);
+        pio.load(pp + io_row * a.pred_stride + io_col);
+
+        // ---- forward stage 1: A = residual row r, columns 16h + 0..15
+        uint32_t x[8];
+        {
+            int f[16], p[16];
+            load_row<P, 16>(pf + r * a.fenc_stride + 16 * h, f);
+            load_row<P, 16>(pp + r * a.pred_stride + 16 * h, p);
+#pragma unroll
+            for (int q = 0; q < 8; q++) x[q] = pack16(f[2 * q] - p[2 * q], f[2 * q + 1] - p[2 * q + 1]);
+        }
+        i32x4 xl, xh;
+        split_bytes(x, xl, xh);
+        i32x16 lo = __builtin_amdgcn_mfma_i32_32x32x32_i8(xl, fc1, (i32x16){}, 0, 0, 0);
+        i32x16 hi = __builtin_amdgcn_mfma_i32_32x32x32_i8(xh, fc1, (i32x16){}, 0, 0, 0);
+        int v[16];
+#pragma unroll
+        for (int i = 0; i < 16; i++) v[i] = (int)(((uint32_t)hi[i] << 8) + (uint32_t)lo[i]) + fk1 >> fsh1;
+        // ---- forward stage 2 from registers: Dst = T * U' (coefficients in the accumulator layout the
+        //      quant / sign hiding below expect); the int16 wrap of stage 1 is the byte split
+#pragma unroll
+        for (int q = 0; q < 8; q++) x[q] = pack16(v[2 * q], v[2 * q + 1]);
+        split_bytes(x, xl, xh);
+        lo = __builtin_amdgcn_mfma_i32_32x32x32_i8(fc2, xl, (i32x16){}, 0, 0, 0);
+        hi = __builtin_amdgcn_mfma_i32_32x32x32_i8(fc2, xh, (i32x16){}, 0, 0, 0);
+
+        // ---- quant in registers: coefficient (row (i&3) + 8(i>>2) + 4h, column r)
+        const int qscale = quant_scale(rem);
+        const int qbits = 14 + per + tshift;
+        const int qadd = (a.i_slice ? 171 : 85) << (qbits - 9);
+        int cnt = 0;
+#pragma unroll
+        for (int i = 0; i < 16; i++)
+        {
+            const int c = (int)(int16_t)(((int)(((uint32_t)hi[i] << 8) + (uint32_t)lo[i]) + fk2 + (i == 0 ? fk20 : 0)) >> fsh2);
+            const int tmp = (c < 0 ? -c : c) * qscale;
+            int lvl = (tmp + qadd) >> qbits;
+            cnt += lvl != 0;
+            lvl = c < 0 ? -lvl : lvl;
+            const int pos = ((i & 3) + 8 * (i >> 2) + 4 * h) * 32 + r;
+            Cs[pos] = (int16_t)c;
+            Q[pos] = (int16_t)clip16(lvl);
+        }
+        int num_sig = group_sum<64>(cnt);
+        wave_sync();
+        if (a.sign_hide && num_sig >= 2)
+        {
+            num_sig += sign_hide<32, 64>(Q, Cs, c_scan.s32, 0, l, qscale, qadd, qbits);
+            wave_sync();
+        }
+
+        // ---- coefficients out (16-element row segments)
+        int16_t* pc = a.coeff + a.coeff_off[j] + io_row * 32 + io_col;
+        stu<uint4>(pc, ldu<uint4>(&Q[io_row * 32 + io_col]));
+        stu<uint4>(pc + 8, ldu<uint4>(&Q[io_row * 32 + io_col + 8]));
+        if (l == 0) a.num_sig[j] = (uint32_t)num_sig;
+
+        // ---- reconstruction
+        int f[16], p[16], res[16];
+#pragma unroll
+        for (int k = 0; k < 16; k++) { f[k] = fio.get(k); p[k] = pio.get(k); }
+        if (num_sig == 0)
+        {
+#pragma unroll
+            for (int k = 0; k < 16; k++) res[k] = f[k] - p[k];
+        }
+        else
+        {
+            const int scale = inv_quant_scale(rem) << per;
+            const int dsh = 20 - 14 - tshift, dadd = 1 << (dsh - 1);
+            const int q0 = Q[0];
+            if (num_sig == 1 && q0 != 0)
+            {
+                const int dq0 = clip16((q0 * scale + dadd) >> dsh);
+                const int sh2 = 12 - (depth - 8) - 3;
+                const int dc = (int16_t)((((dq0 + 1) >> 1) * 8 + (1 << (sh2 - 1))) >> sh2);
+#pragma unroll
+                for (int k = 0; k < 16; k++) res[k] = dc;
+            }
+            else
+            {
+                // inverse stage 1: A = dequantized coefficient column r (rows 16h + 0..15)
+#pragma unroll
+                for (int q = 0; q < 8; q++)
+                    x[q] = pack16(clip16((Q[(16 * h + 2 * q) * 32 + r] * scale + dadd) >> dsh),
+                                  clip16((Q[(16 * h + 2 * q + 1) * 32 + r] * scale + dadd) >> dsh));
+                split_bytes(x, xl, xh);
+                lo = __builtin_amdgcn_mfma_i32_32x32x32_i8(xl, ic1, (i32x16){}, 0, 0, 0);
+                hi = __builtin_amdgcn_mfma_i32_32x32x32_i8(xh, ic1, (i32x16){}, 0, 0, 0);
+#pragma unroll
+                for (int i = 0; i < 16; i++)
+                    v[i] = clip16(((int)(((uint32_t)hi[i] << 8) + (uint32_t)lo[i]) + icol + 64) >> 7);
+#pragma unroll
+                for (int q = 0; q < 8; q++) x[q] = pack16(v[2 * q], v[2 * q + 1]);
+                split_bytes(x, xl, xh);
+                lo = __builtin_amdgcn_mfma_i32_32x32x32_i8(xl, ic2, (i32x16){}, 0, 0, 0);
+                hi = __builtin_amdgcn_mfma_i32_32x32x32_i8(xh, ic2, (i32x16){}, 0, 0, 0);
+                // residual (row (i&3) + 8(i>>2) + 4h, column r) -> LDS -> row segments
+#pragma unroll
+                for (int i = 0; i < 16; i++)
+                    Cs[((i & 3) + 8 * (i >> 2) + 4 * h) * 32 + r] =
+                        (int16_t)clip16(((int)(((uint32_t)hi[i] << 8) + (uint32_t)lo[i]) + icol + (1 << (ish2 - 1))) >> ish2);
+                wave_sync();
+                load_row16<16>(&Cs[io_row * 32 + io_col], res);
+            }
+        }
+        int rec[16];
+#pragma unroll
+        for (int k = 0; k < 16; k++)
+        {
+            const int t = num_sig ? p[k] + res[k] : p[k];
+            rec[k] = t < 0 ? 0 : (t > maxv ? maxv : t);
+        }
+        store_row<P, 16>((P*)a.recon + a.recon_off[j] + io_row * a.recon_stride + io_col, rec);
+        if (a.resi) store_n<int16_t, 16>(a.resi + a.resi_off[j] + io_row * a.resi_stride + io_col, res);
+        wave_sync();                                 // LDS reuse by the next TU of this wave
+    }
+}
+
 // ---------------------------------------------------------------- 4x4: one lane per TU
 // The whole chain in registers (no LDS, no cross-lane traffic): 4x4 TUs are
 // the most frequent residual blocks and too small to share between lanes.
@@ -790,6 +981,19 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_tu4(const TuArgs a)
     }
 }
 
+// the integer-MFMA 32x32 TU kernel, default (X265AMD_TU_I8=0 selects the f16 split form; measured,
+// profiles/r04/tu32_i8_ab.txt: tu_pipeline 32x32 0.20 -> 0.26 of the HBM peak)
+static bool tu_i8()
+{
+    static int v = -1;
+    if (v < 0)
+    {
+        const char* e = getenv("X265AMD_TU_I8");
+        v = e ? atoi(e) != 0 : 1;
+    }
+    return v != 0;
+}
+
 template <typename P>
 static int launch_tu(int log2, const TuArgs& a, hipStream_t st)
 {
@@ -807,7 +1011,10 @@ static int launch_tu(int log2, const TuArgs& a, hipStream_t st)
     {
         // one wavefront per TU, enough waves to fill the chip, each looping over TUs
         const int64_t want = ((int64_t)a.n + kTuWaves - 1) / kTuWaves;
-        hipLaunchKernelGGL((k_tu32_mfma<P>), dim3((uint32_t)(want < 4096 ? want : 4096)), dim3(X265AMD_BLOCK), 0, st, a);
+        if (tu_i8())
+            hipLaunchKernelGGL((k_tu32_i8<P>), dim3((uint32_t)(want < 4096 ? want : 4096)), dim3(X265AMD_BLOCK), 0, st, a);
+        else
+            hipLaunchKernelGGL((k_tu32_mfma<P>), dim3((uint32_t)(want < 4096 ? want : 4096)), dim3(X265AMD_BLOCK), 0, st, a);
         break;
     }
     default: return X265AMD_EINVAL;

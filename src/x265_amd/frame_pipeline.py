@@ -162,7 +162,7 @@ def check_reference_reach(slices_by_fb, fs: FrameSet, plan: BandPlan, ctu: int =
 class GpuFramePipeline:
     def __init__(self, prims, width, height, depth, frames_local, world, rank, census=None, band_rows=None,
                  segment_frames=None, streams=8, device="cuda", seed=11, early_independent=True, exchange="torch",
-                 inplace_store=True, job_wait="band", background=False):
+                 inplace_store=True, job_wait="band", background=False, recon="tu"):
         """exchange: "torch" (torch.distributed P2P batches; local copies on the stream) or "rccl" (the
         native communicator, x265amd_exchange; with inplace_store=False a rank's own reference pictures
         are finished in their own buffers and reach its store as loop-back transfers — the one-GPU check
@@ -172,7 +172,12 @@ class GpuFramePipeline:
         only for the band of the ONE reference picture it reads (the data it actually depends on).
         background (one rank, whole sequence in one graph): the jobs that read no reference run on
         background streams from the start, in step order, and a step's loop filters wait only for the
-        background work of THAT step's pictures — instead of all reference-free work joining step 0"""
+        background work of THAT step's pictures — instead of all reference-free work joining step 0.
+        recon: "tu" — every band's reconstruction is coded by the fused TU pipeline (f3,
+        x265amd_tu_pipeline: residual -> DCT -> quant -> dequant -> iDCT -> prediction + residual) from
+        a motion-compensated prediction out of the picture's first reference as the reference store
+        holds it (the producer's final, filtered band), so each picture's reconstruction depends on its
+        references' published bands; "source" — the source pixels stand in for it (rounds 1-3)."""
         import torch
 
         self.early_independent = early_independent
@@ -241,6 +246,11 @@ class GpuFramePipeline:
         else:
             raise ValueError(f"exchange {exchange!r}")
         self._f4_setup(width, height, device)
+        self.recon = recon
+        if recon == "tu":
+            self.tu = self.tu_setup(lambda k, p: self._store_pred(k, p), self.work)
+        elif recon != "source":
+            raise ValueError(f"recon {recon!r}")
         self.streams = [torch.cuda.Stream() for _ in range(max(1, streams))] if streams > 1 else []
         self.bg_streams = []
         self._bgroups, self._bg_events, self.bg = {}, {}, False
@@ -253,6 +263,79 @@ class GpuFramePipeline:
         if final is None and self.inplace_store and j in self.sof:
             return self.frame_planes(self.src_planes, self.sof[j])
         return self.frame_planes(self.final if final is None else final, k)
+
+    # ---------------------------------------------------------------- f3 reconstruction
+    TU_QP = 30
+
+    def mv_of(self, k):
+        """integer luma displacement of local picture k's prediction from its first reference: the
+        synthetic source pans (+2, +1) pixels per picture (synth.py), so a block at (x, y) of POC p was at
+        (x + 2 d, y + d) in POC p - d"""
+        j = self.local[k]
+        refs = self.sched.refs[j]
+        if not refs:
+            return None
+        d = self.sched.poc[j] - self.sched.poc[refs[0]]
+        return 2 * d, d
+
+    def _store_pred(self, k, p):
+        """(base tensor, element offset of the picture) of local picture k's prediction source for plane p:
+        its first reference as this rank's reference store holds it, or the flat plane (I picture)"""
+        refs = self.sched.refs[self.local[k]]
+        if not refs:
+            return self._flat[p], 0
+        return self.src_planes[p], self.sof[refs[0]] * self._sizes[p]
+
+    def tu_setup(self, pred_of, recon_planes):
+        """TU descriptors of every (local picture, band): 8x8 luma and 4x4 chroma TUs tiling the band,
+        fenc = the picture's source, pred = pred_of(k, plane) displaced by mv_of(k) (a flat mid-grey plane
+        for an I picture), recon = the picture's slot of recon_planes; one TuBatch per (picture, band,
+        plane), each with its own coefficient scratch"""
+        import torch
+
+        from .native import TuBatch
+
+        fs, dev = self.fs, self.fs.luma.device
+        if not hasattr(self, "_flat"):
+            mid = 1 << (self.depth - 1)
+            self._flat = [torch.full((self._sizes[p],), mid, dtype=fs.luma.dtype, device=dev) for p in range(3)]
+        geo = [(fs.stride, fs.mx, fs.my, self.W, self.H, 3), (fs.cstride, fs.cmx, fs.cmy, self.W // 2, self.H // 2, 2),
+               (fs.cstride, fs.cmx, fs.cmy, self.W // 2, self.H // 2, 2)]
+        keep, out = [], {}
+        nb = self.plan.nbands
+        i64 = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.int64)).to(dev)
+        for k in range(self.F):
+            j = self.local[k]
+            intra = not self.sched.refs[j]
+            mv = self.mv_of(k) or (0, 0)
+            for b in range(nb):
+                y0, y1 = self._rows_px(b)
+                arr = (TuBatch * 3)()
+                for p, (stride, mx, my, w, h, lg) in enumerate(geo):
+                    n_ = 1 << lg
+                    ys = np.arange((y0 >> (p > 0)), (y1 >> (p > 0)), n_)
+                    xs = np.arange(0, w, n_)
+                    yy, xx = np.meshgrid(ys, xs, indexing="ij")
+                    yy, xx = yy.reshape(-1), xx.reshape(-1)
+                    org = (my + yy) * stride + mx + xx
+                    dx, dy = (mv[0], mv[1]) if p == 0 else (mv[0] // 2, mv[1] // 2)
+                    pbase, poff = pred_of(k, p)
+                    fo = i64(k * self._sizes[p] + org)
+                    po = i64(poff + org + dy * stride + dx)
+                    ro = i64(k * self._sizes[p] + org)
+                    m = len(org)
+                    co = i64(np.arange(m) * n_ * n_)
+                    coef = torch.empty(m * n_ * n_, dtype=torch.int16, device=dev)
+                    sig = torch.empty(m, dtype=torch.int32, device=dev)
+                    qp = torch.full((m,), self.TU_QP, dtype=torch.uint8, device=dev)
+                    keep += [fo, po, ro, co, coef, sig, qp]
+                    arr[p] = TuBatch(lg, m, int(p == 0), int(intra), int(intra), 1, self.src_planes[p].data_ptr(), stride,
+                                     fo.data_ptr(), pbase.data_ptr(), stride, po.data_ptr(), None, 0, None,
+                                     coef.data_ptr(), co.data_ptr(), recon_planes[p].data_ptr(), stride, ro.data_ptr(),
+                                     sig.data_ptr(), qp.data_ptr(), None)
+                out[(k, b)] = arr
+        self._tu_keep = getattr(self, "_tu_keep", []) + keep
+        return out
 
     # ---------------------------------------------------------------- f4 descriptors
     def _f4_setup(self, width, height, device, work=None, final=None):
@@ -493,12 +576,20 @@ class GpuFramePipeline:
         s, plan = self.sched, self.plan
         items = s.items(self.rank, st)
         cur = torch.cuda.current_stream()
-        if st == 0:
+        if self.recon == "source" and st == 0:
             # the reconstruction of every band (stand-in: the source pixels), written before any band is
             # deblocked: one copy per plane for all local frames
             for p in range(3):
                 n = self.F * self._sizes[p]
                 self.work[p][:n].copy_(self.src_planes[p][:n])
+        if self.recon == "tu" and items:
+            # the step's bands coded: prediction from the reference store (final bands published in
+            # earlier steps), residual through the fused TU pipeline, reconstruction into `work`
+            from .native import TuBatch
+
+            arrs = [self.tu[(self.kof[j], b)] for j, b in items]
+            grp = (TuBatch * (3 * len(arrs)))(*[x for a in arrs for x in a])
+            self.prims.tu_pipeline_grouped(self.depth, grp, ctypes.c_void_p(cur.cuda_stream))
         h = ctypes.c_void_p(cur.cuda_stream)
         if items:
             rows = []

@@ -3,7 +3,7 @@ PUs on the MI355X (integration/gpu_me.cpp over the x265amd_mes_* session entries
 
 oracle/Makefile links the reference CLI + encoder (x265la8 / x265la10) with
 Search::predInterSearch (search.cpp:2050) and MotionEstimate::motionEstimate (motion.cpp:571)
-hooked: the hook forms every search the reference loop is about to make for a PU of >= 32x32,
+hooked: the hook forms every search the reference loop is about to make for a 64x64 PU (X265AMD_ME_MIN),
 runs them in one device launch, and hands each result to the reference's own predInterSearch
 when it makes that exact call.  Every mode decision, RDO cost and bitstream bit downstream
 depends on those searches, so the encode must be BIT-IDENTICAL to the plain reference encoder.
@@ -38,7 +38,7 @@ def test_me_hook_host_prefetch_equals_reference_on_cpu(tmp_path, size, frames, f
     rc, got, _, err = encode(_bin("x265la8"), src, w, h, frames, tmp_path / "me.hevc",
                              {"X265AMD_LOOKAHEAD": "cpu", "X265AMD_ME": "host", "X265AMD_ME_STATS": "1"})
     assert rc == 0, err[-2000:]
-    assert "[x265me] motion searches of PUs >= 1024 pixels on the CPU (hook prefetch)" in err
+    assert "[x265me] motion searches of PUs >= 4096 pixels on the CPU (hook prefetch)" in err
     st = _stats(err)
     assert st["prefetches"] > 0 and st["hits"] > 0
     # every search the reference made after a prefetch was one of the prefetched ones, except those on
@@ -71,7 +71,7 @@ def _gpu_encode_equals_reference(tmp_path, w, h, n, extra_env=None, depth=8):
     env = {"X265AMD_ME_STATS": "1", **(extra_env or {})}
     rc, got, fps, err = encode(exe, src, w, h, n, tmp_path / "me.hevc", env, pools=16, depth=depth)
     assert rc == 0, err[-3000:]
-    assert "[x265me] motion searches of PUs >= 1024 pixels on the MI355X" in err
+    assert "[x265me] motion searches of PUs >= 4096 pixels on the MI355X" in err
     st = _stats(err)
     print(f"\n[x265me] {w}x{h} {n} frames: reference {ref_fps} fps, MI355X lookahead + ME {fps} fps; {st}")
     assert st["prefetches"] > 0 and st["hits"] > 0 and st["misses"] == 0, st

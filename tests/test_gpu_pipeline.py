@@ -3,9 +3,12 @@
 The pictures of a --preset medium GOP (pipeline.Schedule: I, P, B-ref and b pictures with their
 L0 / L1 references) are encoded step by step (census primitive work per band + the f4 row-band
 loop filters) and every final band of a reference picture is copied into the reference store.
-Checked: every picture's final reconstruction equals the whole-frame deblock -> SAO -> border
-chain (x265amd_deblock / _sao_apply / _extend_border, themselves bit-exact vs the reference's
-Deblock / SAO classes in test_f4.py) on the same picture; every store slot holds its producer's
+Every band's reconstruction is coded by the fused TU pipeline (f3) from a motion-compensated
+prediction out of the picture's first reference as the rank's reference store holds it, so a
+picture's reconstruction depends on the bands its references published.  Checked: every picture's
+final reconstruction equals a whole-frame chain run picture by picture in encode order (TU coding
+from the chain's own final references -> x265amd_deblock / _sao_apply / _extend_border, themselves
+bit-exact vs the reference's Deblock / SAO classes in test_f4.py); every store slot holds its producer's
 final reconstruction, margins included; and every census batch still matches the oracle on
 sampled jobs read against the FINAL stores — the stores start out holding the unfiltered source,
 so a job that read a reference before its rows were published would not match.
@@ -68,16 +71,37 @@ def test_gpu_pipeline_gop_equals_whole_frame_chain(gpu_prims, oracle_libs, band_
     pipe.step()
     torch.cuda.synchronize()
     fs, F = pipe.fs, pipe.F
-    # whole-frame f4 chain on a copy of each picture's source (the pipeline's stand-in reconstruction)
-    work = [t[:F * (t.numel() // fs.stored)].clone() for t in (fs.luma, fs.cb, fs.cr)]
-    final = [torch.zeros_like(t) for t in work]
+    # the whole-frame chain in encode order, independent of the pipeline's bands, steps and stores: each
+    # picture coded by the fused TU pipeline from its first reference's CHAIN-final planes (a flat plane
+    # for an I picture), then deblock -> SAO -> border extension of the whole picture
+    work = [torch.zeros_like(t) for t in pipe.work]
+    final = [torch.zeros_like(t) for t in pipe.work]
     saved = (pipe.dbk, pipe.sao, pipe.bor)
     pipe._f4_setup(W, H, "cuda", work=work, final=final)
-    gpu_prims.deblock(8, pipe.dbk)
-    gpu_prims.sao_apply(8, pipe.sao)
-    gpu_prims.extend_border(8, [bp for bps in pipe.bor for bp in bps])
+
+    def chain_pred(k, p):
+        refs = pipe.sched.refs[pipe.local[k]]
+        if not refs:
+            return pipe._flat[p], 0
+        return final[p], pipe.kof[refs[0]] * pipe._sizes[p]
+
+    tu = pipe.tu_setup(chain_pred, work)
+    from src.x265_amd.native import TuBatch
+    for k in sorted(range(F), key=lambda k: pipe.local[k]):          # encode order
+        arrs = [tu[(k, b)] for b in range(pipe.plan.nbands)]
+        gpu_prims.tu_pipeline_grouped(8, (TuBatch * (3 * len(arrs)))(*[x for a in arrs for x in a]))
+        gpu_prims.deblock(8, [pipe.dbk[k]])
+        gpu_prims.sao_apply(8, [pipe.sao[k]])
+        gpu_prims.extend_border(8, pipe.bor[k])
     torch.cuda.synchronize()
     pipe.dbk, pipe.sao, pipe.bor = saved
+    # the reconstruction is a real coding of the source (not a copy of it): P / B pictures differ from
+    # their source but stay close to it
+    k0 = next(k for k in range(F) if pipe.sched.refs[pipe.local[k]])
+    src_k = pipe.frame_planes([fs.luma, fs.cb, fs.cr], k0)[0].view(-1, fs.stride)[fs.my:fs.my + H, fs.mx:fs.mx + W].float()
+    rec_k = pipe.frame_planes(final, k0)[0].view(-1, fs.stride)[fs.my:fs.my + H, fs.mx:fs.mx + W].float()
+    err = (src_k - rec_k).abs()
+    assert err.max() > 0 and err.mean() < 8, f"reconstruction error {err.mean():.2f}"
     # the area the chain defines: the picture and its margins (rows below the CTU-aligned plane's bottom
     # margin and columns right of the right margin are never written or read)
     geo = [(fs.stride, 2 * fs.my + H, 2 * fs.mx + W)] + [(fs.cstride, 2 * fs.cmy + H // 2, 2 * fs.cmx + W // 2)] * 2
