@@ -541,23 +541,24 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_sad_multi(const BatchGroup g)
 static inline int cmp_pack(int op, int uw, int uh) { return (op << 16) | (uw << 8) | uh; }
 
 // 8x8 SAD units (one lane per 8x8 block: twice the rows in flight per lane, each job's descriptors
-// loaded by one lane) instead of 8x4 ones; X265AMD_SAD_UH8=0 selects the 8x4 units
-static bool sad_uh8()
+// loaded by one lane) instead of 8x4 ones: SAD 64x64 0.66 -> 0.79 of the HBM peak, 8x8 / 16x16 level
+// (profiles/r04/sad_uh8_ab_and_me_async.txt); X265AMD_SAD_UH8=0 selects the 8x4 units, =2 also for sad_x3/x4
+static int sad_uh8()
 {
     static int v = -1;
     if (v < 0)
     {
         const char* e = getenv("X265AMD_SAD_UH8");
-        v = e ? atoi(e) != 0 : 1;
+        v = e ? atoi(e) : 1;
     }
-    return v != 0;
+    return v;
 }
 
 static int cmp_class(int op, int w, int h)
 {
     if ((w % 4) || (h % 4) || w > 64 || h > 64 || w < 4 || h < 4) return -X265AMD_EINVAL;
     const int uwd = (w % 8) ? 4 : 8;
-    if (op == X265AMD_SAD && w % 8 == 0 && h % 8 == 0 && sad_uh8()) return cmp_pack(op, 8, 8);
+    if (op == X265AMD_SAD && w % 8 == 0 && h % 8 == 0 && sad_uh8() > 0) return cmp_pack(op, 8, 8);
     switch (op)
     {
     case X265AMD_SAD: case X265AMD_SATD: case X265AMD_SSE_PP: case X265AMD_SSE_SS:
@@ -647,7 +648,8 @@ static int dispatch_cmp(int op, int count, const x265amd_cmp_batch* bt, hipStrea
 static int sad_multi_class(int, int w, int h)
 {
     if ((w % 4) || (h % 4) || w > 64 || h > 64 || w < 4 || h < 4) return -X265AMD_EINVAL;
-    if (w % 8 == 0 && h % 8 == 0 && sad_uh8()) return cmp_pack(X265AMD_SAD, 8, 8);
+    // (8x8 units measured no faster for sad_x4 8x8 and slower for 16x16: profiles/r04/sad_uh8_ab_and_me_async.txt)
+    if (w % 8 == 0 && h % 8 == 0 && sad_uh8() > 1) return cmp_pack(X265AMD_SAD, 8, 8);
     return cmp_pack(X265AMD_SAD, (w % 8) ? 4 : 8, 4);
 }
 

@@ -26,3 +26,5 @@ SyntheticSource(3840, 2160, 64, 8).write_yuv('/tmp/s2160.yuv')" || exit 1
 X265AMD_ME_STATS=1 timeout -k 10 200 oracle/_ref/x265la8s --input /tmp/s2160.yuv --input-res 3840x2160 --fps 30 --frames 64 \
     --preset medium --pools 16 --no-info -o /tmp/o.hevc > gpurun_out/r04f_cu_stats_la8s_me_async.txt 2>&1 || exit 1
 grep -E "encoded|CU:|x265me\] stats" gpurun_out/r04f_cu_stats_la8s_me_async.txt
+timeout -k 10 1000 python3 -u bench.py > gpurun_out/r04f_bench.json 2> gpurun_out/r04f_bench.err || { tail -30 gpurun_out/r04f_bench.err; exit 1; }
+head -c 600 gpurun_out/r04f_bench.json
