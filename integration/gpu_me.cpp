@@ -80,7 +80,10 @@ struct CostPeek : public MotionEstimate
 
 enum { ME_GPU = 0, ME_CPU = 1, ME_HOST = 2, ME_CHECK = 3 };
 int g_mode = ME_GPU;
-bool g_async = true;           /* X265AMD_ME_ASYNC=0: no CTU-start submit, every search synchronous */
+/* X265AMD_ME_ASYNC=1: the 64x64 searches of every reference submitted at the CTU's start and collected at
+ * predInterSearch; measured neutral at 64x64-only (2160p, 3 interleaved runs: 8.29 / 8.39 / 8.54 fps against
+ * 8.60 / 8.27 / 8.44 synchronous, profiles/r04/encoder_me_async_ab.txt), so the synchronous form is the default */
+bool g_async = false;
 int g_min_area = 64 * 64;      /* measured: 64x64 only beats 32x32 + 64x64 (profiles/r04/encoder_me_variants.txt) */
 bool g_stats_on = false;
 pthread_once_t g_once = PTHREAD_ONCE_INIT;

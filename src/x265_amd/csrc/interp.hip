@@ -639,8 +639,8 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_hvpp(const BatchGroup g)
 // or one body ahead, while the current body is computed from registers — PF = 2 — so a lane has
 // 8 row loads in flight instead of one (rows past the block clamp to its last row; their
 // results are never used).
-template <typename P, int SW, bool STG = false, int PF = 0>
-__global__ __launch_bounds__(X265AMD_BLOCK) void k_hvpp_stream(const BatchGroup g)
+template <typename P, int SW, bool STG = false, int PF = 0, int WPE = 1>
+__global__ __launch_bounds__(X265AMD_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void k_hvpp_stream(const BatchGroup g)
 {
     const uint32_t gb = xcd_block();
     const SubBatch& sub = group_sub(g, gb);
@@ -700,10 +700,21 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_hvpp_stream(const BatchGroup 
         }
     };
     uint32_t Pr[8][SW];                  // ring of vertical pairs: Pr[r & 7][x] = (I[r][x], I[r + 1][x])
-    int Iprev[SW];
-    Win wa[PF ? 8 : 1], wn[PF == 2 ? 8 : 1];
-    if constexpr (PF) load_body(1, wa);
-    inter(ps, Iprev);
+    Win wa[PF == 3 ? 4 : PF ? 8 : 1], wn[PF == 2 ? 8 : 1];
+    if constexpr (PF == 3)
+    {
+        // rolling window: row r lives in wa[(r - 1) & 3], loaded four rows ahead of its use
+#pragma unroll
+        for (int i = 0; i < 4; i++) wa[i].load((const uint8_t*)(ps + (intptr_t)(1 + i < R ? 1 + i : R - 1) * ss));
+    }
+    else if constexpr (PF) load_body(1, wa);
+    {
+        // row 0's intermediate as the high half of ring slot 7 (the pair before row 1's)
+        int I0[SW];
+        inter(ps, I0);
+#pragma unroll
+        for (int x = 0; x < SW; x++) Pr[7][x] = (uint32_t)I0[x] << 16;
+    }
     for (int r0 = 1; r0 < R; r0 += 8)
     {
         if constexpr (PF == 1)
@@ -720,15 +731,17 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_hvpp_stream(const BatchGroup 
             const int r = r0 + i;                        // row whose intermediate is formed now
             if (r >= R) break;
             int I[SW];
-            if constexpr (PF) wa[i].sums(cp, I);
-            else inter(ps + (intptr_t)r * ss, I);
-            // P[r - 1] goes to ring slot (r - 1) & 7 = i (r0 = 1 mod 8): compile-time
-#pragma unroll
-            for (int x = 0; x < SW; x++)
+            if constexpr (PF == 3)
             {
-                Pr[i][x] = __builtin_amdgcn_perm((uint32_t)I[x], (uint32_t)Iprev[x], 0x05040100u);
-                Iprev[x] = I[x];
+                wa[i & 3].sums(cp, I);
+                if (r + 4 < R) wa[i & 3].load((const uint8_t*)(ps + (intptr_t)(r + 4) * ss));
             }
+            else if constexpr (PF) wa[i].sums(cp, I);
+            else inter(ps + (intptr_t)r * ss, I);
+            // P[r - 1] goes to ring slot (r - 1) & 7 = i (r0 = 1 mod 8): compile-time; I[r - 1] is the
+            // high half of the previous slot
+#pragma unroll
+            for (int x = 0; x < SW; x++) Pr[i][x] = __builtin_amdgcn_perm((uint32_t)I[x], Pr[(i + 7) & 7][x], 0x05040302u);
             const int y = r - 7;                         // output row ready once P[y + 6] exists
             if (y >= 0)
             {
@@ -761,7 +774,7 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_hvpp_stream(const BatchGroup 
     if constexpr (STG) stage_writeback<STG_WAVE>((const uint8_t*)stg_lds + (threadIdx.x >> 6) * STG_WAVE, pd, lg, w * h, wjob0, n);
 }
 
-// row-prefetch variant of the 8-bit streaming hv_pp (X265AMD_HVPP_PF = 0 / 1 / 2; default below)
+// row-prefetch variant of the 8-bit streaming hv_pp (X265AMD_HVPP_PF = 0 / 1 / 2 / 3; default below)
 static int hvpp_pf()
 {
     static int v = -1;
@@ -769,7 +782,7 @@ static int hvpp_pf()
     {
         const char* e = getenv("X265AMD_HVPP_PF");
         v = e ? atoi(e) : 1;
-        if (v < 0 || v > 2) v = 1;
+        if (v < 0 || v > 3) v = 1;
     }
     return v;
 }
@@ -835,6 +848,36 @@ constexpr int kHvppStream = 8 * 32 + 31, kHvppStream4 = 4 * 32 + 31;
 // class flag: outputs staged through LDS (k_interp STG)
 constexpr int kStaged = 2048;
 
+// 8-bit 8-wide strips: row-prefetch variant x occupancy target (X265AMD_HVPP_WPE = 4: the compiler held to
+// 128 VGPRs, four waves per SIMD instead of three)
+static int hvpp_wpe()
+{
+    static int v = -1;
+    if (v < 0)
+    {
+        const char* e = getenv("X265AMD_HVPP_WPE");
+        v = e ? atoi(e) : 1;
+    }
+    return v;
+}
+
+template <typename P, bool STG>
+static void launch_hvpp8(int pf, const BatchGroup& g, uint32_t blocks, hipStream_t st)
+{
+#define HV(PFV, W) hipLaunchKernelGGL((k_hvpp_stream<P, 8, STG, PFV, W>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, g)
+    if (hvpp_wpe() >= 4)
+    {
+        if (pf == 1) HV(1, 4);
+        else if (pf == 3) HV(3, 4);
+        else HV(0, 4);
+    }
+    else if (pf == 1) HV(1, 1);
+    else if (pf == 2) HV(2, 1);
+    else if (pf == 3) HV(3, 1);
+    else HV(0, 1);
+#undef HV
+}
+
 template <typename P, typename S, typename D, int OP, int TAPS>
 static int launch_interp(int cls, const BatchGroup& g, uint32_t blocks, hipStream_t st)
 {
@@ -844,22 +887,12 @@ static int launch_interp(int cls, const BatchGroup& g, uint32_t blocks, hipStrea
             const int pf = sizeof(P) == 1 ? hvpp_pf() : 0;
             if (cls == kHvppStream)
             {
-                if constexpr (sizeof(P) == 1)
-                {
-                    if (pf == 1) hipLaunchKernelGGL((k_hvpp_stream<P, 8, false, 1>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, g);
-                    else if (pf == 2) hipLaunchKernelGGL((k_hvpp_stream<P, 8, false, 2>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, g);
-                    else hipLaunchKernelGGL((k_hvpp_stream<P, 8>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, g);
-                }
+                if constexpr (sizeof(P) == 1) launch_hvpp8<P, false>(pf, g, blocks, st);
                 else hipLaunchKernelGGL((k_hvpp_stream<P, 8>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, g);
             }
             else if (cls == (kHvppStream | kStaged))
             {
-                if constexpr (sizeof(P) == 1)
-                {
-                    if (pf == 1) hipLaunchKernelGGL((k_hvpp_stream<P, 8, true, 1>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, g);
-                    else if (pf == 2) hipLaunchKernelGGL((k_hvpp_stream<P, 8, true, 2>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, g);
-                    else hipLaunchKernelGGL((k_hvpp_stream<P, 8, true>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, g);
-                }
+                if constexpr (sizeof(P) == 1) launch_hvpp8<P, true>(pf, g, blocks, st);
             }
             else
             {

@@ -4,6 +4,21 @@
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
+# hvpp: ring without the separate previous-row registers (all variants), rolling 4-ahead prefetch (PF=3),
+# compiler held to four waves per SIMD (WPE=4); parity under each, then an interleaved A/B
+for v in "1 4" "3 1" "3 4"; do
+  set -- $v
+  X265AMD_HVPP_PF=$1 X265AMD_HVPP_WPE=$2 timeout -k 10 300 python3 -u -m pytest tests/test_gpu_parity.py -x -q --timeout 250 --timeout-method thread \
+    -k "golden or interp_compact or oracle_random" > gpurun_out/r04g_parity_pf$1_wpe$2.log 2>&1 || { tail -30 gpurun_out/r04g_parity_pf$1_wpe$2.log; exit 1; }
+  echo "parity pf=$1 wpe=$2: $(tail -1 gpurun_out/r04g_parity_pf$1_wpe$2.log)"
+done
+for rep in 1 2; do
+  for v in "1 1" "1 4" "3 1" "3 4"; do
+    set -- $v
+    echo "== hvpp pf=$1 wpe=$2 rep=$rep"
+    X265AMD_HVPP_PF=$1 X265AMD_HVPP_WPE=$2 timeout -k 10 200 python3 -u tools/kernel_roofline.py --only luma_hvpp 2>/dev/null | grep "{" | cut -c1-150 || exit 1
+  done
+done
 for g in "4 4" "2 8" "4 8"; do
   set -- $g
   echo "== intra G16=$1 G32=$2"
