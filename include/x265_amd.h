@@ -554,6 +554,17 @@ typedef struct
 } x265amd_la_bjob;
 int x265amd_la_pcost_n(x265amd_la* la, int n, x265amd_la_pjob* jobs, int rows_per_slice, int num_slices);
 int x265amd_la_bcost_n(x265amd_la* la, int n, x265amd_la_bjob* jobs, int rows_per_slice, int num_slices);
+/* cuTree's propagation of one (p0, p1, b) (Lookahead::estimateCUPropagate, slicetype.cpp:1741-1842)
+ * through x265amd_cutree_propagate, on HOST arrays of the session's CU grid: propagate_in =
+ * frames[b]->propagateCost (NULL for a non-referenced b), intra_cost / inv_qscale / lowres_costs =
+ * frames[b]->intraCost / invQscaleFactor / lowresCosts[b-p0][p1-b], mvs0 / mvs1 =
+ * frames[b]->lowresMvs[0][b-p0-1] / [1][p1-b-1] (mvs1 NULL when b == p1), fps_factor and
+ * bipred_weight[2] as the reference computes them; ref_costs0 / ref_costs1 = frames[p0 / p1]->
+ * propagateCost, updated in place (ref_costs1 ignored without mvs1).  Synchronous. */
+int x265amd_la_propagate(x265amd_la* la, const uint16_t* propagate_in, const int32_t* intra_cost,
+                         const uint16_t* lowres_costs, const int32_t* inv_qscale, const int32_t* mvs0,
+                         const int32_t* mvs1, double fps_factor, const int* bipred_weight, uint16_t* ref_costs0,
+                         uint16_t* ref_costs1);
 
 /* ------------------------------------------------------------------ (e)
  * Frame-parallel schedule, host only: the GOP model of --preset medium

@@ -36,6 +36,7 @@
 #include "primitives.h"
 #include "lowres.h"
 #include "slicetype.h"
+#include "ratecontrol.h"    /* CLIP_DURATION */
 
 #include <cstdio>
 #include <cstdlib>
@@ -53,6 +54,8 @@ extern "C" void x265ref_finishBatch(CostEstimateGroup* self);
 extern "C" void x265ref_lowresIntraEstimate(LookaheadTLD* self, Lowres* fenc);
 extern "C" int64_t x265ref_estimateFrameCost(CostEstimateGroup* self, LookaheadTLD* tld, int p0, int p1, int b,
                                              bool bIntraPenalty);
+extern "C" void x265ref_estimateCUPropagate(Lookahead* self, Lowres** frames, double averageDuration, int p0, int p1,
+                                            int b, int referenced);
 
 namespace {
 
@@ -149,11 +152,12 @@ void report(const char* what, int st)
 }
 
 int g_mismatches = 0;
+int g_prop_mismatches = 0;
 
 /* X265AMD_LA_STATS=1: calls and wall time per kind, printed at exit */
-enum { ST_INTRA, ST_P, ST_B, ST_BATCH_P, ST_BATCH_B, ST_HOST, ST_P_WEIGHTED, ST_HOST_WEIGHTED, ST_N };
+enum { ST_INTRA, ST_P, ST_B, ST_BATCH_P, ST_BATCH_B, ST_HOST, ST_P_WEIGHTED, ST_HOST_WEIGHTED, ST_PROPAGATE, ST_N };
 const char* const st_name[ST_N] = { "intra", "P single", "B single", "P batched", "B batched", "host loops",
-                                    "P weighted", "B weighted" };
+                                    "P weighted", "B weighted", "propagate" };
 struct Stat { long calls, jobs; double sec; };
 Stat g_stat[ST_N];
 bool g_stats_on = false;
@@ -189,6 +193,7 @@ int ncu_of(const Lowres& f) { return (int)(f.maxBlocksInRow * f.maxBlocksInCol);
 void print_check_summary()
 {
     fprintf(stderr, "[x265la] check: %d mismatching estimates\n", g_mismatches);
+    fprintf(stderr, "[x265la] check: %d mismatching propagations\n", g_prop_mismatches);
 }
 
 /* X265AMD_LOOKAHEAD=check: scratch outputs of one device estimate and their comparison with the
@@ -275,6 +280,75 @@ struct CheckBufs
 } // namespace
 
 namespace X265_NS {
+
+/* cuTree's propagation step (slicetype.cpp:1741-1842) on the device: the reference's set-up (bipred
+ * weights, list distances, the fps factor, the zeroed first row of a non-referenced frame's
+ * propagateCost) restated, the per-CU loop one x265amd_la_propagate call.  With VBV the reference's
+ * cuTreeFinish follows the loop, so that configuration runs the reference's function. */
+void Lookahead::estimateCUPropagate(Lowres** frames, double averageDuration, int p0, int p1, int b, int referenced)
+{
+    pthread_once(&g_mode_once, read_mode);
+    if (g_mode == MODE_CPU || g_mode == MODE_HOST || (m_param->rc.vbvBufferSize && m_param->lookaheadDepth && referenced))
+    {
+        x265ref_estimateCUPropagate(this, frames, averageDuration, p0, p1, b, referenced);
+        return;
+    }
+    x265amd_la* la = session(*frames[b]);
+    if (!la)
+    {
+        x265ref_estimateCUPropagate(this, frames, averageDuration, p0, p1, b, referenced);
+        return;
+    }
+    const int32_t distScaleFactor = (((b - p0) << 8) + ((p1 - p0) >> 1)) / (p1 - p0);
+    const int32_t bipredWeight = m_param->bEnableWeightedBiPred ? 64 - (distScaleFactor >> 2) : 32;
+    const int bipredWeights[2] = { bipredWeight, 64 - bipredWeight };
+    memset(m_scratch, 0, m_8x8Width * sizeof(int));
+    const double fpsFactor = CLIP_DURATION((double)m_param->fpsDenom / m_param->fpsNum) / CLIP_DURATION(averageDuration);
+    if (!referenced)
+        memset(frames[b]->propagateCost, 0, m_8x8Width * sizeof(uint16_t));
+    Lowres* f = frames[b];
+    const int ncu = ncu_of(*f);
+    /* list 1 exists only for a B estimate (b < p1); a P estimate's lowres costs never mark it used */
+    const int32_t* mvs0 = (const int32_t*)f->lowresMvs[0][b - p0 - 1];
+    const int32_t* mvs1 = b < p1 ? (const int32_t*)f->lowresMvs[1][p1 - b - 1] : NULL;
+    uint16_t* rc0 = frames[p0]->propagateCost;
+    uint16_t* rc1 = b < p1 ? frames[p1]->propagateCost : NULL;
+    uint16_t* chk0 = NULL;
+    uint16_t* chk1 = NULL;
+    if (g_mode == MODE_CHECK)
+    {
+        /* the device writes into copies; the reference's own loop then updates the real arrays */
+        chk0 = (uint16_t*)malloc(2 * ncu);
+        memcpy(chk0, rc0, 2 * ncu);
+        rc0 = chk0;
+        if (rc1)
+        {
+            chk1 = (uint16_t*)malloc(2 * ncu);
+            memcpy(chk1, rc1, 2 * ncu);
+            rc1 = chk1;
+        }
+    }
+    const double t0 = now_s();
+    const int st = x265amd_la_propagate(la, referenced ? f->propagateCost : NULL, f->intraCost,
+                                        f->lowresCosts[b - p0][p1 - b], f->invQscaleFactor, mvs0, mvs1, fpsFactor,
+                                        bipredWeights, rc0, rc1);
+    report("x265amd_la_propagate", st);
+    stat_add(ST_PROPAGATE, 1, t0);
+    if (g_mode == MODE_CHECK)
+    {
+        x265ref_estimateCUPropagate(this, frames, averageDuration, p0, p1, b, referenced);
+        if (!st && (memcmp(chk0, frames[p0]->propagateCost, 2 * ncu) ||
+                    (chk1 && memcmp(chk1, frames[p1]->propagateCost, 2 * ncu))))
+        {
+            int n = __sync_add_and_fetch(&g_prop_mismatches, 1);
+            if (n <= 20)
+                fprintf(stderr, "[x265la] CHECK MISMATCH propagation (p0 %d, p1 %d, b %d, referenced %d)\n", p0, p1, b,
+                        referenced);
+        }
+        free(chk0);
+        free(chk1);
+    }
+}
 
 void LookaheadTLD::lowresIntraEstimate(Lowres& fenc)
 {

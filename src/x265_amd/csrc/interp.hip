@@ -141,7 +141,24 @@ template <int NB>
 __device__ __forceinline__ void load_win_dw(const uint8_t* p, uint32_t (&W)[(NB + 3) / 4])
 {
     constexpr int ND = (NB + 3) / 4;
-    if constexpr (NB > 8)
+#ifndef X265AMD_WIN_ALIGNED
+#define X265AMD_WIN_ALIGNED 0
+#endif
+    if constexpr (X265AMD_WIN_ALIGNED && NB >= 13 && NB <= 16)
+    {
+        // dword-aligned loads: the four dwords from p rounded down (each holds a window byte, as
+        // NB >= 13) and the fifth only when the window reaches into it (otherwise dword 3 again), then
+        // a per-lane byte shift
+        const uintptr_t a = (uintptr_t)p;
+        const int sh = (int)(a & 3);
+        const uint32_t* q = (const uint32_t*)(a - sh);
+        const uint4 d = *(const uint4*)q;
+        const uint32_t e = q[(sh + NB - 1) >> 2];
+        const uint32_t D[5] = { d.x, d.y, d.z, d.w, e };
+#pragma unroll
+        for (int k = 0; k < ND; k++) W[k] = __builtin_amdgcn_alignbyte(D[k + 1], D[k], sh);
+    }
+    else if constexpr (NB > 8)
     {
         static_assert(NB <= 16, "window too large");
         const uint2 h = ldu<uint2>(p), t = ldu<uint2>(p + NB - 8);

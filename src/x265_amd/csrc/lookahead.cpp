@@ -529,3 +529,60 @@ extern "C" int x265amd_la_bcost(x265amd_la* la, const void* fenc, const void* re
     }
     return st;
 }
+
+// Lookahead::estimateCUPropagate (slicetype.cpp:1741-1842) of the running encoder: the CU arrays
+// from the caller's Lowres staged in one upload, x265amd_cutree_propagate, the two reference
+// propagateCost arrays back (list 1 only when it is used).  cuTree runs on the lookahead's decision
+// thread, one propagation after another (each reads what the previous one accumulated), so the
+// call is synchronous like the estimates.
+extern "C" int x265amd_la_propagate(x265amd_la* la, const uint16_t* propagate_in, const int32_t* intra_cost,
+                                    const uint16_t* lowres_costs, const int32_t* inv_qscale, const int32_t* mvs0,
+                                    const int32_t* mvs1, double fps_factor, const int* bipred_weight,
+                                    uint16_t* ref_costs0, uint16_t* ref_costs1)
+{
+    if (!la || !intra_cost || !lowres_costs || !inv_qscale || !mvs0 || !bipred_weight || !ref_costs0 ||
+        (mvs1 && !ref_costs1))
+        return record(X265AMD_EINVAL);
+    x265amd_la_thread* t;
+    LA_TRY(thread_ctx(la, &t));
+    const size_t ncu = (size_t)la->ncu;
+    // staging: inputs first (one upload), then the two reference arrays (in / out), then device-only scratch
+    size_t o = 0;
+    auto take = [&](size_t b) { size_t r = o; o = (o + b + 255) & ~(size_t)255; return r; };
+    const size_t o_pin = take(2 * ncu), o_ic = take(4 * ncu), o_lc = take(2 * ncu), o_iq = take(4 * ncu),
+                 o_m0 = take(4 * ncu), o_m1 = take(4 * ncu), o_r0 = take(2 * ncu), o_r1 = take(2 * ncu),
+                 o_sc = take(16 * ncu), end = o;
+    LA_TRY(reserve(t, end));
+    uint8_t* H = t->host;
+    if (propagate_in) memcpy(H + o_pin, propagate_in, 2 * ncu);
+    memcpy(H + o_ic, intra_cost, 4 * ncu);
+    memcpy(H + o_lc, lowres_costs, 2 * ncu);
+    memcpy(H + o_iq, inv_qscale, 4 * ncu);
+    memcpy(H + o_m0, mvs0, 4 * ncu);
+    if (mvs1) memcpy(H + o_m1, mvs1, 4 * ncu);
+    memcpy(H + o_r0, ref_costs0, 2 * ncu);
+    if (mvs1) memcpy(H + o_r1, ref_costs1, 2 * ncu);
+    LA_TRY(hipMemcpyAsync(t->dev, H, o_sc, hipMemcpyHostToDevice, t->st));
+    x265amd_propagate_batch b;
+    memset(&b, 0, sizeof(b));
+    b.width_cu = la->cfg.width_cu;
+    b.height_cu = la->cfg.height_cu;
+    b.propagate_in = propagate_in ? (const uint16_t*)(t->dev + o_pin) : nullptr;
+    b.intra_cost = (const int32_t*)(t->dev + o_ic);
+    b.lowres_costs = (const uint16_t*)(t->dev + o_lc);
+    b.inv_qscale = (const int32_t*)(t->dev + o_iq);
+    b.mvs[0] = (const int32_t*)(t->dev + o_m0);
+    b.mvs[1] = mvs1 ? (const int32_t*)(t->dev + o_m1) : nullptr;
+    b.fps_factor = fps_factor;
+    b.bipred_weight[0] = bipred_weight[0];
+    b.bipred_weight[1] = bipred_weight[1];
+    b.ref_costs[0] = (uint16_t*)(t->dev + o_r0);
+    b.ref_costs[1] = mvs1 ? (uint16_t*)(t->dev + o_r1) : nullptr;
+    b.scratch = (int64_t*)(t->dev + o_sc);
+    LA_TRY(x265amd_cutree_propagate(1, &b, t->st));
+    LA_TRY(hipMemcpyAsync(H + o_r0, t->dev + o_r0, o_sc - o_r0, hipMemcpyDeviceToHost, t->st));
+    LA_TRY(wait(t));
+    memcpy(ref_costs0, H + o_r0, 2 * ncu);
+    if (mvs1) memcpy(ref_costs1, H + o_r1, 2 * ncu);
+    return 0;
+}

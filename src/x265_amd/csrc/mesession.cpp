@@ -14,6 +14,11 @@
 //   * per host thread: a non-blocking stream, pinned staging and device scratch for one batch
 //     (the PU's source block and the job descriptors), found by (session address, session id).
 // x265amd_mes_search is synchronous on the calling thread: outputs are in the jobs on return.
+// Coalescing (X265AMD_MES_COALESCE, default on): the searches of all threads that call while a launch
+// is in flight are queued; whichever waiting thread finds the device idle launches every queued
+// request of one PU size as ONE batch on its stream and hands each caller its outputs — one launch
+// and two copies per batch of PUs instead of per PU, and no queueing of 16 workers' small launches
+// behind each other on the process's few hardware queues.
 // Failures are returned AND recorded in the backend's sticky status (x265amd_provider_status).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -21,6 +26,7 @@
 #include <string.h>
 
 #include <atomic>
+#include <condition_variable>
 #include <mutex>
 #include <new>
 #include <unordered_map>
@@ -95,6 +101,22 @@ struct x265amd_mes
     std::unordered_map<const void*, int> tabs;
     std::vector<x265amd_mes_thread*> threads;
     std::atomic<int> next_slot{ 0 };
+
+    // coalesced x265amd_mes_search requests (one per calling thread at a time)
+    struct Request
+    {
+        int w, h;
+        const void* fenc;
+        intptr_t fenc_stride;
+        int n;
+        x265amd_mes_job* jobs;
+        int rc;
+        bool done;
+    };
+    std::mutex cmu;
+    std::condition_variable ccv;
+    std::vector<Request*> queue;
+    bool busy = false;
 };
 
 namespace {
@@ -335,23 +357,55 @@ extern "C" int x265amd_mes_table(x265amd_mes* s, const uint16_t* centre, int* in
 
 namespace {
 
-// stage a batch of one PU's searches in g and enqueue upload, launch and download on the thread's
-// stream; *out = the outputs' offset in g.host
-int enqueue(x265amd_mes* s, x265amd_mes_thread* t, x265amd_mes_stage& g, hipStream_t st, int w, int h,
-            const void* fenc, intptr_t fenc_stride, int n, const x265amd_mes_job* jobs, size_t* out)
+int check_request(const x265amd_mes* s, int w, int h, const void* fenc, intptr_t fenc_stride, int n,
+                  const x265amd_mes_job* jobs)
 {
     if (!s || n < 0 || (n && (!jobs || !fenc)) || w < 4 || h < 4 || w > 64 || h > 64 || fenc_stride < w)
         return X265AMD_EINVAL;
-    const int maxc = s->cfg.max_cand > 0 ? s->cfg.max_cand : 1;
     for (int i = 0; i < n; i++)
         if (jobs[i].slot < 0 || jobs[i].slot >= s->next_slot || jobs[i].table < 0 ||
             jobs[i].table >= s->cfg.max_tables || jobs[i].num_cand < 0 || jobs[i].num_cand > s->cfg.max_cand)
             return X265AMD_EINVAL;
-    const Layout L(n, h, (int)s->pix, maxc, fenc_stride);
+    return 0;
+}
+
+// one PU's share of a batch: its source block and its searches
+struct Part
+{
+    const void* fenc;
+    intptr_t fenc_stride;
+    int n;
+    const x265amd_mes_job* jobs;
+};
+
+// stage the searches of `np` PUs of one size (checked by check_request) in g — the source blocks
+// packed at stride w, one after another — and enqueue upload, launch and download on `st`; *out = the
+// outputs' offset in g.host (job order = part order)
+int enqueue_parts(x265amd_mes* s, x265amd_mes_thread* t, x265amd_mes_stage& g, hipStream_t st, int w, int h,
+                  const Part* parts, int np, size_t* out)
+{
+    const int maxc = s->cfg.max_cand > 0 ? s->cfg.max_cand : 1;
+    int n = 0;
+    for (int k = 0; k < np; k++) n += parts[k].n;
+    const size_t blk = (size_t)w * h;                         // elements per packed source block
+    const Layout L(n, np * h, (int)s->pix, maxc, w);
     if (int rc = reserve(t, g, L.end)) return rc;
     uint8_t* H = g.host;
-    memcpy(H + L.fenc, fenc, (size_t)fenc_stride * h * s->pix);
     int64_t* foff = (int64_t*)(H + L.fenc_off);
+    for (int k = 0, i = 0; k < np; k++)
+    {
+        for (int y = 0; y < h; y++)
+            memcpy(H + L.fenc + (k * blk + (size_t)y * w) * s->pix,
+                   (const uint8_t*)parts[k].fenc + (size_t)y * parts[k].fenc_stride * s->pix, (size_t)w * s->pix);
+        for (int q = 0; q < parts[k].n; q++) foff[i++] = (int64_t)(k * blk);
+    }
+    const x265amd_mes_job* jobs = nullptr;
+    int part = -1, left = 0;
+    auto next_job = [&](int) -> const x265amd_mes_job& {
+        while (left == 0) { part++; jobs = parts[part].jobs; left = parts[part].n; }
+        left--;
+        return *jobs++;
+    };
     int64_t* roff = (int64_t*)(H + L.ref_off);
     int16_t* rng = (int16_t*)(H + L.range);
     int16_t* mvp = (int16_t*)(H + L.mvp);
@@ -360,8 +414,7 @@ int enqueue(x265amd_mes* s, x265amd_mes_thread* t, x265amd_mes_stage& g, hipStre
     int64_t* coff = (int64_t*)(H + L.cost_off);
     for (int i = 0; i < n; i++)
     {
-        const x265amd_mes_job& j = jobs[i];
-        foff[i] = 0;
+        const x265amd_mes_job& j = next_job(i);
         roff[i] = (int64_t)j.slot * s->cfg.plane_elems + s->cfg.org_offset + j.block_off;
         memcpy(rng + 4 * i, j.mv_range, 8);
         memcpy(mvp + 2 * i, j.mvp, 4);
@@ -380,7 +433,7 @@ int enqueue(x265amd_mes* s, x265amd_mes_thread* t, x265amd_mes_stage& g, hipStre
     b.merange = s->cfg.merange;
     b.max_cand = maxc;
     b.fenc = g.dev + L.fenc;
-    b.fenc_stride = fenc_stride;
+    b.fenc_stride = w;
     b.fenc_off = (const int64_t*)(g.dev + L.fenc_off);
     b.ref = s->arena;
     b.ref_stride = s->cfg.stride;
@@ -412,6 +465,74 @@ void unpack(const x265amd_mes_stage& g, size_t out, int n, x265amd_mes_job* jobs
     }
 }
 
+int enqueue(x265amd_mes* s, x265amd_mes_thread* t, x265amd_mes_stage& g, hipStream_t st, int w, int h,
+            const void* fenc, intptr_t fenc_stride, int n, const x265amd_mes_job* jobs, size_t* out)
+{
+    if (int rc = check_request(s, w, h, fenc, fenc_stride, n, jobs)) return rc;
+    const Part p = { fenc, fenc_stride, n, jobs };
+    return enqueue_parts(s, t, g, st, w, h, &p, 1, out);
+}
+
+bool coalescing()
+{
+    static int v = -1;
+    if (v < 0)
+    {
+        const char* e = getenv("X265AMD_MES_COALESCE");
+        v = e ? atoi(e) != 0 : 1;
+    }
+    return v != 0;
+}
+
+// lead one coalesced batch: every queued request of the first request's PU size (s->cmu held on entry
+// and on return, released while the device works)
+void lead_batch(x265amd_mes* s, x265amd_mes_thread* t, std::unique_lock<std::mutex>& lk)
+{
+    std::vector<x265amd_mes::Request*> batch;
+    const int w = s->queue[0]->w, h = s->queue[0]->h;
+    size_t keep = 0;
+    for (size_t i = 0; i < s->queue.size(); i++)
+    {
+        x265amd_mes::Request* r = s->queue[i];
+        if (r->w == w && r->h == h) batch.push_back(r);
+        else s->queue[keep++] = r;
+    }
+    s->queue.resize(keep);
+    s->busy = true;
+    lk.unlock();
+    std::vector<Part> parts(batch.size());
+    int n = 0;
+    for (size_t k = 0; k < batch.size(); k++)
+    {
+        parts[k] = { batch[k]->fenc, batch[k]->fenc_stride, batch[k]->n, batch[k]->jobs };
+        n += batch[k]->n;
+    }
+    size_t out = 0;
+    int rc = enqueue_parts(s, t, t->sync, t->st, w, h, parts.data(), (int)parts.size(), &out);
+    if (!rc) rc = wait(t);
+    if (!rc)
+    {
+        // outputs in part order
+        const int16_t* om = (const int16_t*)(t->sync.host + out);
+        const int32_t* oc = (const int32_t*)(t->sync.host + out + (((size_t)4 * n + 255) & ~(size_t)255));
+        for (size_t k = 0, i = 0; k < batch.size(); k++)
+            for (int q = 0; q < batch[k]->n; q++, i++)
+            {
+                batch[k]->jobs[q].out_mv[0] = om[2 * i];
+                batch[k]->jobs[q].out_mv[1] = om[2 * i + 1];
+                batch[k]->jobs[q].out_cost = oc[i];
+            }
+    }
+    lk.lock();
+    for (auto* r : batch)
+    {
+        r->rc = rc;
+        r->done = true;
+    }
+    s->busy = false;
+    s->ccv.notify_all();
+}
+
 } // namespace
 
 extern "C" int x265amd_mes_search(x265amd_mes* s, int w, int h, const void* fenc, intptr_t fenc_stride, int n,
@@ -421,6 +542,19 @@ extern "C" int x265amd_mes_search(x265amd_mes* s, int w, int h, const void* fenc
     if (!n) return 0;
     x265amd_mes_thread* t;
     MES_TRY(thread_ctx(s, &t));
+    if (coalescing())
+    {
+        MES_TRY(check_request(s, w, h, fenc, fenc_stride, n, jobs));
+        x265amd_mes::Request r = { w, h, fenc, fenc_stride, n, jobs, 0, false };
+        std::unique_lock<std::mutex> lk(s->cmu);
+        s->queue.push_back(&r);
+        while (!r.done)
+        {
+            if (!s->busy) lead_batch(s, t, lk);
+            else s->ccv.wait(lk);
+        }
+        return record(r.rc);
+    }
     size_t out = 0;
     MES_TRY(enqueue(s, t, t->sync, t->st, w, h, fenc, fenc_stride, n, jobs, &out));
     MES_TRY(wait(t));

@@ -28,3 +28,23 @@ python3 -c "
 import json; d=json.load(open('$d/pmc_kernels.json'))
 for k,v in d.items():
     if 'x265amd' in k: print(k[:60], {a: round(b,3) for a,b in v.items() if 'frac' in a or a in ('waves_resident','fetch_bytes','write_bytes','SQ_INSTS_VALU','SQ_INSTS_LDS','SQ_INSTS_SALU','SQ_INSTS_VMEM_RD','SQ_INSTS_VMEM_WR','SQ_WAVES','SQ_LDS_BANK_CONFLICT','SQ_WAIT_INST_LDS')})"
+# where a device motion search's wall time goes inside the encoder: kernel and copy durations
+python3 -c "
+from src.x265_amd.synth import SyntheticSource
+SyntheticSource(3840, 2160, 16, 8).write_yuv('/tmp/s2160.yuv')" || exit 1
+X265AMD_ME_STATS=1 timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --stats -d gpurun_out/r04h_encprof -o enc -- \
+    oracle/_ref/x265la8 --input /tmp/s2160.yuv --input-res 3840x2160 --fps 30 --frames 16 --preset medium --pools 16 --no-info -o /tmp/o.hevc \
+    > gpurun_out/r04h_encprof.log 2>&1 || { tail -20 gpurun_out/r04h_encprof.log; exit 1; }
+grep -E "encoded|x265me\] stats" gpurun_out/r04h_encprof.log
+find gpurun_out/r04h_encprof -name "*stats*.csv" | while read f; do echo "== $f"; head -12 "$f" | cut -c1-200; done
+# copies on blit kernels in the compute queue (no SDMA engine hop) for the per-PU search round trips
+python3 -c "
+from src.x265_amd.synth import SyntheticSource
+SyntheticSource(3840, 2160, 64, 8).write_yuv('/tmp/s2160.yuv')" || exit 1
+for rep in 1 2; do
+  for sd in 1 0; do
+    HSA_ENABLE_SDMA=$sd X265AMD_ME_STATS=1 timeout -k 10 200 oracle/_ref/x265la8 --input /tmp/s2160.yuv --input-res 3840x2160 --fps 30 --frames 64 \
+        --preset medium --pools 16 --no-info -o /tmp/o.hevc > /tmp/e.txt 2>&1 || { tail -5 /tmp/e.txt; exit 1; }
+    echo "rep=$rep sdma=$sd: $(grep encoded /tmp/e.txt) $(md5sum < /tmp/o.hevc | cut -c1-8) $(grep -o '[0-9.]* ms/prefetch' /tmp/e.txt)" | tee -a gpurun_out/r04h_sdma_ab.txt
+  done
+done
