@@ -295,12 +295,12 @@ ENCODER_ARMS = (
     # (key, binary, extra environment, what runs on the MI355X)
     ("reference", "x265ref8", {}, "nothing: the unmodified reference encoder on the host cores"),
     ("mi355x_lookahead", "x265la8", {"X265AMD_ME": "cpu"},
-     "LookaheadTLD::lowresIntraEstimate, every CostEstimateGroup estimate (P / B, lowres motion searches, "
-     "batched per finishBatch) and cuTree's Lookahead::estimateCUPropagate steps"),
+     "LookaheadTLD::lowresIntraEstimate and every CostEstimateGroup estimate (P / B, lowres motion searches, "
+     "batched per finishBatch)"),
     ("mi355x_lookahead_me", "x265la8", {"X265AMD_ME": "gpu"},
-     "the lookahead work as above, plus the main encoder's motion searches of 64x64 PUs "
-     "(Search::predInterSearch's per-reference motionEstimate calls of a CU in one device batch; the batches "
-     "of all workers waiting at once coalesced into one launch; integration/gpu_me.cpp)"),
+     "the lookahead estimates as above, plus the main encoder's motion searches of 64x64 PUs "
+     "(Search::predInterSearch's per-reference motionEstimate calls of a CU in one device batch, "
+     "integration/gpu_me.cpp)"),
 )
 
 

@@ -67,6 +67,7 @@ struct TabBitCost : public BitCost
 enum { MODE_GPU = 0, MODE_CPU = 1, MODE_HOST = 2, MODE_CHECK = 3 };
 
 int g_mode = MODE_GPU;
+bool g_propagate = false;      /* X265AMD_LA_PROPAGATE=1: cuTree's propagation steps on the device */
 int g_la_status = 0;
 pthread_mutex_t g_mu = PTHREAD_MUTEX_INITIALIZER;
 pthread_once_t g_mode_once = PTHREAD_ONCE_INIT;
@@ -85,6 +86,8 @@ void read_mode()
             g_mode == MODE_CHECK ? "the MI355X, each checked against the CPU" : "the MI355X");
     if (g_mode == MODE_CHECK)
         atexit(print_check_summary);
+    const char* pr = getenv("X265AMD_LA_PROPAGATE");
+    g_propagate = pr && atoi(pr) != 0;
     const char* st = getenv("X265AMD_LA_STATS");
     g_stats_on = st && *st && strcmp(st, "0");
     if (g_stats_on)
@@ -284,11 +287,14 @@ namespace X265_NS {
 /* cuTree's propagation step (slicetype.cpp:1741-1842) on the device: the reference's set-up (bipred
  * weights, list distances, the fps factor, the zeroed first row of a non-referenced frame's
  * propagateCost) restated, the per-CU loop one x265amd_la_propagate call.  With VBV the reference's
- * cuTreeFinish follows the loop, so that configuration runs the reference's function. */
+ * cuTreeFinish follows the loop, so that configuration runs the reference's function.
+ * X265AMD_LA_PROPAGATE=1 selects it (built in round 4, off by default until it has run on the box;
+ * X265AMD_LOOKAHEAD=check then compares every propagation with the reference's). */
 void Lookahead::estimateCUPropagate(Lowres** frames, double averageDuration, int p0, int p1, int b, int referenced)
 {
     pthread_once(&g_mode_once, read_mode);
-    if (g_mode == MODE_CPU || g_mode == MODE_HOST || (m_param->rc.vbvBufferSize && m_param->lookaheadDepth && referenced))
+    if (!g_propagate || g_mode == MODE_CPU || g_mode == MODE_HOST ||
+        (m_param->rc.vbvBufferSize && m_param->lookaheadDepth && referenced))
     {
         x265ref_estimateCUPropagate(this, frames, averageDuration, p0, p1, b, referenced);
         return;

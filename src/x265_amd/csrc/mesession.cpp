@@ -14,11 +14,10 @@
 //   * per host thread: a non-blocking stream, pinned staging and device scratch for one batch
 //     (the PU's source block and the job descriptors), found by (session address, session id).
 // x265amd_mes_search is synchronous on the calling thread: outputs are in the jobs on return.
-// Coalescing (X265AMD_MES_COALESCE, default on): the searches of all threads that call while a launch
-// is in flight are queued; whichever waiting thread finds the device idle launches every queued
-// request of one PU size as ONE batch on its stream and hands each caller its outputs — one launch
-// and two copies per batch of PUs instead of per PU, and no queueing of 16 workers' small launches
-// behind each other on the process's few hardware queues.
+// Coalescing (X265AMD_MES_COALESCE=1; built in round 4, off by default until it has run on the box):
+// the searches of all threads that call while a launch is in flight are queued, and whichever waiting
+// thread finds the device idle launches every queued request of one PU size as ONE batch on its stream
+// and hands each caller its outputs.
 // Failures are returned AND recorded in the backend's sticky status (x265amd_provider_status).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -357,6 +356,95 @@ extern "C" int x265amd_mes_table(x265amd_mes* s, const uint16_t* centre, int* in
 
 namespace {
 
+// stage a batch of one PU's searches in g and enqueue upload, launch and download on the thread's
+// stream; *out = the outputs' offset in g.host
+int enqueue(x265amd_mes* s, x265amd_mes_thread* t, x265amd_mes_stage& g, hipStream_t st, int w, int h,
+            const void* fenc, intptr_t fenc_stride, int n, const x265amd_mes_job* jobs, size_t* out)
+{
+    if (!s || n < 0 || (n && (!jobs || !fenc)) || w < 4 || h < 4 || w > 64 || h > 64 || fenc_stride < w)
+        return X265AMD_EINVAL;
+    const int maxc = s->cfg.max_cand > 0 ? s->cfg.max_cand : 1;
+    for (int i = 0; i < n; i++)
+        if (jobs[i].slot < 0 || jobs[i].slot >= s->next_slot || jobs[i].table < 0 ||
+            jobs[i].table >= s->cfg.max_tables || jobs[i].num_cand < 0 || jobs[i].num_cand > s->cfg.max_cand)
+            return X265AMD_EINVAL;
+    const Layout L(n, h, (int)s->pix, maxc, fenc_stride);
+    if (int rc = reserve(t, g, L.end)) return rc;
+    uint8_t* H = g.host;
+    memcpy(H + L.fenc, fenc, (size_t)fenc_stride * h * s->pix);
+    int64_t* foff = (int64_t*)(H + L.fenc_off);
+    int64_t* roff = (int64_t*)(H + L.ref_off);
+    int16_t* rng = (int16_t*)(H + L.range);
+    int16_t* mvp = (int16_t*)(H + L.mvp);
+    int16_t* mvc = (int16_t*)(H + L.mvc);
+    uint8_t* nc = H + L.ncand;
+    int64_t* coff = (int64_t*)(H + L.cost_off);
+    for (int i = 0; i < n; i++)
+    {
+        const x265amd_mes_job& j = jobs[i];
+        foff[i] = 0;
+        roff[i] = (int64_t)j.slot * s->cfg.plane_elems + s->cfg.org_offset + j.block_off;
+        memcpy(rng + 4 * i, j.mv_range, 8);
+        memcpy(mvp + 2 * i, j.mvp, 4);
+        memcpy(mvc + 2 * (size_t)maxc * i, j.mvc, 4 * (size_t)j.num_cand);
+        nc[i] = (uint8_t)j.num_cand;
+        coff[i] = (int64_t)j.table * (int64_t)s->table_elems + s->cfg.mvcost_range;
+    }
+    if (hipError_t e = hipMemcpyAsync(g.dev, H, L.out_mv, hipMemcpyHostToDevice, st)) return (int)e;
+    x265amd_me_batch b;
+    memset(&b, 0, sizeof(b));
+    b.w = w;
+    b.h = h;
+    b.n = n;
+    b.method = s->cfg.method;
+    b.subme = s->cfg.subme;
+    b.merange = s->cfg.merange;
+    b.max_cand = maxc;
+    b.fenc = g.dev + L.fenc;
+    b.fenc_stride = fenc_stride;
+    b.fenc_off = (const int64_t*)(g.dev + L.fenc_off);
+    b.ref = s->arena;
+    b.ref_stride = s->cfg.stride;
+    b.ref_off = (const int64_t*)(g.dev + L.ref_off);
+    b.mv_range = (const int16_t*)(g.dev + L.range);
+    b.mvp = (const int16_t*)(g.dev + L.mvp);
+    b.mvc = (const int16_t*)(g.dev + L.mvc);
+    b.num_cand = g.dev + L.ncand;
+    b.mvcost = s->tables;
+    b.mvcost_off = (const int64_t*)(g.dev + L.cost_off);
+    b.out_mv = (int16_t*)(g.dev + L.out_mv);
+    b.out_cost = (int32_t*)(g.dev + L.out_cost);
+    if (int rc = x265amd_motion_search(s->cfg.depth, 1, &b, st)) return rc;
+    if (hipError_t e = hipMemcpyAsync(H + L.out_mv, g.dev + L.out_mv, L.end - L.out_mv, hipMemcpyDeviceToHost, st))
+        return (int)e;
+    *out = L.out_mv;
+    return 0;
+}
+
+void unpack(const x265amd_mes_stage& g, size_t out, int n, x265amd_mes_job* jobs)
+{
+    const int16_t* om = (const int16_t*)(g.host + out);
+    const int32_t* oc = (const int32_t*)(g.host + out + (((size_t)4 * n + 255) & ~(size_t)255));
+    for (int i = 0; i < n; i++)
+    {
+        jobs[i].out_mv[0] = om[2 * i];
+        jobs[i].out_mv[1] = om[2 * i + 1];
+        jobs[i].out_cost = oc[i];
+    }
+}
+
+// ---- coalescing (X265AMD_MES_COALESCE=1)
+bool coalescing()
+{
+    static int v = -1;
+    if (v < 0)
+    {
+        const char* e = getenv("X265AMD_MES_COALESCE");
+        v = e ? atoi(e) != 0 : 0;
+    }
+    return v != 0;
+}
+
 int check_request(const x265amd_mes* s, int w, int h, const void* fenc, intptr_t fenc_stride, int n,
                   const x265amd_mes_job* jobs)
 {
@@ -369,58 +457,45 @@ int check_request(const x265amd_mes* s, int w, int h, const void* fenc, intptr_t
     return 0;
 }
 
-// one PU's share of a batch: its source block and its searches
-struct Part
-{
-    const void* fenc;
-    intptr_t fenc_stride;
-    int n;
-    const x265amd_mes_job* jobs;
-};
-
-// stage the searches of `np` PUs of one size (checked by check_request) in g — the source blocks
-// packed at stride w, one after another — and enqueue upload, launch and download on `st`; *out = the
-// outputs' offset in g.host (job order = part order)
-int enqueue_parts(x265amd_mes* s, x265amd_mes_thread* t, x265amd_mes_stage& g, hipStream_t st, int w, int h,
-                  const Part* parts, int np, size_t* out)
+// stage the searches of several PUs of one size (requests checked by check_request) in g — their source
+// blocks packed at stride w, one after another, jobs in request order — and enqueue upload, launch and
+// download on `st`; *out = the outputs' offset in g.host
+int enqueue_requests(x265amd_mes* s, x265amd_mes_thread* t, x265amd_mes_stage& g, hipStream_t st, int w, int h,
+                     const std::vector<x265amd_mes::Request*>& reqs, size_t* out)
 {
     const int maxc = s->cfg.max_cand > 0 ? s->cfg.max_cand : 1;
+    const int np = (int)reqs.size();
     int n = 0;
-    for (int k = 0; k < np; k++) n += parts[k].n;
+    for (auto* r : reqs) n += r->n;
     const size_t blk = (size_t)w * h;                         // elements per packed source block
     const Layout L(n, np * h, (int)s->pix, maxc, w);
     if (int rc = reserve(t, g, L.end)) return rc;
     uint8_t* H = g.host;
     int64_t* foff = (int64_t*)(H + L.fenc_off);
-    for (int k = 0, i = 0; k < np; k++)
-    {
-        for (int y = 0; y < h; y++)
-            memcpy(H + L.fenc + (k * blk + (size_t)y * w) * s->pix,
-                   (const uint8_t*)parts[k].fenc + (size_t)y * parts[k].fenc_stride * s->pix, (size_t)w * s->pix);
-        for (int q = 0; q < parts[k].n; q++) foff[i++] = (int64_t)(k * blk);
-    }
-    const x265amd_mes_job* jobs = nullptr;
-    int part = -1, left = 0;
-    auto next_job = [&](int) -> const x265amd_mes_job& {
-        while (left == 0) { part++; jobs = parts[part].jobs; left = parts[part].n; }
-        left--;
-        return *jobs++;
-    };
     int64_t* roff = (int64_t*)(H + L.ref_off);
     int16_t* rng = (int16_t*)(H + L.range);
     int16_t* mvp = (int16_t*)(H + L.mvp);
     int16_t* mvc = (int16_t*)(H + L.mvc);
     uint8_t* nc = H + L.ncand;
     int64_t* coff = (int64_t*)(H + L.cost_off);
-    for (int i = 0; i < n; i++)
+    int i = 0;
+    for (int k = 0; k < np; k++)
     {
-        const x265amd_mes_job& j = next_job(i);
-        roff[i] = (int64_t)j.slot * s->cfg.plane_elems + s->cfg.org_offset + j.block_off;
-        memcpy(rng + 4 * i, j.mv_range, 8);
-        memcpy(mvp + 2 * i, j.mvp, 4);
-        memcpy(mvc + 2 * (size_t)maxc * i, j.mvc, 4 * (size_t)j.num_cand);
-        nc[i] = (uint8_t)j.num_cand;
-        coff[i] = (int64_t)j.table * (int64_t)s->table_elems + s->cfg.mvcost_range;
+        const x265amd_mes::Request& r = *reqs[k];
+        for (int y = 0; y < h; y++)
+            memcpy(H + L.fenc + (k * blk + (size_t)y * w) * s->pix,
+                   (const uint8_t*)r.fenc + (size_t)y * r.fenc_stride * s->pix, (size_t)w * s->pix);
+        for (int q = 0; q < r.n; q++, i++)
+        {
+            const x265amd_mes_job& j = r.jobs[q];
+            foff[i] = (int64_t)(k * blk);
+            roff[i] = (int64_t)j.slot * s->cfg.plane_elems + s->cfg.org_offset + j.block_off;
+            memcpy(rng + 4 * i, j.mv_range, 8);
+            memcpy(mvp + 2 * i, j.mvp, 4);
+            memcpy(mvc + 2 * (size_t)maxc * i, j.mvc, 4 * (size_t)j.num_cand);
+            nc[i] = (uint8_t)j.num_cand;
+            coff[i] = (int64_t)j.table * (int64_t)s->table_elems + s->cfg.mvcost_range;
+        }
     }
     if (hipError_t e = hipMemcpyAsync(g.dev, H, L.out_mv, hipMemcpyHostToDevice, st)) return (int)e;
     x265amd_me_batch b;
@@ -453,37 +528,6 @@ int enqueue_parts(x265amd_mes* s, x265amd_mes_thread* t, x265amd_mes_stage& g, h
     return 0;
 }
 
-void unpack(const x265amd_mes_stage& g, size_t out, int n, x265amd_mes_job* jobs)
-{
-    const int16_t* om = (const int16_t*)(g.host + out);
-    const int32_t* oc = (const int32_t*)(g.host + out + (((size_t)4 * n + 255) & ~(size_t)255));
-    for (int i = 0; i < n; i++)
-    {
-        jobs[i].out_mv[0] = om[2 * i];
-        jobs[i].out_mv[1] = om[2 * i + 1];
-        jobs[i].out_cost = oc[i];
-    }
-}
-
-int enqueue(x265amd_mes* s, x265amd_mes_thread* t, x265amd_mes_stage& g, hipStream_t st, int w, int h,
-            const void* fenc, intptr_t fenc_stride, int n, const x265amd_mes_job* jobs, size_t* out)
-{
-    if (int rc = check_request(s, w, h, fenc, fenc_stride, n, jobs)) return rc;
-    const Part p = { fenc, fenc_stride, n, jobs };
-    return enqueue_parts(s, t, g, st, w, h, &p, 1, out);
-}
-
-bool coalescing()
-{
-    static int v = -1;
-    if (v < 0)
-    {
-        const char* e = getenv("X265AMD_MES_COALESCE");
-        v = e ? atoi(e) != 0 : 1;
-    }
-    return v != 0;
-}
-
 // lead one coalesced batch: every queued request of the first request's PU size (s->cmu held on entry
 // and on return, released while the device works)
 void lead_batch(x265amd_mes* s, x265amd_mes_thread* t, std::unique_lock<std::mutex>& lk)
@@ -500,19 +544,13 @@ void lead_batch(x265amd_mes* s, x265amd_mes_thread* t, std::unique_lock<std::mut
     s->queue.resize(keep);
     s->busy = true;
     lk.unlock();
-    std::vector<Part> parts(batch.size());
-    int n = 0;
-    for (size_t k = 0; k < batch.size(); k++)
-    {
-        parts[k] = { batch[k]->fenc, batch[k]->fenc_stride, batch[k]->n, batch[k]->jobs };
-        n += batch[k]->n;
-    }
     size_t out = 0;
-    int rc = enqueue_parts(s, t, t->sync, t->st, w, h, parts.data(), (int)parts.size(), &out);
+    int rc = enqueue_requests(s, t, t->sync, t->st, w, h, batch, &out);
     if (!rc) rc = wait(t);
     if (!rc)
     {
-        // outputs in part order
+        int n = 0;
+        for (auto* r : batch) n += r->n;
         const int16_t* om = (const int16_t*)(t->sync.host + out);
         const int32_t* oc = (const int32_t*)(t->sync.host + out + (((size_t)4 * n + 255) & ~(size_t)255));
         for (size_t k = 0, i = 0; k < batch.size(); k++)

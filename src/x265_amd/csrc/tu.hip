@@ -277,9 +277,7 @@ struct TuArgs
     int n, is_luma, is_intra, i_slice, sign_hide, depth;
 };
 
-// PF: grid-stride over TUs (gridDim.x blocks of JOBS groups), the next TU's fenc / pred row and QP
-// loaded before the current TU's chain (one TU's inputs in flight behind the dependent work)
-template <typename P, int N, bool PF = false>
+template <typename P, int N>
 __global__ __launch_bounds__(X265AMD_BLOCK) void k_tu(const TuArgs a)
 {
     constexpr int LOG2 = N == 4 ? 2 : N == 8 ? 3 : N == 16 ? 4 : 5;
@@ -288,42 +286,22 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_tu(const TuArgs a)
     constexpr int NCG = N * N / 16;
     __shared__ int16_t lds_t[JOBS][N * PT];   // stage tiles; DCT coefficients (pitch N) during quant/SBH
     __shared__ int16_t lds_q[JOBS][N * N];    // quantized coefficients (raster, as coeff[])
-    const int slot = threadIdx.x / N, lane_r = threadIdx.x % N;
-    const int depth = a.depth, maxv = (1 << depth) - 1;
-    const bool use_dst = N == 4 && a.is_luma && a.is_intra;
-    const int tshift = 15 - depth - LOG2;     // MAX_TR_DYNAMIC_RANGE - depth - log2 (quant.cpp:411)
-    struct In { PixRow<P, N> f, p; int qp; };
-    auto load_in = [&](int64_t jj, In& t) {
-        t.qp = a.qp[jj];
-        t.f.load((const P*)a.fenc + a.fenc_off[jj] + lane_r * a.fenc_stride);
-        t.p.load((const P*)a.pred + a.pred_off[jj] + lane_r * a.pred_stride);
-    };
-    // whole groups only; no block barrier below
-    const int64_t step = PF ? (int64_t)gridDim.x * JOBS : a.n;
-    int64_t j = (int64_t)(PF ? blockIdx.x : xcd_block()) * JOBS + slot;
-    In nxt;
-    if (PF && j < a.n) load_in(j, nxt);
-    for (; j < a.n; j += step)
-    {
-    In in;
-    if constexpr (PF)
-    {
-        in = nxt;
-        if (j + step < a.n) load_in(j + step, nxt);
-    }
-    else
-        load_in(j, in);
-    // the lane's row index, opaque per TU: values derived from it are recomputed here instead of
-    // being hoisted out of the TU loop into registers that stay live across it
-    int r = lane_r;
-    if constexpr (PF) asm volatile("" : "+v"(r));
+    const int slot = threadIdx.x / N, r = threadIdx.x % N;
+    const int64_t j = (int64_t)xcd_block() * JOBS + slot;
+    if (j >= a.n) return;                     // whole groups only; no block barrier below
     int16_t* T = lds_t[slot];
     int16_t* Q = lds_q[slot];
-    const int qp = in.qp, rem = qp % 6, per = qp / 6;
+    const int depth = a.depth, maxv = (1 << depth) - 1;
+    const int qp = a.qp[j], rem = qp % 6, per = qp / 6;
+    const bool use_dst = N == 4 && a.is_luma && a.is_intra;
+    const int tshift = 15 - depth - LOG2;     // MAX_TR_DYNAMIC_RANGE - depth - log2 (quant.cpp:411)
+    const P* pf = (const P*)a.fenc + a.fenc_off[j] + r * a.fenc_stride;
+    const P* pp = (const P*)a.pred + a.pred_off[j] + r * a.pred_stride;
 
     int x[N], y[N];
-    const PixRow<P, N>& frow = in.f;          // kept packed for the reconstruction
-    const PixRow<P, N>& prow = in.p;
+    PixRow<P, N> frow, prow;                  // kept packed for the reconstruction
+    frow.load(pf);
+    prow.load(pp);
 #pragma unroll
     for (int i = 0; i < N; i++) x[i] = frow.get(i) - prow.get(i);
 
@@ -456,8 +434,6 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_tu(const TuArgs a)
     store_n<P, N>((P*)a.recon + a.recon_off[j] + r * a.recon_stride, rec);
     if (a.resi)
         store_n<int16_t, N>(a.resi + a.resi_off[j] + r * a.resi_stride, res);
-    if constexpr (PF) wave_sync();            // the group's LDS tiles are reused by its next TU
-    }
 }
 
 // ---------------------------------------------------------------- 32x32 on the matrix cores
@@ -677,16 +653,7 @@ constexpr ColSumsTu make_colsums_tu()
 }
 static __constant__ ColSumsTu c_colsum128_tu = make_colsums_tu();
 
-// PF: the next TU's fenc / pred rows are loaded before the current TU's chain starts (one TU's
-// inputs in flight behind the dependent MFMA / quant / sign-hiding work of the other)
 template <typename P>
-struct Tu32In
-{
-    PixRow<P, 16> fa, pa, fio, pio;      // row r, columns 16h..; row io_row, columns io_col..
-    int qp;
-};
-
-template <typename P, bool PF = false>
 __global__ __launch_bounds__(X265AMD_BLOCK) void k_tu32_i8(const TuArgs a)
 {
     __shared__ int16_t lds_c[kTuWaves][32 * 32];   // DCT coefficients; later the inverse output
@@ -725,39 +692,25 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_tu32_i8(const TuArgs a)
     const int icol = c_colsum128_tu.v[r];
 
     const int64_t step = (int64_t)gridDim.x * kTuWaves;
-    // the inputs of one TU: the residual's rows (stage-1 layout) and the reconstruction's row segments,
-    // both from the same fenc / pred rows (one global round trip per TU)
-    auto load_in = [&](int64_t jj, Tu32In<P>& t) {
-        const P* pf = (const P*)a.fenc + a.fenc_off[jj];
-        const P* pp = (const P*)a.pred + a.pred_off[jj];
-        t.qp = a.qp[jj];
-        t.fa.load(pf + r * a.fenc_stride + 16 * h);
-        t.pa.load(pp + r * a.pred_stride + 16 * h);
-        t.fio.load(pf + io_row * a.fenc_stride + io_col);
-        t.pio.load(pp + io_row * a.pred_stride + io_col);
-    };
-    int64_t j = (int64_t)blockIdx.x * kTuWaves + w;
-    Tu32In<P> nxt;
-    if (PF && j < a.n) load_in(j, nxt);
-    for (; j < a.n; j += step)
+    for (int64_t j = (int64_t)blockIdx.x * kTuWaves + w; j < a.n; j += step)
     {
-        Tu32In<P> in;
-        if constexpr (PF)
-        {
-            in = nxt;
-            if (j + step < a.n) load_in(j + step, nxt);
-        }
-        else
-            load_in(j, in);
-        const int qp = in.qp, rem = qp % 6, per = qp / 6;
-        const PixRow<P, 16>& fio = in.fio;
-        const PixRow<P, 16>& pio = in.pio;
+        const P* pf = (const P*)a.fenc + a.fenc_off[j];
+        const P* pp = (const P*)a.pred + a.pred_off[j];
+        const int qp = a.qp[j], rem = qp % 6, per = qp / 6;
+        // the reconstruction's row segments, loaded with the residual's (one global round trip per TU)
+        PixRow<P, 16> fio, pio;
+        fio.load(pf + io_row * a.fenc_stride + io_col);
+        pio.load(pp + io_row * a.pred_stride + io_col);
 
         // ---- forward stage 1: A = residual row r, columns 16h + 0..15
         uint32_t x[8];
+        {
+            int f[16], p[16];
+            load_row<P, 16>(pf + r * a.fenc_stride + 16 * h, f);
+            load_row<P, 16>(pp + r * a.pred_stride + 16 * h, p);
 #pragma unroll
-        for (int q = 0; q < 8; q++)
-            x[q] = pack16(in.fa.get(2 * q) - in.pa.get(2 * q), in.fa.get(2 * q + 1) - in.pa.get(2 * q + 1));
+            for (int q = 0; q < 8; q++) x[q] = pack16(f[2 * q] - p[2 * q], f[2 * q + 1] - p[2 * q + 1]);
+        }
         i32x4 xl, xh;
         split_bytes(x, xl, xh);
         i32x16 lo = __builtin_amdgcn_mfma_i32_32x32x32_i8(xl, fc1, (i32x16){}, 0, 0, 0);
@@ -1029,29 +982,16 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_tu4(const TuArgs a)
 }
 
 // the integer-MFMA 32x32 TU kernel, default (X265AMD_TU_I8=0 selects the f16 split form; measured,
-// profiles/r04/tu32_i8_ab.txt: tu_pipeline 32x32 0.20 -> 0.26 of the HBM peak); =2: with the next TU's
-// inputs prefetched
-static int tu_i8()
+// profiles/r04/tu32_i8_ab.txt: tu_pipeline 32x32 0.20 -> 0.26 of the HBM peak)
+static bool tu_i8()
 {
     static int v = -1;
     if (v < 0)
     {
         const char* e = getenv("X265AMD_TU_I8");
-        v = e ? atoi(e) : 1;
+        v = e ? atoi(e) != 0 : 1;
     }
-    return v;
-}
-
-// 8x8 / 16x16: grid-stride groups with the next TU's inputs prefetched (X265AMD_TU_PF=1)
-static int tu_pf()
-{
-    static int v = -1;
-    if (v < 0)
-    {
-        const char* e = getenv("X265AMD_TU_PF");
-        v = e ? atoi(e) : 0;
-    }
-    return v;
+    return v != 0;
 }
 
 template <typename P>
@@ -1065,21 +1005,13 @@ static int launch_tu(int log2, const TuArgs& a, hipStream_t st)
         hipLaunchKernelGGL((k_tu4<P>), dim3((uint32_t)((a.n + X265AMD_BLOCK - 1) / X265AMD_BLOCK)), dim3(X265AMD_BLOCK),
                            0, st, a);
         break;
-    case 3:
-        if (tu_pf()) hipLaunchKernelGGL((k_tu<P, 8, true>), dim3(blocks < 2048 ? blocks : 2048), dim3(X265AMD_BLOCK), 0, st, a);
-        else hipLaunchKernelGGL((k_tu<P, 8>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, a);
-        break;
-    case 4:
-        if (tu_pf()) hipLaunchKernelGGL((k_tu<P, 16, true>), dim3(blocks < 2048 ? blocks : 2048), dim3(X265AMD_BLOCK), 0, st, a);
-        else hipLaunchKernelGGL((k_tu<P, 16>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, a);
-        break;
+    case 3: hipLaunchKernelGGL((k_tu<P, 8>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, a); break;
+    case 4: hipLaunchKernelGGL((k_tu<P, 16>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, a); break;
     case 5:
     {
         // one wavefront per TU, enough waves to fill the chip, each looping over TUs
         const int64_t want = ((int64_t)a.n + kTuWaves - 1) / kTuWaves;
-        if (tu_i8() == 2)
-            hipLaunchKernelGGL((k_tu32_i8<P, true>), dim3((uint32_t)(want < 4096 ? want : 4096)), dim3(X265AMD_BLOCK), 0, st, a);
-        else if (tu_i8())
+        if (tu_i8())
             hipLaunchKernelGGL((k_tu32_i8<P>), dim3((uint32_t)(want < 4096 ? want : 4096)), dim3(X265AMD_BLOCK), 0, st, a);
         else
             hipLaunchKernelGGL((k_tu32_mfma<P>), dim3((uint32_t)(want < 4096 ? want : 4096)), dim3(X265AMD_BLOCK), 0, st, a);

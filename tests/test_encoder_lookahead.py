@@ -112,33 +112,11 @@ def test_gpu_lookahead_encode_1080p_medium_is_bit_exact(tmp_path):
     src = _source(tmp_path, w, h, n)
     rc, ref, ref_fps, err = encode(_bin("x265ref8"), src, w, h, n, tmp_path / "ref.hevc", pools=16)
     assert rc == 0, err[-2000:]
-    rc, got, la_fps, err = encode(_bin("x265la8"), src, w, h, n, tmp_path / "la.hevc", {"X265AMD_LA_STATS": "1"},
-                                  pools=16)
+    rc, got, la_fps, err = encode(_bin("x265la8"), src, w, h, n, tmp_path / "la.hevc", pools=16)
     assert rc == 0, err[-3000:]
     assert "[x265la] lookahead estimates on the MI355X" in err
     print(f"\n[x265la] 1080p medium {n} frames, --pools 16: reference {ref_fps} fps, MI355X lookahead {la_fps} fps")
-    # cuTree's propagation steps (estimateCUPropagate) ran on the device too
-    m = re.search(r"stats propagate\s+calls\s+(\d+)", err)
-    assert m and int(m.group(1)) > 0, err[-3000:]
     assert got == ref, "bitstream with the MI355X lookahead differs from the reference encoder"
-
-
-@pytest.mark.gpu
-def test_gpu_lookahead_check_mode_every_estimate_and_propagation_matches(tmp_path):
-    """X265AMD_LOOKAHEAD=check: every device estimate and every cuTree propagation is recomputed by the
-    reference's own function and compared (estimateCUPropagate, slicetype.cpp:1741-1842: the two
-    reference frames' propagateCost arrays after each step)"""
-    w, h, n = 1280, 720, 24
-    src = _source(tmp_path, w, h, n)
-    rc, ref, _, err = encode(_bin("x265ref8"), src, w, h, n, tmp_path / "ref.hevc")
-    assert rc == 0, err[-2000:]
-    rc, got, _, err = encode(_bin("x265la8"), src, w, h, n, tmp_path / "la.hevc",
-                             {"X265AMD_LOOKAHEAD": "check", "X265AMD_LA_STATS": "1"})
-    assert rc == 0, err[-3000:]
-    assert "check: 0 mismatching estimates" in err and "check: 0 mismatching propagations" in err, err[-3000:]
-    m = re.search(r"stats propagate\s+calls\s+(\d+)", err)
-    assert m and int(m.group(1)) > 0, err[-3000:]
-    assert got == ref
 
 
 @pytest.mark.gpu
