@@ -57,6 +57,8 @@ enum
 int         x265amd_abi_version(void);
 /* Select the HIP device for this host thread; returns 0 or a hipError_t. */
 int         x265amd_set_device(int device);
+/* Number of HIP devices visible to the process (0 on a host without one); returns 0 or a hipError_t. */
+int         x265amd_device_count(int* count);
 /* Human-readable message for a status code returned by any entry. */
 const char* x265amd_strerror(int status);
 /* Name of the gfx target the library was compiled for ("gfx950"). */
@@ -736,6 +738,10 @@ typedef struct
     const void* ref_cr;
     intptr_t ref_cstride;
     const int64_t* ref_coff;
+    /* optional (NULL = not counted): eval_count[0] / [1] += the full-pel / sub-pel block evaluations the
+     * batch's searches make (one SAD of the PU, resp. one interpolated PU + its SAD / SATD), the unit of the
+     * launch's algorithmic bytes; device memory, accumulated with atomics */
+    uint64_t* eval_count;
 } x265amd_me_batch;
 int x265amd_motion_search(int depth, int count, const x265amd_me_batch* batches, void* stream);
 
@@ -765,6 +771,11 @@ typedef struct
     int mvcost_range;              /* table entries [-range, range] are copied (2 * BC_MAX_MV) */
     int method, subme, merange;    /* x265_param searchMethod / subpelRefine / searchRange */
     int max_cand;                  /* most MV candidates of one search (mvc[] of predInterSearch: 12) */
+    int device;                    /* HIP device of the session (round 5; 0 = the first) */
+    int launchers;                 /* launch-service threads (round 5): 0 = every call runs on the calling
+                                      thread's own stream (round-4 form); > 0 = calls only queue requests and
+                                      this many service threads batch ALL queued requests of all threads into
+                                      one upload + launch + download each (x265amd_mes_post / _wait) */
 } x265amd_mes_config;
 int  x265amd_mes_create(const x265amd_mes_config* cfg, x265amd_mes** out);
 void x265amd_mes_destroy(x265amd_mes* mes);
@@ -800,6 +811,39 @@ int x265amd_mes_search(x265amd_mes* mes, int w, int h, const void* fenc, intptr_
 int x265amd_mes_submit(x265amd_mes* mes, int w, int h, const void* fenc, intptr_t fenc_stride, int n,
                        const x265amd_mes_job* jobs);
 int x265amd_mes_collect(x265amd_mes* mes, int n, x265amd_mes_job* jobs);
+/* Launch service (cfg.launchers > 0; round 5).  _post copies one PU's source block and its n <= 64
+ * searches into a request slot of the calling thread and returns at once with *ticket (0..7, valid on the
+ * calling thread only); the session's service threads batch every queued request of every thread into
+ * one launch.  _wait blocks until the ticket's searches are done and writes their outputs into jobs (n =
+ * the posted count), freeing the slot; _drop gives a ticket up (its slot is reused once the service has
+ * finished with it).  ENOMEM (not recorded in the sticky status) when all 8 slots of the thread are
+ * outstanding or n > 64: search on the host.  With launchers, _search is _post + _wait, and _submit /
+ * _collect keep their one-outstanding-per-thread contract on top of a ticket. */
+int x265amd_mes_post(x265amd_mes* mes, int w, int h, const void* fenc, intptr_t fenc_stride, int n,
+                     const x265amd_mes_job* jobs, int* ticket);
+int x265amd_mes_wait(x265amd_mes* mes, int ticket, int n, x265amd_mes_job* jobs);
+int x265amd_mes_drop(x265amd_mes* mes, int ticket);
+/* rows of reference picture `key` (generation gen) resident on the device (0 if unknown) */
+int x265amd_mes_rows(x265amd_mes* mes, const void* key, int64_t gen, int* rows_resident);
+/* session counters: service batches, the requests / searches they carried, device time of the search
+ * launches (HIP events around each launch on its stream), wall time from a batch's start to its outputs on
+ * the host, summed queueing delay of the requests (post -> batch start), reference-row uploads, the time
+ * callers spent blocked in _wait (and how many of those waits had to sleep), and the launches' block
+ * evaluations and algorithmic bytes */
+typedef struct
+{
+    int64_t batches, requests, jobs, max_requests_per_batch;
+    double kernel_ms, batch_ms, queue_ms;
+    int64_t uploads, upload_bytes;
+    double upload_ms;
+    int64_t waits, waits_blocked, dropped;
+    double wait_ms;
+    /* block evaluations of the search launches (full-pel SADs, sub-pel interpolations + compares), their
+     * algorithmic bytes, and the longest launch */
+    int64_t evals_fpel, evals_subpel;
+    double algo_bytes, kernel_ms_max;
+} x265amd_mes_counters;
+int x265amd_mes_stats(x265amd_mes* mes, x265amd_mes_counters* out);
 
 /* ------------------------------------------------------------------- f4
  * In-loop filters and border extension of device-resident 4:2:0 recon frames

@@ -700,3 +700,15 @@ void CostEstimateGroup::finishBatch()
 }
 
 } // namespace X265_NS
+
+/* called by the encoder binding after x265_encoder_close (oracle/hip_encoder_main.cpp): the closed encoder's
+ * lookahead sessions are destroyed, so a later encoder in the same process — whose Lowres objects may sit at
+ * the same addresses with the same frame numbers — never finds the earlier encoder's planes resident */
+extern "C" void x265amd_la_encoder_closed(void)
+{
+    pthread_mutex_lock(&g_mu);
+    for (Session& s : g_sessions)
+        x265amd_la_destroy(s.la);
+    g_sessions.clear();
+    pthread_mutex_unlock(&g_mu);
+}

@@ -41,10 +41,23 @@ extern "C" const char* x265amd_strerror(int status);
 extern "C" int x265amd_provider_status(void);
 
 extern "C" const x265_api* __real_x265_api_get_79(int bitDepth);
+/* x265la builds (integration/gpu_me.cpp, gpu_lookahead.cpp): drop the closed encoder's device sessions */
+extern "C" void x265amd_me_encoder_closed(void) __attribute__((weak));
+extern "C" void x265amd_la_encoder_closed(void) __attribute__((weak));
 
 namespace {
 x265_api g_api;
 int (*g_encode)(x265_encoder*, x265_nal**, uint32_t*, x265_picture*, x265_picture*);
+void (*g_close)(x265_encoder*);
+
+void closing(x265_encoder* enc)
+{
+    g_close(enc);
+    if (x265amd_me_encoder_closed)
+        x265amd_me_encoder_closed();
+    if (x265amd_la_encoder_closed)
+        x265amd_la_encoder_closed();
+}
 
 int checked_encode(x265_encoder* enc, x265_nal** pp_nal, uint32_t* pi_nal, x265_picture* in, x265_picture* out)
 {
@@ -67,6 +80,8 @@ extern "C" const x265_api* __wrap_x265_api_get_79(int bitDepth)
     g_api = *api;
     g_encode = api->encoder_encode;
     g_api.encoder_encode = checked_encode;
+    g_close = api->encoder_close;
+    g_api.encoder_close = closing;
     return &g_api;
 }
 

@@ -246,6 +246,24 @@ __device__ __forceinline__ void store_quad_row(P* p, const int (&o)[N])
     }
 }
 
+// v_pk_mad_u16 with the addend as an SGPR operand (left to the compiler, a constant addend becomes a
+// v_pk_mul_lo_u16 + v_pk_add_u16 pair)
+__device__ __forceinline__ uint32_t pmad_s(uint32_t a, uint32_t b, uint32_t c)
+{
+    uint32_t r;
+    asm("v_pk_mad_u16 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(c));
+    return r;
+}
+
+// v_dot2_u32_u16 in its VOP3P form with the accumulator start as an SGPR operand (the compiler's tied
+// v_dot2c form needs a v_mov of the start into every destination)
+__device__ __forceinline__ uint32_t udot2_sinit(uint32_t a, uint32_t b, uint32_t init)
+{
+    uint32_t r;
+    asm("v_dot2_u32_u16 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(init));
+    return r;
+}
+
 template <typename P, int N, int G = 4>
 __global__ __launch_bounds__(X265AMD_BLOCK) void k_intra_quad(int n, int maxv,
     P* __restrict__ dst, intptr_t ds, const int64_t* __restrict__ doff,
@@ -384,7 +402,9 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_intra_quad(int n, int maxv,
     };
     if (!tr && sizeof(P) == 1)
     {
-        // 8 bit: two pixels of the row per packed-u16 multiply-add pair, v_perm to bytes
+        // 8 bit: two pixels of the row per packed-u16 multiply-add pair.  The weights are scaled by 8
+        // (and the rounding 16 by 8): 8 ((32 - f) a + f b + 16) <= 65408 still fits a u16 lane, and the
+        // pixel ((32 - f) a + f b + 16) >> 5 is its high byte, so one v_perm takes four pixels' bytes
         auto pmad = [](uint32_t a, uint32_t b, uint32_t c) -> uint32_t {
             return __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, a) * __builtin_bit_cast(u16x2, b) +
                                                     __builtin_bit_cast(u16x2, c));
@@ -394,14 +414,13 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_intra_quad(int n, int maxv,
         {
             const int r = i * G + q;
             const int sum = (r + 1) * mi.angle, f = sum & 31;
-            const uint32_t w0 = (uint32_t)(32 - f) * 0x10001u, w1 = (uint32_t)f * 0x10001u;
+            const uint32_t w0 = (uint32_t)(8 * (32 - f)) * 0x10001u, w1 = (uint32_t)(8 * f) * 0x10001u;
             const uint32_t* row = Dj + N + (sum >> 5);
             uint32_t pq[N / 2], w[N / 4];
 #pragma unroll
-            for (int k = 0; k < N / 2; k++)
-                pq[k] = __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, pmad(row[2 * k], w0, pmad(row[2 * k + 1], w1, 0x00100010u))) >> (u16x2){5, 5});
+            for (int k = 0; k < N / 2; k++) pq[k] = pmad(row[2 * k], w0, pmad_s(row[2 * k + 1], w1, 0x00800080u));
 #pragma unroll
-            for (int k = 0; k < N / 4; k++) w[k] = __builtin_amdgcn_perm(pq[2 * k + 1], pq[2 * k], 0x06040200u);
+            for (int k = 0; k < N / 4; k++) w[k] = __builtin_amdgcn_perm(pq[2 * k + 1], pq[2 * k], 0x07050301u);
             if (edge) w[0] = (w[0] & ~0xffu) | (uint32_t)edge_px(sj[flip_index(N2 + 1 + r, N2, fh)]);
             uint8_t* o8 = (uint8_t*)(out + (int64_t)r * os);
             if constexpr (N == 8)
@@ -428,6 +447,51 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_intra_quad(int n, int maxv,
                 o[x] = (int)(__builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, row[x]), wt, 16u, false) >> 5);
             if (edge) o[0] = edge_px(sj[flip_index(N2 + 1 + r, N2, fh)]);
             store_quad_row<P, N>(out + (int64_t)r * os, o);
+        }
+    }
+    else if (sizeof(P) == 1)
+    {
+        // 8 bit, transposed (horizontal modes): output column c of row r reads the pair at row
+        // offset r of the column's reference run; weights scaled by 8 as above, the rounding 128
+        // as the dot's SGPR operand, each pixel the sum's byte 1 (three v_perm per four pixels)
+        int offc[N];
+        uint32_t wc[N];
+#pragma unroll
+        for (int c = 0; c < N; c++)
+        {
+            const int sum = (c + 1) * mi.angle, f = sum & 31;
+            offc[c] = N + (sum >> 5);
+            wc[c] = (uint32_t)(8 * (32 - f)) | ((uint32_t)(8 * f) << 16);
+        }
+#pragma unroll
+        for (int i = 0; i < N / G; i++)
+        {
+            const int r = i * G + q;
+            uint8_t* o8 = (uint8_t*)(out + (int64_t)r * os);
+            if (edge && r == 0)
+            {
+                int o[N];
+#pragma unroll
+                for (int c = 0; c < N; c++) o[c] = edge_px(sj[flip_index(N2 + 1 + c, N2, fh)]);
+                store_quad_row<P, N>(out + (int64_t)r * os, o);
+                continue;
+            }
+            uint32_t w[N / 4];
+#pragma unroll
+            for (int k = 0; k < N / 4; k++)
+            {
+                uint32_t t[4];
+#pragma unroll
+                for (int e = 0; e < 4; e++) t[e] = udot2_sinit(Dj[offc[4 * k + e] + r], wc[4 * k + e], 128);
+                w[k] = __builtin_amdgcn_perm(t[1], t[0], 0x0c0c0501u) | __builtin_amdgcn_perm(t[3], t[2], 0x05010c0cu);
+            }
+            if constexpr (N == 8)
+                stu<uint2>(o8, make_uint2(w[0], w[1]));
+            else
+            {
+#pragma unroll
+                for (int k = 0; k < N / 16; k++) stu<uint4>(o8 + 16 * k, make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]));
+            }
         }
     }
     else

@@ -47,6 +47,7 @@ struct MeArgs
     const void* rcr;
     int64_t rcs;
     const int64_t* rcoff;
+    unsigned long long* evals;    // [2]: full-pel / sub-pel block evaluations of the launch (NULL = not counted)
     int w, h, n, lg, method, subme, merange, max_cand, depth;
 };
 
@@ -68,6 +69,7 @@ struct MeState
     const P* fc[2];         // source Cb / Cr at the PU's chroma origin
     const P* rc[2];         // reference Cb / Cr at the PU's chroma origin
     int64_t fcs, rcs;
+    mutable uint32_t nfp, nsp;   // block evaluations made (uniform over the group)
 
     __device__ __forceinline__ void unit_xy(int k, int& ux, int& uy) const
     {
@@ -123,6 +125,7 @@ template <typename P, int G>
 __device__ __forceinline__ int fpel_sad(const MeState<P>& s, int dx, int dy)
 {
     uint32_t acc = 0;
+    s.nfp++;
 #pragma unroll
     for (int k = 0; k < kMeMaxUnits; k++)
     {
@@ -292,6 +295,7 @@ template <typename P, int G>
 __device__ __noinline__ int subpel_cost(const MeState<P>& s, int qx, int qy, bool satd)
 {
     const int xf = qx & 3, yf = qy & 3;
+    s.nsp++;
     const P* base = s.ref + (qx >> 2) + (int64_t)(qy >> 2) * s.rs;
     const int maxv = (1 << s.a->depth) - 1;
     const int head = 14 - s.a->depth;
@@ -447,6 +451,7 @@ __global__ __launch_bounds__(X265AMD_BLOCK, X265AMD_ME_WAVES) void k_motion_sear
     s.tab = a.mvcost + a.mvcost_off[j];
     s.fenc = (const P*)a.fenc + a.fenc_off[j];
     s.fs = a.fs;
+    s.nfp = s.nsp = 0;
 #pragma unroll
     for (int k = 0; k < kMeMaxUnits; k++)
     {
@@ -874,6 +879,11 @@ __global__ __launch_bounds__(X265AMD_BLOCK, X265AMD_ME_WAVES) void k_motion_sear
         a.out_mv[2 * j] = (int16_t)qx;
         a.out_mv[2 * j + 1] = (int16_t)qy;
         a.out_cost[j] = bcost;
+        if (a.evals)
+        {
+            atomicAdd(&a.evals[0], (unsigned long long)s.nfp);
+            atomicAdd(&a.evals[1], (unsigned long long)s.nsp);
+        }
     }
 }
 
@@ -1050,7 +1060,7 @@ extern "C" int x265amd_motion_search(int depth, int count, const x265amd_me_batc
         MeArgs a{ b.fenc, b.fenc_off, (int64_t)b.fenc_stride, b.ref, b.ref_off, (int64_t)b.ref_stride, b.mv_range,
                   b.mvp, b.mvc, b.num_cand, b.mvcost, b.mvcost_off, b.out_mv, b.out_cost, b.fenc_cb, b.fenc_cr,
                   (int64_t)b.fenc_cstride, b.fenc_coff, b.ref_cb, b.ref_cr, (int64_t)b.ref_cstride, b.ref_coff,
-                  b.w, b.h, b.n, lg, b.method, b.subme, b.merange, b.max_cand, depth };
+                  (unsigned long long*)b.eval_count, b.w, b.h, b.n, lg, b.method, b.subme, b.merange, b.max_cand, depth };
         const int rc = depth == 8 ? launch_me<uint8_t>(a, bs) : launch_me<uint16_t>(a, bs);
         if (rc) { fj.join(); return rc; }
     }

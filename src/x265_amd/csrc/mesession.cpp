@@ -3,31 +3,38 @@
 //
 // Search::predInterSearch (search.cpp:2050-2231) runs one MotionEstimate::motionEstimate per
 // (list, reference) of a PU, one after another on a worker thread; the searches of one PU are
-// independent given their predictors.  A session turns them into one batched launch of the f2
-// kernel (x265amd_motion_search, csrc/me.hip) per PU:
+// independent given their predictors.  A session runs them on the device:
 //   * reference pictures: the padded luma plane of each reconstructed reference PicYuv
 //     (picyuv.cpp:51-91) in one device arena, uploaded CTU row by CTU row as the encoder
 //     publishes them (Frame::m_reconRowCount, framefilter.cpp:520: rows below the count are
 //     deblocked, SAO-filtered and border-extended, so they never change again) — each row once,
 //     whichever thread needs it first;
 //   * MV cost tables: the encoder's BitCost table of each QP (bitcost.cpp:31-57) uploaded once;
-//   * per host thread: a non-blocking stream, pinned staging and device scratch for one batch
-//     (the PU's source block and the job descriptors), found by (session address, session id).
-// x265amd_mes_search is synchronous on the calling thread: outputs are in the jobs on return.
-// Coalescing (X265AMD_MES_COALESCE=1; built in round 4, off by default until it has run on the box):
-// the searches of all threads that call while a launch is in flight are queued, and whichever waiting
-// thread finds the device idle launches every queued request of one PU size as ONE batch on its stream
-// and hands each caller its outputs.
-// Failures are returned AND recorded in the backend's sticky status (x265amd_provider_status).
+//   * the launch service (round 5, cfg.launchers > 0): worker threads only POST requests (the PU's
+//     source block and its job descriptors are copied into a per-thread request slot) and continue;
+//     `launchers` service threads each take EVERY queued request of every worker, stage them in one
+//     pinned buffer, and run one upload + one launch of the f2 kernel (one batch per PU size) + one
+//     download on their own stream, then publish the outputs and wake the waiters.  So a worker never
+//     makes a HIP call on the search path (no launch / copy / event cost on the encoder's cores, no
+//     contention of 16 workers' streams for the 4 hardware queues), and the searches of all workers
+//     that are in flight at once share one launch.  With two launchers one batch gathers while the
+//     other is on the device.
+//   * without launchers (cfg.launchers == 0, the round-4 form): per host thread a non-blocking
+//     stream, pinned staging and device scratch; x265amd_mes_search is synchronous on it.
+// Failures are returned AND recorded in the backend's sticky status (x265amd_provider_status),
+// except the capacity limits (pictures, tables, threads, request slots: ENOMEM), after which the
+// caller searches that PU on the host.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include <atomic>
 #include <condition_variable>
 #include <mutex>
 #include <new>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -56,6 +63,16 @@ int record(int st)
         if (st_) return record(st_);                   \
     } while (0)
 
+double now_s()
+{
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return ts.tv_sec + 1e-9 * ts.tv_nsec;
+}
+
+constexpr int kSlots = 8;          // outstanding requests per host thread (tickets 0..7)
+constexpr int kMaxJobs = 64;       // searches per request
+
 } // namespace
 
 struct x265amd_mes_stage
@@ -65,15 +82,41 @@ struct x265amd_mes_stage
     size_t cap = 0;
 };
 
+// one posted request: a copy of the PU's source block (packed, stride w) and its jobs
+struct x265amd_mes_req
+{
+    int w = 0, h = 0, n = 0;
+    uint8_t* fenc = nullptr;                 // 64 * 64 * pix bytes
+    x265amd_mes_job jobs[kMaxJobs];
+    std::atomic<int> state{ 0 };             // 0 free, 1 queued / on the device, 2 done
+    bool dropped = false;                    // the poster no longer wants it (free once done)
+    int rc = 0;
+    double t_post = 0;
+};
+
 struct x265amd_mes_thread
 {
     hipStream_t st = nullptr;
-    hipStream_t ast = nullptr;  // the outstanding x265amd_mes_submit's stream (never waited on by _search / _ref)
+    hipStream_t ast = nullptr;  // the outstanding x265amd_mes_submit's stream (legacy form)
     hipEvent_t ev = nullptr;    // blocking-sync event: the waiting worker sleeps (X265AMD_MES_SYNC=spin: spin)
-    hipEvent_t aev = nullptr;   // completion of the outstanding x265amd_mes_submit
+    hipEvent_t aev = nullptr;   // completion of the outstanding legacy x265amd_mes_submit
     x265amd_mes_stage sync, async;
     int pending = 0;            // jobs of the outstanding submit (0: none)
     size_t pend_out = 0;        // its output offset in the async staging
+    int pend_ticket = -1;       // service form: the ticket of the outstanding x265amd_mes_submit
+    x265amd_mes_req req[kSlots];
+};
+
+constexpr int kSizes = 8;          // PU sizes whose evaluations one launch counts separately
+
+struct x265amd_mes_launcher
+{
+    hipStream_t st = nullptr;
+    hipEvent_t done = nullptr, k0 = nullptr, k1 = nullptr;
+    x265amd_mes_stage g;
+    uint64_t* evals_dev = nullptr;   // [kSizes][2] evaluation counters of the launch in flight
+    uint64_t* evals_host = nullptr;
+    std::thread th;
 };
 
 struct x265amd_mes
@@ -101,7 +144,7 @@ struct x265amd_mes
     std::vector<x265amd_mes_thread*> threads;
     std::atomic<int> next_slot{ 0 };
 
-    // coalesced x265amd_mes_search requests (one per calling thread at a time)
+    // legacy coalescing of synchronous x265amd_mes_search calls (X265AMD_MES_COALESCE=1, no launchers)
     struct Request
     {
         int w, h;
@@ -116,6 +159,20 @@ struct x265amd_mes
     std::condition_variable ccv;
     std::vector<Request*> queue;
     bool busy = false;
+
+    // launch service
+    std::vector<x265amd_mes_launcher*> launchers;
+    std::mutex qmu;                   // guards rq and stop
+    std::condition_variable qcv;      // a request was queued
+    std::vector<x265amd_mes_req*> rq;
+    bool stop = false;
+    std::mutex dmu;                   // waiters sleep on dcv
+    std::condition_variable dcv;
+    int spin_us = 50;
+
+    // statistics (x265amd_mes_stats)
+    std::mutex smu;
+    x265amd_mes_counters st{};
 };
 
 namespace {
@@ -123,6 +180,14 @@ namespace {
 struct TlsEntry { const x265amd_mes* s; uint64_t id; x265amd_mes_thread* t; };
 thread_local std::vector<TlsEntry> tls;
 std::atomic<uint64_t> g_next_id{ 1 };
+
+int use_device(const x265amd_mes* s)
+{
+    int cur = -1;
+    if (hipGetDevice(&cur) != hipSuccess) return X265AMD_ENODEV;
+    if (cur != s->cfg.device && hipSetDevice(s->cfg.device) != hipSuccess) return X265AMD_ENODEV;
+    return 0;
+}
 
 int wait(x265amd_mes_thread* t)
 {
@@ -134,12 +199,12 @@ int wait(x265amd_mes_thread* t)
     return (int)hipStreamSynchronize(t->st);
 }
 
-int reserve(x265amd_mes_thread* t, x265amd_mes_stage& g, size_t bytes)
+int reserve(hipStream_t a, hipStream_t b, x265amd_mes_stage& g, size_t bytes)
 {
     if (bytes <= g.cap) return 0;
     bytes = (bytes + 65535) & ~(size_t)65535;
-    if (t->st) (void)hipStreamSynchronize(t->st);
-    if (t->ast) (void)hipStreamSynchronize(t->ast);
+    if (a) (void)hipStreamSynchronize(a);
+    if (b) (void)hipStreamSynchronize(b);
     (void)hipFree(g.dev);
     (void)hipHostFree(g.host);
     g.dev = g.host = nullptr;
@@ -151,8 +216,28 @@ int reserve(x265amd_mes_thread* t, x265amd_mes_stage& g, size_t bytes)
     return 0;
 }
 
+void free_thread(x265amd_mes_thread* t)
+{
+    if (t->st) (void)hipStreamSynchronize(t->st);
+    if (t->ast) (void)hipStreamSynchronize(t->ast);
+    for (x265amd_mes_stage* g : { &t->sync, &t->async })
+    {
+        (void)hipFree(g->dev);
+        (void)hipHostFree(g->host);
+    }
+    if (t->st) (void)hipStreamDestroy(t->st);
+    if (t->ast) (void)hipStreamDestroy(t->ast);
+    if (t->ev) (void)hipEventDestroy(t->ev);
+    if (t->aev) (void)hipEventDestroy(t->aev);
+    for (auto& r : t->req) free(r.fenc);
+    delete t;
+}
+
+// the calling thread's context; *out stays null and ENOMEM is returned WITHOUT recording it when the
+// session's thread limit is reached (the caller then searches on the host)
 int thread_ctx(x265amd_mes* s, x265amd_mes_thread** out)
 {
+    *out = nullptr;
     for (size_t i = 0; i < tls.size();)
     {
         if (tls[i].s == s && tls[i].id == s->id)
@@ -168,26 +253,48 @@ int thread_ctx(x265amd_mes* s, x265amd_mes_thread** out)
         }
         i++;
     }
+    {
+        std::lock_guard<std::mutex> g(s->mu);
+        if ((int)s->threads.size() >= s->cfg.max_threads) return X265AMD_ENOMEM;
+    }
     auto* t = new (std::nothrow) x265amd_mes_thread();
-    if (!t) return X265AMD_ENOMEM;
+    if (!t) return record(X265AMD_ENOMEM);
+    int rc = 0;
+    if (s->launchers.empty())
+    {
+        const char* sync = getenv("X265AMD_MES_SYNC");
+        const bool spin = sync && !strcmp(sync, "spin");
+        if (hipStreamCreateWithFlags(&t->st, hipStreamNonBlocking) != hipSuccess ||
+            hipStreamCreateWithFlags(&t->ast, hipStreamNonBlocking) != hipSuccess ||
+            reserve(t->st, t->ast, t->sync, 1 << 16) || reserve(t->st, t->ast, t->async, 1 << 16) ||
+            (!spin && hipEventCreateWithFlags(&t->ev, hipEventBlockingSync | hipEventDisableTiming) != hipSuccess) ||
+            hipEventCreateWithFlags(&t->aev, (spin ? 0 : hipEventBlockingSync) | hipEventDisableTiming) != hipSuccess)
+            rc = X265AMD_ENOMEM;
+    }
+    else
+    {
+        // the worker thread itself makes no HIP call on the search path: only the reference-row uploads
+        // (x265amd_mes_ref / _table) use this stream
+        if (hipStreamCreateWithFlags(&t->st, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&t->ev, hipEventBlockingSync | hipEventDisableTiming) != hipSuccess)
+            rc = X265AMD_ENOMEM;
+        for (auto& r : t->req)
+            if (!rc && !(r.fenc = (uint8_t*)malloc(64 * 64 * s->pix))) rc = X265AMD_ENOMEM;
+    }
+    if (rc)
+    {
+        free_thread(t);
+        return record(rc);
+    }
     {
         std::lock_guard<std::mutex> g(s->mu);
         if ((int)s->threads.size() >= s->cfg.max_threads)
         {
-            delete t;
+            free_thread(t);
             return X265AMD_ENOMEM;
         }
         s->threads.push_back(t);
     }
-    if (hipStreamCreateWithFlags(&t->st, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&t->ast, hipStreamNonBlocking) != hipSuccess || reserve(t, t->sync, 1 << 16) ||
-        reserve(t, t->async, 1 << 16))
-        return X265AMD_ENOMEM;
-    const char* sync = getenv("X265AMD_MES_SYNC");
-    const bool spin = sync && !strcmp(sync, "spin");
-    if ((!spin && hipEventCreateWithFlags(&t->ev, hipEventBlockingSync | hipEventDisableTiming) != hipSuccess) ||
-        hipEventCreateWithFlags(&t->aev, (spin ? 0 : hipEventBlockingSync) | hipEventDisableTiming) != hipSuccess)
-        return X265AMD_ENOMEM;
     tls.push_back({ s, s->id, t });
     *out = t;
     return 0;
@@ -215,6 +322,265 @@ struct Layout
     }
 };
 
+int check_jobs(const x265amd_mes* s, int w, int h, const void* fenc, intptr_t fenc_stride, int n,
+               const x265amd_mes_job* jobs)
+{
+    if (!s || n < 0 || (n && (!jobs || !fenc)) || w < 4 || h < 4 || w > 64 || h > 64 || (w & 3) || (h & 3) ||
+        fenc_stride < w)
+        return X265AMD_EINVAL;
+    for (int i = 0; i < n; i++)
+        if (jobs[i].slot < 0 || jobs[i].slot >= s->next_slot || jobs[i].table < 0 ||
+            jobs[i].table >= s->cfg.max_tables || jobs[i].num_cand < 0 || jobs[i].num_cand > s->cfg.max_cand)
+            return X265AMD_EINVAL;
+    return 0;
+}
+
+// the device batch descriptor of n jobs staged at layout L in g (fenc blocks at stride fstride)
+x265amd_me_batch make_batch(const x265amd_mes* s, const x265amd_mes_stage& g, const Layout& L, int w, int h, int n,
+                            intptr_t fstride)
+{
+    x265amd_me_batch b;
+    memset(&b, 0, sizeof(b));
+    b.w = w;
+    b.h = h;
+    b.n = n;
+    b.method = s->cfg.method;
+    b.subme = s->cfg.subme;
+    b.merange = s->cfg.merange;
+    b.max_cand = s->cfg.max_cand > 0 ? s->cfg.max_cand : 1;
+    b.fenc = g.dev + L.fenc;
+    b.fenc_stride = fstride;
+    b.fenc_off = (const int64_t*)(g.dev + L.fenc_off);
+    b.ref = s->arena;
+    b.ref_stride = s->cfg.stride;
+    b.ref_off = (const int64_t*)(g.dev + L.ref_off);
+    b.mv_range = (const int16_t*)(g.dev + L.range);
+    b.mvp = (const int16_t*)(g.dev + L.mvp);
+    b.mvc = (const int16_t*)(g.dev + L.mvc);
+    b.num_cand = g.dev + L.ncand;
+    b.mvcost = s->tables;
+    b.mvcost_off = (const int64_t*)(g.dev + L.cost_off);
+    b.out_mv = (int16_t*)(g.dev + L.out_mv);
+    b.out_cost = (int32_t*)(g.dev + L.out_cost);
+    return b;
+}
+
+// job i's descriptors into the host staging of layout L (source block at element offset foff)
+void stage_job(const x265amd_mes* s, uint8_t* H, const Layout& L, int i, const x265amd_mes_job& j, int64_t foff)
+{
+    const int maxc = s->cfg.max_cand > 0 ? s->cfg.max_cand : 1;
+    ((int64_t*)(H + L.fenc_off))[i] = foff;
+    ((int64_t*)(H + L.ref_off))[i] = (int64_t)j.slot * s->cfg.plane_elems + s->cfg.org_offset + j.block_off;
+    memcpy((int16_t*)(H + L.range) + 4 * i, j.mv_range, 8);
+    memcpy((int16_t*)(H + L.mvp) + 2 * i, j.mvp, 4);
+    memcpy((int16_t*)(H + L.mvc) + 2 * (size_t)maxc * i, j.mvc, 4 * (size_t)j.num_cand);
+    (H + L.ncand)[i] = (uint8_t)j.num_cand;
+    ((int64_t*)(H + L.cost_off))[i] = (int64_t)j.table * (int64_t)s->table_elems + s->cfg.mvcost_range;
+}
+
+// outputs of n jobs staged at layout L (host copy after the download)
+void read_out(const uint8_t* H, const Layout& L, int i, x265amd_mes_job& j)
+{
+    j.out_mv[0] = ((const int16_t*)(H + L.out_mv))[2 * i];
+    j.out_mv[1] = ((const int16_t*)(H + L.out_mv))[2 * i + 1];
+    j.out_cost = ((const int32_t*)(H + L.out_cost))[i];
+}
+
+// ---------------------------------------------------------------- launch service
+// one service thread: take every queued request, one staged batch per PU size, one upload, one launch
+// (all sizes), one download, publish
+void launcher_main(x265amd_mes* s, x265amd_mes_launcher* L)
+{
+    (void)hipSetDevice(s->cfg.device);
+    std::vector<x265amd_mes_req*> take;
+    std::vector<x265amd_mes_req*> order;
+    std::vector<Layout> lay;
+    std::vector<x265amd_me_batch> bt;
+    std::vector<size_t> base;
+    for (;;)
+    {
+        {
+            std::unique_lock<std::mutex> lk(s->qmu);
+            s->qcv.wait(lk, [&] { return s->stop || !s->rq.empty(); });
+            if (s->rq.empty()) return;                 // stop requested and nothing left
+            take.swap(s->rq);
+            s->rq.clear();
+        }
+        const double t_take = now_s();
+        // group by PU size, keeping the posting order inside a size
+        order.clear();
+        std::vector<std::pair<int, int>> sizes;
+        for (auto* r : take)
+        {
+            bool seen = false;
+            for (auto& z : sizes) seen |= z.first == r->w && z.second == r->h;
+            if (!seen) sizes.push_back({ r->w, r->h });
+        }
+        lay.clear();
+        bt.clear();
+        base.clear();
+        size_t total = 0;
+        const int maxc = s->cfg.max_cand > 0 ? s->cfg.max_cand : 1;
+        for (auto& z : sizes)
+        {
+            int n = 0, np = 0;
+            for (auto* r : take)
+                if (r->w == z.first && r->h == z.second) { n += r->n; np++; }
+            lay.emplace_back(n, np * z.second, (int)s->pix, maxc, z.first);
+            base.push_back(total);
+            total += lay.back().end;
+        }
+        int rc = reserve(L->st, nullptr, L->g, total);
+        int njobs = 0;
+        if (!rc)
+        {
+            for (size_t k = 0; k < sizes.size(); k++)
+            {
+                const int w = sizes[k].first, h = sizes[k].second;
+                uint8_t* H = L->g.host + base[k];
+                const Layout& Ly = lay[k];
+                int i = 0, p = 0;
+                for (auto* r : take)
+                {
+                    if (r->w != w || r->h != h) continue;
+                    memcpy(H + Ly.fenc + (size_t)p * w * h * s->pix, r->fenc, (size_t)w * h * s->pix);
+                    for (int q = 0; q < r->n; q++, i++)
+                        stage_job(s, H, Ly, i, r->jobs[q], (int64_t)p * w * h);
+                    order.push_back(r);
+                    p++;
+                }
+                x265amd_mes_stage sub{ L->g.dev + base[k], L->g.host + base[k], Ly.end };
+                bt.push_back(make_batch(s, sub, Ly, w, h, i, w));
+                if (k < (size_t)kSizes) bt.back().eval_count = L->evals_dev + 2 * k;
+                njobs += i;
+            }
+            rc = (int)hipMemsetAsync(L->evals_dev, 0, sizeof(uint64_t) * 2 * kSizes, L->st);
+            // one upload of every size's inputs (the output regions ride along: staging is contiguous)
+            if (!rc) rc = (int)hipMemcpyAsync(L->g.dev, L->g.host, total, hipMemcpyHostToDevice, L->st);
+            if (!rc) rc = (int)hipEventRecord(L->k0, L->st);
+            if (!rc) rc = x265amd_motion_search(s->cfg.depth, (int)bt.size(), bt.data(), L->st);
+            if (!rc) rc = (int)hipEventRecord(L->k1, L->st);
+            for (size_t k = 0; k < sizes.size() && !rc; k++)
+                rc = (int)hipMemcpyAsync(L->g.host + base[k] + lay[k].out_mv, L->g.dev + base[k] + lay[k].out_mv,
+                                         lay[k].end - lay[k].out_mv, hipMemcpyDeviceToHost, L->st);
+            if (!rc) rc = (int)hipMemcpyAsync(L->evals_host, L->evals_dev, sizeof(uint64_t) * 2 * kSizes,
+                                              hipMemcpyDeviceToHost, L->st);
+            if (!rc) rc = (int)hipEventRecord(L->done, L->st);
+            if (!rc) rc = (int)hipEventSynchronize(L->done);
+        }
+        // algorithmic bytes of the launch: per full-pel evaluation the PU and its reference
+        // block (2 W H b), per sub-pel evaluation the PU and the reference window of the 8-tap filters
+        // ((W + 7) (H + 7) b + W H b)
+        double algo = 0;
+        int64_t efp = 0, esp = 0;
+        if (!rc)
+            for (size_t k = 0; k < sizes.size() && k < (size_t)kSizes; k++)
+            {
+                const double w = sizes[k].first, h = sizes[k].second, b = (double)s->pix;
+                efp += (int64_t)L->evals_host[2 * k];
+                esp += (int64_t)L->evals_host[2 * k + 1];
+                algo += L->evals_host[2 * k] * 2 * w * h * b + L->evals_host[2 * k + 1] * ((w + 7) * (h + 7) + w * h) * b;
+            }
+        float kms = 0;
+        if (!rc) (void)hipEventElapsedTime(&kms, L->k0, L->k1);
+        const double t_done = now_s();
+        // publish: the outputs into each request, then wake the waiters
+        if (!rc)
+            for (size_t k = 0; k < sizes.size(); k++)
+            {
+                const int w = sizes[k].first, h = sizes[k].second;
+                const uint8_t* H = L->g.host + base[k];
+                int i = 0;
+                for (auto* r : take)
+                {
+                    if (r->w != w || r->h != h) continue;
+                    for (int q = 0; q < r->n; q++, i++) read_out(H, lay[k], i, r->jobs[q]);
+                }
+            }
+        double qdelay = 0;
+        for (auto* r : take)
+        {
+            qdelay += t_take - r->t_post;
+            r->rc = rc;
+            r->state.store(2, std::memory_order_release);
+        }
+        {
+            std::lock_guard<std::mutex> g(s->dmu);
+        }
+        s->dcv.notify_all();
+        if (rc) record(rc);
+        {
+            std::lock_guard<std::mutex> g(s->smu);
+            s->st.batches++;
+            s->st.requests += (int64_t)take.size();
+            s->st.jobs += njobs;
+            s->st.kernel_ms += kms;
+            s->st.evals_fpel += efp;
+            s->st.evals_subpel += esp;
+            s->st.algo_bytes += algo;
+            if (kms > s->st.kernel_ms_max) s->st.kernel_ms_max = kms;
+            s->st.batch_ms += 1e3 * (t_done - t_take);
+            s->st.queue_ms += 1e3 * qdelay;
+            if ((int64_t)take.size() > s->st.max_requests_per_batch) s->st.max_requests_per_batch = (int64_t)take.size();
+        }
+        take.clear();
+    }
+}
+
+int start_service(x265amd_mes* s)
+{
+    const int n = s->cfg.launchers;
+    if (const char* e = getenv("X265AMD_MES_SPIN_US")) s->spin_us = atoi(e);
+    for (int i = 0; i < n; i++)
+    {
+        auto* L = new (std::nothrow) x265amd_mes_launcher();
+        if (!L) return X265AMD_ENOMEM;
+        s->launchers.push_back(L);
+        if (hipStreamCreateWithFlags(&L->st, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&L->done, hipEventBlockingSync | hipEventDisableTiming) != hipSuccess ||
+            hipEventCreate(&L->k0) != hipSuccess || hipEventCreate(&L->k1) != hipSuccess ||
+            hipMalloc((void**)&L->evals_dev, sizeof(uint64_t) * 2 * kSizes) != hipSuccess ||
+            hipHostMalloc((void**)&L->evals_host, sizeof(uint64_t) * 2 * kSizes, hipHostMallocDefault) != hipSuccess ||
+            reserve(L->st, nullptr, L->g, 1 << 20))
+            return X265AMD_ENOMEM;
+    }
+    for (auto* L : s->launchers)
+    {
+        try
+        {
+            L->th = std::thread(launcher_main, s, L);
+        }
+        catch (...)
+        {
+            return X265AMD_ENOMEM;
+        }
+    }
+    return 0;
+}
+
+void stop_service(x265amd_mes* s)
+{
+    {
+        std::lock_guard<std::mutex> g(s->qmu);
+        s->stop = true;
+    }
+    s->qcv.notify_all();
+    for (auto* L : s->launchers)
+    {
+        if (L->th.joinable()) L->th.join();
+        if (L->st) (void)hipStreamSynchronize(L->st);
+        (void)hipFree(L->g.dev);
+        (void)hipHostFree(L->g.host);
+        (void)hipFree(L->evals_dev);
+        (void)hipHostFree(L->evals_host);
+        if (L->st) (void)hipStreamDestroy(L->st);
+        for (hipEvent_t e : { L->done, L->k0, L->k1 })
+            if (e) (void)hipEventDestroy(e);
+        delete L;
+    }
+    s->launchers.clear();
+}
+
 } // namespace
 
 extern "C" int x265amd_mes_create(const x265amd_mes_config* cfg, x265amd_mes** out)
@@ -226,9 +592,11 @@ extern "C" int x265amd_mes_create(const x265amd_mes_config* cfg, x265amd_mes** o
         cfg->margin_y < 0 || cfg->ctu_rows <= 0 || cfg->ctu_size <= 0 || cfg->max_pictures <= 0 ||
         cfg->max_threads <= 0 || cfg->max_tables <= 0 || cfg->mvcost_range <= 0 || cfg->method < 0 ||
         cfg->method > 4 || cfg->subme < 0 || cfg->subme > 7 || cfg->merange < 1 || cfg->max_cand < 0 ||
-        cfg->max_cand > 16 || (int64_t)cfg->margin_y * 2 + (int64_t)cfg->ctu_rows * cfg->ctu_size >
-                                  cfg->plane_elems / cfg->stride)
+        cfg->max_cand > 16 || cfg->device < 0 || cfg->launchers < 0 || cfg->launchers > 8 ||
+        (int64_t)cfg->margin_y * 2 + (int64_t)cfg->ctu_rows * cfg->ctu_size > cfg->plane_elems / cfg->stride)
         return X265AMD_EINVAL;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || cfg->device >= ndev) return X265AMD_EINVAL;
     auto* s = new (std::nothrow) x265amd_mes();
     if (!s) return record(X265AMD_ENOMEM);
     s->cfg = *cfg;
@@ -237,11 +605,15 @@ extern "C" int x265amd_mes_create(const x265amd_mes_config* cfg, x265amd_mes** o
     s->rows = cfg->plane_elems / cfg->stride;
     s->plane_bytes = (size_t)cfg->plane_elems * s->pix;
     s->table_elems = 2 * (size_t)cfg->mvcost_range + 1;
-    if (hipMalloc((void**)&s->arena, s->plane_bytes * cfg->max_pictures) != hipSuccess ||
-        hipMalloc((void**)&s->tables, sizeof(uint16_t) * s->table_elems * cfg->max_tables) != hipSuccess)
+    int rc = use_device(s);
+    if (!rc && (hipMalloc((void**)&s->arena, s->plane_bytes * cfg->max_pictures) != hipSuccess ||
+                hipMalloc((void**)&s->tables, sizeof(uint16_t) * s->table_elems * cfg->max_tables) != hipSuccess))
+        rc = X265AMD_ENOMEM;
+    if (!rc && cfg->launchers) rc = start_service(s);
+    if (rc)
     {
         x265amd_mes_destroy(s);
-        return record(X265AMD_ENOMEM);
+        return record(rc);
     }
     *out = s;
     return 0;
@@ -250,21 +622,9 @@ extern "C" int x265amd_mes_create(const x265amd_mes_config* cfg, x265amd_mes** o
 extern "C" void x265amd_mes_destroy(x265amd_mes* s)
 {
     if (!s) return;
-    for (auto* t : s->threads)
-    {
-        if (t->st) (void)hipStreamSynchronize(t->st);
-        for (x265amd_mes_stage* g : { &t->sync, &t->async })
-        {
-            (void)hipFree(g->dev);
-            (void)hipHostFree(g->host);
-        }
-        if (t->ast) (void)hipStreamSynchronize(t->ast);
-        if (t->st) (void)hipStreamDestroy(t->st);
-        if (t->ast) (void)hipStreamDestroy(t->ast);
-        if (t->ev) (void)hipEventDestroy(t->ev);
-        if (t->aev) (void)hipEventDestroy(t->aev);
-        delete t;
-    }
+    (void)use_device(s);
+    stop_service(s);
+    for (auto* t : s->threads) free_thread(t);
     for (auto& p : s->pics)
     {
         if (p.second->pinned) (void)hipHostUnregister((void*)p.second->pinned);
@@ -280,8 +640,9 @@ extern "C" int x265amd_mes_ref(x265amd_mes* s, const void* key, int64_t gen, con
 {
     if (!s || !key || !plane_buf || !slot || rows_final < 0 || rows_final > s->cfg.ctu_rows)
         return record(X265AMD_EINVAL);
+    MES_TRY(use_device(s));
     x265amd_mes_thread* t;
-    MES_TRY(thread_ctx(s, &t));
+    if (int rc = thread_ctx(s, &t)) return rc;
     x265amd_mes::Picture* p;
     {
         std::lock_guard<std::mutex> g(s->mu);
@@ -322,20 +683,42 @@ extern "C" int x265amd_mes_ref(x265amd_mes* s, const void* key, int64_t gen, con
         const int64_t r1 = rows_final == s->cfg.ctu_rows ? s->rows
                                                          : s->cfg.margin_y + (int64_t)rows_final * s->cfg.ctu_size;
         const size_t off = (size_t)(r0 * s->cfg.stride) * s->pix, bytes = (size_t)((r1 - r0) * s->cfg.stride) * s->pix;
+        const double t0 = now_s();
         MES_TRY(hipMemcpyAsync(s->arena + (size_t)p->slot * s->plane_bytes + off, (const uint8_t*)plane_buf + off, bytes,
                                hipMemcpyHostToDevice, t->st));
         MES_TRY(wait(t));
         p->rows_up = rows_final;
+        std::lock_guard<std::mutex> sg(s->smu);
+        s->st.uploads++;
+        s->st.upload_bytes += (int64_t)bytes;
+        s->st.upload_ms += 1e3 * (now_s() - t0);
     }
     *slot = p->slot;
+    return 0;
+}
+
+extern "C" int x265amd_mes_rows(x265amd_mes* s, const void* key, int64_t gen, int* rows_resident)
+{
+    if (!s || !key || !rows_resident) return record(X265AMD_EINVAL);
+    *rows_resident = 0;
+    x265amd_mes::Picture* p = nullptr;
+    {
+        std::lock_guard<std::mutex> g(s->mu);
+        auto it = s->pics.find(key);
+        if (it != s->pics.end()) p = it->second;
+    }
+    if (!p) return 0;
+    std::lock_guard<std::mutex> g(p->mu);
+    *rows_resident = p->gen == gen ? p->rows_up : 0;
     return 0;
 }
 
 extern "C" int x265amd_mes_table(x265amd_mes* s, const uint16_t* centre, int* index)
 {
     if (!s || !centre || !index) return record(X265AMD_EINVAL);
+    MES_TRY(use_device(s));
     x265amd_mes_thread* t;
-    MES_TRY(thread_ctx(s, &t));
+    if (int rc = thread_ctx(s, &t)) return rc;
     std::lock_guard<std::mutex> g(s->mu);
     auto it = s->tabs.find(centre);
     if (it != s->tabs.end())
@@ -354,6 +737,106 @@ extern "C" int x265amd_mes_table(x265amd_mes* s, const uint16_t* centre, int* in
     return 0;
 }
 
+// ---------------------------------------------------------------- service entries
+extern "C" int x265amd_mes_post(x265amd_mes* s, int w, int h, const void* fenc, intptr_t fenc_stride, int n,
+                                const x265amd_mes_job* jobs, int* ticket)
+{
+    if (!s || !ticket) return record(X265AMD_EINVAL);
+    *ticket = -1;
+    if (s->launchers.empty() || n <= 0) return record(X265AMD_EINVAL);
+    if (n > kMaxJobs) return X265AMD_ENOMEM;               // more than a slot holds: search on the host
+    MES_TRY(check_jobs(s, w, h, fenc, fenc_stride, n, jobs));
+    x265amd_mes_thread* t;
+    if (int rc = thread_ctx(s, &t)) return rc;
+    int k = -1;
+    for (int i = 0; i < kSlots && k < 0; i++)
+    {
+        const int stt = t->req[i].state.load(std::memory_order_acquire);
+        if (stt == 0 || (stt == 2 && t->req[i].dropped)) k = i;
+    }
+    if (k < 0) return X265AMD_ENOMEM;                     // every slot outstanding: search on the host
+    x265amd_mes_req& r = t->req[k];
+    r.w = w;
+    r.h = h;
+    r.n = n;
+    r.dropped = false;
+    r.rc = 0;
+    for (int y = 0; y < h; y++)
+        memcpy(r.fenc + (size_t)y * w * s->pix, (const uint8_t*)fenc + (size_t)y * fenc_stride * s->pix, (size_t)w * s->pix);
+    memcpy(r.jobs, jobs, sizeof(x265amd_mes_job) * n);
+    r.t_post = now_s();
+    r.state.store(1, std::memory_order_relaxed);
+    {
+        std::lock_guard<std::mutex> g(s->qmu);
+        s->rq.push_back(&r);
+    }
+    s->qcv.notify_one();
+    *ticket = k;
+    return 0;
+}
+
+extern "C" int x265amd_mes_wait(x265amd_mes* s, int ticket, int n, x265amd_mes_job* jobs)
+{
+    if (!s || ticket < 0 || ticket >= kSlots || n < 0 || (n && !jobs)) return record(X265AMD_EINVAL);
+    x265amd_mes_thread* t;
+    MES_TRY(thread_ctx(s, &t));
+    x265amd_mes_req& r = t->req[ticket];
+    if (r.state.load(std::memory_order_acquire) == 0 || r.dropped || r.n != n) return record(X265AMD_EINVAL);
+    const double t0 = now_s();
+    bool slept = false;
+    if (r.state.load(std::memory_order_acquire) != 2)
+    {
+        // spin briefly (a batch ends within tens of microseconds of its neighbours), then sleep
+        const double until = t0 + 1e-6 * s->spin_us;
+        while (r.state.load(std::memory_order_acquire) != 2 && now_s() < until)
+            __builtin_ia32_pause();
+        if (r.state.load(std::memory_order_acquire) != 2)
+        {
+            slept = true;
+            std::unique_lock<std::mutex> lk(s->dmu);
+            s->dcv.wait(lk, [&] { return r.state.load(std::memory_order_acquire) == 2; });
+        }
+    }
+    const double dt = now_s() - t0;
+    for (int i = 0; i < n; i++)
+    {
+        jobs[i].out_mv[0] = r.jobs[i].out_mv[0];
+        jobs[i].out_mv[1] = r.jobs[i].out_mv[1];
+        jobs[i].out_cost = r.jobs[i].out_cost;
+    }
+    const int rc = r.rc;
+    r.state.store(0, std::memory_order_release);
+    {
+        std::lock_guard<std::mutex> g(s->smu);
+        s->st.waits++;
+        s->st.wait_ms += 1e3 * dt;
+        s->st.waits_blocked += slept;
+    }
+    return rc ? record(rc) : 0;
+}
+
+extern "C" int x265amd_mes_drop(x265amd_mes* s, int ticket)
+{
+    if (!s || ticket < 0 || ticket >= kSlots) return record(X265AMD_EINVAL);
+    x265amd_mes_thread* t;
+    MES_TRY(thread_ctx(s, &t));
+    x265amd_mes_req& r = t->req[ticket];
+    if (r.state.load(std::memory_order_acquire) == 0) return 0;
+    r.dropped = true;                                      // the slot is reused once the launcher is done
+    std::lock_guard<std::mutex> g(s->smu);
+    s->st.dropped++;
+    return 0;
+}
+
+extern "C" int x265amd_mes_stats(x265amd_mes* s, x265amd_mes_counters* out)
+{
+    if (!s || !out) return X265AMD_EINVAL;
+    std::lock_guard<std::mutex> g(s->smu);
+    *out = s->st;
+    return 0;
+}
+
+// ---------------------------------------------------------------- legacy (per-thread) form
 namespace {
 
 // stage a batch of one PU's searches in g and enqueue upload, launch and download on the thread's
@@ -361,59 +844,15 @@ namespace {
 int enqueue(x265amd_mes* s, x265amd_mes_thread* t, x265amd_mes_stage& g, hipStream_t st, int w, int h,
             const void* fenc, intptr_t fenc_stride, int n, const x265amd_mes_job* jobs, size_t* out)
 {
-    if (!s || n < 0 || (n && (!jobs || !fenc)) || w < 4 || h < 4 || w > 64 || h > 64 || fenc_stride < w)
-        return X265AMD_EINVAL;
+    if (int rc = check_jobs(s, w, h, fenc, fenc_stride, n, jobs)) return rc;
     const int maxc = s->cfg.max_cand > 0 ? s->cfg.max_cand : 1;
-    for (int i = 0; i < n; i++)
-        if (jobs[i].slot < 0 || jobs[i].slot >= s->next_slot || jobs[i].table < 0 ||
-            jobs[i].table >= s->cfg.max_tables || jobs[i].num_cand < 0 || jobs[i].num_cand > s->cfg.max_cand)
-            return X265AMD_EINVAL;
     const Layout L(n, h, (int)s->pix, maxc, fenc_stride);
-    if (int rc = reserve(t, g, L.end)) return rc;
+    if (int rc = reserve(t->st, t->ast, g, L.end)) return rc;
     uint8_t* H = g.host;
     memcpy(H + L.fenc, fenc, (size_t)fenc_stride * h * s->pix);
-    int64_t* foff = (int64_t*)(H + L.fenc_off);
-    int64_t* roff = (int64_t*)(H + L.ref_off);
-    int16_t* rng = (int16_t*)(H + L.range);
-    int16_t* mvp = (int16_t*)(H + L.mvp);
-    int16_t* mvc = (int16_t*)(H + L.mvc);
-    uint8_t* nc = H + L.ncand;
-    int64_t* coff = (int64_t*)(H + L.cost_off);
-    for (int i = 0; i < n; i++)
-    {
-        const x265amd_mes_job& j = jobs[i];
-        foff[i] = 0;
-        roff[i] = (int64_t)j.slot * s->cfg.plane_elems + s->cfg.org_offset + j.block_off;
-        memcpy(rng + 4 * i, j.mv_range, 8);
-        memcpy(mvp + 2 * i, j.mvp, 4);
-        memcpy(mvc + 2 * (size_t)maxc * i, j.mvc, 4 * (size_t)j.num_cand);
-        nc[i] = (uint8_t)j.num_cand;
-        coff[i] = (int64_t)j.table * (int64_t)s->table_elems + s->cfg.mvcost_range;
-    }
+    for (int i = 0; i < n; i++) stage_job(s, H, L, i, jobs[i], 0);
     if (hipError_t e = hipMemcpyAsync(g.dev, H, L.out_mv, hipMemcpyHostToDevice, st)) return (int)e;
-    x265amd_me_batch b;
-    memset(&b, 0, sizeof(b));
-    b.w = w;
-    b.h = h;
-    b.n = n;
-    b.method = s->cfg.method;
-    b.subme = s->cfg.subme;
-    b.merange = s->cfg.merange;
-    b.max_cand = maxc;
-    b.fenc = g.dev + L.fenc;
-    b.fenc_stride = fenc_stride;
-    b.fenc_off = (const int64_t*)(g.dev + L.fenc_off);
-    b.ref = s->arena;
-    b.ref_stride = s->cfg.stride;
-    b.ref_off = (const int64_t*)(g.dev + L.ref_off);
-    b.mv_range = (const int16_t*)(g.dev + L.range);
-    b.mvp = (const int16_t*)(g.dev + L.mvp);
-    b.mvc = (const int16_t*)(g.dev + L.mvc);
-    b.num_cand = g.dev + L.ncand;
-    b.mvcost = s->tables;
-    b.mvcost_off = (const int64_t*)(g.dev + L.cost_off);
-    b.out_mv = (int16_t*)(g.dev + L.out_mv);
-    b.out_cost = (int32_t*)(g.dev + L.out_cost);
+    const x265amd_me_batch b = make_batch(s, g, L, w, h, n, fenc_stride);
     if (int rc = x265amd_motion_search(s->cfg.depth, 1, &b, st)) return rc;
     if (hipError_t e = hipMemcpyAsync(H + L.out_mv, g.dev + L.out_mv, L.end - L.out_mv, hipMemcpyDeviceToHost, st))
         return (int)e;
@@ -433,7 +872,6 @@ void unpack(const x265amd_mes_stage& g, size_t out, int n, x265amd_mes_job* jobs
     }
 }
 
-// ---- coalescing (X265AMD_MES_COALESCE=1)
 bool coalescing()
 {
     static int v = -1;
@@ -445,19 +883,7 @@ bool coalescing()
     return v != 0;
 }
 
-int check_request(const x265amd_mes* s, int w, int h, const void* fenc, intptr_t fenc_stride, int n,
-                  const x265amd_mes_job* jobs)
-{
-    if (!s || n < 0 || (n && (!jobs || !fenc)) || w < 4 || h < 4 || w > 64 || h > 64 || fenc_stride < w)
-        return X265AMD_EINVAL;
-    for (int i = 0; i < n; i++)
-        if (jobs[i].slot < 0 || jobs[i].slot >= s->next_slot || jobs[i].table < 0 ||
-            jobs[i].table >= s->cfg.max_tables || jobs[i].num_cand < 0 || jobs[i].num_cand > s->cfg.max_cand)
-            return X265AMD_EINVAL;
-    return 0;
-}
-
-// stage the searches of several PUs of one size (requests checked by check_request) in g — their source
+// stage the searches of several PUs of one size (requests checked by check_jobs) in g — their source
 // blocks packed at stride w, one after another, jobs in request order — and enqueue upload, launch and
 // download on `st`; *out = the outputs' offset in g.host
 int enqueue_requests(x265amd_mes* s, x265amd_mes_thread* t, x265amd_mes_stage& g, hipStream_t st, int w, int h,
@@ -469,15 +895,8 @@ int enqueue_requests(x265amd_mes* s, x265amd_mes_thread* t, x265amd_mes_stage& g
     for (auto* r : reqs) n += r->n;
     const size_t blk = (size_t)w * h;                         // elements per packed source block
     const Layout L(n, np * h, (int)s->pix, maxc, w);
-    if (int rc = reserve(t, g, L.end)) return rc;
+    if (int rc = reserve(t->st, t->ast, g, L.end)) return rc;
     uint8_t* H = g.host;
-    int64_t* foff = (int64_t*)(H + L.fenc_off);
-    int64_t* roff = (int64_t*)(H + L.ref_off);
-    int16_t* rng = (int16_t*)(H + L.range);
-    int16_t* mvp = (int16_t*)(H + L.mvp);
-    int16_t* mvc = (int16_t*)(H + L.mvc);
-    uint8_t* nc = H + L.ncand;
-    int64_t* coff = (int64_t*)(H + L.cost_off);
     int i = 0;
     for (int k = 0; k < np; k++)
     {
@@ -485,42 +904,10 @@ int enqueue_requests(x265amd_mes* s, x265amd_mes_thread* t, x265amd_mes_stage& g
         for (int y = 0; y < h; y++)
             memcpy(H + L.fenc + (k * blk + (size_t)y * w) * s->pix,
                    (const uint8_t*)r.fenc + (size_t)y * r.fenc_stride * s->pix, (size_t)w * s->pix);
-        for (int q = 0; q < r.n; q++, i++)
-        {
-            const x265amd_mes_job& j = r.jobs[q];
-            foff[i] = (int64_t)(k * blk);
-            roff[i] = (int64_t)j.slot * s->cfg.plane_elems + s->cfg.org_offset + j.block_off;
-            memcpy(rng + 4 * i, j.mv_range, 8);
-            memcpy(mvp + 2 * i, j.mvp, 4);
-            memcpy(mvc + 2 * (size_t)maxc * i, j.mvc, 4 * (size_t)j.num_cand);
-            nc[i] = (uint8_t)j.num_cand;
-            coff[i] = (int64_t)j.table * (int64_t)s->table_elems + s->cfg.mvcost_range;
-        }
+        for (int q = 0; q < r.n; q++, i++) stage_job(s, H, L, i, r.jobs[q], (int64_t)(k * blk));
     }
     if (hipError_t e = hipMemcpyAsync(g.dev, H, L.out_mv, hipMemcpyHostToDevice, st)) return (int)e;
-    x265amd_me_batch b;
-    memset(&b, 0, sizeof(b));
-    b.w = w;
-    b.h = h;
-    b.n = n;
-    b.method = s->cfg.method;
-    b.subme = s->cfg.subme;
-    b.merange = s->cfg.merange;
-    b.max_cand = maxc;
-    b.fenc = g.dev + L.fenc;
-    b.fenc_stride = w;
-    b.fenc_off = (const int64_t*)(g.dev + L.fenc_off);
-    b.ref = s->arena;
-    b.ref_stride = s->cfg.stride;
-    b.ref_off = (const int64_t*)(g.dev + L.ref_off);
-    b.mv_range = (const int16_t*)(g.dev + L.range);
-    b.mvp = (const int16_t*)(g.dev + L.mvp);
-    b.mvc = (const int16_t*)(g.dev + L.mvc);
-    b.num_cand = g.dev + L.ncand;
-    b.mvcost = s->tables;
-    b.mvcost_off = (const int64_t*)(g.dev + L.cost_off);
-    b.out_mv = (int16_t*)(g.dev + L.out_mv);
-    b.out_cost = (int32_t*)(g.dev + L.out_cost);
+    const x265amd_me_batch b = make_batch(s, g, L, w, h, n, w);
     if (int rc = x265amd_motion_search(s->cfg.depth, 1, &b, st)) return rc;
     if (hipError_t e = hipMemcpyAsync(H + L.out_mv, g.dev + L.out_mv, L.end - L.out_mv, hipMemcpyDeviceToHost, st))
         return (int)e;
@@ -578,11 +965,19 @@ extern "C" int x265amd_mes_search(x265amd_mes* s, int w, int h, const void* fenc
 {
     if (!s) return record(X265AMD_EINVAL);
     if (!n) return 0;
+    if (!s->launchers.empty())
+    {
+        // the service form: post and wait (the searches share a launch with whatever else is queued)
+        int ticket = -1;
+        if (int rc = x265amd_mes_post(s, w, h, fenc, fenc_stride, n, jobs, &ticket)) return rc;
+        return x265amd_mes_wait(s, ticket, n, jobs);
+    }
+    MES_TRY(use_device(s));
     x265amd_mes_thread* t;
-    MES_TRY(thread_ctx(s, &t));
+    if (int rc = thread_ctx(s, &t)) return rc;
     if (coalescing())
     {
-        MES_TRY(check_request(s, w, h, fenc, fenc_stride, n, jobs));
+        MES_TRY(check_jobs(s, w, h, fenc, fenc_stride, n, jobs));
         x265amd_mes::Request r = { w, h, fenc, fenc_stride, n, jobs, 0, false };
         std::unique_lock<std::mutex> lk(s->cmu);
         s->queue.push_back(&r);
@@ -604,8 +999,20 @@ extern "C" int x265amd_mes_submit(x265amd_mes* s, int w, int h, const void* fenc
                                   const x265amd_mes_job* jobs)
 {
     if (!s || n <= 0) return record(X265AMD_EINVAL);
+    if (!s->launchers.empty())
+    {
+        x265amd_mes_thread* t;
+        if (int rc = thread_ctx(s, &t)) return rc;
+        if (t->pend_ticket >= 0) return record(X265AMD_EINVAL);   // one outstanding submit per thread
+        int ticket = -1;
+        if (int rc = x265amd_mes_post(s, w, h, fenc, fenc_stride, n, jobs, &ticket)) return rc;
+        t->pend_ticket = ticket;
+        t->pending = n;
+        return 0;
+    }
+    MES_TRY(use_device(s));
     x265amd_mes_thread* t;
-    MES_TRY(thread_ctx(s, &t));
+    if (int rc = thread_ctx(s, &t)) return rc;
     if (t->pending) return record(X265AMD_EINVAL);          // one outstanding submit per thread
     size_t out = 0;
     MES_TRY(enqueue(s, t, t->async, t->ast, w, h, fenc, fenc_stride, n, jobs, &out));
@@ -623,6 +1030,17 @@ extern "C" int x265amd_mes_collect(x265amd_mes* s, int n, x265amd_mes_job* jobs)
     if (!t->pending) return record(X265AMD_EINVAL);
     const int pend = t->pending;
     t->pending = 0;
+    if (!s->launchers.empty())
+    {
+        const int ticket = t->pend_ticket;
+        t->pend_ticket = -1;
+        if (n != pend)
+        {
+            (void)x265amd_mes_drop(s, ticket);
+            return record(X265AMD_EINVAL);
+        }
+        return x265amd_mes_wait(s, ticket, n, jobs);
+    }
     MES_TRY(hipEventSynchronize(t->aev));
     if (n != pend) return record(X265AMD_EINVAL);
     unpack(t->async, t->pend_out, n, jobs);

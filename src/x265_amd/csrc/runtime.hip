@@ -18,6 +18,19 @@ extern "C" const char* x265amd_target(void)
     return "gfx950";
 }
 
+extern "C" int x265amd_device_count(int* count)
+{
+    if (!count) return X265AMD_EINVAL;
+    *count = 0;
+    const hipError_t e = hipGetDeviceCount(count);
+    if (e == hipErrorNoDevice)
+    {
+        *count = 0;
+        return 0;
+    }
+    return (int)e;
+}
+
 extern "C" int x265amd_set_device(int device)
 {
     int count = 0;

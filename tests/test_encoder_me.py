@@ -28,17 +28,24 @@ def _stats(err):
     return dict(zip(("prefetches", "searches", "hits", "misses", "fallbacks", "weighted"), map(int, m.groups())))
 
 
-@pytest.mark.parametrize("size,frames,fade", [((640, 360), 16, 0.0), ((1920, 1080), 6, 0.0), ((640, 360), 24, 0.03)],
-                         ids=["360p", "1080p", "360p-weighted-fade"])
-def test_me_hook_host_prefetch_equals_reference_on_cpu(tmp_path, size, frames, fade):
+@pytest.mark.parametrize("size,frames,fade,min_area", [((640, 360), 16, 0.0, 4096), ((1920, 1080), 6, 0.0, 4096),
+                                                       ((640, 360), 24, 0.03, 4096), ((640, 360), 16, 0.0, 1024),
+                                                       ((1280, 720), 8, 0.0, 1024)],
+                         ids=["360p", "1080p", "360p-weighted-fade", "360p-32x32", "720p-32x32"])
+def test_me_hook_host_prefetch_equals_reference_on_cpu(tmp_path, size, frames, fade, min_area):
+    """X265AMD_ME=host: the hook's CU-start prefetch (64x64 at depth 0, and with X265AMD_ME_MIN=1024 the
+    32x32 CUs at depth 1 through the checkMerge2Nx2N_rd0_4 hook) formed exactly as the reference loop makes
+    its calls — every reference call after a prefetch is found in the memo, and the bitstream is the
+    reference's"""
     w, h = size
     src = _source(tmp_path, w, h, frames, fade=fade)
     rc, ref, _, err = encode(_bin("x265ref8"), src, w, h, frames, tmp_path / "ref.hevc")
     assert rc == 0, err[-2000:]
     rc, got, _, err = encode(_bin("x265la8"), src, w, h, frames, tmp_path / "me.hevc",
-                             {"X265AMD_LOOKAHEAD": "cpu", "X265AMD_ME": "host", "X265AMD_ME_STATS": "1"})
+                             {"X265AMD_LOOKAHEAD": "cpu", "X265AMD_ME": "host", "X265AMD_ME_STATS": "1",
+                              "X265AMD_ME_MIN": str(min_area)})
     assert rc == 0, err[-2000:]
-    assert "[x265me] motion searches of PUs >= 4096 pixels on the CPU (hook prefetch)" in err
+    assert f"[x265me] motion searches of PUs >= {min_area} pixels on the CPU (hook prefetch), prefetched at CU start" in err
     st = _stats(err)
     assert st["prefetches"] > 0 and st["hits"] > 0
     # every search the reference made after a prefetch was one of the prefetched ones, except those on
@@ -46,6 +53,60 @@ def test_me_hook_host_prefetch_equals_reference_on_cpu(tmp_path, size, frames, f
     assert st["misses"] == 0, st
     assert (st["weighted"] > 0) == (fade > 0), st
     assert got == ref, "X265AMD_ME=host: bitstream differs from the reference encoder"
+
+
+def test_me_hook_two_device_sessions_on_cpu(tmp_path):
+    """X265AMD_GPUS=2 (host mode): frame encoder i's searches go to device session i mod 2 — both sessions get
+    searches (frames alternate between the encoder's frame threads, encoder.cpp:649-650) and the bitstream
+    is the reference's"""
+    w, h, n = 640, 360, 16
+    src = _source(tmp_path, w, h, n)
+    rc, ref, _, err = encode(_bin("x265ref8"), src, w, h, n, tmp_path / "ref.hevc")
+    assert rc == 0
+    rc, got, _, err = encode(_bin("x265la8"), src, w, h, n, tmp_path / "me.hevc",
+                             {"X265AMD_LOOKAHEAD": "cpu", "X265AMD_ME": "host", "X265AMD_ME_STATS": "1",
+                              "X265AMD_GPUS": "2"})
+    assert rc == 0, err[-2000:]
+    m = re.search(r"searches per device session: (\d+) (\d+)", err)
+    assert m and int(m.group(1)) > 0 and int(m.group(2)) > 0, err[-2000:]
+    assert _stats(err)["misses"] == 0
+    assert got == ref
+
+
+def _twice(tmp_path, src, w, h, n, env, tag):
+    import subprocess
+
+    outs = [tmp_path / f"{tag}1.hevc", tmp_path / f"{tag}2.hevc"]
+    r = subprocess.run([_bin("x265twice8"), str(src), str(w), str(h), str(n), str(outs[0]), str(outs[1])],
+                       capture_output=True, text=True, timeout=600, env=dict(os.environ, **env))
+    assert r.returncode == 0, r.stderr[-2000:]
+    return [o.read_bytes() for o in outs], r.stderr
+
+
+def test_two_encoders_in_one_process_on_cpu(tmp_path):
+    """two encoders of one geometry opened one after the other in one process (oracle/twice_main.cpp, the
+    x265 API): with the hooks' host forms, both bitstreams equal the hooks-off program's"""
+    w, h, n = 640, 360, 12
+    src = _source(tmp_path, w, h, n)
+    ref, _ = _twice(tmp_path, src, w, h, n, {"X265AMD_LOOKAHEAD": "cpu", "X265AMD_ME": "cpu"}, "ref")
+    assert ref[0] == ref[1]
+    got, _ = _twice(tmp_path, src, w, h, n, {"X265AMD_LOOKAHEAD": "cpu", "X265AMD_ME": "host"}, "host")
+    assert got[0] == ref[0] and got[1] == ref[0]
+
+
+@pytest.mark.gpu
+def test_gpu_two_encoders_in_one_process_are_bit_exact(tmp_path):
+    """the second encoder reuses freed PicYuv / Lowres addresses with the same POCs; the
+    binding's teardown after x265_encoder_close (x265amd_me_encoder_closed / x265amd_la_encoder_closed)
+    drops the first encoder's device sessions, so the second encode's device searches and estimates see
+    only its own pictures — both bitstreams equal the hooks-off program's"""
+    w, h, n = 640, 360, 16
+    src = _source(tmp_path, w, h, n)
+    ref, _ = _twice(tmp_path, src, w, h, n, {"X265AMD_LOOKAHEAD": "cpu", "X265AMD_ME": "cpu"}, "ref")
+    got, err = _twice(tmp_path, src, w, h, n, {"X265AMD_ME_STATS": "1"}, "gpu")
+    assert "lookahead estimates on the MI355X" in err and "on the MI355X" in err
+    assert got[0] == ref[0], "first encoder differs"
+    assert got[1] == ref[0], "second encoder in the same process differs (stale device pictures?)"
 
 
 def test_me_hook_cpu_mode_is_the_reference(tmp_path):
@@ -58,7 +119,7 @@ def test_me_hook_cpu_mode_is_the_reference(tmp_path):
     assert "(reference functions)" in err and got == ref
 
 
-def _gpu_encode_equals_reference(tmp_path, w, h, n, extra_env=None, depth=8):
+def _gpu_encode_equals_reference(tmp_path, w, h, n, extra_env=None, depth=8, min_area=4096):
     src = _source(tmp_path, w, h, n, depth=depth)
     if depth == 8:
         rc, ref, ref_fps, err = encode(_bin("x265ref8"), src, w, h, n, tmp_path / "ref.hevc", pools=16)
@@ -71,7 +132,7 @@ def _gpu_encode_equals_reference(tmp_path, w, h, n, extra_env=None, depth=8):
     env = {"X265AMD_ME_STATS": "1", **(extra_env or {})}
     rc, got, fps, err = encode(exe, src, w, h, n, tmp_path / "me.hevc", env, pools=16, depth=depth)
     assert rc == 0, err[-3000:]
-    assert "[x265me] motion searches of PUs >= 4096 pixels on the MI355X" in err
+    assert f"[x265me] motion searches of PUs >= {min_area} pixels on the MI355X" in err
     st = _stats(err)
     print(f"\n[x265me] {w}x{h} {n} frames: reference {ref_fps} fps, MI355X lookahead + ME {fps} fps; {st}")
     assert st["prefetches"] > 0 and st["hits"] > 0 and st["misses"] == 0, st
@@ -97,6 +158,36 @@ def test_gpu_me_check_mode_every_search_matches(tmp_path):
     err = _gpu_encode_equals_reference(tmp_path, 1280, 720, 12, {"X265AMD_ME": "check"})
     m = re.search(r"check: (\d+) mismatching searches", err)
     assert m and int(m.group(1)) == 0, err[-3000:]
+
+
+@pytest.mark.gpu
+def test_gpu_me_service_prefetch_32x32_check_mode(tmp_path):
+    """the launch service with the CU-start prefetch at depth 0 and 1 (64x64 and 32x32 CUs), every used
+    device search recomputed on the host: 0 mismatches, the prefetches were posted and collected (memo
+    hits), and the bitstream is the reference's"""
+    err = _gpu_encode_equals_reference(tmp_path, 1280, 720, 12, {"X265AMD_ME": "check", "X265AMD_ME_MIN": "1024"},
+                                       min_area=1024)
+    m = re.search(r"check: (\d+) mismatching searches", err)
+    assert m and int(m.group(1)) == 0, err[-3000:]
+    m = re.search(r"service: (\d+) launches, (\d+) requests", err)
+    assert m and int(m.group(1)) > 0 and int(m.group(2)) >= int(m.group(1)), err[-3000:]
+    assert re.search(r"posted [1-9]", err), err[-3000:]
+
+
+@pytest.mark.gpu
+def test_gpu_me_two_device_sessions_is_bit_exact(tmp_path):
+    """X265AMD_GPUS=2 on the one-GPU box: two device sessions (frame encoder i on session i mod 2, each with
+    its own reference-row copies) on device 0 — the frame-level shard of config 4 inside one encoder"""
+    err = _gpu_encode_equals_reference(tmp_path, 1280, 720, 16, {"X265AMD_GPUS": "2", "X265AMD_GPU_LIST": "0,0"})
+    m = re.search(r"searches per device session: (\d+) (\d+)", err)
+    assert m and int(m.group(1)) > 0 and int(m.group(2)) > 0, err[-3000:]
+    assert re.search(r"sessions 2", err), err[-3000:]
+
+
+@pytest.mark.gpu
+def test_gpu_me_round4_per_thread_form_is_bit_exact(tmp_path):
+    """X265AMD_MES_LAUNCHERS=0: the round-4 form (each worker launching on its own stream, synchronous)"""
+    _gpu_encode_equals_reference(tmp_path, 1280, 720, 8, {"X265AMD_MES_LAUNCHERS": "0"})
 
 
 @pytest.mark.gpu

@@ -31,7 +31,12 @@ def main():
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     a = ap.parse_args()
-    from bench import _x265_run, host_cores
+    from bench import x265_run
+    from src.x265_amd.replay_bench import host_cores
+
+    def _x265_run(exe, src, w, h, depth, frames, extra, env=None):
+        f, _, m, err = x265_run(exe, src, w, h, depth, frames, extra, env=env)
+        return f, m, err
     from src.x265_amd.synth import SyntheticSource
 
     ref, la = (os.path.join(ROOT, "oracle", "_ref", b) for b in ("x265ref8", "x265la8"))

@@ -43,9 +43,9 @@ def main():
     from src.x265_amd.workload import FrameSet, WorkloadBuilder, census_batches, group_launches, load_census
 
     prims = Primitives(device=0)
-    import bench
+    from src.x265_amd import replay_bench
 
-    census, _ = bench.pick_census(a)            # the census bench.py uses for this configuration
+    census, _ = replay_bench.pick_census(a)            # the census bench.py uses for this configuration
     fs = FrameSet(a.width, a.height, a.frames, a.depth, device="cuda:0")
     batches, _ = census_batches(fs, frames=a.frames, census=census, builder=WorkloadBuilder(fs, seed=11))
     launches = group_launches(batches)
