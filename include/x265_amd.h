@@ -63,6 +63,9 @@ int         x265amd_device_count(int* count);
 const char* x265amd_strerror(int status);
 /* Name of the gfx target the library was compiled for ("gfx950"). */
 const char* x265amd_target(void);
+/* sizeof of a descriptor type of this header by name ("x265amd_me_batch", ...), 0 if unknown: for bindings
+ * in other languages to check their layouts */
+int         x265amd_sizeof(const char* type);
 
 /* -------------------------------------------------------- a4 a6 a7 a8 a15
  * Pixel comparison of block A against block B, one scalar per job.
@@ -738,10 +741,10 @@ typedef struct
     const void* ref_cr;
     intptr_t ref_cstride;
     const int64_t* ref_coff;
-    /* optional (NULL = not counted): eval_count[0] / [1] += the full-pel / sub-pel block evaluations the
-     * batch's searches make (one SAD of the PU, resp. one interpolated PU + its SAD / SATD), the unit of the
-     * launch's algorithmic bytes; device memory, accumulated with atomics */
-    uint64_t* eval_count;
+    /* optional (NULL = not counted): eval_count[2 i] / [2 i + 1] = the full-pel / sub-pel block evaluations
+     * job i's search made (one SAD of the PU, resp. one interpolated PU + its SAD / SATD), the unit of the
+     * launch's algorithmic bytes */
+    uint32_t* eval_count;
 } x265amd_me_batch;
 int x265amd_motion_search(int depth, int count, const x265amd_me_batch* batches, void* stream);
 
@@ -772,6 +775,14 @@ typedef struct
     int method, subme, merange;    /* x265_param searchMethod / subpelRefine / searchRange */
     int max_cand;                  /* most MV candidates of one search (mvc[] of predInterSearch: 12) */
     int device;                    /* HIP device of the session (round 5; 0 = the first) */
+    /* 4:2:0 chroma planes for the sub-pel chroma SATD of subme > 2 (round 5; chroma = 0: luma only).  With
+     * chroma, pictures are made resident with x265amd_mes_ref420 and searches posted with
+     * x265amd_mes_post420; a search's chroma block is at the luma origin's half position */
+    int chroma;
+    intptr_t cstride;              /* PicYuv::m_strideC */
+    int64_t cplane_elems;          /* m_strideC * (maxHeight / 2 + 2 * m_chromaMarginY) */
+    int64_t corg_offset;           /* m_picOrg[1] - m_picBuf[1] (the same for Cr) */
+    int cmargin_y;                 /* m_chromaMarginY */
     int launchers;                 /* launch-service threads (round 5): 0 = every call runs on the calling
                                       thread's own stream (round-4 form); > 0 = calls only queue requests and
                                       this many service threads batch ALL queued requests of all threads into
@@ -823,6 +834,15 @@ int x265amd_mes_post(x265amd_mes* mes, int w, int h, const void* fenc, intptr_t 
                      const x265amd_mes_job* jobs, int* ticket);
 int x265amd_mes_wait(x265amd_mes* mes, int ticket, int n, x265amd_mes_job* jobs);
 int x265amd_mes_drop(x265amd_mes* mes, int ticket);
+/* x265amd_mes_ref for a chroma session: planes = m_picBuf[0..2]; the chroma rows of the same CTU rows go
+ * with the luma rows */
+int x265amd_mes_ref420(x265amd_mes* mes, const void* key, int64_t gen, const void* const planes[3], int rows_final,
+                       int* slot);
+/* x265amd_mes_post with the PU's 4:2:0 chroma source blocks (w/2 x h/2 at fenc_cb / fenc_cr, stride
+ * fenc_cstride): the searches add the chroma SATD where bChromaSATD adds it (motion.cpp:183-197); NULL
+ * chroma = luma only.  Needs a chroma session. */
+int x265amd_mes_post420(x265amd_mes* mes, int w, int h, const void* fenc, intptr_t fenc_stride, const void* fenc_cb,
+                        const void* fenc_cr, intptr_t fenc_cstride, int n, const x265amd_mes_job* jobs, int* ticket);
 /* rows of reference picture `key` (generation gen) resident on the device (0 if unknown) */
 int x265amd_mes_rows(x265amd_mes* mes, const void* key, int64_t gen, int* rows_resident);
 /* session counters: service batches, the requests / searches they carried, device time of the search

@@ -270,6 +270,15 @@ x265amd_mes* session(const PicYuv& pic, const x265_param& p, int sub)
         c.merange = p.searchRange;
         c.max_cand = (MD_ABOVE_LEFT + 1) * 2 + 2;
         c.launchers = g_launchers;
+        /* subme > 2: the 4:2:0 chroma planes too, for the sub-pel chroma SATD (launch service only) */
+        if (p.subpelRefine > 2 && pic.m_picCsp == X265_CSP_I420 && g_launchers > 0)
+        {
+            c.chroma = 1;
+            c.cstride = pic.m_strideC;
+            c.cplane_elems = (int64_t)pic.m_strideC * ((int64_t)rows * ctu / 2 + 2 * (int64_t)pic.m_chromaMarginY);
+            c.corg_offset = pic.m_picOrg[1] - pic.m_picBuf[1];
+            c.cmargin_y = (int)pic.m_chromaMarginY;
+        }
         int ndev = 1;
         if (x265amd_device_count(&ndev) || ndev < 1) ndev = 1;
         c.device = !g_gpu_list.empty() ? g_gpu_list[sub % g_gpu_list.size()] : sub % ndev;
@@ -458,8 +467,9 @@ int form_searches(Search& S, Mode& interMode, const PredictionUnit& pu, const ui
                 const long long r0 = now_ns();
                 /* generation = (encoder epoch, POC): a later encoder's picture at a reused PicYuv address is
                  * never taken for an earlier one's */
-                const int rc = x265amd_mes_ref(mes, mr.reconPic, epoch | (uint32_t)rf->m_poc, mr.reconPic->m_picBuf[0],
-                                               const_cast<Frame*>(rf)->m_reconRowCount.get(), &slot);
+                const void* planes[3] = { mr.reconPic->m_picBuf[0], mr.reconPic->m_picBuf[1], mr.reconPic->m_picBuf[2] };
+                const int rc = x265amd_mes_ref420(mes, mr.reconPic, epoch | (uint32_t)rf->m_poc, planes,
+                                                  const_cast<Frame*>(rf)->m_reconRowCount.get(), &slot);
                 t_ref += now_ns() - r0;
                 if (rc)
                 {
@@ -538,6 +548,19 @@ int form_searches(Search& S, Mode& interMode, const PredictionUnit& pu, const ui
     return pf->n;
 }
 
+/* bChromaSATD of a w x h PU exactly as MotionEstimate::setSourcePU sets it (motion.cpp:193-197) */
+bool chroma_satd(const Search& S, int csp, int w, int h)
+{
+    return S.m_param->subpelRefine > 2 && csp != X265_CSP_I400 && primitives.chroma[csp].pu[partitionFromSizes(w, h)].satd;
+}
+
+/* can the device run this PU's searches: luma-only searches always, chroma-SATD searches (subme > 2) on
+ * 4:2:0 pictures with the launch service (the session then holds the chroma planes) */
+bool device_can(int csp, bool chroma)
+{
+    return !chroma || (csp == X265_CSP_I420 && g_launchers > 0);
+}
+
 /* is a 2Nx2N PU of this CU searched on the device (large enough, the reference loop's plain path) */
 bool eligible(const Search& S, const CUGeom& cuGeom)
 {
@@ -603,6 +626,11 @@ void prefetch_cu(Analysis& A, const CUData& parentCTU, const CUGeom& cuGeom, int
     Prefetch* pf = prefetch_buf(t_apf[d]);
     release(pf);
     Mode& im = A.m_modeDepth[d].pred[Analysis::PRED_2Nx2N];
+    {
+        const int size = 1 << cuGeom.log2CUSize;
+        if (!device_can(im.fencYuv->m_csp, chroma_satd(A, im.fencYuv->m_csp, size, size)))
+            return;
+    }
     im.cu.initSubCU(parentCTU, cuGeom, qp);
     PredictionUnit pu(im.cu, cuGeom, 0);
     const uint32_t all[2] = { (uint32_t)-1, (uint32_t)-1 };
@@ -613,6 +641,7 @@ void prefetch_cu(Analysis& A, const CUData& parentCTU, const CUGeom& cuGeom, int
         return;
     /* the 2Nx2N PU's source block: the CU's own fenc buffer (stride = CU size), what setSourcePU copies */
     const Yuv& fenc = *im.fencYuv;
+    const bool chroma = chroma_satd(A, fenc.m_csp, pu.width, pu.height);
     if (g_mode == ME_HOST)
     {
         /* the CPU check of the early forming: the searches run here on the host, and the reference loop
@@ -631,7 +660,8 @@ void prefetch_cu(Analysis& A, const CUData& parentCTU, const CUGeom& cuGeom, int
     }
     const long long t0 = now_ns();
     int ticket = -1;
-    const int st = x265amd_mes_post(mes, pu.width, pu.height, fenc.m_buf[0], fenc.m_size, n, pf->jobs, &ticket);
+    const int st = x265amd_mes_post420(mes, pu.width, pu.height, fenc.m_buf[0], fenc.m_size, chroma ? fenc.m_buf[1] : NULL,
+                                       chroma ? fenc.m_buf[2] : NULL, fenc.m_csize, n, pf->jobs, &ticket);
     g_ns_post += now_ns() - t0;
     if (st)
     {
@@ -668,7 +698,7 @@ void Search::predInterSearch(Mode& interMode, const CUGeom& cuGeom, bool bChroma
         /* the same source block the reference loop sets up (search.cpp:2077) */
         m_me.setSourcePU(*interMode.fencYuv, pu.ctuAddr, pu.cuAbsPartIdx, pu.puAbsPartIdx, pu.width, pu.height);
         Prefetch* apf = cuGeom.depth < 2 ? t_apf[cuGeom.depth] : NULL;
-        if (m_me.bChromaSATD)
+        if (!device_can(interMode.fencYuv->m_csp, m_me.bChromaSATD))
             ;
         else if (apf && apf->pending && apf->mode == &interMode && apf->epoch == g_epoch.load())
         {
@@ -699,8 +729,18 @@ void Search::predInterSearch(Mode& interMode, const CUGeom& cuGeom, bool bChroma
             else if (ok)
             {
                 const long long t0 = now_ns();
-                const int st = x265amd_mes_search(mes, pu.width, pu.height, m_me.fencPUYuv.m_buf[0], FENC_STRIDE, n,
-                                                  jobs);
+                int st;
+                if (m_me.bChromaSATD)
+                {
+                    /* the PU's chroma as setSourcePU copied it (fencPUYuv: stride FENC_STRIDE / 2) */
+                    int ticket = -1;
+                    st = x265amd_mes_post420(mes, pu.width, pu.height, m_me.fencPUYuv.m_buf[0], FENC_STRIDE,
+                                             m_me.fencPUYuv.m_buf[1], m_me.fencPUYuv.m_buf[2], m_me.fencPUYuv.m_csize, n,
+                                             jobs, &ticket);
+                    if (!st) st = x265amd_mes_wait(mes, ticket, n, jobs);
+                }
+                else
+                    st = x265amd_mes_search(mes, pu.width, pu.height, m_me.fencPUYuv.m_buf[0], FENC_STRIDE, n, jobs);
                 g_ns_wait += now_ns() - t0;
                 g_waits++;
                 if (st)

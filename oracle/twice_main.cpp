@@ -43,6 +43,8 @@ static int encode(const char* in, int w, int h, int frames, const char* out, con
     p->internalCsp = X265_CSP_I420;
     p->bEmitInfoSEI = 0;
     p->totalFrames = frames;
+    /* the GPU box shows the whole machine's CPUs but grants a 16-core share: size the pool for the share */
+    if (api->param_parse(p, "pools", "16") < 0) return 2;
     x265_encoder* enc = api->encoder_open(p);
     if (!enc) return 3;
     FILE* fo = fopen(out, "wb");

@@ -47,7 +47,7 @@ struct MeArgs
     const void* rcr;
     int64_t rcs;
     const int64_t* rcoff;
-    unsigned long long* evals;    // [2]: full-pel / sub-pel block evaluations of the launch (NULL = not counted)
+    uint32_t* evals;              // [2 n]: job j's full-pel / sub-pel block evaluations (NULL = not counted)
     int w, h, n, lg, method, subme, merange, max_cand, depth;
 };
 
@@ -881,8 +881,8 @@ __global__ __launch_bounds__(X265AMD_BLOCK, X265AMD_ME_WAVES) void k_motion_sear
         a.out_cost[j] = bcost;
         if (a.evals)
         {
-            atomicAdd(&a.evals[0], (unsigned long long)s.nfp);
-            atomicAdd(&a.evals[1], (unsigned long long)s.nsp);
+            a.evals[2 * j] = s.nfp;
+            a.evals[2 * j + 1] = s.nsp;
         }
     }
 }
@@ -1060,7 +1060,7 @@ extern "C" int x265amd_motion_search(int depth, int count, const x265amd_me_batc
         MeArgs a{ b.fenc, b.fenc_off, (int64_t)b.fenc_stride, b.ref, b.ref_off, (int64_t)b.ref_stride, b.mv_range,
                   b.mvp, b.mvc, b.num_cand, b.mvcost, b.mvcost_off, b.out_mv, b.out_cost, b.fenc_cb, b.fenc_cr,
                   (int64_t)b.fenc_cstride, b.fenc_coff, b.ref_cb, b.ref_cr, (int64_t)b.ref_cstride, b.ref_coff,
-                  (unsigned long long*)b.eval_count, b.w, b.h, b.n, lg, b.method, b.subme, b.merange, b.max_cand, depth };
+                  b.eval_count, b.w, b.h, b.n, lg, b.method, b.subme, b.merange, b.max_cand, depth };
         const int rc = depth == 8 ? launch_me<uint8_t>(a, bs) : launch_me<uint16_t>(a, bs);
         if (rc) { fj.join(); return rc; }
     }

@@ -26,6 +26,7 @@
 // caller searches that PU on the host.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
@@ -79,6 +80,7 @@ struct x265amd_mes_stage
 {
     uint8_t* dev = nullptr;
     uint8_t* host = nullptr;
+    uint8_t* hdev = nullptr;     // the device's address of the pinned host buffer (null: not mapped)
     size_t cap = 0;
 };
 
@@ -86,7 +88,8 @@ struct x265amd_mes_stage
 struct x265amd_mes_req
 {
     int w = 0, h = 0, n = 0;
-    uint8_t* fenc = nullptr;                 // 64 * 64 * pix bytes
+    bool chroma = false;                     // the 4:2:0 chroma blocks are in fenc after the luma block
+    uint8_t* fenc = nullptr;                 // (64 * 64 + 2 * 32 * 32) * pix bytes
     x265amd_mes_job jobs[kMaxJobs];
     std::atomic<int> state{ 0 };             // 0 free, 1 queued / on the device, 2 done
     bool dropped = false;                    // the poster no longer wants it (free once done)
@@ -107,15 +110,11 @@ struct x265amd_mes_thread
     x265amd_mes_req req[kSlots];
 };
 
-constexpr int kSizes = 8;          // PU sizes whose evaluations one launch counts separately
-
 struct x265amd_mes_launcher
 {
     hipStream_t st = nullptr;
     hipEvent_t done = nullptr, k0 = nullptr, k1 = nullptr;
     x265amd_mes_stage g;
-    uint64_t* evals_dev = nullptr;   // [kSizes][2] evaluation counters of the launch in flight
-    uint64_t* evals_host = nullptr;
     std::thread th;
 };
 
@@ -126,7 +125,9 @@ struct x265amd_mes
     size_t pix = 1;
     int64_t rows = 0;                 // plane rows incl. both margins
     size_t plane_bytes = 0;
-    uint8_t* arena = nullptr;         // max_pictures padded luma planes
+    int64_t slot_elems = 0;           // one picture: luma plane, then (chroma sessions) Cb and Cr planes
+    int64_t crows = 0;                // chroma plane rows incl. both margins
+    uint8_t* arena = nullptr;         // max_pictures padded pictures
     uint16_t* tables = nullptr;       // max_tables BitCost tables of 2 * range + 1 entries
     size_t table_elems = 0;
 
@@ -135,7 +136,7 @@ struct x265amd_mes
         int slot;
         int64_t gen;
         int rows_up;                  // CTU rows resident on the device
-        const void* pinned;           // host buffer registered with hipHostRegister (or null)
+        const void* pinned[3];        // host planes registered with hipHostRegister (or null)
         std::mutex mu;                // one uploader at a time; the others wait for its rows
     };
     std::mutex mu;
@@ -169,6 +170,11 @@ struct x265amd_mes
     std::mutex dmu;                   // waiters sleep on dcv
     std::condition_variable dcv;
     int spin_us = 50;
+    int trace = 0;                    // X265AMD_MES_TRACE=n: log the first n posts / launches / waits
+    bool zerocopy = false;            // X265AMD_MES_ZEROCOPY=1: the kernel reads / writes the pinned staging
+    bool prio = false;                // X265AMD_MES_PRIORITY=1: launch streams at the highest priority
+    bool lspin = false;               // X265AMD_MES_LSPIN=1: launchers poll for completion
+    std::atomic<int> traced{ 0 };
 
     // statistics (x265amd_mes_stats)
     std::mutex smu;
@@ -210,8 +216,11 @@ int reserve(hipStream_t a, hipStream_t b, x265amd_mes_stage& g, size_t bytes)
     g.dev = g.host = nullptr;
     g.cap = 0;
     if (hipMalloc((void**)&g.dev, bytes) != hipSuccess ||
-        hipHostMalloc((void**)&g.host, bytes, hipHostMallocDefault) != hipSuccess)
+        hipHostMalloc((void**)&g.host, bytes, hipHostMallocMapped) != hipSuccess)
         return X265AMD_ENOMEM;
+    g.hdev = nullptr;
+    if (hipHostGetDevicePointer((void**)&g.hdev, g.host, 0) != hipSuccess) g.hdev = nullptr;
+    (void)hipGetLastError();
     g.cap = bytes;
     return 0;
 }
@@ -279,7 +288,7 @@ int thread_ctx(x265amd_mes* s, x265amd_mes_thread** out)
             hipEventCreateWithFlags(&t->ev, hipEventBlockingSync | hipEventDisableTiming) != hipSuccess)
             rc = X265AMD_ENOMEM;
         for (auto& r : t->req)
-            if (!rc && !(r.fenc = (uint8_t*)malloc(64 * 64 * s->pix))) rc = X265AMD_ENOMEM;
+            if (!rc && !(r.fenc = (uint8_t*)malloc((64 * 64 + 2 * 32 * 32) * s->pix))) rc = X265AMD_ENOMEM;
     }
     if (rc)
     {
@@ -303,12 +312,20 @@ int thread_ctx(x265amd_mes* s, x265amd_mes_thread** out)
 // batch layout in the staging buffers (byte offsets, 256-aligned)
 struct Layout
 {
-    size_t fenc, fenc_off, ref_off, range, mvp, mvc, ncand, cost_off, out_mv, out_cost, end;
-    Layout(int n, int h, int pix, int maxc, intptr_t fstride)
+    size_t fenc, fenc_c = 0, fenc_coff = 0, ref_coff = 0, fenc_off, ref_off, range, mvp, mvc, ncand, cost_off, out_mv,
+        out_cost, evals, end;
+    // cblk: elements of one request's chroma block (0: luma only), np requests
+    Layout(int n, int h, int pix, int maxc, intptr_t fstride, size_t cblk = 0, int np = 0)
     {
         size_t o = 0;
         auto take = [&](size_t b) { size_t r = o; o = (o + b + 255) & ~(size_t)255; return r; };
         fenc = take((size_t)fstride * h * pix);
+        if (cblk)
+        {
+            fenc_c = take(2 * cblk * np * pix);
+            fenc_coff = take(8 * (size_t)n);
+            ref_coff = take(8 * (size_t)n);
+        }
         fenc_off = take(8 * (size_t)n);
         ref_off = take(8 * (size_t)n);
         range = take(8 * (size_t)n);
@@ -318,6 +335,7 @@ struct Layout
         cost_off = take(8 * (size_t)n);
         out_mv = take(4 * (size_t)n);
         out_cost = take(4 * (size_t)n);
+        evals = take(8 * (size_t)n);
         end = o;
     }
 };
@@ -365,12 +383,36 @@ x265amd_me_batch make_batch(const x265amd_mes* s, const x265amd_mes_stage& g, co
     return b;
 }
 
-// job i's descriptors into the host staging of layout L (source block at element offset foff)
-void stage_job(const x265amd_mes* s, uint8_t* H, const Layout& L, int i, const x265amd_mes_job& j, int64_t foff)
+// the chroma fields of a batch whose np requests' chroma blocks are staged at L.fenc_c (Cb blocks, then Cr)
+void chroma_batch(const x265amd_mes* s, const x265amd_mes_stage& g, const Layout& L, int w, int h, int np,
+                  x265amd_me_batch& b)
 {
+    const size_t cblk = (size_t)(w / 2) * (h / 2);
+    b.fenc_cb = g.dev + L.fenc_c;
+    b.fenc_cr = g.dev + L.fenc_c + cblk * np * s->pix;
+    b.fenc_cstride = w / 2;
+    b.fenc_coff = (const int64_t*)(g.dev + L.fenc_coff);
+    b.ref_cb = s->arena + (size_t)s->cfg.plane_elems * s->pix;
+    b.ref_cr = s->arena + (size_t)(s->cfg.plane_elems + s->cfg.cplane_elems) * s->pix;
+    b.ref_cstride = s->cfg.cstride;
+    b.ref_coff = (const int64_t*)(g.dev + L.ref_coff);
+}
+
+// job i's descriptors into the host staging of layout L (source block at element offset foff)
+void stage_job(const x265amd_mes* s, uint8_t* H, const Layout& L, int i, const x265amd_mes_job& j, int64_t foff,
+               int64_t fcoff = 0)
+{
+    if (L.fenc_coff) ((int64_t*)(H + L.fenc_coff))[i] = fcoff;
     const int maxc = s->cfg.max_cand > 0 ? s->cfg.max_cand : 1;
     ((int64_t*)(H + L.fenc_off))[i] = foff;
-    ((int64_t*)(H + L.ref_off))[i] = (int64_t)j.slot * s->cfg.plane_elems + s->cfg.org_offset + j.block_off;
+    ((int64_t*)(H + L.ref_off))[i] = (int64_t)j.slot * s->slot_elems + s->cfg.org_offset + j.block_off;
+    if (L.fenc_coff)
+    {
+        // the chroma block of the PU: half the luma origin's position (4:2:0)
+        const int64_t x = j.block_off % s->cfg.stride, y = j.block_off / s->cfg.stride;
+        ((int64_t*)(H + L.ref_coff))[i] = (int64_t)j.slot * s->slot_elems + s->cfg.corg_offset + (y >> 1) * s->cfg.cstride +
+                                          (x >> 1);
+    }
     memcpy((int16_t*)(H + L.range) + 4 * i, j.mv_range, 8);
     memcpy((int16_t*)(H + L.mvp) + 2 * i, j.mvp, 4);
     memcpy((int16_t*)(H + L.mvc) + 2 * (size_t)maxc * i, j.mvc, 4 * (size_t)j.num_cand);
@@ -407,26 +449,34 @@ void launcher_main(x265amd_mes* s, x265amd_mes_launcher* L)
             s->rq.clear();
         }
         const double t_take = now_s();
+        if (s->trace && s->traced.fetch_add(1) < s->trace)
+            fprintf(stderr, "[mes] launcher %p takes %zu requests\n", (void*)L, take.size());
         // group by PU size, keeping the posting order inside a size
         order.clear();
+        // batches: one per (PU size, chroma) — the size in first / second, chroma as a negative height
         std::vector<std::pair<int, int>> sizes;
+        auto key_h = [](const x265amd_mes_req* r) { return r->chroma ? -r->h : r->h; };
         for (auto* r : take)
         {
             bool seen = false;
-            for (auto& z : sizes) seen |= z.first == r->w && z.second == r->h;
-            if (!seen) sizes.push_back({ r->w, r->h });
+            for (auto& z : sizes) seen |= z.first == r->w && z.second == key_h(r);
+            if (!seen) sizes.push_back({ r->w, key_h(r) });
         }
         lay.clear();
         bt.clear();
         base.clear();
         size_t total = 0;
         const int maxc = s->cfg.max_cand > 0 ? s->cfg.max_cand : 1;
+        std::vector<int> nps, nj;
         for (auto& z : sizes)
         {
             int n = 0, np = 0;
             for (auto* r : take)
-                if (r->w == z.first && r->h == z.second) { n += r->n; np++; }
-            lay.emplace_back(n, np * z.second, (int)s->pix, maxc, z.first);
+                if (r->w == z.first && key_h(r) == z.second) { n += r->n; np++; }
+            const int h = z.second < 0 ? -z.second : z.second;
+            lay.emplace_back(n, np * h, (int)s->pix, maxc, z.first, z.second < 0 ? (size_t)(z.first / 2) * (h / 2) : 0, np);
+            nps.push_back(np);
+            nj.push_back(n);
             base.push_back(total);
             total += lay.back().end;
         }
@@ -436,37 +486,81 @@ void launcher_main(x265amd_mes* s, x265amd_mes_launcher* L)
         {
             for (size_t k = 0; k < sizes.size(); k++)
             {
-                const int w = sizes[k].first, h = sizes[k].second;
+                const int w = sizes[k].first, kh = sizes[k].second, h = kh < 0 ? -kh : kh;
+                const size_t cblk = (size_t)(w / 2) * (h / 2);
                 uint8_t* H = L->g.host + base[k];
                 const Layout& Ly = lay[k];
                 int i = 0, p = 0;
                 for (auto* r : take)
                 {
-                    if (r->w != w || r->h != h) continue;
+                    if (r->w != w || key_h(r) != kh) continue;
                     memcpy(H + Ly.fenc + (size_t)p * w * h * s->pix, r->fenc, (size_t)w * h * s->pix);
+                    if (kh < 0)
+                    {
+                        const uint8_t* c = r->fenc + (size_t)w * h * s->pix;
+                        memcpy(H + Ly.fenc_c + (size_t)p * cblk * s->pix, c, cblk * s->pix);
+                        memcpy(H + Ly.fenc_c + ((size_t)nps[k] + p) * cblk * s->pix, c + cblk * s->pix, cblk * s->pix);
+                    }
                     for (int q = 0; q < r->n; q++, i++)
-                        stage_job(s, H, Ly, i, r->jobs[q], (int64_t)p * w * h);
+                        stage_job(s, H, Ly, i, r->jobs[q], (int64_t)p * w * h, (int64_t)p * cblk);
                     order.push_back(r);
                     p++;
                 }
                 x265amd_mes_stage sub{ L->g.dev + base[k], L->g.host + base[k], Ly.end };
                 bt.push_back(make_batch(s, sub, Ly, w, h, i, w));
-                if (k < (size_t)kSizes) bt.back().eval_count = L->evals_dev + 2 * k;
+                if (kh < 0) chroma_batch(s, sub, Ly, w, h, p, bt.back());
+                bt.back().eval_count = (uint32_t*)(sub.dev + Ly.evals);
                 njobs += i;
             }
-            rc = (int)hipMemsetAsync(L->evals_dev, 0, sizeof(uint64_t) * 2 * kSizes, L->st);
+            if (s->zerocopy && L->g.hdev)
+            {
+                // the kernel reads the descriptors and source blocks from the pinned staging and writes its
+                // outputs there (no copies): the batch addresses are the host staging's
+                for (size_t k = 0; k < bt.size(); k++)
+                {
+                    const ptrdiff_t d = L->g.hdev - L->g.dev;
+                    auto mv = [d](const void* p) { return p ? (const void*)((const uint8_t*)p + d) : p; };
+                    x265amd_me_batch& b = bt[k];
+                    b.fenc = mv(b.fenc);
+                    b.fenc_off = (const int64_t*)mv(b.fenc_off);
+                    b.ref_off = (const int64_t*)mv(b.ref_off);
+                    b.mv_range = (const int16_t*)mv(b.mv_range);
+                    b.mvp = (const int16_t*)mv(b.mvp);
+                    b.mvc = (const int16_t*)mv(b.mvc);
+                    b.num_cand = (const uint8_t*)mv(b.num_cand);
+                    b.mvcost_off = (const int64_t*)mv(b.mvcost_off);
+                    b.out_mv = (int16_t*)mv(b.out_mv);
+                    b.out_cost = (int32_t*)mv(b.out_cost);
+                    b.eval_count = (uint32_t*)mv(b.eval_count);
+                    if (b.fenc_cb)
+                    {
+                        b.fenc_cb = mv(b.fenc_cb);
+                        b.fenc_cr = mv(b.fenc_cr);
+                        b.fenc_coff = (const int64_t*)mv(b.fenc_coff);
+                        b.ref_coff = (const int64_t*)mv(b.ref_coff);
+                    }
+                }
+            }
             // one upload of every size's inputs (the output regions ride along: staging is contiguous)
-            if (!rc) rc = (int)hipMemcpyAsync(L->g.dev, L->g.host, total, hipMemcpyHostToDevice, L->st);
+            if (!(s->zerocopy && L->g.hdev))
+                rc = (int)hipMemcpyAsync(L->g.dev, L->g.host, total, hipMemcpyHostToDevice, L->st);
             if (!rc) rc = (int)hipEventRecord(L->k0, L->st);
             if (!rc) rc = x265amd_motion_search(s->cfg.depth, (int)bt.size(), bt.data(), L->st);
             if (!rc) rc = (int)hipEventRecord(L->k1, L->st);
-            for (size_t k = 0; k < sizes.size() && !rc; k++)
+            for (size_t k = 0; k < sizes.size() && !rc && !(s->zerocopy && L->g.hdev); k++)
                 rc = (int)hipMemcpyAsync(L->g.host + base[k] + lay[k].out_mv, L->g.dev + base[k] + lay[k].out_mv,
                                          lay[k].end - lay[k].out_mv, hipMemcpyDeviceToHost, L->st);
-            if (!rc) rc = (int)hipMemcpyAsync(L->evals_host, L->evals_dev, sizeof(uint64_t) * 2 * kSizes,
-                                              hipMemcpyDeviceToHost, L->st);
             if (!rc) rc = (int)hipEventRecord(L->done, L->st);
-            if (!rc) rc = (int)hipEventSynchronize(L->done);
+            if (!rc && s->lspin)
+            {
+                // poll instead of sleeping on the completion interrupt (lower wake-up latency, one busy core)
+                hipError_t q;
+                while ((q = hipEventQuery(L->done)) == hipErrorNotReady)
+                    __builtin_ia32_pause();
+                rc = (int)q;
+            }
+            else if (!rc)
+                rc = (int)hipEventSynchronize(L->done);
         }
         // algorithmic bytes of the launch: per full-pel evaluation the PU and its reference
         // block (2 W H b), per sub-pel evaluation the PU and the reference window of the 8-tap filters
@@ -474,12 +568,23 @@ void launcher_main(x265amd_mes* s, x265amd_mes_launcher* L)
         double algo = 0;
         int64_t efp = 0, esp = 0;
         if (!rc)
-            for (size_t k = 0; k < sizes.size() && k < (size_t)kSizes; k++)
+            for (size_t k = 0; k < sizes.size(); k++)
             {
-                const double w = sizes[k].first, h = sizes[k].second, b = (double)s->pix;
-                efp += (int64_t)L->evals_host[2 * k];
-                esp += (int64_t)L->evals_host[2 * k + 1];
-                algo += L->evals_host[2 * k] * 2 * w * h * b + L->evals_host[2 * k + 1] * ((w + 7) * (h + 7) + w * h) * b;
+                const double w = sizes[k].first, h = sizes[k].second < 0 ? -sizes[k].second : sizes[k].second;
+                const double b = (double)s->pix;
+                // with chroma: each sub-pel evaluation also interpolates and compares the two w/2 x h/2 chroma
+                // blocks (4-tap: (w/2 + 3)(h/2 + 3) window)
+                const double csub = sizes[k].second < 0 ? 2 * ((w / 2 + 3) * (h / 2 + 3) + (w / 2) * (h / 2)) : 0;
+                const uint32_t* ev = (const uint32_t*)(L->g.host + base[k] + lay[k].evals);
+                int64_t fp = 0, sp = 0;
+                for (int i = 0; i < nj[k]; i++)
+                {
+                    fp += ev[2 * i];
+                    sp += ev[2 * i + 1];
+                }
+                efp += fp;
+                esp += sp;
+                algo += fp * 2 * w * h * b + sp * ((w + 7) * (h + 7) + w * h + csub) * b;
             }
         float kms = 0;
         if (!rc) (void)hipEventElapsedTime(&kms, L->k0, L->k1);
@@ -488,12 +593,12 @@ void launcher_main(x265amd_mes* s, x265amd_mes_launcher* L)
         if (!rc)
             for (size_t k = 0; k < sizes.size(); k++)
             {
-                const int w = sizes[k].first, h = sizes[k].second;
+                const int w = sizes[k].first, kh = sizes[k].second;
                 const uint8_t* H = L->g.host + base[k];
                 int i = 0;
                 for (auto* r : take)
                 {
-                    if (r->w != w || r->h != h) continue;
+                    if (r->w != w || key_h(r) != kh) continue;
                     for (int q = 0; q < r->n; q++, i++) read_out(H, lay[k], i, r->jobs[q]);
                 }
             }
@@ -509,6 +614,9 @@ void launcher_main(x265amd_mes* s, x265amd_mes_launcher* L)
         }
         s->dcv.notify_all();
         if (rc) record(rc);
+        if (s->trace && s->traced.fetch_add(1) < s->trace)
+            fprintf(stderr, "[mes] launcher %p done: rc %d, kernel %.3f ms, batch %.3f ms\n", (void*)L, rc, kms,
+                    1e3 * (t_done - t_take));
         {
             std::lock_guard<std::mutex> g(s->smu);
             s->st.batches++;
@@ -531,16 +639,21 @@ int start_service(x265amd_mes* s)
 {
     const int n = s->cfg.launchers;
     if (const char* e = getenv("X265AMD_MES_SPIN_US")) s->spin_us = atoi(e);
+    if (const char* e = getenv("X265AMD_MES_TRACE")) s->trace = atoi(e);
+    if (const char* e = getenv("X265AMD_MES_ZEROCOPY")) s->zerocopy = atoi(e) != 0;
+    if (const char* e = getenv("X265AMD_MES_PRIORITY")) s->prio = atoi(e) != 0;
+    if (const char* e = getenv("X265AMD_MES_LSPIN")) s->lspin = atoi(e) != 0;
     for (int i = 0; i < n; i++)
     {
         auto* L = new (std::nothrow) x265amd_mes_launcher();
         if (!L) return X265AMD_ENOMEM;
         s->launchers.push_back(L);
-        if (hipStreamCreateWithFlags(&L->st, hipStreamNonBlocking) != hipSuccess ||
+        int lo = 0, hi = 0;
+        if (s->prio) (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
+        if ((s->prio ? hipStreamCreateWithPriority(&L->st, hipStreamNonBlocking, hi)
+                     : hipStreamCreateWithFlags(&L->st, hipStreamNonBlocking)) != hipSuccess ||
             hipEventCreateWithFlags(&L->done, hipEventBlockingSync | hipEventDisableTiming) != hipSuccess ||
             hipEventCreate(&L->k0) != hipSuccess || hipEventCreate(&L->k1) != hipSuccess ||
-            hipMalloc((void**)&L->evals_dev, sizeof(uint64_t) * 2 * kSizes) != hipSuccess ||
-            hipHostMalloc((void**)&L->evals_host, sizeof(uint64_t) * 2 * kSizes, hipHostMallocDefault) != hipSuccess ||
             reserve(L->st, nullptr, L->g, 1 << 20))
             return X265AMD_ENOMEM;
     }
@@ -571,8 +684,6 @@ void stop_service(x265amd_mes* s)
         if (L->st) (void)hipStreamSynchronize(L->st);
         (void)hipFree(L->g.dev);
         (void)hipHostFree(L->g.host);
-        (void)hipFree(L->evals_dev);
-        (void)hipHostFree(L->evals_host);
         if (L->st) (void)hipStreamDestroy(L->st);
         for (hipEvent_t e : { L->done, L->k0, L->k1 })
             if (e) (void)hipEventDestroy(e);
@@ -592,7 +703,12 @@ extern "C" int x265amd_mes_create(const x265amd_mes_config* cfg, x265amd_mes** o
         cfg->margin_y < 0 || cfg->ctu_rows <= 0 || cfg->ctu_size <= 0 || cfg->max_pictures <= 0 ||
         cfg->max_threads <= 0 || cfg->max_tables <= 0 || cfg->mvcost_range <= 0 || cfg->method < 0 ||
         cfg->method > 4 || cfg->subme < 0 || cfg->subme > 7 || cfg->merange < 1 || cfg->max_cand < 0 ||
-        cfg->max_cand > 16 || cfg->device < 0 || cfg->launchers < 0 || cfg->launchers > 8 ||
+        cfg->max_cand > 16 || cfg->device < 0 || cfg->launchers < 0 || cfg->launchers > 8 || cfg->chroma < 0 ||
+        cfg->chroma > 1 ||
+        (cfg->chroma && (cfg->cstride <= 0 || cfg->cplane_elems <= 0 || cfg->cplane_elems % cfg->cstride ||
+                         cfg->corg_offset < 0 || cfg->corg_offset >= cfg->cplane_elems || cfg->cmargin_y < 0 ||
+                         (int64_t)cfg->cmargin_y * 2 + (int64_t)cfg->ctu_rows * cfg->ctu_size / 2 >
+                             cfg->cplane_elems / cfg->cstride)) ||
         (int64_t)cfg->margin_y * 2 + (int64_t)cfg->ctu_rows * cfg->ctu_size > cfg->plane_elems / cfg->stride)
         return X265AMD_EINVAL;
     int ndev = 0;
@@ -604,9 +720,11 @@ extern "C" int x265amd_mes_create(const x265amd_mes_config* cfg, x265amd_mes** o
     s->pix = cfg->depth > 8 ? 2 : 1;
     s->rows = cfg->plane_elems / cfg->stride;
     s->plane_bytes = (size_t)cfg->plane_elems * s->pix;
+    s->slot_elems = cfg->plane_elems + (cfg->chroma ? 2 * cfg->cplane_elems : 0);
+    s->crows = cfg->chroma ? cfg->cplane_elems / cfg->cstride : 0;
     s->table_elems = 2 * (size_t)cfg->mvcost_range + 1;
     int rc = use_device(s);
-    if (!rc && (hipMalloc((void**)&s->arena, s->plane_bytes * cfg->max_pictures) != hipSuccess ||
+    if (!rc && (hipMalloc((void**)&s->arena, (size_t)s->slot_elems * s->pix * cfg->max_pictures) != hipSuccess ||
                 hipMalloc((void**)&s->tables, sizeof(uint16_t) * s->table_elems * cfg->max_tables) != hipSuccess))
         rc = X265AMD_ENOMEM;
     if (!rc && cfg->launchers) rc = start_service(s);
@@ -627,7 +745,8 @@ extern "C" void x265amd_mes_destroy(x265amd_mes* s)
     for (auto* t : s->threads) free_thread(t);
     for (auto& p : s->pics)
     {
-        if (p.second->pinned) (void)hipHostUnregister((void*)p.second->pinned);
+        for (const void* pin : p.second->pinned)
+            if (pin) (void)hipHostUnregister((void*)pin);
         delete p.second;
     }
     (void)hipFree(s->arena);
@@ -635,10 +754,11 @@ extern "C" void x265amd_mes_destroy(x265amd_mes* s)
     delete s;
 }
 
-extern "C" int x265amd_mes_ref(x265amd_mes* s, const void* key, int64_t gen, const void* plane_buf, int rows_final,
-                               int* slot)
+extern "C" int x265amd_mes_ref420(x265amd_mes* s, const void* key, int64_t gen, const void* const planes[3],
+                                  int rows_final, int* slot)
 {
-    if (!s || !key || !plane_buf || !slot || rows_final < 0 || rows_final > s->cfg.ctu_rows)
+    if (!s || !key || !planes || !planes[0] || !slot || rows_final < 0 || rows_final > s->cfg.ctu_rows ||
+        (s->cfg.chroma && (!planes[1] || !planes[2])))
         return record(X265AMD_EINVAL);
     MES_TRY(use_device(s));
     x265amd_mes_thread* t;
@@ -657,7 +777,7 @@ extern "C" int x265amd_mes_ref(x265amd_mes* s, const void* key, int64_t gen, con
             p->slot = s->next_slot++;
             p->gen = gen;
             p->rows_up = 0;
-            p->pinned = nullptr;
+            p->pinned[0] = p->pinned[1] = p->pinned[2] = nullptr;
             it = s->pics.emplace(key, p).first;
         }
         p = it->second;
@@ -668,33 +788,55 @@ extern "C" int x265amd_mes_ref(x265amd_mes* s, const void* key, int64_t gen, con
         p->gen = gen;
         p->rows_up = 0;
     }
-    if (p->pinned != plane_buf)
-    {
-        if (p->pinned) (void)hipHostUnregister((void*)p->pinned);
-        p->pinned = hipHostRegister((void*)plane_buf, s->plane_bytes, hipHostRegisterDefault) == hipSuccess ? plane_buf
-                                                                                                          : nullptr;
-        (void)hipGetLastError();
-    }
+    const int np = s->cfg.chroma ? 3 : 1;
+    for (int k = 0; k < np; k++)
+        if (p->pinned[k] != planes[k])
+        {
+            if (p->pinned[k]) (void)hipHostUnregister((void*)p->pinned[k]);
+            const size_t bytes = (size_t)(k ? s->cfg.cplane_elems : s->cfg.plane_elems) * s->pix;
+            p->pinned[k] = hipHostRegister((void*)planes[k], bytes, hipHostRegisterDefault) == hipSuccess ? planes[k]
+                                                                                                        : nullptr;
+            (void)hipGetLastError();
+        }
     if (rows_final > p->rows_up)
     {
         // plane rows of CTU rows [rows_up, rows_final): the top margin goes with row 0, the bottom
-        // margin (and the rows of a partial last CTU row) with the last row
-        const int64_t r0 = p->rows_up == 0 ? 0 : s->cfg.margin_y + (int64_t)p->rows_up * s->cfg.ctu_size;
-        const int64_t r1 = rows_final == s->cfg.ctu_rows ? s->rows
-                                                         : s->cfg.margin_y + (int64_t)rows_final * s->cfg.ctu_size;
-        const size_t off = (size_t)(r0 * s->cfg.stride) * s->pix, bytes = (size_t)((r1 - r0) * s->cfg.stride) * s->pix;
+        // margin (and the rows of a partial last CTU row) with the last row; chroma (4:2:0) the same at half
+        // height
         const double t0 = now_s();
-        MES_TRY(hipMemcpyAsync(s->arena + (size_t)p->slot * s->plane_bytes + off, (const uint8_t*)plane_buf + off, bytes,
-                               hipMemcpyHostToDevice, t->st));
+        size_t total = 0;
+        uint8_t* dst = s->arena + (size_t)p->slot * s->slot_elems * s->pix;
+        for (int k = 0; k < np; k++)
+        {
+            const int64_t margin = k ? s->cfg.cmargin_y : s->cfg.margin_y;
+            const int64_t rh = k ? s->cfg.ctu_size / 2 : s->cfg.ctu_size;
+            const int64_t stride = k ? s->cfg.cstride : s->cfg.stride;
+            const int64_t nrows = k ? s->crows : s->rows;
+            const int64_t r0 = p->rows_up == 0 ? 0 : margin + (int64_t)p->rows_up * rh;
+            const int64_t r1 = rows_final == s->cfg.ctu_rows ? nrows : margin + (int64_t)rows_final * rh;
+            const size_t off = (size_t)(r0 * stride) * s->pix, bytes = (size_t)((r1 - r0) * stride) * s->pix;
+            const size_t plane = k == 0 ? 0 : (size_t)(s->cfg.plane_elems + (k - 1) * s->cfg.cplane_elems) * s->pix;
+            MES_TRY(hipMemcpyAsync(dst + plane + off, (const uint8_t*)planes[k] + off, bytes, hipMemcpyHostToDevice,
+                                   t->st));
+            total += bytes;
+        }
         MES_TRY(wait(t));
         p->rows_up = rows_final;
         std::lock_guard<std::mutex> sg(s->smu);
         s->st.uploads++;
-        s->st.upload_bytes += (int64_t)bytes;
+        s->st.upload_bytes += (int64_t)total;
         s->st.upload_ms += 1e3 * (now_s() - t0);
     }
     *slot = p->slot;
     return 0;
+}
+
+extern "C" int x265amd_mes_ref(x265amd_mes* s, const void* key, int64_t gen, const void* plane_buf, int rows_final,
+                               int* slot)
+{
+    if (s && s->cfg.chroma) return record(X265AMD_EINVAL);      // a chroma session needs the chroma planes
+    const void* planes[3] = { plane_buf, nullptr, nullptr };
+    return x265amd_mes_ref420(s, key, gen, planes, rows_final, slot);
 }
 
 extern "C" int x265amd_mes_rows(x265amd_mes* s, const void* key, int64_t gen, int* rows_resident)
@@ -738,12 +880,14 @@ extern "C" int x265amd_mes_table(x265amd_mes* s, const uint16_t* centre, int* in
 }
 
 // ---------------------------------------------------------------- service entries
-extern "C" int x265amd_mes_post(x265amd_mes* s, int w, int h, const void* fenc, intptr_t fenc_stride, int n,
-                                const x265amd_mes_job* jobs, int* ticket)
+extern "C" int x265amd_mes_post420(x265amd_mes* s, int w, int h, const void* fenc, intptr_t fenc_stride,
+                                   const void* fenc_cb, const void* fenc_cr, intptr_t fenc_cstride, int n,
+                                   const x265amd_mes_job* jobs, int* ticket)
 {
     if (!s || !ticket) return record(X265AMD_EINVAL);
     *ticket = -1;
-    if (s->launchers.empty() || n <= 0) return record(X265AMD_EINVAL);
+    if (s->launchers.empty() || n <= 0 || (fenc_cb && (!fenc_cr || !s->cfg.chroma || fenc_cstride < w / 2)))
+        return record(X265AMD_EINVAL);
     if (n > kMaxJobs) return X265AMD_ENOMEM;               // more than a slot holds: search on the host
     MES_TRY(check_jobs(s, w, h, fenc, fenc_stride, n, jobs));
     x265amd_mes_thread* t;
@@ -759,10 +903,21 @@ extern "C" int x265amd_mes_post(x265amd_mes* s, int w, int h, const void* fenc, 
     r.w = w;
     r.h = h;
     r.n = n;
+    r.chroma = fenc_cb != nullptr;
     r.dropped = false;
     r.rc = 0;
     for (int y = 0; y < h; y++)
         memcpy(r.fenc + (size_t)y * w * s->pix, (const uint8_t*)fenc + (size_t)y * fenc_stride * s->pix, (size_t)w * s->pix);
+    if (r.chroma)
+    {
+        // Cb then Cr blocks, packed at stride w / 2, after the luma block
+        const int cw = w / 2, ch = h / 2;
+        uint8_t* c = r.fenc + (size_t)w * h * s->pix;
+        for (int q = 0; q < 2; q++)
+            for (int y = 0; y < ch; y++)
+                memcpy(c + ((size_t)q * cw * ch + (size_t)y * cw) * s->pix,
+                       (const uint8_t*)(q ? fenc_cr : fenc_cb) + (size_t)y * fenc_cstride * s->pix, (size_t)cw * s->pix);
+    }
     memcpy(r.jobs, jobs, sizeof(x265amd_mes_job) * n);
     r.t_post = now_s();
     r.state.store(1, std::memory_order_relaxed);
@@ -772,7 +927,15 @@ extern "C" int x265amd_mes_post(x265amd_mes* s, int w, int h, const void* fenc, 
     }
     s->qcv.notify_one();
     *ticket = k;
+    if (s->trace && s->traced.fetch_add(1) < s->trace)
+        fprintf(stderr, "[mes] post %dx%d n %d chroma %d ticket %d\n", w, h, n, (int)r.chroma, k);
     return 0;
+}
+
+extern "C" int x265amd_mes_post(x265amd_mes* s, int w, int h, const void* fenc, intptr_t fenc_stride, int n,
+                                const x265amd_mes_job* jobs, int* ticket)
+{
+    return x265amd_mes_post420(s, w, h, fenc, fenc_stride, nullptr, nullptr, 0, n, jobs, ticket);
 }
 
 extern "C" int x265amd_mes_wait(x265amd_mes* s, int ticket, int n, x265amd_mes_job* jobs)
@@ -798,6 +961,8 @@ extern "C" int x265amd_mes_wait(x265amd_mes* s, int ticket, int n, x265amd_mes_j
         }
     }
     const double dt = now_s() - t0;
+    if (s->trace && s->traced.fetch_add(1) < s->trace)
+        fprintf(stderr, "[mes] wait ticket %d: %.3f ms%s\n", ticket, 1e3 * dt, slept ? " (slept)" : "");
     for (int i = 0; i < n; i++)
     {
         jobs[i].out_mv[0] = r.jobs[i].out_mv[0];

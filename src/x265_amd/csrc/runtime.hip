@@ -56,3 +56,20 @@ extern "C" const char* x265amd_strerror(int status)
     default: return hipGetErrorString((hipError_t)status);
     }
 }
+
+/* sizeof of a descriptor type of include/x265_amd.h by name (0 if unknown): lets a binding written in
+ * another language (the ctypes structures of src/x265_amd/native.py) check its layouts against the
+ * library's (tests/test_capi.py) */
+extern "C" int x265amd_sizeof(const char* type)
+{
+    if (!type) return 0;
+#define T(name) if (!strcmp(type, #name)) return (int)sizeof(name);
+    T(x265amd_cmp_batch) T(x265amd_interp_batch) T(x265amd_block_batch) T(x265amd_tu_batch)
+    T(x265amd_lowres_batch) T(x265amd_lowres_intra_batch) T(x265amd_lowres_pcost_batch) T(x265amd_lowres_bcost_batch)
+    T(x265amd_la_config) T(x265amd_la_pjob) T(x265amd_la_bjob) T(x265amd_sched_config) T(x265amd_sched_frame)
+    T(x265amd_transfer) T(x265amd_propagate_batch) T(x265amd_weights_batch) T(x265amd_me_batch) T(x265amd_mes_config)
+    T(x265amd_mes_job) T(x265amd_mes_counters) T(x265amd_sao_param) T(x265amd_sao_frame) T(x265amd_sao_stats_frame)
+    T(x265amd_deblock_unit) T(x265amd_deblock_frame) T(x265amd_border_plane)
+#undef T
+    return 0;
+}

@@ -76,7 +76,7 @@ class MeBatch(C.Structure):
                 ("ref_stride", _ip), ("ref_off", _vp), ("mv_range", _vp), ("mvp", _vp), ("mvc", _vp), ("num_cand", _vp),
                 ("mvcost", _vp), ("mvcost_off", _vp), ("out_mv", _vp), ("out_cost", _vp), ("fenc_cb", _vp),
                 ("fenc_cr", _vp), ("fenc_cstride", _ip), ("fenc_coff", _vp), ("ref_cb", _vp), ("ref_cr", _vp),
-                ("ref_cstride", _ip), ("ref_coff", _vp)]
+                ("ref_cstride", _ip), ("ref_coff", _vp), ("eval_count", _vp)]
 
 
 # f4 frame descriptors (include/x265_amd.h): device addresses of the plane origins

@@ -25,6 +25,33 @@ def test_library_exports_every_declared_symbol(native_lib):
     assert not missing, missing
 
 
+def test_ctypes_descriptors_match_the_library(native_lib):
+    """every ctypes descriptor of src/x265_amd/native.py has the size of the C type it mirrors (a field missing
+    on the Python side would let the library read past the structure)"""
+    import sys
+
+    sys.path.insert(0, ROOT)
+    from src.x265_amd import native as N
+
+    lib = ctypes.CDLL(native_lib)
+    lib.x265amd_sizeof.argtypes = [ctypes.c_char_p]
+    pairs = {"CmpBatch": "x265amd_cmp_batch", "BlockBatch": "x265amd_block_batch", "InterpBatch": "x265amd_interp_batch",
+             "TuBatch": "x265amd_tu_batch", "LowresBatch": "x265amd_lowres_batch",
+             "LowresIntraBatch": "x265amd_lowres_intra_batch", "LowresPcostBatch": "x265amd_lowres_pcost_batch",
+             "LowresBcostBatch": "x265amd_lowres_bcost_batch", "MeBatch": "x265amd_me_batch",
+             "SaoFrame": "x265amd_sao_frame", "SaoStatsFrame": "x265amd_sao_stats_frame",
+             "DeblockFrame": "x265amd_deblock_frame", "PropagateBatch": "x265amd_propagate_batch",
+             "WeightsBatch": "x265amd_weights_batch", "BorderPlane": "x265amd_border_plane"}
+    bad = {}
+    for py, c in pairs.items():
+        want = lib.x265amd_sizeof(c.encode())
+        assert want > 0, c
+        got = ctypes.sizeof(getattr(N, py))
+        if got != want:
+            bad[py] = (got, want)
+    assert not bad, bad
+
+
 def test_library_metadata(native_lib):
     lib = ctypes.CDLL(native_lib)
     lib.x265amd_target.restype = ctypes.c_char_p

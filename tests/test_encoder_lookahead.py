@@ -53,11 +53,11 @@ def _source(tmp_path, w, h, frames, depth=8, fade=0.0):
     return path
 
 
-def encode(exe, src, w, h, frames, out, env_extra=None, pools=8, depth=8, extra=(), timeout=900):
+def encode(exe, src, w, h, frames, out, env_extra=None, pools=8, depth=8, extra=(), timeout=900, preset="medium"):
     """run a reference-CLI build; returns (returncode, md5 of the bitstream or None, fps or None, stderr)"""
     env = dict(os.environ, **(env_extra or {}))
     cmd = [exe, "--input", str(src), "--input-res", f"{w}x{h}", "--input-depth", str(depth), "--fps", "30",
-           "--frames", str(frames), "--preset", "medium", "-F", "2", "--pools", str(pools), "--no-info", "-o",
+           "--frames", str(frames), "--preset", preset, "-F", "2", "--pools", str(pools), "--no-info", "-o",
            str(out), *extra]
     if depth > 8:
         cmd += ["--output-depth", str(depth)]

@@ -119,18 +119,19 @@ def test_me_hook_cpu_mode_is_the_reference(tmp_path):
     assert "(reference functions)" in err and got == ref
 
 
-def _gpu_encode_equals_reference(tmp_path, w, h, n, extra_env=None, depth=8, min_area=4096):
+def _gpu_encode_equals_reference(tmp_path, w, h, n, extra_env=None, depth=8, min_area=4096, preset="medium"):
     src = _source(tmp_path, w, h, n, depth=depth)
     if depth == 8:
-        rc, ref, ref_fps, err = encode(_bin("x265ref8"), src, w, h, n, tmp_path / "ref.hevc", pools=16)
+        rc, ref, ref_fps, err = encode(_bin("x265ref8"), src, w, h, n, tmp_path / "ref.hevc", pools=16, preset=preset)
         exe = _bin("x265la8")
     else:
         exe = _bin("x265la10")
         rc, ref, ref_fps, err = encode(exe, src, w, h, n, tmp_path / "ref.hevc",
-                                       {"X265AMD_LOOKAHEAD": "cpu", "X265AMD_ME": "cpu"}, pools=16, depth=10)
+                                       {"X265AMD_LOOKAHEAD": "cpu", "X265AMD_ME": "cpu"}, pools=16, depth=10,
+                                       preset=preset)
     assert rc == 0, err[-2000:]
     env = {"X265AMD_ME_STATS": "1", **(extra_env or {})}
-    rc, got, fps, err = encode(exe, src, w, h, n, tmp_path / "me.hevc", env, pools=16, depth=depth)
+    rc, got, fps, err = encode(exe, src, w, h, n, tmp_path / "me.hevc", env, pools=16, depth=depth, preset=preset)
     assert rc == 0, err[-3000:]
     assert f"[x265me] motion searches of PUs >= {min_area} pixels on the MI355X" in err
     st = _stats(err)
@@ -188,6 +189,35 @@ def test_gpu_me_two_device_sessions_is_bit_exact(tmp_path):
 def test_gpu_me_round4_per_thread_form_is_bit_exact(tmp_path):
     """X265AMD_MES_LAUNCHERS=0: the round-4 form (each worker launching on its own stream, synchronous)"""
     _gpu_encode_equals_reference(tmp_path, 1280, 720, 8, {"X265AMD_MES_LAUNCHERS": "0"})
+
+
+@pytest.mark.gpu
+def test_gpu_me_encode_2160p_slow_is_bit_exact(tmp_path):
+    """BASELINE config 3 (3840x2160 8-bit --preset slow, 64 frames): STAR searches with subme 3, whose sub-pel
+    refine adds the 4:2:0 chroma SATD (motion.cpp:1204-1230) — the chroma session (reference chroma planes
+    resident, the PU's chroma blocks posted with its searches); bitstream identical to the reference"""
+    err = _gpu_encode_equals_reference(tmp_path, 3840, 2160, 64, preset="slow")
+    m = re.search(r"evaluations (\d+) full-pel (\d+) sub-pel", err)
+    assert m and int(m.group(2)) > 0, err[-3000:]
+
+
+@pytest.mark.gpu
+def test_gpu_me_slow_check_mode_chroma_satd(tmp_path):
+    """--preset slow with the 32x32 CUs too, every used device search (chroma SATD included) recomputed on
+    the host: 0 mismatches"""
+    err = _gpu_encode_equals_reference(tmp_path, 1280, 720, 12, {"X265AMD_ME": "check", "X265AMD_ME_MIN": "1024"},
+                                       min_area=1024, preset="slow")
+    m = re.search(r"check: (\d+) mismatching searches", err)
+    assert m and int(m.group(1)) == 0, err[-3000:]
+    m = re.search(r"check: (\d+) search windows beyond", err)
+    assert m and int(m.group(1)) == 0, err[-3000:]
+
+
+@pytest.mark.gpu
+def test_gpu_me_encode_2160p_main10_is_bit_exact(tmp_path):
+    """BASELINE config 5 (3840x2160 Main10 --preset medium, 64 frames): the 16-bit lookahead and search
+    kernels behind the same hooks, against the same binary's reference functions"""
+    _gpu_encode_equals_reference(tmp_path, 3840, 2160, 64, depth=10)
 
 
 @pytest.mark.gpu
