@@ -506,7 +506,7 @@ void launcher_main(x265amd_mes* s, x265amd_mes_launcher* L)
                     order.push_back(r);
                     p++;
                 }
-                x265amd_mes_stage sub{ L->g.dev + base[k], L->g.host + base[k], Ly.end };
+                x265amd_mes_stage sub{ L->g.dev + base[k], L->g.host + base[k], nullptr, Ly.end };
                 bt.push_back(make_batch(s, sub, Ly, w, h, i, w));
                 if (kh < 0) chroma_batch(s, sub, Ly, w, h, p, bt.back());
                 bt.back().eval_count = (uint32_t*)(sub.dev + Ly.evals);

@@ -555,8 +555,8 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_tr32_i8(int n, int depth,
     }
 }
 
-// the integer-MFMA 32x32 transforms, default (X265AMD_TR_I8=0 selects the f16 split form; measured,
-// profiles/r04/tr32_i8_ab.txt: dct / idct 32x32 0.49 / 0.51 -> 0.61 / 0.60 of the HBM peak)
+// the integer-MFMA 16x16 (round 5) and 32x32 transforms, default (X265AMD_TR_I8=0 selects the f16 split
+// forms; measured, profiles/r04/tr32_i8_ab.txt: dct / idct 32x32 0.49 / 0.51 -> 0.61 / 0.60 of the HBM peak)
 static bool tr_i8()
 {
     static int v = -1;
@@ -675,6 +675,144 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_tr16_mfma(int n, int depth,
             {
                 const int a = (int)hi[b][i] * 1024 + (int)lo[b][i];
                 T[(4 * q + i) * 16 + r] = (int16_t)(FWD ? fwd_round(a, sh2) : inv_round(a, sh2));
+            }
+            wave_sync();
+            if (job0 + b < n) stu<uint2>(d[b] + io_row * ds + io_col, ldu<uint2>(&T[io_row * 16 + io_col]));
+        }
+        wave_sync();                                 // tiles read out before the next iteration rewrites them
+    }
+}
+
+
+// ---------------------------------------------------------------------------------------------
+// k_tr16_i8 (round 5): the 16x16 products on the integer matrix cores, v_mfma_i32_16x16x32_i8 (A lane l:
+// row l & 15, k slots 8q .. 8q + 7 with q = l >> 4; B lane l: column l & 15, the same slots; D lane l:
+// column l & 15, rows 4q .. 4q + 3).  A 16-point transform has K = 16, so each lane fills slots
+// 8q .. 8q + 3 with k = 4q .. 4q + 3 and leaves 8q + 4 .. 8q + 7 zero (the order only has to agree between
+// the two operands): then a lane's four data values are exactly the four accumulator rows it holds from the
+// previous stage — forward stage 2 takes the stage-1 tile as it lies, with no data movement — and its four
+// constant values are one dword (the other dword of the 64-bit operand is zero).  Every int16 operand is
+// split into bytes as in k_tr32_i8 (x = 256 hi + lo, lo entering as lo - 128, the bias 128 x the constant
+// sums folded into the rounding offsets), recombined with one v_lshl_add per element.  JB transforms per
+// wave iteration, software-pipelined loads, LDS tiles for the column sides, as k_tr16_mfma.
+template <bool FWD>
+__global__ __launch_bounds__(X265AMD_BLOCK) void k_tr16_i8(int n, int depth,
+    const int16_t* __restrict__ src, intptr_t ss, const int64_t* __restrict__ soff,
+    int16_t* __restrict__ dst, intptr_t ds, const int64_t* __restrict__ doff)
+{
+    constexpr int JB = 4;
+    __shared__ int16_t tile[kTrWaves][JB][16 * 16];
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63, r = l & 15, q = l >> 4;
+    const int sh1 = FWD ? 3 + depth - 8 : 7, sh2 = FWD ? 10 : 12 - (depth - 8);
+    const int io_row = l >> 2, io_col = 4 * (l & 3);  // 8-byte I/O: four lanes per row
+
+    // the constant operand (both stages use the same fragment, as in k_tr16_mfma): forward T[r][4q + j],
+    // inverse T[4q + j][r] (T = the 16-point matrix, rows of the 32-point one at even indices)
+    uint32_t tc = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++)
+        tc |= (uint32_t)(uint8_t)(int8_t)(FWD ? c_t32.m[2 * r][4 * q + j] : c_t32.m[2 * (4 * q + j)][r]) << (8 * j);
+    const long cop = (long)(uint64_t)tc;
+    // bias of the biased lo plane: 128 x the sum of the constant over k — forward: the row sums of T
+    // (64 x 16 for row 0, 0 for the others), at output column r (stage 1) / output row 4q + i (stage 2);
+    // inverse: the column sums of T at output column r, both stages
+    int csum = 0;
+#pragma unroll
+    for (int k = 0; k < 16; k++) csum += c_t32.m[2 * k][r];
+    const int k1 = (FWD ? (r == 0 ? 128 * 64 * 16 : 0) : 128 * csum) + (1 << (sh1 - 1));
+    const int k2 = FWD ? (1 << (sh2 - 1)) : 128 * csum + (1 << (sh2 - 1));
+    const int k20 = FWD && q == 0 ? 128 * 64 * 16 : 0;   // forward stage 2: row 0 (register 0 of quarter 0)
+
+    const int64_t step = (int64_t)gridDim.x * kTrWaves * JB;
+    int64_t job0 = ((int64_t)blockIdx.x * kTrWaves + w) * JB;
+    uint2 nx[JB];
+    auto fetch = [&](int64_t j0) {
+#pragma unroll
+        for (int b = 0; b < JB; b++)
+        {
+            const int64_t job = j0 + b < n ? j0 + b : j0;   // a tail repeats the first (its result is not stored)
+            const int16_t* sp = src + soff[job];
+            nx[b] = FWD ? ldu<uint2>(sp + r * ss + 4 * q) : ldu<uint2>(sp + io_row * ss + io_col);
+        }
+    };
+    // the two byte planes of 4 int16 values (2 packed pairs) as 64-bit MFMA operands (upper dword zero)
+    auto planes = [](uint32_t u0, uint32_t u1, long& lo, long& hi) {
+        lo = (long)(uint64_t)(__builtin_amdgcn_perm(u1, u0, 0x06040200u) ^ 0x80808080u);
+        hi = (long)(uint64_t)__builtin_amdgcn_perm(u1, u0, 0x07050301u);
+    };
+    if (job0 < n) fetch(job0);
+    for (; job0 < n; job0 += step)
+    {
+        int16_t* d[JB];
+        uint2 cx[JB];
+#pragma unroll
+        for (int b = 0; b < JB; b++)
+        {
+            cx[b] = nx[b];
+            d[b] = dst + doff[job0 + b < n ? job0 + b : job0];
+        }
+        if (job0 + step < n) fetch(job0 + step);
+        if constexpr (!FWD)
+        {
+#pragma unroll
+            for (int b = 0; b < JB; b++) stu<uint2>(&tile[w][b][io_row * 16 + io_col], cx[b]);
+            wave_sync();
+        }
+        i32x4 lo[JB], hi[JB];
+#pragma unroll
+        for (int b = 0; b < JB; b++)
+        {
+            uint32_t u0, u1;
+            if constexpr (FWD)
+            {
+                u0 = cx[b].x;
+                u1 = cx[b].y;
+            }
+            else
+            {
+                u0 = pack16(tile[w][b][(4 * q) * 16 + r], tile[w][b][(4 * q + 1) * 16 + r]);
+                u1 = pack16(tile[w][b][(4 * q + 2) * 16 + r], tile[w][b][(4 * q + 3) * 16 + r]);
+            }
+            long xl, xh;
+            planes(u0, u1, xl, xh);
+            // forward stage 1: U = X T^T (A = the source row, B = T^T); inverse: C^T T (A = the coefficient
+            // column, B = T)
+            lo[b] = __builtin_amdgcn_mfma_i32_16x16x32_i8(xl, cop, i32x4{}, 0, 0, 0);
+            hi[b] = __builtin_amdgcn_mfma_i32_16x16x32_i8(xh, cop, i32x4{}, 0, 0, 0);
+        }
+#pragma unroll
+        for (int b = 0; b < JB; b++)
+        {
+            int x[4];
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+            {
+                const int a = (int)(((uint32_t)hi[b][i] << 8) + (uint32_t)lo[b][i]) + k1;
+                x[i] = FWD ? (a >> sh1) : clip16(a >> sh1);   // forward: the int16 wrap is the byte split
+            }
+            long xl, xh;
+            planes(pack16(x[0], x[1]), pack16(x[2], x[3]), xl, xh);
+            if constexpr (FWD)
+            {
+                // Y = T U: A = T (row r, k = 4q + j), B = the stage-1 tile as it lies
+                lo[b] = __builtin_amdgcn_mfma_i32_16x16x32_i8(cop, xl, i32x4{}, 0, 0, 0);
+                hi[b] = __builtin_amdgcn_mfma_i32_16x16x32_i8(cop, xh, i32x4{}, 0, 0, 0);
+            }
+            else
+            {
+                lo[b] = __builtin_amdgcn_mfma_i32_16x16x32_i8(xl, cop, i32x4{}, 0, 0, 0);
+                hi[b] = __builtin_amdgcn_mfma_i32_16x16x32_i8(xh, cop, i32x4{}, 0, 0, 0);
+            }
+        }
+#pragma unroll
+        for (int b = 0; b < JB; b++)
+        {
+            int16_t* T = tile[w][b];
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+            {
+                const int a = (int)(((uint32_t)hi[b][i] << 8) + (uint32_t)lo[b][i]) + k2 + (i == 0 ? k20 : 0);
+                T[(4 * q + i) * 16 + r] = (int16_t)(FWD ? (a >> sh2) : clip16(a >> sh2));
             }
             wave_sync();
             if (job0 + b < n) stu<uint2>(d[b] + io_row * ds + io_col, ldu<uint2>(&T[io_row * 16 + io_col]));
@@ -1084,6 +1222,7 @@ extern "C" int x265amd_transform(int kind, int depth, int size, int n,
 #define M(K) hipLaunchKernelGGL(K, grid, dim3(X265AMD_BLOCK), 0, st, n, depth, src, src_stride, src_off, dst, dst_stride, dst_off)
         if (size == 32 && tr_i8()) { if (fwd) M(k_tr32_i8<true>); else M(k_tr32_i8<false>); }
         else if (size == 32) { if (fwd) M(k_tr32_mfma<true>); else M(k_tr32_mfma<false>); }
+        else if (tr_i8()) { if (fwd) M(k_tr16_i8<true>); else M(k_tr16_i8<false>); }
         else { if (fwd) M(k_tr16_mfma<true>); else M(k_tr16_mfma<false>); }
 #undef M
         return (int)hipGetLastError();

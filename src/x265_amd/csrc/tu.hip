@@ -137,15 +137,19 @@ __device__ __forceinline__ void sbh_pick(const int (&qv)[16], const int (&cv)[16
         const int c = cv[n], q = qv[n];
         const int tmp = (c < 0 ? -c : c) * qscale;
         const int du = (tmp - (((tmp + qadd) >> qbits) << qbits)) >> qbits8;   // deltaU (quant_c)
-        const bool below = (mask & ((1u << n) - 1)) != 0;   // a significant coefficient before n
-        const bool one = q == 1 || q == -1;
+        // every condition as a 0/1 integer combined with bitwise operators: straight-line selects (the
+        // short-circuit form compiled to a branch per term and candidate)
+        const int below = (mask & ((1u << n) - 1)) != 0;    // a significant coefficient before n
+        const int nz = q != 0;
+        const int one = (q == 1) | (q == -1);
+        const int dneg = du <= 0;
         const int adu = du < 0 ? -du : du;
         // significant: +1 if deltaU > 0, else -1 (never zeroing the first significant one)
         // not significant: +1 (before the first significant one only with the matching sign)
-        const bool blocked = q ? (!below && one && du <= 0) : (!below && (int)(c < 0) != signbit);
-        const int cost = blocked ? 0x7fffffff : (q ? -adu : -du);
-        const int ch = (q && du <= 0) ? -1 : 1;
-        const bool take = n <= top && cost < min_cost;
+        const int blocked = (nz & (below ^ 1) & one & dneg) | ((nz ^ 1) & (below ^ 1) & ((int)(c < 0) ^ signbit));
+        const int cost = blocked ? 0x7fffffff : (nz ? -adu : -du);
+        const int ch = (nz & dneg) ? -1 : 1;
+        const int take = (n <= top) & (cost < min_cost);
         min_cost = take ? cost : min_cost;
         change = take ? ch : change;
         min_n = take ? n : min_n;
@@ -227,6 +231,56 @@ __device__ __forceinline__ int sign_hide(int16_t* Q, const int16_t* C, const uin
     return group_sum<G>(dsig);
 }
 
+// sign_hide as straight-line code (round 5): every lane of every TU group runs the candidate search and the
+// decision is a predicate on the one store — the TUs of a wave (8 or 4 groups) take different branches of
+// sign_hide (no hiding / parity already right / a CG past the last), which the branchy form executes one
+// after another with exec-mask juggling.  `active` = the TU wants hiding (sign_hide && numSig >= 2).
+template <int N, int G>
+__device__ __forceinline__ int sign_hide_bf(int16_t* Q, const int16_t* C, const uint16_t* scan, int type, int lane,
+                                            int qscale, int qadd, int qbits, bool active)
+{
+    constexpr int NCG = N * N / 16;
+    static_assert(NCG <= G, "one coefficient group per lane");
+    const bool has = lane < NCG;
+    const int cg = has ? lane : 0;
+    const int corner = scan[cg * 16];
+    int qv[16], cv[16];
+    uint32_t mask = 0;
+    int sum = 0;
+#pragma unroll
+    for (int n = 0; n < 16; n++)
+    {
+        const int o = corner + cg_offset<N>(type, n);
+        qv[n] = Q[o];
+        cv[n] = C[o];
+        mask |= (uint32_t)(qv[n] != 0) << n;
+        sum += qv[n];
+    }
+    if (!has || !active) mask = 0;
+    const int last = group_max<G>(mask ? cg * 16 + 31 - __builtin_clz(mask) : -1);
+    const int first = __builtin_ctz(mask | 0x10000), lastnz = 31 - __builtin_clz(mask | 1);
+    int fq = 0;
+#pragma unroll
+    for (int n = 0; n < 16; n++) fq = n == first ? qv[n] : fq;
+    const int signbit = fq > 0 ? 0 : 1;
+    const bool go = mask && cg <= (last >> 4) && lastnz - first >= 4 && signbit != (sum & 1);
+    const int top = cg == (last >> 4) ? (last & 15) : 15;
+    int min_n, change;
+    sbh_pick(qv, cv, mask, top, signbit, qscale, qadd, qbits, min_n, change);
+    int qm = 0, cm = 0;
+#pragma unroll
+    for (int n = 0; n < 16; n++)
+    {
+        qm = n == min_n ? qv[n] : qm;
+        cm = n == min_n ? cv[n] : cm;
+    }
+    change = (qm == 32767 || qm == -32768) ? -1 : change;
+    const int dsig = !go ? 0 : !qm ? 1 : (change == -1 && (qm == 1 || qm == -1)) ? -1 : 0;
+    const int sm = cm < 0 ? -1 : 0;
+    if (go) Q[corner + cg_offset<N>(type, min_n)] = (int16_t)(qm + ((change ^ sm) - sm));
+    return group_sum<G>(dsig);
+}
+
 template <typename P, int N>
 __device__ __forceinline__ void load_n(const P* p, int (&o)[N])
 {
@@ -277,7 +331,11 @@ struct TuArgs
     int n, is_luma, is_intra, i_slice, sign_hide, depth;
 };
 
-template <typename P, int N>
+// BF (round 5, default): sign hiding and the reconstruction as straight-line code — every TU group of a
+// wave computes the full inverse and the sign-hiding search, the uncoded / DC-only / coded cases are
+// selects (the DC-only shortcut, quant.cpp:526-538, equals the full inverse of a DC-only block; it is kept
+// as its own select all the same)
+template <typename P, int N, bool BF = false>
 __global__ __launch_bounds__(X265AMD_BLOCK) void k_tu(const TuArgs a)
 {
     constexpr int LOG2 = N == 4 ? 2 : N == 8 ? 3 : N == 16 ? 4 : 5;
@@ -350,7 +408,18 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_tu(const TuArgs a)
     int num_sig = group_sum<N>(cnt);
 
     // ---- sign-bit hiding (signBitHidingHDQ): one coefficient group per lane
-    if (a.sign_hide && num_sig >= 2)
+    if constexpr (BF)
+    {
+        if (a.sign_hide)
+        {
+            wave_sync();
+            const int st = a.scan ? a.scan[j] : 0;
+            const uint16_t* scan = N == 4 ? c_scan.s4[st] : N == 8 ? c_scan.s8[st] : N == 16 ? c_scan.s16 : c_scan.s32;
+            num_sig += sign_hide_bf<N, N>(Q, T, scan, st, r, qscale, qadd, qbits, num_sig >= 2);
+            wave_sync();
+        }
+    }
+    else if (a.sign_hide && num_sig >= 2)
     {
         wave_sync();
         const int st = a.scan ? a.scan[j] : 0;
@@ -377,7 +446,42 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_tu(const TuArgs a)
     int f[N], p[N], res[N];
 #pragma unroll
     for (int i = 0; i < N; i++) { f[i] = frow.get(i); p[i] = prow.get(i); }
-    if (num_sig == 0)
+    if constexpr (BF)
+    {
+        const int scale = inv_quant_scale(rem) << per;
+        const int dsh = 20 - 14 - tshift;
+        const int dadd = 1 << (dsh - 1);
+        const int q0 = Q[0];
+        int c[N];
+#pragma unroll
+        for (int k = 0; k < N; k++) c[k] = clip16((Q[k * N + r] * scale + dadd) >> dsh);
+        if constexpr (N == 4)
+        {
+            if (use_dst) dst_inv(c, y); else inv_1d<4>(c, y);
+        }
+        else
+            inv_1d<N>(c, y);
+#pragma unroll
+        for (int k = 0; k < N; k++) T[r * PT + k] = (int16_t)inv_round(y[k], 7);
+        wave_sync();
+#pragma unroll
+        for (int k = 0; k < N; k++) c[k] = T[k * PT + r];
+        if constexpr (N == 4)
+        {
+            if (use_dst) dst_inv(c, y); else inv_1d<4>(c, y);
+        }
+        else
+            inv_1d<N>(c, y);
+        const int ish2 = 12 - (depth - 8);
+        const int dq0 = clip16((q0 * scale + dadd) >> dsh);
+        const int sh2 = 12 - (depth - 8) - 3;
+        const int dc = (int16_t)((((dq0 + 1) >> 1) * 8 + (1 << (sh2 - 1))) >> sh2);
+        const bool dconly = num_sig == 1 && q0 != 0 && !use_dst;
+#pragma unroll
+        for (int k = 0; k < N; k++)
+            res[k] = num_sig == 0 ? f[k] - p[k] : dconly ? dc : inv_round(y[k], ish2);
+    }
+    else if (num_sig == 0)
     {
 #pragma unroll
         for (int i = 0; i < N; i++) res[i] = f[i] - p[i];
@@ -542,9 +646,9 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_tu32_mfma(const TuArgs a)
         }
         int num_sig = group_sum<64>(cnt);
         wave_sync();
-        if (a.sign_hide && num_sig >= 2)
+        if (a.sign_hide && num_sig >= 2)             // wave-uniform: one TU per wave
         {
-            num_sig += sign_hide<32, 64>(Q, Cs, c_scan.s32, 0, l, qscale, qadd, qbits);
+            num_sig += sign_hide_bf<32, 64>(Q, Cs, c_scan.s32, 0, l, qscale, qadd, qbits, true);
             wave_sync();
         }
 
@@ -745,9 +849,9 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_tu32_i8(const TuArgs a)
         }
         int num_sig = group_sum<64>(cnt);
         wave_sync();
-        if (a.sign_hide && num_sig >= 2)
+        if (a.sign_hide && num_sig >= 2)             // wave-uniform: one TU per wave
         {
-            num_sig += sign_hide<32, 64>(Q, Cs, c_scan.s32, 0, l, qscale, qadd, qbits);
+            num_sig += sign_hide_bf<32, 64>(Q, Cs, c_scan.s32, 0, l, qscale, qadd, qbits, true);
             wave_sync();
         }
 
@@ -994,6 +1098,18 @@ static bool tu_i8()
     return v != 0;
 }
 
+// the straight-line 8x8 / 16x16 form (k_tu<.., true>); X265AMD_TU_BF=0 selects the branchy round-4 form
+static bool tu_bf()
+{
+    static int v = -1;
+    if (v < 0)
+    {
+        const char* e = getenv("X265AMD_TU_BF");
+        v = e ? atoi(e) != 0 : 1;
+    }
+    return v != 0;
+}
+
 template <typename P>
 static int launch_tu(int log2, const TuArgs& a, hipStream_t st)
 {
@@ -1005,8 +1121,14 @@ static int launch_tu(int log2, const TuArgs& a, hipStream_t st)
         hipLaunchKernelGGL((k_tu4<P>), dim3((uint32_t)((a.n + X265AMD_BLOCK - 1) / X265AMD_BLOCK)), dim3(X265AMD_BLOCK),
                            0, st, a);
         break;
-    case 3: hipLaunchKernelGGL((k_tu<P, 8>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, a); break;
-    case 4: hipLaunchKernelGGL((k_tu<P, 16>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, a); break;
+    case 3:
+        if (tu_bf()) hipLaunchKernelGGL((k_tu<P, 8, true>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, a);
+        else hipLaunchKernelGGL((k_tu<P, 8>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, a);
+        break;
+    case 4:
+        if (tu_bf()) hipLaunchKernelGGL((k_tu<P, 16, true>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, a);
+        else hipLaunchKernelGGL((k_tu<P, 16>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, a);
+        break;
     case 5:
     {
         // one wavefront per TU, enough waves to fill the chip, each looping over TUs

@@ -1,10 +1,16 @@
-# round 5: (1) where the --preset slow check mismatches come from — STAR alone, subme 3 (chroma SATD) alone,
-# slow with subme 2 — in check mode at 720p; (2) launch-service latency options at 2160p medium 64 frames:
-# high-priority launch streams, zero-copy staging (the kernel reads / writes the pinned staging), polling
-# launchers, interleaved
+# round 5: (0) parity of the rewritten kernels (fused TU straight-line form, re-applied interpolation / intra
+# rewrites, the search kernel's evaluation counts); (1) where the --preset slow check mismatches come from —
+# STAR alone, subme 3 (chroma SATD) alone, slow with subme 2 — in check mode at 720p; (2) launch-service
+# latency options at 2160p medium 64 frames: high-priority launch streams, zero-copy staging, polling
+# launchers, interleaved; (3) kernel-roofline A/Bs: fused TU straight-line vs branchy, 16x16 DCT on the int8
+# matrix cores vs the f16 split, intra against the round-4 kernels
 set -o pipefail
 mkdir -p gpurun_out/r05
 export TMPDIR=/tmp
+timeout -k 10 400 python3 -u -m pytest tests/test_tu.py tests/test_me.py tests/test_gpu_parity.py -m gpu -x -q \
+    --timeout 300 --timeout-method thread -k "not fullsize" > gpurun_out/r05/c_parity.log 2>&1 \
+    || { grep -E "FAILED|Error" gpurun_out/r05/c_parity.log | head; tail -20 gpurun_out/r05/c_parity.log; exit 1; }
+echo "parity: $(tail -1 gpurun_out/r05/c_parity.log)"
 python3 -c "
 from src.x265_amd.synth import SyntheticSource
 SyntheticSource(1280, 720, 16, 8).write_yuv('/tmp/s720.yuv')
@@ -27,3 +33,28 @@ for rep in 1 2; do
     grep -E "worker time|service" /tmp/e.txt | tee -a gpurun_out/r05/c_service_ab.txt
   done
 done
+for rep in 1 2; do
+  for bf in 0 1; do
+    echo "== X265AMD_TU_BF=$bf rep=$rep" | tee -a gpurun_out/r05/c_tu_bf_ab.txt
+    X265AMD_TU_BF=$bf timeout -k 10 200 python3 -u tools/kernel_roofline.py --only tu_pipeline 2>/dev/null | grep "{" | cut -c1-200 \
+        | tee -a gpurun_out/r05/c_tu_bf_ab.txt || exit 1
+  done
+done
+for rep in 1 2; do
+  for i8 in 0 1; do
+    echo "== X265AMD_TR_I8=$i8 rep=$rep" | tee -a gpurun_out/r05/c_tr16_i8_ab.txt
+    X265AMD_TR_I8=$i8 timeout -k 10 200 python3 -u tools/kernel_roofline.py --only dct_16x16,idct_16x16,dct_32x32,idct_32x32 2>/dev/null \
+        | grep "{" | cut -c1-200 | tee -a gpurun_out/r05/c_tr16_i8_ab.txt || exit 1
+  done
+done
+ONLY=intra_ang_4,intra_ang_8,intra_ang_16,intra_ang_32
+for rep in 1 2; do
+  for v in r4 cur; do
+    unset X265AMD_LIB
+    [ $v = r4 ] && export X265AMD_LIB=$PWD/src/x265_amd/ab/libx265amd_r4.so
+    echo "== $v rep=$rep" | tee -a gpurun_out/r05/c_intra_ab.txt
+    timeout -k 10 300 python3 -u tools/kernel_roofline.py --only "$ONLY" 2>/dev/null | grep "{" | cut -c1-170 \
+        | tee -a gpurun_out/r05/c_intra_ab.txt || exit 1
+  done
+done
+unset X265AMD_LIB
