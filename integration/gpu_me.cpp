@@ -504,10 +504,12 @@ int form_searches(Search& S, Mode& interMode, const PredictionUnit& pu, const ui
                 {
                     /* the rows this search can read (its full-pel range, the PU, the 8-tap filter reach and the
                      * sub-pel refine's pixel beyond the range) must be resident on the device: a search never
-                     * reads a row a later upload would still change */
+                     * reads a row a later upload would still change.  STAR costs points level with an
+                     * out-of-range origin (MV 0), so its lowest row is at least the PU's own */
                     const int ctu = (int)g_maxCUSize;
                     const int last_y = (int)pu.ctuAddr / (int)S.m_frame->m_encData->m_slice->m_sps->numCuInWidth * ctu +
-                                       (int)g_zscanToPelY[pu.cuAbsPartIdx + pu.puAbsPartIdx] + e.mvmax.y + pu.height + 4 + 1;
+                                       (int)g_zscanToPelY[pu.cuAbsPartIdx + pu.puAbsPartIdx] +
+                                       (e.mvmax.y > 0 ? e.mvmax.y : 0) + pu.height + 4 + 1;
                     const int rows_needed = last_y < 0 ? 0 : (last_y + ctu - 1) / ctu;
                     const int nrows = (int)((mr.reconPic->m_picHeight + ctu - 1) / ctu);
                     int resident = 0;

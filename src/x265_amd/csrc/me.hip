@@ -289,133 +289,201 @@ __device__ __forceinline__ int chroma_satd(const MeState<P>& s, int qx, int qy)
     return acc;
 }
 
+// One row of a unit's reference window kept packed as loaded: C = 4 pixels (full-pel columns) or 11
+// (the 8-tap reach, -3 .. +7): an 8-pixel vector and the 4 pixels from +7 (overlapping by one).
+template <typename P, int C>
+struct RawRow
+{
+    static constexpr int WA = (C == 4 ? 4 : 8) * (int)sizeof(P) / 4;
+    static constexpr int WB = C == 4 ? 0 : (int)sizeof(P);
+    uint32_t a[WA];
+    uint32_t b[WB > 0 ? WB : 1];
+    __device__ __forceinline__ void load(const P* p)
+    {
+        if constexpr (WA == 1) a[0] = ldu<uint32_t>(p);
+        else if constexpr (WA == 2) { const uint2 v = ldu<uint2>(p); a[0] = v.x; a[1] = v.y; }
+        else { const uint4 v = ldu<uint4>(p); a[0] = v.x; a[1] = v.y; a[2] = v.z; a[3] = v.w; }
+        if constexpr (WB == 1) b[0] = ldu<uint32_t>(p + 7);
+        else if constexpr (WB == 2) { const uint2 v = ldu<uint2>(p + 7); b[0] = v.x; b[1] = v.y; }
+    }
+    __device__ __forceinline__ int get(int i) const
+    {
+        const uint32_t* w = a;
+        if (C == 11 && i >= 8) { w = b; i -= 7; }
+        if constexpr (sizeof(P) == 1) return (int)((w[i >> 2] >> (8 * (i & 3))) & 0xff);
+        else return (int)((w[i >> 1] >> (16 * (i & 1))) & 0xffff);
+    }
+};
+
+// subpelCompare's luma part over this lane's units for one fractional case (CASE bit 0: horizontal
+// fraction, bit 1: vertical): the reference windows (and source rows) of KU units are all loaded before
+// the first is filtered, so a candidate costs one memory round trip per KU units, not one per unit.
+// Units past the lane's count load unit 0's window again (cache hits) and are not summed.
+template <typename P, int CASE, int KU>
+__device__ __forceinline__ int subpel_units(const MeState<P>& s, const P* base, const int (&cx)[8],
+                                            const int (&cy)[8], bool satd)
+{
+    constexpr int R = (CASE & 2) ? 11 : 4, C = (CASE & 1) ? 11 : 4;
+    const int maxv = (1 << s.a->depth) - 1;
+    const int head = 14 - s.a->depth;
+    const int64_t rs = s.rs, fs = s.fs;
+    int acc = 0;
+    for (int k0 = 0; k0 < s.nu; k0 += KU)
+    {
+        RawRow<P, C> win[KU][R];
+        uint32_t fe[KU][4][sizeof(P) == 1 ? 1 : 2];
+#pragma unroll
+        for (int k = 0; k < KU; k++)
+        {
+            int ux, uy;
+            s.unit_xy(k0 + k < s.nu ? k0 + k : k0, ux, uy);
+            const P* p = base + ux + (int64_t)uy * rs - ((CASE & 2) ? 3 * rs : 0) - ((CASE & 1) ? 3 : 0);
+#pragma unroll
+            for (int r = 0; r < R; r++) win[k][r].load(p + r * rs);
+#pragma unroll
+            for (int r = 0; r < 4; r++) load4<P>(s.fenc + ux + (int64_t)(uy + r) * fs, fe[k][r]);
+        }
+#pragma unroll
+        for (int k = 0; k < KU; k++)
+        {
+            int blk[4][4];
+            if constexpr (CASE == 0)
+            {
+#pragma unroll
+                for (int r = 0; r < 4; r++)
+#pragma unroll
+                    for (int c = 0; c < 4; c++) blk[r][c] = win[k][r].get(c);
+            }
+            else if constexpr (CASE == 1)
+            {
+                // interp_horiz_pp: (int16)((sum + 32) >> 6) clipped
+#pragma unroll
+                for (int r = 0; r < 4; r++)
+#pragma unroll
+                    for (int c = 0; c < 4; c++)
+                    {
+                        int sum = 0;
+#pragma unroll
+                        for (int t = 0; t < 8; t++) sum += cx[t] * win[k][r].get(c + t);
+                        const int val = (int16_t)((sum + 32) >> 6);
+                        blk[r][c] = val < 0 ? 0 : (val > maxv ? maxv : val);
+                    }
+            }
+            else if constexpr (CASE == 2)
+            {
+                // interp_vert_pp
+#pragma unroll
+                for (int r = 0; r < 4; r++)
+#pragma unroll
+                    for (int c = 0; c < 4; c++)
+                    {
+                        int sum = 0;
+#pragma unroll
+                        for (int t = 0; t < 8; t++) sum += cy[t] * win[k][r + t].get(c);
+                        const int val = (int16_t)((sum + 32) >> 6);
+                        blk[r][c] = val < 0 ? 0 : (val > maxv ? maxv : val);
+                    }
+            }
+            else
+            {
+                // interp_hv_pp: horizontal ps over 11 rows (int16), then vertical sp
+                const int ps_shift = 6 - head, ps_off = -8192 * (1 << ps_shift);
+                const int sp_shift = 6 + head, sp_off = (1 << (sp_shift - 1)) + (8192 << 6);
+                int m[11][4];
+#pragma unroll
+                for (int i = 0; i < 11; i++)
+#pragma unroll
+                    for (int c = 0; c < 4; c++)
+                    {
+                        int sum = 0;
+#pragma unroll
+                        for (int t = 0; t < 8; t++) sum += cx[t] * win[k][i].get(c + t);
+                        m[i][c] = (int16_t)((sum + ps_off) >> ps_shift);
+                    }
+#pragma unroll
+                for (int r = 0; r < 4; r++)
+#pragma unroll
+                    for (int c = 0; c < 4; c++)
+                    {
+                        int sum = 0;
+#pragma unroll
+                        for (int t = 0; t < 8; t++) sum += cy[t] * m[r + t][c];
+                        const int val = (int16_t)((sum + sp_off) >> sp_shift);
+                        blk[r][c] = val < 0 ? 0 : (val > maxv ? maxv : val);
+                    }
+            }
+            int cost = 0;
+            if (satd)
+            {
+                int d[4][4];
+#pragma unroll
+                for (int r = 0; r < 4; r++)
+#pragma unroll
+                    for (int c = 0; c < 4; c++) d[r][c] = px<P>(fe[k][r], c) - blk[r][c];
+#pragma unroll
+                for (int r = 0; r < 4; r++) had4m(d[r][0], d[r][1], d[r][2], d[r][3]);
+                int sum = 0;
+#pragma unroll
+                for (int c = 0; c < 4; c++)
+                {
+                    had4m(d[0][c], d[1][c], d[2][c], d[3][c]);
+#pragma unroll
+                    for (int r = 0; r < 4; r++) sum += d[r][c] < 0 ? -d[r][c] : d[r][c];
+                }
+                cost = sum >> 1;      // each 4x4 raw sum is even (SURVEY note a7): any tiling gives satd
+            }
+            else
+            {
+#pragma unroll
+                for (int r = 0; r < 4; r++)
+#pragma unroll
+                    for (int c = 0; c < 4; c++)
+                    {
+                        const int d = px<P>(fe[k][r], c) - blk[r][c];
+                        cost += d < 0 ? -d : d;
+                    }
+            }
+            if (k0 + k < s.nu) acc += cost;
+        }
+    }
+    return acc;
+}
+
 // subpelCompare (motion.cpp:1174-1203): the block at quarter-pel (qx, qy), built by
-// luma_hpp / luma_vpp / luma_hvpp when fractional, compared with SAD or SATD
+// luma_hpp / luma_vpp / luma_hvpp when fractional, compared with SAD or SATD.  8-bit windows of all
+// (at most 4) units of a lane fit in registers; at 16 bits two units go per round trip.
 template <typename P, int G>
 __device__ __noinline__ int subpel_cost(const MeState<P>& s, int qx, int qy, bool satd)
 {
     const int xf = qx & 3, yf = qy & 3;
     s.nsp++;
     const P* base = s.ref + (qx >> 2) + (int64_t)(qy >> 2) * s.rs;
-    const int maxv = (1 << s.a->depth) - 1;
-    const int head = 14 - s.a->depth;
     int cx[8], cy[8];
 #pragma unroll
     for (int t = 0; t < 8; t++) { cx[t] = c_luma.c[xf][t]; cy[t] = c_luma.c[yf][t]; }
-    int acc = 0;
-    for (int k = 0; k < s.nu; k++)
+    // units per lane: 1 below 64 units, 2 for 64x32 / 32x64, 4 for 64x64 (uniform over the batch)
+    const int nmax = (s.uw * (s.a->h >> 2) + s.G - 1) / s.G;
+    int acc;
+    if (nmax == 1)
     {
-        int ux, uy;
-        s.unit_xy(k, ux, uy);
-        const P* p = base + ux + (int64_t)uy * s.rs;
-        int blk[4][4];
-        if (!(xf | yf))
-        {
-#pragma unroll
-            for (int r = 0; r < 4; r++) load_px<P, 4>(p + r * s.rs, blk[r]);
-        }
-        else if (!yf)
-        {
-            // interp_horiz_pp: (int16)((sum + 32) >> 6) clipped
-#pragma unroll
-            for (int r = 0; r < 4; r++)
-            {
-                int v[11];
-                load_px<P, 11>(p + r * s.rs - 3, v);
-#pragma unroll
-                for (int c = 0; c < 4; c++)
-                {
-                    int sum = 0;
-#pragma unroll
-                    for (int t = 0; t < 8; t++) sum += cx[t] * v[c + t];
-                    const int val = (int16_t)((sum + 32) >> 6);
-                    blk[r][c] = val < 0 ? 0 : (val > maxv ? maxv : val);
-                }
-            }
-        }
-        else if (!xf)
-        {
-            // interp_vert_pp
-            int v[11][4];
-#pragma unroll
-            for (int i = 0; i < 11; i++) load_px<P, 4>(p + (i - 3) * s.rs, v[i]);
-#pragma unroll
-            for (int r = 0; r < 4; r++)
-#pragma unroll
-                for (int c = 0; c < 4; c++)
-                {
-                    int sum = 0;
-#pragma unroll
-                    for (int t = 0; t < 8; t++) sum += cy[t] * v[r + t][c];
-                    const int val = (int16_t)((sum + 32) >> 6);
-                    blk[r][c] = val < 0 ? 0 : (val > maxv ? maxv : val);
-                }
-        }
-        else
-        {
-            // interp_hv_pp: horizontal ps over 11 rows (int16), then vertical sp
-            const int ps_shift = 6 - head, ps_off = -8192 * (1 << ps_shift);
-            const int sp_shift = 6 + head, sp_off = (1 << (sp_shift - 1)) + (8192 << 6);
-            int m[11][4];
-#pragma unroll
-            for (int i = 0; i < 11; i++)
-            {
-                int v[11];
-                load_px<P, 11>(p + (i - 3) * s.rs - 3, v);
-#pragma unroll
-                for (int c = 0; c < 4; c++)
-                {
-                    int sum = 0;
-#pragma unroll
-                    for (int t = 0; t < 8; t++) sum += cx[t] * v[c + t];
-                    m[i][c] = (int16_t)((sum + ps_off) >> ps_shift);
-                }
-            }
-#pragma unroll
-            for (int r = 0; r < 4; r++)
-#pragma unroll
-                for (int c = 0; c < 4; c++)
-                {
-                    int sum = 0;
-#pragma unroll
-                    for (int t = 0; t < 8; t++) sum += cy[t] * m[r + t][c];
-                    const int val = (int16_t)((sum + sp_off) >> sp_shift);
-                    blk[r][c] = val < 0 ? 0 : (val > maxv ? maxv : val);
-                }
-        }
-        uint32_t fe[4][sizeof(P) == 1 ? 1 : 2];
-#pragma unroll
-        for (int r = 0; r < 4; r++) load4<P>(s.fenc + ux + (int64_t)(uy + r) * s.fs, fe[r]);
-        if (satd)
-        {
-            int d[4][4];
-#pragma unroll
-            for (int r = 0; r < 4; r++)
-#pragma unroll
-                for (int c = 0; c < 4; c++) d[r][c] = px<P>(fe[r], c) - blk[r][c];
-#pragma unroll
-            for (int r = 0; r < 4; r++) had4m(d[r][0], d[r][1], d[r][2], d[r][3]);
-            int sum = 0;
-#pragma unroll
-            for (int c = 0; c < 4; c++)
-            {
-                had4m(d[0][c], d[1][c], d[2][c], d[3][c]);
-#pragma unroll
-                for (int r = 0; r < 4; r++) sum += d[r][c] < 0 ? -d[r][c] : d[r][c];
-            }
-            acc += sum >> 1;          // each 4x4 raw sum is even (SURVEY note a7): any tiling gives satd
-        }
-        else
-        {
-#pragma unroll
-            for (int r = 0; r < 4; r++)
-#pragma unroll
-                for (int c = 0; c < 4; c++)
-                {
-                    const int d = px<P>(fe[r], c) - blk[r][c];
-                    acc += d < 0 ? -d : d;
-                }
-        }
+        if (!(xf | yf)) acc = subpel_units<P, 0, 1>(s, base, cx, cy, satd);
+        else if (!yf) acc = subpel_units<P, 1, 1>(s, base, cx, cy, satd);
+        else if (!xf) acc = subpel_units<P, 2, 1>(s, base, cx, cy, satd);
+        else acc = subpel_units<P, 3, 1>(s, base, cx, cy, satd);
+    }
+    else if (nmax == 2 || sizeof(P) == 2)
+    {
+        if (!(xf | yf)) acc = subpel_units<P, 0, 2>(s, base, cx, cy, satd);
+        else if (!yf) acc = subpel_units<P, 1, 2>(s, base, cx, cy, satd);
+        else if (!xf) acc = subpel_units<P, 2, 2>(s, base, cx, cy, satd);
+        else acc = subpel_units<P, 3, 2>(s, base, cx, cy, satd);
+    }
+    else
+    {
+        if (!(xf | yf)) acc = subpel_units<P, 0, kMeMaxUnits>(s, base, cx, cy, satd);
+        else if (!yf) acc = subpel_units<P, 1, kMeMaxUnits>(s, base, cx, cy, satd);
+        else if (!xf) acc = subpel_units<P, 2, kMeMaxUnits>(s, base, cx, cy, satd);
+        else acc = subpel_units<P, 3, kMeMaxUnits>(s, base, cx, cy, satd);
     }
     if (s.chroma)
         acc += chroma_satd<P>(s, qx, qy);
@@ -523,15 +591,22 @@ __global__ __launch_bounds__(X265AMD_BLOCK, X265AMD_ME_WAVES) void k_motion_sear
     else if (a.method == 2)
     {
         // STAR (motion.cpp:929-1034, StarPatternSearch :328-569)
-        int bpn = 0, bdist = 0;
-        // one candidate point (every point the reference tests is range-checked; the origin is in range,
-        // so the full check equals the reference's per-side checks)
+        int bpn = 0, bdist = 0, bx0 = bx, by0 = by;
+        // one candidate point, range-checked only on the sides it lies towards from the origin, as the
+        // reference's per-point checks are (:367-385, :425-465, :514-561): the origin itself may be out of
+        // range (MV 0 wins the start over a far MVP), and then points beside it on the far side are still
+        // costed; when the whole pattern is inside the range (the reference's "border" case) every
+        // directional check passes as well
         auto pt = [&](int mx, int my, int pn, int dd) {
-            if (mx < minx || mx > maxx || my < miny || my > maxy) return;
+            const int dx = mx - bx0, dy = my - by0;
+            if ((dx < 0 && mx < minx) || (dx > 0 && mx > maxx) || (dy < 0 && my < miny) || (dy > 0 && my > maxy))
+                return;
             const int c = fpel_sad<P, G>(s, mx, my) + s.mvcost(4 * mx, 4 * my);
             if (c < bcost) { bcost = c; bx = mx; by = my; bpn = pn; bdist = dd; }
         };
         auto star = [&](int early) {
+            bx0 = bx;
+            by0 = by;
             const int ox = bx, oy = by;
             int saved = bcost, rounds = 0;
             // distance 1: points 2, 4, 5, 7

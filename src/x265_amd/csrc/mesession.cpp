@@ -172,8 +172,8 @@ struct x265amd_mes
     int spin_us = 50;
     int trace = 0;                    // X265AMD_MES_TRACE=n: log the first n posts / launches / waits
     bool zerocopy = false;            // X265AMD_MES_ZEROCOPY=1: the kernel reads / writes the pinned staging
-    bool prio = false;                // X265AMD_MES_PRIORITY=1: launch streams at the highest priority
-    bool lspin = false;               // X265AMD_MES_LSPIN=1: launchers poll for completion
+    bool prio = true;                 // X265AMD_MES_PRIORITY=0: launch streams at the default priority
+    bool lspin = true;                // X265AMD_MES_LSPIN=0: launchers sleep in hipEventSynchronize
     std::atomic<int> traced{ 0 };
 
     // statistics (x265amd_mes_stats)
@@ -362,7 +362,10 @@ x265amd_me_batch make_batch(const x265amd_mes* s, const x265amd_mes_stage& g, co
     b.w = w;
     b.h = h;
     b.n = n;
-    b.method = s->cfg.method;
+    // the config carries x265_param::searchMethod (x265.h: DIA 0, HEX 1, UMH 2, STAR 3, FULL 4); the
+    // search kernel numbers STAR 2 and UMH 3
+    static const int kKernelMethod[5] = { 0, 1, 3, 2, 4 };
+    b.method = kKernelMethod[s->cfg.method];
     b.subme = s->cfg.subme;
     b.merange = s->cfg.merange;
     b.max_cand = s->cfg.max_cand > 0 ? s->cfg.max_cand : 1;

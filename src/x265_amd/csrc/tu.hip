@@ -1098,14 +1098,16 @@ static bool tu_i8()
     return v != 0;
 }
 
-// the straight-line 8x8 / 16x16 form (k_tu<.., true>); X265AMD_TU_BF=0 selects the branchy round-4 form
+// X265AMD_TU_BF=1 selects the straight-line 8x8 / 16x16 form (k_tu<.., true>).  Off by default: on the box
+// it measured slower than the branchy form (profiles/r05/tu_bf_ab.txt: 8x8 0.89 -> 0.99 ms, 16x16 0.70 ->
+// 0.74-0.77 ms per launch) although it issues a quarter of the scalar instructions
 static bool tu_bf()
 {
     static int v = -1;
     if (v < 0)
     {
         const char* e = getenv("X265AMD_TU_BF");
-        v = e ? atoi(e) != 0 : 1;
+        v = e ? atoi(e) != 0 : 0;
     }
     return v != 0;
 }

@@ -592,11 +592,13 @@ def me_tables(depth: int) -> np.ndarray:
 
 
 def case_me(w: int, h: int, method: int, subme: int, merange: int, depth: int, n: int, seed: int,
-            box: int = 0) -> Case:
+            box: int = 0, far: int = 0) -> Case:
     """f2: n PUs of the synthetic sequence (frame 1 searched in frame 0; pan (+2, +1) px/frame, moving object,
     noise), both planes edge-padded by 96 px like PicYuv.  MVP = the true pan +- a few quarter-pels, 0..3 AMVP-like
     candidates nearby, per-PU QP from ME_QPS, MV range = the picture + 24 px (the search stays inside the padding);
-    box > 0 also limits it to the full-pel MVP +- box, as Search::setSearchRange does with merange."""
+    box > 0 also limits it to the full-pel MVP +- box, as Search::setSearchRange does with merange; far > 0 moves
+    the MVP that many pixels (or up to 16 more) off the true pan on each axis, so that with box < far MV 0 (which
+    usually beats the far MVP as the search start, motion.cpp:615-624) lies outside the MV range."""
     import os
     import sys
 
@@ -618,6 +620,9 @@ def case_me(w: int, h: int, method: int, subme: int, merange: int, depth: int, n
     rng = np.array([[-int(x) - 24, -int(y) - 24, W - int(x) - w + 24, H - int(y) - h + 24] for x, y in zip(xs, ys)],
                    np.int16).reshape(-1)
     mvp = np.stack([-8 + det.ints(-6, 7, n), -4 + det.ints(-6, 7, n)], 1).astype(np.int16).reshape(-1)
+    if far:
+        sign = np.where(det.ints(0, 2, 2 * n) == 0, -1, 1)
+        mvp = (mvp + sign * 4 * (far + det.ints(0, 17, 2 * n))).astype(np.int16)
     if box:
         r4 = rng.reshape(-1, 4).astype(np.int64)
         fp = (mvp.reshape(-1, 2).astype(np.int64) + 2) >> 2
@@ -643,6 +648,8 @@ def case_me(w: int, h: int, method: int, subme: int, merange: int, depth: int, n
     prm = dict(w=w, h=h, method=method, subme=subme, merange=merange, max_cand=max_cand, depth=depth, n=n, seed=seed)
     if box:
         prm["box"] = box
+    if far:
+        prm["far"] = far
     return Case("me", prm, bufs, ["out_mv", "out_cost"])
 
 

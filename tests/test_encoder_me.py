@@ -119,19 +119,22 @@ def test_me_hook_cpu_mode_is_the_reference(tmp_path):
     assert "(reference functions)" in err and got == ref
 
 
-def _gpu_encode_equals_reference(tmp_path, w, h, n, extra_env=None, depth=8, min_area=4096, preset="medium"):
+def _gpu_encode_equals_reference(tmp_path, w, h, n, extra_env=None, depth=8, min_area=4096, preset="medium",
+                                 extra=()):
     src = _source(tmp_path, w, h, n, depth=depth)
     if depth == 8:
-        rc, ref, ref_fps, err = encode(_bin("x265ref8"), src, w, h, n, tmp_path / "ref.hevc", pools=16, preset=preset)
+        rc, ref, ref_fps, err = encode(_bin("x265ref8"), src, w, h, n, tmp_path / "ref.hevc", pools=16, preset=preset,
+                                       extra=extra)
         exe = _bin("x265la8")
     else:
         exe = _bin("x265la10")
         rc, ref, ref_fps, err = encode(exe, src, w, h, n, tmp_path / "ref.hevc",
                                        {"X265AMD_LOOKAHEAD": "cpu", "X265AMD_ME": "cpu"}, pools=16, depth=10,
-                                       preset=preset)
+                                       preset=preset, extra=extra)
     assert rc == 0, err[-2000:]
     env = {"X265AMD_ME_STATS": "1", **(extra_env or {})}
-    rc, got, fps, err = encode(exe, src, w, h, n, tmp_path / "me.hevc", env, pools=16, depth=depth, preset=preset)
+    rc, got, fps, err = encode(exe, src, w, h, n, tmp_path / "me.hevc", env, pools=16, depth=depth, preset=preset,
+                               extra=extra)
     assert rc == 0, err[-3000:]
     assert f"[x265me] motion searches of PUs >= {min_area} pixels on the MI355X" in err
     st = _stats(err)
@@ -207,6 +210,22 @@ def test_gpu_me_slow_check_mode_chroma_satd(tmp_path):
     the host: 0 mismatches"""
     err = _gpu_encode_equals_reference(tmp_path, 1280, 720, 12, {"X265AMD_ME": "check", "X265AMD_ME_MIN": "1024"},
                                        min_area=1024, preset="slow")
+    m = re.search(r"check: (\d+) mismatching searches", err)
+    assert m and int(m.group(1)) == 0, err[-3000:]
+    m = re.search(r"check: (\d+) search windows beyond", err)
+    assert m and int(m.group(1)) == 0, err[-3000:]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("preset,extra", [("medium", ("--me", "star")), ("medium", ("--me", "umh")),
+                                          ("medium", ("--me", "dia")), ("veryslow", ())],
+                         ids=["star", "umh", "dia", "veryslow"])
+def test_gpu_me_check_mode_search_methods(tmp_path, preset, extra):
+    """every search method of x265_param::searchMethod through the session (x265.h numbers UMH 2 and STAR 3,
+    the kernel STAR 2 and UMH 3: the session maps them) and veryslow's subme 4 / merange, in check mode with
+    the 32x32 CUs: 0 mismatches, 0 windows beyond the resident rows, the reference's bitstream"""
+    err = _gpu_encode_equals_reference(tmp_path, 1280, 720, 8, {"X265AMD_ME": "check", "X265AMD_ME_MIN": "1024"},
+                                       min_area=1024, preset=preset, extra=extra)
     m = re.search(r"check: (\d+) mismatching searches", err)
     assert m and int(m.group(1)) == 0, err[-3000:]
     m = re.search(r"check: (\d+) search windows beyond", err)

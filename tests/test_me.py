@@ -26,6 +26,29 @@ def test_me_oracle_matches_reference(oracle_libs, depth):
                 assert np.array_equal(a[k], b[k]), (c.key(), k)
 
 
+def far_cases(depth, n=24):
+    """MVP far off the motion and the range boxed around it, so the search usually starts at MV 0 outside the
+    range (motion.cpp:615-624): every search method, whose patterns then cost points beside the out-of-range
+    origin on the sides the reference does not check (STAR's per-point checks, :367-561)"""
+    return [case_me(w, h, m, s, 57, depth, n, seed_of("me-far", depth, w, h, m), box=16, far=24)
+            for (w, h) in ((8, 8), (16, 16), (32, 32), (64, 64), (32, 16), (8, 32))
+            for m, s in ((0, 2), (1, 2), (2, 2), (2, 3), (3, 2))]
+
+
+@pytest.mark.skipif(not available("ref", 8), reason="reference library oracle/_ref not built")
+@pytest.mark.parametrize("depth", [8, 10])
+def test_me_far_oracle_matches_reference(oracle_libs, depth):
+    orc, ref = CpuOracle("oracle", depth), CpuOracle("ref", depth)
+    starts_outside = 0
+    for c in far_cases(depth):
+        a, b = run_cpu(c, orc), run_cpu(c, ref)
+        for k in c.outs:
+            assert np.array_equal(a[k], b[k]), (c.key(), k)
+        rng = c.bufs["rng"].reshape(-1, 4)
+        starts_outside += int(((rng[:, 0] > 0) | (rng[:, 2] < 0) | (rng[:, 1] > 0) | (rng[:, 3] < 0)).sum())
+    assert starts_outside > 100
+
+
 def full_cases(depth, n=16):
     """--me full (method 4) over MVP +- 16 (the exhaustive search is slow on the CPU), every luma PU shape,
     subme 2 and (with chroma SATD) 3"""
@@ -65,6 +88,8 @@ def test_me_gpu_matches_oracle(gpu_prims, oracle_libs, depth):
               for (w, h) in ((8, 8), (32, 32), (64, 64)) for s in (3, 5)]
     # --me full (method 4): the exhaustive search kernel, then the lockstep refine
     cases += full_cases(depth, 32)
+    # the search origin outside the MV range (MV 0 against a far MVP), every method
+    cases += far_cases(depth)
     cases += [case_me(w, h, 4, 2, 57, depth, 24, seed_of("me-full-g", depth, w, h), box=57)
               for (w, h) in ((8, 8), (64, 64), (24, 32))]
     bad = []
