@@ -56,12 +56,13 @@ constexpr int kMeMaxUnits = 4;    // 4x4 units per lane (64x64 PU over 64 lanes)
 template <typename P>
 struct MeState
 {
-    const MeArgs* a;
     const P* ref;           // reference at the PU origin
     int64_t rs;
     const uint16_t* tab;
     int mvpx, mvpy;
     int nu, lane, G, uw;    // units of this lane, lane in group, group size, units per PU row
+    int w, h, depth;
+    int nmax;               // most units of any lane (uniform): 1, 2 or 4 of them go per round trip
     const P* fenc;          // source PU origin
     int64_t fs;
     uint32_t fe[kMeMaxUnits][4][sizeof(P) == 1 ? 1 : 2];   // this lane's fenc units, loaded once
@@ -111,37 +112,103 @@ __device__ __forceinline__ void had4m(int& a, int& b, int& c, int& d)
     a = s0 + s2; b = s1 + s3; c = s0 - s2; d = s1 - s3;
 }
 
-// full-pel SAD of the PU at integer displacement (dx, dy), group-reduced
-// sum over the G lanes of a group (G = 1..64, a power of two, known at run time)
-__device__ __forceinline__ int group_sum_rt(int v, int G)
+// sum over the G lanes of a group, every lane getting the sum: DPP lane moves inside rows of 16 (quad
+// permutes, half-row and row mirrors: a few cycles each) and, for a whole wavefront, four lane reads of the
+// row sums; the LDS-crossbar shuffles (one per halving, each an LDS round trip) only for the 16-lane step
+// of a 32-lane group.  A search costs tens of dependent reductions, so their latency is the search's.
+#ifndef X265AMD_ME_DPP
+#define X265AMD_ME_DPP 1
+#endif
+template <int G>
+__device__ __forceinline__ int me_group_sum(int v)
 {
-    for (int m = G >> 1; m > 0; m >>= 1) v += __shfl_xor(v, m, 64);
+#if X265AMD_ME_DPP
+    if constexpr (G >= 2) v += __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false);    // quad_perm [1,0,3,2]
+    if constexpr (G >= 4) v += __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, false);    // quad_perm [2,3,0,1]
+    if constexpr (G >= 8) v += __builtin_amdgcn_mov_dpp(v, 0x141, 0xF, 0xF, false);   // row_half_mirror
+    if constexpr (G >= 16) v += __builtin_amdgcn_mov_dpp(v, 0x140, 0xF, 0xF, false);  // row_mirror
+    if constexpr (G == 32) v += __shfl_xor(v, 16, 64);
+    if constexpr (G == 64)
+        v = __builtin_amdgcn_readlane(v, 0) + __builtin_amdgcn_readlane(v, 16) + __builtin_amdgcn_readlane(v, 32) +
+            __builtin_amdgcn_readlane(v, 48);
     return v;
+#else
+    return group_sum<G>(v);
+#endif
 }
 
-// fenc from registers (loaded once per PU); the unit loop unrolled to kMeMaxUnits with a guard, so
-// every reference row load of a candidate is issued before the first SAD
+// full-pel SADs of the PU at N integer displacements (mx[n], my[n]), group-reduced.  fenc comes from
+// registers (loaded once per PU); every reference row of all N candidates and NU units is loaded before the
+// first SAD, and the N group reductions run side by side, so N candidates cost one memory round trip and
+// one reduction latency instead of N.  Lanes beyond the PU's units (nu = 0) load the PU's first unit.
+template <typename P, int G, int N, int NU>
+__device__ __forceinline__ void fpel_sad_nu(const MeState<P>& s, const int (&mx)[N], const int (&my)[N], int (&out)[N])
+{
+    constexpr int W = sizeof(P) == 1 ? 1 : 2;
+    uint32_t w[N][NU][4][W];
+#pragma unroll
+    for (int k = 0; k < NU; k++)
+    {
+        int ux = 0, uy = 0;
+        if (s.nu) s.unit_xy(k < s.nu ? k : 0, ux, uy);
+#pragma unroll
+        for (int n = 0; n < N; n++)
+        {
+            const P* p = s.ref + (ux + mx[n]) + (int64_t)(uy + my[n]) * s.rs;
+#pragma unroll
+            for (int r = 0; r < 4; r++) load4<P>(p + r * s.rs, w[n][k][r]);
+        }
+    }
+#pragma unroll
+    for (int n = 0; n < N; n++)
+    {
+        uint32_t acc = 0;
+#pragma unroll
+        for (int k = 0; k < NU; k++)
+        {
+            uint32_t a = 0;
+#pragma unroll
+            for (int r = 0; r < 4; r++) a = sad4<P>(s.fe[k][r], w[n][k][r], a);
+            acc += k < s.nu ? a : 0u;
+        }
+        out[n] = (int)acc;
+    }
+#pragma unroll
+    for (int n = 0; n < N; n++) out[n] = me_group_sum<G>(out[n]);
+}
+
+// N candidates' SADs; `counted` of them are real evaluations (the rest are range-failed points whose loads
+// were clamped to a valid position and whose results are ignored)
+template <typename P, int G, int N>
+__device__ __forceinline__ void fpel_sads(const MeState<P>& s, const int (&mx)[N], const int (&my)[N], int (&out)[N],
+                                          int counted = N)
+{
+    s.nfp += counted;
+    if constexpr (G < 64) fpel_sad_nu<P, G, N, 1>(s, mx, my, out);
+    else if (s.nmax == 1) fpel_sad_nu<P, G, N, 1>(s, mx, my, out);
+    else if (s.nmax == 2) fpel_sad_nu<P, G, N, 2>(s, mx, my, out);
+    else fpel_sad_nu<P, G, N, kMeMaxUnits>(s, mx, my, out);
+}
+
+// ... plus the MV cost (quarter-pel MV = 4 x full-pel)
+template <typename P, int G, int N>
+__device__ __forceinline__ void fpel_costs(const MeState<P>& s, const int (&mx)[N], const int (&my)[N], int (&out)[N],
+                                           int counted = N)
+{
+    fpel_sads<P, G, N>(s, mx, my, out, counted);
+#pragma unroll
+    for (int n = 0; n < N; n++) out[n] += s.mvcost(4 * mx[n], 4 * my[n]);
+}
+
+// one candidate's SAD
 template <typename P, int G>
 __device__ __forceinline__ int fpel_sad(const MeState<P>& s, int dx, int dy)
 {
-    uint32_t acc = 0;
-    s.nfp++;
-#pragma unroll
-    for (int k = 0; k < kMeMaxUnits; k++)
-    {
-        if (k >= s.nu) break;
-        int ux, uy;
-        s.unit_xy(k, ux, uy);
-        const P* p = s.ref + (ux + dx) + (int64_t)(uy + dy) * s.rs;
-        uint32_t w[4][sizeof(P) == 1 ? 1 : 2];
-#pragma unroll
-        for (int r = 0; r < 4; r++) load4<P>(p + r * s.rs, w[r]);
-#pragma unroll
-        for (int r = 0; r < 4; r++) acc = sad4<P>(s.fe[k][r], w[r], acc);
-    }
-    return group_sum<G>((int)acc);
+    const int mx[1] = { dx }, my[1] = { dy };
+    int c[1];
+    fpel_sads<P, G, 1>(s, mx, my, c);
+    return c[0];
 }
-
 
 // N consecutive pixels from p as ints, by vector loads that stay inside [p, p + N)
 // (N = 4, 7 or 11; overlapping loads cover the odd widths)
@@ -177,12 +244,12 @@ __device__ __forceinline__ void load_px(const P* p, int (&v)[N])
 template <typename P>
 __device__ __forceinline__ int chroma_satd(const MeState<P>& s, int qx, int qy)
 {
-    const int cw = s.a->w >> 1, ch = s.a->h >> 1;
+    const int cw = s.w >> 1, ch = s.h >> 1;
     const int cuw = cw >> 2, units = cuw * (ch >> 2);
     const int xf = qx & 7, yf = qy & 7;
     const int64_t off = (qx >> 3) + (int64_t)(qy >> 3) * s.rcs;
-    const int maxv = (1 << s.a->depth) - 1;
-    const int head = 14 - s.a->depth;
+    const int maxv = (1 << s.depth) - 1;
+    const int head = 14 - s.depth;
     int cx[4], cy[4];
 #pragma unroll
     for (int t = 0; t < 4; t++) { cx[t] = c_chroma.c[xf][t]; cy[t] = c_chroma.c[yf][t]; }
@@ -324,8 +391,8 @@ __device__ __forceinline__ int subpel_units(const MeState<P>& s, const P* base, 
                                             const int (&cy)[8], bool satd)
 {
     constexpr int R = (CASE & 2) ? 11 : 4, C = (CASE & 1) ? 11 : 4;
-    const int maxv = (1 << s.a->depth) - 1;
-    const int head = 14 - s.a->depth;
+    const int maxv = (1 << s.depth) - 1;
+    const int head = 14 - s.depth;
     const int64_t rs = s.rs, fs = s.fs;
     int acc = 0;
     for (int k0 = 0; k0 < s.nu; k0 += KU)
@@ -452,42 +519,67 @@ __device__ __forceinline__ int subpel_units(const MeState<P>& s, const P* base, 
 // subpelCompare (motion.cpp:1174-1203): the block at quarter-pel (qx, qy), built by
 // luma_hpp / luma_vpp / luma_hvpp when fractional, compared with SAD or SATD.  8-bit windows of all
 // (at most 4) units of a lane fit in registers; at 16 bits two units go per round trip.
+//
+// Out of line (six call sites; inlined, the kernel spills), with the search state passed as values: a
+// reference to the caller's MeState (or to the kernel's argument block) would keep that state in scratch
+// memory.  lane_nu = lane | nu << 8, wh = w | h << 8, dc = depth | chroma << 8.
+#ifndef X265AMD_ME_KU64
+#define X265AMD_ME_KU64 2         // 8-bit unit windows per round trip in 64-lane groups
+#endif
 template <typename P, int G>
-__device__ __noinline__ int subpel_cost(const MeState<P>& s, int qx, int qy, bool satd)
+__device__ __noinline__ int subpel_cost(const P* ref, const P* fenc, int rs, int fs, int lane_nu, int wh, int dc,
+                                        const P* fcb, const P* fcr, const P* rcb, const P* rcr, int fcs, int rcs,
+                                        int qx, int qy, bool satd)
 {
+    MeState<P> s;
+    s.ref = ref;
+    s.rs = rs;
+    s.fenc = fenc;
+    s.fs = fs;
+    s.lane = lane_nu & 255;
+    s.nu = lane_nu >> 8;
+    s.G = G;
+    s.w = wh & 255;
+    s.h = wh >> 8;
+    s.uw = s.w >> 2;
+    s.depth = dc & 255;
+    s.chroma = (dc >> 8) != 0;
+    if (s.chroma)
+    {
+        s.fc[0] = fcb; s.fc[1] = fcr;
+        s.rc[0] = rcb; s.rc[1] = rcr;
+        s.fcs = fcs; s.rcs = rcs;
+    }
     const int xf = qx & 3, yf = qy & 3;
-    s.nsp++;
     const P* base = s.ref + (qx >> 2) + (int64_t)(qy >> 2) * s.rs;
     int cx[8], cy[8];
 #pragma unroll
     for (int t = 0; t < 8; t++) { cx[t] = c_luma.c[xf][t]; cy[t] = c_luma.c[yf][t]; }
     // units per lane: 1 below 64 units, 2 for 64x32 / 32x64, 4 for 64x64 (uniform over the batch)
-    const int nmax = (s.uw * (s.a->h >> 2) + s.G - 1) / s.G;
+    const int nmax = (s.uw * (s.h >> 2) + G - 1) / G;
     int acc;
-    if (nmax == 1)
+    // windows per round trip: up to two units (a 64x64 PU's four units of a lane in two trips; the 16-bit
+    // 2-D case one at a time).  Four would push the function past 256 VGPRs, and the callee-saved registers
+    // it then spills to scratch on every call cost more than the round trips saved
+    // (profiles/r05/me_kernel_variants_ab.txt: 0.081 ms per launch at four 8-bit units, 0.059 at two)
+    constexpr int KU = X265AMD_ME_KU64, KU_HV = sizeof(P) == 1 ? KU : 1;
+    if (G < 64 || nmax == 1)
     {
         if (!(xf | yf)) acc = subpel_units<P, 0, 1>(s, base, cx, cy, satd);
         else if (!yf) acc = subpel_units<P, 1, 1>(s, base, cx, cy, satd);
         else if (!xf) acc = subpel_units<P, 2, 1>(s, base, cx, cy, satd);
         else acc = subpel_units<P, 3, 1>(s, base, cx, cy, satd);
     }
-    else if (nmax == 2 || sizeof(P) == 2)
-    {
-        if (!(xf | yf)) acc = subpel_units<P, 0, 2>(s, base, cx, cy, satd);
-        else if (!yf) acc = subpel_units<P, 1, 2>(s, base, cx, cy, satd);
-        else if (!xf) acc = subpel_units<P, 2, 2>(s, base, cx, cy, satd);
-        else acc = subpel_units<P, 3, 2>(s, base, cx, cy, satd);
-    }
     else
     {
-        if (!(xf | yf)) acc = subpel_units<P, 0, kMeMaxUnits>(s, base, cx, cy, satd);
-        else if (!yf) acc = subpel_units<P, 1, kMeMaxUnits>(s, base, cx, cy, satd);
-        else if (!xf) acc = subpel_units<P, 2, kMeMaxUnits>(s, base, cx, cy, satd);
-        else acc = subpel_units<P, 3, kMeMaxUnits>(s, base, cx, cy, satd);
+        if (!(xf | yf)) acc = subpel_units<P, 0, KU>(s, base, cx, cy, satd);
+        else if (!yf) acc = subpel_units<P, 1, KU>(s, base, cx, cy, satd);
+        else if (!xf) acc = subpel_units<P, 2, KU>(s, base, cx, cy, satd);
+        else acc = subpel_units<P, 3, KU_HV>(s, base, cx, cy, satd);
     }
     if (s.chroma)
         acc += chroma_satd<P>(s, qx, qy);
-    return group_sum<G>(acc);
+    return me_group_sum<G>(acc);
 }
 
 // workload[subme] of motion.cpp:48-58 as {hpel_iters, hpel_dirs, qpel_iters, qpel_dirs}, one
@@ -508,7 +600,6 @@ __global__ __launch_bounds__(X265AMD_BLOCK, X265AMD_ME_WAVES) void k_motion_sear
     const int64_t j = (int64_t)xcd_block() * (X265AMD_BLOCK / G) + threadIdx.x / G;
     if (j >= a.n) return;                               // whole groups
     MeState<P> s;
-    s.a = &a;
     s.lane = threadIdx.x & (G - 1);
     s.G = G;
     s.uw = a.w >> 2;
@@ -520,6 +611,10 @@ __global__ __launch_bounds__(X265AMD_BLOCK, X265AMD_ME_WAVES) void k_motion_sear
     s.fenc = (const P*)a.fenc + a.fenc_off[j];
     s.fs = a.fs;
     s.nfp = s.nsp = 0;
+    s.w = a.w;
+    s.h = a.h;
+    s.depth = a.depth;
+    s.nmax = (units + G - 1) / G;
 #pragma unroll
     for (int k = 0; k < kMeMaxUnits; k++)
     {
@@ -531,6 +626,8 @@ __global__ __launch_bounds__(X265AMD_BLOCK, X265AMD_ME_WAVES) void k_motion_sear
     }
     // bChromaSATD = subpelRefine > 2 && the 4:2:0 chroma satd entry exists (chroma dims % 4 == 0)
     s.chroma = a.subme > 2 && a.fcb && ((a.w >> 1) & 3) == 0 && ((a.h >> 1) & 3) == 0;
+    s.fc[0] = s.fc[1] = s.rc[0] = s.rc[1] = nullptr;
+    s.fcs = s.rcs = 0;
     if (s.chroma)
     {
         s.fc[0] = (const P*)a.fcb + a.fcoff[j]; s.fc[1] = (const P*)a.fcr + a.fcoff[j];
@@ -539,6 +636,13 @@ __global__ __launch_bounds__(X265AMD_BLOCK, X265AMD_ME_WAVES) void k_motion_sear
     }
     const int minx = a.mv_range[4 * j], miny = a.mv_range[4 * j + 1];
     const int maxx = a.mv_range[4 * j + 2], maxy = a.mv_range[4 * j + 3];
+    // the sub-pel compare, out of line
+    auto spc = [&](int qx, int qy, bool satd) {
+        s.nsp++;
+        return subpel_cost<P, G>(s.ref, s.fenc, (int)s.rs, (int)s.fs, s.lane | s.nu << 8, a.w | a.h << 8,
+                                 a.depth | (s.chroma ? 256 : 0), s.fc[0], s.fc[1], s.rc[0], s.rc[1], (int)s.fcs,
+                                 (int)s.rcs, qx, qy, satd);
+    };
     s.mvpx = a.mvp[2 * j];
     s.mvpy = a.mvp[2 * j + 1];
     auto clipq = [&](int& x, int& y) {
@@ -548,7 +652,7 @@ __global__ __launch_bounds__(X265AMD_BLOCK, X265AMD_ME_WAVES) void k_motion_sear
     int pmx = s.mvpx, pmy = s.mvpy;
     clipq(pmx, pmy);
     int bpx = pmx, bpy = pmy;                          // bestpre
-    int bprecost = subpel_cost<P, G>(s, pmx, pmy, false);   // no MV cost (motion.cpp:609)
+    int bprecost = spc(pmx, pmy, false);   // no MV cost (motion.cpp:609)
     int bx = (pmx + 2) >> 2, by = (pmy + 2) >> 2;
     int bcost = bprecost;
     if ((pmx | pmy) & 3) bcost = fpel_sad<P, G>(s, bx, by) + s.mvcost(4 * bx, 4 * by);
@@ -564,11 +668,10 @@ __global__ __launch_bounds__(X265AMD_BLOCK, X265AMD_ME_WAVES) void k_motion_sear
         clipq(cx, cy);
         if ((cx | cy) && (cx != pmx || cy != pmy) && (cx != bpx || cy != bpy))
         {
-            const int c = subpel_cost<P, G>(s, cx, cy, false) + s.mvcost(cx, cy);
+            const int c = spc(cx, cy, false) + s.mvcost(cx, cy);
             if (c < bprecost) { bprecost = c; bpx = cx; bpy = cy; }
         }
     }
-    auto fc = [&](int dx, int dy) { return fpel_sad<P, G>(s, bx + dx, by + dy) + s.mvcost(4 * (bx + dx), 4 * (by + dy)); };
     if (a.method == 0)
     {
         // diamond, radius 1 (motion.cpp:654-676)
@@ -576,11 +679,13 @@ __global__ __launch_bounds__(X265AMD_BLOCK, X265AMD_ME_WAVES) void k_motion_sear
         int i = a.merange;
         do
         {
-            const int c0 = fc(0, -1), c1 = fc(0, 1), c2 = fc(-1, 0), c3 = fc(1, 0);
-            if ((c0 << 4) + 1 < bcost) bcost = (c0 << 4) + 1;
-            if ((c1 << 4) + 3 < bcost) bcost = (c1 << 4) + 3;
-            if ((c2 << 4) + 4 < bcost) bcost = (c2 << 4) + 4;
-            if ((c3 << 4) + 12 < bcost) bcost = (c3 << 4) + 12;
+            const int mx[4] = { bx, bx, bx - 1, bx + 1 }, my[4] = { by - 1, by + 1, by, by };
+            int c[4];
+            fpel_costs<P, G, 4>(s, mx, my, c);
+            if ((c[0] << 4) + 1 < bcost) bcost = (c[0] << 4) + 1;
+            if ((c[1] << 4) + 3 < bcost) bcost = (c[1] << 4) + 3;
+            if ((c[2] << 4) + 4 < bcost) bcost = (c[2] << 4) + 4;
+            if ((c[3] << 4) + 12 < bcost) bcost = (c[3] << 4) + 12;
             if (!(bcost & 15)) break;
             bx -= (int32_t)((uint32_t)bcost << 28) >> 30;
             by -= (int32_t)((uint32_t)bcost << 30) >> 30;
@@ -597,25 +702,37 @@ __global__ __launch_bounds__(X265AMD_BLOCK, X265AMD_ME_WAVES) void k_motion_sear
         // range (MV 0 wins the start over a far MVP), and then points beside it on the far side are still
         // costed; when the whole pattern is inside the range (the reference's "border" case) every
         // directional check passes as well
-        auto pt = [&](int mx, int my, int pn, int dd) {
-            const int dx = mx - bx0, dy = my - by0;
-            if ((dx < 0 && mx < minx) || (dx > 0 && mx > maxx) || (dy < 0 && my < miny) || (dy > 0 && my > maxy))
-                return;
-            const int c = fpel_sad<P, G>(s, mx, my) + s.mvcost(4 * mx, 4 * my);
-            if (c < bcost) { bcost = c; bx = mx; by = my; bpn = pn; bdist = dd; }
+        // up to four candidate points at once, range-checked only on the sides they lie towards from the
+        // origin, as the reference's per-point checks are (:367-385, :425-465, :514-561): the origin itself
+        // may be out of range (MV 0 wins the start over a far MVP), and then points beside it on the far
+        // side are still costed; when the whole pattern is inside the range (the reference's "border" case)
+        // every directional check passes as well.  Results are taken in the reference's point order.
+        auto pts4 = [&](const int (&dx)[4], const int (&dy)[4], const int (&pn)[4], const int (&dd)[4]) {
+            int mx[4], my[4], c[4];
+            bool ok[4];
+            int nok = 0;
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+            {
+                mx[q] = bx0 + dx[q];
+                my[q] = by0 + dy[q];
+                ok[q] = !((dx[q] < 0 && mx[q] < minx) || (dx[q] > 0 && mx[q] > maxx) ||
+                          (dy[q] < 0 && my[q] < miny) || (dy[q] > 0 && my[q] > maxy));
+                nok += ok[q];
+                if (!ok[q]) { mx[q] = bx0; my[q] = by0; }
+            }
+            if (!nok) return;
+            fpel_costs<P, G, 4>(s, mx, my, c, nok);
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+                if (ok[q] && c[q] < bcost) { bcost = c[q]; bx = mx[q]; by = my[q]; bpn = pn[q]; bdist = dd[q]; }
         };
         auto star = [&](int early) {
             bx0 = bx;
             by0 = by;
-            const int ox = bx, oy = by;
             int saved = bcost, rounds = 0;
             // distance 1: points 2, 4, 5, 7
-#pragma unroll 1
-            for (int k = 0; k < 4; k++)
-            {
-                const int dx = k == 1 ? -1 : k == 2 ? 1 : 0, dy = k == 0 ? -1 : k == 3 ? 1 : 0;
-                pt(ox + dx, oy + dy, (int)((0x7542u >> (4 * k)) & 15), 1);
-            }
+            pts4({ 0, -1, 1, 0 }, { -1, 0, 0, 1 }, { 2, 4, 5, 7 }, { 1, 1, 1, 1 });
             if (bcost < saved) rounds = 0;
             else if (++rounds >= early) return;
             // distances 2, 4, 8: points 2, 1, 3, 4, 5, 6, 8, 7 (1, 3, 6, 8 at half distance)
@@ -623,14 +740,8 @@ __global__ __launch_bounds__(X265AMD_BLOCK, X265AMD_ME_WAVES) void k_motion_sear
             {
                 const int h2 = dist >> 1;
                 saved = bcost;
-#pragma unroll 1
-                for (int k = 0; k < 8; k++)
-                {
-                    const int ux = (int)((0x23140312u >> (4 * k)) & 15) - 2;   // x in half-distance units
-                    const int uy = (int)((0x43322110u >> (4 * k)) & 15) - 2;   // y in half-distance units
-                    const bool half = k == 1 || k == 2 || k == 5 || k == 6;
-                    pt(ox + ux * h2, oy + uy * h2, (int)((0x78654312u >> (4 * k)) & 15), half ? h2 : dist);
-                }
+                pts4({ 0, -h2, h2, -dist }, { -dist, -h2, -h2, 0 }, { 2, 1, 3, 4 }, { dist, h2, h2, dist });
+                pts4({ dist, -h2, h2, 0 }, { 0, h2, h2, dist }, { 5, 6, 8, 7 }, { dist, h2, h2, dist });
                 if (bcost < saved) rounds = 0;
                 else if (++rounds >= early) return;
             }
@@ -639,22 +750,12 @@ __global__ __launch_bounds__(X265AMD_BLOCK, X265AMD_ME_WAVES) void k_motion_sear
             {
                 saved = bcost;
                 const int q = dist >> 2;
+                pts4({ 0, -dist, dist, 0 }, { -dist, 0, 0, dist }, { 0, 0, 0, 0 }, { dist, dist, dist, dist });
 #pragma unroll 1
-                for (int k = 0; k < 16; k++)
+                for (int index = 1; index < 4; index++)
                 {
-                    int dx, dy;
-                    if (k < 4)
-                    {
-                        dx = k == 1 ? -dist : k == 2 ? dist : 0;
-                        dy = k == 0 ? -dist : k == 3 ? dist : 0;
-                    }
-                    else
-                    {
-                        const int index = (k >> 2), c = k & 3;
-                        dx = (c & 1 ? 1 : -1) * q * index;
-                        dy = c < 2 ? -dist + q * index : dist - q * index;
-                    }
-                    pt(ox + dx, oy + dy, 0, dist);
+                    const int xl = -q * index, xr = q * index, yt = -dist + q * index, yb = dist - q * index;
+                    pts4({ xl, xr, xl, xr }, { yt, yt, yb, yb }, { 0, 0, 0, 0 }, { dist, dist, dist, dist });
                 }
                 if (bcost < saved) rounds = 0;
                 else if (++rounds >= early) return;
@@ -666,16 +767,14 @@ __global__ __launch_bounds__(X265AMD_BLOCK, X265AMD_ME_WAVES) void k_motion_sear
             const int i0 = (bpn - 1) * 2, i1 = i0 + 1;
             const int m1x = bx + (int)((OX >> (4 * i0)) & 15) - 1, m1y = by + (int)((OY >> (4 * i0)) & 15) - 1;
             const int m2x = bx + (int)((OX >> (4 * i1)) & 15) - 1, m2y = by + (int)((OY >> (4 * i1)) & 15) - 1;
-            if (m1x >= minx && m1x <= maxx && m1y >= miny && m1y <= maxy)
-            {
-                const int c = fpel_sad<P, G>(s, m1x, m1y) + s.mvcost(4 * m1x, 4 * m1y);
-                if (c < bcost) { bcost = c; bx = m1x; by = m1y; }
-            }
-            if (m2x >= minx && m2x <= maxx && m2y >= miny && m2y <= maxy)
-            {
-                const int c = fpel_sad<P, G>(s, m2x, m2y) + s.mvcost(4 * m2x, 4 * m2y);
-                if (c < bcost) { bcost = c; bx = m2x; by = m2y; }
-            }
+            const bool ok1 = m1x >= minx && m1x <= maxx && m1y >= miny && m1y <= maxy;
+            const bool ok2 = m2x >= minx && m2x <= maxx && m2y >= miny && m2y <= maxy;
+            if (!(ok1 || ok2)) return;
+            const int mx[2] = { ok1 ? m1x : bx, ok2 ? m2x : bx }, my[2] = { ok1 ? m1y : by, ok2 ? m2y : by };
+            int c[2];
+            fpel_costs<P, G, 2>(s, mx, my, c, (int)ok1 + (int)ok2);
+            if (ok1 && c[0] < bcost) { bcost = c[0]; bx = m1x; by = m1y; }
+            if (ok2 && c[1] < bcost) { bcost = c[1]; bx = m2x; by = m2y; }
         };
         star(3);
         bool done = false;
@@ -700,13 +799,16 @@ __global__ __launch_bounds__(X265AMD_BLOCK, X265AMD_ME_WAVES) void k_motion_sear
                     {
                         if (tx + 15 <= maxx)
                         {
+                            const int mx[4] = { tx, tx + 5, tx + 10, tx + 15 }, my[4] = { ty, ty, ty, ty };
+                            int c[4];
+                            fpel_sads<P, G, 4>(s, mx, my, c);
 #pragma unroll
                             for (int q = 0; q < 4; q++)
                             {
-                                const int c = fpel_sad<P, G>(s, tx, ty) + s.mvcost((q == 3 ? 8 : 4) * tx, (q == 3 ? 8 : 4) * ty);
-                                if (c < bcost) { bcost = c; bx = tx; by = ty; }
-                                if (q < 3) tx += 5;
+                                const int cq = c[q] + s.mvcost((q == 3 ? 8 : 4) * mx[q], (q == 3 ? 8 : 4) * ty);
+                                if (cq < bcost) { bcost = cq; bx = mx[q]; by = ty; }
                             }
+                            tx += 15;
                         }
                         else
                         {
@@ -749,13 +851,13 @@ __global__ __launch_bounds__(X265AMD_BLOCK, X265AMD_ME_WAVES) void k_motion_sear
             if (c < bcost) { bcost = c; bx = x; by = y; }
         };
         int ox = bx, oy = by;
-        auto cost_x4 = [&](int a0, int b0, int a1, int b1, int a2, int b2, int a3, int b3) {
-            const int c0 = ca(ox + a0, oy + b0), c1 = ca(ox + a1, oy + b1);
-            const int c2 = ca(ox + a2, oy + b2), c3 = ca(ox + a3, oy + b3);
-            if (c0 < bcost) { bcost = c0; bx = ox + a0; by = oy + b0; }
-            if (c1 < bcost) { bcost = c1; bx = ox + a1; by = oy + b1; }
-            if (c2 < bcost) { bcost = c2; bx = ox + a2; by = oy + b2; }
-            if (c3 < bcost) { bcost = c3; bx = ox + a3; by = oy + b3; }
+        auto cost_x4 = [&](int a0, int b0, int a1, int b1, int a2, int b2, int a3, int b3) __attribute__((always_inline)) {
+            const int mx[4] = { ox + a0, ox + a1, ox + a2, ox + a3 }, my[4] = { oy + b0, oy + b1, oy + b2, oy + b3 };
+            int c[4];
+            fpel_costs<P, G, 4>(s, mx, my, c);
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+                if (c[q] < bcost) { bcost = c[q]; bx = mx[q]; by = my[q]; }
         };
         auto dia1 = [&](int mx, int my) { ox = mx; oy = my; cost_x4(0, -1, 0, 1, -1, 0, 1, 0); };
         auto cross = [&](int start, int xm, int ym) {
@@ -874,28 +976,31 @@ __global__ __launch_bounds__(X265AMD_BLOCK, X265AMD_ME_WAVES) void k_motion_sear
     }
     if (do_hex)
     {
-        int c0 = fc(-2, 0), c1 = fc(-1, 2), c2 = fc(1, 2);
-        bcost <<= 3;
-        if ((c0 << 3) + 2 < bcost) bcost = (c0 << 3) + 2;
-        if ((c1 << 3) + 3 < bcost) bcost = (c1 << 3) + 3;
-        if ((c2 << 3) + 4 < bcost) bcost = (c2 << 3) + 4;
-        c0 = fc(2, 0); c1 = fc(1, -2); c2 = fc(-1, -2);
-        if ((c0 << 3) + 5 < bcost) bcost = (c0 << 3) + 5;
-        if ((c1 << 3) + 6 < bcost) bcost = (c1 << 3) + 6;
-        if ((c2 << 3) + 7 < bcost) bcost = (c2 << 3) + 7;
+        // the six hexagon points at once (motion.cpp:1077-1089: two sad_x3), then the tie-ordered updates
+        {
+            const int mx[6] = { bx - 2, bx - 1, bx + 1, bx + 2, bx + 1, bx - 1 };
+            const int my[6] = { by, by + 2, by + 2, by, by - 2, by - 2 };
+            int c[6];
+            fpel_costs<P, G, 6>(s, mx, my, c);
+            bcost <<= 3;
+#pragma unroll
+            for (int q = 0; q < 6; q++)
+                if ((c[q] << 3) + 2 + q < bcost) bcost = (c[q] << 3) + 2 + q;
+        }
         if (bcost & 7)
         {
             int dir = (bcost & 7) - 2;
             bx += hex_dx(dir + 1); by += hex_dy(dir + 1);
             for (int i = (hex_range >> 1) - 1; i > 0 && bx >= minx && bx <= maxx && by >= miny && by <= maxy; i--)
             {
-                c0 = fc(hex_dx(dir), hex_dy(dir));
-                c1 = fc(hex_dx(dir + 1), hex_dy(dir + 1));
-                c2 = fc(hex_dx(dir + 2), hex_dy(dir + 2));
+                const int mx[3] = { bx + hex_dx(dir), bx + hex_dx(dir + 1), bx + hex_dx(dir + 2) };
+                const int my[3] = { by + hex_dy(dir), by + hex_dy(dir + 1), by + hex_dy(dir + 2) };
+                int c[3];
+                fpel_costs<P, G, 3>(s, mx, my, c);
                 bcost &= ~7;
-                if ((c0 << 3) + 1 < bcost) bcost = (c0 << 3) + 1;
-                if ((c1 << 3) + 2 < bcost) bcost = (c1 << 3) + 2;
-                if ((c2 << 3) + 3 < bcost) bcost = (c2 << 3) + 3;
+                if ((c[0] << 3) + 1 < bcost) bcost = (c[0] << 3) + 1;
+                if ((c[1] << 3) + 2 < bcost) bcost = (c[1] << 3) + 2;
+                if ((c[2] << 3) + 3 < bcost) bcost = (c[2] << 3) + 3;
                 if (!(bcost & 7)) break;
                 dir += (bcost & 7) - 2;
                 dir = dir < 0 ? dir + 6 : (dir > 5 ? dir - 6 : dir);   // mod6m1[dir + 1]
@@ -904,10 +1009,16 @@ __global__ __launch_bounds__(X265AMD_BLOCK, X265AMD_ME_WAVES) void k_motion_sear
         }
         bcost >>= 3;
         int sdir = 0;
-        for (int k = 1; k <= 8; k++)
+#pragma unroll
+        for (int k0 = 1; k0 <= 8; k0 += 4)
         {
-            const int c = fc(sq_dx(k), sq_dy(k));
-            if (c < bcost) { bcost = c; sdir = k; }
+            const int mx[4] = { bx + sq_dx(k0), bx + sq_dx(k0 + 1), bx + sq_dx(k0 + 2), bx + sq_dx(k0 + 3) };
+            const int my[4] = { by + sq_dy(k0), by + sq_dy(k0 + 1), by + sq_dy(k0 + 2), by + sq_dy(k0 + 3) };
+            int c[4];
+            fpel_costs<P, G, 4>(s, mx, my, c);
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+                if (c[q] < bcost) { bcost = c[q]; sdir = k0 + q; }
         }
         bx += sq_dx(sdir); by += sq_dy(sdir);
     }
@@ -922,27 +1033,27 @@ __global__ __launch_bounds__(X265AMD_BLOCK, X265AMD_ME_WAVES) void k_motion_sear
         bcost = s.mvcost(qx, qy);
     else
     {
-        if (hsatd) bcost = subpel_cost<P, G>(s, qx, qy, true) + s.mvcost(qx, qy);
+        if (hsatd) bcost = spc(qx, qy, true) + s.mvcost(qx, qy);
         for (int it = 0; it < wl.x; it++)
         {
             int bdir = 0;
             for (int i = 1; i <= wl.y; i++)
             {
                 const int tx = qx + 2 * sq_dx(i), ty = qy + 2 * sq_dy(i);
-                const int c = subpel_cost<P, G>(s, tx, ty, hsatd) + s.mvcost(tx, ty);
+                const int c = spc(tx, ty, hsatd) + s.mvcost(tx, ty);
                 if (c < bcost) { bcost = c; bdir = i; }
             }
             if (!bdir) break;
             qx += 2 * sq_dx(bdir); qy += 2 * sq_dy(bdir);
         }
-        if (!hsatd) bcost = subpel_cost<P, G>(s, qx, qy, true) + s.mvcost(qx, qy);
+        if (!hsatd) bcost = spc(qx, qy, true) + s.mvcost(qx, qy);
         for (int it = 0; it < wl.z; it++)
         {
             int bdir = 0;
             for (int i = 1; i <= wl.w; i++)
             {
                 const int tx = qx + sq_dx(i), ty = qy + sq_dy(i);
-                const int c = subpel_cost<P, G>(s, tx, ty, true) + s.mvcost(tx, ty);
+                const int c = spc(tx, ty, true) + s.mvcost(tx, ty);
                 if (c < bcost) { bcost = c; bdir = i; }
             }
             if (!bdir) break;
