@@ -28,6 +28,9 @@ namespace x265amd {
 
 // -------------------------------------------------------------- unit math
 
+#ifndef X265AMD_NT_LOADS
+#define X265AMD_NT_LOADS 0
+#endif
 template <typename P, int UW, int UH>
 __device__ __forceinline__ uint32_t unit_sad(const P* a, intptr_t sa, const P* b, intptr_t sb)
 {
@@ -39,7 +42,14 @@ __device__ __forceinline__ uint32_t unit_sad(const P* a, intptr_t sa, const P* b
         {
             if constexpr (UW == 8)
             {
+#if X265AMD_NT_LOADS
+                // streaming rows: non-temporal loads (A/B builds only)
+                typedef unsigned int nt_u32x2 __attribute__((ext_vector_type(2)));
+                const nt_u32x2 va = __builtin_nontemporal_load((const nt_u32x2*)(a + y * sa));
+                const nt_u32x2 vb = __builtin_nontemporal_load((const nt_u32x2*)(b + y * sb));
+#else
                 uint2 va = ldu<uint2>(a + y * sa), vb = ldu<uint2>(b + y * sb);
+#endif
                 s = __builtin_amdgcn_sad_u8(va.x, vb.x, s);
                 s = __builtin_amdgcn_sad_u8(va.y, vb.y, s);
             }
@@ -535,6 +545,36 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_sad_multi(const BatchGroup g)
     }
 }
 
+// sad_x3 / sad_x4 of small blocks with one lane per (job, reference): lanes 4j .. 4j + 3 are job j's
+// references 0 .. NREF - 1 (the fourth idle for x3).  The four lanes read the same source rows (one
+// transaction) and four reference blocks, so one load instruction of a wave covers 16 jobs x 4 references;
+// with one lane per job the wave's reference loads step through four separate blocks per lane.  Outputs
+// land contiguously.  For blocks of at most 4 units (8x8, 8x16, 16x8, 4x8 ...), where a lane per job
+// holds little work.
+template <typename P, int NREF, int UW, int UH>
+__global__ __launch_bounds__(X265AMD_BLOCK) void k_sad_multi_ref(const BatchGroup g)
+{
+    const uint32_t gb = xcd_block();
+    const SubBatch& sub = group_sub(g, gb);
+    const int w = sub.w, h = sub.h, n = sub.n;
+    const intptr_t fs = sub.sa, rs = sub.sb;
+    const uint32_t lb = gb - sub.block0;
+    const int64_t job = (int64_t)lb * (X265AMD_BLOCK >> 2) + (threadIdx.x >> 2);
+    const int k = threadIdx.x & 3;
+    const bool live = job < n && k < NREF;
+    if (!live) return;
+    const P* pf = (const P*)sub.a + sub.aoff[job];
+    const P* pr = (const P*)sub.b + sub.boff[job * NREF + k];
+    const int ux = w / UW, units = ux * (h / UH);
+    uint32_t acc = 0;
+    for (int u = 0; u < units; u++)
+    {
+        const int x = (u % ux) * UW, y = (u / ux) * UH;
+        acc += unit_sad<P, UW, UH>(pf + y * fs + x, fs, pr + y * rs + x, rs);
+    }
+    ((int32_t*)sub.d)[job * NREF + k] = (int32_t)acc;
+}
+
 // -------------------------------------------------------------- dispatch
 
 // kernel class of a batch: (op, unit width, unit height) packed in an int
@@ -645,9 +685,25 @@ static int dispatch_cmp(int op, int count, const x265amd_cmp_batch* bt, hipStrea
         [&](int c, const BatchGroup& g, uint32_t blocks) { return launch_cmp_class<P>(c, g, blocks, st); });
 }
 
+// X265AMD_SADX_LANES=0: the lane-per-job form for every size (1, the default: lane per reference for blocks
+// of at most 4 units)
+static int sadx_lanes()
+{
+    static int v = -1;
+    if (v < 0)
+    {
+        const char* e = getenv("X265AMD_SADX_LANES");
+        v = e ? atoi(e) : 1;
+    }
+    return v;
+}
+constexpr int kSadRefOp = 0x7f;   // class tag of k_sad_multi_ref
+
 static int sad_multi_class(int, int w, int h)
 {
     if ((w % 4) || (h % 4) || w > 64 || h > 64 || w < 4 || h < 4) return -X265AMD_EINVAL;
+    const int uw = (w % 8) ? 4 : 8;
+    if (sadx_lanes() && (w / uw) * (h / 4) <= 4) return cmp_pack(kSadRefOp, uw, 4);
     // (8x8 units measured no faster for sad_x4 8x8 and slower for 16x16: profiles/r04/sad_uh8_ab_and_me_async.txt)
     if (w % 8 == 0 && h % 8 == 0 && sad_uh8() > 1) return cmp_pack(X265AMD_SAD, 8, 8);
     return cmp_pack(X265AMD_SAD, (w % 8) ? 4 : 8, 4);
@@ -659,9 +715,16 @@ static int dispatch_multi(int count, const x265amd_cmp_batch* bt, hipStream_t st
     std::vector<int> cls;
     if (int rc = cmp_classes(count, bt, cls, sad_multi_class, 0)) return rc;
     return launch_grouped(count, cls.data(), BatchGroup{},
-        [&](int i, SubBatch& s) { cmp_fill(bt[i], cls[i], s); },
+        [&](int i, SubBatch& s) {
+            cmp_fill(bt[i], cls[i], s);
+            if ((cls[i] >> 16) == kSadRefOp) s.lg = 2;     // four lanes per job
+        },
         [&](int c, const BatchGroup& g, uint32_t blocks) {
-            if (((c >> 8) & 0xff) == 8 && (c & 0xff) == 8)
+            if ((c >> 16) == kSadRefOp && ((c >> 8) & 0xff) == 8)
+                hipLaunchKernelGGL((k_sad_multi_ref<P, NREF, 8, 4>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, g);
+            else if ((c >> 16) == kSadRefOp)
+                hipLaunchKernelGGL((k_sad_multi_ref<P, NREF, 4, 4>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, g);
+            else if (((c >> 8) & 0xff) == 8 && (c & 0xff) == 8)
                 hipLaunchKernelGGL((k_sad_multi<P, NREF, 8, 8>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, g);
             else if (((c >> 8) & 0xff) == 8)
                 hipLaunchKernelGGL((k_sad_multi<P, NREF, 8, 4>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, g);

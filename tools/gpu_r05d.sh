@@ -5,6 +5,10 @@
 set -o pipefail
 mkdir -p gpurun_out/r05/d
 export TMPDIR=/tmp
+echo "== interp diff: round-4 rewrite (a052ed0) lib"
+X265AMD_LIB=$PWD/src/x265_amd/ab/libx265amd_a052.so timeout -k 10 200 python3 -u tools/interp_diff.py 2>&1 | tee gpurun_out/r05/d/interp_diff_a052.txt
+echo "== interp diff: current lib"
+timeout -k 10 200 python3 -u tools/interp_diff.py 2>&1 | tee gpurun_out/r05/d/interp_diff_cur.txt
 timeout -k 10 420 python3 -u bench.py --steps 2 --warmup 0 > gpurun_out/r05/d/bench_short.json 2> gpurun_out/r05/d/bench_short.err \
     || { tail -30 gpurun_out/r05/d/bench_short.err; exit 1; }
 tail -c 2500 gpurun_out/r05/d/bench_short.json
@@ -15,7 +19,7 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_ou
     || { tail -20 $GRAFT_REPO_ROOT/gpurun_out/r05/d/bench_rocprof.err; exit 1; }
 cd $GRAFT_REPO_ROOT
 find gpurun_out/r05/d/prof -name "*kernel_stats.csv" | head -5
-rm -f $(find gpurun_out/r05/d/prof -name "*_trace.csv")
+find gpurun_out/r05/d/prof -type f ! -name "*_stats.csv" -delete
 python3 -c "
 from src.x265_amd.synth import SyntheticSource
 SyntheticSource(3840, 2160, 16, 8).write_yuv('/tmp/s16.yuv')" || exit 1
@@ -25,16 +29,16 @@ for pmc in FETCH_SIZE WRITE_SIZE; do
       $GRAFT_REPO_ROOT/oracle/_ref/x265la8 --input /tmp/s16.yuv --input-res 3840x2160 --fps 30 --frames 16 --preset medium \
       --pools 16 --no-info -o /tmp/p.hevc > $GRAFT_REPO_ROOT/gpurun_out/r05/d/pmc_$pmc.log 2>&1 \
       || { tail -20 $GRAFT_REPO_ROOT/gpurun_out/r05/d/pmc_$pmc.log; exit 1; }
+  python3 $GRAFT_REPO_ROOT/tools/pmc_by_kernel.py $GRAFT_REPO_ROOT/gpurun_out/r05/d/pmc_$pmc \
+      > $GRAFT_REPO_ROOT/gpurun_out/r05/d/pmc_${pmc}_by_kernel.json || exit 1
+  rm -rf $GRAFT_REPO_ROOT/gpurun_out/r05/d/pmc_$pmc
   echo "pmc $pmc done"
+  du -sh $GRAFT_REPO_ROOT/gpurun_out/r05/d
 done
 X265AMD_ME_STATS=1 timeout -k 10 300 rocprofv3 --kernel-trace --hip-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/r05/d/hiptrace -o enc -- \
     $GRAFT_REPO_ROOT/oracle/_ref/x265la8 --input /tmp/s16.yuv --input-res 3840x2160 --fps 30 --frames 16 --preset medium \
     --pools 16 --no-info -o /tmp/p.hevc > $GRAFT_REPO_ROOT/gpurun_out/r05/d/hiptrace.log 2>&1 \
     || { tail -20 $GRAFT_REPO_ROOT/gpurun_out/r05/d/hiptrace.log; exit 1; }
 find $GRAFT_REPO_ROOT/gpurun_out/r05/d/hiptrace -name "*_stats.csv" | head
-rm -f $(find $GRAFT_REPO_ROOT/gpurun_out/r05/d/hiptrace -name "*_trace.csv")
+find $GRAFT_REPO_ROOT/gpurun_out/r05/d/hiptrace -type f ! -name "*_stats.csv" -delete
 cd $GRAFT_REPO_ROOT
-echo "== interp diff: round-4 rewrite (a052ed0) lib"
-X265AMD_LIB=$PWD/src/x265_amd/ab/libx265amd_a052.so timeout -k 10 200 python3 -u tools/interp_diff.py 2>&1 | tee gpurun_out/r05/d/interp_diff_a052.txt
-echo "== interp diff: current lib"
-timeout -k 10 200 python3 -u tools/interp_diff.py 2>&1 | tee gpurun_out/r05/d/interp_diff_cur.txt
