@@ -862,6 +862,12 @@ typedef struct
      * algorithmic bytes, and the longest launch */
     int64_t evals_fpel, evals_subpel;
     double algo_bytes, kernel_ms_max;
+    /* (round 5) where the waiting time goes: waits and their summed ms by duration (< 0.05, < 0.2, < 1,
+     * < 5, >= 5 ms), and service batches (take -> outputs published) by the same bins */
+    int64_t wait_hist[5];
+    double wait_hist_ms[5];
+    int64_t batch_hist[5];
+    double batch_hist_ms[5];
 } x265amd_mes_counters;
 int x265amd_mes_stats(x265amd_mes* mes, x265amd_mes_counters* out);
 

@@ -87,7 +87,7 @@ void read_mode()
     if (g_mode == MODE_CHECK)
         atexit(print_check_summary);
     const char* pr = getenv("X265AMD_LA_PROPAGATE");
-    g_propagate = pr && atoi(pr) != 0;
+    g_propagate = pr ? atoi(pr) != 0 : true;      /* on by default since round 5 (bit-identical, check mode 0 mismatches) */
     const char* st = getenv("X265AMD_LA_STATS");
     g_stats_on = st && *st && strcmp(st, "0");
     if (g_stats_on)

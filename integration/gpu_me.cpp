@@ -155,6 +155,13 @@ void add_counters(x265amd_mes_counters& tot, const x265amd_mes_counters& c)
     tot.algo_bytes += c.algo_bytes;
     if (c.kernel_ms_max > tot.kernel_ms_max) tot.kernel_ms_max = c.kernel_ms_max;
     if (c.max_requests_per_batch > tot.max_requests_per_batch) tot.max_requests_per_batch = c.max_requests_per_batch;
+    for (int b = 0; b < 5; b++)
+    {
+        tot.wait_hist[b] += c.wait_hist[b];
+        tot.wait_hist_ms[b] += c.wait_hist_ms[b];
+        tot.batch_hist[b] += c.batch_hist[b];
+        tot.batch_hist_ms[b] += c.batch_hist_ms[b];
+    }
 }
 
 void print_stats()
@@ -183,6 +190,17 @@ void print_stats()
                 (long long)tot.waits_blocked, (long long)tot.uploads, tot.upload_bytes / 1e6, tot.upload_ms,
                 g_sessions.size(), (long long)tot.evals_fpel, (long long)tot.evals_subpel, tot.algo_bytes / 1e9,
                 tot.kernel_ms_max);
+    if (tot.batches)
+    {
+        static const char* bins[5] = { "<0.05", "<0.2", "<1", "<5", ">=5" };
+        fprintf(stderr, "[x265me] waits by duration (ms: count / summed ms):");
+        for (int b = 0; b < 5; b++)
+            fprintf(stderr, " %s %lld / %.0f", bins[b], (long long)tot.wait_hist[b], tot.wait_hist_ms[b]);
+        fprintf(stderr, "\n[x265me] batches by duration (ms: count / summed ms):");
+        for (int b = 0; b < 5; b++)
+            fprintf(stderr, " %s %lld / %.0f", bins[b], (long long)tot.batch_hist[b], tot.batch_hist_ms[b]);
+        fprintf(stderr, "\n");
+    }
     if (g_gpus > 1)
     {
         fprintf(stderr, "[x265me] searches per device session:");

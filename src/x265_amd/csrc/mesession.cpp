@@ -173,7 +173,8 @@ struct x265amd_mes
     int trace = 0;                    // X265AMD_MES_TRACE=n: log the first n posts / launches / waits
     bool zerocopy = false;            // X265AMD_MES_ZEROCOPY=1: the kernel reads / writes the pinned staging
     bool prio = true;                 // X265AMD_MES_PRIORITY=0: launch streams at the default priority
-    bool lspin = true;                // X265AMD_MES_LSPIN=0: launchers sleep in hipEventSynchronize
+    bool lspin = false;               // X265AMD_MES_LSPIN=1: launchers poll for completion (a busy core each:
+                                      // slower on the encoder's 16-core budget, profiles/r05/bench_lspin_pinned_ab.txt)
     std::atomic<int> traced{ 0 };
 
     // statistics (x265amd_mes_stats)
@@ -431,6 +432,12 @@ void read_out(const uint8_t* H, const Layout& L, int i, x265amd_mes_job& j)
     j.out_cost = ((const int32_t*)(H + L.out_cost))[i];
 }
 
+// duration bins of the wait / batch histograms: < 0.05, < 0.2, < 1, < 5, >= 5 ms
+static int hist_bin(double ms)
+{
+    return ms < 0.05 ? 0 : ms < 0.2 ? 1 : ms < 1 ? 2 : ms < 5 ? 3 : 4;
+}
+
 // ---------------------------------------------------------------- launch service
 // one service thread: take every queued request, one staged batch per PU size, one upload, one launch
 // (all sizes), one download, publish
@@ -630,6 +637,10 @@ void launcher_main(x265amd_mes* s, x265amd_mes_launcher* L)
             s->st.evals_subpel += esp;
             s->st.algo_bytes += algo;
             if (kms > s->st.kernel_ms_max) s->st.kernel_ms_max = kms;
+            const double bms = 1e3 * (t_done - t_take);
+            const int hb = hist_bin(bms);
+            s->st.batch_hist[hb]++;
+            s->st.batch_hist_ms[hb] += bms;
             s->st.batch_ms += 1e3 * (t_done - t_take);
             s->st.queue_ms += 1e3 * qdelay;
             if ((int64_t)take.size() > s->st.max_requests_per_batch) s->st.max_requests_per_batch = (int64_t)take.size();
@@ -978,6 +989,9 @@ extern "C" int x265amd_mes_wait(x265amd_mes* s, int ticket, int n, x265amd_mes_j
         std::lock_guard<std::mutex> g(s->smu);
         s->st.waits++;
         s->st.wait_ms += 1e3 * dt;
+        const int b = hist_bin(1e3 * dt);
+        s->st.wait_hist[b]++;
+        s->st.wait_hist_ms[b] += 1e3 * dt;
         s->st.waits_blocked += slept;
     }
     return rc ? record(rc) : 0;

@@ -28,10 +28,22 @@ namespace x265amd {
 
 // -------------------------------------------------------------- unit math
 
-#ifndef X265AMD_NT_LOADS
-#define X265AMD_NT_LOADS 0
-#endif
-template <typename P, int UW, int UH>
+// a vector load of T; NT: non-temporal (rows read once — a batch of disjoint blocks — are kept from
+// displacing lines that are re-read; measured on disjoint SAD batches 8x8 0.64 -> 0.71, 64x64 0.79 -> 0.89 of
+// the HBM peak, profiles/r05/sad_nt_ab.txt)
+template <typename T, bool NT>
+__device__ __forceinline__ T ldx(const void* p)
+{
+    typedef unsigned int v2u __attribute__((ext_vector_type(2)));
+    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+    if constexpr (!NT) return ldu<T>(p);
+    else if constexpr (sizeof(T) == 4) return __builtin_bit_cast(T, __builtin_nontemporal_load((const unsigned int*)p));
+    else if constexpr (sizeof(T) == 8) return __builtin_bit_cast(T, __builtin_nontemporal_load((const v2u*)p));
+    else return __builtin_bit_cast(T, __builtin_nontemporal_load((const v4u*)p));
+}
+
+// NTA / NTB: non-temporal loads of the first / second block
+template <typename P, int UW, int UH, bool NTA = false, bool NTB = false>
 __device__ __forceinline__ uint32_t unit_sad(const P* a, intptr_t sa, const P* b, intptr_t sb)
 {
     uint32_t s = 0;
@@ -42,20 +54,13 @@ __device__ __forceinline__ uint32_t unit_sad(const P* a, intptr_t sa, const P* b
         {
             if constexpr (UW == 8)
             {
-#if X265AMD_NT_LOADS
-                // streaming rows: non-temporal loads (A/B builds only)
-                typedef unsigned int nt_u32x2 __attribute__((ext_vector_type(2)));
-                const nt_u32x2 va = __builtin_nontemporal_load((const nt_u32x2*)(a + y * sa));
-                const nt_u32x2 vb = __builtin_nontemporal_load((const nt_u32x2*)(b + y * sb));
-#else
-                uint2 va = ldu<uint2>(a + y * sa), vb = ldu<uint2>(b + y * sb);
-#endif
+                const uint2 va = ldx<uint2, NTA>(a + y * sa), vb = ldx<uint2, NTB>(b + y * sb);
                 s = __builtin_amdgcn_sad_u8(va.x, vb.x, s);
                 s = __builtin_amdgcn_sad_u8(va.y, vb.y, s);
             }
             else
             {
-                uint32_t va = ldu<uint32_t>(a + y * sa), vb = ldu<uint32_t>(b + y * sb);
+                const uint32_t va = ldx<uint32_t, NTA>(a + y * sa), vb = ldx<uint32_t, NTB>(b + y * sb);
                 s = __builtin_amdgcn_sad_u8(va, vb, s);
             }
         }
@@ -63,7 +68,7 @@ __device__ __forceinline__ uint32_t unit_sad(const P* a, intptr_t sa, const P* b
         {
             if constexpr (UW == 8)
             {
-                uint4 va = ldu<uint4>(a + y * sa), vb = ldu<uint4>(b + y * sb);
+                const uint4 va = ldx<uint4, NTA>(a + y * sa), vb = ldx<uint4, NTB>(b + y * sb);
                 s = __builtin_amdgcn_sad_u16(va.x, vb.x, s);
                 s = __builtin_amdgcn_sad_u16(va.y, vb.y, s);
                 s = __builtin_amdgcn_sad_u16(va.z, vb.z, s);
@@ -71,7 +76,7 @@ __device__ __forceinline__ uint32_t unit_sad(const P* a, intptr_t sa, const P* b
             }
             else
             {
-                uint2 va = ldu<uint2>(a + y * sa), vb = ldu<uint2>(b + y * sb);
+                const uint2 va = ldx<uint2, NTA>(a + y * sa), vb = ldx<uint2, NTB>(b + y * sb);
                 s = __builtin_amdgcn_sad_u16(va.x, vb.x, s);
                 s = __builtin_amdgcn_sad_u16(va.y, vb.y, s);
             }
@@ -395,7 +400,7 @@ __device__ __forceinline__ int psy_energy4(const P* a, intptr_t sa)
 // -------------------------------------------------------------- kernels
 // (grouped launches, common.h: a = block A, b = block B, d = out)
 
-template <int OP, typename P, int UW, int UH>
+template <int OP, typename P, int UW, int UH, bool NT = false>
 __global__ __launch_bounds__(X265AMD_BLOCK) void k_pixelcmp(const BatchGroup g)
 {
     const uint32_t gb = xcd_block();
@@ -448,7 +453,7 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_pixelcmp(const BatchGroup g)
             const int x = (u % ux) * UW, y = (u / ux) * UH;
             const P* qa = pa + y * sa + x;
             if constexpr (OP == X265AMD_SAD)
-                acc += unit_sad<P, UW, UH>(qa, sa, pb + y * sb + x, sb);
+                acc += unit_sad<P, UW, UH, NT, NT>(qa, sa, pb + y * sb + x, sb);
             else if constexpr (OP == X265AMD_SATD)
                 acc += unit_satd<P, UW>(qa, sa, pb + y * sb + x, sb);
             else if constexpr (OP == X265AMD_SA8D)
@@ -497,7 +502,7 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_pixelcmp(const BatchGroup g)
     }
 }
 
-template <typename P, int NREF, int UW, int UH>
+template <typename P, int NREF, int UW, int UH, bool NT = false>
 __global__ __launch_bounds__(X265AMD_BLOCK) void k_sad_multi(const BatchGroup g)
 {
     const uint32_t gb = xcd_block();
@@ -528,7 +533,7 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_sad_multi(const BatchGroup g)
             const int x = (u % ux) * UW, y = (u / ux) * UH;
 #pragma unroll
             for (int k = 0; k < NREF; k++)
-                acc[k] += unit_sad<P, UW, UH>(pf + y * fs + x, fs, pr[k] + y * rs + x, rs);
+                acc[k] += unit_sad<P, UW, UH, false, NT>(pf + y * fs + x, fs, pr[k] + y * rs + x, rs);
         }
     }
 #pragma unroll
@@ -623,9 +628,30 @@ static int cmp_lg(int cls, int w, int h)
     return lanes_log2((w / uw) * (h / uh));
 }
 
+// X265AMD_NT=0: SAD / sad_x3 / sad_x4 with ordinary loads (1, the default: the blocks a job reads once —
+// both blocks of a SAD, the references of sad_x3 / x4 — non-temporal)
+static bool nt_loads()
+{
+    static int v = -1;
+    if (v < 0)
+    {
+        const char* e = getenv("X265AMD_NT");
+        v = e ? atoi(e) != 0 : 1;
+    }
+    return v != 0;
+}
+
 template <int OP, typename P, int UW, int UH>
 static int launch_cmp(const BatchGroup& g, uint32_t blocks, hipStream_t st)
 {
+    if constexpr (OP == X265AMD_SAD)
+    {
+        if (nt_loads())
+        {
+            hipLaunchKernelGGL((k_pixelcmp<OP, P, UW, UH, true>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, g);
+            return (int)hipGetLastError();
+        }
+    }
     hipLaunchKernelGGL((k_pixelcmp<OP, P, UW, UH>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, g);
     return (int)hipGetLastError();
 }
@@ -685,15 +711,15 @@ static int dispatch_cmp(int op, int count, const x265amd_cmp_batch* bt, hipStrea
         [&](int c, const BatchGroup& g, uint32_t blocks) { return launch_cmp_class<P>(c, g, blocks, st); });
 }
 
-// X265AMD_SADX_LANES=0: the lane-per-job form for every size (1, the default: lane per reference for blocks
-// of at most 4 units)
+// X265AMD_SADX_LANES=1: lane per reference for blocks of at most 4 units (0, the default: lane per job —
+// measured faster, sad_x4 8x8 0.57 against 0.53, profiles/r05/sad_nt_ab.txt)
 static int sadx_lanes()
 {
     static int v = -1;
     if (v < 0)
     {
         const char* e = getenv("X265AMD_SADX_LANES");
-        v = e ? atoi(e) : 1;
+        v = e ? atoi(e) : 0;
     }
     return v;
 }
@@ -725,11 +751,26 @@ static int dispatch_multi(int count, const x265amd_cmp_batch* bt, hipStream_t st
             else if ((c >> 16) == kSadRefOp)
                 hipLaunchKernelGGL((k_sad_multi_ref<P, NREF, 4, 4>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, g);
             else if (((c >> 8) & 0xff) == 8 && (c & 0xff) == 8)
-                hipLaunchKernelGGL((k_sad_multi<P, NREF, 8, 8>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, g);
+            {
+                if (nt_loads())
+                    hipLaunchKernelGGL((k_sad_multi<P, NREF, 8, 8, true>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, g);
+                else
+                    hipLaunchKernelGGL((k_sad_multi<P, NREF, 8, 8>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, g);
+            }
             else if (((c >> 8) & 0xff) == 8)
-                hipLaunchKernelGGL((k_sad_multi<P, NREF, 8, 4>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, g);
+            {
+                if (nt_loads())
+                    hipLaunchKernelGGL((k_sad_multi<P, NREF, 8, 4, true>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, g);
+                else
+                    hipLaunchKernelGGL((k_sad_multi<P, NREF, 8, 4>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, g);
+            }
             else
-                hipLaunchKernelGGL((k_sad_multi<P, NREF, 4, 4>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, g);
+            {
+                if (nt_loads())
+                    hipLaunchKernelGGL((k_sad_multi<P, NREF, 4, 4, true>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, g);
+                else
+                    hipLaunchKernelGGL((k_sad_multi<P, NREF, 4, 4>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, g);
+            }
             return (int)hipGetLastError();
         });
 }

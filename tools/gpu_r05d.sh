@@ -13,7 +13,7 @@ timeout -k 10 420 python3 -u bench.py --steps 2 --warmup 0 > gpurun_out/r05/d/be
     || { tail -30 gpurun_out/r05/d/bench_short.err; exit 1; }
 tail -c 2500 gpurun_out/r05/d/bench_short.json
 cd /tmp
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/r05/d/prof -o bench -- \
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/r05/d/prof -o bench -- \
     python3 $GRAFT_REPO_ROOT/bench.py --steps 1 --warmup 0 --no-replay --no-cpu \
     > $GRAFT_REPO_ROOT/gpurun_out/r05/d/bench_rocprof.json 2> $GRAFT_REPO_ROOT/gpurun_out/r05/d/bench_rocprof.err \
     || { tail -20 $GRAFT_REPO_ROOT/gpurun_out/r05/d/bench_rocprof.err; exit 1; }
@@ -25,7 +25,7 @@ from src.x265_amd.synth import SyntheticSource
 SyntheticSource(3840, 2160, 16, 8).write_yuv('/tmp/s16.yuv')" || exit 1
 cd /tmp
 for pmc in FETCH_SIZE WRITE_SIZE; do
-  X265AMD_ME_STATS=1 timeout -k 10 300 rocprofv3 --pmc $pmc -d $GRAFT_REPO_ROOT/gpurun_out/r05/d/pmc_$pmc -o enc -- \
+  X265AMD_ME_STATS=1 timeout -k 10 300 rocprofv3 --pmc $pmc --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/r05/d/pmc_$pmc -o enc -- \
       $GRAFT_REPO_ROOT/oracle/_ref/x265la8 --input /tmp/s16.yuv --input-res 3840x2160 --fps 30 --frames 16 --preset medium \
       --pools 16 --no-info -o /tmp/p.hevc > $GRAFT_REPO_ROOT/gpurun_out/r05/d/pmc_$pmc.log 2>&1 \
       || { tail -20 $GRAFT_REPO_ROOT/gpurun_out/r05/d/pmc_$pmc.log; exit 1; }
@@ -35,7 +35,7 @@ for pmc in FETCH_SIZE WRITE_SIZE; do
   echo "pmc $pmc done"
   du -sh $GRAFT_REPO_ROOT/gpurun_out/r05/d
 done
-X265AMD_ME_STATS=1 timeout -k 10 300 rocprofv3 --kernel-trace --hip-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/r05/d/hiptrace -o enc -- \
+X265AMD_ME_STATS=1 timeout -k 10 300 rocprofv3 --kernel-trace --hip-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/r05/d/hiptrace -o enc -- \
     $GRAFT_REPO_ROOT/oracle/_ref/x265la8 --input /tmp/s16.yuv --input-res 3840x2160 --fps 30 --frames 16 --preset medium \
     --pools 16 --no-info -o /tmp/p.hevc > $GRAFT_REPO_ROOT/gpurun_out/r05/d/hiptrace.log 2>&1 \
     || { tail -20 $GRAFT_REPO_ROOT/gpurun_out/r05/d/hiptrace.log; exit 1; }

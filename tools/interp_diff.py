@@ -18,8 +18,12 @@ def main():
     from cases import HPP, HVPP, VPP, case_interp, run_cpu, run_gpu
     from pyoracle import CpuOracle
 
+    import torch
+
     from src.x265_amd import Primitives
 
+    # torch's HIP runtime first (as the tests' fixture does): initialised after the library's, it finds no GPU
+    assert torch.cuda.is_available(), "needs the MI355X"
     prims = Primitives(device=0)
     orc = CpuOracle("oracle", 8)
     for op, taps, w, h in ((HPP, 4, 8, 8), (HPP, 4, 4, 4), (HPP, 4, 16, 16), (HPP, 8, 8, 8), (HPP, 8, 16, 16),
