@@ -245,6 +245,20 @@ __device__ __forceinline__ T ldu(const void* p)
     __builtin_memcpy(&v, p, sizeof(T));
     return v;
 }
+// a vector load of T; NT: non-temporal (rows read once — a batch of disjoint blocks — are kept from
+// displacing lines that are re-read; measured on disjoint SAD batches 8x8 0.64 -> 0.71, 64x64 0.79 -> 0.89 of
+// the HBM peak, profiles/r05/sad_nt_ab.txt)
+template <typename T, bool NT>
+__device__ __forceinline__ T ldx(const void* p)
+{
+    typedef unsigned int v2u __attribute__((ext_vector_type(2)));
+    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+    if constexpr (!NT) return ldu<T>(p);
+    else if constexpr (sizeof(T) == 4) return __builtin_bit_cast(T, __builtin_nontemporal_load((const unsigned int*)p));
+    else if constexpr (sizeof(T) == 8) return __builtin_bit_cast(T, __builtin_nontemporal_load((const v2u*)p));
+    else return __builtin_bit_cast(T, __builtin_nontemporal_load((const v4u*)p));
+}
+
 template <typename T>
 __device__ __forceinline__ void stu(void* p, T v)
 {

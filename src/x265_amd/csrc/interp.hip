@@ -135,6 +135,12 @@ __device__ __forceinline__ uint32_t alignb(uint32_t hi, uint32_t lo, int s)
     return s ? __builtin_amdgcn_alignbyte(hi, lo, s) : lo;
 }
 
+// X265AMD_NT_INTERP=1 (A/B builds): the 8-bit filter windows with non-temporal loads
+#ifndef X265AMD_NT_INTERP
+#define X265AMD_NT_INTERP 0
+#endif
+constexpr bool kNtInterp = X265AMD_NT_INTERP != 0;
+
 // bytes [0, NB) at p as biased dwords W[] (bytes past NB unspecified); two
 // overlapping loads that stay inside the NB-byte read window
 template <int NB>
@@ -144,7 +150,7 @@ __device__ __forceinline__ void load_win_dw(const uint8_t* p, uint32_t (&W)[(NB 
     if constexpr (NB > 8)
     {
         static_assert(NB <= 16, "window too large");
-        const uint2 h = ldu<uint2>(p), t = ldu<uint2>(p + NB - 8);
+        const uint2 h = ldx<uint2, kNtInterp>(p), t = ldx<uint2, kNtInterp>(p + NB - 8);
         constexpr int o = NB - 8;
         W[0] = h.x;
         W[1] = h.y;
@@ -158,7 +164,7 @@ __device__ __forceinline__ void load_win_dw(const uint8_t* p, uint32_t (&W)[(NB 
     else
     {
         static_assert(NB > 4, "window too small");
-        const uint32_t h = ldu<uint32_t>(p), t = ldu<uint32_t>(p + NB - 4);
+        const uint32_t h = ldx<uint32_t, kNtInterp>(p), t = ldx<uint32_t, kNtInterp>(p + NB - 4);
         W[0] = h;
         W[1] = alignb(0u, t, 8 - NB);
     }
@@ -256,12 +262,12 @@ __device__ __forceinline__ void vfilter_dot(const uint8_t* col, intptr_t ss, con
         {
             if constexpr (UW == 8)
             {
-                const uint2 v = ldu<uint2>(col + t * ss);
+                const uint2 v = ldx<uint2, kNtInterp>(col + t * ss);
                 rows[t][0] = v.x ^ 0x80808080u;
                 rows[t][1] = v.y ^ 0x80808080u;
             }
             else
-                rows[t][0] = ldu<uint32_t>(col + t * ss) ^ 0x80808080u;
+                rows[t][0] = ldx<uint32_t, kNtInterp>(col + t * ss) ^ 0x80808080u;
         }
         else
         {
@@ -315,12 +321,12 @@ __device__ __forceinline__ void vfilter_pk(const uint8_t* col, intptr_t ss, cons
         uint32_t w[UW / 4];
         if constexpr (UW == 8)
         {
-            const uint2 v = ldu<uint2>(col + t * ss);
+            const uint2 v = ldx<uint2, kNtInterp>(col + t * ss);
             w[0] = v.x;
             w[1] = v.y;
         }
         else
-            w[0] = ldu<uint32_t>(col + t * ss);
+            w[0] = ldx<uint32_t, kNtInterp>(col + t * ss);
         s16x2 pr[UW / 2];
 #pragma unroll
         for (int q = 0; q < UW / 4; q++)

@@ -36,6 +36,7 @@
 #include <mutex>
 #include <new>
 #include <thread>
+#include <sched.h>
 #include <unordered_map>
 #include <vector>
 
@@ -167,9 +168,21 @@ struct x265amd_mes
     std::condition_variable qcv;      // a request was queued
     std::vector<x265amd_mes_req*> rq;
     bool stop = false;
+    std::atomic<bool> stop_flag{ false };
     std::mutex dmu;                   // waiters sleep on dcv
     std::condition_variable dcv;
-    int spin_us = 50;
+    // The host cores are oversubscribed (the encoder's workers, frame and lookahead threads, and these
+    // launchers on its 16 cores): a thread woken from a condition variable waits for a core for 0.2-5 ms
+    // (profiles/r05/service_options_pinned_ab.txt: waits of that length sum to 10 of 13 s), and a
+    // notify can hand the notifier's core to the woken thread.  So waiters and idle launchers first spin
+    // (pause), then yield the core in a loop (sched_yield: any runnable thread goes first, otherwise the
+    // waiter re-checks at once), and only then sleep; notifies go only to threads counted as sleeping.
+    int spin_us = 50;                 // X265AMD_MES_SPIN_US: pause-spin before yielding
+    int yield_us = 5000;              // X265AMD_MES_YIELD_US: yield loop before sleeping (waits)
+    int idle_us = 500;                // X265AMD_MES_IDLE_US: launchers' yield loop on an empty queue
+    std::atomic<int> qsleepers{ 0 };  // launchers sleeping on qcv
+    int dsleepers = 0;                // waiters sleeping on dcv (guarded by dmu)
+    std::atomic<int64_t> queued{ 0 }; // requests posted (the launchers' lock-free "anything new?" check)
     int trace = 0;                    // X265AMD_MES_TRACE=n: log the first n posts / launches / waits
     bool zerocopy = false;            // X265AMD_MES_ZEROCOPY=1: the kernel reads / writes the pinned staging
     bool prio = true;                 // X265AMD_MES_PRIORITY=0: launch streams at the default priority
@@ -452,8 +465,26 @@ void launcher_main(x265amd_mes* s, x265amd_mes_launcher* L)
     for (;;)
     {
         {
+            // nothing queued: yield-loop on the lock-free post count (back to it whenever another launcher
+            // took what was posted), then sleep
             std::unique_lock<std::mutex> lk(s->qmu);
-            s->qcv.wait(lk, [&] { return s->stop || !s->rq.empty(); });
+            while (s->rq.empty() && !s->stop)
+            {
+                const int64_t seen = s->queued.load(std::memory_order_acquire);
+                lk.unlock();
+                const double until = now_s() + 1e-6 * s->idle_us;
+                bool moved = false;
+                while (!(moved = s->queued.load(std::memory_order_acquire) != seen) &&
+                       !s->stop_flag.load(std::memory_order_acquire) && now_s() < until)
+                    sched_yield();
+                lk.lock();
+                if (!moved && s->rq.empty() && !s->stop)
+                {
+                    s->qsleepers.fetch_add(1, std::memory_order_acq_rel);
+                    s->qcv.wait(lk, [&] { return s->stop || !s->rq.empty(); });
+                    s->qsleepers.fetch_sub(1, std::memory_order_acq_rel);
+                }
+            }
             if (s->rq.empty()) return;                 // stop requested and nothing left
             take.swap(s->rq);
             s->rq.clear();
@@ -612,17 +643,22 @@ void launcher_main(x265amd_mes* s, x265amd_mes_launcher* L)
                     for (int q = 0; q < r->n; q++, i++) read_out(H, lay[k], i, r->jobs[q]);
                 }
             }
+        // the states flip under dmu, where sleepers register, so a waiter that checked its state before the
+        // flip is counted before the count is read here (no lost wake-up); spinning / yielding waiters read
+        // the state without the lock
         double qdelay = 0;
-        for (auto* r : take)
-        {
-            qdelay += t_take - r->t_post;
-            r->rc = rc;
-            r->state.store(2, std::memory_order_release);
-        }
+        bool wake;
         {
             std::lock_guard<std::mutex> g(s->dmu);
+            for (auto* r : take)
+            {
+                qdelay += t_take - r->t_post;
+                r->rc = rc;
+                r->state.store(2, std::memory_order_release);
+            }
+            wake = s->dsleepers > 0;
         }
-        s->dcv.notify_all();
+        if (wake) s->dcv.notify_all();
         if (rc) record(rc);
         if (s->trace && s->traced.fetch_add(1) < s->trace)
             fprintf(stderr, "[mes] launcher %p done: rc %d, kernel %.3f ms, batch %.3f ms\n", (void*)L, rc, kms,
@@ -653,6 +689,8 @@ int start_service(x265amd_mes* s)
 {
     const int n = s->cfg.launchers;
     if (const char* e = getenv("X265AMD_MES_SPIN_US")) s->spin_us = atoi(e);
+    if (const char* e = getenv("X265AMD_MES_YIELD_US")) s->yield_us = atoi(e);
+    if (const char* e = getenv("X265AMD_MES_IDLE_US")) s->idle_us = atoi(e);
     if (const char* e = getenv("X265AMD_MES_TRACE")) s->trace = atoi(e);
     if (const char* e = getenv("X265AMD_MES_ZEROCOPY")) s->zerocopy = atoi(e) != 0;
     if (const char* e = getenv("X265AMD_MES_PRIORITY")) s->prio = atoi(e) != 0;
@@ -690,6 +728,7 @@ void stop_service(x265amd_mes* s)
     {
         std::lock_guard<std::mutex> g(s->qmu);
         s->stop = true;
+        s->stop_flag.store(true, std::memory_order_release);
     }
     s->qcv.notify_all();
     for (auto* L : s->launchers)
@@ -939,7 +978,9 @@ extern "C" int x265amd_mes_post420(x265amd_mes* s, int w, int h, const void* fen
         std::lock_guard<std::mutex> g(s->qmu);
         s->rq.push_back(&r);
     }
-    s->qcv.notify_one();
+    s->queued.fetch_add(1, std::memory_order_acq_rel);
+    if (s->qsleepers.load(std::memory_order_acquire) > 0)
+        s->qcv.notify_one();
     *ticket = k;
     if (s->trace && s->traced.fetch_add(1) < s->trace)
         fprintf(stderr, "[mes] post %dx%d n %d chroma %d ticket %d\n", w, h, n, (int)r.chroma, k);
@@ -967,11 +1008,16 @@ extern "C" int x265amd_mes_wait(x265amd_mes* s, int ticket, int n, x265amd_mes_j
         const double until = t0 + 1e-6 * s->spin_us;
         while (r.state.load(std::memory_order_acquire) != 2 && now_s() < until)
             __builtin_ia32_pause();
+        const double yuntil = t0 + 1e-6 * (s->spin_us + s->yield_us);
+        while (r.state.load(std::memory_order_acquire) != 2 && now_s() < yuntil)
+            sched_yield();
         if (r.state.load(std::memory_order_acquire) != 2)
         {
             slept = true;
             std::unique_lock<std::mutex> lk(s->dmu);
+            s->dsleepers++;
             s->dcv.wait(lk, [&] { return r.state.load(std::memory_order_acquire) == 2; });
+            s->dsleepers--;
         }
     }
     const double dt = now_s() - t0;

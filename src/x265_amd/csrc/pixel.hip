@@ -28,20 +28,6 @@ namespace x265amd {
 
 // -------------------------------------------------------------- unit math
 
-// a vector load of T; NT: non-temporal (rows read once — a batch of disjoint blocks — are kept from
-// displacing lines that are re-read; measured on disjoint SAD batches 8x8 0.64 -> 0.71, 64x64 0.79 -> 0.89 of
-// the HBM peak, profiles/r05/sad_nt_ab.txt)
-template <typename T, bool NT>
-__device__ __forceinline__ T ldx(const void* p)
-{
-    typedef unsigned int v2u __attribute__((ext_vector_type(2)));
-    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
-    if constexpr (!NT) return ldu<T>(p);
-    else if constexpr (sizeof(T) == 4) return __builtin_bit_cast(T, __builtin_nontemporal_load((const unsigned int*)p));
-    else if constexpr (sizeof(T) == 8) return __builtin_bit_cast(T, __builtin_nontemporal_load((const v2u*)p));
-    else return __builtin_bit_cast(T, __builtin_nontemporal_load((const v4u*)p));
-}
-
 // NTA / NTB: non-temporal loads of the first / second block
 template <typename P, int UW, int UH, bool NTA = false, bool NTB = false>
 __device__ __forceinline__ uint32_t unit_sad(const P* a, intptr_t sa, const P* b, intptr_t sb)
@@ -628,8 +614,9 @@ static int cmp_lg(int cls, int w, int h)
     return lanes_log2((w / uw) * (h / uh));
 }
 
-// X265AMD_NT=0: SAD / sad_x3 / sad_x4 with ordinary loads (1, the default: the blocks a job reads once —
-// both blocks of a SAD, the references of sad_x3 / x4 — non-temporal)
+// X265AMD_NT=0: SAD with ordinary loads (1, the default: both blocks non-temporal).  sad_x3 / sad_x4 keep
+// ordinary loads: their wave's reference rows share lines between the per-reference load instructions, which
+// non-temporal loads turn into repeated HBM reads (sad_x4 8x8 0.57 -> 0.40, profiles/r05/sad_nt_ab.txt)
 static bool nt_loads()
 {
     static int v = -1;
@@ -751,26 +738,11 @@ static int dispatch_multi(int count, const x265amd_cmp_batch* bt, hipStream_t st
             else if ((c >> 16) == kSadRefOp)
                 hipLaunchKernelGGL((k_sad_multi_ref<P, NREF, 4, 4>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, g);
             else if (((c >> 8) & 0xff) == 8 && (c & 0xff) == 8)
-            {
-                if (nt_loads())
-                    hipLaunchKernelGGL((k_sad_multi<P, NREF, 8, 8, true>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, g);
-                else
-                    hipLaunchKernelGGL((k_sad_multi<P, NREF, 8, 8>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, g);
-            }
+                hipLaunchKernelGGL((k_sad_multi<P, NREF, 8, 8>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, g);
             else if (((c >> 8) & 0xff) == 8)
-            {
-                if (nt_loads())
-                    hipLaunchKernelGGL((k_sad_multi<P, NREF, 8, 4, true>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, g);
-                else
-                    hipLaunchKernelGGL((k_sad_multi<P, NREF, 8, 4>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, g);
-            }
+                hipLaunchKernelGGL((k_sad_multi<P, NREF, 8, 4>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, g);
             else
-            {
-                if (nt_loads())
-                    hipLaunchKernelGGL((k_sad_multi<P, NREF, 4, 4, true>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, g);
-                else
-                    hipLaunchKernelGGL((k_sad_multi<P, NREF, 4, 4>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, g);
-            }
+                hipLaunchKernelGGL((k_sad_multi<P, NREF, 4, 4>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, g);
             return (int)hipGetLastError();
         });
 }
