@@ -134,6 +134,7 @@ long long now_ns()
 struct Session { intptr_t stride; int64_t elems; int64_t org; int rows, method, subme, merange, sub; x265amd_mes* mes; };
 std::vector<Session> g_sessions;
 x265amd_mes_counters g_closed;   /* counters of the sessions of closed encoders */
+long g_sessions_created;         /* device sessions opened over the process (closed encoders' included) */
 
 void add_counters(x265amd_mes_counters& tot, const x265amd_mes_counters& c)
 {
@@ -182,13 +183,13 @@ void print_stats()
     if (tot.batches)
         fprintf(stderr, "[x265me] service: %lld launches, %lld requests (%.2f per launch, max %lld), %lld searches, "
                         "kernel %.3f ms per launch (HIP events), batch %.3f ms, queueing %.3f ms per request, "
-                        "%lld waits slept; %lld row uploads %.1f MB %.1f ms; sessions %zu; evaluations %lld full-pel "
+                        "%lld waits slept; %lld row uploads %.1f MB %.1f ms; sessions %ld; evaluations %lld full-pel "
                         "%lld sub-pel, %.3f GB algorithmic, longest launch %.3f ms\n",
                 (long long)tot.batches, (long long)tot.requests, (double)tot.requests / tot.batches,
                 (long long)tot.max_requests_per_batch, (long long)tot.jobs, tot.kernel_ms / tot.batches,
                 tot.batch_ms / tot.batches, tot.requests ? tot.queue_ms / tot.requests : 0.0,
                 (long long)tot.waits_blocked, (long long)tot.uploads, tot.upload_bytes / 1e6, tot.upload_ms,
-                g_sessions.size(), (long long)tot.evals_fpel, (long long)tot.evals_subpel, tot.algo_bytes / 1e9,
+                g_sessions_created, (long long)tot.evals_fpel, (long long)tot.evals_subpel, tot.algo_bytes / 1e9,
                 tot.kernel_ms_max);
     if (tot.batches)
     {
@@ -310,6 +311,7 @@ x265amd_mes* session(const PicYuv& pic, const x265_param& p, int sub)
         {
             Session s = { pic.m_stride, elems, org, rows, p.searchMethod, p.subpelRefine, p.searchRange, sub, mes };
             g_sessions.push_back(s);
+            g_sessions_created++;
         }
     }
     pthread_mutex_unlock(&g_mu);

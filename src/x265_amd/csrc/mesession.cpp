@@ -139,9 +139,15 @@ struct x265amd_mes
         int rows_up;                  // CTU rows resident on the device
         const void* pinned[3];        // host planes registered with hipHostRegister (or null)
         std::mutex mu;                // one uploader at a time; the others wait for its rows
+        // launch service: uploads are enqueued, not waited for — each on its uploader's stream after the
+        // picture's previous upload (stream wait on up_ev), then up_ev re-recorded, so up_ev completes only
+        // when every upload so far has; a launch waits on up_ev of every picture its searches read
+        hipEvent_t up_ev = nullptr;
+        bool up_any = false;
     };
     std::mutex mu;
     std::unordered_map<const void*, Picture*> pics;
+    std::vector<Picture*> slot_pic;   // slot -> picture (max_pictures entries)
     std::unordered_map<const void*, int> tabs;
     std::vector<x265amd_mes_thread*> threads;
     std::atomic<int> next_slot{ 0 };
@@ -180,6 +186,7 @@ struct x265amd_mes
     int spin_us = 50;                 // X265AMD_MES_SPIN_US: pause-spin before yielding
     int yield_us = 5000;              // X265AMD_MES_YIELD_US: yield loop before sleeping (waits)
     int idle_us = 500;                // X265AMD_MES_IDLE_US: launchers' yield loop on an empty queue
+    bool sync_upload = false;         // X265AMD_MES_SYNC_UPLOAD=1: reference uploads waited for by the uploader
     std::atomic<int> qsleepers{ 0 };  // launchers sleeping on qcv
     int dsleepers = 0;                // waiters sleeping on dcv (guarded by dmu)
     std::atomic<int64_t> queued{ 0 }; // requests posted (the launchers' lock-free "anything new?" check)
@@ -462,6 +469,7 @@ void launcher_main(x265amd_mes* s, x265amd_mes_launcher* L)
     std::vector<Layout> lay;
     std::vector<x265amd_me_batch> bt;
     std::vector<size_t> base;
+    std::vector<uint8_t> seen;
     for (;;)
     {
         {
@@ -582,8 +590,23 @@ void launcher_main(x265amd_mes* s, x265amd_mes_launcher* L)
                     }
                 }
             }
+            // the reference rows these searches read: every picture's uploads so far (enqueued by the workers)
+            {
+                seen.assign(s->slot_pic.size(), 0);          // slots already waited on
+                for (auto* r : take)
+                    for (int q = 0; q < r->n && !rc; q++)
+                    {
+                        const int sl = r->jobs[q].slot;
+                        if (sl < 0 || sl >= (int)seen.size() || seen[sl]) continue;
+                        seen[sl] = 1;
+                        x265amd_mes::Picture* pic = s->slot_pic[sl];
+                        if (!pic) continue;
+                        std::lock_guard<std::mutex> pg(pic->mu);
+                        if (pic->up_any) rc = (int)hipStreamWaitEvent(L->st, pic->up_ev, 0);
+                    }
+            }
             // one upload of every size's inputs (the output regions ride along: staging is contiguous)
-            if (!(s->zerocopy && L->g.hdev))
+            if (!rc && !(s->zerocopy && L->g.hdev))
                 rc = (int)hipMemcpyAsync(L->g.dev, L->g.host, total, hipMemcpyHostToDevice, L->st);
             if (!rc) rc = (int)hipEventRecord(L->k0, L->st);
             if (!rc) rc = x265amd_motion_search(s->cfg.depth, (int)bt.size(), bt.data(), L->st);
@@ -691,6 +714,7 @@ int start_service(x265amd_mes* s)
     if (const char* e = getenv("X265AMD_MES_SPIN_US")) s->spin_us = atoi(e);
     if (const char* e = getenv("X265AMD_MES_YIELD_US")) s->yield_us = atoi(e);
     if (const char* e = getenv("X265AMD_MES_IDLE_US")) s->idle_us = atoi(e);
+    if (const char* e = getenv("X265AMD_MES_SYNC_UPLOAD")) s->sync_upload = atoi(e) != 0;
     if (const char* e = getenv("X265AMD_MES_TRACE")) s->trace = atoi(e);
     if (const char* e = getenv("X265AMD_MES_ZEROCOPY")) s->zerocopy = atoi(e) != 0;
     if (const char* e = getenv("X265AMD_MES_PRIORITY")) s->prio = atoi(e) != 0;
@@ -780,6 +804,7 @@ extern "C" int x265amd_mes_create(const x265amd_mes_config* cfg, x265amd_mes** o
     if (!rc && (hipMalloc((void**)&s->arena, (size_t)s->slot_elems * s->pix * cfg->max_pictures) != hipSuccess ||
                 hipMalloc((void**)&s->tables, sizeof(uint16_t) * s->table_elems * cfg->max_tables) != hipSuccess))
         rc = X265AMD_ENOMEM;
+    if (!rc) s->slot_pic.assign((size_t)cfg->max_pictures, nullptr);
     if (!rc && cfg->launchers) rc = start_service(s);
     if (rc)
     {
@@ -798,6 +823,11 @@ extern "C" void x265amd_mes_destroy(x265amd_mes* s)
     for (auto* t : s->threads) free_thread(t);
     for (auto& p : s->pics)
     {
+        if (p.second->up_ev)
+        {
+            (void)hipEventSynchronize(p.second->up_ev);      // no copy from a pinned plane in flight
+            (void)hipEventDestroy(p.second->up_ev);
+        }
         for (const void* pin : p.second->pinned)
             if (pin) (void)hipHostUnregister((void*)pin);
         delete p.second;
@@ -828,6 +858,7 @@ extern "C" int x265amd_mes_ref420(x265amd_mes* s, const void* key, int64_t gen, 
             p = new (std::nothrow) x265amd_mes::Picture();
             if (!p) return record(X265AMD_ENOMEM);
             p->slot = s->next_slot++;
+            s->slot_pic[p->slot] = p;
             p->gen = gen;
             p->rows_up = 0;
             p->pinned[0] = p->pinned[1] = p->pinned[2] = nullptr;
@@ -859,6 +890,12 @@ extern "C" int x265amd_mes_ref420(x265amd_mes* s, const void* key, int64_t gen, 
         const double t0 = now_s();
         size_t total = 0;
         uint8_t* dst = s->arena + (size_t)p->slot * s->slot_elems * s->pix;
+        const bool async = !s->launchers.empty() && !s->sync_upload;
+        if (async)
+        {
+            if (!p->up_ev) MES_TRY(hipEventCreateWithFlags(&p->up_ev, hipEventDisableTiming));
+            if (p->up_any) MES_TRY(hipStreamWaitEvent(t->st, p->up_ev, 0));
+        }
         for (int k = 0; k < np; k++)
         {
             const int64_t margin = k ? s->cfg.cmargin_y : s->cfg.margin_y;
@@ -873,7 +910,13 @@ extern "C" int x265amd_mes_ref420(x265amd_mes* s, const void* key, int64_t gen, 
                                    t->st));
             total += bytes;
         }
-        MES_TRY(wait(t));
+        if (async)
+        {
+            MES_TRY(hipEventRecord(p->up_ev, t->st));
+            p->up_any = true;
+        }
+        else
+            MES_TRY(wait(t));
         p->rows_up = rows_final;
         std::lock_guard<std::mutex> sg(s->smu);
         s->st.uploads++;
