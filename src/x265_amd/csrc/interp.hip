@@ -135,7 +135,9 @@ __device__ __forceinline__ uint32_t alignb(uint32_t hi, uint32_t lo, int s)
     return s ? __builtin_amdgcn_alignbyte(hi, lo, s) : lo;
 }
 
-// X265AMD_NT_INTERP=1 (A/B builds): the 8-bit filter windows with non-temporal loads
+// X265AMD_NT_INTERP=1 (A/B builds): the 8-bit filter windows with non-temporal loads — slower (hpp 64x64
+// 0.52 -> 0.39, census replay -4 to -7 %, profiles/r05/interp_nt_ab.txt): neighbouring lanes' windows share
+// lines, which non-temporal loads re-fetch
 #ifndef X265AMD_NT_INTERP
 #define X265AMD_NT_INTERP 0
 #endif

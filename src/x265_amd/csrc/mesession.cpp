@@ -186,7 +186,9 @@ struct x265amd_mes
     int spin_us = 50;                 // X265AMD_MES_SPIN_US: pause-spin before yielding
     int yield_us = 5000;              // X265AMD_MES_YIELD_US: yield loop before sleeping (waits)
     int idle_us = 500;                // X265AMD_MES_IDLE_US: launchers' yield loop on an empty queue
-    bool sync_upload = false;         // X265AMD_MES_SYNC_UPLOAD=1: reference uploads waited for by the uploader
+    bool sync_upload = true;          // X265AMD_MES_SYNC_UPLOAD=0: reference uploads enqueued, ordered by events
+                                      // (measured slower: the launches' cross-stream waits cost more than the
+                                      // workers' upload waits, profiles/r05/upload_async_vs_sync_pinned_ab.txt)
     std::atomic<int> qsleepers{ 0 };  // launchers sleeping on qcv
     int dsleepers = 0;                // waiters sleeping on dcv (guarded by dmu)
     std::atomic<int64_t> queued{ 0 }; // requests posted (the launchers' lock-free "anything new?" check)
