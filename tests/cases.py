@@ -805,8 +805,13 @@ def run_cpu(case: Case, orc) -> dict:
     return {k: b[k] for k in case.outs}
 
 
-def run_gpu(case: Case, prims, device="cuda") -> dict:
-    """Run a case through the GPU library (src/x265_amd/native.Primitives)."""
+GUARD = 1 << 16          # elements of canary on each side of a guarded output buffer
+
+
+def run_gpu(case: Case, prims, device="cuda", guard=None) -> dict:
+    """Run a case through the GPU library (src/x265_amd/native.Primitives).  guard = a dict: every output
+    buffer then sits inside GUARD canary elements on each side, and guard[key] records whether they
+    survived (a kernel writing outside its outputs shows up there, not as a wrong result)."""
     import torch
 
     def dev(v):
@@ -815,6 +820,15 @@ def run_gpu(case: Case, prims, device="cuda") -> dict:
         return v
 
     b = {k: dev(v) for k, v in case.bufs.items()}
+    boxes = {}
+    if guard is not None:
+        for k in case.outs:
+            t = b[k]
+            canary = torch.full((t.numel() + 2 * GUARD,), 0x5A if t.dtype == torch.uint8 else 0x5A5A, dtype=t.dtype,
+                                device=t.device)
+            canary[GUARD:GUARD + t.numel()] = t.reshape(-1)
+            boxes[k] = canary
+            b[k] = canary[GUARD:GUARD + t.numel()].view(t.shape)
     p = case.params
     f = case.family
     d = p["depth"]
@@ -870,4 +884,8 @@ def run_gpu(case: Case, prims, device="cuda") -> dict:
     else:
         raise ValueError(f)
     torch.cuda.synchronize()
+    for k, box in boxes.items():
+        ref = 0x5A if box.dtype == torch.uint8 else 0x5A5A
+        n = box.numel() - 2 * GUARD
+        guard[k] = bool((box[:GUARD] == ref).all().item() and (box[GUARD + n:] == ref).all().item())
     return {k: b[k].cpu().numpy() for k in case.outs}

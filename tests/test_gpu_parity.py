@@ -145,3 +145,17 @@ def test_gpu_fullsize_frame_batch(prims, oracle_libs, census_file, width, height
         if b.kind == "pixelcmp" and b.op in (SAD, SATD, SA8D):
             assert int(b.dev["out"].min()) >= 0, b.name
     assert not bad, bad[:10]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("depth", [8, 10])
+def test_gpu_writes_stay_inside_outputs(prims, depth):
+    """every golden case again with each output buffer inside 64 Ki canary elements on both sides: no kernel
+    writes outside the outputs it is given (a stray write corrupts other allocations silently and surfaces
+    later, in another kernel, as wrong data or an illegal address)"""
+    bad = []
+    for c in all_cases(depth):
+        guard = {}
+        run_gpu(c, prims, guard=guard)
+        bad += [f"{c.key()}:{k}" for k, ok in guard.items() if not ok]
+    assert not bad, f"{len(bad)} outputs with writes outside them:\n" + "\n".join(bad[:20])
