@@ -207,22 +207,35 @@ def parse_me_stats(err: str):
     return out
 
 
-def me_roofline(st):
-    """roofline of the batched motion-search launch from the encoder's own HIP-event timing"""
+ME_TRAFFIC = os.path.join(ROOT, "profiles", "r05", "pmc_me_traffic.json")
+
+
+def me_roofline(st, traffic_file=ME_TRAFFIC):
+    """roofline of the batched motion-search launch from the encoder's own HIP-event timing; traffic = the
+    launch's HBM bytes from the committed PMC passes (FETCH_SIZE x 2 per the gfx950 note + WRITE_SIZE, per
+    dispatch) when that table exists"""
     if not st.get("launches") or "algo_GB" not in st:
         return None
     per_launch = st["algo_GB"] * 1e9 / st["launches"]
     ms = st["kernel_ms_per_launch"]
     achieved = per_launch / (ms * 1e-3) / 1e9
+    traffic, tbasis = None, "no PMC table of this launch (profiles/r05/pmc_me_traffic.json)"
+    if traffic_file and os.path.exists(traffic_file):
+        with open(traffic_file) as f:
+            t = json.load(f)
+        traffic = int(t["traffic_bytes_per_launch"])
+        tbasis = (f"traffic: HBM bytes per launch from {os.path.relpath(traffic_file, ROOT)} (rocprofv3 FETCH_SIZE x "
+                  f"{t['fetch_correction']} + WRITE_SIZE per dispatch; {traffic / per_launch:.2f} of the algorithmic "
+                  "bytes: the search's re-reads of its window are served by the caches)")
     return {"bound": "hbm", "kernel": "k_motion_search (x265amd_motion_search, launch-service batches)",
             "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+            "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
             "bytes_per_launch": int(per_launch), "kernel_ms": ms, "launches": st["launches"],
             "searches_per_launch": round(st["searches"] / st["launches"], 2),
             "basis": "algorithmic bytes per launch (DESIGN.md §3c: 2WHb per full-pel evaluation, ((W+7)(H+7)+WH)b "
                      "per sub-pel evaluation, evaluations counted by the kernel) / mean launch time (HIP events "
-                     "around each launch on the launch-service stream, in the encoder process); traffic null: "
-                     "no PMC pass of this launch in profiles/r05"}
+                     "around each launch on the launch-service stream, in the encoder process; the kernel is "
+                     "latency-bound: one wave per search, ~7 searches per launch); " + tbasis}
 
 
 def main():

@@ -21,12 +21,21 @@ def test_parse_me_stats_and_roofline():
     st = bench.parse_me_stats(ERR)
     assert st["launches"] == 55870 and st["searches"] == 502994 and st["memo_misses"] == 0
     assert st["wait_s"] == 12.062 and st["evals_subpel"] == 5042178 and st["algo_GB"] == 108.108
-    r = bench.me_roofline(st)
+    r = bench.me_roofline(st, traffic_file=None)
     per = 108.108e9 / 55870
     assert r["bytes_per_launch"] == int(per)
     assert abs(r["achieved"] - per / 0.093e-3 / 1e9) < 0.01
     assert abs(r["frac"] - r["achieved"] / bench.HBM_PEAK_GBS) < 1e-4
     assert r["bound"] == "hbm" and r["unit"] == "GB/s"
+
+
+def test_roofline_traffic_from_the_committed_pmc_table(tmp_path):
+    import json
+
+    t = tmp_path / "t.json"
+    t.write_text(json.dumps({"traffic_bytes_per_launch": 600000, "fetch_correction": 2.0}))
+    r = bench.me_roofline(bench.parse_me_stats(ERR), traffic_file=str(t))
+    assert r["traffic"] == 600000 and "FETCH_SIZE" in r["basis"]
 
 
 def test_roofline_absent_without_service_counters():
