@@ -130,6 +130,14 @@ __device__ __forceinline__ void pack_taps(int idx, int (&cp)[TAPS / 4])
                       | ((uint32_t)(c[4 * k + 2] & 0xff) << 16) | ((uint32_t)(c[4 * k + 3] & 0xff) << 24));
 }
 
+// gfx950 v_sat_pk_u8_i16: the two int16 halves of x clamped to [0, 255], as the low two bytes
+__device__ __forceinline__ uint32_t sat_pk_u8_i16(uint32_t x)
+{
+    uint32_t r;
+    asm("v_sat_pk_u8_i16 %0, %1" : "=v"(r) : "v"(x));
+    return r;
+}
+
 __device__ __forceinline__ uint32_t alignb(uint32_t hi, uint32_t lo, int s)
 {
     return s ? __builtin_amdgcn_alignbyte(hi, lo, s) : lo;
@@ -149,7 +157,24 @@ template <int NB>
 __device__ __forceinline__ void load_win_dw(const uint8_t* p, uint32_t (&W)[(NB + 3) / 4])
 {
     constexpr int ND = (NB + 3) / 4;
-    if constexpr (NB > 8)
+#ifndef X265AMD_WIN_ALIGNED
+#define X265AMD_WIN_ALIGNED 0
+#endif
+    if constexpr (X265AMD_WIN_ALIGNED && NB >= 13 && NB <= 16)
+    {
+        // dword-aligned loads: the four dwords from p rounded down (each holds a window byte, as
+        // NB >= 13) and the fifth only when the window reaches into it (otherwise dword 3 again), then
+        // a per-lane byte shift
+        const uintptr_t a = (uintptr_t)p;
+        const int sh = (int)(a & 3);
+        const uint32_t* q = (const uint32_t*)(a - sh);
+        const uint4 d = *(const uint4*)q;
+        const uint32_t e = q[(sh + NB - 1) >> 2];
+        const uint32_t D[5] = { d.x, d.y, d.z, d.w, e };
+#pragma unroll
+        for (int k = 0; k < ND; k++) W[k] = __builtin_amdgcn_alignbyte(D[k + 1], D[k], sh);
+    }
+    else if constexpr (NB > 8)
     {
         static_assert(NB <= 16, "window too large");
         const uint2 h = ldx<uint2, kNtInterp>(p), t = ldx<uint2, kNtInterp>(p + NB - 8);
@@ -175,7 +200,8 @@ __device__ __forceinline__ void load_win_dw(const uint8_t* p, uint32_t (&W)[(NB 
 }
 
 template <int TAPS, int UW>
-__device__ __forceinline__ void hfilter_dot(const uint8_t* src, const int (&cp)[TAPS / 4], int (&sum)[UW]);
+__device__ __forceinline__ void hfilter_dot(const uint8_t* src, const int (&cp)[TAPS / 4], int (&sum)[UW],
+                                            int init = 128 * 64);
 
 // the horizontal 8-bit filter split into its window load and its arithmetic, so a kernel can issue
 // the loads of several rows before the first row's sums (and before any store: a store between
@@ -186,17 +212,20 @@ struct HWin
     static constexpr int NB = UW + TAPS - 1, ND = (NB + 3) / 4;
     uint32_t W[ND];
     __device__ __forceinline__ void load(const uint8_t* src) { load_win_dw<NB>(src - (TAPS / 2 - 1), W); }
-    __device__ __forceinline__ void sums(const int (&cp)[TAPS / 4], int (&sum)[UW]) const
+    // init: the bias correction 128 * sum(c) = 128 * 64 of the signed-byte pixels, plus any offset the
+    // caller folds in
+    __device__ __forceinline__ void sums(const int (&cp)[TAPS / 4], int (&sum)[UW], int init = 128 * 64) const
     {
 #pragma unroll
         for (int x = 0; x < UW; x++)
         {
-            int s = 128 * 64;
+            int s = 0;
 #pragma unroll
             for (int k = 0; k < TAPS / 4; k++)
             {
                 const int b = x + 4 * k;
-                s = __builtin_amdgcn_sdot4((int)alignb(W[(b >> 2) + ((b & 3) ? 1 : 0)], W[b >> 2], b & 3), cp[k], s, false);
+                const int v = (int)alignb(W[(b >> 2) + ((b & 3) ? 1 : 0)], W[b >> 2], b & 3);
+                s = __builtin_amdgcn_sdot4(v, cp[k], k ? s : init, false);
             }
             sum[x] = s;
         }
@@ -204,19 +233,20 @@ struct HWin
 };
 
 template <int TAPS, int UW>
-__device__ __forceinline__ void hfilter_dot(const uint8_t* src, const int (&cp)[TAPS / 4], int (&sum)[UW])
+__device__ __forceinline__ void hfilter_dot(const uint8_t* src, const int (&cp)[TAPS / 4], int (&sum)[UW], int init)
 {
     HWin<TAPS, UW> w;
     w.load(src);
-    w.sums(cp, sum);
+    w.sums(cp, sum, init);
 }
 
 typedef short s16x2 __attribute__((ext_vector_type(2)));
 
 // pp output of 8-bit sums: (s + 32) >> 6, (int16) truncation (a no-op: |s| <
 // 2^15 - 32 for every 8-bit filter phase), clamp to [0, 255]; done on packed
-// 16-bit pairs (v_pk_*) and packed 4 pixels per dword
-template <int UW>
+// 16-bit pairs (v_pk_*), clamped and packed by v_sat_pk_u8_i16, 4 pixels per dword.
+// ROUNDED: the sums already carry the +32 (folded into the dot chain's start)
+template <int UW, bool ROUNDED = false>
 __device__ __forceinline__ void store_pp8(uint8_t* p, const int (&s)[UW])
 {
     uint32_t out[UW / 4];
@@ -225,11 +255,15 @@ __device__ __forceinline__ void store_pp8(uint8_t* p, const int (&s)[UW])
     {
         s16x2 lo = __builtin_bit_cast(s16x2, __builtin_amdgcn_perm((uint32_t)s[4 * q + 1], (uint32_t)s[4 * q], 0x05040100u));
         s16x2 hi = __builtin_bit_cast(s16x2, __builtin_amdgcn_perm((uint32_t)s[4 * q + 3], (uint32_t)s[4 * q + 2], 0x05040100u));
-        lo = (lo + (s16x2)32) >> (s16x2)6;
-        hi = (hi + (s16x2)32) >> (s16x2)6;
-        lo = __builtin_elementwise_min(__builtin_elementwise_max(lo, (s16x2)0), (s16x2)255);
-        hi = __builtin_elementwise_min(__builtin_elementwise_max(hi, (s16x2)0), (s16x2)255);
-        out[q] = __builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, hi), __builtin_bit_cast(uint32_t, lo), 0x06040200u);
+        if constexpr (!ROUNDED)
+        {
+            lo = lo + (s16x2)32;
+            hi = hi + (s16x2)32;
+        }
+        lo = lo >> (s16x2)6;
+        hi = hi >> (s16x2)6;
+        out[q] = __builtin_amdgcn_perm(sat_pk_u8_i16(__builtin_bit_cast(uint32_t, hi)),
+                                       sat_pk_u8_i16(__builtin_bit_cast(uint32_t, lo)), 0x05040100u);
     }
     if constexpr (UW == 8) stu<uint2>(p, make_uint2(out[0], out[1]));
     else stu<uint32_t>(p, out[0]);
@@ -423,13 +457,15 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_interp(const BatchGroup g)
             for (int r = 0; r < UH; r++)
             {
                 int sum[UW], o[UW];
-                if constexpr (DOT) win[r].sums(cp, sum);
-                else hfilter<P, TAPS, UW>((const P*)ps + (y0 + r) * ss + x, c, sum);
                 if constexpr (DOT && OP == X265AMD_HPP)
                 {
-                    store_pp8<UW>((uint8_t*)(STG ? stg + (y0 + r) * w + x : pd + (y0 + r) * ds + x), sum);
+                    // the pp rounding 32 folded into the chain's start
+                    win[r].sums(cp, sum, 128 * 64 + 32);
+                    store_pp8<UW, true>((uint8_t*)(STG ? stg + (y0 + r) * w + x : pd + (y0 + r) * ds + x), sum);
                     continue;
                 }
+                if constexpr (DOT) win[r].sums(cp, sum);
+                else hfilter<P, TAPS, UW>((const P*)ps + (y0 + r) * ss + x, c, sum);
 #pragma unroll
                 for (int i = 0; i < UW; i++)
                     o[i] = OP == X265AMD_HPP ? clampp((sum[i] + 32) >> 6, K.maxv)
@@ -469,21 +505,20 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_interp(const BatchGroup g)
                         if constexpr (OP == X265AMD_VPP)
                         {
                             v = (v + (s16x2)32) >> (s16x2)6;
-                            v = __builtin_elementwise_min(__builtin_elementwise_max(v, (s16x2)0), (s16x2)255);
+                            o[p] = sat_pk_u8_i16(__builtin_bit_cast(uint32_t, v));     // clamped, 2 bytes
                         }
                         else
-                            v = v - (s16x2)8192;       // ps at 8-bit: shift 0, offset -IF_INTERNAL_OFFS
-                        o[p] = __builtin_bit_cast(uint32_t, v);
+                            o[p] = __builtin_bit_cast(uint32_t, v - (s16x2)8192);     // ps at 8-bit: shift 0, offset -IF_INTERNAL_OFFS
                     }
                     D* out = STG ? stg + (y0 + r) * w + x : pd + (y0 + r) * ds + x;
                     if constexpr (OP == X265AMD_VPP)
                     {
                         // two pairs -> four pixels per dword
                         if constexpr (UW == 8)
-                            stu<uint2>(out, make_uint2(__builtin_amdgcn_perm(o[1], o[0], 0x06040200u),
-                                                       __builtin_amdgcn_perm(o[3], o[2], 0x06040200u)));
+                            stu<uint2>(out, make_uint2(__builtin_amdgcn_perm(o[1], o[0], 0x05040100u),
+                                                       __builtin_amdgcn_perm(o[3], o[2], 0x05040100u)));
                         else
-                            stu<uint32_t>(out, __builtin_amdgcn_perm(o[1], o[0], 0x06040200u));
+                            stu<uint32_t>(out, __builtin_amdgcn_perm(o[1], o[0], 0x05040100u));
                     }
                     else
                     {
@@ -679,17 +714,26 @@ __global__ __launch_bounds__(X265AMD_BLOCK) __attribute__((amdgpu_waves_per_eu(W
     if constexpr (DOT) pack_taps<8>(cidx & 15, cp);
     else get_taps<8>(cidx & 15, cx);
     get_taps<8>(cidx >> 4, cy);
+    // 8 bit: the vertical taps scaled by 16, so the sp shift of 12 becomes 16 and each output is the
+    // high half of its sum (see below)
     s16x2 cv[4];
 #pragma unroll
-    for (int k = 0; k < 4; k++) cv[k] = s16x2{ (short)cy[2 * k], (short)cy[2 * k + 1] };
+    for (int k = 0; k < 4; k++)
+        cv[k] = DOT ? s16x2{ (short)(16 * cy[2 * k]), (short)(16 * cy[2 * k + 1]) }
+                    : s16x2{ (short)cy[2 * k], (short)cy[2 * k + 1] };
     const int x0 = SW * lane;
     const P* ps = (const P*)sub.a + sub.aoff[job] - 3 * ss + x0;
     P* pd = (P*)sub.d + sub.doff[job] + (STG ? 0 : x0);
     const int R = h + 7;
     // 8 bit: I = S - 8192 exactly (shift 0, |S| <= 88 * 255), and the sp offset adds 8192 * 64
-    // back, so the raw sums S are paired and the output is (t + 2048) >> 12
+    // back, so the raw sums S are paired and the output is (t + 2048) >> 12; the 2048 is carried as
+    // 32 on every S (the vertical taps sum to 64), so the vertical sums start at 0 — an inline
+    // constant of the dot instruction, no accumulator move — and the horizontal sums start at
+    // 128 * 64 + 32, kept in an SGPR for the same reason
+    int hinit = 128 * 64 + 32;
+    if constexpr (DOT) asm volatile("" : "+s"(hinit));
     auto inter = [&](const P* row, int (&I)[SW]) {
-        if constexpr (DOT) hfilter_dot<8, SW>((const uint8_t*)row, cp, I);
+        if constexpr (DOT) hfilter_dot<8, SW>((const uint8_t*)row, cp, I, hinit);
         else
         {
             int S[SW];
@@ -741,10 +785,10 @@ __global__ __launch_bounds__(X265AMD_BLOCK) __attribute__((amdgpu_waves_per_eu(W
             int I[SW];
             if constexpr (PF == 3)
             {
-                wa[i & 3].sums(cp, I);
+                wa[i & 3].sums(cp, I, hinit);
                 if (r + 4 < R) wa[i & 3].load((const uint8_t*)(ps + (intptr_t)(r + 4) * ss));
             }
-            else if constexpr (PF) wa[i].sums(cp, I);
+            else if constexpr (PF) wa[i].sums(cp, I, hinit);
             else inter(ps + (intptr_t)r * ss, I);
             // P[r - 1] goes to ring slot (r - 1) & 7 = i (r0 = 1 mod 8): compile-time; I[r - 1] is the
             // high half of the previous slot
@@ -753,24 +797,41 @@ __global__ __launch_bounds__(X265AMD_BLOCK) __attribute__((amdgpu_waves_per_eu(W
             const int y = r - 7;                         // output row ready once P[y + 6] exists
             if (y >= 0)
             {
-                int o[SW];
+                int t[SW];
 #pragma unroll
                 for (int x = 0; x < SW; x++)
                 {
-                    int t = DOT ? 2048 : 0;        // 8 bit: the sp rounding offset as the accumulator's start
+                    // 8 bit: the sp rounding offset rides on the pairs (hinit), the sums start at 0
+                    t[x] = __builtin_amdgcn_sdot2(__builtin_bit_cast(s16x2, Pr[(i + 2) & 7][x]), cv[0], 0, false);
 #pragma unroll
-                    for (int k = 0; k < 4; k++)
-                        t = __builtin_amdgcn_sdot2(__builtin_bit_cast(s16x2, Pr[(i + 2 + 2 * k) & 7][x]), cv[k], t, false);
-                    if constexpr (DOT)
-                    {
-                        const int v = t >> 12;
-                        o[x] = v < 0 ? 0 : (v > 255 ? 255 : v);
-                    }
-                    else
-                        o[x] = clampp((t + K.sp_off) >> K.sp_shift, K.maxv);
+                    for (int k = 1; k < 4; k++)
+                        t[x] = __builtin_amdgcn_sdot2(__builtin_bit_cast(s16x2, Pr[(i + 2 + 2 * k) & 7][x]), cv[k], t[x], false);
                 }
-                if constexpr (STG) store_row<P, SW>((P*)(stg + y * w + x0), o);
-                else store_row<P, SW>(pd + (intptr_t)y * ds, o);
+                if constexpr (DOT)
+                {
+                    // (16 t) >> 16 = t >> 12 is the high half of each sum (|t| < 2^21, so it fits int16): two
+                    // outputs' high halves with one v_perm, clamped to [0, 255] and packed by one
+                    // v_sat_pk_u8_i16, two such pairs per dword
+                    uint32_t pk[SW / 4];
+#pragma unroll
+                    for (int q = 0; q < SW / 4; q++)
+                    {
+                        const uint32_t h0 = __builtin_amdgcn_perm((uint32_t)t[4 * q + 1], (uint32_t)t[4 * q], 0x07060302u);
+                        const uint32_t h1 = __builtin_amdgcn_perm((uint32_t)t[4 * q + 3], (uint32_t)t[4 * q + 2], 0x07060302u);
+                        pk[q] = __builtin_amdgcn_perm(sat_pk_u8_i16(h1), sat_pk_u8_i16(h0), 0x05040100u);
+                    }
+                    uint8_t* dst = STG ? stg + y * w + x0 : (uint8_t*)(pd + (intptr_t)y * ds);
+                    if constexpr (SW == 8) stu<uint2>(dst, make_uint2(pk[0], pk[1]));
+                    else stu<uint32_t>(dst, pk[0]);
+                }
+                else
+                {
+                    int o[SW];
+#pragma unroll
+                    for (int x = 0; x < SW; x++) o[x] = clampp((t[x] + K.sp_off) >> K.sp_shift, K.maxv);
+                    if constexpr (STG) store_row<P, SW>((P*)(stg + y * w + x0), o);
+                    else store_row<P, SW>(pd + (intptr_t)y * ds, o);
+                }
             }
         }
         if constexpr (PF == 2)

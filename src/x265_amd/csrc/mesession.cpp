@@ -305,10 +305,13 @@ int thread_ctx(x265amd_mes* s, x265amd_mes_thread** out)
     }
     else
     {
-        // the worker thread itself makes no HIP call on the search path: only the reference-row uploads
-        // (x265amd_mes_ref / _table) use this stream
-        if (hipStreamCreateWithFlags(&t->st, hipStreamNonBlocking) != hipSuccess ||
-            hipEventCreateWithFlags(&t->ev, hipEventBlockingSync | hipEventDisableTiming) != hipSuccess)
+        // the worker thread itself makes no HIP call on the search path.  Its reference-row and table uploads
+        // are synchronous copies (no stream of its own: creating one costs tens of ms on the thread, measured
+        // 26 ms per hipStreamCreate in the encode's hip trace, profiles/r05/d/enc_hip_api_stats.csv), except in
+        // the event-ordered upload mode, which needs the stream
+        if (!s->sync_upload &&
+            (hipStreamCreateWithFlags(&t->st, hipStreamNonBlocking) != hipSuccess ||
+             hipEventCreateWithFlags(&t->ev, hipEventBlockingSync | hipEventDisableTiming) != hipSuccess))
             rc = X265AMD_ENOMEM;
         for (auto& r : t->req)
             if (!rc && !(r.fenc = (uint8_t*)malloc((64 * 64 + 2 * 32 * 32) * s->pix))) rc = X265AMD_ENOMEM;
@@ -908,8 +911,11 @@ extern "C" int x265amd_mes_ref420(x265amd_mes* s, const void* key, int64_t gen, 
             const int64_t r1 = rows_final == s->cfg.ctu_rows ? nrows : margin + (int64_t)rows_final * rh;
             const size_t off = (size_t)(r0 * stride) * s->pix, bytes = (size_t)((r1 - r0) * stride) * s->pix;
             const size_t plane = k == 0 ? 0 : (size_t)(s->cfg.plane_elems + (k - 1) * s->cfg.cplane_elems) * s->pix;
-            MES_TRY(hipMemcpyAsync(dst + plane + off, (const uint8_t*)planes[k] + off, bytes, hipMemcpyHostToDevice,
-                                   t->st));
+            if (t->st)
+                MES_TRY(hipMemcpyAsync(dst + plane + off, (const uint8_t*)planes[k] + off, bytes, hipMemcpyHostToDevice,
+                                       t->st));
+            else
+                MES_TRY(hipMemcpy(dst + plane + off, (const uint8_t*)planes[k] + off, bytes, hipMemcpyHostToDevice));
             total += bytes;
         }
         if (async)
@@ -917,7 +923,7 @@ extern "C" int x265amd_mes_ref420(x265amd_mes* s, const void* key, int64_t gen, 
             MES_TRY(hipEventRecord(p->up_ev, t->st));
             p->up_any = true;
         }
-        else
+        else if (t->st)
             MES_TRY(wait(t));
         p->rows_up = rows_final;
         std::lock_guard<std::mutex> sg(s->smu);
@@ -969,9 +975,15 @@ extern "C" int x265amd_mes_table(x265amd_mes* s, const uint16_t* centre, int* in
     const int k = (int)s->tabs.size();
     if (k >= s->cfg.max_tables) return X265AMD_ENOMEM;
     // the BitCost tables are process-wide and never change once built (bitcost.cpp:31-57)
-    MES_TRY(hipMemcpyAsync(s->tables + (size_t)k * s->table_elems, centre - s->cfg.mvcost_range,
-                           sizeof(uint16_t) * s->table_elems, hipMemcpyHostToDevice, t->st));
-    MES_TRY(wait(t));
+    if (t->st)
+    {
+        MES_TRY(hipMemcpyAsync(s->tables + (size_t)k * s->table_elems, centre - s->cfg.mvcost_range,
+                               sizeof(uint16_t) * s->table_elems, hipMemcpyHostToDevice, t->st));
+        MES_TRY(wait(t));
+    }
+    else
+        MES_TRY(hipMemcpy(s->tables + (size_t)k * s->table_elems, centre - s->cfg.mvcost_range,
+                          sizeof(uint16_t) * s->table_elems, hipMemcpyHostToDevice));
     s->tabs.emplace(centre, k);
     *index = k;
     return 0;
