@@ -255,13 +255,13 @@ __device__ __forceinline__ uint32_t pmad_s(uint32_t a, uint32_t b, uint32_t c)
     return r;
 }
 
-// v_dot2_u32_u16 in its VOP3P form with the accumulator start as an SGPR operand (the compiler's tied
-// v_dot2c form needs a v_mov of the start into every destination)
+// v_dot2_u32_u16 with the accumulator start (the builtin: the compiler then knows the instruction and keeps
+// the wait states a dot result needs before its consumer — as inline asm, hidden from its hazard
+// recognizer, the same start-folding trick produced wrong chroma hpp lanes in the interpolation kernels)
 __device__ __forceinline__ uint32_t udot2_sinit(uint32_t a, uint32_t b, uint32_t init)
 {
-    uint32_t r;
-    asm("v_dot2_u32_u16 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(init));
-    return r;
+    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+    return __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, a), __builtin_bit_cast(u16x2, b), init, false);
 }
 
 template <typename P, int N, int G = 4>
