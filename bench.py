@@ -129,13 +129,13 @@ def all_true(v: bool, world: int) -> bool:
 
 def core_slice(local: int, world: int):
     """this rank's host cores: a disjoint slice of CORES_PER_GPU of the process's affinity set when the
-    node has that many (one GPU box shows the whole machine's CPUs), else the whole set"""
+    node has that many for every rank (one GPU box shows the whole machine's CPUs); otherwise an equal
+    disjoint share of the set per rank (at least one core), so ranks never contend for the same cores"""
     cpus = sorted(os.sched_getaffinity(0))
-    if len(cpus) >= CORES_PER_GPU * max(1, world):
-        return cpus[local * CORES_PER_GPU:(local + 1) * CORES_PER_GPU]
-    if len(cpus) >= CORES_PER_GPU:
-        return cpus[:CORES_PER_GPU]
-    return cpus
+    world = max(1, world)
+    per = CORES_PER_GPU if len(cpus) >= CORES_PER_GPU * world else max(1, len(cpus) // world)
+    lo = (local * per) % max(1, len(cpus))
+    return cpus[lo:lo + per] or cpus[:per]
 
 
 def cpu_model() -> str:

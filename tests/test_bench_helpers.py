@@ -61,5 +61,16 @@ def test_core_slices_are_disjoint_when_the_node_has_enough():
     s0, s1 = bench.core_slice(0, 2), bench.core_slice(1, 2)
     if len(cpus) >= 2 * bench.CORES_PER_GPU:
         assert not set(s0) & set(s1) and len(s0) == bench.CORES_PER_GPU
-    else:
-        assert s0 and set(s0) <= set(cpus)
+    elif len(cpus) >= 2:
+        # fewer cores than 16 per rank: an equal disjoint share each
+        assert not set(s0) & set(s1) and len(s0) == len(s1) == len(cpus) // 2
+    assert s0 and set(s0) <= set(cpus)
+
+
+def test_core_slices_share_a_small_node_evenly(monkeypatch):
+    monkeypatch.setattr(bench.os, "sched_getaffinity", lambda _: set(range(96)))
+    slices = [bench.core_slice(r, 8) for r in range(8)]
+    assert all(len(s) == 12 for s in slices)
+    assert len(set().union(*map(set, slices))) == 96
+    monkeypatch.setattr(bench.os, "sched_getaffinity", lambda _: set(range(256)))
+    assert [len(bench.core_slice(r, 8)) for r in range(8)] == [16] * 8
