@@ -144,6 +144,11 @@ struct x265amd_mes
         // when every upload so far has; a launch waits on up_ev of every picture its searches read
         hipEvent_t up_ev = nullptr;
         bool up_any = false;
+        // launcher uploads (X265AMD_MES_LUPLOAD=1, one launcher): the worker only records the rows final
+        // so far and the host planes; the launcher copies the missing rows on its own stream ahead of the
+        // batch that reads them (stream order: no events, no worker waits on copies)
+        const void* planes[3] = { nullptr, nullptr, nullptr };
+        int rows_want = 0;
     };
     std::mutex mu;
     std::unordered_map<const void*, Picture*> pics;
@@ -189,6 +194,7 @@ struct x265amd_mes
     bool sync_upload = true;          // X265AMD_MES_SYNC_UPLOAD=0: reference uploads enqueued, ordered by events
                                       // (measured slower: the launches' cross-stream waits cost more than the
                                       // workers' upload waits, profiles/r05/upload_async_vs_sync_pinned_ab.txt)
+    bool lupload = false;             // X265AMD_MES_LUPLOAD=1 (one launcher): the launcher uploads reference rows
     std::atomic<int> qsleepers{ 0 };  // launchers sleeping on qcv
     int dsleepers = 0;                // waiters sleeping on dcv (guarded by dmu)
     std::atomic<int64_t> queued{ 0 }; // requests posted (the launchers' lock-free "anything new?" check)
@@ -466,6 +472,9 @@ static int hist_bin(double ms)
 // ---------------------------------------------------------------- launch service
 // one service thread: take every queued request, one staged batch per PU size, one upload, one launch
 // (all sizes), one download, publish
+int copy_rows(x265amd_mes* s, x265amd_mes::Picture* p, const void* const planes[3], int rows_final, hipStream_t st,
+              size_t* total);
+
 void launcher_main(x265amd_mes* s, x265amd_mes_launcher* L)
 {
     (void)hipSetDevice(s->cfg.device);
@@ -608,6 +617,17 @@ void launcher_main(x265amd_mes* s, x265amd_mes_launcher* L)
                         if (!pic) continue;
                         std::lock_guard<std::mutex> pg(pic->mu);
                         if (pic->up_any) rc = (int)hipStreamWaitEvent(L->st, pic->up_ev, 0);
+                        if (s->lupload && pic->rows_want > pic->rows_up)
+                        {
+                            const double t0 = now_s();
+                            size_t total = 0;
+                            rc = copy_rows(s, pic, pic->planes, pic->rows_want, L->st, &total);
+                            pic->rows_up = pic->rows_want;
+                            std::lock_guard<std::mutex> sg(s->smu);
+                            s->st.uploads++;
+                            s->st.upload_bytes += (int64_t)total;
+                            s->st.upload_ms += 1e3 * (now_s() - t0);
+                        }
                     }
             }
             // one upload of every size's inputs (the output regions ride along: staging is contiguous)
@@ -713,6 +733,34 @@ void launcher_main(x265amd_mes* s, x265amd_mes_launcher* L)
     }
 }
 
+// copy the plane rows of CTU rows [p->rows_up, rows_final) into the picture's slot: the top margin goes
+// with row 0, the bottom margin (and the rows of a partial last CTU row) with the last row; chroma (4:2:0)
+// the same at half height.  Enqueued on st, or synchronous without a stream.
+int copy_rows(x265amd_mes* s, x265amd_mes::Picture* p, const void* const planes[3], int rows_final, hipStream_t st,
+              size_t* total)
+{
+    uint8_t* dst = s->arena + (size_t)p->slot * s->slot_elems * s->pix;
+    const int np = s->cfg.chroma ? 3 : 1;
+    for (int k = 0; k < np; k++)
+    {
+        const int64_t margin = k ? s->cfg.cmargin_y : s->cfg.margin_y;
+        const int64_t rh = k ? s->cfg.ctu_size / 2 : s->cfg.ctu_size;
+        const int64_t stride = k ? s->cfg.cstride : s->cfg.stride;
+        const int64_t nrows = k ? s->crows : s->rows;
+        const int64_t r0 = p->rows_up == 0 ? 0 : margin + (int64_t)p->rows_up * rh;
+        const int64_t r1 = rows_final == s->cfg.ctu_rows ? nrows : margin + (int64_t)rows_final * rh;
+        const size_t off = (size_t)(r0 * stride) * s->pix, bytes = (size_t)((r1 - r0) * stride) * s->pix;
+        const size_t plane = k == 0 ? 0 : (size_t)(s->cfg.plane_elems + (k - 1) * s->cfg.cplane_elems) * s->pix;
+        const hipError_t e = st ? hipMemcpyAsync(dst + plane + off, (const uint8_t*)planes[k] + off, bytes,
+                                                 hipMemcpyHostToDevice, st)
+                                : hipMemcpy(dst + plane + off, (const uint8_t*)planes[k] + off, bytes,
+                                            hipMemcpyHostToDevice);
+        if (e != hipSuccess) return (int)e;
+        *total += bytes;
+    }
+    return 0;
+}
+
 int start_service(x265amd_mes* s)
 {
     const int n = s->cfg.launchers;
@@ -724,6 +772,7 @@ int start_service(x265amd_mes* s)
     if (const char* e = getenv("X265AMD_MES_ZEROCOPY")) s->zerocopy = atoi(e) != 0;
     if (const char* e = getenv("X265AMD_MES_PRIORITY")) s->prio = atoi(e) != 0;
     if (const char* e = getenv("X265AMD_MES_LSPIN")) s->lspin = atoi(e) != 0;
+    if (const char* e = getenv("X265AMD_MES_LUPLOAD")) s->lupload = atoi(e) != 0 && n == 1;
     for (int i = 0; i < n; i++)
     {
         auto* L = new (std::nothrow) x265amd_mes_launcher();
@@ -876,6 +925,7 @@ extern "C" int x265amd_mes_ref420(x265amd_mes* s, const void* key, int64_t gen, 
     {
         p->gen = gen;
         p->rows_up = 0;
+        p->rows_want = 0;
     }
     const int np = s->cfg.chroma ? 3 : 1;
     for (int k = 0; k < np; k++)
@@ -887,37 +937,22 @@ extern "C" int x265amd_mes_ref420(x265amd_mes* s, const void* key, int64_t gen, 
                                                                                                         : nullptr;
             (void)hipGetLastError();
         }
-    if (rows_final > p->rows_up)
+    if (s->lupload)
     {
-        // plane rows of CTU rows [rows_up, rows_final): the top margin goes with row 0, the bottom
-        // margin (and the rows of a partial last CTU row) with the last row; chroma (4:2:0) the same at half
-        // height
+        for (int k = 0; k < np; k++) p->planes[k] = planes[k];
+        if (rows_final > p->rows_want) p->rows_want = rows_final;
+    }
+    else if (rows_final > p->rows_up)
+    {
         const double t0 = now_s();
         size_t total = 0;
-        uint8_t* dst = s->arena + (size_t)p->slot * s->slot_elems * s->pix;
         const bool async = !s->launchers.empty() && !s->sync_upload;
         if (async)
         {
             if (!p->up_ev) MES_TRY(hipEventCreateWithFlags(&p->up_ev, hipEventDisableTiming));
             if (p->up_any) MES_TRY(hipStreamWaitEvent(t->st, p->up_ev, 0));
         }
-        for (int k = 0; k < np; k++)
-        {
-            const int64_t margin = k ? s->cfg.cmargin_y : s->cfg.margin_y;
-            const int64_t rh = k ? s->cfg.ctu_size / 2 : s->cfg.ctu_size;
-            const int64_t stride = k ? s->cfg.cstride : s->cfg.stride;
-            const int64_t nrows = k ? s->crows : s->rows;
-            const int64_t r0 = p->rows_up == 0 ? 0 : margin + (int64_t)p->rows_up * rh;
-            const int64_t r1 = rows_final == s->cfg.ctu_rows ? nrows : margin + (int64_t)rows_final * rh;
-            const size_t off = (size_t)(r0 * stride) * s->pix, bytes = (size_t)((r1 - r0) * stride) * s->pix;
-            const size_t plane = k == 0 ? 0 : (size_t)(s->cfg.plane_elems + (k - 1) * s->cfg.cplane_elems) * s->pix;
-            if (t->st)
-                MES_TRY(hipMemcpyAsync(dst + plane + off, (const uint8_t*)planes[k] + off, bytes, hipMemcpyHostToDevice,
-                                       t->st));
-            else
-                MES_TRY(hipMemcpy(dst + plane + off, (const uint8_t*)planes[k] + off, bytes, hipMemcpyHostToDevice));
-            total += bytes;
-        }
+        MES_TRY(copy_rows(s, p, planes, rows_final, t->st, &total));
         if (async)
         {
             MES_TRY(hipEventRecord(p->up_ev, t->st));
@@ -955,7 +990,8 @@ extern "C" int x265amd_mes_rows(x265amd_mes* s, const void* key, int64_t gen, in
     }
     if (!p) return 0;
     std::lock_guard<std::mutex> g(p->mu);
-    *rows_resident = p->gen == gen ? p->rows_up : 0;
+    // launcher uploads: the rows recorded are copied ahead of every launch that can read them
+    *rows_resident = p->gen == gen ? (s->lupload ? p->rows_want : p->rows_up) : 0;
     return 0;
 }
 

@@ -542,7 +542,7 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_sad_multi(const BatchGroup g)
 // with one lane per job the wave's reference loads step through four separate blocks per lane.  Outputs
 // land contiguously.  For blocks of at most 4 units (8x8, 8x16, 16x8, 4x8 ...), where a lane per job
 // holds little work.
-template <typename P, int NREF, int UW, int UH>
+template <typename P, int NREF, int UW, int UH, bool NT = false>
 __global__ __launch_bounds__(X265AMD_BLOCK) void k_sad_multi_ref(const BatchGroup g)
 {
     const uint32_t gb = xcd_block();
@@ -561,7 +561,7 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_sad_multi_ref(const BatchGrou
     for (int u = 0; u < units; u++)
     {
         const int x = (u % ux) * UW, y = (u / ux) * UH;
-        acc += unit_sad<P, UW, UH>(pf + y * fs + x, fs, pr + y * rs + x, rs);
+        acc += unit_sad<P, UW, UH, NT, NT>(pf + y * fs + x, fs, pr + y * rs + x, rs);
     }
     ((int32_t*)sub.d)[job * NREF + k] = (int32_t)acc;
 }
@@ -711,11 +711,16 @@ static int sadx_lanes()
     return v;
 }
 constexpr int kSadRefOp = 0x7f;   // class tag of k_sad_multi_ref
+// lane-per-reference variants (X265AMD_SADX_LANES bits): 2 = 8x8 units where the block allows, 4 = non-temporal
+// loads (the four lanes of a job read a row in one instruction, so nothing is re-fetched)
+static bool sadx_uh8() { return (sadx_lanes() & 2) != 0; }
+static bool sadx_nt() { return (sadx_lanes() & 4) != 0; }
 
 static int sad_multi_class(int, int w, int h)
 {
     if ((w % 4) || (h % 4) || w > 64 || h > 64 || w < 4 || h < 4) return -X265AMD_EINVAL;
     const int uw = (w % 8) ? 4 : 8;
+    if (sadx_lanes() && sadx_uh8() && uw == 8 && h % 8 == 0 && (w / 8) * (h / 8) <= 4) return cmp_pack(kSadRefOp, 8, 8);
     if (sadx_lanes() && (w / uw) * (h / 4) <= 4) return cmp_pack(kSadRefOp, uw, 4);
     // (8x8 units measured no faster for sad_x4 8x8 and slower for 16x16: profiles/r04/sad_uh8_ab_and_me_async.txt)
     if (w % 8 == 0 && h % 8 == 0 && sad_uh8() > 1) return cmp_pack(X265AMD_SAD, 8, 8);
@@ -733,8 +738,17 @@ static int dispatch_multi(int count, const x265amd_cmp_batch* bt, hipStream_t st
             if ((cls[i] >> 16) == kSadRefOp) s.lg = 2;     // four lanes per job
         },
         [&](int c, const BatchGroup& g, uint32_t blocks) {
-            if ((c >> 16) == kSadRefOp && ((c >> 8) & 0xff) == 8)
-                hipLaunchKernelGGL((k_sad_multi_ref<P, NREF, 8, 4>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, g);
+            const bool nt = sadx_nt();
+            if ((c >> 16) == kSadRefOp && (c & 0xff) == 8)
+            {
+                if (nt) hipLaunchKernelGGL((k_sad_multi_ref<P, NREF, 8, 8, true>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, g);
+                else hipLaunchKernelGGL((k_sad_multi_ref<P, NREF, 8, 8>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, g);
+            }
+            else if ((c >> 16) == kSadRefOp && ((c >> 8) & 0xff) == 8)
+            {
+                if (nt) hipLaunchKernelGGL((k_sad_multi_ref<P, NREF, 8, 4, true>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, g);
+                else hipLaunchKernelGGL((k_sad_multi_ref<P, NREF, 8, 4>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, g);
+            }
             else if ((c >> 16) == kSadRefOp)
                 hipLaunchKernelGGL((k_sad_multi_ref<P, NREF, 4, 4>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, g);
             else if (((c >> 8) & 0xff) == 8 && (c & 0xff) == 8)
