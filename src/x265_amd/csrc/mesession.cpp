@@ -144,11 +144,13 @@ struct x265amd_mes
         // when every upload so far has; a launch waits on up_ev of every picture its searches read
         hipEvent_t up_ev = nullptr;
         bool up_any = false;
-        // launcher uploads (X265AMD_MES_LUPLOAD=1, one launcher): the worker only records the rows final
-        // so far and the host planes; the launcher copies the missing rows on its own stream ahead of the
-        // batch that reads them (stream order: no events, no worker waits on copies)
+        // launcher uploads (X265AMD_MES_LUPLOAD=1): the worker only records the rows final so far and the
+        // host planes; the launcher copies the missing rows on its own stream ahead of the batch that reads
+        // them (no worker waits on copies; another launcher's rows still in flight are waited for on the
+        // device, after a query)
         const void* planes[3] = { nullptr, nullptr, nullptr };
         int rows_want = 0;
+        const void* up_by = nullptr;  // the launcher that enqueued the last upload
     };
     std::mutex mu;
     std::unordered_map<const void*, Picture*> pics;
@@ -194,7 +196,8 @@ struct x265amd_mes
     bool sync_upload = true;          // X265AMD_MES_SYNC_UPLOAD=0: reference uploads enqueued, ordered by events
                                       // (measured slower: the launches' cross-stream waits cost more than the
                                       // workers' upload waits, profiles/r05/upload_async_vs_sync_pinned_ab.txt)
-    bool lupload = false;             // X265AMD_MES_LUPLOAD=1 (one launcher): the launcher uploads reference rows
+    bool lupload = false;             // X265AMD_MES_LUPLOAD=1: the launchers upload the reference rows
+    bool wstream = false;             // X265AMD_MES_WSTREAM=1: each worker uploads on a stream of its own
     std::atomic<int> qsleepers{ 0 };  // launchers sleeping on qcv
     int dsleepers = 0;                // waiters sleeping on dcv (guarded by dmu)
     std::atomic<int64_t> queued{ 0 }; // requests posted (the launchers' lock-free "anything new?" check)
@@ -315,7 +318,7 @@ int thread_ctx(x265amd_mes* s, x265amd_mes_thread** out)
         // are synchronous copies (no stream of its own: creating one costs tens of ms on the thread, measured
         // 26 ms per hipStreamCreate in the encode's hip trace, profiles/r05/d/enc_hip_api_stats.csv), except in
         // the event-ordered upload mode, which needs the stream
-        if (!s->sync_upload &&
+        if ((!s->sync_upload || s->wstream) && !s->lupload &&
             (hipStreamCreateWithFlags(&t->st, hipStreamNonBlocking) != hipSuccess ||
              hipEventCreateWithFlags(&t->ev, hipEventBlockingSync | hipEventDisableTiming) != hipSuccess))
             rc = X265AMD_ENOMEM;
@@ -616,12 +619,29 @@ void launcher_main(x265amd_mes* s, x265amd_mes_launcher* L)
                         x265amd_mes::Picture* pic = s->slot_pic[sl];
                         if (!pic) continue;
                         std::lock_guard<std::mutex> pg(pic->mu);
-                        if (pic->up_any) rc = (int)hipStreamWaitEvent(L->st, pic->up_ev, 0);
-                        if (s->lupload && pic->rows_want > pic->rows_up)
+                        if (!s->lupload)
+                        {
+                            if (pic->up_any) rc = (int)hipStreamWaitEvent(L->st, pic->up_ev, 0);
+                            continue;
+                        }
+                        // launcher uploads: rows another launcher enqueued may still be in flight (up_ev
+                        // completes only when every upload so far has: each uploader waits for it first)
+                        if (pic->up_any && pic->up_by != L)
+                        {
+                            const hipError_t q = hipEventQuery(pic->up_ev);
+                            if (q == hipErrorNotReady) rc = (int)hipStreamWaitEvent(L->st, pic->up_ev, 0);
+                            else if (q != hipSuccess) rc = (int)q;
+                        }
+                        if (!rc && pic->rows_want > pic->rows_up)
                         {
                             const double t0 = now_s();
                             size_t total = 0;
-                            rc = copy_rows(s, pic, pic->planes, pic->rows_want, L->st, &total);
+                            if (!pic->up_ev) rc = (int)hipEventCreateWithFlags(&pic->up_ev, hipEventDisableTiming);
+                            if (!rc) rc = copy_rows(s, pic, pic->planes, pic->rows_want, L->st, &total);
+                            if (!rc) rc = (int)hipEventRecord(pic->up_ev, L->st);
+                            if (rc) continue;
+                            pic->up_any = true;
+                            pic->up_by = L;
                             pic->rows_up = pic->rows_want;
                             std::lock_guard<std::mutex> sg(s->smu);
                             s->st.uploads++;
@@ -772,7 +792,8 @@ int start_service(x265amd_mes* s)
     if (const char* e = getenv("X265AMD_MES_ZEROCOPY")) s->zerocopy = atoi(e) != 0;
     if (const char* e = getenv("X265AMD_MES_PRIORITY")) s->prio = atoi(e) != 0;
     if (const char* e = getenv("X265AMD_MES_LSPIN")) s->lspin = atoi(e) != 0;
-    if (const char* e = getenv("X265AMD_MES_LUPLOAD")) s->lupload = atoi(e) != 0 && n == 1;
+    if (const char* e = getenv("X265AMD_MES_LUPLOAD")) s->lupload = atoi(e) != 0;
+    if (const char* e = getenv("X265AMD_MES_WSTREAM")) s->wstream = atoi(e) != 0;
     for (int i = 0; i < n; i++)
     {
         auto* L = new (std::nothrow) x265amd_mes_launcher();

@@ -698,21 +698,22 @@ static int dispatch_cmp(int op, int count, const x265amd_cmp_batch* bt, hipStrea
         [&](int c, const BatchGroup& g, uint32_t blocks) { return launch_cmp_class<P>(c, g, blocks, st); });
 }
 
-// X265AMD_SADX_LANES=1: lane per reference for blocks of at most 4 units (0, the default: lane per job —
-// measured faster, sad_x4 8x8 0.57 against 0.53, profiles/r05/sad_nt_ab.txt)
+// sad_x3 / sad_x4 lane layout (X265AMD_SADX_LANES bits): 1 = a lane per (job, reference) for blocks of at most
+// 4 units, 2 = with 8x8 units where the block allows, 4 = non-temporal loads (the four lanes of a job read a row
+// in one instruction, so nothing is re-fetched); 0 = a lane per job everywhere; 8, the default = bits 1 | 2 | 4
+// for 8x8 blocks only (one 8x8 unit per lane: sad_x4 8x8 0.57 -> 0.59, while 16x16 with four 8x8 units per lane
+// drops 0.72 -> 0.43 and 8x4 units measured 0.53-0.58, profiles/r05/sadx_lanes_ab.txt)
 static int sadx_lanes()
 {
     static int v = -1;
     if (v < 0)
     {
         const char* e = getenv("X265AMD_SADX_LANES");
-        v = e ? atoi(e) : 0;
+        v = e ? atoi(e) : 8;
     }
     return v;
 }
 constexpr int kSadRefOp = 0x7f;   // class tag of k_sad_multi_ref
-// lane-per-reference variants (X265AMD_SADX_LANES bits): 2 = 8x8 units where the block allows, 4 = non-temporal
-// loads (the four lanes of a job read a row in one instruction, so nothing is re-fetched)
 static bool sadx_uh8() { return (sadx_lanes() & 2) != 0; }
 static bool sadx_nt() { return (sadx_lanes() & 4) != 0; }
 
@@ -720,8 +721,17 @@ static int sad_multi_class(int, int w, int h)
 {
     if ((w % 4) || (h % 4) || w > 64 || h > 64 || w < 4 || h < 4) return -X265AMD_EINVAL;
     const int uw = (w % 8) ? 4 : 8;
-    if (sadx_lanes() && sadx_uh8() && uw == 8 && h % 8 == 0 && (w / 8) * (h / 8) <= 4) return cmp_pack(kSadRefOp, 8, 8);
-    if (sadx_lanes() && (w / uw) * (h / 4) <= 4) return cmp_pack(kSadRefOp, uw, 4);
+    // the non-temporal flag travels in the class (bit 7 of the unit-height byte)
+    if (sadx_lanes() == 8)
+    {
+        if (w == 8 && h == 8) return cmp_pack(kSadRefOp, 8, 8 | 0x80);
+    }
+    else if (sadx_lanes() & 1)
+    {
+        const int nt = sadx_nt() ? 0x80 : 0;
+        if (sadx_uh8() && uw == 8 && h % 8 == 0 && (w / 8) * (h / 8) <= 4) return cmp_pack(kSadRefOp, 8, 8 | nt);
+        if ((w / uw) * (h / 4) <= 4) return cmp_pack(kSadRefOp, uw, 4 | nt);
+    }
     // (8x8 units measured no faster for sad_x4 8x8 and slower for 16x16: profiles/r04/sad_uh8_ab_and_me_async.txt)
     if (w % 8 == 0 && h % 8 == 0 && sad_uh8() > 1) return cmp_pack(X265AMD_SAD, 8, 8);
     return cmp_pack(X265AMD_SAD, (w % 8) ? 4 : 8, 4);
@@ -738,8 +748,8 @@ static int dispatch_multi(int count, const x265amd_cmp_batch* bt, hipStream_t st
             if ((cls[i] >> 16) == kSadRefOp) s.lg = 2;     // four lanes per job
         },
         [&](int c, const BatchGroup& g, uint32_t blocks) {
-            const bool nt = sadx_nt();
-            if ((c >> 16) == kSadRefOp && (c & 0xff) == 8)
+            const bool nt = (c & 0x80) != 0;
+            if ((c >> 16) == kSadRefOp && (c & 0x7f) == 8)
             {
                 if (nt) hipLaunchKernelGGL((k_sad_multi_ref<P, NREF, 8, 8, true>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, g);
                 else hipLaunchKernelGGL((k_sad_multi_ref<P, NREF, 8, 8>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, g);

@@ -5,10 +5,8 @@
 set -o pipefail
 mkdir -p gpurun_out/r05/d
 export TMPDIR=/tmp
-echo "== interp diff: round-4 rewrite (a052ed0) lib"
-X265AMD_LIB=$PWD/src/x265_amd/ab/libx265amd_a052.so timeout -k 10 200 python3 -u tools/interp_diff.py 2>&1 | tee gpurun_out/r05/d/interp_diff_a052.txt
-echo "== interp diff: current lib"
-timeout -k 10 200 python3 -u tools/interp_diff.py 2>&1 | tee gpurun_out/r05/d/interp_diff_cur.txt
+: 
+: 
 timeout -k 10 420 python3 -u bench.py --steps 2 --warmup 0 > gpurun_out/r05/d/bench_short.json 2> gpurun_out/r05/d/bench_short.err \
     || { tail -30 gpurun_out/r05/d/bench_short.err; exit 1; }
 tail -c 2500 gpurun_out/r05/d/bench_short.json
