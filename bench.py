@@ -225,7 +225,7 @@ def me_roofline(st, traffic_file=ME_TRAFFIC):
             t = json.load(f)
         traffic = int(t["traffic_bytes_per_launch"])
         tbasis = (f"traffic: HBM bytes per launch from {os.path.relpath(traffic_file, ROOT)} (rocprofv3 FETCH_SIZE x "
-                  f"{t['fetch_correction']} + WRITE_SIZE per dispatch; {traffic / per_launch:.2f} of the algorithmic "
+                  f"{t['fetch_correction']} + WRITE_SIZE per launch; {traffic / per_launch:.2f} of the algorithmic "
                   "bytes: the search's re-reads of its window are served by the caches)")
     return {"bound": "hbm", "kernel": "k_motion_search (x265amd_motion_search, launch-service batches)",
             "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -235,7 +235,7 @@ def me_roofline(st, traffic_file=ME_TRAFFIC):
             "basis": "algorithmic bytes per launch (DESIGN.md §3c: 2WHb per full-pel evaluation, ((W+7)(H+7)+WH)b "
                      "per sub-pel evaluation, evaluations counted by the kernel) / mean launch time (HIP events "
                      "around each launch on the launch-service stream, in the encoder process; the kernel is "
-                     "latency-bound: one wave per search, ~7 searches per launch); " + tbasis}
+                     "latency-bound: one workgroup of up to four waves per search, ~7 searches per launch); " + tbasis}
 
 
 def main():

@@ -137,6 +137,41 @@ __device__ __forceinline__ int me_group_sum(int v)
 #endif
 }
 
+// N sums over a group of G lanes.  Up to a wavefront: me_group_sum each.  Groups of 2 or 4 wavefronts (one
+// search per workgroup, X265AMD_ME_GMAX): each wave's sums, then the waves' partial sums through LDS between
+// two barriers (the second keeps a fast wave's next write off the slots until every wave has read them); every
+// wave of the group makes the same calls, since all decisions follow from these group-uniform sums
+template <int G, int N>
+__device__ __forceinline__ void me_group_sums(int (&v)[N])
+{
+    if constexpr (G <= 64)
+    {
+#pragma unroll
+        for (int n = 0; n < N; n++) v[n] = me_group_sum<G>(v[n]);
+    }
+    else
+    {
+        constexpr int NW = G / 64;
+        __shared__ int red[NW][N];
+#pragma unroll
+        for (int n = 0; n < N; n++) v[n] = me_group_sum<64>(v[n]);
+        const int w = threadIdx.x >> 6;
+        if ((threadIdx.x & 63) == 0)
+#pragma unroll
+            for (int n = 0; n < N; n++) red[w][n] = v[n];
+        __syncthreads();
+#pragma unroll
+        for (int n = 0; n < N; n++)
+        {
+            int t = red[0][n];
+#pragma unroll
+            for (int k = 1; k < NW; k++) t += red[k][n];
+            v[n] = t;
+        }
+        __syncthreads();
+    }
+}
+
 // full-pel SADs of the PU at N integer displacements (mx[n], my[n]), group-reduced.  fenc comes from
 // registers (loaded once per PU); every reference row of all N candidates and NU units is loaded before the
 // first SAD, and the N group reductions run side by side, so N candidates cost one memory round trip and
@@ -173,8 +208,7 @@ __device__ __forceinline__ void fpel_sad_nu(const MeState<P>& s, const int (&mx)
         }
         out[n] = (int)acc;
     }
-#pragma unroll
-    for (int n = 0; n < N; n++) out[n] = me_group_sum<G>(out[n]);
+    me_group_sums<G, N>(out);
 }
 
 // N candidates' SADs; `counted` of them are real evaluations (the rest are range-failed points whose loads
@@ -382,17 +416,130 @@ struct RawRow
     }
 };
 
-// subpelCompare's luma part over this lane's units for one fractional case (CASE bit 0: horizontal
-// fraction, bit 1: vertical): the reference windows (and source rows) of KU units are all loaded before
-// the first is filtered, so a candidate costs one memory round trip per KU units, not one per unit.
-// Units past the lane's count load unit 0's window again (cache hits) and are not summed.
+// the 4x4 block at one fractional case (CASE bit 0: horizontal fraction, bit 1: vertical) from its reference
+// window: get(r, c) is the window pixel at row r, column c, the window starting 3 rows above the block when
+// CASE & 2 and 3 columns left of it when CASE & 1 (11 rows / columns then, else 4)
+template <typename P, int CASE, typename Get>
+__device__ __forceinline__ void subpel_block(const Get& get, const int (&cx)[8], const int (&cy)[8], int depth,
+                                             int (&blk)[4][4])
+{
+    const int maxv = (1 << depth) - 1;
+    const int head = 14 - depth;
+    if constexpr (CASE == 0)
+    {
+#pragma unroll
+        for (int r = 0; r < 4; r++)
+#pragma unroll
+            for (int c = 0; c < 4; c++) blk[r][c] = get(r, c);
+    }
+    else if constexpr (CASE == 1)
+    {
+        // interp_horiz_pp: (int16)((sum + 32) >> 6) clipped
+#pragma unroll
+        for (int r = 0; r < 4; r++)
+#pragma unroll
+            for (int c = 0; c < 4; c++)
+            {
+                int sum = 0;
+#pragma unroll
+                for (int t = 0; t < 8; t++) sum += cx[t] * get(r, c + t);
+                const int val = (int16_t)((sum + 32) >> 6);
+                blk[r][c] = val < 0 ? 0 : (val > maxv ? maxv : val);
+            }
+    }
+    else if constexpr (CASE == 2)
+    {
+        // interp_vert_pp
+#pragma unroll
+        for (int r = 0; r < 4; r++)
+#pragma unroll
+            for (int c = 0; c < 4; c++)
+            {
+                int sum = 0;
+#pragma unroll
+                for (int t = 0; t < 8; t++) sum += cy[t] * get(r + t, c);
+                const int val = (int16_t)((sum + 32) >> 6);
+                blk[r][c] = val < 0 ? 0 : (val > maxv ? maxv : val);
+            }
+    }
+    else
+    {
+        // interp_hv_pp: horizontal ps over 11 rows (int16), then vertical sp
+        const int ps_shift = 6 - head, ps_off = -8192 * (1 << ps_shift);
+        const int sp_shift = 6 + head, sp_off = (1 << (sp_shift - 1)) + (8192 << 6);
+        int m[11][4];
+#pragma unroll
+        for (int i = 0; i < 11; i++)
+#pragma unroll
+            for (int c = 0; c < 4; c++)
+            {
+                int sum = 0;
+#pragma unroll
+                for (int t = 0; t < 8; t++) sum += cx[t] * get(i, c + t);
+                m[i][c] = (int16_t)((sum + ps_off) >> ps_shift);
+            }
+#pragma unroll
+        for (int r = 0; r < 4; r++)
+#pragma unroll
+            for (int c = 0; c < 4; c++)
+            {
+                int sum = 0;
+#pragma unroll
+                for (int t = 0; t < 8; t++) sum += cy[t] * m[r + t][c];
+                const int val = (int16_t)((sum + sp_off) >> sp_shift);
+                blk[r][c] = val < 0 ? 0 : (val > maxv ? maxv : val);
+            }
+    }
+}
+
+// SATD (or SAD) of the source unit against a 4x4 block
+template <typename P>
+__device__ __forceinline__ int block_cost(const uint32_t (&fe)[4][sizeof(P) == 1 ? 1 : 2], const int (&blk)[4][4],
+                                          bool satd)
+{
+    int cost = 0;
+    if (satd)
+    {
+        int d[4][4];
+#pragma unroll
+        for (int r = 0; r < 4; r++)
+#pragma unroll
+            for (int c = 0; c < 4; c++) d[r][c] = px<P>(fe[r], c) - blk[r][c];
+#pragma unroll
+        for (int r = 0; r < 4; r++) had4m(d[r][0], d[r][1], d[r][2], d[r][3]);
+        int sum = 0;
+#pragma unroll
+        for (int c = 0; c < 4; c++)
+        {
+            had4m(d[0][c], d[1][c], d[2][c], d[3][c]);
+#pragma unroll
+            for (int r = 0; r < 4; r++) sum += d[r][c] < 0 ? -d[r][c] : d[r][c];
+        }
+        cost = sum >> 1;      // each 4x4 raw sum is even (SURVEY note a7): any tiling gives satd
+    }
+    else
+    {
+#pragma unroll
+        for (int r = 0; r < 4; r++)
+#pragma unroll
+            for (int c = 0; c < 4; c++)
+            {
+                const int d = px<P>(fe[r], c) - blk[r][c];
+                cost += d < 0 ? -d : d;
+            }
+    }
+    return cost;
+}
+
+// subpelCompare's luma part over this lane's units for one fractional case: the reference windows (and
+// source rows) of KU units are all loaded before the first is filtered, so a candidate costs one memory round
+// trip per KU units, not one per unit.  Units past the lane's count load unit 0's window again (cache hits)
+// and are not summed.
 template <typename P, int CASE, int KU>
 __device__ __forceinline__ int subpel_units(const MeState<P>& s, const P* base, const int (&cx)[8],
                                             const int (&cy)[8], bool satd)
 {
     constexpr int R = (CASE & 2) ? 11 : 4, C = (CASE & 1) ? 11 : 4;
-    const int maxv = (1 << s.depth) - 1;
-    const int head = 14 - s.depth;
     const int64_t rs = s.rs, fs = s.fs;
     int acc = 0;
     for (int k0 = 0; k0 < s.nu; k0 += KU)
@@ -414,107 +561,53 @@ __device__ __forceinline__ int subpel_units(const MeState<P>& s, const P* base, 
         for (int k = 0; k < KU; k++)
         {
             int blk[4][4];
-            if constexpr (CASE == 0)
-            {
-#pragma unroll
-                for (int r = 0; r < 4; r++)
-#pragma unroll
-                    for (int c = 0; c < 4; c++) blk[r][c] = win[k][r].get(c);
-            }
-            else if constexpr (CASE == 1)
-            {
-                // interp_horiz_pp: (int16)((sum + 32) >> 6) clipped
-#pragma unroll
-                for (int r = 0; r < 4; r++)
-#pragma unroll
-                    for (int c = 0; c < 4; c++)
-                    {
-                        int sum = 0;
-#pragma unroll
-                        for (int t = 0; t < 8; t++) sum += cx[t] * win[k][r].get(c + t);
-                        const int val = (int16_t)((sum + 32) >> 6);
-                        blk[r][c] = val < 0 ? 0 : (val > maxv ? maxv : val);
-                    }
-            }
-            else if constexpr (CASE == 2)
-            {
-                // interp_vert_pp
-#pragma unroll
-                for (int r = 0; r < 4; r++)
-#pragma unroll
-                    for (int c = 0; c < 4; c++)
-                    {
-                        int sum = 0;
-#pragma unroll
-                        for (int t = 0; t < 8; t++) sum += cy[t] * win[k][r + t].get(c);
-                        const int val = (int16_t)((sum + 32) >> 6);
-                        blk[r][c] = val < 0 ? 0 : (val > maxv ? maxv : val);
-                    }
-            }
-            else
-            {
-                // interp_hv_pp: horizontal ps over 11 rows (int16), then vertical sp
-                const int ps_shift = 6 - head, ps_off = -8192 * (1 << ps_shift);
-                const int sp_shift = 6 + head, sp_off = (1 << (sp_shift - 1)) + (8192 << 6);
-                int m[11][4];
-#pragma unroll
-                for (int i = 0; i < 11; i++)
-#pragma unroll
-                    for (int c = 0; c < 4; c++)
-                    {
-                        int sum = 0;
-#pragma unroll
-                        for (int t = 0; t < 8; t++) sum += cx[t] * win[k][i].get(c + t);
-                        m[i][c] = (int16_t)((sum + ps_off) >> ps_shift);
-                    }
-#pragma unroll
-                for (int r = 0; r < 4; r++)
-#pragma unroll
-                    for (int c = 0; c < 4; c++)
-                    {
-                        int sum = 0;
-#pragma unroll
-                        for (int t = 0; t < 8; t++) sum += cy[t] * m[r + t][c];
-                        const int val = (int16_t)((sum + sp_off) >> sp_shift);
-                        blk[r][c] = val < 0 ? 0 : (val > maxv ? maxv : val);
-                    }
-            }
-            int cost = 0;
-            if (satd)
-            {
-                int d[4][4];
-#pragma unroll
-                for (int r = 0; r < 4; r++)
-#pragma unroll
-                    for (int c = 0; c < 4; c++) d[r][c] = px<P>(fe[k][r], c) - blk[r][c];
-#pragma unroll
-                for (int r = 0; r < 4; r++) had4m(d[r][0], d[r][1], d[r][2], d[r][3]);
-                int sum = 0;
-#pragma unroll
-                for (int c = 0; c < 4; c++)
-                {
-                    had4m(d[0][c], d[1][c], d[2][c], d[3][c]);
-#pragma unroll
-                    for (int r = 0; r < 4; r++) sum += d[r][c] < 0 ? -d[r][c] : d[r][c];
-                }
-                cost = sum >> 1;      // each 4x4 raw sum is even (SURVEY note a7): any tiling gives satd
-            }
-            else
-            {
-#pragma unroll
-                for (int r = 0; r < 4; r++)
-#pragma unroll
-                    for (int c = 0; c < 4; c++)
-                    {
-                        const int d = px<P>(fe[k][r], c) - blk[r][c];
-                        cost += d < 0 ? -d : d;
-                    }
-            }
+            subpel_block<P, CASE>([&](int r, int c) { return win[k][r].get(c); }, cx, cy, s.depth, blk);
+            const int cost = block_cost<P>(fe[k], blk, satd);
             if (k0 + k < s.nu) acc += cost;
         }
     }
     return acc;
 }
+
+// One row of the window shared by a batch of sub-pel candidates: 12 pixels (the 8-tap reach of two integer
+// positions), 8-bit in 3 dwords, 16-bit in 6
+template <typename P>
+struct Row12
+{
+    static constexpr int NW = 3 * (int)sizeof(P);
+    uint32_t w[NW];
+    __device__ __forceinline__ void load(const P* p)
+    {
+        if constexpr (sizeof(P) == 1)
+        {
+            const uint2 v = ldu<uint2>(p);
+            w[0] = v.x; w[1] = v.y; w[2] = ldu<uint32_t>(p + 8);
+        }
+        else
+        {
+            const uint4 v = ldu<uint4>(p);
+            const uint2 u = ldu<uint2>(p + 8);
+            w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w; w[4] = u.x; w[5] = u.y;
+        }
+    }
+    __device__ __forceinline__ int get(int i) const
+    {
+        if constexpr (sizeof(P) == 1) return (int)((w[i >> 2] >> (8 * (i & 3))) & 0xff);
+        else return (int)((w[i >> 1] >> (16 * (i & 1))) & 0xffff);
+    }
+    // this row from row a or b (sel), moved left by o (0 or 1) pixels: get(i) = source.get(i + o)
+    __device__ __forceinline__ void pick(const Row12& a, const Row12& b, bool sel, int o)
+    {
+        const uint32_t sh = (uint32_t)o * 8u * (uint32_t)sizeof(P);
+#pragma unroll
+        for (int j = 0; j < NW; j++)
+        {
+            const uint32_t lo = sel ? b.w[j] : a.w[j];
+            const uint32_t hi = j + 1 < NW ? (sel ? b.w[j + 1] : a.w[j + 1]) : 0u;
+            w[j] = __builtin_amdgcn_alignbit(hi, lo, sh);
+        }
+    }
+};
 
 // subpelCompare (motion.cpp:1174-1203): the block at quarter-pel (qx, qy), built by
 // luma_hpp / luma_vpp / luma_hvpp when fractional, compared with SAD or SATD.  8-bit windows of all
@@ -579,7 +672,92 @@ __device__ __noinline__ int subpel_cost(const P* ref, const P* fenc, int rs, int
     }
     if (s.chroma)
         acc += chroma_satd<P>(s, qx, qy);
-    return me_group_sum<G>(acc);
+    int v[1] = { acc };
+    me_group_sums<G, 1>(v);
+    return v[0];
+}
+
+// Four candidates of one sub-pel refinement round (square directions i0 .. i0 + 3 at distance d quarter-pels
+// around (qx, qy)), 8-bit: every candidate's integer position is X0 or X0 + 1 (Y0 or Y0 + 1), so one 12 x 12
+// window per unit holds all four 8-tap windows; it is loaded once, each candidate's 11 x 11 view is picked
+// from it in registers (row select, byte align), and the four group sums run side by side — one memory round
+// trip and one reduction for the four instead of four of each.  Costs (luma + chroma SATD) in candidate order.
+#ifndef X265AMD_ME_SPB
+#define X265AMD_ME_SPB 1
+#endif
+template <typename P, int G>
+__device__ __noinline__ int4 subpel_cost4(const P* ref, const P* fenc, int rs, int fs, int lane_nu, int wh, int dc,
+                                          const P* fcb, const P* fcr, const P* rcb, const P* rcr, int fcs, int rcs,
+                                          int qx, int qy, int d, int i0, bool satd)
+{
+    MeState<P> s;
+    s.ref = ref;
+    s.rs = rs;
+    s.fenc = fenc;
+    s.fs = fs;
+    s.lane = lane_nu & 255;
+    s.nu = lane_nu >> 8;
+    s.G = G;
+    s.w = wh & 255;
+    s.h = wh >> 8;
+    s.uw = s.w >> 2;
+    s.depth = dc & 255;
+    s.chroma = (dc >> 8) != 0;
+    if (s.chroma)
+    {
+        s.fc[0] = fcb; s.fc[1] = fcr;
+        s.rc[0] = rcb; s.rc[1] = rcr;
+        s.fcs = fcs; s.rcs = rcs;
+    }
+    const int X0 = (qx - d) >> 2, Y0 = (qy - d) >> 2;
+    int acc[4] = { 0, 0, 0, 0 };
+    for (int k = 0; k < s.nu; k++)
+    {
+        int ux, uy;
+        s.unit_xy(k, ux, uy);
+        const P* p = s.ref + (ux + X0 - 3) + (int64_t)(uy + Y0 - 3) * s.rs;
+        Row12<P> W[12];
+#pragma unroll
+        for (int r = 0; r < 12; r++) W[r].load(p + r * s.rs);
+        uint32_t fe[4][sizeof(P) == 1 ? 1 : 2];
+#pragma unroll
+        for (int r = 0; r < 4; r++) load4<P>(s.fenc + ux + (int64_t)(uy + r) * s.fs, fe[r]);
+#pragma unroll 1
+        for (int c = 0; c < 4; c++)
+        {
+            const int tx = qx + d * sq_dx(i0 + c), ty = qy + d * sq_dy(i0 + c);
+            const int ox = (tx >> 2) - X0, oy = (ty >> 2) - Y0;
+            const int xf = tx & 3, yf = ty & 3;
+            int cx[8], cy[8];
+#pragma unroll
+            for (int t = 0; t < 8; t++) { cx[t] = c_luma.c[xf][t]; cy[t] = c_luma.c[yf][t]; }
+            Row12<P> V[11];
+#pragma unroll
+            for (int r = 0; r < 11; r++) V[r].pick(W[r], W[r + 1], oy != 0, ox);
+            int blk[4][4];
+            if (!(xf | yf))
+                subpel_block<P, 0>([&](int r, int q) { return V[r + 3].get(q + 3); }, cx, cy, s.depth, blk);
+            else if (!yf)
+                subpel_block<P, 1>([&](int r, int q) { return V[r + 3].get(q); }, cx, cy, s.depth, blk);
+            else if (!xf)
+                subpel_block<P, 2>([&](int r, int q) { return V[r].get(q + 3); }, cx, cy, s.depth, blk);
+            else
+                subpel_block<P, 3>([&](int r, int q) { return V[r].get(q); }, cx, cy, s.depth, blk);
+            const int cost = block_cost<P>(fe, blk, satd);
+            acc[0] += c == 0 ? cost : 0;
+            acc[1] += c == 1 ? cost : 0;
+            acc[2] += c == 2 ? cost : 0;
+            acc[3] += c == 3 ? cost : 0;
+        }
+    }
+    if (s.chroma)
+    {
+#pragma unroll
+        for (int c = 0; c < 4; c++)
+            acc[c] += chroma_satd<P>(s, qx + d * sq_dx(i0 + c), qy + d * sq_dy(i0 + c));
+    }
+    me_group_sums<G, 4>(acc);
+    return make_int4(acc[0], acc[1], acc[2], acc[3]);
 }
 
 // workload[subme] of motion.cpp:48-58 as {hpel_iters, hpel_dirs, qpel_iters, qpel_dirs}, one
@@ -597,7 +775,9 @@ template <typename P, int G>
 #endif
 __global__ __launch_bounds__(X265AMD_BLOCK, X265AMD_ME_WAVES) void k_motion_search(const MeArgs a)
 {
-    const int64_t j = (int64_t)xcd_block() * (X265AMD_BLOCK / G) + threadIdx.x / G;
+    // searches per workgroup: X265AMD_BLOCK / G up to a wavefront per search; one above (blockDim = G)
+    constexpr int SPB = G > 64 ? 1 : X265AMD_BLOCK / G;
+    const int64_t j = (int64_t)xcd_block() * SPB + threadIdx.x / G;
     if (j >= a.n) return;                               // whole groups
     MeState<P> s;
     s.lane = threadIdx.x & (G - 1);
@@ -1033,29 +1213,51 @@ __global__ __launch_bounds__(X265AMD_BLOCK, X265AMD_ME_WAVES) void k_motion_sear
         bcost = s.mvcost(qx, qy);
     else
     {
+        // one refinement round: directions 1 .. ndir at distance d, the first strictly smaller cost wins
+        // (motion.cpp:700-760); 8-bit costs four directions per call
+        auto refine = [&](int d, int ndir, bool satd) {
+            int bdir = 0;
+            if constexpr (sizeof(P) == 1 && X265AMD_ME_SPB)
+            {
+                for (int i0 = 1; i0 <= ndir; i0 += 4)
+                {
+                    s.nsp += 4;
+                    const int4 c4 = subpel_cost4<P, G>(s.ref, s.fenc, (int)s.rs, (int)s.fs, s.lane | s.nu << 8,
+                                                       a.w | a.h << 8, a.depth | (s.chroma ? 256 : 0), s.fc[0],
+                                                       s.fc[1], s.rc[0], s.rc[1], (int)s.fcs, (int)s.rcs, qx, qy, d,
+                                                       i0, satd);
+                    const int cc[4] = { c4.x, c4.y, c4.z, c4.w };
+#pragma unroll
+                    for (int q = 0; q < 4; q++)
+                    {
+                        const int i = i0 + q, tx = qx + d * sq_dx(i), ty = qy + d * sq_dy(i);
+                        const int c = cc[q] + s.mvcost(tx, ty);
+                        if (c < bcost) { bcost = c; bdir = i; }
+                    }
+                }
+            }
+            else
+            {
+                for (int i = 1; i <= ndir; i++)
+                {
+                    const int tx = qx + d * sq_dx(i), ty = qy + d * sq_dy(i);
+                    const int c = spc(tx, ty, satd) + s.mvcost(tx, ty);
+                    if (c < bcost) { bcost = c; bdir = i; }
+                }
+            }
+            return bdir;
+        };
         if (hsatd) bcost = spc(qx, qy, true) + s.mvcost(qx, qy);
         for (int it = 0; it < wl.x; it++)
         {
-            int bdir = 0;
-            for (int i = 1; i <= wl.y; i++)
-            {
-                const int tx = qx + 2 * sq_dx(i), ty = qy + 2 * sq_dy(i);
-                const int c = spc(tx, ty, hsatd) + s.mvcost(tx, ty);
-                if (c < bcost) { bcost = c; bdir = i; }
-            }
+            const int bdir = refine(2, wl.y, hsatd);
             if (!bdir) break;
             qx += 2 * sq_dx(bdir); qy += 2 * sq_dy(bdir);
         }
         if (!hsatd) bcost = spc(qx, qy, true) + s.mvcost(qx, qy);
         for (int it = 0; it < wl.z; it++)
         {
-            int bdir = 0;
-            for (int i = 1; i <= wl.w; i++)
-            {
-                const int tx = qx + sq_dx(i), ty = qy + sq_dy(i);
-                const int c = spc(tx, ty, true) + s.mvcost(tx, ty);
-                if (c < bcost) { bcost = c; bdir = i; }
-            }
+            const int bdir = refine(1, wl.w, true);
             if (!bdir) break;
             qx += sq_dx(bdir); qy += sq_dy(bdir);
         }
@@ -1191,17 +1393,36 @@ __global__ __launch_bounds__(256) void k_full_search(const MeArgs a)
     }
 }
 
+// largest group of lanes per search (X265AMD_ME_GMAX: 256, the default, or 128 for a search over up to four /
+// two wavefronts of one workgroup — a lane per 4x4 unit up to 64x64, so each candidate's compare is a quarter
+// of the dependent instructions of one wave holding four units per lane; 64 = one wave per search).  Pinned
+// 2160p medium encode: kernel 0.055 -> 0.034 ms per launch, 10.9-11.3 -> 11.2-11.7 fps, identical bitstreams
+// (profiles/r05/z/gmax_ab.txt)
+static int me_gmax()
+{
+    static int v = 0;
+    if (!v)
+    {
+        const char* e = getenv("X265AMD_ME_GMAX");
+        const int g = e ? atoi(e) : 256;
+        v = g >= 256 ? 256 : g >= 128 ? 128 : 64;
+    }
+    return v;
+}
+
 template <typename P>
 static int launch_me(const MeArgs& a, hipStream_t st)
 {
     if (a.method == 4)
         hipLaunchKernelGGL((k_full_search<P>), dim3(a.n), dim3(256), 0, st, a);
     const int G = 1 << a.lg;
-    const uint32_t blocks = (uint32_t)((a.n + X265AMD_BLOCK / G - 1) / (X265AMD_BLOCK / G));
-#define L(g) case g: hipLaunchKernelGGL((k_motion_search<P, g>), dim3(blocks), dim3(X265AMD_BLOCK), 0, st, a); break;
+    const int spb = G > 64 ? 1 : X265AMD_BLOCK / G;
+    const uint32_t blocks = (uint32_t)((a.n + spb - 1) / spb);
+    const int threads = G > 64 ? G : X265AMD_BLOCK;
+#define L(g) case g: hipLaunchKernelGGL((k_motion_search<P, g>), dim3(blocks), dim3(threads), 0, st, a); break;
     switch (G)
     {
-        L(4) L(8) L(16) L(32) L(64)
+        L(4) L(8) L(16) L(32) L(64) L(128) L(256)
     default: return X265AMD_EINVAL;
     }
 #undef L
@@ -1241,7 +1462,7 @@ extern "C" int x265amd_motion_search(int depth, int count, const x265amd_me_batc
         const hipStream_t bs = fj.stream(k++);
         const int units = (b.w / 4) * (b.h / 4);
         int g = 4, lg = 2;                               // groups of at least 4 lanes (fewer kernel variants)
-        while (g < units && g < 64) { g <<= 1; lg++; }
+        while (g < units && g < me_gmax()) { g <<= 1; lg++; }
         if ((units + g - 1) / g > kMeMaxUnits) return X265AMD_EINVAL;
         MeArgs a{ b.fenc, b.fenc_off, (int64_t)b.fenc_stride, b.ref, b.ref_off, (int64_t)b.ref_stride, b.mv_range,
                   b.mvp, b.mvc, b.num_cand, b.mvcost, b.mvcost_off, b.out_mv, b.out_cost, b.fenc_cb, b.fenc_cr,

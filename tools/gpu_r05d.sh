@@ -33,6 +33,7 @@ for pmc in FETCH_SIZE WRITE_SIZE; do
   echo "pmc $pmc done"
   du -sh $GRAFT_REPO_ROOT/gpurun_out/r05/d
 done
+python3 $GRAFT_REPO_ROOT/tools/me_traffic.py $GRAFT_REPO_ROOT/gpurun_out/r05/d $GRAFT_REPO_ROOT/gpurun_out/r05/d/pmc_me_traffic.json || exit 1
 X265AMD_ME_STATS=1 timeout -k 10 300 rocprofv3 --kernel-trace --hip-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/r05/d/hiptrace -o enc -- \
     $GRAFT_REPO_ROOT/oracle/_ref/x265la8 --input /tmp/s16.yuv --input-res 3840x2160 --fps 30 --frames 16 --preset medium \
     --pools 16 --no-info -o /tmp/p.hevc > $GRAFT_REPO_ROOT/gpurun_out/r05/d/hiptrace.log 2>&1 \
