@@ -49,3 +49,21 @@ def gpu_prims(native_lib):
     from src.x265_amd import Primitives
 
     return Primitives(device=0)
+
+
+@pytest.fixture(autouse=True)
+def _gpu_teardown(request):
+    """After every GPU test: collect dead reference cycles (a discarded GpuFramePipeline owns CUDA graphs,
+    streams and device buffers through lambdas that reference itself) and synchronise the device, inside
+    the test that made them.  Without it the cycles die whenever the cyclic GC next runs — in some later
+    test — and any asynchronous device error is reported by a later test's first call instead of the one
+    that caused it (two full runs saw an illegal address surface at the first copy of an unrelated test)."""
+    yield
+    if request.node.get_closest_marker("gpu") is None:
+        return
+    import gc
+
+    gc.collect()
+    torch = sys.modules.get("torch")
+    if torch is not None and torch.cuda.is_initialized():
+        torch.cuda.synchronize()
