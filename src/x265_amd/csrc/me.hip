@@ -218,7 +218,7 @@ __device__ __forceinline__ void fpel_sads(const MeState<P>& s, const int (&mx)[N
                                           int counted = N)
 {
     s.nfp += counted;
-    if constexpr (G < 64) fpel_sad_nu<P, G, N, 1>(s, mx, my, out);
+    if constexpr (G != 64) fpel_sad_nu<P, G, N, 1>(s, mx, my, out);     // one unit per lane below and above
     else if (s.nmax == 1) fpel_sad_nu<P, G, N, 1>(s, mx, my, out);
     else if (s.nmax == 2) fpel_sad_nu<P, G, N, 2>(s, mx, my, out);
     else fpel_sad_nu<P, G, N, kMeMaxUnits>(s, mx, my, out);
@@ -656,7 +656,7 @@ __device__ __noinline__ int subpel_cost(const P* ref, const P* fenc, int rs, int
     // it then spills to scratch on every call cost more than the round trips saved
     // (profiles/r05/me_kernel_variants_ab.txt: 0.081 ms per launch at four 8-bit units, 0.059 at two)
     constexpr int KU = X265AMD_ME_KU64, KU_HV = sizeof(P) == 1 ? KU : 1;
-    if (G < 64 || nmax == 1)
+    if (G != 64 || nmax == 1)      // (multi-unit lanes only in one-wave 64-lane groups, X265AMD_ME_GMAX=64)
     {
         if (!(xf | yf)) acc = subpel_units<P, 0, 1>(s, base, cx, cy, satd);
         else if (!yf) acc = subpel_units<P, 1, 1>(s, base, cx, cy, satd);
@@ -675,6 +675,21 @@ __device__ __noinline__ int subpel_cost(const P* ref, const P* fenc, int rs, int
     int v[1] = { acc };
     me_group_sums<G, 1>(v);
     return v[0];
+}
+
+// 8-bit horizontal 8-tap sums of one 12-pixel view row at output columns 0 .. 3 (output c = taps over pixels
+// c .. c + 7): v_dot4_i32_i8 on pixels biased to signed (p ^ 0x80 = p - 128), so each sum comes out lowered by
+// 128 x (sum of the taps = 64) = 8192 — added back through `init` where the filter needs the true sum
+__device__ __forceinline__ void hsum4_u8(const uint32_t (&w)[3], uint32_t k0, uint32_t k1, int init, int (&out)[4])
+{
+    const uint32_t x0 = w[0] ^ 0x80808080u, x1 = w[1] ^ 0x80808080u, x2 = w[2] ^ 0x80808080u;
+#pragma unroll
+    for (int c = 0; c < 4; c++)
+    {
+        const uint32_t lo = __builtin_amdgcn_alignbyte(x1, x0, (uint32_t)c);
+        const uint32_t hi = __builtin_amdgcn_alignbyte(x2, x1, (uint32_t)c);
+        out[c] = __builtin_amdgcn_sdot4((int)hi, (int)k1, __builtin_amdgcn_sdot4((int)lo, (int)k0, init, false), false);
+    }
 }
 
 // Four candidates of one sub-pel refinement round (square directions i0 .. i0 + 3 at distance d quarter-pels
@@ -735,14 +750,69 @@ __device__ __noinline__ int4 subpel_cost4(const P* ref, const P* fenc, int rs, i
 #pragma unroll
             for (int r = 0; r < 11; r++) V[r].pick(W[r], W[r + 1], oy != 0, ox);
             int blk[4][4];
+            // the horizontal taps packed as signed bytes for the 8-bit dot products
+            uint32_t k0 = 0, k1 = 0;
+#pragma unroll
+            for (int t = 0; t < 4; t++)
+            {
+                k0 |= (uint32_t)(cx[t] & 255) << (8 * t);
+                k1 |= (uint32_t)(cx[t + 4] & 255) << (8 * t);
+            }
             if (!(xf | yf))
                 subpel_block<P, 0>([&](int r, int q) { return V[r + 3].get(q + 3); }, cx, cy, s.depth, blk);
             else if (!yf)
-                subpel_block<P, 1>([&](int r, int q) { return V[r + 3].get(q); }, cx, cy, s.depth, blk);
+            {
+                if constexpr (sizeof(P) == 1)
+                {
+                    // interp_horiz_pp: (int16)((sum + 32) >> 6) clipped (the dot sums are 8192 low)
+#pragma unroll
+                    for (int r = 0; r < 4; r++)
+                    {
+                        int hs[4];
+                        hsum4_u8(V[r + 3].w, k0, k1, 8192 + 32, hs);
+#pragma unroll
+                        for (int q = 0; q < 4; q++)
+                        {
+                            const int val = (int16_t)(hs[q] >> 6);
+                            blk[r][q] = val < 0 ? 0 : (val > 255 ? 255 : val);
+                        }
+                    }
+                }
+                else
+                    subpel_block<P, 1>([&](int r, int q) { return V[r + 3].get(q); }, cx, cy, s.depth, blk);
+            }
             else if (!xf)
                 subpel_block<P, 2>([&](int r, int q) { return V[r].get(q + 3); }, cx, cy, s.depth, blk);
             else
-                subpel_block<P, 3>([&](int r, int q) { return V[r].get(q); }, cx, cy, s.depth, blk);
+            {
+                if constexpr (sizeof(P) == 1)
+                {
+                    // interp_hv_pp at 8 bits: the ps pass is (int16)(sum - 8192) (shift 0, offset -8192), which
+                    // is the biased dot sum itself; then the sp pass as in subpel_block
+                    int m[11][4];
+#pragma unroll
+                    for (int i = 0; i < 11; i++)
+                    {
+                        hsum4_u8(V[i].w, k0, k1, 0, m[i]);
+#pragma unroll
+                        for (int q = 0; q < 4; q++) m[i][q] = (int16_t)m[i][q];
+                    }
+                    constexpr int sp_shift = 12, sp_off = (1 << 11) + (8192 << 6);
+#pragma unroll
+                    for (int r = 0; r < 4; r++)
+#pragma unroll
+                        for (int q = 0; q < 4; q++)
+                        {
+                            int sum = 0;
+#pragma unroll
+                            for (int t = 0; t < 8; t++) sum += cy[t] * m[r + t][q];
+                            const int val = (int16_t)((sum + sp_off) >> sp_shift);
+                            blk[r][q] = val < 0 ? 0 : (val > 255 ? 255 : val);
+                        }
+                }
+                else
+                    subpel_block<P, 3>([&](int r, int q) { return V[r].get(q); }, cx, cy, s.depth, blk);
+            }
             const int cost = block_cost<P>(fe, blk, satd);
             acc[0] += c == 0 ? cost : 0;
             acc[1] += c == 1 ? cost : 0;
@@ -835,8 +905,16 @@ __global__ __launch_bounds__(X265AMD_BLOCK, X265AMD_ME_WAVES) void k_motion_sear
     int bprecost = spc(pmx, pmy, false);   // no MV cost (motion.cpp:609)
     int bx = (pmx + 2) >> 2, by = (pmy + 2) >> 2;
     int bcost = bprecost;
-    if ((pmx | pmy) & 3) bcost = fpel_sad<P, G>(s, bx, by) + s.mvcost(4 * bx, 4 * by);
-    if (pmx | pmy)
+    if (((pmx | pmy) & 3) && (pmx | pmy))
+    {
+        // the rounded MVP and MV 0 in one round trip
+        const int mx[2] = { bx, 0 }, my[2] = { by, 0 };
+        int c[2];
+        fpel_costs<P, G, 2>(s, mx, my, c);
+        bcost = c[0];
+        if (c[1] < bcost) { bcost = c[1]; bx = by = 0; }
+    }
+    else if (pmx | pmy)
     {
         const int c = fpel_sad<P, G>(s, 0, 0) + s.mvcost(0, 0);
         if (c < bcost) { bcost = c; bx = by = 0; }

@@ -918,6 +918,28 @@ extern "C" int x265amd_mes_ref420(x265amd_mes* s, const void* key, int64_t gen, 
     if (!s || !key || !planes || !planes[0] || !slot || rows_final < 0 || rows_final > s->cfg.ctu_rows ||
         (s->cfg.chroma && (!planes[1] || !planes[2])))
         return record(X265AMD_EINVAL);
+    // the common call (every CU asks for each of its references): a known picture whose rows are all
+    // resident (or recorded, with launcher uploads) — no HIP call, one map lookup and the picture's lock
+    {
+        x265amd_mes::Picture* q = nullptr;
+        {
+            std::lock_guard<std::mutex> g(s->mu);
+            auto it = s->pics.find(key);
+            if (it != s->pics.end()) q = it->second;
+        }
+        if (q)
+        {
+            std::lock_guard<std::mutex> g(q->mu);
+            const int np = s->cfg.chroma ? 3 : 1;
+            bool same = q->gen == gen && rows_final <= (s->lupload ? q->rows_want : q->rows_up);
+            for (int k = 0; k < np && same; k++) same = q->pinned[k] == planes[k];
+            if (same)
+            {
+                *slot = q->slot;
+                return 0;
+            }
+        }
+    }
     MES_TRY(use_device(s));
     x265amd_mes_thread* t;
     if (int rc = thread_ctx(s, &t)) return rc;
@@ -1019,6 +1041,16 @@ extern "C" int x265amd_mes_rows(x265amd_mes* s, const void* key, int64_t gen, in
 extern "C" int x265amd_mes_table(x265amd_mes* s, const uint16_t* centre, int* index)
 {
     if (!s || !centre || !index) return record(X265AMD_EINVAL);
+    {
+        // a table already resident (every CU asks): no HIP call
+        std::lock_guard<std::mutex> g(s->mu);
+        auto it = s->tabs.find(centre);
+        if (it != s->tabs.end())
+        {
+            *index = it->second;
+            return 0;
+        }
+    }
     MES_TRY(use_device(s));
     x265amd_mes_thread* t;
     if (int rc = thread_ctx(s, &t)) return rc;
