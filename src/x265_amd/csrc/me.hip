@@ -531,6 +531,79 @@ __device__ __forceinline__ int block_cost(const uint32_t (&fe)[4][sizeof(P) == 1
     return cost;
 }
 
+// 8-bit horizontal 8-tap sums of one 12-pixel view row at output columns 0 .. 3 (output c = taps over pixels
+// c .. c + 7): v_dot4_i32_i8 on pixels biased to signed (p ^ 0x80 = p - 128), so each sum comes out lowered by
+// 128 x (sum of the taps = 64) = 8192 — added back through `init` where the filter needs the true sum
+__device__ __forceinline__ void hsum4_u8(const uint32_t (&w)[3], uint32_t k0, uint32_t k1, int init, int (&out)[4])
+{
+    const uint32_t x0 = w[0] ^ 0x80808080u, x1 = w[1] ^ 0x80808080u, x2 = w[2] ^ 0x80808080u;
+#pragma unroll
+    for (int c = 0; c < 4; c++)
+    {
+        const uint32_t lo = __builtin_amdgcn_alignbyte(x1, x0, (uint32_t)c);
+        const uint32_t hi = __builtin_amdgcn_alignbyte(x2, x1, (uint32_t)c);
+        out[c] = __builtin_amdgcn_sdot4((int)hi, (int)k1, __builtin_amdgcn_sdot4((int)lo, (int)k0, init, false), false);
+    }
+}
+
+// the 8-bit horizontal cases on the dot products: CASE 1 (interp_horiz_pp over the block's 4 rows) or CASE 3
+// (interp_hv_pp: the ps pass over 11 rows is the biased dot sum itself at 8 bits, then the sp pass);
+// roww(r, w) gives window row r as 12 pixels in 3 dwords (the window starts 3 rows up for CASE 3)
+template <int CASE, typename RowW>
+__device__ __forceinline__ void subpel_block_u8(const RowW& roww, const int (&cx)[8], const int (&cy)[8],
+                                                int (&blk)[4][4])
+{
+    uint32_t k0 = 0, k1 = 0;
+#pragma unroll
+    for (int t = 0; t < 4; t++)
+    {
+        k0 |= (uint32_t)(cx[t] & 255) << (8 * t);
+        k1 |= (uint32_t)(cx[t + 4] & 255) << (8 * t);
+    }
+    if constexpr (CASE == 1)
+    {
+#pragma unroll
+        for (int r = 0; r < 4; r++)
+        {
+            uint32_t w[3];
+            roww(r, w);
+            int hs[4];
+            hsum4_u8(w, k0, k1, 8192 + 32, hs);          // (int16)((sum + 32) >> 6) clipped
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+            {
+                const int val = (int16_t)(hs[q] >> 6);
+                blk[r][q] = val < 0 ? 0 : (val > 255 ? 255 : val);
+            }
+        }
+    }
+    else
+    {
+        int m[11][4];
+#pragma unroll
+        for (int i = 0; i < 11; i++)
+        {
+            uint32_t w[3];
+            roww(i, w);
+            hsum4_u8(w, k0, k1, 0, m[i]);
+#pragma unroll
+            for (int q = 0; q < 4; q++) m[i][q] = (int16_t)m[i][q];
+        }
+        constexpr int sp_shift = 12, sp_off = (1 << 11) + (8192 << 6);
+#pragma unroll
+        for (int r = 0; r < 4; r++)
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+            {
+                int sum = 0;
+#pragma unroll
+                for (int t = 0; t < 8; t++) sum += cy[t] * m[r + t][q];
+                const int val = (int16_t)((sum + sp_off) >> sp_shift);
+                blk[r][q] = val < 0 ? 0 : (val > 255 ? 255 : val);
+            }
+    }
+}
+
 // subpelCompare's luma part over this lane's units for one fractional case: the reference windows (and
 // source rows) of KU units are all loaded before the first is filtered, so a candidate costs one memory round
 // trip per KU units, not one per unit.  Units past the lane's count load unit 0's window again (cache hits)
@@ -561,7 +634,15 @@ __device__ __forceinline__ int subpel_units(const MeState<P>& s, const P* base, 
         for (int k = 0; k < KU; k++)
         {
             int blk[4][4];
-            subpel_block<P, CASE>([&](int r, int c) { return win[k][r].get(c); }, cx, cy, s.depth, blk);
+            if constexpr (sizeof(P) == 1 && (CASE & 1))
+                // 8 window bytes and the 4 from +7: bytes 8 .. 10 are the second load's upper three
+                subpel_block_u8<CASE>([&](int r, uint32_t (&w)[3]) {
+                    w[0] = win[k][r].a[0];
+                    w[1] = win[k][r].a[1];
+                    w[2] = win[k][r].b[0] >> 8;
+                }, cx, cy, blk);
+            else
+                subpel_block<P, CASE>([&](int r, int c) { return win[k][r].get(c); }, cx, cy, s.depth, blk);
             const int cost = block_cost<P>(fe[k], blk, satd);
             if (k0 + k < s.nu) acc += cost;
         }
@@ -677,21 +758,6 @@ __device__ __noinline__ int subpel_cost(const P* ref, const P* fenc, int rs, int
     return v[0];
 }
 
-// 8-bit horizontal 8-tap sums of one 12-pixel view row at output columns 0 .. 3 (output c = taps over pixels
-// c .. c + 7): v_dot4_i32_i8 on pixels biased to signed (p ^ 0x80 = p - 128), so each sum comes out lowered by
-// 128 x (sum of the taps = 64) = 8192 — added back through `init` where the filter needs the true sum
-__device__ __forceinline__ void hsum4_u8(const uint32_t (&w)[3], uint32_t k0, uint32_t k1, int init, int (&out)[4])
-{
-    const uint32_t x0 = w[0] ^ 0x80808080u, x1 = w[1] ^ 0x80808080u, x2 = w[2] ^ 0x80808080u;
-#pragma unroll
-    for (int c = 0; c < 4; c++)
-    {
-        const uint32_t lo = __builtin_amdgcn_alignbyte(x1, x0, (uint32_t)c);
-        const uint32_t hi = __builtin_amdgcn_alignbyte(x2, x1, (uint32_t)c);
-        out[c] = __builtin_amdgcn_sdot4((int)hi, (int)k1, __builtin_amdgcn_sdot4((int)lo, (int)k0, init, false), false);
-    }
-}
-
 // Four candidates of one sub-pel refinement round (square directions i0 .. i0 + 3 at distance d quarter-pels
 // around (qx, qy)), 8-bit: every candidate's integer position is X0 or X0 + 1 (Y0 or Y0 + 1), so one 12 x 12
 // window per unit holds all four 8-tap windows; it is loaded once, each candidate's 11 x 11 view is picked
@@ -750,34 +816,14 @@ __device__ __noinline__ int4 subpel_cost4(const P* ref, const P* fenc, int rs, i
 #pragma unroll
             for (int r = 0; r < 11; r++) V[r].pick(W[r], W[r + 1], oy != 0, ox);
             int blk[4][4];
-            // the horizontal taps packed as signed bytes for the 8-bit dot products
-            uint32_t k0 = 0, k1 = 0;
-#pragma unroll
-            for (int t = 0; t < 4; t++)
-            {
-                k0 |= (uint32_t)(cx[t] & 255) << (8 * t);
-                k1 |= (uint32_t)(cx[t + 4] & 255) << (8 * t);
-            }
             if (!(xf | yf))
                 subpel_block<P, 0>([&](int r, int q) { return V[r + 3].get(q + 3); }, cx, cy, s.depth, blk);
             else if (!yf)
             {
                 if constexpr (sizeof(P) == 1)
-                {
-                    // interp_horiz_pp: (int16)((sum + 32) >> 6) clipped (the dot sums are 8192 low)
-#pragma unroll
-                    for (int r = 0; r < 4; r++)
-                    {
-                        int hs[4];
-                        hsum4_u8(V[r + 3].w, k0, k1, 8192 + 32, hs);
-#pragma unroll
-                        for (int q = 0; q < 4; q++)
-                        {
-                            const int val = (int16_t)(hs[q] >> 6);
-                            blk[r][q] = val < 0 ? 0 : (val > 255 ? 255 : val);
-                        }
-                    }
-                }
+                    subpel_block_u8<1>([&](int r, uint32_t (&w)[3]) {
+                        w[0] = V[r + 3].w[0]; w[1] = V[r + 3].w[1]; w[2] = V[r + 3].w[2];
+                    }, cx, cy, blk);
                 else
                     subpel_block<P, 1>([&](int r, int q) { return V[r + 3].get(q); }, cx, cy, s.depth, blk);
             }
@@ -786,30 +832,9 @@ __device__ __noinline__ int4 subpel_cost4(const P* ref, const P* fenc, int rs, i
             else
             {
                 if constexpr (sizeof(P) == 1)
-                {
-                    // interp_hv_pp at 8 bits: the ps pass is (int16)(sum - 8192) (shift 0, offset -8192), which
-                    // is the biased dot sum itself; then the sp pass as in subpel_block
-                    int m[11][4];
-#pragma unroll
-                    for (int i = 0; i < 11; i++)
-                    {
-                        hsum4_u8(V[i].w, k0, k1, 0, m[i]);
-#pragma unroll
-                        for (int q = 0; q < 4; q++) m[i][q] = (int16_t)m[i][q];
-                    }
-                    constexpr int sp_shift = 12, sp_off = (1 << 11) + (8192 << 6);
-#pragma unroll
-                    for (int r = 0; r < 4; r++)
-#pragma unroll
-                        for (int q = 0; q < 4; q++)
-                        {
-                            int sum = 0;
-#pragma unroll
-                            for (int t = 0; t < 8; t++) sum += cy[t] * m[r + t][q];
-                            const int val = (int16_t)((sum + sp_off) >> sp_shift);
-                            blk[r][q] = val < 0 ? 0 : (val > 255 ? 255 : val);
-                        }
-                }
+                    subpel_block_u8<3>([&](int r, uint32_t (&w)[3]) {
+                        w[0] = V[r].w[0]; w[1] = V[r].w[1]; w[2] = V[r].w[2];
+                    }, cx, cy, blk);
                 else
                     subpel_block<P, 3>([&](int r, int q) { return V[r].get(q); }, cx, cy, s.depth, blk);
             }
