@@ -202,7 +202,8 @@ struct x265amd_mes
     int dsleepers = 0;                // waiters sleeping on dcv (guarded by dmu)
     std::atomic<int64_t> queued{ 0 }; // requests posted (the launchers' lock-free "anything new?" check)
     int trace = 0;                    // X265AMD_MES_TRACE=n: log the first n posts / launches / waits
-    bool zerocopy = false;            // X265AMD_MES_ZEROCOPY=1: the kernel reads / writes the pinned staging
+    int zerocopy = 0;                 // X265AMD_MES_ZEROCOPY=1: the kernel reads / writes the pinned staging;
+                                      // 2: it writes its outputs there (inputs still uploaded)
     bool prio = true;                 // X265AMD_MES_PRIORITY=0: launch streams at the default priority
     bool lspin = false;               // X265AMD_MES_LSPIN=1: launchers poll for completion (a busy core each:
                                       // slower on the encoder's 16-core budget, profiles/r05/bench_lspin_pinned_ab.txt)
@@ -578,7 +579,19 @@ void launcher_main(x265amd_mes* s, x265amd_mes_launcher* L)
                 bt.back().eval_count = (uint32_t*)(sub.dev + Ly.evals);
                 njobs += i;
             }
-            if (s->zerocopy && L->g.hdev)
+            if (s->zerocopy == 2 && L->g.hdev)
+            {
+                // the kernel writes its outputs straight into the pinned staging (no download copy)
+                const ptrdiff_t d = L->g.hdev - L->g.dev;
+                for (size_t k = 0; k < bt.size(); k++)
+                {
+                    x265amd_me_batch& b = bt[k];
+                    b.out_mv = (int16_t*)((uint8_t*)b.out_mv + d);
+                    b.out_cost = (int32_t*)((uint8_t*)b.out_cost + d);
+                    if (b.eval_count) b.eval_count = (uint32_t*)((uint8_t*)b.eval_count + d);
+                }
+            }
+            else if (s->zerocopy && L->g.hdev)
             {
                 // the kernel reads the descriptors and source blocks from the pinned staging and writes its
                 // outputs there (no copies): the batch addresses are the host staging's
@@ -651,7 +664,7 @@ void launcher_main(x265amd_mes* s, x265amd_mes_launcher* L)
                     }
             }
             // one upload of every size's inputs (the output regions ride along: staging is contiguous)
-            if (!rc && !(s->zerocopy && L->g.hdev))
+            if (!rc && !(s->zerocopy == 1 && L->g.hdev))
                 rc = (int)hipMemcpyAsync(L->g.dev, L->g.host, total, hipMemcpyHostToDevice, L->st);
             if (!rc) rc = (int)hipEventRecord(L->k0, L->st);
             if (!rc) rc = x265amd_motion_search(s->cfg.depth, (int)bt.size(), bt.data(), L->st);
@@ -789,7 +802,7 @@ int start_service(x265amd_mes* s)
     if (const char* e = getenv("X265AMD_MES_IDLE_US")) s->idle_us = atoi(e);
     if (const char* e = getenv("X265AMD_MES_SYNC_UPLOAD")) s->sync_upload = atoi(e) != 0;
     if (const char* e = getenv("X265AMD_MES_TRACE")) s->trace = atoi(e);
-    if (const char* e = getenv("X265AMD_MES_ZEROCOPY")) s->zerocopy = atoi(e) != 0;
+    if (const char* e = getenv("X265AMD_MES_ZEROCOPY")) s->zerocopy = atoi(e);
     if (const char* e = getenv("X265AMD_MES_PRIORITY")) s->prio = atoi(e) != 0;
     if (const char* e = getenv("X265AMD_MES_LSPIN")) s->lspin = atoi(e) != 0;
     if (const char* e = getenv("X265AMD_MES_LUPLOAD")) s->lupload = atoi(e) != 0;
