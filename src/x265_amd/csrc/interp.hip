@@ -875,7 +875,7 @@ static int uh_override(int op)
 
 // kernel class of a batch: unit width x unit height, packed as uw * 32 + uh
 template <int OP, int TAPS>
-static int interp_class(int w, int h, int rowext, bool pk8)
+static int interp_class(int w, int h, int rowext, bool pk8, bool u8 = false)
 {
     if (w < 2 || h < 2 || w > 64 || h > 64) return -X265AMD_EINVAL;
     const int ov = uh_override(OP);
@@ -895,6 +895,12 @@ static int interp_class(int w, int h, int rowext, bool pk8)
     // 16x16 36.5% -> 37.7%; 8-row units were worse on 8x8 and 16x16)
     // (the packed 8-bit vpp / vps path only: its accumulators are half-size)
     int uh = (pk8 && rows % 16 == 0 && w % 4 == 0) ? 16 : rows % 4 ? 1 : 4;
+    // 8-bit luma, measured on the roofline shapes (profiles/r05/ai/interp_uh_sweep.txt): 64-wide hpp on
+    // single-row units (0.52 -> 0.58 of HBM peak at 64x64), 8x8 vpp on one 8-row unit (0.59 -> 0.62)
+    if constexpr (OP == X265AMD_HPP && TAPS == 8)
+        if (u8 && w == 64) uh = 1;
+    if constexpr (OP == X265AMD_VPP && TAPS == 8)
+        if (u8 && w == 8 && h == 8) uh = 8;
     if (ov && rows % ov == 0 && (ov != 16 || (pk8 && w % 4 == 0)) && (ov == 1 || ov == 2 || ov == 4 || ov == 8 || ov == 16))
         uh = ov;
     if (w % 8 == 0) return 8 * 32 + uh;
@@ -1014,7 +1020,7 @@ static int grouped_interp(int depth, int count, const x265amd_interp_batch* bt, 
         if (bt[i].n == 0) continue;
         if (OP == X265AMD_HVPP && !bt[i].coeff) return X265AMD_EINVAL;
         cls[i] = interp_class<OP, TAPS>(bt[i].w, bt[i].h, bt[i].is_row_ext,
-                                        sizeof(S) == 1 && (OP == X265AMD_VPP || OP == X265AMD_VPS));
+                                        sizeof(S) == 1 && (OP == X265AMD_VPP || OP == X265AMD_VPS), sizeof(S) == 1);
         if (cls[i] < 0) return -cls[i];
         // hv_pp streams its rows through registers on 8-wide strips at 8 bit (4-wide for 4-wide blocks
         // and for 16-bit pixels, whose int32 window doubles the registers;
