@@ -10,7 +10,8 @@ CUs posted to the device at CU start and batched over all worker threads by the 
 csrc/mesession.cpp), on the rank's share of the host cores (16 per GPU, `--pools 16`).  Every step's
 bitstream must equal the plain reference encoder's on the same clip (checked on every rank).
 
-`value` = frames encoded by all ranks / the slowest rank's wall time of the K timed steps.  At N > 1
+`value` = frames encoded by all ranks / the slowest rank's wall time of the K timed steps, or null (and
+exit status 1) when any warmup or timed encode's bitstream differs from the reference's.  At N > 1
 each rank encodes its own closed 64-frame segment of the sequence (frames 64 r .. 64 r + 63) on its own
 GPU and host-core slice: GOP-level frame parallelism with no data-path collective (independent closed
 segments exchange nothing), weak scaling.  The frame-level shard inside one encoder (frame encoder i on
@@ -24,6 +25,8 @@ Also reported (rank 0):
                   the 8 TB/s HBM peak;
   cpu_baseline  — the plain reference encoder (oracle/_ref/x265ref8, C primitives) on the same clip and
                   the same cores (N = 1), and on one core (2 frames);
+  resolutions   — BASELINE names 1080p and 2160p: the same measurement at 1920x1080 (64 frames, its own
+                  reference encode and bitstream check) after the headline 2160p arm;
   encoder       — per-run fps (x265's own clock), the device-path worker time (forming / posting /
                   waiting), launch-service counters;
   primitive_workload — the round 1-4 census replay (src/x265_amd/replay_bench.py) at 1080p with its
@@ -67,6 +70,11 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true", help="skip the reference encoder's one-core sample")
     ap.add_argument("--no-replay", action="store_true", help="skip the primitive-workload replay (N = 1)")
     ap.add_argument("--env", action="append", default=[], help="extra KEY=VALUE for the hooked encoder")
+    ap.add_argument("--second-res", type=int, nargs=2, default=[1920, 1080], metavar=("W", "H"),
+                    help="BASELINE's other resolution, timed after the headline one (reported under "
+                         "`resolutions`; --second-res 0 0 skips it)")
+    ap.add_argument("--host-rehearsal", action="store_true",
+                    help="tests only: the hooks' host forms, no GPU (rank plumbing), value null")
     return ap.parse_args()
 
 
@@ -238,6 +246,52 @@ def me_roofline(st, traffic_file=ME_TRAFFIC):
                      "latency-bound: one workgroup of up to four waves per search, ~7 searches per launch); " + tbasis}
 
 
+def run_arm(args, world, rank, la, ref, W, H, F, D, cpus, extra, env, ref_env, steps, warmup, tag):
+    """one resolution: this rank's segment clip, the plain reference's bitstream (and fps) on it, `warmup`
+    untimed and `steps` timed hooked encodes (bracketed by barriers; the elapsed time is the max over
+    ranks), every bitstream compared with the reference's"""
+    with tempfile.TemporaryDirectory(prefix=f"bench{rank}_{tag}_") as td:
+        src = os.path.join(td, "clip.yuv")
+        progress(f"rank {rank} [{tag}]: writing frames {F * rank}..{F * rank + F - 1} ({W}x{H} {D}-bit)")
+        write_clip(src, W, H, D, F * rank, F)
+        # the reference bitstream of this rank's segment (and, at N = 1, the cpu_baseline): the plain
+        # reference encoder on the same clip and cores (Main10: the same binary with the hooks off)
+        progress(f"rank {rank} [{tag}]: reference encode")
+        if D == 8:
+            ref_fps, ref_wall, ref_md5, _ = x265_run(ref, src, W, H, D, F, extra, env=ref_env, cpus=cpus)
+        else:
+            ref_fps, ref_wall, ref_md5, _ = x265_run(la, src, W, H, D, F, extra, env=ref_env, cpus=cpus)
+        progress(f"rank {rank} [{tag}]: reference {ref_fps} fps")
+        mismatches = 0
+        for i in range(warmup):
+            f, _, m, _ = x265_run(la, src, W, H, D, F, extra, env=env, cpus=cpus)
+            mismatches += m != ref_md5
+            progress(f"rank {rank} [{tag}]: warmup {i}: {f} fps")
+        barrier(world)
+        runs, walls, err = [], [], ""
+        t0 = time.perf_counter()
+        for i in range(steps):
+            f, wall, m, err = x265_run(la, src, W, H, D, F, extra, env=env, cpus=cpus)
+            mismatches += m != ref_md5
+            runs.append(f)
+            walls.append(wall)
+            progress(f"rank {rank} [{tag}]: step {i}: {f} fps (wall {wall:.2f} s){'' if m == ref_md5 else ' BITSTREAM DIFFERS'}")
+        elapsed = time.perf_counter() - t0
+        barrier(world)
+        elapsed = max_over_ranks(elapsed, world)
+        identical = all_true(mismatches == 0, world)
+        one_core = None
+        if rank == 0 and world == 1 and not args.no_cpu and D == 8 and tag == "2160p" and not args.host_rehearsal:
+            n1 = 2
+            f1, _, _, _ = x265_run(ref, src, W, H, D, n1, ["--preset", args.preset, "--pools", "1", "-F", "1"],
+                                   cpus=cpus[:1])
+            one_core = {"fps": f1, "frames": n1}
+    fps = world * F * steps / elapsed
+    return {"fps": fps, "elapsed": elapsed, "identical": identical, "mismatching_encodes_this_rank": mismatches,
+            "runs": runs, "walls": walls, "err": err, "ref_fps": ref_fps, "ref_wall": ref_wall, "one_core": one_core,
+            "W": W, "H": H, "F": F, "steps": steps}
+
+
 def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -248,77 +302,78 @@ def main():
     ref = os.path.join(ROOT, "oracle", "_ref", "x265ref8")
     if not os.path.exists(la):
         raise SystemExit(f"{la} missing (build with __graft_entry__.build())")
-    import torch
+    if not args.host_rehearsal:
+        import torch
 
-    if not torch.cuda.is_available():
-        raise SystemExit("bench.py needs the MI355X (no CPU fallback)")
+        if not torch.cuda.is_available():
+            raise SystemExit("bench.py needs the MI355X (no CPU fallback)")
     cpus = core_slice(local, world)
     pools = str(len(cpus))
     extra = ["--preset", args.preset, "--pools", pools]
     env = dict(os.environ, HIP_VISIBLE_DEVICES=str(local), X265AMD_ME_STATS="1")
+    if args.host_rehearsal:
+        # the hooks' host forms (integration/: the same forming, posting and memo, the searches and estimates
+        # by the reference's own functions): the rank plumbing on a machine without the GPU, NOT a measurement
+        env.update(X265AMD_ME="host", X265AMD_LOOKAHEAD="host")
     env.update(kv.split("=", 1) for kv in args.env)
     ref_env = dict(os.environ, X265AMD_LOOKAHEAD="cpu", X265AMD_ME="cpu")
 
-    with tempfile.TemporaryDirectory(prefix=f"bench{rank}_") as td:
-        src = os.path.join(td, "clip.yuv")
-        progress(f"rank {rank}: writing frames {F * rank}..{F * rank + F - 1} ({W}x{H} {D}-bit)")
-        write_clip(src, W, H, D, F * rank, F)
-        # the reference bitstream of this rank's segment (and, at N = 1, the cpu_baseline): the plain
-        # reference encoder on the same clip and cores (Main10: the same binary with the hooks off)
-        progress(f"rank {rank}: reference encode")
-        if D == 8:
-            ref_fps, ref_wall, ref_md5, _ = x265_run(ref, src, W, H, D, F, extra, cpus=cpus)
-        else:
-            ref_fps, ref_wall, ref_md5, _ = x265_run(la, src, W, H, D, F, extra, env=ref_env, cpus=cpus)
-        progress(f"rank {rank}: reference {ref_fps} fps")
-        identical = True
-        for i in range(args.warmup):
-            f, _, m, _ = x265_run(la, src, W, H, D, F, extra, env=env, cpus=cpus)
-            identical &= m == ref_md5
-            progress(f"rank {rank}: warmup {i}: {f} fps")
-        barrier(world)
-        runs, walls, err = [], [], ""
-        t0 = time.perf_counter()
-        for i in range(args.steps):
-            f, wall, m, err = x265_run(la, src, W, H, D, F, extra, env=env, cpus=cpus)
-            identical &= m == ref_md5
-            runs.append(f)
-            walls.append(wall)
-            progress(f"rank {rank}: step {i}: {f} fps (wall {wall:.2f} s)")
-        elapsed = time.perf_counter() - t0
-        barrier(world)
-        elapsed = max_over_ranks(elapsed, world)
-        identical = all_true(identical, world)
-        one_core = None
-        if rank == 0 and world == 1 and not args.no_cpu and D == 8:
-            n1 = 2
-            f1, _, _, _ = x265_run(ref, src, W, H, D, n1, ["--preset", args.preset, "--pools", "1", "-F", "1"],
-                                   cpus=cpus[:1])
-            one_core = {"fps": f1, "frames": n1}
-        replay = None
-        if rank == 0 and world == 1 and not args.no_replay:
-            progress("primitive-workload replay (1080p census)")
-            try:
-                from src.x265_amd.replay_bench import primitive_workload
+    head = run_arm(args, world, rank, la, ref, W, H, F, D, cpus, extra, env, ref_env, args.steps, args.warmup,
+                   f"{H}p")
+    second = None
+    if args.second_res[0] > 0 and (args.second_res[0], args.second_res[1]) != (W, H):
+        w2, h2 = args.second_res
+        second = run_arm(args, world, rank, la, ref, w2, h2, F, D, cpus, extra, env, ref_env, args.steps, 1,
+                         f"{h2}p")
+    replay = None
+    if rank == 0 and world == 1 and not args.no_replay and not args.host_rehearsal:
+        progress("primitive-workload replay (1080p census)")
+        try:
+            from src.x265_amd.replay_bench import primitive_workload
 
-                replay = primitive_workload(local=local)
-            except Exception as e:   # informational: never fails the bench line
-                replay = {"error": str(e)}
+            replay = primitive_workload(local=local)
+        except Exception as e:   # informational: never fails the bench line
+            replay = {"error": str(e)}
 
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.barrier()
     if rank != 0:
         if world > 1:
-            import torch.distributed as dist
-
             dist.destroy_process_group()
         return
-    fps = world * F * args.steps / elapsed
-    st = parse_me_stats(err)
-    ms_per_step = elapsed * 1000.0 / args.steps
+    identical = head["identical"] and (second is None or second["identical"])
+    st = parse_me_stats(head["err"])
+    ms_per_step = head["elapsed"] * 1000.0 / args.steps
+
+    def arm_summary(a):
+        sm = {"fps": round(a["fps"], 3), "mpix_per_s": round(a["fps"] * a["W"] * a["H"] / 1e6, 1),
+              "resolution": f"{a['W']}x{a['H']}", "frames_per_step_per_gpu": a["F"], "steps": a["steps"],
+              "timed_region_s": round(a["elapsed"], 3), "bitstreams_identical_to_reference": a["identical"],
+              "fps_runs": a["runs"], "wall_s_runs": [round(w, 3) for w in a["walls"]],
+              "speedup_vs_reference_same_cores": round(statistics.median(a["runs"]) / a["ref_fps"], 3),
+              "device_path": parse_me_stats(a["err"])}
+        if world == 1:
+            sm["cpu_baseline"] = {"value": a["ref_fps"], "unit": "fps", "cores": len(cpus), "kind": "reference",
+                                  "wall_s": round(a["ref_wall"], 3),
+                                  "mpix_per_s": round(a["ref_fps"] * a["W"] * a["H"] / 1e6, 2)}
+        if not a["identical"]:
+            sm["fps"] = sm["mpix_per_s"] = None
+        return sm
+
+    res = {f"{head['H']}p": arm_summary(head)}
+    if second is not None:
+        res[f"{second['H']}p"] = arm_summary(second)
+    what = (f"x265 1.9 --preset {args.preset}, {H}p {D}-bit, {F}-frame synthetic clip per GPU, reference encoder with "
+            "its lookahead estimates and motion searches on the MI355X")
     line = {
-        "metric": f"encoded fps (x265 1.9 --preset {args.preset}, {H}p {D}-bit, {F}-frame synthetic clip per GPU, "
-                  "reference encoder with its lookahead estimates and 64x64 motion searches on the MI355X, "
-                  "bitstream identical to the reference) + Mpixels/s",
-        "value": round(fps, 3),
+        # a bitstream that differs from the reference's on any rank voids the number: value null, exit 1
+        "metric": f"encoded fps ({what}, " + ("bitstream identical to the reference" if identical else
+                                             "BITSTREAM DIFFERS FROM THE REFERENCE: not a valid measurement")
+                  + ") + Mpixels/s" + (" [HOST REHEARSAL: hooks in host mode, not a measurement]"
+                                       if args.host_rehearsal else ""),
+        "value": round(head["fps"], 3) if identical and not args.host_rehearsal else None,
         "unit": "fps",
         "n_gpus": world,
         "steps": args.steps,
@@ -333,22 +388,25 @@ def main():
                                f"--pools {pools} (default frame threads), oracle/_ref/{os.path.basename(la)}",
                    "resolution": f"{W}x{H}", "depth": D, "frames_per_step_per_gpu": F, "preset": args.preset,
                    "parallelism": f"GOP shard x{world}: rank r encodes the closed segment of frames {F}r..{F}r+{F - 1} "
-                                  "on its own GPU and host-core slice; no data-path collective",
+                                  "on its own GPU and host-core slice; no data-path collective (DESIGN.md §6)",
                    "host_cores_per_gpu": len(cpus), "cpu_model": cpu_model(),
                    "hooked_env": {k: v for k, v in env.items() if k.startswith("X265AMD")}},
-        "mpix_per_s": round(fps * W * H / 1e6, 1),
-        "timed_region_s": round(elapsed, 3),
+        "mpix_per_s": round(head["fps"] * W * H / 1e6, 1) if identical else None,
+        "timed_region_s": round(head["elapsed"], 3),
         "bitstreams_identical_to_reference": identical,
-        "encoder": {"fps_runs": runs, "fps_min": min(runs), "fps_median": statistics.median(runs), "fps_max": max(runs),
-                    "wall_s_runs": [round(w, 3) for w in walls], "device_path": st},
+        "resolutions": res,
+        "encoder": {"fps_runs": head["runs"], "fps_min": min(head["runs"]), "fps_median": statistics.median(head["runs"]),
+                    "fps_max": max(head["runs"]), "wall_s_runs": [round(w, 3) for w in head["walls"]],
+                    "device_path": st},
         "roofline": me_roofline(st),
-        "cpu_baseline": {"value": ref_fps, "unit": "fps", "cores": len(cpus), "kind": "reference",
+        "cpu_baseline": {"value": head["ref_fps"], "unit": "fps", "cores": len(cpus), "kind": "reference",
                          "sample": f"x265 1.9 CLI --preset {args.preset} (C primitives, oracle/_ref/"
                                    f"{'x265ref8' if D == 8 else 'x265la10 with its hooks off'}, built from the reference "
                                    f"sources; no asm) encoding the same {F}-frame clip on the same {len(cpus)} cores "
-                                   "(--pools), one run", "wall_s": round(ref_wall, 3),
-                         "mpix_per_s": round(ref_fps * W * H / 1e6, 2), "one_core": one_core} if world == 1 else None,
-        "speedup_vs_reference_same_cores": round(statistics.median(runs) / ref_fps, 3),
+                                   "(--pools), one run", "wall_s": round(head["ref_wall"], 3),
+                         "mpix_per_s": round(head["ref_fps"] * W * H / 1e6, 2),
+                         "one_core": head["one_core"]} if world == 1 else None,
+        "speedup_vs_reference_same_cores": round(statistics.median(head["runs"]) / head["ref_fps"], 3),
         "primitive_workload": replay,
     }
     print(json.dumps(line), flush=True)
@@ -356,6 +414,8 @@ def main():
         import torch.distributed as dist
 
         dist.destroy_process_group()
+    if not identical:
+        raise SystemExit("bench.py: a hooked encode's bitstream differs from the reference's")
 
 
 if __name__ == "__main__":

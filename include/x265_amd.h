@@ -506,7 +506,10 @@ typedef struct
 int  x265amd_la_create(const x265amd_la_config* cfg, x265amd_la** out);
 void x265amd_la_destroy(x265amd_la* la);
 /* (re)load picture `key` (generation gen = Lowres::frameNum): its 4 planes and, with AQ, its
- * invQscaleFactor (ncu int32; NULL without AQ) */
+ * invQscaleFactor (ncu int32; NULL without AQ).  The session page-locks `buffer` (hipHostRegister)
+ * until the key is reloaded from another buffer or the session is destroyed: the buffer must stay
+ * allocated until then (x265's Lowres buffers live as long as the encoder).  Memory freed while it is
+ * registered can be unmapped under the GPU's userptr mapping. */
 int x265amd_la_load(x265amd_la* la, const void* key, int gen, const void* buffer, const int32_t* inv_qscale);
 /* lowresIntraEstimate of a loaded picture: intraCost, intraMode, lowresCosts[0][0], rowSatds[0][0],
  * cost_est[0..1] = costEst[0][0] / costEstAq[0][0] */
@@ -870,6 +873,10 @@ typedef struct
     double batch_hist_ms[5];
 } x265amd_mes_counters;
 int x265amd_mes_stats(x265amd_mes* mes, x265amd_mes_counters* out);
+/* host buffers (Lowres / PicYuv planes page-locked by an f1 or f2 session) that were already freed or
+ * unmapped when their session unregistered them, over the process: must stay 0 (a freed registered range
+ * leaves the GPU a mapping of pages the process no longer owns).  No reference counterpart. */
+long long x265amd_host_unregister_stale(void);
 
 /* ------------------------------------------------------------------- f4
  * In-loop filters and border extension of device-resident 4:2:0 recon frames

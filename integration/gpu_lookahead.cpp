@@ -701,8 +701,9 @@ void CostEstimateGroup::finishBatch()
 
 } // namespace X265_NS
 
-/* called by the encoder binding after x265_encoder_close (oracle/hip_encoder_main.cpp): the closed encoder's
- * lookahead sessions are destroyed, so a later encoder in the same process — whose Lowres objects may sit at
+/* called by the encoder binding before x265_encoder_close frees the encoder's Lowres buffers (and again after
+ * it; oracle/hip_encoder_main.cpp): the closing encoder's lookahead sessions are drained, their page-locked
+ * buffers unregistered while still allocated, and destroyed, so a later encoder in the same process — whose Lowres objects may sit at
  * the same addresses with the same frame numbers — never finds the earlier encoder's planes resident */
 extern "C" void x265amd_la_encoder_closed(void)
 {

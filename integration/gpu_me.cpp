@@ -831,8 +831,9 @@ void Analysis::checkMerge2Nx2N_rd0_4(Mode& skip, Mode& merge, const CUGeom& cuGe
 
 } // namespace X265_NS
 
-/* called by the encoder binding after x265_encoder_close (oracle/hip_encoder_main.cpp): the sessions of
- * the closed encoder are destroyed (device arenas freed, pinned reconstruction buffers unregistered) and
+/* called by the encoder binding before x265_encoder_close frees the encoder's frames (and again after it;
+ * oracle/hip_encoder_main.cpp): the sessions of the closing encoder are destroyed (uploads drained, pinned
+ * reconstruction planes unregistered while still allocated, device arenas freed) and
  * the epoch advances, so a later encoder in the same process starts from empty sessions */
 extern "C" void x265amd_me_encoder_closed(void)
 {

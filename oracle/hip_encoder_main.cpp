@@ -44,19 +44,35 @@ extern "C" const x265_api* __real_x265_api_get_79(int bitDepth);
 /* x265la builds (integration/gpu_me.cpp, gpu_lookahead.cpp): drop the closed encoder's device sessions */
 extern "C" void x265amd_me_encoder_closed(void) __attribute__((weak));
 extern "C" void x265amd_la_encoder_closed(void) __attribute__((weak));
+extern "C" long long x265amd_host_unregister_stale(void) __attribute__((weak));
 
 namespace {
 x265_api g_api;
 int (*g_encode)(x265_encoder*, x265_nal**, uint32_t*, x265_picture*, x265_picture*);
 void (*g_close)(x265_encoder*);
 
-void closing(x265_encoder* enc)
+void drop_sessions()
 {
-    g_close(enc);
     if (x265amd_me_encoder_closed)
         x265amd_me_encoder_closed();
     if (x265amd_la_encoder_closed)
         x265amd_la_encoder_closed();
+}
+
+/* The device sessions page-lock the encoder's reconstruction planes (PicYuv) and Lowres buffers and may
+ * still have uploads from them in flight; x265_encoder_close (api.cpp:234-246) frees those buffers in
+ * Encoder::destroy.  So the sessions are drained, unregistered and destroyed BEFORE the encoder frees
+ * its frames: the CLI has flushed the encoder by then (x265.cpp: encoder_encode(NULL) until it returns 0),
+ * so no search or estimate is running.  A session opened during the close itself (none in a flushed
+ * encoder) is dropped after it. */
+void closing(x265_encoder* enc)
+{
+    drop_sessions();
+    g_close(enc);
+    drop_sessions();
+    if (x265amd_host_unregister_stale && x265amd_host_unregister_stale())
+        fprintf(stderr, "[x265hip] %lld page-locked host buffers were freed before their session unregistered them\n",
+                x265amd_host_unregister_stale());
 }
 
 int checked_encode(x265_encoder* enc, x265_nal** pp_nal, uint32_t* pi_nal, x265_picture* in, x265_picture* out)

@@ -1,8 +1,9 @@
 /* twice_main.cpp — TEST INFRASTRUCTURE (oracle/Makefile twice): two encoders of the SAME geometry opened
  * one after the other in ONE process through the public x265 API (x265.h: x265_encoder_open / _headers /
  * _encode / _close), each encoding the same raw 4:2:0 clip, with the MI355X hooks of integration/ linked
- * in.  After each x265_encoder_close the binding's teardown runs (x265amd_me_encoder_closed,
- * x265amd_la_encoder_closed — the calls INTEGRATION.md §3 adds to Encoder::destroy).  The second encoder
+ * in.  Before each x265_encoder_close frees the encoder's frames the binding's teardown runs
+ * (x265amd_me_encoder_closed, x265amd_la_encoder_closed — the calls INTEGRATION.md §3 adds to Encoder::destroy
+ * ahead of the frame teardown), so the page-locked planes are unregistered while still allocated.  The second encoder
  * reuses freed Frame / PicYuv / Lowres addresses and the same POCs, so a device session that kept the first
  * encoder's pictures would search stale reconstructions: tests/test_encoder_me.py checks that both
  * bitstreams equal those of the same program with the hooks off (X265AMD_LOOKAHEAD=cpu X265AMD_ME=cpu: the
@@ -23,6 +24,7 @@
 
 extern "C" void x265amd_me_encoder_closed(void) __attribute__((weak));
 extern "C" void x265amd_la_encoder_closed(void) __attribute__((weak));
+extern "C" long long x265amd_host_unregister_stale(void) __attribute__((weak));
 
 static void write_nals(FILE* f, const x265_nal* nal, uint32_t n)
 {
@@ -79,11 +81,14 @@ static int encode(const char* in, int w, int h, int frames, const char* out, con
         write_nals(fo, nal, nn);
     }
     api->picture_free(pic);
-    api->encoder_close(enc);
-    api->param_free(p);
-    /* the binding's teardown after the encoder is gone */
+    /* the binding's teardown while the flushed encoder's frames still exist */
     if (x265amd_me_encoder_closed) x265amd_me_encoder_closed();
     if (x265amd_la_encoder_closed) x265amd_la_encoder_closed();
+    api->encoder_close(enc);
+    api->param_free(p);
+    if (x265amd_host_unregister_stale && x265amd_host_unregister_stale())
+        fprintf(stderr, "[twice] %lld page-locked host buffers were freed before their session unregistered them\n",
+                x265amd_host_unregister_stale());
     fclose(fi);
     fclose(fo);
     return rc;

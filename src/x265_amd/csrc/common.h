@@ -174,8 +174,33 @@ inline int launch_grouped(int count, const int* cls, const BatchGroup& proto, Fi
 // A call carrying several independent batches spreads their launches over up to kForkStreams
 // internal streams: they wait on an event recorded on the caller's stream, and the caller's stream
 // waits on their completion events, so stream order (and hipGraph capture) is preserved.  Streams
-// and events are created once per host thread and device.
+// and events are created once per (host thread, device, origin priority) — with the origin stream's
+// priority, so a high-priority launcher's forked launches stay high-priority — and destroyed when
+// the thread exits (a session's launcher threads end at encoder close: nothing accumulates).
 constexpr int kForkStreams = 4;
+
+struct ForkCache
+{
+    hipStream_t s[kForkStreams] = {};
+    hipEvent_t f = nullptr, d[kForkStreams] = {};
+    int dev = -1;
+    bool ok = false;
+    ~ForkCache()
+    {
+        if (!ok) return;
+        int cur = 0;
+        if (hipGetDevice(&cur) != hipSuccess) return;
+        if (cur != dev && hipSetDevice(dev) != hipSuccess) return;
+        for (int i = 0; i < kForkStreams; i++)
+        {
+            (void)hipStreamSynchronize(s[i]);
+            (void)hipStreamDestroy(s[i]);
+            (void)hipEventDestroy(d[i]);
+        }
+        (void)hipEventDestroy(f);
+        if (cur != dev) (void)hipSetDevice(cur);
+    }
+};
 
 struct ForkJoin
 {
@@ -190,21 +215,22 @@ struct ForkJoin
         origin = st;
         if (want <= 1) return;                      // nothing to overlap: launch on the caller's stream
         n = want > kForkStreams ? kForkStreams : want;
-        int dev = 0;
+        int dev = 0, prio = 0;
         err = hipGetDevice(&dev);
-        struct Cache { hipStream_t s[kForkStreams]; hipEvent_t f, d[kForkStreams]; bool ok; };
-        static thread_local Cache cache[16] = {};
+        static thread_local ForkCache cache[16][2];
         if (err != hipSuccess || dev < 0 || dev >= 16) { n = 0; return; }
-        Cache& c = cache[dev];
+        if (origin && hipStreamGetPriority(origin, &prio) != hipSuccess) prio = 0;
+        ForkCache& c = cache[dev][prio != 0];
         if (!c.ok)
         {
             for (int i = 0; i < kForkStreams && err == hipSuccess; i++)
             {
-                err = hipStreamCreateWithFlags(&c.s[i], hipStreamNonBlocking);
+                err = hipStreamCreateWithPriority(&c.s[i], hipStreamNonBlocking, prio);
                 if (err == hipSuccess) err = hipEventCreateWithFlags(&c.d[i], hipEventDisableTiming);
             }
             if (err == hipSuccess) err = hipEventCreateWithFlags(&c.f, hipEventDisableTiming);
             if (err != hipSuccess) { n = 0; return; }
+            c.dev = dev;
             c.ok = true;
         }
         fork = c.f;

@@ -31,6 +31,7 @@
 #include <vector>
 
 #include "../../../include/x265_amd.h"
+#include "hostreg.h"
 
 namespace x265amd_provider {
 extern std::atomic<int> g_status;
@@ -253,7 +254,7 @@ extern "C" void x265amd_la_destroy(x265amd_la* la)
         delete t;
     }
     for (auto& f : la->frames)
-        if (f.second.pinned) (void)hipHostUnregister((void*)f.second.pinned);
+        x265amd_hostreg::unregister(f.second.pinned, la->frame_bytes);
     (void)hipFree(la->arena);
     (void)hipFree(la->intra);
     (void)hipFree(la->invq);
@@ -284,7 +285,7 @@ extern "C" int x265amd_la_load(x265amd_la* la, const void* key, int gen, const v
         // cannot be registered is copied pageable
         if (it->second.pinned != buffer)
         {
-            if (it->second.pinned) (void)hipHostUnregister((void*)it->second.pinned);
+            x265amd_hostreg::unregister(it->second.pinned, la->frame_bytes);
             it->second.pinned =
                 hipHostRegister((void*)buffer, la->frame_bytes, hipHostRegisterDefault) == hipSuccess ? buffer : nullptr;
             (void)hipGetLastError();

@@ -40,6 +40,7 @@
 #include <unordered_map>
 #include <vector>
 
+#include "hostreg.h"
 #include "../../../include/x265_amd.h"
 
 namespace x265amd_provider {
@@ -916,8 +917,9 @@ extern "C" void x265amd_mes_destroy(x265amd_mes* s)
             (void)hipEventSynchronize(p.second->up_ev);      // no copy from a pinned plane in flight
             (void)hipEventDestroy(p.second->up_ev);
         }
-        for (const void* pin : p.second->pinned)
-            if (pin) (void)hipHostUnregister((void*)pin);
+        for (int k = 0; k < 3; k++)
+            x265amd_hostreg::unregister(p.second->pinned[k],
+                                        (size_t)(k ? s->cfg.cplane_elems : s->cfg.plane_elems) * s->pix);
         delete p.second;
     }
     (void)hipFree(s->arena);
@@ -987,8 +989,8 @@ extern "C" int x265amd_mes_ref420(x265amd_mes* s, const void* key, int64_t gen, 
     for (int k = 0; k < np; k++)
         if (p->pinned[k] != planes[k])
         {
-            if (p->pinned[k]) (void)hipHostUnregister((void*)p->pinned[k]);
             const size_t bytes = (size_t)(k ? s->cfg.cplane_elems : s->cfg.plane_elems) * s->pix;
+            x265amd_hostreg::unregister(p->pinned[k], bytes);
             p->pinned[k] = hipHostRegister((void*)planes[k], bytes, hipHostRegisterDefault) == hipSuccess ? planes[k]
                                                                                                         : nullptr;
             (void)hipGetLastError();
@@ -1213,6 +1215,11 @@ extern "C" int x265amd_mes_drop(x265amd_mes* s, int ticket)
     std::lock_guard<std::mutex> g(s->smu);
     s->st.dropped++;
     return 0;
+}
+
+extern "C" long long x265amd_host_unregister_stale(void)
+{
+    return x265amd_hostreg::stale_count().load();
 }
 
 extern "C" int x265amd_mes_stats(x265amd_mes* s, x265amd_mes_counters* out)

@@ -255,6 +255,52 @@ class GpuFramePipeline:
         self.bg_streams = []
         self._bgroups, self._bg_events, self.bg = {}, {}, False
         self.graphs = {}
+        self._pool = None
+        self.comm = getattr(self, "comm", None)
+
+    # ---------------------------------------------------------------- teardown
+    def _drop_graphs(self):
+        """reset every captured graph after the device has drained (a graph's replay may still run on a
+        background stream); graphs go before the buffers they read, never in reference-cycle order"""
+        import torch
+
+        if self.graphs:
+            torch.cuda.synchronize()
+            for g in self.graphs.values():
+                g.reset()
+        self.graphs = {}
+        self._pool = None
+
+    def close(self):
+        """explicit teardown: drain every stream, reset the graphs (which releases their shared pool only
+        now that nothing can replay them), close the communicator, then drop the descriptor tables and
+        buffers the graphs pointed into.  The pipeline's lambdas reference the pipeline, so without this
+        it dies as a reference cycle, in whatever order and at whatever later moment the cyclic GC picks."""
+        import torch
+
+        if getattr(self, "_closed", False):
+            return
+        self._closed = True
+        if torch.cuda.is_available() and torch.cuda.is_initialized():
+            torch.cuda.synchronize()
+        self._drop_graphs()
+        if self.comm is not None:
+            self.comm.close()
+        for name in ("_sgroups", "_bgroups", "step_slices", "slices", "tu", "_bg_events"):
+            if hasattr(self, name):
+                setattr(self, name, {})
+        for name in ("batches", "_tu_keep", "dbk", "sao", "bor", "work", "final", "streams", "bg_streams"):
+            if hasattr(self, name):
+                setattr(self, name, [])
+        self.regions = self.frame_planes = self.ex = None
+        if torch.cuda.is_available() and torch.cuda.is_initialized():
+            torch.cuda.synchronize()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
 
     def final_planes(self, k, final=None):
         """where local frame k's final reconstruction lives: its store slot for a reference picture,
@@ -444,9 +490,13 @@ class GpuFramePipeline:
             for g in gs:
                 g.run(self.prims)       # build grouped descriptor tables outside any capture
         torch.cuda.synchronize()
-        self.graphs = {}
+        self._drop_graphs()
         if not graphs:
             return
+        # every graph of this pipeline allocates from one private pool: a tensor first allocated inside one
+        # capture and read by another graph (or a background replay) lives as long as the pool, which is
+        # released only after ALL the pipeline's graphs are reset (close())
+        self._pool = torch.cuda.graph_pool_handle()
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):                        # warm-up pass (allocations, descriptor uploads)
@@ -455,13 +505,13 @@ class GpuFramePipeline:
         torch.cuda.synchronize()
         if self.world == 1 and self.exchange_kind == "torch":
             g = torch.cuda.CUDAGraph()
-            with capture_graph(g):
+            with capture_graph(g, pool=self._pool):
                 self._run_all(exchange=True)                 # exchange = local copies: capturable
             self.graphs["all"] = g
         elif not self.bg:
             for st in range(s.nsteps):
                 g = torch.cuda.CUDAGraph()
-                with capture_graph(g):
+                with capture_graph(g, pool=self._pool):
                     self._step_work(st)
                 self.graphs[st] = g
         else:
@@ -475,7 +525,7 @@ class GpuFramePipeline:
                                        ("b", self._bg_graph_work, bool(self._bgroups.get(st)))):
                     if need:
                         g = torch.cuda.CUDAGraph()
-                        with capture_graph(g):
+                        with capture_graph(g, pool=self._pool):
                             fn(st)
                         self.graphs[(kind, st)] = g
             self._bg_main = torch.cuda.Stream()

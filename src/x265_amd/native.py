@@ -130,10 +130,12 @@ class capture_graph:
     stream is capturing: freeing a graph's private pool there calls hipFree inside
     the capture and aborts the process.  Collect first, then capture with GC off."""
 
-    def __init__(self, g):
+    def __init__(self, g, pool=None):
         import torch
 
-        self._ctx = torch.cuda.graph(g)
+        # pool: another graph's pool() (or torch.cuda.graph_pool_handle()), so graphs that hand tensors to
+        # each other allocate from ONE private pool and none of them can release memory another still reads
+        self._ctx = torch.cuda.graph(g, pool=pool)
 
     def __enter__(self):
         import gc

@@ -150,8 +150,8 @@ def pipeline_rates(prims, args, census, local, skip=()):
         out[f"band_rows_{br or pipe.plan.band_rows}" + (f"_segments_of_{seg}" if seg else "")] = {
             "fps": round(F / dt, 1), "ms_per_step": round(dt * 1e3, 3), "bands_per_frame": pipe.plan.nbands,
             "schedule_steps": pipe.sched.nsteps, "launches_per_step": pipe.launches_per_step}
+        pipe.close()
         del pipe
-        torch.cuda.synchronize()
     return out
 
 

@@ -62,6 +62,10 @@ def encode(exe, src, w, h, frames, out, env_extra=None, pools=8, depth=8, extra=
     if depth > 8:
         cmd += ["--output-depth", str(depth)]
     r = subprocess.run(cmd, capture_output=True, text=True, env=env, timeout=timeout)
+    # the device sessions must unregister the encoder's page-locked planes while they are still allocated
+    # (oracle/hip_encoder_main.cpp closing(); src/x265_amd/csrc/hostreg.h): the binding reports any that
+    # were already freed
+    assert "page-locked host buffers were freed" not in r.stderr, r.stderr[-1500:]
     m = re.search(r"encoded (\d+) frames in ([\d.]+)s \(([\d.]+) fps\)", r.stderr)
     md5 = hashlib.md5(open(out, "rb").read()).hexdigest() if r.returncode == 0 and os.path.exists(out) else None
     return r.returncode, md5, (float(m.group(3)) if m else None), r.stderr

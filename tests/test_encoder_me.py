@@ -80,6 +80,7 @@ def _twice(tmp_path, src, w, h, n, env, tag):
     r = subprocess.run([_bin("x265twice8"), str(src), str(w), str(h), str(n), str(outs[0]), str(outs[1])],
                        capture_output=True, text=True, timeout=600, env=dict(os.environ, **env))
     assert r.returncode == 0, r.stderr[-2000:]
+    assert "page-locked host buffers were freed" not in r.stderr, r.stderr[-1500:]
     return [o.read_bytes() for o in outs], r.stderr
 
 

@@ -51,8 +51,8 @@ def test_gpu_native_exchange_loopback():
     (1, 8, "torch", "band", False), (2, 6, "torch", "band", False), (None, 11, "torch", "band", False),
     (2, 8, "rccl", "band", False), (None, 11, "torch", "reference", False), (2, 8, "torch", "reference", False),
     (None, 11, "torch", "band", True), (2, 8, "rccl", "band", True)])
-def test_gpu_pipeline_gop_equals_whole_frame_chain(gpu_prims, oracle_libs, band_rows, frames, exchange, job_wait,
-                                                   background):
+def test_gpu_pipeline_gop_equals_whole_frame_chain(request, gpu_prims, oracle_libs, band_rows, frames, exchange,
+                                                   job_wait, background):
     """exchange "rccl": the rank's own reference pictures are finished in their own buffers and reach the
     store through the native communicator (loop-back transfers, x265amd_exchange); job_wait "reference":
     a job waits only for the reference picture it reads; background: reference-free jobs on background
@@ -66,6 +66,7 @@ def test_gpu_pipeline_gop_equals_whole_frame_chain(gpu_prims, oracle_libs, band_
     pipe = GpuFramePipeline(gpu_prims, W, H, 8, frames, 1, 0, band_rows=band_rows, streams=4, device="cuda",
                             exchange=exchange, inplace_store=exchange == "torch", job_wait=job_wait,
                             background=background)
+    request.addfinalizer(pipe.close)     # graphs reset after a device drain, before the buffers they read
     pipe.build(graphs=True)
     pipe.reset_stores()                  # the build's warm-up pass already filled them
     pipe.step()
@@ -135,7 +136,6 @@ def test_gpu_pipeline_gop_equals_whole_frame_chain(gpu_prims, oracle_libs, band_
     assert not bad, bad[:5]
     if exchange == "rccl":
         assert sum(len(t) for t in pipe.ex.tables) > 0
-        pipe.comm.close()
 
 
 @pytest.mark.parametrize("band_rows,frames,segment", [(1, 11, 11), (2, 16, 8)])

@@ -123,8 +123,10 @@ def test_la_session_destroy_create_reuse_threads():
     # a second geometry in the same process: a session of its own, its own results
     g2 = Geometry(20, 9, seed=6)
     la2 = _create(lib, g2)
-    r2 = _intra(lib, la2, g2, g2.picture(), keys[0])
+    pic2 = g2.picture()                   # x265amd_la_load page-locks it: it must outlive the session
+    r2 = _intra(lib, la2, g2, pic2, keys[0])
     assert r2[0].shape == (180,) and int(r2[4][0]) > 0
     lib.x265amd_la_destroy(la2)
     lib.x265amd_la_destroy(sessions[1])
+    del pic2, pics
     print(f"session addresses: {first:#x} -> {sessions[1].value:#x}")

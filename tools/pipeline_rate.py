@@ -67,8 +67,8 @@ def main():
             print(json.dumps({"mode": "pipeline", "frames": F, "band_rows": br, "segment_frames": seg or F, "job_wait": jw, "background": bgv, "exchange": ex, "streams": nst, "fps": round(F / dt, 1),
                               "ms_per_step": round(dt * 1e3, 3), "steps": pipe.sched.nsteps,
                               "launches": pipe.launches_per_step, "build_s": round(tb, 1)}), flush=True)
+            pipe.close()
             del pipe
-            torch.cuda.synchronize()
 
 
 if __name__ == "__main__":
