@@ -67,7 +67,11 @@ void drop_sessions()
  * encoder) is dropped after it. */
 void closing(x265_encoder* enc)
 {
-    drop_sessions();
+    /* X265AMD_ROUND5_CLOSE_ORDER=1: the round-5 order (sessions dropped only after the encoder freed its
+     * frames), kept so tests/test_encoder_me.py can show the stale-unregister count catches it */
+    const char* old = getenv("X265AMD_ROUND5_CLOSE_ORDER");
+    if (!(old && *old == '1'))
+        drop_sessions();
     g_close(enc);
     drop_sessions();
     if (x265amd_host_unregister_stale && x265amd_host_unregister_stale())

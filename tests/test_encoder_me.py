@@ -151,6 +151,32 @@ def test_gpu_me_encode_1080p_medium_is_bit_exact(tmp_path):
 
 
 @pytest.mark.gpu
+def test_gpu_sessions_unregister_planes_before_the_encoder_frees_them(tmp_path):
+    """ADVICE r5 / the round-5 GPU-fault audit: the device sessions page-lock the encoder's PicYuv and Lowres
+    planes; the binding must drop the sessions (uploads drained, planes unregistered) BEFORE
+    x265_encoder_close frees them.  The library counts every unregister of a range that is no longer mapped
+    (x265amd_host_unregister_stale, csrc/hostreg.h) and the binding prints it.  Default order: none (encode()
+    asserts it).  The round-5 order (sessions dropped after the close, X265AMD_ROUND5_CLOSE_ORDER=1): the
+    1080p planes are munmapped by then and the count is positive — the check catches the old code."""
+    import subprocess
+
+    w, h, n = 1920, 1080, 8
+    src = _source(tmp_path, w, h, n)
+    rc, ref, _, err = encode(_bin("x265ref8"), src, w, h, n, tmp_path / "ref.hevc")
+    assert rc == 0, err[-2000:]
+    rc, got, _, err = encode(_bin("x265la8"), src, w, h, n, tmp_path / "me.hevc", {"X265AMD_ME_STATS": "1"})
+    assert rc == 0 and got == ref, err[-2000:]
+    cmd = [_bin("x265la8"), "--input", str(src), "--input-res", f"{w}x{h}", "--input-depth", "8", "--fps", "30",
+           "--frames", str(n), "--preset", "medium", "-F", "2", "--pools", "8", "--no-info", "-o",
+           str(tmp_path / "old.hevc")]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600,
+                       env=dict(os.environ, X265AMD_ROUND5_CLOSE_ORDER="1"))
+    assert r.returncode == 0, r.stderr[-2000:]
+    m = re.search(r"(\d+) page-locked host buffers were freed before their session unregistered them", r.stderr)
+    assert m and int(m.group(1)) > 0, r.stderr[-2000:]
+
+
+@pytest.mark.gpu
 def test_gpu_me_encode_2160p_medium_is_bit_exact(tmp_path):
     """BASELINE's 4K configuration (3840x2160 8-bit --preset medium, 64 frames): device lookahead and
     device motion searches, bitstream identical to the reference encoder"""
