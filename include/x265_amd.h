@@ -873,6 +873,62 @@ typedef struct
     double batch_hist_ms[5];
 } x265amd_mes_counters;
 int x265amd_mes_stats(x265amd_mes* mes, x265amd_mes_counters* out);
+/* ------------------------------------------------------------------- f3 in the running encoder
+ * Inter residual coding session (round 6; csrc/rdosession.cpp, hook integration/gpu_rdo.cpp): the
+ * transform units of an inter CU as Search::encodeResAndCalcRdInterCU -> estimateResidualQT
+ * (search.cpp:2562-3140) evaluates them at --preset medium (one RQT level: luma TUs of min(CU, 32), chroma
+ * half that, 4:2:0; no RDOQ, transform skip, lossless, scaling lists or noise reduction).  A worker posts a
+ * CU (its fenc and pred planes and the Quant object's QPs) and waits; service threads run the posted CUs of
+ * all workers in one batch: per TU the fused f3 chain (x265amd_tu_pipeline: Quant::transformNxN ->
+ * invtransformNxN -> recon, quant.cpp:397-546), per 8x8 block of each plane psyCost_pp of fenc against pred
+ * and against the reconstruction (pixel.cpp:672-703; the reference's psyCost of any block made of 8x8
+ * blocks is the sum of these).  Thread-safe; the results of a ticket stay valid until it is released. */
+typedef struct x265amd_rdo x265amd_rdo;
+typedef struct
+{
+    int depth;                      /* 8, 10 or 12 */
+    int device;
+    int launchers;                  /* service threads, 1..8 */
+    int max_threads;                /* distinct posting host threads */
+    int sign_hide;                  /* pps.bSignHideEnabled */
+} x265amd_rdo_config;
+typedef struct
+{
+    int log2_cu;                    /* 4..6: 16x16 .. 64x64 (4:2:0: chroma planes half size) */
+    uint8_t qp[3];                  /* Quant::m_qpParam[ttype].qp (qp + QP_BD_OFFSET) of luma, Cb, Cr */
+    const void* fenc[3];
+    intptr_t fenc_stride[3];        /* elements */
+    const void* pred[3];
+    intptr_t pred_stride[3];
+} x265amd_rdo_cu;
+/* plane p (0 luma, 1 Cb, 2 Cr): TUs of tu_log2[p], ntu[p] of them in raster order over the plane;
+ * recon / resi planes are packed (stride = plane width) */
+typedef struct
+{
+    int log2_cu;
+    int tu_log2[3], ntu[3];
+    const void* recon[3];           /* pred + resi clipped (pred where a TU has no coefficient) */
+    const int16_t* resi[3];         /* invtransformNxN of the TU's coefficients (fenc - pred where none) */
+    const int16_t* coeff[3];        /* TU t's N x N coefficients at coeff[p] + t * N * N */
+    const uint32_t* num_sig[3];     /* transformNxN's return value per TU */
+    const int32_t* psy_pred[3];     /* per 8x8 block (raster): psyCost_pp 8x8 (fenc, pred) */
+    const int32_t* psy_rec[3];      /* per 8x8 block: psyCost_pp 8x8 (fenc, recon) */
+} x265amd_rdo_result;
+typedef struct
+{
+    int64_t batches, requests, tus, blocks, max_requests_per_batch;
+    double kernel_ms, batch_ms, queue_ms;
+    int64_t waits, waits_blocked;
+    double wait_ms;
+} x265amd_rdo_counters;
+int  x265amd_rdo_create(const x265amd_rdo_config* cfg, x265amd_rdo** out);
+void x265amd_rdo_destroy(x265amd_rdo* rdo);
+/* ENOMEM: no free request slot (the caller codes the CU on the host) */
+int  x265amd_rdo_post(x265amd_rdo* rdo, const x265amd_rdo_cu* cu, int* ticket);
+int  x265amd_rdo_wait(x265amd_rdo* rdo, int ticket, const x265amd_rdo_result** out);
+int  x265amd_rdo_release(x265amd_rdo* rdo, int ticket);
+int  x265amd_rdo_stats(x265amd_rdo* rdo, x265amd_rdo_counters* out);
+
 /* host buffers (Lowres / PicYuv planes page-locked by an f1 or f2 session) that were already freed or
  * unmapped when their session unregistered them, over the process: must stay 0 (a freed registered range
  * leaves the GPU a mapping of pages the process no longer owns).  No reference counterpart. */

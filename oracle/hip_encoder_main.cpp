@@ -45,6 +45,9 @@ extern "C" const x265_api* __real_x265_api_get_79(int bitDepth);
 extern "C" void x265amd_me_encoder_closed(void) __attribute__((weak));
 extern "C" void x265amd_la_encoder_closed(void) __attribute__((weak));
 extern "C" long long x265amd_host_unregister_stale(void) __attribute__((weak));
+/* x265la builds (integration/gpu_rdo.cpp): psy_cost_pp thunks into the table, the closed encoder's sessions */
+extern "C" void x265amd_rdo_install(void* table) __attribute__((weak));
+extern "C" void x265amd_rdo_encoder_closed(void) __attribute__((weak));
 
 namespace {
 x265_api g_api;
@@ -57,6 +60,8 @@ void drop_sessions()
         x265amd_me_encoder_closed();
     if (x265amd_la_encoder_closed)
         x265amd_la_encoder_closed();
+    if (x265amd_rdo_encoder_closed)
+        x265amd_rdo_encoder_closed();
 }
 
 /* The device sessions page-lock the encoder's reconstruction planes (PicYuv) and Lowres buffers and may
@@ -146,6 +151,8 @@ int main(int argc, char** argv)
         }
     }
     setupAliasPrimitives(p);
+    if (x265amd_rdo_install)
+        x265amd_rdo_install(&p);
     fprintf(stderr, "[x265hip] provider=%s entries=%d depth=%d\n", hip ? "hip" : "c", n, X265_DEPTH);
     return x265_cli_main(argc, argv);
 }

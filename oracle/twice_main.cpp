@@ -25,6 +25,7 @@
 extern "C" void x265amd_me_encoder_closed(void) __attribute__((weak));
 extern "C" void x265amd_la_encoder_closed(void) __attribute__((weak));
 extern "C" long long x265amd_host_unregister_stale(void) __attribute__((weak));
+extern "C" void x265amd_rdo_encoder_closed(void) __attribute__((weak));
 
 static void write_nals(FILE* f, const x265_nal* nal, uint32_t n)
 {
@@ -84,6 +85,7 @@ static int encode(const char* in, int w, int h, int frames, const char* out, con
     /* the binding's teardown while the flushed encoder's frames still exist */
     if (x265amd_me_encoder_closed) x265amd_me_encoder_closed();
     if (x265amd_la_encoder_closed) x265amd_la_encoder_closed();
+    if (x265amd_rdo_encoder_closed) x265amd_rdo_encoder_closed();
     api->encoder_close(enc);
     api->param_free(p);
     if (x265amd_host_unregister_stale && x265amd_host_unregister_stale())

@@ -22,7 +22,7 @@ MFMA_VGPR = ["-mllvm", "-amdgpu-mfma-vgpr-form"]
 # (source, object, extra flags): the EncoderPrimitives provider is built once per bit depth
 SOURCES = [("pixel.hip", "pixel.o", []), ("interp.hip", "interp.o", []), ("transform.hip", "transform.o", MFMA_VGPR),
            ("intra.hip", "intra.o", []), ("blockops.hip", "blockops.o", []), ("tu.hip", "tu.o", MFMA_VGPR), ("lowres.hip", "lowres.o", []), ("me.hip", "me.o", []), ("loopfilter.hip", "loopfilter.o", []),
-           ("runtime.hip", "runtime.o", []), ("lookahead.cpp", "lookahead.o", []), ("mesession.cpp", "mesession.o", []),
+           ("runtime.hip", "runtime.o", []), ("lookahead.cpp", "lookahead.o", []), ("mesession.cpp", "mesession.o", []), ("rdosession.cpp", "rdosession.o", []),
            ("schedule.cpp", "schedule.o", []), ("exchange.cpp", "exchange.o", []),
            ("provider.cpp", "provider8.o", ["-DX265_DEPTH=8"]),
            ("provider.cpp", "provider10.o", ["-DX265_DEPTH=10"])]

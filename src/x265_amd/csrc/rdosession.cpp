@@ -1,0 +1,665 @@
+// rdosession.cpp — f3 in the running encoder: the residual coding of inter CUs on the MI355X
+// (include/x265_amd.h, x265amd_rdo_*).
+//
+// Search::encodeResAndCalcRdInterCU (search.cpp:2562-2690) codes an inter CU's residual through
+// estimateResidualQT (search.cpp:2838-3140): for every transform unit of the CU — at --preset medium
+// one RQT level, TUs of min(CU, 32) luma and half that chroma — Quant::transformNxN (dct, quant,
+// sign-bit hiding), Quant::invtransformNxN (dequant, idct), the reconstruction pred + residual, and the
+// psy energies psyCost_pp(fenc, pred) / psyCost_pp(fenc, recon) (pixel.cpp:672-703) that its RD costs
+// use; the CABAC bit estimates (codeCoeffNxN) and the decisions stay on the host.  Given the CU's source
+// and prediction these results depend on nothing else, so a worker posts the CU (its fenc and pred
+// planes, the Quant object's QPs) and a service thread runs, for every CU posted at once, one upload,
+// the fused TU kernels (csrc/tu.hip: residual -> DCT -> quant -> SBH -> dequant -> iDCT -> recon) for
+// all luma and all chroma TUs, the per-8x8 psy energies of fenc against pred and against the coded
+// reconstruction (csrc/pixel.hip, X265AMD_PSY 8x8 jobs: psyCost_pp sums |E(src) - E(rec)| over 8x8
+// blocks, so a sum over any block of 8x8 blocks — a TU, the whole CU, a CU whose TUs are partly coded —
+// is a sum of these), and one download.  The encoder binding (integration/gpu_rdo.cpp) serves the
+// reference's own estimateResidualQT from these results, checking every input it can.
+//
+// Service and waiting follow csrc/mesession.cpp's launch service: per host thread a few request slots,
+// launcher threads take every queued request, waiters pause-spin, then yield, then sleep.
+#include <hip/hip_runtime.h>
+#include <sched.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#include <atomic>
+#include <condition_variable>
+#include <mutex>
+#include <new>
+#include <thread>
+#include <vector>
+
+#include "../../../include/x265_amd.h"
+
+namespace x265amd_provider {
+extern std::atomic<int> g_status;
+}
+
+namespace {
+
+int record(int st)
+{
+    if (st)
+    {
+        int zero = 0;
+        x265amd_provider::g_status.compare_exchange_strong(zero, st);
+    }
+    return st;
+}
+
+double now_s()
+{
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return ts.tv_sec + 1e-9 * ts.tv_nsec;
+}
+
+constexpr int kSlots = 4;            // outstanding requests per host thread
+
+// sizes of one CU's planes and TUs (4:2:0)
+struct Geo
+{
+    int c, cc;                       // luma / chroma plane width (= height)
+    int tl, tlc;                     // luma / chroma TU log2
+    int ntu, ntuc;                   // TUs per luma / chroma plane
+    int nb, nbc;                     // 8x8 blocks per luma / chroma plane
+    size_t pix_y, pix_c;             // pixels per luma / chroma plane
+    explicit Geo(int log2)
+    {
+        c = 1 << log2;
+        cc = c >> 1;
+        tl = log2 < 5 ? log2 : 5;
+        tlc = tl - 1;
+        ntu = (c >> tl) * (c >> tl);
+        ntuc = (cc >> tlc) * (cc >> tlc);
+        nb = (c >> 3) * (c >> 3);
+        nbc = (cc >> 3) * (cc >> 3);
+        pix_y = (size_t)c * c;
+        pix_c = (size_t)cc * cc;
+    }
+    size_t pix() const { return pix_y + 2 * pix_c; }
+    int tus() const { return ntu + 2 * ntuc; }
+    int blocks() const { return nb + 2 * nbc; }
+};
+
+} // namespace
+
+// one posted CU: its inputs (packed planes, stride = plane width) and, once done, its results
+struct x265amd_rdo_req
+{
+    x265amd_rdo_cu cu{};
+    uint8_t* in = nullptr;           // fenc Y Cb Cr, pred Y Cb Cr (2 * pix() * bytes per pixel)
+    uint8_t* out = nullptr;          // recon, resi, coeff, num_sig, psy_pred, psy_rec
+    x265amd_rdo_result res{};
+    std::atomic<int> state{ 0 };     // 0 free, 1 queued, 2 done
+    int rc = 0;
+    double t_post = 0;
+};
+
+struct x265amd_rdo_thread
+{
+    x265amd_rdo_req req[kSlots];
+};
+
+struct x265amd_rdo_launcher
+{
+    hipStream_t st = nullptr;
+    hipEvent_t done = nullptr, k0 = nullptr, k1 = nullptr;
+    uint8_t* dev = nullptr;
+    uint8_t* host = nullptr;
+    size_t cap = 0;
+    std::thread th;
+};
+
+struct x265amd_rdo
+{
+    x265amd_rdo_config cfg{};
+    uint64_t id = 0;
+    size_t pix = 1;
+    std::mutex mu;
+    std::vector<x265amd_rdo_thread*> threads;
+    std::vector<x265amd_rdo_launcher*> launchers;
+    std::mutex qmu;
+    std::condition_variable qcv;
+    std::vector<x265amd_rdo_req*> rq;
+    bool stop = false;
+    std::atomic<bool> stop_flag{ false };
+    std::atomic<int64_t> queued{ 0 };
+    std::atomic<int> qsleepers{ 0 };
+    std::mutex dmu;
+    std::condition_variable dcv;
+    int dsleepers = 0;
+    int spin_us = 50, yield_us = 5000, idle_us = 500;
+    std::mutex smu;
+    x265amd_rdo_counters st{};
+};
+
+namespace {
+
+struct TlsEntry { const x265amd_rdo* s; uint64_t id; x265amd_rdo_thread* t; };
+thread_local std::vector<TlsEntry> tls;
+std::atomic<uint64_t> g_next_id{ 1 };
+
+size_t out_bytes(const Geo& g, size_t pix)
+{
+    // recon (pixels), resi + coeff (int16 each), num_sig (uint32 per TU), psy_pred + psy_rec (int32 per block)
+    return g.pix() * pix + 2 * g.pix() * 2 + 4 * (size_t)g.tus() + 8 * (size_t)g.blocks();
+}
+
+void set_result(x265amd_rdo_req* r, size_t pix)
+{
+    const Geo g(r->cu.log2_cu);
+    x265amd_rdo_result& o = r->res;
+    o.log2_cu = r->cu.log2_cu;
+    uint8_t* p = r->out;
+    const size_t sz[3] = { g.pix_y, g.pix_c, g.pix_c };
+    for (int k = 0; k < 3; k++) { o.recon[k] = p; p += sz[k] * pix; }
+    for (int k = 0; k < 3; k++) { o.resi[k] = (const int16_t*)p; p += sz[k] * 2; }
+    for (int k = 0; k < 3; k++) { o.coeff[k] = (const int16_t*)p; p += sz[k] * 2; }
+    const int nt[3] = { g.ntu, g.ntuc, g.ntuc }, nb[3] = { g.nb, g.nbc, g.nbc };
+    for (int k = 0; k < 3; k++) { o.num_sig[k] = (const uint32_t*)p; p += 4 * (size_t)nt[k]; }
+    for (int k = 0; k < 3; k++) { o.psy_pred[k] = (const int32_t*)p; p += 4 * (size_t)nb[k]; }
+    for (int k = 0; k < 3; k++) { o.psy_rec[k] = (const int32_t*)p; p += 4 * (size_t)nb[k]; }
+    for (int k = 0; k < 3; k++)
+    {
+        o.tu_log2[k] = k ? g.tlc : g.tl;
+        o.ntu[k] = nt[k];
+    }
+}
+
+int thread_ctx(x265amd_rdo* s, x265amd_rdo_thread** out)
+{
+    for (size_t i = 0; i < tls.size();)
+    {
+        if (tls[i].s == s && tls[i].id == s->id) { *out = tls[i].t; return 0; }
+        if (tls[i].s == s) { tls[i] = tls.back(); tls.pop_back(); continue; }   // a destroyed session's entry
+        i++;
+    }
+    auto* t = new (std::nothrow) x265amd_rdo_thread();
+    if (!t) return X265AMD_ENOMEM;
+    const Geo g(6);                  // slots sized for the largest CU (64x64)
+    for (auto& r : t->req)
+    {
+        r.in = (uint8_t*)malloc(2 * g.pix() * s->pix);
+        r.out = (uint8_t*)malloc(out_bytes(g, s->pix));
+        if (!r.in || !r.out)
+        {
+            for (auto& q : t->req) { free(q.in); free(q.out); }
+            delete t;
+            return X265AMD_ENOMEM;
+        }
+    }
+    {
+        std::lock_guard<std::mutex> lk(s->mu);
+        if ((int)s->threads.size() >= s->cfg.max_threads)
+        {
+            for (auto& q : t->req) { free(q.in); free(q.out); }
+            delete t;
+            return X265AMD_ENOMEM;
+        }
+        s->threads.push_back(t);
+    }
+    tls.push_back({ s, s->id, t });
+    *out = t;
+    return 0;
+}
+
+int reserve(x265amd_rdo_launcher* L, size_t bytes)
+{
+    if (bytes <= L->cap) return 0;
+    (void)hipStreamSynchronize(L->st);
+    (void)hipFree(L->dev);
+    (void)hipHostFree(L->host);
+    L->dev = L->host = nullptr;
+    L->cap = 0;
+    bytes += bytes / 2;
+    if (hipMalloc((void**)&L->dev, bytes) != hipSuccess ||
+        hipHostMalloc((void**)&L->host, bytes, hipHostMallocDefault) != hipSuccess)
+        return X265AMD_ENOMEM;
+    L->cap = bytes;
+    return 0;
+}
+
+// Staging of one batch (device and pinned host alike, byte offsets):
+//   per request: [in: fenc Y Cb Cr, pred Y Cb Cr][out: recon, resi, coeff, num_sig, psy_pred, psy_rec]
+//   then the job descriptors: per TU fenc / pred / resi / coeff / recon offsets (int64) and qp (uint8), per
+//   8x8 block the fenc / pred / recon offsets (int64)
+// The inputs, offsets and (ride-along) outputs go up in one copy, the outputs come back in one copy per
+// request run (they are contiguous per request).
+struct Batch
+{
+    std::vector<x265amd_rdo_req*> reqs;
+    std::vector<size_t> rbase;       // request k's staging offset
+    size_t total = 0;
+};
+
+struct JobTables
+{
+    // per TU-pipeline batch (one per (CU size, luma / chroma))
+    std::vector<int64_t> fo, po, ro, co, xo;  // fenc, pred, resi, coeff, recon element offsets
+    std::vector<uint8_t> qp;
+    // per 8x8 psy batch (one per (CU size, luma / chroma)): a = fenc, b = pred or recon
+    std::vector<int64_t> pa, pb, pr;
+    std::vector<int64_t> sig, psyp, psyr;     // element offsets of the outputs (num_sig uint32, psy int32)
+};
+
+void launcher_main(x265amd_rdo* s, x265amd_rdo_launcher* L)
+{
+    (void)hipSetDevice(s->cfg.device);
+    std::vector<x265amd_rdo_req*> take;
+    for (;;)
+    {
+        {
+            std::unique_lock<std::mutex> lk(s->qmu);
+            while (s->rq.empty() && !s->stop)
+            {
+                const int64_t seen = s->queued.load(std::memory_order_acquire);
+                lk.unlock();
+                const double until = now_s() + 1e-6 * s->idle_us;
+                bool moved = false;
+                while (!(moved = s->queued.load(std::memory_order_acquire) != seen) &&
+                       !s->stop_flag.load(std::memory_order_acquire) && now_s() < until)
+                    sched_yield();
+                lk.lock();
+                if (!moved && s->rq.empty() && !s->stop)
+                {
+                    s->qsleepers.fetch_add(1, std::memory_order_acq_rel);
+                    s->qcv.wait(lk, [&] { return s->stop || !s->rq.empty(); });
+                    s->qsleepers.fetch_sub(1, std::memory_order_acq_rel);
+                }
+            }
+            if (s->rq.empty()) return;
+            take.swap(s->rq);
+            s->rq.clear();
+        }
+        const double t_take = now_s();
+        const size_t pix = s->pix;
+        // staging: requests, then the descriptor tables of every (CU size, plane class)
+        size_t total = 0;
+        std::vector<size_t> rbase(take.size());
+        for (size_t k = 0; k < take.size(); k++)
+        {
+            const Geo g(take[k]->cu.log2_cu);
+            rbase[k] = total;
+            total += (2 * g.pix() * pix + out_bytes(g, pix) + 255) & ~(size_t)255;
+        }
+        // jobs per CU size (log2 4..6) and class (0 luma, 1 chroma)
+        JobTables jt[3][2];
+        for (size_t k = 0; k < take.size(); k++)
+        {
+            const x265amd_rdo_cu& cu = take[k]->cu;
+            const Geo g(cu.log2_cu);
+            const int64_t R = (int64_t)(rbase[k] / pix);              // request base in pixel elements
+            const int64_t in_f[3] = { R, R + (int64_t)g.pix_y, R + (int64_t)(g.pix_y + g.pix_c) };
+            const int64_t in_p = (int64_t)g.pix();                    // pred planes follow fenc planes
+            const size_t ob = rbase[k] + 2 * g.pix() * pix;           // output base, bytes
+            const int64_t rec0 = (int64_t)(ob / pix);
+            const size_t resi_b = ob + g.pix() * pix, coeff_b = resi_b + 2 * g.pix();
+            const size_t sig_b = coeff_b + 2 * g.pix(), psyp_b = sig_b + 4 * (size_t)g.tus();
+            const size_t psyr_b = psyp_b + 4 * (size_t)g.blocks();
+            // the request's output offsets must be element aligned for every type
+            for (int p = 0; p < 3; p++)
+            {
+                const int cls = p > 0;
+                JobTables& J = jt[cu.log2_cu - 4][cls];
+                const int w = p ? g.cc : g.c, tl = p ? g.tlc : g.tl, n = 1 << tl;
+                const int64_t poff = p == 0 ? 0 : (p == 1 ? (int64_t)g.pix_y : (int64_t)(g.pix_y + g.pix_c));
+                const int ntu = p ? g.ntuc : g.ntu, nbl = p ? g.nbc : g.nb;
+                const int tu0 = p == 0 ? 0 : (p == 1 ? g.ntu : g.ntu + g.ntuc);
+                const int bl0 = p == 0 ? 0 : (p == 1 ? g.nb : g.nb + g.nbc);
+                for (int t = 0; t < ntu; t++)
+                {
+                    const int tx = (t % (w >> tl)) * n, ty = (t / (w >> tl)) * n;
+                    const int64_t o = (int64_t)ty * w + tx;
+                    J.fo.push_back(in_f[p] + o);
+                    J.po.push_back(in_f[p] + in_p + o);
+                    J.xo.push_back(rec0 + poff + o);
+                    J.ro.push_back((int64_t)(resi_b / 2) + poff + o);
+                    J.co.push_back((int64_t)(coeff_b / 2) + poff + (int64_t)t * n * n);
+                    J.sig.push_back((int64_t)(sig_b / 4) + tu0 + t);
+                    J.qp.push_back(cu.qp[p]);
+                }
+                for (int b = 0; b < nbl; b++)
+                {
+                    const int64_t o = (int64_t)(b / (w >> 3)) * 8 * w + (b % (w >> 3)) * 8;
+                    J.pa.push_back(in_f[p] + o);
+                    J.pb.push_back(in_f[p] + in_p + o);
+                    J.pr.push_back(rec0 + poff + o);
+                    J.psyp.push_back((int64_t)(psyp_b / 4) + bl0 + b);
+                    J.psyr.push_back((int64_t)(psyr_b / 4) + bl0 + b);
+                }
+            }
+        }
+        // descriptor tables after the requests
+        size_t tab_base = total;
+        for (auto& a : jt)
+            for (auto& J : a)
+            {
+                const size_t nt = J.fo.size(), nb = J.pa.size();
+                if (!nt) continue;
+                auto r256 = [](size_t b) { return (b + 255) & ~(size_t)255; };
+                // descriptors + qp, the num_sig scratch run, the two psy scratch runs (see the fill below)
+                total += r256(8 * 5 * nt + 8 * 3 * nb + nt) + r256(4 * nt) + 2 * r256(4 * nb);
+            }
+        int rc = reserve(L, total);
+        int njobs = 0, nblocks = 0;
+        std::vector<x265amd_tu_batch> tub;
+        std::vector<x265amd_cmp_batch> psy;
+        if (!rc)
+        {
+            uint8_t* H = L->host;
+            for (size_t k = 0; k < take.size(); k++)
+                memcpy(H + rbase[k], take[k]->in, 2 * Geo(take[k]->cu.log2_cu).pix() * pix);
+            size_t o = tab_base;
+            for (int z = 0; z < 3; z++)
+                for (int cls = 0; cls < 2; cls++)
+                {
+                    JobTables& J = jt[z][cls];
+                    const size_t nt = J.fo.size(), nb = J.pa.size();
+                    if (!nt) continue;
+                    auto put = [&](const std::vector<int64_t>& v) {
+                        memcpy(H + o, v.data(), 8 * v.size());
+                        const int64_t* d = (const int64_t*)(L->dev + o);
+                        o += 8 * v.size();
+                        return d;
+                    };
+                    const int64_t *fo = put(J.fo), *po = put(J.po), *ro = put(J.ro), *co = put(J.co), *xo = put(J.xo);
+                    const int64_t *pa = put(J.pa), *pb = put(J.pb), *pr = put(J.pr);
+                    memcpy(H + o, J.qp.data(), nt);
+                    const uint8_t* qp = L->dev + o;
+                    o = (o + nt + 255) & ~(size_t)255;
+                    const int w = (1 << (z + 4)) >> cls;              // plane width of this CU size and class
+                    const int tl = cls ? Geo(z + 4).tlc : Geo(z + 4).tl;
+                    // num_sig: the TUs of one (CU size, class) are not contiguous in the outputs, so the
+                    // kernel writes them into a scratch run (the descriptors' tail) and the host scatters
+                    x265amd_tu_batch b{};
+                    b.log2_size = tl;
+                    b.n = (int)nt;
+                    b.is_luma = !cls;
+                    b.is_intra = 0;
+                    b.i_slice = 0;
+                    b.sign_hide = s->cfg.sign_hide;
+                    b.fenc = L->dev;
+                    b.fenc_stride = w;
+                    b.fenc_off = fo;
+                    b.pred = L->dev;
+                    b.pred_stride = w;
+                    b.pred_off = po;
+                    b.resi = (int16_t*)L->dev;
+                    b.resi_stride = w;
+                    b.resi_off = ro;
+                    b.coeff = (int16_t*)L->dev;
+                    b.coeff_off = co;
+                    b.recon = L->dev;
+                    b.recon_stride = w;
+                    b.recon_off = xo;
+                    b.num_sig = (uint32_t*)(L->dev + o);
+                    b.qp = qp;
+                    b.scan = nullptr;
+                    o += (4 * nt + 255) & ~(size_t)255;
+                    tub.push_back(b);
+                    njobs += (int)nt;
+                    nblocks += (int)nb;
+                    psy.push_back({ 8, 8, (int)nb, L->dev, w, pa, L->dev, w, pb, nullptr });
+                    psy.push_back({ 8, 8, (int)nb, L->dev, w, pa, L->dev, w, pr, nullptr });
+                    // psy outputs likewise into scratch runs
+                    psy[psy.size() - 2].out = L->dev + o;
+                    o += (4 * nb + 255) & ~(size_t)255;
+                    psy.back().out = L->dev + o;
+                    o += (4 * nb + 255) & ~(size_t)255;
+                }
+            if (o > L->cap) rc = X265AMD_ENOMEM;                      // (the reserve above sized for this)
+            else total = o;
+        }
+        if (!rc) rc = (int)hipMemcpyAsync(L->dev, L->host, total, hipMemcpyHostToDevice, L->st);
+        if (!rc) rc = (int)hipEventRecord(L->k0, L->st);
+        if (!rc) rc = x265amd_tu_pipeline((int)s->cfg.depth, (int)tub.size(), tub.data(), L->st);
+        // the psy energies of fenc against the coded reconstruction need the TU kernels' recon: same stream
+        if (!rc) rc = x265amd_pixelcmp_grouped(X265AMD_PSY, (int)s->cfg.depth, (int)psy.size(), psy.data(), L->st);
+        if (!rc) rc = (int)hipEventRecord(L->k1, L->st);
+        if (!rc) rc = (int)hipMemcpyAsync(L->host, L->dev, total, hipMemcpyDeviceToHost, L->st);
+        if (!rc) rc = (int)hipEventRecord(L->done, L->st);
+        if (!rc) rc = (int)hipEventSynchronize(L->done);
+        float kms = 0;
+        if (!rc) (void)hipEventElapsedTime(&kms, L->k0, L->k1);
+        // publish: every request's outputs (recon, resi, coeff) are contiguous in its staging; num_sig and the
+        // psy energies are scattered back from the per-batch scratch runs
+        if (!rc)
+        {
+            for (size_t k = 0; k < take.size(); k++)
+            {
+                const Geo g(take[k]->cu.log2_cu);
+                memcpy(take[k]->out, L->host + rbase[k] + 2 * g.pix() * pix, out_bytes(g, pix));
+            }
+            size_t ti = 0, pi = 0;
+            for (int z = 0; z < 3; z++)
+                for (int cls = 0; cls < 2; cls++)
+                {
+                    JobTables& J = jt[z][cls];
+                    if (J.fo.empty()) continue;
+                    const uint32_t* sig = (const uint32_t*)(L->host + ((const uint8_t*)tub[ti].num_sig - L->dev));
+                    const int32_t* pp = (const int32_t*)(L->host + ((const uint8_t*)psy[pi].out - L->dev));
+                    const int32_t* pr = (const int32_t*)(L->host + ((const uint8_t*)psy[pi + 1].out - L->dev));
+                    ti++;
+                    pi += 2;
+                    // destination: element offsets into the staging, mapped to each request's output copy
+                    for (size_t j = 0; j < J.sig.size(); j++)
+                        *(uint32_t*)(L->host + 4 * J.sig[j]) = sig[j];
+                    for (size_t j = 0; j < J.psyp.size(); j++)
+                    {
+                        *(int32_t*)(L->host + 4 * J.psyp[j]) = pp[j];
+                        *(int32_t*)(L->host + 4 * J.psyr[j]) = pr[j];
+                    }
+                }
+            // the scattered scalars sit inside each request's staging output region: copy those again
+            for (size_t k = 0; k < take.size(); k++)
+            {
+                const Geo g(take[k]->cu.log2_cu);
+                const size_t ob = rbase[k] + 2 * g.pix() * pix, sc = g.pix() * pix + 4 * g.pix();
+                memcpy(take[k]->out + sc, L->host + ob + sc, out_bytes(g, pix) - sc);
+            }
+        }
+        const double t_done = now_s();
+        double qdelay = 0;
+        bool wake;
+        {
+            std::lock_guard<std::mutex> g(s->dmu);
+            for (auto* r : take)
+            {
+                qdelay += t_take - r->t_post;
+                r->rc = rc;
+                if (!rc) set_result(r, pix);
+                r->state.store(2, std::memory_order_release);
+            }
+            wake = s->dsleepers > 0;
+        }
+        if (wake) s->dcv.notify_all();
+        if (rc) record(rc);
+        {
+            std::lock_guard<std::mutex> g(s->smu);
+            s->st.batches++;
+            s->st.requests += (int64_t)take.size();
+            s->st.tus += njobs;
+            s->st.blocks += nblocks;
+            s->st.kernel_ms += kms;
+            s->st.batch_ms += 1e3 * (t_done - t_take);
+            s->st.queue_ms += 1e3 * qdelay;
+            if ((int64_t)take.size() > s->st.max_requests_per_batch) s->st.max_requests_per_batch = (int64_t)take.size();
+        }
+        take.clear();
+    }
+}
+
+int getenv_int(const char* name, int dflt)
+{
+    const char* e = getenv(name);
+    return e && *e ? atoi(e) : dflt;
+}
+
+} // namespace
+
+extern "C" int x265amd_rdo_create(const x265amd_rdo_config* cfg, x265amd_rdo** out)
+{
+    if (!cfg || !out) return X265AMD_EINVAL;
+    *out = nullptr;
+    if ((cfg->depth != 8 && cfg->depth != 10 && cfg->depth != 12) || cfg->launchers < 1 || cfg->launchers > 8 ||
+        cfg->max_threads <= 0)
+        return X265AMD_EINVAL;
+    auto* s = new (std::nothrow) x265amd_rdo();
+    if (!s) return record(X265AMD_ENOMEM);
+    s->cfg = *cfg;
+    s->id = g_next_id.fetch_add(1);
+    s->pix = cfg->depth > 8 ? 2 : 1;
+    s->spin_us = getenv_int("X265AMD_RDO_SPIN_US", 50);
+    s->yield_us = getenv_int("X265AMD_RDO_YIELD_US", 5000);
+    s->idle_us = getenv_int("X265AMD_RDO_IDLE_US", 500);
+    int cur = 0;
+    if (hipGetDevice(&cur) != hipSuccess || (cur != cfg->device && hipSetDevice(cfg->device) != hipSuccess))
+    {
+        delete s;
+        return record(X265AMD_ENODEV);
+    }
+    int lo = 0, hi = 0;
+    (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
+    for (int i = 0; i < cfg->launchers; i++)
+    {
+        auto* L = new (std::nothrow) x265amd_rdo_launcher();
+        if (!L || hipStreamCreateWithPriority(&L->st, hipStreamNonBlocking, hi) != hipSuccess ||
+            hipEventCreateWithFlags(&L->done, hipEventBlockingSync | hipEventDisableTiming) != hipSuccess ||
+            hipEventCreate(&L->k0) != hipSuccess || hipEventCreate(&L->k1) != hipSuccess)
+        {
+            delete L;
+            x265amd_rdo_destroy(s);
+            return record(X265AMD_ENOMEM);
+        }
+        s->launchers.push_back(L);
+    }
+    for (auto* L : s->launchers) L->th = std::thread(launcher_main, s, L);
+    if (cur != cfg->device) (void)hipSetDevice(cur);
+    *out = s;
+    return 0;
+}
+
+extern "C" void x265amd_rdo_destroy(x265amd_rdo* s)
+{
+    if (!s) return;
+    {
+        std::lock_guard<std::mutex> lk(s->qmu);
+        s->stop = true;
+        s->stop_flag.store(true);
+    }
+    s->qcv.notify_all();
+    for (auto* L : s->launchers)
+        if (L->th.joinable()) L->th.join();
+    for (auto* L : s->launchers)
+    {
+        if (L->st) (void)hipStreamSynchronize(L->st);
+        (void)hipFree(L->dev);
+        (void)hipHostFree(L->host);
+        if (L->st) (void)hipStreamDestroy(L->st);
+        if (L->done) (void)hipEventDestroy(L->done);
+        if (L->k0) (void)hipEventDestroy(L->k0);
+        if (L->k1) (void)hipEventDestroy(L->k1);
+        delete L;
+    }
+    for (auto* t : s->threads)
+    {
+        for (auto& r : t->req) { free(r.in); free(r.out); }
+        delete t;
+    }
+    delete s;
+}
+
+extern "C" int x265amd_rdo_post(x265amd_rdo* s, const x265amd_rdo_cu* cu, int* ticket)
+{
+    if (!s || !cu || !ticket || cu->log2_cu < 4 || cu->log2_cu > 6) return X265AMD_EINVAL;
+    for (int p = 0; p < 3; p++)
+        if (!cu->fenc[p] || !cu->pred[p]) return X265AMD_EINVAL;
+    x265amd_rdo_thread* t;
+    if (int rc = thread_ctx(s, &t)) return rc;
+    int k = 0;
+    while (k < kSlots && t->req[k].state.load(std::memory_order_acquire) != 0) k++;
+    if (k == kSlots) return X265AMD_ENOMEM;                       // caller codes the CU on the host
+    x265amd_rdo_req* r = &t->req[k];
+    r->cu = *cu;
+    const Geo g(cu->log2_cu);
+    // pack fenc and pred planes (stride = plane width): the caller's buffers may change once this returns
+    uint8_t* d = r->in;
+    for (int src = 0; src < 2; src++)
+        for (int p = 0; p < 3; p++)
+        {
+            const int w = p ? g.cc : g.c;
+            const uint8_t* a = (const uint8_t*)(src ? cu->pred[p] : cu->fenc[p]);
+            const intptr_t st = (src ? cu->pred_stride[p] : cu->fenc_stride[p]) * (intptr_t)s->pix;
+            for (int y = 0; y < w; y++, d += w * s->pix) memcpy(d, a + y * st, w * s->pix);
+        }
+    r->rc = 0;
+    r->t_post = now_s();
+    r->state.store(1, std::memory_order_release);
+    {
+        std::lock_guard<std::mutex> lk(s->qmu);
+        s->rq.push_back(r);
+    }
+    s->queued.fetch_add(1, std::memory_order_acq_rel);
+    if (s->qsleepers.load(std::memory_order_acquire) > 0) s->qcv.notify_one();
+    *ticket = k;
+    return 0;
+}
+
+extern "C" int x265amd_rdo_wait(x265amd_rdo* s, int ticket, const x265amd_rdo_result** out)
+{
+    if (!s || ticket < 0 || ticket >= kSlots || !out) return X265AMD_EINVAL;
+    x265amd_rdo_thread* t;
+    if (int rc = thread_ctx(s, &t)) return rc;
+    x265amd_rdo_req* r = &t->req[ticket];
+    if (r->state.load(std::memory_order_acquire) == 0) return X265AMD_EINVAL;
+    const double t0 = now_s();
+    bool slept = false;
+    if (r->state.load(std::memory_order_acquire) != 2)
+    {
+        const double spin_until = t0 + 1e-6 * s->spin_us, yield_until = t0 + 1e-6 * s->yield_us;
+        while (r->state.load(std::memory_order_acquire) != 2 && now_s() < spin_until) __builtin_ia32_pause();
+        while (r->state.load(std::memory_order_acquire) != 2 && now_s() < yield_until) sched_yield();
+        if (r->state.load(std::memory_order_acquire) != 2)
+        {
+            std::unique_lock<std::mutex> lk(s->dmu);
+            s->dsleepers++;
+            s->dcv.wait(lk, [&] { return r->state.load(std::memory_order_acquire) == 2; });
+            s->dsleepers--;
+            slept = true;
+        }
+    }
+    {
+        std::lock_guard<std::mutex> g(s->smu);
+        s->st.waits++;
+        s->st.waits_blocked += slept;
+        s->st.wait_ms += 1e3 * (now_s() - t0);
+    }
+    if (r->rc) return record(r->rc);
+    *out = &r->res;
+    return 0;
+}
+
+extern "C" int x265amd_rdo_release(x265amd_rdo* s, int ticket)
+{
+    if (!s || ticket < 0 || ticket >= kSlots) return X265AMD_EINVAL;
+    x265amd_rdo_thread* t;
+    if (int rc = thread_ctx(s, &t)) return rc;
+    x265amd_rdo_req* r = &t->req[ticket];
+    // a request still queued is left alone: its launcher completes it and it stays reserved until waited for
+    int done = 2;
+    if (!r->state.compare_exchange_strong(done, 0)) return X265AMD_EINVAL;
+    return 0;
+}
+
+extern "C" int x265amd_rdo_stats(x265amd_rdo* s, x265amd_rdo_counters* out)
+{
+    if (!s || !out) return X265AMD_EINVAL;
+    std::lock_guard<std::mutex> g(s->smu);
+    *out = s->st;
+    return 0;
+}

@@ -1,0 +1,74 @@
+"""Round 6: the inter residual coding of the running reference encoder on the device (integration/gpu_rdo.cpp over
+the x265amd_rdo_* session, csrc/rdosession.cpp).
+
+Search::encodeResAndCalcRdInterCU (search.cpp:2562) posts an eligible CU's source and prediction; the device runs
+the fused TU chain of every TU (csrc/tu.hip) and the per-8x8 psy energies (csrc/pixel.hip); the reference's own
+estimateResidualQT then runs with its Quant::transformNxN / invtransformNxN calls and the table's psy_cost_pp
+answered from those results wherever the call's inputs are the device's.
+
+CPU: X265AMD_RDO=host computes the same results with the reference's own functions and serves them through the
+same memo — every call must hit and the bitstream must be the reference's (checks the binding's plumbing).
+GPU: the bitstream equals the reference's, and in check mode every device answer equals the reference function's.
+"""
+import os
+import re
+
+import pytest
+
+from test_encoder_lookahead import _bin, _source, encode
+
+
+def _rdo_stats(err):
+    m = re.search(r"\[x265rdo\] stats CUs posted (\d+) coded on the host (\d+); transformNxN memo hits (\d+) misses "
+                  r"(\d+); invtransformNxN hits (\d+) misses (\d+); psy_cost_pp hits (\d+) misses (\d+)", err)
+    assert m, err[-3000:]
+    k = ("posts", "host", "tq_hit", "tq_miss", "itq_hit", "itq_miss", "psy_hit", "psy_miss")
+    return dict(zip(k, map(int, m.groups())))
+
+
+@pytest.mark.parametrize("min_log2", [6, 4])
+def test_rdo_hook_host_memo_equals_reference_on_cpu(tmp_path, min_log2):
+    w, h, n = 640, 360, 8
+    src = _source(tmp_path, w, h, n)
+    rc, ref, _, err = encode(_bin("x265ref8"), src, w, h, n, tmp_path / "ref.hevc")
+    assert rc == 0, err[-2000:]
+    rc, got, _, err = encode(_bin("x265la8"), src, w, h, n, tmp_path / "rdo.hevc",
+                             {"X265AMD_LOOKAHEAD": "cpu", "X265AMD_ME": "cpu", "X265AMD_RDO": "host",
+                              "X265AMD_RDO_MIN": str(min_log2), "X265AMD_ME_STATS": "1"})
+    assert rc == 0, err[-2000:]
+    st = _rdo_stats(err)
+    assert st["posts"] > 0 and st["tq_hit"] > 0 and st["itq_hit"] > 0 and st["psy_hit"] > 0, st
+    assert st["tq_miss"] == st["itq_miss"] == st["psy_miss"] == 0, st
+    assert got == ref, "X265AMD_RDO=host: bitstream differs from the reference encoder"
+
+
+def _gpu(tmp_path, w, h, n, env, min_log2=6):
+    src = _source(tmp_path, w, h, n)
+    rc, ref, _, err = encode(_bin("x265ref8"), src, w, h, n, tmp_path / "ref.hevc", pools=16)
+    assert rc == 0, err[-2000:]
+    e = {"X265AMD_RDO_MIN": str(min_log2), "X265AMD_ME_STATS": "1"}
+    e.update(env)
+    rc, got, _, err = encode(_bin("x265la8"), src, w, h, n, tmp_path / "rdo.hevc", e, pools=16)
+    assert rc == 0, err[-3000:]
+    assert got == ref, "device residual coding: bitstream differs from the reference encoder\n" + err[-2000:]
+    return err
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("min_log2", [6, 4])
+def test_gpu_rdo_encode_1080p_is_bit_exact(tmp_path, min_log2):
+    """device lookahead, device motion searches and device inter residual coding together, 1080p medium"""
+    err = _gpu(tmp_path, 1920, 1080, 16, {"X265AMD_RDO": "gpu"}, min_log2)
+    st = _rdo_stats(err)
+    assert st["posts"] > 0 and st["tq_hit"] > 0 and st["tq_miss"] == 0 and st["itq_miss"] == 0, st
+    assert st["psy_miss"] == 0, st
+
+
+@pytest.mark.gpu
+def test_gpu_rdo_check_mode_every_answer_matches(tmp_path):
+    """X265AMD_RDO=check: every coefficient block, numSig, inverse-transformed residual and psy energy the
+    device supplied is recomputed by the reference's function when it is used: 0 mismatches"""
+    err = _gpu(tmp_path, 1280, 720, 12, {"X265AMD_RDO": "check"}, 4)
+    m = re.search(r"\[x265rdo\] check: (\d+) mismatches", err)
+    assert m and int(m.group(1)) == 0, err[-3000:]
+    assert _rdo_stats(err)["tq_hit"] > 0
