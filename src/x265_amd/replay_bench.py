@@ -5,7 +5,7 @@ encoder makes per frame at that resolution and preset (exact per-entry census:
 tests/golden/census_<H>p_<preset>[_main10].json, oracle/run_census.py) as batched gfx950 launches
 through the C ABI (include/x265_amd.h).  `ReplayStep` gives its rate and its dominant launch (the
 grouped census SATD) with the PMC-calibrated roofline (profiles/pmc_traffic*.json); `pipeline_rates`
-the frame-parallel GOP-shard forms; `census_replay_cpu` the reference C primitives over
+the frame-parallel GOP-shard forms; tools/census_cpu.py (test infrastructure, round 6: moved out of the product package) the reference C primitives over
 the same descriptors on the host cores.
 """
 from __future__ import annotations
@@ -84,39 +84,6 @@ def pick_census(args):
     base = load_census()
     k = args.width * args.height / (1920 * 1080)
     return {key: v * k for key, v in base.items()}, f"census_1080p_medium.json x {k:.3f} (pixel ratio)"
-
-
-def census_replay_cpu(args, census):
-    """Reference C primitives over a bounded sample of the same census workload."""
-    import torch
-
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    from pyoracle import CpuPrims, available
-
-    from src.x265_amd.workload import FrameSet, WorkloadBuilder, census_batches
-
-    kind = "reference" if available("ref", args.depth) else "port"
-    threads = host_cores()
-    prims = CpuPrims("ref" if kind == "reference" else "oracle", args.depth, nthreads=threads)
-    frames = 2
-    fs = FrameSet(args.width, args.height, frames, args.depth, device="cpu")
-    # the census of `frames` frames, replayed until about args.cpu_seconds of CPU time have passed
-    bs, _ = census_batches(fs, frames=frames, census=census, builder=WorkloadBuilder(fs, seed=4))
-    torch.set_num_threads(1)
-    reps, t0 = 0, time.perf_counter()
-    while True:
-        for b in bs:
-            b.run(prims)
-        reps += 1
-        dt = time.perf_counter() - t0
-        if dt >= args.census_cpu_seconds:
-            break
-    fps = frames * reps / dt
-    return {"value": round(fps, 3), "unit": "fps", "cores": threads, "kind": kind,
-            "sample": f"{reps} x the census workload of {frames} {args.width}x{args.height} frames ({sum(b.n for b in bs)} calls per "
-                      f"pass, the same batch descriptors as the GPU path) in {dt:.1f}s on {threads} host threads "
-                      f"({'x265 1.9 C primitives, oracle/_ref' if kind == 'reference' else 'oracle restatement'})",
-            "mpix_per_s": round(fps * args.width * args.height / 1e6, 3)}
 
 
 def pipeline_rates(prims, args, census, local, skip=()):
