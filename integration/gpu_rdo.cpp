@@ -39,7 +39,8 @@
  *                       invtransformNxN / psyCost_pp (host_result) and served through the same memo: checks
  *                       the binding's plumbing on a CPU-only host (every call must hit, bitstream unchanged)
  *   X265AMD_RDO_MIN=k   smallest CU (log2, 4..6, default 6: 64x64) coded on the device
- *   X265AMD_RDO_LAUNCHERS=n  service threads per session (default 2)
+ *   X265AMD_RDO_LAUNCHERS=n  service threads per session (default 2; 0: each worker launches its CU itself,
+ *                       zero-copy, and polls a completion flag)
  *   X265AMD_ME_STATS=1  posts, memo hits / misses per function, worker wait time, session counters at exit
  */
 #include "common.h"
@@ -152,7 +153,7 @@ void init_once()
     const char* e = getenv("X265AMD_RDO_MIN");
     if (e && *e) g_min_log2 = atoi(e) < 4 ? 4 : (atoi(e) > 6 ? 6 : atoi(e));
     e = getenv("X265AMD_RDO_LAUNCHERS");
-    if (e && *e) g_launchers = atoi(e) < 1 ? 1 : atoi(e);
+    if (e && *e) g_launchers = atoi(e) < 0 ? 0 : atoi(e);     /* 0: direct mode (per-thread zero-copy launches) */
     e = getenv("X265AMD_GPUS");
     if (e && *e) g_gpus = atoi(e) < 1 ? 1 : atoi(e);
     const char* st = getenv("X265AMD_ME_STATS");

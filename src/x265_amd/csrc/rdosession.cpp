@@ -103,6 +103,13 @@ struct x265amd_rdo_req
 struct x265amd_rdo_thread
 {
     x265amd_rdo_req req[kSlots];
+    // direct mode (cfg.launchers == 0): the thread's own stream and one mapped, coherent pinned region per
+    // slot — inputs, descriptors and outputs — that the kernels read and write in place (no copies), and
+    // a completion flag the stream writes after the kernels (hipStreamWriteValue32) and the waiter polls
+    hipStream_t st = nullptr;
+    uint8_t* host = nullptr;
+    uint8_t* hdev = nullptr;
+    size_t region = 0;
 };
 
 struct x265amd_rdo_launcher
@@ -169,6 +176,40 @@ void set_result(x265amd_rdo_req* r, size_t pix)
         o.tu_log2[k] = k ? g.tlc : g.tl;
         o.ntu[k] = nt[k];
     }
+}
+
+void free_thread(x265amd_rdo_thread* t)
+{
+    for (auto& q : t->req) { free(q.in); if (!t->host) free(q.out); }    // direct mode: out is in the region
+    if (t->st) { (void)hipStreamSynchronize(t->st); (void)hipStreamDestroy(t->st); }
+    if (t->host) (void)hipHostFree(t->host);
+    delete t;
+}
+
+// direct mode: per slot [in 2 * pix()][out out_bytes][descriptors][flag], sized for a 64x64 CU
+size_t direct_region(size_t pix)
+{
+    const Geo g(6);
+    const size_t desc = 8 * (5 * (size_t)g.tus() + 3 * (size_t)g.blocks()) + (size_t)g.tus() + 64;
+    return (2 * g.pix() * pix + out_bytes(g, pix) + desc + 4095) & ~(size_t)4095;
+}
+
+int direct_setup(x265amd_rdo* s, x265amd_rdo_thread* t)
+{
+    if (t->host) return 0;
+    int lo = 0, hi = 0;
+    (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
+    t->region = direct_region(s->pix);
+    if (hipStreamCreateWithPriority(&t->st, hipStreamNonBlocking, hi) != hipSuccess ||
+        hipHostMalloc((void**)&t->host, t->region * kSlots, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+        hipHostGetDevicePointer((void**)&t->hdev, t->host, 0) != hipSuccess)
+        return X265AMD_ENOMEM;
+    for (int k = 0; k < kSlots; k++)
+    {
+        free(t->req[k].out);                                     // outputs live in the mapped region
+        t->req[k].out = nullptr;
+    }
+    return 0;
 }
 
 int thread_ctx(x265amd_rdo* s, x265amd_rdo_thread** out)
@@ -506,7 +547,7 @@ extern "C" int x265amd_rdo_create(const x265amd_rdo_config* cfg, x265amd_rdo** o
 {
     if (!cfg || !out) return X265AMD_EINVAL;
     *out = nullptr;
-    if ((cfg->depth != 8 && cfg->depth != 10 && cfg->depth != 12) || cfg->launchers < 1 || cfg->launchers > 8 ||
+    if ((cfg->depth != 8 && cfg->depth != 10 && cfg->depth != 12) || cfg->launchers < 0 || cfg->launchers > 8 ||
         cfg->max_threads <= 0)
         return X265AMD_EINVAL;
     auto* s = new (std::nothrow) x265amd_rdo();
@@ -566,13 +607,136 @@ extern "C" void x265amd_rdo_destroy(x265amd_rdo* s)
         if (L->k1) (void)hipEventDestroy(L->k1);
         delete L;
     }
-    for (auto* t : s->threads)
-    {
-        for (auto& r : t->req) { free(r.in); free(r.out); }
-        delete t;
-    }
+    for (auto* t : s->threads) free_thread(t);
     delete s;
 }
+
+namespace {
+
+// direct mode: stage the CU in the slot's mapped region and enqueue its kernels on the thread's stream
+int direct_post(x265amd_rdo* s, x265amd_rdo_thread* t, int k, const x265amd_rdo_cu* cu)
+{
+    x265amd_rdo_req* r = &t->req[k];
+    const size_t pix = s->pix;
+    const Geo g(cu->log2_cu);
+    uint8_t* H = t->host + (size_t)k * t->region;
+    uint8_t* D = t->hdev + (size_t)k * t->region;
+    // inputs: fenc Y Cb Cr then pred Y Cb Cr, packed
+    uint8_t* d = H;
+    for (int src = 0; src < 2; src++)
+        for (int p = 0; p < 3; p++)
+        {
+            const int w = p ? g.cc : g.c;
+            const uint8_t* a = (const uint8_t*)(src ? cu->pred[p] : cu->fenc[p]);
+            const intptr_t st = (src ? cu->pred_stride[p] : cu->fenc_stride[p]) * (intptr_t)pix;
+            for (int y = 0; y < w; y++, d += w * pix) memcpy(d, a + y * st, w * pix);
+        }
+    const size_t ob = 2 * g.pix() * pix;                      // outputs (the out_bytes layout, set_result)
+    const size_t resi_b = ob + g.pix() * pix, coeff_b = resi_b + 2 * g.pix();
+    const size_t sig_b = coeff_b + 2 * g.pix(), psyp_b = sig_b + 4 * (size_t)g.tus();
+    const size_t psyr_b = psyp_b + 4 * (size_t)g.blocks();
+    size_t o = (ob + out_bytes(g, pix) + 255) & ~(size_t)255;   // descriptors
+    r->out = H + ob;
+    volatile uint32_t* flag = (volatile uint32_t*)(H + t->region - 64);
+    *flag = 0;
+    x265amd_tu_batch tb[2];
+    x265amd_cmp_batch pb[4];
+    for (int cls = 0; cls < 2; cls++)
+    {
+        const int w = cls ? g.cc : g.c, tl = cls ? g.tlc : g.tl, n = 1 << tl;
+        const int nt = cls ? 2 * g.ntuc : g.ntu, nb = cls ? 2 * g.nbc : g.nb;
+        int64_t* fo = (int64_t*)(H + o);
+        int64_t* po = fo + nt;
+        int64_t* ro = po + nt;
+        int64_t* co = ro + nt;
+        int64_t* xo = co + nt;
+        int64_t* pa = xo + nt;
+        int64_t* pbb = pa + nb;
+        int64_t* pr = pbb + nb;
+        uint8_t* qp = (uint8_t*)(pr + nb);
+        const size_t used = 8 * (5 * (size_t)nt + 3 * (size_t)nb) + (size_t)nt;
+        int j = 0, b = 0;
+        for (int p = cls ? 1 : 0; p < (cls ? 3 : 1); p++)
+        {
+            const int64_t poff = p == 0 ? 0 : (p == 1 ? (int64_t)g.pix_y : (int64_t)(g.pix_y + g.pix_c));
+            const int per = w >> tl, ntu = per * per, nbl = (w >> 3) * (w >> 3);
+            for (int q = 0; q < ntu; q++, j++)
+            {
+                const int64_t e = (int64_t)((q / per) * n) * w + (q % per) * n;
+                fo[j] = poff + e;
+                po[j] = (int64_t)g.pix() + poff + e;
+                xo[j] = (int64_t)(ob / pix) + poff + e;
+                ro[j] = (int64_t)(resi_b / 2) + poff + e;
+                co[j] = (int64_t)(coeff_b / 2) + poff + (int64_t)q * n * n;
+                qp[j] = cu->qp[p];
+            }
+            for (int q = 0; q < nbl; q++, b++)
+            {
+                const int64_t e = (int64_t)(q / (w >> 3)) * 8 * w + (q % (w >> 3)) * 8;
+                pa[b] = poff + e;
+                pbb[b] = (int64_t)g.pix() + poff + e;
+                pr[b] = (int64_t)(ob / pix) + poff + e;
+            }
+        }
+        auto dv = [&](const void* hp) { return (const void*)(D + ((const uint8_t*)hp - H)); };
+        x265amd_tu_batch& B = tb[cls];
+        B = x265amd_tu_batch{};
+        B.log2_size = tl;
+        B.n = nt;
+        B.is_luma = !cls;
+        B.sign_hide = s->cfg.sign_hide;
+        B.fenc = D;
+        B.fenc_stride = w;
+        B.fenc_off = (const int64_t*)dv(fo);
+        B.pred = D;
+        B.pred_stride = w;
+        B.pred_off = (const int64_t*)dv(po);
+        B.resi = (int16_t*)D;
+        B.resi_stride = w;
+        B.resi_off = (const int64_t*)dv(ro);
+        B.coeff = (int16_t*)D;
+        B.coeff_off = (const int64_t*)dv(co);
+        B.recon = D;
+        B.recon_stride = w;
+        B.recon_off = (const int64_t*)dv(xo);
+        // num_sig and the psy energies of one class are contiguous in the outputs (luma, then Cb, then Cr)
+        B.num_sig = (uint32_t*)(D + sig_b) + (cls ? g.ntu : 0);
+        B.qp = (const uint8_t*)dv(qp);
+        pb[2 * cls] = { 8, 8, nb, D, w, (const int64_t*)dv(pa), D, w, (const int64_t*)dv(pbb),
+                        (int32_t*)(D + psyp_b) + (cls ? g.nb : 0) };
+        pb[2 * cls + 1] = { 8, 8, nb, D, w, (const int64_t*)dv(pa), D, w, (const int64_t*)dv(pr),
+                            (int32_t*)(D + psyr_b) + (cls ? g.nb : 0) };
+        o = (o + used + 255) & ~(size_t)255;
+    }
+    if (o + 64 > t->region) return X265AMD_ENOMEM;
+    int rc = x265amd_tu_pipeline((int)s->cfg.depth, 2, tb, t->st);
+    if (!rc) rc = x265amd_pixelcmp_grouped(X265AMD_PSY, (int)s->cfg.depth, 4, pb, t->st);
+    if (!rc) rc = (int)hipStreamWriteValue32(t->st, D + t->region - 64, 1, 0);
+    return rc;
+}
+
+int direct_wait(x265amd_rdo* s, x265amd_rdo_thread* t, int k)
+{
+    volatile uint32_t* flag = (volatile uint32_t*)(t->host + (size_t)k * t->region + t->region - 64);
+    const double t0 = now_s();
+    const double spin_until = t0 + 1e-6 * s->spin_us;
+    while (*flag != 1)
+    {
+        const double now = now_s();
+        if (now < spin_until) { __builtin_ia32_pause(); continue; }
+        sched_yield();
+        if (now - t0 > 0.05)
+        {
+            // a stream that failed never writes the flag
+            const hipError_t q = hipStreamQuery(t->st);
+            if (q != hipSuccess && q != hipErrorNotReady) return (int)q;
+        }
+    }
+    __atomic_thread_fence(__ATOMIC_ACQUIRE);
+    return 0;
+}
+
+} // namespace
 
 extern "C" int x265amd_rdo_post(x265amd_rdo* s, const x265amd_rdo_cu* cu, int* ticket)
 {
@@ -586,6 +750,17 @@ extern "C" int x265amd_rdo_post(x265amd_rdo* s, const x265amd_rdo_cu* cu, int* t
     if (k == kSlots) return X265AMD_ENOMEM;                       // caller codes the CU on the host
     x265amd_rdo_req* r = &t->req[k];
     r->cu = *cu;
+    if (s->launchers.empty())
+    {
+        if (int rc = direct_setup(s, t)) return record(rc);
+        r->t_post = now_s();
+        const int rc = direct_post(s, t, k, cu);
+        r->rc = rc;
+        r->state.store(1, std::memory_order_release);
+        *ticket = k;
+        if (rc) return record(rc);
+        return 0;
+    }
     const Geo g(cu->log2_cu);
     // pack fenc and pred planes (stride = plane width): the caller's buffers may change once this returns
     uint8_t* d = r->in;
@@ -619,6 +794,21 @@ extern "C" int x265amd_rdo_wait(x265amd_rdo* s, int ticket, const x265amd_rdo_re
     if (r->state.load(std::memory_order_acquire) == 0) return X265AMD_EINVAL;
     const double t0 = now_s();
     bool slept = false;
+    if (s->launchers.empty())
+    {
+        int rc = r->rc ? r->rc : direct_wait(s, t, ticket);
+        if (!rc) set_result(r, s->pix);
+        r->state.store(2, std::memory_order_release);
+        std::lock_guard<std::mutex> g(s->smu);
+        s->st.waits++;
+        s->st.requests++;
+        s->st.batches++;
+        s->st.wait_ms += 1e3 * (now_s() - t0);
+        s->st.batch_ms += 1e3 * (now_s() - r->t_post);
+        if (rc) return record(rc);
+        *out = &r->res;
+        return 0;
+    }
     if (r->state.load(std::memory_order_acquire) != 2)
     {
         const double spin_until = t0 + 1e-6 * s->spin_us, yield_until = t0 + 1e-6 * s->yield_us;
