@@ -234,8 +234,14 @@ def me_roofline(st, traffic_file=ME_TRAFFIC):
         traffic = int(t["traffic_bytes_per_launch"])
         tbasis = (f"traffic: HBM bytes per launch from {os.path.relpath(traffic_file, ROOT)} (rocprofv3 FETCH_SIZE x "
                   f"{t['fetch_correction']} + WRITE_SIZE per launch; {traffic / per_launch:.2f} of the algorithmic "
-                  "bytes: the search's re-reads of its window are served by the caches)")
-    return {"bound": "hbm", "kernel": "k_motion_search (x265amd_motion_search, launch-service batches)",
+                  "bytes_per_launch: the algorithmic count charges every candidate evaluation its block and "
+                  "reference window, and the overlapping windows of neighbouring candidates are served by L1 / L2, "
+                  "so HBM sees each window about once)")
+    # "bound" names the roof frac is measured against (the contract's hbm | mfma); what actually limits this
+    # kernel is latency / occupancy ("limiter"): one workgroup per search, a few searches per launch
+    return {"bound": "hbm", "limiter": "latency / occupancy (one workgroup of up to four waves per search, a few "
+                                       "searches per launch on an otherwise idle GPU; not bandwidth)",
+            "kernel": "k_motion_search (x265amd_motion_search, launch-service batches)",
             "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
             "bytes_per_launch": int(per_launch), "kernel_ms": ms, "launches": st["launches"],

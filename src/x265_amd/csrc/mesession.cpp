@@ -194,6 +194,9 @@ struct x265amd_mes
     int spin_us = 50;                 // X265AMD_MES_SPIN_US: pause-spin before yielding
     int yield_us = 5000;              // X265AMD_MES_YIELD_US: yield loop before sleeping (waits)
     int idle_us = 500;                // X265AMD_MES_IDLE_US: launchers' yield loop on an empty queue
+    int batch_us = 0;                 // X265AMD_MES_BATCH_US (round 6): a launcher that took fewer than batch_min
+    int batch_min = 8;                // requests keeps gathering until the oldest has waited batch_us (bigger
+                                      // launches: more searches per launch for the same kernel time)
     bool sync_upload = true;          // X265AMD_MES_SYNC_UPLOAD=0: reference uploads enqueued, ordered by events
                                       // (measured slower: the launches' cross-stream waits cost more than the
                                       // workers' upload waits, profiles/r05/upload_async_vs_sync_pinned_ab.txt)
@@ -516,6 +519,22 @@ void launcher_main(x265amd_mes* s, x265amd_mes_launcher* L)
             take.swap(s->rq);
             s->rq.clear();
         }
+        if (s->batch_us > 0 && (int)take.size() < s->batch_min)
+        {
+            double oldest = take[0]->t_post;
+            for (auto* r : take) oldest = r->t_post < oldest ? r->t_post : oldest;
+            const double until = oldest + 1e-6 * s->batch_us;
+            while ((int)take.size() < s->batch_min && now_s() < until && !s->stop_flag.load(std::memory_order_acquire))
+            {
+                sched_yield();
+                std::lock_guard<std::mutex> lk(s->qmu);
+                if (!s->rq.empty())
+                {
+                    take.insert(take.end(), s->rq.begin(), s->rq.end());
+                    s->rq.clear();
+                }
+            }
+        }
         const double t_take = now_s();
         if (s->trace && s->traced.fetch_add(1) < s->trace)
             fprintf(stderr, "[mes] launcher %p takes %zu requests\n", (void*)L, take.size());
@@ -801,6 +820,8 @@ int start_service(x265amd_mes* s)
     if (const char* e = getenv("X265AMD_MES_SPIN_US")) s->spin_us = atoi(e);
     if (const char* e = getenv("X265AMD_MES_YIELD_US")) s->yield_us = atoi(e);
     if (const char* e = getenv("X265AMD_MES_IDLE_US")) s->idle_us = atoi(e);
+    if (const char* e = getenv("X265AMD_MES_BATCH_US")) s->batch_us = atoi(e);
+    if (const char* e = getenv("X265AMD_MES_BATCH_MIN")) s->batch_min = atoi(e);
     if (const char* e = getenv("X265AMD_MES_SYNC_UPLOAD")) s->sync_upload = atoi(e) != 0;
     if (const char* e = getenv("X265AMD_MES_TRACE")) s->trace = atoi(e);
     if (const char* e = getenv("X265AMD_MES_ZEROCOPY")) s->zerocopy = atoi(e);
