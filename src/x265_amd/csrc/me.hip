@@ -49,15 +49,23 @@ struct MeArgs
     const int64_t* rcoff;
     uint32_t* evals;              // [2 n]: job j's full-pel / sub-pel block evaluations (NULL = not counted)
     int w, h, n, lg, method, subme, merange, max_cand, depth;
+    int win_bytes;                // dynamic LDS of a search-window launch (k_motion_search<P, G, true>), else 0
+    int win_r;                    // its window's reach around the search start (full-pel)
 };
 
 constexpr int kMeMaxUnits = 4;    // 4x4 units per lane (64x64 PU over 64 lanes)
 
-template <typename P>
+// W: the search window is staged in LDS (k_motion_search<P, G, true>): lref / lrs address it with the PU origin
+// as (0, 0), and [wx0, wx1) x [wy0, wy1) is the part of the reference plane (PU-relative pixels) it holds; a
+// block whose reads all fall inside is read from LDS, any other from the reference plane
+template <typename P, bool W = false>
 struct MeState
 {
     const P* ref;           // reference at the PU origin
     int64_t rs;
+    const P* lref;
+    int64_t lrs;
+    int wx0, wx1, wy0, wy1;
     const uint16_t* tab;
     int mvpx, mvpy;
     int nu, lane, G, uw;    // units of this lane, lane in group, group size, units per PU row
@@ -81,6 +89,14 @@ struct MeState
     __device__ __forceinline__ int mvcost(int qx, int qy) const
     {
         return (uint16_t)(tab[qx - mvpx] + tab[qy - mvpy]);
+    }
+    // the plane to read a footprint [x0, x1) x [y0, y1) from (wave-uniform: the footprint is the group's)
+    __device__ __forceinline__ void source(int x0, int x1, int y0, int y1, const P*& r, int64_t& stride) const
+    {
+        r = ref;
+        stride = rs;
+        if constexpr (W)
+            if (x0 >= wx0 && x1 <= wx1 && y0 >= wy0 && y1 <= wy1) { r = lref; stride = lrs; }
     }
 };
 
@@ -176,10 +192,21 @@ __device__ __forceinline__ void me_group_sums(int (&v)[N])
 // registers (loaded once per PU); every reference row of all N candidates and NU units is loaded before the
 // first SAD, and the N group reductions run side by side, so N candidates cost one memory round trip and
 // one reduction latency instead of N.  Lanes beyond the PU's units (nu = 0) load the PU's first unit.
-template <typename P, int G, int N, int NU>
-__device__ __forceinline__ void fpel_sad_nu(const MeState<P>& s, const int (&mx)[N], const int (&my)[N], int (&out)[N])
+template <typename P, int G, int N, int NU, bool WIN>
+__device__ __forceinline__ void fpel_sad_nu(const MeState<P, WIN>& s, const int (&mx)[N], const int (&my)[N],
+                                            int (&out)[N])
 {
     constexpr int W = sizeof(P) == 1 ? 1 : 2;
+    int x0 = mx[0], x1 = mx[0], y0 = my[0], y1 = my[0];
+#pragma unroll
+    for (int n = 1; n < N; n++)
+    {
+        x0 = min(x0, mx[n]); x1 = max(x1, mx[n]);
+        y0 = min(y0, my[n]); y1 = max(y1, my[n]);
+    }
+    const P* ref;
+    int64_t rs;
+    s.source(x0, x1 + s.w, y0, y1 + s.h, ref, rs);
     uint32_t w[N][NU][4][W];
 #pragma unroll
     for (int k = 0; k < NU; k++)
@@ -189,9 +216,9 @@ __device__ __forceinline__ void fpel_sad_nu(const MeState<P>& s, const int (&mx)
 #pragma unroll
         for (int n = 0; n < N; n++)
         {
-            const P* p = s.ref + (ux + mx[n]) + (int64_t)(uy + my[n]) * s.rs;
+            const P* p = ref + (ux + mx[n]) + (int64_t)(uy + my[n]) * rs;
 #pragma unroll
-            for (int r = 0; r < 4; r++) load4<P>(p + r * s.rs, w[n][k][r]);
+            for (int r = 0; r < 4; r++) load4<P>(p + r * rs, w[n][k][r]);
         }
     }
 #pragma unroll
@@ -213,9 +240,9 @@ __device__ __forceinline__ void fpel_sad_nu(const MeState<P>& s, const int (&mx)
 
 // N candidates' SADs; `counted` of them are real evaluations (the rest are range-failed points whose loads
 // were clamped to a valid position and whose results are ignored)
-template <typename P, int G, int N>
-__device__ __forceinline__ void fpel_sads(const MeState<P>& s, const int (&mx)[N], const int (&my)[N], int (&out)[N],
-                                          int counted = N)
+template <typename P, int G, int N, bool WIN>
+__device__ __forceinline__ void fpel_sads(const MeState<P, WIN>& s, const int (&mx)[N], const int (&my)[N],
+                                          int (&out)[N], int counted = N)
 {
     s.nfp += counted;
     if constexpr (G != 64) fpel_sad_nu<P, G, N, 1>(s, mx, my, out);     // one unit per lane below and above
@@ -225,9 +252,9 @@ __device__ __forceinline__ void fpel_sads(const MeState<P>& s, const int (&mx)[N
 }
 
 // ... plus the MV cost (quarter-pel MV = 4 x full-pel)
-template <typename P, int G, int N>
-__device__ __forceinline__ void fpel_costs(const MeState<P>& s, const int (&mx)[N], const int (&my)[N], int (&out)[N],
-                                           int counted = N)
+template <typename P, int G, int N, bool WIN>
+__device__ __forceinline__ void fpel_costs(const MeState<P, WIN>& s, const int (&mx)[N], const int (&my)[N],
+                                           int (&out)[N], int counted = N)
 {
     fpel_sads<P, G, N>(s, mx, my, out, counted);
 #pragma unroll
@@ -235,8 +262,8 @@ __device__ __forceinline__ void fpel_costs(const MeState<P>& s, const int (&mx)[
 }
 
 // one candidate's SAD
-template <typename P, int G>
-__device__ __forceinline__ int fpel_sad(const MeState<P>& s, int dx, int dy)
+template <typename P, int G, bool WIN>
+__device__ __forceinline__ int fpel_sad(const MeState<P, WIN>& s, int dx, int dy)
 {
     const int mx[1] = { dx }, my[1] = { dy };
     int c[1];
@@ -390,6 +417,11 @@ __device__ __forceinline__ int chroma_satd(const MeState<P>& s, int qx, int qy)
     return acc;
 }
 
+// 8-bit reference rows are read as dwords (X265AMD_ME_B32=1): the rows may be in an LDS search window, where a
+// 64-bit read off its 8-byte alignment is replayed (32-bit reads are not)
+#ifndef X265AMD_ME_B32
+#define X265AMD_ME_B32 1
+#endif
 // One row of a unit's reference window kept packed as loaded: C = 4 pixels (full-pel columns) or 11
 // (the 8-tap reach, -3 .. +7): an 8-pixel vector and the 4 pixels from +7 (overlapping by one).
 template <typename P, int C>
@@ -402,6 +434,11 @@ struct RawRow
     __device__ __forceinline__ void load(const P* p)
     {
         if constexpr (WA == 1) a[0] = ldu<uint32_t>(p);
+        else if constexpr (WA == 2 && X265AMD_ME_B32)
+        {
+            a[0] = ldu<uint32_t>(p);
+            a[1] = ldu<uint32_t>((const uint8_t*)p + 4);
+        }
         else if constexpr (WA == 2) { const uint2 v = ldu<uint2>(p); a[0] = v.x; a[1] = v.y; }
         else { const uint4 v = ldu<uint4>(p); a[0] = v.x; a[1] = v.y; a[2] = v.z; a[3] = v.w; }
         if constexpr (WB == 1) b[0] = ldu<uint32_t>(p + 7);
@@ -659,7 +696,11 @@ struct Row12
     uint32_t w[NW];
     __device__ __forceinline__ void load(const P* p)
     {
-        if constexpr (sizeof(P) == 1)
+        if constexpr (sizeof(P) == 1 && X265AMD_ME_B32)
+        {
+            w[0] = ldu<uint32_t>(p); w[1] = ldu<uint32_t>(p + 4); w[2] = ldu<uint32_t>(p + 8);
+        }
+        else if constexpr (sizeof(P) == 1)
         {
             const uint2 v = ldu<uint2>(p);
             w[0] = v.x; w[1] = v.y; w[2] = ldu<uint32_t>(p + 8);
@@ -864,7 +905,7 @@ __device__ __forceinline__ int4 subpel_workload(int subme)
     return make_int4(v & 15, (v >> 4) & 15, (v >> 8) & 15, v >> 12);
 }
 
-template <typename P, int G>
+template <typename P, int G, bool WIN = false>
 #ifndef X265AMD_ME_WAVES
 #define X265AMD_ME_WAVES 1
 #endif
@@ -874,7 +915,7 @@ __global__ __launch_bounds__(X265AMD_BLOCK, X265AMD_ME_WAVES) void k_motion_sear
     constexpr int SPB = G > 64 ? 1 : X265AMD_BLOCK / G;
     const int64_t j = (int64_t)xcd_block() * SPB + threadIdx.x / G;
     if (j >= a.n) return;                               // whole groups
-    MeState<P> s;
+    MeState<P, WIN> s;
     s.lane = threadIdx.x & (G - 1);
     s.G = G;
     s.uw = a.w >> 2;
@@ -911,10 +952,72 @@ __global__ __launch_bounds__(X265AMD_BLOCK, X265AMD_ME_WAVES) void k_motion_sear
     }
     const int minx = a.mv_range[4 * j], miny = a.mv_range[4 * j + 1];
     const int maxx = a.mv_range[4 * j + 2], maxy = a.mv_range[4 * j + 3];
+    s.lref = s.ref;
+    s.lrs = s.rs;
+    s.wx0 = s.wy0 = 1 << 30;
+    s.wx1 = s.wy1 = -(1 << 30);
+    // stage the search window around full-pel (cx, cy) in LDS: up to win_r pixels either way within the MV
+    // range box, 8 pixels around that and the PU (the reach of a DIA / HEX search, whose full-pel best may sit
+    // up to 3 pixels outside the range, plus the sub-pel step and the 8-tap filter).  x265 clips the range 8
+    // pixels short of its 64 + 8 pixel padding (CUData::clipMv, cudata.cpp:1870-1886), so the window is inside
+    // the plane.  Whole aligned 16-byte chunks are copied (a row keeps its alignment, lead), all of a lane's
+    // loads before its first store; a search that later steps outside the window reads the plane.
+    auto stage = [&](int cx, int cy) {
+        if constexpr (WIN)
+        {
+            extern __shared__ __attribute__((aligned(16))) uint4 me_win[];
+            const int R = a.win_r;
+            const int x0 = max(minx, cx - R) - 8, x1 = min(maxx, cx + R) + a.w + 9;
+            const int y0 = max(miny, cy - R) - 8, y1 = min(maxy, cy + R) + a.h + 9;
+            const int ww = x1 - x0, wh = y1 - y0;
+            if (ww < 16 || wh <= 0) return;                          // (uniform over the workgroup)
+            const uint8_t* g0 = (const uint8_t*)(s.ref + x0 + (int64_t)y0 * s.rs);
+            const int lead = (int)((uintptr_t)g0 & 15);
+            const int nc = (lead + ww * (int)sizeof(P) + 15) >> 4;   // 16-byte chunks per row (>= 2)
+            if ((int64_t)nc * wh * 16 > a.win_bytes) return;
+            const uint4* gs = (const uint4*)(g0 - lead);
+            const int64_t gc = s.rs * (int64_t)sizeof(P) / 16;       // plane stride in chunks (host-checked)
+            const int total = nc * wh;
+            const uint32_t mag = 0xffffffffu / (uint32_t)nc + 1u;    // row = i / nc as a high multiply
+            constexpr int B = G > 64 ? G : X265AMD_BLOCK, K = 8;
+            for (int i0 = threadIdx.x; i0 < total; i0 += K * B)
+            {
+                uint4 v[K];
+#pragma unroll
+                for (int k = 0; k < K; k++)
+                {
+                    const int i = min(i0 + k * B, total - 1);
+                    const int r = (int)__umulhi((uint32_t)i, mag);
+                    v[k] = gs[r * gc + (i - r * nc)];
+                }
+#pragma unroll
+                for (int k = 0; k < K; k++)
+                    if (i0 + k * B < total) me_win[i0 + k * B] = v[k];
+            }
+            __syncthreads();
+            s.lrs = nc * 16 / (int)sizeof(P);
+            // lref (the PU origin) may lie outside the window — before the LDS array when the window sits
+            // right of / below the PU origin.  Formed from the LDS pointer, the compiler does that arithmetic in
+            // the 32-bit LDS address space, and the wrapped offset then carries out of the shared aperture when
+            // a read adds its displacement back (an aperture violation); the generic address is laundered first
+            // so the origin arithmetic is 64-bit flat arithmetic that every in-window read undoes exactly
+            const uint8_t* wbase = (const uint8_t*)me_win;
+            asm volatile("" : "+v"(wbase));
+            s.lref = (const P*)(wbase + lead) - x0 - (int64_t)y0 * s.lrs;
+            s.wx0 = x0; s.wx1 = x1;
+            s.wy0 = y0; s.wy1 = y1;
+        }
+    };
+    // the plane a sub-pel compare around full-pel (x, y) reads from: the 8-tap windows of the block at
+    // (x, y) .. (x + 1, y + 1) span [x - 3, x + w + 5) x [y - 3, y + h + 5)
+    auto spsrc = [&](int x, int y, const P*& r, int64_t& rs) { s.source(x - 3, x + a.w + 5, y - 3, y + a.h + 5, r, rs); };
     // the sub-pel compare, out of line
     auto spc = [&](int qx, int qy, bool satd) {
         s.nsp++;
-        return subpel_cost<P, G>(s.ref, s.fenc, (int)s.rs, (int)s.fs, s.lane | s.nu << 8, a.w | a.h << 8,
+        const P* r;
+        int64_t rs;
+        spsrc(qx >> 2, qy >> 2, r, rs);
+        return subpel_cost<P, G>(r, s.fenc, (int)rs, (int)s.fs, s.lane | s.nu << 8, a.w | a.h << 8,
                                  a.depth | (s.chroma ? 256 : 0), s.fc[0], s.fc[1], s.rc[0], s.rc[1], (int)s.fcs,
                                  (int)s.rcs, qx, qy, satd);
     };
@@ -955,6 +1058,8 @@ __global__ __launch_bounds__(X265AMD_BLOCK, X265AMD_ME_WAVES) void k_motion_sear
             if (c < bprecost) { bprecost = c; bpx = cx; bpy = cy; }
         }
     }
+    if (a.method <= 1)
+        stage(bx, by);                                 // (the window variant runs DIA / HEX only)
     if (a.method == 0)
     {
         // diamond, radius 1 (motion.cpp:654-676)
@@ -1325,7 +1430,10 @@ __global__ __launch_bounds__(X265AMD_BLOCK, X265AMD_ME_WAVES) void k_motion_sear
                 for (int i0 = 1; i0 <= ndir; i0 += 4)
                 {
                     s.nsp += 4;
-                    const int4 c4 = subpel_cost4<P, G>(s.ref, s.fenc, (int)s.rs, (int)s.fs, s.lane | s.nu << 8,
+                    const P* r;
+                    int64_t rs;
+                    spsrc((qx - d) >> 2, (qy - d) >> 2, r, rs);
+                    const int4 c4 = subpel_cost4<P, G>(r, s.fenc, (int)rs, (int)s.fs, s.lane | s.nu << 8,
                                                        a.w | a.h << 8, a.depth | (s.chroma ? 256 : 0), s.fc[0],
                                                        s.fc[1], s.rc[0], s.rc[1], (int)s.fcs, (int)s.rcs, qx, qy, d,
                                                        i0, satd);
@@ -1513,8 +1621,25 @@ static int me_gmax()
     return v;
 }
 
+// search windows in LDS (X265AMD_ME_LDS_R = r > 0; read at every launch, default 0 = off) for the
+// one-search-per-workgroup sizes (G = 128 / 256: PUs of 128 or more 4x4 units) of DIA / HEX searches: once the
+// search start is known, the reference around it (r pixels either way, within the MV range box) is staged in
+// LDS and every later candidate there reads LDS instead of taking an L2 / HBM round trip.  The window is at
+// most (2r + w + 17) x (2r + h + 17) pixels (64x64, r 16: 14 KB at 8-bit).  Bit-exact (test_me.py), but
+// measured slower in the running encoder — 0.026 ms per launch without, 0.032-0.035 with r = 8 / 16 / 32 / the
+// whole range (profiles/r06/me_lds_window_ab.txt): the reads go through flat (generic) addressing and the
+// staging round trip costs more than the L2 hits it replaces.
+static int me_lds_r()
+{
+    const char* e = getenv("X265AMD_ME_LDS");
+    const char* r = getenv("X265AMD_ME_LDS_R");
+    const int v = (e && atoi(e) == 0) ? 0 : r ? atoi(r) : 0;
+    return v < 0 ? 0 : v;
+}
+constexpr int kMeWinMaxBytes = 64 * 1024;
+
 template <typename P>
-static int launch_me(const MeArgs& a, hipStream_t st)
+static int launch_me(MeArgs a, hipStream_t st)
 {
     if (a.method == 4)
         hipLaunchKernelGGL((k_full_search<P>), dim3(a.n), dim3(256), 0, st, a);
@@ -1522,6 +1647,21 @@ static int launch_me(const MeArgs& a, hipStream_t st)
     const int spb = G > 64 ? 1 : X265AMD_BLOCK / G;
     const uint32_t blocks = (uint32_t)((a.n + spb - 1) / spb);
     const int threads = G > 64 ? G : X265AMD_BLOCK;
+    a.win_bytes = 0;
+    const int lr = me_lds_r();
+    a.win_r = lr < a.merange ? lr : a.merange;
+    if (G > 64 && (a.method == 0 || a.method == 1) && a.win_r > 0 && (a.rs * (int64_t)sizeof(P)) % 16 == 0)
+    {
+        const int64_t ww = 2 * (int64_t)a.win_r + a.w + 17, wh = 2 * (int64_t)a.win_r + a.h + 17;
+        const int64_t bytes = ((ww * (int64_t)sizeof(P) + 30) >> 4) * 16 * wh;
+        if (bytes <= kMeWinMaxBytes) a.win_bytes = (int)bytes;
+    }
+    if (a.win_bytes)
+    {
+        if (G == 128) hipLaunchKernelGGL((k_motion_search<P, 128, true>), dim3(blocks), dim3(threads), a.win_bytes, st, a);
+        else hipLaunchKernelGGL((k_motion_search<P, 256, true>), dim3(blocks), dim3(threads), a.win_bytes, st, a);
+        return (int)hipGetLastError();
+    }
 #define L(g) case g: hipLaunchKernelGGL((k_motion_search<P, g>), dim3(blocks), dim3(threads), 0, st, a); break;
     switch (G)
     {
@@ -1570,7 +1710,7 @@ extern "C" int x265amd_motion_search(int depth, int count, const x265amd_me_batc
         MeArgs a{ b.fenc, b.fenc_off, (int64_t)b.fenc_stride, b.ref, b.ref_off, (int64_t)b.ref_stride, b.mv_range,
                   b.mvp, b.mvc, b.num_cand, b.mvcost, b.mvcost_off, b.out_mv, b.out_cost, b.fenc_cb, b.fenc_cr,
                   (int64_t)b.fenc_cstride, b.fenc_coff, b.ref_cb, b.ref_cr, (int64_t)b.ref_cstride, b.ref_coff,
-                  b.eval_count, b.w, b.h, b.n, lg, b.method, b.subme, b.merange, b.max_cand, depth };
+                  b.eval_count, b.w, b.h, b.n, lg, b.method, b.subme, b.merange, b.max_cand, depth, 0, 0 };
         const int rc = depth == 8 ? launch_me<uint8_t>(a, bs) : launch_me<uint16_t>(a, bs);
         if (rc) { fj.join(); return rc; }
     }

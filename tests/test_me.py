@@ -127,3 +127,49 @@ def test_me_gpu_multi_batch_call(gpu_prims, oracle_libs, depth):
         exp = run_cpu(c, orc)
         for k in c.outs:
             np.testing.assert_array_equal(b[k].cpu().numpy(), exp[k])
+
+
+def window_cases(depth, n=96):
+    """Round 6: with X265AMD_ME_LDS_R = r, PUs of 128 or more 4x4 units searched by DIA / HEX stage the
+    reference within r pixels of the search start in LDS (k_motion_search<P, G, true>).  With the range boxed
+    to the MVP +- merange, as Search::setSearchRange makes it, and r = merange the window (2 merange + w + 17)^2
+    fits the launch's LDS (merange 57 at 8-bit: 195 x 195 bytes; merange 32 at 10-bit), so every candidate
+    reads LDS; with r = 8 searches step out of the window and mix LDS and plane reads, as do the far cases
+    (MV 0 outside the box)."""
+    m = 57 if depth == 8 else 32
+    out = [case_me(w, h, meth, s, m, depth, n, seed_of("me-win", depth, w, h, meth, s), box=m)
+           for (w, h) in ((64, 64), (64, 32), (32, 64), (48, 64), (64, 48))
+           for meth, s in ((1, 2), (0, 0), (0, 1), (1, 3))]
+    out += [case_me(w, h, meth, 2, m, depth, n, seed_of("me-win-far", depth, w, h, meth), box=16, far=24)
+            for (w, h) in ((64, 64), (64, 32)) for meth in (0, 1)]
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("depth", [8, 10])
+@pytest.mark.parametrize("reach", [8, 57])
+def test_me_gpu_lds_window_matches_oracle(gpu_prims, oracle_libs, depth, reach, monkeypatch):
+    monkeypatch.setenv("X265AMD_ME_LDS_R", str(reach))     # read by the library at every launch
+    orc = CpuOracle("oracle", depth)
+    bad = []
+    for c in window_cases(depth):
+        got, exp = run_gpu(c, gpu_prims), run_cpu(c, orc)
+        for k in c.outs:
+            if not np.array_equal(got[k], exp[k]):
+                bad.append((c.key(), k, int((got[k] != exp[k]).sum())))
+    assert not bad, bad[:6]
+
+
+@pytest.mark.parametrize("depth", [8, 10])
+def test_me_window_cases_fit_the_window(depth):
+    """host-side arithmetic of the window launch (me.hip launch_me): the boxed cases' windows fit"""
+    for c in window_cases(depth):
+        p = c.params
+        if p.get("far"):
+            continue
+        rng = c.bufs["rng"].reshape(-1, 4).astype(np.int64)
+        sz = 1 if depth == 8 else 2
+        ww, wh = 2 * p["merange"] + p["w"] + 17, 2 * p["merange"] + p["h"] + 17
+        cap = ((ww * sz + 6) >> 2) * 4 * wh
+        assert cap <= 64 * 1024
+        assert (rng[:, 2] - rng[:, 0] <= 2 * p["merange"]).all() and (rng[:, 3] - rng[:, 1] <= 2 * p["merange"]).all()
