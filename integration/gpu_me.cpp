@@ -89,6 +89,8 @@ extern "C" int x265ref_motionEstimate(MotionEstimate* self, ReferencePlanes* ref
 extern "C" SplitData x265ref_compressInterCU_rd0_4(Analysis* self, const CUData& parentCTU, const CUGeom& cuGeom,
                                                    int32_t qp);
 extern "C" void x265ref_checkMerge2Nx2N_rd0_4(Analysis* self, Mode& skip, Mode& merge, const CUGeom& cuGeom);
+/* gpu_rdo.cpp: the 2Nx2N prediction just made is final (X265AMD_RDO_EARLY) */
+extern "C" void x265amd_rdo_early_inter(void* search, void* mode, const void* geom, int chroma_mc);
 
 namespace {
 
@@ -787,6 +789,7 @@ void Search::predInterSearch(Mode& interMode, const CUGeom& cuGeom, bool bChroma
         }
     }
     x265ref_predInterSearch(this, interMode, cuGeom, bChromaMC, refMasks);
+    x265amd_rdo_early_inter(this, &interMode, &cuGeom, bChromaMC ? 1 : 0);
     if (used)
     {
         used->me = NULL;

@@ -39,6 +39,23 @@
  *                       invtransformNxN / psyCost_pp (host_result) and served through the same memo: checks
  *                       the binding's plumbing on a CPU-only host (every call must hit, bitstream unchanged)
  *   X265AMD_RDO_MIN=k   smallest CU (log2, 4..6, default 6: 64x64) coded on the device
+ *   X265AMD_RDO_EARLY=1 post each CU's request as soon as its prediction is final, ahead of the call that codes
+ *                       it, instead of posting and waiting inside encodeResAndCalcRdInterCU (below); a call with
+ *                       no matching early post is coded on the host
+ *
+ * Early posts (X265AMD_RDO_EARLY=1).  The three predictions --preset medium's inter analysis codes at a depth
+ * (compressInterCU_rd0_4, analysis.cpp:818-1298) are final well before their encodeResAndCalcRdInterCU:
+ *   Search::predInterSearch (hooked in gpu_me.cpp)       the 2Nx2N prediction (luma and, at --rd >= 3, chroma
+ *                                                       MC done, search.cpp:2405-2420) — coded after the
+ *                                                       bidir and rectangular checks (analysis.cpp:943-1118);
+ *   Analysis::checkBidir2Nx2N (analysis.cpp:2013)        the bidir prediction — coded after the best inter mode
+ *                                                       (:1121-1126);
+ *   Search::encodeResAndCalcRdSkipCU (search.cpp:2512)   the best merge candidate's prediction — coded with
+ *                                                       residual right after the skip costing (:1739-1752).
+ * Each is posted there, with the Quant object's QPs of the moment (the CU's: the analysis sets them before the
+ * CU's modes, :926-927) and a copy of the prediction; encodeResAndCalcRdInterCU takes the post whose source
+ * buffer, QPs, size and prediction (compared) are the call's, so a post whose prediction changed or was never
+ * coded is simply not used (dropped when its slot is posted again or the encoder closes).
  *   X265AMD_RDO_LAUNCHERS=n  service threads per session (default 2; 0: each worker launches its CU itself,
  *                       zero-copy, and polls a completion flag)
  *   X265AMD_ME_STATS=1  posts, memo hits / misses per function, worker wait time, session counters at exit
@@ -50,6 +67,7 @@
 #include "picyuv.h"
 #include "slice.h"
 #include "search.h"
+#include "analysis.h"
 #include "quant.h"
 #include "scalinglist.h"
 #include "yuv.h"
@@ -68,6 +86,8 @@
 using namespace X265_NS;
 
 extern "C" void x265ref_encodeResAndCalcRdInterCU(Search* self, Mode& interMode, const CUGeom& cuGeom);
+extern "C" void x265ref_encodeResAndCalcRdSkipCU(Search* self, Mode& interMode);
+extern "C" void x265ref_checkBidir2Nx2N(Analysis* self, Mode& inter2Nx2N, Mode& bidir2Nx2N, const CUGeom& cuGeom);
 extern "C" uint32_t x265ref_transformNxN(Quant* self, const CUData& cu, const pixel* fenc, uint32_t fencStride,
                                          const int16_t* residual, uint32_t resiStride, coeff_t* coeff,
                                          uint32_t log2TrSize, TextType ttype, uint32_t absPartIdx,
@@ -91,6 +111,8 @@ enum { RDO_CPU = 0, RDO_GPU = 1, RDO_CHECK = 2, RDO_HOST = 3 };
 int g_mode = RDO_CPU;
 int g_min_log2 = 6;
 int g_launchers = 2;
+bool g_early = false;
+std::atomic<int> g_rdo_epoch{ 0 };     /* bumped when an encoder closes: earlier early posts are abandoned */
 int g_gpus = 1;
 bool g_stats_on = false;
 pthread_once_t g_once = PTHREAD_ONCE_INIT;
@@ -106,7 +128,7 @@ std::vector<Session> g_sessions;     /* per device session index (frame encoder 
 x265amd_rdo_counters g_closed{};
 
 enum { ST_POSTS, ST_HOST_CUS, ST_TQ_HIT, ST_TQ_MISS, ST_ITQ_HIT, ST_ITQ_MISS, ST_PSY_HIT, ST_PSY_MISS, ST_CHECK_BAD,
-       ST_N };
+       ST_EARLY_MERGE, ST_EARLY_INTER, ST_EARLY_BIDIR, ST_EARLY_USED, ST_EARLY_DROPPED, ST_N };
 std::atomic<int64_t> g_st[ST_N];
 std::atomic<int64_t> g_wait_ns{ 0 };
 
@@ -133,6 +155,11 @@ void print_stats()
             (long long)g_st[ST_POSTS].load(), (long long)g_st[ST_HOST_CUS].load(), (long long)g_st[ST_TQ_HIT].load(),
             (long long)g_st[ST_TQ_MISS].load(), (long long)g_st[ST_ITQ_HIT].load(), (long long)g_st[ST_ITQ_MISS].load(),
             (long long)g_st[ST_PSY_HIT].load(), (long long)g_st[ST_PSY_MISS].load(), 1e-9 * g_wait_ns.load());
+    if (g_early)
+        fprintf(stderr, "[x265rdo] early posts merge %lld inter %lld bidir %lld; used %lld, dropped %lld\n",
+                (long long)g_st[ST_EARLY_MERGE].load(), (long long)g_st[ST_EARLY_INTER].load(),
+                (long long)g_st[ST_EARLY_BIDIR].load(), (long long)g_st[ST_EARLY_USED].load(),
+                (long long)g_st[ST_EARLY_DROPPED].load());
     if (c.batches)
         fprintf(stderr, "[x265rdo] service: %lld batches, %lld CUs (%.2f per batch, max %lld), %lld TUs, %lld 8x8 blocks, "
                         "kernels %.3f ms per batch (HIP events), batch %.3f ms, queueing %.3f ms per CU, %lld waits slept\n",
@@ -154,6 +181,8 @@ void init_once()
     if (e && *e) g_min_log2 = atoi(e) < 4 ? 4 : (atoi(e) > 6 ? 6 : atoi(e));
     e = getenv("X265AMD_RDO_LAUNCHERS");
     if (e && *e) g_launchers = atoi(e) < 0 ? 0 : atoi(e);     /* 0: direct mode (per-thread zero-copy launches) */
+    e = getenv("X265AMD_RDO_EARLY");
+    g_early = e && *e == '1' && (g_mode == RDO_GPU || g_mode == RDO_CHECK);
     e = getenv("X265AMD_GPUS");
     if (e && *e) g_gpus = atoi(e) < 1 ? 1 : atoi(e);
     const char* st = getenv("X265AMD_ME_STATS");
@@ -163,6 +192,7 @@ void init_once()
         fprintf(stderr, "[x265rdo] inter residual coding of CUs >= %dx%d %s\n", 1 << g_min_log2, 1 << g_min_log2,
                 g_mode == RDO_CHECK ? "on the MI355X (check mode)" : g_mode == RDO_HOST ? "on the CPU (hook memo)" :
                                                                            "on the MI355X");
+        if (g_early) fprintf(stderr, "[x265rdo] requests posted when the prediction is final (early posts)\n");
         if (g_stats_on) atexit(print_stats);
     }
 }
@@ -284,10 +314,9 @@ int psy_thunk(const pixel* source, intptr_t sstride, const pixel* recon, intptr_
 /* CU eligible for the device: the TU structure and quantisation the session restates (one RQT level of
  * min(CU, 32) TUs, plain quant with sign hiding, no transform skip / lossless / RDOQ / scaling lists /
  * noise reduction, 4:2:0 2Nx2N) */
-bool eligible(Search& s, int csp, const Mode& mode, const CUGeom& geom)
+bool eligible(Search& s, int csp, const Mode& mode, int log2)
 {
     const CUData& cu = mode.cu;
-    const int log2 = (int)geom.log2CUSize;
     if (log2 < g_min_log2 || log2 > 6 || csp != X265_CSP_I420) return false;
     if (cu.m_tqBypass[0] || cu.m_partSize[0] != SIZE_2Nx2N || cu.isIntra(0)) return false;
     if (s.m_bEnableRDOQ || s.m_quant.*QuantPeek::rdoq()) return false;
@@ -338,6 +367,7 @@ extern "C" void x265amd_rdo_install(void* table)
 /* called by the encoder binding before x265_encoder_close frees the encoder (oracle/hip_encoder_main.cpp) */
 extern "C" void x265amd_rdo_encoder_closed(void)
 {
+    g_rdo_epoch++;
     pthread_mutex_lock(&g_mu);
     for (Session& s : g_sessions)
     {
@@ -431,17 +461,168 @@ const x265amd_rdo_result* host_result(Quant& q, const CUData& cu, int log2cu, co
     return &r;
 }
 
+/* the request of one CU posted when its prediction became final (X265AMD_RDO_EARLY=1) */
+enum { EARLY_MERGE, EARLY_INTER, EARLY_BIDIR, EARLY_N };
+struct Early
+{
+    x265amd_rdo* rdo = nullptr;
+    int ticket = -1;
+    int epoch = 0;
+    int log2 = 0;
+    uint8_t qp[3];
+    const pixel* fenc[3];
+    pixel pred[64 * 64 + 2 * 32 * 32];       /* the posted prediction, planes packed (stride = plane width) */
+};
+thread_local Early* t_early;
+
+void early_drop(Early& e)
+{
+    if (e.ticket < 0) return;
+    if (e.epoch == g_rdo_epoch.load())
+    {
+        /* (a request's slot is reusable once its results are in; an early post is long done by now) */
+        const x265amd_rdo_result* r;
+        (void)x265amd_rdo_wait(e.rdo, e.ticket, &r);
+        (void)x265amd_rdo_release(e.rdo, e.ticket);
+    }
+    e.ticket = -1;
+}
+
+/* fill the request of the CU whose prediction is `pred` with the Quant object's current QPs */
+void request_of(Search& s, int log2, const Yuv& fenc, const Yuv& pred, x265amd_rdo_cu& in)
+{
+    in = {};
+    in.log2_cu = log2;
+    for (int p = 0; p < 3; p++)
+    {
+        in.qp[p] = (uint8_t)(s.m_quant.*QuantPeek::qp())[p].qp;
+        in.fenc[p] = fenc.m_buf[p];
+        in.fenc_stride[p] = p ? fenc.m_csize : fenc.m_size;
+        in.pred[p] = pred.m_buf[p];
+        in.pred_stride[p] = p ? pred.m_csize : pred.m_size;
+    }
+}
+
+void early_post(Search& s, const Mode& mode, int log2, int slot)
+{
+    pthread_once(&g_once, init_once);
+    if (!g_early || !mode.fencYuv || !eligible(s, mode.cu.m_chromaFormat, mode, log2)) return;
+    if (!t_early) t_early = new Early[EARLY_N];
+    Early& e = t_early[slot];
+    if (e.ticket >= 0)
+    {
+        g_st[ST_EARLY_DROPPED]++;
+        early_drop(e);
+    }
+    x265amd_rdo* rdo = session_for(mode.cu, s.m_slice->m_pps->bSignHideEnabled ? 1 : 0);
+    if (!rdo) return;
+    const int c = 1 << log2;
+    x265amd_rdo_cu in;
+    request_of(s, log2, *mode.fencYuv, mode.predYuv, in);
+    int ticket = -1;
+    if (x265amd_rdo_post(rdo, &in, &ticket)) return;
+    e.rdo = rdo;
+    e.ticket = ticket;
+    e.epoch = g_rdo_epoch.load();
+    e.log2 = log2;
+    pixel* d = e.pred;
+    for (int p = 0; p < 3; p++)
+    {
+        e.qp[p] = in.qp[p];
+        e.fenc[p] = mode.fencYuv->m_buf[p];
+        const int w = p ? c >> 1 : c;
+        for (int y = 0; y < w; y++, d += w)
+            memcpy(d, mode.predYuv.m_buf[p] + y * in.pred_stride[p], w * sizeof(pixel));
+    }
+    g_st[ST_EARLY_MERGE + slot]++;
+}
+
+/* the early post made for this call, if any: same size, source buffer, QPs and prediction */
+Early* early_match(Search& s, const Mode& mode, int log2)
+{
+    if (!t_early) return nullptr;
+    const int c = 1 << log2;
+    for (int k = 0; k < EARLY_N; k++)
+    {
+        Early& e = t_early[k];
+        if (e.ticket < 0 || e.epoch != g_rdo_epoch.load() || e.log2 != log2) continue;
+        bool same = true;
+        const pixel* d = e.pred;
+        for (int p = 0; p < 3 && same; p++)
+        {
+            const int w = p ? c >> 1 : c;
+            const intptr_t ps = p ? mode.predYuv.m_csize : mode.predYuv.m_size;
+            same = e.fenc[p] == mode.fencYuv->m_buf[p] &&
+                   e.qp[p] == (uint8_t)(s.m_quant.*QuantPeek::qp())[p].qp;
+            for (int y = 0; y < w && same; y++, d += w)
+                same = !memcmp(d, mode.predYuv.m_buf[p] + y * ps, w * sizeof(pixel));
+        }
+        if (same) return &e;
+    }
+    return nullptr;
+}
+
 } // namespace
 
+/* Search::predInterSearch's hook (gpu_me.cpp) after the reference's search: the 2Nx2N prediction is final */
+extern "C" void x265amd_rdo_early_inter(void* search, void* mode, const void* geom, int chroma_mc)
+{
+    Mode& m = *(Mode*)mode;
+    if (chroma_mc && m.cu.m_partSize[0] == SIZE_2Nx2N)
+        early_post(*(Search*)search, m, (int)((const CUGeom*)geom)->log2CUSize, EARLY_INTER);
+}
+
 namespace X265_NS {
+
+void Analysis::checkBidir2Nx2N(Mode& inter2Nx2N, Mode& bidir2Nx2N, const CUGeom& cuGeom)
+{
+    x265ref_checkBidir2Nx2N(this, inter2Nx2N, bidir2Nx2N, cuGeom);
+    if (g_early && bidir2Nx2N.sa8dCost != MAX_INT64 && m_bChromaSa8d)
+        early_post(*this, bidir2Nx2N, (int)cuGeom.log2CUSize, EARLY_BIDIR);
+}
+
+void Search::encodeResAndCalcRdSkipCU(Mode& interMode)
+{
+    pthread_once(&g_once, init_once);
+    /* the best merge candidate's prediction, coded next with residual (analysis.cpp:1739-1752) */
+    if (g_early)
+        early_post(*this, interMode, (int)interMode.cu.m_log2CUSize[0], EARLY_MERGE);
+    x265ref_encodeResAndCalcRdSkipCU(this, interMode);
+}
 
 void Search::encodeResAndCalcRdInterCU(Mode& interMode, const CUGeom& cuGeom)
 {
     pthread_once(&g_once, init_once);
     Memo& m = t_memo;
-    if (g_mode == RDO_CPU || m.active || !eligible(*this, m_csp, interMode, cuGeom))
+    if (g_mode == RDO_CPU || m.active || !eligible(*this, m_csp, interMode, (int)cuGeom.log2CUSize))
     {
         x265ref_encodeResAndCalcRdInterCU(this, interMode, cuGeom);
+        return;
+    }
+    if (g_early)
+    {
+        Early* e = early_match(*this, interMode, (int)cuGeom.log2CUSize);
+        const x265amd_rdo_result* res = nullptr;
+        struct timespec t0, t1;
+        clock_gettime(CLOCK_MONOTONIC, &t0);
+        const int rc = e ? x265amd_rdo_wait(e->rdo, e->ticket, &res) : -1;
+        clock_gettime(CLOCK_MONOTONIC, &t1);
+        g_wait_ns += (int64_t)(t1.tv_sec - t0.tv_sec) * 1000000000 + (t1.tv_nsec - t0.tv_nsec);
+        if (!e || rc)
+        {
+            if (e) { (void)x265amd_rdo_release(e->rdo, e->ticket); e->ticket = -1; }
+            g_st[ST_HOST_CUS]++;
+            x265ref_encodeResAndCalcRdInterCU(this, interMode, cuGeom);
+            return;
+        }
+        g_st[ST_POSTS]++;
+        g_st[ST_EARLY_USED]++;
+        activate(m, res, *interMode.fencYuv, interMode.predYuv, m_rqt[cuGeom.depth].tmpResiYuv, (int)cuGeom.log2CUSize);
+        x265ref_encodeResAndCalcRdInterCU(this, interMode, cuGeom);
+        m.active = false;
+        m.res = nullptr;
+        (void)x265amd_rdo_release(e->rdo, e->ticket);
+        e->ticket = -1;
         return;
     }
     const Yuv& fenc = *interMode.fencYuv;

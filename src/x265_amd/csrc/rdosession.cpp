@@ -613,6 +613,19 @@ extern "C" void x265amd_rdo_destroy(x265amd_rdo* s)
 
 namespace {
 
+// the completion flag written by a one-lane kernel instead of hipStreamWriteValue32 (X265AMD_RDO_FLAG=kernel:
+// a form rocprofv3's kernel trace can follow)
+__global__ void k_rdo_flag(uint32_t* f)
+{
+    if (threadIdx.x == 0) __hip_atomic_store(f, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+bool flag_kernel()
+{
+    static const int v = [] { const char* e = getenv("X265AMD_RDO_FLAG"); return e && !strcmp(e, "kernel") ? 1 : 0; }();
+    return v != 0;
+}
+
 // direct mode: stage the CU in the slot's mapped region and enqueue its kernels on the thread's stream
 int direct_post(x265amd_rdo* s, x265amd_rdo_thread* t, int k, const x265amd_rdo_cu* cu)
 {
@@ -711,7 +724,13 @@ int direct_post(x265amd_rdo* s, x265amd_rdo_thread* t, int k, const x265amd_rdo_
     if (o + 64 > t->region) return X265AMD_ENOMEM;
     int rc = x265amd_tu_pipeline((int)s->cfg.depth, 2, tb, t->st);
     if (!rc) rc = x265amd_pixelcmp_grouped(X265AMD_PSY, (int)s->cfg.depth, 4, pb, t->st);
-    if (!rc) rc = (int)hipStreamWriteValue32(t->st, D + t->region - 64, 1, 0);
+    if (!rc && flag_kernel())
+    {
+        hipLaunchKernelGGL(k_rdo_flag, dim3(1), dim3(64), 0, t->st, (uint32_t*)(D + t->region - 64));
+        rc = (int)hipGetLastError();
+    }
+    else if (!rc)
+        rc = (int)hipStreamWriteValue32(t->st, D + t->region - 64, 1, 0);
     return rc;
 }
 

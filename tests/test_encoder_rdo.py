@@ -72,3 +72,24 @@ def test_gpu_rdo_check_mode_every_answer_matches(tmp_path):
     m = re.search(r"\[x265rdo\] check: (\d+) mismatches", err)
     assert m and int(m.group(1)) == 0, err[-3000:]
     assert _rdo_stats(err)["tq_hit"] > 0
+
+
+def _early_stats(err):
+    m = re.search(r"\[x265rdo\] early posts merge (\d+) inter (\d+) bidir (\d+); used (\d+), dropped (\d+)", err)
+    assert m, err[-3000:]
+    return dict(zip(("merge", "inter", "bidir", "used", "dropped"), map(int, m.groups())))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["gpu", "check"])
+def test_gpu_rdo_early_posts_bit_exact(tmp_path, mode):
+    """X265AMD_RDO_EARLY=1: each CU's request is posted when its prediction becomes final (2Nx2N search, bidir,
+    best merge candidate) and taken by the encodeResAndCalcRdInterCU whose inputs it matches; the bitstream is the
+    reference's, every kind of post is made and used, and in check mode every device answer matches"""
+    err = _gpu(tmp_path, 1280, 720, 12, {"X265AMD_RDO": mode, "X265AMD_RDO_EARLY": "1"}, 5)
+    st, es = _rdo_stats(err), _early_stats(err)
+    assert es["merge"] > 0 and es["inter"] > 0 and es["bidir"] > 0 and es["used"] > 0, es
+    assert st["posts"] == es["used"] and st["tq_hit"] > 0 and st["tq_miss"] == 0, (st, es)
+    if mode == "check":
+        m = re.search(r"\[x265rdo\] check: (\d+) mismatches", err)
+        assert m and int(m.group(1)) == 0, err[-3000:]
