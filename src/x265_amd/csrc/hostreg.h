@@ -19,6 +19,8 @@
 #include <atomic>
 #include <vector>
 
+#include "devsync.h"
+
 namespace x265amd_hostreg {
 
 inline std::atomic<long long>& stale_count()
@@ -42,6 +44,7 @@ inline void unregister(const void* p, size_t bytes)
 {
     if (!p) return;
     if (!range_mapped(p, bytes)) stale_count().fetch_add(1, std::memory_order_relaxed);
+    DevSyncScope quiet;                        // (hipHostUnregister waits for every running kernel)
     (void)hipHostUnregister((void*)p);
     (void)hipGetLastError();
 }

@@ -140,6 +140,7 @@ int reserve(x265amd_la_thread* t, size_t bytes)
 {
     if (bytes <= t->cap) return 0;
     if (t->st) (void)hipStreamSynchronize(t->st);
+    DevSyncScope quiet;                        // (hipFree / hipHostFree wait for every running kernel)
     (void)hipFree(t->dev);
     (void)hipHostFree(t->host);
     t->dev = t->host = nullptr;
@@ -181,8 +182,11 @@ int thread_ctx(x265amd_la* la, x265amd_la_thread** out)
         t->wslot = la->cfg.max_frames + la->next_thread++;
         la->threads.push_back(t);
     }
-    if (hipStreamCreateWithFlags(&t->st, hipStreamNonBlocking) != hipSuccess || reserve(t, la->scratch))
-        return X265AMD_ENOMEM;
+    {
+        DevSyncScope quiet;                    // (stream creation and allocation wait for running kernels)
+        if (hipStreamCreateWithFlags(&t->st, hipStreamNonBlocking) != hipSuccess || reserve(t, la->scratch))
+            return X265AMD_ENOMEM;
+    }
     const char* sync = getenv("X265AMD_LA_SYNC");
     if (sync && !strcmp(sync, "block") &&
         hipEventCreateWithFlags(&t->ev, hipEventBlockingSync | hipEventDisableTiming) != hipSuccess)
@@ -244,6 +248,7 @@ extern "C" int x265amd_la_create(const x265amd_la_config* cfg, x265amd_la** out)
 extern "C" void x265amd_la_destroy(x265amd_la* la)
 {
     if (!la) return;
+    DevSyncScope quiet;                        // (the frees wait for running kernels)
     for (auto* t : la->threads)
     {
         if (t->st) (void)hipStreamSynchronize(t->st);
@@ -286,6 +291,7 @@ extern "C" int x265amd_la_load(x265amd_la* la, const void* key, int gen, const v
         if (it->second.pinned != buffer)
         {
             x265amd_hostreg::unregister(it->second.pinned, la->frame_bytes);
+            DevSyncScope quiet;                  // (hipHostRegister waits for every running kernel)
             it->second.pinned =
                 hipHostRegister((void*)buffer, la->frame_bytes, hipHostRegisterDefault) == hipSuccess ? buffer : nullptr;
             (void)hipGetLastError();

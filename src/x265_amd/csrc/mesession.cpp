@@ -248,6 +248,7 @@ int reserve(hipStream_t a, hipStream_t b, x265amd_mes_stage& g, size_t bytes)
     bytes = (bytes + 65535) & ~(size_t)65535;
     if (a) (void)hipStreamSynchronize(a);
     if (b) (void)hipStreamSynchronize(b);
+    DevSyncScope quiet;                        // (hipFree / hipHostFree wait for every running kernel)
     (void)hipFree(g.dev);
     (void)hipHostFree(g.host);
     g.dev = g.host = nullptr;
@@ -306,6 +307,7 @@ int thread_ctx(x265amd_mes* s, x265amd_mes_thread** out)
     auto* t = new (std::nothrow) x265amd_mes_thread();
     if (!t) return record(X265AMD_ENOMEM);
     int rc = 0;
+    DevSyncScope quiet;                        // (stream creation and allocation wait for running kernels)
     if (s->launchers.empty())
     {
         const char* sync = getenv("X265AMD_MES_SYNC");
@@ -804,10 +806,14 @@ int copy_rows(x265amd_mes* s, x265amd_mes::Picture* p, const void* const planes[
         const int64_t r1 = rows_final == s->cfg.ctu_rows ? nrows : margin + (int64_t)rows_final * rh;
         const size_t off = (size_t)(r0 * stride) * s->pix, bytes = (size_t)((r1 - r0) * stride) * s->pix;
         const size_t plane = k == 0 ? 0 : (size_t)(s->cfg.plane_elems + (k - 1) * s->cfg.cplane_elems) * s->pix;
-        const hipError_t e = st ? hipMemcpyAsync(dst + plane + off, (const uint8_t*)planes[k] + off, bytes,
-                                                 hipMemcpyHostToDevice, st)
-                                : hipMemcpy(dst + plane + off, (const uint8_t*)planes[k] + off, bytes,
-                                            hipMemcpyHostToDevice);
+        hipError_t e;
+        if (st)
+            e = hipMemcpyAsync(dst + plane + off, (const uint8_t*)planes[k] + off, bytes, hipMemcpyHostToDevice, st);
+        else
+        {
+            DevSyncScope quiet;                // (a synchronous copy waits for running kernels)
+            e = hipMemcpy(dst + plane + off, (const uint8_t*)planes[k] + off, bytes, hipMemcpyHostToDevice);
+        }
         if (e != hipSuccess) return (int)e;
         *total += bytes;
     }
@@ -928,6 +934,7 @@ extern "C" int x265amd_mes_create(const x265amd_mes_config* cfg, x265amd_mes** o
 extern "C" void x265amd_mes_destroy(x265amd_mes* s)
 {
     if (!s) return;
+    DevSyncScope quiet;                        // (the frees wait for running kernels)
     (void)use_device(s);
     stop_service(s);
     for (auto* t : s->threads) free_thread(t);
@@ -1012,6 +1019,7 @@ extern "C" int x265amd_mes_ref420(x265amd_mes* s, const void* key, int64_t gen, 
         {
             const size_t bytes = (size_t)(k ? s->cfg.cplane_elems : s->cfg.plane_elems) * s->pix;
             x265amd_hostreg::unregister(p->pinned[k], bytes);
+            DevSyncScope quiet;                  // (hipHostRegister waits for every running kernel)
             p->pinned[k] = hipHostRegister((void*)planes[k], bytes, hipHostRegisterDefault) == hipSuccess ? planes[k]
                                                                                                         : nullptr;
             (void)hipGetLastError();
@@ -1107,8 +1115,11 @@ extern "C" int x265amd_mes_table(x265amd_mes* s, const uint16_t* centre, int* in
         MES_TRY(wait(t));
     }
     else
+    {
+        DevSyncScope quiet;                    // (a synchronous copy waits for running kernels)
         MES_TRY(hipMemcpy(s->tables + (size_t)k * s->table_elems, centre - s->cfg.mvcost_range,
                           sizeof(uint16_t) * s->table_elems, hipMemcpyHostToDevice));
+    }
     s->tabs.emplace(centre, k);
     *index = k;
     return 0;

@@ -1,0 +1,40 @@
+// rdojob.h — one request of the resident residual-coding server (X265AMD_RDO_SERVER, round 6): the TU batches
+// and 8x8 psy jobs of one inter CU, laid out in the request's slot of mapped, coherent host memory by the
+// posting thread (rdosession.cpp) and served by k_rdo_server (tu.hip), which polls the slots' sequence words.
+#pragma once
+#include <stddef.h>
+#include <stdint.h>
+
+#include "../../../include/x265_amd.h"
+
+namespace x265amd {
+
+struct RdoJob
+{
+    x265amd_tu_batch tu[2];        // luma TUs (32x32), chroma TUs of both planes (16x16)
+    x265amd_cmp_batch psy[4];      // 8x8 psy: luma (fenc, pred), luma (fenc, recon), chroma (fenc, pred), (fenc, recon)
+    uint32_t pad[3];
+    uint32_t seq;                  // the request's sequence number; written last (release)
+};
+
+constexpr size_t kRdoJobFromEnd = 2048;    // the RdoJob's offset from the end of its slot
+constexpr size_t kRdoDoneFromEnd = 64;     // the done word (= seq once served) from the end of the slot
+constexpr int kRdoServerMaxOwned = 64;     // slots one server workgroup polls (nslots <= 64 x workgroups)
+constexpr int kRdoBellWord = 16;           // ctl[kRdoBellWord + g]: workgroup g's doorbell (ctl[0]: stop)
+constexpr int kRdoCtlWords = kRdoBellWord + 256;
+static_assert(sizeof(RdoJob) + kRdoDoneFromEnd <= kRdoJobFromEnd, "RdoJob does not fit its place in the slot");
+
+struct RdoServerArgs
+{
+    uint8_t* base;                 // device address of slot 0 (slot k at base + k * region)
+    uint64_t region;
+    int nslots;
+    int depth;
+    uint32_t* ctl;                 // mapped: ctl[0] = stop
+    uint64_t max_ticks;            // lifetime bound in s_memrealtime ticks (100 MHz)
+};
+
+} // namespace x265amd
+
+// launches the server (nwg workgroups) on `stream`; csrc/tu.hip
+extern "C" int x265amd_rdo_server_launch(const x265amd::RdoServerArgs* a, int nwg, int cooperative, void* stream);

@@ -34,6 +34,8 @@
 #include <vector>
 
 #include "../../../include/x265_amd.h"
+#include "rdojob.h"
+#include "devsync.h"
 
 namespace x265amd_provider {
 extern std::atomic<int> g_status;
@@ -98,6 +100,8 @@ struct x265amd_rdo_req
     std::atomic<int> state{ 0 };     // 0 free, 1 queued, 2 done
     int rc = 0;
     double t_post = 0;
+    uint32_t want = 1;               // direct mode: the completion word's value once served (1, or the server seq)
+    uint32_t seq = 0;                // server mode: the slot's last sequence number
 };
 
 struct x265amd_rdo_thread
@@ -110,6 +114,9 @@ struct x265amd_rdo_thread
     uint8_t* host = nullptr;
     uint8_t* hdev = nullptr;
     size_t region = 0;
+    hipEvent_t ev[kSlots][2] = {};   // X265AMD_RDO_TIMING=1: the device span of each slot's kernels
+    int index = -1;                  // server mode: the thread's slots are slots index * kSlots .. + kSlots - 1
+    bool owns_host = true;           // (server mode: the region is the session's)
 };
 
 struct x265amd_rdo_launcher
@@ -141,8 +148,24 @@ struct x265amd_rdo
     std::condition_variable dcv;
     int dsleepers = 0;
     int spin_us = 50, yield_us = 5000, idle_us = 500;
+    bool timing = false;
     std::mutex smu;
     x265amd_rdo_counters st{};
+    // server mode (X265AMD_RDO_SERVER=1, direct mode only): one resident kernel (tu.hip k_rdo_server) serves
+    // the slots of every posting thread, all in one mapped region; it is relaunched before its lifetime ends
+    bool server = false;
+    std::atomic<bool> srv_broken{ false };   // a request went unserved for a second: no more posts to the server
+    uint8_t* srv_host = nullptr;     // kSrvThreads * kSlots slots of `region` bytes
+    uint8_t* srv_dev = nullptr;
+    uint32_t* srv_ctl = nullptr;     // mapped: [0] stop
+    uint32_t* srv_ctl_dev = nullptr;
+    size_t srv_region = 0;
+    hipStream_t srv_st = nullptr;
+    std::mutex srv_mu;
+    std::atomic<double> srv_launched{ -1.0 };   // host time of the running server's launch (< 0: none)
+    int srv_nwg = 32;
+    bool srv_coop = true;
+    bool srv_probe = false;          // X265AMD_RDO_SERVER_PROBE=1: run the server, post nothing to it
 };
 
 namespace {
@@ -182,7 +205,10 @@ void free_thread(x265amd_rdo_thread* t)
 {
     for (auto& q : t->req) { free(q.in); if (!t->host) free(q.out); }    // direct mode: out is in the region
     if (t->st) { (void)hipStreamSynchronize(t->st); (void)hipStreamDestroy(t->st); }
-    if (t->host) (void)hipHostFree(t->host);
+    for (auto& e : t->ev)
+        for (hipEvent_t v : e)
+            if (v) (void)hipEventDestroy(v);
+    if (t->host && t->owns_host) (void)hipHostFree(t->host);
     delete t;
 }
 
@@ -191,12 +217,118 @@ size_t direct_region(size_t pix)
 {
     const Geo g(6);
     const size_t desc = 8 * (5 * (size_t)g.tus() + 3 * (size_t)g.blocks()) + (size_t)g.tus() + 64;
-    return (2 * g.pix() * pix + out_bytes(g, pix) + desc + 4095) & ~(size_t)4095;
+    return (2 * g.pix() * pix + out_bytes(g, pix) + desc + x265amd::kRdoJobFromEnd + 4095) & ~(size_t)4095;
+}
+
+int getenv_int(const char* name, int dflt);
+
+// the sessions whose server may be running, and the device-synchronising calls in progress (devsync.h)
+std::mutex g_srv_reg_mu;
+std::vector<x265amd_rdo*> g_srv_reg;
+std::atomic<int> g_quiesce{ 0 };
+
+constexpr int kSrvThreads = 64;         // posting threads a server session serves (more: their CUs stay on the host)
+constexpr double kSrvHostLife = 0.5;    // the host relaunches the server this long after its launch ...
+constexpr double kSrvGpuLife = 2.0;     // ... well before it leaves on its own
+
+int server_alloc(x265amd_rdo* s);
+
+int server_setup(x265amd_rdo* s)
+{
+    bool fresh = false;
+    {
+        std::lock_guard<std::mutex> lk(s->srv_mu);
+        if (s->srv_host) return 0;
+        if (int rc = server_alloc(s)) return rc;
+        fresh = true;
+    }
+    if (fresh)
+    {
+        // (registered without holding srv_mu: x265amd_devsync_begin takes the registry lock, then srv_mu)
+        std::lock_guard<std::mutex> rl(g_srv_reg_mu);
+        g_srv_reg.push_back(s);
+    }
+    return 0;
+}
+
+int server_alloc(x265amd_rdo* s)
+{
+    s->srv_region = direct_region(s->pix);
+    const size_t bytes = s->srv_region * kSlots * kSrvThreads;
+    // a non-blocking stream of its own; the server is a cooperative launch (tu.hip), which the runtime gives
+    // a hardware queue of its own with every workgroup resident — a resident kernel in a queue shared with
+    // other streams held back every launch behind it (the motion searches' waits went 1 -> 40-52 s per 2160p
+    // encode), and a CU-masked stream (hipExtStreamCreateWithCUMask) is a blocking stream that synchronises
+    // with the null stream
+    {
+        // X265AMD_RDO_SERVER_QUEUE: coop (default: a cooperative launch), low / high (a stream of that
+        // priority, ordinary launch)
+        const char* q = getenv("X265AMD_RDO_SERVER_QUEUE");
+        int lo = 0, hi = 0;
+        (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
+        s->srv_coop = !q || !strcmp(q, "coop");
+        const int prio = q && !strcmp(q, "low") ? lo : (q && !strcmp(q, "high") ? hi : 0);
+        if (hipStreamCreateWithPriority(&s->srv_st, hipStreamNonBlocking, prio) != hipSuccess) return X265AMD_ENOMEM;
+    }
+    if (hipHostMalloc((void**)&s->srv_host, bytes, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+        hipHostGetDevicePointer((void**)&s->srv_dev, s->srv_host, 0) != hipSuccess ||
+        hipHostMalloc((void**)&s->srv_ctl, 4 * x265amd::kRdoCtlWords, hipHostMallocMapped | hipHostMallocCoherent) !=
+            hipSuccess ||
+        hipHostGetDevicePointer((void**)&s->srv_ctl_dev, s->srv_ctl, 0) != hipSuccess)
+        return X265AMD_ENOMEM;
+    memset(s->srv_host, 0, bytes);             // every sequence and done word 0
+    memset(s->srv_ctl, 0, 4 * x265amd::kRdoCtlWords);
+    return 0;
+}
+
+// stop a session's server (it serves what it finds pending and leaves); the caller holds s->srv_mu
+int stop_server_locked(x265amd_rdo* s)
+{
+    if (s->srv_launched.load(std::memory_order_acquire) < 0) return 0;
+    __atomic_store_n(&s->srv_ctl[0], 1u, __ATOMIC_SEQ_CST);
+    const hipError_t e = hipStreamSynchronize(s->srv_st);
+    __atomic_store_n(&s->srv_ctl[0], 0u, __ATOMIC_SEQ_CST);
+    s->srv_launched.store(-1.0, std::memory_order_release);
+    return e != hipSuccess ? record((int)e) : 0;
+}
+
+// the server is running and will be for a while: relaunch it when its host-side lifetime is over (or, with
+// force, when a wait found it gone); the old one serves what it finds pending and leaves first
+int ensure_server(x265amd_rdo* s, bool force)
+{
+    const double seen = s->srv_launched.load(std::memory_order_acquire);
+    if (!force && seen >= 0 && now_s() - seen < kSrvHostLife) return 0;
+    if (g_quiesce.load(std::memory_order_acquire) > 0) return 0;          // relaunched after the device sync
+    std::lock_guard<std::mutex> lk(s->srv_mu);
+    if (g_quiesce.load(std::memory_order_acquire) > 0) return 0;
+    const double at = s->srv_launched.load(std::memory_order_acquire);
+    if (at != seen && at >= 0 && now_s() - at < kSrvHostLife) return 0;     // another thread relaunched it
+    if (int rc = stop_server_locked(s)) return rc;
+    x265amd::RdoServerArgs a{ s->srv_dev, (uint64_t)s->srv_region, kSrvThreads * kSlots, (int)s->cfg.depth,
+                              s->srv_ctl_dev, (uint64_t)(kSrvGpuLife * 1e8) };
+    const int rc = x265amd_rdo_server_launch(&a, s->srv_nwg, s->srv_coop ? 1 : 0, s->srv_st);
+    s->srv_launched.store(rc ? -1.0 : now_s(), std::memory_order_release);
+    return rc ? record(rc) : 0;
 }
 
 int direct_setup(x265amd_rdo* s, x265amd_rdo_thread* t)
 {
     if (t->host) return 0;
+    if (s->server)
+    {
+        if (t->index < 0 || t->index >= kSrvThreads) return X265AMD_ENOMEM;
+        if (int rc = server_setup(s)) return rc;
+        t->region = s->srv_region;
+        t->host = s->srv_host + (size_t)t->index * kSlots * t->region;
+        t->hdev = s->srv_dev + (size_t)t->index * kSlots * t->region;
+        t->owns_host = false;
+        for (int k = 0; k < kSlots; k++)
+        {
+            free(t->req[k].out);
+            t->req[k].out = nullptr;
+        }
+        return 0;
+    }
     int lo = 0, hi = 0;
     (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
     t->region = direct_region(s->pix);
@@ -208,6 +340,9 @@ int direct_setup(x265amd_rdo* s, x265amd_rdo_thread* t)
     {
         free(t->req[k].out);                                     // outputs live in the mapped region
         t->req[k].out = nullptr;
+        if (s->timing)
+            for (int e = 0; e < 2; e++)
+                if (hipEventCreate(&t->ev[k][e]) != hipSuccess) return X265AMD_ENOMEM;
     }
     return 0;
 }
@@ -242,6 +377,7 @@ int thread_ctx(x265amd_rdo* s, x265amd_rdo_thread** out)
             delete t;
             return X265AMD_ENOMEM;
         }
+        t->index = (int)s->threads.size();
         s->threads.push_back(t);
     }
     tls.push_back({ s, s->id, t });
@@ -556,6 +692,12 @@ extern "C" int x265amd_rdo_create(const x265amd_rdo_config* cfg, x265amd_rdo** o
     s->id = g_next_id.fetch_add(1);
     s->pix = cfg->depth > 8 ? 2 : 1;
     s->spin_us = getenv_int("X265AMD_RDO_SPIN_US", 50);
+    s->timing = getenv_int("X265AMD_RDO_TIMING", 0) != 0 && cfg->launchers == 0;
+    s->server = getenv_int("X265AMD_RDO_SERVER", 0) != 0 && cfg->launchers == 0;
+    s->srv_probe = s->server && getenv_int("X265AMD_RDO_SERVER_PROBE", 0) != 0;
+    s->srv_nwg = getenv_int("X265AMD_RDO_SERVER_WG", 32);
+    s->srv_nwg = s->srv_nwg < 4 ? 4 : (s->srv_nwg > 256 ? 256 : s->srv_nwg);
+    if (s->server) s->timing = false;
     s->yield_us = getenv_int("X265AMD_RDO_YIELD_US", 5000);
     s->idle_us = getenv_int("X265AMD_RDO_IDLE_US", 500);
     int cur = 0;
@@ -608,6 +750,20 @@ extern "C" void x265amd_rdo_destroy(x265amd_rdo* s)
         delete L;
     }
     for (auto* t : s->threads) free_thread(t);
+    {
+        std::lock_guard<std::mutex> rl(g_srv_reg_mu);
+        for (size_t i = 0; i < g_srv_reg.size(); i++)
+            if (g_srv_reg[i] == s) { g_srv_reg[i] = g_srv_reg.back(); g_srv_reg.pop_back(); break; }
+    }
+    if (s->srv_st)
+    {
+        // the server serves what is pending and leaves; then its region goes
+        if (s->srv_ctl) __atomic_store_n(&s->srv_ctl[0], 1u, __ATOMIC_SEQ_CST);
+        (void)hipStreamSynchronize(s->srv_st);
+        (void)hipStreamDestroy(s->srv_st);
+    }
+    if (s->srv_host) (void)hipHostFree(s->srv_host);
+    if (s->srv_ctl) (void)hipHostFree(s->srv_ctl);
     delete s;
 }
 
@@ -651,7 +807,7 @@ int direct_post(x265amd_rdo* s, x265amd_rdo_thread* t, int k, const x265amd_rdo_
     size_t o = (ob + out_bytes(g, pix) + 255) & ~(size_t)255;   // descriptors
     r->out = H + ob;
     volatile uint32_t* flag = (volatile uint32_t*)(H + t->region - 64);
-    *flag = 0;
+    if (!s->server) *flag = 0;
     x265amd_tu_batch tb[2];
     x265amd_cmp_batch pb[4];
     for (int cls = 0; cls < 2; cls++)
@@ -721,9 +877,27 @@ int direct_post(x265amd_rdo* s, x265amd_rdo_thread* t, int k, const x265amd_rdo_
                             (int32_t*)(D + psyr_b) + (cls ? g.nb : 0) };
         o = (o + used + 255) & ~(size_t)255;
     }
-    if (o + 64 > t->region) return X265AMD_ENOMEM;
-    int rc = x265amd_tu_pipeline((int)s->cfg.depth, 2, tb, t->st);
+    if (o + x265amd::kRdoJobFromEnd > t->region) return X265AMD_ENOMEM;
+    if (s->server)
+    {
+        // the request for the resident server: its job, then its sequence word (release: the inputs,
+        // descriptors and job are in memory before the server can see the new sequence number)
+        x265amd::RdoJob* job = (x265amd::RdoJob*)(H + t->region - x265amd::kRdoJobFromEnd);
+        for (int c = 0; c < 2; c++) job->tu[c] = tb[c];
+        for (int c = 0; c < 4; c++) job->psy[c] = pb[c];
+        r->seq++;
+        r->want = r->seq;
+        __atomic_store_n(&job->seq, r->seq, __ATOMIC_RELEASE);
+        // ring the doorbell of the workgroup that polls this slot
+        const int wg = (t->index * kSlots + k) % s->srv_nwg;
+        __atomic_fetch_add(&s->srv_ctl[x265amd::kRdoBellWord + wg], 1u, __ATOMIC_RELEASE);
+        return ensure_server(s, false);
+    }
+    r->want = 1;
+    int rc = s->timing ? (int)hipEventRecord(t->ev[k][0], t->st) : 0;
+    if (!rc) rc = x265amd_tu_pipeline((int)s->cfg.depth, 2, tb, t->st);
     if (!rc) rc = x265amd_pixelcmp_grouped(X265AMD_PSY, (int)s->cfg.depth, 4, pb, t->st);
+    if (!rc && s->timing) rc = (int)hipEventRecord(t->ev[k][1], t->st);
     if (!rc && flag_kernel())
     {
         hipLaunchKernelGGL(k_rdo_flag, dim3(1), dim3(64), 0, t->st, (uint32_t*)(D + t->region - 64));
@@ -737,18 +911,33 @@ int direct_post(x265amd_rdo* s, x265amd_rdo_thread* t, int k, const x265amd_rdo_
 int direct_wait(x265amd_rdo* s, x265amd_rdo_thread* t, int k)
 {
     volatile uint32_t* flag = (volatile uint32_t*)(t->host + (size_t)k * t->region + t->region - 64);
+    const uint32_t want = t->req[k].want;
     const double t0 = now_s();
     const double spin_until = t0 + 1e-6 * s->spin_us;
-    while (*flag != 1)
+    double next_check = t0 + 0.02;
+    while (*flag != want)
     {
         const double now = now_s();
         if (now < spin_until) { __builtin_ia32_pause(); continue; }
         sched_yield();
-        if (now - t0 > 0.05)
+        // a server stopped for a device-synchronising call is relaunched when the call is over
+        if (s->server && s->srv_launched.load(std::memory_order_acquire) < 0 &&
+            g_quiesce.load(std::memory_order_acquire) == 0)
+            if (int rc = ensure_server(s, true)) return rc;
+        if (now < next_check) continue;
+        next_check = now + 0.02;
+        // a stream that failed never writes the flag; a server that left (its lifetime over with nothing
+        // relaunched since) is relaunched
+        const hipError_t q = hipStreamQuery(s->server ? s->srv_st : t->st);
+        if (q != hipSuccess && q != hipErrorNotReady) return (int)q;
+        if (s->server && q == hipSuccess)
+            if (int rc = ensure_server(s, true)) return rc;
+        // a request no server picked up for a second is an error (sticky; the CU is coded on the host),
+        // never an endless wait
+        if (s->server && now - t0 > 1.0)
         {
-            // a stream that failed never writes the flag
-            const hipError_t q = hipStreamQuery(t->st);
-            if (q != hipSuccess && q != hipErrorNotReady) return (int)q;
+            s->srv_broken.store(true);
+            return (int)hipErrorLaunchTimeOut;
         }
     }
     __atomic_thread_fence(__ATOMIC_ACQUIRE);
@@ -771,9 +960,22 @@ extern "C" int x265amd_rdo_post(x265amd_rdo* s, const x265amd_rdo_cu* cu, int* t
     r->cu = *cu;
     if (s->launchers.empty())
     {
-        if (int rc = direct_setup(s, t)) return record(rc);
+        if (s->server && (cu->log2_cu < 5 || s->srv_broken.load(std::memory_order_relaxed)))
+            return X265AMD_ENOMEM;                                  // (the server codes 32x32 / 64x64 CUs)
+        if (s->srv_probe)
+        {
+            // (measurement: the server runs and is relaunched, every CU is coded on the host)
+            if (!server_setup(s)) (void)ensure_server(s, false);
+            return X265AMD_ENOMEM;
+        }
+        if (int rc = direct_setup(s, t)) return rc == X265AMD_ENOMEM ? rc : record(rc);
         r->t_post = now_s();
         const int rc = direct_post(s, t, k, cu);
+        {
+            // direct mode: the "queueing" counter is the worker's own posting time (staging + launches)
+            std::lock_guard<std::mutex> g(s->smu);
+            s->st.queue_ms += 1e3 * (now_s() - r->t_post);
+        }
         r->rc = rc;
         r->state.store(1, std::memory_order_release);
         *ticket = k;
@@ -817,6 +1019,15 @@ extern "C" int x265amd_rdo_wait(x265amd_rdo* s, int ticket, const x265amd_rdo_re
     {
         int rc = r->rc ? r->rc : direct_wait(s, t, ticket);
         if (!rc) set_result(r, s->pix);
+        if (rc && s->server)
+        {
+            // a server request that was not served may still be: its slot is never posted to again
+            r->state.store(3, std::memory_order_release);
+            return record(rc);
+        }
+        float span = 0.f;
+        if (!rc && s->timing && hipEventSynchronize(t->ev[ticket][1]) == hipSuccess)
+            (void)hipEventElapsedTime(&span, t->ev[ticket][0], t->ev[ticket][1]);
         r->state.store(2, std::memory_order_release);
         std::lock_guard<std::mutex> g(s->smu);
         s->st.waits++;
@@ -824,6 +1035,7 @@ extern "C" int x265amd_rdo_wait(x265amd_rdo* s, int ticket, const x265amd_rdo_re
         s->st.batches++;
         s->st.wait_ms += 1e3 * (now_s() - t0);
         s->st.batch_ms += 1e3 * (now_s() - r->t_post);
+        s->st.kernel_ms += span;
         if (rc) return record(rc);
         *out = &r->res;
         return 0;
@@ -871,4 +1083,20 @@ extern "C" int x265amd_rdo_stats(x265amd_rdo* s, x265amd_rdo_counters* out)
     std::lock_guard<std::mutex> g(s->smu);
     *out = s->st;
     return 0;
+}
+
+extern "C" void x265amd_devsync_begin(void)
+{
+    g_quiesce.fetch_add(1, std::memory_order_acq_rel);
+    std::lock_guard<std::mutex> rl(g_srv_reg_mu);
+    for (x265amd_rdo* s : g_srv_reg)
+    {
+        std::lock_guard<std::mutex> lk(s->srv_mu);
+        (void)stop_server_locked(s);
+    }
+}
+
+extern "C" void x265amd_devsync_end(void)
+{
+    g_quiesce.fetch_sub(1, std::memory_order_acq_rel);
 }

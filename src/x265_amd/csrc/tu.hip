@@ -27,9 +27,12 @@
 // coefficient kept in LDS instead of stored (it is a pure function of it).
 #include "common.h"
 #include "transform1d.h"
+#include "rdojob.h"
 #include "../../../include/x265_amd.h"
 
 namespace x265amd {
+
+#include "hadamard.h"
 
 // ---------------------------------------------------------------- scan orders
 // HEVC scans (spec 6.5.3-6.5.5; x265 g_scanOrder, constants.cpp:359-456),
@@ -331,12 +334,20 @@ struct TuArgs
     int n, is_luma, is_intra, i_slice, sign_hide, depth;
 };
 
+__host__ __device__ inline TuArgs tu_args(const x265amd_tu_batch& b, int depth)
+{
+    return TuArgs{ b.fenc, b.fenc_off, (int64_t)b.fenc_stride, b.pred, b.pred_off, (int64_t)b.pred_stride,
+                   b.resi, b.resi_off, (int64_t)b.resi_stride, b.coeff, b.coeff_off, b.recon, b.recon_off,
+                   (int64_t)b.recon_stride, b.num_sig, b.qp, b.scan, b.n, !!b.is_luma, !!b.is_intra, !!b.i_slice,
+                   !!b.sign_hide, depth };
+}
+
 // BF (round 5, default): sign hiding and the reconstruction as straight-line code — every TU group of a
 // wave computes the full inverse and the sign-hiding search, the uncoded / DC-only / coded cases are
 // selects (the DC-only shortcut, quant.cpp:526-538, equals the full inverse of a DC-only block; it is kept
 // as its own select all the same)
 template <typename P, int N, bool BF = false>
-__global__ __launch_bounds__(X265AMD_BLOCK) void k_tu(const TuArgs a)
+__device__ __forceinline__ void tu_groups(const TuArgs& a, int64_t blk)
 {
     constexpr int LOG2 = N == 4 ? 2 : N == 8 ? 3 : N == 16 ? 4 : 5;
     constexpr int PT = N + 2;                 // transposition tile pitch (int16), spreads LDS banks
@@ -345,7 +356,7 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_tu(const TuArgs a)
     __shared__ int16_t lds_t[JOBS][N * PT];   // stage tiles; DCT coefficients (pitch N) during quant/SBH
     __shared__ int16_t lds_q[JOBS][N * N];    // quantized coefficients (raster, as coeff[])
     const int slot = threadIdx.x / N, r = threadIdx.x % N;
-    const int64_t j = (int64_t)xcd_block() * JOBS + slot;
+    const int64_t j = blk * JOBS + slot;
     if (j >= a.n) return;                     // whole groups only; no block barrier below
     int16_t* T = lds_t[slot];
     int16_t* Q = lds_q[slot];
@@ -538,6 +549,13 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_tu(const TuArgs a)
     store_n<P, N>((P*)a.recon + a.recon_off[j] + r * a.recon_stride, rec);
     if (a.resi)
         store_n<int16_t, N>(a.resi + a.resi_off[j] + r * a.resi_stride, res);
+}
+
+// one workgroup = X265AMD_BLOCK / N TU groups (the body above with the workgroup's block index)
+template <typename P, int N, bool BF = false>
+__global__ __launch_bounds__(X265AMD_BLOCK) void k_tu(const TuArgs a)
+{
+    tu_groups<P, N, BF>(a, xcd_block());
 }
 
 // ---------------------------------------------------------------- 32x32 on the matrix cores
@@ -758,7 +776,7 @@ constexpr ColSumsTu make_colsums_tu()
 static __constant__ ColSumsTu c_colsum128_tu = make_colsums_tu();
 
 template <typename P>
-__global__ __launch_bounds__(X265AMD_BLOCK) void k_tu32_i8(const TuArgs a)
+__device__ __forceinline__ void tu32_i8_waves(const TuArgs& a, int64_t blk, int64_t nblk)
 {
     __shared__ int16_t lds_c[kTuWaves][32 * 32];   // DCT coefficients; later the inverse output
     __shared__ int16_t lds_q[kTuWaves][32 * 32];   // quantized coefficients
@@ -795,8 +813,8 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_tu32_i8(const TuArgs a)
     const int fk2 = (1 << (fsh2 - 1)), fk20 = h == 0 ? 128 * 64 * 32 : 0;
     const int icol = c_colsum128_tu.v[r];
 
-    const int64_t step = (int64_t)gridDim.x * kTuWaves;
-    for (int64_t j = (int64_t)blockIdx.x * kTuWaves + w; j < a.n; j += step)
+    const int64_t step = nblk * kTuWaves;
+    for (int64_t j = blk * kTuWaves + w; j < a.n; j += step)
     {
         const P* pf = (const P*)a.fenc + a.fenc_off[j];
         const P* pp = (const P*)a.pred + a.pred_off[j];
@@ -921,6 +939,12 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_tu32_i8(const TuArgs a)
         if (a.resi) store_n<int16_t, 16>(a.resi + a.resi_off[j] + io_row * a.resi_stride + io_col, res);
         wave_sync();                                 // LDS reuse by the next TU of this wave
     }
+}
+
+template <typename P>
+__global__ __launch_bounds__(X265AMD_BLOCK) void k_tu32_i8(const TuArgs a)
+{
+    tu32_i8_waves<P>(a, blockIdx.x, gridDim.x);
 }
 
 // ---------------------------------------------------------------- 4x4: one lane per TU
@@ -1146,6 +1170,155 @@ static int launch_tu(int log2, const TuArgs& a, hipStream_t st)
     return (int)hipGetLastError();
 }
 
+// ---------------------------------------------------------------- the resident residual-coding server
+// X265AMD_RDO_SERVER (round 6; rdojob.h, rdosession.cpp): one launch serves every request of a session for its
+// lifetime, so a CU's residual coding costs no launches — the posting thread writes the CU's inputs,
+// descriptors and RdoJob into its slot of mapped host memory and then the slot's sequence word; a workgroup
+// polls the sequence words of its slots (slot g, g + G, ...), runs the CU's luma TUs (tu32_i8_waves: a wave per
+// 32x32 TU), its chroma TUs (tu_groups<16>) and its 8x8 psy energies against the prediction and the
+// reconstruction (psy_energy8, hadamard.h), then writes the slot's done word.  Every workgroup leaves when the
+// stop word is set or its lifetime (max_ticks of the 100 MHz real-time counter) has passed — after serving what
+// it finds pending in one last poll; the host relaunches before the lifetime ends (and whenever a wait finds the
+// server gone), so nothing posted is left unserved and no launch outlives its bound.
+__device__ __forceinline__ uint32_t ld_sys(const uint32_t* p)
+{
+    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+template <typename P>
+__global__ __launch_bounds__(X265AMD_BLOCK) void k_rdo_server(const RdoServerArgs a)
+{
+    __shared__ uint32_t s_done[kRdoServerMaxOwned];
+    __shared__ int s_pick;
+    __shared__ uint32_t s_seq;
+    __shared__ int s_leave;
+    __shared__ RdoJob s_job;
+    const int g = blockIdx.x, G = gridDim.x;
+    const int owned = (a.nslots - g + G - 1) / G;            // <= kRdoServerMaxOwned (host-checked)
+    auto slot = [&](int i) { return a.base + (size_t)(g + i * G) * a.region; };
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    for (int i = threadIdx.x; i < owned; i += blockDim.x)
+        s_done[i] = ld_sys((const uint32_t*)(slot(i) + a.region - kRdoDoneFromEnd));
+    // the workgroup's doorbell (bumped by every post to one of its slots): while it is unchanged and nothing
+    // was pending at the last scan, one word is read per poll instead of every slot's sequence word
+    const uint32_t* bell = a.ctl + kRdoBellWord + g;
+    uint32_t seen_bell = ld_sys(bell) - 1u;                  // (scan once at the start)
+    bool leaving = false;
+    int last = -1, budget = 0;
+    for (;;)
+    {
+        __syncthreads();
+        if (threadIdx.x < 64)
+        {
+            // wave 0 polls: the doorbell, then (if it moved, or work was found last time) the sequence words;
+            // the first pending slot after the last one served (round robin) is served next
+            const int i = threadIdx.x;
+            const uint32_t b = ld_sys(bell);
+            const bool scan = b != seen_bell || last >= 0;
+            seen_bell = b;
+            bool pend = false;
+            if (scan && i < owned)
+                pend = ld_sys((const uint32_t*)(slot(i) + a.region - kRdoJobFromEnd + offsetof(RdoJob, seq))) != s_done[i];
+            const uint64_t m = __ballot(pend);
+            if (i == 0)
+            {
+                int pick = -1;
+                if (m)
+                {
+                    const uint64_t after = last + 1 < 64 ? (m >> (last + 1)) << (last + 1) : 0;
+                    pick = (int)__builtin_ctzll(after ? after : m);
+                }
+                s_pick = pick;
+                const bool stop = ld_sys(a.ctl) != 0 || __builtin_amdgcn_s_memrealtime() - t0 > a.max_ticks;
+                s_leave = stop ? 1 : 0;
+            }
+        }
+        __syncthreads();
+        const int pick = s_pick;
+        if (s_leave && !leaving)
+        {
+            leaving = true;
+            budget = owned;                                  // at most one more request per slot, then leave
+        }
+        if (pick < 0 || (leaving && budget-- <= 0))
+        {
+            if (leaving) break;                              // nothing pending in the last poll (or budget spent)
+            last = -1;                                       // idle: the doorbell only, about every 2 us
+            __builtin_amdgcn_s_sleep(80);
+            continue;
+        }
+        last = pick;
+        uint8_t* base = slot(pick);
+        if (threadIdx.x == 0)
+            s_seq = ld_sys((const uint32_t*)(base + a.region - kRdoJobFromEnd + offsetof(RdoJob, seq)));
+        // the job and its inputs were written before the sequence word (release): read them fresh
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+        {
+            const uint32_t* src = (const uint32_t*)(base + a.region - kRdoJobFromEnd);
+            uint32_t* dst = (uint32_t*)&s_job;
+            for (int i = threadIdx.x; i < (int)(offsetof(RdoJob, seq) / 4); i += blockDim.x) dst[i] = src[i];
+        }
+        __syncthreads();
+        // (a request is one 64x64 or 32x32 CU: 4 / 1 luma TUs, 8 / 2 chroma TUs, at most 64 8x8 blocks a
+        // batch; anything else is not served, only marked done)
+        const bool sane = s_job.tu[0].log2_size == 5 && s_job.tu[1].log2_size == 4 && s_job.tu[0].n >= 0 &&
+                          s_job.tu[0].n <= 4 && s_job.tu[1].n >= 0 && s_job.tu[1].n <= 8 &&
+                          s_job.psy[0].n >= 0 && s_job.psy[0].n <= 64 && s_job.psy[1].n >= 0 && s_job.psy[1].n <= 64 &&
+                          s_job.psy[2].n >= 0 && s_job.psy[2].n <= 32 && s_job.psy[3].n >= 0 && s_job.psy[3].n <= 32;
+        if (sane)
+        {
+            tu32_i8_waves<P>(tu_args(s_job.tu[0], a.depth), 0, 1);
+            tu_groups<P, 16, false>(tu_args(s_job.tu[1], a.depth), 0);
+        }
+        // the reconstruction the waves wrote is read back by others for its psy energies
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        __syncthreads();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        {
+            const int n0 = s_job.psy[0].n, n1 = s_job.psy[1].n, n2 = s_job.psy[2].n, n3 = s_job.psy[3].n;
+            const int total = sane ? n0 + n1 + n2 + n3 : 0;
+            for (int q = threadIdx.x; q < total; q += blockDim.x)
+            {
+                int b = 0, j = q;
+                if (j >= n0) { j -= n0; b = 1; if (j >= n1) { j -= n1; b = 2; if (j >= n2) { j -= n2; b = 3; } } }
+                const x265amd_cmp_batch& c = s_job.psy[b];
+                const P* pa = (const P*)c.a + c.a_off[j];
+                const P* pb = (const P*)c.b + c.b_off[j];
+                const int e = psy_energy8<P>(pa, c.a_stride) - psy_energy8<P>(pb, c.b_stride);
+                ((int32_t*)c.out)[j] = e < 0 ? -e : e;
+            }
+        }
+        // every output of the request is visible to the host before its done word
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        __syncthreads();
+        if (threadIdx.x == 0)
+        {
+            __hip_atomic_store((uint32_t*)(base + a.region - kRdoDoneFromEnd), s_seq, __ATOMIC_RELEASE,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+            s_done[pick] = s_seq;
+        }
+    }
+}
+
+} // namespace x265amd
+
+extern "C" int x265amd_rdo_server_launch(const x265amd::RdoServerArgs* a, int nwg, int cooperative, void* stream)
+{
+    using namespace x265amd;
+    if (!a || !a->base || !a->ctl || nwg < 1 || a->nslots < 1 || a->nslots > nwg * kRdoServerMaxOwned ||
+        a->region < kRdoJobFromEnd || (a->depth != 8 && a->depth != 10 && a->depth != 12))
+        return X265AMD_EINVAL;
+    // a cooperative launch: every workgroup is resident at once (a workgroup waiting for a free CU would leave
+    // its slots unserved), in the runtime's own queue for cooperative work, apart from the streams' queues
+    RdoServerArgs args = *a;
+    void* params[] = { &args };
+    const void* f = a->depth == 8 ? (const void*)k_rdo_server<uint8_t> : (const void*)k_rdo_server<uint16_t>;
+    if (cooperative)
+        return (int)hipLaunchCooperativeKernel(f, dim3(nwg), dim3(X265AMD_BLOCK), params, 0, (hipStream_t)stream);
+    return (int)hipLaunchKernel(f, dim3(nwg), dim3(X265AMD_BLOCK), params, 0, (hipStream_t)stream);
+}
+
+namespace x265amd {
 } // namespace x265amd
 
 using namespace x265amd;
@@ -1168,10 +1341,7 @@ extern "C" int x265amd_tu_pipeline(int depth, int count, const x265amd_tu_batch*
     {
         const x265amd_tu_batch& b = bt[i];
         if (!b.n) continue;
-        TuArgs a{ b.fenc, b.fenc_off, (int64_t)b.fenc_stride, b.pred, b.pred_off, (int64_t)b.pred_stride,
-                  b.resi, b.resi_off, (int64_t)b.resi_stride, b.coeff, b.coeff_off, b.recon, b.recon_off,
-                  (int64_t)b.recon_stride, b.num_sig, b.qp, b.scan, b.n, !!b.is_luma, !!b.is_intra, !!b.i_slice,
-                  !!b.sign_hide, depth };
+        const TuArgs a = tu_args(b, depth);
         const int rc = depth == 8 ? launch_tu<uint8_t>(b.log2_size, a, st) : launch_tu<uint16_t>(b.log2_size, a, st);
         if (rc) return rc;
     }

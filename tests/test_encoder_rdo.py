@@ -80,13 +80,21 @@ def _early_stats(err):
     return dict(zip(("merge", "inter", "bidir", "used", "dropped"), map(int, m.groups())))
 
 
+FORMS = {"service": {}, "direct": {"X265AMD_RDO_LAUNCHERS": "0"},
+         "server": {"X265AMD_RDO_LAUNCHERS": "0", "X265AMD_RDO_SERVER": "1"}}
+
+
 @pytest.mark.gpu
+@pytest.mark.parametrize("form", list(FORMS))
 @pytest.mark.parametrize("mode", ["gpu", "check"])
-def test_gpu_rdo_early_posts_bit_exact(tmp_path, mode):
+def test_gpu_rdo_early_posts_bit_exact(tmp_path, mode, form):
     """X265AMD_RDO_EARLY=1: each CU's request is posted when its prediction becomes final (2Nx2N search, bidir,
     best merge candidate) and taken by the encodeResAndCalcRdInterCU whose inputs it matches; the bitstream is the
-    reference's, every kind of post is made and used, and in check mode every device answer matches"""
-    err = _gpu(tmp_path, 1280, 720, 12, {"X265AMD_RDO": mode, "X265AMD_RDO_EARLY": "1"}, 5)
+    reference's, every kind of post is made and used, and in check mode every device answer matches.  Forms: the
+    launch service, direct launches by the worker, and the resident server kernel (X265AMD_RDO_SERVER: no launch
+    per CU; tu.hip k_rdo_server polls the slots)"""
+    env = {"X265AMD_RDO": mode, "X265AMD_RDO_EARLY": "1", **FORMS[form]}
+    err = _gpu(tmp_path, 1280, 720, 12, env, 5)
     st, es = _rdo_stats(err), _early_stats(err)
     assert es["merge"] > 0 and es["inter"] > 0 and es["bidir"] > 0 and es["used"] > 0, es
     assert st["posts"] == es["used"] and st["tq_hit"] > 0 and st["tq_miss"] == 0, (st, es)
