@@ -70,6 +70,9 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true", help="skip the reference encoder's one-core sample")
     ap.add_argument("--no-replay", action="store_true", help="skip the primitive-workload replay (N = 1)")
     ap.add_argument("--env", action="append", default=[], help="extra KEY=VALUE for the hooked encoder")
+    ap.add_argument("--rdo", choices=["server", "off"], default="server",
+                    help="inter residual coding of 64x64 CUs on the device through the resident server "
+                         "(integration/gpu_rdo.cpp, X265AMD_RDO_SERVER; DESIGN §14), or on the host")
     ap.add_argument("--second-res", type=int, nargs=2, default=[1920, 1080], metavar=("W", "H"),
                     help="BASELINE's other resolution, timed after the headline one (reported under "
                          "`resolutions`; --second-res 0 0 skips it)")
@@ -212,6 +215,19 @@ def parse_me_stats(err: str):
     m = re.search(r"stats prefetches (\d+) searches (\d+) memo hits (\d+) misses (\d+)", err)
     if m:
         out.update(prefetches=int(m.group(1)), memo_hits=int(m.group(3)), memo_misses=int(m.group(4)))
+    # inter residual coding (integration/gpu_rdo.cpp print_stats)
+    m = re.search(r"\[x265rdo\] stats CUs posted (\d+) coded on the host (\d+); transformNxN memo hits (\d+) misses (\d+);"
+                  r".*?worker wait ([\d.]+) s", err)
+    if m:
+        rdo = dict(cus_on_device=int(m.group(1)), cus_on_host=int(m.group(2)), tq_memo_hits=int(m.group(3)),
+                   tq_memo_misses=int(m.group(4)), worker_wait_s=float(m.group(5)))
+        m = re.search(r"\[x265rdo\] early posts merge (\d+) inter (\d+) bidir (\d+); used (\d+), dropped (\d+)", err)
+        if m:
+            rdo.update(early_posts=int(m.group(1)) + int(m.group(2)) + int(m.group(3)), early_used=int(m.group(4)))
+        m = re.search(r"\[x265rdo\] service: .*? batch ([\d.]+) ms, queueing ([\d.]+) ms per CU", err)
+        if m:
+            rdo.update(post_to_result_ms=float(m.group(1)), posting_ms_per_cu=float(m.group(2)))
+        out["rdo"] = rdo
     return out
 
 
@@ -317,10 +333,18 @@ def main():
     pools = str(len(cpus))
     extra = ["--preset", args.preset, "--pools", pools]
     env = dict(os.environ, HIP_VISIBLE_DEVICES=str(local), X265AMD_ME_STATS="1")
+    if args.rdo == "server":
+        # each 64x64 inter CU's residual coding posted when its prediction is final and served by the resident
+        # kernel (measured faster than the host and than per-CU launches)
+        env.update(X265AMD_RDO="gpu", X265AMD_RDO_EARLY="1", X265AMD_RDO_LAUNCHERS="0", X265AMD_RDO_SERVER="1")
     if args.host_rehearsal:
-        # the hooks' host forms (integration/: the same forming, posting and memo, the searches and estimates
-        # by the reference's own functions): the rank plumbing on a machine without the GPU, NOT a measurement
+        # the hooks' host forms (integration/: the same forming, posting and memo, the searches, estimates and
+        # residual coding by the reference's own functions): the rank plumbing on a machine without the GPU,
+        # NOT a measurement
         env.update(X265AMD_ME="host", X265AMD_LOOKAHEAD="host")
+        env.update(X265AMD_RDO="host" if args.rdo == "server" else "cpu")
+        for k in ("X265AMD_RDO_EARLY", "X265AMD_RDO_LAUNCHERS", "X265AMD_RDO_SERVER"):
+            env.pop(k, None)
     env.update(kv.split("=", 1) for kv in args.env)
     ref_env = dict(os.environ, X265AMD_LOOKAHEAD="cpu", X265AMD_ME="cpu")
 
@@ -372,7 +396,8 @@ def main():
     if second is not None:
         res[f"{second['H']}p"] = arm_summary(second)
     what = (f"x265 1.9 --preset {args.preset}, {H}p {D}-bit, {F}-frame synthetic clip per GPU, reference encoder with "
-            "its lookahead estimates and motion searches on the MI355X")
+            "its lookahead estimates, motion searches" + (" and inter residual coding" if args.rdo == "server" else "")
+            + " on the MI355X")
     line = {
         # a bitstream that differs from the reference's on any rank voids the number: value null, exit 1
         "metric": f"encoded fps ({what}, " + ("bitstream identical to the reference" if identical else

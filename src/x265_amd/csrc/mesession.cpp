@@ -48,6 +48,17 @@ extern std::atomic<int> g_status;
 }
 
 namespace {
+// X265AMD_DEVSYNC_COPIES=1: the workers' synchronous row uploads stop a resident RDO server first (measured
+// unnecessary: a synchronous copy on the null stream does not wait for the server's non-blocking stream, and the
+// guard costs a server stop per upload; profiles/r06/rdo_server_ab.jsonl, call r06zf)
+bool guard_copies()
+{
+    static const bool v = [] { const char* e = getenv("X265AMD_DEVSYNC_COPIES"); return e && *e == '1'; }();
+    return v;
+}
+} // namespace
+
+namespace {
 
 int record(int st)
 {
@@ -809,11 +820,13 @@ int copy_rows(x265amd_mes* s, x265amd_mes::Picture* p, const void* const planes[
         hipError_t e;
         if (st)
             e = hipMemcpyAsync(dst + plane + off, (const uint8_t*)planes[k] + off, bytes, hipMemcpyHostToDevice, st);
-        else
+        else if (guard_copies())
         {
-            DevSyncScope quiet;                // (a synchronous copy waits for running kernels)
+            DevSyncScope quiet;                // (a synchronous copy may wait for running kernels)
             e = hipMemcpy(dst + plane + off, (const uint8_t*)planes[k] + off, bytes, hipMemcpyHostToDevice);
         }
+        else
+            e = hipMemcpy(dst + plane + off, (const uint8_t*)planes[k] + off, bytes, hipMemcpyHostToDevice);
         if (e != hipSuccess) return (int)e;
         *total += bytes;
     }
