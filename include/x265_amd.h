@@ -928,6 +928,12 @@ int  x265amd_rdo_post(x265amd_rdo* rdo, const x265amd_rdo_cu* cu, int* ticket);
 int  x265amd_rdo_wait(x265amd_rdo* rdo, int ticket, const x265amd_rdo_result** out);
 int  x265amd_rdo_release(x265amd_rdo* rdo, int ticket);
 int  x265amd_rdo_stats(x265amd_rdo* rdo, x265amd_rdo_counters* out);
+/* Resident server (X265AMD_RDO_SERVER=1 with launchers == 0: one kernel serves every request; no reference
+ * counterpart).  HIP entries that synchronise the whole device (hipHostRegister / hipHostUnregister, hipFree,
+ * hipStreamCreate) wait for every running kernel, the server too: a caller brackets such calls with these
+ * (nesting allowed), which stop the running servers and hold their relaunch until the last end. */
+void x265amd_devsync_begin(void);
+void x265amd_devsync_end(void);
 
 /* host buffers (Lowres / PicYuv planes page-locked by an f1 or f2 session) that were already freed or
  * unmapped when their session unregistered them, over the process: must stay 0 (a freed registered range
