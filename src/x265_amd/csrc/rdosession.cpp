@@ -163,7 +163,7 @@ struct x265amd_rdo
     hipStream_t srv_st = nullptr;
     std::mutex srv_mu;
     std::atomic<double> srv_launched{ -1.0 };   // host time of the running server's launch (< 0: none)
-    int srv_nwg = 32;
+    int srv_nwg = 16;
     bool srv_coop = true;
     bool srv_probe = false;          // X265AMD_RDO_SERVER_PROBE=1: run the server, post nothing to it
 };
@@ -695,7 +695,10 @@ extern "C" int x265amd_rdo_create(const x265amd_rdo_config* cfg, x265amd_rdo** o
     s->timing = getenv_int("X265AMD_RDO_TIMING", 0) != 0 && cfg->launchers == 0;
     s->server = getenv_int("X265AMD_RDO_SERVER", 0) != 0 && cfg->launchers == 0;
     s->srv_probe = s->server && getenv_int("X265AMD_RDO_SERVER_PROBE", 0) != 0;
-    s->srv_nwg = getenv_int("X265AMD_RDO_SERVER_WG", 32);
+    // 16 workgroups: fewer queue the CUs longer, more slow the motion-search kernel running beside them
+    // (8 / 12 / 16 / 20 / 24 / 32: 11.0 / 11.5 / 12.3-12.5 / 12.3 / 12.1 / 11.7 fps at 2160p, profiles/r06/
+    // rdo_server_ab.jsonl calls r06zh-r06zi)
+    s->srv_nwg = getenv_int("X265AMD_RDO_SERVER_WG", 16);
     s->srv_nwg = s->srv_nwg < 4 ? 4 : (s->srv_nwg > 256 ? 256 : s->srv_nwg);
     if (s->server) s->timing = false;
     s->yield_us = getenv_int("X265AMD_RDO_YIELD_US", 5000);
