@@ -1180,9 +1180,13 @@ static int launch_tu(int log2, const TuArgs& a, hipStream_t st)
 // stop word is set or its lifetime (max_ticks of the 100 MHz real-time counter) has passed — after serving what
 // it finds pending in one last poll; the host relaunches before the lifetime ends (and whenever a wait finds the
 // server gone), so nothing posted is left unserved and no launch outlives its bound.
+// a word the host writes, read past the caches (global_load sc0 sc1) and WITHOUT acquire ordering: a
+// system-scope acquire is a buffer_inv sc0 sc1, which invalidates the XCD's L2 — at every poll of every
+// workgroup it slowed the motion-search kernel beside the server (0.025 -> 0.037 ms per launch).  The one
+// acquire a request needs is taken once, after its sequence word was seen.
 __device__ __forceinline__ uint32_t ld_sys(const uint32_t* p)
 {
-    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 template <typename P>
@@ -1251,8 +1255,10 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_rdo_server(const RdoServerArg
         uint8_t* base = slot(pick);
         if (threadIdx.x == 0)
             s_seq = ld_sys((const uint32_t*)(base + a.region - kRdoJobFromEnd + offsetof(RdoJob, seq)));
-        // the job and its inputs were written before the sequence word (release): read them fresh
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+        // the job and its inputs were written before the sequence word (release): read them fresh.  They are
+        // in fine-grained host memory, never held by the L2 as device data is: an agent-scope acquire (the
+        // CU's L1 and the L2's non-coherent lines) suffices, and leaves the device's L2 lines alone
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         {
             const uint32_t* src = (const uint32_t*)(base + a.region - kRdoJobFromEnd);
             uint32_t* dst = (uint32_t*)&s_job;
@@ -1270,8 +1276,9 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_rdo_server(const RdoServerArg
             tu32_i8_waves<P>(tu_args(s_job.tu[0], a.depth), 0, 1);
             tu_groups<P, 16, false>(tu_args(s_job.tu[1], a.depth), 0);
         }
-        // the reconstruction the waves wrote is read back by others for its psy energies
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        // the reconstruction the waves wrote (to host memory) is read back by others for its psy energies:
+        // their stores complete (workgroup release: s_waitcnt), then the readers' L1 is invalidated
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __syncthreads();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         {
@@ -1293,7 +1300,8 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_rdo_server(const RdoServerArg
         __syncthreads();
         if (threadIdx.x == 0)
         {
-            __hip_atomic_store((uint32_t*)(base + a.region - kRdoDoneFromEnd), s_seq, __ATOMIC_RELEASE,
+            // (ordered after the outputs by the system-scope release fence above: one L2 write-back a request)
+            __hip_atomic_store((uint32_t*)(base + a.region - kRdoDoneFromEnd), s_seq, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_SYSTEM);
             s_done[pick] = s_seq;
         }
