@@ -19,6 +19,14 @@ struct RdoJob
 
 constexpr size_t kRdoJobFromEnd = 2048;    // the RdoJob's offset from the end of its slot
 constexpr size_t kRdoDoneFromEnd = 64;     // the done word (= seq once served) from the end of the slot
+constexpr size_t kRdoStampsFromEnd = 256;  // X265AMD_RDO_TIMING: 6 real-time stamps of the request's phases
+// slot layout (direct and server mode): the CU's packed inputs from 0 (fenc Y Cb Cr, pred Y Cb Cr; room for a
+// 64x64 CU), its descriptors from rdo_desc_at(), its outputs from rdo_out_at(); the server stages the first
+// rdo_out_at() bytes in LDS
+constexpr size_t kRdoMaxPix = 64 * 64 + 2 * 32 * 32;
+constexpr size_t kRdoDescBytes = 4096;
+__host__ __device__ constexpr size_t rdo_desc_at(size_t bytes_per_pixel) { return 2 * kRdoMaxPix * bytes_per_pixel; }
+__host__ __device__ constexpr size_t rdo_out_at(size_t bytes_per_pixel) { return rdo_desc_at(bytes_per_pixel) + kRdoDescBytes; }
 constexpr int kRdoServerMaxOwned = 64;     // slots one server workgroup polls (nslots <= 64 x workgroups)
 constexpr int kRdoBellWord = 16;           // ctl[kRdoBellWord + g]: workgroup g's doorbell (ctl[0]: stop)
 constexpr int kRdoCtlWords = kRdoBellWord + 256;
@@ -32,6 +40,7 @@ struct RdoServerArgs
     int depth;
     uint32_t* ctl;                 // mapped: ctl[0] = stop
     uint64_t max_ticks;            // lifetime bound in s_memrealtime ticks (100 MHz)
+    int timing;                    // write the phase stamps of every request (kRdoStampsFromEnd)
 };
 
 } // namespace x265amd

@@ -166,6 +166,9 @@ struct x265amd_rdo
     int srv_nwg = 16;
     bool srv_coop = true;
     bool srv_probe = false;          // X265AMD_RDO_SERVER_PROBE=1: run the server, post nothing to it
+    bool srv_timing = false;         // X265AMD_RDO_SERVER_TIMING=1: phase stamps of every request, printed at destroy
+    double srv_phase[5] = {};        // job copy, luma TUs, chroma TUs, psy, release (us, summed)
+    int64_t srv_stamped = 0;
 };
 
 namespace {
@@ -216,8 +219,7 @@ void free_thread(x265amd_rdo_thread* t)
 size_t direct_region(size_t pix)
 {
     const Geo g(6);
-    const size_t desc = 8 * (5 * (size_t)g.tus() + 3 * (size_t)g.blocks()) + (size_t)g.tus() + 64;
-    return (2 * g.pix() * pix + out_bytes(g, pix) + desc + x265amd::kRdoJobFromEnd + 4095) & ~(size_t)4095;
+    return (x265amd::rdo_out_at(pix) + out_bytes(g, pix) + x265amd::kRdoJobFromEnd + 4095) & ~(size_t)4095;
 }
 
 int getenv_int(const char* name, int dflt);
@@ -261,13 +263,15 @@ int server_alloc(x265amd_rdo* s)
     // encode), and a CU-masked stream (hipExtStreamCreateWithCUMask) is a blocking stream that synchronises
     // with the null stream
     {
-        // X265AMD_RDO_SERVER_QUEUE: coop (default: a cooperative launch), low / high (a stream of that
-        // priority, ordinary launch)
+        // X265AMD_RDO_SERVER_QUEUE: low (default: an ordinary launch on a stream of the lowest priority, which
+        // no other stream of the library uses, so it has a hardware queue to itself), coop (a cooperative
+        // launch: the same speed, but rocprofv3's kernel trace crashes at the exit of a process that made one),
+        // high, normal (a stream of that priority; normal shares a queue: slow)
         const char* q = getenv("X265AMD_RDO_SERVER_QUEUE");
         int lo = 0, hi = 0;
         (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
-        s->srv_coop = !q || !strcmp(q, "coop");
-        const int prio = q && !strcmp(q, "low") ? lo : (q && !strcmp(q, "high") ? hi : 0);
+        s->srv_coop = q && !strcmp(q, "coop");
+        const int prio = !q || !strcmp(q, "low") ? lo : (!strcmp(q, "high") ? hi : 0);
         if (hipStreamCreateWithPriority(&s->srv_st, hipStreamNonBlocking, prio) != hipSuccess) return X265AMD_ENOMEM;
     }
     if (hipHostMalloc((void**)&s->srv_host, bytes, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
@@ -305,7 +309,7 @@ int ensure_server(x265amd_rdo* s, bool force)
     if (at != seen && at >= 0 && now_s() - at < kSrvHostLife) return 0;     // another thread relaunched it
     if (int rc = stop_server_locked(s)) return rc;
     x265amd::RdoServerArgs a{ s->srv_dev, (uint64_t)s->srv_region, kSrvThreads * kSlots, (int)s->cfg.depth,
-                              s->srv_ctl_dev, (uint64_t)(kSrvGpuLife * 1e8) };
+                              s->srv_ctl_dev, (uint64_t)(kSrvGpuLife * 1e8), s->srv_timing ? 1 : 0 };
     const int rc = x265amd_rdo_server_launch(&a, s->srv_nwg, s->srv_coop ? 1 : 0, s->srv_st);
     s->srv_launched.store(rc ? -1.0 : now_s(), std::memory_order_release);
     return rc ? record(rc) : 0;
@@ -695,6 +699,7 @@ extern "C" int x265amd_rdo_create(const x265amd_rdo_config* cfg, x265amd_rdo** o
     s->timing = getenv_int("X265AMD_RDO_TIMING", 0) != 0 && cfg->launchers == 0;
     s->server = getenv_int("X265AMD_RDO_SERVER", 0) != 0 && cfg->launchers == 0;
     s->srv_probe = s->server && getenv_int("X265AMD_RDO_SERVER_PROBE", 0) != 0;
+    s->srv_timing = s->server && getenv_int("X265AMD_RDO_SERVER_TIMING", 0) != 0;
     // 16 workgroups: fewer queue the CUs longer, more slow the motion-search kernel running beside them
     // (8 / 12 / 16 / 20 / 24 / 32: 11.0 / 11.5 / 12.3-12.5 / 12.3 / 12.1 / 11.7 fps at 2160p, profiles/r06/
     // rdo_server_ab.jsonl calls r06zh-r06zi)
@@ -765,6 +770,11 @@ extern "C" void x265amd_rdo_destroy(x265amd_rdo* s)
         (void)hipStreamSynchronize(s->srv_st);
         (void)hipStreamDestroy(s->srv_st);
     }
+    if (s->srv_timing && s->srv_stamped)
+        fprintf(stderr, "[x265rdo] server phases over %lld requests (us each): job %.2f, luma TUs %.2f, chroma TUs %.2f, "
+                        "psy %.2f, release %.2f\n", (long long)s->srv_stamped, s->srv_phase[0] / s->srv_stamped,
+                s->srv_phase[1] / s->srv_stamped, s->srv_phase[2] / s->srv_stamped, s->srv_phase[3] / s->srv_stamped,
+                s->srv_phase[4] / s->srv_stamped);
     if (s->srv_host) (void)hipHostFree(s->srv_host);
     if (s->srv_ctl) (void)hipHostFree(s->srv_ctl);
     delete s;
@@ -803,11 +813,11 @@ int direct_post(x265amd_rdo* s, x265amd_rdo_thread* t, int k, const x265amd_rdo_
             const intptr_t st = (src ? cu->pred_stride[p] : cu->fenc_stride[p]) * (intptr_t)pix;
             for (int y = 0; y < w; y++, d += w * pix) memcpy(d, a + y * st, w * pix);
         }
-    const size_t ob = 2 * g.pix() * pix;                      // outputs (the out_bytes layout, set_result)
+    const size_t ob = x265amd::rdo_out_at(pix);              // outputs (the out_bytes layout, set_result)
     const size_t resi_b = ob + g.pix() * pix, coeff_b = resi_b + 2 * g.pix();
     const size_t sig_b = coeff_b + 2 * g.pix(), psyp_b = sig_b + 4 * (size_t)g.tus();
     const size_t psyr_b = psyp_b + 4 * (size_t)g.blocks();
-    size_t o = (ob + out_bytes(g, pix) + 255) & ~(size_t)255;   // descriptors
+    size_t o = x265amd::rdo_desc_at(pix);                       // descriptors (rdojob.h slot layout)
     r->out = H + ob;
     volatile uint32_t* flag = (volatile uint32_t*)(H + t->region - 64);
     if (!s->server) *flag = 0;
@@ -880,7 +890,7 @@ int direct_post(x265amd_rdo* s, x265amd_rdo_thread* t, int k, const x265amd_rdo_
                             (int32_t*)(D + psyr_b) + (cls ? g.nb : 0) };
         o = (o + used + 255) & ~(size_t)255;
     }
-    if (o + x265amd::kRdoJobFromEnd > t->region) return X265AMD_ENOMEM;
+    if (o > ob || ob + out_bytes(g, pix) + x265amd::kRdoJobFromEnd > t->region) return X265AMD_ENOMEM;
     if (s->server)
     {
         // the request for the resident server: its job, then its sequence word (release: the inputs,
@@ -1022,6 +1032,14 @@ extern "C" int x265amd_rdo_wait(x265amd_rdo* s, int ticket, const x265amd_rdo_re
     {
         int rc = r->rc ? r->rc : direct_wait(s, t, ticket);
         if (!rc) set_result(r, s->pix);
+        if (!rc && s->server && s->srv_timing)
+        {
+            const uint64_t* st = (const uint64_t*)(t->host + (size_t)ticket * t->region + t->region -
+                                                   x265amd::kRdoStampsFromEnd);
+            std::lock_guard<std::mutex> g(s->smu);
+            for (int p = 0; p < 5; p++) s->srv_phase[p] += 1e-2 * (double)(st[p + 1] - st[p]);   // 100 MHz -> us
+            s->srv_stamped++;
+        }
         if (rc && s->server)
         {
             // a server request that was not served may still be: its slot is never posted to again

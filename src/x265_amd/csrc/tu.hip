@@ -25,6 +25,8 @@
 // lane — CGs are independent (quant.cpp:273-391) except for the last-position
 // search, which is a group max — with deltaU recomputed from the DCT
 // coefficient kept in LDS instead of stored (it is a pure function of it).
+#include <type_traits>
+
 #include "common.h"
 #include "transform1d.h"
 #include "rdojob.h"
@@ -1197,6 +1199,9 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_rdo_server(const RdoServerArg
     __shared__ uint32_t s_seq;
     __shared__ int s_leave;
     __shared__ RdoJob s_job;
+    // the request's inputs and descriptors, staged from host memory in one round trip (rdojob.h slot layout)
+    constexpr int kStage = (int)rdo_out_at(sizeof(P));
+    __shared__ __attribute__((aligned(16))) uint8_t s_in[kStage];
     const int g = blockIdx.x, G = gridDim.x;
     const int owned = (a.nslots - g + G - 1) / G;            // <= kRdoServerMaxOwned (host-checked)
     auto slot = [&](int i) { return a.base + (size_t)(g + i * G) * a.region; };
@@ -1253,6 +1258,8 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_rdo_server(const RdoServerArg
         }
         last = pick;
         uint8_t* base = slot(pick);
+        uint64_t* stamps = (uint64_t*)(base + a.region - kRdoStampsFromEnd);
+        const uint64_t ts0 = a.timing ? __builtin_amdgcn_s_memrealtime() : 0;
         if (threadIdx.x == 0)
             s_seq = ld_sys((const uint32_t*)(base + a.region - kRdoJobFromEnd + offsetof(RdoJob, seq)));
         // the job and its inputs were written before the sequence word (release): read them fresh.  They are
@@ -1260,9 +1267,57 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_rdo_server(const RdoServerArg
         // CU's L1 and the L2's non-coherent lines) suffices, and leaves the device's L2 lines alone
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         {
-            const uint32_t* src = (const uint32_t*)(base + a.region - kRdoJobFromEnd);
-            uint32_t* dst = (uint32_t*)&s_job;
-            for (int i = threadIdx.x; i < (int)(offsetof(RdoJob, seq) / 4); i += blockDim.x) dst[i] = src[i];
+            // the job and the slot's first kStage bytes (inputs, descriptors): every load issued before the
+            // first store, one PCIe round trip
+            constexpr int NJ = (int)(offsetof(RdoJob, seq) / 4), NI = kStage / 16;
+            constexpr int PJ = (NJ + X265AMD_BLOCK - 1) / X265AMD_BLOCK, PI = (NI + X265AMD_BLOCK - 1) / X265AMD_BLOCK;
+            const uint32_t* srcj = (const uint32_t*)(base + a.region - kRdoJobFromEnd);
+            const uint4* srci = (const uint4*)base;
+            uint32_t vj[PJ];
+            uint4 vi[PI];
+#pragma unroll
+            for (int k = 0; k < PJ; k++)
+            {
+                const int i = threadIdx.x + k * X265AMD_BLOCK;
+                vj[k] = srcj[i < NJ ? i : 0];
+            }
+#pragma unroll
+            for (int k = 0; k < PI; k++)
+            {
+                const int i = threadIdx.x + k * X265AMD_BLOCK;
+                vi[k] = srci[i < NI ? i : 0];
+            }
+#pragma unroll
+            for (int k = 0; k < PJ; k++)
+                if (threadIdx.x + k * X265AMD_BLOCK < NJ) ((uint32_t*)&s_job)[threadIdx.x + k * X265AMD_BLOCK] = vj[k];
+#pragma unroll
+            for (int k = 0; k < PI; k++)
+                if (threadIdx.x + k * X265AMD_BLOCK < NI) ((uint4*)s_in)[threadIdx.x + k * X265AMD_BLOCK] = vi[k];
+        }
+        __syncthreads();
+        if (threadIdx.x == 0)
+        {
+            // every pointer of the job into the staged bytes now points into LDS (outputs stay in host memory)
+            const uintptr_t lo = (uintptr_t)base, hi = lo + kStage;
+            uint8_t* lds = (uint8_t*)s_in;
+            auto rel = [&](auto& ptr) {
+                const uintptr_t v = (uintptr_t)ptr;
+                if (v >= lo && v < hi) ptr = (std::remove_reference_t<decltype(ptr)>)(void*)(lds + (v - lo));
+            };
+            for (int c = 0; c < 2; c++)
+            {
+                x265amd_tu_batch& b = s_job.tu[c];
+                rel(b.fenc); rel(b.fenc_off); rel(b.pred); rel(b.pred_off); rel(b.resi_off); rel(b.coeff_off);
+                rel(b.recon_off); rel(b.qp);
+            }
+            for (int c = 0; c < 4; c++)
+            {
+                // (batches 1 and 3 compare against the reconstruction, an output: their b stays in host memory —
+                // every batch's b is the slot base, told apart only by its offsets)
+                x265amd_cmp_batch& b = s_job.psy[c];
+                rel(b.a); rel(b.a_off); rel(b.b_off);
+                if (!(c & 1)) rel(b.b);
+            }
         }
         __syncthreads();
         // (a request is one 64x64 or 32x32 CU: 4 / 1 luma TUs, 8 / 2 chroma TUs, at most 64 8x8 blocks a
@@ -1271,10 +1326,14 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_rdo_server(const RdoServerArg
                           s_job.tu[0].n <= 4 && s_job.tu[1].n >= 0 && s_job.tu[1].n <= 8 &&
                           s_job.psy[0].n >= 0 && s_job.psy[0].n <= 64 && s_job.psy[1].n >= 0 && s_job.psy[1].n <= 64 &&
                           s_job.psy[2].n >= 0 && s_job.psy[2].n <= 32 && s_job.psy[3].n >= 0 && s_job.psy[3].n <= 32;
+        const uint64_t ts1 = a.timing ? __builtin_amdgcn_s_memrealtime() : 0;
+        uint64_t ts2 = 0, ts3 = 0;
         if (sane)
         {
             tu32_i8_waves<P>(tu_args(s_job.tu[0], a.depth), 0, 1);
+            if (a.timing) { __syncthreads(); ts2 = __builtin_amdgcn_s_memrealtime(); }
             tu_groups<P, 16, false>(tu_args(s_job.tu[1], a.depth), 0);
+            if (a.timing) { __syncthreads(); ts3 = __builtin_amdgcn_s_memrealtime(); }
         }
         // the reconstruction the waves wrote (to host memory) is read back by others for its psy energies:
         // their stores complete (workgroup release: s_waitcnt), then the readers' L1 is invalidated
@@ -1296,8 +1355,16 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_rdo_server(const RdoServerArg
             }
         }
         // every output of the request is visible to the host before its done word
+        if (a.timing) __syncthreads();
+        const uint64_t ts4 = a.timing ? __builtin_amdgcn_s_memrealtime() : 0;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
         __syncthreads();
+        if (threadIdx.x == 0 && a.timing)
+        {
+            const uint64_t ts5 = __builtin_amdgcn_s_memrealtime();
+            stamps[0] = ts0; stamps[1] = ts1; stamps[2] = ts2; stamps[3] = ts3; stamps[4] = ts4; stamps[5] = ts5;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        }
         if (threadIdx.x == 0)
         {
             // (ordered after the outputs by the system-scope release fence above: one L2 write-back a request)
