@@ -41,6 +41,10 @@ struct RdoServerArgs
     uint32_t* ctl;                 // mapped: ctl[0] = stop
     uint64_t max_ticks;            // lifetime bound in s_memrealtime ticks (100 MHz)
     int timing;                    // write the phase stamps of every request (kRdoStampsFromEnd)
+    // device-memory input slots (large-BAR hosts, X265AMD_RDO_SERVER_VRAM): slot k's staged bytes at
+    // in_base + k * in_region, its RdoJob right after them (rdo_out_at); null: both in the host slot
+    uint8_t* in_base;
+    uint64_t in_region;
 };
 
 } // namespace x265amd

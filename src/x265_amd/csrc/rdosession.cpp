@@ -167,6 +167,13 @@ struct x265amd_rdo
     bool srv_coop = true;
     bool srv_probe = false;          // X265AMD_RDO_SERVER_PROBE=1: run the server, post nothing to it
     bool srv_timing = false;         // X265AMD_RDO_SERVER_TIMING=1: phase stamps of every request, printed at destroy
+    // device-memory input slots and control words (large-BAR hosts; X265AMD_RDO_SERVER_VRAM=0: host memory):
+    // the host writes each request's inputs, descriptors, job and sequence word straight into device memory
+    // through the BAR (no reads), so the server stages them from HBM instead of across PCIe
+    uint8_t* srv_in = nullptr;
+    size_t srv_in_region = 0;
+    uint32_t* srv_vctl = nullptr;    // (in srv_in's allocation) [0] stop, [kRdoBellWord + g] doorbells
+    std::atomic<uint32_t> srv_bells[256];
     double srv_phase[5] = {};        // job copy, luma TUs, chroma TUs, psy, release (us, summed)
     int64_t srv_stamped = 0;
 };
@@ -282,16 +289,47 @@ int server_alloc(x265amd_rdo* s)
         return X265AMD_ENOMEM;
     memset(s->srv_host, 0, bytes);             // every sequence and done word 0
     memset(s->srv_ctl, 0, 4 * x265amd::kRdoCtlWords);
+    int dev = 0, large_bar = 0;
+    if (getenv_int("X265AMD_RDO_SERVER_VRAM", 1) != 0 && hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&large_bar, hipDeviceAttributeIsLargeBar, dev) == hipSuccess && large_bar)
+    {
+        s->srv_in_region = (x265amd::rdo_out_at(s->pix) + sizeof(x265amd::RdoJob) + 255) & ~(size_t)255;
+        const size_t in_bytes = s->srv_in_region * kSlots * kSrvThreads + 4 * x265amd::kRdoCtlWords;
+        if (hipExtMallocWithFlags((void**)&s->srv_in, in_bytes, hipDeviceMallocFinegrained) == hipSuccess &&
+            hipMemset(s->srv_in, 0, in_bytes) == hipSuccess && hipDeviceSynchronize() == hipSuccess)
+        {
+            s->srv_vctl = (uint32_t*)(s->srv_in + s->srv_in_region * kSlots * kSrvThreads);
+            for (auto& b : s->srv_bells) b.store(0);
+        }
+        else
+        {
+            if (s->srv_in) (void)hipFree(s->srv_in);
+            s->srv_in = nullptr;
+            (void)hipGetLastError();
+        }
+    }
     return 0;
+}
+
+// the server's stop word (host or device memory; plain stores to device memory, fenced: write-combined)
+void set_stop(x265amd_rdo* s, uint32_t v)
+{
+    if (s->srv_vctl)
+    {
+        *(volatile uint32_t*)&s->srv_vctl[0] = v;
+        __builtin_ia32_sfence();
+    }
+    else
+        __atomic_store_n(&s->srv_ctl[0], v, __ATOMIC_SEQ_CST);
 }
 
 // stop a session's server (it serves what it finds pending and leaves); the caller holds s->srv_mu
 int stop_server_locked(x265amd_rdo* s)
 {
     if (s->srv_launched.load(std::memory_order_acquire) < 0) return 0;
-    __atomic_store_n(&s->srv_ctl[0], 1u, __ATOMIC_SEQ_CST);
+    set_stop(s, 1u);
     const hipError_t e = hipStreamSynchronize(s->srv_st);
-    __atomic_store_n(&s->srv_ctl[0], 0u, __ATOMIC_SEQ_CST);
+    set_stop(s, 0u);
     s->srv_launched.store(-1.0, std::memory_order_release);
     return e != hipSuccess ? record((int)e) : 0;
 }
@@ -309,7 +347,8 @@ int ensure_server(x265amd_rdo* s, bool force)
     if (at != seen && at >= 0 && now_s() - at < kSrvHostLife) return 0;     // another thread relaunched it
     if (int rc = stop_server_locked(s)) return rc;
     x265amd::RdoServerArgs a{ s->srv_dev, (uint64_t)s->srv_region, kSrvThreads * kSlots, (int)s->cfg.depth,
-                              s->srv_ctl_dev, (uint64_t)(kSrvGpuLife * 1e8), s->srv_timing ? 1 : 0 };
+                              s->srv_vctl ? s->srv_vctl : s->srv_ctl_dev, (uint64_t)(kSrvGpuLife * 1e8),
+                              s->srv_timing ? 1 : 0, s->srv_in, (uint64_t)s->srv_in_region };
     const int rc = x265amd_rdo_server_launch(&a, s->srv_nwg, s->srv_coop ? 1 : 0, s->srv_st);
     s->srv_launched.store(rc ? -1.0 : now_s(), std::memory_order_release);
     return rc ? record(rc) : 0;
@@ -766,7 +805,7 @@ extern "C" void x265amd_rdo_destroy(x265amd_rdo* s)
     if (s->srv_st)
     {
         // the server serves what is pending and leaves; then its region goes
-        if (s->srv_ctl) __atomic_store_n(&s->srv_ctl[0], 1u, __ATOMIC_SEQ_CST);
+        if (s->srv_ctl) set_stop(s, 1u);
         (void)hipStreamSynchronize(s->srv_st);
         (void)hipStreamDestroy(s->srv_st);
     }
@@ -777,6 +816,7 @@ extern "C" void x265amd_rdo_destroy(x265amd_rdo* s)
                 s->srv_phase[4] / s->srv_stamped);
     if (s->srv_host) (void)hipHostFree(s->srv_host);
     if (s->srv_ctl) (void)hipHostFree(s->srv_ctl);
+    if (s->srv_in) (void)hipFree(s->srv_in);
     delete s;
 }
 
@@ -803,8 +843,13 @@ int direct_post(x265amd_rdo* s, x265amd_rdo_thread* t, int k, const x265amd_rdo_
     const Geo g(cu->log2_cu);
     uint8_t* H = t->host + (size_t)k * t->region;
     uint8_t* D = t->hdev + (size_t)k * t->region;
+    // where the inputs and descriptors go: the slot itself, or (server with device-memory input slots) the
+    // slot's input area in device memory, which the host writes through the BAR at the same address
+    uint8_t* I = H;
+    uint8_t* DI = D;
+    if (s->server && s->srv_in) I = DI = s->srv_in + (size_t)(t->index * kSlots + k) * s->srv_in_region;
     // inputs: fenc Y Cb Cr then pred Y Cb Cr, packed
-    uint8_t* d = H;
+    uint8_t* d = I;
     for (int src = 0; src < 2; src++)
         for (int p = 0; p < 3; p++)
         {
@@ -827,7 +872,7 @@ int direct_post(x265amd_rdo* s, x265amd_rdo_thread* t, int k, const x265amd_rdo_
     {
         const int w = cls ? g.cc : g.c, tl = cls ? g.tlc : g.tl, n = 1 << tl;
         const int nt = cls ? 2 * g.ntuc : g.ntu, nb = cls ? 2 * g.nbc : g.nb;
-        int64_t* fo = (int64_t*)(H + o);
+        int64_t* fo = (int64_t*)(I + o);
         int64_t* po = fo + nt;
         int64_t* ro = po + nt;
         int64_t* co = ro + nt;
@@ -860,17 +905,17 @@ int direct_post(x265amd_rdo* s, x265amd_rdo_thread* t, int k, const x265amd_rdo_
                 pr[b] = (int64_t)(ob / pix) + poff + e;
             }
         }
-        auto dv = [&](const void* hp) { return (const void*)(D + ((const uint8_t*)hp - H)); };
+        auto dv = [&](const void* hp) { return (const void*)(DI + ((const uint8_t*)hp - I)); };
         x265amd_tu_batch& B = tb[cls];
         B = x265amd_tu_batch{};
         B.log2_size = tl;
         B.n = nt;
         B.is_luma = !cls;
         B.sign_hide = s->cfg.sign_hide;
-        B.fenc = D;
+        B.fenc = DI;
         B.fenc_stride = w;
         B.fenc_off = (const int64_t*)dv(fo);
-        B.pred = D;
+        B.pred = DI;
         B.pred_stride = w;
         B.pred_off = (const int64_t*)dv(po);
         B.resi = (int16_t*)D;
@@ -884,9 +929,9 @@ int direct_post(x265amd_rdo* s, x265amd_rdo_thread* t, int k, const x265amd_rdo_
         // num_sig and the psy energies of one class are contiguous in the outputs (luma, then Cb, then Cr)
         B.num_sig = (uint32_t*)(D + sig_b) + (cls ? g.ntu : 0);
         B.qp = (const uint8_t*)dv(qp);
-        pb[2 * cls] = { 8, 8, nb, D, w, (const int64_t*)dv(pa), D, w, (const int64_t*)dv(pbb),
+        pb[2 * cls] = { 8, 8, nb, DI, w, (const int64_t*)dv(pa), DI, w, (const int64_t*)dv(pbb),
                         (int32_t*)(D + psyp_b) + (cls ? g.nb : 0) };
-        pb[2 * cls + 1] = { 8, 8, nb, D, w, (const int64_t*)dv(pa), D, w, (const int64_t*)dv(pr),
+        pb[2 * cls + 1] = { 8, 8, nb, DI, w, (const int64_t*)dv(pa), D, w, (const int64_t*)dv(pr),
                             (int32_t*)(D + psyr_b) + (cls ? g.nb : 0) };
         o = (o + used + 255) & ~(size_t)255;
     }
@@ -895,15 +940,29 @@ int direct_post(x265amd_rdo* s, x265amd_rdo_thread* t, int k, const x265amd_rdo_
     {
         // the request for the resident server: its job, then its sequence word (release: the inputs,
         // descriptors and job are in memory before the server can see the new sequence number)
-        x265amd::RdoJob* job = (x265amd::RdoJob*)(H + t->region - x265amd::kRdoJobFromEnd);
+        x265amd::RdoJob* job = (x265amd::RdoJob*)(s->srv_in ? I + x265amd::rdo_out_at(pix)
+                                                             : H + t->region - x265amd::kRdoJobFromEnd);
         for (int c = 0; c < 2; c++) job->tu[c] = tb[c];
         for (int c = 0; c < 4; c++) job->psy[c] = pb[c];
         r->seq++;
         r->want = r->seq;
-        __atomic_store_n(&job->seq, r->seq, __ATOMIC_RELEASE);
-        // ring the doorbell of the workgroup that polls this slot
         const int wg = (t->index * kSlots + k) % s->srv_nwg;
-        __atomic_fetch_add(&s->srv_ctl[x265amd::kRdoBellWord + wg], 1u, __ATOMIC_RELEASE);
+        if (s->srv_in)
+        {
+            // device memory through the BAR is write-combined: fence the inputs and job before the sequence
+            // word, and the sequence word before the doorbell (never read back: BAR reads are slow)
+            __builtin_ia32_sfence();
+            *(volatile uint32_t*)&job->seq = r->seq;
+            __builtin_ia32_sfence();
+            *(volatile uint32_t*)&s->srv_vctl[x265amd::kRdoBellWord + wg] = s->srv_bells[wg].fetch_add(1) + 1;
+            __builtin_ia32_sfence();
+        }
+        else
+        {
+            __atomic_store_n(&job->seq, r->seq, __ATOMIC_RELEASE);
+            // ring the doorbell of the workgroup that polls this slot
+            __atomic_fetch_add(&s->srv_ctl[x265amd::kRdoBellWord + wg], 1u, __ATOMIC_RELEASE);
+        }
         return ensure_server(s, false);
     }
     r->want = 1;

@@ -1205,6 +1205,11 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_rdo_server(const RdoServerArg
     const int g = blockIdx.x, G = gridDim.x;
     const int owned = (a.nslots - g + G - 1) / G;            // <= kRdoServerMaxOwned (host-checked)
     auto slot = [&](int i) { return a.base + (size_t)(g + i * G) * a.region; };
+    // where slot i's staged bytes and job are: its device-memory input slot, or the host slot itself
+    auto in_slot = [&](int i) { return a.in_base ? a.in_base + (size_t)(g + i * G) * a.in_region : slot(i); };
+    auto job_of = [&](int i) {
+        return a.in_base ? in_slot(i) + kStage : slot(i) + a.region - kRdoJobFromEnd;
+    };
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     for (int i = threadIdx.x; i < owned; i += blockDim.x)
         s_done[i] = ld_sys((const uint32_t*)(slot(i) + a.region - kRdoDoneFromEnd));
@@ -1227,7 +1232,7 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_rdo_server(const RdoServerArg
             seen_bell = b;
             bool pend = false;
             if (scan && i < owned)
-                pend = ld_sys((const uint32_t*)(slot(i) + a.region - kRdoJobFromEnd + offsetof(RdoJob, seq))) != s_done[i];
+                pend = ld_sys((const uint32_t*)(job_of(i) + offsetof(RdoJob, seq))) != s_done[i];
             const uint64_t m = __ballot(pend);
             if (i == 0)
             {
@@ -1258,10 +1263,11 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_rdo_server(const RdoServerArg
         }
         last = pick;
         uint8_t* base = slot(pick);
+        uint8_t* ibase = in_slot(pick);
+        const uint8_t* jbase = job_of(pick);
         uint64_t* stamps = (uint64_t*)(base + a.region - kRdoStampsFromEnd);
         const uint64_t ts0 = a.timing ? __builtin_amdgcn_s_memrealtime() : 0;
-        if (threadIdx.x == 0)
-            s_seq = ld_sys((const uint32_t*)(base + a.region - kRdoJobFromEnd + offsetof(RdoJob, seq)));
+        if (threadIdx.x == 0) s_seq = ld_sys((const uint32_t*)(jbase + offsetof(RdoJob, seq)));
         // the job and its inputs were written before the sequence word (release): read them fresh.  They are
         // in fine-grained host memory, never held by the L2 as device data is: an agent-scope acquire (the
         // CU's L1 and the L2's non-coherent lines) suffices, and leaves the device's L2 lines alone
@@ -1271,10 +1277,13 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_rdo_server(const RdoServerArg
             // first store, one PCIe round trip
             constexpr int NJ = (int)(offsetof(RdoJob, seq) / 4), NI = kStage / 16;
             constexpr int PJ = (NJ + X265AMD_BLOCK - 1) / X265AMD_BLOCK, PI = (NI + X265AMD_BLOCK - 1) / X265AMD_BLOCK;
-            const uint32_t* srcj = (const uint32_t*)(base + a.region - kRdoJobFromEnd);
-            const uint4* srci = (const uint4*)base;
+            // (volatile: flat_load sc0 sc1, past every cache — the host writes these bytes, through the PCIe
+            // BAR when they are in device memory, and no GPU cache may hold an older copy)
+            typedef unsigned v4u __attribute__((ext_vector_type(4)));
+            const volatile uint32_t* srcj = (const volatile uint32_t*)jbase;
+            const volatile v4u* srci = (const volatile v4u*)ibase;
             uint32_t vj[PJ];
-            uint4 vi[PI];
+            v4u vi[PI];
 #pragma unroll
             for (int k = 0; k < PJ; k++)
             {
@@ -1292,13 +1301,13 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_rdo_server(const RdoServerArg
                 if (threadIdx.x + k * X265AMD_BLOCK < NJ) ((uint32_t*)&s_job)[threadIdx.x + k * X265AMD_BLOCK] = vj[k];
 #pragma unroll
             for (int k = 0; k < PI; k++)
-                if (threadIdx.x + k * X265AMD_BLOCK < NI) ((uint4*)s_in)[threadIdx.x + k * X265AMD_BLOCK] = vi[k];
+                if (threadIdx.x + k * X265AMD_BLOCK < NI) ((v4u*)s_in)[threadIdx.x + k * X265AMD_BLOCK] = vi[k];
         }
         __syncthreads();
         if (threadIdx.x == 0)
         {
             // every pointer of the job into the staged bytes now points into LDS (outputs stay in host memory)
-            const uintptr_t lo = (uintptr_t)base, hi = lo + kStage;
+            const uintptr_t lo = (uintptr_t)ibase, hi = lo + kStage;
             uint8_t* lds = (uint8_t*)s_in;
             auto rel = [&](auto& ptr) {
                 const uintptr_t v = (uintptr_t)ptr;
