@@ -814,12 +814,20 @@ def run_gpu(case: Case, prims, device="cuda", guard=None) -> dict:
     survived (a kernel writing outside its outputs shows up there, not as a wrong result)."""
     import torch
 
-    def dev(v):
-        if isinstance(v, np.ndarray):
-            return torch.from_numpy(np.ascontiguousarray(v)).to(device)
-        return v
+    def dev(k, v):
+        if not isinstance(v, np.ndarray):
+            return v
+        h = np.ascontiguousarray(v)
+        try:
+            return torch.from_numpy(h).to(device)
+        except Exception:
+            # (an asynchronous device error surfacing here: say where the copy's host side was)
+            print(f"run_gpu: copy of {case.key()} buffer {k} failed: host {h.ctypes.data:#x} + {h.nbytes} bytes; "
+                  f"device memory allocated {torch.cuda.memory_allocated()} reserved {torch.cuda.memory_reserved()}",
+                  flush=True)
+            raise
 
-    b = {k: dev(v) for k, v in case.bufs.items()}
+    b = {k: dev(k, v) for k, v in case.bufs.items()}
     boxes = {}
     if guard is not None:
         for k in case.outs:
