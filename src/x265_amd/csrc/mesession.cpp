@@ -128,6 +128,8 @@ struct x265amd_mes_launcher
     hipStream_t st = nullptr;
     hipEvent_t done = nullptr, k0 = nullptr, k1 = nullptr;
     x265amd_mes_stage g;
+    uint8_t* vin = nullptr;     // X265AMD_MES_ZEROCOPY=3: the batch inputs in device memory the host writes
+    size_t vcap = 0;            // through the large BAR (write-combined, never read back)
     std::thread th;
 };
 
@@ -217,8 +219,11 @@ struct x265amd_mes
     int dsleepers = 0;                // waiters sleeping on dcv (guarded by dmu)
     std::atomic<int64_t> queued{ 0 }; // requests posted (the launchers' lock-free "anything new?" check)
     int trace = 0;                    // X265AMD_MES_TRACE=n: log the first n posts / launches / waits
-    int zerocopy = 0;                 // X265AMD_MES_ZEROCOPY=1: the kernel reads / writes the pinned staging;
-                                      // 2: it writes its outputs there (inputs still uploaded)
+    int zerocopy = 3;                 // X265AMD_MES_ZEROCOPY (default 3, round 6; 0: staged copies both ways)
+                                      // 1: the kernel reads / writes the pinned staging;
+                                      // 2: it writes its outputs there (inputs still uploaded); 3: the host
+                                      // writes the inputs straight into device memory (large BAR) and the kernel
+                                      // writes its outputs into the pinned staging: no copies at all
     bool prio = true;                 // X265AMD_MES_PRIORITY=0: launch streams at the default priority
     bool lspin = false;               // X265AMD_MES_LSPIN=1: launchers poll for completion (a busy core each:
                                       // slower on the encoder's 16-core budget, profiles/r05/bench_lspin_pinned_ab.txt)
@@ -496,6 +501,28 @@ static int hist_bin(double ms)
 int copy_rows(x265amd_mes* s, x265amd_mes::Picture* p, const void* const planes[3], int rows_final, hipStream_t st,
               size_t* total);
 
+// grow the launcher's device-memory input buffer to its staging's capacity (fine-grained device memory the
+// host writes through the large BAR); without a large BAR or on failure the launcher keeps the copies
+void reserve_vin(x265amd_mes_launcher* L)
+{
+    (void)hipStreamSynchronize(L->st);
+    DevSyncScope quiet;                        // (hipFree / hipExtMallocWithFlags wait for every running kernel)
+    if (L->vin) (void)hipFree(L->vin);
+    L->vin = nullptr;
+    L->vcap = 0;
+    int dev = 0, large_bar = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&large_bar, hipDeviceAttributeIsLargeBar, dev) !=
+        hipSuccess || !large_bar)
+        return;
+    if (hipExtMallocWithFlags((void**)&L->vin, L->g.cap, hipDeviceMallocFinegrained) != hipSuccess)
+    {
+        L->vin = nullptr;
+        (void)hipGetLastError();
+        return;
+    }
+    L->vcap = L->g.cap;
+}
+
 void launcher_main(x265amd_mes* s, x265amd_mes_launcher* L)
 {
     (void)hipSetDevice(s->cfg.device);
@@ -582,13 +609,18 @@ void launcher_main(x265amd_mes* s, x265amd_mes_launcher* L)
         }
         int rc = reserve(L->st, nullptr, L->g, total);
         int njobs = 0;
+        if (!rc && s->zerocopy == 3 && L->g.hdev && L->vcap < L->g.cap) reserve_vin(L);
+        // mode 3: inputs written into device memory (the kernel reads them there), outputs into the pinned staging
+        const bool v3 = s->zerocopy == 3 && L->g.hdev && L->vin;
+        uint8_t* const in_host = v3 ? L->vin : L->g.host;
+        uint8_t* const in_dev = v3 ? L->vin : L->g.dev;
         if (!rc)
         {
             for (size_t k = 0; k < sizes.size(); k++)
             {
                 const int w = sizes[k].first, kh = sizes[k].second, h = kh < 0 ? -kh : kh;
                 const size_t cblk = (size_t)(w / 2) * (h / 2);
-                uint8_t* H = L->g.host + base[k];
+                uint8_t* H = in_host + base[k];
                 const Layout& Ly = lay[k];
                 int i = 0, p = 0;
                 for (auto* r : take)
@@ -606,16 +638,16 @@ void launcher_main(x265amd_mes* s, x265amd_mes_launcher* L)
                     order.push_back(r);
                     p++;
                 }
-                x265amd_mes_stage sub{ L->g.dev + base[k], L->g.host + base[k], nullptr, Ly.end };
+                x265amd_mes_stage sub{ in_dev + base[k], in_host + base[k], nullptr, Ly.end };
                 bt.push_back(make_batch(s, sub, Ly, w, h, i, w));
                 if (kh < 0) chroma_batch(s, sub, Ly, w, h, p, bt.back());
                 bt.back().eval_count = (uint32_t*)(sub.dev + Ly.evals);
                 njobs += i;
             }
-            if (s->zerocopy == 2 && L->g.hdev)
+            if ((s->zerocopy == 2 && L->g.hdev) || v3)
             {
                 // the kernel writes its outputs straight into the pinned staging (no download copy)
-                const ptrdiff_t d = L->g.hdev - L->g.dev;
+                const ptrdiff_t d = L->g.hdev - in_dev;
                 for (size_t k = 0; k < bt.size(); k++)
                 {
                     x265amd_me_batch& b = bt[k];
@@ -624,7 +656,7 @@ void launcher_main(x265amd_mes* s, x265amd_mes_launcher* L)
                     if (b.eval_count) b.eval_count = (uint32_t*)((uint8_t*)b.eval_count + d);
                 }
             }
-            else if (s->zerocopy && L->g.hdev)
+            else if (s->zerocopy == 1 && L->g.hdev)
             {
                 // the kernel reads the descriptors and source blocks from the pinned staging and writes its
                 // outputs there (no copies): the batch addresses are the host staging's
@@ -697,12 +729,14 @@ void launcher_main(x265amd_mes* s, x265amd_mes_launcher* L)
                     }
             }
             // one upload of every size's inputs (the output regions ride along: staging is contiguous)
-            if (!rc && !(s->zerocopy == 1 && L->g.hdev))
+            if (!rc && !(s->zerocopy == 1 && L->g.hdev) && !v3)
                 rc = (int)hipMemcpyAsync(L->g.dev, L->g.host, total, hipMemcpyHostToDevice, L->st);
+            // (the write-combined stores into device memory drain before the launch's doorbell)
+            if (v3) __builtin_ia32_sfence();
             if (!rc) rc = (int)hipEventRecord(L->k0, L->st);
             if (!rc) rc = x265amd_motion_search(s->cfg.depth, (int)bt.size(), bt.data(), L->st);
             if (!rc) rc = (int)hipEventRecord(L->k1, L->st);
-            for (size_t k = 0; k < sizes.size() && !rc && !(s->zerocopy && L->g.hdev); k++)
+            for (size_t k = 0; k < sizes.size() && !rc && !(s->zerocopy && L->g.hdev) && !v3; k++)
                 rc = (int)hipMemcpyAsync(L->g.host + base[k] + lay[k].out_mv, L->g.dev + base[k] + lay[k].out_mv,
                                          lay[k].end - lay[k].out_mv, hipMemcpyDeviceToHost, L->st);
             if (!rc) rc = (int)hipEventRecord(L->done, L->st);
@@ -890,6 +924,7 @@ void stop_service(x265amd_mes* s)
         if (L->st) (void)hipStreamSynchronize(L->st);
         (void)hipFree(L->g.dev);
         (void)hipHostFree(L->g.host);
+        if (L->vin) (void)hipFree(L->vin);
         if (L->st) (void)hipStreamDestroy(L->st);
         for (hipEvent_t e : { L->done, L->k0, L->k1 })
             if (e) (void)hipEventDestroy(e);

@@ -184,9 +184,13 @@ def test_gpu_me_encode_2160p_medium_is_bit_exact(tmp_path):
 
 
 @pytest.mark.gpu
-def test_gpu_me_check_mode_every_search_matches(tmp_path):
-    """X265AMD_ME=check: every device search the encoder uses is recomputed on the host and compared"""
-    err = _gpu_encode_equals_reference(tmp_path, 1280, 720, 12, {"X265AMD_ME": "check"})
+@pytest.mark.parametrize("transfer", ["3", "0", "1"])
+def test_gpu_me_check_mode_every_search_matches(tmp_path, transfer):
+    """X265AMD_ME=check: every device search the encoder uses is recomputed on the host and compared — for each
+    form of the launch service's transfer (X265AMD_MES_ZEROCOPY): 3 the default, inputs written by the host into
+    device memory through the BAR and outputs written by the kernel into host memory; 0 staged copies both
+    ways; 1 the kernel reads and writes host memory"""
+    err = _gpu_encode_equals_reference(tmp_path, 1280, 720, 12, {"X265AMD_ME": "check", "X265AMD_MES_ZEROCOPY": transfer})
     m = re.search(r"check: (\d+) mismatching searches", err)
     assert m and int(m.group(1)) == 0, err[-3000:]
 

@@ -50,7 +50,8 @@ def main():
                 e = dict(os.environ, X265AMD_ME_STATS="1", **env)
                 f, w, m, err = bench.x265_run(os.path.join(R, "x265la8"), src, a.width, a.height, 8, a.frames,
                                               ["--preset", "medium", "--pools", str(pools), *extra], env=e, cpus=cpus)
-                lines = [ln for ln in err.splitlines() if ln.startswith(("[x265rdo]", "[x265la]")) or "waiting for the device" in ln]
+                lines = [ln for ln in err.splitlines() if ln.startswith(("[x265rdo]", "[x265la]", "[x265me] service", "[x265me] check"))
+                         or "waiting for the device" in ln]
                 print(json.dumps({"variant": name, "rep": rep, "fps": f, "wall_s": round(w, 3), "identical": m == rmd5,
                                   "hook": lines}), flush=True)
                 out.setdefault(name, []).append((f, w, m == rmd5))
