@@ -920,6 +920,8 @@ typedef struct
     double kernel_ms, batch_ms, queue_ms;
     int64_t waits, waits_blocked;
     double wait_ms;
+    int64_t sao_ctus;               /* CTUs whose SAO statistics the server computed (x265amd_rdo_sao_stats) */
+    double sao_ms;                  /* their post-to-result time */
 } x265amd_rdo_counters;
 int  x265amd_rdo_create(const x265amd_rdo_config* cfg, x265amd_rdo** out);
 void x265amd_rdo_destroy(x265amd_rdo* rdo);
@@ -934,6 +936,25 @@ int  x265amd_rdo_stats(x265amd_rdo* rdo, x265amd_rdo_counters* out);
  * (nesting allowed), which stop the running servers and hold their relaunch until the last end. */
 void x265amd_devsync_begin(void);
 void x265amd_devsync_end(void);
+/* SAO::calcSaoStatsCu (sao.cpp:772-943) of one CTU, all three planes, by the resident server: replaces the
+ * three calls SAO::rdoSaoUnitCu makes for a CTU (sao.cpp:1385-1392).  rec[p] / fenc[p]: plane p's CTU origin
+ * in the deblocked reconstruction / the source, with the picture's margins around it (the reconstruction is
+ * read from 4 pixels left of the CTU to 16 right and one row above and below).  Outputs m_offsetOrg and
+ * m_count of the CTU: stats / count [3 planes][5 types: EO_0..EO_3, BO][33 classes].  Synchronous.
+ * ENOMEM: not served (no server, no device-memory slots, not 8-bit 4:2:0 64x64, no free slot, or the server
+ * broken): the caller computes the statistics on the host. */
+typedef struct
+{
+    int width, height;              /* picture (luma) */
+    int ctu_log2, cx, cy;           /* CTU size, column and row */
+    int non_deblocked;              /* --sao-non-deblock */
+    int chroma_format;              /* X265_CSP_I420 = 1 only */
+    const void* rec[3];
+    intptr_t rec_stride[3];         /* elements */
+    const void* fenc[3];
+    intptr_t fenc_stride[3];
+} x265amd_rdo_sao_ctu;
+int  x265amd_rdo_sao_stats(x265amd_rdo* rdo, const x265amd_rdo_sao_ctu* ctu, int32_t* stats, int32_t* count);
 
 /* host buffers (Lowres / PicYuv planes page-locked by an f1 or f2 session) that were already freed or
  * unmapped when their session unregistered them, over the process: must stay 0 (a freed registered range

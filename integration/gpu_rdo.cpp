@@ -72,6 +72,7 @@
 #include "scalinglist.h"
 #include "yuv.h"
 #include "shortyuv.h"
+#include "sao.h"
 
 #include <atomic>
 #include <cstdio>
@@ -95,6 +96,7 @@ extern "C" uint32_t x265ref_transformNxN(Quant* self, const CUData& cu, const pi
 extern "C" void x265ref_invtransformNxN(Quant* self, const CUData& cu, int16_t* residual, uint32_t resiStride,
                                         const coeff_t* coeff, uint32_t log2TrSize, TextType ttype, bool bIntra,
                                         bool useTransformSkip, uint32_t numSig);
+extern "C" void x265ref_calcSaoStatsCu(SAO* self, int addr, int plane);
 
 namespace {
 
@@ -112,6 +114,7 @@ int g_mode = RDO_CPU;
 int g_min_log2 = 6;
 int g_launchers = 2;
 bool g_early = false;
+bool g_sao = false;                    /* X265AMD_RDO_SAO: each CTU's SAO statistics by the resident server */
 std::atomic<int> g_rdo_epoch{ 0 };     /* bumped when an encoder closes: earlier early posts are abandoned */
 int g_gpus = 1;
 bool g_stats_on = false;
@@ -128,7 +131,8 @@ std::vector<Session> g_sessions;     /* per device session index (frame encoder 
 x265amd_rdo_counters g_closed{};
 
 enum { ST_POSTS, ST_HOST_CUS, ST_TQ_HIT, ST_TQ_MISS, ST_ITQ_HIT, ST_ITQ_MISS, ST_PSY_HIT, ST_PSY_MISS, ST_CHECK_BAD,
-       ST_EARLY_MERGE, ST_EARLY_INTER, ST_EARLY_BIDIR, ST_EARLY_USED, ST_EARLY_DROPPED, ST_N };
+       ST_EARLY_MERGE, ST_EARLY_INTER, ST_EARLY_BIDIR, ST_EARLY_USED, ST_EARLY_DROPPED, ST_SAO_DEV, ST_SAO_HOST,
+       ST_SAO_BAD, ST_N };
 std::atomic<int64_t> g_st[ST_N];
 std::atomic<int64_t> g_wait_ns{ 0 };
 
@@ -146,6 +150,7 @@ void print_stats()
             c.batches += t.batches; c.requests += t.requests; c.tus += t.tus; c.blocks += t.blocks;
             c.kernel_ms += t.kernel_ms; c.batch_ms += t.batch_ms; c.queue_ms += t.queue_ms;
             c.waits += t.waits; c.waits_blocked += t.waits_blocked; c.wait_ms += t.wait_ms;
+            c.sao_ctus += t.sao_ctus; c.sao_ms += t.sao_ms;
             if (t.max_requests_per_batch > c.max_requests_per_batch) c.max_requests_per_batch = t.max_requests_per_batch;
         }
     }
@@ -166,8 +171,12 @@ void print_stats()
                 (long long)c.batches, (long long)c.requests, (double)c.requests / c.batches,
                 (long long)c.max_requests_per_batch, (long long)c.tus, (long long)c.blocks, c.kernel_ms / c.batches,
                 c.batch_ms / c.batches, c.requests ? c.queue_ms / c.requests : 0.0, (long long)c.waits_blocked);
+    if (g_sao)
+        fprintf(stderr, "[x265rdo] SAO statistics: %lld CTUs on the device (%.3f ms each, post to result), %lld on the "
+                        "host\n", (long long)g_st[ST_SAO_DEV].load(), c.sao_ctus ? c.sao_ms / c.sao_ctus : 0.0,
+                (long long)g_st[ST_SAO_HOST].load());
     if (g_mode == RDO_CHECK)
-        fprintf(stderr, "[x265rdo] check: %lld mismatches\n", (long long)g_st[ST_CHECK_BAD].load());
+        fprintf(stderr, "[x265rdo] check: %lld mismatches\n", (long long)(g_st[ST_CHECK_BAD].load() + g_st[ST_SAO_BAD].load()));
 }
 
 void init_once()
@@ -185,6 +194,11 @@ void init_once()
     g_early = e && *e == '1' && (g_mode == RDO_GPU || g_mode == RDO_CHECK);
     e = getenv("X265AMD_GPUS");
     if (e && *e) g_gpus = atoi(e) < 1 ? 1 : atoi(e);
+    /* the SAO statistics go to the resident server (direct mode with X265AMD_RDO_SERVER=1; default on there) */
+    e = getenv("X265AMD_RDO_SAO");
+    const char* srv = getenv("X265AMD_RDO_SERVER");
+    g_sao = (g_mode == RDO_GPU || g_mode == RDO_CHECK) && g_launchers == 0 && srv && *srv == '1' && X265_DEPTH == 8 &&
+            !(e && *e == '0');
     const char* st = getenv("X265AMD_ME_STATS");
     g_stats_on = (st && *st == '1') || g_mode == RDO_CHECK;
     if (g_mode != RDO_CPU)
@@ -193,6 +207,7 @@ void init_once()
                 g_mode == RDO_CHECK ? "on the MI355X (check mode)" : g_mode == RDO_HOST ? "on the CPU (hook memo)" :
                                                                            "on the MI355X");
         if (g_early) fprintf(stderr, "[x265rdo] requests posted when the prediction is final (early posts)\n");
+        if (g_sao) fprintf(stderr, "[x265rdo] SAO statistics of each CTU on the MI355X (resident server)\n");
         if (g_stats_on) atexit(print_stats);
     }
 }
@@ -378,6 +393,7 @@ extern "C" void x265amd_rdo_encoder_closed(void)
             g_closed.blocks += t.blocks; g_closed.kernel_ms += t.kernel_ms; g_closed.batch_ms += t.batch_ms;
             g_closed.queue_ms += t.queue_ms; g_closed.waits += t.waits; g_closed.waits_blocked += t.waits_blocked;
             g_closed.wait_ms += t.wait_ms;
+            g_closed.sao_ctus += t.sao_ctus; g_closed.sao_ms += t.sao_ms;
             if (t.max_requests_per_batch > g_closed.max_requests_per_batch)
                 g_closed.max_requests_per_batch = t.max_requests_per_batch;
         }
@@ -738,6 +754,95 @@ void Quant::invtransformNxN(const CUData& cu, int16_t* residual, uint32_t resiSt
         g_st[ST_ITQ_MISS]++;
     }
     x265ref_invtransformNxN(this, cu, residual, resiStride, coeff, log2TrSize, ttype, bIntra, useTransformSkip, numSig);
+}
+
+/* SAO::calcSaoStatsCu (sao.cpp:772-943): rdoSaoUnitCu / rdoSaoUnitRow call it for planes 0, 1, 2 of a CTU in turn
+ * (sao.cpp:1276-1283, 1385-1392), on m_count / m_offsetOrg zeroed (or holding the pre-deblocking statistics) just
+ * before.  The first call of a CTU has the server compute all three planes from the deblocked reconstruction as it
+ * is at that moment (x265amd_rdo_sao_stats, synchronous: the reference reads it at the same point); each call adds
+ * its plane's part, as the reference's primitives add theirs.  Anything not served runs the reference's code. */
+namespace {
+struct SaoMemo
+{
+    const SAO* sao = nullptr;
+    const Frame* frame = nullptr;
+    int poc = -1, addr = -1;
+    int32_t stats[3 * 5 * 33], count[3 * 5 * 33];
+};
+thread_local SaoMemo t_sao;
+}
+
+void SAO::calcSaoStatsCu(int addr, int plane)
+{
+    pthread_once(&g_once, init_once);
+    SaoMemo& mm = t_sao;
+    if (!g_sao || m_chromaFormat != X265_CSP_I420 || g_maxLog2CUSize != 6 || plane < 0 || plane > 2)
+    {
+        x265ref_calcSaoStatsCu(this, addr, plane);
+        return;
+    }
+    if (!(mm.sao == this && mm.frame == m_frame && mm.poc == m_frame->m_poc && mm.addr == addr))
+    {
+        mm.sao = nullptr;
+        const CUData* ctu = m_frame->m_encData->getPicCTU(addr);
+        x265amd_rdo* rdo = session_for(*ctu, m_frame->m_encData->m_slice->m_pps->bSignHideEnabled ? 1 : 0);
+        if (rdo)
+        {
+            const PicYuv* rec = m_frame->m_reconPic;
+            const PicYuv* src = m_frame->m_fencPic;
+            x265amd_rdo_sao_ctu q = {};
+            q.width = m_param->sourceWidth;
+            q.height = m_param->sourceHeight;
+            q.ctu_log2 = (int)g_maxLog2CUSize;
+            q.cx = (int)(ctu->m_cuPelX >> g_maxLog2CUSize);
+            q.cy = (int)(ctu->m_cuPelY >> g_maxLog2CUSize);
+            q.non_deblocked = m_param->bSaoNonDeblocked ? 1 : 0;
+            q.chroma_format = m_chromaFormat;
+            for (int p = 0; p < 3; p++)
+            {
+                q.rec[p] = rec->getPlaneAddr(p, addr);
+                q.rec_stride[p] = p ? rec->m_strideC : rec->m_stride;
+                q.fenc[p] = src->getPlaneAddr(p, addr);
+                q.fenc_stride[p] = p ? src->m_strideC : src->m_stride;
+            }
+            if (x265amd_rdo_sao_stats(rdo, &q, mm.stats, mm.count) == 0)
+            {
+                mm.sao = this;
+                mm.frame = m_frame;
+                mm.poc = m_frame->m_poc;
+                mm.addr = addr;
+            }
+        }
+        if (!mm.sao)
+        {
+            g_st[ST_SAO_HOST]++;
+            x265ref_calcSaoStatsCu(this, addr, plane);
+            return;
+        }
+        g_st[ST_SAO_DEV]++;
+    }
+    const int32_t* ds = mm.stats + plane * 5 * 33;
+    const int32_t* dc = mm.count + plane * 5 * 33;
+    if (g_mode == RDO_CHECK)
+    {
+        /* the reference's own statistics of the plane, compared with the device's part (the reference's stay) */
+        int32_t s0[5][33], c0[5][33];
+        memcpy(s0, m_offsetOrg[plane], sizeof(s0));
+        memcpy(c0, m_count[plane], sizeof(c0));
+        x265ref_calcSaoStatsCu(this, addr, plane);
+        bool bad = false;
+        for (int t = 0; t < 5; t++)
+            for (int k = 0; k < 33; k++)
+                bad |= m_offsetOrg[plane][t][k] - s0[t][k] != ds[t * 33 + k] || m_count[plane][t][k] - c0[t][k] != dc[t * 33 + k];
+        if (bad) g_st[ST_SAO_BAD]++;
+        return;
+    }
+    for (int t = 0; t < 5; t++)
+        for (int k = 0; k < 33; k++)
+        {
+            m_offsetOrg[plane][t][k] += ds[t * 33 + k];
+            m_count[plane][t][k] += dc[t * 33 + k];
+        }
 }
 
 } // namespace X265_NS

@@ -49,15 +49,8 @@ constexpr int kMaxFrames = 32;
 constexpr int kDbkFrames = 16;
 constexpr int kStatFrames = 24;
 
-__device__ __forceinline__ int clip3(int lo, int hi, int v) { return v < lo ? lo : (v > hi ? hi : v); }
-// sign as one v_med3_i32 (clamp to [-1, 1]); written as asm because the compiler turns
-// (v > 0) - (v < 0) and min / max of a difference back into two compares and selects
-__device__ __forceinline__ int sgn(int v)
-{
-    int r;
-    asm("v_med3_i32 %0, %1, -1, 1" : "=v"(r) : "v"(v));
-    return r;
-}
+// clip3, sgn, load_row10 and the SAO statistics of one CTU (sao_stats_wave), shared with tu.hip's server
+#include "saostats.h"
 // the compare form, kept where it measured faster (SAO apply: its selects fold into the offset pick)
 __device__ __forceinline__ int sgn_cmp(int v) { return (v > 0) - (v < 0); }
 __device__ __forceinline__ int iabs(int v) { return v < 0 ? -v : v; }
@@ -362,28 +355,6 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_deblock(const DbkLaunch L)
     }
 }
 
-// o[i] = p[i - 1], i = 0..9: a row segment with its left / right neighbour in one (8-bit) or
-// two (16-bit) 16-byte loads; planes are readable 16 pixels around the picture
-template <typename P>
-__device__ __forceinline__ void load_row10(const P* p, int (&o)[10])
-{
-    if constexpr (sizeof(P) == 1)
-    {
-        const uint4 v = ldu<uint4>(p - 4);
-        const uint32_t w[4] = { v.x, v.y, v.z, v.w };
-#pragma unroll
-        for (int i = 0; i < 10; i++) o[i] = (int)((w[(i + 3) >> 2] >> (8 * ((i + 3) & 3))) & 0xff);
-    }
-    else
-    {
-        const uint4 a = ldu<uint4>(p - 2), b = ldu<uint4>(p + 6);
-        const uint32_t w[8] = { a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w };
-#pragma unroll
-        for (int i = 0; i < 10; i++)   // element i + 1 of the window p - 2 .. p + 13
-            o[i] = (int)((w[(i + 1) >> 1] >> (16 * ((i + 1) & 1))) & 0xffff);
-    }
-}
-
 // ================================================================ SAO apply
 struct SaoFrame
 {
@@ -509,188 +480,34 @@ struct StatLaunch
     int count, bo_shift;
 };
 
-// One wavefront per CTU.  Pass 0: luma, lane = 8x8 strip of the CTU (<= 64 strips); pass 1: Cb on
-// lanes 0-31, Cr on lanes 32-63 (<= 16 strips each).  A lane walks its strip row by row (one new
-// 16-byte load per row) and adds, per EO type, (d << 7) + 1 to its private LDS bin of the pixel's
-// edge class (<= 64 pixels of <= 12 bits per lane: no overflow; a conflict-free ds_add instead of a
-// five-way select chain); band classes merge runs of equal band and add them to LDS as
-// (count << 40) + sum.  The lanes' bins then reduce across the wave (or half-wave).
+// One wavefront per CTU (saostats.h sao_stats_wave): the CTU's planes seen through the frame's planes
 template <typename P>
 __global__ __launch_bounds__(64) void k_sao_stats(const StatLaunch L)
 {
-    __shared__ int32_t eo_sum[3][4][5], eo_cnt[3][4][5];
-    __shared__ unsigned long long bo[3][32];
-    __shared__ int32_t bins[64][21];              // per lane: [EO type][edge type] (sum << 7) + count; [20] sink
     const uint32_t b = xcd_block();
     const StatFrame& f = L.f[frame_of<kStatFrames>(L, b)];
     const uint32_t c = b - f.block0;
-    const int lane = threadIdx.x;
-    for (int i = lane; i < 3 * 32; i += 64) (&bo[0][0])[i] = 0;
-    for (int i = lane; i < 3 * 4 * 5; i += 64) { (&eo_sum[0][0][0])[i] = 0; (&eo_cnt[0][0][0])[i] = 0; }
-    __syncthreads();
     const int cxi = (int)(c % f.wc), cyi = (int)(c / f.wc);
-#pragma unroll 1
-    for (int pass = 0; pass < 2; pass++)
+    SaoCtuView v;
+    v.nd = f.nd;
+    for (int pc = 0; pc < 2; pc++)
     {
-        const int p = pass ? 1 + (lane >> 5) : 0;
-        const int sl = pass ? lane & 31 : lane, nl = pass ? 32 : 64;
-        const int pw = p ? f.w >> f.hs : f.w, ph = p ? f.h >> f.vs : f.h;
-        const int csw = (1 << f.ctu_log2) >> (p ? f.hs : 0), csh = (1 << f.ctu_log2) >> (p ? f.vs : 0);
-        const int x0 = cxi * csw, y0 = cyi * csh;
-        const int cw = (x0 + csw < pw ? x0 + csw : pw) - x0, ch = (y0 + csh < ph ? y0 + csh : ph) - y0;
-        const bool right = x0 + cw == pw, bottom = y0 + ch == ph;
-        const int po = p ? 2 : 0;
-        // regions per type (sao.cpp:825-925): EO_0, EO_1, EO_2, EO_3, BO; EO_0 keeps its bottom
-        // skip at the picture edge (sao.cpp:852)
-        int xs[5], xe[5], ys[5], ye[5];
-#pragma unroll
-        for (int t = 0; t < 5; t++)
-        {
-            const int sb = f.nd ? (t == 0 || t == 4 ? 3 : 4) : 4;
-            const int sr = f.nd ? (t == 1 || t == 4 ? 4 : 5) : 5;
-            const bool eox = t == 0 || t == 2 || t == 3, eoy = t >= 1 && t <= 3;
-            xs[t] = eox ? (x0 == 0) : 0;
-            xe[t] = right ? (eox ? cw - 1 : cw) : cw - sr + po;
-            ys[t] = eoy ? (y0 == 0) : 0;
-            ye[t] = t == 0 ? ch - sb + po : (bottom ? (eoy ? ch - 1 : ch) : ch - sb + po);
-        }
-        const int nsx = (cw + 7) >> 3, nsy = (ch + 7) >> 3;
-        // chroma strips per plane: 16 (4:2:0), 32 (4:2:2), 64 (4:4:4) over 32 lanes; Cb and Cr have the
-        // same geometry, so the round count is uniform over the wave
-        const int rounds = (nsx * nsy + nl - 1) / nl;
-#pragma unroll 1
-        for (int round = 0; round < rounds; round++)
-        {
-#pragma unroll
-            for (int k = 0; k < 20; k++) bins[lane][k] = 0;
-            const int strip = sl + round * nl;
-            if (strip < nsx * nsy)
-            {
-                const int lx0 = 8 * (strip % nsx), ly0 = 8 * (strip / nsx);
-                const int rows = ch - ly0 < 8 ? ch - ly0 : 8;
-                uint32_t xm[5];
-#pragma unroll
-                for (int t = 0; t < 5; t++)
-                {
-                    const int lo = clip3(0, 8, xs[t] - lx0), hi = clip3(0, 8, xe[t] - lx0);
-                    xm[t] = hi > lo ? ((1u << hi) - 1) & ~((1u << lo) - 1) : 0u;
-                }
-                const int64_t rs = p ? f.rcs : f.rs, fs = p ? f.fcs : f.fs;
-                const P* r = (const P*)f.rec[p] + (int64_t)(y0 + ly0) * rs + x0 + lx0;
-                const P* fe = (const P*)f.fenc[p] + (int64_t)(y0 + ly0) * fs + x0 + lx0;
-                int up[10], mid[10], dn[10];
-                load_row10<P>(r - rs, up);
-                load_row10<P>(r, mid);
-                // signs against the row above for EO_1 / EO_2 / EO_3: after the first row they are the
-                // negated signs against the row below of the previous row (sao.cpp's signUp buffers)
-                int u1[8], u2[8], u3[8];
-#pragma unroll
-                for (int i = 0; i < 8; i++)
-                {
-                    u1[i] = sgn(mid[i + 1] - up[i + 1]);
-                    u2[i] = sgn(mid[i + 1] - up[i]);
-                    u3[i] = sgn(mid[i + 1] - up[i + 2]);
-                }
-#pragma unroll
-                for (int yy = 0; yy < 8; yy++)
-                {
-                    if (yy >= rows) break;
-                    load_row10<P>(r + (yy + 1) * rs, dn);
-                    int h[9];                 // EO_0: sign of each pixel against its left neighbour
-#pragma unroll
-                    for (int k = 0; k < 9; k++) h[k] = sgn(mid[k + 1] - mid[k]);
-                    int n1[8], n2[8], n3[8];
-                    n2[0] = sgn(dn[1] - mid[0]);
-                    n3[7] = sgn(dn[8] - mid[9]);
-                    int fv[8];
-                    load_row<P, 8>(fe + yy * fs, fv);
-                    const int ly = ly0 + yy;
-                    uint32_t m[5];
-#pragma unroll
-                    for (int t = 0; t < 5; t++) m[t] = (ly >= ys[t] && ly < ye[t]) ? xm[t] : 0u;
-                    int run_band = -1;
-                    unsigned long long run = 0;
-#pragma unroll
-                    for (int i = 0; i < 8; i++)
-                    {
-                        const int v = mid[i + 1], d = fv[i] - v;
-                        const int val = (d << 7) + 1;
-                        const int d1 = sgn(v - dn[i + 1]), d2 = sgn(v - dn[i + 2]), d3 = sgn(v - dn[i]);
-                        const int e[4] = { h[i] - h[i + 1], u1[i] + d1, u2[i] + d2, u3[i] + d3 };
-                        n1[i] = -d1;
-                        if (i < 7) n2[i + 1] = -d2;
-                        if (i > 0) n3[i - 1] = -d3;
-#pragma unroll
-                        for (int t = 0; t < 4; t++)
-                        {
-                            // masked-off pixels go to the sink bin 20: no branch around the ds_add
-                            const int bi = ((m[t] >> i) & 1) ? 5 * t + e[t] + 2 : 20;
-                            atomicAdd(&bins[lane][bi], val);
-                        }
-                        if ((m[4] >> i) & 1)
-                        {
-                            const int band = v >> L.bo_shift;
-                            if (band != run_band)
-                            {
-                                if (run_band >= 0) atomicAdd(&bo[p][run_band], run);
-                                run_band = band;
-                                run = 0;
-                            }
-                            run += (1ull << 40) + (unsigned long long)(int64_t)d;
-                        }
-                    }
-                    if (run_band >= 0) atomicAdd(&bo[p][run_band], run);
-#pragma unroll
-                    for (int i = 0; i < 8; i++) { u1[i] = n1[i]; u2[i] = n2[i]; u3[i] = n3[i]; }
-#pragma unroll
-                    for (int i = 0; i < 10; i++) mid[i] = dn[i];
-                }
-            }
-            __syncthreads();
-            // wave (pass 0) / half-wave (pass 1) totals: lane r < 20 of each half sums bin r over the
-            // lanes of its plane; edge type j = e + 2 -> class s_eoTable[j] (sao.cpp:65-72): 1, 2, 0, 3, 4
-            const int r = pass ? lane & 31 : lane;
-            if (r < 20)
-            {
-                const int l0 = pass ? lane & 32 : 0;
-                int vsum = 0, vc = 0;
-                for (int l = 0; l < nl; l++)
-                {
-                    const int v = bins[l0 + l][r];
-                    const int cn = v & 127;
-                    vc += cn;
-                    vsum += (v - cn) >> 7;
-                }
-                const int t = r / 5, j = r % 5;
-                const int k = j == 0 ? 1 : j == 1 ? 2 : j == 2 ? 0 : j;
-                eo_sum[p][t][k] += vsum;
-                eo_cnt[p][t][k] += vc;
-            }
-            __syncthreads();
-        }
+        v.pw[pc] = pc ? f.w >> f.hs : f.w;
+        v.ph[pc] = pc ? f.h >> f.vs : f.h;
+        v.csw[pc] = (1 << f.ctu_log2) >> (pc ? f.hs : 0);
+        v.csh[pc] = (1 << f.ctu_log2) >> (pc ? f.vs : 0);
+        v.x0[pc] = cxi * v.csw[pc];
+        v.y0[pc] = cyi * v.csh[pc];
     }
-    __syncthreads();
-    // every entry of the CTU's [3][5][33] block
-    int32_t* os = f.stats + (int64_t)c * 3 * 5 * 33;
-    int32_t* oc = f.count + (int64_t)c * 3 * 5 * 33;
-    for (int i = lane; i < 3 * 5 * 33; i += 64)
+    for (int p = 0; p < 3; p++)
     {
-        const int p = i / 165, t = (i % 165) / 33, k = i % 33;
-        int sv = 0, cv = 0;
-        if (t < 4)
-        {
-            if (k < 5) { sv = eo_sum[p][t][k]; cv = eo_cnt[p][t][k]; }
-        }
-        else if (k >= 1)
-        {
-            const long long tot = (long long)bo[p][k - 1];
-            const long long lo = (long long)((unsigned long long)tot << 24) >> 24;   // sign-extend 40 bits
-            sv = (int)lo;
-            cv = (int)((tot - lo) >> 40);
-        }
-        os[i] = sv;
-        oc[i] = cv;
+        const int pc = p ? 1 : 0;
+        v.rs[p] = p ? f.rcs : f.rs;
+        v.fs[p] = p ? f.fcs : f.fs;
+        v.rec[p] = (const P*)f.rec[p] + (int64_t)v.y0[pc] * v.rs[p] + v.x0[pc];
+        v.fenc[p] = (const P*)f.fenc[p] + (int64_t)v.y0[pc] * v.fs[p] + v.x0[pc];
     }
+    sao_stats_wave<P>(v, L.bo_shift, f.stats + (int64_t)c * 3 * 5 * 33, f.count + (int64_t)c * 3 * 5 * 33);
 }
 
 // ================================================================ border extension

@@ -1,5 +1,5 @@
 // rdojob.h — one request of the resident residual-coding server (X265AMD_RDO_SERVER, round 6): the TU batches
-// and 8x8 psy jobs of one inter CU, laid out in the request's slot of mapped, coherent host memory by the
+// and 8x8 psy jobs of one inter CU (or the SAO statistics of one CTU), laid out in the request's slot of mapped, coherent host memory by the
 // posting thread (rdosession.cpp) and served by k_rdo_server (tu.hip), which polls the slots' sequence words.
 #pragma once
 #include <stddef.h>
@@ -9,11 +9,26 @@
 
 namespace x265amd {
 
+// a request of the second kind (kind 1): SAO::calcSaoStatsCu of one CTU, all three planes (sao.cpp:772-943).
+// The CTU's deblocked windows and source blocks are the request's staged bytes; the statistics go to host memory.
+struct RdoSaoJob
+{
+    int32_t w, h;                  // picture size (luma)
+    int32_t ctu_log2, nd, cx, cy;  // CTU size, --sao-non-deblock, CTU column and row
+    int32_t hs, vs;                // chroma shifts
+    int64_t rec_at[3], fenc_at[3]; // byte offset in the staged bytes of each plane's CTU origin
+    int64_t rs[3], fs[3];          // their strides (pixels)
+    int32_t* stats;                // [3][5][33] m_offsetOrg, then
+    int32_t* count;                // [3][5][33] m_count (device addresses of host memory)
+};
+
 struct RdoJob
 {
     x265amd_tu_batch tu[2];        // luma TUs (32x32), chroma TUs of both planes (16x16)
     x265amd_cmp_batch psy[4];      // 8x8 psy: luma (fenc, pred), luma (fenc, recon), chroma (fenc, pred), (fenc, recon)
-    uint32_t pad[3];
+    RdoSaoJob sao;
+    uint32_t kind;                 // 0: the CU's residual coding (tu, psy); 1: SAO statistics (sao)
+    uint32_t pad[2];
     uint32_t seq;                  // the request's sequence number; written last (release)
 };
 

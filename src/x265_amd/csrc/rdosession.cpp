@@ -163,7 +163,7 @@ struct x265amd_rdo
     hipStream_t srv_st = nullptr;
     std::mutex srv_mu;
     std::atomic<double> srv_launched{ -1.0 };   // host time of the running server's launch (< 0: none)
-    int srv_nwg = 16;
+    int srv_nwg = 32;
     bool srv_coop = true;
     bool srv_probe = false;          // X265AMD_RDO_SERVER_PROBE=1: run the server, post nothing to it
     bool srv_timing = false;         // X265AMD_RDO_SERVER_TIMING=1: phase stamps of every request, printed at destroy
@@ -742,7 +742,7 @@ extern "C" int x265amd_rdo_create(const x265amd_rdo_config* cfg, x265amd_rdo** o
     // 16 workgroups: fewer queue the CUs longer, more slow the motion-search kernel running beside them
     // (8 / 12 / 16 / 20 / 24 / 32: 11.0 / 11.5 / 12.3-12.5 / 12.3 / 12.1 / 11.7 fps at 2160p, profiles/r06/
     // rdo_server_ab.jsonl calls r06zh-r06zi)
-    s->srv_nwg = getenv_int("X265AMD_RDO_SERVER_WG", 16);
+    s->srv_nwg = getenv_int("X265AMD_RDO_SERVER_WG", 32);   // (16 until the SAO requests joined)
     s->srv_nwg = s->srv_nwg < 4 ? 4 : (s->srv_nwg > 256 ? 256 : s->srv_nwg);
     if (s->server) s->timing = false;
     s->yield_us = getenv_int("X265AMD_RDO_YIELD_US", 5000);
@@ -833,6 +833,33 @@ bool flag_kernel()
 {
     static const int v = [] { const char* e = getenv("X265AMD_RDO_FLAG"); return e && !strcmp(e, "kernel") ? 1 : 0; }();
     return v != 0;
+}
+
+// the request of slot k for the resident server, its job written: its sequence word (release: the inputs,
+// descriptors and job are in memory before the server can see the new sequence number), the doorbell
+int server_publish(x265amd_rdo* s, x265amd_rdo_thread* t, int k, x265amd::RdoJob* job)
+{
+    x265amd_rdo_req* r = &t->req[k];
+    r->seq++;
+    r->want = r->seq;
+    const int wg = (t->index * kSlots + k) % s->srv_nwg;
+    if (s->srv_in)
+    {
+        // device memory through the BAR is write-combined: fence the inputs and job before the sequence
+        // word, and the sequence word before the doorbell (never read back: BAR reads are slow)
+        __builtin_ia32_sfence();
+        *(volatile uint32_t*)&job->seq = r->seq;
+        __builtin_ia32_sfence();
+        *(volatile uint32_t*)&s->srv_vctl[x265amd::kRdoBellWord + wg] = s->srv_bells[wg].fetch_add(1) + 1;
+        __builtin_ia32_sfence();
+    }
+    else
+    {
+        __atomic_store_n(&job->seq, r->seq, __ATOMIC_RELEASE);
+        // ring the doorbell of the workgroup that polls this slot
+        __atomic_fetch_add(&s->srv_ctl[x265amd::kRdoBellWord + wg], 1u, __ATOMIC_RELEASE);
+    }
+    return ensure_server(s, false);
 }
 
 // direct mode: stage the CU in the slot's mapped region and enqueue its kernels on the thread's stream
@@ -938,32 +965,12 @@ int direct_post(x265amd_rdo* s, x265amd_rdo_thread* t, int k, const x265amd_rdo_
     if (o > ob || ob + out_bytes(g, pix) + x265amd::kRdoJobFromEnd > t->region) return X265AMD_ENOMEM;
     if (s->server)
     {
-        // the request for the resident server: its job, then its sequence word (release: the inputs,
-        // descriptors and job are in memory before the server can see the new sequence number)
         x265amd::RdoJob* job = (x265amd::RdoJob*)(s->srv_in ? I + x265amd::rdo_out_at(pix)
                                                              : H + t->region - x265amd::kRdoJobFromEnd);
         for (int c = 0; c < 2; c++) job->tu[c] = tb[c];
         for (int c = 0; c < 4; c++) job->psy[c] = pb[c];
-        r->seq++;
-        r->want = r->seq;
-        const int wg = (t->index * kSlots + k) % s->srv_nwg;
-        if (s->srv_in)
-        {
-            // device memory through the BAR is write-combined: fence the inputs and job before the sequence
-            // word, and the sequence word before the doorbell (never read back: BAR reads are slow)
-            __builtin_ia32_sfence();
-            *(volatile uint32_t*)&job->seq = r->seq;
-            __builtin_ia32_sfence();
-            *(volatile uint32_t*)&s->srv_vctl[x265amd::kRdoBellWord + wg] = s->srv_bells[wg].fetch_add(1) + 1;
-            __builtin_ia32_sfence();
-        }
-        else
-        {
-            __atomic_store_n(&job->seq, r->seq, __ATOMIC_RELEASE);
-            // ring the doorbell of the workgroup that polls this slot
-            __atomic_fetch_add(&s->srv_ctl[x265amd::kRdoBellWord + wg], 1u, __ATOMIC_RELEASE);
-        }
-        return ensure_server(s, false);
+        job->kind = 0;
+        return server_publish(s, t, k, job);
     }
     r->want = 1;
     int rc = s->timing ? (int)hipEventRecord(t->ev[k][0], t->st) : 0;
@@ -1154,6 +1161,85 @@ extern "C" int x265amd_rdo_release(x265amd_rdo* s, int ticket)
     // a request still queued is left alone: its launcher completes it and it stays reserved until waited for
     int done = 2;
     if (!r->state.compare_exchange_strong(done, 0)) return X265AMD_EINVAL;
+    return 0;
+}
+
+extern "C" int x265amd_rdo_sao_stats(x265amd_rdo* s, const x265amd_rdo_sao_ctu* q, int32_t* stats, int32_t* count)
+{
+    if (!s || !q || !stats || !count) return X265AMD_EINVAL;
+    for (int p = 0; p < 3; p++)
+        if (!q->rec[p] || !q->fenc[p]) return X265AMD_EINVAL;
+    // the server's staged bytes hold an 8-bit 4:2:0 64x64 CTU's windows (below); anything else stays on the host
+    if (!s->launchers.empty() || !s->server || s->srv_probe || s->pix != 1 || q->ctu_log2 != 6 ||
+        q->chroma_format != 1 || q->cx < 0 || q->cy < 0 || q->cx * 64 >= q->width || q->cy * 64 >= q->height ||
+        s->srv_broken.load(std::memory_order_relaxed))
+        return X265AMD_ENOMEM;
+    x265amd_rdo_thread* t;
+    if (int rc = thread_ctx(s, &t)) return rc;
+    int k = 0;
+    while (k < kSlots && t->req[k].state.load(std::memory_order_acquire) != 0) k++;
+    if (k == kSlots) return X265AMD_ENOMEM;
+    if (int rc = direct_setup(s, t)) return rc == X265AMD_ENOMEM ? rc : record(rc);
+    if (!s->srv_in) return X265AMD_ENOMEM;
+    x265amd_rdo_req* r = &t->req[k];
+    r->t_post = now_s();
+    uint8_t* I = s->srv_in + (size_t)(t->index * kSlots + k) * s->srv_in_region;
+    uint8_t* H = t->host + (size_t)k * t->region;
+    uint8_t* D = t->hdev + (size_t)k * t->region;
+    // staged bytes (tu.hip k_rdo_server, kind 1): per plane the deblocked window — one row above to one row below
+    // the CTU, 4 pixels left to 12 right (rows 16-byte multiples, so every strip's p - 4 is 8-byte aligned) — then
+    // the source blocks, packed
+    x265amd::RdoSaoJob js{};
+    js.w = q->width;
+    js.h = q->height;
+    js.ctu_log2 = 6;
+    js.nd = q->non_deblocked;
+    js.cx = q->cx;
+    js.cy = q->cy;
+    js.hs = js.vs = 1;
+    size_t o = 0;
+    for (int p = 0; p < 3; p++)
+    {
+        const int cs = p ? 32 : 64, ww = cs + 16;
+        const int ph = p ? q->height >> 1 : q->height, y0 = q->cy * cs;
+        const int ch = y0 + cs < ph ? cs : ph - y0;
+        const uint8_t* src = (const uint8_t*)q->rec[p] - q->rec_stride[p] - 4;
+        for (int y = 0; y < ch + 2; y++) memcpy(I + o + (size_t)y * ww, src + y * q->rec_stride[p], ww);
+        js.rec_at[p] = (int64_t)(o + ww + 4);
+        js.rs[p] = ww;
+        o = (o + (size_t)ww * (cs + 2) + 15) & ~(size_t)15;
+    }
+    for (int p = 0; p < 3; p++)
+    {
+        const int cs = p ? 32 : 64;
+        const int ph = p ? q->height >> 1 : q->height, y0 = q->cy * cs;
+        const int ch = y0 + cs < ph ? cs : ph - y0;
+        const uint8_t* src = (const uint8_t*)q->fenc[p];
+        for (int y = 0; y < ch; y++) memcpy(I + o + (size_t)y * cs, src + y * q->fenc_stride[p], cs);
+        js.fenc_at[p] = (int64_t)o;
+        js.fs[p] = cs;
+        o = (o + (size_t)cs * cs + 15) & ~(size_t)15;
+    }
+    if (o > x265amd::rdo_out_at(1)) return X265AMD_ENOMEM;
+    const size_t ob = x265amd::rdo_out_at(1);
+    js.stats = (int32_t*)(D + ob);
+    js.count = (int32_t*)(D + ob) + 3 * 5 * 33;
+    x265amd::RdoJob* job = (x265amd::RdoJob*)(I + x265amd::rdo_out_at(1));
+    job->sao = js;
+    job->kind = 1;
+    int rc = server_publish(s, t, k, job);
+    if (!rc) rc = direct_wait(s, t, k);
+    if (rc)
+    {
+        // a request that was not served may still be: its slot is never posted to again
+        r->state.store(3, std::memory_order_release);
+        return record(rc);
+    }
+    memcpy(stats, H + ob, 4 * 3 * 5 * 33);
+    memcpy(count, H + ob + 4 * 3 * 5 * 33, 4 * 3 * 5 * 33);
+    std::lock_guard<std::mutex> g(s->smu);
+    s->st.sao_ctus++;
+    s->st.sao_ms += 1e3 * (now_s() - r->t_post);
     return 0;
 }
 

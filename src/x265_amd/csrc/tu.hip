@@ -35,6 +35,7 @@
 namespace x265amd {
 
 #include "hadamard.h"
+#include "saostats.h"
 
 // ---------------------------------------------------------------- scan orders
 // HEVC scans (spec 6.5.3-6.5.5; x265 g_scanOrder, constants.cpp:359-456),
@@ -1304,7 +1305,8 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_rdo_server(const RdoServerArg
                 if (threadIdx.x + k * X265AMD_BLOCK < NI) ((v4u*)s_in)[threadIdx.x + k * X265AMD_BLOCK] = vi[k];
         }
         __syncthreads();
-        if (threadIdx.x == 0)
+        const bool sao = s_job.kind == 1;
+        if (threadIdx.x == 0 && !sao)
         {
             // every pointer of the job into the staged bytes now points into LDS (outputs stay in host memory)
             const uintptr_t lo = (uintptr_t)ibase, hi = lo + kStage;
@@ -1331,7 +1333,7 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_rdo_server(const RdoServerArg
         __syncthreads();
         // (a request is one 64x64 or 32x32 CU: 4 / 1 luma TUs, 8 / 2 chroma TUs, at most 64 8x8 blocks a
         // batch; anything else is not served, only marked done)
-        const bool sane = s_job.tu[0].log2_size == 5 && s_job.tu[1].log2_size == 4 && s_job.tu[0].n >= 0 &&
+        const bool sane = !sao && s_job.tu[0].log2_size == 5 && s_job.tu[1].log2_size == 4 && s_job.tu[0].n >= 0 &&
                           s_job.tu[0].n <= 4 && s_job.tu[1].n >= 0 && s_job.tu[1].n <= 8 &&
                           s_job.psy[0].n >= 0 && s_job.psy[0].n <= 64 && s_job.psy[1].n >= 0 && s_job.psy[1].n <= 64 &&
                           s_job.psy[2].n >= 0 && s_job.psy[2].n <= 32 && s_job.psy[3].n >= 0 && s_job.psy[3].n <= 32;
@@ -1343,6 +1345,36 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_rdo_server(const RdoServerArg
             if (a.timing) { __syncthreads(); ts2 = __builtin_amdgcn_s_memrealtime(); }
             tu_groups<P, 16, false>(tu_args(s_job.tu[1], a.depth), 0);
             if (a.timing) { __syncthreads(); ts3 = __builtin_amdgcn_s_memrealtime(); }
+        }
+        // a CTU's SAO statistics (8-bit 4:2:0, 64x64: the windows fit the staged bytes): the four waves, from LDS
+        const RdoSaoJob& q = s_job.sao;
+        if (sao && sizeof(P) == 1 && q.ctu_log2 == 6 && q.hs == 1 && q.vs == 1)
+        {
+            bool inside = true;
+            for (int p = 0; p < 3; p++)
+                inside = inside && q.rec_at[p] > 0 && q.rec_at[p] < kStage && q.fenc_at[p] >= 0 && q.fenc_at[p] < kStage;
+            if (inside)
+            {
+                SaoCtuView v;
+                v.nd = q.nd;
+                for (int pc = 0; pc < 2; pc++)
+                {
+                    v.pw[pc] = pc ? q.w >> q.hs : q.w;
+                    v.ph[pc] = pc ? q.h >> q.vs : q.h;
+                    v.csw[pc] = (1 << q.ctu_log2) >> (pc ? q.hs : 0);
+                    v.csh[pc] = (1 << q.ctu_log2) >> (pc ? q.vs : 0);
+                    v.x0[pc] = q.cx * v.csw[pc];
+                    v.y0[pc] = q.cy * v.csh[pc];
+                }
+                for (int p = 0; p < 3; p++)
+                {
+                    v.rec[p] = s_in + q.rec_at[p];
+                    v.fenc[p] = s_in + q.fenc_at[p];
+                    v.rs[p] = q.rs[p];
+                    v.fs[p] = q.fs[p];
+                }
+                sao_stats_wave<P, true, X265AMD_BLOCK / 64>(v, a.depth - 5, q.stats, q.count);
+            }
         }
         // the reconstruction the waves wrote (to host memory) is read back by others for its psy energies:
         // their stores complete (workgroup release: s_waitcnt), then the readers' L1 is invalidated
@@ -1401,9 +1433,6 @@ extern "C" int x265amd_rdo_server_launch(const x265amd::RdoServerArgs* a, int nw
         return (int)hipLaunchCooperativeKernel(f, dim3(nwg), dim3(X265AMD_BLOCK), params, 0, (hipStream_t)stream);
     return (int)hipLaunchKernel(f, dim3(nwg), dim3(X265AMD_BLOCK), params, 0, (hipStream_t)stream);
 }
-
-namespace x265amd {
-} // namespace x265amd
 
 using namespace x265amd;
 

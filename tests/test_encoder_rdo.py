@@ -101,3 +101,10 @@ def test_gpu_rdo_early_posts_bit_exact(tmp_path, mode, form):
     if mode == "check":
         m = re.search(r"\[x265rdo\] check: (\d+) mismatches", err)
         assert m and int(m.group(1)) == 0, err[-3000:]
+    # the server form also computes every CTU's SAO statistics (SAO::calcSaoStatsCu; in check mode each plane's
+    # statistics are recomputed by the reference and compared: the mismatch count above includes them)
+    m = re.search(r"\[x265rdo\] SAO statistics: (\d+) CTUs on the device .*, (\d+) on the host", err)
+    if form == "server":
+        assert m and int(m.group(1)) > 0 and int(m.group(2)) == 0, err[-3000:]
+    else:
+        assert m is None, err[-3000:]
