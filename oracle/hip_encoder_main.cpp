@@ -33,6 +33,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <ctime>
 #include <execinfo.h>
 #include <unistd.h>
 
@@ -50,6 +51,18 @@ extern "C" void x265amd_rdo_install(void* table) __attribute__((weak));
 extern "C" void x265amd_rdo_encoder_closed(void) __attribute__((weak));
 
 namespace {
+/* X265AMD_PHASES=1: wall-clock stamps of the process's phases (main, the encoder's close, exit) on stderr, for
+ * the start-up / teardown share of a bench step (tools/phases.py) */
+bool g_phases = false;
+void phase(const char* what)
+{
+    if (!g_phases) return;
+    struct timespec t;
+    clock_gettime(CLOCK_REALTIME, &t);
+    fprintf(stderr, "[phase] %s %.6f\n", what, t.tv_sec + 1e-9 * t.tv_nsec);
+}
+void phase_exit() { phase("exit"); }
+
 x265_api g_api;
 int (*g_encode)(x265_encoder*, x265_nal**, uint32_t*, x265_picture*, x265_picture*);
 void (*g_close)(x265_encoder*);
@@ -58,8 +71,10 @@ void drop_sessions()
 {
     if (x265amd_me_encoder_closed)
         x265amd_me_encoder_closed();
+    phase("me_dropped");
     if (x265amd_la_encoder_closed)
         x265amd_la_encoder_closed();
+    phase("la_dropped");
     if (x265amd_rdo_encoder_closed)
         x265amd_rdo_encoder_closed();
 }
@@ -75,17 +90,36 @@ void closing(x265_encoder* enc)
     /* X265AMD_ROUND5_CLOSE_ORDER=1: the round-5 order (sessions dropped only after the encoder freed its
      * frames), kept so tests/test_encoder_me.py can show the stale-unregister count catches it */
     const char* old = getenv("X265AMD_ROUND5_CLOSE_ORDER");
+    phase("close");
     if (!(old && *old == '1'))
         drop_sessions();
+    phase("sessions_dropped");
     g_close(enc);
     drop_sessions();
+    phase("closed");
     if (x265amd_host_unregister_stale && x265amd_host_unregister_stale())
         fprintf(stderr, "[x265hip] %lld page-locked host buffers were freed before their session unregistered them\n",
                 x265amd_host_unregister_stale());
 }
 
+x265_encoder* (*g_open)(x265_param*);
+bool g_first = true;
+
+x265_encoder* opening(x265_param* p)
+{
+    phase("open");
+    x265_encoder* e = g_open(p);
+    phase("opened");
+    return e;
+}
+
 int checked_encode(x265_encoder* enc, x265_nal** pp_nal, uint32_t* pi_nal, x265_picture* in, x265_picture* out)
 {
+    if (g_first)
+    {
+        g_first = false;
+        phase("first_encode");
+    }
     int n = g_encode(enc, pp_nal, pi_nal, in, out);
     int st = x265amd_provider_status();
     if (st)
@@ -107,6 +141,8 @@ extern "C" const x265_api* __wrap_x265_api_get_79(int bitDepth)
     g_api.encoder_encode = checked_encode;
     g_close = api->encoder_close;
     g_api.encoder_close = closing;
+    g_open = api->encoder_open;
+    g_api.encoder_open = opening;
     return &g_api;
 }
 
@@ -127,6 +163,12 @@ static void on_fatal(int sig)
 
 int main(int argc, char** argv)
 {
+    {
+        const char* e = getenv("X265AMD_PHASES");
+        g_phases = e && *e == '1';
+        phase("main");
+        if (g_phases) atexit(phase_exit);
+    }
     signal(SIGSEGV, on_fatal);
     signal(SIGBUS, on_fatal);
     const char* which = getenv("X265AMD_PROVIDER");
