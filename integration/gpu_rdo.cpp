@@ -115,6 +115,7 @@ int g_min_log2 = 6;
 int g_launchers = 2;
 bool g_early = false;
 bool g_sao = false;                    /* X265AMD_RDO_SAO: each CTU's SAO statistics by the resident server */
+bool g_sao_host = false;               /* X265AMD_RDO_SAO=host: the same memo, filled by the reference's function */
 std::atomic<int> g_rdo_epoch{ 0 };     /* bumped when an encoder closes: earlier early posts are abandoned */
 int g_gpus = 1;
 bool g_stats_on = false;
@@ -172,9 +173,9 @@ void print_stats()
                 (long long)c.max_requests_per_batch, (long long)c.tus, (long long)c.blocks, c.kernel_ms / c.batches,
                 c.batch_ms / c.batches, c.requests ? c.queue_ms / c.requests : 0.0, (long long)c.waits_blocked);
     if (g_sao)
-        fprintf(stderr, "[x265rdo] SAO statistics: %lld CTUs on the device (%.3f ms each, post to result), %lld on the "
-                        "host\n", (long long)g_st[ST_SAO_DEV].load(), c.sao_ctus ? c.sao_ms / c.sao_ctus : 0.0,
-                (long long)g_st[ST_SAO_HOST].load());
+        fprintf(stderr, "[x265rdo] SAO statistics: %lld CTUs on the %s (%.3f ms each, post to result), %lld on the "
+                        "host\n", (long long)g_st[ST_SAO_DEV].load(), g_sao_host ? "hook memo" : "device",
+                c.sao_ctus ? c.sao_ms / c.sao_ctus : 0.0, (long long)g_st[ST_SAO_HOST].load());
     if (g_mode == RDO_CHECK)
         fprintf(stderr, "[x265rdo] check: %lld mismatches\n", (long long)(g_st[ST_CHECK_BAD].load() + g_st[ST_SAO_BAD].load()));
 }
@@ -199,15 +200,22 @@ void init_once()
     const char* srv = getenv("X265AMD_RDO_SERVER");
     g_sao = (g_mode == RDO_GPU || g_mode == RDO_CHECK) && g_launchers == 0 && srv && *srv == '1' && X265_DEPTH == 8 &&
             !(e && *e == '0');
+    g_sao_host = e && !strcmp(e, "host");
+    if (g_sao_host) g_sao = true;
     const char* st = getenv("X265AMD_ME_STATS");
     g_stats_on = (st && *st == '1') || g_mode == RDO_CHECK;
+    if (g_sao_host)
+    {
+        fprintf(stderr, "[x265rdo] SAO statistics of each CTU on the CPU (hook memo)\n");
+        if (g_mode == RDO_CPU && g_stats_on) atexit(print_stats);
+    }
     if (g_mode != RDO_CPU)
     {
         fprintf(stderr, "[x265rdo] inter residual coding of CUs >= %dx%d %s\n", 1 << g_min_log2, 1 << g_min_log2,
                 g_mode == RDO_CHECK ? "on the MI355X (check mode)" : g_mode == RDO_HOST ? "on the CPU (hook memo)" :
                                                                            "on the MI355X");
         if (g_early) fprintf(stderr, "[x265rdo] requests posted when the prediction is final (early posts)\n");
-        if (g_sao) fprintf(stderr, "[x265rdo] SAO statistics of each CTU on the MI355X (resident server)\n");
+        if (g_sao && !g_sao_host) fprintf(stderr, "[x265rdo] SAO statistics of each CTU on the MI355X (resident server)\n");
         if (g_stats_on) atexit(print_stats);
     }
 }
@@ -785,8 +793,27 @@ void SAO::calcSaoStatsCu(int addr, int plane)
     {
         mm.sao = nullptr;
         const CUData* ctu = m_frame->m_encData->getPicCTU(addr);
-        x265amd_rdo* rdo = session_for(*ctu, m_frame->m_encData->m_slice->m_pps->bSignHideEnabled ? 1 : 0);
-        if (rdo)
+        x265amd_rdo* rdo = g_sao_host ? nullptr : session_for(*ctu, m_frame->m_encData->m_slice->m_pps->bSignHideEnabled ? 1 : 0);
+        if (g_sao_host)
+        {
+            /* the plumbing on a CPU-only host: all three planes by the reference's function on zeroed statistics
+             * (the members are restored), served through the memo like the device's */
+            PerPlane c0, s0;
+            memcpy(c0, m_count, sizeof(c0));
+            memcpy(s0, m_offsetOrg, sizeof(s0));
+            memset(m_count, 0, sizeof(m_count));
+            memset(m_offsetOrg, 0, sizeof(m_offsetOrg));
+            for (int p = 0; p < 3; p++) x265ref_calcSaoStatsCu(this, addr, p);
+            memcpy(mm.stats, m_offsetOrg, sizeof(mm.stats));
+            memcpy(mm.count, m_count, sizeof(mm.count));
+            memcpy(m_count, c0, sizeof(c0));
+            memcpy(m_offsetOrg, s0, sizeof(s0));
+            mm.sao = this;
+            mm.frame = m_frame;
+            mm.poc = m_frame->m_poc;
+            mm.addr = addr;
+        }
+        else if (rdo)
         {
             const PicYuv* rec = m_frame->m_reconPic;
             const PicYuv* src = m_frame->m_fencPic;

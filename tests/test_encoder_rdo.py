@@ -42,6 +42,27 @@ def test_rdo_hook_host_memo_equals_reference_on_cpu(tmp_path, min_log2):
     assert got == ref, "X265AMD_RDO=host: bitstream differs from the reference encoder"
 
 
+@pytest.mark.parametrize("size", [(640, 360), (456, 264)], ids=["360p", "456x264"])
+def test_sao_hook_host_memo_equals_reference_on_cpu(tmp_path, size):
+    """X265AMD_RDO_SAO=host: SAO::calcSaoStatsCu's hook computes each CTU's three planes at its first call (here by
+    the reference's own function on zeroed statistics) and adds one plane's part per call, as the device path
+    does — every CTU is served by the memo and the bitstream is the reference's; a picture whose size is no CTU
+    multiple (456x264: partial right and bottom CTUs) included"""
+    w, h = size
+    n = 8
+    src = _source(tmp_path, w, h, n)
+    rc, ref, _, err = encode(_bin("x265ref8"), src, w, h, n, tmp_path / "ref.hevc")
+    assert rc == 0, err[-2000:]
+    rc, got, _, err = encode(_bin("x265la8"), src, w, h, n, tmp_path / "sao.hevc",
+                             {"X265AMD_LOOKAHEAD": "cpu", "X265AMD_ME": "cpu", "X265AMD_RDO_SAO": "host",
+                              "X265AMD_ME_STATS": "1"})
+    assert rc == 0, err[-2000:]
+    m = re.search(r"\[x265rdo\] SAO statistics: (\d+) CTUs on the hook memo .*, (\d+) on the host", err)
+    ctus = ((w + 63) // 64) * ((h + 63) // 64) * n
+    assert m and int(m.group(1)) == ctus and int(m.group(2)) == 0, err[-2000:]
+    assert got == ref, "X265AMD_RDO_SAO=host: bitstream differs from the reference encoder"
+
+
 def _gpu(tmp_path, w, h, n, env, min_log2=6):
     src = _source(tmp_path, w, h, n)
     rc, ref, _, err = encode(_bin("x265ref8"), src, w, h, n, tmp_path / "ref.hevc", pools=16)
