@@ -913,6 +913,8 @@ typedef struct
     const uint32_t* num_sig[3];     /* transformNxN's return value per TU */
     const int32_t* psy_pred[3];     /* per 8x8 block (raster): psyCost_pp 8x8 (fenc, pred) */
     const int32_t* psy_rec[3];      /* per 8x8 block: psyCost_pp 8x8 (fenc, recon) */
+    const int32_t* sse_pred[3];     /* per 8x8 block: sse_pp 8x8 (fenc, pred); NULL unless served by the server */
+    const int32_t* sse_rec[3];      /* per 8x8 block: sse_pp 8x8 (fenc, recon); NULL unless served by the server */
 } x265amd_rdo_result;
 typedef struct
 {

@@ -133,11 +133,12 @@ x265amd_rdo_counters g_closed{};
 
 enum { ST_POSTS, ST_HOST_CUS, ST_TQ_HIT, ST_TQ_MISS, ST_ITQ_HIT, ST_ITQ_MISS, ST_PSY_HIT, ST_PSY_MISS, ST_CHECK_BAD,
        ST_EARLY_MERGE, ST_EARLY_INTER, ST_EARLY_BIDIR, ST_EARLY_USED, ST_EARLY_DROPPED, ST_SAO_DEV, ST_SAO_HOST,
-       ST_SAO_BAD, ST_N };
+       ST_SAO_BAD, ST_SSE_HIT, ST_SSE_MISS, ST_N };
 std::atomic<int64_t> g_st[ST_N];
 std::atomic<int64_t> g_wait_ns{ 0 };
 
 pixelcmp_t g_psy_orig[NUM_CU_SIZES];
+pixel_sse_t g_sse_orig[2][NUM_CU_SIZES];   /* the table's sse_pp: luma cu[], chroma[4:2:0].cu[] */
 
 void print_stats()
 {
@@ -161,6 +162,8 @@ void print_stats()
             (long long)g_st[ST_POSTS].load(), (long long)g_st[ST_HOST_CUS].load(), (long long)g_st[ST_TQ_HIT].load(),
             (long long)g_st[ST_TQ_MISS].load(), (long long)g_st[ST_ITQ_HIT].load(), (long long)g_st[ST_ITQ_MISS].load(),
             (long long)g_st[ST_PSY_HIT].load(), (long long)g_st[ST_PSY_MISS].load(), 1e-9 * g_wait_ns.load());
+    fprintf(stderr, "[x265rdo] sse_pp memo hits %lld misses %lld\n", (long long)g_st[ST_SSE_HIT].load(),
+            (long long)g_st[ST_SSE_MISS].load());
     if (g_early)
         fprintf(stderr, "[x265rdo] early posts merge %lld inter %lld bidir %lld; used %lld, dropped %lld\n",
                 (long long)g_st[ST_EARLY_MERGE].load(), (long long)g_st[ST_EARLY_INTER].load(),
@@ -317,6 +320,57 @@ bool memo_psy(int size, const pixel* source, intptr_t sstride, const pixel* reco
     return false;
 }
 
+/* the CU's sse_pp (fenc against its prediction or its reconstruction, search.cpp:2591-2595, 2668-2679) from the
+ * device's 8x8 SSEs: plane p's block at `source`, every 8x8 block of `recon` equal (compared) to the prediction's
+ * (the device's sse_pred) or the device's reconstruction's (sse_rec) */
+bool memo_sse(int dim, const pixel* source, intptr_t sstride, const pixel* recon, intptr_t rstride, sse_t& out)
+{
+    const Memo& m = t_memo;
+    const x265amd_rdo_result& r = *m.res;
+    if (!r.sse_pred[0]) return false;
+    for (int p = 0; p < 3; p++)
+    {
+        /* a block of plane p of the CU (the whole CU, or a TU of it: estimateResidualQT's per-TU distortions) */
+        if (sstride != m.fstride[p]) continue;
+        const ptrdiff_t off = source - m.fenc[p];
+        if (off < 0) continue;
+        const int y = (int)(off / m.fstride[p]), x = (int)(off % m.fstride[p]);
+        const int w = m.width[p];
+        if (x + dim > w || y + dim > w || (x & 7) || (y & 7)) continue;
+        const pixel* rec = (const pixel*)r.recon[p];
+        sse_t v = 0;
+        for (int by = 0; by < dim; by += 8)
+            for (int bx = 0; bx < dim; bx += 8)
+            {
+                const int b = ((y + by) >> 3) * (w >> 3) + ((x + bx) >> 3);
+                const pixel* q = recon + by * rstride + bx;
+                if (same8(q, rstride, m.pred[p] + (y + by) * m.pstride[p] + x + bx, m.pstride[p])) v += (sse_t)r.sse_pred[p][b];
+                else if (same8(q, rstride, rec + (y + by) * w + x + bx, w)) v += (sse_t)r.sse_rec[p][b];
+                else return false;
+            }
+        out = v;
+        return true;
+    }
+    return false;
+}
+
+template <int chroma, int size>
+sse_t sse_thunk(const pixel* fenc, intptr_t fstride, const pixel* ref, intptr_t rstride)
+{
+    if (t_memo.active)
+    {
+        sse_t v;
+        if (memo_sse(chroma ? 1 << (size + 1) : 1 << (size + 2), fenc, fstride, ref, rstride, v))
+        {
+            g_st[ST_SSE_HIT]++;
+            if (g_mode == RDO_CHECK && v != g_sse_orig[chroma][size](fenc, fstride, ref, rstride)) g_st[ST_CHECK_BAD]++;
+            return v;
+        }
+        g_st[ST_SSE_MISS]++;
+    }
+    return g_sse_orig[chroma][size](fenc, fstride, ref, rstride);
+}
+
 template <int size>
 int psy_thunk(const pixel* source, intptr_t sstride, const pixel* recon, intptr_t rstride)
 {
@@ -385,6 +439,21 @@ extern "C" void x265amd_rdo_install(void* table)
     p.cu[BLOCK_16x16].psy_cost_pp = psy_thunk<2>;
     p.cu[BLOCK_32x32].psy_cost_pp = psy_thunk<3>;
     p.cu[BLOCK_64x64].psy_cost_pp = psy_thunk<4>;
+    /* the distortions of a device CU and of its TUs: luma 8..64, 4:2:0 chroma 8..32 (X265AMD_RDO_SSE=0: the table's) */
+    const char* e = getenv("X265AMD_RDO_SSE");
+    if (e && *e == '0') return;
+    for (int i = 0; i < NUM_CU_SIZES; i++)
+    {
+        g_sse_orig[0][i] = p.cu[i].sse_pp;
+        g_sse_orig[1][i] = p.chroma[X265_CSP_I420].cu[i].sse_pp;
+    }
+    p.cu[BLOCK_8x8].sse_pp = sse_thunk<0, 1>;
+    p.cu[BLOCK_16x16].sse_pp = sse_thunk<0, 2>;
+    p.cu[BLOCK_32x32].sse_pp = sse_thunk<0, 3>;
+    p.cu[BLOCK_64x64].sse_pp = sse_thunk<0, 4>;
+    p.chroma[X265_CSP_I420].cu[BLOCK_16x16].sse_pp = sse_thunk<1, 2>;
+    p.chroma[X265_CSP_I420].cu[BLOCK_32x32].sse_pp = sse_thunk<1, 3>;
+    p.chroma[X265_CSP_I420].cu[BLOCK_64x64].sse_pp = sse_thunk<1, 4>;
 }
 
 /* called by the encoder binding before x265_encoder_close frees the encoder (oracle/hip_encoder_main.cpp) */

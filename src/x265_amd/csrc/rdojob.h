@@ -28,7 +28,8 @@ struct RdoJob
     x265amd_cmp_batch psy[4];      // 8x8 psy: luma (fenc, pred), luma (fenc, recon), chroma (fenc, pred), (fenc, recon)
     RdoSaoJob sao;
     uint32_t kind;                 // 0: the CU's residual coding (tu, psy); 1: SAO statistics (sao)
-    uint32_t pad[2];
+    uint32_t pad[2];               // kind 0: pad[0] = the CU's 8x8 blocks B (> 0: each psy energy's block also
+                                   // gets its sse_pp 8x8 at out + 2 B)
     uint32_t seq;                  // the request's sequence number; written last (release)
 };
 

@@ -186,11 +186,12 @@ std::atomic<uint64_t> g_next_id{ 1 };
 
 size_t out_bytes(const Geo& g, size_t pix)
 {
-    // recon (pixels), resi + coeff (int16 each), num_sig (uint32 per TU), psy_pred + psy_rec (int32 per block)
-    return g.pix() * pix + 2 * g.pix() * 2 + 4 * (size_t)g.tus() + 8 * (size_t)g.blocks();
+    // recon (pixels), resi + coeff (int16 each), num_sig (uint32 per TU), psy_pred + psy_rec (int32 per block),
+    // sse_pred + sse_rec (int32 per block; the server's requests only)
+    return g.pix() * pix + 2 * g.pix() * 2 + 4 * (size_t)g.tus() + 16 * (size_t)g.blocks();
 }
 
-void set_result(x265amd_rdo_req* r, size_t pix)
+void set_result(x265amd_rdo_req* r, size_t pix, bool sse = false)
 {
     const Geo g(r->cu.log2_cu);
     x265amd_rdo_result& o = r->res;
@@ -204,6 +205,8 @@ void set_result(x265amd_rdo_req* r, size_t pix)
     for (int k = 0; k < 3; k++) { o.num_sig[k] = (const uint32_t*)p; p += 4 * (size_t)nt[k]; }
     for (int k = 0; k < 3; k++) { o.psy_pred[k] = (const int32_t*)p; p += 4 * (size_t)nb[k]; }
     for (int k = 0; k < 3; k++) { o.psy_rec[k] = (const int32_t*)p; p += 4 * (size_t)nb[k]; }
+    for (int k = 0; k < 3; k++) { o.sse_pred[k] = sse ? (const int32_t*)p : nullptr; p += 4 * (size_t)nb[k]; }
+    for (int k = 0; k < 3; k++) { o.sse_rec[k] = sse ? (const int32_t*)p : nullptr; p += 4 * (size_t)nb[k]; }
     for (int k = 0; k < 3; k++)
     {
         o.tu_log2[k] = k ? g.tlc : g.tl;
@@ -970,6 +973,7 @@ int direct_post(x265amd_rdo* s, x265amd_rdo_thread* t, int k, const x265amd_rdo_
         for (int c = 0; c < 2; c++) job->tu[c] = tb[c];
         for (int c = 0; c < 4; c++) job->psy[c] = pb[c];
         job->kind = 0;
+        job->pad[0] = (uint32_t)g.blocks();        // the 8x8 SSEs go 2 * blocks int32 after each psy energy
         return server_publish(s, t, k, job);
     }
     r->want = 1;
@@ -1097,7 +1101,7 @@ extern "C" int x265amd_rdo_wait(x265amd_rdo* s, int ticket, const x265amd_rdo_re
     if (s->launchers.empty())
     {
         int rc = r->rc ? r->rc : direct_wait(s, t, ticket);
-        if (!rc) set_result(r, s->pix);
+        if (!rc) set_result(r, s->pix, s->server);
         if (!rc && s->server && s->srv_timing)
         {
             const uint64_t* st = (const uint64_t*)(t->host + (size_t)ticket * t->region + t->region -

@@ -1383,6 +1383,7 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_rdo_server(const RdoServerArg
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         {
             const int n0 = s_job.psy[0].n, n1 = s_job.psy[1].n, n2 = s_job.psy[2].n, n3 = s_job.psy[3].n;
+            const int64_t sse_at = s_job.pad[0] <= 96 ? 2 * (int64_t)s_job.pad[0] : 0;
             const int total = sane ? n0 + n1 + n2 + n3 : 0;
             for (int q = threadIdx.x; q < total; q += blockDim.x)
             {
@@ -1393,6 +1394,18 @@ __global__ __launch_bounds__(X265AMD_BLOCK) void k_rdo_server(const RdoServerArg
                 const P* pb = (const P*)c.b + c.b_off[j];
                 const int e = psy_energy8<P>(pa, c.a_stride) - psy_energy8<P>(pb, c.b_stride);
                 ((int32_t*)c.out)[j] = e < 0 ? -e : e;
+                if (sse_at)
+                {
+                    // sse_pp 8x8 of the same pair (pixel.cpp sse<8, 8>), for the CU's distortions
+                    int v = 0;
+                    for (int y = 0; y < 8; y++)
+                        for (int x = 0; x < 8; x++)
+                        {
+                            const int d = (int)pa[y * c.a_stride + x] - (int)pb[y * c.b_stride + x];
+                            v += d * d;
+                        }
+                    ((int32_t*)c.out)[j + sse_at] = v;
+                }
             }
         }
         // every output of the request is visible to the host before its done word

@@ -129,3 +129,9 @@ def test_gpu_rdo_early_posts_bit_exact(tmp_path, mode, form):
         assert m and int(m.group(1)) > 0 and int(m.group(2)) == 0, err[-3000:]
     else:
         assert m is None, err[-3000:]
+    # the server also returns every 8x8 block's sse_pp against the prediction and the reconstruction: the CU's
+    # distortions (search.cpp:2591-2595, 2668-2679) are served from them (compared in check mode)
+    m = re.search(r"\[x265rdo\] sse_pp memo hits (\d+) misses (\d+)", err)
+    assert m, err[-3000:]
+    if form == "server":
+        assert int(m.group(1)) > 0 and int(m.group(2)) == 0, err[-3000:]
