@@ -818,10 +818,8 @@ def run_gpu(case: Case, prims, device="cuda", guard=None) -> dict:
         if not isinstance(v, np.ndarray):
             return v
         h = np.ascontiguousarray(v)
-        # (through a page-locked copy: every occurrence of the suite's intermittent illegal-address error was a
-        # pageable host-to-device copy of a fresh numpy array)
         try:
-            return torch.from_numpy(h).pin_memory().to(device)
+            return torch.from_numpy(h).to(device)
         except Exception:
             # (an asynchronous device error surfacing here: say where the copy's host side was)
             print(f"run_gpu: copy of {case.key()} buffer {k} failed: host {h.ctypes.data:#x} + {h.nbytes} bytes; "

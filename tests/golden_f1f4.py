@@ -71,9 +71,9 @@ def bcost_gpu(prims, depth, c):
     W, H, n, rps, ns, aq = c
     g, planes, fo, r0o, r1o, iq = _bcost_inputs(depth, c)
     ncu, hcu = g["wcu"] * g["hcu"], g["hcu"]
-    T = torch.from_numpy(mvcost_table(depth)).pin_memory().cuda()
-    pl = torch.from_numpy(planes.view(np.int16) if planes.dtype == np.uint16 else planes).pin_memory().cuda()
-    dv = lambda a: None if a is None else torch.from_numpy(np.ascontiguousarray(a)).pin_memory().cuda()
+    T = torch.from_numpy(mvcost_table(depth)).cuda()
+    pl = torch.from_numpy(planes.view(np.int16) if planes.dtype == np.uint16 else planes).cuda()
+    dv = lambda a: None if a is None else torch.from_numpy(np.ascontiguousarray(a)).cuda()
     m0, m1 = dv(np.zeros(2 * n * ncu, np.int16)), dv(np.zeros(2 * n * ncu, np.int16))
     c0, c1 = dv(np.zeros(n * ncu, np.int32)), dv(np.zeros(n * ncu, np.int32))
     lc = torch.zeros(n * ncu, dtype=torch.int16, device="cuda")
@@ -123,12 +123,12 @@ def f4_gpu(prims, depth, c):
 
     W, H, cl, csp = c
     pl, U, dp, prm, fenc = _f4_inputs(depth, c)
-    dev = lambda planes: tuple(torch.from_numpy(p.view(np.int16) if p.dtype == np.uint16 else p).pin_memory().cuda()
+    dev = lambda planes: tuple(torch.from_numpy(p.view(np.int16) if p.dtype == np.uint16 else p).cuda()
                                for p in planes)
     M = F.MARGIN
     org = lambda t: t.data_ptr() + (M * t.shape[1] + M) * t.element_size()
     d = dev(pl)
-    du = torch.from_numpy(U.view(np.uint8).reshape(U.shape[0], -1)).pin_memory().cuda()
+    du = torch.from_numpy(U.view(np.uint8).reshape(U.shape[0], -1)).cuda()
     fr = DeblockFrame()
     fr.width, fr.height, fr.chroma_format = W, H, csp
     for p in range(3):
@@ -142,7 +142,7 @@ def f4_gpu(prims, depth, c):
             fr.ref_poc[lst][k] = dp.ref_poc[lst][k]
     prims.deblock(depth, [fr])
     out_t = dev(tuple(np.zeros_like(p) for p in pl))
-    dprm = torch.from_numpy(prm.view(np.uint8)).pin_memory().cuda()
+    dprm = torch.from_numpy(prm.view(np.uint8)).cuda()
     sf = SaoFrame()
     sf.width, sf.height, sf.ctu_log2, sf.luma_on, sf.chroma_on, sf.chroma_format = W, H, cl, 1, 1, csp
     for p in range(3):

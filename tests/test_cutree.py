@@ -47,7 +47,7 @@ def test_cutree_gpu_matches_oracle(gpu_prims, oracle_libs, case):
     p0, b, p1 = 0, bp0, bp0 + p1b
     ds = (((b - p0) << 8) + ((p1 - p0) >> 1)) // (p1 - p0)
     w0 = 64 - (ds >> 2) if wb else 32
-    t = lambda a: torch.from_numpy(a.view(np.int16) if a.dtype == np.uint16 else a).pin_memory().cuda()
+    t = lambda a: torch.from_numpy(a.view(np.int16) if a.dtype == np.uint16 else a).cuda()
     d = {k: t(c[k].copy()) for k in ("intra", "lowres", "invq", "mvs0", "mvs1", "prop", "ref0", "ref1")}
     if not ref:
         d["prop"][:wcu] = 0

@@ -129,7 +129,7 @@ GPU_SIZES = [(200, 136, 6), (128, 64, 5), (96, 48, 4), (1920, 1080, 6)]
 def _dev(planes):
     import torch
 
-    return tuple(torch.from_numpy(p.view(np.int16) if p.dtype == np.uint16 else p).pin_memory().cuda() for p in planes)
+    return tuple(torch.from_numpy(p.view(np.int16) if p.dtype == np.uint16 else p).cuda() for p in planes)
 
 
 def _host(t, dtype):
@@ -159,7 +159,7 @@ def test_gpu_deblock(gpu_prims, depth):
             ref = F.copy_planes(pl)
             O.deblock(W, H, cl, ref, F.MARGIN, U, dp)
             d = _dev(pl)
-            du = torch.from_numpy(U.view(np.uint8).reshape(U.shape[0], -1)).pin_memory().cuda()
+            du = torch.from_numpy(U.view(np.uint8).reshape(U.shape[0], -1)).cuda()
             fr = DeblockFrame()
             fr.width, fr.height = W, H
             for p in range(3):
@@ -197,7 +197,7 @@ def test_gpu_sao_apply(gpu_prims, depth):
             ref = F.copy_planes(pl)
             O.sao_apply(W, H, cl, ref, F.MARGIN, prm, *on)
             src, dst = _dev(pl), _dev(tuple(np.zeros_like(p) for p in pl))
-            dprm = torch.from_numpy(prm.view(np.uint8)).pin_memory().cuda()
+            dprm = torch.from_numpy(prm.view(np.uint8)).cuda()
             fr = SaoFrame()
             fr.width, fr.height, fr.ctu_log2, fr.luma_on, fr.chroma_on = W, H, cl, on[0], on[1]
             for p in range(3):
@@ -265,7 +265,7 @@ def test_gpu_extend_border(gpu_prims, depth):
         p = rng.integers(0, 1 << depth, size=(H + 2 * my, stride)).astype(dt)
         ref = p.copy()
         O.extend_border(ref, mx, my, W, H)
-        d = torch.from_numpy(p.view(np.int16) if dt == np.uint16 else p).pin_memory().cuda()
+        d = torch.from_numpy(p.view(np.int16) if dt == np.uint16 else p).cuda()
         bp = BorderPlane()
         bp.plane = d.data_ptr() + (my * stride + mx) * d.element_size()
         bp.stride, bp.width, bp.height, bp.margin_x, bp.margin_y = stride, W, H, mx, my
@@ -304,8 +304,8 @@ def test_gpu_loop_filter_row_bands_equal_whole_frame(gpu_prims, depth):
         # GPU: row bands
         d = _dev(pl)
         out = _dev(tuple(np.zeros_like(p) for p in pl))
-        du = torch.from_numpy(U.view(np.uint8).reshape(U.shape[0], -1)).pin_memory().cuda()
-        dprm = torch.from_numpy(prm.view(np.uint8)).pin_memory().cuda()
+        du = torch.from_numpy(U.view(np.uint8).reshape(U.shape[0], -1)).cuda()
+        dprm = torch.from_numpy(prm.view(np.uint8)).cuda()
         fr = DeblockFrame()
         fr.width, fr.height = W, H
         for p in range(3):
@@ -367,7 +367,7 @@ def test_gpu_f4_chroma_formats(gpu_prims, csp, depth):
         ref = F.copy_planes(pl)
         O.deblock(W, H, cl, ref, F.MARGIN, U, dp, csp=csp)
         d = _dev(pl)
-        du = torch.from_numpy(U.view(np.uint8).reshape(U.shape[0], -1)).pin_memory().cuda()
+        du = torch.from_numpy(U.view(np.uint8).reshape(U.shape[0], -1)).cuda()
         fr = DeblockFrame()
         fr.width, fr.height, fr.chroma_format = W, H, csp
         for p in range(3):
@@ -385,7 +385,7 @@ def test_gpu_f4_chroma_formats(gpu_prims, csp, depth):
         sref = F.copy_planes(ref)
         O.sao_apply(W, H, cl, sref, F.MARGIN, prm, 1, 1, csp=csp)
         out = _dev(tuple(np.zeros_like(p) for p in pl))
-        dprm = torch.from_numpy(prm.view(np.uint8)).pin_memory().cuda()
+        dprm = torch.from_numpy(prm.view(np.uint8)).cuda()
         sf = SaoFrame()
         sf.width, sf.height, sf.ctu_log2, sf.luma_on, sf.chroma_on, sf.chroma_format = W, H, cl, 1, 1, csp
         for p in range(3):
@@ -429,7 +429,7 @@ def test_gpu_loop_filters_luma_only_i400(gpu_prims, depth):
     pl = F.frame_planes(W, H, depth, rng)
     U = F.deblock_units(W, H, cl, depth, rng, "P", 0.0)
     dp = F.deblock_params(rng, "P", 0)
-    du = torch.from_numpy(U.view(np.uint8).reshape(U.shape[0], -1)).pin_memory().cuda()
+    du = torch.from_numpy(U.view(np.uint8).reshape(U.shape[0], -1)).cuda()
     outs = []
     for csp in (1, 4):
         d = _dev(F.copy_planes(pl))
@@ -448,7 +448,7 @@ def test_gpu_loop_filters_luma_only_i400(gpu_prims, depth):
     np.testing.assert_array_equal(outs[1][1], _dev(pl)[1].cpu().numpy())     # chroma untouched
     # SAO apply, luma only, NULL chroma planes: luma equals the 4:2:0 run's luma
     prm = F.sao_params(W, H, cl, depth, rng)
-    dprm = torch.from_numpy(np.ascontiguousarray(prm).view(np.uint8).reshape(-1).copy()).pin_memory().cuda()
+    dprm = torch.from_numpy(np.ascontiguousarray(prm).view(np.uint8).reshape(-1).copy()).cuda()
     res = []
     for csp in (1, 4):
         src, dst = _dev(F.copy_planes(pl)), _dev(F.copy_planes(pl))

@@ -48,7 +48,7 @@ def test_group_launches_one_class_per_launch():
 def _dev(v):
     import torch
 
-    return torch.from_numpy(np.ascontiguousarray(v)).pin_memory().cuda() if isinstance(v, np.ndarray) else v
+    return torch.from_numpy(np.ascontiguousarray(v)).cuda() if isinstance(v, np.ndarray) else v
 
 
 def _run_grouped(family, op, cases, prims, taps=8, nref=4):

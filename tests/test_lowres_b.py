@@ -103,12 +103,12 @@ def test_gpu_bcost(gpu_prims, depth):
 
     O = po.LowresB("oracle", depth)
     tab = mvcost_table(depth)
-    T = torch.from_numpy(tab).pin_memory().cuda()
+    T = torch.from_numpy(tab).cuda()
     for (W, H, n, rps, ns, aq) in CASES + [(1920, 1080, 3, 10, 6, True)]:
         g, planes, fo, r0o, r1o, iq = make_case(W, H, n, depth, 7 * depth + W, aq)
         ncu, hcu = g["wcu"] * g["hcu"], g["hcu"]
-        pl = torch.from_numpy(planes.view(np.int16) if planes.dtype == np.uint16 else planes).pin_memory().cuda()
-        dv = lambda a: None if a is None else torch.from_numpy(np.ascontiguousarray(a)).pin_memory().cuda()
+        pl = torch.from_numpy(planes.view(np.int16) if planes.dtype == np.uint16 else planes).cuda()
+        dv = lambda a: None if a is None else torch.from_numpy(np.ascontiguousarray(a)).cuda()
         for ds in (np.ones(2 * n, np.uint8), np.tile([1, 0], n).astype(np.uint8)):
             # stored list-1 results for the reuse pass come from a first full pass on both sides
             mvs0, mvs1 = np.zeros(2 * n * ncu, np.int16), np.zeros(2 * n * ncu, np.int16)

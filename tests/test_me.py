@@ -111,7 +111,7 @@ def test_me_gpu_multi_batch_call(gpu_prims, oracle_libs, depth):
     orc = CpuOracle("oracle", depth)
     cases = [case_me(w, h, m, 2, 57, depth, 384, seed_of("me-m", depth, w, h, m))
              for (w, h, m) in ((8, 8, 1), (16, 16, 0), (32, 32, 1), (64, 64, 2), (12, 16, 1), (64, 16, 1))]
-    dv = lambda v: torch.from_numpy(np.ascontiguousarray(v)).pin_memory().cuda() if isinstance(v, np.ndarray) else v
+    dv = lambda v: torch.from_numpy(np.ascontiguousarray(v)).cuda() if isinstance(v, np.ndarray) else v
     jobs, keep = [], []
     for c in cases:
         b = {k: dv(v) for k, v in c.bufs.items()}

@@ -90,7 +90,7 @@ def test_tu_without_residual_output(gpu_prims, oracle_libs):
     orc = CpuOracle("oracle", 8)
     c = case_tu(4, 1, 0, 0, 1, 8, 512, seed_of("tu-nores"))
     exp = run_cpu(c, orc)
-    b = {k: (torch.from_numpy(np.ascontiguousarray(v)).pin_memory().cuda() if isinstance(v, np.ndarray) else v)
+    b = {k: (torch.from_numpy(np.ascontiguousarray(v)).cuda() if isinstance(v, np.ndarray) else v)
          for k, v in c.bufs.items()}
     p = c.params
     gpu_prims.tu_pipeline(8, p["log2"], p["luma"], p["intra"], p["islice"], p["sh"], b["f"], b["fs"], b["fo"], b["p"],

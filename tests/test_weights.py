@@ -48,7 +48,7 @@ def test_weights_gpu_matches_oracle(gpu_prims, oracle_libs, depth, kind):
     W, H = 1920, 1080
     g, fb, rb, intra, st = weights_case(kind, W, H, depth, seed=depth)
     out, delta, wb = _oracle(kind, "oracle", depth, W, H, seed=depth)
-    t = lambda a: torch.from_numpy(a.view(np.int16) if a.dtype == np.uint16 else a).pin_memory().cuda()
+    t = lambda a: torch.from_numpy(a.view(np.int16) if a.dtype == np.uint16 else a).cuda()
     dfb, drb, dint = t(fb), t(rb), t(intra)
     dwb = torch.zeros_like(drb)
     res = gpu_prims.weights_analyse(depth, g["width"], g["lines"], g["stride"], g["padded"], g["padoff"], dfb, drb,
